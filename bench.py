@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Higgs-shaped GBDT, sec/tree, on 1..8 MI355X (one rank per GPU).
+
+Config (BASELINE.json / BASELINE.md target (b)): 10.5M train + 0.5M test rows x 28
+features (the Higgs split, docs/gbdt_experiments.md:9), level-wise depth 6
+(max_leaf_cnt 255 -> min(255, 2^6) = 64 leaves), 255 quantile bins (alpha 0.5),
+lr 0.1, l1 = l2 = 0, min_child_hessian_sum 100 -- the reference's
+experiment/higgs/local_gbdt.conf with tree_grow_policy=level, max_depth=6.
+``--policy loss`` runs the reference-identical leaf-wise 255-leaf shape (a).
+
+A "step" is one boosting round = one tree + train-score update + train loss/
+gradients for the next tree + incremental test-set scoring and test loss
+(the reference's loss-monitoring loop, GBDTOptimizer.java:406-447).
+Scaling is STRONG: the 10.5M rows are sharded over the N ranks.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+For N>1 the driver launches it under torch.distributed.run (RANK/WORLD_SIZE env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from ytk_learn_amd.data.synthetic import higgs_like  # noqa: E402
+from ytk_learn_amd.models.gbdt.builder import TreeParams  # noqa: E402
+from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer  # noqa: E402
+from ytk_learn_amd.parallel.comm import Comm  # noqa: E402
+from ytk_learn_amd.utils.logging import YtkLogger  # noqa: E402
+
+BASELINE_SEC_PER_TREE = 1.136  # ytk-learn 567.83 s / 500 trees (docs/gbdt_experiments.md:104)
+METRIC = "Higgs-11M GBDT: sec/tree (500 trees, depth 6, 255 bins) at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--train-rows", type=int, default=10_500_000)
+    ap.add_argument("--test-rows", type=int, default=500_000)
+    ap.add_argument("--policy", default="level", choices=["level", "loss"])
+    ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--leaves", type=int, default=255)
+    ap.add_argument("--bins", type=int, default=255)
+    ap.add_argument("--seed", type=int, default=17)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--profile", action="store_true", help="sync per phase and print time stats")
+    ap.add_argument("--quiet", action="store_true")
+    a = ap.parse_args()
+
+    comm = Comm.from_env(device=a.device)
+    dev = comm.device
+    world, rank = comm.world, comm.rank
+    if world != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    # strong scaling: shard the fixed global row count
+    def shard(n):
+        base, rem = divmod(n, world)
+        return base + (1 if rank < rem else 0)
+
+    n_tr, n_te = shard(a.train_rows), shard(a.test_rows)
+    t0 = time.perf_counter()
+    X, y = higgs_like(n_tr, seed=a.seed * 1000 + rank, device=dev)
+    Xt, yt = higgs_like(n_te, seed=a.seed * 1000 + 500 + rank, device=dev)
+    gen_s = time.perf_counter() - t0
+
+    tp = TreeParams(max_depth=a.depth if a.policy == "level" else -1, max_leaf_cnt=a.leaves,
+                    min_child_hessian_sum=100.0, min_split_loss=0.0, min_split_samples=-1,
+                    learning_rate=0.1, l1=0.0, l2=0.0, grow_policy=a.policy)
+    if a.policy == "level":
+        tp.max_leaf_cnt = min(a.leaves, 1 << a.depth)  # GBDTOptimizationParams.java:148-154
+    total_rounds = a.warmup + a.steps
+    params = GBDTParams(round_num=total_rounds, loss_function="sigmoid", eval_metric=["auc"],
+                        missing_value="value@0",
+                        approximate=[{"cols": "default", "type": "sample_by_quantile", "max_cnt": a.bins,
+                                      "use_sample_weight": False, "alpha": 0.5}],
+                        tree=tp)
+    log = YtkLogger(rank, stream=sys.stderr, every=10)
+    if a.quiet:
+        log.quiet = True
+    tr = GBDTTrainer(params, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log, profile=a.profile)
+    t0 = time.perf_counter()
+    tr.prepare()
+    # initial prediction + gradients (GBDTOptimizer.initPred)
+    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
+    tr._loss_grad(tr.te_score, tr.te_init, yt, None, tr.te_pred, tr.te_gh, 0, False)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    prep_s = time.perf_counter() - t0
+
+    for i in range(a.warmup):
+        tr.step(i)
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.warmup, a.warmup + a.steps):
+        tr.step(i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    comm.barrier()
+    el = time.perf_counter() - t0
+    el_max = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+
+    # quality check after the timed rounds (outside timing)
+    auc = tr.eval_test.evals[0].compute(yt, tr.te_pred, None, comm)[0]
+    sec_per_tree = el_max / a.steps
+    if a.profile and rank == 0:
+        print(tr.builder.total_stats.stats(), file=sys.stderr)
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(sec_per_tree, 6),
+            "unit": "s/tree",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * sec_per_tree, 4),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(sec_per_tree / BASELINE_SEC_PER_TREE, 6),
+            "dtype": "fp32",
+            "data": "synthetic Higgs-shape (10.5M train + 0.5M test x 28 dense float features, random-init trees)",
+            "config": {
+                "model": f"gbdt {a.policy}-wise depth{a.depth} leaves{tp.max_leaf_cnt} bins{a.bins} sigmoid lr0.1",
+                "global_batch": a.train_rows,
+                "seq_len": 28,
+                "parallelism": f"dp{world}",
+                "test_rows": a.test_rows,
+                "rounds_timed": a.steps,
+                "device": str(dev),
+            },
+            "train_loss": round(float(tr.last_train_loss), 6),
+            "test_loss": round(float(tr.last_test_loss), 6),
+            "test_auc": round(float(auc), 6),
+            "prep_s": round(prep_s, 3),
+            "datagen_s": round(gen_s, 3),
+        }
+        print(json.dumps(res), flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+"""HIP GBDT kernels vs the CPU (PyTorch/NumPy fp32/fp64) reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+from ytk_learn_amd.ops import gbdt as gops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_bins(N, F, nb, seed=0, dtype=torch.uint8):
+    g = torch.Generator().manual_seed(seed)
+    stride = ((F + 31) // 32) * 32
+    bins = torch.zeros((N, stride), dtype=dtype)
+    b = torch.randint(0, nb, (N, F), generator=g)
+    bins[:, :F] = b.to(dtype)
+    return bins
+
+
+def _gh(N, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    gh = torch.empty((N, 2))
+    gh[:, 0] = torch.randn(N, generator=g)
+    gh[:, 1] = torch.rand(N, generator=g) * 0.25
+    return gh
+
+
+@pytest.mark.parametrize("F,nb", [(28, 255), (7, 16), (40, 64)])
+def test_hist_build_matches_cpu(cuda, F, nb):
+    N = 50000
+    bins = _rand_bins(N, F, nb)
+    gh = _gh(N)
+    B = ((nb + 3) // 4) * 4
+    perm = torch.randperm(N, generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    work = torch.tensor([[0, 0, 20000, 0], [0, 20000, 31000, 0], [2, 31000, 50000, 0]], dtype=torch.int32)
+    hc = torch.zeros((3, B, F, 2))
+    gops.hist_build(bins, F, gh, perm, work, hc, B)
+    hg = torch.zeros((3, B, F, 2), device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), perm.to(cuda), work.to(cuda), hg, B)
+    torch.testing.assert_close(hg.cpu(), hc, rtol=1e-4, atol=1e-3)
+    # identity rows (root path)
+    hc2 = torch.zeros((1, B, F, 2))
+    w2 = torch.tensor([[0, 0, N, 0]], dtype=torch.int32)
+    gops.hist_build(bins, F, gh, None, w2, hc2, B)
+    hg2 = torch.zeros((1, B, F, 2), device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, w2.to(cuda), hg2, B)
+    torch.testing.assert_close(hg2.cpu(), hc2, rtol=1e-4, atol=2e-3)
+
+
+def test_hist_build_uint16_global(cuda):
+    N, F, nb = 20000, 5, 1000
+    bins = _rand_bins(N, F, nb, dtype=torch.int16)
+    gh = _gh(N)
+    B = 1000
+    work = torch.tensor([[0, 0, N, 0]], dtype=torch.int32)
+    hc = torch.zeros((1, B, F, 2))
+    gops.hist_build(bins, F, gh, None, work, hc, B)
+    hg = torch.zeros((1, B, F, 2), device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, work.to(cuda), hg, B)
+    torch.testing.assert_close(hg.cpu(), hc, rtol=1e-4, atol=1e-3)
+
+
+def _hist_from(N, F, nb, B, seed):
+    bins = _rand_bins(N, F, nb, seed)
+    gh = _gh(N, seed + 1)
+    h = torch.zeros((1, B, F, 2))
+    gops.hist_build(bins, F, gh, None, torch.tensor([[0, 0, N, 0]], dtype=torch.int32), h, B)
+    return h[0]
+
+
+@pytest.mark.parametrize("l1,l2,mal", [(0.0, 0.0, -1.0), (0.5, 1.0, -1.0), (0.0, 1.0, 0.3)])
+def test_split_find_matches_cpu(cuda, l1, l2, mal):
+    F, nb, B = 28, 200, 200
+    parent = _hist_from(40000, F, nb, B, 5)
+    small = _hist_from(15000, F, nb, B, 6)
+    hist = torch.zeros((4, B, F, 2))
+    hist[0] = parent
+    hist[1] = small
+    # make bins sparse for some features (empty-bin skipping)
+    hist[1, 50:120, 3] = 0
+    nbins = torch.full((F,), nb, dtype=torch.int32)
+    nbins[7] = 30
+    fmask = torch.ones(F, dtype=torch.uint8)
+    fmask[2] = 0
+    items = torch.tensor([[0, 0, 0, 0], [1, 0, 0, 0], [2, 0, 1, 1]], dtype=torch.int32)
+    params = {"mcw": 10.0, "l1": l1, "l2": l2, "max_abs_leaf": mal}
+    hc = hist.clone()
+    oc = gops.split_find(hc, B, F, nbins, fmask, 0, items, params).numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+    hg = hist.to(cuda)
+    og = gops.split_find(hg, B, F, nbins.to(cuda), fmask.to(cuda), 0, items.to(cuda), params)
+    og = og.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+    for a, b in zip(oc, og):
+        assert a["feat"] == b["feat"] and a["bin_a"] == b["bin_a"] and a["bin_b"] == b["bin_b"]
+        np.testing.assert_allclose(a["loss_chg"], b["loss_chg"], rtol=1e-5)
+        np.testing.assert_allclose([a["gl"], a["hl"], a["g"], a["h"]], [b["gl"], b["hl"], b["g"], b["h"]],
+                                   rtol=1e-9, atol=1e-9)
+    # derived histogram written back
+    torch.testing.assert_close(hg[2].cpu()[:, fmask.bool()], (hist[0] - hist[1])[:, fmask.bool()])
+
+
+def test_partition_matches_cpu(cuda):
+    N, F = 100000, 28
+    bins = _rand_bins(N, F, 255, 9)
+    rows = torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32)
+    segs = [(0, 30000), (30000, 45000), (75000, 25000)]
+    feat = torch.tensor([3, 17, 0], dtype=torch.int32)
+    thr = torch.tensor([100, 7, 250], dtype=torch.int32)
+    ch = 4096
+    items, first, nblk = [], [], []
+    for i, (b, c) in enumerate(segs):
+        first.append(len(items))
+        k = 0
+        for s in range(b, b + c, ch):
+            items.append((i, s, min(s + ch, b + c), k))
+            k += 1
+        nblk.append(k)
+    args = [torch.tensor(items, dtype=torch.int32), feat, thr,
+            torch.tensor([s[0] for s in segs], dtype=torch.int32),
+            torch.tensor(first, dtype=torch.int32), torch.tensor(nblk, dtype=torch.int32)]
+    oc = torch.zeros(N, dtype=torch.int32)
+    lc = gops.partition(bins, rows, oc, *args, 3)
+    og = torch.zeros(N, dtype=torch.int32, device=cuda)
+    lg = gops.partition(bins.to(cuda), rows.to(cuda), og, *[a.to(cuda) for a in args], 3)
+    assert lg.cpu().tolist() == lc.tolist()
+    assert torch.equal(og.cpu(), oc)
+
+
+def test_tree_add_bins_and_forest(cuda):
+    from ytk_learn_amd.models.gbdt.tree import GBDTModel, Tree
+
+    t = Tree()
+    l, r = t.add_children(0)
+    t.set_split(0, 2, 10, 12)
+    ll, lr_ = t.add_children(l)
+    t.set_split(l, 5, 3, 4)
+    for n, v in [(ll, 0.5), (lr_, -0.25), (r, 1.5)]:
+        t.set_leaf(n, v)
+    N, F = 10000, 8
+    bins = _rand_bins(N, F, 20, 4)
+    arrs = tuple(torch.from_numpy(a) for a in t.bin_arrays())
+    sc = torch.zeros((N, 2))
+    gops.tree_add_bins(bins, arrs, sc, 1)
+    sg = torch.zeros((N, 2), device=cuda)
+    gops.tree_add_bins(bins.to(cuda), tuple(a.to(cuda) for a in arrs), sg, 1)
+    torch.testing.assert_close(sg.cpu(), sc)
+    # raw forest predict with NaN defaults
+    cands = [np.arange(20, dtype=np.float32) * 0.5 for _ in range(F)]
+    t.convert_split_values(cands)
+    t.default_left = [True, False, True, True, True]
+    m = GBDTModel(0.5, 1, "sigmoid")
+    m.trees = [t, t]
+    fl = {k: torch.from_numpy(v) for k, v in m.flatten().items()}
+    X = torch.randn(N, F) * 5
+    X[::7, 2] = float("nan")
+    oc = torch.zeros((N, 1))
+    gops.forest_predict(X, fl, oc, 0.5)
+    og = torch.zeros((N, 1), device=cuda)
+    gops.forest_predict(X.to(cuda), {k: v.to(cuda) for k, v in fl.items()}, og, 0.5)
+    torch.testing.assert_close(og.cpu(), oc)
+    lo_c = torch.zeros((N, 2), dtype=torch.int32)
+    gops.forest_predict(X, fl, None, 1.0, lo_c)
+    lo_g = torch.zeros((N, 2), dtype=torch.int32, device=cuda)
+    gops.forest_predict(X.to(cuda), {k: v.to(cuda) for k, v in fl.items()}, None, 1.0, lo_g)
+    assert torch.equal(lo_g.cpu(), lo_c)
+
+
+def test_bin_assign_matches_cpu(cuda):
+    N, F = 30000, 6
+    X = torch.randn(N, F)
+    X[:, 3] = torch.round(X[:, 3] * 2) / 2  # ties with candidates
+    cands = [np.sort(np.unique(np.random.default_rng(f).normal(size=50).astype(np.float32))) for f in range(F)]
+    cands[3] = np.array([-1.0, -0.5, 0.0, 0.5, 1.0], np.float32)
+    cands[5] = np.array([0.0], np.float32)
+    cand = torch.from_numpy(np.concatenate(cands))
+    coff = torch.from_numpy(np.concatenate([[0], np.cumsum([len(c) for c in cands])]).astype(np.int32))
+    oc = torch.zeros((N, 32), dtype=torch.uint8)
+    gops.bin_assign(X, cand, coff, oc)
+    og = torch.zeros((N, 32), dtype=torch.uint8, device=cuda)
+    gops.bin_assign(X.to(cuda), cand.to(cuda), coff.to(cuda), og)
+    assert torch.equal(og.cpu(), oc)
+
+
+@pytest.mark.parametrize("loss,K", [("sigmoid", 1), ("l2", 1), ("l1", 1), ("poisson", 1), ("huber", 1), ("softmax", 4)])
+def test_grad_hess_matches_cpu(cuda, loss, K):
+    N = 20000
+    g = torch.Generator().manual_seed(0)
+    score = torch.randn((N, K), generator=g)
+    init = torch.randn((N, K), generator=g) * 0.1
+    if loss == "softmax":
+        lab = torch.nn.functional.one_hot(torch.randint(0, K, (N,), generator=g), K).float()
+    elif loss == "sigmoid":
+        lab = (torch.rand((N, K), generator=g) < 0.4).float()
+    elif loss == "poisson":
+        lab = torch.randint(0, 5, (N, K), generator=g).float()
+    else:
+        lab = torch.randn((N, K), generator=g)
+    w = torch.rand(N, generator=g) + 0.5
+    param = 0.5 if loss == "huber" else 0.0
+    pc, ghc = torch.zeros((N, K)), torch.zeros((K, N, 2))
+    ac = gops.grad_hess(score, init, lab, w, loss, param, 1.0, pc, ghc)
+    pg, ghg = torch.zeros((N, K), device=cuda), torch.zeros((K, N, 2), device=cuda)
+    ag = gops.grad_hess(score.to(cuda), init.to(cuda), lab.to(cuda), w.to(cuda), loss, param, 1.0, pg, ghg)
+    torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ghg.cpu(), ghc, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(ag.cpu().numpy(), ac.numpy(), rtol=1e-9)

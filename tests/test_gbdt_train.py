@@ -1,0 +1,114 @@
+import numpy as np
+import pytest
+import torch
+
+from ytk_learn_amd.data.synthetic import higgs_like
+from ytk_learn_amd.models.gbdt.builder import TreeParams
+from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer
+from ytk_learn_amd.models.gbdt.tree import GBDTModel
+from ytk_learn_amd.ops import gbdt as gops
+
+
+def _data(n, seed, dev="cpu"):
+    X, y = higgs_like(n, seed=seed, device=dev)
+    return GBDTData(X, y)
+
+
+def _params(policy, rounds=4, **kw):
+    tp = TreeParams(max_depth=5 if policy == "level" else -1, max_leaf_cnt=24 if policy == "loss" else 32,
+                    min_child_hessian_sum=5.0, grow_policy=policy, learning_rate=0.2, **kw)
+    return GBDTParams(round_num=rounds, tree=tp, watch_test=True)
+
+
+@pytest.mark.parametrize("policy", ["level", "loss"])
+def test_train_cpu_loss_decreases(policy):
+    tr = GBDTTrainer(_params(policy), _data(20000, 1), _data(4000, 2))
+    tr.prepare()
+    losses = []
+    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
+    for i in range(4):
+        tr.step(i)
+        losses.append(tr.last_train_loss)
+    assert all(b < a for a, b in zip(losses, losses[1:]))
+    t = tr.model.trees[0]
+    assert t.leaf_count() <= (32 if policy == "level" else 24)
+    if policy == "level":
+        assert t.max_depth() <= 5
+
+
+def test_model_roundtrip_and_forest_matches_training_scores():
+    tr = GBDTTrainer(_params("level", rounds=3), _data(8000, 3), None)
+    m = tr.train()
+    text = m.dumps()
+    m2 = GBDTModel.loads(text)
+    assert m2.dumps() == text
+    name2idx = {n: i for i, n in enumerate(tr.feature_names)}
+    for t in m2.trees:
+        t.update_feature_index(name2idx)
+    fl = {k: torch.from_numpy(v) for k, v in m2.flatten().items()}
+    out = torch.zeros((8000, 1))
+    X = torch.where(torch.isnan(tr.train_data.X), 0.0, tr.train_data.X)
+    gops.forest_predict(X, fl, out, 1.0)
+    # raw-threshold inference reproduces the bin-threshold training scores
+    torch.testing.assert_close(out, tr.score, rtol=1e-5, atol=1e-5)
+
+
+def test_subsample_and_feature_sample_cpu():
+    p = _params("level", rounds=2, instance_sample_rate=0.5, feature_sample_rate=0.5)
+    tr = GBDTTrainer(p, _data(10000, 4), None)
+    tr.train()
+    used = {tr.model.trees[0].feat[i] for i in range(tr.model.trees[0].num_nodes) if not tr.model.trees[0].is_leaf[i]}
+    assert len(used) <= 14
+    assert tr.model.trees[0].sample_cnt[0] < 6000
+
+
+@pytest.mark.parametrize("loss,K", [("l2", 1), ("l1", 1), ("softmax", 3), ("poisson", 1)])
+def test_other_losses_cpu(loss, K):
+    X, y = higgs_like(6000, seed=5)
+    if loss == "softmax":
+        c = torch.clamp((X[:, 25] * 1.5).long(), 0, K - 1)
+        y = torch.nn.functional.one_hot(c, K).float()
+    elif loss == "poisson":
+        y = torch.poisson(torch.exp(0.3 * X[:, 25:26]))
+    else:
+        y = X[:, 25:26] * 2.0 + 0.1 * torch.randn(6000, 1)
+    p = _params("level", rounds=3)
+    p.loss_function = loss
+    p.class_num = K
+    p.uniform_base_prediction = 1.0 if loss == "poisson" else (0.0 if loss != "softmax" else 0.0)
+    p.eval_metric = ["confusion_matrix"] if loss == "softmax" else ["rmse", "mae"]
+    tr = GBDTTrainer(p, GBDTData(X, y), GBDTData(X[:1000], y[:1000]))
+    tr.prepare()
+    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
+    l0 = None
+    for i in range(3):
+        tr.step(i)
+        l0 = tr.last_train_loss if l0 is None else l0
+    assert tr.last_train_loss < l0 or loss == "l1"
+    assert len(tr.model.trees) == 3 * K
+    tr.final_eval()
+
+
+def test_random_forest_cpu():
+    p = _params("level", rounds=3)
+    p.type = "random_forest"
+    tr = GBDTTrainer(p, _data(6000, 6), None)
+    tr.train()
+    assert np.isfinite(tr.last_train_loss)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["level", "loss"])
+def test_train_gpu_matches_cpu(cuda, policy):
+    d_cpu = _data(30000, 7)
+    d_gpu = GBDTData(d_cpu.X.to(cuda), d_cpu.y.to(cuda))
+    t_cpu = GBDTTrainer(_params(policy, rounds=3), d_cpu, None)
+    t_gpu = GBDTTrainer(_params(policy, rounds=3), d_gpu, None)
+    t_cpu.train()
+    t_gpu.train()
+    assert t_gpu.bins.is_cuda
+    np.testing.assert_allclose(t_gpu.last_train_loss, t_cpu.last_train_loss, rtol=2e-4)
+    # first tree: identical structure (ties aside)
+    a, b = t_cpu.model.trees[0], t_gpu.model.trees[0]
+    assert a.feat[0] == b.feat[0] and a.slot_a[0] == b.slot_a[0]
+    assert a.num_nodes == b.num_nodes

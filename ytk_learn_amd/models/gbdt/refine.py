@@ -1,0 +1,90 @@
+"""L1 (least-absolute-deviation) leaf refinement.
+
+Reference: ``J/optimizer/gbdt/TreeRefiner.java:72-254`` -- for ``l1`` loss every
+leaf value is replaced by learning_rate x weighted median of the residuals
+(label - current score) of the rows in that leaf. ``lad_refine_appr`` selects the
+mergeable-summary (approximate) or the exact distributed quantile.
+
+Device-native: leaf ids come from the bin-threshold traversal kernel, the
+per-leaf weighted medians from one segmented sort on the device (sort by
+(leaf, residual), segmented cumulative weights). Across GPUs each rank sends a
+256-point weighted summary per leaf (approximate) or its whole per-leaf residual
+list (exact) and the merge happens on the host in rank order.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ...ops import gbdt as gops
+from ...parallel.comm import Comm
+
+SUMMARY_POINTS = 256
+
+
+def _weighted_median_sorted(v: np.ndarray, w: np.ndarray) -> float:
+    c = np.cumsum(w)
+    i = int(np.searchsorted(c, 0.5 * c[-1], side="left"))
+    return float(v[min(i, len(v) - 1)])
+
+
+class TreeRefiner:
+    def __init__(self, comm: Comm, approximate: bool = True):
+        self.comm = comm
+        self.approximate = approximate
+
+    def leaf_ids(self, tree, bins: torch.Tensor) -> torch.Tensor:
+        n = tree.num_nodes
+        # score column trick: value = node id, so tree_add_bins writes the leaf id
+        feat, thr, left, right, _ = tree.bin_arrays()
+        ids = np.arange(n, dtype=np.float32)
+        out = torch.zeros((bins.shape[0], 1), dtype=torch.float32, device=bins.device)
+        arrs = tuple(torch.from_numpy(a).to(bins.device) for a in (feat, thr, left, right, ids))
+        gops.tree_add_bins(bins, arrs, out, 0)
+        return out[:, 0].round().to(torch.int64)
+
+    def refine(self, tree, builder, y: torch.Tensor, cur_score: torch.Tensor,
+               w: torch.Tensor, lr: float):
+        leaf = self.leaf_ids(tree, builder.bins)
+        keep = getattr(builder, "last_keep", None)
+        resid = (y.double() - cur_score.double())
+        ww = w.double() if w is not None else torch.ones_like(resid)
+        if keep is not None:
+            leaf, resid, ww = leaf[keep], resid[keep], ww[keep]
+        # segmented sort on device: key = leaf * big + rank(resid)
+        o = torch.argsort(resid)
+        leaf_o = leaf[o]
+        o2 = torch.argsort(leaf_o, stable=True)
+        idx = o[o2]
+        lv = leaf[idx].cpu().numpy()
+        rv = resid[idx].cpu().numpy()
+        wv = ww[idx].cpu().numpy()
+        leaves = tree.leaf_nodes()
+        bounds = {}
+        if lv.size:
+            starts = np.flatnonzero(np.r_[True, lv[1:] != lv[:-1]])
+            ends = np.r_[starts[1:], lv.size]
+            for s, e in zip(starts, ends):
+                bounds[int(lv[s])] = (s, e)
+        local = {}
+        for nid in leaves:
+            if nid not in bounds:
+                local[nid] = (np.zeros(0), np.zeros(0))
+                continue
+            s, e = bounds[nid]
+            v, wt = rv[s:e], wv[s:e]
+            if self.comm.is_dist and self.approximate and v.size > SUMMARY_POINTS:
+                c = np.cumsum(wt)
+                q = (np.arange(1, SUMMARY_POINTS + 1) / SUMMARY_POINTS) * c[-1]
+                j = np.searchsorted(c, q, side="left").clip(max=v.size - 1)
+                v, wt = v[j], np.full(SUMMARY_POINTS, c[-1] / SUMMARY_POINTS)
+            local[nid] = (v, wt)
+        parts = self.comm.allgather_object(local) if self.comm.is_dist else [local]
+        for nid in leaves:
+            vs = np.concatenate([p[nid][0] for p in parts])
+            ws = np.concatenate([p[nid][1] for p in parts])
+            if vs.size == 0:
+                continue
+            o = np.argsort(vs, kind="stable")
+            med = _weighted_median_sorted(vs[o], ws[o])
+            tree.leaf[nid] = float(np.float32(med) * np.float32(lr))

@@ -1,0 +1,304 @@
+"""GBDT training driver (gradient boosting and random forest).
+
+Reference: ``J/optimizer/GBDTOptimizer.java`` (init :211-335, train loop :406-480,
+doBoost :482-488, predictAndCalcLossGrad :513-609, convertModel :663-690) and
+``J/operation/GBDTOperation.java``.
+
+Device-resident design: raw test features, binned train matrix, scores, predictions,
+labels, weights and (g, h) all live in HBM for the whole run. Per round the host
+only sees the tree structure and two loss scalars.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...losses import create_loss
+from ...metrics.evaluators import EvalSet
+from ...ops import gbdt as gops
+from ...parallel.comm import Comm
+from ...utils.logging import get_logger
+from .binning import BinMapper, SamplerSpec, compute_missing_fill
+from .builder import TimeStats, TreeBuilder, TreeParams
+from .refine import TreeRefiner
+from .tree import GBDTModel, Tree
+
+
+@dataclass
+class GBDTParams:
+    round_num: int = 50
+    loss_function: str = "sigmoid"
+    class_num: int = 1
+    type: str = "gradient_boosting"  # | random_forest
+    uniform_base_prediction: float = 0.5
+    sample_dependent_base_prediction: bool = False
+    sigmoid_zmax: float = 0.0
+    lad_refine_appr: bool = True
+    eval_metric: List[str] = field(default_factory=lambda: ["auc"])
+    watch_train: bool = False
+    watch_test: bool = False
+    split_type: str = "mean"
+    missing_value: str = "value"
+    approximate: List[dict] = field(default_factory=lambda: [{"cols": "default", "type": "sample_by_quantile", "max_cnt": 255}])
+    dump_freq: int = -1
+    verbose: bool = False
+    tree: TreeParams = field(default_factory=TreeParams)
+
+
+@dataclass
+class GBDTData:
+    """One dataset shard on a device. X is raw float features (NaN = missing)."""
+    X: torch.Tensor                     # [N, F] float32
+    y: torch.Tensor                     # [N, K] float32
+    weight: Optional[torch.Tensor] = None  # [N] float32
+    init_pred: Optional[torch.Tensor] = None  # [N, K] prediction-space init (sample dependent)
+
+    @property
+    def n(self):
+        return self.X.shape[0]
+
+
+class GBDTTrainer:
+    def __init__(self, params: GBDTParams, train: GBDTData, test: Optional[GBDTData] = None,
+                 comm: Optional[Comm] = None, feature_names: Optional[Sequence[str]] = None,
+                 model: Optional[GBDTModel] = None, log=None, profile: bool = False):
+        self.p = params
+        self.comm = comm or Comm.local(train.X.device)
+        self.dev = train.X.device
+        self.train_data = train
+        self.test_data = test
+        self.F = train.X.shape[1]
+        self.K = params.class_num
+        self.feature_names = list(feature_names) if feature_names is not None else [str(i) for i in range(self.F)]
+        self.log = log or get_logger(self.comm)
+        self.loss = create_loss(params.loss_function)
+        if params.loss_function.lower().startswith("sigmoid"):
+            self.loss.set_param(sigmoid_zmax=params.sigmoid_zmax)
+        self.rf = params.type == "random_forest"
+        self.model = model or GBDTModel(params.uniform_base_prediction, self.K, self.loss.name)
+        self.profile = profile
+        self.kernel_loss = self.loss.gbdt_kernel_id
+        self.time_stats = TimeStats()
+        self._prepared = False
+
+    # ------------------------------------------------------------ preparation
+    def _specs(self) -> List[SamplerSpec]:
+        default = SamplerSpec()
+        per_col = {}
+        name2idx = {n: i for i, n in enumerate(self.feature_names)}
+        for ent in self.p.approximate:
+            spec = SamplerSpec.from_dict(ent)
+            cols = str(ent.get("cols", "default"))
+            if cols == "default":
+                default = spec
+            else:
+                for c in cols.split(","):
+                    c = c.strip()
+                    if c in name2idx:
+                        per_col[name2idx[c]] = spec
+        return [per_col.get(i, default) for i in range(self.F)]
+
+    def _base_score(self, data: GBDTData) -> torch.Tensor:
+        base = float(np.float32(self.loss.pred2score(self.p.uniform_base_prediction)))
+        init = torch.full((data.n, self.K), base, dtype=torch.float32, device=self.dev)
+        if self.p.sample_dependent_base_prediction and data.init_pred is not None:
+            ip = data.init_pred.double()
+            init += self.loss.pred2score(ip).float()
+        return init
+
+    def prepare(self):
+        t0 = time.perf_counter()
+        tr = self.train_data
+        # missing values (FillMissingValue): computed on train, applied to train/test
+        self.missing_fill = compute_missing_fill(tr.X, tr.weight, self.p.missing_value, self.comm)
+        fill = torch.from_numpy(self.missing_fill).to(self.dev)
+        Xf = torch.where(torch.isnan(tr.X), fill[None, :], tr.X)
+        self.mapper = BinMapper.fit(Xf, tr.weight, self._specs(), self.comm, self.p.split_type,
+                                    seed=self.p.tree.seed)
+        self.bins = self.mapper.transform(Xf)
+        del Xf
+        self.B = self.mapper.hist_bins()
+        self.builder = TreeBuilder(self.bins, self.F, self.B, self.mapper.nbins, self.p.tree,
+                                   self.comm, profile=self.profile)
+        N = tr.n
+        self.score = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
+        self.init_score = self._base_score(tr)
+        self.pred = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
+        self.gh = torch.zeros((self.K, N, 2), dtype=torch.float32, device=self.dev)
+        self.y = tr.y.contiguous()
+        self.w = tr.weight.contiguous() if tr.weight is not None else None
+        self.train_wsum = float(self.comm.allreduce_scalars([float(tr.weight.sum()) if tr.weight is not None else float(N)])[0])
+        self.train_real = float(self.comm.allreduce_scalars([float(N)])[0])
+        if self.test_data is not None:
+            te = self.test_data
+            self.Xte = torch.where(torch.isnan(te.X), fill[None, :], te.X).contiguous()
+            self.te_score = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
+            self.te_init = self._base_score(te)
+            self.te_pred = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
+            self.te_gh = torch.zeros((self.K, te.n, 2), dtype=torch.float32, device=self.dev)
+            self.te_wsum = float(self.comm.allreduce_scalars([float(te.weight.sum()) if te.weight is not None else float(te.n)])[0])
+            self.te_real = float(self.comm.allreduce_scalars([float(te.n)])[0])
+        self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
+        self.eval_train = EvalSet(self.p.eval_metric, self.comm)
+        self.eval_test = EvalSet(self.p.eval_metric, self.comm)
+        # continue-train: replay loaded trees on train/test scores
+        if self.model.trees:
+            self._replay_loaded_trees()
+        self._prepared = True
+        self.prep_time = time.perf_counter() - t0
+        nb = self.mapper.nbins
+        self.log.info(f"[GBDT] generate sorted global feature bins complete! feature dim:{self.F}, "
+                      f"total feature bin cnt:{int(nb.sum())}")
+
+    def _replay_loaded_trees(self):
+        """continue_train: score existing trees with raw features (isOriginTree)."""
+        name2idx = {n: i for i, n in enumerate(self.feature_names)}
+        for t in self.model.trees:
+            t.update_feature_index(name2idx)
+        fl = {k: torch.from_numpy(v).to(self.dev) for k, v in self.model.flatten().items()}
+        fill = torch.from_numpy(self.missing_fill).to(self.dev)
+        Xf = torch.where(torch.isnan(self.train_data.X), fill[None, :], self.train_data.X).contiguous()
+        gops.forest_predict(Xf, fl, self.score, 1.0)
+        if self.test_data is not None:
+            gops.forest_predict(self.Xte, fl, self.te_score, 1.0)
+
+    # ------------------------------------------------------------ loss / grad
+    def _score_div(self, rounds_done: int) -> float:
+        if self.rf:
+            return float(rounds_done if rounds_done > 0 else 1)
+        return 1.0
+
+    def _loss_grad(self, score, init, y, w, pred, gh, rounds_done, want_grad=True):
+        div = self._score_div(rounds_done)
+        if self.kernel_loss is not None:
+            param = self.p.sigmoid_zmax if self.kernel_loss == "sigmoid" else getattr(self.loss, "delta", 0.0)
+            return gops.grad_hess(score, init, y, w, self.kernel_loss, param, div, pred, gh, want_grad)
+        # generic loss (torch on device): GBDT derivative from the float prediction
+        z = score.double() / div + init.double()
+        yy = y.double()
+        ww = w.double() if w is not None else torch.ones(score.shape[0], dtype=torch.float64, device=score.device)
+        if self.loss.multi:
+            lv = self.loss.loss(z, yy)
+            p = self.loss.predict(z)
+        else:
+            lv = self.loss.loss(z[:, 0], yy[:, 0])[:, None]
+            p = self.loss.predict(z)
+        pred.copy_(p.float())
+        if want_grad:
+            g, h = self.loss.fast_deriv(pred.double(), yy)
+            gh[:, :, 0] = (g * ww[:, None]).float().t()
+            gh[:, :, 1] = (h * ww[:, None]).float().t()
+        return torch.stack([(lv.reshape(lv.shape[0], -1).sum(1) * ww).sum(), ww.sum()])
+
+    # ------------------------------------------------------------------ train
+    def train(self, rounds: Optional[int] = None, on_round: Optional[Callable[[int, "GBDTTrainer"], None]] = None,
+              dump_cb: Optional[Callable[[int], None]] = None):
+        if not self._prepared:
+            self.prepare()
+        p = self.p
+        total_rounds = p.round_num if rounds is None else rounds
+        cur = len(self.model.trees) // self.K
+        self.log.info(f"gbdt start train! total round_num={total_rounds}, current round_num={cur}")
+        # initial prediction + gradients (initPred)
+        self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, cur)
+        if self.test_data is not None:
+            te = self.test_data
+            self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh, cur, False)
+        start = time.perf_counter()
+        for i in range(cur, total_rounds):
+            self.step(i)
+            if on_round is not None:
+                on_round(i, self)
+            if dump_cb is not None and p.dump_freq != 0 and ((i + 1) % p.dump_freq == 0):
+                dump_cb(i)
+            if self.p.verbose or self.log.enabled_for_round(i):
+                cost = time.perf_counter() - start
+                self.log.info(f"[model=gbdt] [loss={self.loss.name}] [iter={i + 1}]  {cost:.5f} sec elapse\n"
+                              f"{self.last_report}")
+        self.total_train_time = time.perf_counter() - start
+        final = self.final_eval()
+        self.log.info(f"training end, {self.total_train_time:.5f} sec in all\n{final}")
+        return self.model
+
+    def step(self, i: int) -> str:
+        """One boosting round: K trees, score update, loss + next gradients."""
+        lr = 1.0 if self.rf else self.p.tree.learning_rate
+        self.builder.p.learning_rate = lr
+        new_trees = []
+        for k in range(self.K):
+            tree = self.builder.build(self.gh[k])
+            if self.refiner is not None:
+                self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
+                                    + self.init_score[:, k], self.w, lr)
+            gops.tree_add_bins(self.bins, tuple(torch.from_numpy(a).to(self.dev) for a in tree.bin_arrays()),
+                               self.score, k)
+            new_trees.append(tree)
+        # loss on train after this round + gradients for the next
+        acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
+        # convert model (slot -> raw threshold, names, default direction)
+        for tree in new_trees:
+            tree.convert_split_values(self.mapper.cands, self.p.split_type)
+            tree.add_feature_names(self.feature_names)
+            tree.add_default_direction(self.missing_fill)
+            self.model.trees.append(tree)
+        report = []
+        if self.test_data is not None:
+            fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
+            fl.trees = new_trees
+            flat = {k: torch.from_numpy(v).to(self.dev) for k, v in fl.flatten().items()}
+            gops.forest_predict(self.Xte, flat, self.te_score, 1.0)
+            te = self.test_data
+            acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
+                                     i + 1, False)
+            both = torch.stack([acc, acc_te]).cpu()
+            if self.comm.is_dist:
+                self.comm.allreduce_(both)
+            tr_loss = float(both[0, 0]) / max(self.train_wsum, 1e-300)
+            te_loss = float(both[1, 0]) / max(self.te_wsum, 1e-300)
+        else:
+            a = acc.cpu()
+            if self.comm.is_dist:
+                self.comm.allreduce_(a)
+            tr_loss = float(a[0]) / max(self.train_wsum, 1e-300)
+            te_loss = None
+        from ...utils.javafmt import java_double_str as jd
+        report.append(f"train loss = {jd(tr_loss)}\n")
+        if self.p.watch_train:
+            report.append(self._eval_str(True))
+        if te_loss is not None:
+            report.append(f"test loss = {jd(te_loss)}\n")
+            if self.p.watch_test:
+                report.append(self._eval_str(False))
+        self.last_train_loss = tr_loss
+        self.last_test_loss = te_loss
+        self.last_report = "".join(report)
+        return self.last_report
+
+    def _info(self):
+        if self.loss.name == "sigmoid":
+            return (2, False)
+        if self.loss.name == "softmax":
+            return (self.K, True)
+        return None
+
+    def _eval_str(self, train: bool) -> str:
+        if train:
+            wr = abs(self.train_wsum - self.train_real) > 1e-6
+            return self.eval_train.eval(self.y, self.pred, self.w, "train", wr, self._info())
+        te = self.test_data
+        wr = abs(self.te_wsum - self.te_real) > 1e-6
+        return self.eval_test.eval(te.y, self.te_pred, te.weight, "test", wr, self._info())
+
+    def final_eval(self) -> str:
+        s = self._eval_str(True)
+        if self.test_data is not None:
+            s += self._eval_str(False)
+        return s
+
+    def feature_importance(self):
+        return self.model.feature_importance()

@@ -1,0 +1,374 @@
+"""GBDT device ops.
+
+Each op takes torch tensors. Tensors on the GPU go to the hand-written HIP
+kernels in ``csrc/hip/gbdt_kernels.hip`` (no fallback: a missing extension
+raises). CPU tensors use a plain PyTorch/NumPy implementation of the same
+semantics; that path is the numerics reference for the kernel tests and the
+engine for CPU-only (gloo) runs.
+
+Reference semantics are cited in the kernel file header.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._ext import check_cuda, hip, ptr, stream
+
+SPLIT_DTYPE = np.dtype(
+    [("loss_chg", "<f4"), ("feat", "<i4"), ("bin_a", "<i4"), ("bin_b", "<i4"),
+     ("gl", "<f8"), ("hl", "<f8"), ("g", "<f8"), ("h", "<f8")]
+)
+assert SPLIT_DTYPE.itemsize == 48
+
+LOSS_IDS = {"sigmoid": 0, "l2": 1, "l1": 2, "poisson": 3, "huber": 4, "softmax": 5}
+
+
+def _bin_bytes(bins: torch.Tensor) -> int:
+    if bins.dtype == torch.uint8:
+        return 1
+    if bins.dtype == torch.int16:
+        return 2
+    raise ValueError(f"bins must be uint8 or int16, got {bins.dtype}")
+
+
+# ---------------------------------------------------------------------------
+# histogram build
+# ---------------------------------------------------------------------------
+def hist_build(bins, F, gh, rows, work, hist, B):
+    """Accumulate (g, h) histograms.
+
+    bins: [N, S] uint8/int16 row-major (S >= F, S % 32 == 0 for the LDS path)
+    gh:   [N, 2] float32
+    rows: int32 row permutation or None (identity positions)
+    work: int32 [nwork, 4] = (slot, begin, end, 0); positions index ``rows``
+    hist: float32 [slots, B, F, 2], target slots must be zeroed by the caller
+    """
+    nwork = work.shape[0]
+    if nwork == 0:
+        return
+    if bins.is_cuda:
+        check_cuda(bins, gh, rows, work, hist)
+        assert hist.shape[1] == B and hist.shape[2] == F and hist.shape[3] == 2
+        assert gh.shape[0] == bins.shape[0] and gh.shape[1] == 2
+        stride = bins.shape[1]
+        h = hip()
+        if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
+            h.hist_u8(ptr(bins), stride, F, ptr(gh), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                      stream(bins))
+        else:
+            h.hist_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(gh), ptr(rows), ptr(work),
+                          nwork, ptr(hist), B, stream(bins))
+        return
+    # CPU reference
+    w = work.numpy() if not work.is_cuda else work.cpu().numpy()
+    hv = hist.view(-1, 2)
+    for slot, b, e, _ in w:
+        if e <= b:
+            continue
+        r = rows[b:e].long() if rows is not None else torch.arange(b, e, dtype=torch.long)
+        bb = bins[r, :F].long() & (0xFFFF if bins.dtype == torch.int16 else 0xFF)
+        idx = (int(slot) * B + bb) * F + torch.arange(F, dtype=torch.long)[None, :]
+        v = gh[r][:, None, :].expand(-1, F, 2)
+        hv.index_add_(0, idx.reshape(-1), v.reshape(-1, 2))
+
+
+# ---------------------------------------------------------------------------
+# split finding
+# ---------------------------------------------------------------------------
+def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
+    """Best split per item. items int32 [n, 4] = (slot, parent, sibling, derived).
+
+    Returns a uint8 tensor [n, 48] (view with SPLIT_DTYPE after moving to host).
+    Derived items also write their (parent - sibling) histogram into ``slot``.
+    """
+    n = items.shape[0]
+    mcw, l1, l2, mal = (float(params[k]) for k in ("mcw", "l1", "l2", "max_abs_leaf"))
+    if hist.is_cuda:
+        out = torch.empty((n, 48), dtype=torch.uint8, device=hist.device)
+        if n == 0:
+            return out
+        check_cuda(hist, nbins_f, fmask, items)
+        hip().split_find(ptr(hist), B, F, ptr(nbins_f), ptr(fmask), int(f0), ptr(items), n,
+                         ptr(out), mcw, l1, l2, mal, stream(hist))
+        return out
+    res = np.zeros(n, dtype=SPLIT_DTYPE)
+    it = items.numpy()
+    nb = nbins_f.numpy()
+    fm = fmask.numpy().astype(bool)
+    for i, (slot, par, sib, der) in enumerate(it):
+        if der:
+            hist[slot] = hist[par] - hist[sib]
+        hn = hist[slot].numpy()  # [B, F, 2] float32
+        res[i] = _split_one_cpu(hn, nb, fm, int(f0), mcw, l1, l2, mal)
+    return torch.from_numpy(res.view(np.uint8).reshape(n, 48).copy())
+
+
+def _thr_l1(w, lam):
+    return np.where(w > lam, w - lam, np.where(w < -lam, w + lam, 0.0))
+
+
+def node_value_np(g, h, mcw, l1, l2, mal):
+    g = np.asarray(g, dtype=np.float64)
+    h = np.asarray(h, dtype=np.float64)
+    v = (-g / (h + l2)) if l1 == 0.0 else (-_thr_l1(g, l1) / (h + l2))
+    if mal > 0:
+        v = np.clip(v, -mal, mal)
+    return np.where(h < mcw, 0.0, v)
+
+
+def calc_gain_np(g, h, mcw, l1, l2, mal):
+    g = np.asarray(g, dtype=np.float64)
+    h = np.asarray(h, dtype=np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if mal <= 0:
+            t = g if l1 == 0.0 else _thr_l1(g, l1)
+            gain = t * t / (h + l2)
+        else:
+            v = node_value_np(g, h, mcw, l1, l2, mal)
+            gain = -2.0 * (g * v + 0.5 * (h + l2) * v * v + l1 * np.abs(v))
+    return np.where(h < mcw, 0.0, gain)
+
+
+def _split_one_cpu(hn, nb, fm, f0, mcw, l1, l2, mal):
+    Bn, Fn, _ = hn.shape
+    hd = hn.astype(np.float64)
+    G = float(hd[: nb[f0], f0, 0].sum())
+    H = float(hd[: nb[f0], f0, 1].sum())
+    root_gain = np.float32(calc_gain_np(G, H, mcw, l1, l2, mal))
+    best = (-np.inf, 1 << 30, 1 << 30)
+    rec = (np.float32(-np.inf), -1, -1, -1, 0.0, 0.0)
+    for f in range(Fn):
+        if not fm[f]:
+            continue
+        m = min(nb[f], Bn)
+        g = hd[:m, f, 0]
+        h = hd[:m, f, 1]
+        ne = (hn[:m, f, 0] != 0) | (hn[:m, f, 1] != 0)
+        pg = np.concatenate([[0.0], np.cumsum(g)[:-1]])  # exclusive prefix
+        ph = np.concatenate([[0.0], np.cumsum(h)[:-1]])
+        idx = np.where(ne, np.arange(m), -1)
+        lastne = np.maximum.accumulate(idx) if m else idx
+        prev = np.concatenate([[-1], lastne[:-1]])
+        ok = ne & (prev >= 0) & (ph != 0.0) & (ph >= mcw)
+        rg, rh = G - pg, H - ph
+        ok &= rh >= mcw
+        if not ok.any():
+            continue
+        chg = (calc_gain_np(pg, ph, mcw, l1, l2, mal) + calc_gain_np(rg, rh, mcw, l1, l2, mal)
+               - np.float64(root_gain)).astype(np.float32)
+        chg = np.where(ok, chg, np.float32(-np.inf))
+        j = int(np.argmax(chg))  # first max -> lowest bin
+        c = chg[j]
+        if (c > best[0]) or (c == best[0] and f < best[1]):
+            best = (c, f, j)
+            rec = (np.float32(c), f, int(prev[j]), j, float(pg[j]), float(ph[j]))
+    out = np.zeros((), dtype=SPLIT_DTYPE)
+    out["loss_chg"], out["feat"], out["bin_a"], out["bin_b"], out["gl"], out["hl"] = rec
+    out["g"], out["h"] = G, H
+    return out
+
+
+# ---------------------------------------------------------------------------
+# partition
+# ---------------------------------------------------------------------------
+def partition(bins, rows, rows_out, items, feat, thr, node_begin, first_blk, nblk, n_split):
+    """Stable partition of node segments; returns left counts (int32 [n_split]).
+
+    items int32 [nblk_total, 4] = (split_idx, begin, end, blk_in_node).
+    """
+    if bins.is_cuda:
+        left = torch.zeros(n_split, dtype=torch.int32, device=bins.device)
+        nitems = items.shape[0]
+        if nitems == 0:
+            return left
+        check_cuda(bins, rows, rows_out, items, feat, thr, node_begin, first_blk, nblk)
+        counts = torch.empty(nitems, dtype=torch.int32, device=bins.device)
+        hip().partition(ptr(bins), _bin_bytes(bins), bins.shape[1], ptr(rows), ptr(rows_out),
+                        ptr(items), nitems, ptr(feat), ptr(thr), ptr(node_begin), ptr(first_blk),
+                        ptr(nblk), ptr(counts), ptr(left), stream(bins))
+        return left
+    left = torch.zeros(n_split, dtype=torch.int32)
+    nbv, fv, tv, nb_ = node_begin.numpy(), feat.numpy(), thr.numpy(), nblk.numpy()
+    fb = first_blk.numpy()
+    it = items.numpy()
+    mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
+    for i in range(n_split):
+        if nb_[i] == 0:
+            continue
+        b = int(it[fb[i], 1])
+        e = int(it[fb[i] + nb_[i] - 1, 2])
+        assert b == nbv[i]
+        r = rows[b:e]
+        go = (bins[r.long(), int(fv[i])].long() & mask) <= int(tv[i])
+        lft, rgt = r[go], r[~go]
+        rows_out[b:b + lft.numel()] = lft
+        rows_out[b + lft.numel():e] = rgt
+        left[i] = lft.numel()
+    return left
+
+
+# ---------------------------------------------------------------------------
+# scoring
+# ---------------------------------------------------------------------------
+def tree_add_bins(bins, tree_arrays, score, col):
+    """score[:, col] += value(leaf(row)) traversing a bin-threshold tree."""
+    tfeat, tthr, tleft, tright, tval = tree_arrays
+    N = bins.shape[0]
+    if bins.is_cuda:
+        check_cuda(bins, tfeat, tthr, tleft, tright, tval, score)
+        hip().tree_add_bins(ptr(bins), _bin_bytes(bins), bins.shape[1], N, ptr(tfeat), ptr(tthr),
+                            ptr(tleft), ptr(tright), ptr(tval), tfeat.shape[0], ptr(score),
+                            score.shape[1], col, stream(bins))
+        return
+    node = torch.zeros(N, dtype=torch.long)
+    tf, tt, tl, tr = (t.long() for t in (tfeat, tthr, tleft, tright))
+    mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
+    ar = torch.arange(N)
+    for _ in range(64):
+        f = tf[node]
+        active = f >= 0
+        if not bool(active.any()):
+            break
+        b = bins[ar, f.clamp(min=0)].long() & mask
+        nxt = torch.where(b <= tt[node], tl[node], tr[node])
+        node = torch.where(active, nxt, node)
+    score[:, col] += tval[node]
+
+
+def forest_predict(X, forest, out, scale=1.0, leaf_out=None):
+    """out[:, tout[t]] += scale * leaf_value(tree t, row) over raw float features.
+
+    forest: dict of tensors nfeat, nthr, nleft, nright, ndefl (uint8), nval, troot, tout.
+    With ``leaf_out`` (int32 [N, T]) writes per-tree leaf indices instead.
+    """
+    T = forest["troot"].shape[0]
+    N = X.shape[0]
+    if X.is_cuda:
+        check_cuda(X, out, leaf_out, *forest.values())
+        hip().forest_predict(ptr(X), X.shape[1], N, ptr(forest["nfeat"]), ptr(forest["nthr"]),
+                             ptr(forest["nleft"]), ptr(forest["nright"]), ptr(forest["ndefl"]),
+                             ptr(forest["nval"]), ptr(forest["troot"]), ptr(forest["tout"]), T,
+                             ptr(out), out.shape[1] if out is not None else 0, float(scale),
+                             ptr(leaf_out), stream(X))
+        return
+    nf = forest["nfeat"].long()
+    nt = forest["nthr"]
+    nl = forest["nleft"].long()
+    nr = forest["nright"].long()
+    nd = forest["ndefl"].bool()
+    nv = forest["nval"]
+    ar = torch.arange(N)
+    for t in range(T):
+        root = int(forest["troot"][t])
+        node = torch.full((N,), root, dtype=torch.long)
+        for _ in range(1 << 12):
+            f = nf[node]
+            active = f >= 0
+            if not bool(active.any()):
+                break
+            v = X[ar, f.clamp(min=0)]
+            left = torch.where(torch.isnan(v), nd[node], v <= nt[node])
+            node = torch.where(active, torch.where(left, nl[node], nr[node]), node)
+        if leaf_out is not None:
+            leaf_out[:, t] = (node - root).int()
+        else:
+            out[:, int(forest["tout"][t])] += scale * nv[node]
+
+
+# ---------------------------------------------------------------------------
+# binning
+# ---------------------------------------------------------------------------
+def bin_assign(X, cand, coff, out):
+    """Nearest-candidate bin id per element (FeatureApprData semantics)."""
+    N, F = X.shape
+    if X.is_cuda:
+        check_cuda(X, cand, coff, out)
+        hip().bin_assign(ptr(X), X.shape[1], N, F, ptr(cand), ptr(coff), ptr(out),
+                         _bin_bytes(out), out.shape[1], stream(X))
+        return
+    co = coff.numpy()
+    for f in range(F):
+        c = cand[co[f]:co[f + 1]]
+        n = c.numel()
+        if n <= 1:
+            out[:, f] = 0
+            continue
+        x = X[:, f].contiguous()
+        # index of first candidate > x  (== lo in the binary search)
+        lo = torch.searchsorted(c, x, right=True)
+        u = (lo - 1).clamp(min=0)
+        eq = c[u] == x
+        idx = torch.where(eq, u, lo.clamp(max=n - 1))
+        prevv = c[(idx - 1).clamp(min=0)]
+        down = (idx >= 1) & (x < (c[idx] + prevv) * 0.5)
+        idx = torch.where(down, idx - 1, idx)
+        idx = torch.where(x > c[n - 1], torch.full_like(idx, n - 1), idx)
+        out[:, f] = idx.to(out.dtype)
+
+
+# ---------------------------------------------------------------------------
+# gradients
+# ---------------------------------------------------------------------------
+def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True):
+    """Fill pred [N,K] and gh [K,N,2]; return (weighted loss sum, weight sum) as a
+    float64 tensor of shape [2] on the data device (no host sync)."""
+    N, K = score.shape
+    loss_id = LOSS_IDS[loss]
+    if score.is_cuda:
+        check_cuda(score, init, label, weight, pred, gh)
+        acc = torch.zeros(2, dtype=torch.float64, device=score.device)
+        hip().grad_hess(ptr(score), ptr(init), ptr(label), ptr(weight), N, K, loss_id,
+                        float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
+                        1 if want_grad else 0, stream(score))
+        return acc
+    z = score.double() / score_div + init.double()
+    y = label.double()
+    w = weight.double() if weight is not None else torch.ones(N, dtype=torch.float64)
+    if loss_id == 5:
+        lse = torch.logsumexp(z, dim=1, keepdim=True)
+        p = torch.exp(z - lse)
+        lv = -(y * (z - lse)).sum(1)
+        g = p - y
+        h = 2.0 * p * (1.0 - p)
+    else:
+        z1, y1 = z[:, 0], y[:, 0]
+        if loss_id == 0:
+            lv = torch.where(z1 >= 0, torch.log1p(torch.exp(-z1)) + z1 * (1 - y1),
+                             torch.log1p(torch.exp(z1)) - z1 * y1)
+            p = torch.sigmoid(z1).float().double()
+            g = p - y1
+            h = p * (1 - p)
+            if param != 0:
+                zz = torch.where(h != 0, -(g / h), torch.zeros_like(h))
+                h = torch.where(zz > param, -(g / param), torch.where(zz < -param, -(g / -param), h))
+        elif loss_id == 1:
+            lv = 0.5 * (y1 - z1) ** 2
+            p = z1.float().double()
+            g = p - y1
+            h = torch.ones_like(p)
+        elif loss_id == 2:
+            lv = (y1 - z1).abs()
+            p = z1.float().double()
+            g = torch.sign(p - y1)
+            h = torch.ones_like(p)
+        elif loss_id == 3:
+            zc = torch.clamp(z1, max=30.0)
+            lv = -y1 * z1 + torch.exp(zc) + torch.lgamma(y1 + 1)
+            p = torch.exp(zc).float().double()
+            g = p - y1
+            h = p
+        else:
+            a = z1 - y1
+            d = float(param)
+            lv = torch.where(a.abs() <= d, 0.5 * a * a, d * (a.abs() - 0.5 * d))
+            p = z1.float().double()
+            aa = p - y1
+            g = torch.where(aa.abs() <= d, aa, torch.sign(aa) * d)
+            h = torch.zeros_like(p)
+        p, g, h = p[:, None], g[:, None], h[:, None]
+    pred.copy_(p.float())
+    if want_grad:
+        gh[:, :, 0] = (g * w[:, None]).float().t()
+        gh[:, :, 1] = (h * w[:, None]).float().t()
+    return torch.tensor([float((w * lv).sum()), float(w.sum())], dtype=torch.float64)

@@ -1,0 +1,165 @@
+"""Communicator facade (replaces the reference's external ytk-mp4j ThreadCommSlave).
+
+Reference call surface: allreduce / allreduceArray /
+reduceScatterArray / allgatherArray / allreduceMap / allreduceRpc / barrier, plus
+``info/error`` log shipping to a master (``J/utils/LogUtils.java:41-65``).
+
+MI355X-native design: one process per GPU, ``torch.distributed`` with the
+``nccl`` backend (= RCCL over xGMI on ROCm) for device tensors and ``gloo`` for
+CPU tensors / host objects. A "worker" is a rank (the reference's
+(process, thread) pairs collapse to GPUs). Map/object collectives go through
+``all_gather_object`` and a caller-supplied merge (deterministic rank order).
+With ``world_size == 1`` every collective is a no-op, so single-GPU runs pay
+nothing.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Any, Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+_OPS = {
+    "sum": dist.ReduceOp.SUM,
+    "max": dist.ReduceOp.MAX,
+    "min": dist.ReduceOp.MIN,
+}
+
+
+class Comm:
+    """Collective facade. ``Comm.local()`` is the single-worker instance."""
+
+    def __init__(self, rank: int = 0, world: int = 1, device: Optional[torch.device] = None,
+                 group=None, cpu_group=None):
+        self.rank = rank
+        self.world = world
+        self.device = device if device is not None else torch.device("cpu")
+        self.group = group
+        self.cpu_group = cpu_group
+
+    # -- construction ---------------------------------------------------------
+    @classmethod
+    def local(cls, device=None) -> "Comm":
+        return cls(0, 1, torch.device(device) if device is not None else None)
+
+    @classmethod
+    def from_env(cls, device: Optional[str] = None, timeout_s: int = 1800) -> "Comm":
+        """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
+
+        device: "cuda", "cpu" or None (auto: cuda if available).
+        """
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device == "cuda":
+            torch.cuda.set_device(local_rank)
+            dev = torch.device("cuda", local_rank)
+        else:
+            dev = torch.device("cpu")
+        if world <= 1:
+            return cls(0, 1, dev)
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            backend = "nccl" if dev.type == "cuda" else "gloo"
+            kw = {}
+            if dev.type == "cuda":
+                kw["device_id"] = dev
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        group = dist.group.WORLD
+        cpu_group = group
+        if dev.type == "cuda":
+            cpu_group = dist.new_group(backend="gloo")
+        return cls(dist.get_rank(), dist.get_world_size(), dev, group, cpu_group)
+
+    @property
+    def is_dist(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+    # -- tensor collectives -----------------------------------------------------
+    def allreduce_(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):
+        """In-place allreduce (RCCL for device tensors, gloo for host tensors)."""
+        if not self.is_dist:
+            return None
+        g = self.group if t.device.type == "cuda" else self.cpu_group
+        return dist.all_reduce(t, op=_OPS[op], group=g, async_op=async_op)
+
+    def allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        t = t.clone()
+        self.allreduce_(t, op)
+        return t
+
+    def allreduce_scalars(self, values, op: str = "sum", dtype=torch.float64) -> List[float]:
+        """Batch several scalars into one collective (reference issues one each)."""
+        t = torch.tensor(list(values), dtype=dtype)
+        if self.is_dist:
+            dist.all_reduce(t, op=_OPS[op], group=self.cpu_group)
+        return t.tolist()
+
+    def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
+        if not self.is_dist:
+            out.copy_(inp.view_as(out) if inp.numel() == out.numel() else inp[: out.numel()])
+            return
+        dist.reduce_scatter_tensor(out, inp, op=_OPS[op], group=self.group)
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate equal-size shards along dim 0."""
+        if not self.is_dist:
+            return t.clone()
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                          device=t.device)
+        g = self.group if t.device.type == "cuda" else self.cpu_group
+        dist.all_gather_into_tensor(out, t.contiguous(), group=g)
+        return out
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if not self.is_dist:
+            return
+        g = self.group if t.device.type == "cuda" else self.cpu_group
+        dist.broadcast(t, src=src, group=g)
+
+    def barrier(self):
+        if self.is_dist:
+            dist.barrier(group=self.cpu_group)
+
+    # -- object collectives ---------------------------------------------------
+    def allgather_object(self, obj: Any) -> List[Any]:
+        if not self.is_dist:
+            return [obj]
+        out: List[Any] = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.cpu_group)
+        return out
+
+    def allreduce_object(self, obj: Any, merge: Callable[[Any, Any], Any]) -> Any:
+        """allreduceMap / allreduceRpc equivalent: fold objects in rank order."""
+        objs = self.allgather_object(obj)
+        acc = objs[0]
+        for o in objs[1:]:
+            acc = merge(acc, o)
+        return acc
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.is_dist:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.cpu_group)
+        return lst[0]
+
+    # -- even partition helper (CommUtils.createThreadArrayFroms/Tos) ---------
+    def shard_range(self, dim: int, rank: Optional[int] = None):
+        r = self.rank if rank is None else rank
+        base, rem = divmod(dim, self.world)
+        start = r * base + min(r, rem)
+        return start, start + base + (1 if r < rem else 0)
+
+    def close(self):
+        if self.is_dist and dist.is_initialized():
+            dist.destroy_process_group()
