@@ -1,0 +1,195 @@
+// Stable partition of tree-node row segments (gfx950 / CDNA4, wave64).
+//
+// Reference semantics: J/data/gbdt/SamplePositionData.java:115-165 -- after a
+// split every row of the node goes left iff bin <= cond; left rows first, in
+// their previous order, then right rows.
+//
+// Design (two launches per level, all split nodes batched):
+//  1. flags: one pass over each node segment: row id (coalesced) + ONE BYTE from the
+//     COLUMN-MAJOR copy of the bin matrix (binsT[f][row]: neighbouring positions of a
+//     node hit neighbouring bytes of the same column instead of 32-B-strided rows),
+//     writes a 1-byte go-left flag per position and a per-block left count.
+//  2. scatter: coalesced reads of flags / row ids / (g,h) in position order,
+//     4 sub-tiles of 256 positions per step, wave ballots + one LDS scan of the
+//     16 (sub-tile, wave) counts -> stable destinations; writes the row id AND the
+//     (g,h) pair so the next level's histogram reads (g,h) contiguously.
+// items[blk] = {split_idx, begin, end, blk_in_node}
+#include "common.h"
+
+namespace ytk {
+
+constexpr int kPartThreads = 256;
+constexpr int kPartSub = 4;
+
+template <typename BinT>
+__global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
+    const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
+    const int4* __restrict__ items, const int* __restrict__ feat, const int* __restrict__ thr,
+    uint8_t* __restrict__ flags, int* __restrict__ counts) {
+  __shared__ int s_cnt[kPartThreads / kWave];
+  const int4 it = items[blockIdx.x];
+  const BinT* col = binsT + (size_t)feat[it.x] * ncol;
+  const int t = thr[it.x];
+  int c = 0;
+  int pos = it.y + threadIdx.x;
+  for (; pos + 3 * kPartThreads < it.z; pos += 4 * kPartThreads) {
+    int r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = rows[pos + j * kPartThreads];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint8_t fl = (int)col[(unsigned)r[j]] <= t;
+      flags[pos + j * kPartThreads] = fl;
+      c += fl;
+    }
+  }
+  for (; pos < it.z; pos += kPartThreads) {
+    const uint8_t fl = (int)col[(unsigned)rows[pos]] <= t;
+    flags[pos] = fl;
+    c += fl;
+  }
+  c = wave_sumi(c);
+  if (lane_id() == 0) s_cnt[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+__global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
+    const uint8_t* __restrict__ flags, const int* __restrict__ rows,
+    const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
+    const int4* __restrict__ items, const int* __restrict__ node_begin,
+    const int* __restrict__ first_blk, const int* __restrict__ nblk,
+    const int* __restrict__ counts, int* __restrict__ left_total_out) {
+  constexpr int NW = kPartThreads / kWave;
+  __shared__ int s_red[2 * NW];
+  __shared__ int s_l[kPartSub * NW], s_v[kPartSub * NW];
+  const int4 it = items[blockIdx.x];
+  const int si = it.x;
+  const int nbeg = node_begin[si], fb = first_blk[si], nb = nblk[si];
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+
+  int before = 0, total = 0;
+  for (int j = tid; j < nb; j += kPartThreads) {
+    const int c = counts[fb + j];
+    total += c;
+    if (fb + j < (int)blockIdx.x) before += c;
+  }
+  before = wave_sumi(before);
+  total = wave_sumi(total);
+  if (l == 0) { s_red[wid] = before; s_red[NW + wid] = total; }
+  __syncthreads();
+  before = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) { before += s_red[w]; total += s_red[NW + w]; }
+  if (it.w == 0 && tid == 0) left_total_out[si] = total;
+
+  int lbase = nbeg + before;
+  int rbase = nbeg + total + (it.y - nbeg - before);
+  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  for (int tile = it.y; tile < it.z; tile += kPartSub * kPartThreads) {
+    int r[kPartSub];
+    float2 g[kPartSub];
+    bool valid[kPartSub], left[kPartSub];
+#pragma unroll
+    for (int j = 0; j < kPartSub; ++j) {
+      const int pos = tile + j * kPartThreads + tid;
+      valid[j] = pos < it.z;
+      left[j] = false;
+      r[j] = 0;
+      g[j] = make_float2(0.f, 0.f);
+      if (valid[j]) {
+        left[j] = flags[pos] != 0;
+        r[j] = rows[pos];
+        g[j] = ghp[pos];
+      }
+    }
+    int lrank[kPartSub], vrank[kPartSub];
+#pragma unroll
+    for (int j = 0; j < kPartSub; ++j) {
+      const unsigned long long lm = __ballot(left[j]);
+      const unsigned long long vm = __ballot(valid[j]);
+      lrank[j] = __popcll(lm & lt_mask);
+      vrank[j] = __popcll(vm & lt_mask);
+      if (l == 0) { s_l[j * NW + wid] = __popcll(lm); s_v[j * NW + wid] = __popcll(vm); }
+    }
+    __syncthreads();
+    int tl = 0, tv = 0;
+    int pl[kPartSub], pv[kPartSub];
+#pragma unroll
+    for (int j = 0; j < kPartSub; ++j) { pl[j] = 0; pv[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < kPartSub * NW; ++k) {
+      const int kl = s_l[k], kv = s_v[k];
+#pragma unroll
+      for (int j = 0; j < kPartSub; ++j) {
+        if (k < j * NW + wid) { pl[j] += kl; pv[j] += kv; }
+      }
+      tl += kl;
+      tv += kv;
+    }
+#pragma unroll
+    for (int j = 0; j < kPartSub; ++j) {
+      if (valid[j]) {
+        int dst;
+        if (left[j]) dst = lbase + pl[j] + lrank[j];
+        else dst = rbase + (pv[j] - pl[j]) + (vrank[j] - lrank[j]);
+        rows_out[dst] = r[j];
+        gh_out[dst] = g[j];
+      }
+    }
+    lbase += tl;
+    rbase += tv - tl;
+    __syncthreads();  // s_l / s_v reused next tile
+  }
+}
+
+}  // namespace ytk
+
+using namespace ytk;
+
+// Count-only variant (children that become leaves immediately: their rows are never
+// read again, only the per-block left counts are needed for the node statistics).
+extern "C" void ytk_partition_count(uintptr_t binsT, int bin_bytes, long long ncol,
+                                    uintptr_t rows, uintptr_t flags, uintptr_t items, int nitems,
+                                    uintptr_t feat, uintptr_t thr, uintptr_t counts,
+                                    uintptr_t stream) {
+  if (nitems <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (bin_bytes == 1) {
+    hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+  } else {
+    hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
+                       (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+  }
+  YTK_LAUNCH_CHECK();
+}
+
+extern "C" void ytk_partition(uintptr_t binsT, int bin_bytes, long long ncol, uintptr_t rows,
+                              uintptr_t rows_out, uintptr_t ghp, uintptr_t gh_out,
+                              uintptr_t flags, uintptr_t items, int nitems, uintptr_t feat,
+                              uintptr_t thr, uintptr_t node_begin, uintptr_t first_blk,
+                              uintptr_t nblk, uintptr_t counts, uintptr_t left_total,
+                              uintptr_t stream) {
+  if (nitems <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (bin_bytes == 1) {
+    hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+  } else {
+    hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
+                       (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+  }
+  YTK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(partition_scatter_kernel, dim3(nitems), dim3(kPartThreads), 0, s,
+                     (const uint8_t*)flags, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                     (float2*)gh_out, (const int4*)items, (const int*)node_begin,
+                     (const int*)first_blk, (const int*)nblk, (const int*)counts,
+                     (int*)left_total);
+  YTK_LAUNCH_CHECK();
+}

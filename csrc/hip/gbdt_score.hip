@@ -1,0 +1,351 @@
+// GBDT scoring, binning and gradient kernels (gfx950 / CDNA4, wave64).
+//
+// Reference semantics:
+//   tree scoring (train, bin space)  J/data/gbdt/Tree.java:142-154, GBDTOptimizer.java:641-658
+//   forest inference (raw floats)    J/data/gbdt/Tree.java:114-168 (x <= cond -> left,
+//                                    missing -> default child), GBDTOnlinePredictor.java:170-270
+//   bin assignment                   J/data/gbdt/FeatureApprData.java:179-205
+//   grad / hess / loss               J/optimizer/GBDTOptimizer.java:513-609 + J/loss/*
+//
+// Design: the training-score update is FUSED with the loss/gradient pass
+// (tree_grad_kernel): one read of score/label/weight per row per round, the new
+// tree's leaf found by walking the COLUMN-MAJOR bin matrix (coalesced bytes), the
+// tree's node arrays staged in LDS, float math per row and an fp64 block sum of the
+// weighted loss.
+#include "common.h"
+
+namespace ytk {
+
+// ------------------------------------------------------------------ scoring
+template <typename BinT>
+__global__ __launch_bounds__(256) void tree_add_bins_kernel(
+    const BinT* __restrict__ binsT, long long N, const int* __restrict__ tfeat,
+    const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
+    const float* __restrict__ tval, int nnodes, float* __restrict__ score, int sstride,
+    int soff) {
+  extern __shared__ __attribute__((aligned(16))) int tsm[];
+  int* sf = tsm;
+  int* st = tsm + nnodes;
+  int* sl = tsm + 2 * nnodes;
+  int* sr = tsm + 3 * nnodes;
+  float* sv = reinterpret_cast<float*>(tsm + 4 * nnodes);
+  for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
+    sf[i] = tfeat[i]; st[i] = tthr[i]; sl[i] = tleft[i]; sr[i] = tright[i]; sv[i] = tval[i];
+  }
+  __syncthreads();
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    int n = 0;
+    while (sf[n] >= 0) n = ((int)binsT[(size_t)sf[n] * N + r] <= st[n]) ? sl[n] : sr[n];
+    score[r * sstride + soff] += sv[n];
+  }
+}
+
+// Forest inference on raw float features. Trees flattened: node arrays indexed
+// globally, troot[t], tout[t] (output column).
+__global__ __launch_bounds__(256) void forest_predict_kernel(
+    const float* __restrict__ X, long long xstride, long long N,
+    const int* __restrict__ nfeat, const float* __restrict__ nthr,
+    const int* __restrict__ nleft, const int* __restrict__ nright,
+    const uint8_t* __restrict__ ndefl, const float* __restrict__ nval,
+    const int* __restrict__ troot, const int* __restrict__ tout, int T,
+    float* __restrict__ out, int ostride, float scale, int* __restrict__ leaf_out) {
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    const float* x = X + r * xstride;
+    for (int t = 0; t < T; ++t) {
+      int n = troot[t];
+      while (nfeat[n] >= 0) {
+        const float v = x[nfeat[n]];
+        const bool left = (v != v) ? (ndefl[n] != 0) : (v <= nthr[n]);
+        n = left ? nleft[n] : nright[n];
+      }
+      if (leaf_out) leaf_out[r * T + t] = n - troot[t];
+      else out[r * ostride + tout[t]] += scale * nval[n];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ binning
+template <typename BinT>
+__global__ __launch_bounds__(256) void bin_assign_kernel(
+    const float* __restrict__ X, long long xstride, long long N, int F,
+    const float* __restrict__ cand, const int* __restrict__ coff,
+    BinT* __restrict__ out, long long ostride, BinT* __restrict__ outT) {
+  const long long total = N * F;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / F;
+    const int f = (int)(i - r * F);
+    const float* c = cand + coff[f];
+    const int n = coff[f + 1] - coff[f];
+    int idx = 0;
+    if (n > 1) {
+      const float x = X[r * xstride + f];
+      if (x > c[n - 1]) {
+        idx = n - 1;
+      } else {
+        int lo = 0, hi = n - 1;
+        while (lo <= hi) {
+          const int mid = (lo + hi) >> 1;
+          if (x >= c[mid]) lo = mid + 1; else hi = mid - 1;
+        }
+        const int u = max(0, hi);
+        idx = (c[u] == x) ? u : min(n - 1, lo);
+        if (idx >= 1 && x < (c[idx] + c[idx - 1]) * 0.5f) idx -= 1;
+      }
+    }
+    out[r * ostride + f] = (BinT)idx;
+    if (outT) outT[(size_t)f * N + r] = (BinT)idx;
+  }
+}
+
+// ------------------------------------------------------------------ loss / grad
+// loss ids: 0 sigmoid, 1 l2, 2 l1, 3 poisson, 4 huber(delta=p0), 5 softmax (K>1)
+struct LossOut {
+  float p, g, h;
+  double l;
+};
+
+__device__ __forceinline__ LossOut point_loss(int loss_id, float z, float y, float p0) {
+  LossOut o;
+  switch (loss_id) {
+    case 0: {  // sigmoid (SigmoidFunction: stable log-loss, zmax hessian clamp)
+      const float az = fabsf(z);
+      o.l = (double)log1pf(expf(-az)) + (double)(z >= 0.f ? z * (1.f - y) : -z * y);
+      const float e = expf(-az);
+      o.p = (z >= 0.f) ? 1.f / (1.f + e) : e / (1.f + e);
+      o.g = o.p - y;
+      o.h = o.p * (1.f - o.p);
+      if (p0 != 0.f) {
+        const float zz = (o.h != 0.f) ? -(o.g / o.h) : 0.f;
+        if (zz > p0) o.h = -(o.g / p0);
+        else if (zz < -p0) o.h = -(o.g / -p0);
+      }
+      break;
+    }
+    case 1:
+      o.l = 0.5 * (double)(y - z) * (double)(y - z);
+      o.p = z; o.g = z - y; o.h = 1.f;
+      break;
+    case 2:
+      o.l = fabs((double)y - (double)z);
+      o.p = z; o.g = (float)((z - y > 0.f) - (z - y < 0.f)); o.h = 1.f;
+      break;
+    case 3: {
+      const float zc = fminf(z, 30.f);
+      o.p = expf(zc);
+      o.l = -(double)y * z + (double)o.p + (double)lgammaf(y + 1.f);
+      o.g = o.p - y; o.h = o.p;
+      break;
+    }
+    default: {
+      const float a = z - y, d = p0;
+      o.l = (fabsf(a) <= d) ? 0.5 * (double)a * a : (double)d * (fabsf(a) - 0.5f * d);
+      o.p = z;
+      o.g = (fabsf(a) <= d) ? a : ((a > 0.f) - (a < 0.f)) * d;
+      o.h = 0.f;
+      break;
+    }
+  }
+  return o;
+}
+
+__device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss_acc) {
+  __shared__ double s_loss[4], s_w[4];
+  lsum = wave_sum(lsum);
+  wsum = wave_sum(wsum);
+  const int wid = threadIdx.x >> 6;
+  if (lane_id() == 0) { s_loss[wid] = lsum; s_w[wid] = wsum; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&loss_acc[0], s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3]);
+    atomicAdd(&loss_acc[1], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+  }
+}
+
+// K == 1 losses, optionally fused with the new tree's score update.
+template <typename BinT>
+__global__ __launch_bounds__(256) void tree_grad_kernel(
+    const BinT* __restrict__ binsT, const int* __restrict__ tfeat, const int* __restrict__ tthr,
+    const int* __restrict__ tleft, const int* __restrict__ tright, const float* __restrict__ tval,
+    int nnodes, float* __restrict__ score, const float* __restrict__ init,
+    const float* __restrict__ label, const float* __restrict__ weight, long long N, int loss_id,
+    float p0, float score_div, float* __restrict__ pred, float2* __restrict__ gh,
+    double* __restrict__ loss_acc, int want_grad) {
+  extern __shared__ __attribute__((aligned(16))) int tsm[];
+  int* sf = tsm;
+  int* st = tsm + nnodes;
+  int* sl = tsm + 2 * nnodes;
+  int* sr = tsm + 3 * nnodes;
+  float* sv = reinterpret_cast<float*>(tsm + 4 * nnodes);
+  for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
+    sf[i] = tfeat[i]; st[i] = tthr[i]; sl[i] = tleft[i]; sr[i] = tright[i]; sv[i] = tval[i];
+  }
+  __syncthreads();
+  double lsum = 0.0, wsum = 0.0;
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    float s = score[r];
+    if (nnodes > 0) {
+      int n = 0;
+      while (sf[n] >= 0) n = ((int)binsT[(size_t)sf[n] * N + r] <= st[n]) ? sl[n] : sr[n];
+      s += sv[n];
+      score[r] = s;
+    }
+    const float w = weight ? weight[r] : 1.f;
+    const LossOut o = point_loss(loss_id, s / score_div + init[r], label[r], p0);
+    lsum += (double)w * o.l;
+    wsum += (double)w;
+    pred[r] = o.p;
+    if (want_grad) gh[r] = make_float2(o.g * w, o.h * w);
+  }
+  block_acc(lsum, wsum, loss_acc);
+}
+
+__global__ __launch_bounds__(256) void softmax_grad_kernel(
+    const float* __restrict__ score, const float* __restrict__ init,
+    const float* __restrict__ label, const float* __restrict__ weight, long long N, int K,
+    float score_div, float* __restrict__ pred, float2* __restrict__ gh,
+    double* __restrict__ loss_acc, int want_grad) {
+  double lsum = 0.0, wsum = 0.0;
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    const float w = weight ? weight[r] : 1.f;
+    wsum += (double)w;
+    double zmax = -INFINITY;
+    for (int k = 0; k < K; ++k)
+      zmax = fmax(zmax, (double)(score[r * K + k] / score_div + init[r * K + k]));
+    double den = 0.0, sy = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double z = (double)(score[r * K + k] / score_div + init[r * K + k]) - zmax;
+      den += exp(z);
+      sy += z * (double)label[r * K + k];
+    }
+    lsum += (double)w * (log(den) - sy);
+    const double inv = 1.0 / den;
+    for (int k = 0; k < K; ++k) {
+      const double z = (double)(score[r * K + k] / score_div + init[r * K + k]) - zmax;
+      const double p = exp(z) * inv;
+      const double y = label[r * K + k];
+      pred[r * K + k] = (float)p;
+      if (want_grad) gh[k * N + r] = make_float2((float)((p - y) * w), (float)(2.0 * p * (1.0 - p) * w));
+    }
+  }
+  block_acc(lsum, wsum, loss_acc);
+}
+
+}  // namespace ytk
+
+using namespace ytk;
+
+static inline int grid_for(long long n, int cap) {
+  return (int)std::min<long long>((n + 255) / 256, (long long)cap);
+}
+
+extern "C" {
+
+void ytk_tree_add_bins(uintptr_t binsT, int bin_bytes, long long N, uintptr_t tfeat,
+                       uintptr_t tthr, uintptr_t tleft, uintptr_t tright, uintptr_t tval,
+                       int nnodes, uintptr_t score, int sstride, int soff, uintptr_t stream) {
+  if (N <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  const int grid = grid_for(N, 256 * 16);
+  if (bin_bytes == 1) {
+    hipLaunchKernelGGL(tree_add_bins_kernel<uint8_t>, dim3(grid), dim3(256), lds, s,
+                       (const uint8_t*)binsT, N, (const int*)tfeat, (const int*)tthr,
+                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
+                       (float*)score, sstride, soff);
+  } else {
+    hipLaunchKernelGGL(tree_add_bins_kernel<uint16_t>, dim3(grid), dim3(256), lds, s,
+                       (const uint16_t*)binsT, N, (const int*)tfeat, (const int*)tthr,
+                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
+                       (float*)score, sstride, soff);
+  }
+  YTK_LAUNCH_CHECK();
+}
+
+void ytk_forest_predict(uintptr_t X, long long xstride, long long N, uintptr_t nfeat,
+                        uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
+                        uintptr_t nval, uintptr_t troot, uintptr_t tout, int T, uintptr_t out,
+                        int ostride, float scale, uintptr_t leaf_out, uintptr_t stream) {
+  if (N <= 0 || T <= 0) return;
+  hipLaunchKernelGGL(forest_predict_kernel, dim3(grid_for(N, 256 * 16)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const float*)X, xstride, N,
+                     (const int*)nfeat, (const float*)nthr, (const int*)nleft,
+                     (const int*)nright, (const uint8_t*)ndefl, (const float*)nval,
+                     (const int*)troot, (const int*)tout, T, (float*)out, ostride, scale,
+                     (int*)leaf_out);
+  YTK_LAUNCH_CHECK();
+}
+
+void ytk_bin_assign(uintptr_t X, long long xstride, long long N, int F, uintptr_t cand,
+                    uintptr_t coff, uintptr_t out, int bin_bytes, long long ostride,
+                    uintptr_t outT, uintptr_t stream) {
+  if (N <= 0) return;
+  const int grid = grid_for(N * F, 256 * 16);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (bin_bytes == 1) {
+    hipLaunchKernelGGL(bin_assign_kernel<uint8_t>, dim3(grid), dim3(256), 0, s,
+                       (const float*)X, xstride, N, F, (const float*)cand, (const int*)coff,
+                       (uint8_t*)out, ostride, (uint8_t*)outT);
+  } else {
+    hipLaunchKernelGGL(bin_assign_kernel<uint16_t>, dim3(grid), dim3(256), 0, s,
+                       (const float*)X, xstride, N, F, (const float*)cand, (const int*)coff,
+                       (uint16_t*)out, ostride, (uint16_t*)outT);
+  }
+  YTK_LAUNCH_CHECK();
+}
+
+// score [N][K], init [N][K], label [N][K], gh [K][N]
+void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
+                   long long N, int K, int loss_id, float p0, float score_div, uintptr_t pred,
+                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t stream) {
+  if (N <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_for(N, 256 * 8);
+  if (loss_id == 5) {
+    hipLaunchKernelGGL(softmax_grad_kernel, dim3(grid), dim3(256), 0, s, (const float*)score,
+                       (const float*)init, (const float*)label, (const float*)weight, N, K,
+                       score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad);
+  } else {
+    hipLaunchKernelGGL(tree_grad_kernel<uint8_t>, dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)nullptr, (const int*)nullptr, (const int*)nullptr,
+                       (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,
+                       (float*)score, (const float*)init, (const float*)label,
+                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
+                       (float2*)gh, (double*)loss_acc, want_grad);
+  }
+  YTK_LAUNCH_CHECK();
+}
+
+// Fused: score += tree(row) then loss / grad (K == 1).
+void ytk_tree_grad(uintptr_t binsT, int bin_bytes, uintptr_t tfeat, uintptr_t tthr,
+                   uintptr_t tleft, uintptr_t tright, uintptr_t tval, int nnodes,
+                   uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
+                   long long N, int loss_id, float p0, float score_div, uintptr_t pred,
+                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t stream) {
+  if (N <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  const int grid = grid_for(N, 256 * 8);
+  if (bin_bytes == 1) {
+    hipLaunchKernelGGL(tree_grad_kernel<uint8_t>, dim3(grid), dim3(256), lds, s,
+                       (const uint8_t*)binsT, (const int*)tfeat, (const int*)tthr,
+                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
+                       (float*)score, (const float*)init, (const float*)label,
+                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
+                       (float2*)gh, (double*)loss_acc, want_grad);
+  } else {
+    hipLaunchKernelGGL(tree_grad_kernel<uint16_t>, dim3(grid), dim3(256), lds, s,
+                       (const uint16_t*)binsT, (const int*)tfeat, (const int*)tthr,
+                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
+                       (float*)score, (const float*)init, (const float*)label,
+                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
+                       (float2*)gh, (double*)loss_acc, want_grad);
+  }
+  YTK_LAUNCH_CHECK();
+}
+
+}  // extern "C"

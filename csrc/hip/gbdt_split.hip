@@ -1,0 +1,219 @@
+// GBDT best-split search (gfx950 / CDNA4, wave64).
+//
+// Reference semantics:
+//   split enumeration    J/optimizer/gbdt/DataParallelTreeMaker.java:598-637
+//     (left-to-right bin scan, empty bins (g==0 && h==0) skipped, first hit only
+//      initialises the left sum, min_child_hessian_sum on both sides)
+//   gain / leaf value    J/optimizer/gbdt/UpdateStrategy.java:50-100
+//   node totals          DataParallelTreeMaker.java:543-573 (first sampled feature)
+//   tie-break            J/data/gbdt/SplitInfo.java:99-104 (max lossChg, then
+//                        lower feature; within a feature the first bin)
+//
+// Design: one workgroup (4 waves) per node; each wave owns features
+// f = wave, wave+4, ...; a lane owns 4 consecutive bins; fp64 wave prefix scans
+// (shuffle) give the left sums; argmax reduces (chg, feature, bin)
+// lexicographically -> deterministic. Sibling subtraction (parent - small child)
+// is fused into the load and the derived histogram is written back for the
+// node's own children.
+#include "common.h"
+
+namespace ytk {
+
+struct SplitOut {
+  float loss_chg;
+  int feat;
+  int bin_a;  // last non-empty bin going left
+  int bin_b;  // first non-empty bin going right
+  double gl, hl;  // left sums
+  double g, h;    // node sums
+};
+static_assert(sizeof(SplitOut) == 48, "SplitOut layout");
+
+struct GainParams {
+  float mcw;  // min_child_hessian_sum
+  float l1, l2;
+  float max_abs_leaf;
+};
+
+__device__ __forceinline__ double thr_l1(double w, double lam) {
+  if (w > lam) return w - lam;
+  if (w < -lam) return w + lam;
+  return 0.0;
+}
+
+__device__ __forceinline__ double node_value(double g, double h, const GainParams& p) {
+  if (h < (double)p.mcw) return 0.0;
+  double v = (p.l1 == 0.f) ? -g / (h + p.l2) : -thr_l1(g, p.l1) / (h + p.l2);
+  if (p.max_abs_leaf > 0.f) {
+    if (v > p.max_abs_leaf) v = p.max_abs_leaf;
+    else if (v < -p.max_abs_leaf) v = -p.max_abs_leaf;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double calc_gain(double g, double h, const GainParams& p) {
+  if (h < (double)p.mcw) return 0.0;
+  if (p.max_abs_leaf <= 0.f) {
+    if (p.l1 == 0.f) return g * g / (h + p.l2);
+    const double t = thr_l1(g, p.l1);
+    return t * t / (h + p.l2);
+  }
+  const double v = node_value(g, h, p);
+  return -2.0 * (g * v + 0.5 * (h + p.l2) * v * v + p.l1 * fabs(v));
+}
+
+// (chg, feat, bin) lexicographic "better": larger chg, then lower feat, then lower bin.
+__device__ __forceinline__ bool better(float c1, int f1, int b1, float c2, int f2, int b2) {
+  if (c1 != c2) return c1 > c2;
+  if (f1 != f2) return f1 < f2;
+  return b1 < b2;
+}
+
+// items[blk] = {slot, parent_slot, sibling_slot, derived}
+__global__ __launch_bounds__(256) void split_find_kernel(
+    float2* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
+    const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
+    SplitOut* __restrict__ out, GainParams gp) {
+  __shared__ float s_chg[4];
+  __shared__ int s_feat[4], s_a[4], s_b[4];
+  __shared__ double s_gl[4], s_hl[4];
+
+  const int4 it = items[blockIdx.x];
+  const int wid = threadIdx.x >> 6;
+  const int l = lane_id();
+  float2* hn = hist + (size_t)it.x * B * F;
+  const float2* hp = hist + (size_t)it.y * B * F;
+  const float2* hs = hist + (size_t)it.z * B * F;
+  const bool derived = it.w != 0;
+
+  auto load = [&](int f, int bin) -> float2 {
+    const size_t idx = (size_t)bin * F + f;
+    if (derived) {
+      const float2 p = hp[idx], s = hs[idx];
+      return make_float2(p.x - s.x, p.y - s.y);
+    }
+    return hn[idx];
+  };
+
+  // Node totals from the first sampled feature; every wave computes them
+  // identically (no cross-wave hand-off needed).
+  double G = 0.0, H = 0.0;
+  {
+    const int nb0 = nbins_f[f0];
+    double sg = 0.0, sh = 0.0;
+    for (int bin = l; bin < nb0; bin += kWave) {
+      const float2 v = load(f0, bin);
+      sg += v.x;
+      sh += v.y;
+    }
+    G = wave_sum(sg);
+    H = wave_sum(sh);
+  }
+  const float root_gain = (float)calc_gain(G, H, gp);
+
+  float best_chg = -INFINITY;
+  int best_f = 0x7fffffff, best_a = -1, best_b = 0x7fffffff;
+  double best_gl = 0.0, best_hl = 0.0;
+
+  for (int f = wid; f < F; f += 4) {
+    if (!fmask[f]) continue;
+    const int nb = nbins_f[f];
+    double carry_g = 0.0, carry_h = 0.0;
+    int carry_last = -1;
+    for (int c = 0; c < B; c += 4 * kWave) {
+      float2 v[4];
+      double sg = 0.0, sh = 0.0;
+      int lastne = -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bin = c + 4 * l + k;
+        v[k] = make_float2(0.f, 0.f);
+        if (bin < nb) v[k] = load(f, bin);
+        if (derived && bin < B) hn[(size_t)bin * F + f] = v[k];
+        sg += v[k].x;
+        sh += v[k].y;
+        if (v[k].x != 0.f || v[k].y != 0.f) lastne = bin;
+      }
+      const double ig = wave_incl_scan(sg);
+      const double ih = wave_incl_scan(sh);
+      const int im = wave_incl_max(lastne);
+      int em = __shfl_up(im, 1, kWave);
+      if (l == 0) em = -1;
+      double pg = ig - sg + carry_g;
+      double ph = ih - sh + carry_h;
+      int prev = max(em, carry_last);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bin = c + 4 * l + k;
+        const bool ne = (v[k].x != 0.f || v[k].y != 0.f);
+        if (ne) {
+          if (prev >= 0 && ph != 0.0 && ph >= (double)gp.mcw) {
+            const double rg = G - pg, rh = H - ph;
+            if (rh >= (double)gp.mcw) {
+              const float chg =
+                  (float)(calc_gain(pg, ph, gp) + calc_gain(rg, rh, gp) - (double)root_gain);
+              if (better(chg, f, bin, best_chg, best_f, best_b)) {
+                best_chg = chg; best_f = f; best_a = prev; best_b = bin;
+                best_gl = pg; best_hl = ph;
+              }
+            }
+          }
+          pg += v[k].x;
+          ph += v[k].y;
+          prev = bin;
+        }
+      }
+      carry_g += __shfl(ig, kWave - 1, kWave);
+      carry_h += __shfl(ih, kWave - 1, kWave);
+      carry_last = max(carry_last, __shfl(im, kWave - 1, kWave));
+    }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const float oc = __shfl_xor(best_chg, off, kWave);
+    const int of = __shfl_xor(best_f, off, kWave);
+    const int oa = __shfl_xor(best_a, off, kWave);
+    const int ob = __shfl_xor(best_b, off, kWave);
+    const double ogl = __shfl_xor(best_gl, off, kWave);
+    const double ohl = __shfl_xor(best_hl, off, kWave);
+    if (better(oc, of, ob, best_chg, best_f, best_b)) {
+      best_chg = oc; best_f = of; best_a = oa; best_b = ob; best_gl = ogl; best_hl = ohl;
+    }
+  }
+  if (l == 0) {
+    s_chg[wid] = best_chg; s_feat[wid] = best_f; s_a[wid] = best_a; s_b[wid] = best_b;
+    s_gl[wid] = best_gl; s_hl[wid] = best_hl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int bw = 0;
+    for (int w2 = 1; w2 < 4; ++w2)
+      if (better(s_chg[w2], s_feat[w2], s_b[w2], s_chg[bw], s_feat[bw], s_b[bw])) bw = w2;
+    SplitOut o;
+    o.loss_chg = s_chg[bw];
+    o.feat = (s_feat[bw] == 0x7fffffff) ? -1 : s_feat[bw];
+    o.bin_a = s_a[bw];
+    o.bin_b = (s_b[bw] == 0x7fffffff) ? -1 : s_b[bw];
+    o.gl = s_gl[bw];
+    o.hl = s_hl[bw];
+    o.g = G;
+    o.h = H;
+    out[blockIdx.x] = o;
+  }
+}
+
+}  // namespace ytk
+
+using namespace ytk;
+
+extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
+                               int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
+                               float l1, float l2, float max_abs_leaf, uintptr_t stream) {
+  if (nitems <= 0) return;
+  GainParams gp{mcw, l1, l2, max_abs_leaf};
+  hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (float2*)hist, B, F,
+                     (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
+                     (SplitOut*)out, gp);
+  YTK_LAUNCH_CHECK();
+}

@@ -187,15 +187,17 @@ class BinMapper:
         """Bin stride of the histogram buffers (multiple of 4, >= max bins)."""
         return max(4, ((self.max_bins + 3) // 4) * 4)
 
-    def transform(self, X: torch.Tensor) -> torch.Tensor:
-        """Raw (NaN-filled) float features [N, F] -> bins [N, stride]."""
+    def transform(self, X: torch.Tensor, with_transposed: bool = True):
+        """Raw (NaN-filled) float features [N, F] -> (bins [N, stride] row-major,
+        binsT [F, N] column-major or None)."""
         N, F = X.shape
         assert F == self.num_features
         out = torch.zeros((N, self.stride), dtype=self.dtype, device=X.device)
+        outT = torch.empty((F, N), dtype=self.dtype, device=X.device) if with_transposed else None
         cand = torch.from_numpy(np.concatenate(self.cands).astype(np.float32)).to(X.device)
         coff = torch.from_numpy(np.concatenate([[0], np.cumsum([len(c) for c in self.cands])]).astype(np.int32)).to(X.device)
-        gops.bin_assign(X.contiguous(), cand, coff, out)
-        return out
+        gops.bin_assign(X.contiguous(), cand, coff, out, outT)
+        return out, outT
 
 
 def parse_missing_value(spec: str):

@@ -6,23 +6,26 @@ node stats :543-573, split enumeration :598-637, best-split sync :640-653) and
 ``J/optimizer/gbdt/UpdateStrategy.java``.
 
 MI355X-first structure (not a translation):
-  * all per-row state (bins, g/h, row permutation) stays resident in HBM;
+  * all per-row state (row-major + column-major bins, position-ordered (g,h), row
+    permutation) stays resident in HBM;
   * one batched launch per level for histogram build / split search / partition
     (level-wise); loss-guided growth uses the same kernels with batch size 1;
+  * the partition moves (g,h) along with the row ids, so histogram builds read
+    (g,h) contiguously and only gather the 32-B bin rows;
   * histograms are indexed by a per-tree slot counter (no LRU pool: even 509
     slots x 28 features x 256 bins is 29 MB of the 288 GB HBM);
+  * per-call metadata (work lists, split items) is built with vectorised numpy and
+    shipped in ONE pinned host->device copy per launch group;
   * multi-GPU: rows are sharded; the level's freshly built histograms are one
-    contiguous slab -> ONE RCCL all-reduce per level (owner-compute reduce-scatter
-    is unnecessary at these sizes: the reduced slab is what every rank's split
-    kernel reads, and identical inputs give identical split decisions on every
-    rank, so no SplitInfo exchange is needed).
+    contiguous slab -> ONE RCCL all-reduce per level. Every rank then runs the
+    same split kernel on identical inputs, so split decisions agree without a
+    SplitInfo exchange.
 """
 from __future__ import annotations
 
 import heapq
-import math
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -57,8 +60,8 @@ class TreeParams:
 
 @dataclass
 class TimeStats:
-    """Per-phase timers mirroring ``J/data/gbdt/TimeStats.java`` names (host wall
-    time incl. the device work the phase waits for)."""
+    """Per-phase timers mirroring ``J/data/gbdt/TimeStats.java`` (host wall time;
+    with ``profile=True`` each phase synchronises so device time is attributed)."""
     build_hist: float = 0.0
     comm_hist: float = 0.0
     find_split: float = 0.0
@@ -90,14 +93,68 @@ class _Node:
     H: float = 0.0
 
 
-class TreeBuilder:
-    # blocks of the histogram / partition launches: rows per block bounds
-    MIN_ROWS_PER_BLOCK = 2048
-    TARGET_BLOCKS = 1024
+class _Uploader:
+    """Packs small int32 host arrays into one pinned buffer -> one H2D copy.
 
-    def __init__(self, bins: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
+    Safe to reuse after every device->host sync (each tree level has one)."""
+
+    def __init__(self, dev: torch.device, cap: int = 1 << 20):
+        self.dev = dev
+        self.cuda = dev.type == "cuda"
+        self.cap = cap
+        if self.cuda:
+            self.host = torch.empty(cap, dtype=torch.int32, pin_memory=True)
+            self.devbuf = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.off = 0
+
+    def reset(self):
+        self.off = 0
+
+    def put(self, *arrays: np.ndarray):
+        arrays = [np.ascontiguousarray(a, dtype=np.int32) for a in arrays]
+        if not self.cuda:
+            return [torch.from_numpy(a) for a in arrays]
+        n = sum(a.size for a in arrays)
+        if self.off + n > self.cap:
+            torch.cuda.current_stream(self.dev).synchronize()
+            self.off = 0
+            if n > self.cap:
+                self.cap = 1 << int(np.ceil(np.log2(n)))
+                self.host = torch.empty(self.cap, dtype=torch.int32, pin_memory=True)
+                self.devbuf = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
+        o = self.off
+        hv = self.host.numpy()
+        outs = []
+        p = o
+        for a in arrays:
+            hv[p:p + a.size] = a.reshape(-1)
+            outs.append((p, a.shape))
+            p += a.size
+        self.devbuf[o:p].copy_(self.host[o:p], non_blocking=True)
+        self.off = p
+        return [self.devbuf[s:s + int(np.prod(shape))].view(*shape) for s, shape in outs]
+
+
+def _chunk_segments(begins: np.ndarray, counts: np.ndarray, ch: int):
+    """Vectorised chunking of segments -> (seg_idx, chunk_begin, chunk_end, blk_in_seg)."""
+    nb = np.where(counts > 0, (counts + ch - 1) // ch, 0).astype(np.int64)
+    total = int(nb.sum())
+    seg = np.repeat(np.arange(len(counts)), nb)
+    first = np.concatenate([[0], np.cumsum(nb)[:-1]]) if len(nb) else np.zeros(0, np.int64)
+    k = np.arange(total) - np.repeat(first, nb)
+    s = begins[seg] + k * ch
+    e = np.minimum(s + ch, (begins + counts)[seg])
+    return seg, s, e, k, first, nb
+
+
+class TreeBuilder:
+    MIN_ROWS_PER_BLOCK = 2048
+    TARGET_BLOCKS = 1024  # histogram blocks per launch: 2 resident per CU x 256 CUs x 2 waves
+
+    def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Optional[Comm] = None, profile: bool = False):
         self.bins = bins
+        self.binsT = binsT
         self.dev = bins.device
         self.N = bins.shape[0]
         self.F = F
@@ -116,75 +173,77 @@ class TreeBuilder:
         self.hist = torch.zeros((self.max_nodes, B, F, 2), dtype=torch.float32, device=self.dev)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=self.dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=self.dev)
+        self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=self.dev)
+        self.gh_tmp = torch.empty((self.N, 2), dtype=torch.float32, device=self.dev)
+        self.flags = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
         self.iota = torch.arange(self.N, dtype=torch.int32, device=self.dev)
+        self.up = _Uploader(self.dev)
         self.profile = profile
         self.last_stats = TimeStats()
         self.total_stats = TimeStats()
         self.tree_count = 0
+        self.last_keep = None
+        self.fmask_np = np.ones(F, np.uint8)
 
     # ------------------------------------------------------------------ utils
     def _sync(self):
         if self.profile and self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
 
-    def _to_dev(self, a: np.ndarray) -> torch.Tensor:
-        t = torch.from_numpy(np.ascontiguousarray(a))
-        return t.to(self.dev, non_blocking=True) if self.dev.type == "cuda" else t
-
-    def _chunks(self, total: int) -> int:
+    def _chunk(self, total: int) -> int:
         return max(self.MIN_ROWS_PER_BLOCK, -(-total // self.TARGET_BLOCKS))
 
-    def _hist_work(self, segs):
-        """segs: list of (slot, begin, count) -> int32 [nwork, 4]"""
-        total = sum(c for _, _, c in segs)
-        ch = self._chunks(total)
-        w = []
-        for slot, b, c in segs:
-            e = b + c
-            for s in range(b, e, ch):
-                w.append((slot, s, min(s + ch, e), 0))
-        return np.array(w, np.int32).reshape(-1, 4)
-
     # ----------------------------------------------------------- primitives
-    def _build_and_find(self, tree: Tree, nodes: Dict[int, _Node], build: List[int],
-                        derived: List[tuple], gh: torch.Tensor, fmask: torch.Tensor, f0: int,
-                        identity_rows: bool = False):
+    def _build_and_find(self, nodes: Dict[int, _Node], build: List[int], derived: List[tuple],
+                        fmask: torch.Tensor, f0: int, identity_rows: bool = False):
         """Histogram the ``build`` nodes, derive ``derived`` = (node, parent, sibling),
         then find the best split of every one of them."""
         st = self.last_stats
         t0 = time.perf_counter()
         s0 = self.next_slot
+        nb = len(build)
         for i, nid in enumerate(build):
             nodes[nid].slot = s0 + i
         for j, (nid, _, _) in enumerate(derived):
-            nodes[nid].slot = s0 + len(build) + j
-        self.next_slot += len(build) + len(derived)
-        nb = len(build)
+            nodes[nid].slot = s0 + nb + j
+        self.next_slot += nb + len(derived)
+        items = np.zeros((nb + len(derived), 4), np.int32)
+        items[:nb, 0] = np.arange(s0, s0 + nb)
+        for j, (n, p, s) in enumerate(derived):
+            items[nb + j] = (nodes[n].slot, nodes[p].slot, nodes[s].slot, 1)
+        work = np.zeros((0, 4), np.int32)
+        if nb:
+            begins = np.array([nodes[n].begin for n in build], np.int64)
+            counts = np.array([nodes[n].cnt_local for n in build], np.int64)
+            seg, s, e, _, _, _ = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
+            work = np.zeros((len(seg), 4), np.int32)
+            work[:, 0] = s0 + seg
+            work[:, 1] = s
+            work[:, 2] = e
+        work_d, items_d = self.up.put(work, items)
         if nb:
             self.hist[s0:s0 + nb].zero_()
-            work = self._hist_work([(nodes[n].slot, nodes[n].begin, nodes[n].cnt_local) for n in build])
-            gops.hist_build(self.bins, self.F, gh, None if identity_rows else self.rows,
-                            self._to_dev(work), self.hist, self.B)
+            gops.hist_build(self.bins, self.F, self.ghp, None if identity_rows else self.rows,
+                            work_d, self.hist, self.B)
         self._sync()
         t1 = time.perf_counter()
         if nb and self.comm.is_dist:
             self.comm.allreduce_(self.hist[s0:s0 + nb])
             self._sync()
         t2 = time.perf_counter()
-        items = [(nodes[n].slot, 0, 0, 0) for n in build]
-        items += [(nodes[n].slot, nodes[p].slot, nodes[s].slot, 1) for n, p, s in derived]
         order = list(build) + [n for n, _, _ in derived]
-        out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0,
-                              self._to_dev(np.array(items, np.int32).reshape(-1, 4)), self.gp)
+        out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp)
         recs = out.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+        self.up.reset()  # the .cpu() above synchronised the stream
         t3 = time.perf_counter()
+        mcw2 = self.p.min_child_hessian_sum * 2.0
         for nid, r in zip(order, recs):
             nd = nodes[nid]
             nd.rec = r
             nd.G = float(r["g"])
             nd.H = float(r["h"])
             # canSplit (UpdateStrategy.canSplit): H >= 2*mcw and n >= min_split_samples
-            if not (nd.H >= self.p.min_child_hessian_sum * 2.0 and nd.cnt_global >= self.p.min_split_samples):
+            if not (nd.H >= mcw2 and nd.cnt_global >= self.p.min_split_samples):
                 r["loss_chg"] = -np.inf
                 r["feat"] = -1
         st.build_hist += t1 - t0
@@ -195,46 +254,36 @@ class TreeBuilder:
         """splits: list of (nid, left_child, right_child). Updates child segments/counts."""
         t0 = time.perf_counter()
         n = len(splits)
-        total = sum(nodes[s[0]].cnt_local for s in splits)
-        ch = self._chunks(total)
-        items, first_blk, nblk = [], [], []
-        feat = np.empty(n, np.int32)
-        thr = np.empty(n, np.int32)
-        nbeg = np.empty(n, np.int32)
-        for i, (nid, _, _) in enumerate(splits):
-            nd = nodes[nid]
-            r = nd.rec
-            feat[i] = int(r["feat"])
-            thr[i] = (int(r["bin_a"]) + int(r["bin_b"])) // 2
-            nbeg[i] = nd.begin
-            first_blk.append(len(items))
-            k = 0
-            for s in range(nd.begin, nd.begin + nd.cnt_local, ch):
-                items.append((i, s, min(s + ch, nd.begin + nd.cnt_local), k))
-                k += 1
-            nblk.append(k)
-        left = gops.partition(self.bins, self.rows, self.rows_tmp,
-                              self._to_dev(np.array(items, np.int32).reshape(-1, 4)),
-                              self._to_dev(feat), self._to_dev(thr), self._to_dev(nbeg),
-                              self._to_dev(np.array(first_blk, np.int32)),
-                              self._to_dev(np.array(nblk, np.int32)), n)
+        begins = np.array([nodes[s[0]].begin for s in splits], np.int64)
+        counts = np.array([nodes[s[0]].cnt_local for s in splits], np.int64)
+        seg, s, e, k, first, nblk = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
+        items = np.stack([seg, s, e, k], axis=1).astype(np.int32).reshape(-1, 4)
+        feat = np.array([int(nodes[x[0]].rec["feat"]) for x in splits], np.int32)
+        thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
+                       np.int32)
+        items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d = self.up.put(
+            items, feat, thr, begins, first, nblk)
+        left = gops.partition(self.binsT, self.rows, self.rows_tmp, self.ghp, self.gh_tmp, self.flags,
+                              items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d, n)
         if copy_back:
             for nid, _, _ in splits:
                 nd = nodes[nid]
                 if nd.cnt_local:
-                    self.rows[nd.begin:nd.begin + nd.cnt_local].copy_(
-                        self.rows_tmp[nd.begin:nd.begin + nd.cnt_local])
+                    sl = slice(nd.begin, nd.begin + nd.cnt_local)
+                    self.rows[sl].copy_(self.rows_tmp[sl])
+                    self.ghp[sl].copy_(self.gh_tmp[sl])
         else:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
-        left_l = left.to(torch.int64)
+            self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
         if self.comm.is_dist:
-            both = torch.stack([left_l, left_l]).to(self.dev)
+            both = torch.stack([left, left]).to(torch.int64)
             self.comm.allreduce_(both[1])
             both = both.cpu().numpy()
             lloc, lglob = both[0], both[1]
         else:
-            lloc = left_l.cpu().numpy()
+            lloc = left.to(torch.int64).cpu().numpy()
             lglob = lloc
+        self.up.reset()
         for i, (nid, lc, rc) in enumerate(splits):
             nd = nodes[nid]
             nodes[lc] = _Node(begin=nd.begin, cnt_local=int(lloc[i]), cnt_global=int(lglob[i]),
@@ -243,13 +292,46 @@ class TreeBuilder:
                               cnt_global=nd.cnt_global - int(lglob[i]), depth=nd.depth + 1)
         self.last_stats.partition += time.perf_counter() - t0
 
+    def _count_children(self, nodes: Dict[int, _Node], splits: List[tuple]):
+        """Children that become leaves right away: only their sample counts are needed
+        (node statistics in the dump), so run the flag/count pass without the scatter."""
+        t0 = time.perf_counter()
+        begins = np.array([nodes[s[0]].begin for s in splits], np.int64)
+        counts = np.array([nodes[s[0]].cnt_local for s in splits], np.int64)
+        seg, s, e, k, first, nblk = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
+        items = np.stack([seg, s, e, k], axis=1).astype(np.int32).reshape(-1, 4)
+        feat = np.array([int(nodes[x[0]].rec["feat"]) for x in splits], np.int32)
+        thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
+                       np.int32)
+        items_d, feat_d, thr_d = self.up.put(items, feat, thr)
+        bc = gops.partition_count(self.binsT, self.rows, self.flags, items_d, feat_d, thr_d)
+        left = torch.zeros(len(splits), dtype=torch.int64, device=self.dev)
+        if len(seg):
+            left.index_add_(0, torch.from_numpy(seg).to(self.dev), bc.to(torch.int64))
+        if self.comm.is_dist:
+            both = torch.stack([left, left])
+            self.comm.allreduce_(both[1])
+            both = both.cpu().numpy()
+            lloc, lglob = both[0], both[1]
+        else:
+            lloc = left.cpu().numpy()
+            lglob = lloc
+        self.up.reset()
+        for i, (nid, lc, rc) in enumerate(splits):
+            nd = nodes[nid]
+            nodes[lc] = _Node(cnt_local=int(lloc[i]), cnt_global=int(lglob[i]), depth=nd.depth + 1)
+            nodes[rc] = _Node(cnt_local=nd.cnt_local - int(lloc[i]),
+                              cnt_global=nd.cnt_global - int(lglob[i]), depth=nd.depth + 1)
+        self.last_stats.partition += time.perf_counter() - t0
+
     # ------------------------------------------------------------------ build
     def build(self, gh: torch.Tensor) -> Tree:
-        """Grow one tree from gh [N, 2] (grad*w, hess*w)."""
+        """Grow one tree from gh [N, 2] (grad*w, hess*w) in row order."""
         p = self.p
         t_start = time.perf_counter()
         self.last_stats = TimeStats()
         self.next_slot = 0
+        self.up.reset()
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))
         # --- instance subsampling (DataParallelTreeMaker.initAssistData :405-423)
@@ -261,11 +343,13 @@ class TreeBuilder:
             sel = torch.nonzero(keep, as_tuple=False).flatten().to(torch.int32)
             n_local = int(sel.numel())
             self.rows[:n_local].copy_(sel)
+            self.ghp[:n_local].copy_(gh.index_select(0, sel.long()))
             identity = False
             self.last_keep = keep
         else:
             n_local = self.N
             self.rows.copy_(self.iota)
+            self.ghp.copy_(gh)
             self.last_keep = None
         # --- feature subsampling with a globally agreed seed (:432-461)
         if p.feature_sample_rate < 1.0:
@@ -276,15 +360,19 @@ class TreeBuilder:
         else:
             fm = np.ones(self.F, np.uint8)
         f0 = int(np.nonzero(fm)[0][0])
-        fmask = self._to_dev(fm)
+        if not np.array_equal(fm, self.fmask_np) or not hasattr(self, "fmask"):
+            self.fmask_np = fm
+            self.fmask = torch.from_numpy(fm).to(self.dev)
+        fmask = self.fmask
 
         n_global = int(self.comm.allreduce_scalars([n_local], dtype=torch.int64)[0]) if self.comm.is_dist else n_local
         tree = Tree()
         nodes: Dict[int, _Node] = {0: _Node(begin=0, cnt_local=n_local, cnt_global=n_global, depth=0, seq=0)}
-        self._build_and_find(tree, nodes, [0], [], gh, fmask, f0, identity_rows=identity)
+        self._build_and_find(nodes, [0], [], fmask, f0, identity_rows=identity)
         seq = 1
         num_leaf = 1
         max_leaf = p.max_leaf_cnt
+        lr32 = np.float32(p.learning_rate)
 
         def pop_is_leaf(nd: _Node):
             return (nd.rec["loss_chg"] <= p.min_split_loss
@@ -292,26 +380,30 @@ class TreeBuilder:
                     or (max_leaf > 0 and max_leaf == num_leaf)
                     or (p.min_split_samples > 0 and nd.cnt_global < p.min_split_samples))
 
-        def leaf_value(G, H):
-            v = np.float32(gops.node_value_np(G, H, self.gp["mcw"], self.gp["l1"], self.gp["l2"],
-                                              self.gp["max_abs_leaf"]))
-            return float(v * np.float32(p.learning_rate))
-
         def make_leaf(nid):
             nd = nodes[nid]
-            tree.set_leaf(nid, leaf_value(nd.G, nd.H))
+            v = np.float32(gops.node_value_np(nd.G, nd.H, self.gp["mcw"], self.gp["l1"], self.gp["l2"],
+                                              self.gp["max_abs_leaf"]))
+            tree.set_leaf(nid, float(v * lr32))
 
-        def children_terminal(nd_l: _Node, nd_r: _Node):
+        def children_terminal(nd_l: _Node, nd_r: _Node, nleaf: int):
             return ((p.max_depth >= 0 and p.max_depth == nd_l.depth)
-                    or (max_leaf > 0 and max_leaf == num_leaf)
+                    or (max_leaf > 0 and max_leaf == nleaf)
                     or (p.min_split_samples > 0 and nd_l.cnt_global < p.min_split_samples
                         and nd_r.cnt_global < p.min_split_samples))
+
+        def leafify_children(nid, lc, rc):
+            r = nodes[nid].rec
+            nl, nr = nodes[lc], nodes[rc]
+            nl.G, nl.H = float(r["gl"]), float(r["hl"])
+            nr.G, nr.H = nodes[nid].G - nl.G, nodes[nid].H - nl.H
+            make_leaf(lc)
+            make_leaf(rc)
 
         if p.grow_policy == "level":
             level = [0]
             while level:
-                splits = []
-                snapshot = []
+                splits, snapshot = [], []
                 for nid in level:  # FIFO by seq
                     nd = nodes[nid]
                     if pop_is_leaf(nd):
@@ -325,20 +417,19 @@ class TreeBuilder:
                     snapshot.append(num_leaf)
                 if not splits:
                     break
+                # children of the deepest level never need their rows: skip the partition
+                last_level = p.max_depth >= 0 and nodes[splits[0][0]].depth + 1 == p.max_depth
+                if last_level:
+                    self._count_children(nodes, splits)
+                    for nid, lc, rc in splits:
+                        leafify_children(nid, lc, rc)
+                    break
                 self._partition(nodes, splits, copy_back=False)
                 build, derived, nxt = [], [], []
                 for (nid, lc, rc), nl_snap in zip(splits, snapshot):
                     nl, nr = nodes[lc], nodes[rc]
-                    saved = num_leaf
-                    num_leaf = nl_snap
-                    term = children_terminal(nl, nr)
-                    num_leaf = saved
-                    r = nodes[nid].rec
-                    if term:
-                        nl.G, nl.H = float(r["gl"]), float(r["hl"])
-                        nr.G, nr.H = nodes[nid].G - nl.G, nodes[nid].H - nl.H
-                        make_leaf(lc)
-                        make_leaf(rc)
+                    if children_terminal(nl, nr, nl_snap):
+                        leafify_children(nid, lc, rc)
                     else:
                         small, large = (lc, rc) if nl.cnt_global < nr.cnt_global else (rc, lc)
                         build.append(small)
@@ -347,7 +438,7 @@ class TreeBuilder:
                         seq += 2
                         nxt += [lc, rc]
                 if build:
-                    self._build_and_find(tree, nodes, build, derived, gh, fmask, f0)
+                    self._build_and_find(nodes, build, derived, fmask, f0)
                 level = nxt
         else:  # loss-guided
             heap = [(-float(nodes[0].rec["loss_chg"]), 0, 0)]
@@ -361,16 +452,19 @@ class TreeBuilder:
                 lc, rc = tree.add_children(nid)
                 tree.set_split(nid, int(r["feat"]), int(r["bin_a"]), int(r["bin_b"]))
                 num_leaf += 1
+                if (p.max_depth >= 0 and nd.depth + 1 == p.max_depth) or (max_leaf > 0 and max_leaf == num_leaf
+                                                                        and p.min_split_samples <= 0):
+                    # terminal children whose rows are never needed again
+                    self._count_children(nodes, [(nid, lc, rc)])
+                    leafify_children(nid, lc, rc)
+                    continue
                 self._partition(nodes, [(nid, lc, rc)], copy_back=True)
                 nl, nr = nodes[lc], nodes[rc]
-                if children_terminal(nl, nr):
-                    nl.G, nl.H = float(r["gl"]), float(r["hl"])
-                    nr.G, nr.H = nd.G - nl.G, nd.H - nl.H
-                    make_leaf(lc)
-                    make_leaf(rc)
+                if children_terminal(nl, nr, num_leaf):
+                    leafify_children(nid, lc, rc)
                 else:
                     small, large = (lc, rc) if nl.cnt_global < nr.cnt_global else (rc, lc)
-                    self._build_and_find(tree, nodes, [small], [(large, nid, small)], gh, fmask, f0)
+                    self._build_and_find(nodes, [small], [(large, nid, small)], fmask, f0)
                     nl.seq, nr.seq = seq, seq + 1
                     heapq.heappush(heap, (-float(nl.rec["loss_chg"]), seq, lc))
                     heapq.heappush(heap, (-float(nr.rec["loss_chg"]), seq + 1, rc))

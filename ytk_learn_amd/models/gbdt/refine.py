@@ -33,19 +33,19 @@ class TreeRefiner:
         self.comm = comm
         self.approximate = approximate
 
-    def leaf_ids(self, tree, bins: torch.Tensor) -> torch.Tensor:
+    def leaf_ids(self, tree, binsT: torch.Tensor) -> torch.Tensor:
         n = tree.num_nodes
         # score column trick: value = node id, so tree_add_bins writes the leaf id
         feat, thr, left, right, _ = tree.bin_arrays()
         ids = np.arange(n, dtype=np.float32)
-        out = torch.zeros((bins.shape[0], 1), dtype=torch.float32, device=bins.device)
-        arrs = tuple(torch.from_numpy(a).to(bins.device) for a in (feat, thr, left, right, ids))
-        gops.tree_add_bins(bins, arrs, out, 0)
+        out = torch.zeros((binsT.shape[1], 1), dtype=torch.float32, device=binsT.device)
+        arrs = tuple(torch.from_numpy(a).to(binsT.device) for a in (feat, thr, left, right, ids))
+        gops.tree_add_bins(binsT, arrs, out, 0)
         return out[:, 0].round().to(torch.int64)
 
     def refine(self, tree, builder, y: torch.Tensor, cur_score: torch.Tensor,
                w: torch.Tensor, lr: float):
-        leaf = self.leaf_ids(tree, builder.bins)
+        leaf = self.leaf_ids(tree, builder.binsT)
         keep = getattr(builder, "last_keep", None)
         resid = (y.double() - cur_score.double())
         ww = w.double() if w is not None else torch.ones_like(resid)

@@ -120,10 +120,10 @@ class GBDTTrainer:
         Xf = torch.where(torch.isnan(tr.X), fill[None, :], tr.X)
         self.mapper = BinMapper.fit(Xf, tr.weight, self._specs(), self.comm, self.p.split_type,
                                     seed=self.p.tree.seed)
-        self.bins = self.mapper.transform(Xf)
+        self.bins, self.binsT = self.mapper.transform(Xf)
         del Xf
         self.B = self.mapper.hist_bins()
-        self.builder = TreeBuilder(self.bins, self.F, self.B, self.mapper.nbins, self.p.tree,
+        self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, self.p.tree,
                                    self.comm, profile=self.profile)
         N = tr.n
         self.score = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
@@ -195,6 +195,16 @@ class GBDTTrainer:
             gh[:, :, 1] = (h * ww[:, None]).float().t()
         return torch.stack([(lv.reshape(lv.shape[0], -1).sum(1) * ww).sum(), ww.sum()])
 
+    def _tree_to_dev(self, tree):
+        """Bin-threshold node arrays of a tree packed into one H2D copy."""
+        f, t, l, r, v = tree.bin_arrays()
+        n = f.shape[0]
+        packed = np.concatenate([f, t, l, r, v.view(np.int32)]).astype(np.int32)
+        d = torch.from_numpy(packed)
+        if self.dev.type == "cuda":
+            d = d.pin_memory().to(self.dev, non_blocking=True)
+        return (d[:n], d[n:2 * n], d[2 * n:3 * n], d[3 * n:4 * n], d[4 * n:5 * n].view(torch.float32))
+
     # ------------------------------------------------------------------ train
     def train(self, rounds: Optional[int] = None, on_round: Optional[Callable[[int, "GBDTTrainer"], None]] = None,
               dump_cb: Optional[Callable[[int], None]] = None):
@@ -230,16 +240,23 @@ class GBDTTrainer:
         lr = 1.0 if self.rf else self.p.tree.learning_rate
         self.builder.p.learning_rate = lr
         new_trees = []
+        arrays = []
         for k in range(self.K):
             tree = self.builder.build(self.gh[k])
             if self.refiner is not None:
                 self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
                                     + self.init_score[:, k], self.w, lr)
-            gops.tree_add_bins(self.bins, tuple(torch.from_numpy(a).to(self.dev) for a in tree.bin_arrays()),
-                               self.score, k)
             new_trees.append(tree)
-        # loss on train after this round + gradients for the next
-        acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
+            arrays.append(self._tree_to_dev(tree))
+        # score update + loss on train after this round + gradients for the next round
+        if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
+            param = self.p.sigmoid_zmax if self.kernel_loss == "sigmoid" else getattr(self.loss, "delta", 0.0)
+            acc = gops.tree_grad(self.binsT, arrays[0], self.score, self.init_score, self.y, self.w,
+                                 self.kernel_loss, param, self._score_div(i + 1), self.pred, self.gh[0])
+        else:
+            for k in range(self.K):
+                gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
+            acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
         # convert model (slot -> raw threshold, names, default direction)
         for tree in new_trees:
             tree.convert_split_values(self.mapper.cands, self.p.split_type)

@@ -35,11 +35,11 @@ def _bin_bytes(bins: torch.Tensor) -> int:
 # ---------------------------------------------------------------------------
 # histogram build
 # ---------------------------------------------------------------------------
-def hist_build(bins, F, gh, rows, work, hist, B):
+def hist_build(bins, F, ghp, rows, work, hist, B):
     """Accumulate (g, h) histograms.
 
     bins: [N, S] uint8/int16 row-major (S >= F, S % 32 == 0 for the LDS path)
-    gh:   [N, 2] float32
+    ghp:  [M, 2] float32 (g, h) in POSITION order (ghp[pos] belongs to rows[pos])
     rows: int32 row permutation or None (identity positions)
     work: int32 [nwork, 4] = (slot, begin, end, 0); positions index ``rows``
     hist: float32 [slots, B, F, 2], target slots must be zeroed by the caller
@@ -48,28 +48,31 @@ def hist_build(bins, F, gh, rows, work, hist, B):
     if nwork == 0:
         return
     if bins.is_cuda:
-        check_cuda(bins, gh, rows, work, hist)
+        check_cuda(bins, ghp, rows, work, hist)
         assert hist.shape[1] == B and hist.shape[2] == F and hist.shape[3] == 2
-        assert gh.shape[0] == bins.shape[0] and gh.shape[1] == 2
+        assert ghp.shape[1] == 2 and ghp.dtype == torch.float32
+        if rows is None:
+            assert ghp.shape[0] >= bins.shape[0]
         stride = bins.shape[1]
         h = hip()
         if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
-            h.hist_u8(ptr(bins), stride, F, ptr(gh), ptr(rows), ptr(work), nwork, ptr(hist), B,
+            h.hist_u8(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                       stream(bins))
         else:
-            h.hist_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(gh), ptr(rows), ptr(work),
+            h.hist_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                           nwork, ptr(hist), B, stream(bins))
         return
     # CPU reference
-    w = work.numpy() if not work.is_cuda else work.cpu().numpy()
+    w = work.numpy()
     hv = hist.view(-1, 2)
+    mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
     for slot, b, e, _ in w:
         if e <= b:
             continue
         r = rows[b:e].long() if rows is not None else torch.arange(b, e, dtype=torch.long)
-        bb = bins[r, :F].long() & (0xFFFF if bins.dtype == torch.int16 else 0xFF)
+        bb = bins[r, :F].long() & mask
         idx = (int(slot) * B + bb) * F + torch.arange(F, dtype=torch.long)[None, :]
-        v = gh[r][:, None, :].expand(-1, F, 2)
+        v = ghp[b:e][:, None, :].expand(-1, F, 2)
         hv.index_add_(0, idx.reshape(-1), v.reshape(-1, 2))
 
 
@@ -172,27 +175,31 @@ def _split_one_cpu(hn, nb, fm, f0, mcw, l1, l2, mal):
 # ---------------------------------------------------------------------------
 # partition
 # ---------------------------------------------------------------------------
-def partition(bins, rows, rows_out, items, feat, thr, node_begin, first_blk, nblk, n_split):
-    """Stable partition of node segments; returns left counts (int32 [n_split]).
+def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_begin, first_blk,
+              nblk, n_split):
+    """Stable partition of node segments; moves row ids AND position-ordered (g, h).
 
-    items int32 [nblk_total, 4] = (split_idx, begin, end, blk_in_node).
+    binsT: column-major bins [F, N]; items int32 [nblk_total, 4] = (split_idx, begin, end,
+    blk_in_node); go left iff binsT[feat, row] <= thr. Returns left counts int32 [n_split].
     """
-    if bins.is_cuda:
-        left = torch.zeros(n_split, dtype=torch.int32, device=bins.device)
+    if binsT.is_cuda:
+        left = torch.zeros(n_split, dtype=torch.int32, device=binsT.device)
         nitems = items.shape[0]
         if nitems == 0:
             return left
-        check_cuda(bins, rows, rows_out, items, feat, thr, node_begin, first_blk, nblk)
-        counts = torch.empty(nitems, dtype=torch.int32, device=bins.device)
-        hip().partition(ptr(bins), _bin_bytes(bins), bins.shape[1], ptr(rows), ptr(rows_out),
-                        ptr(items), nitems, ptr(feat), ptr(thr), ptr(node_begin), ptr(first_blk),
-                        ptr(nblk), ptr(counts), ptr(left), stream(bins))
+        check_cuda(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_begin,
+                   first_blk, nblk)
+        counts = torch.empty(nitems, dtype=torch.int32, device=binsT.device)
+        hip().partition(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(rows_out),
+                        ptr(ghp), ptr(gh_out), ptr(flags), ptr(items), nitems, ptr(feat), ptr(thr),
+                        ptr(node_begin), ptr(first_blk), ptr(nblk), ptr(counts), ptr(left),
+                        stream(binsT))
         return left
     left = torch.zeros(n_split, dtype=torch.int32)
     nbv, fv, tv, nb_ = node_begin.numpy(), feat.numpy(), thr.numpy(), nblk.numpy()
     fb = first_blk.numpy()
     it = items.numpy()
-    mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
+    mask = 0xFFFF if binsT.dtype == torch.int16 else 0xFF
     for i in range(n_split):
         if nb_[i] == 0:
             continue
@@ -200,40 +207,69 @@ def partition(bins, rows, rows_out, items, feat, thr, node_begin, first_blk, nbl
         e = int(it[fb[i] + nb_[i] - 1, 2])
         assert b == nbv[i]
         r = rows[b:e]
-        go = (bins[r.long(), int(fv[i])].long() & mask) <= int(tv[i])
-        lft, rgt = r[go], r[~go]
-        rows_out[b:b + lft.numel()] = lft
-        rows_out[b + lft.numel():e] = rgt
-        left[i] = lft.numel()
+        g = ghp[b:e]
+        go = (binsT[int(fv[i])][r.long()].long() & mask) <= int(tv[i])
+        nl = int(go.sum())
+        rows_out[b:b + nl] = r[go]
+        rows_out[b + nl:e] = r[~go]
+        gh_out[b:b + nl] = g[go]
+        gh_out[b + nl:e] = g[~go]
+        left[i] = nl
     return left
+
+
+def partition_count(binsT, rows, flags, items, feat, thr):
+    """Per-block left counts only (no scatter). Returns int32 [nblk_total]."""
+    nitems = items.shape[0]
+    if binsT.is_cuda:
+        counts = torch.zeros(max(nitems, 1), dtype=torch.int32, device=binsT.device)[:nitems]
+        if nitems == 0:
+            return counts
+        check_cuda(binsT, rows, flags, items, feat, thr)
+        hip().partition_count(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(flags),
+                              ptr(items), nitems, ptr(feat), ptr(thr), ptr(counts), stream(binsT))
+        return counts
+    counts = torch.zeros(nitems, dtype=torch.int32)
+    it = items.numpy()
+    mask = 0xFFFF if binsT.dtype == torch.int16 else 0xFF
+    for j, (si, b, e, _) in enumerate(it):
+        r = rows[b:e].long()
+        counts[j] = int(((binsT[int(feat[si])][r].long() & mask) <= int(thr[si])).sum())
+    return counts
 
 
 # ---------------------------------------------------------------------------
 # scoring
 # ---------------------------------------------------------------------------
-def tree_add_bins(bins, tree_arrays, score, col):
-    """score[:, col] += value(leaf(row)) traversing a bin-threshold tree."""
+def _walk_bins(binsT, tree_arrays):
     tfeat, tthr, tleft, tright, tval = tree_arrays
-    N = bins.shape[0]
-    if bins.is_cuda:
-        check_cuda(bins, tfeat, tthr, tleft, tright, tval, score)
-        hip().tree_add_bins(ptr(bins), _bin_bytes(bins), bins.shape[1], N, ptr(tfeat), ptr(tthr),
-                            ptr(tleft), ptr(tright), ptr(tval), tfeat.shape[0], ptr(score),
-                            score.shape[1], col, stream(bins))
-        return
+    N = binsT.shape[1]
     node = torch.zeros(N, dtype=torch.long)
     tf, tt, tl, tr = (t.long() for t in (tfeat, tthr, tleft, tright))
-    mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
+    mask = 0xFFFF if binsT.dtype == torch.int16 else 0xFF
     ar = torch.arange(N)
-    for _ in range(64):
+    for _ in range(1 << 12):
         f = tf[node]
         active = f >= 0
         if not bool(active.any()):
             break
-        b = bins[ar, f.clamp(min=0)].long() & mask
+        b = binsT[f.clamp(min=0), ar].long() & mask
         nxt = torch.where(b <= tt[node], tl[node], tr[node])
         node = torch.where(active, nxt, node)
-    score[:, col] += tval[node]
+    return tval[node]
+
+
+def tree_add_bins(binsT, tree_arrays, score, col):
+    """score[:, col] += value(leaf(row)) traversing a bin-threshold tree (binsT column-major)."""
+    tfeat, tthr, tleft, tright, tval = tree_arrays
+    N = binsT.shape[1]
+    if binsT.is_cuda:
+        check_cuda(binsT, tfeat, tthr, tleft, tright, tval, score)
+        hip().tree_add_bins(ptr(binsT), _bin_bytes(binsT), N, ptr(tfeat), ptr(tthr), ptr(tleft),
+                            ptr(tright), ptr(tval), tfeat.shape[0], ptr(score), score.shape[1], col,
+                            stream(binsT))
+        return
+    score[:, col] += _walk_bins(binsT, tree_arrays)
 
 
 def forest_predict(X, forest, out, scale=1.0, leaf_out=None):
@@ -279,13 +315,14 @@ def forest_predict(X, forest, out, scale=1.0, leaf_out=None):
 # ---------------------------------------------------------------------------
 # binning
 # ---------------------------------------------------------------------------
-def bin_assign(X, cand, coff, out):
-    """Nearest-candidate bin id per element (FeatureApprData semantics)."""
+def bin_assign(X, cand, coff, out, outT=None):
+    """Nearest-candidate bin id per element (FeatureApprData semantics).
+    out: row-major [N, S]; outT (optional): column-major copy [F, N]."""
     N, F = X.shape
     if X.is_cuda:
-        check_cuda(X, cand, coff, out)
+        check_cuda(X, cand, coff, out, outT)
         hip().bin_assign(ptr(X), X.shape[1], N, F, ptr(cand), ptr(coff), ptr(out),
-                         _bin_bytes(out), out.shape[1], stream(X))
+                         _bin_bytes(out), out.shape[1], ptr(outT), stream(X))
         return
     co = coff.numpy()
     for f in range(F):
@@ -293,18 +330,19 @@ def bin_assign(X, cand, coff, out):
         n = c.numel()
         if n <= 1:
             out[:, f] = 0
-            continue
-        x = X[:, f].contiguous()
-        # index of first candidate > x  (== lo in the binary search)
-        lo = torch.searchsorted(c, x, right=True)
-        u = (lo - 1).clamp(min=0)
-        eq = c[u] == x
-        idx = torch.where(eq, u, lo.clamp(max=n - 1))
-        prevv = c[(idx - 1).clamp(min=0)]
-        down = (idx >= 1) & (x < (c[idx] + prevv) * 0.5)
-        idx = torch.where(down, idx - 1, idx)
-        idx = torch.where(x > c[n - 1], torch.full_like(idx, n - 1), idx)
-        out[:, f] = idx.to(out.dtype)
+        else:
+            x = X[:, f].contiguous()
+            lo = torch.searchsorted(c, x, right=True)  # first candidate > x
+            u = (lo - 1).clamp(min=0)
+            eq = c[u] == x
+            idx = torch.where(eq, u, lo.clamp(max=n - 1))
+            prevv = c[(idx - 1).clamp(min=0)]
+            down = (idx >= 1) & (x < (c[idx] + prevv) * 0.5)
+            idx = torch.where(down, idx - 1, idx)
+            idx = torch.where(x > c[n - 1], torch.full_like(idx, n - 1), idx)
+            out[:, f] = idx.to(out.dtype)
+        if outT is not None:
+            outT[f] = out[:, f]
 
 
 # ---------------------------------------------------------------------------
@@ -372,3 +410,29 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
         gh[:, :, 0] = (g * w[:, None]).float().t()
         gh[:, :, 1] = (h * w[:, None]).float().t()
     return torch.tensor([float((w * lv).sum()), float(w.sum())], dtype=torch.float64)
+
+
+def tree_grad(binsT, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
+              want_grad=True):
+    """Fused K==1 round tail: score += tree(row) (bin space), then pred / (g, h) / loss sums.
+    ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum)."""
+    loss_id = LOSS_IDS[loss]
+    assert loss_id != 5 and score.shape[1] == 1
+    if score.is_cuda:
+        N = score.shape[0]
+        acc = torch.zeros(2, dtype=torch.float64, device=score.device)
+        if tree_arrays is None:
+            tf = tt = tl = tr = tv = None
+            nn = 0
+        else:
+            tf, tt, tl, tr, tv = tree_arrays
+            nn = tf.shape[0]
+        check_cuda(binsT, score, init, label, weight, pred, gh, tf, tt, tl, tr, tv)
+        hip().tree_grad(ptr(binsT), _bin_bytes(binsT) if binsT is not None else 1, ptr(tf), ptr(tt),
+                        ptr(tl), ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label),
+                        ptr(weight), N, loss_id, float(param), float(score_div), ptr(pred), ptr(gh),
+                        ptr(acc), 1 if want_grad else 0, stream(score))
+        return acc
+    if tree_arrays is not None:
+        tree_add_bins(binsT, tree_arrays, score, 0)
+    return grad_hess(score, init, label, weight, loss, param, score_div, pred, gh.unsqueeze(0), want_grad)
