@@ -7,13 +7,13 @@
 
 extern "C" {
 // gbdt_hist.hip
-void ytk_hist_u8(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
-                 uintptr_t);
-void ytk_hist_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
-                     uintptr_t, int, uintptr_t);
+void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
+                 float, float, uintptr_t);
+void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
+                        uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
-                    float, float, float, float, uintptr_t);
+                    float, float, float, float, double, double, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -39,8 +39,8 @@ namespace py = pybind11;
 
 PYBIND11_MODULE(_ytk_hip, m) {
   m.doc() = "ytk-learn-amd HIP kernels (gfx950)";
-  m.def("hist_u8", &ytk_hist_u8);
-  m.def("hist_global", &ytk_hist_global);
+  m.def("hist_fx", &ytk_hist_fx);
+  m.def("hist_fx_global", &ytk_hist_fx_global);
   m.def("split_find", &ytk_split_find);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);

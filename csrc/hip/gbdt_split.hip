@@ -1,20 +1,19 @@
-// GBDT best-split search (gfx950 / CDNA4, wave64).
+// GBDT best-split search over exact int64 fixed-point histograms (gfx950, wave64).
 //
 // Reference semantics:
 //   split enumeration    J/optimizer/gbdt/DataParallelTreeMaker.java:598-637
-//     (left-to-right bin scan, empty bins (g==0 && h==0) skipped, first hit only
-//      initialises the left sum, min_child_hessian_sum on both sides)
+//     (left-to-right bin scan, empty bins (g==0 && h==0) skipped, a hit on an
+//      empty left sum (H==0) only initialises it, min_child_hessian_sum both sides)
 //   gain / leaf value    J/optimizer/gbdt/UpdateStrategy.java:50-100
 //   node totals          DataParallelTreeMaker.java:543-573 (first sampled feature)
-//   tie-break            J/data/gbdt/SplitInfo.java:99-104 (max lossChg, then
-//                        lower feature; within a feature the first bin)
+//   tie-break            J/data/gbdt/SplitInfo.java:99-104 (max lossChg, then lower
+//                        feature; within a feature the first bin)
 //
-// Design: one workgroup (4 waves) per node; each wave owns features
-// f = wave, wave+4, ...; a lane owns 4 consecutive bins; fp64 wave prefix scans
-// (shuffle) give the left sums; argmax reduces (chg, feature, bin)
-// lexicographically -> deterministic. Sibling subtraction (parent - small child)
-// is fused into the load and the derived histogram is written back for the
-// node's own children.
+// Design: one workgroup (4 waves) per node; wave w owns features w, w+4, ...; a lane
+// owns 4 consecutive bins; int64 wave prefix scans (exact) -> prefix sums are
+// converted to double only to evaluate gains; (chg, feature, bin) argmax is
+// lexicographic -> deterministic. Sibling subtraction (parent - small child) is
+// fused into the load (exact in int64) and written back for the node's children.
 #include "common.h"
 
 namespace ytk {
@@ -33,6 +32,7 @@ struct GainParams {
   float mcw;  // min_child_hessian_sum
   float l1, l2;
   float max_abs_leaf;
+  double inv_sg, inv_sh;  // fixed-point -> real
 };
 
 __device__ __forceinline__ double thr_l1(double w, double lam) {
@@ -69,9 +69,25 @@ __device__ __forceinline__ bool better(float c1, int f1, int b1, float c2, int f
   return b1 < b2;
 }
 
-// items[blk] = {slot, parent_slot, sibling_slot, derived}
+__device__ __forceinline__ long long wave_incl_scan_ll(long long v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const long long o = __shfl_up(v, off, kWave);
+    if (l >= off) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ long long wave_sum_ll(long long v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// hist: int64 [slot][B][F][2]. items[blk] = {slot, parent_slot, sibling_slot, derived}
 __global__ __launch_bounds__(256) void split_find_kernel(
-    float2* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
+    long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp) {
   __shared__ float s_chg[4];
@@ -81,34 +97,35 @@ __global__ __launch_bounds__(256) void split_find_kernel(
   const int4 it = items[blockIdx.x];
   const int wid = threadIdx.x >> 6;
   const int l = lane_id();
-  float2* hn = hist + (size_t)it.x * B * F;
-  const float2* hp = hist + (size_t)it.y * B * F;
-  const float2* hs = hist + (size_t)it.z * B * F;
+  const size_t slot_sz = (size_t)B * F * 2;
+  longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
+  const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
+  const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
   const bool derived = it.w != 0;
 
-  auto load = [&](int f, int bin) -> float2 {
+  auto load = [&](int f, int bin) -> longlong2 {
     const size_t idx = (size_t)bin * F + f;
     if (derived) {
-      const float2 p = hp[idx], s = hs[idx];
-      return make_float2(p.x - s.x, p.y - s.y);
+      const longlong2 p = hp[idx], s = hs[idx];
+      return make_longlong2(p.x - s.x, p.y - s.y);
     }
     return hn[idx];
   };
 
-  // Node totals from the first sampled feature; every wave computes them
-  // identically (no cross-wave hand-off needed).
-  double G = 0.0, H = 0.0;
+  // Node totals from the first sampled feature (exact; every wave computes them).
+  long long Gq = 0, Hq = 0;
   {
     const int nb0 = nbins_f[f0];
-    double sg = 0.0, sh = 0.0;
+    long long sg = 0, sh = 0;
     for (int bin = l; bin < nb0; bin += kWave) {
-      const float2 v = load(f0, bin);
+      const longlong2 v = load(f0, bin);
       sg += v.x;
       sh += v.y;
     }
-    G = wave_sum(sg);
-    H = wave_sum(sh);
+    Gq = wave_sum_ll(sg);
+    Hq = wave_sum_ll(sh);
   }
+  const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
   const float root_gain = (float)calc_gain(G, H, gp);
 
   float best_chg = -INFINITY;
@@ -118,43 +135,44 @@ __global__ __launch_bounds__(256) void split_find_kernel(
   for (int f = wid; f < F; f += 4) {
     if (!fmask[f]) continue;
     const int nb = nbins_f[f];
-    double carry_g = 0.0, carry_h = 0.0;
+    long long carry_g = 0, carry_h = 0;
     int carry_last = -1;
     for (int c = 0; c < B; c += 4 * kWave) {
-      float2 v[4];
-      double sg = 0.0, sh = 0.0;
+      longlong2 v[4];
+      long long sg = 0, sh = 0;
       int lastne = -1;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int bin = c + 4 * l + k;
-        v[k] = make_float2(0.f, 0.f);
+        v[k] = make_longlong2(0, 0);
         if (bin < nb) v[k] = load(f, bin);
         if (derived && bin < B) hn[(size_t)bin * F + f] = v[k];
         sg += v[k].x;
         sh += v[k].y;
-        if (v[k].x != 0.f || v[k].y != 0.f) lastne = bin;
+        if (v[k].x != 0 || v[k].y != 0) lastne = bin;
       }
-      const double ig = wave_incl_scan(sg);
-      const double ih = wave_incl_scan(sh);
+      const long long ig = wave_incl_scan_ll(sg);
+      const long long ih = wave_incl_scan_ll(sh);
       const int im = wave_incl_max(lastne);
       int em = __shfl_up(im, 1, kWave);
       if (l == 0) em = -1;
-      double pg = ig - sg + carry_g;
-      double ph = ih - sh + carry_h;
+      long long pg = ig - sg + carry_g;
+      long long ph = ih - sh + carry_h;
       int prev = max(em, carry_last);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int bin = c + 4 * l + k;
-        const bool ne = (v[k].x != 0.f || v[k].y != 0.f);
+        const bool ne = (v[k].x != 0 || v[k].y != 0);
         if (ne) {
-          if (prev >= 0 && ph != 0.0 && ph >= (double)gp.mcw) {
-            const double rg = G - pg, rh = H - ph;
-            if (rh >= (double)gp.mcw) {
+          const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
+          if (prev >= 0 && ph != 0 && dhl >= (double)gp.mcw) {
+            const double dgr = (double)(Gq - pg) * gp.inv_sg, dhr = (double)(Hq - ph) * gp.inv_sh;
+            if (dhr >= (double)gp.mcw) {
               const float chg =
-                  (float)(calc_gain(pg, ph, gp) + calc_gain(rg, rh, gp) - (double)root_gain);
+                  (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
               if (better(chg, f, bin, best_chg, best_f, best_b)) {
                 best_chg = chg; best_f = f; best_a = prev; best_b = bin;
-                best_gl = pg; best_hl = ph;
+                best_gl = dgl; best_hl = dhl;
               }
             }
           }
@@ -208,11 +226,12 @@ using namespace ytk;
 
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
                                int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
-                               float l1, float l2, float max_abs_leaf, uintptr_t stream) {
+                               float l1, float l2, float max_abs_leaf, double inv_sg,
+                               double inv_sh, uintptr_t stream) {
   if (nitems <= 0) return;
-  GainParams gp{mcw, l1, l2, max_abs_leaf};
+  GainParams gp{mcw, l1, l2, max_abs_leaf, inv_sg, inv_sh};
   hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), (float2*)hist, B, F,
+                     reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
                      (SplitOut*)out, gp);
   YTK_LAUNCH_CHECK();

@@ -25,6 +25,10 @@ def _gh(N, seed=1):
     return gh
 
 
+
+SG, SH = gops.fixed_point_scales(3.0, 0.25, 200000)
+
+
 @pytest.mark.parametrize("F,nb", [(28, 255), (7, 16), (40, 64)])
 def test_hist_build_matches_cpu(cuda, F, nb):
     N = 50000
@@ -33,18 +37,26 @@ def test_hist_build_matches_cpu(cuda, F, nb):
     B = ((nb + 3) // 4) * 4
     perm = torch.randperm(N, generator=torch.Generator().manual_seed(3)).to(torch.int32)
     work = torch.tensor([[0, 0, 20000, 0], [0, 20000, 31000, 0], [2, 31000, 50000, 0]], dtype=torch.int32)
-    hc = torch.zeros((3, B, F, 2))
-    gops.hist_build(bins, F, gh, perm, work, hc, B)
-    hg = torch.zeros((3, B, F, 2), device=cuda)
-    gops.hist_build(bins.to(cuda), F, gh.to(cuda), perm.to(cuda), work.to(cuda), hg, B)
-    torch.testing.assert_close(hg.cpu(), hc, rtol=1e-4, atol=1e-3)
+    hc = torch.zeros((3, B, F, 2), dtype=torch.int64)
+    gops.hist_build(bins, F, gh, perm, work, hc, B, SG, SH)
+    hg = torch.zeros((3, B, F, 2), dtype=torch.int64, device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), perm.to(cuda), work.to(cuda), hg, B, SG, SH)
+    assert torch.equal(hg.cpu(), hc)  # exact integer sums: bitwise identical
     # identity rows (root path)
-    hc2 = torch.zeros((1, B, F, 2))
+    hc2 = torch.zeros((1, B, F, 2), dtype=torch.int64)
     w2 = torch.tensor([[0, 0, N, 0]], dtype=torch.int32)
-    gops.hist_build(bins, F, gh, None, w2, hc2, B)
-    hg2 = torch.zeros((1, B, F, 2), device=cuda)
-    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, w2.to(cuda), hg2, B)
-    torch.testing.assert_close(hg2.cpu(), hc2, rtol=1e-4, atol=2e-3)
+    gops.hist_build(bins, F, gh, None, w2, hc2, B, SG, SH)
+    hg2 = torch.zeros((1, B, F, 2), dtype=torch.int64, device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, w2.to(cuda), hg2, B, SG, SH)
+    assert torch.equal(hg2.cpu(), hc2)
+    # fixed point is faithful to the fp64 sums
+    ref = torch.zeros((B, F, 2), dtype=torch.float64)
+    b64 = bins[:, :F].long()
+    for f in range(F):
+        ref[:, f, 0].index_add_(0, b64[:, f], gh[:, 0].double())
+        ref[:, f, 1].index_add_(0, b64[:, f], gh[:, 1].double())
+    got = hc2[0].double() * torch.tensor([1.0 / SG, 1.0 / SH], dtype=torch.float64)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-6)
 
 
 def test_hist_build_uint16_global(cuda):
@@ -53,18 +65,18 @@ def test_hist_build_uint16_global(cuda):
     gh = _gh(N)
     B = 1000
     work = torch.tensor([[0, 0, N, 0]], dtype=torch.int32)
-    hc = torch.zeros((1, B, F, 2))
-    gops.hist_build(bins, F, gh, None, work, hc, B)
-    hg = torch.zeros((1, B, F, 2), device=cuda)
-    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, work.to(cuda), hg, B)
-    torch.testing.assert_close(hg.cpu(), hc, rtol=1e-4, atol=1e-3)
+    hc = torch.zeros((1, B, F, 2), dtype=torch.int64)
+    gops.hist_build(bins, F, gh, None, work, hc, B, SG, SH)
+    hg = torch.zeros((1, B, F, 2), dtype=torch.int64, device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), None, work.to(cuda), hg, B, SG, SH)
+    assert torch.equal(hg.cpu(), hc)
 
 
 def _hist_from(N, F, nb, B, seed):
     bins = _rand_bins(N, F, nb, seed)
     gh = _gh(N, seed + 1)
-    h = torch.zeros((1, B, F, 2))
-    gops.hist_build(bins, F, gh, None, torch.tensor([[0, 0, N, 0]], dtype=torch.int32), h, B)
+    h = torch.zeros((1, B, F, 2), dtype=torch.int64)
+    gops.hist_build(bins, F, gh, None, torch.tensor([[0, 0, N, 0]], dtype=torch.int32), h, B, SG, SH)
     return h[0]
 
 
@@ -73,17 +85,16 @@ def test_split_find_matches_cpu(cuda, l1, l2, mal):
     F, nb, B = 28, 200, 200
     parent = _hist_from(40000, F, nb, B, 5)
     small = _hist_from(15000, F, nb, B, 6)
-    hist = torch.zeros((4, B, F, 2))
-    hist[0] = parent
+    hist = torch.zeros((4, B, F, 2), dtype=torch.int64)
+    hist[0] = parent + small  # parent contains the small child
     hist[1] = small
-    # make bins sparse for some features (empty-bin skipping)
-    hist[1, 50:120, 3] = 0
+    hist[1, 50:120, 3] = 0  # sparse bins (empty-bin skipping)
     nbins = torch.full((F,), nb, dtype=torch.int32)
     nbins[7] = 30
     fmask = torch.ones(F, dtype=torch.uint8)
     fmask[2] = 0
     items = torch.tensor([[0, 0, 0, 0], [1, 0, 0, 0], [2, 0, 1, 1]], dtype=torch.int32)
-    params = {"mcw": 10.0, "l1": l1, "l2": l2, "max_abs_leaf": mal}
+    params = {"mcw": 10.0, "l1": l1, "l2": l2, "max_abs_leaf": mal, "sg": SG, "sh": SH}
     hc = hist.clone()
     oc = gops.split_find(hc, B, F, nbins, fmask, 0, items, params).numpy().view(gops.SPLIT_DTYPE).reshape(-1)
     hg = hist.to(cuda)
@@ -91,15 +102,15 @@ def test_split_find_matches_cpu(cuda, l1, l2, mal):
     og = og.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
     for a, b in zip(oc, og):
         assert a["feat"] == b["feat"] and a["bin_a"] == b["bin_a"] and a["bin_b"] == b["bin_b"]
-        np.testing.assert_allclose(a["loss_chg"], b["loss_chg"], rtol=1e-5)
+        assert a["loss_chg"] == b["loss_chg"]
         np.testing.assert_allclose([a["gl"], a["hl"], a["g"], a["h"]], [b["gl"], b["hl"], b["g"], b["h"]],
-                                   rtol=1e-9, atol=1e-9)
-    # derived histogram written back (bins < nbins of each sampled feature)
+                                   rtol=1e-12, atol=0)
+    # derived histogram written back exactly (bins < nbins of each sampled feature)
     ref = hist[0] - hist[1]
     for f in range(F):
         if fmask[f]:
             n = int(nbins[f])
-            torch.testing.assert_close(hg[2, :n, f].cpu(), ref[:n, f])
+            assert torch.equal(hg[2, :n, f].cpu(), ref[:n, f])
 
 
 def test_partition_matches_cpu(cuda):

@@ -170,7 +170,9 @@ class TreeBuilder:
         else:
             max_nodes = 2 * ml - 1
         self.max_nodes = int(max_nodes)
-        self.hist = torch.zeros((self.max_nodes, B, F, 2), dtype=torch.float32, device=self.dev)
+        # exact int64 fixed-point histograms (see csrc/hip/gbdt_hist.hip)
+        self.hist = torch.zeros((self.max_nodes, B, F, 2), dtype=torch.int64, device=self.dev)
+        self.gp_tree = dict(self.gp, sg=1.0, sh=1.0)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=self.dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=self.dev)
         self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=self.dev)
@@ -224,7 +226,7 @@ class TreeBuilder:
         if nb:
             self.hist[s0:s0 + nb].zero_()
             gops.hist_build(self.bins, self.F, self.ghp, None if identity_rows else self.rows,
-                            work_d, self.hist, self.B)
+                            work_d, self.hist, self.B, self.gp_tree["sg"], self.gp_tree["sh"])
         self._sync()
         t1 = time.perf_counter()
         if nb and self.comm.is_dist:
@@ -232,7 +234,7 @@ class TreeBuilder:
             self._sync()
         t2 = time.perf_counter()
         order = list(build) + [n for n, _, _ in derived]
-        out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp)
+        out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp_tree)
         recs = out.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
         self.up.reset()  # the .cpu() above synchronised the stream
         t3 = time.perf_counter()
@@ -366,6 +368,16 @@ class TreeBuilder:
         fmask = self.fmask
 
         n_global = int(self.comm.allreduce_scalars([n_local], dtype=torch.int64)[0]) if self.comm.is_dist else n_local
+        # per-tree fixed-point scales from the global max |g|, |h| (identical on every rank)
+        if n_local > 0:
+            mx = self.ghp[:n_local].abs().amax(dim=0).double()
+        else:
+            mx = torch.zeros(2, dtype=torch.float64, device=self.dev)
+        if self.comm.is_dist:
+            self.comm.allreduce_(mx, op="max")
+        mx = mx.cpu().numpy()
+        sg, sh = gops.fixed_point_scales(mx[0], mx[1], n_global)
+        self.gp_tree = dict(self.gp, sg=sg, sh=sh)
         tree = Tree()
         nodes: Dict[int, _Node] = {0: _Node(begin=0, cnt_local=n_local, cnt_global=n_global, depth=0, seq=0)}
         self._build_and_find(nodes, [0], [], fmask, f0, identity_rows=identity)

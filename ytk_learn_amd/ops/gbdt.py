@@ -35,18 +35,45 @@ def _bin_bytes(bins: torch.Tensor) -> int:
 # ---------------------------------------------------------------------------
 # histogram build
 # ---------------------------------------------------------------------------
-def hist_build(bins, F, ghp, rows, work, hist, B):
-    """Accumulate (g, h) histograms.
+def fixed_point_scales(max_abs_g: float, max_h: float, n_rows: int):
+    """Per-tree power-of-two scales so |sum over all rows| < 2^62 (exact int64 sums).
+
+    Returns (sg, sh) as float32-representable powers of two."""
+    out = []
+    for m in (max_abs_g, max_h):
+        m = float(m)
+        if not np.isfinite(m):
+            raise ValueError("non-finite gradient/hessian")
+        if m <= 0.0:
+            out.append(1.0)
+            continue
+        k = int(np.floor(np.log2((2.0 ** 62) / (m * max(1, int(n_rows))))))
+        out.append(float(2.0 ** min(max(k, -120), 120)))
+    return out[0], out[1]
+
+
+def quantize_gh(gh: torch.Tensor, sg: float, sh: float) -> torch.Tensor:
+    """Reference of the kernels' rounding: __float2ll_rn(x * 2^k) per component."""
+    q = torch.empty(gh.shape, dtype=torch.int64, device=gh.device)
+    q[..., 0] = torch.round(gh[..., 0].float() * np.float32(sg)).to(torch.int64)
+    q[..., 1] = torch.round(gh[..., 1].float() * np.float32(sh)).to(torch.int64)
+    return q
+
+
+def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh):
+    """Accumulate exact int64 fixed-point (g, h) histograms.
 
     bins: [N, S] uint8/int16 row-major (S >= F, S % 32 == 0 for the LDS path)
     ghp:  [M, 2] float32 (g, h) in POSITION order (ghp[pos] belongs to rows[pos])
     rows: int32 row permutation or None (identity positions)
     work: int32 [nwork, 4] = (slot, begin, end, 0); positions index ``rows``
-    hist: float32 [slots, B, F, 2], target slots must be zeroed by the caller
+    hist: int64 [slots, B, F, 2], target slots must be zeroed by the caller
+    sg, sh: power-of-two fixed-point scales (``fixed_point_scales``)
     """
     nwork = work.shape[0]
     if nwork == 0:
         return
+    assert hist.dtype == torch.int64
     if bins.is_cuda:
         check_cuda(bins, ghp, rows, work, hist)
         assert hist.shape[1] == B and hist.shape[2] == F and hist.shape[3] == 2
@@ -56,13 +83,13 @@ def hist_build(bins, F, ghp, rows, work, hist, B):
         stride = bins.shape[1]
         h = hip()
         if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
-            h.hist_u8(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
-                      stream(bins))
+            h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                      float(sg), float(sh), stream(bins))
         else:
-            h.hist_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
-                          nwork, ptr(hist), B, stream(bins))
+            h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
+                             nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
         return
-    # CPU reference
+    # CPU reference (bitwise identical: integer sums)
     w = work.numpy()
     hv = hist.view(-1, 2)
     mask = 0xFFFF if bins.dtype == torch.int16 else 0xFF
@@ -72,7 +99,7 @@ def hist_build(bins, F, ghp, rows, work, hist, B):
         r = rows[b:e].long() if rows is not None else torch.arange(b, e, dtype=torch.long)
         bb = bins[r, :F].long() & mask
         idx = (int(slot) * B + bb) * F + torch.arange(F, dtype=torch.long)[None, :]
-        v = ghp[b:e][:, None, :].expand(-1, F, 2)
+        v = quantize_gh(ghp[b:e], sg, sh)[:, None, :].expand(-1, F, 2)
         hv.index_add_(0, idx.reshape(-1), v.reshape(-1, 2))
 
 
@@ -87,13 +114,15 @@ def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
     """
     n = items.shape[0]
     mcw, l1, l2, mal = (float(params[k]) for k in ("mcw", "l1", "l2", "max_abs_leaf"))
+    inv_sg, inv_sh = 1.0 / float(params["sg"]), 1.0 / float(params["sh"])
+    assert hist.dtype == torch.int64
     if hist.is_cuda:
         out = torch.empty((n, 48), dtype=torch.uint8, device=hist.device)
         if n == 0:
             return out
         check_cuda(hist, nbins_f, fmask, items)
         hip().split_find(ptr(hist), B, F, ptr(nbins_f), ptr(fmask), int(f0), ptr(items), n,
-                         ptr(out), mcw, l1, l2, mal, stream(hist))
+                         ptr(out), mcw, l1, l2, mal, inv_sg, inv_sh, stream(hist))
         return out
     res = np.zeros(n, dtype=SPLIT_DTYPE)
     it = items.numpy()
@@ -102,8 +131,8 @@ def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
     for i, (slot, par, sib, der) in enumerate(it):
         if der:
             hist[slot] = hist[par] - hist[sib]
-        hn = hist[slot].numpy()  # [B, F, 2] float32
-        res[i] = _split_one_cpu(hn, nb, fm, int(f0), mcw, l1, l2, mal)
+        hn = hist[slot].numpy()  # [B, F, 2] int64
+        res[i] = _split_one_cpu(hn, nb, fm, int(f0), mcw, l1, l2, mal, inv_sg, inv_sh)
     return torch.from_numpy(res.view(np.uint8).reshape(n, 48).copy())
 
 
@@ -133,11 +162,11 @@ def calc_gain_np(g, h, mcw, l1, l2, mal):
     return np.where(h < mcw, 0.0, gain)
 
 
-def _split_one_cpu(hn, nb, fm, f0, mcw, l1, l2, mal):
+def _split_one_cpu(hn, nb, fm, f0, mcw, l1, l2, mal, inv_sg, inv_sh):
     Bn, Fn, _ = hn.shape
-    hd = hn.astype(np.float64)
-    G = float(hd[: nb[f0], f0, 0].sum())
-    H = float(hd[: nb[f0], f0, 1].sum())
+    Gq = int(hn[: nb[f0], f0, 0].sum())
+    Hq = int(hn[: nb[f0], f0, 1].sum())
+    G, H = float(np.float64(Gq) * inv_sg), float(np.float64(Hq) * inv_sh)
     root_gain = np.float32(calc_gain_np(G, H, mcw, l1, l2, mal))
     best = (-np.inf, 1 << 30, 1 << 30)
     rec = (np.float32(-np.inf), -1, -1, -1, 0.0, 0.0)
@@ -145,16 +174,17 @@ def _split_one_cpu(hn, nb, fm, f0, mcw, l1, l2, mal):
         if not fm[f]:
             continue
         m = min(nb[f], Bn)
-        g = hd[:m, f, 0]
-        h = hd[:m, f, 1]
-        ne = (hn[:m, f, 0] != 0) | (hn[:m, f, 1] != 0)
-        pg = np.concatenate([[0.0], np.cumsum(g)[:-1]])  # exclusive prefix
-        ph = np.concatenate([[0.0], np.cumsum(h)[:-1]])
+        gq = hn[:m, f, 0]
+        hq = hn[:m, f, 1]
+        ne = (gq != 0) | (hq != 0)
+        pgq = np.concatenate([[0], np.cumsum(gq)[:-1]]).astype(np.int64)  # exclusive prefix
+        phq = np.concatenate([[0], np.cumsum(hq)[:-1]]).astype(np.int64)
+        pg, ph = pgq.astype(np.float64) * inv_sg, phq.astype(np.float64) * inv_sh
         idx = np.where(ne, np.arange(m), -1)
         lastne = np.maximum.accumulate(idx) if m else idx
         prev = np.concatenate([[-1], lastne[:-1]])
-        ok = ne & (prev >= 0) & (ph != 0.0) & (ph >= mcw)
-        rg, rh = G - pg, H - ph
+        ok = ne & (prev >= 0) & (phq != 0) & (ph >= mcw)
+        rg, rh = (Gq - pgq).astype(np.float64) * inv_sg, (Hq - phq).astype(np.float64) * inv_sh
         ok &= rh >= mcw
         if not ok.any():
             continue
