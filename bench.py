@@ -92,9 +92,7 @@ def main():
     tr = GBDTTrainer(params, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log, profile=a.profile)
     t0 = time.perf_counter()
     tr.prepare()
-    # initial prediction + gradients (GBDTOptimizer.initPred)
-    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
-    tr._loss_grad(tr.te_score, tr.te_init, yt, None, tr.te_pred, tr.te_gh, 0, False)
+    tr.init_gradients()  # initial prediction + gradients (GBDTOptimizer.initPred)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     prep_s = time.perf_counter() - t0
@@ -115,9 +113,10 @@ def main():
 
     # quality check after the timed rounds (outside timing)
     auc = tr.eval_test.evals[0].compute(yt, tr.te_pred, None, comm)[0]
+    train_loss, test_loss = tr._losses()  # collective: every rank calls it
     sec_per_tree = el_max / a.steps
     if a.profile and rank == 0:
-        print(tr.builder.total_stats.stats(), file=sys.stderr)
+        print(getattr(tr.builder, "total_stats", ""), file=sys.stderr)
     if rank == 0:
         res = {
             "metric": METRIC,

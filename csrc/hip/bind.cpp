@@ -2,24 +2,27 @@
 // (tensor.data_ptr()), streams as the raw hipStream_t of the current torch stream.
 // Shape/dtype/device validation happens in ytk_learn_amd/ops/*.py before any call.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
+#include <stdexcept>
+#include <vector>
 
 extern "C" {
 // gbdt_hist.hip
 void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
-                 float, float, uintptr_t);
+                 float, float, uintptr_t, uintptr_t, uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
-                    float, float, float, float, double, double, uintptr_t);
+                    float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                   uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+                   uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_partition_count(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, int,
-                         uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+                         uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_score.hip
 void ytk_tree_add_bins(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, int, uintptr_t, int, int, uintptr_t);
@@ -33,6 +36,11 @@ void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, i
 void ytk_tree_grad(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
                    uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, float, float,
                    uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+// gbdt_level.hip
+void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
+void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
+                     uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 }
 
 namespace py = pybind11;
@@ -49,5 +57,20 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("bin_assign", &ytk_bin_assign);
   m.def("grad_hess", &ytk_grad_hess);
   m.def("tree_grad", &ytk_tree_grad);
+  m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
+                      const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
+    if (ptrs.size() != 25 || ip.size() != 6 || fp.size() != 6)
+      throw std::invalid_argument("lv_step: bad argument sizes");
+    ytk_lv_step(which, ptrs.data(), ip.data(), fp.data(), a0, a1, stream);
+  });
+  m.def("lv_raw_tree", [](const std::vector<uintptr_t>& ptrs, int max_nodes, uintptr_t cand,
+                          uintptr_t coff, uintptr_t fill, int split_median, uintptr_t nfeat,
+                          uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
+                          uintptr_t nval, uintptr_t stream) {
+    if (ptrs.size() != 25) throw std::invalid_argument("lv_raw_tree: bad ptrs");
+    ytk_lv_raw_tree(ptrs.data(), max_nodes, cand, coff, fill, split_median, nfeat, nthr, nleft,
+                    nright, ndefl, nval, stream);
+  });
+  m.def("lv_scales", &ytk_lv_scales);
   m.attr("arch") = "gfx950";
 }

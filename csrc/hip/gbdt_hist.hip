@@ -33,10 +33,16 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const uint8_t* __restrict__ bins, long long stride, int F,
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B, int nb_lds,
-    float sg, float sh) {
+    float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];
   unsigned long long* lg = sm64;
   unsigned long long* lh = sm64 + nb_lds * 32;
+  // device-resident work count (fixed maximal grid launched by the level engine)
+  if (nwork_dev && (int)blockIdx.x >= *nwork_dev) return;
+  if (scales_dev) {
+    sg = scales_dev[0];
+    sh = scales_dev[1];
+  }
   const int4 w = work[blockIdx.x];
   const int fg = blockIdx.y;
   const int tid = threadIdx.x;
@@ -123,9 +129,11 @@ using namespace ytk;
 
 extern "C" {
 
+// nwork_dev / scales_dev (optional): device-resident work count (grid = nwork is the
+// maximum) and fixed-point scales, used by the GPU-resident level engine.
 void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
                  uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
-                 uintptr_t stream) {
+                 uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t stream) {
   if (nwork <= 0) return;
   const int groups = (F + 31) / 32;
   const int nb_lds = B;  // caller guarantees B <= 256
@@ -135,11 +143,13 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
   if (rows == 0) {
     hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh);
+                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
+                       (const int*)nwork_dev, (const float*)scales_dev);
   } else {
     hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh);
+                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
+                       (const int*)nwork_dev, (const float*)scales_dev);
   }
   YTK_LAUNCH_CHECK();
 }

@@ -25,8 +25,9 @@ template <typename BinT>
 __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const int4* __restrict__ items, const int* __restrict__ feat, const int* __restrict__ thr,
-    uint8_t* __restrict__ flags, int* __restrict__ counts) {
+    uint8_t* __restrict__ flags, int* __restrict__ counts, const int* __restrict__ nitems_dev) {
   __shared__ int s_cnt[kPartThreads / kWave];
+  if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   const int4 it = items[blockIdx.x];
   const BinT* col = binsT + (size_t)feat[it.x] * ncol;
   const int t = thr[it.x];
@@ -59,10 +60,12 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
     const int4* __restrict__ items, const int* __restrict__ node_begin,
     const int* __restrict__ first_blk, const int* __restrict__ nblk,
-    const int* __restrict__ counts, int* __restrict__ left_total_out) {
+    const int* __restrict__ counts, int* __restrict__ left_total_out,
+    const int* __restrict__ nitems_dev) {
   constexpr int NW = kPartThreads / kWave;
   __shared__ int s_red[2 * NW];
   __shared__ int s_l[kPartSub * NW], s_v[kPartSub * NW];
+  if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   const int4 it = items[blockIdx.x];
   const int si = it.x;
   const int nbeg = node_begin[si], fb = first_blk[si], nb = nblk[si];
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
   total = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) { before += s_red[w]; total += s_red[NW + w]; }
-  if (it.w == 0 && tid == 0) left_total_out[si] = total;
+  if (left_total_out && it.w == 0 && tid == 0) left_total_out[si] = total;
 
   int lbase = nbeg + before;
   int rbase = nbeg + total + (it.y - nbeg - before);
@@ -153,17 +156,19 @@ using namespace ytk;
 extern "C" void ytk_partition_count(uintptr_t binsT, int bin_bytes, long long ncol,
                                     uintptr_t rows, uintptr_t flags, uintptr_t items, int nitems,
                                     uintptr_t feat, uintptr_t thr, uintptr_t counts,
-                                    uintptr_t stream) {
+                                    uintptr_t nitems_dev, uintptr_t stream) {
   if (nitems <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (bin_bytes == 1) {
     hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
-                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
+                       (const int*)nitems_dev);
   } else {
     hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
-                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
+                       (const int*)nitems_dev);
   }
   YTK_LAUNCH_CHECK();
 }
@@ -173,23 +178,25 @@ extern "C" void ytk_partition(uintptr_t binsT, int bin_bytes, long long ncol, ui
                               uintptr_t flags, uintptr_t items, int nitems, uintptr_t feat,
                               uintptr_t thr, uintptr_t node_begin, uintptr_t first_blk,
                               uintptr_t nblk, uintptr_t counts, uintptr_t left_total,
-                              uintptr_t stream) {
+                              uintptr_t nitems_dev, uintptr_t stream) {
   if (nitems <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (bin_bytes == 1) {
     hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
-                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
+                       (const int*)nitems_dev);
   } else {
     hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
-                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts);
+                       (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
+                       (const int*)nitems_dev);
   }
   YTK_LAUNCH_CHECK();
   hipLaunchKernelGGL(partition_scatter_kernel, dim3(nitems), dim3(kPartThreads), 0, s,
                      (const uint8_t*)flags, (const int*)rows, (const float2*)ghp, (int*)rows_out,
                      (float2*)gh_out, (const int4*)items, (const int*)node_begin,
                      (const int*)first_blk, (const int*)nblk, (const int*)counts,
-                     (int*)left_total);
+                     (int*)left_total, (const int*)nitems_dev);
   YTK_LAUNCH_CHECK();
 }

@@ -89,11 +89,17 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
 __global__ __launch_bounds__(256) void split_find_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
-    SplitOut* __restrict__ out, GainParams gp) {
+    SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
+    const double* __restrict__ inv_dev) {
   __shared__ float s_chg[4];
   __shared__ int s_feat[4], s_a[4], s_b[4];
   __shared__ double s_gl[4], s_hl[4];
 
+  if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
+  if (inv_dev) {
+    gp.inv_sg = inv_dev[0];
+    gp.inv_sh = inv_dev[1];
+  }
   const int4 it = items[blockIdx.x];
   const int wid = threadIdx.x >> 6;
   const int l = lane_id();
@@ -227,12 +233,13 @@ using namespace ytk;
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
                                int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
                                float l1, float l2, float max_abs_leaf, double inv_sg,
-                               double inv_sh, uintptr_t stream) {
+                               double inv_sh, uintptr_t nitems_dev, uintptr_t inv_dev,
+                               uintptr_t stream) {
   if (nitems <= 0) return;
   GainParams gp{mcw, l1, l2, max_abs_leaf, inv_sg, inv_sh};
   hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
-                     (SplitOut*)out, gp);
+                     (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev);
   YTK_LAUNCH_CHECK();
 }

@@ -102,7 +102,8 @@ def test_split_find_matches_cpu(cuda, l1, l2, mal):
     og = og.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
     for a, b in zip(oc, og):
         assert a["feat"] == b["feat"] and a["bin_a"] == b["bin_a"] and a["bin_b"] == b["bin_b"]
-        assert a["loss_chg"] == b["loss_chg"]
+        # fp64 gain evaluation may contract to FMA on the GPU: 1 float ulp
+        np.testing.assert_allclose(a["loss_chg"], b["loss_chg"], rtol=1e-6)
         np.testing.assert_allclose([a["gl"], a["hl"], a["g"], a["h"]], [b["gl"], b["hl"], b["g"], b["h"]],
                                    rtol=1e-12, atol=0)
     # derived histogram written back exactly (bins < nbins of each sampled feature)

@@ -25,7 +25,7 @@ def test_train_cpu_loss_decreases(policy):
     tr = GBDTTrainer(_params(policy), _data(20000, 1), _data(4000, 2))
     tr.prepare()
     losses = []
-    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
+    tr.init_gradients()
     for i in range(4):
         tr.step(i)
         losses.append(tr.last_train_loss)
@@ -79,7 +79,7 @@ def test_other_losses_cpu(loss, K):
     p.eval_metric = ["confusion_matrix"] if loss == "softmax" else ["rmse", "mae"]
     tr = GBDTTrainer(p, GBDTData(X, y), GBDTData(X[:1000], y[:1000]))
     tr.prepare()
-    tr._loss_grad(tr.score, tr.init_score, tr.y, tr.w, tr.pred, tr.gh, 0)
+    tr.init_gradients()
     l0 = None
     for i in range(3):
         tr.step(i)
@@ -112,3 +112,22 @@ def test_train_gpu_matches_cpu(cuda, policy):
     a, b = t_cpu.model.trees[0], t_gpu.model.trees[0]
     assert a.feat[0] == b.feat[0] and a.slot_a[0] == b.slot_a[0]
     assert a.num_nodes == b.num_nodes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 11}, {"min_split_samples": 3000}, {"l2": 1.0, "l1": 0.5}])
+def test_device_builder_matches_host_builder(cuda, kw):
+    """GPU-resident level builder == host-driven builder (integer histograms => identical trees)."""
+    d = _data(40000, 9, cuda)
+    trees = []
+    for dev_builder in (False, True):
+        p = _params("level", rounds=3, **{k: v for k, v in kw.items() if k not in ("max_leaf_cnt",)})
+        if "max_leaf_cnt" in kw:
+            p.tree.max_leaf_cnt = kw["max_leaf_cnt"]
+        p.device_builder = dev_builder
+        tr = GBDTTrainer(p, d, _data(5000, 10, cuda))
+        tr.train()
+        assert tr.use_device_builder == dev_builder
+        trees.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert trees[0][0] == trees[1][0]
+    assert trees[0][1] == trees[1][1] and trees[0][2] == trees[1][2]

@@ -1,0 +1,269 @@
+"""GPU-resident level-wise tree builder (no host synchronisation inside a tree).
+
+Same semantics as :class:`.builder.TreeBuilder` with ``grow_policy="level"`` and a
+bounded depth (reference: ``J/optimizer/gbdt/DataParallelTreeMaker.java`` make(),
+FIFO queue). Every per-level decision (leaf or split, children counts, terminal
+children, smaller-child choice, work lists) is taken on the device by the planner
+kernels of ``csrc/hip/gbdt_level.hip``; partition / histogram / split kernels are
+launched with fixed maximal grids and read their work counts from device memory.
+A tree is therefore a fixed launch sequence that the host enqueues without
+waiting; multi-GPU all-reduces (root count, max |g|/|h|, per-level child counts,
+per-level histogram slab) are fixed-size RCCL calls on the same stream.
+
+Histogram slot layout: the nodes at depth c use slots [2^c - 1, 2^(c+1) - 1):
+built (smaller) children in the first half, derived children in the second.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ...ops import gbdt as gops
+from ...ops._ext import hip, ptr, stream
+from ...parallel.comm import Comm
+from .builder import TimeStats, TreeParams
+from .tree import Tree
+
+DNODE_DTYPE = np.dtype([
+    ("G", "<f8"), ("H", "<f8"), ("gl", "<f8"), ("hl", "<f8"), ("cnt_global", "<i8"),
+    ("begin", "<i4"), ("cnt_local", "<i4"), ("depth", "<i4"), ("slot", "<i4"),
+    ("feat", "<i4"), ("bin_a", "<i4"), ("bin_b", "<i4"), ("left", "<i4"), ("right", "<i4"),
+    ("loss_chg", "<f4"), ("value", "<f4"), ("is_leaf", "<i4")])
+assert DNODE_DTYPE.itemsize == 88
+ST_NUM_NODES = 0
+
+MAX_DEPTH_DEVICE = 12
+
+
+class DeviceTree:
+    """Handle of a tree built on the device: node-table snapshot + scoring arrays."""
+
+    def __init__(self, nodes: torch.Tensor, st: torch.Tensor, bin_arrays, max_nodes: int):
+        self.nodes = nodes
+        self.st = st
+        self.bin_arrays = bin_arrays
+        self.max_nodes = max_nodes
+
+    def to_tree(self, nodes_np=None, st_np=None) -> Tree:
+        nd = (nodes_np if nodes_np is not None else self.nodes.cpu().numpy()).view(DNODE_DTYPE).reshape(-1)
+        nn = int((st_np if st_np is not None else self.st.cpu().numpy())[ST_NUM_NODES])
+        t = Tree()
+        for _ in range(nn - 1):
+            t._alloc(-1)
+        for i in range(nn):
+            n = nd[i]
+            leaf = bool(n["is_leaf"]) or n["left"] < 0
+            if leaf:
+                t.set_leaf(i, float(n["value"]))
+            else:
+                t.is_leaf[i] = False
+                t.left[i], t.right[i] = int(n["left"]), int(n["right"])
+                t.parent[t.left[i]] = i
+                t.parent[t.right[i]] = i
+                t.set_split(i, int(n["feat"]), int(n["bin_a"]), int(n["bin_b"]))
+            t.loss_chg[i] = float(n["loss_chg"])
+            t.hess_sum[i] = float(np.float32(n["H"]))
+            t.sample_cnt[i] = int(n["cnt_global"])
+        return t
+
+
+class DeviceLevelBuilder:
+    HIST_TARGET = 512   # 1 block/CU (128 KiB LDS) x 256 CUs x 2
+    PART_TARGET = 1024
+    MIN_ROWS = 2048
+
+    def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
+                 params: TreeParams, comm: Comm = None):
+        assert bins.is_cuda
+        p = params
+        if not (1 <= p.max_depth <= MAX_DEPTH_DEVICE) or p.grow_policy != "level":
+            raise ValueError("device builder needs level-wise growth with 1 <= max_depth <= 12")
+        self.p = p
+        self.bins, self.binsT = bins, binsT
+        self.dev = bins.device
+        self.N = bins.shape[0]
+        self.F, self.B = F, B
+        self.comm = comm or Comm.local(self.dev)
+        self.nbins_f = torch.from_numpy(np.asarray(nbins_f, np.int32)).to(self.dev)
+        D = p.max_depth
+        ml = p.max_leaf_cnt if p.max_leaf_cnt > 0 else (1 << 30)
+        self.max_nodes = int(min((1 << (D + 1)) - 1, 2 * ml - 1))
+        self.maxp = 1 << D
+        self.max_items = max(self.HIST_TARGET, self.PART_TARGET) + self.maxp + 16
+        dev = self.dev
+        i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
+        self.st = i32(16)
+        self.nodes = torch.zeros(self.max_nodes * DNODE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self.pending, self.next_pending = i32(self.maxp), i32(self.maxp)
+        self.split_nid, self.split_snap = i32(self.maxp), i32(self.maxp)
+        self.part_items = i32(self.max_items * 4)
+        self.part_feat, self.part_thr, self.part_begin = i32(self.maxp), i32(self.maxp), i32(self.maxp)
+        self.part_first, self.part_nblk = i32(self.maxp), i32(self.maxp)
+        self.part_counts = i32(self.max_items)
+        self.left_loc = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
+        self.left_glob = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
+        self.hist_items = i32(self.max_items * 4)
+        self.split_items = i32(2 * self.maxp * 4)
+        self.item_nid = i32(2 * self.maxp)
+        self.split_out = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
+        self.tfeat, self.tthr = i32(self.max_nodes), i32(self.max_nodes)
+        self.tleft, self.tright = i32(self.max_nodes), i32(self.max_nodes)
+        self.tval = torch.zeros(self.max_nodes, dtype=torch.float32, device=dev)
+        self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.n_slots = (1 << D) - 1
+        self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
+        self.rows = torch.empty(self.N, dtype=torch.int32, device=dev)
+        self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=dev)
+        self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
+        self.gh_tmp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
+        self.flags = torch.empty(self.N, dtype=torch.uint8, device=dev)
+        self.iota = torch.arange(self.N, dtype=torch.int32, device=dev)
+        self.scales = torch.ones(2, dtype=torch.float32, device=dev)
+        self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
+        self.gp = p.gain_params()
+        self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.HIST_TARGET, self.PART_TARGET,
+                   self.MIN_ROWS]
+        self.tree_count = 0
+        self.last_keep = None
+        self.total_stats = TimeStats()
+        self._fmask_cache = {}
+
+    def _fp(self):
+        p = self.p
+        return [float(np.float32(v)) for v in (p.min_split_loss, p.min_child_hessian_sum, p.l1, p.l2,
+                                              p.max_abs_leaf_val, p.learning_rate)]
+
+    def _ptrs(self):
+        return [ptr(t) for t in (self.st, self.nodes, self.pending, self.next_pending, self.split_nid,
+                                 self.split_snap, self.part_items, self.part_feat, self.part_thr,
+                                 self.part_begin, self.part_first, self.part_nblk, self.part_counts,
+                                 self.left_loc, self.left_glob, self.hist_items, self.split_items,
+                                 self.item_nid, self.split_out, self.tfeat, self.tthr, self.tleft,
+                                 self.tright, self.tval, self.root_cnt)]
+
+    def _fmask(self, rng):
+        p = self.p
+        if p.feature_sample_rate < 1.0:
+            n_sam = max(1, int(round(p.feature_sample_rate * self.F)))
+            perm = rng.permutation(self.F)
+            fm = np.zeros(self.F, np.uint8)
+            fm[np.sort(perm[:n_sam])] = 1
+        else:
+            fm = np.ones(self.F, np.uint8)
+        key = fm.tobytes()
+        if key not in self._fmask_cache:
+            if len(self._fmask_cache) > 64:
+                self._fmask_cache.clear()
+            self._fmask_cache[key] = torch.from_numpy(fm).to(self.dev)
+        return self._fmask_cache[key], int(np.nonzero(fm)[0][0])
+
+    # ------------------------------------------------------------------ build
+    def build(self, gh: torch.Tensor) -> DeviceTree:
+        p = self.p
+        h = hip()
+        s = stream(self.bins)
+        ptrs = self._ptrs()
+        fp = self._fp()
+        ip = self.ip
+        rng = np.random.default_rng((p.seed, self.tree_count))
+        seed_rows = int(rng.integers(1 << 62))
+        dist = self.comm.is_dist
+        # rows / position-ordered (g, h)
+        if p.instance_sample_rate < 1.0:
+            g = torch.Generator(device=self.dev)
+            g.manual_seed(seed_rows + self.comm.rank)
+            keep = torch.rand(self.N, generator=g, device=self.dev) < p.instance_sample_rate
+            # stable compaction without a host sync: sampled rows first, in order
+            key = (~keep).to(torch.int32)
+            _, order = torch.sort(key, stable=True)
+            self.rows.copy_(order.to(torch.int32))
+            self.ghp.copy_(gh.index_select(0, order))
+            self.root_cnt[0] = keep.sum()
+            self.last_keep = keep
+        else:
+            self.rows.copy_(self.iota)
+            self.ghp.copy_(gh)
+            self.root_cnt[0] = self.N
+            self.last_keep = None
+        fmask, f0 = self._fmask(rng)
+        self.root_cnt[1] = self.root_cnt[0]
+        if dist:
+            self.comm.allreduce_(self.root_cnt[1:2])
+        # fixed-point scales from the global max |g|, |h| over the tree's rows
+        if p.instance_sample_rate < 1.0:
+            mx = (gh.abs() * keep[:, None]).amax(dim=0).double()
+        else:
+            mx = gh.abs().amax(dim=0).double()
+        if dist:
+            self.comm.allreduce_(mx, op="max")
+        h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
+        # root
+        st_ptr = self.st.data_ptr()
+        off = lambda w: st_ptr + 4 * w
+        h.lv_step(0, ptrs, ip, fp, 0, 0, s)
+        self.hist[0:1].zero_()
+        h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, ptr(self.ghp),
+                  0 if p.instance_sample_rate >= 1.0 else ptr(self.rows),
+                  ptr(self.hist_items), self.HIST_TARGET + 1, ptr(self.hist), self.B, 1.0, 1.0,
+                  off(5), ptr(self.scales), s)
+        if dist:
+            self.comm.allreduce_(self.hist[0:1])
+        gp = self.gp
+        h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
+                     ptr(self.split_items), 1, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
+                     gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
+        bb = 1 if self.bins.dtype == torch.uint8 else 2
+        for d in range(p.max_depth):
+            c = d + 1  # depth of the children created at this level
+            h.lv_step(1, ptrs, ip, fp, 0, 0, s)  # apply splits + pop nodes of depth d
+            npart = self.PART_TARGET + (1 << d) + 1
+            last = c == p.max_depth
+            if last:
+                h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.flags),
+                                  ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),
+                                  ptr(self.part_counts), off(4), s)
+            else:
+                h.partition(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.rows_tmp),
+                            ptr(self.ghp), ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
+                            ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
+                            ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4), s)
+            h.lv_step(2, ptrs, ip, fp, 0 if dist else 1, 0, s)
+            if dist:
+                self.left_glob.copy_(self.left_loc)
+                self.comm.allreduce_(self.left_glob)
+            base, half = (1 << c) - 1, 1 << (c - 1)
+            h.lv_step(3, ptrs, ip, fp, base, half, s)
+            if last:
+                break
+            self.rows, self.rows_tmp = self.rows_tmp, self.rows
+            self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
+            ptrs = self._ptrs()
+            self.hist[base:base + half].zero_()
+            h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, ptr(self.ghp), ptr(self.rows),
+                      ptr(self.hist_items), self.HIST_TARGET + half + 1, ptr(self.hist), self.B, 1.0, 1.0,
+                      off(5), ptr(self.scales), s)
+            if dist:
+                self.comm.allreduce_(self.hist[base:base + half])
+            h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
+                         ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
+                         gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
+        h.lv_step(4, ptrs, ip, fp, self.max_nodes, 0, s)
+        self.tree_count += 1
+        arrays = tuple(t.clone() for t in (self.tfeat, self.tthr, self.tleft, self.tright, self.tval))
+        return DeviceTree(self.nodes.clone(), self.st.clone(), arrays, self.max_nodes)
+
+    def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
+        """Raw-threshold arrays of the LAST built tree (for test-set scoring), one forest entry."""
+        mn = self.max_nodes
+        out = {
+            "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nthr": torch.empty(mn, dtype=torch.float32, device=self.dev),
+            "nleft": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nright": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "ndefl": torch.empty(mn, dtype=torch.uint8, device=self.dev),
+            "nval": torch.empty(mn, dtype=torch.float32, device=self.dev),
+        }
+        hip().lv_raw_tree(self._ptrs(), mn, ptr(cand), ptr(coff), ptr(fill), 1 if split_median else 0,
+                          ptr(out["nfeat"]), ptr(out["nthr"]), ptr(out["nleft"]), ptr(out["nright"]),
+                          ptr(out["ndefl"]), ptr(out["nval"]), stream(self.bins))
+        return out

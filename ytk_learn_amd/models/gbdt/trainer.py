@@ -4,13 +4,15 @@ Reference: ``J/optimizer/GBDTOptimizer.java`` (init :211-335, train loop :406-48
 doBoost :482-488, predictAndCalcLossGrad :513-609, convertModel :663-690) and
 ``J/operation/GBDTOperation.java``.
 
-Device-resident design: raw test features, binned train matrix, scores, predictions,
-labels, weights and (g, h) all live in HBM for the whole run. Per round the host
-only sees the tree structure and two loss scalars.
+Device-resident design: raw test features, binned train matrix (row- and
+column-major), scores, predictions, labels, weights and (g, h) live in HBM for the
+whole run. On a GPU with level-wise growth the tree builder is GPU-resident too
+(``device_builder.py``): a boosting round is enqueued without any host
+synchronisation; the host only reads loss scalars when it logs and converts the
+device node tables into model trees lazily (``materialize``).
 """
 from __future__ import annotations
 
-import math
 import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence
@@ -22,9 +24,11 @@ from ...losses import create_loss
 from ...metrics.evaluators import EvalSet
 from ...ops import gbdt as gops
 from ...parallel.comm import Comm
+from ...utils.javafmt import java_double_str as jd
 from ...utils.logging import get_logger
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
+from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder
 from .refine import TreeRefiner
 from .tree import GBDTModel, Tree
 
@@ -47,6 +51,7 @@ class GBDTParams:
     approximate: List[dict] = field(default_factory=lambda: [{"cols": "default", "type": "sample_by_quantile", "max_cnt": 255}])
     dump_freq: int = -1
     verbose: bool = False
+    device_builder: bool = True  # use the GPU-resident builder when applicable
     tree: TreeParams = field(default_factory=TreeParams)
 
 
@@ -83,8 +88,10 @@ class GBDTTrainer:
         self.model = model or GBDTModel(params.uniform_base_prediction, self.K, self.loss.name)
         self.profile = profile
         self.kernel_loss = self.loss.gbdt_kernel_id
-        self.time_stats = TimeStats()
         self._prepared = False
+        self._pending = []          # device trees not yet converted to host Trees
+        self._acc = None            # (train acc, test acc) device tensors of the last round
+        self.rounds_done = 0
 
     # ------------------------------------------------------------ preparation
     def _specs(self) -> List[SamplerSpec]:
@@ -107,8 +114,7 @@ class GBDTTrainer:
         base = float(np.float32(self.loss.pred2score(self.p.uniform_base_prediction)))
         init = torch.full((data.n, self.K), base, dtype=torch.float32, device=self.dev)
         if self.p.sample_dependent_base_prediction and data.init_pred is not None:
-            ip = data.init_pred.double()
-            init += self.loss.pred2score(ip).float()
+            init += self.loss.pred2score(data.init_pred.double()).float()
         return init
 
     def prepare(self):
@@ -116,15 +122,25 @@ class GBDTTrainer:
         tr = self.train_data
         # missing values (FillMissingValue): computed on train, applied to train/test
         self.missing_fill = compute_missing_fill(tr.X, tr.weight, self.p.missing_value, self.comm)
-        fill = torch.from_numpy(self.missing_fill).to(self.dev)
-        Xf = torch.where(torch.isnan(tr.X), fill[None, :], tr.X)
+        self.fill_dev = torch.from_numpy(self.missing_fill).to(self.dev)
+        Xf = torch.where(torch.isnan(tr.X), self.fill_dev[None, :], tr.X)
         self.mapper = BinMapper.fit(Xf, tr.weight, self._specs(), self.comm, self.p.split_type,
                                     seed=self.p.tree.seed)
         self.bins, self.binsT = self.mapper.transform(Xf)
         del Xf
         self.B = self.mapper.hist_bins()
-        self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, self.p.tree,
-                                   self.comm, profile=self.profile)
+        self.cand_dev = torch.from_numpy(np.concatenate(self.mapper.cands).astype(np.float32)).to(self.dev)
+        self.coff_dev = torch.from_numpy(np.concatenate(
+            [[0], np.cumsum([len(c) for c in self.mapper.cands])]).astype(np.int32)).to(self.dev)
+        self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
+        tp = self.p.tree
+        self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
+                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None)
+        if self.use_device_builder:
+            self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm)
+        else:
+            self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
+                                       self.comm, profile=self.profile)
         N = tr.n
         self.score = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
         self.init_score = self._base_score(tr)
@@ -132,23 +148,25 @@ class GBDTTrainer:
         self.gh = torch.zeros((self.K, N, 2), dtype=torch.float32, device=self.dev)
         self.y = tr.y.contiguous()
         self.w = tr.weight.contiguous() if tr.weight is not None else None
-        self.train_wsum = float(self.comm.allreduce_scalars([float(tr.weight.sum()) if tr.weight is not None else float(N)])[0])
-        self.train_real = float(self.comm.allreduce_scalars([float(N)])[0])
+        sums = self.comm.allreduce_scalars([float(tr.weight.sum()) if tr.weight is not None else float(N), float(N)])
+        self.train_wsum, self.train_real = sums
         if self.test_data is not None:
             te = self.test_data
-            self.Xte = torch.where(torch.isnan(te.X), fill[None, :], te.X).contiguous()
+            self.Xte = torch.where(torch.isnan(te.X), self.fill_dev[None, :], te.X).contiguous()
             self.te_score = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
             self.te_init = self._base_score(te)
             self.te_pred = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
             self.te_gh = torch.zeros((self.K, te.n, 2), dtype=torch.float32, device=self.dev)
-            self.te_wsum = float(self.comm.allreduce_scalars([float(te.weight.sum()) if te.weight is not None else float(te.n)])[0])
-            self.te_real = float(self.comm.allreduce_scalars([float(te.n)])[0])
-        self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
+            sums = self.comm.allreduce_scalars([float(te.weight.sum()) if te.weight is not None else float(te.n),
+                                                float(te.n)])
+            self.te_wsum, self.te_real = sums
         self.eval_train = EvalSet(self.p.eval_metric, self.comm)
         self.eval_test = EvalSet(self.p.eval_metric, self.comm)
-        # continue-train: replay loaded trees on train/test scores
-        if self.model.trees:
+        self._one_tree = {k: (torch.zeros(1, dtype=torch.int32, device=self.dev),
+                              torch.full((1,), k, dtype=torch.int32, device=self.dev)) for k in range(self.K)}
+        if self.model.trees:  # continue-train: replay loaded trees on train/test scores
             self._replay_loaded_trees()
+        self.rounds_done = len(self.model.trees) // self.K
         self._prepared = True
         self.prep_time = time.perf_counter() - t0
         nb = self.mapper.nbins
@@ -161,8 +179,7 @@ class GBDTTrainer:
         for t in self.model.trees:
             t.update_feature_index(name2idx)
         fl = {k: torch.from_numpy(v).to(self.dev) for k, v in self.model.flatten().items()}
-        fill = torch.from_numpy(self.missing_fill).to(self.dev)
-        Xf = torch.where(torch.isnan(self.train_data.X), fill[None, :], self.train_data.X).contiguous()
+        Xf = torch.where(torch.isnan(self.train_data.X), self.fill_dev[None, :], self.train_data.X).contiguous()
         gops.forest_predict(Xf, fl, self.score, 1.0)
         if self.test_data is not None:
             gops.forest_predict(self.Xte, fl, self.te_score, 1.0)
@@ -173,11 +190,13 @@ class GBDTTrainer:
             return float(rounds_done if rounds_done > 0 else 1)
         return 1.0
 
+    def _kparam(self):
+        return self.p.sigmoid_zmax if self.kernel_loss == "sigmoid" else getattr(self.loss, "delta", 0.0)
+
     def _loss_grad(self, score, init, y, w, pred, gh, rounds_done, want_grad=True):
         div = self._score_div(rounds_done)
         if self.kernel_loss is not None:
-            param = self.p.sigmoid_zmax if self.kernel_loss == "sigmoid" else getattr(self.loss, "delta", 0.0)
-            return gops.grad_hess(score, init, y, w, self.kernel_loss, param, div, pred, gh, want_grad)
+            return gops.grad_hess(score, init, y, w, self.kernel_loss, self._kparam(), div, pred, gh, want_grad)
         # generic loss (torch on device): GBDT derivative from the float prediction
         z = score.double() / div + init.double()
         yy = y.double()
@@ -195,15 +214,15 @@ class GBDTTrainer:
             gh[:, :, 1] = (h * ww[:, None]).float().t()
         return torch.stack([(lv.reshape(lv.shape[0], -1).sum(1) * ww).sum(), ww.sum()])
 
-    def _tree_to_dev(self, tree):
-        """Bin-threshold node arrays of a tree packed into one H2D copy."""
-        f, t, l, r, v = tree.bin_arrays()
-        n = f.shape[0]
-        packed = np.concatenate([f, t, l, r, v.view(np.int32)]).astype(np.int32)
-        d = torch.from_numpy(packed)
-        if self.dev.type == "cuda":
-            d = d.pin_memory().to(self.dev, non_blocking=True)
-        return (d[:n], d[n:2 * n], d[2 * n:3 * n], d[3 * n:4 * n], d[4 * n:5 * n].view(torch.float32))
+    def init_gradients(self):
+        """initPred: prediction, loss and gradients of the current model."""
+        r = self.rounds_done
+        acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, r)
+        acc_te = None
+        if self.test_data is not None:
+            te = self.test_data
+            acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh, r, False)
+        self._acc = (acc, acc_te)
 
     # ------------------------------------------------------------------ train
     def train(self, rounds: Optional[int] = None, on_round: Optional[Callable[[int, "GBDTTrainer"], None]] = None,
@@ -212,89 +231,142 @@ class GBDTTrainer:
             self.prepare()
         p = self.p
         total_rounds = p.round_num if rounds is None else rounds
-        cur = len(self.model.trees) // self.K
+        cur = self.rounds_done
         self.log.info(f"gbdt start train! total round_num={total_rounds}, current round_num={cur}")
-        # initial prediction + gradients (initPred)
-        self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, cur)
-        if self.test_data is not None:
-            te = self.test_data
-            self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh, cur, False)
+        self.init_gradients()
         start = time.perf_counter()
         for i in range(cur, total_rounds):
             self.step(i)
             if on_round is not None:
                 on_round(i, self)
+            # GBDTOptimizer.java:434-435 -- note Java's (i+1) % -1 == 0 dumps every round
             if dump_cb is not None and p.dump_freq != 0 and ((i + 1) % p.dump_freq == 0):
+                self.materialize()
                 dump_cb(i)
             if self.p.verbose or self.log.enabled_for_round(i):
                 cost = time.perf_counter() - start
                 self.log.info(f"[model=gbdt] [loss={self.loss.name}] [iter={i + 1}]  {cost:.5f} sec elapse\n"
-                              f"{self.last_report}")
+                              f"{self.report()}")
+        self.materialize()
         self.total_train_time = time.perf_counter() - start
         final = self.final_eval()
         self.log.info(f"training end, {self.total_train_time:.5f} sec in all\n{final}")
         return self.model
 
-    def step(self, i: int) -> str:
-        """One boosting round: K trees, score update, loss + next gradients."""
+    def _tree_to_dev(self, tree):
+        """Bin-threshold node arrays of a host tree packed into one H2D copy."""
+        f, t, l, r, v = tree.bin_arrays()
+        n = f.shape[0]
+        packed = np.concatenate([f, t, l, r, v.view(np.int32)]).astype(np.int32)
+        d = torch.from_numpy(packed)
+        if self.dev.type == "cuda":
+            d = d.pin_memory().to(self.dev, non_blocking=True)
+        return (d[:n], d[n:2 * n], d[2 * n:3 * n], d[3 * n:4 * n], d[4 * n:5 * n].view(torch.float32))
+
+    def step(self, i: int):
+        """One boosting round: K trees, score update, loss + next gradients, test scoring.
+        Enqueues device work only (no host synchronisation on the device-builder path)."""
         lr = 1.0 if self.rf else self.p.tree.learning_rate
         self.builder.p.learning_rate = lr
-        new_trees = []
-        arrays = []
+        arrays, raws, host_trees, dev_trees = [], [], [], []
         for k in range(self.K):
-            tree = self.builder.build(self.gh[k])
-            if self.refiner is not None:
-                self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
-                                    + self.init_score[:, k], self.w, lr)
-            new_trees.append(tree)
-            arrays.append(self._tree_to_dev(tree))
-        # score update + loss on train after this round + gradients for the next round
+            if self.use_device_builder:
+                dt = self.builder.build(self.gh[k])
+                dev_trees.append(dt)
+                arrays.append(dt.bin_arrays)
+                if self.test_data is not None:
+                    raw = self.builder.raw_tree(self.cand_dev, self.coff_dev, self.fill_dev,
+                                                self.p.split_type == "median")
+                    raw["troot"], raw["tout"] = self._one_tree[k]
+                    raws.append(raw)
+            else:
+                tree = self.builder.build(self.gh[k])
+                if self.refiner is not None:
+                    self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
+                                        + self.init_score[:, k], self.w, lr)
+                host_trees.append(tree)
+                arrays.append(self._tree_to_dev(tree))
+        # score update + train loss after this round + gradients for the next round
         if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
-            param = self.p.sigmoid_zmax if self.kernel_loss == "sigmoid" else getattr(self.loss, "delta", 0.0)
             acc = gops.tree_grad(self.binsT, arrays[0], self.score, self.init_score, self.y, self.w,
-                                 self.kernel_loss, param, self._score_div(i + 1), self.pred, self.gh[0])
+                                 self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0])
         else:
             for k in range(self.K):
                 gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
             acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
-        # convert model (slot -> raw threshold, names, default direction)
-        for tree in new_trees:
-            tree.convert_split_values(self.mapper.cands, self.p.split_type)
-            tree.add_feature_names(self.feature_names)
-            tree.add_default_direction(self.missing_fill)
+        # model conversion (slot -> raw threshold, names, default direction) for host trees
+        for tree in host_trees:
+            self._convert(tree)
             self.model.trees.append(tree)
-        report = []
+        if dev_trees:
+            self._pending.append(dev_trees)
+        acc_te = None
         if self.test_data is not None:
-            fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
-            fl.trees = new_trees
-            flat = {k: torch.from_numpy(v).to(self.dev) for k, v in fl.flatten().items()}
-            gops.forest_predict(self.Xte, flat, self.te_score, 1.0)
+            if host_trees:
+                fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
+                fl.trees = host_trees
+                raws = [{k: torch.from_numpy(v).to(self.dev) for k, v in fl.flatten().items()}]
+            for raw in raws:
+                gops.forest_predict(self.Xte, raw, self.te_score, 1.0)
             te = self.test_data
             acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
                                      i + 1, False)
+        self._acc = (acc, acc_te)
+        self.rounds_done = i + 1
+
+    def _convert(self, tree: Tree):
+        tree.convert_split_values(self.mapper.cands, self.p.split_type)
+        tree.add_feature_names(self.feature_names)
+        tree.add_default_direction(self.missing_fill)
+
+    def materialize(self):
+        """Convert pending device trees into host model trees (one bulk D2H)."""
+        if not self._pending:
+            return
+        flat = [dt for group in self._pending for dt in group]
+        nodes = torch.stack([dt.nodes for dt in flat]).cpu().numpy()
+        sts = torch.stack([dt.st for dt in flat]).cpu().numpy()
+        for dt, nd, st in zip(flat, nodes, sts):
+            tree = dt.to_tree(nd, st)
+            self._convert(tree)
+            self.model.trees.append(tree)
+        self._pending = []
+
+    # ------------------------------------------------------------------ report
+    def _losses(self):
+        acc, acc_te = self._acc
+        if acc_te is not None:
             both = torch.stack([acc, acc_te]).cpu()
-            if self.comm.is_dist:
-                self.comm.allreduce_(both)
-            tr_loss = float(both[0, 0]) / max(self.train_wsum, 1e-300)
-            te_loss = float(both[1, 0]) / max(self.te_wsum, 1e-300)
         else:
-            a = acc.cpu()
-            if self.comm.is_dist:
-                self.comm.allreduce_(a)
-            tr_loss = float(a[0]) / max(self.train_wsum, 1e-300)
-            te_loss = None
-        from ...utils.javafmt import java_double_str as jd
-        report.append(f"train loss = {jd(tr_loss)}\n")
+            both = acc.cpu()[None, :]
+        if self.comm.is_dist:
+            self.comm.allreduce_(both)
+        tr = float(both[0, 0]) / max(self.train_wsum, 1e-300)
+        te = float(both[1, 0]) / max(self.te_wsum, 1e-300) if acc_te is not None else None
+        return tr, te
+
+    @property
+    def last_train_loss(self):
+        return self._losses()[0]
+
+    @property
+    def last_test_loss(self):
+        return self._losses()[1]
+
+    def report(self) -> str:
+        tr_loss, te_loss = self._losses()
+        out = [f"train loss = {jd(tr_loss)}\n"]
         if self.p.watch_train:
-            report.append(self._eval_str(True))
+            out.append(self._eval_str(True))
         if te_loss is not None:
-            report.append(f"test loss = {jd(te_loss)}\n")
+            out.append(f"test loss = {jd(te_loss)}\n")
             if self.p.watch_test:
-                report.append(self._eval_str(False))
-        self.last_train_loss = tr_loss
-        self.last_test_loss = te_loss
-        self.last_report = "".join(report)
-        return self.last_report
+                out.append(self._eval_str(False))
+        return "".join(out)
+
+    @property
+    def last_report(self) -> str:
+        return self.report()
 
     def _info(self):
         if self.loss.name == "sigmoid":
@@ -318,4 +390,5 @@ class GBDTTrainer:
         return s
 
     def feature_importance(self):
+        self.materialize()
         return self.model.feature_importance()

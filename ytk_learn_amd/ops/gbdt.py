@@ -84,7 +84,7 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh):
         h = hip()
         if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
             h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
-                      float(sg), float(sh), stream(bins))
+                      float(sg), float(sh), 0, 0, stream(bins))
         else:
             h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                              nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
@@ -122,7 +122,7 @@ def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
             return out
         check_cuda(hist, nbins_f, fmask, items)
         hip().split_find(ptr(hist), B, F, ptr(nbins_f), ptr(fmask), int(f0), ptr(items), n,
-                         ptr(out), mcw, l1, l2, mal, inv_sg, inv_sh, stream(hist))
+                         ptr(out), mcw, l1, l2, mal, inv_sg, inv_sh, 0, 0, stream(hist))
         return out
     res = np.zeros(n, dtype=SPLIT_DTYPE)
     it = items.numpy()
@@ -222,7 +222,7 @@ def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_
         counts = torch.empty(nitems, dtype=torch.int32, device=binsT.device)
         hip().partition(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(rows_out),
                         ptr(ghp), ptr(gh_out), ptr(flags), ptr(items), nitems, ptr(feat), ptr(thr),
-                        ptr(node_begin), ptr(first_blk), ptr(nblk), ptr(counts), ptr(left),
+                        ptr(node_begin), ptr(first_blk), ptr(nblk), ptr(counts), ptr(left), 0,
                         stream(binsT))
         return left
     left = torch.zeros(n_split, dtype=torch.int32)
@@ -257,7 +257,7 @@ def partition_count(binsT, rows, flags, items, feat, thr):
             return counts
         check_cuda(binsT, rows, flags, items, feat, thr)
         hip().partition_count(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(flags),
-                              ptr(items), nitems, ptr(feat), ptr(thr), ptr(counts), stream(binsT))
+                              ptr(items), nitems, ptr(feat), ptr(thr), ptr(counts), 0, stream(binsT))
         return counts
     counts = torch.zeros(nitems, dtype=torch.int32)
     it = items.numpy()
