@@ -20,9 +20,9 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
 // gbdt_partition.hip
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                   uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+                   uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_partition_count(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, int,
-                         uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+                         uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_score.hip
 void ytk_tree_add_bins(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, int, uintptr_t, int, int, uintptr_t);

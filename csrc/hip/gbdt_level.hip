@@ -7,14 +7,15 @@
 // max_depth / the leaf budget is used / both children are below min_split_samples,
 // smaller child histogram + sibling subtraction, canSplit (UpdateStrategy:50-53).
 //
-// MI355X design: the sequential decisions of a level (<= 2^depth nodes) run in a
-// one-lane "planner" kernel that also writes the work lists (partition chunks,
-// histogram chunks, split items) and their counts into device memory. The heavy
-// kernels (partition / histogram / split) are launched with a FIXED maximal grid
-// and read their item count from device memory (blocks past it exit at once).
-// Hence a whole tree is a fixed, host-known launch sequence: no device->host
-// synchronisation inside a tree (and multi-GPU all-reduces operate on fixed-size
-// slabs, enqueued on the same stream).
+// MI355X design: the decisions of a level (<= 2^depth nodes) run in one 256-thread
+// "planner" workgroup: node fields are staged in LDS by all lanes, the only truly
+// sequential rule (the running leaf count under max_leaf_cnt) is a lane-0 loop over
+// LDS, and the work lists (partition chunks, histogram chunks, split items) are
+// emitted in parallel after block scans. The heavy kernels (partition / histogram /
+// split) are launched with FIXED maximal grids and read their item counts from
+// device memory, so a whole tree is a fixed launch sequence: no device->host
+// synchronisation inside a tree, and multi-GPU all-reduces are fixed-size RCCL calls
+// on the same stream.
 #include "common.h"
 
 namespace ytk {
@@ -47,6 +48,9 @@ enum {
   ST_N_SITEMS, ST_N_BUILD, ST_WORDS = 16
 };
 
+constexpr int kPlanThreads = 256;
+constexpr int kMaxPend = 4096;  // 2^12 = MAX_DEPTH_DEVICE
+
 struct LvParams {
   int max_depth, max_leaf_cnt, min_split_samples;
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
@@ -67,8 +71,8 @@ struct LvBufs {
   int* part_first;
   int* part_nblk;
   int* part_counts;      // per partition block
-  long long* left_loc;   // per split
-  long long* left_glob;  // per split (all-reduced)
+  long long* left_loc;   // per split (accumulated by the partition flag kernel)
+  long long* left_glob;  // per split (all-reduced; == left_loc on one rank)
   int4* hist_items;
   int4* split_items;
   int* item_nid;
@@ -113,45 +117,102 @@ __device__ void reset_node(DNode& n, int depth) {
   n.is_leaf = 1;
 }
 
-__device__ void emit_chunks(int4* items, int& k, int tag, int b, int c, int ch, bool blk_index) {
-  for (int j = 0; j * ch < c; ++j) {
-    const int s = b + j * ch;
-    items[k++] = make_int4(tag, s, min(s + ch, b + c), blk_index ? j : 0);
+// In-place exclusive scan of a[0..n) (n <= kMaxPend) by one 256-thread block.
+// Returns the total. Each thread scans a contiguous run, then the run totals.
+__device__ int block_exclusive_scan(int* a, int n, int* s_tmp) {
+  const int tid = threadIdx.x;
+  const int per = (n + kPlanThreads - 1) / kPlanThreads;
+  const int b = min(n, tid * per), e = min(n, b + per);
+  int run = 0;
+  for (int i = b; i < e; ++i) run += a[i];
+  s_tmp[tid] = run;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int i = 0; i < kPlanThreads; ++i) {
+      const int v = s_tmp[i];
+      s_tmp[i] = acc;
+      acc += v;
+    }
+    s_tmp[kPlanThreads] = acc;
+  }
+  __syncthreads();
+  int acc = s_tmp[tid];
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = acc;
+    acc += v;
+  }
+  const int total = s_tmp[kPlanThreads];
+  __syncthreads();
+  return total;
+}
+
+// Parallel chunk emission: segment s (begin[s], count[s]) -> first[s] .. first[s]+nblk[s]
+// items {tag(s), chunk_begin, chunk_end, j}. first[] holds the exclusive scan of nblk.
+__device__ void emit_all_chunks(int4* items, int total_items, int nseg, const int* first,
+                                const int* begin, const int* count, const int* tag, int ch,
+                                bool blk_index) {
+  for (int k = threadIdx.x; k < total_items; k += kPlanThreads) {
+    int lo = 0, hi = nseg - 1;  // last s with first[s] <= k
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (first[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const int s = lo;
+    const int j = k - first[s];
+    const int cb = begin[s] + j * ch;
+    items[k] = make_int4(tag ? tag[s] : s, cb, min(cb + ch, begin[s] + count[s]), blk_index ? j : 0);
   }
 }
 
 // Root: node 0 holds all (local) rows; one build item; chunked histogram work.
-__global__ void lv_init_kernel(LvParams p, LvBufs b) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBufs b) {
+  __shared__ int s_first[2], s_begin[1], s_count[1], s_tag[1];
   const int n_local = (int)b.root_cnt[0];
-  DNode& r = b.nodes[0];
-  reset_node(r, 0);
-  r.begin = 0;
-  r.cnt_local = n_local;
-  r.cnt_global = b.root_cnt[1];
-  r.slot = 0;
-  int* st = b.st;
-  for (int i = 0; i < ST_WORDS; ++i) st[i] = 0;
-  st[ST_NUM_NODES] = 1;
-  st[ST_NUM_LEAF] = 1;
-  b.pending[0] = 0;
-  st[ST_N_PENDING] = 1;
   const int ch = max(p.min_rows, (n_local + p.hist_target - 1) / max(1, p.hist_target));
-  int k = 0;
-  emit_chunks(b.hist_items, k, 0, 0, n_local, ch, false);
-  st[ST_N_HIST] = k;
-  st[ST_N_BUILD] = 1;
-  b.split_items[0] = make_int4(0, 0, 0, 0);
-  b.item_nid[0] = 0;
-  st[ST_N_SITEMS] = 1;
+  const int nblk = (n_local + ch - 1) / ch;
+  if (threadIdx.x == 0) {
+    DNode& r = b.nodes[0];
+    reset_node(r, 0);
+    r.begin = 0;
+    r.cnt_local = n_local;
+    r.cnt_global = b.root_cnt[1];
+    r.slot = 0;
+    int* st = b.st;
+    for (int i = 0; i < ST_WORDS; ++i) st[i] = 0;
+    st[ST_NUM_NODES] = 1;
+    st[ST_NUM_LEAF] = 1;
+    b.pending[0] = 0;
+    st[ST_N_PENDING] = 1;
+    st[ST_N_HIST] = nblk;
+    st[ST_N_BUILD] = 1;
+    b.split_items[0] = make_int4(0, 0, 0, 0);
+    b.item_nid[0] = 0;
+    st[ST_N_SITEMS] = 1;
+    s_first[0] = 0;
+    s_begin[0] = 0;
+    s_count[0] = n_local;
+    s_tag[0] = 0;
+  }
+  __syncthreads();
+  emit_all_chunks(b.hist_items, nblk, 1, s_first, s_begin, s_count, s_tag, ch, false);
 }
 
-// Apply split results to the node table, then pop the level's nodes in FIFO order.
-__global__ void lv_plan_split_kernel(LvParams p, LvBufs b) {
-  if (threadIdx.x != 0) return;
+// Apply split results, pop the level's nodes in FIFO order, emit partition chunks.
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b) {
+  __shared__ float s_chg[kMaxPend];
+  __shared__ int s_aux[kMaxPend];       // depth, later: split index / -1
+  __shared__ long long s_cnt[kMaxPend];
+  __shared__ int s_tmp[kPlanThreads + 1];
+  __shared__ int s_nsplit, s_num_nodes0;
+  __shared__ long long s_total;
   int* st = b.st;
+  const int tid = threadIdx.x;
   const double mcw2 = (double)p.mcw * 2.0;
-  for (int i = 0; i < st[ST_N_SITEMS]; ++i) {
+  // 1. apply split-finder results to the node table (canSplit)
+  const int nsi = st[ST_N_SITEMS];
+  for (int i = tid; i < nsi; i += kPlanThreads) {
     DNode& n = b.nodes[b.item_nid[i]];
     const SplitOut& o = b.split_out[i];
     n.G = o.g;
@@ -162,79 +223,107 @@ __global__ void lv_plan_split_kernel(LvParams p, LvBufs b) {
     n.bin_a = o.bin_a;
     n.bin_b = o.bin_b;
     n.loss_chg = o.loss_chg;
-    if (!(n.H >= mcw2 && n.cnt_global >= (long long)p.min_split_samples)) {  // canSplit
+    if (!(o.h >= mcw2 && n.cnt_global >= (long long)p.min_split_samples)) {
       n.loss_chg = -INFINITY;
       n.feat = -1;
     }
   }
-  int num_nodes = st[ST_NUM_NODES], num_leaf = st[ST_NUM_LEAF], nsplit = 0;
-  long long total = 0;
-  for (int i = 0; i < st[ST_N_PENDING]; ++i) {
+  __syncthreads();
+  // 2. stage the pending nodes' decision inputs in LDS
+  const int npend = st[ST_N_PENDING];
+  for (int i = tid; i < npend; i += kPlanThreads) {
+    const DNode& n = b.nodes[b.pending[i]];
+    s_chg[i] = n.loss_chg;
+    s_aux[i] = n.depth;
+    s_cnt[i] = n.cnt_global;
+  }
+  if (tid == 0) s_total = 0;
+  __syncthreads();
+  // 3. sequential FIFO decisions (running leaf count) on LDS data
+  if (tid == 0) {
+    int num_nodes = st[ST_NUM_NODES], num_leaf = st[ST_NUM_LEAF], nsplit = 0;
+    s_num_nodes0 = num_nodes;
+    for (int i = 0; i < npend; ++i) {
+      const bool leaf = !(s_chg[i] > p.min_split_loss) ||
+                        (p.max_depth >= 0 && p.max_depth == s_aux[i]) ||
+                        (p.max_leaf_cnt > 0 && p.max_leaf_cnt == num_leaf) ||
+                        (p.min_split_samples > 0 && s_cnt[i] < p.min_split_samples);
+      if (leaf) {
+        s_aux[i] = -1;
+      } else {
+        num_leaf += 1;
+        s_aux[i] = nsplit;
+        s_cnt[i] = num_leaf;  // snapshot of the leaf count after this split
+        ++nsplit;
+      }
+    }
+    st[ST_NUM_NODES] = num_nodes + 2 * nsplit;
+    st[ST_NUM_LEAF] = num_leaf;
+    st[ST_N_SPLIT] = nsplit;
+    s_nsplit = nsplit;
+  }
+  __syncthreads();
+  // 4. write decisions back; per-split partition descriptors
+  const int nsplit = s_nsplit;
+  for (int i = tid; i < npend; i += kPlanThreads) {
     const int id = b.pending[i];
     DNode& n = b.nodes[id];
-    const bool leaf = !(n.loss_chg > p.min_split_loss) ||
-                      (p.max_depth >= 0 && p.max_depth == n.depth) ||
-                      (p.max_leaf_cnt > 0 && p.max_leaf_cnt == num_leaf) ||
-                      (p.min_split_samples > 0 && n.cnt_global < p.min_split_samples);
-    if (leaf) {
+    const int s = s_aux[i];
+    if (s < 0) {
       n.is_leaf = 1;
       n.value = leaf_value(n.G, n.H, p);
-      continue;
+    } else {
+      n.is_leaf = 0;
+      n.left = s_num_nodes0 + 2 * s;
+      n.right = s_num_nodes0 + 2 * s + 1;
+      b.split_nid[s] = id;
+      b.split_snap[s] = (int)s_cnt[i];
+      b.part_feat[s] = n.feat;
+      b.part_thr[s] = (n.bin_a + n.bin_b) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
+      b.part_begin[s] = n.begin;
+      b.part_nblk[s] = n.cnt_local;              // temporarily: count
+      b.left_loc[s] = 0;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_total), (unsigned long long)n.cnt_local);
     }
-    n.is_leaf = 0;
-    n.left = num_nodes;
-    n.right = num_nodes + 1;
-    num_nodes += 2;
-    num_leaf += 1;
-    b.split_nid[nsplit] = id;
-    b.split_snap[nsplit] = num_leaf;
-    ++nsplit;
-    total += n.cnt_local;
   }
-  st[ST_NUM_NODES] = num_nodes;
-  st[ST_NUM_LEAF] = num_leaf;
-  st[ST_N_SPLIT] = nsplit;
-  const int ch = max((long long)p.min_rows, (total + p.part_target - 1) / max(1, p.part_target));
-  int k = 0;
-  for (int s = 0; s < nsplit; ++s) {
-    const DNode& n = b.nodes[b.split_nid[s]];
-    b.part_feat[s] = n.feat;
-    b.part_thr[s] = (n.bin_a + n.bin_b) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2 rule
-    b.part_begin[s] = n.begin;
-    b.part_first[s] = k;
-    emit_chunks(b.part_items, k, s, n.begin, n.cnt_local, ch, true);
-    b.part_nblk[s] = k - b.part_first[s];
+  __syncthreads();
+  const long long total = s_total;
+  const int ch = (int)max((long long)p.min_rows, (total + p.part_target - 1) / max(1, p.part_target));
+  // counts -> chunk counts (stage counts in LDS for emission)
+  int* s_count = s_aux;  // reuse: per split row count
+  for (int s = tid; s < nsplit; s += kPlanThreads) {
+    const int c = b.part_nblk[s];
+    s_count[s] = c;
+    b.part_first[s] = (c + ch - 1) / ch;
   }
-  st[ST_N_PART] = k;
+  __syncthreads();
+  const int nitems = block_exclusive_scan(b.part_first, nsplit, s_tmp);
+  for (int s = tid; s < nsplit; s += kPlanThreads) b.part_nblk[s] = (s + 1 < nsplit ? b.part_first[s + 1] : nitems) - b.part_first[s];
+  if (tid == 0) st[ST_N_PART] = nitems;
+  __syncthreads();
+  emit_all_chunks(b.part_items, nitems, nsplit, b.part_first, b.part_begin, s_count, nullptr, ch, true);
 }
 
-// Per-split left counts from the partition block counts (local; the host
-// all-reduces left_glob across ranks when distributed).
-__global__ void lv_sum_counts_kernel(LvBufs b, int copy_glob) {
-  const int nsplit = b.st[ST_N_SPLIT];
-  for (int s = threadIdx.x; s < nsplit; s += blockDim.x) {
-    long long c = 0;
-    const int f = b.part_first[s], n = b.part_nblk[s];
-    for (int j = 0; j < n; ++j) c += b.part_counts[f + j];
-    b.left_loc[s] = c;
-    if (copy_glob) b.left_glob[s] = c;
-  }
-}
-
-// Children of this level's splits: segments, terminal check, build / derive lists.
-// build_base: first histogram slot of this level, half: slots reserved for builds.
-__global__ void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base, int half) {
-  if (threadIdx.x != 0) return;
+// Children of this level's splits: segments, terminal check, build / derive lists,
+// histogram chunks. build_base: first slot of this level, half: slots for builds.
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base,
+                                                                    int half, int use_loc) {
+  __shared__ int s_nb[kMaxPend];     // 1 if the split's children get histograms
+  __shared__ int s_small[kMaxPend];  // small child node id
+  __shared__ int s_tmp[kPlanThreads + 1];
+  __shared__ long long s_total;
+  __shared__ int s_hbeg[kMaxPend], s_hcnt[kMaxPend], s_hslot[kMaxPend];
   int* st = b.st;
+  const int tid = threadIdx.x;
   const int nsplit = st[ST_N_SPLIT];
-  int nb = 0, npend = 0;
-  long long total = 0;
-  int nd = 0;
-  for (int s = 0; s < nsplit; ++s) {
+  const long long* lglob_arr = use_loc ? b.left_loc : b.left_glob;
+  if (tid == 0) s_total = 0;
+  __syncthreads();
+  for (int s = tid; s < nsplit; s += kPlanThreads) {
     DNode& P = b.nodes[b.split_nid[s]];
     DNode& L = b.nodes[P.left];
     DNode& R = b.nodes[P.right];
-    const long long lloc = b.left_loc[s], lglob = b.left_glob[s];
+    const long long lloc = b.left_loc[s], lglob = lglob_arr[s];
     reset_node(L, P.depth + 1);
     reset_node(R, P.depth + 1);
     L.begin = P.begin;
@@ -252,63 +341,61 @@ __global__ void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base, in
       R.G = P.G - P.gl; R.H = P.H - P.hl;
       L.value = leaf_value(L.G, L.H, p);
       R.value = leaf_value(R.G, R.H, p);
-      continue;
-    }
-    DNode& small = (L.cnt_global < R.cnt_global) ? L : R;
-    DNode& large = (L.cnt_global < R.cnt_global) ? R : L;
-    const int small_id = (L.cnt_global < R.cnt_global) ? P.left : P.right;
-    const int large_id = (L.cnt_global < R.cnt_global) ? P.right : P.left;
-    small.slot = build_base + nb;
-    large.slot = build_base + half + nd;
-    b.split_items[nb] = make_int4(small.slot, 0, 0, 0);
-    b.item_nid[nb] = small_id;
-    // derived items are appended after all builds (indices fixed below)
-    b.next_pending[npend++] = P.left;
-    b.next_pending[npend++] = P.right;
-    total += small.cnt_local;
-    ++nb;
-    ++nd;
-    (void)large_id;
-  }
-  // derived items: second pass keeps build items contiguous
-  int di = nb;
-  for (int s = 0; s < nsplit; ++s) {
-    const DNode& P = b.nodes[b.split_nid[s]];
-    const DNode& L = b.nodes[P.left];
-    const DNode& R = b.nodes[P.right];
-    if (L.slot < 0 && R.slot < 0) continue;  // terminal pair
-    const bool left_small = L.cnt_global < R.cnt_global;
-    const DNode& small = left_small ? L : R;
-    const DNode& large = left_small ? R : L;
-    b.split_items[di] = make_int4(large.slot, P.slot, small.slot, 1);
-    b.item_nid[di] = left_small ? P.right : P.left;
-    ++di;
-  }
-  for (int i = 0; i < npend; ++i) b.pending[i] = b.next_pending[i];
-  st[ST_N_PENDING] = npend;
-  st[ST_N_BUILD] = nb;
-  st[ST_N_SITEMS] = di;
-  const int ch = max((long long)p.min_rows, (total + p.hist_target - 1) / max(1, p.hist_target));
-  int k = 0;
-  for (int i = 0; i < nb; ++i) {
-    const DNode& n = b.nodes[b.item_nid[i]];
-    emit_chunks(b.hist_items, k, n.slot, n.begin, n.cnt_local, ch, false);
-  }
-  st[ST_N_HIST] = k;
-}
-
-// Remaining pending nodes become leaves (only when the level loop stopped early)
-// and the bin-threshold arrays used by the fused score/gradient kernel are built.
-__global__ void lv_finalize_kernel(LvParams p, LvBufs b, int max_nodes) {
-  int* st = b.st;
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < st[ST_N_PENDING]; ++i) {
-      DNode& n = b.nodes[b.pending[i]];
-      if (n.is_leaf && n.left < 0) n.value = leaf_value(n.G, n.H, p);
+      s_nb[s] = 0;
+    } else {
+      const bool left_small = L.cnt_global < R.cnt_global;
+      s_small[s] = left_small ? P.left : P.right;
+      s_nb[s] = 1;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_total),
+                (unsigned long long)(left_small ? L.cnt_local : R.cnt_local));
     }
   }
   __syncthreads();
-  const int nn = st[ST_NUM_NODES];
+  // keep a copy of the flags (scan is in place)
+  for (int s = tid; s < nsplit; s += kPlanThreads) s_hslot[s] = s_nb[s];
+  __syncthreads();
+  const int nb = block_exclusive_scan(s_nb, nsplit, s_tmp);  // s_nb = build index
+  const long long total = s_total;
+  const int ch = (int)max((long long)p.min_rows, (total + p.hist_target - 1) / max(1, p.hist_target));
+  for (int s = tid; s < nsplit; s += kPlanThreads) {
+    if (!s_hslot[s]) continue;
+    const int k = s_nb[s];
+    DNode& P = b.nodes[b.split_nid[s]];
+    const int small_id = s_small[s];
+    const int large_id = (small_id == P.left) ? P.right : P.left;
+    DNode& S = b.nodes[small_id];
+    DNode& Lg = b.nodes[large_id];
+    S.slot = build_base + k;
+    Lg.slot = build_base + half + k;
+    b.split_items[k] = make_int4(S.slot, 0, 0, 0);
+    b.item_nid[k] = small_id;
+    b.split_items[nb + k] = make_int4(Lg.slot, P.slot, S.slot, 1);
+    b.item_nid[nb + k] = large_id;
+    b.next_pending[2 * k] = P.left;
+    b.next_pending[2 * k + 1] = P.right;
+    s_hbeg[k] = S.begin;
+    s_hcnt[k] = S.cnt_local;
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * nb; i += kPlanThreads) b.pending[i] = b.next_pending[i];
+  // histogram chunks of the build nodes
+  for (int k = tid; k < nb; k += kPlanThreads) s_hslot[k] = build_base + k;
+  __syncthreads();
+  for (int k = tid; k < nb; k += kPlanThreads) s_small[k] = (s_hcnt[k] + ch - 1) / ch;
+  __syncthreads();
+  const int nitems = block_exclusive_scan(s_small, nb, s_tmp);
+  emit_all_chunks(b.hist_items, nitems, nb, s_small, s_hbeg, s_hcnt, s_hslot, ch, false);
+  if (tid == 0) {
+    st[ST_N_PENDING] = 2 * nb;
+    st[ST_N_BUILD] = nb;
+    st[ST_N_SITEMS] = 2 * nb;
+    st[ST_N_HIST] = nitems;
+  }
+}
+
+// Bin-threshold arrays used by the fused score/gradient kernel.
+__global__ void lv_finalize_kernel(LvBufs b, int max_nodes) {
+  const int nn = b.st[ST_NUM_NODES];
   for (int i = threadIdx.x; i < max_nodes; i += blockDim.x) {
     if (i < nn) {
       const DNode& n = b.nodes[i];
@@ -416,9 +503,8 @@ static LvBufs make_bufs(const uintptr_t* a) {
 
 extern "C" {
 
-// ptrs: 25 device pointers (see make_bufs); iparams: max_depth, max_leaf_cnt,
-// min_split_samples, hist_target, part_target, min_rows; fparams: min_split_loss,
-// mcw, l1, l2, max_abs_leaf, lr.
+// which: 0 init, 1 plan_split, 3 plan_children(arg0=build_base, arg1=half | use_loc<<30),
+//        4 finalize(arg0=max_nodes)
 void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* fp, int arg0,
                  int arg1, uintptr_t stream) {
   LvParams p;
@@ -437,11 +523,13 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
-    case 0: hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(64), 0, s, p, b); break;
-    case 1: hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(64), 0, s, p, b); break;
-    case 2: hipLaunchKernelGGL(lv_sum_counts_kernel, dim3(1), dim3(256), 0, s, b, arg0); break;
-    case 3: hipLaunchKernelGGL(lv_plan_children_kernel, dim3(1), dim3(64), 0, s, p, b, arg0, arg1); break;
-    case 4: hipLaunchKernelGGL(lv_finalize_kernel, dim3(1), dim3(256), 0, s, p, b, arg0); break;
+    case 0: hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
+    case 1: hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
+    case 3:
+      hipLaunchKernelGGL(lv_plan_children_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg0,
+                         arg1 & 0x3fffffff, (arg1 >> 30) & 1);
+      break;
+    case 4: hipLaunchKernelGGL(lv_finalize_kernel, dim3(1), dim3(256), 0, s, b, arg0); break;
     default: throw std::runtime_error("bad lv step");
   }
   YTK_LAUNCH_CHECK();

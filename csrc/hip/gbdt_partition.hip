@@ -25,7 +25,8 @@ template <typename BinT>
 __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const int4* __restrict__ items, const int* __restrict__ feat, const int* __restrict__ thr,
-    uint8_t* __restrict__ flags, int* __restrict__ counts, const int* __restrict__ nitems_dev) {
+    uint8_t* __restrict__ flags, int* __restrict__ counts, const int* __restrict__ nitems_dev,
+    long long* __restrict__ left_acc) {
   __shared__ int s_cnt[kPartThreads / kWave];
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   const int4 it = items[blockIdx.x];
@@ -52,7 +53,13 @@ __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
   c = wave_sumi(c);
   if (lane_id() == 0) s_cnt[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  if (threadIdx.x == 0) {
+    const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    counts[blockIdx.x] = tot;
+    // per-split left total (level engine): one 64-bit atomic per block
+    if (left_acc) atomicAdd(reinterpret_cast<unsigned long long*>(&left_acc[it.x]),
+                            (unsigned long long)tot);
+  }
 }
 
 __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
@@ -156,19 +163,19 @@ using namespace ytk;
 extern "C" void ytk_partition_count(uintptr_t binsT, int bin_bytes, long long ncol,
                                     uintptr_t rows, uintptr_t flags, uintptr_t items, int nitems,
                                     uintptr_t feat, uintptr_t thr, uintptr_t counts,
-                                    uintptr_t nitems_dev, uintptr_t stream) {
+                                    uintptr_t nitems_dev, uintptr_t left_acc, uintptr_t stream) {
   if (nitems <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (bin_bytes == 1) {
     hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
                        (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
-                       (const int*)nitems_dev);
+                       (const int*)nitems_dev, (long long*)left_acc);
   } else {
     hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
                        (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
-                       (const int*)nitems_dev);
+                       (const int*)nitems_dev, (long long*)left_acc);
   }
   YTK_LAUNCH_CHECK();
 }
@@ -178,19 +185,19 @@ extern "C" void ytk_partition(uintptr_t binsT, int bin_bytes, long long ncol, ui
                               uintptr_t flags, uintptr_t items, int nitems, uintptr_t feat,
                               uintptr_t thr, uintptr_t node_begin, uintptr_t first_blk,
                               uintptr_t nblk, uintptr_t counts, uintptr_t left_total,
-                              uintptr_t nitems_dev, uintptr_t stream) {
+                              uintptr_t nitems_dev, uintptr_t left_acc, uintptr_t stream) {
   if (nitems <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (bin_bytes == 1) {
     hipLaunchKernelGGL(partition_flags_kernel<uint8_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint8_t*)binsT, ncol, (const int*)rows, (const int4*)items,
                        (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
-                       (const int*)nitems_dev);
+                       (const int*)nitems_dev, (long long*)left_acc);
   } else {
     hipLaunchKernelGGL(partition_flags_kernel<uint16_t>, dim3(nitems), dim3(kPartThreads), 0, s,
                        (const uint16_t*)binsT, ncol, (const int*)rows, (const int4*)items,
                        (const int*)feat, (const int*)thr, (uint8_t*)flags, (int*)counts,
-                       (const int*)nitems_dev);
+                       (const int*)nitems_dev, (long long*)left_acc);
   }
   YTK_LAUNCH_CHECK();
   hipLaunchKernelGGL(partition_scatter_kernel, dim3(nitems), dim3(kPartThreads), 0, s,

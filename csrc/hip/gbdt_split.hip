@@ -86,14 +86,16 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
 }
 
 // hist: int64 [slot][B][F][2]. items[blk] = {slot, parent_slot, sibling_slot, derived}
-__global__ __launch_bounds__(256) void split_find_kernel(
+constexpr int kSplitWaves = 8;  // 512 threads: 3-4 features per wave at F=28 (latency bound)
+
+__global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
     const double* __restrict__ inv_dev) {
-  __shared__ float s_chg[4];
-  __shared__ int s_feat[4], s_a[4], s_b[4];
-  __shared__ double s_gl[4], s_hl[4];
+  __shared__ float s_chg[kSplitWaves];
+  __shared__ int s_feat[kSplitWaves], s_a[kSplitWaves], s_b[kSplitWaves];
+  __shared__ double s_gl[kSplitWaves], s_hl[kSplitWaves];
 
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   if (inv_dev) {
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(256) void split_find_kernel(
   int best_f = 0x7fffffff, best_a = -1, best_b = 0x7fffffff;
   double best_gl = 0.0, best_hl = 0.0;
 
-  for (int f = wid; f < F; f += 4) {
+  for (int f = wid; f < F; f += kSplitWaves) {
     if (!fmask[f]) continue;
     const int nb = nbins_f[f];
     long long carry_g = 0, carry_h = 0;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void split_find_kernel(
   __syncthreads();
   if (threadIdx.x == 0) {
     int bw = 0;
-    for (int w2 = 1; w2 < 4; ++w2)
+    for (int w2 = 1; w2 < kSplitWaves; ++w2)
       if (better(s_chg[w2], s_feat[w2], s_b[w2], s_chg[bw], s_feat[bw], s_b[bw])) bw = w2;
     SplitOut o;
     o.loss_chg = s_chg[bw];
@@ -237,7 +239,7 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
                                uintptr_t stream) {
   if (nitems <= 0) return;
   GainParams gp{mcw, l1, l2, max_abs_leaf, inv_sg, inv_sh};
-  hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(256), 0,
+  hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(kSplitWaves * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
                      (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev);

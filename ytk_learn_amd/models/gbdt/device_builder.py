@@ -218,21 +218,22 @@ class DeviceLevelBuilder:
             h.lv_step(1, ptrs, ip, fp, 0, 0, s)  # apply splits + pop nodes of depth d
             npart = self.PART_TARGET + (1 << d) + 1
             last = c == p.max_depth
+            # the flag kernel also accumulates the per-split left totals into left_loc
             if last:
                 h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.flags),
                                   ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),
-                                  ptr(self.part_counts), off(4), s)
+                                  ptr(self.part_counts), off(4), ptr(self.left_loc), s)
             else:
                 h.partition(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.rows_tmp),
                             ptr(self.ghp), ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
-                            ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4), s)
-            h.lv_step(2, ptrs, ip, fp, 0 if dist else 1, 0, s)
+                            ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
+                            ptr(self.left_loc), s)
             if dist:
                 self.left_glob.copy_(self.left_loc)
                 self.comm.allreduce_(self.left_glob)
             base, half = (1 << c) - 1, 1 << (c - 1)
-            h.lv_step(3, ptrs, ip, fp, base, half, s)
+            h.lv_step(3, ptrs, ip, fp, base, half | ((0 if dist else 1) << 30), s)
             if last:
                 break
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
@@ -247,7 +248,7 @@ class DeviceLevelBuilder:
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                          ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
                          gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
-        h.lv_step(4, ptrs, ip, fp, self.max_nodes, 0, s)
+        h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         self.tree_count += 1
         arrays = tuple(t.clone() for t in (self.tfeat, self.tthr, self.tleft, self.tright, self.tval))
         return DeviceTree(self.nodes.clone(), self.st.clone(), arrays, self.max_nodes)

@@ -222,7 +222,7 @@ def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_
         counts = torch.empty(nitems, dtype=torch.int32, device=binsT.device)
         hip().partition(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(rows_out),
                         ptr(ghp), ptr(gh_out), ptr(flags), ptr(items), nitems, ptr(feat), ptr(thr),
-                        ptr(node_begin), ptr(first_blk), ptr(nblk), ptr(counts), ptr(left), 0,
+                        ptr(node_begin), ptr(first_blk), ptr(nblk), ptr(counts), ptr(left), 0, 0,
                         stream(binsT))
         return left
     left = torch.zeros(n_split, dtype=torch.int32)
@@ -257,7 +257,7 @@ def partition_count(binsT, rows, flags, items, feat, thr):
             return counts
         check_cuda(binsT, rows, flags, items, feat, thr)
         hip().partition_count(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(flags),
-                              ptr(items), nitems, ptr(feat), ptr(thr), ptr(counts), 0, stream(binsT))
+                              ptr(items), nitems, ptr(feat), ptr(thr), ptr(counts), 0, 0, stream(binsT))
         return counts
     counts = torch.zeros(nitems, dtype=torch.int32)
     it = items.numpy()
