@@ -32,10 +32,10 @@ void ytk_forest_predict(uintptr_t, long long, long long, uintptr_t, uintptr_t, u
 void ytk_bin_assign(uintptr_t, long long, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                     long long, uintptr_t, uintptr_t);
 void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, int, float, float,
-                   uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
-void ytk_tree_grad(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
-                   uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, float, float,
-                   uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+                   uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
+void ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                   uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
+                   float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,

@@ -452,10 +452,10 @@ __global__ void lv_raw_tree_kernel(LvBufs b, int max_nodes, const float* __restr
 }
 
 // Fixed-point scales from the (all-reduced) max |g|, |h| and global row count.
-__global__ void lv_scales_kernel(const double* __restrict__ mx, const long long* __restrict__ cnt,
+__global__ void lv_scales_kernel(const float* __restrict__ mx, const long long* __restrict__ cnt,
                                  float* __restrict__ scales, double* __restrict__ inv_scales) {
   if (threadIdx.x >= 2) return;
-  const double m = mx[threadIdx.x];
+  const double m = (double)mx[threadIdx.x];
   double s = 1.0;
   if (m > 0.0) {
     const double n = (double)max(1LL, cnt[1]);
@@ -550,7 +550,7 @@ void ytk_lv_raw_tree(const uintptr_t* ptrs, int max_nodes, uintptr_t cand, uintp
 void ytk_lv_scales(uintptr_t mx, uintptr_t cnt, uintptr_t scales, uintptr_t inv_scales,
                    uintptr_t stream) {
   hipLaunchKernelGGL(lv_scales_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
-                     (const double*)mx, (const long long*)cnt, (float*)scales, (double*)inv_scales);
+                     (const float*)mx, (const long long*)cnt, (float*)scales, (double*)inv_scales);
   YTK_LAUNCH_CHECK();
 }
 

@@ -13,7 +13,8 @@
 //     4 sub-tiles of 256 positions per step, wave ballots + one LDS scan of the
 //     16 (sub-tile, wave) counts -> stable destinations; writes the row id AND the
 //     (g,h) pair so the next level's histogram reads (g,h) contiguously.
-// items[blk] = {split_idx, begin, end, blk_in_node}
+// items[blk] = {split_idx, begin, end, blk_in_node}; rows == nullptr means the identity
+// permutation (root level without instance sampling: no iota copy).
 #include "common.h"
 
 namespace ytk {
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
   for (; pos + 3 * kPartThreads < it.z; pos += 4 * kPartThreads) {
     int r[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = rows[pos + j * kPartThreads];
+    for (int j = 0; j < 4; ++j) r[j] = rows ? rows[pos + j * kPartThreads] : pos + j * kPartThreads;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint8_t fl = (int)col[(unsigned)r[j]] <= t;
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
     }
   }
   for (; pos < it.z; pos += kPartThreads) {
-    const uint8_t fl = (int)col[(unsigned)rows[pos]] <= t;
+    const uint8_t fl = (int)col[(unsigned)(rows ? rows[pos] : pos)] <= t;
     flags[pos] = fl;
     c += fl;
   }
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
       g[j] = make_float2(0.f, 0.f);
       if (valid[j]) {
         left[j] = flags[pos] != 0;
-        r[j] = rows[pos];
+        r[j] = rows ? rows[pos] : pos;
         g[j] = ghp[pos];
       }
     }

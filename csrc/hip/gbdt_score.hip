@@ -9,9 +9,11 @@
 //
 // Design: the training-score update is FUSED with the loss/gradient pass
 // (tree_grad_kernel): one read of score/label/weight per row per round, the new
-// tree's leaf found by walking the COLUMN-MAJOR bin matrix (coalesced bytes), the
-// tree's node arrays staged in LDS, float math per row and an fp64 block sum of the
-// weighted loss.
+// tree's leaf found by walking the ROW-MAJOR bin matrix (all levels of the walk hit
+// the same 32-B row segment: ~32 B/row vs ~118 B/row for a column-major walk whose
+// lanes diverge over features), the node arrays staged in LDS, float math per row,
+// an fp64 block sum of the weighted loss, and the max |g| / |h| the next tree's
+// fixed-point histogram scales need (block max -> one uint atomicMax per block).
 #include "common.h"
 
 namespace ytk {
@@ -112,8 +114,8 @@ __device__ __forceinline__ LossOut point_loss(int loss_id, float z, float y, flo
   switch (loss_id) {
     case 0: {  // sigmoid (SigmoidFunction: stable log-loss, zmax hessian clamp)
       const float az = fabsf(z);
-      o.l = (double)log1pf(expf(-az)) + (double)(z >= 0.f ? z * (1.f - y) : -z * y);
       const float e = expf(-az);
+      o.l = (double)log1pf(e) + (double)(z >= 0.f ? z * (1.f - y) : -z * y);
       o.p = (z >= 0.f) ? 1.f / (1.f + e) : e / (1.f + e);
       o.g = o.p - y;
       o.h = o.p * (1.f - o.p);
@@ -151,28 +153,75 @@ __device__ __forceinline__ LossOut point_loss(int loss_id, float z, float y, flo
   return o;
 }
 
-__device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss_acc) {
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Block reduction of (loss, weight) sums and (max|g|, max|h|); one atomic each per block.
+__device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss_acc, float mg,
+                                          float mh, float* ghmax) {
   __shared__ double s_loss[4], s_w[4];
+  __shared__ float s_mg[4], s_mh[4];
   lsum = wave_sum(lsum);
   wsum = wave_sum(wsum);
+  mg = wave_maxf(mg);
+  mh = wave_maxf(mh);
   const int wid = threadIdx.x >> 6;
-  if (lane_id() == 0) { s_loss[wid] = lsum; s_w[wid] = wsum; }
+  if (lane_id() == 0) { s_loss[wid] = lsum; s_w[wid] = wsum; s_mg[wid] = mg; s_mh[wid] = mh; }
   __syncthreads();
   if (threadIdx.x == 0) {
     atomicAdd(&loss_acc[0], s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3]);
     atomicAdd(&loss_acc[1], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+    if (ghmax) {  // non-negative floats order like their bit patterns
+      atomicMax(reinterpret_cast<unsigned*>(&ghmax[0]),
+                __float_as_uint(fmaxf(fmaxf(s_mg[0], s_mg[1]), fmaxf(s_mg[2], s_mg[3]))));
+      atomicMax(reinterpret_cast<unsigned*>(&ghmax[1]),
+                __float_as_uint(fmaxf(fmaxf(s_mh[0], s_mh[1]), fmaxf(s_mh[2], s_mh[3]))));
+    }
   }
 }
 
-// K == 1 losses, optionally fused with the new tree's score update.
-template <typename BinT>
+// Leaf of a bin-threshold tree for one row held in registers (kDw dwords, packed bins):
+// the whole row is fetched with 16-B loads (a wave reads 64 contiguous rows), then
+// every level extracts its feature with a select chain -- no dependent memory loads.
+template <typename BinT, int kDw>
+__device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, const int* st,
+                                             const int* sl, const int* sr) {
+  constexpr int kPer = 4 / sizeof(BinT);
+  constexpr unsigned kMask = sizeof(BinT) == 1 ? 0xffu : 0xffffu;
+  uint32_t d[kDw];
+  const uint4* r4 = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+  for (int i = 0; i < kDw / 4; ++i) {
+    const uint4 v = r4[i];
+    d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+  }
+  int n = 0;
+  while (sf[n] >= 0) {
+    const int f = sf[n];
+    const int w = f / kPer;
+    uint32_t v = d[0];
+#pragma unroll
+    for (int i = 1; i < kDw; ++i) v = (w == i) ? d[i] : v;
+    const int b = (int)((v >> ((f % kPer) * 8 * sizeof(BinT))) & kMask);
+    n = (b <= st[n]) ? sl[n] : sr[n];
+  }
+  return n;
+}
+
+// K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
+// kDw > 0: rows of exactly kDw dwords walked in registers; kDw == 0: generic byte loads.
+template <typename BinT, int kDw>
 __global__ __launch_bounds__(256) void tree_grad_kernel(
-    const BinT* __restrict__ binsT, const int* __restrict__ tfeat, const int* __restrict__ tthr,
-    const int* __restrict__ tleft, const int* __restrict__ tright, const float* __restrict__ tval,
-    int nnodes, float* __restrict__ score, const float* __restrict__ init,
-    const float* __restrict__ label, const float* __restrict__ weight, long long N, int loss_id,
-    float p0, float score_div, float* __restrict__ pred, float2* __restrict__ gh,
-    double* __restrict__ loss_acc, int want_grad) {
+    const BinT* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
+    const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
+    const float* __restrict__ tval, int nnodes, float* __restrict__ score,
+    const float* __restrict__ init, const float* __restrict__ label,
+    const float* __restrict__ weight, long long N, int loss_id, float p0, float score_div,
+    float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
+    int want_grad, float* __restrict__ ghmax) {
   extern __shared__ __attribute__((aligned(16))) int tsm[];
   int* sf = tsm;
   int* st = tsm + nnodes;
@@ -184,12 +233,18 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
   }
   __syncthreads();
   double lsum = 0.0, wsum = 0.0;
+  float mg = 0.f, mh = 0.f;
   for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
        r += (long long)gridDim.x * blockDim.x) {
     float s = score[r];
     if (nnodes > 0) {
+      const BinT* row = bins + r * stride;
       int n = 0;
-      while (sf[n] >= 0) n = ((int)binsT[(size_t)sf[n] * N + r] <= st[n]) ? sl[n] : sr[n];
+      if constexpr (kDw > 0) {
+        n = walk_row_regs<BinT, kDw>(row, sf, st, sl, sr);
+      } else {
+        while (sf[n] >= 0) n = ((int)row[sf[n]] <= st[n]) ? sl[n] : sr[n];
+      }
       s += sv[n];
       score[r] = s;
     }
@@ -197,17 +252,23 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     const LossOut o = point_loss(loss_id, s / score_div + init[r], label[r], p0);
     lsum += (double)w * o.l;
     wsum += (double)w;
-    pred[r] = o.p;
-    if (want_grad) gh[r] = make_float2(o.g * w, o.h * w);
+    if (pred) pred[r] = o.p;
+    if (want_grad) {
+      const float gg = o.g * w, hh = o.h * w;
+      gh[r] = make_float2(gg, hh);
+      mg = fmaxf(mg, fabsf(gg));
+      mh = fmaxf(mh, fabsf(hh));
+    }
   }
-  block_acc(lsum, wsum, loss_acc);
+  block_acc(lsum, wsum, loss_acc, mg, mh, ghmax);
 }
 
+// softmax over K classes; ghmax is [K][2] (one (max|g|, max|h|) pair per class tree)
 __global__ __launch_bounds__(256) void softmax_grad_kernel(
     const float* __restrict__ score, const float* __restrict__ init,
     const float* __restrict__ label, const float* __restrict__ weight, long long N, int K,
     float score_div, float* __restrict__ pred, float2* __restrict__ gh,
-    double* __restrict__ loss_acc, int want_grad) {
+    double* __restrict__ loss_acc, int want_grad, float* __restrict__ ghmax) {
   double lsum = 0.0, wsum = 0.0;
   for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
        r += (long long)gridDim.x * blockDim.x) {
@@ -228,11 +289,18 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(
       const double z = (double)(score[r * K + k] / score_div + init[r * K + k]) - zmax;
       const double p = exp(z) * inv;
       const double y = label[r * K + k];
-      pred[r * K + k] = (float)p;
-      if (want_grad) gh[k * N + r] = make_float2((float)((p - y) * w), (float)(2.0 * p * (1.0 - p) * w));
+      if (pred) pred[r * K + k] = (float)p;
+      if (want_grad) {
+        const float gg = (float)((p - y) * w), hh = (float)(2.0 * p * (1.0 - p) * w);
+        gh[k * N + r] = make_float2(gg, hh);
+        if (ghmax) {
+          atomicMax(reinterpret_cast<unsigned*>(&ghmax[2 * k]), __float_as_uint(fabsf(gg)));
+          atomicMax(reinterpret_cast<unsigned*>(&ghmax[2 * k + 1]), __float_as_uint(fabsf(hh)));
+        }
+      }
     }
   }
-  block_acc(lsum, wsum, loss_acc);
+  block_acc(lsum, wsum, loss_acc, 0.f, 0.f, nullptr);
 }
 
 }  // namespace ytk
@@ -298,53 +366,65 @@ void ytk_bin_assign(uintptr_t X, long long xstride, long long N, int F, uintptr_
   YTK_LAUNCH_CHECK();
 }
 
-// score [N][K], init [N][K], label [N][K], gh [K][N]
+// score [N][K], init [N][K], label [N][K], gh [K][N]; pred / ghmax optional (0)
 void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
                    long long N, int K, int loss_id, float p0, float score_div, uintptr_t pred,
-                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t stream) {
+                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
+                   uintptr_t stream) {
   if (N <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_for(N, 256 * 8);
   if (loss_id == 5) {
     hipLaunchKernelGGL(softmax_grad_kernel, dim3(grid), dim3(256), 0, s, (const float*)score,
                        (const float*)init, (const float*)label, (const float*)weight, N, K,
-                       score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad);
+                       score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,
+                       (float*)ghmax);
   } else {
-    hipLaunchKernelGGL(tree_grad_kernel<uint8_t>, dim3(grid), dim3(256), 0, s,
-                       (const uint8_t*)nullptr, (const int*)nullptr, (const int*)nullptr,
+    hipLaunchKernelGGL((tree_grad_kernel<uint8_t, 0>), dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)nullptr, 0LL, (const int*)nullptr, (const int*)nullptr,
                        (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,
                        (float*)score, (const float*)init, (const float*)label,
                        (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
-                       (float2*)gh, (double*)loss_acc, want_grad);
+                       (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax);
   }
   YTK_LAUNCH_CHECK();
 }
 
-// Fused: score += tree(row) then loss / grad (K == 1).
-void ytk_tree_grad(uintptr_t binsT, int bin_bytes, uintptr_t tfeat, uintptr_t tthr,
-                   uintptr_t tleft, uintptr_t tright, uintptr_t tval, int nnodes,
+// Fused: score += tree(row) (row-major bins walk) then loss / grad (K == 1).
+void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfeat,
+                   uintptr_t tthr, uintptr_t tleft, uintptr_t tright, uintptr_t tval, int nnodes,
                    uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
                    long long N, int loss_id, float p0, float score_div, uintptr_t pred,
-                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t stream) {
+                   uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
+                   uintptr_t stream) {
   if (N <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t lds = (size_t)nnodes * 5 * sizeof(int);
   const int grid = grid_for(N, 256 * 8);
+  const long long row_bytes = stride * bin_bytes;
+  const bool aligned = (bins % 16) == 0;
+  // register walk for 16/32/64-byte rows (F <= 64 uint8 features), byte loads otherwise
+  const int dw = (aligned && (row_bytes == 16 || row_bytes == 32 || row_bytes == 64))
+                     ? (int)(row_bytes / 4) : 0;
+#define YTK_TG_LAUNCH(BT, DW)                                                                   \
+  hipLaunchKernelGGL((tree_grad_kernel<BT, DW>), dim3(grid), dim3(256), lds, s, (const BT*)bins, \
+                     stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,            \
+                     (const int*)tright, (const float*)tval, nnodes, (float*)score,             \
+                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id, \
+                     p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,    \
+                     (float*)ghmax)
   if (bin_bytes == 1) {
-    hipLaunchKernelGGL(tree_grad_kernel<uint8_t>, dim3(grid), dim3(256), lds, s,
-                       (const uint8_t*)binsT, (const int*)tfeat, (const int*)tthr,
-                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
-                       (float*)score, (const float*)init, (const float*)label,
-                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
-                       (float2*)gh, (double*)loss_acc, want_grad);
+    if (dw == 4) YTK_TG_LAUNCH(uint8_t, 4);
+    else if (dw == 8) YTK_TG_LAUNCH(uint8_t, 8);
+    else if (dw == 16) YTK_TG_LAUNCH(uint8_t, 16);
+    else YTK_TG_LAUNCH(uint8_t, 0);
   } else {
-    hipLaunchKernelGGL(tree_grad_kernel<uint16_t>, dim3(grid), dim3(256), lds, s,
-                       (const uint16_t*)binsT, (const int*)tfeat, (const int*)tthr,
-                       (const int*)tleft, (const int*)tright, (const float*)tval, nnodes,
-                       (float*)score, (const float*)init, (const float*)label,
-                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
-                       (float2*)gh, (double*)loss_acc, want_grad);
+    if (dw == 4) YTK_TG_LAUNCH(uint16_t, 4);
+    else if (dw == 8) YTK_TG_LAUNCH(uint16_t, 8);
+    else if (dw == 16) YTK_TG_LAUNCH(uint16_t, 16);
+    else YTK_TG_LAUNCH(uint16_t, 0);
   }
+#undef YTK_TG_LAUNCH
   YTK_LAUNCH_CHECK();
 }
 

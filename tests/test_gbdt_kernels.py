@@ -228,11 +228,14 @@ def test_tree_grad_fused_matches_cpu(cuda):
     t = Tree()
     l, r = t.add_children(0)
     t.set_split(0, 1, 5, 6)
-    t.set_leaf(l, 0.3)
-    t.set_leaf(r, -0.2)
-    N, F = 40000, 4
-    bins = _rand_bins(N, F, 12, 8)
-    binsT = bins[:, :F].t().contiguous()
+    ll, lr = t.add_children(l)
+    t.set_split(l, 13, 3, 4)
+    rl, rr = t.add_children(r)
+    t.set_split(r, 27, 8, 9)
+    for leaf, v in ((ll, 0.3), (lr, 0.1), (rl, -0.2), (rr, -0.05)):
+        t.set_leaf(leaf, v)
+    N, F = 40000, 28
+    bins = _rand_bins(N, F, 12, 8)  # row-major, padded row stride 32 -> register walk
     arrs = tuple(torch.from_numpy(a) for a in t.bin_arrays())
     g = torch.Generator().manual_seed(2)
     score = torch.randn((N, 1), generator=g)
@@ -240,14 +243,35 @@ def test_tree_grad_fused_matches_cpu(cuda):
     lab = (torch.rand((N, 1), generator=g) < 0.5).float()
     w = torch.rand(N, generator=g) + 0.5
     sc, pc, ghc = score.clone(), torch.zeros((N, 1)), torch.zeros((1, N, 2))
-    ac = gops.tree_grad(binsT, arrs, sc, init, lab, w, "sigmoid", 0.0, 1.0, pc, ghc[0])
+    mc = torch.zeros(2)
+    ac = gops.tree_grad(bins, arrs, sc, init, lab, w, "sigmoid", 0.0, 1.0, pc, ghc[0], True, mc)
+    # the bin-space walk equals a column walk on the same tree
+    ref = score[:, 0] + gops._walk_bins(bins[:, :F].t().contiguous(), arrs)
+    torch.testing.assert_close(sc[:, 0], ref)
+    torch.testing.assert_close(mc, ghc[0].abs().amax(dim=0))
     sg, pg, ghg = score.to(cuda), torch.zeros((N, 1), device=cuda), torch.zeros((1, N, 2), device=cuda)
-    ag = gops.tree_grad(binsT.to(cuda), tuple(a.to(cuda) for a in arrs), sg, init.to(cuda), lab.to(cuda),
-                        w.to(cuda), "sigmoid", 0.0, 1.0, pg, ghg[0])
+    mg = torch.zeros(2, device=cuda)
+    ag = gops.tree_grad(bins.to(cuda), tuple(a.to(cuda) for a in arrs), sg, init.to(cuda), lab.to(cuda),
+                        w.to(cuda), "sigmoid", 0.0, 1.0, pg, ghg[0], True, mg)
     torch.testing.assert_close(sg.cpu(), sc)
     torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(ghg.cpu(), ghc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mg.cpu(), ghg[0].abs().amax(dim=0).cpu(), rtol=0, atol=0)
     np.testing.assert_allclose(ag.cpu().numpy(), ac.numpy(), rtol=1e-6)
+    # pred is optional
+    sg2, ghg2 = score.to(cuda), torch.zeros((N, 2), device=cuda)
+    gops.tree_grad(bins.to(cuda), tuple(a.to(cuda) for a in arrs), sg2, init.to(cuda), lab.to(cuda),
+                   w.to(cuda), "sigmoid", 0.0, 1.0, None, ghg2)
+    torch.testing.assert_close(ghg2, ghg[0], rtol=0, atol=0)
+    # generic byte-load walk (row stride 40 B) and uint16 rows (64 B register walk)
+    wide = torch.zeros((N, 40), dtype=torch.uint8)
+    wide[:, :32] = bins
+    b16 = bins.to(torch.int16)
+    for bb in (wide, b16):
+        s3 = score.to(cuda)
+        gops.tree_grad(bb.to(cuda), tuple(a.to(cuda) for a in arrs), s3, init.to(cuda), lab.to(cuda),
+                       w.to(cuda), "sigmoid", 0.0, 1.0, None, torch.zeros((N, 2), device=cuda))
+        torch.testing.assert_close(s3.cpu(), sc, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("loss,K", [("sigmoid", 1), ("l2", 1), ("l1", 1), ("poisson", 1), ("huber", 1), ("softmax", 4)])
@@ -269,7 +293,10 @@ def test_grad_hess_matches_cpu(cuda, loss, K):
     pc, ghc = torch.zeros((N, K)), torch.zeros((K, N, 2))
     ac = gops.grad_hess(score, init, lab, w, loss, param, 1.0, pc, ghc)
     pg, ghg = torch.zeros((N, K), device=cuda), torch.zeros((K, N, 2), device=cuda)
-    ag = gops.grad_hess(score.to(cuda), init.to(cuda), lab.to(cuda), w.to(cuda), loss, param, 1.0, pg, ghg)
+    mg = torch.zeros((K, 2), device=cuda)
+    ag = gops.grad_hess(score.to(cuda), init.to(cuda), lab.to(cuda), w.to(cuda), loss, param, 1.0, pg, ghg,
+                        True, mg)
     torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(ghg.cpu(), ghc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mg.cpu(), ghg.abs().amax(dim=1).cpu(), rtol=0, atol=0)
     np.testing.assert_allclose(ag.cpu().numpy(), ac.numpy(), rtol=2e-6)

@@ -92,8 +92,13 @@ class DeviceLevelBuilder:
         self.max_items = max(self.HIST_TARGET, self.PART_TARGET) + self.maxp + 16
         dev = self.dev
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
-        self.st = i32(16)
-        self.nodes = torch.zeros(self.max_nodes * DNODE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        # everything a finished tree is (state, node table, scoring arrays) lives in ONE
+        # buffer so the per-tree snapshot is a single device copy
+        mn = self.max_nodes
+        self._snap_sizes = [64, mn * DNODE_DTYPE.itemsize] + [4 * mn] * 5
+        self.snap = torch.zeros(sum(self._snap_sizes), dtype=torch.uint8, device=dev)
+        (self.st, self.nodes, self.tfeat, self.tthr, self.tleft, self.tright,
+         self.tval) = self._snap_views(self.snap)
         self.pending, self.next_pending = i32(self.maxp), i32(self.maxp)
         self.split_nid, self.split_snap = i32(self.maxp), i32(self.maxp)
         self.part_items = i32(self.max_items * 4)
@@ -106,18 +111,17 @@ class DeviceLevelBuilder:
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)
         self.split_out = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
-        self.tfeat, self.tthr = i32(self.max_nodes), i32(self.max_nodes)
-        self.tleft, self.tright = i32(self.max_nodes), i32(self.max_nodes)
-        self.tval = torch.zeros(self.max_nodes, dtype=torch.float32, device=dev)
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
         self.n_slots = (1 << D) - 1
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
+        # one fill per tree beats one per level while the slab is small; deep trees zero
+        # only the built half of each level (the derived half is written by split_find)
+        self._zero_all = self.hist.numel() * 8 <= (64 << 20)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=dev)
         self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
         self.gh_tmp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
         self.flags = torch.empty(self.N, dtype=torch.uint8, device=dev)
-        self.iota = torch.arange(self.N, dtype=torch.int32, device=dev)
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
@@ -127,6 +131,14 @@ class DeviceLevelBuilder:
         self.last_keep = None
         self.total_stats = TimeStats()
         self._fmask_cache = {}
+
+    def _snap_views(self, buf):
+        out, off = [], 0
+        dts = [torch.int32, torch.uint8, torch.int32, torch.int32, torch.int32, torch.int32, torch.float32]
+        for sz, dt in zip(self._snap_sizes, dts):
+            out.append(buf[off:off + sz].view(dt))
+            off += sz
+        return out
 
     def _fp(self):
         p = self.p
@@ -158,18 +170,22 @@ class DeviceLevelBuilder:
         return self._fmask_cache[key], int(np.nonzero(fm)[0][0])
 
     # ------------------------------------------------------------------ build
-    def build(self, gh: torch.Tensor) -> DeviceTree:
+    def build(self, gh: torch.Tensor, ghmax: torch.Tensor = None) -> DeviceTree:
+        """Enqueue one tree. ``gh`` [N, 2] contiguous (g, h); ``ghmax`` (float32 [2], optional)
+        = max |g|, max |h| over all local rows, already produced by the gradient kernel."""
         p = self.p
         h = hip()
         s = stream(self.bins)
-        ptrs = self._ptrs()
         fp = self._fp()
         ip = self.ip
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))
         dist = self.comm.is_dist
-        # rows / position-ordered (g, h)
-        if p.instance_sample_rate < 1.0:
+        sampled = p.instance_sample_rate < 1.0
+        assert gh.is_contiguous() and gh.shape == (self.N, 2)
+        # rows / position-ordered (g, h). Without sampling the root level reads the identity
+        # permutation and the caller's gh directly; the first partition writes the buffers.
+        if sampled:
             g = torch.Generator(device=self.dev)
             g.manual_seed(seed_rows + self.comm.rank)
             keep = torch.rand(self.N, generator=g, device=self.dev) < p.instance_sample_rate
@@ -180,30 +196,36 @@ class DeviceLevelBuilder:
             self.ghp.copy_(gh.index_select(0, order))
             self.root_cnt[0] = keep.sum()
             self.last_keep = keep
+            rows0, gh0 = ptr(self.rows), ptr(self.ghp)
         else:
-            self.rows.copy_(self.iota)
-            self.ghp.copy_(gh)
             self.root_cnt[0] = self.N
             self.last_keep = None
+            rows0, gh0 = 0, ptr(gh)
         fmask, f0 = self._fmask(rng)
         self.root_cnt[1] = self.root_cnt[0]
         if dist:
             self.comm.allreduce_(self.root_cnt[1:2])
         # fixed-point scales from the global max |g|, |h| over the tree's rows
-        if p.instance_sample_rate < 1.0:
-            mx = (gh.abs() * keep[:, None]).amax(dim=0).double()
+        if sampled:
+            mx = (gh.abs() * keep[:, None]).amax(dim=0)
+        elif ghmax is not None:
+            mx = ghmax
         else:
-            mx = gh.abs().amax(dim=0).double()
+            mx = gh.abs().amax(dim=0)
         if dist:
+            mx = mx.clone()
             self.comm.allreduce_(mx, op="max")
         h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
         # root
+        ptrs = self._ptrs()
         st_ptr = self.st.data_ptr()
         off = lambda w: st_ptr + 4 * w
         h.lv_step(0, ptrs, ip, fp, 0, 0, s)
-        self.hist[0:1].zero_()
-        h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, ptr(self.ghp),
-                  0 if p.instance_sample_rate >= 1.0 else ptr(self.rows),
+        if self._zero_all:
+            self.hist.zero_()  # every slot of the tree in one fill (small slabs)
+        else:
+            self.hist[0:1].zero_()
+        h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh0, rows0,
                   ptr(self.hist_items), self.HIST_TARGET + 1, ptr(self.hist), self.B, 1.0, 1.0,
                   off(5), ptr(self.scales), s)
         if dist:
@@ -218,14 +240,16 @@ class DeviceLevelBuilder:
             h.lv_step(1, ptrs, ip, fp, 0, 0, s)  # apply splits + pop nodes of depth d
             npart = self.PART_TARGET + (1 << d) + 1
             last = c == p.max_depth
+            rows_in = rows0 if d == 0 else ptr(self.rows)
+            gh_in = gh0 if d == 0 else ptr(self.ghp)
             # the flag kernel also accumulates the per-split left totals into left_loc
             if last:
-                h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.flags),
+                h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.flags),
                                   ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),
                                   ptr(self.part_counts), off(4), ptr(self.left_loc), s)
             else:
-                h.partition(ptr(self.binsT), bb, self.binsT.shape[1], ptr(self.rows), ptr(self.rows_tmp),
-                            ptr(self.ghp), ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
+                h.partition(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
+                            gh_in, ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
                             ptr(self.left_loc), s)
@@ -239,7 +263,8 @@ class DeviceLevelBuilder:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
-            self.hist[base:base + half].zero_()
+            if not self._zero_all:
+                self.hist[base:base + half].zero_()
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, ptr(self.ghp), ptr(self.rows),
                       ptr(self.hist_items), self.HIST_TARGET + half + 1, ptr(self.hist), self.B, 1.0, 1.0,
                       off(5), ptr(self.scales), s)
@@ -250,8 +275,8 @@ class DeviceLevelBuilder:
                          gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         self.tree_count += 1
-        arrays = tuple(t.clone() for t in (self.tfeat, self.tthr, self.tleft, self.tright, self.tval))
-        return DeviceTree(self.nodes.clone(), self.st.clone(), arrays, self.max_nodes)
+        st, nodes, *arrays = self._snap_views(self.snap.clone())
+        return DeviceTree(nodes, st, tuple(arrays), self.max_nodes)
 
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (for test-set scoring), one forest entry."""

@@ -146,6 +146,8 @@ class GBDTTrainer:
         self.init_score = self._base_score(tr)
         self.pred = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
         self.gh = torch.zeros((self.K, N, 2), dtype=torch.float32, device=self.dev)
+        # max |g|, |h| per class, produced by the gradient kernel for the next trees' scales
+        self.ghmax = torch.zeros((self.K, 2), dtype=torch.float32, device=self.dev)
         self.y = tr.y.contiguous()
         self.w = tr.weight.contiguous() if tr.weight is not None else None
         sums = self.comm.allreduce_scalars([float(tr.weight.sum()) if tr.weight is not None else float(N), float(N)])
@@ -196,7 +198,12 @@ class GBDTTrainer:
     def _loss_grad(self, score, init, y, w, pred, gh, rounds_done, want_grad=True):
         div = self._score_div(rounds_done)
         if self.kernel_loss is not None:
-            return gops.grad_hess(score, init, y, w, self.kernel_loss, self._kparam(), div, pred, gh, want_grad)
+            ghmax = None
+            if want_grad:
+                ghmax = self.ghmax
+                ghmax.zero_()
+            return gops.grad_hess(score, init, y, w, self.kernel_loss, self._kparam(), div, pred, gh, want_grad,
+                                  ghmax)
         # generic loss (torch on device): GBDT derivative from the float prediction
         z = score.double() / div + init.double()
         yy = y.double()
@@ -212,6 +219,7 @@ class GBDTTrainer:
             g, h = self.loss.fast_deriv(pred.double(), yy)
             gh[:, :, 0] = (g * ww[:, None]).float().t()
             gh[:, :, 1] = (h * ww[:, None]).float().t()
+            self.ghmax.copy_(gh.abs().amax(dim=1))
         return torch.stack([(lv.reshape(lv.shape[0], -1).sum(1) * ww).sum(), ww.sum()])
 
     def init_gradients(self):
@@ -271,7 +279,7 @@ class GBDTTrainer:
         arrays, raws, host_trees, dev_trees = [], [], [], []
         for k in range(self.K):
             if self.use_device_builder:
-                dt = self.builder.build(self.gh[k])
+                dt = self.builder.build(self.gh[k], self.ghmax[k])
                 dev_trees.append(dt)
                 arrays.append(dt.bin_arrays)
                 if self.test_data is not None:
@@ -288,8 +296,10 @@ class GBDTTrainer:
                 arrays.append(self._tree_to_dev(tree))
         # score update + train loss after this round + gradients for the next round
         if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
-            acc = gops.tree_grad(self.binsT, arrays[0], self.score, self.init_score, self.y, self.w,
-                                 self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0])
+            self.ghmax.zero_()
+            acc = gops.tree_grad(self.bins, arrays[0], self.score, self.init_score, self.y, self.w,
+                                 self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0],
+                                 True, self.ghmax[0])
         else:
             for k in range(self.K):
                 gops.tree_add_bins(self.binsT, arrays[k], self.score, k)

@@ -378,17 +378,21 @@ def bin_assign(X, cand, coff, out, outT=None):
 # ---------------------------------------------------------------------------
 # gradients
 # ---------------------------------------------------------------------------
-def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True):
-    """Fill pred [N,K] and gh [K,N,2]; return (weighted loss sum, weight sum) as a
-    float64 tensor of shape [2] on the data device (no host sync)."""
+def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True,
+              ghmax=None):
+    """Fill pred [N,K] (optional) and gh [K,N,2]; return (weighted loss sum, weight sum) as a
+    float64 tensor of shape [2] on the data device (no host sync).
+
+    ``ghmax`` (float32 [K,2], optional) is max-accumulated with max|g|, max|h| per class —
+    the next trees' fixed-point histogram scales (see DeviceLevelBuilder)."""
     N, K = score.shape
     loss_id = LOSS_IDS[loss]
     if score.is_cuda:
-        check_cuda(score, init, label, weight, pred, gh)
+        check_cuda(score, init, label, weight, pred, gh, ghmax)
         acc = torch.zeros(2, dtype=torch.float64, device=score.device)
         hip().grad_hess(ptr(score), ptr(init), ptr(label), ptr(weight), N, K, loss_id,
                         float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
-                        1 if want_grad else 0, stream(score))
+                        1 if want_grad else 0, ptr(ghmax), stream(score))
         return acc
     z = score.double() / score_div + init.double()
     y = label.double()
@@ -435,16 +439,21 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
             g = torch.where(aa.abs() <= d, aa, torch.sign(aa) * d)
             h = torch.zeros_like(p)
         p, g, h = p[:, None], g[:, None], h[:, None]
-    pred.copy_(p.float())
+    if pred is not None:
+        pred.copy_(p.float())
     if want_grad:
         gh[:, :, 0] = (g * w[:, None]).float().t()
         gh[:, :, 1] = (h * w[:, None]).float().t()
+        if ghmax is not None:
+            m = gh.abs().amax(dim=1).reshape(ghmax.shape)
+            ghmax.copy_(torch.maximum(ghmax, m))
     return torch.tensor([float((w * lv).sum()), float(w.sum())], dtype=torch.float64)
 
 
-def tree_grad(binsT, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
-              want_grad=True):
-    """Fused K==1 round tail: score += tree(row) (bin space), then pred / (g, h) / loss sums.
+def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
+              want_grad=True, ghmax=None):
+    """Fused K==1 round tail: score += tree(row) (bin space, ROW-MAJOR bins [N, S]), then
+    pred (optional) / (g, h) / loss sums / max|g|,|h| (optional ``ghmax`` [1,2]).
     ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum)."""
     loss_id = LOSS_IDS[loss]
     assert loss_id != 5 and score.shape[1] == 1
@@ -457,12 +466,15 @@ def tree_grad(binsT, tree_arrays, score, init, label, weight, loss, param, score
         else:
             tf, tt, tl, tr, tv = tree_arrays
             nn = tf.shape[0]
-        check_cuda(binsT, score, init, label, weight, pred, gh, tf, tt, tl, tr, tv)
-        hip().tree_grad(ptr(binsT), _bin_bytes(binsT) if binsT is not None else 1, ptr(tf), ptr(tt),
-                        ptr(tl), ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label),
-                        ptr(weight), N, loss_id, float(param), float(score_div), ptr(pred), ptr(gh),
-                        ptr(acc), 1 if want_grad else 0, stream(score))
+            assert bins is not None and bins.shape[0] == N and bins.stride(1) == 1
+        check_cuda(bins, score, init, label, weight, pred, gh, ghmax, tf, tt, tl, tr, tv)
+        hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
+                        bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
+                        ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
+                        loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
+                        1 if want_grad else 0, ptr(ghmax), stream(score))
         return acc
     if tree_arrays is not None:
-        tree_add_bins(binsT, tree_arrays, score, 0)
-    return grad_hess(score, init, label, weight, loss, param, score_div, pred, gh.unsqueeze(0), want_grad)
+        score[:, 0] += _walk_bins(bins.t(), tree_arrays)
+    return grad_hess(score, init, label, weight, loss, param, score_div, pred, gh.unsqueeze(0),
+                     want_grad, ghmax)
