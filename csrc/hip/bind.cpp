@@ -36,6 +36,10 @@ void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, i
 void ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
                    float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
+// sparse.hip
+void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, long long, int,
+                  uintptr_t, long long, float, int, int, int, uintptr_t);
+void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
@@ -57,6 +61,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("bin_assign", &ytk_bin_assign);
   m.def("grad_hess", &ytk_grad_hess);
   m.def("tree_grad", &ytk_tree_grad);
+  m.def("seg_spmm", &ytk_seg_spmm);
+  m.def("chunk_reduce", &ytk_chunk_reduce);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 25 || ip.size() != 6 || fp.size() != 6)

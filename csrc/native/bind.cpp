@@ -4,9 +4,73 @@
 #include <pybind11/stl.h>
 
 #include "native.h"
+#include "parser.h"
 
 namespace py = pybind11;
 using namespace ytk_native;
+
+namespace {
+
+// Hand a std::vector to numpy without copying (the capsule owns the heap vector).
+template <typename T>
+py::array_t<T> to_numpy(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
+  return py::array_t<T>({(py::ssize_t)heap->size()}, {(py::ssize_t)sizeof(T)}, heap->data(), owner);
+}
+
+ParseOptions options_from(const py::dict& d) {
+  ParseOptions o;
+  auto get_s = [&](const char* k, std::string& dst) {
+    if (d.contains(k)) dst = d[k].cast<std::string>();
+  };
+  get_s("x_delim", o.x_delim);
+  get_s("y_delim", o.y_delim);
+  get_s("features_delim", o.feat_delim);
+  get_s("feature_name_val_delim", o.kv_delim);
+  get_s("field_delim", o.field_delim);
+  get_s("hash_prefix", o.hash_prefix);
+  if (d.contains("feature_hash")) o.feature_hash = d["feature_hash"].cast<bool>();
+  if (d.contains("hash_bucket")) o.hash_bucket = d["hash_bucket"].cast<int64_t>();
+  if (d.contains("hash_seed")) o.hash_seed = (uint32_t)d["hash_seed"].cast<int64_t>();
+  if (d.contains("split_field")) o.split_field = d["split_field"].cast<bool>();
+  if (d.contains("max_error_tol")) o.max_error_tol = d["max_error_tol"].cast<int64_t>();
+  if (d.contains("y_sampling")) o.y_sampling = d["y_sampling"].cast<std::vector<float>>();
+  if (d.contains("sample_seed")) o.sample_seed = d["sample_seed"].cast<uint64_t>();
+  if (d.contains("line_mod")) o.line_mod = d["line_mod"].cast<int64_t>();
+  if (d.contains("line_rem")) o.line_rem = d["line_rem"].cast<int64_t>();
+  if (d.contains("want_stats")) o.want_stats = d["want_stats"].cast<bool>();
+  if (d.contains("threads")) o.threads = d["threads"].cast<int>();
+  return o;
+}
+
+py::dict result_to_dict(ParseResult&& r) {
+  py::dict out;
+  out["n_lines"] = r.n_lines;
+  out["n_rows"] = r.n_rows;
+  out["n_errors"] = r.n_errors;
+  out["n_sampled_out"] = r.n_sampled_out;
+  out["weight"] = to_numpy(std::move(r.weight));
+  out["label_ptr"] = to_numpy(std::move(r.label_ptr));
+  out["labels"] = to_numpy(std::move(r.labels));
+  out["init_ptr"] = to_numpy(std::move(r.init_ptr));
+  out["init"] = to_numpy(std::move(r.init));
+  out["indptr"] = to_numpy(std::move(r.indptr));
+  out["feat"] = to_numpy(std::move(r.feat));
+  out["val"] = to_numpy(std::move(r.val));
+  out["field"] = to_numpy(std::move(r.field));
+  out["names"] = py::cast(r.names);
+  out["counts"] = to_numpy(std::move(r.counts));
+  out["st_sum"] = to_numpy(std::move(r.st_sum));
+  out["st_sum2"] = to_numpy(std::move(r.st_sum2));
+  out["st_max"] = to_numpy(std::move(r.st_max));
+  out["st_min"] = to_numpy(std::move(r.st_min));
+  out["fields"] = py::cast(r.fields);
+  out["error_samples"] = py::cast(r.error_samples);
+  return out;
+}
+
+}  // namespace
 
 PYBIND11_MODULE(_ytk_native, m) {
   m.doc() = "ytk-learn-amd native host runtime";
@@ -20,4 +84,29 @@ PYBIND11_MODULE(_ytk_native, m) {
       o(i) = murmur3_128_aslong(names[i].data(), names[i].size(), seed);
     return out;
   });
+  m.def(
+      "parse_buffer",
+      [](py::bytes data, const py::dict& opts) {
+        const ParseOptions o = options_from(opts);
+        std::string_view s = data;  // keep the bytes object alive in this frame
+        ParseResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = parse_ytk(s.data(), s.size(), o);
+        }
+        return result_to_dict(std::move(r));
+      },
+      py::arg("data"), py::arg("opts"));
+  m.def(
+      "parse_files",
+      [](const std::vector<std::string>& paths, const py::dict& opts) {
+        const ParseOptions o = options_from(opts);
+        ParseResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = parse_ytk_files(paths, o);
+        }
+        return result_to_dict(std::move(r));
+      },
+      py::arg("paths"), py::arg("opts"));
 }

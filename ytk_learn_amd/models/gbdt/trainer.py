@@ -52,6 +52,10 @@ class GBDTParams:
     dump_freq: int = -1
     verbose: bool = False
     device_builder: bool = True  # use the GPU-resident builder when applicable
+    tree_maker: str = "data"      # "data" (histogram, data parallel) | "feature" (exact greedy)
+    histogram_pool_capacity: float = -1.0
+    just_evaluate: bool = False
+    filter_threshold: int = 0
     tree: TreeParams = field(default_factory=TreeParams)
 
 

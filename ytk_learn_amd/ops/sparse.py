@@ -1,0 +1,143 @@
+"""Device sparse matrix for the L-BFGS model family (linear, multiclass, FM, GBMLR...).
+
+Holds CSR (rows) and CSC (columns, split into fixed-size chunks) of the same matrix so
+that both ``X @ W`` and ``X^T @ D`` run as the deterministic segmented kernel of
+``csrc/hip/sparse.hip`` (no float atomics). On CPU the same products use torch
+index ops (reference path for tests).
+
+Reference hot loops: ``J/optimizer/LinearHoagOptimizer.java:76-106`` (Xv / XTv) and the
+per-model loops listed in SURVEY.md §2.A K16-K21.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._ext import check_cuda, hip, ptr, stream
+
+CHUNK = 4096  # nnz per CSC chunk: balances the bias column (all rows) against short columns
+
+
+def _lanes(avg_nnz: float) -> int:
+    L = 1
+    while L < avg_nnz and L < 64:
+        L <<= 1
+    return max(L, 4)
+
+
+class SparseMatrix:
+    """Immutable CSR/CSC pair. ``indptr`` int64 [n+1], ``indices`` int32, ``values`` float32."""
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, ncols: int,
+                 build_csc: bool = True):
+        self.device = indices.device
+        self.n = int(indptr.shape[0] - 1)
+        self.ncols = int(ncols)
+        self.indptr = indptr.to(torch.int64).contiguous()
+        self.indices = indices.to(torch.int32).contiguous()
+        self.values = values.to(torch.float32).contiguous()
+        self.nnz = int(self.indices.shape[0])
+        self.row_beg = self.indptr[:-1].contiguous()
+        self.row_end = self.indptr[1:].contiguous()
+        self.row_lanes = _lanes(self.nnz / max(self.n, 1))
+        self.rows_of_nnz = torch.repeat_interleave(torch.arange(self.n, device=self.device),
+                                                   self.indptr[1:] - self.indptr[:-1])
+        self._csc = None
+        if build_csc:
+            self._build_csc()
+
+    def _build_csc(self):
+        cols = self.indices.to(torch.int64)
+        order = torch.sort(cols * (self.n + 1) + self.rows_of_nnz, stable=True).indices
+        self.csc_perm = order
+        self.csc_rows = self.rows_of_nnz[order].to(torch.int32).contiguous()
+        self.csc_vals = self.values[order].contiguous()
+        counts = torch.bincount(cols, minlength=self.ncols)
+        colptr = torch.zeros(self.ncols + 1, dtype=torch.int64, device=self.device)
+        colptr[1:] = torch.cumsum(counts, 0)
+        self.colptr = colptr
+        # chunks: column c is split into ceil(len/CHUNK) segments (at least 1 when non-empty)
+        nch = (counts + CHUNK - 1) // CHUNK
+        cbeg = torch.zeros(self.ncols + 1, dtype=torch.int64, device=self.device)
+        cbeg[1:] = torch.cumsum(nch, 0)
+        total = int(cbeg[-1])
+        chunk_col = torch.repeat_interleave(torch.arange(self.ncols, device=self.device), nch)
+        within = torch.arange(total, device=self.device) - cbeg[:-1][chunk_col]
+        self.chunk_beg = (colptr[:-1][chunk_col] + within * CHUNK).contiguous()
+        self.chunk_end = torch.minimum(self.chunk_beg + CHUNK, colptr[1:][chunk_col]).contiguous()
+        self.chunk_ptr = cbeg.contiguous()
+        self.n_chunks = total
+        self.chunk_lanes = _lanes(self.nnz / max(total, 1))
+        self._csc = True
+
+    # ------------------------------------------------------------------ products
+    def matmul(self, W: torch.Tensor, out: Optional[torch.Tensor] = None, square: bool = False,
+               alpha: float = 1.0, accumulate: bool = False, values: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """out[n, J] = alpha * X @ W  (W: [ncols] or [ncols, J]); ``square`` uses X∘X.
+        ``values`` overrides the stored values (e.g. FFM/FM variants)."""
+        W2 = W.reshape(W.shape[0], -1)
+        J = W2.shape[1]
+        vals = self.values if values is None else values
+        if out is None:
+            out = torch.zeros((self.n,) if W.dim() == 1 else (self.n, J), dtype=torch.float32, device=self.device)
+            accumulate = False
+        o2 = out.reshape(self.n, -1)
+        if self.device.type == "cuda":
+            check_cuda(W2, o2, vals)
+            hip().seg_spmm(ptr(self.row_beg), ptr(self.row_end), self.n, ptr(self.indices), ptr(vals), ptr(W2),
+                           W2.stride(0), J, ptr(o2), o2.stride(0), float(alpha), int(accumulate), int(square),
+                           self.row_lanes if J == 1 else min(64, J), stream(W2))
+        else:
+            v = vals * vals if square else vals
+            prod = W2.index_select(0, self.indices.long()) * v[:, None]
+            res = torch.zeros((self.n, J), dtype=torch.float32)
+            res.index_add_(0, self.rows_of_nnz, prod)
+            if accumulate:
+                o2 += alpha * res
+            else:
+                o2.copy_(alpha * res)
+        return out
+
+    def t_matmul(self, D: torch.Tensor, out: Optional[torch.Tensor] = None, square: bool = False,
+                 alpha: float = 1.0, accumulate: bool = False, values: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """out[ncols, J] = alpha * X^T @ D  (D: [n] or [n, J])."""
+        if self._csc is None:
+            self._build_csc()
+        D2 = D.reshape(self.n, -1)
+        J = D2.shape[1]
+        if out is None:
+            out = torch.zeros((self.ncols,) if D.dim() == 1 else (self.ncols, J), dtype=torch.float32,
+                              device=self.device)
+            accumulate = False
+        o2 = out.reshape(self.ncols, -1)
+        if self.device.type == "cuda":
+            csc_vals = self.csc_vals if values is None else values
+            check_cuda(D2, o2, csc_vals)
+            part = torch.empty((max(self.n_chunks, 1), J), dtype=torch.float32, device=self.device)
+            h = hip()
+            s = stream(D2)
+            h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), self.n_chunks, ptr(self.csc_rows), ptr(csc_vals),
+                       ptr(D2), D2.stride(0), J, ptr(part), J, 1.0, 0, int(square),
+                       self.chunk_lanes if J == 1 else min(64, J), s)
+            h.chunk_reduce(ptr(self.chunk_ptr), self.ncols, ptr(part), J, ptr(o2), o2.stride(0), float(alpha),
+                           int(accumulate), s)
+        else:
+            vals = self.csc_vals if values is None else values
+            v = vals * vals if square else vals
+            prod = D2.index_select(0, self.csc_rows.long()) * v[:, None]
+            # column-ordered segment sums (deterministic, same chunk order as the GPU path)
+            res = torch.zeros((self.ncols, J), dtype=torch.float32)
+            cols = torch.repeat_interleave(torch.arange(self.ncols), self.colptr[1:] - self.colptr[:-1])
+            res.index_add_(0, cols, prod)
+            if accumulate:
+                o2 += alpha * res
+            else:
+                o2.copy_(alpha * res)
+        return out
+
+    def csc_values_of(self, nnz_values: torch.Tensor) -> torch.Tensor:
+        """Permute a per-nnz CSR-ordered tensor into CSC order (for custom-valued products)."""
+        if self._csc is None:
+            self._build_csc()
+        return nnz_values[self.csc_perm].contiguous()
