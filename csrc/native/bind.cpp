@@ -85,6 +85,17 @@ PYBIND11_MODULE(_ytk_native, m) {
     return out;
   });
   m.def(
+      "java_random",
+      [](int64_t seed, int64_t n, int mode, double a, double b) {
+        std::vector<double> v;
+        {
+          py::gil_scoped_release nogil;
+          v = java_random_fill(seed, n, mode, a, b);
+        }
+        return to_numpy(std::move(v));
+      },
+      py::arg("seed"), py::arg("n"), py::arg("mode"), py::arg("a") = 0.0, py::arg("b") = 1.0);
+  m.def(
       "parse_buffer",
       [](py::bytes data, const py::dict& opts) {
         const ParseOptions o = options_from(opts);

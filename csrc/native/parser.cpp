@@ -250,12 +250,6 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
       }
     }
     if (bad) { fail(); continue; }
-    // field split (FFM) must succeed for every feature before the row is committed
-    if (opt.split_field) {
-      for (auto& kv : S.kv)
-        if (kv.first.find(opt.field_delim) == sv::npos) { bad = true; break; }
-      if (bad) { fail(); continue; }
-    }
     // commit row
     L.weight.push_back(w);
     L.labels.insert(L.labels.end(), S.tmp.begin(), S.tmp.end());
@@ -273,9 +267,9 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
         L.st_max[id] = std::max(L.st_max[id], (double)v);
         L.st_min[id] = std::min(L.st_min[id], (double)v);
       }
-      if (opt.split_field) {
+      if (opt.split_field) {  // field = name prefix before field_delim (whole name if absent)
         const size_t q = name.find(opt.field_delim);
-        L.field.push_back(L.field_of(name.substr(0, q)));
+        L.field.push_back(L.field_of(q == std::string::npos ? name : name.substr(0, q)));
       }
     };
     if (opt.feature_hash) {
