@@ -96,6 +96,33 @@ PYBIND11_MODULE(_ytk_native, m) {
       },
       py::arg("seed"), py::arg("n"), py::arg("mode"), py::arg("a") = 0.0, py::arg("b") = 1.0);
   m.def(
+      "java_random_seq",
+      [](int64_t seed, const std::vector<std::tuple<int, int64_t, double, double>>& segs) {
+        // several draw segments from ONE java.util.Random stream (e.g. GBSDT: dim draws of
+        // next(), then K leaf draws of nextUniform(range))
+        std::vector<double> v;
+        {
+          py::gil_scoped_release nogil;
+          JavaRandom r(seed);
+          for (const auto& s : segs) {
+            const int mode = std::get<0>(s);
+            const double a = std::get<2>(s), b = std::get<3>(s);
+            for (int64_t i = 0; i < std::get<1>(s); ++i) {
+              double x;
+              switch (mode) {
+                case 0: x = r.next_gaussian() * b + a; break;
+                case 1: x = a + (b - a) * r.next_double(); break;
+                case 2: x = (double)r.next_float(); break;
+                default: x = r.next_double(); break;
+              }
+              v.push_back(x);
+            }
+          }
+        }
+        return to_numpy(std::move(v));
+      },
+      py::arg("seed"), py::arg("segments"));
+  m.def(
       "parse_buffer",
       [](py::bytes data, const py::dict& opts) {
         const ParseOptions o = options_from(opts);
