@@ -51,6 +51,7 @@ py::dict result_to_dict(ParseResult&& r) {
   out["n_errors"] = r.n_errors;
   out["n_sampled_out"] = r.n_sampled_out;
   out["weight"] = to_numpy(std::move(r.weight));
+  out["row_line"] = to_numpy(std::move(r.row_line));
   out["label_ptr"] = to_numpy(std::move(r.label_ptr));
   out["labels"] = to_numpy(std::move(r.labels));
   out["init_ptr"] = to_numpy(std::move(r.init_ptr));

@@ -119,6 +119,7 @@ struct SvHash {
 struct Local {
   // rows
   std::vector<float> weight, labels, init, val;
+  std::vector<int64_t> row_line;
   std::vector<int64_t> label_ptr{0}, init_ptr{0}, indptr{0};
   std::vector<int32_t> feat, field;
   // dictionary (names owned here; map keys view into `names`)
@@ -252,6 +253,7 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
     if (bad) { fail(); continue; }
     // commit row
     L.weight.push_back(w);
+    L.row_line.push_back(idx);
     L.labels.insert(L.labels.end(), S.tmp.begin(), S.tmp.end());
     L.label_ptr.push_back((int64_t)L.labels.size());
     L.init.insert(L.init.end(), initv.begin(), initv.end());
@@ -443,6 +445,7 @@ ParseResult parse_ytk(const char* data, size_t len, const ParseOptions& opt) {
     const int64_t lo = (int64_t)R.labels.size(), io = (int64_t)R.init.size(),
                   fo = (int64_t)R.feat.size();
     R.weight.insert(R.weight.end(), L.weight.begin(), L.weight.end());
+    R.row_line.insert(R.row_line.end(), L.row_line.begin(), L.row_line.end());
     R.labels.insert(R.labels.end(), L.labels.begin(), L.labels.end());
     R.init.insert(R.init.end(), L.init.begin(), L.init.end());
     for (size_t i = 1; i < L.label_ptr.size(); ++i) R.label_ptr.push_back(L.label_ptr[i] + lo);

@@ -38,6 +38,7 @@ struct ParseResult {
   int64_t n_errors = 0;
   int64_t n_sampled_out = 0;
   std::vector<float> weight;
+  std::vector<int64_t> row_line;   // source line index (0-based, all lines counted) per row
   std::vector<int64_t> label_ptr;  // [n_rows + 1]
   std::vector<float> labels;
   std::vector<int64_t> init_ptr;   // [n_rows + 1] (4th field; empty ranges when absent)

@@ -37,6 +37,34 @@ VARIANTS = {"gbmlr": ("softmax", "linear"), "gbsdt": ("softmax", "scalar"),
             "gbhmlr": ("tree", "linear"), "gbhsdt": ("tree", "scalar")}
 
 
+def gbst_mixture(A: torch.Tensor, K: int, gate_kind: str, expert_kind: str, leaves: Optional[torch.Tensor]):
+    """Mixture pieces from A = X W (fp64 [n, 2K-1] or [n, K-1]).
+
+    Returns (g [n,K] gate probabilities, H [n,K] expert values, mu [n,2K] heap node sums
+    (hierarchical gates only, mu[:,1] = sum g*H), sig [n,K-1] node sigmoids or None)."""
+    Km1 = K - 1
+    logits = A[:, :Km1]
+    if expert_kind == "linear":
+        H = A[:, Km1:Km1 + K]
+    else:
+        H = leaves.double()[None, :].expand(A.shape[0], K)
+    if gate_kind == "softmax":
+        full = torch.cat([logits, torch.zeros_like(logits[:, :1])], dim=1)
+        return torch.softmax(full, dim=1), H, None, None
+    sig = torch.sigmoid(logits)
+    n = A.shape[0]
+    prob = torch.ones((n, 2 * K), dtype=torch.float64, device=A.device)  # heap nodes 1..2K-1
+    for p in range(1, K):
+        prob[:, 2 * p] = prob[:, p] * sig[:, p - 1]          # left child (even heap index): sigma
+        prob[:, 2 * p + 1] = prob[:, p] * (1.0 - sig[:, p - 1])
+    g = prob[:, K:2 * K]
+    mu = torch.zeros((n, 2 * K), dtype=torch.float64, device=A.device)
+    mu[:, K:] = g * H
+    for p in range(K - 1, 0, -1):
+        mu[:, p] = mu[:, 2 * p] + mu[:, 2 * p + 1]
+    return g, H, mu, sig
+
+
 def _jlist(vals) -> str:
     """Java Arrays.toString(double[])."""
     return "[" + ", ".join(java_double_str(float(v)) for v in vals) + "]"
@@ -148,27 +176,8 @@ class GBSTModel(ContinuousModelBase):
     def _mixture(self, X, w, fmask):
         """(gate probs g [n,K], expert values H [n,K], mu_nodes or None, sig [n,K-1] or None) in fp64."""
         A = X.matmul(self._masked_W(w, fmask).contiguous()).double()
-        logits = A[:, :self.Km1]
-        if self.expert_kind == "linear":
-            H = A[:, self.Km1:]
-        else:
-            H = w[:self.K].double()[None, :].expand(A.shape[0], self.K)
-        if self.gate_kind == "softmax":
-            full = torch.cat([logits, torch.zeros_like(logits[:, :1])], dim=1)
-            g = torch.softmax(full, dim=1)
-            return g, H, None, None
-        sig = torch.sigmoid(logits)
-        n = A.shape[0]
-        prob = torch.ones((n, 2 * self.K), dtype=torch.float64, device=A.device)  # heap 1..2K-1
-        for p in range(1, self.K):
-            prob[:, 2 * p] = prob[:, p] * sig[:, p - 1]
-            prob[:, 2 * p + 1] = prob[:, p] * (1.0 - sig[:, p - 1])
-        g = prob[:, self.K:2 * self.K]
-        mu = torch.zeros((n, 2 * self.K), dtype=torch.float64, device=A.device)
-        mu[:, self.K:] = g * H
-        for p in range(self.K - 1, 0, -1):
-            mu[:, p] = mu[:, 2 * p] + mu[:, 2 * p + 1]
-        return g, H, mu, sig
+        leaves = w[:self.K] if self.expert_kind == "scalar" else None
+        return gbst_mixture(A, self.K, self.gate_kind, self.expert_kind, leaves)
 
     def _forward(self, X, d, z, w, g_out, train: bool):
         fmask = self.fmask
