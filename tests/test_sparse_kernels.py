@@ -1,0 +1,138 @@
+"""Sparse products (segmented SpMV/SpMM, CSC chunk reduce) and FFM pair kernels:
+CPU torch path vs a dense fp64 reference, and the HIP kernels vs the CPU path."""
+import numpy as np
+import pytest
+import torch
+
+from ytk_learn_amd.ops.ffm import ffm_backward, ffm_forward
+from ytk_learn_amd.ops.sparse import CHUNK, SparseMatrix
+
+
+def _rand_csr(n, F, avg, seed=0, bias=True):
+    g = np.random.default_rng(seed)
+    rows, cols, vals = [], [], []
+    for r in range(n):
+        k = int(g.integers(1, 2 * avg))
+        c = np.unique(g.integers(1 if bias else 0, F, size=k))
+        rows += [r] * len(c)
+        cols += c.tolist()
+        vals += g.normal(size=len(c)).tolist()
+        if bias:
+            rows.append(r); cols.append(0); vals.append(1.0)
+    rows, cols, vals = np.array(rows), np.array(cols), np.array(vals, np.float32)
+    o = np.lexsort((cols, rows))
+    rows, cols, vals = rows[o], cols[o], vals[o]
+    indptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(rows, minlength=n), out=indptr[1:])
+    dense = np.zeros((n, F), np.float64)
+    dense[rows, cols] = vals
+    return torch.from_numpy(indptr), torch.from_numpy(cols.astype(np.int32)), torch.from_numpy(vals), dense
+
+
+def test_spmm_cpu_matches_dense():
+    n, F = 3000, 50
+    ip, ix, vv, D = _rand_csr(n, F, 6)
+    X = SparseMatrix(ip, ix, vv, F)
+    g = torch.Generator().manual_seed(1)
+    w = torch.randn(F, generator=g)
+    W = torch.randn((F, 5), generator=g)
+    d = torch.randn(n, generator=g)
+    Dm = torch.randn((n, 5), generator=g)
+    np.testing.assert_allclose(X.matmul(w).numpy(), D @ w.double().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(X.matmul(W).numpy(), D @ W.double().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(X.t_matmul(d).numpy(), D.T @ d.double().numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(X.t_matmul(Dm).numpy(), D.T @ Dm.double().numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(X.t_matmul(d, square=True).numpy(), (D * D).T @ d.double().numpy(), rtol=1e-4,
+                               atol=1e-3)
+    # the bias column spans several CSC chunks
+    assert n > CHUNK // 2 or X.n_chunks >= F
+
+
+def _pairs_dense(ip, ix, vv, fl, V, nf, k):
+    """fp64 reference of the FFM pair sum per row."""
+    V3 = V.double().view(-1, nf, k)
+    out = torch.zeros(ip.shape[0] - 1, dtype=torch.float64)
+    for r in range(ip.shape[0] - 1):
+        a, b = int(ip[r]), int(ip[r + 1])
+        for p in range(a, b):
+            for q in range(p + 1, b):
+                out[r] += (V3[ix[p], fl[q]] * V3[ix[q], fl[p]]).sum() * float(vv[p]) * float(vv[q])
+    return out
+
+
+def test_ffm_cpu_matches_loops():
+    n, F, nf, k = 40, 20, 4, 4
+    ip, ix, vv, _ = _rand_csr(n, F, 5, seed=3)
+    g = torch.Generator().manual_seed(2)
+    fl = torch.randint(0, nf, (ix.shape[0],), generator=g, dtype=torch.int32)
+    V = torch.randn(F * nf * k, generator=g) * 0.3
+    fx = ffm_forward(ip, ix, vv, fl, V, nf, k)
+    np.testing.assert_allclose(fx.numpy(), _pairs_dense(ip, ix, vv, fl, V, nf, k).numpy(), rtol=1e-4, atol=1e-5)
+    # gradient vs autograd of the dense formulation
+    Vg = V.clone().double().requires_grad_(True)
+    c = torch.randn(n, generator=g)
+    tot = (_pairs_dense_t(ip, ix, vv, fl, Vg, nf, k) * c.double()).sum()
+    tot.backward()
+    gV = torch.zeros_like(V)
+    ffm_backward(ip, ix, vv, fl, V, nf, k, c, gV)
+    np.testing.assert_allclose(gV.numpy(), Vg.grad.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _pairs_dense_t(ip, ix, vv, fl, V, nf, k):
+    V3 = V.view(-1, nf, k)
+    outs = []
+    for r in range(ip.shape[0] - 1):
+        a, b = int(ip[r]), int(ip[r + 1])
+        s = torch.zeros((), dtype=V.dtype)
+        for p in range(a, b):
+            for q in range(p + 1, b):
+                s = s + (V3[ix[p], fl[q]] * V3[ix[q], fl[p]]).sum() * float(vv[p]) * float(vv[q])
+        outs.append(s)
+    return torch.stack(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("J", [1, 3, 16, 31, 70])
+def test_spmm_gpu_matches_cpu(cuda, J):
+    n, F = 20000, 300
+    ip, ix, vv, _ = _rand_csr(n, F, 12, seed=J)
+    Xc = SparseMatrix(ip, ix, vv, F)
+    Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    g = torch.Generator().manual_seed(5)
+    W = torch.randn((F, J), generator=g) if J > 1 else torch.randn(F, generator=g)
+    Dm = torch.randn((n, J), generator=g) if J > 1 else torch.randn(n, generator=g)
+    torch.testing.assert_close(Xg.matmul(W.to(cuda)).cpu(), Xc.matmul(W), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(Xg.matmul(W.to(cuda), square=True).cpu(), Xc.matmul(W, square=True),
+                               rtol=1e-5, atol=1e-4)
+    tg = Xg.t_matmul(Dm.to(cuda))
+    torch.testing.assert_close(tg.cpu(), Xc.t_matmul(Dm), rtol=1e-4, atol=2e-3)
+    # deterministic: identical bits on a second run
+    assert torch.equal(Xg.t_matmul(Dm.to(cuda)), tg)
+    # accumulate / alpha
+    out = torch.ones_like(tg)
+    Xg.t_matmul(Dm.to(cuda), out=out, alpha=2.0, accumulate=True)
+    torch.testing.assert_close(out, 1.0 + 2.0 * tg, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(4, 12), (3, 8), (8, 70)])
+def test_ffm_gpu_matches_cpu(cuda, k, m):
+    n, F, nf = 3000, 400, 7
+    ip, ix, vv, _ = _rand_csr(n, F, m, seed=k)
+    g = torch.Generator().manual_seed(9)
+    fl = torch.randint(0, nf, (ix.shape[0],), generator=g, dtype=torch.int32)
+    V = torch.randn(F * nf * k, generator=g) * 0.2
+    c = torch.randn(n, generator=g)
+    fx_c = ffm_forward(ip, ix, vv, fl, V, nf, k)
+    fx_g = ffm_forward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k)
+    torch.testing.assert_close(fx_g.cpu(), fx_c, rtol=1e-4, atol=1e-4)
+    gc = torch.zeros_like(V)
+    ffm_backward(ip, ix, vv, fl, V, nf, k, c, gc)
+    gg = torch.zeros_like(V).to(cuda)
+    ffm_backward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gg)
+    torch.testing.assert_close(gg.cpu(), gc, rtol=1e-3, atol=1e-3)
+    # misaligned V (linear weights in front, as inside the model vector)
+    big = torch.zeros(V.numel() + 3).to(cuda)
+    big[3:] = V.to(cuda)
+    fx_m = ffm_forward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), big[3:], nf, k)
+    torch.testing.assert_close(fx_m.cpu(), fx_c, rtol=1e-4, atol=1e-4)
