@@ -140,8 +140,8 @@ def main():
                 "rounds_timed": a.steps,
                 "device": str(dev),
             },
-            "train_loss": round(float(tr.last_train_loss), 6),
-            "test_loss": round(float(tr.last_test_loss), 6),
+            "train_loss": round(float(train_loss), 6),
+            "test_loss": round(float(test_loss), 6),
             "test_auc": round(float(auc), 6),
             "prep_s": round(prep_s, 3),
             "datagen_s": round(gen_s, 3),

@@ -1,0 +1,117 @@
+"""Worker script for the multi-process tests (launched by torch.distributed.run).
+
+usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+           --master-port P tests/dist_worker.py TASK OUT_DIR DEVICE
+TASK: gbdt | gbdt_loss | linear | gbst | comm. Each task writes rank-0 results to OUT_DIR.
+Row sharding: rank r takes rows r, r+N, ... of one fixed synthetic dataset, so any world
+size sees the same global data.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("YTK_QUIET", "1")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ytk_learn_amd.parallel.comm import Comm  # noqa: E402
+
+
+def gbdt_data(n, F, seed, rank, world, device):
+    g = np.random.default_rng(seed)
+    X = g.integers(0, 40, size=(n, F)).astype(np.float32)  # < max_cnt distinct -> exact bins
+    X[g.random((n, F)) < 0.05] = np.nan
+    z = np.nansum(X[:, :4], axis=1) / 40.0 - 2.0 + 0.3 * g.normal(size=n)
+    y = (z > 0).astype(np.float32)[:, None]
+    sl = slice(rank, n, world)
+    return torch.from_numpy(X[sl]).to(device), torch.from_numpy(y[sl]).to(device)
+
+
+def run_gbdt(comm, out, device, policy):
+    from ytk_learn_amd.models.gbdt.builder import TreeParams
+    from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer
+    X, y = gbdt_data(20000, 10, 7, comm.rank, comm.world, device)
+    Xt, yt = gbdt_data(4000, 10, 8, comm.rank, comm.world, device)
+    tp = TreeParams(max_depth=5 if policy == "level" else -1, max_leaf_cnt=32 if policy == "level" else 20,
+                    min_child_hessian_sum=1.0, learning_rate=0.2, l2=1.0, grow_policy=policy)
+    p = GBDTParams(round_num=6, loss_function="sigmoid", missing_value="value@0",
+                   approximate=[{"cols": "default", "type": "sample_by_quantile", "max_cnt": 255}], tree=tp)
+    tr = GBDTTrainer(p, GBDTData(X, y), GBDTData(Xt, yt), comm=comm)
+    model = tr.train()
+    tl, te = tr._losses()
+    if comm.rank == 0:
+        with open(os.path.join(out, "model.txt"), "w") as f:
+            f.write(model.dumps())
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump({"train_loss": tl, "test_loss": te}, f)
+
+
+def write_lines(path, n, seed):
+    w = np.random.default_rng(99).normal(size=30)
+    g = np.random.default_rng(seed)
+    with open(path, "w") as f:
+        for _ in range(n):
+            idx = np.unique(g.integers(0, 30, size=6))
+            v = g.random(len(idx))
+            y = int((w[idx] * v).sum() > 0)
+            f.write("1###%d###%s\n" % (y, ",".join(f"x{i}:{x:.4f}" for i, x in zip(idx, v))))
+
+
+def run_linear(comm, out, device, model_name):
+    from ytk_learn_amd.config.hocon import parse_file
+    from ytk_learn_amd.train import train
+    tr_path, te_path = os.path.join(out, "train.txt"), os.path.join(out, "test.txt")
+    if comm.rank == 0 and not os.path.exists(tr_path):
+        write_lines(tr_path, 4000, 1)
+        write_lines(te_path, 1000, 2)
+    comm.barrier()
+    cfg = parse_file(os.path.join(ROOT, "config", "model", f"{model_name}.conf")).with_overrides({
+        "data.train.data_path": tr_path, "data.test.data_path": te_path,
+        "model.data_path": os.path.join(out, f"{model_name}_w{comm.world}.model"),
+        "optimization.line_search.lbfgs.convergence.max_iter": 10, "k": 4 if model_name != "fm" else [1, 4],
+        "tree_num": 2})
+    res = train(model_name, cfg, comm=comm)
+    if comm.rank == 0:
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump({"loss": res.loss, "test_loss": res.test_loss}, f)
+
+
+def run_comm(comm, out, device):
+    t = torch.full((4,), float(comm.rank + 1), device=device)
+    comm.allreduce_(t)
+    m = comm.allreduce(torch.tensor([float(comm.rank)], device=device), op="max")
+    g = comm.allgather(torch.tensor([comm.rank], device=device))
+    o = comm.allreduce_object({f"k{comm.rank}": 1, "shared": 2}, lambda a, b: {k: a.get(k, 0) + b.get(k, 0)
+                                                                               for k in set(a) | set(b)})
+    rs = torch.empty(2, device=device)
+    comm.reduce_scatter_(rs, torch.arange(2 * comm.world, dtype=torch.float32, device=device))
+    if comm.rank == 0:
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump({"sum": t.tolist(), "max": m.tolist(), "gather": g.tolist(), "obj": o,
+                       "rs": rs.tolist(), "range": list(comm.shard_range(10))}, f)
+
+
+def main():
+    task, out, device = sys.argv[1], sys.argv[2], sys.argv[3]
+    comm = Comm.from_env(device)
+    dev = comm.device
+    try:
+        if task == "gbdt":
+            run_gbdt(comm, out, dev, "level")
+        elif task == "gbdt_loss":
+            run_gbdt(comm, out, dev, "loss")
+        elif task in ("linear", "fm", "gbmlr", "gbhsdt"):
+            run_linear(comm, out, dev, task)
+        elif task == "comm":
+            run_comm(comm, out, dev)
+        else:
+            raise SystemExit(f"unknown task {task}")
+    finally:
+        comm.close()
+
+
+if __name__ == "__main__":
+    main()

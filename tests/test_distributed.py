@@ -1,0 +1,84 @@
+"""Multi-process tests of the distributed paths (torch.distributed.run, 127.0.0.1).
+
+CPU: gloo, world 1 vs world 2 -- GBDT must produce the IDENTICAL model text (exact int64
+histograms, feature-ownership-free all-reduce), L-BFGS models must reach the same loss.
+GPU (@gpu): two ranks share the one GPU of the test box over gloo (YTK_DIST_BACKEND=gloo),
+exercising the GPU-resident level builder's collectives (root count, max |g|/|h|, per-level
+left counts and histogram slabs) -- RCCL itself needs one GPU per rank.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(task, out, world, device="cpu", timeout=600, extra_env=None):
+    os.makedirs(out, exist_ok=True)
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    env["OMP_NUM_THREADS"] = "2"
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, task, str(out), device]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    with open(os.path.join(out, "res.json")) as f:
+        return json.load(f)
+
+
+def test_comm_collectives_gloo(tmp_path):
+    res = _run("comm", tmp_path, 2)
+    assert res["sum"] == [3.0] * 4
+    assert res["max"] == [1.0]
+    assert res["gather"] == [0, 1]
+    assert res["obj"] == {"k0": 1, "k1": 1, "shared": 4}
+    assert res["rs"] == [0.0, 2.0]  # rank 0 gets elements [0, 2) summed over 2 ranks
+    assert res["range"] == [0, 5]
+
+
+@pytest.mark.parametrize("task", ["gbdt", "gbdt_loss"])
+def test_gbdt_world2_identical_to_world1(tmp_path, task):
+    r1 = _run(task, tmp_path / "w1", 1)
+    r2 = _run(task, tmp_path / "w2", 2)
+    m1 = open(tmp_path / "w1" / "model.txt").read()
+    m2 = open(tmp_path / "w2" / "model.txt").read()
+    assert m1 == m2
+    np.testing.assert_allclose(r2["train_loss"], r1["train_loss"], rtol=1e-9)
+    np.testing.assert_allclose(r2["test_loss"], r1["test_loss"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("task", ["linear", "gbmlr"])
+def test_lbfgs_world2_matches_world1(tmp_path, task):
+    r1 = _run(task, tmp_path / "w1", 1)
+    r2 = _run(task, tmp_path / "w2", 2)
+    np.testing.assert_allclose(r2["loss"], r1["loss"], rtol=1e-4)
+    np.testing.assert_allclose(r2["test_loss"], r1["test_loss"], rtol=1e-3)
+    if task == "linear":
+        parts = os.listdir(tmp_path / "w2" / "linear_w2.model")
+        assert sorted(parts) == ["model-00000", "model-00001"]  # each rank dumps its feature range
+
+
+@pytest.mark.gpu
+def test_gpu_level_builder_two_ranks_one_gpu(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_DIST_BACKEND": "gloo"}
+    _run("gbdt", tmp_path / "w1", 1, "cuda", extra_env=env)
+    _run("gbdt", tmp_path / "w2", 2, "cuda", extra_env=env)
+    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / "w2" / "model.txt").read()

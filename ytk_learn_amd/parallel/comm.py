@@ -56,23 +56,26 @@ class Comm:
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         if device == "cuda":
-            torch.cuda.set_device(local_rank)
-            dev = torch.device("cuda", local_rank)
+            idx = local_rank % max(1, torch.cuda.device_count())  # >1 rank per GPU only with gloo
+            torch.cuda.set_device(idx)
+            dev = torch.device("cuda", idx)
         else:
             dev = torch.device("cpu")
         if world <= 1:
             return cls(0, 1, dev)
+        # YTK_DIST_BACKEND=gloo forces gloo even for GPU tensors: lets several ranks share ONE
+        # GPU to rehearse the multi-GPU code paths (RCCL needs one GPU per rank).
+        backend = os.environ.get("YTK_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            backend = "nccl" if dev.type == "cuda" else "gloo"
             kw = {}
-            if dev.type == "cuda":
+            if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         group = dist.group.WORLD
         cpu_group = group
-        if dev.type == "cuda":
+        if dev.type == "cuda" and backend == "nccl":
             cpu_group = dist.new_group(backend="gloo")
         return cls(dist.get_rank(), dist.get_world_size(), dev, group, cpu_group)
 
