@@ -12,6 +12,8 @@ extern "C" {
 // gbdt_hist.hip
 void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
                  float, float, uintptr_t, uintptr_t, uintptr_t);
+void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
+                        int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip
@@ -56,6 +58,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.doc() = "ytk-learn-amd HIP kernels (gfx950)";
   m.def("hist_fx", &ytk_hist_fx);
   m.def("hist_fx_global", &ytk_hist_fx_global);
+  m.def("hist_fx_staged", &ytk_hist_fx_staged);
   m.def("split_find", &ytk_split_find);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);

@@ -33,7 +33,8 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const uint8_t* __restrict__ bins, long long stride, int F,
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B, int nb_lds,
-    float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev) {
+    float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
+    long long* __restrict__ staging) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];
   unsigned long long* lg = sm64;
   unsigned long long* lh = sm64 + nb_lds * 32;
@@ -87,8 +88,27 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   }
   __syncthreads();
 
+  if (staging) {
+    // two-stage flush: plain 16-B stores of this block's partial (g, h) pairs; the slot
+    // sums are formed by hist_reduce_kernel. Global u64 atomics execute at the memory
+    // side at ~1.3 TB/s chip-wide, which made the atomic flush the floor of every
+    // launch (~45 us per level at 256 blocks); stores + one ordered read are ~4x cheaper.
+    const int E = nb_lds * 32;
+    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)blockIdx.x * gridDim.y + fg) * E;
+    for (int i = tid; i < E; i += kHistThreads) st[i] = make_longlong2((long long)lg[i], (long long)lh[i]);
+    return;
+  }
   long long* out = hist + (size_t)w.x * B * F * 2;
-  for (int i = tid; i < nb_lds * 32; i += kHistThreads) {
+  // Flush order rotated per block: every block of a level flushes into the SAME few
+  // thousand addresses at about the same time; starting each block at a different
+  // 1024-entry tile spreads the global atomics over the L2 channels instead of
+  // serialising hundreds of blocks on one address at a time.
+  const int E = nb_lds * 32;
+  const int ntile = (E + kHistThreads - 1) / kHistThreads;
+  const int rot = (int)(blockIdx.x % (unsigned)ntile);
+  for (int t = 0; t < ntile; ++t) {
+    const int i = ((t + rot) % ntile) * kHistThreads + tid;
+    if (i >= E) continue;
     const int bin = i >> 5, l = i & 31, ff = fg * 32 + l;
     if (ff < F) {
       const unsigned long long g = lg[i], h = lh[i];
@@ -98,6 +118,62 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
         atomicAdd(o + 1, h);
       }
     }
+  }
+}
+
+// Second stage of the staged flush: hist[slot][bin][f] = sum over the work items of that
+// slot of their block partials. One thread per (entry, slot, feature group); the items of
+// the slot are collected into LDS first (<= 1024 items per level). Integer sums: exact and
+// order independent. Every slot in [slot_base, slot_base + nslots) is written (zero when
+// it has no items), so the built half of a level needs no zero fill.
+// Split-K over the slot's items (blockIdx.z of kReduceSplit): each block sums a strided
+// subset of the items with 8 independent 16-B loads in flight per thread and adds its
+// partial with one int64 atomic per value (exact; kReduceSplit-way contention only).
+// The slots must be zero on entry.
+constexpr int kReduceSplit = 8;
+
+__global__ __launch_bounds__(256) void hist_reduce_kernel(
+    const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
+    const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
+    int groups, int slot_base) {
+  __shared__ int s_sel[1024];
+  __shared__ int s_n;
+  const int n = nwork_dev ? min(*nwork_dev, nwork) : nwork;
+  const int slot = slot_base + (int)blockIdx.y / groups;
+  const int fg = (int)blockIdx.y % groups;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += blockDim.x)
+    if (work[k].x == slot) {
+      const int p = atomicAdd(&s_n, 1);
+      if (p < 1024) s_sel[p] = k;
+    }
+  __syncthreads();
+  const int cnt = min(s_n, 1024);
+  const int E = nb_lds * 32;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E || cnt == 0) return;
+  const int bin = i >> 5, ff = fg * 32 + (i & 31);
+  if (ff >= F || bin >= B) return;
+  const longlong2* st = reinterpret_cast<const longlong2*>(staging);
+  long long g = 0, h = 0;
+  int t = (int)blockIdx.z;
+  for (; t + 7 * kReduceSplit < cnt; t += 8 * kReduceSplit) {
+    longlong2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)s_sel[t + u * kReduceSplit] * groups + fg) * E + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
+  }
+  for (; t < cnt; t += kReduceSplit) {
+    const longlong2 v = st[((size_t)s_sel[t] * groups + fg) * E + i];
+    g += v.x;
+    h += v.y;
+  }
+  if (g | h) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(hist + (((size_t)slot * B + bin) * F + ff) * 2);
+    atomicAdd(o, (unsigned long long)g);
+    atomicAdd(o + 1, (unsigned long long)h);
   }
 }
 
@@ -144,13 +220,44 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
     hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr);
   } else {
     hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr);
   }
+  YTK_LAUNCH_CHECK();
+}
+
+// Staged variant: block partials to ``staging`` (>= nwork * groups * B * 32 * 16 bytes),
+// then accumulated into the slots [slot_base, slot_base + nslots), which must be zero.
+void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
+                        uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
+                        uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
+                        int slot_base, int nslots, uintptr_t stream) {
+  if (nwork <= 0 || nslots <= 0) return;
+  const int groups = (F + 31) / 32;
+  const int nb_lds = B;
+  const size_t lds = (size_t)nb_lds * 64 * sizeof(unsigned long long);
+  dim3 grid(nwork, groups);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
+                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
+                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging);
+  } else {
+    hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
+                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging);
+  }
+  YTK_LAUNCH_CHECK();
+  const int E = nb_lds * 32;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
+                     (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
+                     (long long*)hist, B, F, nb_lds, groups, slot_base);
   YTK_LAUNCH_CHECK();
 }
 

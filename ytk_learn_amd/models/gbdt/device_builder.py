@@ -15,6 +15,8 @@ built (smaller) children in the first half, derived children in the second.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -68,9 +70,9 @@ class DeviceTree:
 
 
 class DeviceLevelBuilder:
-    HIST_TARGET = 512   # 1 block/CU (128 KiB LDS) x 256 CUs x 2
+    HIST_TARGET = int(os.environ.get("YTK_HIST_TARGET", 256))  # 1 block per CU (128 KiB LDS each)
     PART_TARGET = 1024
-    MIN_ROWS = 2048
+    MIN_ROWS = int(os.environ.get("YTK_HIST_MIN_ROWS", 2048))
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Comm = None):
@@ -114,8 +116,13 @@ class DeviceLevelBuilder:
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
         self.n_slots = (1 << D) - 1
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
-        # one fill per tree beats one per level while the slab is small; deep trees zero
-        # only the built half of each level (the derived half is written by split_find)
+        # staged histogram flush: block partials to a staging slab with plain stores, then a
+        # split-K slot reduce (8 int64 atomics per value instead of one per block)
+        groups = (F + 31) // 32
+        max_hist_items = self.HIST_TARGET + (self.maxp // 2) + 2
+        self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0"
+        self.staging = (torch.empty(max_hist_items * groups * B * 32 * 2, dtype=torch.int64, device=dev)
+                        if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=dev)
@@ -221,13 +228,22 @@ class DeviceLevelBuilder:
         st_ptr = self.st.data_ptr()
         off = lambda w: st_ptr + 4 * w
         h.lv_step(0, ptrs, ip, fp, 0, 0, s)
-        if self._zero_all:
-            self.hist.zero_()  # every slot of the tree in one fill (small slabs)
-        else:
-            self.hist[0:1].zero_()
-        h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh0, rows0,
-                  ptr(self.hist_items), self.HIST_TARGET + 1, ptr(self.hist), self.B, 1.0, 1.0,
-                  off(5), ptr(self.scales), s)
+
+        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots):
+            if self._zero_all:
+                if slot_base == 0:
+                    self.hist.zero_()  # every slot of the tree in one fill (small slabs)
+            else:
+                self.hist[slot_base:slot_base + nslots].zero_()
+            if self.staged:
+                h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
+                                 ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5),
+                                 ptr(self.scales), ptr(self.staging), slot_base, nslots, s)
+                return
+            h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
+                      nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
+
+        build_hist(gh0, rows0, self.HIST_TARGET + 1, 0, 1)
         if dist:
             self.comm.allreduce_(self.hist[0:1])
         gp = self.gp
@@ -263,11 +279,7 @@ class DeviceLevelBuilder:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
-            if not self._zero_all:
-                self.hist[base:base + half].zero_()
-            h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, ptr(self.ghp), ptr(self.rows),
-                      ptr(self.hist_items), self.HIST_TARGET + half + 1, ptr(self.hist), self.B, 1.0, 1.0,
-                      off(5), ptr(self.scales), s)
+            build_hist(ptr(self.ghp), ptr(self.rows), self.HIST_TARGET + half + 1, base, half)
             if dist:
                 self.comm.allreduce_(self.hist[base:base + half])
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
