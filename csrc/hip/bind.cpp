@@ -18,7 +18,8 @@ void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, ui
                         uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
-                    float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t);
+                    float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
+                    uintptr_t, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,

@@ -88,16 +88,25 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
 // hist: int64 [slot][B][F][2]. items[blk] = {slot, parent_slot, sibling_slot, derived}
 constexpr int kSplitWaves = 8;  // 512 threads: 3-4 features per wave at F=28 (latency bound)
 
+// Grid (items, feature groups): block y owns features y*kSplitWaves + wave (one wave per
+// feature when F <= groups*8), so a level's nodes fill many CUs instead of one block each
+// walking ~F/8 features serially. With more than one group, every block writes its best
+// candidate to part[item][group]; the last block of an item (device-scope counter)
+// combines them with the same lexicographic tie-break and resets the counter.
 __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
-    const double* __restrict__ inv_dev) {
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters) {
   __shared__ float s_chg[kSplitWaves];
   __shared__ int s_feat[kSplitWaves], s_a[kSplitWaves], s_b[kSplitWaves];
   __shared__ double s_gl[kSplitWaves], s_hl[kSplitWaves];
+  __shared__ int s_last;
 
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
+  const int ngroups = (int)gridDim.y;
+  const int fstart = (int)blockIdx.y * kSplitWaves;
+  const int fstep = ngroups * kSplitWaves;
   if (inv_dev) {
     gp.inv_sg = inv_dev[0];
     gp.inv_sh = inv_dev[1];
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
   int best_f = 0x7fffffff, best_a = -1, best_b = 0x7fffffff;
   double best_gl = 0.0, best_hl = 0.0;
 
-  for (int f = wid; f < F; f += kSplitWaves) {
+  for (int f = fstart + wid; f < F; f += fstep) {
     if (!fmask[f]) continue;
     const int nb = nbins_f[f];
     long long carry_g = 0, carry_h = 0;
@@ -217,14 +226,38 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
       if (better(s_chg[w2], s_feat[w2], s_b[w2], s_chg[bw], s_feat[bw], s_b[bw])) bw = w2;
     SplitOut o;
     o.loss_chg = s_chg[bw];
-    o.feat = (s_feat[bw] == 0x7fffffff) ? -1 : s_feat[bw];
+    o.feat = s_feat[bw];  // 0x7fffffff = none (mapped to -1 below)
     o.bin_a = s_a[bw];
-    o.bin_b = (s_b[bw] == 0x7fffffff) ? -1 : s_b[bw];
+    o.bin_b = s_b[bw];
     o.gl = s_gl[bw];
     o.hl = s_hl[bw];
     o.g = G;
     o.h = H;
-    out[blockIdx.x] = o;
+    s_last = 1;
+    if (ngroups > 1) {
+      part[(size_t)blockIdx.x * ngroups + blockIdx.y] = o;
+      __threadfence();
+      const int prev = atomicAdd(&counters[blockIdx.x], 1);
+      s_last = (prev == ngroups - 1);
+      if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see the other groups' parts
+        counters[blockIdx.x] = 0;
+        const volatile SplitOut* pp = part + (size_t)blockIdx.x * ngroups;
+        for (int y = 0; y < ngroups; ++y) {
+          const float c = pp[y].loss_chg;
+          const int f = pp[y].feat, b = pp[y].bin_b;
+          if (y == 0 || better(c, f, b, o.loss_chg, o.feat, o.bin_b)) {
+            o.loss_chg = c; o.feat = f; o.bin_a = pp[y].bin_a; o.bin_b = b;
+            o.gl = pp[y].gl; o.hl = pp[y].hl;
+          }
+        }
+      }
+    }
+    if (s_last) {
+      if (o.feat == 0x7fffffff) o.feat = -1;
+      if (o.bin_b == 0x7fffffff) o.bin_b = -1;
+      out[blockIdx.x] = o;
+    }
   }
 }
 
@@ -232,16 +265,20 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
 
 using namespace ytk;
 
+// part / counters (optional): scratch of nitems * ceil(F/8) SplitOut and nitems zeroed ints;
+// when given, the features of a node are spread over ceil(F/8) blocks.
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
                                int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
                                float l1, float l2, float max_abs_leaf, double inv_sg,
                                double inv_sh, uintptr_t nitems_dev, uintptr_t inv_dev,
-                               uintptr_t stream) {
+                               uintptr_t part, uintptr_t counters, uintptr_t stream) {
   if (nitems <= 0) return;
   GainParams gp{mcw, l1, l2, max_abs_leaf, inv_sg, inv_sh};
-  hipLaunchKernelGGL(split_find_kernel, dim3(nitems), dim3(kSplitWaves * 64), 0,
+  const int groups = (part && counters) ? (F + kSplitWaves - 1) / kSplitWaves : 1;
+  hipLaunchKernelGGL(split_find_kernel, dim3(nitems, groups), dim3(kSplitWaves * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
-                     (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev);
+                     (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev,
+                     (SplitOut*)part, (int*)counters);
   YTK_LAUNCH_CHECK();
 }

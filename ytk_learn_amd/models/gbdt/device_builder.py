@@ -113,6 +113,10 @@ class DeviceLevelBuilder:
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)
         self.split_out = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
+        # split_find spreads a node's features over ceil(F/8) blocks: per-group candidates +
+        # per-item arrival counters (reset by the combining block)
+        self.split_part = torch.zeros(2 * self.maxp * ((F + 7) // 8) * 48, dtype=torch.uint8, device=dev)
+        self.split_cnt = torch.zeros(2 * self.maxp, dtype=torch.int32, device=dev)
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
         self.n_slots = (1 << D) - 1
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
@@ -249,7 +253,8 @@ class DeviceLevelBuilder:
         gp = self.gp
         h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                      ptr(self.split_items), 1, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
-                     gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
+                     gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
+                     ptr(self.split_cnt), s)
         bb = 1 if self.bins.dtype == torch.uint8 else 2
         for d in range(p.max_depth):
             c = d + 1  # depth of the children created at this level
@@ -284,7 +289,8 @@ class DeviceLevelBuilder:
                 self.comm.allreduce_(self.hist[base:base + half])
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                          ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
-                         gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), s)
+                         gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
+                         ptr(self.split_cnt), s)
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         self.tree_count += 1
         st, nodes, *arrays = self._snap_views(self.snap.clone())
