@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Secondary benchmark: L-BFGS loss+gradient evaluations of the sparse models on a
+synthetic Criteo-shaped dataset (BASELINE.json configs 4/5: FM k=16, FFM 39 fields k=4,
+45M rows x 1M features at 8 GPUs).
+
+A "step" is one full loss + gradient evaluation over the local rows (the unit of work of
+every L-BFGS line-search step, HoagOptimizer.calcLossAndGrad) INCLUDING the gradient
+all-reduce over RCCL; the L-BFGS/OWL-QN vector algebra of one iteration is timed
+separately (``lbfgs_iter_ms``). Data-parallel weak scaling: --rows is per GPU.
+
+  python bench_sparse.py --model fm --rows 4000000 --steps 10
+  python -m torch.distributed.run --nproc-per-node 8 ... bench_sparse.py --model ffm
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+from ytk_learn_amd.config.params import CommonParams, LineSearchParams  # noqa: E402
+from ytk_learn_amd.data.dataflow import SparseData  # noqa: E402
+from ytk_learn_amd.data.synthetic import criteo_like  # noqa: E402
+from ytk_learn_amd.models.continuous.base import LoadedData  # noqa: E402
+from ytk_learn_amd.optim.lbfgs import HoagOptimizer  # noqa: E402
+from ytk_learn_amd.parallel.comm import Comm  # noqa: E402
+from ytk_learn_amd.utils.logging import YtkLogger  # noqa: E402
+
+
+class _Names(list):
+    """Lazy 'f<i>' feature names (the model only indexes them at dump time)."""
+
+    def __init__(self, n):
+        super().__init__()
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return f"f{i}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="fm", choices=["linear", "fm", "ffm"])
+    ap.add_argument("--rows", type=int, default=4_000_000, help="rows per GPU")
+    ap.add_argument("--features", type=int, default=1_000_000)
+    ap.add_argument("--fields", type=int, default=39)
+    ap.add_argument("--k", type=int, default=0, help="latent dim (default fm 16, ffm 4)")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    comm = Comm.from_env()
+    dev = comm.device
+    k = a.k or (16 if a.model == "fm" else 4)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    indptr, idx, vals, fields, y = criteo_like(a.rows, a.fields, a.features, seed=11 + comm.rank, device=dev)
+    F = a.fields * max(1, a.features // a.fields) + 1  # + bias column 0
+    idx = idx + 1
+    n = a.rows
+    # append the bias (index 0) to every row
+    ip2 = indptr + torch.arange(n + 1, device=dev, dtype=torch.int64)
+    nnz = idx.numel() + n
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), indptr[1:] - indptr[:-1])
+    pos = torch.arange(idx.numel(), device=dev, dtype=torch.int64) + rows  # shift by row index
+    idx2 = torch.zeros(nnz, dtype=torch.int32, device=dev)
+    val2 = torch.ones(nnz, dtype=torch.float32, device=dev)
+    fld2 = torch.zeros(nnz, dtype=torch.int32, device=dev)
+    idx2[pos] = idx
+    val2[pos] = vals
+    fld2[pos] = fields + 1
+    del idx, vals, fields, rows, pos
+    w = torch.ones(n, dtype=torch.float32, device=dev)
+    tot = comm.allreduce_scalars([float(n)])[0]
+    data = SparseData(ip2, idx2, val2, y, w, fld2 if a.model == "ffm" else None, None, tot, tot, float(n))
+    params = CommonParams()
+    params.loss.loss_function = "sigmoid"
+    params.loss.evaluate_metric = []
+    params.model.need_bias = True
+    params.model.data_path = "/tmp/ytk_bench_sparse_model"
+    params.extra = {"k": [1, k], "bias_need_latent_factor": False}
+    log = YtkLogger(comm.rank, stream=sys.stderr)
+    log.quiet = True
+    loaded = LoadedData(data, None, _Names(F), {}, ["_bias_"] + [f"c{i}" for i in range(a.fields)])
+    t0 = time.perf_counter()
+    if a.model == "linear":
+        from ytk_learn_amd.models.continuous.linear import LinearModel
+        model = LinearModel(params, loaded, comm, log)
+    elif a.model == "fm":
+        from ytk_learn_amd.models.continuous.fm import FMModel
+        model = FMModel(params, loaded, comm, log)
+    else:
+        from ytk_learn_amd.models.continuous.ffm import FFMModel
+        model = FFMModel(params, loaded, comm, log)
+    setup_s = time.perf_counter() - t0
+    opt = HoagOptimizer(model, LineSearchParams(m=12), [0.0] * model.ngroups if hasattr(model, "ngroups") else [0.0],
+                        [1e-6] * (model.ngroups if hasattr(model, "ngroups") else 1), comm, log, tot)
+    g = torch.zeros_like(model.w)
+    for _ in range(a.warmup):
+        opt.loss_and_grad(model.w, g)
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    loss = 0.0
+    for _ in range(a.steps):
+        _, loss = opt.loss_and_grad(model.w, g)
+    sync()
+    comm.barrier()
+    el = time.perf_counter() - t0
+    el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+    # one L-BFGS two-loop + direction update (history full: m pairs)
+    m = 12
+    S = torch.randn((m, model.w.numel()), device=dev) * 1e-3
+    Y = torch.randn((m, model.w.numel()), device=dev) * 1e-3
+    opt.S, opt.Y, opt.YS = S, Y, [1.0] * m
+    p = -g
+    sync()
+    t1 = time.perf_counter()
+    opt.hv(p, 0, m, 1.0, 1.0)
+    sync()
+    hv_ms = (time.perf_counter() - t1) * 1000
+    ms = 1000.0 * el / a.steps
+    if comm.rank == 0:
+        print(json.dumps({
+            "metric": f"{a.model} L-BFGS loss+grad evaluation (criteo-shape, {a.fields} fields, "
+                      f"{a.features} features, k={k})",
+            "value": round(a.rows * comm.world / (el / a.steps), 1), "unit": "rows/s",
+            "ms_per_step": round(ms, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows, "dim": int(model.w.numel()),
+            "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "setup_s": round(setup_s, 2),
+            "scaling": "weak", "dtype": "fp32", "data": "synthetic Criteo-shape", "loss": loss / tot,
+        }), flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()
