@@ -71,9 +71,71 @@ py::dict result_to_dict(ParseResult&& r) {
   return out;
 }
 
+WQSummary summary_from(const py::array_t<double, py::array::c_style | py::array::forcecast>& a) {
+  WQSummary s;
+  if (a.ndim() != 2 || (a.shape(0) > 0 && a.shape(1) != 4))
+    throw std::invalid_argument("summary must be a [n, 4] float64 array (v, rmin, rmax, wmin)");
+  auto r = a.unchecked<2>();
+  s.e.resize((size_t)a.shape(0));
+  for (py::ssize_t i = 0; i < a.shape(0); ++i) s.e[(size_t)i] = {r(i, 0), r(i, 1), r(i, 2), r(i, 3)};
+  return s;
+}
+
+py::array_t<double> summary_to(const WQSummary& s) {
+  py::array_t<double> out({(py::ssize_t)s.e.size(), (py::ssize_t)4});
+  auto w = out.mutable_unchecked<2>();
+  for (size_t i = 0; i < s.e.size(); ++i) {
+    w((py::ssize_t)i, 0) = s.e[i].v;
+    w((py::ssize_t)i, 1) = s.e[i].rmin;
+    w((py::ssize_t)i, 2) = s.e[i].rmax;
+    w((py::ssize_t)i, 3) = s.e[i].wmin;
+  }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_ytk_native, m) {
+  using darr = py::array_t<double, py::array::c_style | py::array::forcecast>;
+  m.def(
+      "wq_build",
+      [](const darr& v, const darr& w, int64_t size) {
+        // sort (value, weight) pairs, build the exact summary, prune to `size` entries
+        const py::ssize_t n = v.size();
+        if (w.size() != n) throw std::invalid_argument("values / weights length mismatch");
+        std::vector<std::pair<double, double>> p((size_t)n);
+        const double* pv = v.data();
+        const double* pw = w.data();
+        for (py::ssize_t i = 0; i < n; ++i) p[(size_t)i] = {pv[i], pw[i]};
+        WQSummary s;
+        {
+          py::gil_scoped_release nogil;
+          std::sort(p.begin(), p.end(),
+                    [](const std::pair<double, double>& a, const std::pair<double, double>& b) {
+                      return a.first < b.first;
+                    });
+          std::vector<double> sv(p.size()), sw(p.size());
+          for (size_t i = 0; i < p.size(); ++i) { sv[i] = p[i].first; sw[i] = p[i].second; }
+          s = WQSummary::from_sorted(sv.data(), sw.data(), sv.size());
+          if (size > 0) s = s.prune((size_t)size);
+        }
+        return summary_to(s);
+      },
+      py::arg("values"), py::arg("weights"), py::arg("size") = 0);
+  m.def("wq_combine", [](const darr& a, const darr& b, int64_t size) {
+    WQSummary s = WQSummary::combine(summary_from(a), summary_from(b));
+    if (size > 0) s = s.prune((size_t)size);
+    return summary_to(s);
+  }, py::arg("a"), py::arg("b"), py::arg("size") = 0);
+  m.def("wq_prune", [](const darr& a, int64_t size) { return summary_to(summary_from(a).prune((size_t)size)); });
+  m.def("wq_query", [](const darr& a, const darr& ranks) {
+    const WQSummary s = summary_from(a);
+    py::array_t<double> out(ranks.size());
+    auto o = out.mutable_unchecked<1>();
+    const double* r = ranks.data();
+    for (py::ssize_t i = 0; i < ranks.size(); ++i) o(i) = s.query(r[i]);
+    return out;
+  });
   m.doc() = "ytk-learn-amd native host runtime";
   m.def("murmur3_128_aslong", [](const std::string& s, uint32_t seed) {
     return murmur3_128_aslong(s.data(), s.size(), seed);

@@ -29,4 +29,17 @@ class JavaRandom {
 // mode 0: nextGaussian*b + a, 1: a + (b-a)*nextDouble, 2: nextFloat, 3: nextDouble
 std::vector<double> java_random_fill(int64_t seed, int64_t n, int mode, double a, double b);
 
+// weighted mergeable quantile summary (wquantile.cpp)
+struct WQSummary {
+  struct Entry {
+    double v, rmin, rmax, wmin;
+  };
+  std::vector<Entry> e;
+  static WQSummary from_sorted(const double* v, const double* w, size_t n);
+  static WQSummary combine(const WQSummary& a, const WQSummary& b);
+  WQSummary prune(size_t size) const;
+  double query(double rank) const;
+  double total() const;
+};
+
 }  // namespace ytk_native

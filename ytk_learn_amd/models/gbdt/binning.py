@@ -106,20 +106,12 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
     if not comm.is_dist:
         out = _weighted_quantile_values(vals, wv, qs)
         return np.unique(out.cpu().numpy().astype(np.float32))
-    # distributed: each rank ships factor*max_cnt weighted summary points
+    # distributed: weighted mergeable summaries with eps = 1 / (bin_factor * max_cnt)
+    # (WeightApproximateQuantile: build locally, all-gather, merge in rank order, query)
+    from ...utils import quantile as wq
     K = spec.quantile_approximate_bin_factor * spec.max_cnt
-    kq = torch.arange(1, K + 1, dtype=torch.float64, device=x.device) / K
-    pts = _weighted_quantile_values(vals, wv, kq)
-    Wl = float(wv.sum())
-    summ = (pts.cpu().numpy().astype(np.float32), np.full(K, Wl / K))
-    parts = comm.allgather_object(summ)
-    pv = np.concatenate([p[0] for p in parts])
-    pw = np.concatenate([p[1] for p in parts])
-    o = np.argsort(pv, kind="stable")
-    pv, pw = pv[o], pw[o]
-    cum = np.cumsum(pw)
-    idx = np.searchsorted(cum, qs.cpu().numpy() * cum[-1], side="left").clip(max=len(pv) - 1)
-    return np.unique(pv[idx])
+    out = wq.distributed_quantiles(vals.double().cpu().numpy(), wv.cpu().numpy(), qs.cpu().numpy(), comm, K)
+    return np.unique(out.astype(np.float32))
 
 
 def _precision_candidates(x, spec: SamplerSpec, comm: Comm) -> np.ndarray:
@@ -228,14 +220,17 @@ def compute_missing_fill(X: torch.Tensor, weight: Optional[torch.Tensor], spec: 
             comm.allreduce_(both)
         s, c = both[0].numpy(), both[1].numpy()
         return np.where(c > 0, s / np.maximum(c, 1e-300), 0.0).astype(np.float32)
+    # quantile (ComputeQuantile): weighted summary per feature, merged across ranks
+    from ...utils import quantile as wq
     out = np.zeros(F, np.float32)
+    local = []
     for f in range(F):
         col = X[:, f]
-        col = col[~torch.isnan(col)]
-        if comm.is_dist:
-            parts = comm.allgather_object(col.cpu().numpy())
-            col = torch.from_numpy(np.concatenate(parts))
-        if col.numel() == 0:
-            continue
-        out[f] = float(torch.quantile(col.double().cpu(), arg))
+        keep = ~torch.isnan(col)
+        local.append(wq.build(col[keep].double().cpu().numpy(), w[keep].double().cpu().numpy(), 4096))
+    parts = comm.allgather_object(local) if comm.is_dist else [local]
+    for f in range(F):
+        s = wq.merge([p[f] for p in parts], 4096)
+        if len(s):
+            out[f] = float(wq.query(s, [arg])[0])
     return out

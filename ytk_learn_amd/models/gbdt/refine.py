@@ -73,18 +73,24 @@ class TreeRefiner:
                 continue
             s, e = bounds[nid]
             v, wt = rv[s:e], wv[s:e]
-            if self.comm.is_dist and self.approximate and v.size > SUMMARY_POINTS:
-                c = np.cumsum(wt)
-                q = (np.arange(1, SUMMARY_POINTS + 1) / SUMMARY_POINTS) * c[-1]
-                j = np.searchsorted(c, q, side="left").clip(max=v.size - 1)
-                v, wt = v[j], np.full(SUMMARY_POINTS, c[-1] / SUMMARY_POINTS)
             local[nid] = (v, wt)
+        summarize = self.comm.is_dist and self.approximate
+        if summarize:
+            # weighted mergeable summaries (WeightApproximateQuantile) instead of raw values
+            from ...utils import quantile as wq
+            local = {nid: wq.build(v, wt, SUMMARY_POINTS) for nid, (v, wt) in local.items()}
         parts = self.comm.allgather_object(local) if self.comm.is_dist else [local]
         for nid in leaves:
-            vs = np.concatenate([p[nid][0] for p in parts])
-            ws = np.concatenate([p[nid][1] for p in parts])
-            if vs.size == 0:
-                continue
-            o = np.argsort(vs, kind="stable")
-            med = _weighted_median_sorted(vs[o], ws[o])
+            if summarize:
+                s = wq.merge([p[nid] for p in parts], SUMMARY_POINTS)
+                if len(s) == 0:
+                    continue
+                med = float(wq.query(s, [0.5])[0])
+            else:
+                vs = np.concatenate([p[nid][0] for p in parts])
+                ws = np.concatenate([p[nid][1] for p in parts])
+                if vs.size == 0:
+                    continue
+                o = np.argsort(vs, kind="stable")
+                med = _weighted_median_sorted(vs[o], ws[o])
             tree.leaf[nid] = float(np.float32(med) * np.float32(lr))
