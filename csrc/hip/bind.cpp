@@ -45,7 +45,10 @@ void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, lo
 void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t);
 // ffm.hip
 void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, int,
-                   uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+                   uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                      uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
+                      int, int, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
@@ -71,6 +74,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("seg_spmm", &ytk_seg_spmm);
   m.def("chunk_reduce", &ytk_chunk_reduce);
   m.def("ffm_pairs", &ytk_ffm_pairs);
+  m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 25 || ip.size() != 6 || fp.size() != 6)

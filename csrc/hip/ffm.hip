@@ -36,7 +36,8 @@ template <bool kBackward>
 __global__ __launch_bounds__(256) void ffm_pairs_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
     const int* __restrict__ fld, long long nrows, const float* __restrict__ V, int nfield, int k,
-    float* __restrict__ fx, const float* __restrict__ coef, float* __restrict__ gV, int vec4) {
+    float* __restrict__ fx, const float* __restrict__ coef, float* __restrict__ gV, int vec4,
+    int skip_feat) {
   const long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
@@ -61,7 +62,10 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
         const int P = pt + pp;
         const int ipb = __shfl(ip, pp, 64), fpb = __shfl(fp, pp, 64);
         const float xpb = __shfl(xp, pp, 64);
-        if (qj < m && qj > P) {
+        // skip_feat: a feature whose latent block is identically zero (the bias without a
+        // latent factor): its pairs contribute nothing, and skipping them removes the
+        // hottest atomic targets (the bias occurs in every row)
+        if (qj < m && qj > P && ipb != skip_feat && iq != skip_feat) {
           const float* vp = V + (long long)ipb * stride + (long long)fq * k;  // V[i_p, f_q]
           const float* vq = V + (long long)iq * stride + (long long)fpb * k;  // V[i_q, f_p]
           const float xx = xpb * xq;
@@ -87,6 +91,148 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
   }
 }
 
+
+// Column-ordered (gather) backward: no global atomics.
+//   gV[i, f_q, :] = sum over entries e of feature i (row r, value x, field f_i) and every
+//                   other entry q of row r:  c_r x x_q V[i_q, f_i, :]
+// which is the same sum as the pair scatter above, regrouped by the target feature i.
+// One wave per CSC chunk (<= CHUNK entries of one column), four independent waves per
+// 256-thread block (64-thread blocks cap residency at ~12 waves/CU). The chunk's
+// [nfield][k] accumulator lives in LDS and is written once to part[chunk] (an ordered
+// chunk_reduce then sums the chunks of a column). Lane e of a 64-entry batch loads entry
+// e's row descriptor; the wave then walks kUnroll entries at a time with lane = position
+// q in the row, so the row's idx/val/fld loads are coalesced and kUnroll rows' gathers are
+// in flight together. When every row has distinct fields (one-hot-per-field data such as
+// Criteo) the lanes of one entry hit distinct accumulator slots and the update is a plain
+// LDS read-add-write (b128 for k % 4 == 0); otherwise it falls back to ds_add_f32.
+// All LDS traffic is wave-private: wave_sync() orders it.
+constexpr int kCscUnroll = 4;
+constexpr int kCscWaves = 4;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool kVec4, bool kDistinct>
+__global__ __launch_bounds__(256) void ffm_grad_csc_kernel(
+    const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
+    const int* __restrict__ csc_rows, const float* __restrict__ csc_vals,
+    const long long* __restrict__ csc_pos, const long long* __restrict__ indptr,
+    const unsigned* __restrict__ pk, int sh, const float* __restrict__ val,
+    const float* __restrict__ Vt, long long nfeat, int nfield, int k, const float* __restrict__ coef,
+    float* __restrict__ part, int skip_feat) {
+  extern __shared__ float lds_acc[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long ch = blockIdx.x * (long long)kCscWaves + wave;
+  if (ch >= nch) return;  // no block-level barriers below
+  const int J = nfield * k;
+  const unsigned mask = (1u << sh) - 1u;
+  const long long fstride = nfeat * k;  // Vt is [nfield][nfeat][k]
+  float* acc = lds_acc + wave * J;  // [nfield][k]
+  for (int j = lane; j < J; j += 64) acc[j] = 0.f;
+  wave_sync();
+  const long long e0 = chunk_beg[ch], e1 = chunk_end[ch];
+  const int feat = (int)(pk[csc_pos[e0]] & mask);
+  if (feat != skip_feat) {
+    for (long long eb = e0; eb < e1; eb += 64) {
+      const long long e = eb + lane;
+      long long d_b = 0, d_pos = -1;
+      int d_len = 0, d_f = 0;
+      float d_s = 0.f;
+      if (e < e1) {
+        d_pos = csc_pos[e];
+        const int r = csc_rows[e];
+        d_b = indptr[r];
+        d_len = (int)(indptr[r + 1] - d_b);
+        d_s = coef[r] * csc_vals[e];
+        d_f = (int)(pk[d_pos] >> sh);
+      }
+      const int nb = (int)min<long long>(64, e1 - eb);
+      for (int e2 = 0; e2 < nb; e2 += kCscUnroll) {
+        long long qb[kCscUnroll], qpos[kCscUnroll];
+        int len[kCscUnroll];
+        const float* vbase[kCscUnroll];
+        float sc[kCscUnroll];
+        int maxlen = 0;
+#pragma unroll
+        for (int u = 0; u < kCscUnroll; ++u) {
+          const int src = min(e2 + u, nb - 1);
+          len[u] = e2 + u < nb ? __shfl(d_len, src, 64) : 0;
+          qb[u] = __shfl(d_b, src, 64);
+          qpos[u] = __shfl(d_pos, src, 64);
+          vbase[u] = Vt + (long long)__shfl(d_f, src, 64) * fstride;  // Vt[f_i]
+          sc[u] = __shfl(d_s, src, 64);
+          maxlen = max(maxlen, len[u]);
+        }
+        for (int qt = 0; qt < maxlen; qt += 64) {
+          int slot[kCscUnroll];
+          float tv[kCscUnroll];
+          const float* vq[kCscUnroll];
+#pragma unroll
+          for (int u = 0; u < kCscUnroll; ++u) {
+            const int q = qt + lane;
+            slot[u] = -1;
+            tv[u] = 0.f;
+            vq[u] = Vt;
+            if (q < len[u] && qb[u] + q != qpos[u]) {
+              const long long g = qb[u] + q;
+              const unsigned code = pk[g];
+              const int iq = (int)(code & mask);
+              if (iq != skip_feat) {
+                slot[u] = (int)(code >> sh) * k;
+                tv[u] = val ? sc[u] * val[g] : sc[u];
+                vq[u] = vbase[u] + (long long)iq * k;  // V[i_q, f_i]
+              }
+            }
+          }
+          if (kVec4) {
+            for (int f = 0; f < k; f += 4) {
+              float4 v4[kCscUnroll];
+#pragma unroll
+              for (int u = 0; u < kCscUnroll; ++u)
+                v4[u] = slot[u] >= 0 ? *reinterpret_cast<const float4*>(vq[u] + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+              for (int u = 0; u < kCscUnroll; ++u) {
+                if (slot[u] < 0) continue;
+                float* a = acc + slot[u] + f;
+                if (kDistinct) {
+                  float4 o = *reinterpret_cast<float4*>(a);
+                  o.x += tv[u] * v4[u].x;
+                  o.y += tv[u] * v4[u].y;
+                  o.z += tv[u] * v4[u].z;
+                  o.w += tv[u] * v4[u].w;
+                  *reinterpret_cast<float4*>(a) = o;
+                } else {
+                  atomicAdd(a, tv[u] * v4[u].x);
+                  atomicAdd(a + 1, tv[u] * v4[u].y);
+                  atomicAdd(a + 2, tv[u] * v4[u].z);
+                  atomicAdd(a + 3, tv[u] * v4[u].w);
+                }
+              }
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < kCscUnroll; ++u) {
+              if (slot[u] < 0) continue;
+              float* a = acc + slot[u];
+              for (int f = 0; f < k; ++f) {
+                if (kDistinct) a[f] += tv[u] * vq[u][f];
+                else atomicAdd(a + f, tv[u] * vq[u][f]);
+              }
+            }
+          }
+          wave_sync();
+        }
+      }
+    }
+  }
+  wave_sync();
+  float* out = part + ch * (long long)J;
+  for (int j = lane; j < J; j += 64) out[j] = acc[j];
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -96,7 +242,7 @@ extern "C" {
 // fx[row] = pair interaction sum (forward) or g += pair gradients scaled by coef[row].
 void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld, long long nrows,
                    uintptr_t V, int nfield, int k, uintptr_t fx, uintptr_t coef, uintptr_t gV,
-                   int backward, uintptr_t stream) {
+                   int backward, int skip_feat, uintptr_t stream) {
   if (nrows <= 0 || k <= 0) return;
   const long long threads = nrows * 64;
   const dim3 grid((unsigned)((threads + 255) / 256));
@@ -105,11 +251,43 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
   if (backward)
     hipLaunchKernelGGL(ffm_pairs_kernel<true>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
-                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4);
+                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat);
   else
     hipLaunchKernelGGL(ffm_pairs_kernel<false>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
-                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4);
+                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat);
+  YTK_LAUNCH_CHECK();
+}
+
+
+// part[chunk, nfield*k] = per-chunk gradient blocks (column-ordered gather backward).
+// pk[entry] = feature | field << sh; val may be 0 (all values 1); Vt is V transposed to
+// [nfield][nfeat][k] so the gathers of one chunk stay inside one field's slice.
+void ytk_ffm_grad_csc(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows,
+                      uintptr_t csc_vals, uintptr_t csc_pos, uintptr_t indptr, uintptr_t pk, int sh,
+                      uintptr_t val, uintptr_t Vt, long long nfeat, int nfield, int k, uintptr_t coef,
+                      uintptr_t part, int skip_feat, int distinct_fields, uintptr_t stream) {
+  if (nch <= 0 || k <= 0) return;
+  const int J = nfield * k;
+  if (J > 2048) throw std::invalid_argument("ffm_grad_csc: nfield*k > 2048");  // 4 x 8 KB LDS
+  if (sh <= 0 || sh > 31) throw std::invalid_argument("ffm_grad_csc: bad pack shift");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)kCscWaves * J * sizeof(float);
+  const bool vec4 = (k & 3) == 0 && (Vt & 15) == 0;  // 16-B gathers and b128 LDS updates
+#define YTK_FFM_CSC(VEC, DIS)                                                                  \
+  hipLaunchKernelGGL((ffm_grad_csc_kernel<VEC, DIS>),                                         \
+                     dim3((unsigned)((nch + kCscWaves - 1) / kCscWaves)), dim3(64 * kCscWaves), \
+                     lds, s, (const long long*)chunk_beg, (const long long*)chunk_end, nch,   \
+                     (const int*)csc_rows, (const float*)csc_vals, (const long long*)csc_pos,  \
+                     (const long long*)indptr, (const unsigned*)pk, sh, (const float*)val,     \
+                     (const float*)Vt, nfeat, nfield, k, (const float*)coef, (float*)part,     \
+                     skip_feat)
+  if (vec4) {
+    if (distinct_fields) YTK_FFM_CSC(true, true); else YTK_FFM_CSC(true, false);
+  } else {
+    if (distinct_fields) YTK_FFM_CSC(false, true); else YTK_FFM_CSC(false, false);
+  }
+#undef YTK_FFM_CSC
   YTK_LAUNCH_CHECK();
 }
 

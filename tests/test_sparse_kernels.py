@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from ytk_learn_amd.ops.ffm import ffm_backward, ffm_forward
+from ytk_learn_amd.ops.ffm import ffm_backward, ffm_backward_csc, ffm_forward
 from ytk_learn_amd.ops.sparse import CHUNK, SparseMatrix
 
 
@@ -116,7 +116,7 @@ def test_spmm_gpu_matches_cpu(cuda, J):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m", [(4, 12), (3, 8), (8, 70)])
-def test_ffm_gpu_matches_cpu(cuda, k, m):
+def test_ffm_gpu_matches_cpu(cuda, k, m, monkeypatch):
     n, F, nf = 3000, 400, 7
     ip, ix, vv, _ = _rand_csr(n, F, m, seed=k)
     g = torch.Generator().manual_seed(9)
@@ -131,8 +131,48 @@ def test_ffm_gpu_matches_cpu(cuda, k, m):
     gg = torch.zeros_like(V).to(cuda)
     ffm_backward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gg)
     torch.testing.assert_close(gg.cpu(), gc, rtol=1e-3, atol=1e-3)
+    # column-ordered backward (no atomics), with and without a skipped feature
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    monkeypatch.setattr(sparse_mod, "CHUNK", 100)  # several chunks per column
+    Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    assert Xg.n_chunks > F
+    gcsc = torch.ones_like(V).to(cuda)
+    ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gcsc)
+    torch.testing.assert_close(gcsc.cpu(), gc + 1.0, rtol=1e-3, atol=1e-3)
+    for skip in (0, int(ix[0])):
+        gs = torch.zeros_like(V)
+        ffm_backward(ip, ix, vv, fl, V, nf, k, c, gs, skip_feat=skip)
+        gsg = torch.zeros_like(V).to(cuda)
+        ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gsg, skip_feat=skip)
+        torch.testing.assert_close(gsg.cpu(), gs, rtol=1e-3, atol=1e-3)
+        fs = ffm_forward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k, skip_feat=skip)
+        torch.testing.assert_close(fs.cpu(), ffm_forward(ip, ix, vv, fl, V, nf, k, skip_feat=skip), rtol=1e-4,
+                                   atol=1e-4)
     # misaligned V (linear weights in front, as inside the model vector)
     big = torch.zeros(V.numel() + 3).to(cuda)
     big[3:] = V.to(cuda)
     fx_m = ffm_forward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), big[3:], nf, k)
     torch.testing.assert_close(fx_m.cpu(), fx_c, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_ffm_csc_backward_one_hot(cuda):
+    """Distinct fields per row and unit values: the atomic-free LDS path and the value-free
+    codes; checked against the CPU pair scatter, and bitwise repeatable."""
+    from ytk_learn_amd.data.synthetic import criteo_like
+    nf, k = 9, 4
+    ip, ix, vv, fl, _ = criteo_like(5000, nf, 900, seed=3)
+    F = nf * (900 // nf)
+    g = torch.Generator().manual_seed(2)
+    V = torch.randn(F * nf * k, generator=g) * 0.2
+    c = torch.randn(5000, generator=g)
+    gc = torch.zeros_like(V)
+    ffm_backward(ip, ix, vv, fl, V, nf, k, c, gc)
+    Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    gg = torch.zeros_like(V).to(cuda)
+    ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gg)
+    assert Xg._ffm_layout[1][0] is True and Xg._ffm_layout[1][3] is None
+    torch.testing.assert_close(gg.cpu(), gc, rtol=1e-3, atol=1e-3)
+    g2 = torch.zeros_like(V).to(cuda)
+    ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g2)
+    assert torch.equal(g2, gg)

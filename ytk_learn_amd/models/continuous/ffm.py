@@ -7,7 +7,8 @@ maps bias -> field 0 when need_bias; dim = F + F*nfield*k1; latent init from
 java.util.Random; dump ``name,%f(w),[nfield*k values]``).
 
 Device path: linear part on the deterministic SpMV kernels, pair part on
-``csrc/hip/ffm.hip`` (one wave per row, k-wide gathers, atomic scatter for gradients).
+``csrc/hip/ffm.hip`` (forward: one wave per row, k-wide gathers; backward: column-ordered
+gather over the CSC chunks with an LDS accumulator per chunk, no global atomics).
 """
 from __future__ import annotations
 
@@ -17,7 +18,7 @@ import numpy as np
 import torch
 
 from ...data.dataflow import read_dict_files
-from ...ops.ffm import _pairs_cpu, ffm_backward, ffm_forward
+from ...ops.ffm import _pairs_cpu, ffm_backward_csc, ffm_forward
 from ...utils.errors import YtkLearnError
 from ...utils.javafmt import java_double_str
 from .base import ContinuousModelBase, fmt_f, jfloat
@@ -68,6 +69,8 @@ class FFMModel(ContinuousModelBase):
                                                                               cols[1:1 + self.stride]]
         self.w = torch.from_numpy(w).to(self.device)
         self._cache = {}
+        # the bias without a latent factor keeps an all-zero latent block: skip its pairs
+        self._skip = 0 if (params.model.need_bias and not self.bias_latent) else -1
         log.info(f"field dict size:{self.nf}, K:[{self.k0}, {self.k1}], dim:{self.dim}")
 
     def regular_groups(self) -> List[Tuple[int, int]]:
@@ -85,7 +88,8 @@ class FFMModel(ContinuousModelBase):
         V = w[self.F:]
         cache = self._pairs(key, d)
         if self.stride > 0:
-            fx = fx + ffm_forward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, cache=cache).double()
+            fx = fx + ffm_forward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, cache=cache,
+                                 skip_feat=self._skip).double()
         y = d.y[:, 0].double()
         wt = d.weight.double()
         lv = self.loss.loss(fx, y)
@@ -96,7 +100,7 @@ class FFMModel(ContinuousModelBase):
             if self.stride > 0:
                 gv = g[self.F:]
                 gv.zero_()
-                ffm_backward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, c, gv, cache=cache)
+                ffm_backward_csc(X, d.fields, V, self.nf, self.kk, c, gv, skip_feat=self._skip, cache=cache)
             if not self.need_first:
                 g[self.bias_delta:self.F] = 0.0
             if not self.need_second:

@@ -30,7 +30,16 @@ def _pairs_cpu(indptr: torch.Tensor):
     return torch.cat(rows_all), torch.cat(ps), torch.cat(qs)
 
 
-def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=None):
+def _skip(pairs, idx, skip_feat):
+    """Drop pairs touching ``skip_feat`` (a feature with an all-zero latent block)."""
+    if skip_feat < 0:
+        return pairs
+    r, p, q = pairs
+    keep = (idx[p] != skip_feat) & (idx[q] != skip_feat)
+    return r[keep], p[keep], q[keep]
+
+
+def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=None, skip_feat: int = -1):
     """Pair-interaction sum per row (float32 [n])."""
     n = indptr.shape[0] - 1
     if out is None:
@@ -38,9 +47,9 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, out)
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, ptr(out), 0, 0, 0,
-                        stream(V))
+                        int(skip_feat), stream(V))
         return out
-    r, p, q = cache if cache is not None else _pairs_cpu(indptr)
+    r, p, q = _skip(cache if cache is not None else _pairs_cpu(indptr), idx, skip_feat)
     V3 = V.view(-1, nfield, k)
     ip, iq = idx[p].long(), idx[q].long()
     fp, fq = fld[p].long(), fld[q].long()
@@ -50,15 +59,15 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
     return out
 
 
-def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=None):
+def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=None, skip_feat: int = -1):
     """gV += pair gradients (gV, V: [F * nfield * k] flat)."""
     n = indptr.shape[0] - 1
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, coef, gV)
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, 0, ptr(coef), ptr(gV), 1,
-                        stream(V))
+                        int(skip_feat), stream(V))
         return gV
-    r, p, q = cache if cache is not None else _pairs_cpu(indptr)
+    r, p, q = _skip(cache if cache is not None else _pairs_cpu(indptr), idx, skip_feat)
     V3 = V.view(-1, nfield, k)
     G3 = gV.view(-1, nfield, k)
     ip, iq = idx[p].long(), idx[q].long()
@@ -68,4 +77,52 @@ def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=
     G2 = G3.view(-1, k)
     G2.index_add_(0, flat(ip, fq), s * V3[iq, fp])
     G2.index_add_(0, flat(iq, fp), s * V3[ip, fq])
+    return gV
+
+
+def _csc_layout(X, fld, nfield: int):
+    """Per-dataset inputs of the column-ordered backward, cached on X: whether rows have
+    distinct fields (then the LDS accumulator needs no atomics), the packed entry codes
+    ``feature | field << sh`` (one 4-B load per entry instead of two) and the values (None
+    when all are 1, e.g. one-hot data). Returns None when the codes do not fit 32 bits."""
+    key = (fld.data_ptr(), int(nfield))
+    cached = getattr(X, "_ffm_layout", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    sh = max(1, int(X.ncols - 1).bit_length())
+    if sh + max(1, int(nfield - 1).bit_length()) > 32:
+        X._ffm_layout = (key, None)
+        return None
+    f64 = fld.to(torch.int64)
+    ks = torch.sort(X.rows_of_nnz.to(torch.int64) * nfield + f64).values
+    distinct = bool(ks.numel() < 2 or not bool((ks[1:] == ks[:-1]).any()))
+    del ks
+    code = X.indices.to(torch.int64) | (f64 << sh)
+    code = torch.where(code >= 2 ** 31, code - 2 ** 32, code).to(torch.int32).contiguous()  # uint32 bits
+    vals = None if bool((X.values == 1).all()) else X.values
+    lay = (distinct, code, sh, vals)
+    X._ffm_layout = (key, lay)
+    return lay
+
+
+def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = -1, cache=None):
+    """gV += pair gradients, column-ordered (no global atomics; deterministic for rows with
+    distinct fields). ``X`` is the :class:`~ytk_learn_amd.ops.sparse.SparseMatrix` of the same
+    rows (its CSC chunks define the work split). Falls back to :func:`ffm_backward` on CPU."""
+    lay = _csc_layout(X, fld, nfield) if V.is_cuda and nfield * k <= 2048 else None
+    if lay is None:
+        return ffm_backward(X.indptr, X.indices, X.values, fld, V, nfield, k, coef, gV, cache=cache,
+                            skip_feat=skip_feat)
+    if X._csc is None:
+        X._build_csc()
+    distinct, code, sh, vals = lay
+    J = nfield * k
+    check_cuda(fld, V, coef, gV)
+    Vt = V.view(X.ncols, nfield, k).transpose(0, 1).contiguous()  # [nfield][F][k]
+    part = torch.empty((max(X.n_chunks, 1), J), dtype=torch.float32, device=V.device)
+    h, s = hip(), stream(V)
+    h.ffm_grad_csc(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
+                   ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0, ptr(Vt),
+                   X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), s)
+    h.chunk_reduce(ptr(X.chunk_ptr), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, s)
     return gV
