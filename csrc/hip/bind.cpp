@@ -49,6 +49,13 @@ void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintpt
 void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
                       int, int, uintptr_t);
+// fm.hip
+void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
+                    uintptr_t, uintptr_t);
+void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
+                     uintptr_t, uintptr_t);
+// blas.hip
+void ytk_dot(uintptr_t, uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
@@ -75,6 +82,9 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("chunk_reduce", &ytk_chunk_reduce);
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
+  m.def("dot", &ytk_dot);
+  m.def("fm_forward", &ytk_fm_forward);
+  m.def("fm_backward", &ytk_fm_backward);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 25 || ip.size() != 6 || fp.size() != 6)

@@ -1,0 +1,90 @@
+// Vector reductions for the L-BFGS/OWL-QN driver (gfx950 / CDNA4, wave64).
+//
+// The two-loop recursion (optim/lbfgs.py, reference J/optimizer/HoagOptimizer.java:904-929)
+// and the line search need fp64 dot products of fp32 vectors of the full model dimension
+// (161M for FFM on Criteo). Converting both operands to fp64 tensors costs ~8 bytes of
+// traffic per byte of input; here each thread streams 16-B fp32 loads, accumulates in
+// fp64, and a fixed-shape two-stage reduction (per-block partials in block order, then one
+// block) makes the result bitwise reproducible.
+#include "common.h"
+
+#include <algorithm>
+
+namespace ytk {
+
+constexpr int kDotBlocks = 1024;
+
+// mode 0: sum a*b; 1: sum a*a; 2: sum |a|
+template <int kMode>
+__global__ __launch_bounds__(256) void dot_partial_kernel(const float* __restrict__ a,
+                                                          const float* __restrict__ b, long long n,
+                                                          int vec, double* __restrict__ part) {
+  double acc = 0.0;
+  const long long tid = blockIdx.x * 256LL + threadIdx.x, nth = (long long)gridDim.x * 256;
+  long long tail = 0;
+  if (vec) {
+    const long long n4 = n >> 2;
+    const float4* a4 = reinterpret_cast<const float4*>(a);
+    const float4* b4 = reinterpret_cast<const float4*>(b);
+    for (long long i = tid; i < n4; i += nth) {
+      const float4 x = a4[i];
+      if (kMode == 0) {
+        const float4 y = b4[i];
+        acc += (double)x.x * y.x + (double)x.y * y.y + (double)x.z * y.z + (double)x.w * y.w;
+      } else if (kMode == 1) {
+        acc += (double)x.x * x.x + (double)x.y * x.y + (double)x.z * x.z + (double)x.w * x.w;
+      } else {
+        acc += (double)fabsf(x.x) + (double)fabsf(x.y) + (double)fabsf(x.z) + (double)fabsf(x.w);
+      }
+    }
+    tail = n4 << 2;
+  }
+  for (long long i = tail + tid; i < n; i += nth) {
+    const float x = a[i];
+    acc += kMode == 0 ? (double)x * b[i] : kMode == 1 ? (double)x * x : (double)fabsf(x);
+  }
+  __shared__ double s[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+__global__ __launch_bounds__(256) void dot_final_kernel(const double* __restrict__ part, int nb,
+                                                        double* __restrict__ out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) acc += part[i];
+  __shared__ double s[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+}  // namespace ytk
+
+using namespace ytk;
+
+extern "C" {
+
+// *out (fp64, device) = reduction of a (and b) per mode; part: >= 1024 doubles of scratch.
+void ytk_dot(uintptr_t a, uintptr_t b, long long n, int mode, uintptr_t part, uintptr_t out,
+             uintptr_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int vec = ((a | (mode == 0 ? b : 0)) & 15) == 0;
+  long long want = (n / 4 + 255) / 256;
+  const int nb = (int)std::max<long long>(1, std::min<long long>(kDotBlocks, want));
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(dot_partial_kernel<0>, dim3(nb), dim3(256), 0, s, (const float*)a,
+                               (const float*)b, n, vec, (double*)part); break;
+    case 1: hipLaunchKernelGGL(dot_partial_kernel<1>, dim3(nb), dim3(256), 0, s, (const float*)a,
+                               (const float*)b, n, vec, (double*)part); break;
+    default: hipLaunchKernelGGL(dot_partial_kernel<2>, dim3(nb), dim3(256), 0, s, (const float*)a,
+                                (const float*)b, n, vec, (double*)part); break;
+  }
+  hipLaunchKernelGGL(dot_final_kernel, dim3(1), dim3(256), 0, s, (const double*)part, nb,
+                     (double*)out);
+  YTK_LAUNCH_CHECK();
+}
+
+}  // extern "C"

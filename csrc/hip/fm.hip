@@ -1,0 +1,180 @@
+// Factorization machine loss/gradient kernels (gfx950 / CDNA4, wave64).
+//
+// Reference: J/optimizer/FMHoagOptimizer.java:60-160
+//   fx(r)   = sum_i w_i x_i + 1/2 sum_f [ S_rf^2 - sum_i V_if^2 x_i^2 ],  S_rf = sum_i V_if x_i
+//   g_w(i)  = sum_r c_r x_ri
+//   g_V(if) = sum_r c_r x_ri (S_rf - V_if x_ri) = sum_r c_r x_ri S_rf - V_if sum_r c_r x_ri^2
+// The unfused form costs five segmented products (X w, X V, (X∘X)(V∘V), X^T c, X^T(c∘S),
+// (X∘X)^T c) -- six passes over the nonzeros. Here the forward is one pass over the rows
+// (each V row gathered once, giving S, the square term and the linear term together) and
+// the backward one pass over the CSC chunks (each S row gathered once per nonzero, giving
+// the three column sums together); an ordered chunk_reduce + elementwise finish the
+// gradient. Lanes map to latent index f in groups of G = pow2 >= k (<= 64), so a wave
+// works on 64/G rows (or chunks) at once and the V / S row gathers are G-wide and
+// contiguous. Deterministic: fixed reduction orders, no atomics.
+#include "common.h"
+
+namespace ytk {
+
+template <int G>
+__global__ __launch_bounds__(256) void fm_forward_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
+    long long nrows, const float* __restrict__ w, const float* __restrict__ V, int k,
+    double* __restrict__ fx, float* __restrict__ S) {
+  const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
+  const int f = threadIdx.x & (G - 1);
+  if (gid >= nrows) return;
+  const long long b = indptr[gid], e = indptr[gid + 1];
+  float s = 0.f, q = 0.f, lin = 0.f;
+  for (long long t = b; t < e; t += G) {
+    // lane f loads entry t+f, then the group walks the G entries by shuffle
+    int my_i = 0;
+    float my_x = 0.f;
+    if (t + f < e) { my_i = idx[t + f]; my_x = val[t + f]; lin += w[my_i] * my_x; }
+    const int n = (int)min<long long>(G, e - t);
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {  // four independent gathers in flight
+      float v[4], xs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = __shfl(my_i, j + u, G);
+        xs[u] = __shfl(my_x, j + u, G);
+        v[u] = f < k ? V[(long long)i * k + f] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float vx = v[u] * xs[u];
+        s += vx;
+        q += vx * vx;
+      }
+    }
+    for (; j < n; ++j) {
+      const int i = __shfl(my_i, j, G);
+      const float x = __shfl(my_x, j, G);
+      if (f < k) {
+        const float vx = V[(long long)i * k + f] * x;
+        s += vx;
+        q += vx * vx;
+      }
+    }
+  }
+  double part = 0.5 * ((double)s * s - (double)q) + (double)lin;
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, G);
+  if (f < k) S[gid * k + f] = s;
+  if (f == 0) fx[gid] = part;
+}
+
+// part[chunk, 0:k] = sum c_r x S_r;  part[chunk, k] = sum c_r x;  part[chunk, k+1] = sum c_r x^2
+template <int G>
+__global__ __launch_bounds__(256) void fm_backward_kernel(
+    const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
+    const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const float* __restrict__ coef,
+    const float* __restrict__ S, int k, float* __restrict__ part) {
+  const long long ch = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
+  const int f = threadIdx.x & (G - 1);
+  if (ch >= nch) return;
+  const long long b = chunk_beg[ch], e = chunk_end[ch];
+  float gs = 0.f, lin = 0.f, sq = 0.f;
+  for (long long t = b; t < e; t += G) {
+    int my_r = 0;
+    float my_cx = 0.f;
+    if (t + f < e) {
+      my_r = csc_rows[t + f];
+      const float x = csc_vals[t + f];
+      my_cx = coef[my_r] * x;
+      lin += my_cx;
+      sq += my_cx * x;
+    }
+    const int n = (int)min<long long>(G, e - t);
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {  // four independent gathers in flight
+      float sv[4], cs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = __shfl(my_r, j + u, G);
+        cs[u] = __shfl(my_cx, j + u, G);
+        sv[u] = f < k ? S[(long long)r * k + f] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) gs += cs[u] * sv[u];
+    }
+    for (; j < n; ++j) {
+      const int r = __shfl(my_r, j, G);
+      const float cx = __shfl(my_cx, j, G);
+      if (f < k) gs += cx * S[(long long)r * k + f];
+    }
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) {
+    lin += __shfl_xor(lin, off, G);
+    sq += __shfl_xor(sq, off, G);
+  }
+  float* o = part + ch * (long long)(k + 2);
+  if (f < k) o[f] = gs;
+  if (f == 0) { o[k] = lin; o[k + 1] = sq; }
+}
+
+}  // namespace ytk
+
+using namespace ytk;
+
+static int fm_group(int k) {
+  int g = 4;
+  while (g < k) g <<= 1;
+  return g;
+}
+
+extern "C" {
+
+// fx[r] (double) and S[r, k] for every row; w: linear weights [F], V: [F, k] (any alignment).
+void ytk_fm_forward(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
+                    uintptr_t V, int k, uintptr_t fx, uintptr_t S, uintptr_t stream) {
+  if (nrows <= 0) return;
+  if (k < 1 || k > 64) throw std::invalid_argument("fm_forward: 1 <= k <= 64");
+  const int G = fm_group(k);
+  const long long threads = nrows * G;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_FM_F(GG)                                                                           \
+  hipLaunchKernelGGL(fm_forward_kernel<GG>, grid, dim3(256), 0, s, (const long long*)indptr,  \
+                     (const int*)idx, (const float*)val, nrows, (const float*)w,               \
+                     (const float*)V, k, (double*)fx, (float*)S)
+  switch (G) {
+    case 4: YTK_FM_F(4); break;
+    case 8: YTK_FM_F(8); break;
+    case 16: YTK_FM_F(16); break;
+    case 32: YTK_FM_F(32); break;
+    default: YTK_FM_F(64); break;
+  }
+#undef YTK_FM_F
+  YTK_LAUNCH_CHECK();
+}
+
+// part[chunk, k + 2] column sums of the FM gradient (see kernel comment).
+void ytk_fm_backward(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows,
+                     uintptr_t csc_vals, uintptr_t coef, uintptr_t S, int k, uintptr_t part,
+                     uintptr_t stream) {
+  if (nch <= 0) return;
+  if (k < 1 || k > 64) throw std::invalid_argument("fm_backward: 1 <= k <= 64");
+  const int G = fm_group(k);
+  const long long threads = nch * G;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_FM_B(GG)                                                                           \
+  hipLaunchKernelGGL(fm_backward_kernel<GG>, grid, dim3(256), 0, s,                            \
+                     (const long long*)chunk_beg, (const long long*)chunk_end, nch,            \
+                     (const int*)csc_rows, (const float*)csc_vals, (const float*)coef,         \
+                     (const float*)S, k, (float*)part)
+  switch (G) {
+    case 4: YTK_FM_B(4); break;
+    case 8: YTK_FM_B(8); break;
+    case 16: YTK_FM_B(16); break;
+    case 32: YTK_FM_B(32); break;
+    default: YTK_FM_B(64); break;
+  }
+#undef YTK_FM_B
+  YTK_LAUNCH_CHECK();
+}
+
+}  // extern "C"

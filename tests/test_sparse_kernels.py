@@ -176,3 +176,31 @@ def test_ffm_csc_backward_one_hot(cuda):
     g2 = torch.zeros_like(V).to(cuda)
     ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g2)
     assert torch.equal(g2, gg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(3, 10), (16, 40), (40, 70)])
+def test_fm_fused_gpu_matches_cpu(cuda, k, m, monkeypatch):
+    from ytk_learn_amd.ops.fm import fm_backward, fm_forward
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    n, F = 3000, 500
+    ip, ix, vv, _ = _rand_csr(n, F, m, seed=k)
+    g = torch.Generator().manual_seed(k)
+    w = torch.randn(F + F * k + 1, generator=g) * 0.1
+    c = torch.randn(n, generator=g)
+    Xc = SparseMatrix(ip, ix, vv, F)
+    monkeypatch.setattr(sparse_mod, "CHUNK", 64)
+    Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    wg = w.to(cuda)
+    # V deliberately misaligned (starts at float offset F + 1 inside the model vector)
+    Vc, Vg = w[F + 1:].view(F, k), wg[F + 1:].view(F, k)
+    fc, Sc = fm_forward(Xc, w[:F], Vc)
+    fg, Sg = fm_forward(Xg, wg[:F], Vg)
+    torch.testing.assert_close(fg.cpu(), fc, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(Sg.cpu(), Sc, rtol=1e-5, atol=1e-5)
+    glc, gVc = torch.zeros(F), torch.zeros(F, k)
+    fm_backward(Xc, c, Sc, Vc, glc, gVc)
+    glg, gVg = torch.zeros(F, device=cuda), torch.zeros(F, k, device=cuda)
+    fm_backward(Xg, c.to(cuda), Sg, Vg, glg, gVg)
+    torch.testing.assert_close(glg.cpu(), glc, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gVg.cpu(), gVc, rtol=1e-4, atol=1e-3)

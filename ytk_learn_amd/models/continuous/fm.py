@@ -7,8 +7,9 @@ gradient blocks zeroed when k[0] < 1 / k[1] < 1 / the bias has no latent factor)
 N(mean, std) or U(a, b) with the configured seed, bias latent = 0; dump
 ``name,%f(w),v_1..v_k``).
 
-Device path (all deterministic segmented SpMM, ``csrc/hip/sparse.hip``):
-  wx = X w,  S = X V,  Q = (X∘X)(V∘V)
+Device path (deterministic, ``csrc/hip/fm.hip``): one fused pass over the rows gives
+  fx = X w + 1/2 sum_f [S^2 - (X∘X)(V∘V)],  S = X V
+and one fused pass over the CSC chunks gives
   g_w = X^T c,  G_V = X^T (c∘S) - V ∘ ((X∘X)^T c)
 """
 from __future__ import annotations
@@ -19,6 +20,7 @@ import numpy as np
 import torch
 
 from ...ops._ext import native
+from ...ops.fm import fm_backward, fm_forward
 from .base import ContinuousModelBase, fmt_f, jfloat
 from ...utils.javafmt import java_double_str
 
@@ -70,15 +72,9 @@ class FMModel(ContinuousModelBase):
         return [(self.bias_delta, self.F), (self.F, self.dim)]
 
     def _fx(self, X, w):
-        wl = w[:self.F]
-        fx = X.matmul(wl).double()
-        S = Q = None
         if self.kk > 0:
-            V = w[self.F:].view(self.F, self.kk)
-            S = X.matmul(V)
-            Q = X.matmul((V * V).contiguous(), square=True)
-            fx = fx + 0.5 * (S.double() ** 2 - Q.double()).sum(1)
-        return fx, S
+            return fm_forward(X, w[:self.F], w[self.F:].view(self.F, self.kk))
+        return X.matmul(w[:self.F]).double(), None
 
     def _forward(self, X, d, w, g):
         fx, S = self._fx(X, w)
@@ -88,12 +84,10 @@ class FMModel(ContinuousModelBase):
         pred = self.loss.predict(fx).float()
         if g is not None:
             c = (wt * self.loss.grad(fx, y)).float()
-            X.t_matmul(c, out=g[:self.F])
             if self.kk > 0:
-                GV = g[self.F:].view(self.F, self.kk)
-                X.t_matmul((c[:, None] * S).contiguous(), out=GV)
-                sq = X.t_matmul(c, square=True)
-                GV.sub_(w[self.F:].view(self.F, self.kk) * sq[:, None])
+                fm_backward(X, c, S, w[self.F:].view(self.F, self.kk), g[:self.F], g[self.F:].view(self.F, self.kk))
+            else:
+                X.t_matmul(c, out=g[:self.F])
             if not self.need_first:
                 g[self.bias_delta:self.F] = 0.0
             if not self.need_second:

@@ -1,0 +1,58 @@
+"""fp64-accumulated reductions of fp32 vectors (``csrc/hip/blas.hip``).
+
+Used by the L-BFGS/OWL-QN driver for the two-loop dot products, line-search directional
+derivatives and regularizer sums over the full model vector. On CPU: torch in fp64.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import check_cuda, hip, ptr, stream
+
+_scratch = {}
+
+
+def _buffers(dev):
+    key = (dev.type, dev.index)
+    if key not in _scratch:
+        _scratch[key] = torch.empty(1024 + 8, dtype=torch.float64, device=dev)
+    return _scratch[key]
+
+
+def _reduce(a: torch.Tensor, b, mode: int) -> float:
+    if a.device.type != "cuda":
+        a64 = a.reshape(-1).double()
+        if mode == 0:
+            return float(torch.dot(a64, b.reshape(-1).double()))
+        if mode == 1:
+            return float(torch.dot(a64, a64))
+        return float(a64.abs().sum())
+    a = a.reshape(-1)
+    if not a.is_contiguous():
+        a = a.contiguous()
+    if b is not None:
+        b = b.reshape(-1)
+        if not b.is_contiguous():
+            b = b.contiguous()
+        if b.numel() != a.numel():
+            raise ValueError("dot: size mismatch")
+        check_cuda(a, b)
+    else:
+        check_cuda(a)
+    if a.dtype != torch.float32 or (b is not None and b.dtype != torch.float32):
+        raise TypeError("dot: float32 operands expected")
+    buf = _buffers(a.device)
+    hip().dot(ptr(a), ptr(b) if b is not None else 0, a.numel(), mode, ptr(buf), ptr(buf[1024:]), stream(a))
+    return float(buf[1024])
+
+
+def dot(a: torch.Tensor, b: torch.Tensor) -> float:
+    return _reduce(a, b, 0)
+
+
+def sum_sq(a: torch.Tensor) -> float:
+    return _reduce(a, None, 1)
+
+
+def sum_abs(a: torch.Tensor) -> float:
+    return _reduce(a, None, 2)

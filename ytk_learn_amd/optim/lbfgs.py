@@ -28,6 +28,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 
 from ..config.params import HyperParams, LineSearchParams
+from ..ops import blas
 from ..utils.javafmt import java_double_str as jd
 
 
@@ -73,12 +74,11 @@ class ContinuousModel:
 
 
 def _dot(a: torch.Tensor, b: torch.Tensor) -> float:
-    return float(torch.dot(a.double(), b.double())) if a.device.type == "cpu" else \
-        float(torch.sum(a.to(torch.float64) * b.to(torch.float64)))
+    return blas.dot(a, b)
 
 
 def _norm(a: torch.Tensor) -> float:
-    return float(torch.linalg.vector_norm(a, dtype=torch.float64))
+    return math.sqrt(blas.sum_sq(a))
 
 
 @dataclass
@@ -142,9 +142,9 @@ class HoagOptimizer:
                 continue
             ws = w[s:e]
             if self.l2[r] > 0.0:
-                reg += 0.5 * self.l2[r] * float(torch.sum(ws * ws, dtype=torch.float64))
+                reg += 0.5 * self.l2[r] * blas.sum_sq(ws)
             if self.l1[r] > 0.0:
-                reg += self.l1[r] * float(torch.sum(ws.abs(), dtype=torch.float64))
+                reg += self.l1[r] * blas.sum_abs(ws)
         # local pure loss is summed over ranks; the regularizer is added once with the global W
         tot = torch.tensor([pure], dtype=torch.float64)
         if self.comm is not None and self.comm.is_dist:
