@@ -1,0 +1,7 @@
+#!/usr/bin/env bash
+# demo: gbhsdt/binary_classification (gbhsdt). Run from anywhere; paths are relative to the repo root.
+set -euo pipefail
+cd "$(dirname "$0")/../../.."
+bash demo/prepare_data.sh
+bash bin/local_optimizer.sh gbhsdt demo/gbhsdt/binary_classification/gbhsdt.conf 1 
+bash bin/predict.sh gbhsdt demo/data/ytklearn/agaricus.test.ytklearn demo/gbhsdt/binary_classification/gbhsdt.conf LABEL_AND_PREDICT value auc 

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from ...data.dataflow import read_dict_files
-from ...ops.ffm import _pairs_cpu, ffm_backward_csc, ffm_forward
+from ...ops.ffm import ffm_backward_csc, ffm_forward, ffm_pairs_cpu
 from ...utils.errors import YtkLearnError
 from ...utils.javafmt import java_double_str
 from .base import ContinuousModelBase, fmt_f, jfloat
@@ -80,7 +80,7 @@ class FFMModel(ContinuousModelBase):
         if d.indptr.is_cuda:
             return None
         if key not in self._cache:
-            self._cache[key] = _pairs_cpu(d.indptr)
+            self._cache[key] = ffm_pairs_cpu(d.indptr, d.indices, d.values, self._skip)
         return self._cache[key]
 
     def _forward(self, X, d, w, g, key):

@@ -30,17 +30,19 @@ def _pairs_cpu(indptr: torch.Tensor):
     return torch.cat(rows_all), torch.cat(ps), torch.cat(qs)
 
 
-def _skip(pairs, idx, skip_feat):
-    """Drop pairs touching ``skip_feat`` (a feature with an all-zero latent block)."""
-    if skip_feat < 0:
-        return pairs
-    r, p, q = pairs
-    keep = (idx[p] != skip_feat) & (idx[q] != skip_feat)
+def ffm_pairs_cpu(indptr, idx, val, skip_feat: int = -1):
+    """CPU pair list without the pairs that contribute nothing: a zero value on either side
+    (dense-style rows such as agaricus carry many explicit ``name:0`` entries) or the
+    ``skip_feat`` feature (all-zero latent block). Cache it per dataset and pass as ``cache``."""
+    r, p, q = _pairs_cpu(indptr)
+    keep = (val[p] != 0) & (val[q] != 0)
+    if skip_feat >= 0:
+        keep &= (idx[p] != skip_feat) & (idx[q] != skip_feat)
     return r[keep], p[keep], q[keep]
 
 
 def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=None, skip_feat: int = -1):
-    """Pair-interaction sum per row (float32 [n])."""
+    """Pair-interaction sum per row (float32 [n]). CPU: ``cache`` = :func:`ffm_pairs_cpu` output."""
     n = indptr.shape[0] - 1
     if out is None:
         out = torch.zeros(n, dtype=torch.float32, device=V.device)
@@ -49,7 +51,7 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, ptr(out), 0, 0, 0,
                         int(skip_feat), stream(V))
         return out
-    r, p, q = _skip(cache if cache is not None else _pairs_cpu(indptr), idx, skip_feat)
+    r, p, q = cache if cache is not None else ffm_pairs_cpu(indptr, idx, val, skip_feat)
     V3 = V.view(-1, nfield, k)
     ip, iq = idx[p].long(), idx[q].long()
     fp, fq = fld[p].long(), fld[q].long()
@@ -67,7 +69,7 @@ def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, 0, ptr(coef), ptr(gV), 1,
                         int(skip_feat), stream(V))
         return gV
-    r, p, q = _skip(cache if cache is not None else _pairs_cpu(indptr), idx, skip_feat)
+    r, p, q = cache if cache is not None else ffm_pairs_cpu(indptr, idx, val, skip_feat)
     V3 = V.view(-1, nfield, k)
     G3 = gV.view(-1, nfield, k)
     ip, iq = idx[p].long(), idx[q].long()
