@@ -116,7 +116,7 @@ def main():
     train_loss, test_loss = tr._losses()  # collective: every rank calls it
     sec_per_tree = el_max / a.steps
     if a.profile and rank == 0:
-        print(getattr(tr.builder, "total_stats", ""), file=sys.stderr)
+        print(tr.timer.report() if tr.use_device_builder else tr.builder.total_stats, file=sys.stderr)
     if rank == 0:
         res = {
             "metric": METRIC,

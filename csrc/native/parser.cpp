@@ -54,9 +54,14 @@ inline bool parse_float(sv s, float* out) {
     if (c == 'f' || c == 'F' || c == 'd' || c == 'D') s.remove_suffix(1);
   }
   if (s.empty()) return false;
-  if (s == "NaN") {
+  if (s == "NaN" || s == "-NaN") {
     *out = std::nanf("");
     return true;
+  }
+  // from_chars also takes "nan"/"inf"/"infinity" in any case; Java only "NaN" / "Infinity"
+  {
+    const char c0 = s.front() == '-' && s.size() > 1 ? s[1] : s.front();
+    if (c0 == 'n' || c0 == 'N' || c0 == 'i' || c0 == 'I') return false;
   }
   float v;
   auto r = std::from_chars(s.data(), s.data() + s.size(), v);
@@ -334,8 +339,10 @@ ParseResult parse_ytk(const char* data, size_t len, const ParseOptions& opt) {
   }
   cut.push_back(len);
   const int C = (int)cut.size() - 1;
+  // global line index of every chunk's first line: sharding (line_mod), y-sampling (keyed
+  // by line index) and row_line must not depend on the thread count
   std::vector<int64_t> first_line(C, 0);
-  if (opt.line_mod > 1 && C > 1) {
+  if (C > 1) {
     std::vector<int64_t> nlines(C);
     std::vector<std::thread> th;
     for (int c = 0; c < C; ++c)

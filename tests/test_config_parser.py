@@ -115,11 +115,19 @@ def test_parser_multithreaded_deterministic():
     g = np.random.default_rng(0)
     lines = "".join("1###%d###%s\n" % (i % 2, ",".join(f"x{j}:{g.random():.3f}" for j in g.integers(0, 500, 8)))
                     for i in range(60000))
-    a = _parse(lines, threads=1)
-    b = _parse(lines, threads=8)
-    assert a["names"] == b["names"]
-    for k in ("indptr", "feat", "val", "weight", "labels"):
-        np.testing.assert_array_equal(a[k], b[k])
+    for opts in ({}, {"y_sampling": [0.3, 1.0], "sample_seed": 5}):
+        a = _parse(lines, threads=1, **opts)
+        b = _parse(lines, threads=8, **opts)
+        assert a["names"] == b["names"] and a["n_rows"] == b["n_rows"]
+        for k in ("indptr", "feat", "val", "weight", "labels", "row_line"):
+            np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_parser_java_float_grammar():
+    r = _parse("1###1###a:NaN,b:1.5f,c:2d,d:+3\n1###1###a:nan\n1###1###a:inf\n1###1###a:Infinity\n"
+               "1###1###a:1e400\n", max_error_tol=10)
+    assert r["n_rows"] == 1 and r["n_errors"] == 4  # lowercase nan/inf and +-Infinity rejected
+    assert np.isnan(r["val"][0]) and list(r["val"][1:]) == [1.5, 2.0, 3.0]
 
 
 def test_java_random_stream():

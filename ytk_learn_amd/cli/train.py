@@ -13,6 +13,7 @@ The reference's positional form is also accepted:
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 
 from ..config.hocon import parse_override_value
@@ -28,6 +29,10 @@ def parse_args(argv):
     ap.add_argument("--device", default=None)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
+    ap.add_argument("--profile", action="store_true",
+                    help="per-phase device timers (TimeStats) per tree / iteration and in total")
+    ap.add_argument("--metrics-jsonl", default=None, metavar="PATH",
+                    help="append per-round / per-iteration metrics as JSON lines (rank 0)")
     a = ap.parse_args(argv)
     if a.legacy:
         py_script = a.legacy[0]
@@ -50,6 +55,10 @@ def main(argv=None) -> int:
             raise YtkLearnError(f"--set expects KEY=VALUE, got {kv}")
         k, v = kv.split("=", 1)
         overrides[k.strip()] = parse_override_value(v)
+    if a.profile:
+        os.environ["YTK_PROFILE"] = "1"
+    if a.metrics_jsonl:
+        os.environ["YTK_METRICS_JSONL"] = a.metrics_jsonl
     from ..train import train
     from ..parallel.comm import Comm
     comm = Comm.from_env(a.device)

@@ -96,8 +96,9 @@ class LocalFileSystem(FileSystem):
         d = os.path.dirname(p)
         if d:
             os.makedirs(d, exist_ok=True)
-        mode = ("a" if append else "w") + ("b" if binary else "")
-        return open(p, mode, encoding=None if binary else "utf-8")
+        if append:
+            return open(p, "ab" if binary else "a", encoding=None if binary else "utf-8")
+        return _AtomicWriter(p, binary)
 
     def is_dir(self, path):
         return os.path.isdir(self._p(path))
@@ -117,6 +118,41 @@ class LocalFileSystem(FileSystem):
 
     def local_path(self, path):
         return self._p(path)
+
+
+class _AtomicWriter:
+    """Write to a hidden temp file next to ``path`` and rename it over ``path`` on a clean
+    close, so a worker killed mid-dump never leaves a truncated model / checkpoint behind
+    (``continue_train`` then resumes from the previous complete dump). Hidden temp names
+    are skipped by ``recur_get_paths``."""
+
+    def __init__(self, path: str, binary: bool):
+        d, name = os.path.split(path)
+        self.path = path
+        self.tmp = os.path.join(d, f".{name}.tmp-{os.getpid()}")
+        self.f = open(self.tmp, "wb" if binary else "w", encoding=None if binary else "utf-8")
+
+    def __getattr__(self, name):
+        return getattr(self.f, name)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is not None:
+            self.f.close()
+            os.remove(self.tmp)
+            return False
+        self.close()
+        return False
+
+    def close(self):
+        if self.f.closed:
+            return
+        self.f.flush()
+        os.fsync(self.f.fileno())
+        self.f.close()
+        os.replace(self.tmp, self.path)
 
 
 class FsspecFileSystem(FileSystem):

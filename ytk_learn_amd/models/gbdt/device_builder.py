@@ -16,6 +16,7 @@ built (smaller) children in the first half, derived children in the second.
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -23,6 +24,7 @@ import torch
 from ...ops import gbdt as gops
 from ...ops._ext import hip, ptr, stream
 from ...parallel.comm import Comm
+from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams
 from .tree import Tree
 
@@ -75,8 +77,9 @@ class DeviceLevelBuilder:
     MIN_ROWS = int(os.environ.get("YTK_HIST_MIN_ROWS", 2048))
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
-                 params: TreeParams, comm: Comm = None):
+                 params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
         assert bins.is_cuda
+        self.timer = timer if timer is not None else PhaseTimer()
         p = params
         if not (1 <= p.max_depth <= MAX_DEPTH_DEVICE) or p.grow_policy != "level":
             raise ValueError("device builder needs level-wise growth with 1 <= max_depth <= 12")
@@ -227,6 +230,8 @@ class DeviceLevelBuilder:
             mx = mx.clone()
             self.comm.allreduce_(mx, op="max")
         h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
+        tm = self.timer
+        tm.mark("init_stats")
         # root
         ptrs = self._ptrs()
         st_ptr = self.st.data_ptr()
@@ -248,17 +253,21 @@ class DeviceLevelBuilder:
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
 
         build_hist(gh0, rows0, self.HIST_TARGET + 1, 0, 1)
+        tm.mark("build_hist_compute")
         if dist:
             self.comm.allreduce_(self.hist[0:1])
+            tm.mark("build_hist_comm")
         gp = self.gp
         h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                      ptr(self.split_items), 1, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
                      gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
                      ptr(self.split_cnt), s)
+        tm.mark("find_best_split")
         bb = 1 if self.bins.dtype == torch.uint8 else 2
         for d in range(p.max_depth):
             c = d + 1  # depth of the children created at this level
             h.lv_step(1, ptrs, ip, fp, 0, 0, s)  # apply splits + pop nodes of depth d
+            tm.mark("plan")
             npart = self.PART_TARGET + (1 << d) + 1
             last = c == p.max_depth
             rows_in = rows0 if d == 0 else ptr(self.rows)
@@ -274,24 +283,31 @@ class DeviceLevelBuilder:
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
                             ptr(self.left_loc), s)
+            tm.mark("partition")
             if dist:
                 self.left_glob.copy_(self.left_loc)
                 self.comm.allreduce_(self.left_glob)
+                tm.mark("sync_counts")
             base, half = (1 << c) - 1, 1 << (c - 1)
             h.lv_step(3, ptrs, ip, fp, base, half | ((0 if dist else 1) << 30), s)
+            tm.mark("plan")
             if last:
                 break
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
             build_hist(ptr(self.ghp), ptr(self.rows), self.HIST_TARGET + half + 1, base, half)
+            tm.mark("build_hist_compute")
             if dist:
                 self.comm.allreduce_(self.hist[base:base + half])
+                tm.mark("build_hist_comm")
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                          ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
                          gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
                          ptr(self.split_cnt), s)
+            tm.mark("find_best_split")
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
+        tm.mark("plan")
         self.tree_count += 1
         st, nodes, *arrays = self._snap_views(self.snap.clone())
         return DeviceTree(nodes, st, tuple(arrays), self.max_nodes)

@@ -25,7 +25,9 @@ from ...metrics.evaluators import EvalSet
 from ...ops import gbdt as gops
 from ...parallel.comm import Comm
 from ...utils.javafmt import java_double_str as jd
+from ...utils.fault import fault_point
 from ...utils.logging import get_logger
+from ...utils.timestats import PhaseTimer, profiling_enabled
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
 from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder
@@ -90,7 +92,8 @@ class GBDTTrainer:
             self.loss.set_param(sigmoid_zmax=params.sigmoid_zmax)
         self.rf = params.type == "random_forest"
         self.model = model or GBDTModel(params.uniform_base_prediction, self.K, self.loss.name)
-        self.profile = profile
+        self.profile = profiling_enabled(profile or None)
+        self.timer = PhaseTimer(self.dev, self.profile)
         self.kernel_loss = self.loss.gbdt_kernel_id
         self._prepared = False
         self._pending = []          # device trees not yet converted to host Trees
@@ -141,7 +144,8 @@ class GBDTTrainer:
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
                                    and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None)
         if self.use_device_builder:
-            self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm)
+            self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
+                                              timer=self.timer)
         else:
             self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
                                        self.comm, profile=self.profile)
@@ -248,7 +252,14 @@ class GBDTTrainer:
         self.init_gradients()
         start = time.perf_counter()
         for i in range(cur, total_rounds):
+            fault_point("gbdt", i, self.comm.rank)
+            self.timer.begin()
             self.step(i)
+            per = self.timer.end()
+            if per and (self.p.verbose or self.log.enabled_for_round(i)):
+                self.log.info(f"[GBDT] time stats tree {i + 1}: {PhaseTimer.fmt(per)}")
+            elif self.profile and not self.use_device_builder and (self.p.verbose or self.log.enabled_for_round(i)):
+                self.log.info(f"[GBDT] time stats tree {i + 1}: {self.builder.last_stats}")
             if on_round is not None:
                 on_round(i, self)
             # GBDTOptimizer.java:434-435 -- note Java's (i+1) % -1 == 0 dumps every round
@@ -263,6 +274,8 @@ class GBDTTrainer:
         self.total_train_time = time.perf_counter() - start
         final = self.final_eval()
         self.log.info(f"training end, {self.total_train_time:.5f} sec in all\n{final}")
+        if self.profile:
+            self.log.info(self.timer.report() if self.use_device_builder else f"[GBDT] {self.builder.total_stats}")
         return self.model
 
     def _tree_to_dev(self, tree):
@@ -298,6 +311,8 @@ class GBDTTrainer:
                                         + self.init_score[:, k], self.w, lr)
                 host_trees.append(tree)
                 arrays.append(self._tree_to_dev(tree))
+        if not self.use_device_builder:
+            self.timer.mark("build_tree")
         # score update + train loss after this round + gradients for the next round
         if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
             self.ghmax.zero_()
@@ -308,6 +323,7 @@ class GBDTTrainer:
             for k in range(self.K):
                 gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
             acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
+        self.timer.mark("grad_and_score")
         # model conversion (slot -> raw threshold, names, default direction) for host trees
         for tree in host_trees:
             self._convert(tree)
@@ -325,6 +341,7 @@ class GBDTTrainer:
             te = self.test_data
             acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
                                      i + 1, False)
+            self.timer.mark("test_eval")
         self._acc = (acc, acc_te)
         self.rounds_done = i + 1
 
@@ -369,6 +386,10 @@ class GBDTTrainer:
 
     def report(self) -> str:
         tr_loss, te_loss = self._losses()
+        metric = getattr(self.log, "metric", None)
+        if metric is not None:
+            metric(model="gbdt", loss=self.loss.name, round=self.rounds_done, train_loss=tr_loss, test_loss=te_loss,
+                   time_stats=dict(self.timer.last) if self.timer.enabled else None)
         out = [f"train loss = {jd(tr_loss)}\n"]
         if self.p.watch_train:
             out.append(self._eval_str(True))

@@ -4,6 +4,7 @@ from __future__ import annotations
 from ...config.params import CommonParams
 from ...io.fs import create_fs
 from ...optim.lbfgs import HoagOptimizer
+from ...utils.fault import fault_point
 from ..continuous.base import ContinuousDataLoader
 from .model import GBSTModel
 
@@ -26,6 +27,7 @@ def run_gbst(model_name, cfg, comm, log, transform_fn=None, threads=0):
     prev = float("inf")
     res = None
     while True:
+        fault_point("gbst", tree, comm.rank)
         log.info(f"finished tree num:{model.finished}, now constructing treeid:{tree}")
         opt = HoagOptimizer(model, params.line_search, params.loss.l1, params.loss.l2, comm, log,
                             model.data.train.weight_sum,

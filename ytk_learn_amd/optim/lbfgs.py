@@ -29,6 +29,8 @@ import torch
 
 from ..config.params import HyperParams, LineSearchParams
 from ..ops import blas
+from ..utils.fault import fault_point
+from ..utils.timestats import PhaseTimer, profiling_enabled
 from ..utils.javafmt import java_double_str as jd
 
 
@@ -119,6 +121,8 @@ class HoagOptimizer:
         self.hyper_idx = 1
         self.loss_prev = 0.0
         self.pure_prev = 0.0
+        dev = getattr(model, "device", None)
+        self.timer = PhaseTimer(dev if isinstance(dev, torch.device) else None, profiling_enabled())
 
     # ------------------------------------------------------------------ logging
     def _info(self, it: int, msg: str):
@@ -127,6 +131,14 @@ class HoagOptimizer:
         else:
             head = f"[model={self.m.name}] [loss={self.m.loss_name}] [iter={it}] "
         self.log.info(head + self.m.extra_info() + msg)
+
+    def _metric(self, it: int, start: float, test_loss: Optional[float]):
+        metric = getattr(self.log, "metric", None)
+        if metric is not None:
+            metric(model=self.m.name, loss=self.m.loss_name, iter=it, hyper=self.hyper_idx,
+                   train_loss=self.pure_prev / self.W, regularized_loss=self.loss_prev / self.W,
+                   test_loss=(test_loss / self.Wt) if (test_loss is not None and self.Wt > 0) else None,
+                   elapsed=time.perf_counter() - start)
 
     def _verbose(self, it: int, msg: str):
         if getattr(self.log, "verbose", False):
@@ -320,10 +332,13 @@ class HoagOptimizer:
             step = 1.0 / gnorm if gnorm > 0 else 1.0
             cursor = 0
             while True:
+                fault_point("lbfgs", it, getattr(self.comm, "rank", 0))
+                self.timer.begin()
                 wprev.copy_(w)
                 gprev.copy_(g)
                 self._verbose(it, "begin line search...")
                 cnt = self.line_search(it, step, w, wprev, g, gprev, p)
+                self.timer.mark("line_search_loss_grad")
                 if cnt < 0:
                     self._verbose(it, "line search failed, move to prev point!")
                     w.copy_(wprev)
@@ -340,6 +355,8 @@ class HoagOptimizer:
                         best_l1, best_l2 = list(self.l1), list(self.l2)
                     msg += f"test loss = {jd(test_loss / self.Wt)}\n" + self.m.other_test_info() + \
                         self.m.test_eval()
+                    self.timer.mark("test_eval")
+                self._metric(it, start, test_loss)
                 self._info(it, msg)
                 wnorm, gnorm = _norm(w), _norm(g)
                 wnorm = max(wnorm, 1.0)
@@ -371,6 +388,10 @@ class HoagOptimizer:
                 for r, (s, e) in enumerate(self.groups):  # constrain the direction (l1)
                     if self.l1[r] > 0.0 and e > s:
                         p[s:e].masked_fill_(p[s:e] * g[s:e] >= 0.0, 0.0)
+                self.timer.mark("two_loop")
+                per = self.timer.end()
+                if per:
+                    self._info(it, f"time stats: {PhaseTimer.fmt(per)}")
                 step = 1.0
                 it += 1
             self._verbose(it, f"status:{status}")
@@ -395,6 +416,8 @@ class HoagOptimizer:
             self.loss_prev, self.pure_prev = loss, pure
         self._dump(w)
         self._final_report(start, test_loss, it)
+        if self.timer.enabled:
+            self._info(it, self.timer.report())
         return LbfgsResult(self.loss_prev, self.pure_prev, status, it, test_loss, self.l1, self.l2)
 
     def _final_report(self, start, test_loss, it=0):

@@ -52,6 +52,8 @@ class Comm:
         """
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
+        # collective watchdog: a rank stuck longer than this in a collective aborts the job
+        timeout_s = int(os.environ.get("YTK_COMM_TIMEOUT", timeout_s))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"

@@ -75,7 +75,7 @@ def train(model_name: str, conf: Union[str, Config], overrides: Optional[Dict[st
     comm = comm or Comm.from_env(device)
     dev = comm.device
     verbose = cfg.get_bool("verbose", False)
-    log = log or get_logger(comm, verbose=verbose)
+    log = log or get_logger(comm, verbose=verbose, jsonl_path=os.environ.get("YTK_METRICS_JSONL") or None)
     log.info(f"model:{model_name}, world:{comm.world}, device:{dev}")
     transform_fn = load_transform_fn(transform_script)
     t0 = time.perf_counter()
