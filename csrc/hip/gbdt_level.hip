@@ -8,10 +8,10 @@
 // smaller child histogram + sibling subtraction, canSplit (UpdateStrategy:50-53).
 //
 // MI355X design: the decisions of a level (<= 2^depth nodes) run in one 256-thread
-// "planner" workgroup: node fields are staged in LDS by all lanes, the only truly
-// sequential rule (the running leaf count under max_leaf_cnt) is a lane-0 loop over
-// LDS, and the work lists (partition chunks, histogram chunks, split items) are
-// emitted in parallel after block scans. The heavy kernels (partition / histogram /
+// "planner" workgroup: node fields are staged in LDS by all lanes, the FIFO leaf
+// budget (running leaf count under max_leaf_cnt) is a block scan over the candidate
+// flags, and the work lists (partition chunks, histogram chunks, split items) are
+// emitted in parallel after block scans (wave64 shuffle scans, no serial loops). The heavy kernels (partition / histogram /
 // split) are launched with FIXED maximal grids and read their item counts from
 // device memory, so a whole tree is a fixed launch sequence: no device->host
 // synchronisation inside a tree, and multi-GPU all-reduces are fixed-size RCCL calls
@@ -117,33 +117,48 @@ __device__ void reset_node(DNode& n, int depth) {
   n.is_leaf = 1;
 }
 
+// Exclusive scan of one int per thread over the 256-thread block (wave64 shuffles +
+// 4 wave totals through LDS). Returns this thread's exclusive prefix; *total = sum.
+// Must be called by every thread of the block. s_tmp: >= kPlanThreads/64 + 1 ints.
+__device__ __forceinline__ int block_scan_excl(int v, int* s_tmp, int* total) {
+  const int tid = threadIdx.x, l = tid & (kWave - 1), w = tid >> 6;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int o = __shfl_up(inc, off, kWave);
+    if (l >= off) inc += o;
+  }
+  if (l == kWave - 1) s_tmp[w] = inc;
+  __syncthreads();
+  int before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kPlanThreads / kWave; ++k) {
+    const int t = s_tmp[k];
+    if (k < w) before += t;
+    all += t;
+  }
+  __syncthreads();  // s_tmp reusable afterwards
+  *total = all;
+  return before + inc - v;
+}
+
 // In-place exclusive scan of a[0..n) (n <= kMaxPend) by one 256-thread block.
-// Returns the total. Each thread scans a contiguous run, then the run totals.
+// Returns the total. Each thread owns a contiguous run of ceil(n/256) entries; the
+// run totals are scanned with wave shuffles (no serial lane-0 loop: the old
+// 256-step LDS chain cost ~10 us per planner launch).
 __device__ int block_exclusive_scan(int* a, int n, int* s_tmp) {
   const int tid = threadIdx.x;
   const int per = (n + kPlanThreads - 1) / kPlanThreads;
   const int b = min(n, tid * per), e = min(n, b + per);
   int run = 0;
   for (int i = b; i < e; ++i) run += a[i];
-  s_tmp[tid] = run;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int i = 0; i < kPlanThreads; ++i) {
-      const int v = s_tmp[i];
-      s_tmp[i] = acc;
-      acc += v;
-    }
-    s_tmp[kPlanThreads] = acc;
-  }
-  __syncthreads();
-  int acc = s_tmp[tid];
+  int total;
+  int acc = block_scan_excl(run, s_tmp, &total);
   for (int i = b; i < e; ++i) {
     const int v = a[i];
     a[i] = acc;
     acc += v;
   }
-  const int total = s_tmp[kPlanThreads];
   __syncthreads();
   return total;
 }
@@ -200,16 +215,26 @@ __global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBuf
 }
 
 // Apply split results, pop the level's nodes in FIFO order, emit partition chunks.
-__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b) {
-  __shared__ float s_chg[kMaxPend];
-  __shared__ int s_aux[kMaxPend];       // depth, later: split index / -1
-  __shared__ long long s_cnt[kMaxPend];
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b, int fused) {
+  __shared__ int s_aux[kMaxPend];   // candidate flag, later: split index / -1
+  __shared__ int s_rank[kMaxPend];  // rank among the candidates (FIFO order)
   __shared__ int s_tmp[kPlanThreads + 1];
-  __shared__ int s_nsplit, s_num_nodes0;
   __shared__ long long s_total;
   int* st = b.st;
   const int tid = threadIdx.x;
   const double mcw2 = (double)p.mcw * 2.0;
+  // 0. fused counts: the children of the previous level's splits get their global row
+  //    counts from the (now all-reduced) count slots
+  if (fused) {
+    const int nprev = st[ST_N_SPLIT];
+    for (int s = tid; s < nprev; s += kPlanThreads) {
+      const DNode& P = b.nodes[b.split_nid[s]];
+      const long long lg = b.left_glob[s];
+      b.nodes[P.left].cnt_global = lg;
+      b.nodes[P.right].cnt_global = P.cnt_global - lg;
+    }
+    __syncthreads();
+  }
   // 1. apply split-finder results to the node table (canSplit)
   const int nsi = st[ST_N_SITEMS];
   for (int i = tid; i < nsi; i += kPlanThreads) {
@@ -229,55 +254,46 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
     }
   }
   __syncthreads();
-  // 2. stage the pending nodes' decision inputs in LDS
+  // 2. pop-time leaf rules that do not depend on the running leaf count
   const int npend = st[ST_N_PENDING];
+  const int num_nodes0 = st[ST_NUM_NODES], num_leaf0 = st[ST_NUM_LEAF];
   for (int i = tid; i < npend; i += kPlanThreads) {
     const DNode& n = b.nodes[b.pending[i]];
-    s_chg[i] = n.loss_chg;
-    s_aux[i] = n.depth;
-    s_cnt[i] = n.cnt_global;
+    const bool leaf = !(n.loss_chg > p.min_split_loss) ||
+                      (p.max_depth >= 0 && p.max_depth == n.depth) ||
+                      (p.min_split_samples > 0 && n.cnt_global < p.min_split_samples);
+    s_aux[i] = leaf ? 0 : 1;
+    s_rank[i] = leaf ? 0 : 1;
   }
   if (tid == 0) s_total = 0;
   __syncthreads();
-  // 3. sequential FIFO decisions (running leaf count) on LDS data
+  // 3. FIFO leaf budget, in parallel: the running leaf count before candidate i is
+  // num_leaf0 + rank(i) (each split adds one leaf) and the reference makes a node a
+  // leaf once that count == max_leaf_cnt, so exactly the first
+  // (max_leaf_cnt - num_leaf0) candidates split.
+  const int ncand = block_exclusive_scan(s_rank, npend, s_tmp);
+  const int limit = (p.max_leaf_cnt > 0 && num_leaf0 <= p.max_leaf_cnt) ? p.max_leaf_cnt - num_leaf0
+                                                                         : 0x7fffffff;
+  const int nsplit = min(ncand, limit);
   if (tid == 0) {
-    int num_nodes = st[ST_NUM_NODES], num_leaf = st[ST_NUM_LEAF], nsplit = 0;
-    s_num_nodes0 = num_nodes;
-    for (int i = 0; i < npend; ++i) {
-      const bool leaf = !(s_chg[i] > p.min_split_loss) ||
-                        (p.max_depth >= 0 && p.max_depth == s_aux[i]) ||
-                        (p.max_leaf_cnt > 0 && p.max_leaf_cnt == num_leaf) ||
-                        (p.min_split_samples > 0 && s_cnt[i] < p.min_split_samples);
-      if (leaf) {
-        s_aux[i] = -1;
-      } else {
-        num_leaf += 1;
-        s_aux[i] = nsplit;
-        s_cnt[i] = num_leaf;  // snapshot of the leaf count after this split
-        ++nsplit;
-      }
-    }
-    st[ST_NUM_NODES] = num_nodes + 2 * nsplit;
-    st[ST_NUM_LEAF] = num_leaf;
+    st[ST_NUM_NODES] = num_nodes0 + 2 * nsplit;
+    st[ST_NUM_LEAF] = num_leaf0 + nsplit;
     st[ST_N_SPLIT] = nsplit;
-    s_nsplit = nsplit;
   }
-  __syncthreads();
   // 4. write decisions back; per-split partition descriptors
-  const int nsplit = s_nsplit;
   for (int i = tid; i < npend; i += kPlanThreads) {
     const int id = b.pending[i];
     DNode& n = b.nodes[id];
-    const int s = s_aux[i];
+    const int s = (s_aux[i] && s_rank[i] < limit) ? s_rank[i] : -1;
     if (s < 0) {
       n.is_leaf = 1;
       n.value = leaf_value(n.G, n.H, p);
     } else {
       n.is_leaf = 0;
-      n.left = s_num_nodes0 + 2 * s;
-      n.right = s_num_nodes0 + 2 * s + 1;
+      n.left = num_nodes0 + 2 * s;
+      n.right = num_nodes0 + 2 * s + 1;
       b.split_nid[s] = id;
-      b.split_snap[s] = (int)s_cnt[i];
+      b.split_snap[s] = num_leaf0 + s + 1;  // leaf count after this split
       b.part_feat[s] = n.feat;
       b.part_thr[s] = (n.bin_a + n.bin_b) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
       b.part_begin[s] = n.begin;
@@ -305,9 +321,15 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
 }
 
 // Children of this level's splits: segments, terminal check, build / derive lists,
-// histogram chunks. build_base: first slot of this level, half: slots for builds.
+// histogram chunks. build_base: first slot of this level, half: slots for builds,
+// dgap: derived slot = built slot + dgap (half, plus the count slots when fused).
+// fused (multi-GPU, min_split_samples <= 0): the left counts are still LOCAL here --
+// they ride in count slots of the level's histogram all-reduce -- so the smaller child
+// is chosen by the (globally identical) hessian sums and cnt_global is patched by the
+// next lv_plan_split. Exact int64 histograms make the choice result-neutral.
 __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base,
-                                                                    int half, int use_loc) {
+                                                                    int half, int dgap, int use_loc,
+                                                                    int fused) {
   __shared__ int s_nb[kMaxPend];     // 1 if the split's children get histograms
   __shared__ int s_small[kMaxPend];  // small child node id
   __shared__ int s_tmp[kPlanThreads + 1];
@@ -343,7 +365,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
       R.value = leaf_value(R.G, R.H, p);
       s_nb[s] = 0;
     } else {
-      const bool left_small = L.cnt_global < R.cnt_global;
+      const bool left_small = fused ? (P.hl < P.H - P.hl) : (L.cnt_global < R.cnt_global);
       s_small[s] = left_small ? P.left : P.right;
       s_nb[s] = 1;
       atomicAdd(reinterpret_cast<unsigned long long*>(&s_total),
@@ -366,7 +388,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
     DNode& S = b.nodes[small_id];
     DNode& Lg = b.nodes[large_id];
     S.slot = build_base + k;
-    Lg.slot = build_base + half + k;
+    Lg.slot = build_base + dgap + k;
     b.split_items[k] = make_int4(S.slot, 0, 0, 0);
     b.item_nid[k] = small_id;
     b.split_items[nb + k] = make_int4(Lg.slot, P.slot, S.slot, 1);
@@ -503,7 +525,9 @@ static LvBufs make_bufs(const uintptr_t* a) {
 
 extern "C" {
 
-// which: 0 init, 1 plan_split, 3 plan_children(arg0=build_base, arg1=half | use_loc<<30),
+// which: 0 init, 1 plan_split (arg1 = fused: patch the previous level's cnt_global from
+//        left_glob), 3 plan_children(arg0=build_base, arg1=half | ncs<<14 | fused<<29 |
+//        use_loc<<30; derived slots start at build_base + half + ncs),
 //        4 finalize(arg0=max_nodes)
 void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* fp, int arg0,
                  int arg1, uintptr_t stream) {
@@ -524,10 +548,11 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
     case 0: hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
-    case 1: hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
+    case 1: hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1); break;
     case 3:
       hipLaunchKernelGGL(lv_plan_children_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg0,
-                         arg1 & 0x3fffffff, (arg1 >> 30) & 1);
+                         arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), (arg1 >> 30) & 1,
+                         (arg1 >> 29) & 1);
       break;
     case 4: hipLaunchKernelGGL(lv_finalize_kernel, dim3(1), dim3(256), 0, s, b, arg0); break;
     default: throw std::runtime_error("bad lv step");

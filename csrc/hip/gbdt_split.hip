@@ -16,6 +16,8 @@
 // fused into the load (exact in int64) and written back for the node's children.
 #include "common.h"
 
+#include <rocprim/block/block_scan.hpp>
+
 namespace ytk {
 
 struct SplitOut {
@@ -86,13 +88,15 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
 }
 
 // hist: int64 [slot][B][F][2]. items[blk] = {slot, parent_slot, sibling_slot, derived}
-constexpr int kSplitWaves = 8;  // 512 threads: 3-4 features per wave at F=28 (latency bound)
+constexpr int kSplitWaves = 8;   // 512 threads (<= 256 VGPRs): one block covers F <= 32 (<= 4 / wave)
+constexpr int kFPW = 4;          // features per wave per block (hoisted loads)
 
-// Grid (items, feature groups): block y owns features y*kSplitWaves + wave (one wave per
-// feature when F <= groups*8), so a level's nodes fill many CUs instead of one block each
-// walking ~F/8 features serially. With more than one group, every block writes its best
-// candidate to part[item][group]; the last block of an item (device-scope counter)
-// combines them with the same lexicographic tie-break and resets the counter.
+// Latency design (a level's split search is a chain of dependent memory round trips,
+// not bandwidth): each wave issues the loads of ALL its features (<= 4) plus the
+// node-total feature up front -- one HBM/L2 round trip -- then scans/evaluates from
+// registers. With F <= 32 one block owns a whole node: no cross-block combine.
+// For F > 32 the features are spread over gridDim.y blocks and the last block of an
+// item (device-scope counter) combines the per-block candidates (same tie-break).
 __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
@@ -105,7 +109,6 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
 
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   const int ngroups = (int)gridDim.y;
-  const int fstart = (int)blockIdx.y * kSplitWaves;
   const int fstep = ngroups * kSplitWaves;
   if (inv_dev) {
     gp.inv_sg = inv_dev[0];
@@ -129,12 +132,49 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
     return hn[idx];
   };
 
-  // Node totals from the first sampled feature (exact; every wave computes them).
-  long long Gq = 0, Hq = 0;
+  // this wave's features: fw[j] = blockIdx.y*kSplitWaves + wid + j*fstep
+  int fw[kFPW];
+  int nfw = 0;
+#pragma unroll
+  for (int j = 0; j < kFPW; ++j) {
+    const int f = (int)blockIdx.y * kSplitWaves + wid + j * fstep;
+    fw[j] = f;
+    if (f < F) nfw = j + 1;
+  }
+  const bool one_chunk = B <= 4 * kWave;
+
+  // ---- one batch of loads: node-total feature f0 + the first chunk of every feature
+  longlong2 v0[4];
+  longlong2 vf[kFPW][4];
   {
     const int nb0 = nbins_f[f0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int bin = l + k * kWave;  // strided: only a sum is needed
+      v0[k] = (bin < nb0 && bin < B) ? load(f0, bin) : make_longlong2(0, 0);
+    }
+  }
+  if (one_chunk) {
+#pragma unroll
+    for (int j = 0; j < kFPW; ++j) {
+      const int f = fw[j];
+      const int nb = (j < nfw && fmask[f]) ? nbins_f[f] : 0;
+      const int nbd = (j < nfw) ? B : 0;  // derived write-back covers every bin
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bin = 4 * l + k;
+        vf[j][k] = make_longlong2(0, 0);
+        if (bin < nb || (derived && bin < nbd)) vf[j][k] = load(f, bin);
+      }
+    }
+  }
+  // node totals (exact int64; the first sampled feature, DataParallelTreeMaker:543-573)
+  long long Gq, Hq;
+  {
     long long sg = 0, sh = 0;
-    for (int bin = l; bin < nb0; bin += kWave) {
+    const int nb0 = nbins_f[f0];
+    for (int k = 0; k < 4; ++k) { sg += v0[k].x; sh += v0[k].y; }
+    for (int bin = l + 4 * kWave; bin < nb0; bin += kWave) {  // B > 256 only
       const longlong2 v = load(f0, bin);
       sg += v.x;
       sh += v.y;
@@ -149,8 +189,11 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
   int best_f = 0x7fffffff, best_a = -1, best_b = 0x7fffffff;
   double best_gl = 0.0, best_hl = 0.0;
 
-  for (int f = fstart + wid; f < F; f += fstep) {
-    if (!fmask[f]) continue;
+#pragma unroll
+  for (int j = 0; j < kFPW; ++j) {
+    const int f = fw[j];
+    const bool on = j < nfw && fmask[f] != 0;
+    if (j >= nfw || (!on && !derived)) continue;
     const int nb = nbins_f[f];
     long long carry_g = 0, carry_h = 0;
     int carry_last = -1;
@@ -161,13 +204,19 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int bin = c + 4 * l + k;
-        v[k] = make_longlong2(0, 0);
-        if (bin < nb) v[k] = load(f, bin);
+        if (one_chunk) {
+          v[k] = vf[j][k];
+        } else {
+          v[k] = make_longlong2(0, 0);
+          if ((on && bin < nb) || (derived && bin < B)) v[k] = load(f, bin);
+        }
         if (derived && bin < B) hn[(size_t)bin * F + f] = v[k];
+        if (!on || bin >= nb) v[k] = make_longlong2(0, 0);
         sg += v[k].x;
         sh += v[k].y;
         if (v[k].x != 0 || v[k].y != 0) lastne = bin;
       }
+      if (!on) continue;  // derived write-back only
       const long long ig = wave_incl_scan_ll(sg);
       const long long ih = wave_incl_scan_ll(sh);
       const int im = wave_incl_max(lastne);
@@ -261,12 +310,178 @@ __global__ __launch_bounds__(kSplitWaves * 64) void split_find_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// One block per (node, feature), one bin per thread (B <= 256) -- the default path.
+// A level's split search is latency bound (tiny data, dependent steps), so the work is
+// spread as wide as possible: nodes x F blocks; every block does ONE load round trip
+// (its feature's bins + the node-total feature f0's bins), one rocPRIM (DPP) block scan
+// of (g, h, last-non-empty-bin), the gain of its bin, and a block argmax. The last
+// block of a node (device-scope counter) combines the F per-feature candidates with the
+// reference tie-break (max lossChg, then lower feature, then lower bin).
+struct ScanT {
+  long long g, h;
+  int last;
+};
+struct ScanOp {
+  __device__ __forceinline__ ScanT operator()(const ScanT& a, const ScanT& b) const {
+    return ScanT{a.g + b.g, a.h + b.h, max(a.last, b.last)};
+  }
+};
+constexpr int kFeatThreads = 256;
+using FeatScan = rocprim::block_scan<ScanT, kFeatThreads>;
+
+__global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
+    long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
+    const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
+    SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters) {
+  __shared__ typename FeatScan::storage_type s_scan;
+  __shared__ long long s_tg[kFeatThreads / kWave], s_th[kFeatThreads / kWave];
+  __shared__ float s_chg[kFeatThreads / kWave];
+  __shared__ int s_bin[kFeatThreads / kWave], s_a[kFeatThreads / kWave];
+  __shared__ double s_gl[kFeatThreads / kWave], s_hl[kFeatThreads / kWave];
+  __shared__ int s_last;
+  __shared__ SplitOut s_part[64];
+
+  if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
+  if (inv_dev) {
+    gp.inv_sg = inv_dev[0];
+    gp.inv_sh = inv_dev[1];
+  }
+  const int f = (int)blockIdx.y;
+  const int t = threadIdx.x, wid = t >> 6, l = lane_id();
+  const int4 it = items[blockIdx.x];
+  const size_t slot_sz = (size_t)B * F * 2;
+  longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
+  const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
+  const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
+  const bool derived = it.w != 0;
+  auto load = [&](int ff, int bin) -> longlong2 {
+    const size_t idx = (size_t)bin * F + ff;
+    if (derived) {
+      const longlong2 p = hp[idx], s = hs[idx];
+      return make_longlong2(p.x - s.x, p.y - s.y);
+    }
+    return hn[idx];
+  };
+  const int nb = nbins_f[f], nb0 = nbins_f[f0];
+  const bool on = fmask[f] != 0;
+  // ---- one load round trip
+  longlong2 v = make_longlong2(0, 0), v0 = make_longlong2(0, 0);
+  if (t < B && (derived || (on && t < nb))) v = load(f, t);
+  if (f != f0 && t < nb0) v0 = load(f0, t);
+  if (derived && t < B) hn[(size_t)t * F + f] = v;  // materialise the derived histogram
+  if (f == f0) v0 = (t < nb0) ? v : make_longlong2(0, 0);
+  // ---- node totals (exact int64, first sampled feature: DataParallelTreeMaker:543-573)
+  {
+    const long long sg = wave_sum_ll(v0.x), sh = wave_sum_ll(v0.y);
+    if (l == 0) { s_tg[wid] = sg; s_th[wid] = sh; }
+  }
+  __syncthreads();
+  long long Gq = 0, Hq = 0;
+#pragma unroll
+  for (int w = 0; w < kFeatThreads / kWave; ++w) { Gq += s_tg[w]; Hq += s_th[w]; }
+  const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
+
+  float best_chg = -INFINITY;
+  int best_b = 0x7fffffff, best_a = -1;
+  double best_gl = 0.0, best_hl = 0.0;
+  if (on) {  // block-uniform
+    if (t >= nb) v = make_longlong2(0, 0);
+    const bool ne = (v.x != 0 || v.y != 0);
+    ScanT ex;
+    FeatScan().exclusive_scan(ScanT{v.x, v.y, ne ? t : -1}, ex, ScanT{0, 0, -1}, s_scan, ScanOp());
+    if (ne && ex.last >= 0 && ex.h != 0) {
+      const double dgl = (double)ex.g * gp.inv_sg, dhl = (double)ex.h * gp.inv_sh;
+      const double dgr = (double)(Gq - ex.g) * gp.inv_sg, dhr = (double)(Hq - ex.h) * gp.inv_sh;
+      if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
+        const float root_gain = (float)calc_gain(G, H, gp);
+        best_chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
+        best_b = t;
+        best_a = ex.last;
+        best_gl = dgl;
+        best_hl = dhl;
+      }
+    }
+  }
+  // ---- block argmax (chg desc, bin asc)
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const float oc = __shfl_xor(best_chg, off, kWave);
+    const int ob = __shfl_xor(best_b, off, kWave);
+    const int oa = __shfl_xor(best_a, off, kWave);
+    const double ogl = __shfl_xor(best_gl, off, kWave);
+    const double ohl = __shfl_xor(best_hl, off, kWave);
+    if (better(oc, 0, ob, best_chg, 0, best_b)) {
+      best_chg = oc; best_b = ob; best_a = oa; best_gl = ogl; best_hl = ohl;
+    }
+  }
+  if (l == 0) {
+    s_chg[wid] = best_chg; s_bin[wid] = best_b; s_a[wid] = best_a; s_gl[wid] = best_gl; s_hl[wid] = best_hl;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int bw = 0;
+    for (int w = 1; w < kFeatThreads / kWave; ++w)
+      if (better(s_chg[w], 0, s_bin[w], s_chg[bw], 0, s_bin[bw])) bw = w;
+    SplitOut o;
+    o.loss_chg = s_chg[bw];
+    o.feat = (s_bin[bw] == 0x7fffffff) ? 0x7fffffff : f;
+    o.bin_a = s_a[bw];
+    o.bin_b = s_bin[bw];
+    o.gl = s_gl[bw];
+    o.hl = s_hl[bw];
+    o.g = G;
+    o.h = H;
+    part[(size_t)blockIdx.x * F + f] = o;
+    __threadfence();
+    const int prev = atomicAdd(&counters[blockIdx.x], 1);
+    s_last = (prev == F - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // ---- last block of the node: combine the F feature candidates (64 per pass)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  SplitOut best;
+  best.loss_chg = -INFINITY;
+  best.feat = 0x7fffffff;
+  best.bin_a = -1;
+  best.bin_b = 0x7fffffff;
+  best.gl = best.hl = 0.0;
+  for (int c0 = 0; c0 < F; c0 += 64) {
+    const int n = min(64, F - c0);
+    if (t < n) {
+      const volatile SplitOut* pp = part + (size_t)blockIdx.x * F + c0 + t;
+      SplitOut q;
+      q.loss_chg = pp->loss_chg; q.feat = pp->feat; q.bin_a = pp->bin_a; q.bin_b = pp->bin_b;
+      q.gl = pp->gl; q.hl = pp->hl; q.g = pp->g; q.h = pp->h;
+      s_part[t] = q;
+    }
+    __syncthreads();
+    if (t == 0)
+      for (int y = 0; y < n; ++y)
+        if (better(s_part[y].loss_chg, s_part[y].feat, s_part[y].bin_b, best.loss_chg, best.feat, best.bin_b))
+          best = s_part[y];
+    __syncthreads();
+  }
+  if (t == 0) {
+    counters[blockIdx.x] = 0;
+    best.g = G;
+    best.h = H;
+    if (best.feat == 0x7fffffff) best.feat = -1;
+    if (best.bin_b == 0x7fffffff) best.bin_b = -1;
+    out[blockIdx.x] = best;
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
 
-// part / counters (optional): scratch of nitems * ceil(F/8) SplitOut and nitems zeroed ints;
-// when given, the features of a node are spread over ceil(F/8) blocks.
+// part / counters (optional): scratch of nitems * F SplitOut and nitems zeroed ints. With
+// them and B <= 256 the (node, feature)-parallel kernel runs; otherwise the wave-per-
+// feature kernel (features spread over ceil(F/32) blocks when the scratch is given).
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
                                int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
                                float l1, float l2, float max_abs_leaf, double inv_sg,
@@ -274,7 +489,21 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
                                uintptr_t part, uintptr_t counters, uintptr_t stream) {
   if (nitems <= 0) return;
   GainParams gp{mcw, l1, l2, max_abs_leaf, inv_sg, inv_sh};
-  const int groups = (part && counters) ? (F + kSplitWaves - 1) / kSplitWaves : 1;
+  if (B <= kFeatThreads && part && counters) {
+    // part: >= nitems * F SplitOut; counters: nitems zeroed ints
+    hipLaunchKernelGGL(split_feat_kernel, dim3(nitems, F), dim3(kFeatThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
+                       (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
+                       (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev,
+                       (SplitOut*)part, (int*)counters);
+    YTK_LAUNCH_CHECK();
+    return;
+  }
+  // F <= 32: one block per node; otherwise ceil(F / 32) blocks combined via part/counters
+  const int need = (F + kSplitWaves * kFPW - 1) / (kSplitWaves * kFPW);
+  if (need > 1 && !(part && counters))
+    throw std::invalid_argument("split_find: F > 32 needs the part/counters scratch");
+  const int groups = need;
   hipLaunchKernelGGL(split_find_kernel, dim3(nitems, groups), dim3(kSplitWaves * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,

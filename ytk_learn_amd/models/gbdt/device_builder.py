@@ -116,13 +116,32 @@ class DeviceLevelBuilder:
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)
         self.split_out = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
-        # split_find spreads a node's features over ceil(F/8) blocks: per-group candidates +
-        # per-item arrival counters (reset by the combining block)
-        self.split_part = torch.zeros(2 * self.maxp * ((F + 7) // 8) * 48, dtype=torch.uint8, device=dev)
+        # split_find runs one block per (node, feature): per-feature candidates + per-item
+        # arrival counters (reset by the combining block)
+        self.split_part = torch.zeros(2 * self.maxp * F * 48, dtype=torch.uint8, device=dev)
         self.split_cnt = torch.zeros(2 * self.maxp, dtype=torch.int32, device=dev)
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.n_slots = (1 << D) - 1
+        # Histogram slots. Level c (children at depth c, 1 <= c < D) owns `half = 2^(c-1)`
+        # built slots, then `ncs` count slots, then `half` derived slots; the root is slot 0.
+        # Multi-GPU with fused counts: the partition kernel accumulates the level's per-split
+        # left-row counts straight into the count slots, so ONE all-reduce of
+        # [built slots + count slots] carries the histograms and the counts of the level
+        # (reference: DataParallelTreeMaker.java:518,538 count allreduce + HistogramBuilder
+        # .java:95 reduce-scatter -> one fixed-size RCCL call).
+        self.fuse_counts = (self.comm.is_dist and p.min_split_samples <= 0
+                            and os.environ.get("YTK_FUSE_COUNTS", "1") != "0")
+        slot_elems = B * F * 2
+        self.ncs = -(-self.maxp // slot_elems) if self.fuse_counts else 0
+        self.level_slots = {}
+        nxt = 1
+        for c in range(1, D):
+            half = 1 << (c - 1)
+            self.level_slots[c] = (nxt, nxt + half, nxt + half + self.ncs)  # build, count, derived
+            nxt += 2 * half + self.ncs
+        self.n_slots = max(1, nxt)
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
+        self._slot_bytes = slot_elems * 8
+        self._n_global = None
         # staged histogram flush: block partials to a staging slab with plain stores, then a
         # split-K slot reduce (8 int64 atomics per value instead of one per block)
         groups = (F + 31) // 32
@@ -159,13 +178,22 @@ class DeviceLevelBuilder:
         return [float(np.float32(v)) for v in (p.min_split_loss, p.min_child_hessian_sum, p.l1, p.l2,
                                               p.max_abs_leaf_val, p.learning_rate)]
 
-    def _ptrs(self):
-        return [ptr(t) for t in (self.st, self.nodes, self.pending, self.next_pending, self.split_nid,
-                                 self.split_snap, self.part_items, self.part_feat, self.part_thr,
-                                 self.part_begin, self.part_first, self.part_nblk, self.part_counts,
-                                 self.left_loc, self.left_glob, self.hist_items, self.split_items,
-                                 self.item_nid, self.split_out, self.tfeat, self.tthr, self.tleft,
-                                 self.tright, self.tval, self.root_cnt)]
+    def _count_ptr(self, c: int) -> int:
+        """Device address of level c's count slots (fused-count mode)."""
+        return ptr(self.hist) + self.level_slots[c][1] * self._slot_bytes
+
+    def _ptrs(self, loc: int = None, glob: int = None):
+        out = [ptr(t) for t in (self.st, self.nodes, self.pending, self.next_pending, self.split_nid,
+                                self.split_snap, self.part_items, self.part_feat, self.part_thr,
+                                self.part_begin, self.part_first, self.part_nblk, self.part_counts,
+                                self.left_loc, self.left_glob, self.hist_items, self.split_items,
+                                self.item_nid, self.split_out, self.tfeat, self.tthr, self.tleft,
+                                self.tright, self.tval, self.root_cnt)]
+        if loc is not None:
+            out[13] = loc
+        if glob is not None:
+            out[14] = glob
+        return out
 
     def _fmask(self, rng):
         p = self.p
@@ -218,7 +246,13 @@ class DeviceLevelBuilder:
         fmask, f0 = self._fmask(rng)
         self.root_cnt[1] = self.root_cnt[0]
         if dist:
-            self.comm.allreduce_(self.root_cnt[1:2])
+            if sampled:
+                self.comm.allreduce_(self.root_cnt[1:2])
+            else:  # the global row count is fixed: one all-reduce for the whole run
+                if self._n_global is None:
+                    self._n_global = self.root_cnt[1:2].clone()
+                    self.comm.allreduce_(self._n_global)
+                self.root_cnt[1:2].copy_(self._n_global)
         # fixed-point scales from the global max |g|, |h| over the tree's rows
         if sampled:
             mx = (gh.abs() * keep[:, None]).amax(dim=0)
@@ -264,32 +298,50 @@ class DeviceLevelBuilder:
                      ptr(self.split_cnt), s)
         tm.mark("find_best_split")
         bb = 1 if self.bins.dtype == torch.uint8 else 2
+        fused = self.fuse_counts
         for d in range(p.max_depth):
             c = d + 1  # depth of the children created at this level
-            h.lv_step(1, ptrs, ip, fp, 0, 0, s)  # apply splits + pop nodes of depth d
+            last = c == p.max_depth
+            if fused:
+                # split counters of this level accumulate into level c's count slots; the
+                # previous level's (all-reduced) count slots patch cnt_global of depth d
+                loc = self.left_loc if last else None
+                ptrs = self._ptrs(loc=ptr(loc) if loc is not None else self._count_ptr(c),
+                                  glob=self._count_ptr(d) if d >= 1 else None)
+            h.lv_step(1, ptrs, ip, fp, 0, 1 if (fused and d >= 1) else 0, s)  # apply splits + pop depth d
             tm.mark("plan")
             npart = self.PART_TARGET + (1 << d) + 1
-            last = c == p.max_depth
+            lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
             # the flag kernel also accumulates the per-split left totals into left_loc
             if last:
                 h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.flags),
                                   ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),
-                                  ptr(self.part_counts), off(4), ptr(self.left_loc), s)
+                                  ptr(self.part_counts), off(4), lloc, s)
             else:
                 h.partition(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
                             gh_in, ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
-                            ptr(self.left_loc), s)
+                            lloc, s)
             tm.mark("partition")
-            if dist:
+            lvl_fused = fused and not last
+            if dist and not lvl_fused:
                 self.left_glob.copy_(self.left_loc)
                 self.comm.allreduce_(self.left_glob)
                 tm.mark("sync_counts")
-            base, half = (1 << c) - 1, 1 << (c - 1)
-            h.lv_step(3, ptrs, ip, fp, base, half | ((0 if dist else 1) << 30), s)
+            half = 1 << (c - 1)
+            if last:
+                base, ncs = 0, 0  # no histograms at the last level
+            else:
+                base, cbase, dbase = self.level_slots[c]
+                ncs = dbase - cbase
+            use_loc = (not dist) or lvl_fused
+            if fused and last:  # the last level reads the separately all-reduced counts
+                ptrs = self._ptrs()
+            h.lv_step(3, ptrs, ip, fp, base,
+                      half | (ncs << 14) | ((1 if lvl_fused else 0) << 29) | ((1 if use_loc else 0) << 30), s)
             tm.mark("plan")
             if last:
                 break
@@ -299,7 +351,8 @@ class DeviceLevelBuilder:
             build_hist(ptr(self.ghp), ptr(self.rows), self.HIST_TARGET + half + 1, base, half)
             tm.mark("build_hist_compute")
             if dist:
-                self.comm.allreduce_(self.hist[base:base + half])
+                # built slots (+ this level's count slots when fused): one all-reduce
+                self.comm.allreduce_(self.hist[base:base + half + ncs])
                 tm.mark("build_hist_comm")
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                          ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],

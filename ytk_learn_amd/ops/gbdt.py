@@ -121,8 +121,7 @@ def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
         if n == 0:
             return out
         check_cuda(hist, nbins_f, fmask, items)
-        groups = (F + 7) // 8
-        part = torch.empty((n * groups, 48), dtype=torch.uint8, device=hist.device)
+        part = torch.empty((n * F, 48), dtype=torch.uint8, device=hist.device)
         counters = torch.zeros(n, dtype=torch.int32, device=hist.device)
         hip().split_find(ptr(hist), B, F, ptr(nbins_f), ptr(fmask), int(f0), ptr(items), n,
                          ptr(out), mcw, l1, l2, mal, inv_sg, inv_sh, 0, 0, ptr(part), ptr(counters),
