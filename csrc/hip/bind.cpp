@@ -13,7 +13,7 @@ extern "C" {
 void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
                  float, float, uintptr_t, uintptr_t, uintptr_t);
 void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
-                        int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+                        int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip
@@ -21,6 +21,7 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
                     uintptr_t, uintptr_t);
 // gbdt_partition.hip
+void ytk_segment_copy(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
@@ -73,6 +74,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("split_find", &ytk_split_find);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
+  m.def("segment_copy", &ytk_segment_copy);
   m.def("tree_add_bins", &ytk_tree_add_bins);
   m.def("forest_predict", &ytk_forest_predict);
   m.def("bin_assign", &ytk_bin_assign);

@@ -135,20 +135,35 @@ constexpr int kReduceSplit = 8;
 __global__ __launch_bounds__(256) void hist_reduce_kernel(
     const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
     const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
-    int groups, int slot_base) {
+    int groups, int slot_base, const int* __restrict__ slot_ids) {
   __shared__ int s_sel[1024];
+  __shared__ int s_wcnt[4];
   __shared__ int s_n;
   const int n = nwork_dev ? min(*nwork_dev, nwork) : nwork;
-  const int slot = slot_base + (int)blockIdx.y / groups;
+  // slot_ids (optional): explicit, possibly non-contiguous target slots (recycled slot pool)
+  const int slot = slot_ids ? slot_ids[(int)blockIdx.y / groups] : slot_base + (int)blockIdx.y / groups;
   const int fg = (int)blockIdx.y % groups;
-  if (threadIdx.x == 0) s_n = 0;
+  // Ordered (stable) compaction of this slot's items: the kReduceSplit blocks of a slot
+  // each take a strided subset s_sel[z], s_sel[z + 8], ..., so every block must see the
+  // SAME order (an LDS-atomic compaction orders items differently per block whenever a
+  // slot's items straddle waves, dropping and double counting items).
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_n = 0;
   __syncthreads();
-  for (int k = threadIdx.x; k < n; k += blockDim.x)
-    if (work[k].x == slot) {
-      const int p = atomicAdd(&s_n, 1);
-      if (p < 1024) s_sel[p] = k;
-    }
-  __syncthreads();
+  for (int k0 = 0; k0 < n; k0 += 256) {
+    const int k = k0 + tid;
+    const bool m = k < n && work[k].x == slot;
+    const unsigned long long bal = __ballot(m);
+    if (lane == 0) s_wcnt[wid] = __popcll(bal);
+    __syncthreads();
+    int off = s_n;
+    for (int w = 0; w < wid; ++w) off += s_wcnt[w];
+    const int p = off + __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    if (m && p < 1024) s_sel[p] = k;
+    __syncthreads();
+    if (tid == 0) s_n += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    __syncthreads();
+  }
   const int cnt = min(s_n, 1024);
   const int E = nb_lds * 32;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -231,11 +246,12 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
 }
 
 // Staged variant: block partials to ``staging`` (>= nwork * groups * B * 32 * 16 bytes),
-// then accumulated into the slots [slot_base, slot_base + nslots), which must be zero.
+// then accumulated into the slots [slot_base, slot_base + nslots) -- or slot_ids[0..nslots)
+// when given -- which must be zero.
 void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
                         uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
                         uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
-                        int slot_base, int nslots, uintptr_t stream) {
+                        int slot_base, int nslots, uintptr_t slot_ids, uintptr_t stream) {
   if (nwork <= 0 || nslots <= 0) return;
   const int groups = (F + 31) / 32;
   const int nb_lds = B;
@@ -257,7 +273,7 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   const int E = nb_lds * 32;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
-                     (long long*)hist, B, F, nb_lds, groups, slot_base);
+                     (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids);
   YTK_LAUNCH_CHECK();
 }
 

@@ -208,3 +208,25 @@ extern "C" void ytk_partition(uintptr_t binsT, int bin_bytes, long long ncol, ui
                      (int*)left_total, (const int*)nitems_dev);
   YTK_LAUNCH_CHECK();
 }
+
+// Copy-back of partitioned segments (loss-guided batches partition a few node segments
+// in place): rows[p] = rows_out[p], ghp[p] = gh_out[p] for p in every chunk [b, e) of
+// items (the partition's own chunk list) -- one launch instead of two copies per node.
+__global__ __launch_bounds__(kPartThreads) void segment_copy_kernel(
+    const int4* __restrict__ items, const int* __restrict__ src_rows, int* __restrict__ dst_rows,
+    const float2* __restrict__ src_gh, float2* __restrict__ dst_gh) {
+  const int4 it = items[blockIdx.x];
+  for (int p = it.y + threadIdx.x; p < it.z; p += kPartThreads) {
+    dst_rows[p] = src_rows[p];
+    dst_gh[p] = src_gh[p];
+  }
+}
+
+extern "C" void ytk_segment_copy(uintptr_t items, int nitems, uintptr_t src_rows, uintptr_t dst_rows,
+                                 uintptr_t src_gh, uintptr_t dst_gh, uintptr_t stream) {
+  if (nitems <= 0) return;
+  hipLaunchKernelGGL(segment_copy_kernel, dim3(nitems), dim3(kPartThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const int4*)items,
+                     (const int*)src_rows, (int*)dst_rows, (const float2*)src_gh, (float2*)dst_gh);
+  YTK_LAUNCH_CHECK();
+}

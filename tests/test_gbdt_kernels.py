@@ -300,3 +300,30 @@ def test_grad_hess_matches_cpu(cuda, loss, K):
     torch.testing.assert_close(ghg.cpu(), ghc, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mg.cpu(), ghg.abs().amax(dim=1).cpu(), rtol=0, atol=0)
     np.testing.assert_allclose(ag.cpu().numpy(), ac.numpy(), rtol=2e-6)
+
+
+@pytest.mark.parametrize("F,nb,N,items_per_slot", [(28, 255, 1_000_000, 64), (28, 255, 300_000, 7),
+                                                   (40, 64, 200_000, 33)])
+def test_hist_build_staged_matches_cpu(cuda, F, nb, N, items_per_slot):
+    """Two-stage (staging + split-K reduce) flush, contiguous slots and scattered slot ids."""
+    bins = _rand_bins(N, F, nb, seed=5)
+    gh = _gh(N, seed=6)
+    B = ((nb + 3) // 4) * 4
+    perm = torch.randperm(N, generator=torch.Generator().manual_seed(7)).to(torch.int32)
+    nslot = 3
+    edges = np.linspace(0, N, nslot * items_per_slot + 1).astype(np.int64)
+    slots_scattered = [5, 1, 3]
+    for slot_ids in (None, slots_scattered):
+        ids = list(range(2, 2 + nslot)) if slot_ids is None else slot_ids
+        work = np.zeros((nslot * items_per_slot, 4), np.int32)
+        for k in range(nslot * items_per_slot):
+            work[k] = (ids[k // items_per_slot], edges[k], edges[k + 1], 0)
+        work_t = torch.from_numpy(work)
+        hc = torch.zeros((6, B, F, 2), dtype=torch.int64)
+        gops.hist_build(bins, F, gh, perm, work_t, hc, B, SG, SH)
+        hg = torch.zeros((6, B, F, 2), dtype=torch.int64, device=cuda)
+        staging = torch.empty(len(work) * ((F + 31) // 32) * B * 64, dtype=torch.int64, device=cuda)
+        gops.hist_build(bins.to(cuda), F, gh.to(cuda), perm.to(cuda), work_t.to(cuda), hg, B, SG, SH,
+                        staging=staging, slot_base=2, nslots=nslot,
+                        slot_ids=None if slot_ids is None else torch.tensor(slot_ids, dtype=torch.int32, device=cuda))
+        assert torch.equal(hg.cpu(), hc), f"slot_ids={slot_ids}"

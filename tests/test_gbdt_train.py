@@ -131,3 +131,23 @@ def test_device_builder_matches_host_builder(cuda, kw):
         trees.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
     assert trees[0][0] == trees[1][0]
     assert trees[0][1] == trees[1][1] and trees[0][2] == trees[1][2]
+
+
+@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 7}, {"max_depth": 4, "max_leaf_cnt": 20},
+                                {"min_split_samples": 900}, {"min_split_loss": 2.0},
+                                {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6}])
+def test_loss_guided_speculation_is_exact(monkeypatch, kw):
+    """Speculative batched leaf-wise growth == one-leaf-at-a-time growth (node ids, splits,
+    values and node statistics), on CPU."""
+    dumps = []
+    for spec in ("0", "1"):
+        monkeypatch.setenv("YTK_LOSSGUIDE_SPEC", spec)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 40
+        for k, v in kw.items():
+            setattr(p.tree, k, v)
+        tr = GBDTTrainer(p, _data(12000, 11), _data(3000, 12))
+        tr.train()
+        dumps.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert dumps[0] == dumps[1]
+    assert dumps[0][0].count("leaf=") > 3

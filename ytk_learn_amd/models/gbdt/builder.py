@@ -24,6 +24,7 @@ MI355X-first structure (not a translation):
 from __future__ import annotations
 
 import heapq
+import os
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -91,6 +92,8 @@ class _Node:
     rec: Optional[np.void] = None
     G: float = 0.0
     H: float = 0.0
+    children: Optional[tuple] = None  # (left, right) ids once expanded (loss-guided)
+    rec_used: bool = True             # False: leafified child -> dump lossChg = -inf
 
 
 class _Uploader:
@@ -149,7 +152,7 @@ def _chunk_segments(begins: np.ndarray, counts: np.ndarray, ch: int):
 
 class TreeBuilder:
     MIN_ROWS_PER_BLOCK = 2048
-    TARGET_BLOCKS = 1024  # histogram blocks per launch: 2 resident per CU x 256 CUs x 2 waves
+    TARGET_BLOCKS = 256  # histogram blocks per launch: one 128-KiB-LDS block per CU
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Optional[Comm] = None, profile: bool = False):
@@ -170,8 +173,20 @@ class TreeBuilder:
         else:
             max_nodes = 2 * ml - 1
         self.max_nodes = int(max_nodes)
+        # Loss-guided growth expands speculative batches (see build()): every real split
+        # uses two slots, and up to `spec_waste` further expansions may be discarded.
+        n_slots = self.max_nodes
+        self.spec_waste = 0
+        if params.grow_policy == "loss" and params.max_leaf_cnt > 0:
+            slot_bytes = B * F * 16
+            self.spec_waste = int(min(params.max_leaf_cnt, max(0, (4 << 30) // max(1, 2 * slot_bytes))))
+            n_slots += 2 * self.spec_waste
+        self.n_slots = n_slots
+        # YTK_LOSSGUIDE_SPEC=0: expand one leaf per step (the plain sequential schedule;
+        # used by the tests to check that speculation does not change the tree)
+        self.speculate = os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0"
         # exact int64 fixed-point histograms (see csrc/hip/gbdt_hist.hip)
-        self.hist = torch.zeros((self.max_nodes, B, F, 2), dtype=torch.int64, device=self.dev)
+        self.hist = torch.zeros((n_slots, B, F, 2), dtype=torch.int64, device=self.dev)
         self.gp_tree = dict(self.gp, sg=1.0, sh=1.0)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=self.dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=self.dev)
@@ -185,6 +200,9 @@ class TreeBuilder:
         self.total_stats = TimeStats()
         self.tree_count = 0
         self.last_keep = None
+        self._root_gh = None
+        self._staging = None
+        self.free_slots = None
         self.fmask_np = np.ones(F, np.uint8)
 
     # ------------------------------------------------------------------ utils
@@ -202,15 +220,20 @@ class TreeBuilder:
         then find the best split of every one of them."""
         st = self.last_stats
         t0 = time.perf_counter()
-        s0 = self.next_slot
         nb = len(build)
+        if self.free_slots is not None:  # recycled pool (loss-guided): any free slots
+            ids = [self.free_slots.pop() for _ in range(nb + len(derived))]
+            s0 = -1
+        else:  # one contiguous range per call
+            s0 = self.next_slot
+            ids = list(range(s0, s0 + nb + len(derived)))
+            self.next_slot += nb + len(derived)
         for i, nid in enumerate(build):
-            nodes[nid].slot = s0 + i
+            nodes[nid].slot = ids[i]
         for j, (nid, _, _) in enumerate(derived):
-            nodes[nid].slot = s0 + nb + j
-        self.next_slot += nb + len(derived)
+            nodes[nid].slot = ids[nb + j]
         items = np.zeros((nb + len(derived), 4), np.int32)
-        items[:nb, 0] = np.arange(s0, s0 + nb)
+        items[:nb, 0] = ids[:nb]
         for j, (n, p, s) in enumerate(derived):
             items[nb + j] = (nodes[n].slot, nodes[p].slot, nodes[s].slot, 1)
         work = np.zeros((0, 4), np.int32)
@@ -219,18 +242,36 @@ class TreeBuilder:
             counts = np.array([nodes[n].cnt_local for n in build], np.int64)
             seg, s, e, _, _, _ = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
             work = np.zeros((len(seg), 4), np.int32)
-            work[:, 0] = s0 + seg
+            work[:, 0] = np.asarray(ids[:nb], np.int32)[seg]
             work[:, 1] = s
             work[:, 2] = e
-        work_d, items_d = self.up.put(work, items)
+        work_d, items_d, ids_d = self.up.put(work, items, np.asarray(ids[:nb], np.int32))
         if nb:
-            self.hist[s0:s0 + nb].zero_()
-            gops.hist_build(self.bins, self.F, self.ghp, None if identity_rows else self.rows,
-                            work_d, self.hist, self.B, self.gp_tree["sg"], self.gp_tree["sh"])
+            if s0 >= 0:
+                self.hist[s0:s0 + nb].zero_()
+            else:
+                self.hist.index_fill_(0, ids_d.long(), 0)
+            src_gh = self._root_gh if (identity_rows and self._root_gh is not None) else self.ghp
+            staging = None
+            if self.dev.type == "cuda" and os.environ.get("YTK_HOST_STAGED", "1") != "0":
+                need = len(work) * ((self.F + 31) // 32) * self.B * 64
+                if self._staging is None or self._staging.numel() < need:
+                    self._staging = torch.empty(int(need * 1.25), dtype=torch.int64, device=self.dev)
+                staging = self._staging
+            gops.hist_build(self.bins, self.F, src_gh, None if identity_rows else self.rows,
+                            work_d, self.hist, self.B, self.gp_tree["sg"], self.gp_tree["sh"],
+                            staging=staging, slot_base=max(s0, 0), nslots=nb,
+                            slot_ids=ids_d if s0 < 0 else None)
         self._sync()
         t1 = time.perf_counter()
         if nb and self.comm.is_dist:
-            self.comm.allreduce_(self.hist[s0:s0 + nb])
+            if s0 >= 0:
+                self.comm.allreduce_(self.hist[s0:s0 + nb])
+            else:  # gather the scattered slots into one buffer -> one all-reduce
+                idx = ids_d.long()
+                buf = self.hist.index_select(0, idx)
+                self.comm.allreduce_(buf)
+                self.hist.index_copy_(0, idx, buf)
             self._sync()
         t2 = time.perf_counter()
         order = list(build) + [n for n, _, _ in derived]
@@ -265,15 +306,15 @@ class TreeBuilder:
                        np.int32)
         items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d = self.up.put(
             items, feat, thr, begins, first, nblk)
-        left = gops.partition(self.binsT, self.rows, self.rows_tmp, self.ghp, self.gh_tmp, self.flags,
+        root = self._root_gh is not None  # first partition of an unsampled tree: identity rows
+        left = gops.partition(self.binsT, None if root else self.rows, self.rows_tmp,
+                              self._root_gh if root else self.ghp, self.gh_tmp, self.flags,
                               items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d, n)
-        if copy_back:
-            for nid, _, _ in splits:
-                nd = nodes[nid]
-                if nd.cnt_local:
-                    sl = slice(nd.begin, nd.begin + nd.cnt_local)
-                    self.rows[sl].copy_(self.rows_tmp[sl])
-                    self.ghp[sl].copy_(self.gh_tmp[sl])
+        if root:  # the root segment is every row: take the output buffers whole
+            copy_back = False
+            self._root_gh = None
+        if copy_back:  # only these segments were partitioned: copy them back in one launch
+            gops.segment_copy(items_d, self.rows_tmp, self.rows, self.gh_tmp, self.ghp)
         else:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
@@ -306,7 +347,8 @@ class TreeBuilder:
         thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
                        np.int32)
         items_d, feat_d, thr_d = self.up.put(items, feat, thr)
-        bc = gops.partition_count(self.binsT, self.rows, self.flags, items_d, feat_d, thr_d)
+        bc = gops.partition_count(self.binsT, None if self._root_gh is not None else self.rows, self.flags,
+                                  items_d, feat_d, thr_d)
         left = torch.zeros(len(splits), dtype=torch.int64, device=self.dev)
         if len(seg):
             left.index_add_(0, torch.from_numpy(seg).to(self.dev), bc.to(torch.int64))
@@ -326,13 +368,155 @@ class TreeBuilder:
                               cnt_global=nd.cnt_global - int(lglob[i]), depth=nd.depth + 1)
         self.last_stats.partition += time.perf_counter() - t0
 
+    # ------------------------------------------------------- loss-guided growth
+    def _grow_loss_guided(self, tree: Tree, nodes: Dict[int, _Node], fmask, f0, pop_is_leaf, make_leaf,
+                          children_terminal, leafify_children) -> Dict[int, int]:
+        """Exact leaf-wise growth (reference: priority queue ordered by lossChg,
+        DataParallelTreeMaker.java:104-115,219-295) without one device round trip per node.
+
+        The reference pops the best leaf, splits it, histograms its children and pushes
+        them -- 254 strictly sequential steps for 255 leaves. Splitting a leaf never
+        changes another leaf's best split, so the pop ORDER can be replayed on the host
+        from the gains alone. Here the replay runs until it reaches a leaf that must be
+        split but whose children are not computed yet; then that leaf AND the next
+        best candidates (up to the remaining leaf budget) are expanded together in one
+        batched partition + histogram + split launch group. Expansions the replay never
+        pops are discarded (their rows were only permuted inside their own segment), so
+        the tree -- node ids, splits, values, statistics -- is identical to the
+        sequential algorithm, in ~log2(leaves) + a few batches instead of leaves - 1.
+
+        ``nodes`` is keyed by speculative ids; returns {speculative id: tree node id}.
+        """
+        p = self.p
+        max_leaf = p.max_leaf_cnt
+        self.last_batches = self.last_expanded = 0
+        tid = {0: 0}
+        next_sid = [1]
+        state = {"num_leaf": 1, "seq": 1}
+        heap = [(-float(nodes[0].rec["loss_chg"]), 0, 0)]
+
+        def would_split(nd: _Node):  # pop-time rules that do not depend on the leaf count
+            return not (nd.rec["loss_chg"] <= p.min_split_loss
+                        or (p.max_depth >= 0 and p.max_depth == nd.depth)
+                        or (p.min_split_samples > 0 and nd.cnt_global < p.min_split_samples))
+
+        def expand(batch: List[int]):
+            splits, counts_only = [], []
+            for sid in batch:
+                lc, rc = next_sid[0], next_sid[0] + 1
+                next_sid[0] += 2
+                nodes[sid].children = (lc, rc)
+                # children at max_depth are always terminal: only their counts are needed
+                (counts_only if (p.max_depth >= 0 and nodes[sid].depth + 1 == p.max_depth)
+                 else splits).append((sid, lc, rc))
+            if counts_only:
+                self._count_children(nodes, counts_only)
+            if splits:
+                self._partition(nodes, splits, copy_back=True)
+                build, derived = [], []
+                for sid, lc, rc in splits:
+                    nl, nr = nodes[lc], nodes[rc]
+                    small, large = (lc, rc) if nl.cnt_global < nr.cnt_global else (rc, lc)
+                    build.append(small)
+                    derived.append((large, sid, small))
+                self._build_and_find(nodes, build, derived, fmask, f0)
+            for sid in batch:  # parents' histograms are no longer needed
+                release(sid)
+
+        def release(sid):
+            nd = nodes[sid]
+            if nd.slot >= 0:
+                self.free_slots.append(nd.slot)
+                nd.slot = -1
+
+        while True:
+            # replay the sequential priority-queue growth as far as the known gains allow
+            blocked = False
+            while heap:
+                _, _, sid = heap[0]
+                nd = nodes[sid]
+                if pop_is_leaf(nd, state["num_leaf"]):
+                    heapq.heappop(heap)
+                    make_leaf(sid, tid[sid])
+                    if nd.children is None:
+                        release(sid)
+                    continue
+                if nd.children is None:
+                    blocked = True
+                    break
+                heapq.heappop(heap)
+                t = tid[sid]
+                lc_t, rc_t = tree.add_children(t)
+                r = nd.rec
+                tree.set_split(t, int(r["feat"]), int(r["bin_a"]), int(r["bin_b"]))
+                state["num_leaf"] += 1
+                lcs, rcs = nd.children
+                tid[lcs], tid[rcs] = lc_t, rc_t
+                nl, nr = nodes[lcs], nodes[rcs]
+                if children_terminal(nl, nr, state["num_leaf"]):
+                    leafify_children(sid, lcs, rcs, lc_t, rc_t)
+                    nl.rec_used = nr.rec_used = False
+                    for c in (lcs, rcs):
+                        if nodes[c].children is None:
+                            release(c)
+                else:
+                    sq = state["seq"]
+                    nl.seq, nr.seq = sq, sq + 1
+                    heapq.heappush(heap, (-float(nl.rec["loss_chg"]), sq, lcs))
+                    heapq.heappush(heap, (-float(nr.rec["loss_chg"]), sq + 1, rcs))
+                    state["seq"] = sq + 2
+            if not blocked:
+                break
+            # expansion batch: the blocked leaf + the next candidates in pop order
+            remaining = (max_leaf - state["num_leaf"]) if max_leaf > 0 else 1
+            # each expansion takes 2 slots and frees its own; keep one net slot per future split
+            slack = (len(self.free_slots) - remaining - 1) // 2
+            k = max(1, min(remaining, slack)) if self.speculate else 1
+            # candidates: continue the replay VIRTUALLY, treating the not-yet-computed
+            # children of unexpanded splits as absent; the unexpanded nodes this virtual
+            # replay pops as splits (within the leaf budget) are exactly the ones the real
+            # replay will split unless an unknown child outranks them -> expand them now
+            _, _, blocked_sid = heap[0]
+            batch = [blocked_sid]
+            if k > 1:
+                vheap = list(heap)
+                vleaf = state["num_leaf"]
+                vseq = state["seq"]
+                chosen = {blocked_sid}
+                while vheap and len(batch) < k:
+                    _, _, sid = heapq.heappop(vheap)
+                    nd = nodes[sid]
+                    if pop_is_leaf(nd, vleaf):
+                        continue
+                    vleaf += 1
+                    if nd.children is None:
+                        if sid not in chosen:
+                            chosen.add(sid)
+                            batch.append(sid)
+                        continue
+                    lcs, rcs = nd.children
+                    nl, nr = nodes[lcs], nodes[rcs]
+                    if nl.rec is None or nr.rec is None or children_terminal(nl, nr, vleaf):
+                        continue
+                    heapq.heappush(vheap, (-float(nl.rec["loss_chg"]), vseq, lcs))
+                    heapq.heappush(vheap, (-float(nr.rec["loss_chg"]), vseq + 1, rcs))
+                    vseq += 2
+            expand(batch)
+            self.last_batches += 1
+            self.last_expanded += len(batch)
+        return tid
+
     # ------------------------------------------------------------------ build
-    def build(self, gh: torch.Tensor) -> Tree:
-        """Grow one tree from gh [N, 2] (grad*w, hess*w) in row order."""
+    def build(self, gh: torch.Tensor, ghmax: Optional[torch.Tensor] = None) -> Tree:
+        """Grow one tree from gh [N, 2] (grad*w, hess*w) in row order. ``ghmax`` (optional,
+        float32 [2]): max |g|, |h| over the rows, already produced by the gradient kernel."""
         p = self.p
         t_start = time.perf_counter()
         self.last_stats = TimeStats()
         self.next_slot = 0
+        # loss-guided growth recycles histogram slots (a slot is free again once its node is
+        # expanded or finalised as a leaf): live slots = the known-gain frontier only
+        self.free_slots = list(range(self.n_slots - 1, -1, -1)) if p.grow_policy == "loss" else None
         self.up.reset()
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))
@@ -347,9 +531,17 @@ class TreeBuilder:
             self.rows[:n_local].copy_(sel)
             self.ghp[:n_local].copy_(gh.index_select(0, sel.long()))
             identity = False
+            self._root_gh = None
             self.last_keep = keep
+        elif os.environ.get("YTK_HOST_IDROOT", "1") != "0":
+            # no copies: the root histogram and the first partition read the identity
+            # permutation and the caller's gh directly
+            n_local = self.N
+            self._root_gh = gh.contiguous()
+            self.last_keep = None
         else:
             n_local = self.N
+            self._root_gh = None
             self.rows.copy_(self.iota)
             self.ghp.copy_(gh)
             self.last_keep = None
@@ -369,8 +561,10 @@ class TreeBuilder:
 
         n_global = int(self.comm.allreduce_scalars([n_local], dtype=torch.int64)[0]) if self.comm.is_dist else n_local
         # per-tree fixed-point scales from the global max |g|, |h| (identical on every rank)
-        if n_local > 0:
-            mx = self.ghp[:n_local].abs().amax(dim=0).double()
+        if ghmax is not None and identity:
+            mx = ghmax.double()
+        elif n_local > 0:
+            mx = (self._root_gh if identity else self.ghp[:n_local]).abs().amax(dim=0).double()
         else:
             mx = torch.zeros(2, dtype=torch.float64, device=self.dev)
         if self.comm.is_dist:
@@ -386,17 +580,17 @@ class TreeBuilder:
         max_leaf = p.max_leaf_cnt
         lr32 = np.float32(p.learning_rate)
 
-        def pop_is_leaf(nd: _Node):
+        def pop_is_leaf(nd: _Node, num_leaf: int):
             return (nd.rec["loss_chg"] <= p.min_split_loss
                     or (p.max_depth >= 0 and p.max_depth == nd.depth)
                     or (max_leaf > 0 and max_leaf == num_leaf)
                     or (p.min_split_samples > 0 and nd.cnt_global < p.min_split_samples))
 
-        def make_leaf(nid):
+        def make_leaf(nid, t=None):
             nd = nodes[nid]
             v = np.float32(gops.node_value_np(nd.G, nd.H, self.gp["mcw"], self.gp["l1"], self.gp["l2"],
                                               self.gp["max_abs_leaf"]))
-            tree.set_leaf(nid, float(v * lr32))
+            tree.set_leaf(nid if t is None else t, float(v * lr32))
 
         def children_terminal(nd_l: _Node, nd_r: _Node, nleaf: int):
             return ((p.max_depth >= 0 and p.max_depth == nd_l.depth)
@@ -404,13 +598,13 @@ class TreeBuilder:
                     or (p.min_split_samples > 0 and nd_l.cnt_global < p.min_split_samples
                         and nd_r.cnt_global < p.min_split_samples))
 
-        def leafify_children(nid, lc, rc):
+        def leafify_children(nid, lc, rc, lt=None, rt=None):
             r = nodes[nid].rec
             nl, nr = nodes[lc], nodes[rc]
             nl.G, nl.H = float(r["gl"]), float(r["hl"])
             nr.G, nr.H = nodes[nid].G - nl.G, nodes[nid].H - nl.H
-            make_leaf(lc)
-            make_leaf(rc)
+            make_leaf(lc, lt)
+            make_leaf(rc, rt)
 
         if p.grow_policy == "level":
             level = [0]
@@ -418,7 +612,7 @@ class TreeBuilder:
                 splits, snapshot = [], []
                 for nid in level:  # FIFO by seq
                     nd = nodes[nid]
-                    if pop_is_leaf(nd):
+                    if pop_is_leaf(nd, num_leaf):
                         make_leaf(nid)
                         continue
                     r = nd.rec
@@ -452,35 +646,16 @@ class TreeBuilder:
                 if build:
                     self._build_and_find(nodes, build, derived, fmask, f0)
                 level = nxt
-        else:  # loss-guided
-            heap = [(-float(nodes[0].rec["loss_chg"]), 0, 0)]
-            while heap:
-                _, _, nid = heapq.heappop(heap)
-                nd = nodes[nid]
-                if pop_is_leaf(nd):
-                    make_leaf(nid)
-                    continue
-                r = nd.rec
-                lc, rc = tree.add_children(nid)
-                tree.set_split(nid, int(r["feat"]), int(r["bin_a"]), int(r["bin_b"]))
-                num_leaf += 1
-                if (p.max_depth >= 0 and nd.depth + 1 == p.max_depth) or (max_leaf > 0 and max_leaf == num_leaf
-                                                                        and p.min_split_samples <= 0):
-                    # terminal children whose rows are never needed again
-                    self._count_children(nodes, [(nid, lc, rc)])
-                    leafify_children(nid, lc, rc)
-                    continue
-                self._partition(nodes, [(nid, lc, rc)], copy_back=True)
-                nl, nr = nodes[lc], nodes[rc]
-                if children_terminal(nl, nr, num_leaf):
-                    leafify_children(nid, lc, rc)
-                else:
-                    small, large = (lc, rc) if nl.cnt_global < nr.cnt_global else (rc, lc)
-                    self._build_and_find(nodes, [small], [(large, nid, small)], fmask, f0)
-                    nl.seq, nr.seq = seq, seq + 1
-                    heapq.heappush(heap, (-float(nl.rec["loss_chg"]), seq, lc))
-                    heapq.heappush(heap, (-float(nr.rec["loss_chg"]), seq + 1, rc))
-                    seq += 2
+        else:  # loss-guided (leaf-wise), exact, expanded in speculative batches
+            tid = self._grow_loss_guided(tree, nodes, fmask, f0, pop_is_leaf, make_leaf,
+                                         children_terminal, leafify_children)
+            for sid, t in tid.items():
+                nd = nodes[sid]
+                tree.loss_chg[t] = (float(np.float32(nd.rec["loss_chg"])) if nd.rec is not None and nd.rec_used
+                                    else float("-inf"))
+                tree.hess_sum[t] = float(np.float32(nd.H))
+                tree.sample_cnt[t] = nd.cnt_global
+            nodes = {}
 
         # node stats for the dump (updateTreeNodeStat)
         for nid in range(tree.num_nodes):

@@ -281,7 +281,7 @@ class DeviceLevelBuilder:
             if self.staged:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
                                  ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5),
-                                 ptr(self.scales), ptr(self.staging), slot_base, nslots, s)
+                                 ptr(self.scales), ptr(self.staging), slot_base, nslots, 0, s)
                 return
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)

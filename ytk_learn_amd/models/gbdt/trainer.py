@@ -305,7 +305,7 @@ class GBDTTrainer:
                     raw["troot"], raw["tout"] = self._one_tree[k]
                     raws.append(raw)
             else:
-                tree = self.builder.build(self.gh[k])
+                tree = self.builder.build(self.gh[k], self.ghmax[k])
                 if self.refiner is not None:
                     self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
                                         + self.init_score[:, k], self.w, lr)

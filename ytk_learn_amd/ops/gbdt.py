@@ -60,7 +60,7 @@ def quantize_gh(gh: torch.Tensor, sg: float, sh: float) -> torch.Tensor:
     return q
 
 
-def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh):
+def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_base=0, nslots=0, slot_ids=None):
     """Accumulate exact int64 fixed-point (g, h) histograms.
 
     bins: [N, S] uint8/int16 row-major (S >= F, S % 32 == 0 for the LDS path)
@@ -69,6 +69,11 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh):
     work: int32 [nwork, 4] = (slot, begin, end, 0); positions index ``rows``
     hist: int64 [slots, B, F, 2], target slots must be zeroed by the caller
     sg, sh: power-of-two fixed-point scales (``fixed_point_scales``)
+    staging: optional int64 scratch (>= nwork * ceil(F/32) * B * 64 elements): block
+      partials are stored, then reduced into the work's slots, which must be the
+      contiguous range [slot_base, slot_base + nslots) (two-stage flush, no per-block
+      global atomics -- see csrc/hip/gbdt_hist.hip); ``slot_ids`` (int32 device tensor of
+      nslots ids) replaces the contiguous range when given
     """
     nwork = work.shape[0]
     if nwork == 0:
@@ -83,8 +88,14 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh):
         stride = bins.shape[1]
         h = hip()
         if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
-            h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
-                      float(sg), float(sh), 0, 0, stream(bins))
+            if staging is not None and nslots > 0:
+                assert staging.numel() >= nwork * ((F + 31) // 32) * B * 64
+                h.hist_fx_staged(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                                 float(sg), float(sh), 0, 0, ptr(staging), slot_base, nslots, ptr(slot_ids),
+                                 stream(bins))
+            else:
+                h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                          float(sg), float(sh), 0, 0, stream(bins))
         else:
             h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                              nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
@@ -239,7 +250,7 @@ def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_
         b = int(it[fb[i], 1])
         e = int(it[fb[i] + nb_[i] - 1, 2])
         assert b == nbv[i]
-        r = rows[b:e]
+        r = rows[b:e] if rows is not None else torch.arange(b, e, dtype=torch.int32)
         g = ghp[b:e]
         go = (binsT[int(fv[i])][r.long()].long() & mask) <= int(tv[i])
         nl = int(go.sum())
@@ -249,6 +260,21 @@ def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_
         gh_out[b + nl:e] = g[~go]
         left[i] = nl
     return left
+
+
+def segment_copy(items, src_rows, dst_rows, src_gh, dst_gh):
+    """dst[p] = src[p] (row ids and (g, h)) for every chunk [b, e) of ``items`` [n, 4]."""
+    n = items.shape[0]
+    if n == 0:
+        return
+    if dst_rows.is_cuda:
+        check_cuda(items, src_rows, dst_rows, src_gh, dst_gh)
+        hip().segment_copy(ptr(items), n, ptr(src_rows), ptr(dst_rows), ptr(src_gh), ptr(dst_gh),
+                           stream(dst_rows))
+        return
+    for _, b, e, _ in items.numpy():
+        dst_rows[b:e] = src_rows[b:e]
+        dst_gh[b:e] = src_gh[b:e]
 
 
 def partition_count(binsT, rows, flags, items, feat, thr):
@@ -266,7 +292,7 @@ def partition_count(binsT, rows, flags, items, feat, thr):
     it = items.numpy()
     mask = 0xFFFF if binsT.dtype == torch.int16 else 0xFF
     for j, (si, b, e, _) in enumerate(it):
-        r = rows[b:e].long()
+        r = rows[b:e].long() if rows is not None else torch.arange(b, e)
         counts[j] = int(((binsT[int(feat[si])][r].long() & mask) <= int(thr[si])).sum())
     return counts
 
