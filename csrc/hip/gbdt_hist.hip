@@ -26,7 +26,8 @@
 namespace ytk {
 
 constexpr int kHistThreads = 1024;
-constexpr int kHistU = 4;
+constexpr int kHistU = 8;
+constexpr int kHistUGather = 16; // gathered rows: more loads in flight per wave
 
 template <bool kIdentity>
 __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
@@ -57,12 +58,13 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   constexpr int RW = (kHistThreads / 64) * 8;  // rows per block step
   const uint8_t* bseg = bins + fg * 32 + 4 * q;
   const int fbase = fg * 32 + 4 * q;
-  for (int base = w.y + wave * 8; base < w.z; base += RW * kHistU) {
-    unsigned d[kHistU];
-    float2 v[kHistU];
-    bool ok[kHistU];
+  constexpr int U = kIdentity ? kHistU : kHistUGather;
+  for (int base = w.y + wave * 8; base < w.z; base += RW * U) {
+    unsigned d[U];
+    float2 v[U];
+    bool ok[U];
 #pragma unroll
-    for (int j = 0; j < kHistU; ++j) {
+    for (int j = 0; j < U; ++j) {
       const int pos = base + j * RW + wr;
       ok[j] = pos < w.z;
       const int p = ok[j] ? pos : w.y;
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
       v[j] = ghp[p];
     }
 #pragma unroll
-    for (int j = 0; j < kHistU; ++j) {
+    for (int j = 0; j < U; ++j) {
       if (!ok[j]) continue;
       const unsigned long long gi = (unsigned long long)__float2ll_rn(v[j].x * sg);
       const unsigned long long hi = (unsigned long long)__float2ll_rn(v[j].y * sh);
