@@ -151,3 +151,25 @@ def test_loss_guided_speculation_is_exact(monkeypatch, kw):
         dumps.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
     assert dumps[0] == dumps[1]
     assert dumps[0][0].count("leaf=") > 3
+
+
+def test_histogram_pool_capacity_misses_do_not_change_the_tree():
+    """histogram_pool_capacity (MB) bounds the live histograms of leaf-wise growth; evicted
+    parents are rebuilt (pool miss) instead of derived -- exact int64 sums => same model."""
+    dumps, misses, slot_mb = [], [], None
+    for pool in (-1.0, "tiny"):
+        p = _params("loss", rounds=2)
+        p.tree.max_leaf_cnt = 30
+        if pool == "tiny":
+            p.histogram_pool_capacity = 5 * slot_mb  # 5 live histograms
+        tr = GBDTTrainer(p, _data(8000, 13), None)
+        tr.prepare()
+        slot_mb = tr.B * tr.F * 16 / float(1 << 20)
+        tr.init_gradients()
+        for i in range(2):
+            tr.step(i)
+        tr.materialize()
+        dumps.append(tr.model.dumps())
+        misses.append(tr.builder.hist_miss)
+    assert dumps[0] == dumps[1]
+    assert misses[0] == 0 and misses[1] > 0

@@ -26,6 +26,7 @@ from __future__ import annotations
 import heapq
 import os
 import time
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -155,7 +156,8 @@ class TreeBuilder:
     TARGET_BLOCKS = 256  # histogram blocks per launch: one 128-KiB-LDS block per CU
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
-                 params: TreeParams, comm: Optional[Comm] = None, profile: bool = False):
+                 params: TreeParams, comm: Optional[Comm] = None, profile: bool = False,
+                 pool_mb: float = -1.0):
         self.bins = bins
         self.binsT = binsT
         self.dev = bins.device
@@ -181,12 +183,21 @@ class TreeBuilder:
             slot_bytes = B * F * 16
             self.spec_waste = int(min(params.max_leaf_cnt, max(0, (4 << 30) // max(1, 2 * slot_bytes))))
             n_slots += 2 * self.spec_waste
+        # histogram_pool_capacity (MB, <= 0: unlimited; reference HistogramPool.java:36-273,
+        # DataParallelTreeMaker.java:192-204,489-508): bounds the live histogram slots of
+        # loss-guided growth. When the pool is full the least recently built histogram is
+        # evicted; expanding an evicted node then builds BOTH children (a pool miss)
+        # instead of deriving the larger one by subtraction.
+        self.slot_bytes = B * F * 16
+        if pool_mb is not None and pool_mb > 0 and params.grow_policy == "loss":
+            n_slots = int(min(n_slots, max(3, (pool_mb * (1 << 20)) // self.slot_bytes)))
         self.n_slots = n_slots
+        self.hist_miss = 0
         # YTK_LOSSGUIDE_SPEC=0: expand one leaf per step (the plain sequential schedule;
         # used by the tests to check that speculation does not change the tree)
         self.speculate = os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0"
         # exact int64 fixed-point histograms (see csrc/hip/gbdt_hist.hip)
-        self.hist = torch.zeros((n_slots, B, F, 2), dtype=torch.int64, device=self.dev)
+        self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=self.dev)
         self.gp_tree = dict(self.gp, sg=1.0, sh=1.0)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=self.dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=self.dev)
@@ -222,7 +233,13 @@ class TreeBuilder:
         t0 = time.perf_counter()
         nb = len(build)
         if self.free_slots is not None:  # recycled pool (loss-guided): any free slots
-            ids = [self.free_slots.pop() for _ in range(nb + len(derived))]
+            need = nb + len(derived)
+            keep = {p for _, p, _ in derived}
+            while len(self.free_slots) < need:
+                self._evict(nodes, keep)
+            ids = [self.free_slots.pop() for _ in range(need)]
+            for nid, sl in zip(list(build) + [n for n, _, _ in derived], ids):
+                self.lru[nid] = sl
             s0 = -1
         else:  # one contiguous range per call
             s0 = self.next_slot
@@ -292,6 +309,17 @@ class TreeBuilder:
         st.build_hist += t1 - t0
         st.comm_hist += t2 - t1
         st.find_split += t3 - t2
+
+    def _evict(self, nodes: Dict[int, _Node], keep):
+        """Drop the least recently built histogram not needed by the current call."""
+        for sid in list(self.lru):
+            if sid in keep:
+                continue
+            sl = self.lru.pop(sid)
+            nodes[sid].slot = -1
+            self.free_slots.append(sl)
+            return
+        raise RuntimeError("histogram_pool_capacity too small for one expansion")
 
     def _partition(self, nodes: Dict[int, _Node], splits: List[tuple], copy_back: bool):
         """splits: list of (nid, left_child, right_child). Updates child segments/counts."""
@@ -418,7 +446,11 @@ class TreeBuilder:
                     nl, nr = nodes[lc], nodes[rc]
                     small, large = (lc, rc) if nl.cnt_global < nr.cnt_global else (rc, lc)
                     build.append(small)
-                    derived.append((large, sid, small))
+                    if nodes[sid].slot >= 0:
+                        derived.append((large, sid, small))
+                    else:  # parent histogram evicted from the pool: rebuild (pool miss)
+                        build.append(large)
+                        self.hist_miss += 1
                 self._build_and_find(nodes, build, derived, fmask, f0)
             for sid in batch:  # parents' histograms are no longer needed
                 release(sid)
@@ -426,6 +458,7 @@ class TreeBuilder:
         def release(sid):
             nd = nodes[sid]
             if nd.slot >= 0:
+                self.lru.pop(sid, None)
                 self.free_slots.append(nd.slot)
                 nd.slot = -1
 
@@ -517,6 +550,7 @@ class TreeBuilder:
         # loss-guided growth recycles histogram slots (a slot is free again once its node is
         # expanded or finalised as a leaf): live slots = the known-gain frontier only
         self.free_slots = list(range(self.n_slots - 1, -1, -1)) if p.grow_policy == "loss" else None
+        self.lru = OrderedDict()  # speculative node id -> slot, oldest first
         self.up.reset()
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))

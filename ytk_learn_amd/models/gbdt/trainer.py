@@ -148,7 +148,8 @@ class GBDTTrainer:
                                               timer=self.timer)
         else:
             self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
-                                       self.comm, profile=self.profile)
+                                       self.comm, profile=self.profile,
+                                       pool_mb=self.p.histogram_pool_capacity)
         N = tr.n
         self.score = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
         self.init_score = self._base_score(tr)
