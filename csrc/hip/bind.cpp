@@ -13,7 +13,8 @@ extern "C" {
 void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int,
                  float, float, uintptr_t, uintptr_t, uintptr_t);
 void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
-                        int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
+                        int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t,
+                        uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 // gbdt_split.hip

@@ -35,17 +35,20 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B, int nb_lds,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
-    long long* __restrict__ staging) {
+    long long* __restrict__ staging, const int* __restrict__ work_off_dev) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];
   unsigned long long* lg = sm64;
   unsigned long long* lh = sm64 + nb_lds * 32;
   // device-resident work count (fixed maximal grid launched by the level engine)
-  if (nwork_dev && (int)blockIdx.x >= *nwork_dev) return;
+  // work_off_dev (optional): this launch covers work items [*work_off_dev, *nwork_dev) --
+  // the second half of a level whose first half is already being all-reduced
+  const int bx = (int)blockIdx.x + (work_off_dev ? *work_off_dev : 0);
+  if (nwork_dev && bx >= *nwork_dev) return;
   if (scales_dev) {
     sg = scales_dev[0];
     sh = scales_dev[1];
   }
-  const int4 w = work[blockIdx.x];
+  const int4 w = work[bx];
   const int fg = blockIdx.y;
   const int tid = threadIdx.x;
   for (int i = tid; i < nb_lds * 64; i += kHistThreads) sm64[i] = 0ull;
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     // side at ~1.3 TB/s chip-wide, which made the atomic flush the floor of every
     // launch (~45 us per level at 256 blocks); stores + one ordered read are ~4x cheaper.
     const int E = nb_lds * 32;
-    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)blockIdx.x * gridDim.y + fg) * E;
+    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.y + fg) * E;
     for (int i = tid; i < E; i += kHistThreads) st[i] = make_longlong2((long long)lg[i], (long long)lh[i]);
     return;
   }
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   // serialising hundreds of blocks on one address at a time.
   const int E = nb_lds * 32;
   const int ntile = (E + kHistThreads - 1) / kHistThreads;
-  const int rot = (int)(blockIdx.x % (unsigned)ntile);
+  const int rot = (int)((unsigned)bx % (unsigned)ntile);
   for (int t = 0; t < ntile; ++t) {
     const int i = ((t + rot) % ntile) * kHistThreads + tid;
     if (i >= E) continue;
@@ -149,10 +152,29 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   // each take a strided subset s_sel[z], s_sel[z + 8], ..., so every block must see the
   // SAME order (an LDS-atomic compaction orders items differently per block whenever a
   // slot's items straddle waves, dropping and double counting items).
+  // Fast path: every caller emits a slot's items contiguously -> one pass finds the
+  // range [lo, hi] (min/max of matching indices) and the match count; contiguous iff
+  // count == hi - lo + 1. Otherwise fall back to the ordered compaction below.
+  __shared__ int s_lo, s_hi, s_cnt;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_n = 0;
+  if (tid == 0) { s_n = 0; s_lo = 0x7fffffff; s_hi = -1; s_cnt = 0; }
   __syncthreads();
-  for (int k0 = 0; k0 < n; k0 += 256) {
+  for (int k0 = 0; k0 < n; k0 += 256) {  // one LDS atomic per wave, not per item
+    const int k = k0 + tid;
+    const unsigned long long bal = __ballot(k < n && work[k].x == slot);
+    if (lane == 0 && bal) {
+      const int wbase = k0 + wid * 64;
+      atomicMin(&s_lo, wbase + __ffsll((long long)bal) - 1);
+      atomicMax(&s_hi, wbase + 63 - __clzll((long long)bal));
+      atomicAdd(&s_cnt, __popcll(bal));
+    }
+  }
+  __syncthreads();
+  const bool contiguous = s_cnt == 0 || s_cnt == s_hi - s_lo + 1;
+  if (contiguous) {
+    if (tid == 0) s_n = s_cnt;
+  }
+  for (int k0 = 0; !contiguous && k0 < n; k0 += 256) {
     const int k = k0 + tid;
     const bool m = k < n && work[k].x == slot;
     const unsigned long long bal = __ballot(m);
@@ -166,7 +188,11 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     if (tid == 0) s_n += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
     __syncthreads();
   }
-  const int cnt = min(s_n, 1024);
+  __syncthreads();
+  const int cnt = contiguous ? s_n : min(s_n, 1024);
+  const int lo = s_lo;
+  // t-th item of the slot
+#define YTK_SEL(t) (contiguous ? lo + (t) : s_sel[(t)])
   const int E = nb_lds * 32;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E || cnt == 0) return;
@@ -178,12 +204,12 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   for (; t + 7 * kReduceSplit < cnt; t += 8 * kReduceSplit) {
     longlong2 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)s_sel[t + u * kReduceSplit] * groups + fg) * E + i];
+    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)YTK_SEL(t + u * kReduceSplit) * groups + fg) * E + i];
 #pragma unroll
     for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
   }
   for (; t < cnt; t += kReduceSplit) {
-    const longlong2 v = st[((size_t)s_sel[t] * groups + fg) * E + i];
+    const longlong2 v = st[((size_t)YTK_SEL(t) * groups + fg) * E + i];
     g += v.x;
     h += v.y;
   }
@@ -193,6 +219,7 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     atomicAdd(o + 1, (unsigned long long)h);
   }
 }
+#undef YTK_SEL
 
 // Generic histogram (uint8 or uint16 bins, any bin count): direct global int64
 // atomics. Fallback for > 256 bins (e.g. the 5000-bin communication-stress config).
@@ -237,12 +264,14 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
     hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr,
+                       (const int*)nullptr);
   } else {
     hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr,
+                       (const int*)nullptr);
   }
   YTK_LAUNCH_CHECK();
 }
@@ -253,7 +282,8 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
 void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
                         uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
                         uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
-                        int slot_base, int nslots, uintptr_t slot_ids, uintptr_t stream) {
+                        int slot_base, int nslots, uintptr_t slot_ids, uintptr_t work_off_dev,
+                        uintptr_t stream) {
   if (nwork <= 0 || nslots <= 0) return;
   const int groups = (F + 31) / 32;
   const int nb_lds = B;
@@ -264,12 +294,14 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
     hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
+                       (const int*)work_off_dev);
   } else {
     hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
                        (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
                        (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging);
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
+                       (const int*)work_off_dev);
   }
   YTK_LAUNCH_CHECK();
   const int E = nb_lds * 32;

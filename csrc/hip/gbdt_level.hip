@@ -45,7 +45,7 @@ static_assert(sizeof(DNode) == 88, "DNode layout");
 
 enum {
   ST_NUM_NODES = 0, ST_NUM_LEAF, ST_N_PENDING, ST_N_SPLIT, ST_N_PART, ST_N_HIST,
-  ST_N_SITEMS, ST_N_BUILD, ST_WORDS = 16
+  ST_N_SITEMS, ST_N_BUILD, ST_N_HIST_A, ST_WORDS = 16
 };
 
 constexpr int kPlanThreads = 256;
@@ -408,6 +408,10 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
   const int nitems = block_exclusive_scan(s_small, nb, s_tmp);
   emit_all_chunks(b.hist_items, nitems, nb, s_small, s_hbeg, s_hcnt, s_hslot, ch, false);
   if (tid == 0) {
+    // items of the first half of the build slots (k < half/2): the multi-GPU engine
+    // all-reduces that half while the second half is still being built
+    const int hs = half >> 1;
+    st[ST_N_HIST_A] = (hs > 0 && nb > hs) ? s_small[hs] : nitems;
     st[ST_N_PENDING] = 2 * nb;
     st[ST_N_BUILD] = nb;
     st[ST_N_SITEMS] = 2 * nb;

@@ -35,6 +35,7 @@ DNODE_DTYPE = np.dtype([
     ("loss_chg", "<f4"), ("value", "<f4"), ("is_leaf", "<i4")])
 assert DNODE_DTYPE.itemsize == 88
 ST_NUM_NODES = 0
+ST_N_HIST_A = 8  # st word: hist items of the first half of a level's build slots
 
 MAX_DEPTH_DEVICE = 12
 
@@ -147,6 +148,9 @@ class DeviceLevelBuilder:
         groups = (F + 31) // 32
         max_hist_items = self.HIST_TARGET + (self.maxp // 2) + 2
         self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0"
+        # multi-GPU: overlap the all-reduce of half a level's histograms with the build of
+        # the other half (BASELINE: histogram all-reduce overlapped with the next block's build)
+        self.overlap = os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
         self.staging = (torch.empty(max_hist_items * groups * B * 32 * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
@@ -272,7 +276,7 @@ class DeviceLevelBuilder:
         off = lambda w: st_ptr + 4 * w
         h.lv_step(0, ptrs, ip, fp, 0, 0, s)
 
-        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots):
+        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0):
             if self._zero_all:
                 if slot_base == 0:
                     self.hist.zero_()  # every slot of the tree in one fill (small slabs)
@@ -280,8 +284,9 @@ class DeviceLevelBuilder:
                 self.hist[slot_base:slot_base + nslots].zero_()
             if self.staged:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
-                                 ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5),
-                                 ptr(self.scales), ptr(self.staging), slot_base, nslots, 0, s)
+                                 ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0,
+                                 off(5) if n_dev is None else n_dev, ptr(self.scales), ptr(self.staging),
+                                 slot_base, nslots, 0, work_off, s)
                 return
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
@@ -348,12 +353,27 @@ class DeviceLevelBuilder:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
-            build_hist(ptr(self.ghp), ptr(self.rows), self.HIST_TARGET + half + 1, base, half)
-            tm.mark("build_hist_compute")
-            if dist:
-                # built slots (+ this level's count slots when fused): one all-reduce
-                self.comm.allreduce_(self.hist[base:base + half + ncs])
+            nmax = self.HIST_TARGET + half + 1
+            if dist and self.overlap and half >= 2 and self.staged:
+                # two node halves: the first half's all-reduce (RCCL, async) overlaps the
+                # second half's histogram build; the split search waits for both
+                hs = half // 2
+                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A))
+                work = self.comm.allreduce_(self.hist[base:base + hs], async_op=True)
+                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
+                           work_off=off(ST_N_HIST_A))
+                tm.mark("build_hist_compute")
+                if work is not None:
+                    work.wait()
+                self.comm.allreduce_(self.hist[base + hs:base + half + ncs])
                 tm.mark("build_hist_comm")
+            else:
+                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base, half)
+                tm.mark("build_hist_compute")
+                if dist:
+                    # built slots (+ this level's count slots when fused): one all-reduce
+                    self.comm.allreduce_(self.hist[base:base + half + ncs])
+                    tm.mark("build_hist_comm")
             h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                          ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
                          gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),

@@ -92,7 +92,7 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
                 assert staging.numel() >= nwork * ((F + 31) // 32) * B * 64
                 h.hist_fx_staged(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                                  float(sg), float(sh), 0, 0, ptr(staging), slot_base, nslots, ptr(slot_ids),
-                                 stream(bins))
+                                 0, stream(bins))
             else:
                 h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                           float(sg), float(sh), 0, 0, stream(bins))
