@@ -22,6 +22,9 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
                     uintptr_t, uintptr_t);
 // gbdt_partition.hip
+void ytk_partition_atomic(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                          uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                          int, uintptr_t);
 void ytk_segment_copy(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -76,6 +79,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
   m.def("segment_copy", &ytk_segment_copy);
+  m.def("partition_atomic", &ytk_partition_atomic);
   m.def("tree_add_bins", &ytk_tree_add_bins);
   m.def("forest_predict", &ytk_forest_predict);
   m.def("bin_assign", &ytk_bin_assign);
@@ -90,7 +94,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fm_backward", &ytk_fm_backward);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
-    if (ptrs.size() != 25 || ip.size() != 6 || fp.size() != 6)
+    if (ptrs.size() != 26 || ip.size() != 6 || fp.size() != 6)
       throw std::invalid_argument("lv_step: bad argument sizes");
     ytk_lv_step(which, ptrs.data(), ip.data(), fp.data(), a0, a1, stream);
   });
@@ -98,7 +102,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                           uintptr_t coff, uintptr_t fill, int split_median, uintptr_t nfeat,
                           uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
                           uintptr_t nval, uintptr_t stream) {
-    if (ptrs.size() != 25) throw std::invalid_argument("lv_raw_tree: bad ptrs");
+    if (ptrs.size() != 26) throw std::invalid_argument("lv_raw_tree: bad ptrs");
     ytk_lv_raw_tree(ptrs.data(), max_nodes, cand, coff, fill, split_median, nfeat, nthr, nleft,
                     nright, ndefl, nval, stream);
   });

@@ -83,6 +83,7 @@ struct LvBufs {
   int* tright;
   float* tval;
   long long* root_cnt;   // [0] local, [1] global
+  int* part_cnt;         // per split: rows of this rank's segment (single-pass partition)
 };
 
 __device__ __forceinline__ double thr_l1d(double w, double lam) {
@@ -215,7 +216,8 @@ __global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBuf
 }
 
 // Apply split results, pop the level's nodes in FIFO order, emit partition chunks.
-__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b, int fused) {
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b, int fused,
+                                                                   int implicit_items) {
   __shared__ int s_aux[kMaxPend];   // candidate flag, later: split index / -1
   __shared__ int s_rank[kMaxPend];  // rank among the candidates (FIFO order)
   __shared__ int s_tmp[kPlanThreads + 1];
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
     const int nprev = st[ST_N_SPLIT];
     for (int s = tid; s < nprev; s += kPlanThreads) {
       const DNode& P = b.nodes[b.split_nid[s]];
-      const long long lg = b.left_glob[s];
+      const long long lg = b.left_glob[s] & 0xffffffffll;  // low half: left rows (see partition)
       b.nodes[P.left].cnt_global = lg;
       b.nodes[P.right].cnt_global = P.cnt_global - lg;
     }
@@ -298,6 +300,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
       b.part_thr[s] = (n.bin_a + n.bin_b) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
       b.part_begin[s] = n.begin;
       b.part_nblk[s] = n.cnt_local;              // temporarily: count
+      b.part_cnt[s] = n.cnt_local;
       b.left_loc[s] = 0;
       atomicAdd(reinterpret_cast<unsigned long long*>(&s_total), (unsigned long long)n.cnt_local);
     }
@@ -317,7 +320,9 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
   for (int s = tid; s < nsplit; s += kPlanThreads) b.part_nblk[s] = (s + 1 < nsplit ? b.part_first[s + 1] : nitems) - b.part_first[s];
   if (tid == 0) st[ST_N_PART] = nitems;
   __syncthreads();
-  emit_all_chunks(b.part_items, nitems, nsplit, b.part_first, b.part_begin, s_count, nullptr, ch, true);
+  // the single-pass partition maps its blocks to (split, chunk) itself from part_first
+  if (!implicit_items)
+    emit_all_chunks(b.part_items, nitems, nsplit, b.part_first, b.part_begin, s_count, nullptr, ch, true);
 }
 
 // Children of this level's splits: segments, terminal check, build / derive lists,
@@ -345,7 +350,9 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
     DNode& P = b.nodes[b.split_nid[s]];
     DNode& L = b.nodes[P.left];
     DNode& R = b.nodes[P.right];
-    const long long lloc = b.left_loc[s], lglob = lglob_arr[s];
+    // split cursors pack (right rows << 32) | left rows (single-pass partition); the
+    // count-only pass accumulates the left rows alone -- either way the low half
+    const long long lloc = b.left_loc[s] & 0xffffffffll, lglob = lglob_arr[s] & 0xffffffffll;
     reset_node(L, P.depth + 1);
     reset_node(R, P.depth + 1);
     L.begin = P.begin;
@@ -524,6 +531,7 @@ static LvBufs make_bufs(const uintptr_t* a) {
   b.tright = (int*)a[22];
   b.tval = (float*)a[23];
   b.root_cnt = (long long*)a[24];
+  b.part_cnt = (int*)a[25];
   return b;
 }
 
@@ -552,7 +560,9 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
     case 0: hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
-    case 1: hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1); break;
+    case 1:  // arg0 = 1: no partition work list (single-pass partition maps blocks itself)
+      hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1, arg0);
+      break;
     case 3:
       hipLaunchKernelGGL(lv_plan_children_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg0,
                          arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), (arg1 >> 30) & 1,

@@ -21,6 +21,7 @@ namespace ytk {
 
 constexpr int kPartThreads = 256;
 constexpr int kPartSub = 4;
+constexpr int kAtomSub = 8;  // single-pass partition: rows per block = 8 x 256 (one chunk)
 
 template <typename BinT>
 __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
@@ -155,6 +156,108 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
   }
 }
 
+
+// Single-pass partition (level engine): each block holds one <= 2048-row chunk in
+// registers, gathers its go-left flags, ranks them with wave ballots, reserves its left
+// run at the front and its right run at the BACK of the node segment with ONE 64-bit
+// atomic on the split's cursor ((right << 32) | left), and scatters row ids and (g, h). No flag
+// array, no count pass, one launch: 25 B/row instead of 31 B/row and two launches.
+// Chunks land in arbitrary order inside the left / right runs (rows inside a chunk keep
+// their order): positions are a free permutation for everything downstream -- the
+// int64 histograms, split counts and leaf values are order independent, so trees are
+// bitwise identical to the stable two-pass partition.
+template <typename BinT, bool kScatter>
+__global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
+    const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
+    const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
+    const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
+    const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
+    const int* __restrict__ node_begin, const int* __restrict__ node_count,
+    unsigned long long* __restrict__ cursor) {
+  // one chunk (<= kAtomSub * 256 rows) per block, held in registers: all loads issued
+  // up front, ONE cursor reservation per block, then the scatter. The block finds its
+  // (split, chunk) by binary search of first_blk (exclusive scan of the splits' chunk
+  // counts) -- no per-block work list. kScatter = false: left counts only (last level).
+  constexpr int NW = kPartThreads / kWave;
+  constexpr int S = kAtomSub;
+  constexpr int CH = kAtomSub * kPartThreads;
+  __shared__ int s_l[S * NW], s_v[S * NW];
+  __shared__ unsigned long long s_base;
+  const int bid = (int)blockIdx.x;
+  if (bid >= *nblocks_dev) return;
+  int lo = 0, hi = *nsplit_dev - 1;  // last split with first_blk <= bid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first_blk[mid] <= bid) lo = mid; else hi = mid - 1;
+  }
+  const int si = lo;
+  int4 it;
+  it.y = node_begin[si] + (bid - first_blk[si]) * CH;
+  it.z = min(it.y + CH, node_begin[si] + node_count[si]);
+  const BinT* col = binsT + (size_t)feat[si] * ncol;
+  const int th = thr[si];
+  const int nbeg = node_begin[si], nend = nbeg + node_count[si];
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  int r[S];
+  float2 g[S];
+  bool valid[S], left[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int pos = it.y + j * kPartThreads + tid;
+    valid[j] = pos < it.z;
+    r[j] = valid[j] ? (rows ? rows[pos] : pos) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int pos = it.y + j * kPartThreads + tid;
+    g[j] = (kScatter && valid[j]) ? ghp[pos] : make_float2(0.f, 0.f);
+    left[j] = valid[j] && (int)col[(unsigned)r[j]] <= th;
+  }
+  int lrank[S], vrank[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const unsigned long long lm = __ballot(left[j]);
+    const unsigned long long vm = __ballot(valid[j]);
+    lrank[j] = __popcll(lm & lt_mask);
+    vrank[j] = __popcll(vm & lt_mask);
+    if (l == 0) { s_l[j * NW + wid] = __popcll(lm); s_v[j * NW + wid] = __popcll(vm); }
+  }
+  __syncthreads();
+  int tl = 0, tv = 0;
+  int pl[S], pv[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) { pl[j] = 0; pv[j] = 0; }
+#pragma unroll
+  for (int k = 0; k < S * NW; ++k) {
+    const int kl = s_l[k], kv = s_v[k];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (k < j * NW + wid) { pl[j] += kl; pv[j] += kv; }
+    }
+    tl += kl;
+    tv += kv;
+  }
+  if (!kScatter) {  // count-only: the left rows of this chunk
+    if (tid == 0) atomicAdd(&cursor[si], (unsigned long long)tl);
+    return;
+  }
+  if (tid == 0)
+    s_base = atomicAdd(&cursor[si], ((unsigned long long)(tv - tl) << 32) | (unsigned long long)tl);
+  __syncthreads();
+  const int lofs = (int)(s_base & 0xffffffffull), rofs = (int)(s_base >> 32);
+  const int rstart = nend - rofs - (tv - tl);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    if (valid[j]) {
+      const int dst = left[j] ? nbeg + lofs + pl[j] + lrank[j]
+                              : rstart + (pv[j] - pl[j]) + (vrank[j] - lrank[j]);
+      rows_out[dst] = r[j];
+      gh_out[dst] = g[j];
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -228,5 +331,32 @@ extern "C" void ytk_segment_copy(uintptr_t items, int nitems, uintptr_t src_rows
   hipLaunchKernelGGL(segment_copy_kernel, dim3(nitems), dim3(kPartThreads), 0,
                      reinterpret_cast<hipStream_t>(stream), (const int4*)items,
                      (const int*)src_rows, (int*)dst_rows, (const float2*)src_gh, (float2*)dst_gh);
+  YTK_LAUNCH_CHECK();
+}
+
+// cursor: per split, zeroed by the caller; on return low 32 bits = left rows, high 32 =
+// right rows (scatter) or the left rows alone (count_only). first_blk: exclusive scan of
+// ceil(node_count / 2048) per split; nsplit_dev / nblocks_dev: device-resident counts;
+// grid = max_blocks (blocks past *nblocks_dev exit).
+extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long ncol, uintptr_t rows,
+                                     uintptr_t rows_out, uintptr_t ghp, uintptr_t gh_out,
+                                     uintptr_t first_blk, uintptr_t nsplit_dev, uintptr_t nblocks_dev,
+                                     int max_blocks, uintptr_t feat, uintptr_t thr, uintptr_t node_begin,
+                                     uintptr_t node_count, uintptr_t cursor, int count_only,
+                                     uintptr_t stream) {
+  if (max_blocks <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_PART_ATOMIC(BT, SC)                                                                   \
+  hipLaunchKernelGGL((partition_atomic_kernel<BT, SC>), dim3(max_blocks), dim3(kPartThreads), 0, s, \
+                     (const BT*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,  \
+                     (float2*)gh_out, (const int*)first_blk, (const int*)nsplit_dev,               \
+                     (const int*)nblocks_dev, (const int*)feat, (const int*)thr,                   \
+                     (const int*)node_begin, (const int*)node_count, (unsigned long long*)cursor)
+  if (bin_bytes == 1) {
+    if (count_only) YTK_PART_ATOMIC(uint8_t, false); else YTK_PART_ATOMIC(uint8_t, true);
+  } else {
+    if (count_only) YTK_PART_ATOMIC(uint16_t, false); else YTK_PART_ATOMIC(uint16_t, true);
+  }
+#undef YTK_PART_ATOMIC
   YTK_LAUNCH_CHECK();
 }

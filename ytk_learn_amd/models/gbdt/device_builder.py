@@ -95,7 +95,13 @@ class DeviceLevelBuilder:
         ml = p.max_leaf_cnt if p.max_leaf_cnt > 0 else (1 << 30)
         self.max_nodes = int(min((1 << (D + 1)) - 1, 2 * ml - 1))
         self.maxp = 1 << D
-        self.max_items = max(self.HIST_TARGET, self.PART_TARGET) + self.maxp + 16
+        # single-pass partition: one tile reservation (a global atomic round trip) per
+        # 1024 rows, so chunks stay at MIN_ROWS (2 tiles) and the latency hides behind
+        # ~N/2048 resident blocks instead of ~10 serial reservations per block
+        # (the kernel holds one chunk of <= 2048 rows per block in registers)
+        self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0" and self.MIN_ROWS == 2048
+        self.part_target = (-(-self.N // self.MIN_ROWS) + 1) if self.part_atomic else self.PART_TARGET
+        self.max_items = max(self.HIST_TARGET, self.part_target) + self.maxp + 16
         dev = self.dev
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
         # everything a finished tree is (state, node table, scoring arrays) lives in ONE
@@ -111,6 +117,7 @@ class DeviceLevelBuilder:
         self.part_feat, self.part_thr, self.part_begin = i32(self.maxp), i32(self.maxp), i32(self.maxp)
         self.part_first, self.part_nblk = i32(self.maxp), i32(self.maxp)
         self.part_counts = i32(self.max_items)
+        self.part_cnt = i32(self.maxp)
         self.left_loc = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
         self.left_glob = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
         self.hist_items = i32(self.max_items * 4)
@@ -162,7 +169,7 @@ class DeviceLevelBuilder:
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
-        self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.HIST_TARGET, self.PART_TARGET,
+        self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.HIST_TARGET, self.part_target,
                    self.MIN_ROWS]
         self.tree_count = 0
         self.last_keep = None
@@ -192,7 +199,7 @@ class DeviceLevelBuilder:
                                 self.part_begin, self.part_first, self.part_nblk, self.part_counts,
                                 self.left_loc, self.left_glob, self.hist_items, self.split_items,
                                 self.item_nid, self.split_out, self.tfeat, self.tthr, self.tleft,
-                                self.tright, self.tval, self.root_cnt)]
+                                self.tright, self.tval, self.root_cnt, self.part_cnt)]
         if loc is not None:
             out[13] = loc
         if glob is not None:
@@ -313,14 +320,22 @@ class DeviceLevelBuilder:
                 loc = self.left_loc if last else None
                 ptrs = self._ptrs(loc=ptr(loc) if loc is not None else self._count_ptr(c),
                                   glob=self._count_ptr(d) if d >= 1 else None)
-            h.lv_step(1, ptrs, ip, fp, 0, 1 if (fused and d >= 1) else 0, s)  # apply splits + pop depth d
+            # apply splits + pop depth d (arg0 = 1: the single-pass partition needs no work list)
+            h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, 1 if (fused and d >= 1) else 0, s)
             tm.mark("plan")
-            npart = self.PART_TARGET + (1 << d) + 1
+            npart = self.part_target + (1 << d) + 1
             lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
             # the flag kernel also accumulates the per-split left totals into left_loc
-            if last:
+            if self.part_atomic:
+                # the split cursors are the (zeroed) per-split left counters: low half = left
+                # rows, high half = right rows; the last level only counts
+                h.partition_atomic(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
+                                   gh_in, ptr(self.gh_tmp), ptr(self.part_first), off(3), off(4), npart,
+                                   ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
+                                   ptr(self.part_cnt), lloc, 1 if last else 0, s)
+            elif last:
                 h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.flags),
                                   ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),
                                   ptr(self.part_counts), off(4), lloc, s)
