@@ -540,7 +540,7 @@ class TreeBuilder:
         return tid
 
     # ------------------------------------------------------------------ build
-    def build(self, gh: torch.Tensor, ghmax: Optional[torch.Tensor] = None) -> Tree:
+    def build(self, gh: torch.Tensor, ghmax: Optional[torch.Tensor] = None, ghmax_global: bool = False) -> Tree:
         """Grow one tree from gh [N, 2] (grad*w, hess*w) in row order. ``ghmax`` (optional,
         float32 [2]): max |g|, |h| over the rows, already produced by the gradient kernel."""
         p = self.p
@@ -595,13 +595,13 @@ class TreeBuilder:
 
         n_global = int(self.comm.allreduce_scalars([n_local], dtype=torch.int64)[0]) if self.comm.is_dist else n_local
         # per-tree fixed-point scales from the global max |g|, |h| (identical on every rank)
-        if ghmax is not None and identity:
+        if ghmax is not None and (identity or ghmax_global):
             mx = ghmax.double()
         elif n_local > 0:
             mx = (self._root_gh if identity else self.ghp[:n_local]).abs().amax(dim=0).double()
         else:
             mx = torch.zeros(2, dtype=torch.float64, device=self.dev)
-        if self.comm.is_dist:
+        if self.comm.is_dist and not ghmax_global:
             self.comm.allreduce_(mx, op="max")
         mx = mx.cpu().numpy()
         sg, sh = gops.fixed_point_scales(mx[0], mx[1], n_global)

@@ -223,7 +223,7 @@ class DeviceLevelBuilder:
         return self._fmask_cache[key], int(np.nonzero(fm)[0][0])
 
     # ------------------------------------------------------------------ build
-    def build(self, gh: torch.Tensor, ghmax: torch.Tensor = None) -> DeviceTree:
+    def build(self, gh: torch.Tensor, ghmax: torch.Tensor = None, ghmax_global: bool = False) -> DeviceTree:
         """Enqueue one tree. ``gh`` [N, 2] contiguous (g, h); ``ghmax`` (float32 [2], optional)
         = max |g|, max |h| over all local rows, already produced by the gradient kernel."""
         p = self.p
@@ -265,13 +265,15 @@ class DeviceLevelBuilder:
                     self.comm.allreduce_(self._n_global)
                 self.root_cnt[1:2].copy_(self._n_global)
         # fixed-point scales from the global max |g|, |h| over the tree's rows
-        if sampled:
+        if ghmax is not None and ghmax_global:  # a global bound: identical on every rank
+            mx = ghmax
+        elif sampled:
             mx = (gh.abs() * keep[:, None]).amax(dim=0)
         elif ghmax is not None:
             mx = ghmax
         else:
             mx = gh.abs().amax(dim=0)
-        if dist:
+        if dist and not ghmax_global:
             mx = mx.clone()
             self.comm.allreduce_(mx, op="max")
         h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
@@ -369,7 +371,8 @@ class DeviceLevelBuilder:
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
             nmax = self.HIST_TARGET + half + 1
-            if dist and self.overlap and half >= 2 and self.staged:
+            if dist and self.overlap and half >= 8 and self.staged:  # large levels only:
+                # small ones are latency bound and a second collective would cost more
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
                 # second half's histogram build; the split search waits for both
                 hs = half // 2

@@ -13,6 +13,7 @@ device node tables into model trees lazily (``materialize``).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence
@@ -161,6 +162,16 @@ class GBDTTrainer:
         self.w = tr.weight.contiguous() if tr.weight is not None else None
         sums = self.comm.allreduce_scalars([float(tr.weight.sum()) if tr.weight is not None else float(N), float(N)])
         self.train_wsum, self.train_real = sums
+        # Sigmoid: |g| <= w and h <= w * max(1/4, 1/zmax) for every row, so the fixed-point
+        # scales come from this global bound instead of a per-tree max all-reduce (one RCCL
+        # latency less per tree). Used on any world size -> trees stay bitwise identical.
+        self.ghmax_fixed = None
+        if self.kernel_loss == "sigmoid" and self.K == 1 and os.environ.get("YTK_GH_BOUND", "1") != "0":
+            wmax = float(tr.weight.max()) if (tr.weight is not None and N > 0) else 1.0
+            wmax = self.comm.allreduce_scalars([wmax], op="max")[0]
+            zmax = float(self.p.sigmoid_zmax)
+            hb = max(0.25, 1.0 / zmax) if zmax > 0 else 0.25
+            self.ghmax_fixed = torch.tensor([wmax, wmax * hb], dtype=torch.float32, device=self.dev)
         if self.test_data is not None:
             te = self.test_data
             self.Xte = torch.where(torch.isnan(te.X), self.fill_dev[None, :], te.X).contiguous()
@@ -297,7 +308,10 @@ class GBDTTrainer:
         arrays, raws, host_trees, dev_trees = [], [], [], []
         for k in range(self.K):
             if self.use_device_builder:
-                dt = self.builder.build(self.gh[k], self.ghmax[k])
+                if self.ghmax_fixed is not None:
+                    dt = self.builder.build(self.gh[k], self.ghmax_fixed, ghmax_global=True)
+                else:
+                    dt = self.builder.build(self.gh[k], self.ghmax[k])
                 dev_trees.append(dt)
                 arrays.append(dt.bin_arrays)
                 if self.test_data is not None:
@@ -306,7 +320,8 @@ class GBDTTrainer:
                     raw["troot"], raw["tout"] = self._one_tree[k]
                     raws.append(raw)
             else:
-                tree = self.builder.build(self.gh[k], self.ghmax[k])
+                tree = self.builder.build(self.gh[k], self.ghmax_fixed if self.ghmax_fixed is not None
+                                          else self.ghmax[k], ghmax_global=self.ghmax_fixed is not None)
                 if self.refiner is not None:
                     self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
                                         + self.init_score[:, k], self.w, lr)
