@@ -423,11 +423,6 @@ class TreeBuilder:
         state = {"num_leaf": 1, "seq": 1}
         heap = [(-float(nodes[0].rec["loss_chg"]), 0, 0)]
 
-        def would_split(nd: _Node):  # pop-time rules that do not depend on the leaf count
-            return not (nd.rec["loss_chg"] <= p.min_split_loss
-                        or (p.max_depth >= 0 and p.max_depth == nd.depth)
-                        or (p.min_split_samples > 0 and nd.cnt_global < p.min_split_samples))
-
         def expand(batch: List[int]):
             splits, counts_only = [], []
             for sid in batch:
