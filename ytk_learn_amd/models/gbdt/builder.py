@@ -68,18 +68,19 @@ class TimeStats:
     comm_hist: float = 0.0
     find_split: float = 0.0
     partition: float = 0.0
+    plan: float = 0.0  # host-side expansion planning (leaf-wise replay)
     total: float = 0.0
     trees: int = 0
 
     def add(self, o: "TimeStats"):
-        for k in ("build_hist", "comm_hist", "find_split", "partition", "total"):
+        for k in ("build_hist", "comm_hist", "find_split", "partition", "plan", "total"):
             setattr(self, k, getattr(self, k) + getattr(o, k))
         self.trees += o.trees
 
     def stats(self) -> str:
         return (f"[time stats] trees={self.trees} total={self.total:.4f}s build_hist={self.build_hist:.4f}s "
                 f"comm_hist={self.comm_hist:.4f}s find_split={self.find_split:.4f}s "
-                f"partition={self.partition:.4f}s")
+                f"partition={self.partition:.4f}s plan={self.plan:.4f}s")
 
 
 @dataclass
@@ -214,6 +215,7 @@ class TreeBuilder:
         self._root_gh = None
         self._staging = None
         self.free_slots = None
+        self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0"
         self.fmask_np = np.ones(F, np.uint8)
 
     # ------------------------------------------------------------------ utils
@@ -297,11 +299,14 @@ class TreeBuilder:
         self.up.reset()  # the .cpu() above synchronised the stream
         t3 = time.perf_counter()
         mcw2 = self.p.min_child_hessian_sum * 2.0
-        for nid, r in zip(order, recs):
+        names = gops.SPLIT_DTYPE.names
+        # plain dicts of Python scalars: the host bookkeeping then avoids numpy scalar ops
+        for nid, tup in zip(order, recs.tolist()):
+            r = dict(zip(names, tup))  # loss_chg: the exact double of the float32 gain
             nd = nodes[nid]
             nd.rec = r
-            nd.G = float(r["g"])
-            nd.H = float(r["h"])
+            nd.G = r["g"]
+            nd.H = r["h"]
             # canSplit (UpdateStrategy.canSplit): H >= 2*mcw and n >= min_split_samples
             if not (nd.H >= mcw2 and nd.cnt_global >= self.p.min_split_samples):
                 r["loss_chg"] = -np.inf
@@ -332,12 +337,22 @@ class TreeBuilder:
         feat = np.array([int(nodes[x[0]].rec["feat"]) for x in splits], np.int32)
         thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
                        np.int32)
-        items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d = self.up.put(
-            items, feat, thr, begins, first, nblk)
         root = self._root_gh is not None  # first partition of an unsampled tree: identity rows
-        left = gops.partition(self.binsT, None if root else self.rows, self.rows_tmp,
-                              self._root_gh if root else self.ghp, self.gh_tmp, self.flags,
-                              items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d, n)
+        rows_in, gh_in = (None, self._root_gh) if root else (self.rows, self.ghp)
+        if self.dev.type == "cuda" and self.part_atomic:
+            # single-pass partition: 2048-row chunks mapped from an exclusive block scan
+            nb_a = (counts + gops.PART_CHUNK - 1) // gops.PART_CHUNK
+            first_a = np.concatenate([[0], np.cumsum(nb_a)[:-1]]) if n else np.zeros(0, np.int64)
+            hdr = np.array([n, int(nb_a.sum())], np.int32)
+            items_d, feat_d, thr_d, nbeg_d, cnt_d, first_d, hdr_d = self.up.put(
+                items, feat, thr, begins, counts, first_a, hdr)
+            left = gops.partition_atomic(self.binsT, rows_in, self.rows_tmp, gh_in, self.gh_tmp, first_d,
+                                         hdr_d, int(hdr[1]), feat_d, thr_d, nbeg_d, cnt_d)
+        else:
+            items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d = self.up.put(
+                items, feat, thr, begins, first, nblk)
+            left = gops.partition(self.binsT, rows_in, self.rows_tmp, gh_in, self.gh_tmp, self.flags,
+                                  items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d, n)
         if root:  # the root segment is every row: take the output buffers whole
             copy_back = False
             self._root_gh = None
@@ -458,6 +473,7 @@ class TreeBuilder:
                 nd.slot = -1
 
         while True:
+            t_plan = time.perf_counter()
             # replay the sequential priority-queue growth as far as the known gains allow
             blocked = False
             while heap:
@@ -529,6 +545,8 @@ class TreeBuilder:
                     heapq.heappush(vheap, (-float(nl.rec["loss_chg"]), vseq, lcs))
                     heapq.heappush(vheap, (-float(nr.rec["loss_chg"]), vseq + 1, rcs))
                     vseq += 2
+            t_exp = time.perf_counter()
+            self.last_stats.plan += t_exp - t_plan
             expand(batch)
             self.last_batches += 1
             self.last_expanded += len(batch)
@@ -610,15 +628,17 @@ class TreeBuilder:
         lr32 = np.float32(p.learning_rate)
 
         def pop_is_leaf(nd: _Node, num_leaf: int):
-            return (nd.rec["loss_chg"] <= p.min_split_loss
+            return (nd.rec["loss_chg"] <= msl32
                     or (p.max_depth >= 0 and p.max_depth == nd.depth)
                     or (max_leaf > 0 and max_leaf == num_leaf)
                     or (p.min_split_samples > 0 and nd.cnt_global < p.min_split_samples))
 
+        gpv = (self.gp["mcw"], self.gp["l1"], self.gp["l2"], self.gp["max_abs_leaf"])
+        msl32 = float(np.float32(p.min_split_loss))  # the kernels compare float32 gains to it
+
         def make_leaf(nid, t=None):
             nd = nodes[nid]
-            v = np.float32(gops.node_value_np(nd.G, nd.H, self.gp["mcw"], self.gp["l1"], self.gp["l2"],
-                                              self.gp["max_abs_leaf"]))
+            v = np.float32(gops.node_value_py(nd.G, nd.H, *gpv))
             tree.set_leaf(nid if t is None else t, float(v * lr32))
 
         def children_terminal(nd_l: _Node, nd_r: _Node, nleaf: int):

@@ -362,7 +362,9 @@ class GBDTTrainer:
         self.rounds_done = i + 1
 
     def _convert(self, tree: Tree):
-        tree.convert_split_values(self.mapper.cands, self.p.split_type)
+        if getattr(self, "_cands32", None) is None:  # float32 candidate tables, built once
+            self._cands32 = [np.asarray(c, dtype=np.float32) for c in self.mapper.cands]
+        tree.convert_split_values(self._cands32, self.p.split_type)
         tree.add_feature_names(self.feature_names)
         tree.add_default_direction(self.missing_fill)
 

@@ -131,7 +131,9 @@ class Tree:
         for i in range(self.num_nodes):
             if self.is_leaf[i]:
                 continue
-            c = cand_sorted[self.feat[i]].astype(np.float32)
+            c = cand_sorted[self.feat[i]]
+            if c.dtype != np.float32:
+                c = c.astype(np.float32)
             a, b = self.slot_a[i], self.slot_b[i]
             if split_type == "mean":
                 v = np.float32(0.5) * (c[a] + c[b])

@@ -163,6 +163,20 @@ def node_value_np(g, h, mcw, l1, l2, mal):
     return np.where(h < mcw, 0.0, v)
 
 
+def node_value_py(g: float, h: float, mcw: float, l1: float, l2: float, mal: float) -> float:
+    """Scalar ``node_value_np`` in plain Python floats (IEEE double, same results)."""
+    if h < mcw:
+        return 0.0
+    if l1 == 0.0:
+        v = -g / (h + l2)
+    else:
+        t = g - l1 if g > l1 else (g + l1 if g < -l1 else 0.0)
+        v = -t / (h + l2)
+    if mal > 0:
+        v = min(max(v, -mal), mal)
+    return v
+
+
 def calc_gain_np(g, h, mcw, l1, l2, mal):
     g = np.asarray(g, dtype=np.float64)
     h = np.asarray(h, dtype=np.float64)
@@ -260,6 +274,27 @@ def partition(binsT, rows, rows_out, ghp, gh_out, flags, items, feat, thr, node_
         gh_out[b + nl:e] = g[~go]
         left[i] = nl
     return left
+
+
+PART_CHUNK = 2048  # rows per block of the single-pass partition kernel
+
+
+def partition_atomic(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, nblocks, feat, thr,
+                     node_begin, node_count):
+    """Single-pass partition (GPU): each 2048-row chunk reserves its left run at the front
+    and its right run at the back of its node segment with one atomic; chunks land in
+    any order (rows inside a chunk keep theirs). hdr int32 [2] = (n_split, n_blocks) on the
+    device; first_blk = exclusive scan of ceil(count / 2048). Returns left counts (int64)."""
+    n = feat.shape[0]
+    cursor = torch.zeros(max(n, 1), dtype=torch.int64, device=binsT.device)[:n]
+    if nblocks == 0 or n == 0:
+        return cursor
+    check_cuda(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, feat, thr, node_begin, node_count)
+    hip().partition_atomic(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(rows_out),
+                           ptr(ghp), ptr(gh_out), ptr(first_blk), ptr(hdr), ptr(hdr) + 4, nblocks,
+                           ptr(feat), ptr(thr), ptr(node_begin), ptr(node_count), ptr(cursor), 0,
+                           stream(binsT))
+    return cursor & 0xFFFFFFFF
 
 
 def segment_copy(items, src_rows, dst_rows, src_gh, dst_gh):
