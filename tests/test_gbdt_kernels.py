@@ -327,3 +327,52 @@ def test_hist_build_staged_matches_cpu(cuda, F, nb, N, items_per_slot):
                         staging=staging, slot_base=2, nslots=nslot,
                         slot_ids=None if slot_ids is None else torch.tensor(slot_ids, dtype=torch.int32, device=cuda))
         assert torch.equal(hg.cpu(), hc), f"slot_ids={slot_ids}"
+
+
+@pytest.mark.parametrize("identity", [False, True])
+def test_partition_atomic_is_a_segmentwise_partition(cuda, identity):
+    """Single-pass partition: same left counts as the stable CPU partition and, per segment,
+    the same SET of (row, g, h) on each side (chunk order inside a side is free); rows
+    outside the split segments are untouched."""
+    N, F = 100000, 28
+    bins = _rand_bins(N, F, 255, 9)
+    rows = (torch.arange(N, dtype=torch.int32) if identity
+            else torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32))
+    segs = [(0, 30000), (30000, 4500), (40000, 1), (75000, 25000)]
+    feat = torch.tensor([3, 17, 5, 0], dtype=torch.int32)
+    thr = torch.tensor([100, 7, 30, 250], dtype=torch.int32)
+    binsT = bins[:, :F].t().contiguous()
+    gh = _gh(N, 11)
+    # CPU reference: stable partition of every segment
+    items, first, nblk = [], [], []
+    for i, (b, c) in enumerate(segs):
+        first.append(len(items))
+        items.append((i, b, b + c, 0))
+        nblk.append(1)
+    args = [torch.tensor(items, dtype=torch.int32), feat, thr, torch.tensor([s[0] for s in segs], dtype=torch.int32),
+            torch.tensor(first, dtype=torch.int32), torch.tensor(nblk, dtype=torch.int32)]
+    oc = torch.full((N,), -1, dtype=torch.int32)
+    ghc = torch.zeros(N, 2)
+    lc = gops.partition(binsT, rows, oc, gh, ghc, torch.zeros(N, dtype=torch.uint8), *args, len(segs))
+    # GPU single pass
+    counts = np.array([c for _, c in segs], np.int64)
+    nb = (counts + gops.PART_CHUNK - 1) // gops.PART_CHUNK
+    first_a = np.concatenate([[0], np.cumsum(nb)[:-1]])
+    hdr = torch.tensor([len(segs), int(nb.sum())], dtype=torch.int32, device=cuda)
+    og = torch.full((N,), -1, dtype=torch.int32, device=cuda)
+    ghg = torch.zeros(N, 2, device=cuda)
+    lg = gops.partition_atomic(binsT.to(cuda), None if identity else rows.to(cuda), og,
+                               gh.to(cuda), ghg, torch.from_numpy(first_a.astype(np.int32)).to(cuda), hdr,
+                               int(nb.sum()), feat.to(cuda), thr.to(cuda),
+                               torch.tensor([s[0] for s in segs], dtype=torch.int32, device=cuda),
+                               torch.from_numpy(counts.astype(np.int32)).to(cuda))
+    assert lg.cpu().tolist() == lc.tolist()
+    og, ghg = og.cpu(), ghg.cpu()
+    covered = torch.zeros(N, dtype=torch.bool)
+    for (b, c), nl in zip(segs, lc.tolist()):
+        for lo, hi in ((b, b + nl), (b + nl, b + c)):
+            covered[lo:hi] = True
+            kc = sorted(zip(oc[lo:hi].tolist(), ghc[lo:hi, 0].tolist(), ghc[lo:hi, 1].tolist()))
+            kg = sorted(zip(og[lo:hi].tolist(), ghg[lo:hi, 0].tolist(), ghg[lo:hi, 1].tolist()))
+            assert kc == kg
+    assert bool((og[~covered] == -1).all())
