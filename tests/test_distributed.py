@@ -74,11 +74,15 @@ def test_lbfgs_world2_matches_world1(tmp_path, task):
 
 
 @pytest.mark.gpu
-def test_gpu_level_builder_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("task,world", [("gbdt", 2), ("gbdt", 4), ("gbdt_loss", 3)])
+def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world):
+    """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
+    overlapped half-level all-reduce, global gradient bound) and the leaf-wise speculative
+    builder (scattered slot all-reduce) must give the world-1 model byte for byte."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = {"YTK_DIST_BACKEND": "gloo"}
-    _run("gbdt", tmp_path / "w1", 1, "cuda", extra_env=env)
-    _run("gbdt", tmp_path / "w2", 2, "cuda", extra_env=env)
-    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / "w2" / "model.txt").read()
+    _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
+    _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
+    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
