@@ -149,7 +149,7 @@ class DeviceLevelBuilder:
         self.n_slots = max(1, nxt)
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
         self._slot_bytes = slot_elems * 8
-        self._n_global = None
+        self._root_fixed = False
         # staged histogram flush: block partials to a staging slab with plain stores, then a
         # split-K slot reduce (8 int64 atomics per value instead of one per block)
         groups = (F + 31) // 32
@@ -251,19 +251,21 @@ class DeviceLevelBuilder:
             self.last_keep = keep
             rows0, gh0 = ptr(self.rows), ptr(self.ghp)
         else:
-            self.root_cnt[0] = self.N
             self.last_keep = None
             rows0, gh0 = 0, ptr(gh)
         fmask, f0 = self._fmask(rng)
-        self.root_cnt[1] = self.root_cnt[0]
-        if dist:
-            if sampled:
+        if sampled:
+            self.root_cnt[1] = self.root_cnt[0]
+            if dist:
                 self.comm.allreduce_(self.root_cnt[1:2])
-            else:  # the global row count is fixed: one all-reduce for the whole run
-                if self._n_global is None:
-                    self._n_global = self.root_cnt[1:2].clone()
-                    self.comm.allreduce_(self._n_global)
-                self.root_cnt[1:2].copy_(self._n_global)
+            self._root_fixed = False
+        elif not self._root_fixed:
+            # unsampled: (local, global) row counts are constants -- set once, not per tree
+            self.root_cnt[0] = self.N
+            self.root_cnt[1] = self.N
+            if dist:
+                self.comm.allreduce_(self.root_cnt[1:2])
+            self._root_fixed = True
         # fixed-point scales from the global max |g|, |h| over the tree's rows
         if ghmax is not None and ghmax_global:  # a global bound: identical on every rank
             mx = ghmax

@@ -331,10 +331,12 @@ class GBDTTrainer:
             self.timer.mark("build_tree")
         # score update + train loss after this round + gradients for the next round
         if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
-            self.ghmax.zero_()
+            need_max = self.ghmax_fixed is None  # the global bound replaces the per-tree max
+            if need_max:
+                self.ghmax.zero_()
             acc = gops.tree_grad(self.bins, arrays[0], self.score, self.init_score, self.y, self.w,
                                  self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0],
-                                 True, self.ghmax[0])
+                                 True, self.ghmax[0] if need_max else None)
         else:
             for k in range(self.K):
                 gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
