@@ -1,6 +1,6 @@
-# quick GPU iteration: gpu tests, full + 1/8-shard bench, 1/8-shard kernel timeline
+# quick GPU iteration: gpu tests, full + 1/8-shard bench, 1/8-shard one-round kernel timeline
 set -o pipefail
-O=gpurun_out/g3; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/iter; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
