@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="latent dim (default fm 16, ffm 4)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--optimizer", default="lbfgs", choices=["lbfgs", "sgd"],
+                    help="sgd: a step is one epoch of mini-batch Hogwild!-style SGD over the local rows")
+    ap.add_argument("--batch", type=int, default=65536, help="sgd mini-batch rows")
     a = ap.parse_args()
     comm = Comm.from_env()
     dev = comm.device
@@ -100,6 +103,41 @@ def main():
         from ytk_learn_amd.models.continuous.ffm import FFMModel
         model = FFMModel(params, loaded, comm, log)
     setup_s = time.perf_counter() - t0
+    if a.optimizer == "sgd":
+        from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
+        ng = model.ngroups if hasattr(model, "ngroups") else 1
+        sgd = SGDOptimizer(model, SGDParams(learning_rate=0.01, batch_size=a.batch, epochs=1), [0.0] * ng,
+                           [1e-6] * ng, comm, log, tot, tot)
+        bounds = [(b, min(b + a.batch, n)) for b in range(0, n, a.batch)]
+
+        def epoch():
+            for b, e in bounds:
+                sgd._step(model.w, b, e, 0.01)
+            sgd._average(model.w)
+
+        for _ in range(a.warmup):
+            epoch()
+        comm.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            epoch()
+        sync()
+        comm.barrier()
+        el = time.perf_counter() - t0
+        el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+        pure, _ = sgd._losses(model.w)
+        if comm.rank == 0:
+            print(json.dumps({
+                "metric": f"{a.model} SGD epoch (criteo-shape, {a.fields} fields, {a.features} features, k={k}, "
+                          f"batch {a.batch})",
+                "value": round(a.rows * comm.world / (el / a.steps), 1), "unit": "rows/s",
+                "ms_per_step": round(1000.0 * el / a.steps, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows,
+                "dim": int(model.w.numel()), "nnz_per_row": a.fields + 1, "scaling": "weak", "dtype": "fp32",
+                "data": "synthetic Criteo-shape", "train_loss": pure / tot,
+            }), flush=True)
+        comm.close()
+        return
     opt = HoagOptimizer(model, LineSearchParams(m=12), [0.0] * model.ngroups if hasattr(model, "ngroups") else [0.0],
                         [1e-6] * (model.ngroups if hasattr(model, "ngroups") else 1), comm, log, tot)
     g = torch.zeros_like(model.w)

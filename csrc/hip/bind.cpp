@@ -55,6 +55,8 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
                       int, int, uintptr_t);
 // fm.hip
+void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
+                       uintptr_t, float, float, float, int, int, int, uintptr_t);
 void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                     uintptr_t, uintptr_t);
 void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
@@ -92,6 +94,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("dot", &ytk_dot);
   m.def("fm_forward", &ytk_fm_forward);
   m.def("fm_backward", &ytk_fm_backward);
+  m.def("fm_sgd_update", &ytk_fm_sgd_update);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 26 || ip.size() != 6 || fp.size() != 6)

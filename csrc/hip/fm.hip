@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void fm_forward_kernel(
 #pragma unroll
   for (int off = G / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, G);
   if (f < k) S[gid * k + f] = s;
-  if (f == 0) fx[gid] = part;
+  if (f == 0) fx[gid] = part;  // (k == 0: no latent lanes, S may be null)
 }
 
 // part[chunk, 0:k] = sum c_r x S_r;  part[chunk, k] = sum c_r x;  part[chunk, k+1] = sum c_r x^2
@@ -115,6 +115,52 @@ __global__ __launch_bounds__(256) void fm_backward_kernel(
   if (f == 0) { o[k] = lin; o[k + 1] = sq; }
 }
 
+
+// Hogwild!-style SGD update for linear / FM weights (optimization.optimizer = "sgd").
+// One G-lane group per row of a mini-batch (the same mapping as fm_forward, whose S = X V
+// rows it reuses): after the batch's loss derivatives c_r are known, every lane f walks
+// the row's entries and applies, without locks, the per-sample gradient step
+//   w_i  -= lr * (c_r x_i + l2w w_i)                       (lane 0)
+//   V_if -= lr * (c_r x_i (S_rf - V_if x_i) + l2v V_if)     (lane f < k)
+// with no-return hardware float atomics -- concurrent rows touching the same feature
+// race exactly as in Hogwild! (updates are never lost, reads may be stale). reg_skip is
+// the bias index (not regularised; its latent row is frozen unless bias_latent);
+// upd_w = 0 leaves all linear weights but the bias untouched (k[0] < 1).
+template <int G>
+__global__ __launch_bounds__(256) void fm_sgd_update_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
+    long long nrows, float* __restrict__ w, float* __restrict__ V, int k, const float* __restrict__ S,
+    const float* __restrict__ c, float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent) {
+  const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
+  const int f = threadIdx.x & (G - 1);
+  if (gid >= nrows) return;
+  const float cr = c[gid];
+  if (cr == 0.f) return;  // group-uniform
+  const long long b = indptr[gid], e = indptr[gid + 1];
+  const float s = (f < k) ? S[gid * k + f] : 0.f;
+  for (long long t = b; t < e; t += G) {
+    int my_i = 0;
+    float my_x = 0.f;
+    if (t + f < e) { my_i = idx[t + f]; my_x = val[t + f]; }
+    const int n = (int)min<long long>(G, e - t);
+    for (int j = 0; j < n; ++j) {
+      const int i = __shfl(my_i, j, G);
+      const float x = __shfl(my_x, j, G);
+      const bool is_bias = i == reg_skip;
+      if (f == 0 && (upd_w || is_bias)) {
+        const float gw = cr * x + (is_bias ? 0.f : l2w * w[i]);
+        unsafeAtomicAdd(w + i, -lr * gw);
+      }
+      if (f < k && (!is_bias || bias_latent)) {
+        float* vp = V + (long long)i * k + f;
+        const float v = *vp;
+        const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
+        unsafeAtomicAdd(vp, -lr * gv);
+      }
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -131,7 +177,8 @@ extern "C" {
 void ytk_fm_forward(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
                     uintptr_t V, int k, uintptr_t fx, uintptr_t S, uintptr_t stream) {
   if (nrows <= 0) return;
-  if (k < 1 || k > 64) throw std::invalid_argument("fm_forward: 1 <= k <= 64");
+  // k == 0: the linear score alone (S unused) -- the SGD optimizer's linear-model forward
+  if (k < 0 || k > 64) throw std::invalid_argument("fm_forward: 0 <= k <= 64");
   const int G = fm_group(k);
   const long long threads = nrows * G;
   const dim3 grid((unsigned)((threads + 255) / 256));
@@ -177,4 +224,31 @@ void ytk_fm_backward(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, ui
   YTK_LAUNCH_CHECK();
 }
 
+// indptr: the batch's row pointers (absolute offsets into idx / val); V / S may be null
+// when k == 0 (linear model).
+void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
+                       uintptr_t V, int k, uintptr_t S, uintptr_t c, float lr, float l2w, float l2v,
+                       int reg_skip, int upd_w, int bias_latent, uintptr_t stream) {
+  if (nrows <= 0) return;
+  if (k < 0 || k > 64) throw std::invalid_argument("fm_sgd_update: 0 <= k <= 64");
+  const int G = k == 0 ? 4 : fm_group(k);
+  const long long threads = nrows * G;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_FM_S(GG)                                                                            \
+  hipLaunchKernelGGL(fm_sgd_update_kernel<GG>, grid, dim3(256), 0, s, (const long long*)indptr, \
+                     (const int*)idx, (const float*)val, nrows, (float*)w, (float*)V, k,        \
+                     (const float*)S, (const float*)c, lr, l2w, l2v, reg_skip, upd_w, bias_latent)
+  switch (G) {
+    case 4: YTK_FM_S(4); break;
+    case 8: YTK_FM_S(8); break;
+    case 16: YTK_FM_S(16); break;
+    case 32: YTK_FM_S(32); break;
+    default: YTK_FM_S(64); break;
+  }
+#undef YTK_FM_S
+  YTK_LAUNCH_CHECK();
+}
+
 }  // extern "C"
+

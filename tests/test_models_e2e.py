@@ -198,3 +198,44 @@ def test_ffm_gpu_matches_cpu_training(cuda, bin_data, tmp_path):
     rg = train("ffm", _cfg("ffm", str(tmp_path / "g"), str(bin_data / "ftrain.txt"), str(bin_data / "ftest.txt"),
                            **kw), comm=_local(cuda))
     np.testing.assert_allclose(rg.loss, rc.loss, rtol=5e-3)
+
+
+def _sgd_kw(**kw):
+    base = {"optimization.optimizer": "sgd", "optimization.sgd.learning_rate": 0.05,
+            "optimization.sgd.batch_size": 64, "optimization.sgd.epochs": 6, "optimization.sgd.seed": 3}
+    base.update(kw)
+    return base
+
+
+@pytest.mark.parametrize("model", ["linear", "fm", "ffm"])
+def test_sgd_optimizer_learns(bin_data, tmp_path, model):
+    """optimization.optimizer = sgd (extension): mini-batch Hogwild!-style SGD reaches a
+    test loss well below the constant predictor's log(2) and writes the usual model files."""
+    tr, te = ("ftrain.txt", "ftest.txt") if model == "ffm" else ("train.txt", "test.txt")
+    kw = _sgd_kw()
+    if model == "ffm":
+        kw.update({"model.field_dict_path": str(bin_data / "fields.dict"), "k": [1, 2]})
+    if model == "fm":
+        kw["k"] = [1, 4]
+    cfg = _cfg(model, str(tmp_path), str(bin_data / tr), str(bin_data / te), **kw)
+    train_loss, test_loss = train(model, cfg, comm=_local())
+    assert test_loss < 0.55 and train_loss < 0.55, (train_loss, test_loss)
+    assert os.path.exists(os.path.join(str(tmp_path), f"{model}.model", "model-00000"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["linear", "fm", "ffm"])
+def test_sgd_optimizer_gpu(cuda, bin_data, tmp_path, model):
+    """The HIP Hogwild!-style update learns like the CPU mini-batch step (races differ)."""
+    tr, te = ("ftrain.txt", "ftest.txt") if model == "ffm" else ("train.txt", "test.txt")
+    kw = _sgd_kw()
+    if model == "ffm":
+        kw.update({"model.field_dict_path": str(bin_data / "fields.dict"), "k": [1, 2]})
+    if model == "fm":
+        kw["k"] = [1, 4]
+    rc = train(model, _cfg(model, str(tmp_path / "c"), str(bin_data / tr), str(bin_data / te), **kw),
+               comm=_local("cpu"))
+    rg = train(model, _cfg(model, str(tmp_path / "g"), str(bin_data / tr), str(bin_data / te), **kw),
+               comm=_local(cuda))
+    assert rg[1] < 0.55
+    assert abs(rg[1] - rc[1]) < 0.05, (rg, rc)

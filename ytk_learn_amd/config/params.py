@@ -226,7 +226,10 @@ class LineSearchParams:
     def from_config(cls, c: Config, prefix: str = "optimization.") -> "LineSearchParams":
         k = prefix + "line_search."
         opt = c.get_string(prefix + "optimizer", "line_search")
-        check(opt == "line_search", "optimization.optimizer:%s, only support line_search", opt)
+        # "sgd" is this framework's extension (optim/sgd.py); ytk-learn only has line_search
+        check(opt in ("line_search", "sgd"), "optimization.optimizer:%s, only support line_search or sgd", opt)
+        if opt == "sgd" and not c.has(k.rstrip(".")):
+            return cls()
         b = k + "backtracking."
         p = cls(mode=_mode(c.get_string(k + "mode"), ("sufficient_decrease", "wolfe", "strong_wolfe"), k + "mode"),
                 step_decr=c.get_double(b + "step_decr"), step_incr=c.get_double(b + "step_incr"),
@@ -312,6 +315,8 @@ class CommonParams:
     loss: LossParams = field(default_factory=LossParams)
     line_search: LineSearchParams = field(default_factory=LineSearchParams)
     hyper: HyperParams = field(default_factory=HyperParams)
+    optimizer: str = "line_search"
+    sgd: Optional[object] = None  # optim.sgd.SGDParams when optimizer == "sgd"
     random: Optional[RandomParams] = None
     extra: Dict[str, object] = field(default_factory=dict)  # model-specific keys (k, tree_num, ...)
 
@@ -325,6 +330,10 @@ class CommonParams:
         p.model = ModelParams.from_config(c)
         p.loss = LossParams.from_config(c)
         p.line_search = LineSearchParams.from_config(c)
+        p.optimizer = str(c.get_string("optimization.optimizer", "line_search")).lower()
+        if p.optimizer == "sgd":
+            from ..optim.sgd import SGDParams
+            p.sgd = SGDParams.from_config(c)
         p.hyper = HyperParams.from_config(c)
         if c.has("random"):
             p.random = RandomParams.from_config(c)

@@ -14,13 +14,13 @@ from ._ext import check_cuda, hip, ptr, stream
 def fm_forward(X, w_lin: torch.Tensor, V: torch.Tensor):
     """(fx float64 [n], S float32 [n, k]) for the rows of SparseMatrix X; V: [F, k] view."""
     k = V.shape[1]
-    if X.device.type == "cuda" and 1 <= k <= 64:
+    if X.device.type == "cuda" and 0 <= k <= 64:
         check_cuda(w_lin, V)
         V = V.contiguous()
         fx = torch.empty(X.n, dtype=torch.float64, device=X.device)
         S = torch.empty((X.n, k), dtype=torch.float32, device=X.device)
-        hip().fm_forward(ptr(X.indptr), ptr(X.indices), ptr(X.values), X.n, ptr(w_lin), ptr(V), k, ptr(fx), ptr(S),
-                         stream(V))
+        hip().fm_forward(ptr(X.indptr), ptr(X.indices), ptr(X.values), X.n, ptr(w_lin),
+                         ptr(V) if k > 0 else 0, k, ptr(fx), ptr(S) if k > 0 else 0, stream(w_lin))
         return fx, S
     fx = X.matmul(w_lin).double()
     S = X.matmul(V.contiguous())
@@ -51,3 +51,40 @@ def fm_backward(X, c: torch.Tensor, S: torch.Tensor, V: torch.Tensor, g_lin: tor
     sq = X.t_matmul(c, square=True)
     gV.sub_(V * sq[:, None])
     return g_lin, gV
+
+
+def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float, l2v: float,
+                  reg_skip: int = -1, upd_w: bool = True, bias_latent: bool = False):
+    """One Hogwild!-style SGD step over the rows of ``indptr`` (absolute offsets into
+    ``indices`` / ``values``): w_i -= lr (c_r x_i + l2w w_i), V_if -= lr (c_r x_i (S_rf - V_if x_i)
+    + l2v V_if) for every entry of every row. ``V`` [F, k] / ``S`` [n, k] are None for the
+    linear model. ``reg_skip``: the bias index (no regularisation; latent row frozen unless
+    ``bias_latent``); ``upd_w = False`` updates only the bias among the linear weights.
+    GPU: lock-free float atomics, concurrent rows race as in Hogwild!. CPU: the same
+    per-sample gradients applied as one synchronous mini-batch step."""
+    n = int(indptr.shape[0] - 1)
+    k = 0 if V is None else int(V.shape[1])
+    c = c.float().contiguous()
+    if w_lin.is_cuda:
+        check_cuda(indptr, indices, values, w_lin, V, S, c)
+        hip().fm_sgd_update(ptr(indptr), ptr(indices), ptr(values), n, ptr(w_lin), ptr(V), k, ptr(S), ptr(c),
+                            float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0,
+                            1 if bias_latent else 0, stream(w_lin))
+        return
+    b0, e0 = int(indptr[0]), int(indptr[-1])
+    rows = torch.repeat_interleave(torch.arange(n), (indptr[1:] - indptr[:-1]).long())
+    idx = indices[b0:e0].long()
+    x = values[b0:e0]
+    cr = c[rows]
+    is_bias = idx == reg_skip
+    zero = torch.zeros((), dtype=torch.float32)
+    gw = cr * x + torch.where(is_bias, zero, l2w * w_lin[idx])
+    if not upd_w:
+        gw = torch.where(is_bias, gw, zero)
+    if k > 0:
+        v = V[idx]
+        gv = (cr * x)[:, None] * (S[rows] - v * x[:, None]) + torch.where(is_bias[:, None], zero, l2v * v)
+        if not bias_latent:
+            gv[is_bias] = 0.0
+        V.index_add_(0, idx, -lr * gv)
+    w_lin.index_add_(0, idx, -lr * gw)

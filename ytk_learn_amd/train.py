@@ -84,6 +84,16 @@ def train(model_name: str, conf: Union[str, Config], overrides: Optional[Dict[st
         model = build_continuous_model(model_name, params, comm, dev, log, transform_fn, threads)
         t_load = time.perf_counter() - t0
         log.info(f"LoadDataFlow cost:{t_load:.3f}s")
+        if params.optimizer == "sgd":  # extension: mini-batch Hogwild!-style SGD (optim/sgd.py)
+            from .optim.sgd import SGDOptimizer
+            opt = SGDOptimizer(model, params.sgd, params.loss.l1, params.loss.l2, comm, log,
+                               model.data.train.weight_sum,
+                               model.data.test.weight_sum if model.data.test is not None else 0.0,
+                               params.model.dump_freq)
+            res = opt.run(model.w)
+            log.info(f"Train cost details: LoadDataFlow:{t_load:.3f}s, PreprocessAndTrain:"
+                     f"{time.perf_counter() - t0 - t_load:.3f}s")
+            return res
         from .optim.lbfgs import HoagOptimizer
         opt = HoagOptimizer(model, params.line_search, params.loss.l1, params.loss.l2, comm, log,
                             model.data.train.weight_sum,
