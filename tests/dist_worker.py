@@ -60,7 +60,7 @@ def write_lines(path, n, seed):
             f.write("1###%d###%s\n" % (y, ",".join(f"x{i}:{x:.4f}" for i, x in zip(idx, v))))
 
 
-def run_linear(comm, out, device, model_name):
+def run_linear(comm, out, device, model_name, sgd=False):
     from ytk_learn_amd.config.hocon import parse_file
     from ytk_learn_amd.train import train
     tr_path, te_path = os.path.join(out, "train.txt"), os.path.join(out, "test.txt")
@@ -73,10 +73,17 @@ def run_linear(comm, out, device, model_name):
         "model.data_path": os.path.join(out, f"{model_name}_w{comm.world}.model"),
         "optimization.line_search.lbfgs.convergence.max_iter": 10, "k": 4 if model_name != "fm" else [1, 4],
         "tree_num": 2})
+    if sgd:
+        cfg = cfg.with_overrides({"optimization.optimizer": "sgd", "optimization.sgd.learning_rate": 0.05,
+                                  "optimization.sgd.batch_size": 128, "optimization.sgd.epochs": 4,
+                                  "optimization.sgd.sync_every": 5})
     res = train(model_name, cfg, comm=comm)
     if comm.rank == 0:
         with open(os.path.join(out, "res.json"), "w") as f:
-            json.dump({"loss": res.loss, "test_loss": res.test_loss}, f)
+            if sgd:
+                json.dump({"loss": res[0], "test_loss": res[1]}, f)
+            else:
+                json.dump({"loss": res.loss, "test_loss": res.test_loss}, f)
 
 
 def run_comm(comm, out, device):
@@ -105,6 +112,8 @@ def main():
             run_gbdt(comm, out, dev, "loss")
         elif task in ("linear", "fm", "gbmlr", "gbhsdt"):
             run_linear(comm, out, dev, task)
+        elif task in ("fm_sgd", "linear_sgd"):
+            run_linear(comm, out, dev, task.split("_")[0], sgd=True)
         elif task == "comm":
             run_comm(comm, out, dev)
         else:

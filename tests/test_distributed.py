@@ -86,3 +86,13 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world):
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
+
+
+@pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
+def test_sgd_world2_model_averaging(tmp_path, task):
+    """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every
+    averaging point) learns like the single-rank run."""
+    r1 = _run(task, tmp_path / "w1", 1)
+    r2 = _run(task, tmp_path / "w2", 2)
+    assert r2["test_loss"] < 0.6 and r1["test_loss"] < 0.6
+    assert abs(r2["test_loss"] - r1["test_loss"]) < 0.1
