@@ -132,7 +132,7 @@ def main():
             "dtype": "fp32",
             "data": "synthetic Higgs-shape (10.5M train + 0.5M test x 28 dense float features, random-init trees)",
             "config": {
-                "model": f"gbdt {a.policy}-wise depth{a.depth} leaves{tp.max_leaf_cnt} bins{a.bins} sigmoid lr0.1",
+                "model": f"gbdt {a.policy}-wise depth{a.depth if a.policy == 'level' else '-unlimited'} leaves{tp.max_leaf_cnt} bins{a.bins} sigmoid lr0.1",
                 "global_batch": a.train_rows,
                 "seq_len": 28,
                 "parallelism": f"dp{world}",

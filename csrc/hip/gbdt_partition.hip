@@ -315,20 +315,40 @@ extern "C" void ytk_partition(uintptr_t binsT, int bin_bytes, long long ncol, ui
 // Copy-back of partitioned segments (loss-guided batches partition a few node segments
 // in place): rows[p] = rows_out[p], ghp[p] = gh_out[p] for p in every chunk [b, e) of
 // items (the partition's own chunk list) -- one launch instead of two copies per node.
+// Copy the partitioned segments back (leaf-wise growth partitions only the batch's
+// segments). An item's range is split over gridDim.y blocks and every thread keeps 4
+// independent loads in flight: the item ranges are large (a batch's rows / ~256) and
+// one 256-thread block per item left the copy latency bound at ~1/4 of HBM bandwidth.
+constexpr int kCopySplit = 16;
+constexpr int kCopyUnroll = 4;
+
 __global__ __launch_bounds__(kPartThreads) void segment_copy_kernel(
     const int4* __restrict__ items, const int* __restrict__ src_rows, int* __restrict__ dst_rows,
     const float2* __restrict__ src_gh, float2* __restrict__ dst_gh) {
   const int4 it = items[blockIdx.x];
-  for (int p = it.y + threadIdx.x; p < it.z; p += kPartThreads) {
-    dst_rows[p] = src_rows[p];
-    dst_gh[p] = src_gh[p];
+  const int len = it.z - it.y;
+  const int per = (len + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int b = it.y + (int)blockIdx.y * per, e = min(it.z, b + per);
+  for (int p0 = b; p0 < e; p0 += kPartThreads * kCopyUnroll) {
+    int r[kCopyUnroll];
+    float2 g[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const int p = p0 + u * kPartThreads + (int)threadIdx.x;
+      if (p < e) { r[u] = src_rows[p]; g[u] = src_gh[p]; }
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const int p = p0 + u * kPartThreads + (int)threadIdx.x;
+      if (p < e) { dst_rows[p] = r[u]; dst_gh[p] = g[u]; }
+    }
   }
 }
 
 extern "C" void ytk_segment_copy(uintptr_t items, int nitems, uintptr_t src_rows, uintptr_t dst_rows,
                                  uintptr_t src_gh, uintptr_t dst_gh, uintptr_t stream) {
   if (nitems <= 0) return;
-  hipLaunchKernelGGL(segment_copy_kernel, dim3(nitems), dim3(kPartThreads), 0,
+  hipLaunchKernelGGL(segment_copy_kernel, dim3(nitems, kCopySplit), dim3(kPartThreads), 0,
                      reinterpret_cast<hipStream_t>(stream), (const int4*)items,
                      (const int*)src_rows, (int*)dst_rows, (const float2*)src_gh, (float2*)dst_gh);
   YTK_LAUNCH_CHECK();
