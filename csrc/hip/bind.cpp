@@ -26,6 +26,8 @@ void ytk_partition_atomic(uintptr_t, int, long long, uintptr_t, uintptr_t, uintp
                           uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                           int, uintptr_t);
 void ytk_segment_copy(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_zero_slots(uintptr_t, long long, uintptr_t, int, uintptr_t);
+void ytk_memset_async(uintptr_t, int, long long, uintptr_t);
 void ytk_partition(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
@@ -81,6 +83,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
   m.def("segment_copy", &ytk_segment_copy);
+  m.def("zero_slots", &ytk_zero_slots);
+  m.def("memset_async", &ytk_memset_async);
   m.def("partition_atomic", &ytk_partition_atomic);
   m.def("tree_add_bins", &ytk_tree_add_bins);
   m.def("forest_predict", &ytk_forest_predict);

@@ -17,6 +17,8 @@
 // permutation (root level without instance sampling: no iota copy).
 #include "common.h"
 
+#include <algorithm>
+
 namespace ytk {
 
 constexpr int kPartThreads = 256;
@@ -352,6 +354,31 @@ extern "C" void ytk_segment_copy(uintptr_t items, int nitems, uintptr_t src_rows
                      reinterpret_cast<hipStream_t>(stream), (const int4*)items,
                      (const int*)src_rows, (int*)dst_rows, (const float2*)src_gh, (float2*)dst_gh);
   YTK_LAUNCH_CHECK();
+}
+
+// hist[ids[i]] = 0 for the nslots listed slots (16-byte stores; one launch instead of an
+// id conversion + index_fill from the host).
+__global__ __launch_bounds__(256) void zero_slots_kernel(longlong2* __restrict__ hist, long long slot_v2,
+                                                         const int* __restrict__ ids) {
+  longlong2* h = hist + (size_t)ids[blockIdx.y] * slot_v2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < slot_v2; i += (long long)gridDim.x * 256)
+    h[i] = make_longlong2(0, 0);
+}
+
+extern "C" void ytk_zero_slots(uintptr_t hist, long long slot_bytes, uintptr_t ids, int nslots,
+                               uintptr_t stream) {
+  if (nslots <= 0) return;
+  const long long v2 = slot_bytes / 16;
+  const int gx = (int)std::min<long long>(64, (v2 + 255) / 256);
+  hipLaunchKernelGGL(zero_slots_kernel, dim3(gx, nslots), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (longlong2*)hist, v2, (const int*)ids);
+  YTK_LAUNCH_CHECK();
+}
+
+extern "C" void ytk_memset_async(uintptr_t dst, int value, long long bytes, uintptr_t stream) {
+  if (bytes <= 0) return;
+  if (hipMemsetAsync((void*)dst, value, (size_t)bytes, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+    throw std::runtime_error("hipMemsetAsync failed");
 }
 
 // cursor: per split, zeroed by the caller; on return low 32 bits = left rows, high 32 =

@@ -12,8 +12,10 @@ MI355X-first structure (not a translation):
     (level-wise); loss-guided growth uses the same kernels with batch size 1;
   * the partition moves (g,h) along with the row ids, so histogram builds read
     (g,h) contiguously and only gather the 32-B bin rows;
-  * histograms are indexed by a per-tree slot counter (no LRU pool: even 509
-    slots x 28 features x 256 bins is 29 MB of the 288 GB HBM);
+  * level-wise histograms are indexed by a per-tree slot counter (even 509 slots x
+    28 features x 256 bins is 29 MB of the 288 GB HBM); loss-guided growth recycles
+    slots from a free list, bounded like the reference's LRU pool when
+    ``histogram_pool_capacity`` is set;
   * per-call metadata (work lists, split items) is built with vectorised numpy and
     shipped in ONE pinned host->device copy per launch group;
   * multi-GPU: rows are sharded; the level's freshly built histograms are one
@@ -34,6 +36,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
+from ...ops._ext import hip, stream
 from ...parallel.comm import Comm
 from .tree import Tree
 
@@ -214,6 +217,7 @@ class TreeBuilder:
         self.last_keep = None
         self._root_gh = None
         self._staging = None
+        self._cursor = None
         self.free_slots = None
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0"
         self.fmask_np = np.ones(F, np.uint8)
@@ -268,6 +272,8 @@ class TreeBuilder:
         if nb:
             if s0 >= 0:
                 self.hist[s0:s0 + nb].zero_()
+            elif self.dev.type == "cuda":  # one launch, no id conversion
+                hip().zero_slots(self.hist.data_ptr(), self.slot_bytes, ids_d.data_ptr(), nb, stream(self.hist))
             else:
                 self.hist.index_fill_(0, ids_d.long(), 0)
             src_gh = self._root_gh if (identity_rows and self._root_gh is not None) else self.ghp
@@ -346,8 +352,11 @@ class TreeBuilder:
             hdr = np.array([n, int(nb_a.sum())], np.int32)
             items_d, feat_d, thr_d, nbeg_d, cnt_d, first_d, hdr_d = self.up.put(
                 items, feat, thr, begins, counts, first_a, hdr)
+            if self._cursor is None or self._cursor.numel() < n:
+                self._cursor = torch.empty(max(n, 1024), dtype=torch.int64, device=self.dev)
+            # raw split cursors (right << 32 | left): masked on the host after the copy
             left = gops.partition_atomic(self.binsT, rows_in, self.rows_tmp, gh_in, self.gh_tmp, first_d,
-                                         hdr_d, int(hdr[1]), feat_d, thr_d, nbeg_d, cnt_d)
+                                         hdr_d, int(hdr[1]), feat_d, thr_d, nbeg_d, cnt_d, cursor=self._cursor)
         else:
             items_d, feat_d, thr_d, nbeg_d, first_d, nblk_d = self.up.put(
                 items, feat, thr, begins, first, nblk)
@@ -362,14 +371,15 @@ class TreeBuilder:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
         if self.comm.is_dist:
-            both = torch.stack([left, left]).to(torch.int64)
+            both = torch.stack([left, left]).to(torch.int64) & 0xFFFFFFFF
             self.comm.allreduce_(both[1])
             both = both.cpu().numpy()
             lloc, lglob = both[0], both[1]
         else:
-            lloc = left.to(torch.int64).cpu().numpy()
+            lloc = left.to(torch.int64).cpu().numpy() & 0xFFFFFFFF
             lglob = lloc
         self.up.reset()
+        lloc, lglob = lloc.tolist(), lglob.tolist()
         for i, (nid, lc, rc) in enumerate(splits):
             nd = nodes[nid]
             nodes[lc] = _Node(begin=nd.begin, cnt_local=int(lloc[i]), cnt_global=int(lglob[i]),
@@ -698,12 +708,17 @@ class TreeBuilder:
         else:  # loss-guided (leaf-wise), exact, expanded in speculative batches
             tid = self._grow_loss_guided(tree, nodes, fmask, f0, pop_is_leaf, make_leaf,
                                          children_terminal, leafify_children)
+            ts, lcs, hs = [], [], []
             for sid, t in tid.items():
                 nd = nodes[sid]
-                tree.loss_chg[t] = (float(np.float32(nd.rec["loss_chg"])) if nd.rec is not None and nd.rec_used
-                                    else float("-inf"))
-                tree.hess_sum[t] = float(np.float32(nd.H))
+                ts.append(t)
+                lcs.append(nd.rec["loss_chg"] if nd.rec is not None and nd.rec_used else float("-inf"))
+                hs.append(nd.H)
                 tree.sample_cnt[t] = nd.cnt_global
+            # float32 rounding of the dumped statistics, vectorised
+            for t, lc, h in zip(ts, np.asarray(lcs, np.float32).tolist(), np.asarray(hs, np.float32).tolist()):
+                tree.loss_chg[t] = lc
+                tree.hess_sum[t] = h
             nodes = {}
 
         # node stats for the dump (updateTreeNodeStat)

@@ -70,7 +70,8 @@ class Tree:
         self.feat[nid] = int(feat)
         self.slot_a[nid] = int(a)
         self.slot_b[nid] = int(b)
-        self.cond[nid] = float(np.float32(0.5) * (np.float32(a) + np.float32(b)))
+        # == float32 0.5 * (a + b): bin ids are < 2^24, so the double result is exact
+        self.cond[nid] = 0.5 * (int(a) + int(b))
         self.is_leaf[nid] = False
 
     def set_leaf(self, nid: int, value: float):

@@ -71,8 +71,15 @@ def native():
     return _NATIVE
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream(t: torch.Tensor) -> int:
-    """Raw hipStream_t of the current torch stream for ``t``'s device."""
+    """Raw hipStream_t of the current torch stream for ``t``'s device (the raw query
+    skips building a Stream object: ~1 us instead of ~7 us per launch from Python)."""
+    if _raw_stream is not None:
+        idx = t.device.index
+        return _raw_stream(torch.cuda.current_device() if idx is None else idx)
     return torch.cuda.current_stream(t.device).cuda_stream
 
 

@@ -10,6 +10,8 @@ Reference semantics are cited in the kernel file header.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -117,6 +119,13 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
 # ---------------------------------------------------------------------------
 # split finding
 # ---------------------------------------------------------------------------
+def split_node_fits(B: int, F: int) -> bool:
+    """Whether split_find runs the node-resident LDS kernel (same test as ytk_split_find
+    in csrc/hip/gbdt_split.hip): then it needs no per-feature scratch."""
+    return (B <= 256 and F * (B + 1) * 16 <= 144 * 1024 and B * F <= 8 * 1024 and F <= 256
+            and os.environ.get("YTK_SPLIT_NODE") != "0")
+
+
 def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
     """Best split per item. items int32 [n, 4] = (slot, parent, sibling, derived).
 
@@ -132,8 +141,10 @@ def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
         if n == 0:
             return out
         check_cuda(hist, nbins_f, fmask, items)
-        part = torch.empty((n * F, 48), dtype=torch.uint8, device=hist.device)
-        counters = torch.zeros(n, dtype=torch.int32, device=hist.device)
+        part = counters = None
+        if not split_node_fits(B, F):  # the (node, feature) kernel combines through scratch
+            part = torch.empty((n * F, 48), dtype=torch.uint8, device=hist.device)
+            counters = torch.zeros(n, dtype=torch.int32, device=hist.device)
         hip().split_find(ptr(hist), B, F, ptr(nbins_f), ptr(fmask), int(f0), ptr(items), n,
                          ptr(out), mcw, l1, l2, mal, inv_sg, inv_sh, 0, 0, ptr(part), ptr(counters),
                          stream(hist))
@@ -280,13 +291,22 @@ PART_CHUNK = 2048  # rows per block of the single-pass partition kernel
 
 
 def partition_atomic(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, nblocks, feat, thr,
-                     node_begin, node_count):
+                     node_begin, node_count, cursor=None):
     """Single-pass partition (GPU): each 2048-row chunk reserves its left run at the front
     and its right run at the back of its node segment with one atomic; chunks land in
     any order (rows inside a chunk keep theirs). hdr int32 [2] = (n_split, n_blocks) on the
-    device; first_blk = exclusive scan of ceil(count / 2048). Returns left counts (int64)."""
+    device; first_blk = exclusive scan of ceil(count / 2048). Returns left counts (int64).
+    ``cursor`` (optional int64 device buffer >= n_split): zeroed here with one async
+    memset and returned RAW -- (right rows << 32) | left rows; mask on the host."""
     n = feat.shape[0]
-    cursor = torch.zeros(max(n, 1), dtype=torch.int64, device=binsT.device)[:n]
+    if cursor is None:
+        cursor = torch.zeros(max(n, 1), dtype=torch.int64, device=binsT.device)[:n]
+        raw = False
+    else:
+        cursor = cursor[:n]
+        raw = True
+        if n:
+            hip().memset_async(ptr(cursor), 0, n * 8, stream(binsT))
     if nblocks == 0 or n == 0:
         return cursor
     check_cuda(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, feat, thr, node_begin, node_count)
@@ -294,7 +314,7 @@ def partition_atomic(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, nblocks
                            ptr(ghp), ptr(gh_out), ptr(first_blk), ptr(hdr), ptr(hdr) + 4, nblocks,
                            ptr(feat), ptr(thr), ptr(node_begin), ptr(node_count), ptr(cursor), 0,
                            stream(binsT))
-    return cursor & 0xFFFFFFFF
+    return cursor if raw else cursor & 0xFFFFFFFF
 
 
 def segment_copy(items, src_rows, dst_rows, src_gh, dst_gh):
