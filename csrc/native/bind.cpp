@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "native.h"
+#include "leafwise.h"
 #include "parser.h"
 
 namespace py = pybind11;
@@ -210,4 +211,87 @@ PYBIND11_MODULE(_ytk_native, m) {
         return result_to_dict(std::move(r));
       },
       py::arg("paths"), py::arg("opts"));
+
+  // ---- exact leaf-wise growth planner (leafwise.h)
+  using i32arr = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+  using i64arr = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+  py::class_<LwParams>(m, "LwParams")
+      .def(py::init<>())
+      .def_readwrite("max_leaf", &LwParams::max_leaf)
+      .def_readwrite("max_depth", &LwParams::max_depth)
+      .def_readwrite("min_split_samples", &LwParams::min_split_samples)
+      .def_readwrite("min_split_loss", &LwParams::min_split_loss)
+      .def_readwrite("mcw", &LwParams::mcw)
+      .def_readwrite("l1", &LwParams::l1)
+      .def_readwrite("l2", &LwParams::l2)
+      .def_readwrite("max_abs_leaf", &LwParams::max_abs_leaf)
+      .def_readwrite("mcw2", &LwParams::mcw2)
+      .def_readwrite("lr", &LwParams::lr)
+      .def_readwrite("speculate", &LwParams::speculate);
+  py::class_<LeafGrower>(m, "LeafGrower")
+      .def(py::init<const LwParams&, int>())
+      .def("root", &LeafGrower::root)
+      .def("apply_recs",
+           [](LeafGrower& g, const i32arr& ids, const py::array& recs) {
+             if ((size_t)recs.nbytes() != (size_t)ids.size() * sizeof(LwRec))
+               throw std::invalid_argument("apply_recs: recs must hold 48 bytes per id");
+             g.apply_recs(ids.data(), reinterpret_cast<const LwRec*>(recs.data()), (int)ids.size());
+           })
+      .def("replay", &LeafGrower::replay)
+      .def("expand",
+           [](LeafGrower& g, const std::vector<int32_t>& batch) {
+             auto ex = g.expand(batch);
+             return py::make_tuple(ex.split_sid, ex.count_sid);
+           })
+      .def("segments",  // parents -> (begin, count, feat, thr) int64 arrays
+           [](const LeafGrower& g, const std::vector<int32_t>& sids) {
+             const py::ssize_t n = (py::ssize_t)sids.size();
+             i64arr out({(py::ssize_t)4, n});
+             auto w = out.mutable_unchecked<2>();
+             for (py::ssize_t i = 0; i < n; ++i) {
+               w(0, i) = g.begin(sids[i]);
+               w(1, i) = g.cnt_local(sids[i]);
+               w(2, i) = g.feat(sids[i]);
+               w(3, i) = g.thr(sids[i]);
+             }
+             return out;
+           })
+      .def("set_children",
+           [](LeafGrower& g, const std::vector<int32_t>& parents, const i64arr& lloc, const i64arr& lglob,
+              bool with_begin) {
+             if ((size_t)lloc.size() != parents.size() || (size_t)lglob.size() != parents.size())
+               throw std::invalid_argument("set_children: size mismatch");
+             g.set_children(parents, lloc.data(), lglob.data(), with_begin);
+           })
+      .def("plan_hist",
+           [](LeafGrower& g, const std::vector<int32_t>& parents) {
+             auto hp = g.plan_hist(parents);
+             const py::ssize_t n = (py::ssize_t)hp.order.size();
+             i32arr items({n, (py::ssize_t)4});
+             std::copy(hp.items.begin(), hp.items.end(), items.mutable_data());
+             return py::make_tuple(hp.order, hp.slots, hp.nbuild, i64arr((py::ssize_t)hp.begin.size(), hp.begin.data()),
+                                   i64arr((py::ssize_t)hp.count.size(), hp.count.data()), items);
+           })
+      .def("release_batch", &LeafGrower::release_batch)
+      .def("finish",
+           [](LeafGrower& g) {
+             auto t = g.finish();
+             py::dict d;
+             d["left"] = t.left;
+             d["right"] = t.right;
+             d["parent"] = t.parent;
+             d["feat"] = t.feat;
+             d["slot_a"] = t.slot_a;
+             d["slot_b"] = t.slot_b;
+             d["cond"] = t.cond;
+             d["leaf"] = std::vector<double>(t.leaf.begin(), t.leaf.end());
+             d["is_leaf"] = std::vector<bool>(t.is_leaf.begin(), t.is_leaf.end());
+             d["loss_chg"] = std::vector<double>(t.loss_chg.begin(), t.loss_chg.end());
+             d["hess_sum"] = std::vector<double>(t.hess_sum.begin(), t.hess_sum.end());
+             d["sample_cnt"] = t.sample_cnt;
+             return d;
+           })
+      .def_readonly("batches", &LeafGrower::batches)
+      .def_readonly("expanded", &LeafGrower::expanded)
+      .def_readonly("hist_miss", &LeafGrower::hist_miss);
 }

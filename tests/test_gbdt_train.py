@@ -153,6 +153,35 @@ def test_loss_guided_speculation_is_exact(monkeypatch, kw):
     assert dumps[0][0].count("leaf=") > 3
 
 
+@pytest.mark.parametrize("kw", [{}, {"max_depth": 4, "max_leaf_cnt": 20}, {"min_split_samples": 900},
+                                {"min_split_loss": 2.0}, {"l1": 0.5, "max_abs_leaf_val": 0.3},
+                                {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6}, {"pool": 5},
+                                {"spec": "0"}])
+def test_native_leafwise_planner_matches_python(monkeypatch, kw):
+    """The native leaf-wise planner (csrc/native/leafwise.cpp) == the Python reference
+    planner (TreeBuilder._grow_loss_guided): model dump, losses, batches, pool misses."""
+    kw = dict(kw)
+    pool = kw.pop("pool", None)
+    monkeypatch.setenv("YTK_LOSSGUIDE_SPEC", kw.pop("spec", "1"))
+    res = []
+    for native in ("0", "1"):
+        monkeypatch.setenv("YTK_LEAF_NATIVE", native)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 40
+        for k, v in kw.items():
+            setattr(p.tree, k, v)
+        if pool is not None:
+            p.histogram_pool_capacity = pool * 256 * 28 * 16 / float(1 << 20)  # ~pool live slots
+        tr = GBDTTrainer(p, _data(12000, 11), _data(3000, 12))
+        tr.train()
+        assert tr.builder.native_leafwise == (native == "1")
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss, tr.builder.last_batches,
+                    tr.builder.last_expanded, tr.builder.hist_miss))
+    assert res[0] == res[1]
+    if pool is not None:
+        assert res[0][5] > 0
+
+
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():
     """histogram_pool_capacity (MB) bounds the live histograms of leaf-wise growth; evicted
     parents are rebuilt (pool miss) instead of derived -- exact int64 sums => same model."""

@@ -200,6 +200,8 @@ class TreeBuilder:
         # YTK_LOSSGUIDE_SPEC=0: expand one leaf per step (the plain sequential schedule;
         # used by the tests to check that speculation does not change the tree)
         self.speculate = os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0"
+        # YTK_LEAF_NATIVE=0: the Python planner (_grow_loss_guided) instead of the native one
+        self.native_leafwise = os.environ.get("YTK_LEAF_NATIVE", "1") != "0"
         # exact int64 fixed-point histograms (see csrc/hip/gbdt_hist.hip)
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=self.dev)
         self.gp_tree = dict(self.gp, sg=1.0, sh=1.0)
@@ -235,8 +237,6 @@ class TreeBuilder:
                         fmask: torch.Tensor, f0: int, identity_rows: bool = False):
         """Histogram the ``build`` nodes, derive ``derived`` = (node, parent, sibling),
         then find the best split of every one of them."""
-        st = self.last_stats
-        t0 = time.perf_counter()
         nb = len(build)
         if self.free_slots is not None:  # recycled pool (loss-guided): any free slots
             need = nb + len(derived)
@@ -259,16 +259,41 @@ class TreeBuilder:
         items[:nb, 0] = ids[:nb]
         for j, (n, p, s) in enumerate(derived):
             items[nb + j] = (nodes[n].slot, nodes[p].slot, nodes[s].slot, 1)
+        begins = np.array([nodes[n].begin for n in build], np.int64)
+        counts = np.array([nodes[n].cnt_local for n in build], np.int64)
+        recs = self._hist_split(begins, counts, np.asarray(ids, np.int32), nb, items, fmask, f0,
+                                identity_rows=identity_rows, s0=s0)
+        mcw2 = self.p.min_child_hessian_sum * 2.0
+        names = gops.SPLIT_DTYPE.names
+        order = list(build) + [n for n, _, _ in derived]
+        # plain dicts of Python scalars: the host bookkeeping then avoids numpy scalar ops
+        for nid, tup in zip(order, recs.tolist()):
+            r = dict(zip(names, tup))  # loss_chg: the exact double of the float32 gain
+            nd = nodes[nid]
+            nd.rec = r
+            nd.G = r["g"]
+            nd.H = r["h"]
+            # canSplit (UpdateStrategy.canSplit): H >= 2*mcw and n >= min_split_samples
+            if not (nd.H >= mcw2 and nd.cnt_global >= self.p.min_split_samples):
+                r["loss_chg"] = -np.inf
+                r["feat"] = -1
+
+    def _hist_split(self, begins: np.ndarray, counts: np.ndarray, ids: np.ndarray, nb: int, items: np.ndarray,
+                    fmask: torch.Tensor, f0: int, identity_rows: bool = False, s0: int = -1) -> np.ndarray:
+        """Device part of a histogram + split step: build the nb nodes' histograms
+        (segments begins/counts -> slots ids[:nb]; s0 >= 0: the contiguous range s0..),
+        all-reduce them, run the split search over ``items`` [n, 4]; returns the split
+        records (host structured array, SPLIT_DTYPE)."""
+        st = self.last_stats
+        t0 = time.perf_counter()
         work = np.zeros((0, 4), np.int32)
         if nb:
-            begins = np.array([nodes[n].begin for n in build], np.int64)
-            counts = np.array([nodes[n].cnt_local for n in build], np.int64)
             seg, s, e, _, _, _ = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
             work = np.zeros((len(seg), 4), np.int32)
-            work[:, 0] = np.asarray(ids[:nb], np.int32)[seg]
+            work[:, 0] = ids[:nb][seg]
             work[:, 1] = s
             work[:, 2] = e
-        work_d, items_d, ids_d = self.up.put(work, items, np.asarray(ids[:nb], np.int32))
+        work_d, items_d, ids_d = self.up.put(work, items, ids[:nb])
         if nb:
             if s0 >= 0:
                 self.hist[s0:s0 + nb].zero_()
@@ -299,27 +324,14 @@ class TreeBuilder:
                 self.hist.index_copy_(0, idx, buf)
             self._sync()
         t2 = time.perf_counter()
-        order = list(build) + [n for n, _, _ in derived]
         out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp_tree)
         recs = out.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
         self.up.reset()  # the .cpu() above synchronised the stream
         t3 = time.perf_counter()
-        mcw2 = self.p.min_child_hessian_sum * 2.0
-        names = gops.SPLIT_DTYPE.names
-        # plain dicts of Python scalars: the host bookkeeping then avoids numpy scalar ops
-        for nid, tup in zip(order, recs.tolist()):
-            r = dict(zip(names, tup))  # loss_chg: the exact double of the float32 gain
-            nd = nodes[nid]
-            nd.rec = r
-            nd.G = r["g"]
-            nd.H = r["h"]
-            # canSplit (UpdateStrategy.canSplit): H >= 2*mcw and n >= min_split_samples
-            if not (nd.H >= mcw2 and nd.cnt_global >= self.p.min_split_samples):
-                r["loss_chg"] = -np.inf
-                r["feat"] = -1
         st.build_hist += t1 - t0
         st.comm_hist += t2 - t1
         st.find_split += t3 - t2
+        return recs
 
     def _evict(self, nodes: Dict[int, _Node], keep):
         """Drop the least recently built histogram not needed by the current call."""
@@ -332,17 +344,32 @@ class TreeBuilder:
             return
         raise RuntimeError("histogram_pool_capacity too small for one expansion")
 
-    def _partition(self, nodes: Dict[int, _Node], splits: List[tuple], copy_back: bool):
-        """splits: list of (nid, left_child, right_child). Updates child segments/counts."""
-        t0 = time.perf_counter()
-        n = len(splits)
+    def _split_arrays(self, nodes: Dict[int, _Node], splits: List[tuple]):
         begins = np.array([nodes[s[0]].begin for s in splits], np.int64)
         counts = np.array([nodes[s[0]].cnt_local for s in splits], np.int64)
-        seg, s, e, k, first, nblk = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
-        items = np.stack([seg, s, e, k], axis=1).astype(np.int32).reshape(-1, 4)
         feat = np.array([int(nodes[x[0]].rec["feat"]) for x in splits], np.int32)
         thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
                        np.int32)
+        return begins, counts, feat, thr
+
+    def _partition(self, nodes: Dict[int, _Node], splits: List[tuple], copy_back: bool):
+        """splits: list of (nid, left_child, right_child). Updates child segments/counts."""
+        lloc, lglob = self._partition_arrays(*self._split_arrays(nodes, splits), copy_back)
+        lloc, lglob = lloc.tolist(), lglob.tolist()
+        for i, (nid, lc, rc) in enumerate(splits):
+            nd = nodes[nid]
+            nodes[lc] = _Node(begin=nd.begin, cnt_local=lloc[i], cnt_global=lglob[i], depth=nd.depth + 1)
+            nodes[rc] = _Node(begin=nd.begin + lloc[i], cnt_local=nd.cnt_local - lloc[i],
+                              cnt_global=nd.cnt_global - lglob[i], depth=nd.depth + 1)
+
+    def _partition_arrays(self, begins: np.ndarray, counts: np.ndarray, feat: np.ndarray, thr: np.ndarray,
+                          copy_back: bool):
+        """Partition the segments (begins, counts) by bin(feat) <= thr; returns the left
+        row counts (local, global) as int64 arrays."""
+        t0 = time.perf_counter()
+        n = len(begins)
+        seg, s, e, k, first, nblk = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
+        items = np.stack([seg, s, e, k], axis=1).astype(np.int32).reshape(-1, 4)
         root = self._root_gh is not None  # first partition of an unsampled tree: identity rows
         rows_in, gh_in = (None, self._root_gh) if root else (self.rows, self.ghp)
         if self.dev.type == "cuda" and self.part_atomic:
@@ -379,30 +406,29 @@ class TreeBuilder:
             lloc = left.to(torch.int64).cpu().numpy() & 0xFFFFFFFF
             lglob = lloc
         self.up.reset()
-        lloc, lglob = lloc.tolist(), lglob.tolist()
-        for i, (nid, lc, rc) in enumerate(splits):
-            nd = nodes[nid]
-            nodes[lc] = _Node(begin=nd.begin, cnt_local=int(lloc[i]), cnt_global=int(lglob[i]),
-                              depth=nd.depth + 1)
-            nodes[rc] = _Node(begin=nd.begin + int(lloc[i]), cnt_local=nd.cnt_local - int(lloc[i]),
-                              cnt_global=nd.cnt_global - int(lglob[i]), depth=nd.depth + 1)
         self.last_stats.partition += time.perf_counter() - t0
+        return lloc, lglob
 
     def _count_children(self, nodes: Dict[int, _Node], splits: List[tuple]):
         """Children that become leaves right away: only their sample counts are needed
         (node statistics in the dump), so run the flag/count pass without the scatter."""
+        lloc, lglob = self._count_arrays(*self._split_arrays(nodes, splits))
+        lloc, lglob = lloc.tolist(), lglob.tolist()
+        for i, (nid, lc, rc) in enumerate(splits):
+            nd = nodes[nid]
+            nodes[lc] = _Node(cnt_local=lloc[i], cnt_global=lglob[i], depth=nd.depth + 1)
+            nodes[rc] = _Node(cnt_local=nd.cnt_local - lloc[i],
+                              cnt_global=nd.cnt_global - lglob[i], depth=nd.depth + 1)
+
+    def _count_arrays(self, begins: np.ndarray, counts: np.ndarray, feat: np.ndarray, thr: np.ndarray):
+        """Left row counts (local, global) of the segments without moving rows."""
         t0 = time.perf_counter()
-        begins = np.array([nodes[s[0]].begin for s in splits], np.int64)
-        counts = np.array([nodes[s[0]].cnt_local for s in splits], np.int64)
         seg, s, e, k, first, nblk = _chunk_segments(begins, counts, self._chunk(int(counts.sum())))
         items = np.stack([seg, s, e, k], axis=1).astype(np.int32).reshape(-1, 4)
-        feat = np.array([int(nodes[x[0]].rec["feat"]) for x in splits], np.int32)
-        thr = np.array([(int(nodes[x[0]].rec["bin_a"]) + int(nodes[x[0]].rec["bin_b"])) // 2 for x in splits],
-                       np.int32)
         items_d, feat_d, thr_d = self.up.put(items, feat, thr)
         bc = gops.partition_count(self.binsT, None if self._root_gh is not None else self.rows, self.flags,
                                   items_d, feat_d, thr_d)
-        left = torch.zeros(len(splits), dtype=torch.int64, device=self.dev)
+        left = torch.zeros(len(begins), dtype=torch.int64, device=self.dev)
         if len(seg):
             left.index_add_(0, torch.from_numpy(seg).to(self.dev), bc.to(torch.int64))
         if self.comm.is_dist:
@@ -414,14 +440,65 @@ class TreeBuilder:
             lloc = left.cpu().numpy()
             lglob = lloc
         self.up.reset()
-        for i, (nid, lc, rc) in enumerate(splits):
-            nd = nodes[nid]
-            nodes[lc] = _Node(cnt_local=int(lloc[i]), cnt_global=int(lglob[i]), depth=nd.depth + 1)
-            nodes[rc] = _Node(cnt_local=nd.cnt_local - int(lloc[i]),
-                              cnt_global=nd.cnt_global - int(lglob[i]), depth=nd.depth + 1)
         self.last_stats.partition += time.perf_counter() - t0
+        return lloc, lglob
 
     # ------------------------------------------------------- loss-guided growth
+    def _grow_native(self, tree: Tree, fmask, f0: int, identity: bool, n_local: int, n_global: int):
+        """Loss-guided growth with the native planner (csrc/native/leafwise.cpp): the same
+        schedule, trees and statistics as ``_grow_loss_guided`` -- replay, speculative batch
+        choice, child bookkeeping, slot recycling/LRU eviction and the tree itself live in
+        C++; this loop only runs the device steps of each batch."""
+        from ...ops._ext import native
+
+        nat = native()
+        p = self.p
+        lp = nat.LwParams()
+        lp.max_leaf = int(p.max_leaf_cnt)
+        lp.max_depth = int(p.max_depth)
+        lp.min_split_samples = int(p.min_split_samples)
+        lp.min_split_loss = float(np.float32(p.min_split_loss))
+        lp.mcw, lp.l1, lp.l2, lp.max_abs_leaf = (self.gp[k] for k in ("mcw", "l1", "l2", "max_abs_leaf"))
+        lp.mcw2 = p.min_child_hessian_sum * 2.0
+        lp.lr = float(np.float32(p.learning_rate))
+        lp.speculate = bool(self.speculate)
+        g = nat.LeafGrower(lp, int(self.n_slots))
+        slot0 = g.root(int(n_local), int(n_global))
+        items = np.array([[slot0, 0, 0, 0]], np.int32)
+        recs = self._hist_split(np.array([0], np.int64), np.array([n_local], np.int64),
+                                np.array([slot0], np.int32), 1, items, fmask, f0, identity_rows=identity)
+        g.apply_recs(np.zeros(1, np.int32), recs)
+        while True:
+            t_plan = time.perf_counter()
+            batch = g.replay()
+            if not batch:
+                self.last_stats.plan += time.perf_counter() - t_plan
+                break
+            splits, counts_only = g.expand(batch)
+            self.last_stats.plan += time.perf_counter() - t_plan
+            if counts_only:
+                sg = g.segments(counts_only)
+                lloc, lglob = self._count_arrays(sg[0], sg[1], sg[2], sg[3])
+                g.set_children(counts_only, lloc, lglob, False)
+            if splits:
+                sg = g.segments(splits)
+                lloc, lglob = self._partition_arrays(sg[0], sg[1], sg[2], sg[3], copy_back=True)
+                g.set_children(splits, lloc, lglob, True)
+                order, slots, nb, hb, hc, items = g.plan_hist(splits)
+                recs = self._hist_split(hb, hc, np.asarray(slots, np.int32), nb, items, fmask, f0)
+                g.apply_recs(np.asarray(order, np.int32), recs)
+            g.release_batch(batch)
+        t = g.finish()
+        n = len(t["left"])
+        tree.left, tree.right, tree.parent = t["left"], t["right"], t["parent"]
+        tree.feat, tree.slot_a, tree.slot_b, tree.cond = t["feat"], t["slot_a"], t["slot_b"], t["cond"]
+        tree.leaf, tree.is_leaf = t["leaf"], t["is_leaf"]
+        tree.loss_chg, tree.hess_sum, tree.sample_cnt = t["loss_chg"], t["hess_sum"], t["sample_cnt"]
+        tree.feat_name = [None] * n
+        tree.default_left = [True] * n
+        self.last_batches, self.last_expanded = g.batches, g.expanded
+        self.hist_miss += g.hist_miss
+
     def _grow_loss_guided(self, tree: Tree, nodes: Dict[int, _Node], fmask, f0, pop_is_leaf, make_leaf,
                           children_terminal, leafify_children) -> Dict[int, int]:
         """Exact leaf-wise growth (reference: priority queue ordered by lossChg,
@@ -630,6 +707,9 @@ class TreeBuilder:
         sg, sh = gops.fixed_point_scales(mx[0], mx[1], n_global)
         self.gp_tree = dict(self.gp, sg=sg, sh=sh)
         tree = Tree()
+        if p.grow_policy == "loss" and self.native_leafwise:
+            self._grow_native(tree, fmask, f0, identity, n_local, n_global)
+            return self._finish_tree(tree, {}, t_start)
         nodes: Dict[int, _Node] = {0: _Node(begin=0, cnt_local=n_local, cnt_global=n_global, depth=0, seq=0)}
         self._build_and_find(nodes, [0], [], fmask, f0, identity_rows=identity)
         seq = 1
@@ -721,6 +801,9 @@ class TreeBuilder:
                 tree.hess_sum[t] = h
             nodes = {}
 
+        return self._finish_tree(tree, nodes, t_start)
+
+    def _finish_tree(self, tree: Tree, nodes: Dict[int, _Node], t_start: float) -> Tree:
         # node stats for the dump (updateTreeNodeStat)
         for nid in range(tree.num_nodes):
             nd = nodes.get(nid)
