@@ -272,6 +272,20 @@ PYBIND11_MODULE(_ytk_native, m) {
              return py::make_tuple(hp.order, hp.slots, hp.nbuild, i64arr((py::ssize_t)hp.begin.size(), hp.begin.data()),
                                    i64arr((py::ssize_t)hp.count.size(), hp.count.data()), items);
            })
+      .def("pack_partition",
+           [](const LeafGrower& g, const std::vector<int32_t>& parents, int part_chunk, int target_blocks,
+              int min_rows) {
+             auto pk = g.pack_partition(parents, part_chunk, target_blocks, min_rows);
+             return py::make_tuple(i32arr((py::ssize_t)pk.data.size(), pk.data.data()), pk.off, pk.n_items,
+                                   pk.n_blocks);
+           })
+      .def("plan_hist_packed",  // plan_hist + pack_hist: (order, nbuild, pack, offsets, nwork)
+           [](LeafGrower& g, const std::vector<int32_t>& parents, int target_blocks, int min_rows) {
+             auto hp = g.plan_hist(parents);
+             auto pk = LeafGrower::pack_hist(hp, target_blocks, min_rows);
+             return py::make_tuple(hp.order, hp.nbuild, i32arr((py::ssize_t)pk.data.size(), pk.data.data()),
+                                   pk.off, pk.n_items);
+           })
       .def("release_batch", &LeafGrower::release_batch)
       .def("finish",
            [](LeafGrower& g) {

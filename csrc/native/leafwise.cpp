@@ -320,6 +320,83 @@ LeafGrower::HistPlan LeafGrower::plan_hist(const std::vector<int32_t>& split_par
   return hp;
 }
 
+namespace {
+
+int64_t chunk_rows(int64_t total, int target_blocks, int min_rows) {
+  return std::max<int64_t>(min_rows, (total + target_blocks - 1) / std::max(1, target_blocks));
+}
+
+// segment i = [begin[i], begin[i] + count[i]) -> items (tag[i], b, e, k) of <= ch rows
+void emit_chunks(const std::vector<int64_t>& begin, const std::vector<int64_t>& count,
+                 const std::vector<int32_t>& tag, int64_t ch, bool blk_index, std::vector<int32_t>& out) {
+  for (size_t i = 0; i < begin.size(); ++i) {
+    const int64_t end = begin[i] + count[i];
+    int64_t k = 0;
+    for (int64_t b = begin[i]; b < end; b += ch, ++k) {
+      out.push_back(tag[i]);
+      out.push_back((int32_t)b);
+      out.push_back((int32_t)std::min(b + ch, end));
+      out.push_back(blk_index ? (int32_t)k : 0);
+    }
+  }
+}
+
+}  // namespace
+
+LeafGrower::Pack LeafGrower::pack_partition(const std::vector<int32_t>& parents, int part_chunk,
+                                            int target_blocks, int min_rows) const {
+  Pack pk;
+  const size_t n = parents.size();
+  std::vector<int64_t> begin(n), count(n);
+  std::vector<int32_t> tag(n);
+  int64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    begin[i] = nodes_[parents[i]].begin;
+    count[i] = nodes_[parents[i]].cnt_local;
+    tag[i] = (int32_t)i;
+    total += count[i];
+  }
+  auto& d = pk.data;
+  pk.off.push_back(0);
+  emit_chunks(begin, count, tag, chunk_rows(total, target_blocks, min_rows), true, d);
+  pk.n_items = (int64_t)d.size() / 4;
+  pk.off.push_back((int64_t)d.size());
+  for (int sid : parents) d.push_back(nodes_[sid].feat);
+  pk.off.push_back((int64_t)d.size());
+  for (int sid : parents) d.push_back((nodes_[sid].bin_a + nodes_[sid].bin_b) >> 1);
+  pk.off.push_back((int64_t)d.size());
+  for (size_t i = 0; i < n; ++i) d.push_back((int32_t)begin[i]);
+  pk.off.push_back((int64_t)d.size());
+  for (size_t i = 0; i < n; ++i) d.push_back((int32_t)count[i]);
+  pk.off.push_back((int64_t)d.size());
+  int64_t acc = 0;
+  for (size_t i = 0; i < n; ++i) {
+    d.push_back((int32_t)acc);
+    acc += (count[i] + part_chunk - 1) / part_chunk;
+  }
+  pk.n_blocks = acc;
+  pk.off.push_back((int64_t)d.size());
+  d.push_back((int32_t)n);
+  d.push_back((int32_t)acc);
+  return pk;
+}
+
+LeafGrower::Pack LeafGrower::pack_hist(const HistPlan& hp, int target_blocks, int min_rows) {
+  Pack pk;
+  int64_t total = 0;
+  for (int64_t c : hp.count) total += c;
+  std::vector<int32_t> tag(hp.slots.begin(), hp.slots.begin() + hp.nbuild);
+  auto& d = pk.data;
+  pk.off.push_back(0);
+  if (hp.nbuild > 0) emit_chunks(hp.begin, hp.count, tag, chunk_rows(total, target_blocks, min_rows), false, d);
+  pk.n_items = (int64_t)d.size() / 4;
+  pk.off.push_back((int64_t)d.size());
+  d.insert(d.end(), hp.items.begin(), hp.items.end());
+  pk.off.push_back((int64_t)d.size());
+  d.insert(d.end(), tag.begin(), tag.end());
+  return pk;
+}
+
 void LeafGrower::release_batch(const std::vector<int32_t>& batch) {
   for (int sid : batch) release(sid);
 }

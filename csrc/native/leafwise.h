@@ -68,6 +68,20 @@ class LeafGrower {
     int nbuild = 0;
   };
   HistPlan plan_hist(const std::vector<int32_t>& split_parents);
+
+  // Launch-ready int32 packs for the device steps (one pinned upload each). Chunking:
+  // ch = max(min_rows, ceil(rows / target_blocks)) rows per item, as TreeBuilder._chunk.
+  // partition: [items (split, b, e, k) x nitems | feat | thr | begin | count | first_blk
+  //   (exclusive scan of ceil(count / part_chunk)) | hdr (n, nblocks)]
+  struct Pack {
+    std::vector<int32_t> data;
+    std::vector<int64_t> off;  // section offsets (int32 elements)
+    int64_t n_items = 0, n_blocks = 0;
+  };
+  Pack pack_partition(const std::vector<int32_t>& parents, int part_chunk, int target_blocks,
+                      int min_rows) const;
+  // histogram step of `hp`: [work (slot, b, e, 0) x nwork | items x norder | build slots]
+  static Pack pack_hist(const HistPlan& hp, int target_blocks, int min_rows);
   void release_batch(const std::vector<int32_t>& batch);
 
   // node accessors for the driver

@@ -182,6 +182,29 @@ def test_native_leafwise_planner_matches_python(monkeypatch, kw):
         assert res[0][5] > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["plain", "pool", "depth"])
+def test_native_leafwise_gpu_paths_match_python(monkeypatch, mode):
+    """GPU: native planner with the lean launch path == native planner through the generic
+    helpers == Python planner (exact int64 histograms => identical models)."""
+    res = []
+    for native, fast in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("YTK_LEAF_NATIVE", native)
+        monkeypatch.setenv("YTK_LEAF_FAST", fast)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 63
+        if mode == "pool":
+            p.histogram_pool_capacity = 6 * 256 * 28 * 16 / float(1 << 20)
+        if mode == "depth":
+            p.tree.max_depth = 5
+        tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
+        tr.train()
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss, tr.builder.hist_miss))
+    assert res[0] == res[1] == res[2]
+    if mode == "pool":
+        assert res[0][3] > 0
+
+
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():
     """histogram_pool_capacity (MB) bounds the live histograms of leaf-wise growth; evicted
     parents are rebuilt (pool miss) instead of derived -- exact int64 sums => same model."""

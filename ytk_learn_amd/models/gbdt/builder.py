@@ -143,6 +143,12 @@ class _Uploader:
         return [self.devbuf[s:s + int(np.prod(shape))].view(*shape) for s, shape in outs]
 
 
+def _put_flat(up: "_Uploader", a: np.ndarray) -> int:
+    """One int32 array -> the uploader's device buffer; returns its device address."""
+    t, = up.put(a)
+    return t.data_ptr()
+
+
 def _chunk_segments(begins: np.ndarray, counts: np.ndarray, ch: int):
     """Vectorised chunking of segments -> (seg_idx, chunk_begin, chunk_end, blk_in_seg)."""
     nb = np.where(counts > 0, (counts + ch - 1) // ch, 0).astype(np.int64)
@@ -220,6 +226,7 @@ class TreeBuilder:
         self._root_gh = None
         self._staging = None
         self._cursor = None
+        self._split_out = None
         self.free_slots = None
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0"
         self.fmask_np = np.ones(F, np.uint8)
@@ -444,6 +451,79 @@ class TreeBuilder:
         return lloc, lglob
 
     # ------------------------------------------------------- loss-guided growth
+    def _fast_leafwise_ok(self) -> bool:
+        """Lean launch path for the native planner: one GPU, single-pass partition, staged
+        uint8 histograms and the node-resident split kernel (what the packs encode)."""
+        stride = self.bins.shape[1]
+        return (self.dev.type == "cuda" and not self.comm.is_dist and self.part_atomic
+                and self.bins.dtype == torch.uint8 and self.binsT.dtype == torch.uint8 and self.B <= 256
+                and stride % 32 == 0 and stride >= ((self.F + 31) // 32) * 32
+                and gops.split_node_fits(self.B, self.F)
+                and os.environ.get("YTK_HOST_STAGED", "1") != "0"
+                and os.environ.get("YTK_LEAF_FAST", "1") != "0")
+
+    def _fast_partition(self, g, splits) -> np.ndarray:
+        """Partition of the batch's split segments from one native pack (one upload, raw
+        kernel launches); returns the left row counts."""
+        t0 = time.perf_counter()
+        h, s = hip(), stream(self.rows)
+        arr, off, nitems, nblocks = g.pack_partition(splits, gops.PART_CHUNK, self.TARGET_BLOCKS,
+                                                     self.MIN_ROWS_PER_BLOCK)
+        base = _put_flat(self.up, arr)
+        a = lambda i: base + 4 * off[i]  # noqa: E731
+        n = len(splits)
+        if self._cursor is None or self._cursor.numel() < n:
+            self._cursor = torch.empty(max(n, 1024), dtype=torch.int64, device=self.dev)
+        cur = self._cursor.data_ptr()
+        h.memset_async(cur, 0, n * 8, s)
+        root = self._root_gh is not None  # first partition of an unsampled tree: identity rows
+        rows_in = 0 if root else self.rows.data_ptr()
+        gh_in = (self._root_gh if root else self.ghp).data_ptr()
+        if nblocks > 0:
+            h.partition_atomic(self.binsT.data_ptr(), 1, self.binsT.shape[1], rows_in, self.rows_tmp.data_ptr(),
+                               gh_in, self.gh_tmp.data_ptr(), a(5), a(6), a(6) + 4, int(nblocks), a(1), a(2),
+                               a(3), a(4), cur, 0, s)
+        if root:  # the root segment is every row: take the output buffers whole
+            self._root_gh = None
+            self.rows, self.rows_tmp = self.rows_tmp, self.rows
+            self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
+        elif nitems > 0:
+            h.segment_copy(a(0), int(nitems), self.rows_tmp.data_ptr(), self.rows.data_ptr(),
+                           self.gh_tmp.data_ptr(), self.ghp.data_ptr(), s)
+        lloc = self._cursor[:n].cpu().numpy() & 0xFFFFFFFF
+        self.up.reset()
+        self.last_stats.partition += time.perf_counter() - t0
+        return lloc
+
+    def _fast_hist_split(self, g, splits, fmask, f0):
+        """Histograms + split search of the batch's children from one native pack."""
+        t0 = time.perf_counter()
+        h, s = hip(), stream(self.hist)
+        order, nb, arr, off, nwork = g.plan_hist_packed(splits, self.TARGET_BLOCKS, self.MIN_ROWS_PER_BLOCK)
+        base = _put_flat(self.up, arr)
+        n = len(order)
+        gp = self.gp_tree
+        if nb:
+            h.zero_slots(self.hist.data_ptr(), self.slot_bytes, base + 4 * off[2], nb, s)
+            need = nwork * ((self.F + 31) // 32) * self.B * 64
+            if self._staging is None or self._staging.numel() < need:
+                self._staging = torch.empty(int(need * 1.25), dtype=torch.int64, device=self.dev)
+            h.hist_fx_staged(self.bins.data_ptr(), self.bins.shape[1], self.F, self.ghp.data_ptr(),
+                             self.rows.data_ptr(), base, int(nwork), self.hist.data_ptr(), self.B,
+                             float(gp["sg"]), float(gp["sh"]), 0, 0, self._staging.data_ptr(), 0, nb,
+                             base + 4 * off[2], 0, s)
+        t1 = time.perf_counter()
+        if self._split_out is None or self._split_out.numel() < n * 48:
+            self._split_out = torch.empty(max(n, 512) * 48, dtype=torch.uint8, device=self.dev)
+        h.split_find(self.hist.data_ptr(), self.B, self.F, self.nbins_f.data_ptr(), fmask.data_ptr(), int(f0),
+                     base + 4 * off[1], n, self._split_out.data_ptr(), gp["mcw"], gp["l1"], gp["l2"],
+                     gp["max_abs_leaf"], 1.0 / float(gp["sg"]), 1.0 / float(gp["sh"]), 0, 0, 0, 0, s)
+        recs = self._split_out[:n * 48].cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+        self.up.reset()
+        self.last_stats.build_hist += t1 - t0
+        self.last_stats.find_split += time.perf_counter() - t1
+        return order, recs
+
     def _grow_native(self, tree: Tree, fmask, f0: int, identity: bool, n_local: int, n_global: int):
         """Loss-guided growth with the native planner (csrc/native/leafwise.cpp): the same
         schedule, trees and statistics as ``_grow_loss_guided`` -- replay, speculative batch
@@ -468,6 +548,7 @@ class TreeBuilder:
         recs = self._hist_split(np.array([0], np.int64), np.array([n_local], np.int64),
                                 np.array([slot0], np.int32), 1, items, fmask, f0, identity_rows=identity)
         g.apply_recs(np.zeros(1, np.int32), recs)
+        fast = self._fast_leafwise_ok()
         while True:
             t_plan = time.perf_counter()
             batch = g.replay()
@@ -481,11 +562,16 @@ class TreeBuilder:
                 lloc, lglob = self._count_arrays(sg[0], sg[1], sg[2], sg[3])
                 g.set_children(counts_only, lloc, lglob, False)
             if splits:
-                sg = g.segments(splits)
-                lloc, lglob = self._partition_arrays(sg[0], sg[1], sg[2], sg[3], copy_back=True)
-                g.set_children(splits, lloc, lglob, True)
-                order, slots, nb, hb, hc, items = g.plan_hist(splits)
-                recs = self._hist_split(hb, hc, np.asarray(slots, np.int32), nb, items, fmask, f0)
+                if fast:
+                    lloc = self._fast_partition(g, splits)
+                    g.set_children(splits, lloc, lloc, True)
+                    order, recs = self._fast_hist_split(g, splits, fmask, f0)
+                else:
+                    sg = g.segments(splits)
+                    lloc, lglob = self._partition_arrays(sg[0], sg[1], sg[2], sg[3], copy_back=True)
+                    g.set_children(splits, lloc, lglob, True)
+                    order, slots, nb, hb, hc, items = g.plan_hist(splits)
+                    recs = self._hist_split(hb, hc, np.asarray(slots, np.int32), nb, items, fmask, f0)
                 g.apply_recs(np.asarray(order, np.int32), recs)
             g.release_batch(batch)
         t = g.finish()
