@@ -452,19 +452,19 @@ class TreeBuilder:
 
     # ------------------------------------------------------- loss-guided growth
     def _fast_leafwise_ok(self) -> bool:
-        """Lean launch path for the native planner: one GPU, single-pass partition, staged
-        uint8 histograms and the node-resident split kernel (what the packs encode)."""
+        """Lean launch path for the native planner: single-pass partition, staged uint8
+        histograms and the node-resident split kernel (what the packs encode)."""
         stride = self.bins.shape[1]
-        return (self.dev.type == "cuda" and not self.comm.is_dist and self.part_atomic
+        return (self.dev.type == "cuda" and self.part_atomic
                 and self.bins.dtype == torch.uint8 and self.binsT.dtype == torch.uint8 and self.B <= 256
                 and stride % 32 == 0 and stride >= ((self.F + 31) // 32) * 32
                 and gops.split_node_fits(self.B, self.F)
                 and os.environ.get("YTK_HOST_STAGED", "1") != "0"
                 and os.environ.get("YTK_LEAF_FAST", "1") != "0")
 
-    def _fast_partition(self, g, splits) -> np.ndarray:
+    def _fast_partition(self, g, splits):
         """Partition of the batch's split segments from one native pack (one upload, raw
-        kernel launches); returns the left row counts."""
+        kernel launches); returns the left row counts (local, global)."""
         t0 = time.perf_counter()
         h, s = hip(), stream(self.rows)
         arr, off, nitems, nblocks = g.pack_partition(splits, gops.PART_CHUNK, self.TARGET_BLOCKS,
@@ -490,10 +490,17 @@ class TreeBuilder:
         elif nitems > 0:
             h.segment_copy(a(0), int(nitems), self.rows_tmp.data_ptr(), self.rows.data_ptr(),
                            self.gh_tmp.data_ptr(), self.ghp.data_ptr(), s)
-        lloc = self._cursor[:n].cpu().numpy() & 0xFFFFFFFF
+        if self.comm.is_dist:  # global counts: one all-reduce of the masked cursors
+            both = (self._cursor[:n] & 0xFFFFFFFF).repeat(2, 1)
+            self.comm.allreduce_(both[1])
+            both = both.cpu().numpy()
+            lloc, lglob = both[0], both[1]
+        else:
+            lloc = self._cursor[:n].cpu().numpy() & 0xFFFFFFFF
+            lglob = lloc
         self.up.reset()
         self.last_stats.partition += time.perf_counter() - t0
-        return lloc
+        return lloc, lglob
 
     def _fast_hist_split(self, g, splits, fmask, f0):
         """Histograms + split search of the batch's children from one native pack."""
@@ -512,6 +519,11 @@ class TreeBuilder:
                              self.rows.data_ptr(), base, int(nwork), self.hist.data_ptr(), self.B,
                              float(gp["sg"]), float(gp["sh"]), 0, 0, self._staging.data_ptr(), 0, nb,
                              base + 4 * off[2], 0, s)
+            if self.comm.is_dist:  # the built slots, gathered -> one all-reduce -> scattered
+                idx = torch.from_numpy(arr[off[2]:off[2] + nb].astype(np.int64)).to(self.dev)
+                buf = self.hist.index_select(0, idx)
+                self.comm.allreduce_(buf)
+                self.hist.index_copy_(0, idx, buf)
         t1 = time.perf_counter()
         if self._split_out is None or self._split_out.numel() < n * 48:
             self._split_out = torch.empty(max(n, 512) * 48, dtype=torch.uint8, device=self.dev)
@@ -563,8 +575,8 @@ class TreeBuilder:
                 g.set_children(counts_only, lloc, lglob, False)
             if splits:
                 if fast:
-                    lloc = self._fast_partition(g, splits)
-                    g.set_children(splits, lloc, lloc, True)
+                    lloc, lglob = self._fast_partition(g, splits)
+                    g.set_children(splits, lloc, lglob, True)
                     order, recs = self._fast_hist_split(g, splits, fmask, f0)
                 else:
                     sg = g.segments(splits)
