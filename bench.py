@@ -8,10 +8,19 @@ lr 0.1, l1 = l2 = 0, min_child_hessian_sum 100 -- the reference's
 experiment/higgs/local_gbdt.conf with tree_grow_policy=level, max_depth=6.
 ``--policy loss`` runs the reference-identical leaf-wise 255-leaf shape (a).
 
-A "step" is one boosting round = one tree + train-score update + train loss/
-gradients for the next tree + incremental test-set scoring and test loss
-(the reference's loss-monitoring loop, GBDTOptimizer.java:406-447).
+A "step" is one whole reference boosting round (GBDTOptimizer.java:406-462): one
+tree + train-score update + train loss/gradients for the next tree + incremental
+test-set scoring and test loss + the round's model conversion (convertModel: slot ->
+raw threshold, feature names, default directions, :431 / :663-690) + the per-round
+(train, test) loss readback (:457-462). Conversion and readback are pipelined one
+round behind the GPU (pinned buffers + events); the timed region ends only after
+every timed tree is a host model tree and every loss has landed.
 Scaling is STRONG: the 10.5M rows are sharded over the N ranks.
+
+``vs_baseline`` is null: the reference publishes no depth-6 level-wise number. The
+reference-identical shape (leaf-wise, 255 leaves) is timed separately on the same
+data at N=1 and reported as ``leafwise_s_per_tree`` / ``leafwise_vs_reference``
+(÷ 1.136 s/tree, docs/gbdt_experiments.md:104).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 For N>1 the driver launches it under torch.distributed.run (RANK/WORLD_SIZE env).
@@ -41,6 +50,25 @@ BASELINE_SEC_PER_TREE = 1.136  # ytk-learn 567.83 s / 500 trees (docs/gbdt_exper
 METRIC = "Higgs-11M GBDT: sec/tree (500 trees, depth 6, 255 bins) at 1/2/4/8 MI355X"
 
 
+def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
+    """W untimed + K timed whole rounds; returns the max-over-ranks wall time of the K."""
+    for i in range(warmup):
+        tr.run_round(i)
+    tr.materialize()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        tr.run_round(i)
+    tr.materialize()  # the last round's trees and losses land inside the timed region
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    comm.barrier()
+    el = time.perf_counter() - t0
+    return comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -56,6 +84,8 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--profile", action="store_true", help="sync per phase and print time stats")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--leafwise-steps", type=int, default=None,
+                    help="extra timed leaf-wise 255-leaf rounds on the same data (default 10 at N=1, 0 at N>1)")
     a = ap.parse_args()
 
     comm = Comm.from_env(device=a.device)
@@ -97,26 +127,27 @@ def main():
         torch.cuda.synchronize(dev)
     prep_s = time.perf_counter() - t0
 
-    for i in range(a.warmup):
-        tr.step(i)
-    comm.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.warmup, a.warmup + a.steps):
-        tr.step(i)
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    comm.barrier()
-    el = time.perf_counter() - t0
-    el_max = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
-
+    el_max = timed_rounds(tr, comm, dev, a.warmup, a.steps)
+    assert len(tr.model.trees) == total_rounds, "every timed tree must be a converted host tree"
     # quality check after the timed rounds (outside timing)
     auc = tr.eval_test.evals[0].compute(yt, tr.te_pred, None, comm)[0]
-    train_loss, test_loss = tr._losses()  # collective: every rank calls it
+    train_loss, test_loss = tr.round_losses[total_rounds - 1]
     sec_per_tree = el_max / a.steps
     if a.profile and rank == 0:
         print(tr.timer.report() if tr.use_device_builder else tr.builder.total_stats, file=sys.stderr)
+    leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else (10 if world == 1 else 0)
+    leaf = None
+    if leaf_steps > 0 and a.policy == "level":
+        del tr
+        tpl = TreeParams(max_depth=-1, max_leaf_cnt=255, min_child_hessian_sum=100.0, min_split_loss=0.0,
+                         min_split_samples=-1, learning_rate=0.1, l1=0.0, l2=0.0, grow_policy="loss")
+        pl = GBDTParams(round_num=3 + leaf_steps, loss_function="sigmoid", eval_metric=["auc"],
+                        missing_value="value@0", approximate=params.approximate, tree=tpl)
+        trl = GBDTTrainer(pl, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log)
+        trl.prepare()
+        trl.init_gradients()
+        leaf = timed_rounds(trl, comm, dev, 3, leaf_steps) / leaf_steps
+        assert len(trl.model.trees) == 3 + leaf_steps
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -128,7 +159,8 @@ def main():
             "ms_per_step": round(1000.0 * sec_per_tree, 4),
             "higher_is_better": False,
             "scaling": "strong",
-            "vs_baseline": round(sec_per_tree / BASELINE_SEC_PER_TREE, 6),
+            "vs_baseline": (round(sec_per_tree / BASELINE_SEC_PER_TREE, 6) if a.policy == "loss"
+                            and a.leaves == 255 else None),
             "dtype": "fp32",
             "data": "synthetic Higgs-shape (10.5M train + 0.5M test x 28 dense float features, random-init trees)",
             "config": {
@@ -145,7 +177,13 @@ def main():
             "test_auc": round(float(auc), 6),
             "prep_s": round(prep_s, 3),
             "datagen_s": round(gen_s, 3),
+            "timed_region": "step + convertModel + per-round loss readback (pipelined), all trees landed",
+            "trees_converted": total_rounds,
         }
+        if leaf is not None:
+            res["leafwise_s_per_tree"] = round(leaf, 6)
+            res["leafwise_vs_reference"] = round(leaf / BASELINE_SEC_PER_TREE, 6)
+            res["leafwise_rounds_timed"] = leaf_steps
         print(json.dumps(res), flush=True)
     comm.close()
 

@@ -17,6 +17,9 @@ void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr
                         uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
+int ytk_hist_wide(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, float,
+                  float, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+int ytk_hist_wide_group(int, int);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
@@ -79,6 +82,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_fx", &ytk_hist_fx);
   m.def("hist_fx_global", &ytk_hist_fx_global);
   m.def("hist_fx_staged", &ytk_hist_fx_staged);
+  m.def("hist_wide", &ytk_hist_wide);
+  m.def("hist_wide_group", &ytk_hist_wide_group);
   m.def("split_find", &ytk_split_find);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);

@@ -23,6 +23,9 @@
 //   * Block partials -> global int64 atomics (zero entries skipped).
 #include "common.h"
 
+#include <algorithm>
+#include <stdexcept>
+
 namespace ytk {
 
 constexpr int kHistThreads = 1024;
@@ -243,11 +246,88 @@ __global__ __launch_bounds__(256) void hist_fx_global_kernel(
   }
 }
 
+// Wide-bin histogram (B > 256, uint16 bins -- e.g. the 5000-bin communication-stress
+// config, docs/gbdt_experiments.md:156-168; reference loop HistogramBuilder.java:56-90).
+// The 32-feature x B-bin LDS planes of hist_fx_kernel do not fit, so a block owns a
+// GROUP of FG features (FG = floor(LDS budget / (B * 16 B)), >= 1) and reads their
+// bins from the COLUMN-major matrix binsT [F][ncol] (2 B per row per feature,
+// coalesced for the identity root, monotone row ids inside a node otherwise).
+// LDS holds interleaved exact int64 (g, h) pairs lds[(f_in_group * B + bin) * 2 + {0,1}],
+// accumulated with ds_add_u64 (same fixed point as hist_fx_kernel -> bitwise equal to
+// the CPU path). Block partials are flushed with global int64 atomics, zero entries
+// skipped (deep nodes touch few bins). grid = (work items, ceil(F / FG)).
+constexpr int kWideThreads = 512;
+constexpr int kWideU = 4;                    // rows in flight per thread
+constexpr int kWideLdsBytes = 160 * 1024;    // one block per CU at the widest groups
+
+template <bool kIdentity>
+__global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
+    const uint16_t* __restrict__ binsT, long long ncol, int F, int FG,
+    const float2* __restrict__ ghp, const int* __restrict__ rows,
+    const int4* __restrict__ work, long long* __restrict__ hist, int B,
+    float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
+    const int* __restrict__ work_off_dev) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long wl[];
+  const int bx = (int)blockIdx.x + (work_off_dev ? *work_off_dev : 0);
+  if (nwork_dev && bx >= *nwork_dev) return;
+  if (scales_dev) {
+    sg = scales_dev[0];
+    sh = scales_dev[1];
+  }
+  const int4 w = work[bx];
+  const int f_lo = (int)blockIdx.y * FG;
+  const int nf = min(FG, F - f_lo);
+  const int tid = threadIdx.x;
+  const int E = nf * B;
+  for (int i = tid; i < 2 * E; i += kWideThreads) wl[i] = 0ull;
+  __syncthreads();
+  const uint16_t* col = binsT + (size_t)f_lo * ncol;
+  for (int base = w.y + tid; base < w.z; base += kWideThreads * kWideU) {
+    int r[kWideU];
+    float2 v[kWideU];
+    bool ok[kWideU];
+#pragma unroll
+    for (int j = 0; j < kWideU; ++j) {
+      const int pos = base + j * kWideThreads;
+      ok[j] = pos < w.z;
+      const int p = ok[j] ? pos : w.y;
+      r[j] = kIdentity ? p : rows[p];
+      v[j] = ghp[p];
+    }
+#pragma unroll
+    for (int j = 0; j < kWideU; ++j) {
+      if (!ok[j]) continue;
+      const unsigned long long gi = (unsigned long long)__float2ll_rn(v[j].x * sg);
+      const unsigned long long hi = (unsigned long long)__float2ll_rn(v[j].y * sh);
+      const uint16_t* c = col + (size_t)(unsigned)r[j];
+      for (int fi = 0; fi < nf; ++fi) {
+        const int bin = c[(size_t)fi * ncol];
+        unsigned long long* e = &wl[(size_t)(fi * B + bin) * 2];
+        atomicAdd(e, gi);
+        atomicAdd(e + 1, hi);
+      }
+    }
+  }
+  __syncthreads();
+  long long* out = hist + (size_t)w.x * B * F * 2;
+  for (int i = tid; i < E; i += kWideThreads) {
+    const unsigned long long g = wl[2 * i], h = wl[2 * i + 1];
+    if (g | h) {
+      const int fi = i / B, bin = i - fi * B;
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(&out[((size_t)bin * F + f_lo + fi) * 2]);
+      atomicAdd(o, g);
+      atomicAdd(o + 1, h);
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
 
 extern "C" {
+
+int ytk_hist_wide_group(int B, int F);
 
 // nwork_dev / scales_dev (optional): device-resident work count (grid = nwork is the
 // maximum) and fixed-point scales, used by the GPU-resident level engine.
@@ -326,6 +406,40 @@ void ytk_hist_fx_global(uintptr_t bins, int bin_bytes, long long stride, int F, 
                        (const int4*)work, (long long*)hist, B, sg, sh);
   }
   YTK_LAUNCH_CHECK();
+}
+
+// Wide-bin histogram (uint16 binsT [F][ncol], any B up to the LDS budget of one feature:
+// B * 16 <= 160 KiB). Target slots must be zero. Returns the feature-group size used.
+int ytk_hist_wide(uintptr_t binsT, long long ncol, int F, uintptr_t ghp, uintptr_t rows,
+                  uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
+                  uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t work_off_dev,
+                  uintptr_t stream) {
+  const int FG = ytk_hist_wide_group(B, F);
+  if (FG <= 0) throw std::invalid_argument("hist_wide: one feature's bins exceed the LDS budget");
+  if (nwork <= 0) return FG;
+  const size_t lds = (size_t)FG * B * 2 * sizeof(unsigned long long);
+  dim3 grid(nwork, (F + FG - 1) / FG);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    hipLaunchKernelGGL(hist_wide_kernel<true>, grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT,
+                       ncol, F, FG, (const float2*)ghp, (const int*)nullptr, (const int4*)work,
+                       (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,
+                       (const int*)work_off_dev);
+  } else {
+    hipLaunchKernelGGL(hist_wide_kernel<false>, grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT,
+                       ncol, F, FG, (const float2*)ghp, (const int*)rows, (const int4*)work,
+                       (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,
+                       (const int*)work_off_dev);
+  }
+  YTK_LAUNCH_CHECK();
+  return FG;
+}
+
+// Features per block of hist_wide_kernel (0: a single feature does not fit).
+int ytk_hist_wide_group(int B, int F) {
+  const long long per = (long long)B * 16;
+  if (B <= 0 || per > kWideLdsBytes) return 0;
+  return (int)std::min<long long>(F, kWideLdsBytes / per);
 }
 
 }  // extern "C"

@@ -376,3 +376,23 @@ def test_partition_atomic_is_a_segmentwise_partition(cuda, identity):
             kg = sorted(zip(og[lo:hi].tolist(), ghg[lo:hi, 0].tolist(), ghg[lo:hi, 1].tolist()))
             assert kc == kg
     assert bool((og[~covered] == -1).all())
+
+
+@pytest.mark.parametrize("F,nb,B", [(7, 300, 300), (28, 5000, 5000), (3, 9000, 9000), (40, 700, 704)])
+@pytest.mark.parametrize("gathered", [False, True])
+def test_hist_build_wide_matches_cpu(cuda, F, nb, B, gathered):
+    """Wide-bin (uint16, B > 256) LDS kernel == the exact CPU integer histogram, with
+    several work items over several slots and (optionally) a row permutation."""
+    N = 60000
+    bins = _rand_bins(N, F, nb, seed=3, dtype=torch.int16)
+    binsT = bins[:, :F].t().contiguous()
+    gh = _gh(N, 4)
+    rows = torch.randperm(N, generator=torch.Generator().manual_seed(5)).to(torch.int32) if gathered else None
+    work = torch.tensor([[0, 0, 20000, 0], [0, 20000, 31000, 0], [1, 31000, 31001, 0], [2, 31001, N, 0]],
+                        dtype=torch.int32)
+    hc = torch.zeros((3, B, F, 2), dtype=torch.int64)
+    gops.hist_build(bins, F, gh, rows, work, hc, B, SG, SH)
+    hg = torch.zeros((3, B, F, 2), dtype=torch.int64, device=cuda)
+    gops.hist_build(bins.to(cuda), F, gh.to(cuda), rows.to(cuda) if rows is not None else None, work.to(cuda),
+                    hg, B, SG, SH, binsT=binsT.to(cuda))
+    assert torch.equal(hg.cpu(), hc)

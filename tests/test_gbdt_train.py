@@ -225,3 +225,41 @@ def test_histogram_pool_capacity_misses_do_not_change_the_tree():
         misses.append(tr.builder.hist_miss)
     assert dumps[0] == dumps[1]
     assert misses[0] == 0 and misses[1] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_cnt", [300, 5000])
+def test_wide_bins_device_builder_matches_cpu(cuda, max_cnt):
+    """> 256 bins (uint16): the GPU level builder (wide LDS histograms) == the host builder
+    on the GPU == the CPU path, tree for tree (silent corruption above 256)."""
+    d_cpu = _data(40000, 21)
+    approx = [{"cols": "default", "type": "sample_by_quantile", "max_cnt": max_cnt, "alpha": 0.5}]
+    dumps = []
+    for dev, dev_builder in (("cpu", False), (cuda, False), (cuda, True)):
+        p = _params("level", rounds=3)
+        p.approximate = approx
+        p.device_builder = dev_builder
+        d = GBDTData(d_cpu.X.to(dev), d_cpu.y.to(dev))
+        tr = GBDTTrainer(p, d, GBDTData(d.X[:5000], d.y[:5000]))
+        tr.train()
+        assert tr.bins.dtype == torch.int16 and tr.B > 256
+        assert tr.use_device_builder == (dev_builder and dev != "cpu")
+        dumps.append((tr.model.dumps(), tr.last_train_loss))
+    # integer histograms: the two GPU builders agree bitwise; the CPU gradient path agrees
+    # to float rounding (same check as test_train_gpu_matches_cpu)
+    assert dumps[1][0] == dumps[2][0]
+    assert dumps[1][1] == dumps[2][1]
+    assert dumps[0][0].split("\n")[5] == dumps[1][0].split("\n")[5]  # root split line
+    np.testing.assert_allclose(dumps[0][1], dumps[1][1], rtol=2e-4)
+
+
+def test_more_than_65536_candidates_is_an_error():
+    from ytk_learn_amd.utils.errors import YtkLearnError
+
+    X = torch.arange(70000, dtype=torch.float32)[:, None].repeat(1, 2)
+    y = (torch.rand(70000, 1) < 0.5).float()
+    p = _params("level", rounds=1)
+    p.approximate = [{"cols": "default", "type": "no_sample"}]
+    tr = GBDTTrainer(p, GBDTData(X, y), None)
+    with pytest.raises(YtkLearnError, match="65536"):
+        tr.prepare()

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
+from ...utils.errors import YtkLearnError
 from ...parallel.comm import Comm
 
 
@@ -171,6 +172,11 @@ class BinMapper:
                 c = np.zeros(1, np.float32)
             cands.append(np.sort(c.astype(np.float32)))
         mb = max(len(c) for c in cands)
+        if mb > 65536:
+            # bins are stored as uint16: more candidates would wrap bin ids (mis-binned rows)
+            worst = int(np.argmax([len(c) for c in cands]))
+            raise YtkLearnError(f"[GBDT] feature {worst} has {mb} split candidates; at most 65536 are "
+                                f"supported (set feature.approximate max_cnt / sample_by_quantile for it)")
         dtype = torch.uint8 if mb <= 256 else torch.int16
         stride = ((F + 31) // 32) * 32
         return cls(cands, mb, dtype, stride, split_type)

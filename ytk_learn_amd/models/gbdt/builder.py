@@ -310,7 +310,8 @@ class TreeBuilder:
                 self.hist.index_fill_(0, ids_d.long(), 0)
             src_gh = self._root_gh if (identity_rows and self._root_gh is not None) else self.ghp
             staging = None
-            if self.dev.type == "cuda" and os.environ.get("YTK_HOST_STAGED", "1") != "0":
+            if (self.dev.type == "cuda" and os.environ.get("YTK_HOST_STAGED", "1") != "0"
+                    and self.bins.dtype == torch.uint8 and self.B <= 256):
                 need = len(work) * ((self.F + 31) // 32) * self.B * 64
                 if self._staging is None or self._staging.numel() < need:
                     self._staging = torch.empty(int(need * 1.25), dtype=torch.int64, device=self.dev)
@@ -318,7 +319,7 @@ class TreeBuilder:
             gops.hist_build(self.bins, self.F, src_gh, None if identity_rows else self.rows,
                             work_d, self.hist, self.B, self.gp_tree["sg"], self.gp_tree["sh"],
                             staging=staging, slot_base=max(s0, 0), nslots=nb,
-                            slot_ids=ids_d if s0 < 0 else None)
+                            slot_ids=ids_d if s0 < 0 else None, binsT=self.binsT)
         self._sync()
         t1 = time.perf_counter()
         if nb and self.comm.is_dist:

@@ -43,33 +43,33 @@ MAX_DEPTH_DEVICE = 12
 class DeviceTree:
     """Handle of a tree built on the device: node-table snapshot + scoring arrays."""
 
-    def __init__(self, nodes: torch.Tensor, st: torch.Tensor, bin_arrays, max_nodes: int):
+    def __init__(self, nodes: torch.Tensor, st: torch.Tensor, bin_arrays, max_nodes: int,
+                 snap: Optional[torch.Tensor] = None, st_bytes: int = 64):
         self.nodes = nodes
         self.st = st
         self.bin_arrays = bin_arrays
         self.max_nodes = max_nodes
+        self.snap = snap          # the whole snapshot buffer (st | nodes | scoring arrays)
+        self.st_bytes = st_bytes
+
+    def split_host_snap(self, host: np.ndarray):
+        """(node-table bytes, st words) views of a host copy of ``snap``."""
+        nb = self.max_nodes * DNODE_DTYPE.itemsize
+        return host[self.st_bytes:self.st_bytes + nb], host[:self.st_bytes].view(np.int32)
 
     def to_tree(self, nodes_np=None, st_np=None) -> Tree:
-        nd = (nodes_np if nodes_np is not None else self.nodes.cpu().numpy()).view(DNODE_DTYPE).reshape(-1)
-        nn = int((st_np if st_np is not None else self.st.cpu().numpy())[ST_NUM_NODES])
-        t = Tree()
-        for _ in range(nn - 1):
-            t._alloc(-1)
-        for i in range(nn):
-            n = nd[i]
-            leaf = bool(n["is_leaf"]) or n["left"] < 0
-            if leaf:
-                t.set_leaf(i, float(n["value"]))
-            else:
-                t.is_leaf[i] = False
-                t.left[i], t.right[i] = int(n["left"]), int(n["right"])
-                t.parent[t.left[i]] = i
-                t.parent[t.right[i]] = i
-                t.set_split(i, int(n["feat"]), int(n["bin_a"]), int(n["bin_b"]))
-            t.loss_chg[i] = float(n["loss_chg"])
-            t.hess_sum[i] = float(np.float32(n["H"]))
-            t.sample_cnt[i] = int(n["cnt_global"])
-        return t
+        nd = (nodes_np if nodes_np is not None else self.nodes.cpu().numpy())
+        st = st_np if st_np is not None else self.st.cpu().numpy()
+        return node_table_to_tree(nd, st)
+
+
+def node_table_to_tree(nodes_bytes: np.ndarray, st: np.ndarray) -> Tree:
+    """Device node table (DNODE_DTYPE records) -> host Tree, vectorised (no per-node loop)."""
+    nn = int(st[ST_NUM_NODES])
+    nd = np.asarray(nodes_bytes).view(DNODE_DTYPE).reshape(-1)[:nn]
+    leaf = (nd["is_leaf"] != 0) | (nd["left"] < 0)
+    return Tree.from_arrays(nd["left"], nd["right"], nd["feat"], nd["bin_a"], nd["bin_b"], nd["value"], leaf,
+                            nd["loss_chg"], nd["H"], nd["cnt_global"])
 
 
 class DeviceLevelBuilder:
@@ -84,6 +84,12 @@ class DeviceLevelBuilder:
         p = params
         if not (1 <= p.max_depth <= MAX_DEPTH_DEVICE) or p.grow_policy != "level":
             raise ValueError("device builder needs level-wise growth with 1 <= max_depth <= 12")
+        if not self.supports(bins, binsT, B, F):
+            raise ValueError(f"device builder: unsupported bin layout (dtype {bins.dtype}, B={B}, F={F})")
+        # wide mode: uint16 bins with B > 256 -> feature-grouped LDS histograms over binsT
+        self.wide = bins.dtype == torch.int16
+        self.hist_target = (min(self.HIST_TARGET, max(32, 1024 // (-(-F // gops.wide_group(B, F)))))
+                            if self.wide else self.HIST_TARGET)
         self.p = p
         self.bins, self.binsT = bins, binsT
         self.dev = bins.device
@@ -101,7 +107,7 @@ class DeviceLevelBuilder:
         # (the kernel holds one chunk of <= 2048 rows per block in registers)
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0" and self.MIN_ROWS == 2048
         self.part_target = (-(-self.N // self.MIN_ROWS) + 1) if self.part_atomic else self.PART_TARGET
-        self.max_items = max(self.HIST_TARGET, self.part_target) + self.maxp + 16
+        self.max_items = max(self.hist_target, self.part_target) + self.maxp + 16
         dev = self.dev
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
         # everything a finished tree is (state, node table, scoring arrays) lives in ONE
@@ -153,8 +159,8 @@ class DeviceLevelBuilder:
         # staged histogram flush: block partials to a staging slab with plain stores, then a
         # split-K slot reduce (8 int64 atomics per value instead of one per block)
         groups = (F + 31) // 32
-        max_hist_items = self.HIST_TARGET + (self.maxp // 2) + 2
-        self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0"
+        max_hist_items = self.hist_target + (self.maxp // 2) + 2
+        self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0" and not self.wide
         # multi-GPU: overlap the all-reduce of half a level's histograms with the build of
         # the other half (BASELINE: histogram all-reduce overlapped with the next block's build)
         self.overlap = os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
@@ -169,12 +175,25 @@ class DeviceLevelBuilder:
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
-        self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.HIST_TARGET, self.part_target,
+        self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.hist_target, self.part_target,
                    self.MIN_ROWS]
         self.tree_count = 0
         self.last_keep = None
         self.total_stats = TimeStats()
         self._fmask_cache = {}
+
+    @staticmethod
+    def supports(bins: torch.Tensor, binsT: Optional[torch.Tensor], B: int, F: int) -> bool:
+        """Bin layouts the device kernels handle: uint8 row-major bins (B <= 256, 32-aligned
+        stride) for the 32-feature LDS histogram, or uint16 bins + a contiguous column-major
+        binsT with one feature's planes within the LDS budget for the wide kernel."""
+        if bins.dtype == torch.uint8:
+            stride = bins.shape[1]
+            return B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32
+        if bins.dtype == torch.int16:
+            return (binsT is not None and binsT.dtype == torch.int16 and binsT.shape[0] == F
+                    and binsT.is_contiguous() and gops.wide_group(B, F) > 0)
+        return False
 
     def _snap_views(self, buf):
         out, off = [], 0
@@ -293,6 +312,11 @@ class DeviceLevelBuilder:
                     self.hist.zero_()  # every slot of the tree in one fill (small slabs)
             else:
                 self.hist[slot_base:slot_base + nslots].zero_()
+            if self.wide:
+                h.hist_wide(ptr(self.binsT), self.binsT.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
+                            nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5) if n_dev is None else n_dev,
+                            ptr(self.scales), work_off, s)
+                return
             if self.staged:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
                                  ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0,
@@ -302,7 +326,7 @@ class DeviceLevelBuilder:
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
 
-        build_hist(gh0, rows0, self.HIST_TARGET + 1, 0, 1)
+        build_hist(gh0, rows0, self.hist_target + 1, 0, 1)
         tm.mark("build_hist_compute")
         if dist:
             self.comm.allreduce_(self.hist[0:1])
@@ -372,7 +396,7 @@ class DeviceLevelBuilder:
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
-            nmax = self.HIST_TARGET + half + 1
+            nmax = self.hist_target + half + 1
             if dist and self.overlap and half >= 8 and self.staged:  # large levels only:
                 # small ones are latency bound and a second collective would cost more
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
@@ -402,8 +426,9 @@ class DeviceLevelBuilder:
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         tm.mark("plan")
         self.tree_count += 1
-        st, nodes, *arrays = self._snap_views(self.snap.clone())
-        return DeviceTree(nodes, st, tuple(arrays), self.max_nodes)
+        snap = self.snap.clone()
+        st, nodes, *arrays = self._snap_views(snap)
+        return DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
 
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (for test-set scoring), one forest entry."""

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import os
 import time
+from collections import deque
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence
 
@@ -31,9 +32,9 @@ from ...utils.logging import get_logger
 from ...utils.timestats import PhaseTimer, profiling_enabled
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
-from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder
+from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder, node_table_to_tree
 from .refine import TreeRefiner
-from .tree import GBDTModel, Tree
+from .tree import CandTable, GBDTModel, Tree
 
 
 @dataclass
@@ -97,9 +98,13 @@ class GBDTTrainer:
         self.timer = PhaseTimer(self.dev, self.profile)
         self.kernel_loss = self.loss.gbdt_kernel_id
         self._prepared = False
-        self._pending = []          # device trees not yet converted to host Trees
         self._acc = None            # (train acc, test acc) device tensors of the last round
         self.rounds_done = 0
+        # rounds whose trees / losses are still in flight: (round, dev trees, host buffer, event)
+        self._inflight = deque()
+        self._rb_free = []          # recycled pinned readback buffers
+        self.round_losses = {}      # round -> (train loss, test loss), filled as rounds land
+        self._names_arr = None
 
     # ------------------------------------------------------------ preparation
     def _specs(self) -> List[SamplerSpec]:
@@ -143,7 +148,8 @@ class GBDTTrainer:
         self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
         tp = self.p.tree
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
-                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None)
+                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None
+                                   and DeviceLevelBuilder.supports(self.bins, self.binsT, self.B, self.F))
         if self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
                                               timer=self.timer)
@@ -262,33 +268,114 @@ class GBDTTrainer:
         cur = self.rounds_done
         self.log.info(f"gbdt start train! total round_num={total_rounds}, current round_num={cur}")
         self.init_gradients()
-        start = time.perf_counter()
+        self._train_start = time.perf_counter()
         for i in range(cur, total_rounds):
             fault_point("gbdt", i, self.comm.rank)
-            self.timer.begin()
-            self.step(i)
-            per = self.timer.end()
-            if per and (self.p.verbose or self.log.enabled_for_round(i)):
-                self.log.info(f"[GBDT] time stats tree {i + 1}: {PhaseTimer.fmt(per)}")
-            elif self.profile and not self.use_device_builder and (self.p.verbose or self.log.enabled_for_round(i)):
-                self.log.info(f"[GBDT] time stats tree {i + 1}: {self.builder.last_stats}")
+            self.run_round(i)
             if on_round is not None:
+                self.materialize()
                 on_round(i, self)
             # GBDTOptimizer.java:434-435 -- note Java's (i+1) % -1 == 0 dumps every round
             if dump_cb is not None and p.dump_freq != 0 and ((i + 1) % p.dump_freq == 0):
                 self.materialize()
                 dump_cb(i)
-            if self.p.verbose or self.log.enabled_for_round(i):
-                cost = time.perf_counter() - start
-                self.log.info(f"[model=gbdt] [loss={self.loss.name}] [iter={i + 1}]  {cost:.5f} sec elapse\n"
-                              f"{self.report()}")
         self.materialize()
-        self.total_train_time = time.perf_counter() - start
+        self.total_train_time = time.perf_counter() - self._train_start
         final = self.final_eval()
         self.log.info(f"training end, {self.total_train_time:.5f} sec in all\n{final}")
         if self.profile:
             self.log.info(self.timer.report() if self.use_device_builder else f"[GBDT] {self.builder.total_stats}")
         return self.model
+
+    def run_round(self, i: int, lag: int = 1):
+        """One reference round (GBDTOptimizer.java:406-462): build the tree(s), update the
+        train score + gradients, score the test set, then -- pipelined -- read the round's
+        trees and (train, test) losses back through pinned memory and convert / log them.
+        With ``lag`` = 1 the host converts round i-1 while the GPU runs round i, so the
+        model conversion and the per-round loss readback cost no GPU idle time. Rounds that
+        log eval metrics (watch_train / watch_test) drain synchronously: the metrics read
+        the current predictions."""
+        if not hasattr(self, "_train_start"):
+            self._train_start = time.perf_counter()
+        self.timer.begin()
+        self.step(i)
+        per = self.timer.end()
+        logs = self.p.verbose or self.log.enabled_for_round(i)
+        if per and logs:
+            self.log.info(f"[GBDT] time stats tree {i + 1}: {PhaseTimer.fmt(per)}")
+        elif self.profile and not self.use_device_builder and logs:
+            self.log.info(f"[GBDT] time stats tree {i + 1}: {self.builder.last_stats}")
+        watch = logs and (self.p.watch_train or self.p.watch_test)
+        self._drain(0 if watch else lag)
+
+    # ----------------------------------------------------------- readback pipe
+    def _rb_buffer(self, nbytes: int) -> torch.Tensor:
+        while self._rb_free:
+            buf = self._rb_free.pop()
+            if buf.numel() >= nbytes:
+                return buf
+        buf = torch.empty(max(nbytes, 64), dtype=torch.uint8)
+        return buf.pin_memory() if self.dev.type == "cuda" else buf
+
+    def _enqueue_readback(self, i: int, dev_trees, acc, acc_te):
+        """Copy the round's tree snapshots + loss sums into one pinned buffer (async)."""
+        while len(self._inflight) >= 4:  # bounded: at most 4 rounds in flight
+            self._drain(len(self._inflight) - 1)
+        accs = torch.stack([acc, acc_te if acc_te is not None else torch.zeros_like(acc)]).to(self.dev)
+        if self.comm.is_dist:
+            self.comm.allreduce_(accs)  # GBDTOptimizer.java:502 (loss, weight) allreduce
+        sizes = [dt.snap.numel() for dt in dev_trees]
+        host = self._rb_buffer(32 + sum(sizes))
+        host[:32].view(torch.float64).copy_(accs.reshape(-1), non_blocking=True)
+        off = 32
+        for dt, sz in zip(dev_trees, sizes):
+            host[off:off + sz].copy_(dt.snap, non_blocking=True)
+            off += sz
+        ev = None
+        if self.dev.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+        self._inflight.append((i, dev_trees, host, ev, acc_te is not None))
+
+    def _drain(self, lag: int = 0):
+        """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log."""
+        while len(self._inflight) > lag:
+            i, dev_trees, host, ev, has_te = self._inflight.popleft()
+            if ev is not None:
+                ev.synchronize()
+            hb = host.numpy()
+            a = hb[:32].view(np.float64)
+            off = 32
+            for dt in dev_trees:
+                sz = dt.snap.numel()
+                nodes_b, st = dt.split_host_snap(hb[off:off + sz])
+                tree = node_table_to_tree(nodes_b, st)
+                self._convert(tree)
+                self.model.trees.append(tree)
+                off += sz
+            trl = float(a[0]) / max(self.train_wsum, 1e-300)
+            tel = float(a[2]) / max(self.te_wsum, 1e-300) if has_te else None
+            self._rb_free.append(host)
+            self.round_losses[i] = (trl, tel)
+            self._log_round(i, trl, tel, current=(i + 1 == self.rounds_done))
+
+    def _log_round(self, i: int, trl: float, tel: Optional[float], current: bool):
+        if not (self.p.verbose or self.log.enabled_for_round(i)):
+            return
+        metric = getattr(self.log, "metric", None)
+        if metric is not None:
+            metric(model="gbdt", loss=self.loss.name, round=i + 1, train_loss=trl, test_loss=tel,
+                   time_stats=dict(self.timer.last) if self.timer.enabled else None)
+        out = [f"train loss = {jd(trl)}\n"]
+        if self.p.watch_train and current:
+            out.append(self._eval_str(True))
+        if tel is not None:
+            out.append(f"test loss = {jd(tel)}\n")
+            if self.p.watch_test and current:
+                out.append(self._eval_str(False))
+        cost = time.perf_counter() - getattr(self, "_train_start", time.perf_counter())
+        self.log.info(f"[model=gbdt] [loss={self.loss.name}] [iter={i + 1}]  {cost:.5f} sec elapse\n"
+                      + "".join(out))
 
     def _tree_to_dev(self, tree):
         """Bin-threshold node arrays of a host tree packed into one H2D copy."""
@@ -346,8 +433,6 @@ class GBDTTrainer:
         for tree in host_trees:
             self._convert(tree)
             self.model.trees.append(tree)
-        if dev_trees:
-            self._pending.append(dev_trees)
         acc_te = None
         if self.test_data is not None:
             if host_trees:
@@ -362,26 +447,21 @@ class GBDTTrainer:
             self.timer.mark("test_eval")
         self._acc = (acc, acc_te)
         self.rounds_done = i + 1
+        self._enqueue_readback(i, dev_trees, acc, acc_te)
 
     def _convert(self, tree: Tree):
-        if getattr(self, "_cands32", None) is None:  # float32 candidate tables, built once
-            self._cands32 = [np.asarray(c, dtype=np.float32) for c in self.mapper.cands]
-        tree.convert_split_values(self._cands32, self.p.split_type)
-        tree.add_feature_names(self.feature_names)
+        """convertModel (GBDTOptimizer.java:663-690): slot -> raw threshold, names, default
+        direction -- vectorised per tree."""
+        if getattr(self, "_cand_tab", None) is None:  # float32 candidate table, built once
+            self._cand_tab = CandTable(self.mapper.cands)
+            self._names_arr = np.asarray(self.feature_names, dtype=object)
+        tree.convert_split_values(self._cand_tab, self.p.split_type)
+        tree.add_feature_names(self._names_arr)
         tree.add_default_direction(self.missing_fill)
 
     def materialize(self):
-        """Convert pending device trees into host model trees (one bulk D2H)."""
-        if not self._pending:
-            return
-        flat = [dt for group in self._pending for dt in group]
-        nodes = torch.stack([dt.nodes for dt in flat]).cpu().numpy()
-        sts = torch.stack([dt.st for dt in flat]).cpu().numpy()
-        for dt, nd, st in zip(flat, nodes, sts):
-            tree = dt.to_tree(nd, st)
-            self._convert(tree)
-            self.model.trees.append(tree)
-        self._pending = []
+        """Land every in-flight round: device trees -> host model trees, losses -> log."""
+        self._drain(0)
 
     # ------------------------------------------------------------------ report
     def _losses(self):

@@ -26,6 +26,27 @@ LEAF_RE = re.compile(r"(\S+):leaf=([^,\s]+),hess_sum=(\S+),sample_cnt=(\S+)")
 LEAF_NOSTAT_RE = re.compile(r"(\S+):leaf=([^,\s]+)")
 
 
+class CandTable:
+    """Sorted split candidates of every feature, concatenated (float32) + offsets, for
+    vectorised slot -> threshold conversion (FeatureSplitType.java:32-78)."""
+
+    def __init__(self, cands: Sequence[np.ndarray]):
+        cands = [np.asarray(c, np.float32) for c in cands]
+        self.cat = np.concatenate(cands).astype(np.float32) if cands else np.zeros(0, np.float32)
+        self.off = np.concatenate([[0], np.cumsum([len(c) for c in cands])]).astype(np.int64)
+
+    def split_values(self, f: np.ndarray, a: np.ndarray, b: np.ndarray, split_type: str) -> np.ndarray:
+        base = self.off[f]
+        c = self.cat
+        if split_type == "mean":
+            return np.float32(0.5) * (c[base + a] + c[base + b])
+        s = a + b
+        even = (s & 1) == 0
+        lo = np.where(even, s >> 1, (s - 1) >> 1)
+        hi = np.where(even, s >> 1, (s + 1) >> 1)
+        return np.where(even, c[base + lo], np.float32(0.5) * (c[base + lo] + c[base + hi])).astype(np.float32)
+
+
 class Tree:
     def __init__(self):
         self.left: List[int] = [-1]
@@ -103,18 +124,21 @@ class Tree:
 
     def bin_arrays(self):
         """Arrays for the training scorer: go left iff bin <= floor((a+b)/2)."""
-        n = self.num_nodes
-        feat = np.array([(-1 if self.is_leaf[i] else self.feat[i]) for i in range(n)], np.int32)
-        thr = np.array([(self.slot_a[i] + self.slot_b[i]) // 2 for i in range(n)], np.int32)
-        return (feat, thr, np.array(self.left, np.int32), np.array(self.right, np.int32),
-                np.array(self.leaf, np.float32))
+        isl = np.asarray(self.is_leaf, bool)
+        feat = np.where(isl, -1, np.asarray(self.feat, np.int32)).astype(np.int32)
+        thr = ((np.asarray(self.slot_a, np.int64) + np.asarray(self.slot_b, np.int64)) // 2).astype(np.int32)
+        return (feat, thr, np.asarray(self.left, np.int32), np.asarray(self.right, np.int32),
+                np.asarray(self.leaf, np.float32))
 
     def raw_arrays(self):
-        n = self.num_nodes
-        feat = np.array([(-1 if self.is_leaf[i] else self.feat[i]) for i in range(n)], np.int32)
-        return (feat, np.array(self.cond, np.float32), np.array(self.left, np.int32),
-                np.array(self.right, np.int32), np.array(self.default_left, np.uint8),
-                np.array(self.leaf, np.float32))
+        isl = np.asarray(self.is_leaf, bool)
+        feat = np.where(isl, -1, np.asarray(self.feat, np.int32)).astype(np.int32)
+        return (feat, np.asarray(self.cond, np.float32), np.asarray(self.left, np.int32),
+                np.asarray(self.right, np.int32), np.asarray(self.default_left, np.uint8),
+                np.asarray(self.leaf, np.float32))
+
+    def _inner(self) -> np.ndarray:
+        return np.flatnonzero(~np.asarray(self.is_leaf, bool))
 
     def predict_one(self, x: Dict[str, float]) -> int:
         """Leaf index for a name->value map (missing -> default child)."""
@@ -128,26 +152,27 @@ class Tree:
         return n
 
     # -- conversions ----------------------------------------------------------
-    def convert_split_values(self, cand_sorted: Sequence[np.ndarray], split_type: str = "mean"):
-        for i in range(self.num_nodes):
-            if self.is_leaf[i]:
-                continue
-            c = cand_sorted[self.feat[i]]
-            if c.dtype != np.float32:
-                c = c.astype(np.float32)
-            a, b = self.slot_a[i], self.slot_b[i]
-            if split_type == "mean":
-                v = np.float32(0.5) * (c[a] + c[b])
-            else:
-                s = a + b
-                v = c[s // 2] if s % 2 == 0 else np.float32(0.5) * (c[(s - 1) // 2] + c[(s + 1) // 2])
-            self.cond[i] = float(np.float32(v))
+    def convert_split_values(self, cand_sorted, split_type: str = "mean"):
+        """Bin-slot interval -> raw float32 threshold for every inner node (vectorised).
+        ``cand_sorted``: a :class:`CandTable` or a per-feature list of sorted candidates."""
+        tab = cand_sorted if isinstance(cand_sorted, CandTable) else CandTable(cand_sorted)
+        inner = self._inner()
+        if inner.size:
+            f = np.asarray(self.feat, np.int64)[inner]
+            a = np.asarray(self.slot_a, np.int64)[inner]
+            b = np.asarray(self.slot_b, np.int64)[inner]
+            cond = np.asarray(self.cond, np.float64)
+            cond[inner] = tab.split_values(f, a, b, split_type)
+            self.cond = cond.tolist()
         self.converted = True
 
     def add_feature_names(self, index2name: Sequence[str]):
-        for i in range(self.num_nodes):
-            if not self.is_leaf[i]:
-                self.feat_name[i] = index2name[self.feat[i]]
+        inner = self._inner()
+        if inner.size:
+            names = index2name if isinstance(index2name, np.ndarray) else np.asarray(index2name, dtype=object)
+            fn = np.asarray(self.feat_name, dtype=object)
+            fn[inner] = names[np.asarray(self.feat, np.int64)[inner]]
+            self.feat_name = fn.tolist()
 
     def update_feature_index(self, name2index: Dict[str, int]):
         for i in range(self.num_nodes):
@@ -158,11 +183,45 @@ class Tree:
                 self.feat[i] = idx
 
     def add_default_direction(self, fill: Optional[np.ndarray]):
+        """Missing values go left iff fill < cond (Tree.java:357-375), float32 compare."""
         if fill is None or len(fill) == 0:
             return
-        for i in range(self.num_nodes):
-            if not self.is_leaf[i]:
-                self.default_left[i] = bool(np.float32(fill[self.feat[i]]) < np.float32(self.cond[i]))
+        inner = self._inner()
+        if inner.size:
+            f32 = np.asarray(fill, np.float32)
+            dl = np.asarray(self.default_left, bool)
+            dl[inner] = f32[np.asarray(self.feat, np.int64)[inner]] < np.asarray(self.cond, np.float32)[inner]
+            self.default_left = dl.tolist()
+
+    @classmethod
+    def from_arrays(cls, left, right, feat, slot_a, slot_b, leaf, is_leaf, loss_chg, hess_sum,
+                    sample_cnt) -> "Tree":
+        """Build a tree from per-node numpy arrays (node ids = array positions) without a
+        per-node Python loop. ``leaf`` values are float32; inner nodes get cond = (a+b)/2."""
+        n = len(left)
+        isl = np.asarray(is_leaf, bool)
+        left = np.where(isl, -1, np.asarray(left, np.int64))
+        right = np.where(isl, -1, np.asarray(right, np.int64))
+        parent = np.full(n, -1, np.int64)
+        inner = np.flatnonzero(~isl)
+        parent[left[inner]] = inner
+        parent[right[inner]] = inner
+        a = np.where(isl, 0, np.asarray(slot_a, np.int64))
+        b = np.where(isl, 0, np.asarray(slot_b, np.int64))
+        t = cls.__new__(cls)
+        t.left, t.right, t.parent = left.tolist(), right.tolist(), parent.tolist()
+        t.feat = np.where(isl, -1, np.asarray(feat, np.int64)).tolist()
+        t.feat_name = [None] * n
+        t.cond = (0.5 * (a + b)).tolist()
+        t.slot_a, t.slot_b = a.tolist(), b.tolist()
+        t.leaf = np.where(isl, np.asarray(leaf, np.float32), np.float32(0)).astype(np.float64).tolist()
+        t.is_leaf = isl.tolist()
+        t.default_left = [True] * n
+        t.loss_chg = np.asarray(loss_chg, np.float32).astype(np.float64).tolist()
+        t.hess_sum = np.asarray(hess_sum, np.float32).astype(np.float64).tolist()
+        t.sample_cnt = np.asarray(sample_cnt, np.int64).tolist()
+        t.converted = False
+        return t
 
     # -- text format ----------------------------------------------------------
     def dump(self, it: int, with_stats: bool = True) -> str:

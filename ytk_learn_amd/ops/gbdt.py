@@ -62,7 +62,21 @@ def quantize_gh(gh: torch.Tensor, sg: float, sh: float) -> torch.Tensor:
     return q
 
 
-def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_base=0, nslots=0, slot_ids=None):
+WIDE_LDS_BYTES = 160 * 1024  # == kWideLdsBytes in csrc/hip/gbdt_hist.hip
+
+
+def wide_group(B: int, F: int) -> int:
+    """Features per block of the wide-bin (uint16, B > 256) LDS histogram kernel; 0 when
+    one feature's B x 16-byte (g, h) planes exceed the LDS budget (mirrors
+    ytk_hist_wide_group)."""
+    per = B * 16
+    if B <= 0 or per > WIDE_LDS_BYTES:
+        return 0
+    return min(F, WIDE_LDS_BYTES // per)
+
+
+def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_base=0, nslots=0, slot_ids=None,
+               binsT=None):
     """Accumulate exact int64 fixed-point (g, h) histograms.
 
     bins: [N, S] uint8/int16 row-major (S >= F, S % 32 == 0 for the LDS path)
@@ -76,6 +90,8 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
       contiguous range [slot_base, slot_base + nslots) (two-stage flush, no per-block
       global atomics -- see csrc/hip/gbdt_hist.hip); ``slot_ids`` (int32 device tensor of
       nslots ids) replaces the contiguous range when given
+    binsT: optional column-major [F, N] copy of the bins; with uint16 bins and B > 256 it
+      feeds the wide-bin LDS kernel (feature groups per block) instead of global atomics
     """
     nwork = work.shape[0]
     if nwork == 0:
@@ -98,6 +114,11 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
             else:
                 h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                           float(sg), float(sh), 0, 0, stream(bins))
+        elif (binsT is not None and binsT.dtype == torch.int16 and bins.dtype == torch.int16
+              and wide_group(B, F) > 0 and binsT.shape[0] == F and binsT.is_contiguous()):
+            check_cuda(binsT)
+            h.hist_wide(ptr(binsT), binsT.shape[1], F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                        float(sg), float(sh), 0, 0, 0, stream(bins))
         else:
             h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                              nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
