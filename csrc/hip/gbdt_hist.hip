@@ -29,8 +29,34 @@
 namespace ytk {
 
 constexpr int kHistThreads = 1024;
+
+// Position of local feature fl (0..31) inside the 32 g (or h) words of an LDS bin row. ds_add_u64 is
+// serviced in four 16-lane groups with bank = (byte address / 4) mod 32, so a 64-bit
+// word w occupies banks 2(w mod 16), 2(w mod 16)+1. A 16-lane group updates the
+// features {4q + c0, 4q + c1 : q = 0..7}: features fl and fl + 16 would share banks
+// (2-way conflict, measured SQ_LDS_BANK_CONFLICT = 50 % of SQ_LDS_IDX_ACTIVE). Rotating
+// the upper 16 features by 2 words makes the 16 lanes hit 16 distinct bank pairs.
+// Exact float -> int64 round-half-even for the fixed-point (g, h): y = x * 2^k is an
+// exact float; rint makes it integral. On its magnitude a, hi = floor(a / 2^32) and
+// lo = a - hi * 2^32 are exact (lo < 2^32 is a multiple of ulp(a), so it has <= 24
+// significant bits) and 32-bit convertible; the sign is applied to the 64-bit value
+// ((u ^ m) - m). ~10 VALU instead of the generic __float2ll_rn sequence; bitwise equal
+// to it (and to torch.round(x * s).to(int64) on the CPU) for |y| < 2^63.
+__device__ __forceinline__ unsigned long long fx_round(float y) {
+  const float r = __builtin_rintf(y);
+  const float a = fabsf(r);
+  const float hi = floorf(a * 0x1p-32f);
+  const float lo = __builtin_fmaf(hi, -0x1p32f, a);
+  const unsigned long long u = ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+  const unsigned long long m = r < 0.f ? ~0ull : 0ull;
+  return (u ^ m) - m;
+}
+
+__device__ __forceinline__ int hist_lds_pos(int fl) {
+  return fl < 16 ? fl : 16 + ((fl - 14) & 15);
+}
 constexpr int kHistU = 8;
-constexpr int kHistUGather = 16; // gathered rows: more loads in flight per wave
+constexpr int kHistUGather = 8;  // gathered rows (pipelined: rows two steps ahead)
 
 template <bool kIdentity>
 __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
@@ -39,9 +65,9 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const int4* __restrict__ work, long long* __restrict__ hist, int B, int nb_lds,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
     long long* __restrict__ staging, const int* __restrict__ work_off_dev) {
+  // LDS bin rows of 64 words: [32 g words | 32 h words]; the h atomic of a (bin, feature)
+  // is the g address + 256 B (instruction offset), both conflict-free (hist_lds_pos)
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];
-  unsigned long long* lg = sm64;
-  unsigned long long* lh = sm64 + nb_lds * 32;
   // device-resident work count (fixed maximal grid launched by the level engine)
   // work_off_dev (optional): this launch covers work items [*work_off_dev, *nwork_dev) --
   // the second half of a level whose first half is already being all-reduced
@@ -64,33 +90,78 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   constexpr int RW = (kHistThreads / 64) * 8;  // rows per block step
   const uint8_t* bseg = bins + fg * 32 + 4 * q;
   const int fbase = fg * 32 + 4 * q;
+  // LDS word of local feature 4q + c inside a bin row (hist_lds_pos: bank-conflict-free
+  // 64-bit atomics)
+  int lpos[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) lpos[c] = hist_lds_pos(4 * q + c);
   constexpr int U = kIdentity ? kHistU : kHistUGather;
-  for (int base = w.y + wave * 8; base < w.z; base += RW * U) {
-    unsigned d[U];
-    float2 v[U];
-    bool ok[U];
+  constexpr int STEP = RW * U;
+  // Software pipeline: the bin dwords and (g, h) of step i+1 are in flight while step i
+  // is accumulated into LDS (measured: the un-pipelined loop left the kernel latency
+  // bound at ~2.2 TB/s with LDS only ~36 % busy). Gathered rows are loaded one further
+  // step ahead so the dependent bin loads of step i+1 never wait on their row ids.
+  auto load_rows = [&](int base, int (&r)[U]) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int pos = base + j * RW + wr;
+      const int p = pos < w.z ? pos : w.y;
+      r[j] = kIdentity ? p : rows[p];
+    }
+  };
+  auto load_data = [&](int base, const int (&r)[U], unsigned (&d)[U], float2 (&v)[U], bool (&ok)[U]) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const int pos = base + j * RW + wr;
       ok[j] = pos < w.z;
       const int p = ok[j] ? pos : w.y;
-      const int r = kIdentity ? p : rows[p];
-      d[j] = *reinterpret_cast<const unsigned*>(bseg + (size_t)(unsigned)r * stride);
-      v[j] = ghp[p];
+      d[j] = *reinterpret_cast<const unsigned*>(bseg + (size_t)(unsigned)r[j] * stride);
+      const float2 t = ghp[p];
+      v[j] = ok[j] ? t : make_float2(0.f, 0.f);  // rows past the end add 0
     }
+  };
+  const int base0 = w.y + wave * 8;
+  unsigned d[U];
+  float2 v[U];
+  bool ok[U];
+  int rn[U];
+  if (base0 < w.z) {
+    int r0[U];
+    load_rows(base0, r0);
+    load_data(base0, r0, d, v, ok);
+    load_rows(base0 + STEP, rn);
+  }
+  for (int base = base0; base < w.z; base += STEP) {
+    unsigned dn[U];
+    float2 vn[U];
+    bool okn[U];
+    const bool more = base + STEP < w.z;  // wave-uniform
+    if (more) {
+      load_data(base + STEP, rn, dn, vn, okn);
+      load_rows(base + 2 * STEP, rn);
+    }
+    // Branch-free inner body (the VALU, not LDS or memory, bounds this loop: measured
+    // ~60 VALU per 8-row step with a guarded body): rows past the end add 0, features
+    // >= F (bin-row padding, bin 0) land in LDS columns the flush never reads.
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      if (!ok[j]) continue;
-      const unsigned long long gi = (unsigned long long)__float2ll_rn(v[j].x * sg);
-      const unsigned long long hi = (unsigned long long)__float2ll_rn(v[j].y * sh);
+      const unsigned long long gi = fx_round(v[j].x * sg);
+      const unsigned long long hi = fx_round(v[j].y * sh);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int c = (k + wr) & 3;
-        const int bin = (d[j] >> (8 * c)) & 255;
-        if (fbase + c < F) {
-          atomicAdd(&lg[bin * 32 + 4 * q + c], gi);
-          atomicAdd(&lh[bin * 32 + 4 * q + c], hi);
-        }
+        const unsigned bin = __builtin_amdgcn_ubfe(d[j], 8 * c, 8);
+        unsigned long long* e = sm64 + (bin * 64 + lpos[c]);
+        atomicAdd(e, gi);
+        atomicAdd(e + 32, hi);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        d[j] = dn[j];
+        v[j] = vn[j];
+        ok[j] = okn[j];
       }
     }
   }
@@ -103,7 +174,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     // launch (~45 us per level at 256 blocks); stores + one ordered read are ~4x cheaper.
     const int E = nb_lds * 32;
     longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.y + fg) * E;
-    for (int i = tid; i < E; i += kHistThreads) st[i] = make_longlong2((long long)lg[i], (long long)lh[i]);
+    for (int i = tid; i < E; i += kHistThreads) {
+      const int li = 2 * (i & ~31) + hist_lds_pos(i & 31);
+      st[i] = make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
+    }
     return;
   }
   long long* out = hist + (size_t)w.x * B * F * 2;
@@ -119,7 +193,8 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     if (i >= E) continue;
     const int bin = i >> 5, l = i & 31, ff = fg * 32 + l;
     if (ff < F) {
-      const unsigned long long g = lg[i], h = lh[i];
+      const int li = 2 * (i & ~31) + hist_lds_pos(l);
+      const unsigned long long g = sm64[li], h = sm64[li + 32];
       if (g | h) {
         unsigned long long* o = reinterpret_cast<unsigned long long*>(&out[((size_t)bin * F + ff) * 2]);
         atomicAdd(o, g);
@@ -252,66 +327,78 @@ __global__ __launch_bounds__(256) void hist_fx_global_kernel(
 // GROUP of FG features (FG = floor(LDS budget / (B * 16 B)), >= 1) and reads their
 // bins from the COLUMN-major matrix binsT [F][ncol] (2 B per row per feature,
 // coalesced for the identity root, monotone row ids inside a node otherwise).
-// LDS holds interleaved exact int64 (g, h) pairs lds[(f_in_group * B + bin) * 2 + {0,1}],
+// LDS holds two exact int64 planes g[f_in_group * B + bin], h[...] (separate planes: a
+// 64-bit word index e uses bank pair e mod 16, interleaving would leave half unused),
 // accumulated with ds_add_u64 (same fixed point as hist_fx_kernel -> bitwise equal to
 // the CPU path). Block partials are flushed with global int64 atomics, zero entries
-// skipped (deep nodes touch few bins). grid = (work items, ceil(F / FG)).
-constexpr int kWideThreads = 512;
-constexpr int kWideU = 4;                    // rows in flight per thread
+// skipped (deep nodes touch few bins). grid = (ceil(F / FG), work items).
+constexpr int kWideThreads = 1024;
 constexpr int kWideLdsBytes = 160 * 1024;    // one block per CU at the widest groups
 
-template <bool kIdentity>
+// kFG features per block (power of two <= 32); every row's kFG bin loads of kU rows are
+// issued together before the LDS atomics (kU * kFG = 16 loads in flight per thread).
+template <bool kIdentity, int kFG>
 __global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
-    const uint16_t* __restrict__ binsT, long long ncol, int F, int FG,
+    const uint16_t* __restrict__ binsT, long long ncol, int F,
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
     const int* __restrict__ work_off_dev) {
+  constexpr int kU = kFG >= 16 ? 1 : 16 / kFG;
   extern __shared__ __attribute__((aligned(16))) unsigned long long wl[];
-  const int bx = (int)blockIdx.x + (work_off_dev ? *work_off_dev : 0);
+  // grid = (feature groups, work items): the groups of one item are dispatched together,
+  // so the (g, h) and row-id lines they all read are shared on chip
+  const int bx = (int)blockIdx.y + (work_off_dev ? *work_off_dev : 0);
   if (nwork_dev && bx >= *nwork_dev) return;
   if (scales_dev) {
     sg = scales_dev[0];
     sh = scales_dev[1];
   }
   const int4 w = work[bx];
-  const int f_lo = (int)blockIdx.y * FG;
-  const int nf = min(FG, F - f_lo);
+  const int f_lo = (int)blockIdx.x * kFG;
+  const int nf = min(kFG, F - f_lo);
   const int tid = threadIdx.x;
   const int E = nf * B;
   for (int i = tid; i < 2 * E; i += kWideThreads) wl[i] = 0ull;
   __syncthreads();
   const uint16_t* col = binsT + (size_t)f_lo * ncol;
-  for (int base = w.y + tid; base < w.z; base += kWideThreads * kWideU) {
-    int r[kWideU];
-    float2 v[kWideU];
-    bool ok[kWideU];
+  for (int base = w.y + tid; base < w.z; base += kWideThreads * kU) {
+    int r[kU];
+    float2 v[kU];
+    bool ok[kU];
 #pragma unroll
-    for (int j = 0; j < kWideU; ++j) {
+    for (int j = 0; j < kU; ++j) {
       const int pos = base + j * kWideThreads;
       ok[j] = pos < w.z;
       const int p = ok[j] ? pos : w.y;
       r[j] = kIdentity ? p : rows[p];
-      v[j] = ghp[p];
+      const float2 t = ghp[p];
+      v[j] = ok[j] ? t : make_float2(0.f, 0.f);  // rows past the end add 0
+    }
+    int bn[kU][kFG];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const uint16_t* c = col + (size_t)(unsigned)r[j];
+#pragma unroll
+      for (int fi = 0; fi < kFG; ++fi) bn[j][fi] = (fi < nf) ? (int)c[(size_t)fi * ncol] : 0;
     }
 #pragma unroll
-    for (int j = 0; j < kWideU; ++j) {
-      if (!ok[j]) continue;
-      const unsigned long long gi = (unsigned long long)__float2ll_rn(v[j].x * sg);
-      const unsigned long long hi = (unsigned long long)__float2ll_rn(v[j].y * sh);
-      const uint16_t* c = col + (size_t)(unsigned)r[j];
-      for (int fi = 0; fi < nf; ++fi) {
-        const int bin = c[(size_t)fi * ncol];
-        unsigned long long* e = &wl[(size_t)(fi * B + bin) * 2];
-        atomicAdd(e, gi);
-        atomicAdd(e + 1, hi);
+    for (int j = 0; j < kU; ++j) {
+      const unsigned long long gi = fx_round(v[j].x * sg);
+      const unsigned long long hi = fx_round(v[j].y * sh);
+#pragma unroll
+      for (int fi = 0; fi < kFG; ++fi) {
+        if (fi >= nf) break;
+        const int e = fi * B + bn[j][fi];
+        atomicAdd(&wl[e], gi);
+        atomicAdd(&wl[E + e], hi);
       }
     }
   }
   __syncthreads();
   long long* out = hist + (size_t)w.x * B * F * 2;
   for (int i = tid; i < E; i += kWideThreads) {
-    const unsigned long long g = wl[2 * i], h = wl[2 * i + 1];
+    const unsigned long long g = wl[i], h = wl[E + i];
     if (g | h) {
       const int fi = i / B, bin = i - fi * B;
       unsigned long long* o = reinterpret_cast<unsigned long long*>(&out[((size_t)bin * F + f_lo + fi) * 2]);
@@ -418,28 +505,42 @@ int ytk_hist_wide(uintptr_t binsT, long long ncol, int F, uintptr_t ghp, uintptr
   if (FG <= 0) throw std::invalid_argument("hist_wide: one feature's bins exceed the LDS budget");
   if (nwork <= 0) return FG;
   const size_t lds = (size_t)FG * B * 2 * sizeof(unsigned long long);
-  dim3 grid(nwork, (F + FG - 1) / FG);
+  dim3 grid((F + FG - 1) / FG, nwork);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (rows == 0) {
-    hipLaunchKernelGGL(hist_wide_kernel<true>, grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT,
-                       ncol, F, FG, (const float2*)ghp, (const int*)nullptr, (const int4*)work,
-                       (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,
-                       (const int*)work_off_dev);
-  } else {
-    hipLaunchKernelGGL(hist_wide_kernel<false>, grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT,
-                       ncol, F, FG, (const float2*)ghp, (const int*)rows, (const int4*)work,
-                       (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,
-                       (const int*)work_off_dev);
+#define YTK_WIDE(ID, G)                                                                              \
+  hipLaunchKernelGGL((hist_wide_kernel<ID, G>), grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT, \
+                     ncol, F, (const float2*)ghp, (const int*)(ID ? 0 : rows), (const int4*)work,     \
+                     (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,    \
+                     (const int*)work_off_dev)
+#define YTK_WIDE_G(ID)                  \
+  switch (FG) {                         \
+    case 1: YTK_WIDE(ID, 1); break;     \
+    case 2: YTK_WIDE(ID, 2); break;     \
+    case 4: YTK_WIDE(ID, 4); break;     \
+    case 8: YTK_WIDE(ID, 8); break;     \
+    case 16: YTK_WIDE(ID, 16); break;   \
+    default: YTK_WIDE(ID, 32); break;   \
   }
+  if (rows == 0) {
+    YTK_WIDE_G(true)
+  } else {
+    YTK_WIDE_G(false)
+  }
+#undef YTK_WIDE_G
+#undef YTK_WIDE
   YTK_LAUNCH_CHECK();
   return FG;
 }
 
-// Features per block of hist_wide_kernel (0: a single feature does not fit).
+// Features per block of hist_wide_kernel: the largest power of two <= 32 whose (g, h)
+// planes fit the LDS budget (0: a single feature does not fit).
 int ytk_hist_wide_group(int B, int F) {
   const long long per = (long long)B * 16;
   if (B <= 0 || per > kWideLdsBytes) return 0;
-  return (int)std::min<long long>(F, kWideLdsBytes / per);
+  const long long fit = std::min<long long>(32, kWideLdsBytes / per);
+  int g = 1;
+  while (2 * g <= fit) g *= 2;
+  return g;
 }
 
 }  // extern "C"

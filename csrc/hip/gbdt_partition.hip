@@ -23,6 +23,7 @@ namespace ytk {
 
 constexpr int kPartThreads = 256;
 constexpr int kPartSub = 4;
+constexpr int kPartGrid = 256 * 8;  // persistent partition blocks: 8 per CU
 constexpr int kAtomSub = 8;  // single-pass partition: rows per block = 8 x 256 (one chunk)
 
 template <typename BinT>
@@ -183,80 +184,104 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
   constexpr int NW = kPartThreads / kWave;
   constexpr int S = kAtomSub;
   constexpr int CH = kAtomSub * kPartThreads;
-  __shared__ int s_l[S * NW], s_v[S * NW];
+  constexpr int kSplitLds = 1024;  // splits whose chunk table is staged in LDS
+  __shared__ int s_l[S * NW];
+  __shared__ int s_first[kSplitLds];
   __shared__ unsigned long long s_base;
-  const int bid = (int)blockIdx.x;
-  if (bid >= *nblocks_dev) return;
-  int lo = 0, hi = *nsplit_dev - 1;  // last split with first_blk <= bid
+  __shared__ int s_tl;
+  const int nblocks = *nblocks_dev, nsplit = *nsplit_dev;
+  if ((int)blockIdx.x >= nblocks) return;
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+  // Persistent blocks: the grid is capped (kPartGrid) and each block walks chunks
+  // bid, bid + gridDim.x, ... Measured: with one short-lived 4-wave block per 2048-row
+  // chunk (~5k blocks per level) the workgroup launch rate, not memory, set the time
+  // (~4 us wave lifetime, < 1/8 of the wave slots ever occupied).
+  // The chunk table is staged in LDS once per block, so locating a chunk's split costs
+  // no dependent global round trips.
+  const bool lds_tab = nsplit <= kSplitLds;
+  if (lds_tab) {
+    for (int i = tid; i < nsplit; i += kPartThreads) s_first[i] = first_blk[i];
+    __syncthreads();
+  }
+  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  for (int bid = (int)blockIdx.x; bid < nblocks; bid += (int)gridDim.x) {
+  int lo = 0, hi = nsplit - 1;  // last split with first_blk <= bid
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (first_blk[mid] <= bid) lo = mid; else hi = mid - 1;
+    if ((lds_tab ? s_first[mid] : first_blk[mid]) <= bid) lo = mid; else hi = mid - 1;
   }
   const int si = lo;
-  int4 it;
-  it.y = node_begin[si] + (bid - first_blk[si]) * CH;
-  it.z = min(it.y + CH, node_begin[si] + node_count[si]);
-  const BinT* col = binsT + (size_t)feat[si] * ncol;
-  const int th = thr[si];
-  const int nbeg = node_begin[si], nend = nbeg + node_count[si];
-  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
-  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  // independent loads of the split's parameters (one round trip)
+  const int fb = first_blk[si], nbeg = node_begin[si], ncnt = node_count[si], fs = feat[si], th = thr[si];
+  const int beg = nbeg + (bid - fb) * CH;
+  const int end = min(beg + CH, nbeg + ncnt);
+  const int nend = nbeg + ncnt;
+  const BinT* col = binsT + (size_t)fs * ncol;
+  // valid rows form a prefix of the chunk in position order: the rank of a valid row
+  // among the chunk's rows is simply j * 256 + tid (no ballot needed)
   int r[S];
   float2 g[S];
-  bool valid[S], left[S];
+  bool left[S];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
-    const int pos = it.y + j * kPartThreads + tid;
-    valid[j] = pos < it.z;
-    r[j] = valid[j] ? (rows ? rows[pos] : pos) : 0;
+    const int pos = beg + j * kPartThreads + tid;
+    r[j] = pos < end ? (rows ? rows[pos] : pos) : 0;
   }
 #pragma unroll
   for (int j = 0; j < S; ++j) {
-    const int pos = it.y + j * kPartThreads + tid;
-    g[j] = (kScatter && valid[j]) ? ghp[pos] : make_float2(0.f, 0.f);
-    left[j] = valid[j] && (int)col[(unsigned)r[j]] <= th;
+    const int pos = beg + j * kPartThreads + tid;
+    const bool valid = pos < end;
+    g[j] = (kScatter && valid) ? ghp[pos] : make_float2(0.f, 0.f);
+    left[j] = valid && (int)col[(unsigned)r[j]] <= th;
   }
-  int lrank[S], vrank[S];
+  int lrank[S];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const unsigned long long lm = __ballot(left[j]);
-    const unsigned long long vm = __ballot(valid[j]);
     lrank[j] = __popcll(lm & lt_mask);
-    vrank[j] = __popcll(vm & lt_mask);
-    if (l == 0) { s_l[j * NW + wid] = __popcll(lm); s_v[j * NW + wid] = __popcll(vm); }
+    if (l == 0) s_l[j * NW + wid] = __popcll(lm);
   }
   __syncthreads();
-  int tl = 0, tv = 0;
-  int pl[S], pv[S];
+  // exclusive scan of the S * NW (= 32) per-(sub-chunk, wave) left counts by wave 0
+  if (wid == 0) {
+    const int x = l < S * NW ? s_l[l] : 0;
+    int incl = x;
 #pragma unroll
-  for (int j = 0; j < S; ++j) { pl[j] = 0; pv[j] = 0; }
-#pragma unroll
-  for (int k = 0; k < S * NW; ++k) {
-    const int kl = s_l[k], kv = s_v[k];
+    for (int off = 1; off < S * NW; off <<= 1) {
+      const int y = __shfl_up(incl, off, kWave);
+      if (l >= off) incl += y;
+    }
+    if (l < S * NW) s_l[l] = incl - x;
+    const int tl_all = __shfl(incl, S * NW - 1, kWave);
+    if (l == 0) {
+      const int tv = end - beg;
+      if (!kScatter) {
+        atomicAdd(&cursor[si], (unsigned long long)tl_all);  // count-only: the left rows
+      } else {
+        s_base = atomicAdd(&cursor[si], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
+        s_tl = tl_all;
+      }
+    }
+  }
+  __syncthreads();
+  if (kScatter) {
+    const int tl = s_tl;
+    const int tv = end - beg;
+    const unsigned long long base = s_base;
+    const int lofs = (int)(base & 0xffffffffull), rofs = (int)(base >> 32);
+    const int rstart = nend - rofs - (tv - tl);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      if (k < j * NW + wid) { pl[j] += kl; pv[j] += kv; }
+      const int rank = j * kPartThreads + tid;  // rank among the chunk's rows
+      if (rank < tv) {
+        const int lb = s_l[j * NW + wid] + lrank[j];  // left rows before this one
+        const int dst = left[j] ? nbeg + lofs + lb : rstart + (rank - lb);
+        rows_out[dst] = r[j];
+        gh_out[dst] = g[j];
+      }
     }
-    tl += kl;
-    tv += kv;
   }
-  if (!kScatter) {  // count-only: the left rows of this chunk
-    if (tid == 0) atomicAdd(&cursor[si], (unsigned long long)tl);
-    return;
-  }
-  if (tid == 0)
-    s_base = atomicAdd(&cursor[si], ((unsigned long long)(tv - tl) << 32) | (unsigned long long)tl);
-  __syncthreads();
-  const int lofs = (int)(s_base & 0xffffffffull), rofs = (int)(s_base >> 32);
-  const int rstart = nend - rofs - (tv - tl);
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    if (valid[j]) {
-      const int dst = left[j] ? nbeg + lofs + pl[j] + lrank[j]
-                              : rstart + (pv[j] - pl[j]) + (vrank[j] - lrank[j]);
-      rows_out[dst] = r[j];
-      gh_out[dst] = g[j];
-    }
+  __syncthreads();  // s_l / s_base / s_tl are reused by the next chunk
   }
 }
 
@@ -394,7 +419,7 @@ extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long n
   if (max_blocks <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define YTK_PART_ATOMIC(BT, SC)                                                                   \
-  hipLaunchKernelGGL((partition_atomic_kernel<BT, SC>), dim3(max_blocks), dim3(kPartThreads), 0, s, \
+  hipLaunchKernelGGL((partition_atomic_kernel<BT, SC>), dim3(std::min(max_blocks, kPartGrid)), dim3(kPartThreads), 0, s, \
                      (const BT*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,  \
                      (float2*)gh_out, (const int*)first_blk, (const int*)nsplit_dev,               \
                      (const int*)nblocks_dev, (const int*)feat, (const int*)thr,                   \

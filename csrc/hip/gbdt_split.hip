@@ -281,6 +281,11 @@ struct ScanOp {
 constexpr int kFeatThreads = 256;
 using FeatScan = rocprim::block_scan<ScanT, kFeatThreads>;
 
+// kR bins per thread: thread t owns the contiguous bins [t * kR, t * kR + kR) so one
+// block covers B <= 256 * kR (kR > 1: the wide-bin configs). The exclusive block scan
+// of the per-thread run totals gives each run its left prefix; the run is then walked
+// bin by bin exactly like the wave kernel (same gain, same tie-break).
+template <int kR>
 __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
@@ -317,15 +322,30 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   };
   const int nb = nbins_f[f], nb0 = nbins_f[f0];
   const bool on = fmask[f] != 0;
-  // ---- one load round trip
-  longlong2 v = make_longlong2(0, 0), v0 = make_longlong2(0, 0);
-  if (t < B && (derived || (on && t < nb))) v = load(f, t);
-  if (f != f0 && t < nb0) v0 = load(f0, t);
-  if (derived && t < B) hn[(size_t)t * F + f] = v;  // materialise the derived histogram
-  if (f == f0) v0 = (t < nb0) ? v : make_longlong2(0, 0);
+  const int b0 = t * kR;
+  // ---- one load round trip (this feature's run + the node-total feature's run)
+  longlong2 v[kR], v0[kR];
+#pragma unroll
+  for (int k = 0; k < kR; ++k) {
+    const int bin = b0 + k;
+    v[k] = make_longlong2(0, 0);
+    v0[k] = make_longlong2(0, 0);
+    if (bin < B && (derived || (on && bin < nb))) v[k] = load(f, bin);
+    if (f != f0 && bin < nb0) v0[k] = load(f0, bin);
+  }
+#pragma unroll
+  for (int k = 0; k < kR; ++k) {
+    const int bin = b0 + k;
+    if (derived && bin < B) hn[(size_t)bin * F + f] = v[k];  // materialise the derived histogram
+    if (f == f0) v0[k] = (bin < nb0) ? v[k] : make_longlong2(0, 0);
+  }
   // ---- node totals (exact int64, first sampled feature: DataParallelTreeMaker:543-573)
   {
-    const long long sg = wave_sum_ll(v0.x), sh = wave_sum_ll(v0.y);
+    long long sg = 0, sh = 0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) { sg += v0[k].x; sh += v0[k].y; }
+    sg = wave_sum_ll(sg);
+    sh = wave_sum_ll(sh);
     if (l == 0) { s_tg[wid] = sg; s_th[wid] = sh; }
   }
   __syncthreads();
@@ -338,21 +358,41 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   int best_b = 0x7fffffff, best_a = -1;
   double best_gl = 0.0, best_hl = 0.0;
   if (on) {  // block-uniform
-    if (t >= nb) v = make_longlong2(0, 0);
-    const bool ne = (v.x != 0 || v.y != 0);
+    long long rg = 0, rh = 0;
+    int rlast = -1;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      if (b0 + k >= nb) v[k] = make_longlong2(0, 0);
+      rg += v[k].x;
+      rh += v[k].y;
+      if (v[k].x != 0 || v[k].y != 0) rlast = b0 + k;
+    }
     ScanT ex;
-    FeatScan().exclusive_scan(ScanT{v.x, v.y, ne ? t : -1}, ex, ScanT{0, 0, -1}, s_scan, ScanOp());
-    if (ne && ex.last >= 0 && ex.h != 0) {
-      const double dgl = (double)ex.g * gp.inv_sg, dhl = (double)ex.h * gp.inv_sh;
-      const double dgr = (double)(Gq - ex.g) * gp.inv_sg, dhr = (double)(Hq - ex.h) * gp.inv_sh;
-      if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
-        const float root_gain = (float)calc_gain(G, H, gp);
-        best_chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
-        best_b = t;
-        best_a = ex.last;
-        best_gl = dgl;
-        best_hl = dhl;
+    FeatScan().exclusive_scan(ScanT{rg, rh, rlast}, ex, ScanT{0, 0, -1}, s_scan, ScanOp());
+    const float root_gain = (float)calc_gain(G, H, gp);
+    long long pg = ex.g, ph = ex.h;
+    int prev = ex.last;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const bool ne = (v[k].x != 0 || v[k].y != 0);
+      if (!ne) continue;
+      if (prev >= 0 && ph != 0) {
+        const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
+        const double dgr = (double)(Gq - pg) * gp.inv_sg, dhr = (double)(Hq - ph) * gp.inv_sh;
+        if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
+          const float chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
+          if (better(chg, 0, b0 + k, best_chg, 0, best_b)) {
+            best_chg = chg;
+            best_b = b0 + k;
+            best_a = prev;
+            best_gl = dgl;
+            best_hl = dhl;
+          }
+        }
       }
+      pg += v[k].x;
+      ph += v[k].y;
+      prev = b0 + k;
     }
   }
   // ---- block argmax (chg desc, bin asc)
@@ -475,13 +515,21 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
     YTK_LAUNCH_CHECK();
     return;
   }
-  if (B <= kFeatThreads && part && counters) {
+  if (B <= 32 * kFeatThreads && part && counters) {
     // part: >= nitems * F SplitOut; counters: nitems zeroed ints
-    hipLaunchKernelGGL(split_feat_kernel, dim3(nitems, F), dim3(kFeatThreads), 0,
-                       reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,
-                       (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,
-                       (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev,
-                       (SplitOut*)part, (int*)counters);
+#define YTK_SPLIT_FEAT(R)                                                                          \
+  hipLaunchKernelGGL(split_feat_kernel<R>, dim3(nitems, F), dim3(kFeatThreads), 0,                 \
+                     reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,                \
+                     (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,           \
+                     (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev,           \
+                     (SplitOut*)part, (int*)counters)
+    if (B <= kFeatThreads) YTK_SPLIT_FEAT(1);
+    else if (B <= 2 * kFeatThreads) YTK_SPLIT_FEAT(2);
+    else if (B <= 4 * kFeatThreads) YTK_SPLIT_FEAT(4);
+    else if (B <= 8 * kFeatThreads) YTK_SPLIT_FEAT(8);
+    else if (B <= 16 * kFeatThreads) YTK_SPLIT_FEAT(16);
+    else YTK_SPLIT_FEAT(32);
+#undef YTK_SPLIT_FEAT
     YTK_LAUNCH_CHECK();
     return;
   }

@@ -80,9 +80,10 @@ def _hist_from(N, F, nb, B, seed):
     return h[0]
 
 
-@pytest.mark.parametrize("l1,l2,mal", [(0.0, 0.0, -1.0), (0.5, 1.0, -1.0), (0.0, 1.0, 0.3)])
-def test_split_find_matches_cpu(cuda, l1, l2, mal):
-    F, nb, B = 28, 200, 200
+@pytest.mark.parametrize("l1,l2,mal,nb", [(0.0, 0.0, -1.0, 200), (0.5, 1.0, -1.0, 200), (0.0, 1.0, 0.3, 200),
+                                         (0.0, 0.0, -1.0, 600), (0.5, 1.0, -1.0, 5000), (0.0, 0.0, -1.0, 9000)])
+def test_split_find_matches_cpu(cuda, l1, l2, mal, nb):
+    F, B = 28, nb
     parent = _hist_from(40000, F, nb, B, 5)
     small = _hist_from(15000, F, nb, B, 6)
     hist = torch.zeros((4, B, F, 2), dtype=torch.int64)

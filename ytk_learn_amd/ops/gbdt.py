@@ -66,13 +66,18 @@ WIDE_LDS_BYTES = 160 * 1024  # == kWideLdsBytes in csrc/hip/gbdt_hist.hip
 
 
 def wide_group(B: int, F: int) -> int:
-    """Features per block of the wide-bin (uint16, B > 256) LDS histogram kernel; 0 when
+    """Features per block (a power of two <= 32) of the wide-bin (uint16, B > 256) LDS
+    histogram kernel; 0 when
     one feature's B x 16-byte (g, h) planes exceed the LDS budget (mirrors
     ytk_hist_wide_group)."""
     per = B * 16
     if B <= 0 or per > WIDE_LDS_BYTES:
         return 0
-    return min(F, WIDE_LDS_BYTES // per)
+    fit = min(32, WIDE_LDS_BYTES // per)
+    g = 1
+    while 2 * g <= fit:
+        g *= 2
+    return g
 
 
 def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_base=0, nslots=0, slot_ids=None,
