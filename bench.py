@@ -58,6 +58,7 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    comm.reset_stats()
     t0 = time.perf_counter()
     for i in range(warmup, warmup + steps):
         tr.run_round(i)
@@ -66,7 +67,10 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
         torch.cuda.synchronize(dev)
     comm.barrier()
     el = time.perf_counter() - t0
-    return comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+    timed_stats = dict(comm.stats)
+    el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
+    comm.stats = timed_stats  # the timed rounds' collectives only
+    return el
 
 
 def main():
@@ -133,8 +137,10 @@ def main():
     auc = tr.eval_test.evals[0].compute(yt, tr.te_pred, None, comm)[0]
     train_loss, test_loss = tr.round_losses[total_rounds - 1]
     sec_per_tree = el_max / a.steps
+    coll = dict(comm.stats)
     if a.profile and rank == 0:
         print(tr.timer.report() if tr.use_device_builder else tr.builder.total_stats, file=sys.stderr)
+    tr_builder = tr.builder
     leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else (10 if world == 1 else 0)
     leaf = None
     if leaf_steps > 0 and a.policy == "level":
@@ -178,6 +184,9 @@ def main():
             "prep_s": round(prep_s, 3),
             "datagen_s": round(gen_s, 3),
             "timed_region": "step + convertModel + per-round loss readback (pipelined), all trees landed",
+            "collectives_per_tree": round(coll["calls"] / a.steps, 2),
+            "collective_bytes_per_tree": int(coll["bytes"] / a.steps),
+            "hist_sync": ("owner" if getattr(tr_builder, "owner", False) else "allreduce") if world > 1 else "none",
             "trees_converted": total_rounds,
         }
         if leaf is not None:

@@ -24,6 +24,7 @@ int ytk_hist_wide_group(int, int);
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
                     uintptr_t, uintptr_t);
+void ytk_split_combine(uintptr_t, int, int, uintptr_t, int, int, uintptr_t, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition_atomic(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                           uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -85,6 +86,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_wide", &ytk_hist_wide);
   m.def("hist_wide_group", &ytk_hist_wide_group);
   m.def("split_find", &ytk_split_find);
+  m.def("split_combine", &ytk_split_combine);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
   m.def("segment_copy", &ytk_segment_copy);

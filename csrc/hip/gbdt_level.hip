@@ -17,17 +17,9 @@
 // synchronisation inside a tree, and multi-GPU all-reduces are fixed-size RCCL calls
 // on the same stream.
 #include "common.h"
+#include "gbdt_split_node.h"  // SplitOut (one definition, layout static_assert'ed there)
 
 namespace ytk {
-
-struct SplitOut {
-  float loss_chg;
-  int feat;
-  int bin_a;
-  int bin_b;
-  double gl, hl;
-  double g, h;
-};
 
 struct DNode {
   double G, H;           // node sums

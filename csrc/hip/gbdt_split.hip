@@ -487,6 +487,30 @@ __global__ __launch_bounds__(kNodeThreads) void split_node_kernel(
 
 using namespace ytk;
 
+// Owner-computes combine (multi-GPU, hist_sync = owner): every rank searched only the
+// features it owns; ``all`` holds the P ranks' records ([P][cap]) after an allgather.
+// The global best per item uses the kernels' own total order (better(): larger lossChg,
+// then lower feature, then lower bin -- SplitInfo.needReplace), so the result is the
+// record the all-reduce mode finds; node totals (g, h) come from rank ``tot_rank``, the
+// first rank owning a sampled feature (exact int64 sums: equal for every feature).
+__global__ __launch_bounds__(256) void split_combine_kernel(const SplitOut* __restrict__ all, int P, int cap,
+                                                            const int* __restrict__ n_dev, int n_max,
+                                                            int tot_rank, SplitOut* __restrict__ out) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int n = n_dev ? min(*n_dev, n_max) : n_max;
+  if (i >= n) return;
+  auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
+  SplitOut best = all[i];
+  for (int r = 1; r < P; ++r) {
+    const SplitOut c = all[(size_t)r * cap + i];
+    if (better(c.loss_chg, fkey(c.feat), fkey(c.bin_b), best.loss_chg, fkey(best.feat), fkey(best.bin_b))) best = c;
+  }
+  const SplitOut t = all[(size_t)tot_rank * cap + i];
+  best.g = t.g;
+  best.h = t.h;
+  out[i] = best;
+}
+
 // "0" in the environment variable disables an optional kernel path (read once per process)
 static bool getenv_flag_off(const char* name) {
   const char* v = getenv(name);
@@ -496,6 +520,15 @@ static bool getenv_flag_off(const char* name) {
 // part / counters (optional): scratch of nitems * F SplitOut and nitems zeroed ints. With
 // them and B <= 256 the (node, feature)-parallel kernel runs; otherwise the wave-per-
 // feature kernel (features spread over ceil(F/32) blocks when the scratch is given).
+extern "C" void ytk_split_combine(uintptr_t all, int P, int cap, uintptr_t n_dev, int n_max, int tot_rank,
+                                  uintptr_t out, uintptr_t stream) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(split_combine_kernel, dim3((n_max + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const SplitOut*)all, P, cap, (const int*)n_dev,
+                     n_max, tot_rank, (SplitOut*)out);
+  YTK_LAUNCH_CHECK();
+}
+
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,
                                int f0, uintptr_t items, int nitems, uintptr_t out, float mcw,
                                float l1, float l2, float max_abs_leaf, double inv_sg,

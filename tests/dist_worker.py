@@ -36,17 +36,19 @@ def run_gbdt(comm, out, device, policy):
     X, y = gbdt_data(20000, 10, 7, comm.rank, comm.world, device)
     Xt, yt = gbdt_data(4000, 10, 8, comm.rank, comm.world, device)
     tp = TreeParams(max_depth=5 if policy == "level" else -1, max_leaf_cnt=32 if policy == "level" else 20,
-                    min_child_hessian_sum=1.0, learning_rate=0.2, l2=1.0, grow_policy=policy)
+                    min_child_hessian_sum=1.0, learning_rate=0.2, l2=1.0, grow_policy=policy,
+                    feature_sample_rate=float(os.environ.get("YTK_TEST_FSAMPLE", "1.0")))
     p = GBDTParams(round_num=6, loss_function="sigmoid", missing_value="value@0",
                    approximate=[{"cols": "default", "type": "sample_by_quantile", "max_cnt": 255}], tree=tp)
     tr = GBDTTrainer(p, GBDTData(X, y), GBDTData(Xt, yt), comm=comm)
     model = tr.train()
     tl, te = tr._losses()
+    owner = bool(getattr(tr.builder, "owner", False))
     if comm.rank == 0:
         with open(os.path.join(out, "model.txt"), "w") as f:
             f.write(model.dumps())
         with open(os.path.join(out, "res.json"), "w") as f:
-            json.dump({"train_loss": tl, "test_loss": te}, f)
+            json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats}, f)
 
 
 def write_lines(path, n, seed):

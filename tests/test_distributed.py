@@ -62,27 +62,47 @@ def test_gbdt_world2_identical_to_world1(tmp_path, task):
     np.testing.assert_allclose(r2["test_loss"], r1["test_loss"], rtol=1e-9)
 
 
-@pytest.mark.parametrize("task", ["linear", "gbmlr"])
-def test_lbfgs_world2_matches_world1(tmp_path, task):
+@pytest.mark.parametrize("task,world,mode,fs", [
+    ("gbdt", 2, "owner", "1.0"), ("gbdt", 4, "owner", "0.6"), ("gbdt", 8, "owner", "1.0"),
+    ("gbdt", 8, "allreduce", "0.6"), ("gbdt_loss", 4, "owner", "1.0"), ("gbdt_loss", 8, "allreduce", "1.0"),
+    ("gbdt_loss", 8, "owner", "0.6")])
+def test_gbdt_world_n_both_sync_modes(tmp_path, task, world, mode, fs):
+    """World 2/4/8 (gloo, CPU) == world 1 byte for byte, with the histogram all-reduce
+    and with owner-computes (reduce-scatter by feature block + allgather of split records;
+    with 10 features and 8 ranks some ranks own one feature, with feature sampling some
+    own no sampled feature at all)."""
+    env = {"YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": fs}
+    _run(task, tmp_path / "w1", 1, extra_env=env)
+    r = _run(task, tmp_path / f"w{world}", world, extra_env=env)
+    assert r["owner"] == (mode == "owner")
+    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
+
+
+@pytest.mark.parametrize("task,world", [("linear", 2), ("gbmlr", 2), ("linear", 8), ("gbmlr", 4)])
+def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
     r1 = _run(task, tmp_path / "w1", 1)
-    r2 = _run(task, tmp_path / "w2", 2)
+    r2 = _run(task, tmp_path / f"w{world}", world)
     np.testing.assert_allclose(r2["loss"], r1["loss"], rtol=1e-4)
     np.testing.assert_allclose(r2["test_loss"], r1["test_loss"], rtol=1e-3)
     if task == "linear":
-        parts = os.listdir(tmp_path / "w2" / "linear_w2.model")
-        assert sorted(parts) == ["model-00000", "model-00001"]  # each rank dumps its feature range
+        parts = os.listdir(tmp_path / f"w{world}" / f"linear_w{world}.model")
+        assert sorted(parts) == [f"model-{r:05d}" for r in range(world)]  # each rank dumps its feature range
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("task,world", [("gbdt", 2), ("gbdt", 4), ("gbdt_loss", 3)])
-def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world):
+@pytest.mark.parametrize("task,world,mode", [("gbdt", 2, "allreduce"), ("gbdt", 4, "allreduce"),
+                                             ("gbdt_loss", 3, "allreduce"), ("gbdt", 3, "owner"),
+                                             ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner")])
+def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
-    overlapped half-level all-reduce, global gradient bound) and the leaf-wise speculative
-    builder (scattered slot all-reduce) must give the world-1 model byte for byte."""
+    overlapped half-level all-reduce, global gradient bound; or owner-computes:
+    reduce-scatter by feature block + device split-record argmax) and the leaf-wise
+    speculative builder (scattered slot all-reduce / reduce-scatter) must give the world-1
+    model byte for byte."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_DIST_BACKEND": "gloo"}
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0"}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
@@ -96,3 +116,22 @@ def test_sgd_world2_model_averaging(tmp_path, task):
     r2 = _run(task, tmp_path / "w2", 2)
     assert r2["test_loss"] < 0.6 and r1["test_loss"] < 0.6
     assert abs(r2["test_loss"] - r1["test_loss"]) < 0.1
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "owner"])
+def test_bench_under_torchrun_world2(tmp_path, mode):
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run, one JSON line from
+    rank 0, max-over-ranks time, per-tree collective accounting)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", YTK_HIST_SYNC=mode)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--device", "cpu", "--train-rows", "8000", "--test-rows", "1000",
+           "--depth", "3", "--quiet"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["steps"] == 2
+    assert res["collectives_per_tree"] > 0 and res["collective_bytes_per_tree"] > 0
+    assert res["hist_sync"] == mode and res["trees_converted"] == 3

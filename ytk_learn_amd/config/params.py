@@ -403,7 +403,10 @@ def gbdt_params_from_config(c: Config):
                     min_split_samples=min_split_samples, learning_rate=lr, l1=l1, l2=l2, grow_policy=policy,
                     instance_sample_rate=c.get_double(k + "instance_sample_rate"),
                     feature_sample_rate=c.get_double(k + "feature_sample_rate"),
-                    seed=c.get_int(k + "seed", 2018))
+                    seed=c.get_int(k + "seed", 2018),
+                    hist_sync=str(c.get_string(k + "hist_sync", "auto")).lower())
+    check(tp.hist_sync in ("auto", "allreduce", "owner"), "[GBDT] hist_sync (%s) invalid: auto, allreduce or owner",
+          tp.hist_sync)
     f = "feature."
     approx = c.get_list(f + "approximate", [{"cols": "default", "type": "no_sample"}])
     gp = GBDTParams(round_num=round_num, loss_function=objective, class_num=class_num, type=learn_type,

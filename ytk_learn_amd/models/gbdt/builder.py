@@ -56,11 +56,31 @@ class TreeParams:
     instance_sample_rate: float = 1.0
     feature_sample_rate: float = 1.0
     seed: int = 2018
+    # multi-GPU histogram synchronisation: "allreduce" (every rank gets every global
+    # histogram and searches all features), "owner" (reduce-scatter by feature block,
+    # owner-computes split search, allgather of 48-B split records + deterministic argmax:
+    # HistogramBuilder.java:95, DataParallelTreeMaker.java:575-653) or "auto" (owner when
+    # a level's histogram slab is large, where halving the bytes pays for the extra
+    # small collective)
+    hist_sync: str = "auto"
 
     def gain_params(self):
         f = lambda v: float(np.float32(v))  # kernel receives float32 params
         return {"mcw": f(self.min_child_hessian_sum), "l1": f(self.l1), "l2": f(self.l2),
                 "max_abs_leaf": f(self.max_abs_leaf_val)}
+
+
+OWNER_MIN_SLOT_BYTES = 1 << 20  # "auto": owner-computes once one node histogram is >= 1 MiB
+
+
+def resolve_hist_sync(mode: str, slot_bytes: int) -> str:
+    """Effective multi-GPU histogram sync mode (env YTK_HIST_SYNC overrides the config)."""
+    mode = os.environ.get("YTK_HIST_SYNC", mode or "auto").lower()
+    if mode == "auto":
+        return "owner" if slot_bytes >= OWNER_MIN_SLOT_BYTES else "allreduce"
+    if mode not in ("allreduce", "owner"):
+        raise ValueError(f"hist_sync must be auto, allreduce or owner, got {mode!r}")
+    return mode
 
 
 @dataclass
@@ -230,6 +250,12 @@ class TreeBuilder:
         self.free_slots = None
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0"
         self.fmask_np = np.ones(F, np.uint8)
+        # owner-computes histogram sync (multi-GPU): see TreeParams.hist_sync
+        self.owner = self.comm.is_dist and resolve_hist_sync(params.hist_sync, self.slot_bytes) == "owner"
+        if self.owner:
+            self.fr, self.fblocks = self.comm.feature_blocks(F)
+            self.own = self.fblocks[self.comm.rank]
+            self._own_masks = {}
 
     # ------------------------------------------------------------------ utils
     def _sync(self):
@@ -323,7 +349,10 @@ class TreeBuilder:
         self._sync()
         t1 = time.perf_counter()
         if nb and self.comm.is_dist:
-            if s0 >= 0:
+            if self.owner:
+                idx = (torch.arange(s0, s0 + nb, device=self.dev) if s0 >= 0 else ids_d.long())
+                self._owner_reduce(idx)
+            elif s0 >= 0:
                 self.comm.allreduce_(self.hist[s0:s0 + nb])
             else:  # gather the scattered slots into one buffer -> one all-reduce
                 idx = ids_d.long()
@@ -332,14 +361,82 @@ class TreeBuilder:
                 self.hist.index_copy_(0, idx, buf)
             self._sync()
         t2 = time.perf_counter()
-        out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp_tree)
-        recs = out.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+        if self.owner:
+            fm_own, f0_own = self._owner_mask(f0)
+            out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fm_own, f0_own, items_d, self.gp_tree)
+            recs = self._owner_combine(out)
+        else:
+            out = gops.split_find(self.hist, self.B, self.F, self.nbins_f, fmask, f0, items_d, self.gp_tree)
+            recs = out.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
         self.up.reset()  # the .cpu() above synchronised the stream
         t3 = time.perf_counter()
         st.build_hist += t1 - t0
         st.comm_hist += t2 - t1
         st.find_split += t3 - t2
         return recs
+
+    # ------------------------------------------------ owner-computes histogram sync
+    def _owner_reduce(self, idx: torch.Tensor):
+        """Reduce-scatter the built slots ``idx`` by feature block: afterwards this rank
+        holds the GLOBAL sums of its own features [lo, hi) (HistogramBuilder.java:95);
+        the other feature columns keep local partials and are never read."""
+        P, fr = self.comm.world, self.fr
+        nb = int(idx.numel())
+        buf = self.hist.index_select(0, idx)  # [nb, B, F, 2]
+        if P * fr != self.F:
+            pad = torch.zeros((nb, self.B, P * fr - self.F, 2), dtype=buf.dtype, device=buf.device)
+            x = torch.cat([buf, pad], dim=2)
+        else:
+            x = buf
+        x = x.reshape(nb, self.B, P, fr, 2).permute(2, 0, 1, 3, 4).contiguous()
+        out = torch.empty((nb, self.B, fr, 2), dtype=buf.dtype, device=buf.device)
+        self.comm.reduce_scatter_(out, x)
+        lo, hi = self.own
+        if hi > lo:
+            buf[:, :, lo:hi] = out[:, :, :hi - lo]
+        self.hist.index_copy_(0, idx, buf)
+
+    def _owner_mask(self, f0: int):
+        """(device fmask of the sampled features this rank owns, node-total feature).
+        A rank owning no sampled feature searches nothing; its totals are ignored."""
+        lo, hi = self.own
+        fm = self.fmask_np.copy()
+        fm[:lo] = 0
+        fm[hi:] = 0
+        key = fm.tobytes()
+        if key not in self._own_masks:
+            if len(self._own_masks) > 64:
+                self._own_masks.clear()
+            self._own_masks[key] = torch.from_numpy(fm).to(self.dev)
+        nz = np.flatnonzero(fm)
+        return self._own_masks[key], (int(nz[0]) if nz.size else (lo if hi > lo else 0))
+
+    def _owner_combine(self, out: torch.Tensor) -> np.ndarray:
+        """Allgather the per-rank best splits (48-B records) and take the global argmax with
+        the reference tie-break (SplitInfo.needReplace: larger lossChg, then lower feature,
+        then lower bin) -- the same total order the split kernels use, so the result is
+        bitwise the all-reduce mode's record. Node totals come from the first rank owning
+        a sampled feature (exact int64 sums: every feature's total is the same)."""
+        n = out.shape[0]
+        allr = self.comm.allgather(out.contiguous().view(n, 48))
+        recs = allr.cpu().numpy().view(gops.SPLIT_DTYPE).reshape(self.comm.world, n)
+        big = np.int64(0x7fffffff)
+        best = recs[0].copy()
+        for r in range(1, self.comm.world):
+            c = recs[r]
+            cf = np.where(c["feat"] < 0, big, c["feat"])
+            bf = np.where(best["feat"] < 0, big, best["feat"])
+            cb = np.where(c["bin_b"] < 0, big, c["bin_b"])
+            bb = np.where(best["bin_b"] < 0, big, best["bin_b"])
+            rep = ((c["loss_chg"] > best["loss_chg"])
+                   | ((c["loss_chg"] == best["loss_chg"]) & ((cf < bf) | ((cf == bf) & (cb < bb)))))
+            best[rep] = c[rep]
+        for r, (lo, hi) in enumerate(self.fblocks):
+            if hi > lo and self.fmask_np[lo:hi].any():
+                best["g"] = recs[r]["g"]
+                best["h"] = recs[r]["h"]
+                break
+        return best
 
     def _evict(self, nodes: Dict[int, _Node], keep):
         """Drop the least recently built histogram not needed by the current call."""
@@ -522,16 +619,24 @@ class TreeBuilder:
                              base + 4 * off[2], 0, s)
             if self.comm.is_dist:  # the built slots, gathered -> one all-reduce -> scattered
                 idx = torch.from_numpy(arr[off[2]:off[2] + nb].astype(np.int64)).to(self.dev)
-                buf = self.hist.index_select(0, idx)
-                self.comm.allreduce_(buf)
-                self.hist.index_copy_(0, idx, buf)
+                if self.owner:
+                    self._owner_reduce(idx)
+                else:
+                    buf = self.hist.index_select(0, idx)
+                    self.comm.allreduce_(buf)
+                    self.hist.index_copy_(0, idx, buf)
         t1 = time.perf_counter()
         if self._split_out is None or self._split_out.numel() < n * 48:
             self._split_out = torch.empty(max(n, 512) * 48, dtype=torch.uint8, device=self.dev)
+        if self.owner:
+            fmask, f0 = self._owner_mask(f0)
         h.split_find(self.hist.data_ptr(), self.B, self.F, self.nbins_f.data_ptr(), fmask.data_ptr(), int(f0),
                      base + 4 * off[1], n, self._split_out.data_ptr(), gp["mcw"], gp["l1"], gp["l2"],
                      gp["max_abs_leaf"], 1.0 / float(gp["sg"]), 1.0 / float(gp["sh"]), 0, 0, 0, 0, s)
-        recs = self._split_out[:n * 48].cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
+        if self.owner:
+            recs = self._owner_combine(self._split_out[:n * 48].view(n, 48))
+        else:
+            recs = self._split_out[:n * 48].cpu().numpy().view(gops.SPLIT_DTYPE).reshape(-1)
         self.up.reset()
         self.last_stats.build_hist += t1 - t0
         self.last_stats.find_split += time.perf_counter() - t1

@@ -25,7 +25,7 @@ from ...ops import gbdt as gops
 from ...ops._ext import hip, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
-from .builder import TimeStats, TreeParams
+from .builder import TimeStats, TreeParams, resolve_hist_sync
 from .tree import Tree
 
 DNODE_DTYPE = np.dtype([
@@ -154,6 +154,15 @@ class DeviceLevelBuilder:
             nxt += 2 * half + self.ncs
         self.n_slots = max(1, nxt)
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
+        # owner-computes sync (TreeParams.hist_sync): reduce-scatter by feature block (the
+        # level's count slots ride along in every rank's block), split search on the owned
+        # features, allgather of the 48-B records, device-side argmax (split_combine)
+        self.owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, slot_elems * 8) == "owner"
+        if self.owner:
+            self.fr, self.fblocks = self.comm.feature_blocks(F)
+            self.own = self.fblocks[self.comm.rank]
+            self.split_local = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
+            self._own_cache = {}
         self._slot_bytes = slot_elems * 8
         self._root_fixed = False
         # staged histogram flush: block partials to a staging slab with plain stores, then a
@@ -225,6 +234,63 @@ class DeviceLevelBuilder:
             out[14] = glob
         return out
 
+    def _owner_reduce(self, base: int, nslots: int, ncs: int = 0):
+        """Reduce-scatter slots [base, base + nslots) by feature block (+ the ncs count slots
+        that follow them, replicated into every block so every rank gets their sums)."""
+        P, fr, B = self.comm.world, self.fr, self.B
+        built = self.hist[base:base + nslots]
+        nb_el = nslots * B * fr * 2
+        cnt = self.hist[base + nslots:base + nslots + ncs].reshape(-1) if ncs else None
+        C = cnt.numel() if cnt is not None else 0
+        x = torch.zeros((P, nb_el + C), dtype=torch.int64, device=self.dev)
+        xb = x[:, :nb_el].view(P, nslots, B, fr, 2)
+        for r, (lo, hi) in enumerate(self.fblocks):
+            if hi > lo:
+                xb[r, :, :, :hi - lo] = built[:, :, lo:hi]
+        if C:
+            x[:, nb_el:] = cnt
+        out = torch.empty(nb_el + C, dtype=torch.int64, device=self.dev)
+        self.comm.reduce_scatter_(out, x)
+        lo, hi = self.own
+        if hi > lo:
+            built[:, :, lo:hi] = out[:nb_el].view(nslots, B, fr, 2)[:, :, :hi - lo]
+        if C:
+            cnt.copy_(out[nb_el:])
+
+    def _owner_fmask(self, fmask_np: np.ndarray):
+        """(owned sampled-feature mask on the device, its first feature, totals rank)."""
+        key = fmask_np.tobytes()
+        if key not in self._own_cache:
+            lo, hi = self.own
+            fm = fmask_np.copy()
+            fm[:lo] = 0
+            fm[hi:] = 0
+            nz = np.flatnonzero(fm)
+            f0 = int(nz[0]) if nz.size else (lo if hi > lo else 0)
+            tot = next(r for r, (a, b) in enumerate(self.fblocks) if b > a and fmask_np[a:b].any())
+            if len(self._own_cache) > 64:
+                self._own_cache.clear()
+            self._own_cache[key] = (torch.from_numpy(fm).to(self.dev), f0, tot)
+        return self._own_cache[key]
+
+    def _split(self, fmask, f0: int, fmask_np: np.ndarray, nitems: int, nitems_dev: int, s):
+        """Split search over the items (all-reduce mode: every feature; owner mode: the
+        owned features, then allgather + device argmax into split_out)."""
+        gp, h = self.gp, hip()
+        out = self.split_out
+        if self.owner:
+            fmask, f0, tot = self._owner_fmask(fmask_np)
+            out = self.split_local
+        h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
+                     ptr(self.split_items), nitems, ptr(out), gp["mcw"], gp["l1"], gp["l2"],
+                     gp["max_abs_leaf"], 1.0, 1.0, nitems_dev, ptr(self.inv_scales), ptr(self.split_part),
+                     ptr(self.split_cnt), s)
+        if self.owner:
+            allr = self.comm.allgather(self.split_local)
+            cap = self.split_local.numel() // 48
+            h.split_combine(ptr(allr), self.comm.world, cap, nitems_dev, min(nitems, cap), tot,
+                            ptr(self.split_out), s)
+
     def _fmask(self, rng):
         p = self.p
         if p.feature_sample_rate < 1.0:
@@ -239,6 +305,7 @@ class DeviceLevelBuilder:
             if len(self._fmask_cache) > 64:
                 self._fmask_cache.clear()
             self._fmask_cache[key] = torch.from_numpy(fm).to(self.dev)
+        self._fmask_np = fm
         return self._fmask_cache[key], int(np.nonzero(fm)[0][0])
 
     # ------------------------------------------------------------------ build
@@ -329,13 +396,12 @@ class DeviceLevelBuilder:
         build_hist(gh0, rows0, self.hist_target + 1, 0, 1)
         tm.mark("build_hist_compute")
         if dist:
-            self.comm.allreduce_(self.hist[0:1])
+            if self.owner:
+                self._owner_reduce(0, 1)
+            else:
+                self.comm.allreduce_(self.hist[0:1])
             tm.mark("build_hist_comm")
-        gp = self.gp
-        h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
-                     ptr(self.split_items), 1, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
-                     gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
-                     ptr(self.split_cnt), s)
+        self._split(fmask, f0, self._fmask_np, 1, off(6), s)
         tm.mark("find_best_split")
         bb = 1 if self.bins.dtype == torch.uint8 else 2
         fused = self.fuse_counts
@@ -397,7 +463,7 @@ class DeviceLevelBuilder:
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
             nmax = self.hist_target + half + 1
-            if dist and self.overlap and half >= 8 and self.staged:  # large levels only:
+            if dist and self.overlap and half >= 8 and self.staged and not self.owner:  # large levels only:
                 # small ones are latency bound and a second collective would cost more
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
                 # second half's histogram build; the split search waits for both
@@ -415,13 +481,13 @@ class DeviceLevelBuilder:
                 build_hist(ptr(self.ghp), ptr(self.rows), nmax, base, half)
                 tm.mark("build_hist_compute")
                 if dist:
-                    # built slots (+ this level's count slots when fused): one all-reduce
-                    self.comm.allreduce_(self.hist[base:base + half + ncs])
+                    # built slots (+ this level's count slots when fused): one collective
+                    if self.owner:
+                        self._owner_reduce(base, half, ncs)
+                    else:
+                        self.comm.allreduce_(self.hist[base:base + half + ncs])
                     tm.mark("build_hist_comm")
-            h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
-                         ptr(self.split_items), 1 << c, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"],
-                         gp["max_abs_leaf"], 1.0, 1.0, off(6), ptr(self.inv_scales), ptr(self.split_part),
-                         ptr(self.split_cnt), s)
+            self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
             tm.mark("find_best_split")
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         tm.mark("plan")

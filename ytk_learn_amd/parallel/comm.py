@@ -38,6 +38,15 @@ class Comm:
         self.device = device if device is not None else torch.device("cpu")
         self.group = group
         self.cpu_group = cpu_group
+        # per-collective accounting (calls, payload bytes) for the bench / profile reports
+        self.stats = {"calls": 0, "bytes": 0}
+
+    def _count(self, t: torch.Tensor):
+        self.stats["calls"] += 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+
+    def reset_stats(self):
+        self.stats = {"calls": 0, "bytes": 0}
 
     # -- construction ---------------------------------------------------------
     @classmethod
@@ -94,6 +103,7 @@ class Comm:
         """In-place allreduce (RCCL for device tensors, gloo for host tensors)."""
         if not self.is_dist:
             return None
+        self._count(t)
         g = self.group if t.device.type == "cuda" else self.cpu_group
         return dist.all_reduce(t, op=_OPS[op], group=g, async_op=async_op)
 
@@ -106,14 +116,20 @@ class Comm:
         """Batch several scalars into one collective (reference issues one each)."""
         t = torch.tensor(list(values), dtype=dtype)
         if self.is_dist:
+            self._count(t)
             dist.all_reduce(t, op=_OPS[op], group=self.cpu_group)
         return t.tolist()
 
     def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
+        """out = this rank's 1/world block (dim 0) of the element-wise reduction of inp."""
         if not self.is_dist:
-            out.copy_(inp.view_as(out) if inp.numel() == out.numel() else inp[: out.numel()])
+            out.copy_(inp.view_as(out) if inp.numel() == out.numel() else inp.reshape(-1)[: out.numel()].view_as(out))
             return
-        dist.reduce_scatter_tensor(out, inp, op=_OPS[op], group=self.group)
+        self._count(inp)
+        g = self.group if inp.device.type == "cuda" else self.cpu_group
+        # rank blocks stacked along dim 0 with out's trailing shape (gloo checks shapes)
+        inp = inp.reshape((self.world * out.shape[0],) + tuple(out.shape[1:]))
+        dist.reduce_scatter_tensor(out, inp, op=_OPS[op], group=g)
 
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate equal-size shards along dim 0."""
@@ -121,6 +137,7 @@ class Comm:
             return t.clone()
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
+        self._count(t)
         g = self.group if t.device.type == "cuda" else self.cpu_group
         dist.all_gather_into_tensor(out, t.contiguous(), group=g)
         return out
@@ -128,6 +145,7 @@ class Comm:
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         if not self.is_dist:
             return
+        self._count(t)
         g = self.group if t.device.type == "cuda" else self.cpu_group
         dist.broadcast(t, src=src, group=g)
 
@@ -140,6 +158,7 @@ class Comm:
         if not self.is_dist:
             return [obj]
         out: List[Any] = [None] * self.world
+        self.stats["calls"] += 1
         dist.all_gather_object(out, obj, group=self.cpu_group)
         return out
 
@@ -159,6 +178,12 @@ class Comm:
         return lst[0]
 
     # -- even partition helper (CommUtils.createThreadArrayFroms/Tos) ---------
+    def feature_blocks(self, F: int):
+        """Owner-computes feature partition: rank r owns [r * Fr, min(F, (r + 1) * Fr)) with
+        Fr = ceil(F / world) (GBDTDataFlow.java:252-272 assigns contiguous column ranges)."""
+        fr = -(-F // self.world)
+        return fr, [(min(F, r * fr), min(F, (r + 1) * fr)) for r in range(self.world)]
+
     def shard_range(self, dim: int, rank: Optional[int] = None):
         r = self.rank if rank is None else rank
         base, rem = divmod(dim, self.world)
