@@ -49,7 +49,8 @@ class _Names(list):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="fm", choices=["linear", "fm", "ffm"])
+    ap.add_argument("--model", default="fm", choices=["linear", "fm", "ffm", "gbmlr", "gbsdt", "gbhmlr", "gbhsdt"])
+    ap.add_argument("--experts", type=int, default=16, help="soft-tree experts K (gbmlr/gbsdt/gbhmlr/gbhsdt)")
     ap.add_argument("--rows", type=int, default=4_000_000, help="rows per GPU")
     ap.add_argument("--features", type=int, default=1_000_000)
     ap.add_argument("--fields", type=int, default=39)
@@ -89,6 +90,8 @@ def main():
     params.model.need_bias = True
     params.model.data_path = "/tmp/ytk_bench_sparse_model"
     params.extra = {"k": [1, k], "bias_need_latent_factor": False}
+    if a.model.startswith("gb"):
+        params.extra = {"k": a.experts, "tree_num": 1, "learning_rate": 1.0}
     log = YtkLogger(comm.rank, stream=sys.stderr)
     log.quiet = True
     loaded = LoadedData(data, None, _Names(F), {}, ["_bias_"] + [f"c{i}" for i in range(a.fields)])
@@ -99,9 +102,15 @@ def main():
     elif a.model == "fm":
         from ytk_learn_amd.models.continuous.fm import FMModel
         model = FMModel(params, loaded, comm, log)
-    else:
+    elif a.model == "ffm":
         from ytk_learn_amd.models.continuous.ffm import FFMModel
         model = FFMModel(params, loaded, comm, log)
+    else:  # gradient-boosted soft trees: one tree's L-BFGS evaluations (fused HIP epilogue)
+        from ytk_learn_amd.models.gbst.model import GBSTModel
+        model = GBSTModel(a.model, params, loaded, comm, log)
+        model.init_w()
+        model.next_sample(1.0, 1.0)
+        k = a.experts
     setup_s = time.perf_counter() - t0
     if a.optimizer == "sgd":
         from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
@@ -138,8 +147,8 @@ def main():
             }), flush=True)
         comm.close()
         return
-    opt = HoagOptimizer(model, LineSearchParams(m=12), [0.0] * model.ngroups if hasattr(model, "ngroups") else [0.0],
-                        [1e-6] * (model.ngroups if hasattr(model, "ngroups") else 1), comm, log, tot)
+    ng = len(model.regular_groups()) if hasattr(model, "regular_groups") else getattr(model, "ngroups", 1)
+    opt = HoagOptimizer(model, LineSearchParams(m=12), [0.0] * ng, [1e-6] * ng, comm, log, tot)
     g = torch.zeros_like(model.w)
     for _ in range(a.warmup):
         opt.loss_and_grad(model.w, g)
@@ -173,6 +182,7 @@ def main():
             "ms_per_step": round(ms, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows, "dim": int(model.w.numel()),
             "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "setup_s": round(setup_s, 2),
             "scaling": "weak", "dtype": "fp32", "data": "synthetic Criteo-shape", "loss": loss / tot,
+            "gbst_fused": (os.environ.get("YTK_GBST_FUSED", "1") != "0") if a.model.startswith("gb") else None,
         }), flush=True)
     comm.close()
 

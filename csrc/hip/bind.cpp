@@ -25,6 +25,9 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
                     uintptr_t, uintptr_t);
 void ytk_split_combine(uintptr_t, int, int, uintptr_t, int, int, uintptr_t, uintptr_t);
+// gbst.hip
+void ytk_gbst_epilogue(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, double, uintptr_t, int, int, int,
+                       int, int, int, int, int, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition_atomic(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                           uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -87,6 +90,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_wide_group", &ytk_hist_wide_group);
   m.def("split_find", &ytk_split_find);
   m.def("split_combine", &ytk_split_combine);
+  m.def("gbst_epilogue", &ytk_gbst_epilogue);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
   m.def("segment_copy", &ytk_segment_copy);

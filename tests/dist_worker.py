@@ -30,7 +30,7 @@ def gbdt_data(n, F, seed, rank, world, device):
     return torch.from_numpy(X[sl]).to(device), torch.from_numpy(y[sl]).to(device)
 
 
-def run_gbdt(comm, out, device, policy):
+def run_gbdt(comm, out, device, policy, loss="sigmoid"):
     from ytk_learn_amd.models.gbdt.builder import TreeParams
     from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer
     X, y = gbdt_data(20000, 10, 7, comm.rank, comm.world, device)
@@ -38,12 +38,16 @@ def run_gbdt(comm, out, device, policy):
     tp = TreeParams(max_depth=5 if policy == "level" else -1, max_leaf_cnt=32 if policy == "level" else 20,
                     min_child_hessian_sum=1.0, learning_rate=0.2, l2=1.0, grow_policy=policy,
                     feature_sample_rate=float(os.environ.get("YTK_TEST_FSAMPLE", "1.0")))
-    p = GBDTParams(round_num=6, loss_function="sigmoid", missing_value="value@0",
+    p = GBDTParams(round_num=6, loss_function=loss, missing_value="value@0",
+                   lad_refine_appr=os.environ.get("YTK_TEST_LAD_APPR", "0") == "1",
                    approximate=[{"cols": "default", "type": "sample_by_quantile", "max_cnt": 255}], tree=tp)
     tr = GBDTTrainer(p, GBDTData(X, y), GBDTData(Xt, yt), comm=comm)
     model = tr.train()
     tl, te = tr._losses()
     owner = bool(getattr(tr.builder, "owner", False))
+    if comm.log is not None:  # every rank's collective sequence (deadlock-freedom check)
+        with open(os.path.join(out, f"comm_log_{comm.rank}.json"), "w") as f:
+            json.dump(comm.log, f)
     if comm.rank == 0:
         with open(os.path.join(out, "model.txt"), "w") as f:
             f.write(model.dumps())
@@ -112,6 +116,8 @@ def main():
             run_gbdt(comm, out, dev, "level")
         elif task == "gbdt_loss":
             run_gbdt(comm, out, dev, "loss")
+        elif task == "gbdt_l1":  # l1 loss: leaf refine by the exact distributed weighted median
+            run_gbdt(comm, out, dev, "level", loss="l1")
         elif task in ("linear", "fm", "gbmlr", "gbhsdt"):
             run_linear(comm, out, dev, task)
         elif task in ("fm_sgd", "linear_sgd"):

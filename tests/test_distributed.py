@@ -71,11 +71,32 @@ def test_gbdt_world_n_both_sync_modes(tmp_path, task, world, mode, fs):
     and with owner-computes (reduce-scatter by feature block + allgather of split records;
     with 10 features and 8 ranks some ranks own one feature, with feature sampling some
     own no sampled feature at all)."""
-    env = {"YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": fs}
+    env = {"YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": fs, "YTK_COMM_LOG": "1"}
     _run(task, tmp_path / "w1", 1, extra_env=env)
     r = _run(task, tmp_path / f"w{world}", world, extra_env=env)
     assert r["owner"] == (mode == "owner")
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
+    _same_collective_sequence(tmp_path / f"w{world}", world)
+
+
+def _same_collective_sequence(out, world):
+    """Every rank issued the identical collective sequence (op, dtype, size): under RCCL a
+    mismatch would hang, so this is the CPU-checkable form of the ordering contract."""
+    logs = [json.load(open(os.path.join(out, f"comm_log_{r}.json"))) for r in range(world)]
+    assert len(logs[0]) > 0
+    for r in range(1, world):
+        assert logs[r] == logs[0], f"rank {r} collective sequence differs from rank 0"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gbdt_l1_exact_refine_world_n(tmp_path, world):
+    """TreeRefiner exact mode (lad_refine_appr = false) across ranks: the bucketed
+    distributed weighted median gives the world-1 (single sort) leaf values."""
+    _run("gbdt_l1", tmp_path / "w1", 1)
+    _run("gbdt_l1", tmp_path / f"w{world}", world,
+         extra_env={"YTK_COMM_LOG": "1", "YTK_MEDIAN_GATHER_MAX": "64" if world == 4 else "8192"})
+    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
+    _same_collective_sequence(tmp_path / f"w{world}", world)
 
 
 @pytest.mark.parametrize("task,world", [("linear", 2), ("gbmlr", 2), ("linear", 8), ("gbmlr", 4)])
@@ -102,10 +123,12 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0"}
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0",
+           "YTK_COMM_LOG": "1"}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
+    _same_collective_sequence(tmp_path / f"w{world}", world)
 
 
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])

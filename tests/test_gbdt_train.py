@@ -115,15 +115,24 @@ def test_train_gpu_matches_cpu(cuda, policy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 11}, {"min_split_samples": 3000}, {"l2": 1.0, "l1": 0.5}])
+@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 11}, {"min_split_samples": 3000}, {"l2": 1.0, "l1": 0.5},
+                                {"split_type": "median"}, {"feature_sample_rate": 0.6},
+                                {"instance_sample_rate": 0.7, "feature_sample_rate": 0.5, "split_type": "median"},
+                                {"max_cnt": 300, "feature_sample_rate": 0.6}])
 def test_device_builder_matches_host_builder(cuda, kw):
-    """GPU-resident level builder == host-driven builder (integer histograms => identical trees)."""
+    """GPU-resident level builder == host-driven builder (integer histograms => identical trees),
+    including median split values, feature / instance sampling and > 256 (uint16) bins."""
     d = _data(40000, 9, cuda)
     trees = []
+    special = ("max_leaf_cnt", "split_type", "max_cnt")
     for dev_builder in (False, True):
-        p = _params("level", rounds=3, **{k: v for k, v in kw.items() if k not in ("max_leaf_cnt",)})
+        p = _params("level", rounds=3, **{k: v for k, v in kw.items() if k not in special})
         if "max_leaf_cnt" in kw:
             p.tree.max_leaf_cnt = kw["max_leaf_cnt"]
+        if "split_type" in kw:
+            p.split_type = kw["split_type"]
+        if "max_cnt" in kw:
+            p.approximate = [{"cols": "default", "type": "sample_by_quantile", "max_cnt": kw["max_cnt"]}]
         p.device_builder = dev_builder
         tr = GBDTTrainer(p, d, _data(5000, 10, cuda))
         tr.train()

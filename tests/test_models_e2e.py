@@ -239,3 +239,55 @@ def test_sgd_optimizer_gpu(cuda, bin_data, tmp_path, model):
                comm=_local(cuda))
     assert rg[1] < 0.55
     assert abs(rg[1] - rc[1]) < 0.05, (rg, rc)
+
+
+def _agaricus_ytk(tmp_path):
+    """The reference demo's agaricus libsvm files (bundled gzip copies, public dataset)
+    converted to the ytk format with the LibSVM tool."""
+    import gzip
+
+    from ytk_learn_amd.tools.libsvm_convert import convert
+    data = os.path.join(ROOT, "tests", "data")
+    out = {}
+    for part in ("train", "test"):
+        raw = tmp_path / f"agaricus.{part}.libsvm"
+        raw.write_bytes(gzip.decompress(open(os.path.join(data, f"agaricus.{part}.libsvm.gz"), "rb").read()))
+        out[part] = tmp_path / f"{part}.ytk"
+        convert("binary_classification@0,1", "###", ",", ",", ":", "local", str(raw), str(out[part]),
+                log=lambda *_: None)
+    return out
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_gbdt_demo_readme_losses_on_device(tmp_path, dev):
+    """demo/gbdt/binary_classification (loss-wise, 3 rounds, sigmoid) through this repo's
+    demo config: the reference README's per-round losses to 1e-12 -- on the CPU path and on
+    the HIP path (exact int64 histograms make the GPU trees identical)."""
+    import torch
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _agaricus_ytk(tmp_path)
+    cfg = parse_file(os.path.join(ROOT, "demo", "gbdt", "binary_classification", "gbdt.conf")).with_overrides({
+        "data.train.data_path": str(d["train"]), "data.test.data_path": str(d["test"]),
+        "model.data_path": str(tmp_path / "gbdt.model"), "model.feature_importance_path": str(tmp_path / "fi")})
+    losses = []
+
+    class Log:
+        verbose = False
+
+        def info(self, msg, all_ranks=False):
+            for line in msg.splitlines():
+                if line.startswith("train loss = ") or line.startswith("test loss = "):
+                    losses.append(float(line.split("=")[1]))
+
+        def enabled_for_round(self, i):
+            return True
+
+        def error(self, msg):
+            pass
+
+    tr = train("gbdt", cfg, comm=_local(dev), log=Log())
+    assert tr.bins.device.type == dev
+    # README (demo/gbdt/binary_classification/README.md:42-58): iter 2 and iter 3
+    np.testing.assert_allclose(losses[2:6], [0.17249267375913763, 0.17219528385526198, 0.09960066518065772,
+                                             0.09943817574378232], rtol=1e-12)

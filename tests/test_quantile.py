@@ -35,3 +35,30 @@ def test_exact_when_small():
     np.testing.assert_array_equal(s[:, 3], [1.0, 2.0, 1.0, 1.0])
     assert wq.query(s, [0.5])[0] == 2.0
     assert wq.total(s) == 5.0
+
+
+@pytest.mark.parametrize("seed,gather_max,buckets", [(0, 8192, 1024), (1, 40, 8), (2, 5, 4)])
+def test_distributed_weighted_median_matches_sort(seed, gather_max, buckets):
+    """Bucketed exact median (PreciseQuantile-style rounds) == single-process sorted median,
+    with ties, integer and fractional weights, degenerate and empty groups."""
+    import torch
+
+    from ytk_learn_amd.models.gbdt.refine import _weighted_median_sorted
+    from ytk_learn_amd.parallel.comm import Comm
+    from ytk_learn_amd.utils.quantile import distributed_weighted_median
+
+    rng = np.random.default_rng(seed)
+    n, G = 20000, 9
+    g = rng.integers(0, G - 1, n)  # group G-1 stays empty
+    v = np.round(rng.normal(size=n) * 3, 1)  # many ties
+    v[g == 3] = 2.5  # one distinct value
+    w = rng.integers(1, 4, n).astype(np.float64) if seed != 1 else rng.random(n) + 0.5
+    got = distributed_weighted_median(torch.from_numpy(v), torch.from_numpy(w), torch.from_numpy(g), G,
+                                      Comm.local(), buckets=buckets, gather_max=gather_max)
+    for k in range(G):
+        m = g == k
+        if not m.any():
+            assert np.isnan(got[k])
+            continue
+        o = np.argsort(v[m], kind="stable")
+        assert got[k] == _weighted_median_sorted(v[m][o], w[m][o]), k

@@ -7,11 +7,19 @@ mergeable-summary (approximate) or the exact distributed quantile.
 
 Device-native: leaf ids come from the bin-threshold traversal kernel, the
 per-leaf weighted medians from one segmented sort on the device (sort by
-(leaf, residual), segmented cumulative weights). Across GPUs each rank sends a
-256-point weighted summary per leaf (approximate) or its whole per-leaf residual
-list (exact) and the merge happens on the host in rank order.
+(leaf, residual), segmented cumulative weights).
+  * approximate (lad_refine_appr = true, the reference default, TreeRefiner.java
+    getLeafRefineValForLADAppr): weighted mergeable summaries per leaf on EVERY world
+    size, sized like the reference's (eps 1e-5, exact up to 1e5 samples,
+    Constants.java:55-56), merged in rank order;
+  * exact (false, getLeafRefineValForLADPrecise + PreciseQuantile.java:237-320): one
+    process sorts; across GPUs the bucketed distributed median of
+    ``utils.quantile.distributed_weighted_median`` (fixed-size tensor collectives, no
+    pickled residual lists).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -19,7 +27,7 @@ import torch
 from ...ops import gbdt as gops
 from ...parallel.comm import Comm
 
-SUMMARY_POINTS = 256
+SUMMARY_POINTS = 100_000  # 1 / QUNANTILE_APPROXIMATE_EPS and QUNANTILE_PRECISION_MAX_SAMPLE_CNT
 
 
 def _weighted_median_sorted(v: np.ndarray, w: np.ndarray) -> float:
@@ -51,6 +59,15 @@ class TreeRefiner:
         ww = w.double() if w is not None else torch.ones_like(resid)
         if keep is not None:
             leaf, resid, ww = leaf[keep], resid[keep], ww[keep]
+        leaves = tree.leaf_nodes()
+        if not self.approximate and self.comm.is_dist:
+            from ...utils.quantile import distributed_weighted_median
+            gmax = int(os.environ.get("YTK_MEDIAN_GATHER_MAX", 8192))  # tests force bucket rounds
+            med = distributed_weighted_median(resid, ww, leaf, tree.num_nodes, self.comm, gather_max=gmax)
+            for nid in leaves:
+                if not np.isnan(med[nid]):
+                    tree.leaf[nid] = float(np.float32(med[nid]) * np.float32(lr))
+            return
         # segmented sort on device: key = leaf * big + rank(resid)
         o = torch.argsort(resid)
         leaf_o = leaf[o]
@@ -59,7 +76,6 @@ class TreeRefiner:
         lv = leaf[idx].cpu().numpy()
         rv = resid[idx].cpu().numpy()
         wv = ww[idx].cpu().numpy()
-        leaves = tree.leaf_nodes()
         bounds = {}
         if lv.size:
             starts = np.flatnonzero(np.r_[True, lv[1:] != lv[:-1]])
@@ -72,25 +88,22 @@ class TreeRefiner:
                 local[nid] = (np.zeros(0), np.zeros(0))
                 continue
             s, e = bounds[nid]
-            v, wt = rv[s:e], wv[s:e]
-            local[nid] = (v, wt)
-        summarize = self.comm.is_dist and self.approximate
-        if summarize:
-            # weighted mergeable summaries (WeightApproximateQuantile) instead of raw values
+            local[nid] = (rv[s:e], wv[s:e])
+        if self.approximate:
+            # weighted mergeable summaries (WeightApproximateQuantile), on every world size
             from ...utils import quantile as wq
             local = {nid: wq.build(v, wt, SUMMARY_POINTS) for nid, (v, wt) in local.items()}
-        parts = self.comm.allgather_object(local) if self.comm.is_dist else [local]
-        for nid in leaves:
-            if summarize:
-                s = wq.merge([p[nid] for p in parts], SUMMARY_POINTS)
-                if len(s) == 0:
+            parts = self.comm.allgather_object(local) if self.comm.is_dist else [local]
+            for nid in leaves:
+                sm = wq.merge([p[nid] for p in parts], SUMMARY_POINTS)
+                if len(sm) == 0:
                     continue
-                med = float(wq.query(s, [0.5])[0])
-            else:
-                vs = np.concatenate([p[nid][0] for p in parts])
-                ws = np.concatenate([p[nid][1] for p in parts])
-                if vs.size == 0:
-                    continue
-                o = np.argsort(vs, kind="stable")
-                med = _weighted_median_sorted(vs[o], ws[o])
+                med = float(wq.query(sm, [0.5])[0])
+                tree.leaf[nid] = float(np.float32(med) * np.float32(lr))
+            return
+        for nid in leaves:  # exact, one process
+            vs, ws = local[nid]
+            if vs.size == 0:
+                continue
+            med = _weighted_median_sorted(vs, ws)
             tree.leaf[nid] = float(np.float32(med) * np.float32(lr))

@@ -179,7 +179,46 @@ class GBSTModel(ContinuousModelBase):
         leaves = w[:self.K] if self.expert_kind == "scalar" else None
         return gbst_mixture(A, self.K, self.gate_kind, self.expert_kind, leaves)
 
+    def _fused_ok(self, X) -> bool:
+        """The fused HIP epilogue (csrc/hip/gbst.hip) covers sigmoid / l2 losses, K <= 64
+        (hierarchical gates: power-of-two K); otherwise the fp64 torch path runs."""
+        K = self.K
+        return (X.values.is_cuda and self.loss.name in ("sigmoid", "l2") and 2 <= K <= 64
+                and (self.gate_kind == "softmax" or (K & (K - 1)) == 0)
+                and os.environ.get("YTK_GBST_FUSED", "1") != "0")
+
+    def _forward_fused(self, X, d, z, w, g_out, train: bool):
+        from ...ops._ext import hip, ptr, stream
+        fmask = self.fmask
+        A = X.matmul(self._masked_W(w, fmask).contiguous())  # float32 [n, stride] (segmented SpMM)
+        n, K = A.shape[0], self.K
+        acc = torch.zeros(2 + 2 * K, dtype=torch.float64, device=A.device)
+        pred = torch.empty(n, dtype=torch.float32, device=A.device)
+        want = g_out is not None
+        D = torch.empty((n, self.stride), dtype=torch.float32, device=A.device) if want else None
+        y = d.y[:, 0].contiguous()
+        wt = d.weight.contiguous()
+        mask = self.rmask.view(torch.uint8) if train else None
+        leaves = w[:K].contiguous() if self.expert_kind == "scalar" else None
+        hip().gbst_epilogue(ptr(A), A.stride(0), ptr(z), ptr(y), ptr(wt), ptr(mask), float(1.0 / self.rate),
+                            ptr(leaves), n, K, 1 if self.gate_kind == "tree" else 0,
+                            1 if self.expert_kind == "linear" else 0, 0 if self.loss.name == "sigmoid" else 1,
+                            1 if self.rf else 0, self.finished + 1, 1 if want else 0, ptr(D), self.stride,
+                            ptr(pred), ptr(acc), stream(A))
+        if want:
+            G = g_out[self.gate_off:].view(self.F, self.stride)
+            X.t_matmul(D, out=G)
+            if fmask is not None and not bool(fmask.all()):
+                G[~fmask, :self.Km1] = 0.0
+        a = acc.cpu()
+        if want and self.expert_kind == "scalar":
+            g_out[:K] = a[2 + K:2 + 2 * K].float().to(g_out.device)
+        samples = a[2:2 + K].clone() if train else None
+        return float(a[0]), pred, float(a[1]), samples
+
     def _forward(self, X, d, z, w, g_out, train: bool):
+        if self._fused_ok(X):
+            return self._forward_fused(X, d, z, w, g_out, train)
         fmask = self.fmask
         gk, H, mu, sig = self._mixture(X, w, fmask)
         purefx_mix = (gk * H).sum(1) if mu is None else mu[:, 1]

@@ -40,10 +40,15 @@ class Comm:
         self.cpu_group = cpu_group
         # per-collective accounting (calls, payload bytes) for the bench / profile reports
         self.stats = {"calls": 0, "bytes": 0}
+        # YTK_COMM_LOG=1: record every collective (op, dtype, numel) -- ranks must issue the
+        # identical sequence (a mismatch is a hang under RCCL); checked by the tests
+        self.log = [] if os.environ.get("YTK_COMM_LOG") == "1" else None
 
-    def _count(self, t: torch.Tensor):
+    def _count(self, t: torch.Tensor, op: str = ""):
         self.stats["calls"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
+        if self.log is not None:
+            self.log.append((op, str(t.dtype), int(t.numel())))
 
     def reset_stats(self):
         self.stats = {"calls": 0, "bytes": 0}
@@ -103,7 +108,7 @@ class Comm:
         """In-place allreduce (RCCL for device tensors, gloo for host tensors)."""
         if not self.is_dist:
             return None
-        self._count(t)
+        self._count(t, "allreduce_" + op)
         g = self.group if t.device.type == "cuda" else self.cpu_group
         return dist.all_reduce(t, op=_OPS[op], group=g, async_op=async_op)
 
@@ -116,7 +121,7 @@ class Comm:
         """Batch several scalars into one collective (reference issues one each)."""
         t = torch.tensor(list(values), dtype=dtype)
         if self.is_dist:
-            self._count(t)
+            self._count(t, "allreduce_scalars_" + op)
             dist.all_reduce(t, op=_OPS[op], group=self.cpu_group)
         return t.tolist()
 
@@ -125,7 +130,7 @@ class Comm:
         if not self.is_dist:
             out.copy_(inp.view_as(out) if inp.numel() == out.numel() else inp.reshape(-1)[: out.numel()].view_as(out))
             return
-        self._count(inp)
+        self._count(inp, "reduce_scatter")
         g = self.group if inp.device.type == "cuda" else self.cpu_group
         # rank blocks stacked along dim 0 with out's trailing shape (gloo checks shapes)
         inp = inp.reshape((self.world * out.shape[0],) + tuple(out.shape[1:]))
@@ -137,7 +142,7 @@ class Comm:
             return t.clone()
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
-        self._count(t)
+        self._count(t, "allgather")
         g = self.group if t.device.type == "cuda" else self.cpu_group
         dist.all_gather_into_tensor(out, t.contiguous(), group=g)
         return out
@@ -145,7 +150,7 @@ class Comm:
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         if not self.is_dist:
             return
-        self._count(t)
+        self._count(t, "broadcast")
         g = self.group if t.device.type == "cuda" else self.cpu_group
         dist.broadcast(t, src=src, group=g)
 
@@ -159,6 +164,8 @@ class Comm:
             return [obj]
         out: List[Any] = [None] * self.world
         self.stats["calls"] += 1
+        if self.log is not None:
+            self.log.append(("allgather_object", "object", 0))
         dist.all_gather_object(out, obj, group=self.cpu_group)
         return out
 

@@ -45,3 +45,98 @@ def distributed_quantiles(values, weights, fractions, comm, size: int) -> np.nda
     local = build(values, weights, size)
     parts: List[np.ndarray] = comm.allgather_object(local) if comm is not None and comm.is_dist else [local]
     return query(merge(parts, size), fractions)
+
+
+def _first_reaching(cum: "np.ndarray", target: "np.ndarray") -> "np.ndarray":
+    """Per row of cum [G, K]: first column whose value >= target[g] (K if none)."""
+    ok = cum >= target[:, None]
+    return np.where(ok.any(axis=1), ok.argmax(axis=1), cum.shape[1])
+
+
+def distributed_weighted_median(values, weights, groups, n_groups: int, comm, buckets: int = 1024,
+                                gather_max: int = 8192, max_rounds: int = 8):
+    """EXACT weighted median per group of the union of every rank's rows, with fixed-size
+    tensor collectives only (reference: J/utils/PreciseQuantile.java:237-320 -- count,
+    bucket, per-bucket weight sums, locate the bucket holding the median, gather that
+    bucket's values).
+
+    Each round histograms the surviving rows of every group into ``buckets`` equal-width
+    value buckets over the group's global [min, max] (one all-reduce of G x K weights and
+    counts), keeps only the bucket where the cumulative weight reaches half the group's
+    weight (adding the weight below it to an offset), until every group has at most
+    ``gather_max`` survivors; those are all-gathered (padded tensors) and the median is the
+    first sorted survivor whose offset + cumulative weight >= W / 2 -- the same rule as a
+    single-process sort (``_weighted_median_sorted``). Returns float64 [G] (NaN for empty
+    groups). values / weights: float64 tensors, groups: int64 tensor in [0, G)."""
+    import torch
+
+    v = values.double().reshape(-1)
+    w = weights.double().reshape(-1)
+    g = groups.long().reshape(-1)
+    G, K = int(n_groups), int(buckets)
+    dev = v.device
+    W = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, g, w)
+    lo = torch.full((G,), float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, g, v, "amin")
+    hi = torch.full((G,), float("-inf"), dtype=torch.float64, device=dev).scatter_reduce(0, g, v, "amax")
+    comm.allreduce_(W)
+    comm.allreduce_(lo, op="min")
+    comm.allreduce_(hi, op="max")
+    target = 0.5 * W.cpu().numpy()
+    below = np.zeros(G, np.float64)
+    alive = torch.ones_like(g, dtype=torch.bool)
+    lo_np, hi_np = lo.cpu().numpy(), hi.cpu().numpy()
+    for _ in range(max_rounds):
+        cnt = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, g[alive], torch.ones_like(g[alive]))
+        comm.allreduce_(cnt)
+        cnt_np = cnt.cpu().numpy()
+        if cnt_np.max(initial=0) <= gather_max:
+            break
+        width = (hi_np - lo_np) / K
+        width = np.where(width > 0, width, 1.0)
+        gi = g[alive]
+        vi = v[alive]
+        lo_t = torch.from_numpy(lo_np).to(dev)
+        wd_t = torch.from_numpy(width).to(dev)
+        b = torch.floor((vi - lo_t[gi]) / wd_t[gi]).clamp_(0, K - 1).long()
+        hw = torch.zeros(G * K, dtype=torch.float64, device=dev).index_add_(0, gi * K + b, w[alive])
+        comm.allreduce_(hw)
+        cum = below[:, None] + np.cumsum(hw.view(G, K).cpu().numpy(), axis=1)
+        kstar = np.minimum(_first_reaching(cum, target), K - 1)
+        prev = np.where(kstar > 0, cum[np.arange(G), np.maximum(kstar - 1, 0)], below)
+        # groups already small (or degenerate: one distinct value) keep all survivors
+        small = (cnt_np <= gather_max) | (hi_np <= lo_np)
+        kk = torch.from_numpy(np.where(small, -1, kstar)).to(dev)
+        keep = (kk[gi] < 0) | (b == kk[gi])
+        below = np.where(small, below, prev)
+        new_lo = np.where(small, lo_np, lo_np + kstar * width)
+        new_hi = np.where(small, hi_np, np.minimum(hi_np, lo_np + (kstar + 1) * width))
+        lo_np, hi_np = new_lo, new_hi
+        alive_idx = torch.nonzero(alive).flatten()
+        alive[alive_idx[~keep]] = False
+    # gather the survivors (padded all-gather of (group, value, weight))
+    idx = torch.nonzero(alive).flatten()
+    n_loc = torch.tensor([idx.numel()], dtype=torch.int64, device=dev)
+    if comm.is_dist:
+        ns = comm.allgather(n_loc).cpu().numpy()
+        m = int(ns.max())
+        pad = torch.zeros((m, 3), dtype=torch.float64, device=dev)
+        pad[:idx.numel(), 0] = g[idx].double()
+        pad[:idx.numel(), 1] = v[idx]
+        pad[:idx.numel(), 2] = w[idx]
+        allr = comm.allgather(pad).cpu().numpy().reshape(comm.world, m, 3)
+        rows = np.concatenate([allr[r, :ns[r]] for r in range(comm.world)])
+    else:
+        rows = torch.stack([g[idx].double(), v[idx], w[idx]], 1).cpu().numpy()
+    out = np.full(G, np.nan)
+    if rows.size:
+        o = np.lexsort((rows[:, 1], rows[:, 0]))
+        rows = rows[o]
+        gs = rows[:, 0].astype(np.int64)
+        starts = np.flatnonzero(np.r_[True, gs[1:] != gs[:-1]])
+        ends = np.r_[starts[1:], len(gs)]
+        for s, e in zip(starts, ends):
+            k = gs[s]
+            c = below[k] + np.cumsum(rows[s:e, 2])
+            i = int(np.searchsorted(c, target[k], side="left"))
+            out[k] = rows[s + min(i, e - s - 1), 1]
+    return out
