@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--optimizer", default="lbfgs", choices=["lbfgs", "sgd"],
                     help="sgd: a step is one epoch of mini-batch Hogwild!-style SGD over the local rows")
     ap.add_argument("--batch", type=int, default=65536, help="sgd mini-batch rows")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="sgd: storage of the FM latent factors read by the row passes (fp32 master kept)")
     a = ap.parse_args()
     comm = Comm.from_env()
     dev = comm.device
@@ -115,8 +117,9 @@ def main():
     if a.optimizer == "sgd":
         from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
         ng = model.ngroups if hasattr(model, "ngroups") else 1
-        sgd = SGDOptimizer(model, SGDParams(learning_rate=0.01, batch_size=a.batch, epochs=1), [0.0] * ng,
-                           [1e-6] * ng, comm, log, tot, tot)
+        sgd = SGDOptimizer(model, SGDParams(learning_rate=0.01, batch_size=a.batch, epochs=1, dtype=a.dtype),
+                           [0.0] * ng, [1e-6] * ng, comm, log, tot, tot)
+        sgd._sync_copy(model.w)
         bounds = [(b, min(b + a.batch, n)) for b in range(0, n, a.batch)]
 
         def epoch():
@@ -142,7 +145,7 @@ def main():
                           f"batch {a.batch})",
                 "value": round(a.rows * comm.world / (el / a.steps), 1), "unit": "rows/s",
                 "ms_per_step": round(1000.0 * el / a.steps, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows,
-                "dim": int(model.w.numel()), "nnz_per_row": a.fields + 1, "scaling": "weak", "dtype": "fp32",
+                "dim": int(model.w.numel()), "nnz_per_row": a.fields + 1, "scaling": "weak", "dtype": a.dtype,
                 "data": "synthetic Criteo-shape", "train_loss": pure / tot,
             }), flush=True)
         comm.close()

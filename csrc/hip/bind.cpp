@@ -65,9 +65,9 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
                       int, int, uintptr_t);
 // fm.hip
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
-                       uintptr_t, float, float, float, int, int, int, uintptr_t);
+                       uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t);
 void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
-                    uintptr_t, uintptr_t);
+                    uintptr_t, int, uintptr_t);
 void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
                      uintptr_t, uintptr_t);
 // blas.hip

@@ -14,12 +14,20 @@
 // contiguous. Deterministic: fixed reduction orders, no atomics.
 #include "common.h"
 
+#include <hip/hip_bf16.h>
+
 namespace ytk {
 
-template <int G>
+// Latent factors may be stored in bf16 (SGD with optimization.sgd.dtype = bf16): the
+// row passes gather half the bytes; math stays fp32 and the fp32 master copy takes the
+// updates (see fm_sgd_update_kernel).
+__device__ __forceinline__ float ld_v(const float* p) { return *p; }
+__device__ __forceinline__ float ld_v(const __hip_bfloat16* p) { return __bfloat162float(*p); }
+
+template <int G, typename VT>
 __global__ __launch_bounds__(256) void fm_forward_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
-    long long nrows, const float* __restrict__ w, const float* __restrict__ V, int k,
+    long long nrows, const float* __restrict__ w, const VT* __restrict__ V, int k,
     double* __restrict__ fx, float* __restrict__ S) {
   const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
   const int f = threadIdx.x & (G - 1);
@@ -39,7 +47,7 @@ __global__ __launch_bounds__(256) void fm_forward_kernel(
       for (int u = 0; u < 4; ++u) {
         const int i = __shfl(my_i, j + u, G);
         xs[u] = __shfl(my_x, j + u, G);
-        v[u] = f < k ? V[(long long)i * k + f] : 0.f;
+        v[u] = f < k ? ld_v(V + (long long)i * k + f) : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -52,7 +60,7 @@ __global__ __launch_bounds__(256) void fm_forward_kernel(
       const int i = __shfl(my_i, j, G);
       const float x = __shfl(my_x, j, G);
       if (f < k) {
-        const float vx = V[(long long)i * k + f] * x;
+        const float vx = ld_v(V + (long long)i * k + f) * x;
         s += vx;
         q += vx * vx;
       }
@@ -130,7 +138,8 @@ template <int G>
 __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
     long long nrows, float* __restrict__ w, float* __restrict__ V, int k, const float* __restrict__ S,
-    const float* __restrict__ c, float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent) {
+    const float* __restrict__ c, float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent,
+    __hip_bfloat16* __restrict__ Vb) {
   const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
   const int f = threadIdx.x & (G - 1);
   if (gid >= nrows) return;
@@ -152,10 +161,20 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
         unsafeAtomicAdd(w + i, -lr * gw);
       }
       if (f < k && (!is_bias || bias_latent)) {
-        float* vp = V + (long long)i * k + f;
-        const float v = *vp;
-        const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
-        unsafeAtomicAdd(vp, -lr * gv);
+        const long long o = (long long)i * k + f;
+        if (Vb) {  // bf16 working copy: gradient from the value the forward used, fp32
+                   // master takes the update (returning atomic), mirror re-rounded from it
+          const float v = __bfloat162float(Vb[o]);
+          const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
+          const float d = -lr * gv;
+          const float old = atomicAdd(V + o, d);
+          Vb[o] = __float2bfloat16(old + d);  // races with other rows: Hogwild!-tolerant
+        } else {
+          float* vp = V + o;
+          const float v = *vp;
+          const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
+          unsafeAtomicAdd(vp, -lr * gv);
+        }
       }
     }
   }
@@ -175,7 +194,7 @@ extern "C" {
 
 // fx[r] (double) and S[r, k] for every row; w: linear weights [F], V: [F, k] (any alignment).
 void ytk_fm_forward(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
-                    uintptr_t V, int k, uintptr_t fx, uintptr_t S, uintptr_t stream) {
+                    uintptr_t V, int k, uintptr_t fx, uintptr_t S, int v_bf16, uintptr_t stream) {
   if (nrows <= 0) return;
   // k == 0: the linear score alone (S unused) -- the SGD optimizer's linear-model forward
   if (k < 0 || k > 64) throw std::invalid_argument("fm_forward: 0 <= k <= 64");
@@ -183,10 +202,15 @@ void ytk_fm_forward(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nr
   const long long threads = nrows * G;
   const dim3 grid((unsigned)((threads + 255) / 256));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define YTK_FM_F(GG)                                                                           \
-  hipLaunchKernelGGL(fm_forward_kernel<GG>, grid, dim3(256), 0, s, (const long long*)indptr,  \
-                     (const int*)idx, (const float*)val, nrows, (const float*)w,               \
-                     (const float*)V, k, (double*)fx, (float*)S)
+#define YTK_FM_F(GG)                                                                               \
+  if (v_bf16)                                                                                      \
+    hipLaunchKernelGGL((fm_forward_kernel<GG, __hip_bfloat16>), grid, dim3(256), 0, s,              \
+                       (const long long*)indptr, (const int*)idx, (const float*)val, nrows,         \
+                       (const float*)w, (const __hip_bfloat16*)V, k, (double*)fx, (float*)S);       \
+  else                                                                                             \
+    hipLaunchKernelGGL((fm_forward_kernel<GG, float>), grid, dim3(256), 0, s,                       \
+                       (const long long*)indptr, (const int*)idx, (const float*)val, nrows,         \
+                       (const float*)w, (const float*)V, k, (double*)fx, (float*)S)
   switch (G) {
     case 4: YTK_FM_F(4); break;
     case 8: YTK_FM_F(8); break;
@@ -228,7 +252,7 @@ void ytk_fm_backward(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, ui
 // when k == 0 (linear model).
 void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
                        uintptr_t V, int k, uintptr_t S, uintptr_t c, float lr, float l2w, float l2v,
-                       int reg_skip, int upd_w, int bias_latent, uintptr_t stream) {
+                       int reg_skip, int upd_w, int bias_latent, uintptr_t Vb, uintptr_t stream) {
   if (nrows <= 0) return;
   if (k < 0 || k > 64) throw std::invalid_argument("fm_sgd_update: 0 <= k <= 64");
   const int G = k == 0 ? 4 : fm_group(k);
@@ -238,7 +262,8 @@ void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long
 #define YTK_FM_S(GG)                                                                            \
   hipLaunchKernelGGL(fm_sgd_update_kernel<GG>, grid, dim3(256), 0, s, (const long long*)indptr, \
                      (const int*)idx, (const float*)val, nrows, (float*)w, (float*)V, k,        \
-                     (const float*)S, (const float*)c, lr, l2w, l2v, reg_skip, upd_w, bias_latent)
+                     (const float*)S, (const float*)c, lr, l2w, l2v, reg_skip, upd_w, bias_latent,     \
+                     (__hip_bfloat16*)Vb)
   switch (G) {
     case 4: YTK_FM_S(4); break;
     case 8: YTK_FM_S(8); break;

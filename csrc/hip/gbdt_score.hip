@@ -104,49 +104,60 @@ __global__ __launch_bounds__(256) void bin_assign_kernel(
 
 // ------------------------------------------------------------------ loss / grad
 // loss ids: 0 sigmoid, 1 l2, 2 l1, 3 poisson, 4 huber(delta=p0), 5 softmax (K>1)
+// fp64 like the CPU path and the reference (z = score / div + init in double, the
+// prediction rounded to float, g / h from that float prediction in double, then g * w and
+// h * w rounded to float): the GPU path reproduces the reference's per-round losses to
+// 1e-12 (test_gbdt_demo_readme_losses_on_device).
 struct LossOut {
-  float p, g, h;
+  float p;
+  double g, h;
   double l;
 };
 
-__device__ __forceinline__ LossOut point_loss(int loss_id, float z, float y, float p0) {
+__device__ __forceinline__ LossOut point_loss(int loss_id, double z, double y, double p0) {
   LossOut o;
   switch (loss_id) {
     case 0: {  // sigmoid (SigmoidFunction: stable log-loss, zmax hessian clamp)
-      const float az = fabsf(z);
-      const float e = expf(-az);
-      o.l = (double)log1pf(e) + (double)(z >= 0.f ? z * (1.f - y) : -z * y);
-      o.p = (z >= 0.f) ? 1.f / (1.f + e) : e / (1.f + e);
-      o.g = o.p - y;
-      o.h = o.p * (1.f - o.p);
-      if (p0 != 0.f) {
-        const float zz = (o.h != 0.f) ? -(o.g / o.h) : 0.f;
+      const double az = fabs(z);
+      const double e = exp(-az);
+      o.l = log1p(e) + (z >= 0.0 ? z * (1.0 - y) : -z * y);
+      o.p = (float)((z >= 0.0) ? 1.0 / (1.0 + e) : e / (1.0 + e));
+      const double p = (double)o.p;
+      o.g = p - y;
+      o.h = p * (1.0 - p);
+      if (p0 != 0.0) {
+        const double zz = (o.h != 0.0) ? -(o.g / o.h) : 0.0;
         if (zz > p0) o.h = -(o.g / p0);
         else if (zz < -p0) o.h = -(o.g / -p0);
       }
       break;
     }
     case 1:
-      o.l = 0.5 * (double)(y - z) * (double)(y - z);
-      o.p = z; o.g = z - y; o.h = 1.f;
+      o.l = 0.5 * (y - z) * (y - z);
+      o.p = (float)z; o.g = (double)o.p - y; o.h = 1.0;
       break;
-    case 2:
-      o.l = fabs((double)y - (double)z);
-      o.p = z; o.g = (float)((z - y > 0.f) - (z - y < 0.f)); o.h = 1.f;
+    case 2: {
+      o.l = fabs(y - z);
+      o.p = (float)z;
+      const double d = (double)o.p - y;
+      o.g = (double)((d > 0.0) - (d < 0.0)); o.h = 1.0;
       break;
+    }
     case 3: {
-      const float zc = fminf(z, 30.f);
-      o.p = expf(zc);
-      o.l = -(double)y * z + (double)o.p + (double)lgammaf(y + 1.f);
-      o.g = o.p - y; o.h = o.p;
+      const double zc = fmin(z, 30.0);
+      const double ez = exp(zc);
+      o.l = -y * z + ez + lgamma(y + 1.0);
+      o.p = (float)ez;
+      o.g = (double)o.p - y; o.h = (double)o.p;
       break;
     }
     default: {
-      const float a = z - y, d = p0;
-      o.l = (fabsf(a) <= d) ? 0.5 * (double)a * a : (double)d * (fabsf(a) - 0.5f * d);
-      o.p = z;
-      o.g = (fabsf(a) <= d) ? a : ((a > 0.f) - (a < 0.f)) * d;
-      o.h = 0.f;
+      const double a = z - y, d = p0;
+      o.l = (fabs(a) <= d) ? 0.5 * a * a : d * (fabs(a) - 0.5 * d);
+      o.p = (float)z;
+      const double aa = (double)o.p - y;
+      o.g = (fabs(aa) <= d) ? aa : ((aa > 0.0) - (aa < 0.0)) * d;
+      o.h = 0.0;
       break;
     }
   }
@@ -249,12 +260,13 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
       score[r] = s;
     }
     const float w = weight ? weight[r] : 1.f;
-    const LossOut o = point_loss(loss_id, s / score_div + init[r], label[r], p0);
+    const LossOut o = point_loss(loss_id, (double)s / (double)score_div + (double)init[r], (double)label[r],
+                                 (double)p0);
     lsum += (double)w * o.l;
     wsum += (double)w;
     if (pred) pred[r] = o.p;
     if (want_grad) {
-      const float gg = o.g * w, hh = o.h * w;
+      const float gg = (float)(o.g * (double)w), hh = (float)(o.h * (double)w);
       gh[r] = make_float2(gg, hh);
       mg = fmaxf(mg, fabsf(gg));
       mh = fmaxf(mh, fabsf(hh));
@@ -274,24 +286,23 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(
        r += (long long)gridDim.x * blockDim.x) {
     const float w = weight ? weight[r] : 1.f;
     wsum += (double)w;
+    // the CPU path's order: z = score / div + init in fp64, lse = max + log(sum exp(z - max)),
+    // p = exp(z - lse), loss = -sum y (z - lse)
+    auto zk = [&](int k) { return (double)score[r * K + k] / (double)score_div + (double)init[r * K + k]; };
     double zmax = -INFINITY;
-    for (int k = 0; k < K; ++k)
-      zmax = fmax(zmax, (double)(score[r * K + k] / score_div + init[r * K + k]));
-    double den = 0.0, sy = 0.0;
+    for (int k = 0; k < K; ++k) zmax = fmax(zmax, zk(k));
+    double den = 0.0;
+    for (int k = 0; k < K; ++k) den += exp(zk(k) - zmax);
+    const double lse = zmax + log(den);
+    double lt = 0.0;
+    for (int k = 0; k < K; ++k) lt += (double)label[r * K + k] * (zk(k) - lse);
+    lsum += (double)w * -lt;
     for (int k = 0; k < K; ++k) {
-      const double z = (double)(score[r * K + k] / score_div + init[r * K + k]) - zmax;
-      den += exp(z);
-      sy += z * (double)label[r * K + k];
-    }
-    lsum += (double)w * (log(den) - sy);
-    const double inv = 1.0 / den;
-    for (int k = 0; k < K; ++k) {
-      const double z = (double)(score[r * K + k] / score_div + init[r * K + k]) - zmax;
-      const double p = exp(z) * inv;
+      const double p = exp(zk(k) - lse);
       const double y = label[r * K + k];
       if (pred) pred[r * K + k] = (float)p;
       if (want_grad) {
-        const float gg = (float)((p - y) * w), hh = (float)(2.0 * p * (1.0 - p) * w);
+        const float gg = (float)((p - y) * (double)w), hh = (float)(2.0 * p * (1.0 - p) * (double)w);
         gh[k * N + r] = make_float2(gg, hh);
         if (ghmax) {
           atomicMax(reinterpret_cast<unsigned*>(&ghmax[2 * k]), __float_as_uint(fabsf(gg)));

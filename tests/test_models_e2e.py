@@ -241,6 +241,24 @@ def test_sgd_optimizer_gpu(cuda, bin_data, tmp_path, model):
     assert abs(rg[1] - rc[1]) < 0.05, (rg, rc)
 
 
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_fm_sgd_bf16_matches_fp32(bin_data, tmp_path, dev):
+    """optimization.sgd.dtype = bf16 (bf16 working copy of the FM latents, fp32 master):
+    the training run reaches the fp32 run's test loss within tolerance."""
+    import torch
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    kw = _sgd_kw()
+    kw["k"] = [1, 8]
+    res = {}
+    for dt in ("fp32", "bf16"):
+        kw["optimization.sgd.dtype"] = dt
+        res[dt] = train("fm", _cfg("fm", str(tmp_path / dt), str(bin_data / "train.txt"), str(bin_data / "test.txt"),
+                                   **kw), comm=_local(dev))
+    assert res["bf16"][1] < 0.55
+    assert abs(res["bf16"][1] - res["fp32"][1]) < 0.02, res
+
+
 def _agaricus_ytk(tmp_path):
     """The reference demo's agaricus libsvm files (bundled gzip copies, public dataset)
     converted to the ytk format with the LibSVM tool."""

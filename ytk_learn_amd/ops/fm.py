@@ -12,16 +12,20 @@ from ._ext import check_cuda, hip, ptr, stream
 
 
 def fm_forward(X, w_lin: torch.Tensor, V: torch.Tensor):
-    """(fx float64 [n], S float32 [n, k]) for the rows of SparseMatrix X; V: [F, k] view."""
+    """(fx float64 [n], S float32 [n, k]) for the rows of SparseMatrix X; V: [F, k] view,
+    float32 or bfloat16 (bf16 working copy of the SGD path: half the gathered bytes)."""
     k = V.shape[1]
     if X.device.type == "cuda" and 0 <= k <= 64:
         check_cuda(w_lin, V)
+        assert V.dtype in (torch.float32, torch.bfloat16)
         V = V.contiguous()
         fx = torch.empty(X.n, dtype=torch.float64, device=X.device)
         S = torch.empty((X.n, k), dtype=torch.float32, device=X.device)
         hip().fm_forward(ptr(X.indptr), ptr(X.indices), ptr(X.values), X.n, ptr(w_lin),
-                         ptr(V) if k > 0 else 0, k, ptr(fx), ptr(S) if k > 0 else 0, stream(w_lin))
+                         ptr(V) if k > 0 else 0, k, ptr(fx), ptr(S) if k > 0 else 0,
+                         1 if V.dtype == torch.bfloat16 else 0, stream(w_lin))
         return fx, S
+    V = V.float()
     fx = X.matmul(w_lin).double()
     S = X.matmul(V.contiguous())
     Q = X.matmul((V * V).contiguous(), square=True)
@@ -54,23 +58,30 @@ def fm_backward(X, c: torch.Tensor, S: torch.Tensor, V: torch.Tensor, g_lin: tor
 
 
 def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float, l2v: float,
-                  reg_skip: int = -1, upd_w: bool = True, bias_latent: bool = False):
+                  reg_skip: int = -1, upd_w: bool = True, bias_latent: bool = False, Vb=None):
     """One Hogwild!-style SGD step over the rows of ``indptr`` (absolute offsets into
     ``indices`` / ``values``): w_i -= lr (c_r x_i + l2w w_i), V_if -= lr (c_r x_i (S_rf - V_if x_i)
     + l2v V_if) for every entry of every row. ``V`` [F, k] / ``S`` [n, k] are None for the
     linear model. ``reg_skip``: the bias index (no regularisation; latent row frozen unless
     ``bias_latent``); ``upd_w = False`` updates only the bias among the linear weights.
     GPU: lock-free float atomics, concurrent rows race as in Hogwild!. CPU: the same
-    per-sample gradients applied as one synchronous mini-batch step."""
+    per-sample gradients applied as one synchronous mini-batch step.
+    ``Vb`` (bf16 [F, k], optional): working copy the forward read; the gradient uses its
+    values, ``V`` stays the fp32 master and the touched entries of ``Vb`` are re-rounded."""
     n = int(indptr.shape[0] - 1)
     k = 0 if V is None else int(V.shape[1])
     c = c.float().contiguous()
     if w_lin.is_cuda:
-        check_cuda(indptr, indices, values, w_lin, V, S, c)
+        check_cuda(indptr, indices, values, w_lin, V, S, c, Vb)
+        assert Vb is None or (Vb.dtype == torch.bfloat16 and Vb.shape == V.shape and Vb.is_contiguous())
         hip().fm_sgd_update(ptr(indptr), ptr(indices), ptr(values), n, ptr(w_lin), ptr(V), k, ptr(S), ptr(c),
                             float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0,
-                            1 if bias_latent else 0, stream(w_lin))
+                            1 if bias_latent else 0, ptr(Vb), stream(w_lin))
         return
+    if Vb is not None:  # CPU reference of the bf16 path: gradient from the working copy
+        V_use = Vb.float()
+    else:
+        V_use = V
     b0, e0 = int(indptr[0]), int(indptr[-1])
     rows = torch.repeat_interleave(torch.arange(n), (indptr[1:] - indptr[:-1]).long())
     idx = indices[b0:e0].long()
@@ -82,9 +93,11 @@ def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float
     if not upd_w:
         gw = torch.where(is_bias, gw, zero)
     if k > 0:
-        v = V[idx]
+        v = V_use[idx]
         gv = (cr * x)[:, None] * (S[rows] - v * x[:, None]) + torch.where(is_bias[:, None], zero, l2v * v)
         if not bias_latent:
             gv[is_bias] = 0.0
         V.index_add_(0, idx, -lr * gv)
+        if Vb is not None:
+            Vb.copy_(V)
     w_lin.index_add_(0, idx, -lr * gw)

@@ -46,6 +46,7 @@ class SGDParams:
     epochs: int = 10
     sync_every: int = 0               # batches between cross-rank weight averaging; 0 = per epoch
     seed: int = 1
+    dtype: str = "fp32"               # "bf16": FM latents read from a bf16 working copy (fp32 master)
 
     @classmethod
     def from_config(cls, c, prefix: str = "optimization.sgd.") -> "SGDParams":
@@ -53,7 +54,9 @@ class SGDParams:
         p = cls(learning_rate=c.get_double(prefix + "learning_rate", 0.05),
                 learning_rate_decay=c.get_double(prefix + "learning_rate_decay", 1.0),
                 batch_size=c.get_int(prefix + "batch_size", 65536), epochs=c.get_int(prefix + "epochs", 10),
-                sync_every=c.get_int(prefix + "sync_every", 0), seed=c.get_int(prefix + "seed", 1))
+                sync_every=c.get_int(prefix + "sync_every", 0), seed=c.get_int(prefix + "seed", 1),
+                dtype=str(c.get_string(prefix + "dtype", "fp32")).lower())
+        check(p.dtype in ("fp32", "bf16"), "%sdtype:%s must be fp32 or bf16", prefix, p.dtype)
         check(p.learning_rate > 0, "%slearning_rate:%f must > 0", prefix, p.learning_rate)
         check(0 < p.learning_rate_decay <= 1.0, "%slearning_rate_decay:%f must be in (0, 1]", prefix,
               p.learning_rate_decay)
@@ -86,6 +89,13 @@ class SGDOptimizer:
         self.l2v = float(l2[1]) if len(l2) > 1 else 0.0
         self.dump_freq = dump_freq
         self.dist = comm is not None and comm.is_dist
+        # bf16 storage (BASELINE config 4, "FM k=16 ... bf16 SGD"): the FM latent matrix is
+        # gathered from a bf16 working copy by the forward and gradient passes (half the
+        # bytes of the dominant V-row gathers); updates land in the fp32 master, whose
+        # touched entries re-round the copy; full re-sync after every weight averaging.
+        self.Vb = None
+        if sp.dtype == "bf16" and model.name == "fm" and getattr(model, "kk", 0) > 0:
+            self.Vb = torch.empty((model.F, model.kk), dtype=torch.bfloat16, device=model.w.device)
 
     # ------------------------------------------------------------------ one batch
     def _step(self, w: torch.Tensor, b: int, e: int, lr: float):
@@ -104,7 +114,8 @@ class SGDOptimizer:
         if w.is_cuda and (m.name != "fm" or m.kk <= 64):
             # fused row pass (k = 0: linear score only): fx and S = X V of the batch
             kk = m.kk if m.name == "fm" else 0
-            fx, S = fm_forward(sl, w_lin, w[F:].view(F, kk) if kk > 0 else w_lin.new_zeros((F, 0)))
+            Vf = (self.Vb if self.Vb is not None else w[F:].view(F, kk)) if kk > 0 else w_lin.new_zeros((F, 0))
+            fx, S = fm_forward(sl, w_lin, Vf)
             if kk == 0:
                 S = None
         else:
@@ -112,7 +123,7 @@ class SGDOptimizer:
             lin = w_lin[X.indices[o0:o1].long()] * X.values[o0:o1]
             fx = torch.zeros(e - b, dtype=torch.float64, device=w.device).index_add_(0, rows, lin.double())
             if m.name == "fm" and m.kk > 0:  # CPU: S = X V and the square term from index ops
-                V = w[F:].view(F, m.kk)
+                V = self.Vb.float() if self.Vb is not None else w[F:].view(F, m.kk)
                 vx = V[X.indices[o0:o1].long()] * X.values[o0:o1, None]
                 S = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx)
                 Q = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx * vx)
@@ -128,7 +139,7 @@ class SGDOptimizer:
         c = (d.weight[b:e].double() * m.loss.grad(fx, y)).float().contiguous()
         V = w[F:].view(F, m.kk) if (m.name == "fm" and m.kk > 0) else None
         fm_sgd_update(sl.indptr, X.indices, X.values, w_lin, V, S, c, lr, self.l2w, self.l2v, reg_skip, upd_w,
-                      bool(getattr(m, "bias_latent", False)))
+                      bool(getattr(m, "bias_latent", False)), Vb=self.Vb)
         if m.name == "ffm" and m.stride > 0 and getattr(m, "need_second", True):
             ffm_backward(ip, idx, val, fl, w[F:], m.nf, m.kk, (-lr * c).contiguous(), w[F:], skip_feat=m._skip)
 
@@ -136,6 +147,11 @@ class SGDOptimizer:
         if self.dist:
             self.comm.allreduce_(w)
             w.mul_(1.0 / self.comm.world)
+        self._sync_copy(w)
+
+    def _sync_copy(self, w):
+        if self.Vb is not None:
+            self.Vb.copy_(w[self.m.F:].view(self.m.F, self.m.kk))
 
     def _losses(self, w):
         t = torch.tensor([self.m.pure_loss_grad(w, None), self.m.test_pure_loss_grad(w, None)
@@ -158,6 +174,7 @@ class SGDOptimizer:
             nb_all = int(self.comm.allreduce_scalars([nb], op="max", dtype=torch.int64)[0])
         rng = np.random.default_rng(sp.seed + (self.comm.rank if self.comm is not None else 0))
         lr = sp.learning_rate
+        self._sync_copy(w)
         start = time.perf_counter()
         train_loss = test_loss = float("nan")
         rank = self.comm.rank if self.comm is not None else 0
