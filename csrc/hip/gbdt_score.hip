@@ -171,10 +171,21 @@ __device__ __forceinline__ float wave_maxf(float v) {
 }
 
 // Block reduction of (loss, weight) sums and (max|g|, max|h|); one atomic each per block.
+// Deterministic grid reduction of the (loss, weight) sums: every block stores its partial
+// into loss_acc[kAccPart + 2 * block], the last block to finish (device-scope counter at
+// loss_acc[2]) adds them in block order -- the fp64 sums are bitwise reproducible run to
+// run (float atomics would add in arrival order). (max|g|, max|h|) use integer atomicMax
+// (order independent). loss_acc must hold kAccLen doubles, zero on entry.
+constexpr int kAccPart = 4;
+constexpr int kAccMaxBlocks = 256 * 8;
+constexpr int kAccLen = kAccPart + 2 * kAccMaxBlocks;
+
 __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss_acc, float mg,
                                           float mh, float* ghmax) {
   __shared__ double s_loss[4], s_w[4];
   __shared__ float s_mg[4], s_mh[4];
+  __shared__ int s_last;
+  __shared__ double s_red[2][256];
   lsum = wave_sum(lsum);
   wsum = wave_sum(wsum);
   mg = wave_maxf(mg);
@@ -183,14 +194,37 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
   if (lane_id() == 0) { s_loss[wid] = lsum; s_w[wid] = wsum; s_mg[wid] = mg; s_mh[wid] = mh; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(&loss_acc[0], s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3]);
-    atomicAdd(&loss_acc[1], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+    double* part = loss_acc + kAccPart;
+    part[2 * blockIdx.x] = s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3];
+    part[2 * blockIdx.x + 1] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
     if (ghmax) {  // non-negative floats order like their bit patterns
       atomicMax(reinterpret_cast<unsigned*>(&ghmax[0]),
                 __float_as_uint(fmaxf(fmaxf(s_mg[0], s_mg[1]), fmaxf(s_mg[2], s_mg[3]))));
       atomicMax(reinterpret_cast<unsigned*>(&ghmax[1]),
                 __float_as_uint(fmaxf(fmaxf(s_mh[0], s_mh[1]), fmaxf(s_mh[2], s_mh[3]))));
     }
+    __threadfence();
+    const unsigned prev = atomicAdd(reinterpret_cast<unsigned*>(loss_acc + 2), 1u);
+    s_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see every block's partial
+  const volatile double* part = loss_acc + kAccPart;
+  double a = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {  // fixed order per thread
+    a += part[2 * i];
+    c += part[2 * i + 1];
+  }
+  s_red[0][threadIdx.x] = a;
+  s_red[1][threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ta = 0.0, tc = 0.0;
+    for (int t = 0; t < (int)blockDim.x; ++t) { ta += s_red[0][t]; tc += s_red[1][t]; }
+    loss_acc[0] = ta;
+    loss_acc[1] = tc;
+    *reinterpret_cast<unsigned*>(loss_acc + 2) = 0u;
   }
 }
 

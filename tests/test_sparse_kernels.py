@@ -92,12 +92,18 @@ def _pairs_dense_t(ip, ix, vv, fl, V, nf, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("J", [1, 3, 16, 31, 70])
-def test_spmm_gpu_matches_cpu(cuda, J):
+@pytest.mark.parametrize("J,one_hot,nnz", [(1, False, 12), (3, False, 12), (16, False, 12), (31, False, 12),
+                                           (70, False, 12), (1, True, 40), (1, False, 130), (5, True, 40)])
+def test_spmm_gpu_matches_cpu(cuda, J, one_hot, nnz):
+    """Segmented SpMV / SpMM (CSR rows and CSC chunks) vs the CPU index-op reference,
+    including one-hot matrices (value loads skipped) and long rows (4 loads per lane)."""
     n, F = 20000, 300
-    ip, ix, vv, _ = _rand_csr(n, F, 12, seed=J)
+    ip, ix, vv, _ = _rand_csr(n, F, nnz, seed=J)
+    if one_hot:
+        vv = torch.ones_like(vv)
     Xc = SparseMatrix(ip, ix, vv, F)
     Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    assert Xg.one_hot == one_hot
     g = torch.Generator().manual_seed(5)
     W = torch.randn((F, J), generator=g) if J > 1 else torch.randn(F, generator=g)
     Dm = torch.randn((n, J), generator=g) if J > 1 else torch.randn(n, generator=g)

@@ -488,6 +488,9 @@ def bin_assign(X, cand, coff, out, outT=None):
 # ---------------------------------------------------------------------------
 # gradients
 # ---------------------------------------------------------------------------
+ACC_LEN = 4 + 2 * 256 * 8  # == kAccLen (gbdt_score.hip): (loss, weight), counter, block partials
+
+
 def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True,
               ghmax=None):
     """Fill pred [N,K] (optional) and gh [K,N,2]; return (weighted loss sum, weight sum) as a
@@ -499,11 +502,11 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
     loss_id = LOSS_IDS[loss]
     if score.is_cuda:
         check_cuda(score, init, label, weight, pred, gh, ghmax)
-        acc = torch.zeros(2, dtype=torch.float64, device=score.device)
+        acc = torch.zeros(ACC_LEN, dtype=torch.float64, device=score.device)
         hip().grad_hess(ptr(score), ptr(init), ptr(label), ptr(weight), N, K, loss_id,
                         float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), stream(score))
-        return acc
+        return acc[:2]
     z = score.double() / score_div + init.double()
     y = label.double()
     w = weight.double() if weight is not None else torch.ones(N, dtype=torch.float64)
@@ -569,7 +572,7 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
     assert loss_id != 5 and score.shape[1] == 1
     if score.is_cuda:
         N = score.shape[0]
-        acc = torch.zeros(2, dtype=torch.float64, device=score.device)
+        acc = torch.zeros(ACC_LEN, dtype=torch.float64, device=score.device)
         if tree_arrays is None:
             tf = tt = tl = tr = tv = None
             nn = 0
@@ -583,7 +586,7 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
                         ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
                         loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), stream(score))
-        return acc
+        return acc[:2]
     if tree_arrays is not None:
         score[:, 0] += _walk_bins(bins.t(), tree_arrays)
     return grad_hess(score, init, label, weight, loss, param, score_div, pred, gh.unsqueeze(0),

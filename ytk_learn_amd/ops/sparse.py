@@ -20,8 +20,10 @@ CHUNK = 4096  # nnz per CSC chunk: balances the bias column (all rows) against s
 
 
 def _lanes(avg_nnz: float) -> int:
+    """Lanes per segment for the J == 1 kernel: each lane takes ~4 entries per pass (its four
+    loads are issued together), so L = pow2 >= avg / 4, in [4, 64]."""
     L = 1
-    while L < avg_nnz and L < 64:
+    while L * 4 < avg_nnz and L < 64:
         L <<= 1
     return max(L, 4)
 
@@ -41,6 +43,8 @@ class SparseMatrix:
         self.row_beg = self.indptr[:-1].contiguous()
         self.row_end = self.indptr[1:].contiguous()
         self.row_lanes = _lanes(self.nnz / max(self.n, 1))
+        # one-hot matrix (e.g. Criteo categorical fields): the products skip the value loads
+        self.one_hot = bool(self.nnz > 0 and bool((self.values == 1.0).all()))
         self.rows_of_nnz = torch.repeat_interleave(torch.arange(self.n, device=self.device),
                                                    self.indptr[1:] - self.indptr[:-1])
         self._csc = None
@@ -69,6 +73,17 @@ class SparseMatrix:
         self.chunk_ptr = cbeg.contiguous()
         self.n_chunks = total
         self.chunk_lanes = _lanes(self.nnz / max(total, 1))
+        # power-law columns (Criteo: a few hot features, a long tail of short columns): one
+        # lane count for all chunks idles most lanes on the tail, so J == 1 products launch
+        # three length buckets (<= 16, <= 64, longer: 4 / 16 / 64 lanes per chunk)
+        clen = (self.chunk_end - self.chunk_beg)
+        self.chunk_buckets = []
+        for lo, hi, lanes in ((0, 16, 4), (16, 64, 16), (64, 1 << 62, 64)):
+            ids = torch.nonzero((clen > lo) & (clen <= hi)).flatten().to(torch.int32).contiguous()
+            if lo == 0:  # empty chunks never exist, but keep them in the first bucket if they did
+                ids = torch.nonzero(clen <= hi).flatten().to(torch.int32).contiguous()
+            if ids.numel():
+                self.chunk_buckets.append((lanes, ids))
         self._csc = True
 
     # ------------------------------------------------------------------ products
@@ -85,9 +100,10 @@ class SparseMatrix:
         o2 = out.reshape(self.n, -1)
         if self.device.type == "cuda":
             check_cuda(W2, o2, vals)
-            hip().seg_spmm(ptr(self.row_beg), ptr(self.row_end), self.n, ptr(self.indices), ptr(vals), ptr(W2),
+            vp = 0 if (values is None and self.one_hot) else ptr(vals)
+            hip().seg_spmm(ptr(self.row_beg), ptr(self.row_end), self.n, ptr(self.indices), vp, ptr(W2),
                            W2.stride(0), J, ptr(o2), o2.stride(0), float(alpha), int(accumulate), int(square),
-                           self.row_lanes if J == 1 else min(64, J), stream(W2))
+                           self.row_lanes if J == 1 else min(64, J), 0, stream(W2))
         else:
             v = vals * vals if square else vals
             prod = W2.index_select(0, self.indices.long()) * v[:, None]
@@ -117,9 +133,14 @@ class SparseMatrix:
             part = torch.empty((max(self.n_chunks, 1), J), dtype=torch.float32, device=self.device)
             h = hip()
             s = stream(D2)
-            h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), self.n_chunks, ptr(self.csc_rows), ptr(csc_vals),
-                       ptr(D2), D2.stride(0), J, ptr(part), J, 1.0, 0, int(square),
-                       self.chunk_lanes if J == 1 else min(64, J), s)
+            vp = 0 if (values is None and self.one_hot) else ptr(csc_vals)
+            if J == 1:  # chunks bucketed by length, each bucket with its own lane count
+                for lanes, perm in self.chunk_buckets:
+                    h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), perm.numel(), ptr(self.csc_rows), vp,
+                               ptr(D2), D2.stride(0), 1, ptr(part), 1, 1.0, 0, int(square), lanes, ptr(perm), s)
+            else:
+                h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), self.n_chunks, ptr(self.csc_rows), vp,
+                           ptr(D2), D2.stride(0), J, ptr(part), J, 1.0, 0, int(square), min(64, J), 0, s)
             h.chunk_reduce(ptr(self.chunk_ptr), self.ncols, ptr(part), J, ptr(o2), o2.stride(0), float(alpha),
                            int(accumulate), s)
         else:
