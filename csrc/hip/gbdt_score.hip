@@ -114,9 +114,12 @@ struct LossOut {
   double l;
 };
 
-__device__ __forceinline__ LossOut point_loss(int loss_id, double z, double y, double p0) {
+// kLoss is a compile-time parameter of the kernels: only the selected loss's fp64 code is
+// compiled into a kernel (a runtime switch over all five kept ~200 VGPRs live: 2 waves/SIMD)
+template <int kLoss>
+__device__ __forceinline__ LossOut point_loss(double z, double y, double p0) {
   LossOut o;
-  switch (loss_id) {
+  switch (kLoss) {
     case 0: {  // sigmoid (SigmoidFunction: stable log-loss, zmax hessian clamp)
       const double az = fabs(z);
       const double e = exp(-az);
@@ -172,10 +175,11 @@ __device__ __forceinline__ float wave_maxf(float v) {
 
 // Block reduction of (loss, weight) sums and (max|g|, max|h|); one atomic each per block.
 // Deterministic grid reduction of the (loss, weight) sums: every block stores its partial
-// into loss_acc[kAccPart + 2 * block], the last block to finish (device-scope counter at
-// loss_acc[2]) adds them in block order -- the fp64 sums are bitwise reproducible run to
-// run (float atomics would add in arrival order). (max|g|, max|h|) use integer atomicMax
-// (order independent). loss_acc must hold kAccLen doubles, zero on entry.
+// into loss_acc[kAccPart + 2 * block]; acc_finish_kernel (one block, launched right after)
+// adds them in block order -- the fp64 sums are bitwise reproducible run to run (float
+// atomics would add in arrival order; a last-block-done counter serialised ~2k returning
+// atomics on one address: measured +40 us per launch). (max|g|, max|h|) use integer
+// atomicMax (order independent). loss_acc must hold kAccLen doubles.
 constexpr int kAccPart = 4;
 constexpr int kAccMaxBlocks = 256 * 8;
 constexpr int kAccLen = kAccPart + 2 * kAccMaxBlocks;
@@ -184,8 +188,6 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
                                           float mh, float* ghmax) {
   __shared__ double s_loss[4], s_w[4];
   __shared__ float s_mg[4], s_mh[4];
-  __shared__ int s_last;
-  __shared__ double s_red[2][256];
   lsum = wave_sum(lsum);
   wsum = wave_sum(wsum);
   mg = wave_maxf(mg);
@@ -203,16 +205,16 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
       atomicMax(reinterpret_cast<unsigned*>(&ghmax[1]),
                 __float_as_uint(fmaxf(fmaxf(s_mh[0], s_mh[1]), fmaxf(s_mh[2], s_mh[3]))));
     }
-    __threadfence();
-    const unsigned prev = atomicAdd(reinterpret_cast<unsigned*>(loss_acc + 2), 1u);
-    s_last = prev == gridDim.x - 1;
   }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see every block's partial
-  const volatile double* part = loss_acc + kAccPart;
+}
+
+// loss_acc[0:2] = sum over the nblocks partials, in block order (fixed per-thread strides,
+// then thread order).
+__global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ loss_acc, int nblocks) {
+  __shared__ double s_red[2][256];
+  const double* part = loss_acc + kAccPart;
   double a = 0.0, c = 0.0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {  // fixed order per thread
+  for (int i = threadIdx.x; i < nblocks; i += 256) {
     a += part[2 * i];
     c += part[2 * i + 1];
   }
@@ -221,10 +223,9 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
   __syncthreads();
   if (threadIdx.x == 0) {
     double ta = 0.0, tc = 0.0;
-    for (int t = 0; t < (int)blockDim.x; ++t) { ta += s_red[0][t]; tc += s_red[1][t]; }
+    for (int t = 0; t < 256; ++t) { ta += s_red[0][t]; tc += s_red[1][t]; }
     loss_acc[0] = ta;
     loss_acc[1] = tc;
-    *reinterpret_cast<unsigned*>(loss_acc + 2) = 0u;
   }
 }
 
@@ -258,7 +259,7 @@ __device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, con
 
 // K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
 // kDw > 0: rows of exactly kDw dwords walked in registers; kDw == 0: generic byte loads.
-template <typename BinT, int kDw>
+template <typename BinT, int kDw, int kLoss>
 __global__ __launch_bounds__(256) void tree_grad_kernel(
     const BinT* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
     const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
@@ -294,8 +295,8 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
       score[r] = s;
     }
     const float w = weight ? weight[r] : 1.f;
-    const LossOut o = point_loss(loss_id, (double)s / (double)score_div + (double)init[r], (double)label[r],
-                                 (double)p0);
+    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)init[r], (double)label[r],
+                                        (double)p0);
     lsum += (double)w * o.l;
     wsum += (double)w;
     if (pred) pred[r] = o.p;
@@ -425,13 +426,24 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
                        score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,
                        (float*)ghmax);
   } else {
-    hipLaunchKernelGGL((tree_grad_kernel<uint8_t, 0>), dim3(grid), dim3(256), 0, s,
-                       (const uint8_t*)nullptr, 0LL, (const int*)nullptr, (const int*)nullptr,
-                       (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,
-                       (float*)score, (const float*)init, (const float*)label,
-                       (const float*)weight, N, loss_id, p0, score_div, (float*)pred,
-                       (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax);
+#define YTK_GH(LID)                                                                                \
+  hipLaunchKernelGGL((tree_grad_kernel<uint8_t, 0, LID>), dim3(grid), dim3(256), 0, s,             \
+                     (const uint8_t*)nullptr, 0LL, (const int*)nullptr, (const int*)nullptr,        \
+                     (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,            \
+                     (float*)score, (const float*)init, (const float*)label,                        \
+                     (const float*)weight, N, loss_id, p0, score_div, (float*)pred,                 \
+                     (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax)
+    switch (loss_id) {
+      case 0: YTK_GH(0); break;
+      case 1: YTK_GH(1); break;
+      case 2: YTK_GH(2); break;
+      case 3: YTK_GH(3); break;
+      default: YTK_GH(4); break;
+    }
+#undef YTK_GH
   }
+  YTK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
   YTK_LAUNCH_CHECK();
 }
 
@@ -451,13 +463,23 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
   // register walk for 16/32/64-byte rows (F <= 64 uint8 features), byte loads otherwise
   const int dw = (aligned && (row_bytes == 16 || row_bytes == 32 || row_bytes == 64))
                      ? (int)(row_bytes / 4) : 0;
-#define YTK_TG_LAUNCH(BT, DW)                                                                   \
-  hipLaunchKernelGGL((tree_grad_kernel<BT, DW>), dim3(grid), dim3(256), lds, s, (const BT*)bins, \
-                     stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,            \
-                     (const int*)tright, (const float*)tval, nnodes, (float*)score,             \
-                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id, \
-                     p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,    \
+#define YTK_TG_ONE(BT, DW, LID)                                                                   \
+  hipLaunchKernelGGL((tree_grad_kernel<BT, DW, LID>), dim3(grid), dim3(256), lds, s, (const BT*)bins, \
+                     stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,                \
+                     (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
+                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
+                     p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,        \
                      (float*)ghmax)
+#define YTK_TG_LAUNCH(BT, DW)                   \
+  do {                                          \
+    switch (loss_id) {                          \
+      case 0: YTK_TG_ONE(BT, DW, 0); break;     \
+      case 1: YTK_TG_ONE(BT, DW, 1); break;     \
+      case 2: YTK_TG_ONE(BT, DW, 2); break;     \
+      case 3: YTK_TG_ONE(BT, DW, 3); break;     \
+      default: YTK_TG_ONE(BT, DW, 4); break;    \
+    }                                           \
+  } while (0)
   if (bin_bytes == 1) {
     if (dw == 4) YTK_TG_LAUNCH(uint8_t, 4);
     else if (dw == 8) YTK_TG_LAUNCH(uint8_t, 8);
@@ -470,6 +492,8 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
     else YTK_TG_LAUNCH(uint16_t, 0);
   }
 #undef YTK_TG_LAUNCH
+#undef YTK_TG_ONE
+  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
   YTK_LAUNCH_CHECK();
 }
 

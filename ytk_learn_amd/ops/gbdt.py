@@ -502,7 +502,7 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
     loss_id = LOSS_IDS[loss]
     if score.is_cuda:
         check_cuda(score, init, label, weight, pred, gh, ghmax)
-        acc = torch.zeros(ACC_LEN, dtype=torch.float64, device=score.device)
+        acc = torch.empty(ACC_LEN, dtype=torch.float64, device=score.device)  # fully written by the kernels
         hip().grad_hess(ptr(score), ptr(init), ptr(label), ptr(weight), N, K, loss_id,
                         float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), stream(score))
@@ -572,7 +572,7 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
     assert loss_id != 5 and score.shape[1] == 1
     if score.is_cuda:
         N = score.shape[0]
-        acc = torch.zeros(ACC_LEN, dtype=torch.float64, device=score.device)
+        acc = torch.empty(ACC_LEN, dtype=torch.float64, device=score.device)  # fully written by the kernels
         if tree_arrays is None:
             tf = tt = tl = tr = tv = None
             nn = 0
