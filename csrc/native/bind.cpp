@@ -123,6 +123,30 @@ PYBIND11_MODULE(_ytk_native, m) {
         return summary_to(s);
       },
       py::arg("values"), py::arg("weights"), py::arg("size") = 0);
+  m.def(
+      "csr_to_dense",
+      [](const py::array_t<int64_t, py::array::c_style | py::array::forcecast>& indptr,
+         const py::array_t<int32_t, py::array::c_style | py::array::forcecast>& feat,
+         const py::array_t<float, py::array::c_style | py::array::forcecast>& val,
+         const py::array_t<int64_t, py::array::c_style | py::array::forcecast>& lut, int64_t F, int threads) {
+        const int64_t n = indptr.size() - 1;
+        if (n < 0 || feat.size() != val.size() || (n > 0 && indptr.at(n) > feat.size()))
+          throw std::invalid_argument("csr_to_dense: inconsistent CSR arrays");
+        py::array_t<float> out({(py::ssize_t)std::max<int64_t>(n, 0), (py::ssize_t)F});
+        if (n > 0) {
+          const int64_t* ip = indptr.data();
+          const int32_t* fp = feat.data();
+          const float* vp = val.data();
+          const int64_t* lp = lut.data();
+          const int64_t nl = lut.size();
+          float* op = out.mutable_data();
+          py::gil_scoped_release nogil;
+          csr_to_dense(ip, fp, vp, n, lp, nl, F, op, threads);
+        }
+        return out;
+      },
+      py::arg("indptr"), py::arg("feat"), py::arg("val"), py::arg("lut"), py::arg("F"), py::arg("threads") = 0);
+  m.def("default_threads", &default_threads);
   m.def("wq_combine", [](const darr& a, const darr& b, int64_t size) {
     WQSummary s = WQSummary::combine(summary_from(a), summary_from(b));
     if (size > 0) s = s.prune((size_t)size);

@@ -23,6 +23,13 @@
 #include <charconv>
 #include <cmath>
 #include <cstring>
+#include <deque>
+#include <fcntl.h>
+#include <limits>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <fstream>
 #include <stdexcept>
 #include <string_view>
@@ -62,6 +69,53 @@ inline bool parse_float(sv s, float* out) {
   {
     const char c0 = s.front() == '-' && s.size() > 1 ? s[1] : s.front();
     if (c0 == 'n' || c0 == 'N' || c0 == 'i' || c0 == 'I') return false;
+  }
+  // fast exact path: [-]digits[.digits][e[+-]digits] with <= 9 significant digits and a
+  // mantissa < 2^24 and |exp10| <= 10 -- both operands exact in float, so one IEEE
+  // multiply / divide is the correctly rounded result (what from_chars / Java return)
+  {
+    const char* c = s.data();
+    const char* e = c + s.size();
+    bool neg = false;
+    if (*c == '-') { neg = true; ++c; }
+    uint32_t m = 0;
+    int nd = 0, frac = 0;
+    bool dot = false, any = false, ok = c < e;
+    for (; c < e; ++c) {
+      const unsigned d = (unsigned)(*c - '0');
+      if (d < 10) {
+        any = true;
+        if (nd || d) ++nd;
+        if (nd > 9) { ok = false; break; }
+        m = m * 10 + d;
+        frac += dot;
+      } else if (*c == '.' && !dot) {
+        dot = true;
+      } else {
+        break;
+      }
+    }
+    int ex = 0;
+    if (ok && c < e && (*c == 'e' || *c == 'E')) {
+      ++c;
+      bool eneg = false;
+      if (c < e && (*c == '-' || *c == '+')) eneg = *c++ == '-';
+      if (c == e) ok = false;
+      for (; ok && c < e; ++c) {
+        const unsigned d = (unsigned)(*c - '0');
+        if (d >= 10 || ex > 100) { ok = false; break; }
+        ex = ex * 10 + (int)d;
+      }
+      if (eneg) ex = -ex;
+    }
+    ex -= frac;
+    if (ok && any && c == e && m < (1u << 24) && ex >= -10 && ex <= 10) {
+      static const float p10[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+      float v = (float)m;
+      v = ex >= 0 ? v * p10[ex] : v / p10[-ex];
+      *out = neg ? -v : v;
+      return true;
+    }
   }
   float v;
   auto r = std::from_chars(s.data(), s.data() + s.size(), v);
@@ -129,7 +183,11 @@ struct Local {
   std::vector<int32_t> feat, field;
   // dictionary (names owned here; map keys view into `names`)
   std::vector<std::string> names;
-  std::unordered_map<std::string, int32_t> dict;
+  std::deque<std::string> store;                    // stable storage the dict keys view into
+  std::unordered_map<sv, int32_t, SvHash> dict;
+  std::vector<int64_t> stamp;                       // last line index each id appeared on
+  std::vector<int32_t> slot;                        // its position in that row
+  std::vector<int32_t> pos_guess;                   // id seen at each token position last line
   std::vector<int64_t> counts;
   std::vector<double> st_sum, st_sum2, st_max, st_min;
   std::vector<std::string> fields;
@@ -137,13 +195,16 @@ struct Local {
   int64_t n_lines = 0, n_errors = 0, n_sampled_out = 0;
   std::vector<std::string> errs;
 
-  int32_t id_of(const std::string& name, bool stats) {
+  int32_t id_of(sv name, bool stats) {
     auto it = dict.find(name);
     if (it != dict.end()) return it->second;
     const int32_t id = (int32_t)names.size();
-    names.push_back(name);
-    dict.emplace(name, id);
+    store.emplace_back(name);
+    names.emplace_back(name);
+    dict.emplace(sv(store.back()), id);
     counts.push_back(0);
+    stamp.push_back(-1);
+    slot.push_back(0);
     if (stats) {
       st_sum.push_back(0.0);
       st_sum2.push_back(0.0);
@@ -167,7 +228,7 @@ struct LineScratch {
   std::unordered_map<sv, int, SvHash> seen;      // name -> slot in kv
   std::vector<std::pair<std::string, float>> hashed;
   std::unordered_map<std::string, int> hseen;
-  std::vector<float> tmp;
+  std::vector<float> tmp, initv;
 };
 
 void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions& opt, Local& L) {
@@ -233,6 +294,10 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
           if (q2 != sv::npos) vs = vs.substr(0, q2);
           float v;
           if (name.empty() || !parse_float(vs, &v)) { bad = true; return; }
+          if (!opt.feature_hash) {  // deduplicated by dictionary id at commit
+            S.kv.emplace_back(name, v);
+            return;
+          }
           auto it = S.seen.find(name);
           if (it != S.seen.end()) S.kv[it->second].second = v;
           else {
@@ -244,7 +309,8 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
     }
     if (bad) { fail(); continue; }
     // init prediction(s)
-    std::vector<float> initv;
+    auto& initv = S.initv;
+    initv.clear();
     if (np >= 4) {
       sv is = trim(parts[3]);
       if (!is.empty()) {
@@ -263,21 +329,29 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
     L.label_ptr.push_back((int64_t)L.labels.size());
     L.init.insert(L.init.end(), initv.begin(), initv.end());
     L.init_ptr.push_back((int64_t)L.init.size());
-    auto emit = [&](const std::string& name, float v) {
-      const int32_t id = L.id_of(name, stats);
+    // row entries: first-appearance order, last value wins (stamp/slot by dictionary id)
+    const size_t row0 = L.feat.size();
+    size_t pos_k = 0;
+    auto put = [&](sv name, float v) {
+      // dense data repeats the previous line's name at each position: check that guess
+      // before hashing
+      int32_t id;
+      if (pos_k < L.pos_guess.size() && L.names[L.pos_guess[pos_k]] == name) {
+        id = L.pos_guess[pos_k];
+      } else {
+        id = L.id_of(name, stats);
+        if (pos_k < L.pos_guess.size()) L.pos_guess[pos_k] = id;
+        else L.pos_guess.push_back(id);
+      }
+      ++pos_k;
+      if (L.stamp[id] == idx) {
+        L.val[row0 + L.slot[id]] = v;
+        return;
+      }
+      L.stamp[id] = idx;
+      L.slot[id] = (int32_t)(L.feat.size() - row0);
       L.feat.push_back(id);
       L.val.push_back(v);
-      L.counts[id]++;
-      if (stats) {
-        L.st_sum[id] += v;
-        L.st_sum2[id] += (double)(v * v);
-        L.st_max[id] = std::max(L.st_max[id], (double)v);
-        L.st_min[id] = std::min(L.st_min[id], (double)v);
-      }
-      if (opt.split_field) {  // field = name prefix before field_delim (whole name if absent)
-        const size_t q = name.find(opt.field_delim);
-        L.field.push_back(L.field_of(q == std::string::npos ? name : name.substr(0, q)));
-      }
     };
     if (opt.feature_hash) {
       S.hashed.clear();
@@ -294,12 +368,24 @@ void parse_chunk(const char* p, size_t n, int64_t first_line, const ParseOptions
           S.hashed.emplace_back(std::move(hn), sign * kv.second);
         }
       }
-      for (auto& hv : S.hashed) emit(hv.first, hv.second);
+      for (auto& hv : S.hashed) put(sv(hv.first), hv.second);
     } else {
-      std::string name;
-      for (auto& kv : S.kv) {
-        name.assign(kv.first.data(), kv.first.size());
-        emit(name, kv.second);
+      for (auto& kv : S.kv) put(kv.first, kv.second);
+    }
+    for (size_t e = row0; e < L.feat.size(); ++e) {
+      const int32_t id = L.feat[e];
+      const float v = L.val[e];
+      L.counts[id]++;
+      if (stats) {
+        L.st_sum[id] += v;
+        L.st_sum2[id] += (double)(v * v);
+        L.st_max[id] = std::max(L.st_max[id], (double)v);
+        L.st_min[id] = std::min(L.st_min[id], (double)v);
+      }
+      if (opt.split_field) {  // field = name prefix before field_delim (whole name if absent)
+        const std::string& name = L.names[id];
+        const size_t q = name.find(opt.field_delim);
+        L.field.push_back(L.field_of(q == std::string::npos ? name : name.substr(0, q)));
       }
     }
     L.indptr.push_back((int64_t)L.feat.size());
@@ -320,12 +406,47 @@ int64_t count_lines(const char* p, size_t n) {
 
 }  // namespace
 
+int default_threads() {
+  // the process's CPU share, not the machine's: OMP_NUM_THREADS if set (the GPU pool sets
+  // it to the job's share), else the affinity mask
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return v;
+  }
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) return std::max(1, CPU_COUNT(&cs));
+  return (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
+void csr_to_dense(const int64_t* indptr, const int32_t* feat, const float* val, int64_t n_rows, const int64_t* lut,
+                  int64_t n_lut, int64_t F, float* out, int threads) {
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads > 0 ? threads : default_threads(),
+                                                            n_rows / 65536 + 1));
+  auto work = [&](int t) {
+    const int64_t r0 = n_rows * t / T, r1 = n_rows * (t + 1) / T;
+    std::fill(out + r0 * F, out + r1 * F, std::numeric_limits<float>::quiet_NaN());
+    for (int64_t r = r0; r < r1; ++r) {
+      float* o = out + r * F;
+      for (int64_t e = indptr[r]; e < indptr[r + 1]; ++e) {
+        const int32_t f = feat[e];
+        if (f < 0 || f >= n_lut) continue;
+        const int64_t c = lut[f];
+        if (c >= 0 && c < F) o[c] = val[e];
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
 ParseResult parse_ytk(const char* data, size_t len, const ParseOptions& opt) {
   if (opt.line_mod < 1 || opt.line_rem < 0 || opt.line_rem >= opt.line_mod)
     throw std::invalid_argument("parse_ytk: bad line sharding");
   if (opt.feature_hash && opt.hash_bucket <= 0)
     throw std::invalid_argument("parse_ytk: hash bucket_size must be > 0");
-  int T = opt.threads > 0 ? opt.threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int T = opt.threads > 0 ? opt.threads : default_threads();
   if (len < (size_t)(1 << 20)) T = 1;
   T = std::max(1, std::min(T, 64));
   // chunk boundaries at newlines
@@ -426,48 +547,85 @@ ParseResult parse_ytk(const char* data, size_t len, const ParseOptions& opt) {
       }
     }
   }
-  // concatenate rows
-  size_t nrows = 0, nnz = 0, nlab = 0, ninit = 0;
-  for (auto& L : loc) {
-    nrows += L.weight.size();
-    nnz += L.feat.size();
-    nlab += L.labels.size();
-    ninit += L.init.size();
-  }
-  R.n_rows = (int64_t)nrows;
-  R.weight.reserve(nrows);
-  R.label_ptr.reserve(nrows + 1);
-  R.init_ptr.reserve(nrows + 1);
-  R.indptr.reserve(nrows + 1);
-  R.labels.reserve(nlab);
-  R.init.reserve(ninit);
-  R.feat.reserve(nnz);
-  R.val.reserve(nnz);
-  if (opt.split_field) R.field.reserve(nnz);
-  R.label_ptr.push_back(0);
-  R.init_ptr.push_back(0);
-  R.indptr.push_back(0);
+  // concatenate rows: per-chunk output offsets, then every chunk copies (and remaps its
+  // local ids) into the preallocated result on its own thread
+  std::vector<size_t> ro(C + 1, 0), fo(C + 1, 0), lo(C + 1, 0), io(C + 1, 0);
   for (int c = 0; c < C; ++c) {
-    auto& L = loc[c];
-    const int64_t lo = (int64_t)R.labels.size(), io = (int64_t)R.init.size(),
-                  fo = (int64_t)R.feat.size();
-    R.weight.insert(R.weight.end(), L.weight.begin(), L.weight.end());
-    R.row_line.insert(R.row_line.end(), L.row_line.begin(), L.row_line.end());
-    R.labels.insert(R.labels.end(), L.labels.begin(), L.labels.end());
-    R.init.insert(R.init.end(), L.init.begin(), L.init.end());
-    for (size_t i = 1; i < L.label_ptr.size(); ++i) R.label_ptr.push_back(L.label_ptr[i] + lo);
-    for (size_t i = 1; i < L.init_ptr.size(); ++i) R.init_ptr.push_back(L.init_ptr[i] + io);
-    for (size_t i = 1; i < L.indptr.size(); ++i) R.indptr.push_back(L.indptr[i] + fo);
-    for (int32_t f : L.feat) R.feat.push_back(remap[c][f]);
-    R.val.insert(R.val.end(), L.val.begin(), L.val.end());
-    if (opt.split_field)
-      for (int32_t f : L.field) R.field.push_back(fremap[c][f]);
+    ro[c + 1] = ro[c] + loc[c].weight.size();
+    fo[c + 1] = fo[c] + loc[c].feat.size();
+    lo[c + 1] = lo[c] + loc[c].labels.size();
+    io[c + 1] = io[c] + loc[c].init.size();
+  }
+  const size_t nrows = ro[C], nnz = fo[C];
+  R.n_rows = (int64_t)nrows;
+  R.weight.resize(nrows);
+  R.row_line.resize(nrows);
+  R.label_ptr.resize(nrows + 1);
+  R.init_ptr.resize(nrows + 1);
+  R.indptr.resize(nrows + 1);
+  R.labels.resize(lo[C]);
+  R.init.resize(io[C]);
+  R.feat.resize(nnz);
+  R.val.resize(nnz);
+  if (opt.split_field) R.field.resize(nnz);
+  R.label_ptr[0] = R.init_ptr[0] = R.indptr[0] = 0;
+  auto copy_chunk = [&](int c) {
+    Local& L = loc[c];
+    const size_t r0 = ro[c];
+    std::copy(L.weight.begin(), L.weight.end(), R.weight.begin() + r0);
+    std::copy(L.row_line.begin(), L.row_line.end(), R.row_line.begin() + r0);
+    std::copy(L.labels.begin(), L.labels.end(), R.labels.begin() + lo[c]);
+    std::copy(L.init.begin(), L.init.end(), R.init.begin() + io[c]);
+    for (size_t i = 1; i < L.label_ptr.size(); ++i) R.label_ptr[r0 + i] = L.label_ptr[i] + (int64_t)lo[c];
+    for (size_t i = 1; i < L.init_ptr.size(); ++i) R.init_ptr[r0 + i] = L.init_ptr[i] + (int64_t)io[c];
+    for (size_t i = 1; i < L.indptr.size(); ++i) R.indptr[r0 + i] = L.indptr[i] + (int64_t)fo[c];
+    const int32_t* rm = remap[c].data();
+    int32_t* dst = R.feat.data() + fo[c];
+    for (size_t i = 0; i < L.feat.size(); ++i) dst[i] = rm[L.feat[i]];
+    std::copy(L.val.begin(), L.val.end(), R.val.begin() + fo[c]);
+    if (opt.split_field) {
+      const int32_t* fm = fremap[c].data();
+      for (size_t i = 0; i < L.field.size(); ++i) R.field[fo[c] + i] = fm[L.field[i]];
+    }
     L = Local();  // release
+  };
+  if (C == 1) {
+    copy_chunk(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int c = 0; c < C; ++c) th.emplace_back(copy_chunk, c);
+    for (auto& t : th) t.join();
   }
   return R;
 }
 
 ParseResult parse_ytk_files(const std::vector<std::string>& paths, const ParseOptions& opt) {
+  if (paths.size() == 1) {  // one file: parse the mapped pages in place (no 3-GB copy)
+    const int fd = ::open(paths[0].c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open data file: " + paths[0]);
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+      ::close(fd);
+      throw std::runtime_error("cannot stat data file: " + paths[0]);
+    }
+    const size_t sz = (size_t)st.st_size;
+    if (sz == 0) {
+      ::close(fd);
+      return parse_ytk("", 0, opt);
+    }
+    void* p = ::mmap(nullptr, sz, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error("cannot map data file: " + paths[0]);
+    ::madvise(p, sz, MADV_SEQUENTIAL);
+    try {
+      ParseResult r = parse_ytk(static_cast<const char*>(p), sz, opt);
+      ::munmap(p, sz);
+      return r;
+    } catch (...) {
+      ::munmap(p, sz);
+      throw;
+    }
+  }
   std::string buf;
   for (const auto& path : paths) {
     std::ifstream f(path, std::ios::binary);

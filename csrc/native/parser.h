@@ -54,6 +54,14 @@ struct ParseResult {
   std::vector<std::string> error_samples;  // first few malformed lines (for messages)
 };
 
+// Threads for host work: OMP_NUM_THREADS if set, else the CPU affinity count.
+int default_threads();
+
+// CSR rows (local feature ids) -> dense row-major float32 [n_rows, F], NaN where absent;
+// column = lut[local id] (-1 drops the feature). Multithreaded over row blocks.
+void csr_to_dense(const int64_t* indptr, const int32_t* feat, const float* val, int64_t n_rows, const int64_t* lut,
+                  int64_t n_lut, int64_t F, float* out, int threads);
+
 // Parse a whole buffer (e.g. file contents or transformed lines joined by '\n').
 ParseResult parse_ytk(const char* data, size_t len, const ParseOptions& opt);
 

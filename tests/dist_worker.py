@@ -101,10 +101,39 @@ def run_comm(comm, out, device):
                                                                                for k in set(a) | set(b)})
     rs = torch.empty(2, device=device)
     comm.reduce_scatter_(rs, torch.arange(2 * comm.world, dtype=torch.float32, device=device))
+    # keyed merge: rank r holds names f0..f(10+r), "only_r", and unicode "xé" (sum, max, min)
+    names = [f"f{i}" for i in range(10 + comm.rank)] + [f"only_{comm.rank}", "x\u00e9"]
+    vals = [[1.0, float(comm.rank), float(comm.rank)] for _ in names]
+    mn, mv = comm.merge_named(names, vals, ["sum", "max", "min"])
     if comm.rank == 0:
         with open(os.path.join(out, "res.json"), "w") as f:
             json.dump({"sum": t.tolist(), "max": m.tolist(), "gather": g.tolist(), "obj": o,
-                       "rs": rs.tolist(), "range": list(comm.shard_range(10))}, f)
+                       "rs": rs.tolist(), "range": list(comm.shard_range(10)),
+                       "merged": dict(zip(mn, mv.tolist()))}, f)
+
+
+def run_binning(comm, out, device):
+    """Batched tensor-exchange binning vs the per-feature path (and the quantile fill)."""
+    from ytk_learn_amd.models.gbdt import binning as bn
+    g = torch.Generator().manual_seed(7 + comm.rank)
+    n = 3000 + 500 * comm.rank
+    cols = [torch.randint(0, 40, (n,), generator=g).float(),               # few distinct: union path
+            torch.round(torch.randn(n, generator=g) * 100) / 10,           # many distinct: summaries
+            torch.randn(n, generator=g),
+            torch.full((n,), float(comm.rank))]
+    X = torch.stack(cols, 1).to(device)
+    w = (torch.rand(n, generator=g) + 0.5).to(device)
+    specs = [bn.SamplerSpec(max_cnt=63), bn.SamplerSpec(max_cnt=31, use_sample_weight=True),
+             bn.SamplerSpec(max_cnt=255, quantile_approximate_bin_factor=4), bn.SamplerSpec(max_cnt=8)]
+    fit = bn.BinMapper.fit(X, w, specs, comm)
+    per = [bn.feature_candidates(X[:, f].contiguous(), w, specs[f], comm) for f in range(4)]
+    Xn = X.clone()
+    Xn[::7, 1] = float("nan")
+    fill = bn.compute_missing_fill(Xn, w, "quantile@0.3", comm)
+    if comm.rank == 0:
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump({"fit": [c.tolist() for c in fit.cands], "per": [c.tolist() for c in per],
+                       "fill": fill.tolist()}, f)
 
 
 def main():
@@ -122,6 +151,8 @@ def main():
             run_linear(comm, out, dev, task)
         elif task in ("fm_sgd", "linear_sgd"):
             run_linear(comm, out, dev, task.split("_")[0], sgd=True)
+        elif task == "binning":
+            run_binning(comm, out, dev)
         elif task == "comm":
             run_comm(comm, out, dev)
         else:

@@ -136,3 +136,43 @@ def test_java_random_stream():
     assert abs(n.java_random(42, 1, 3)[0] - 0.7275636800328681) < 1e-16
     assert abs(n.java_random(42, 1, 0, 0.0, 1.0)[0] - 1.1419053154730547) < 1e-15
     assert abs(n.java_random(0, 1, 2)[0] - 0.73096776) < 1e-7
+
+
+def _nearest_f32(s):
+    """Correctly rounded float32 of a decimal string (exact rational arithmetic, ties to even)."""
+    from fractions import Fraction
+    x = Fraction(s)
+    f = np.float32(float(s))
+    best = None
+    for c in (np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))):
+        if not np.isfinite(c):
+            continue
+        d = abs(Fraction(float(c)) - x)
+        key = (d, int(np.frombuffer(np.float32(c).tobytes(), np.uint32)[0]) & 1)
+        if best is None or key < best[0]:
+            best = (key, c)
+    return best[1]
+
+
+def test_parser_float_fast_path_correctly_rounded():
+    """The parser's fast decimal path (mantissa < 2^24, |exp10| <= 10) and the from_chars
+    fallback both give the correctly rounded float32 (Java Float.parseFloat semantics)."""
+    rng = np.random.default_rng(3)
+    toks = ["0", "-0", "5.", ".5", "1e3", "1E-3", "-2.5e+2", "16777215", "16777217", "0.1", "3.4e38",
+            "1.17549435e-38", "123456789", "1234567890", "0.000001234", "9.99999e9", "7e10", "7e11", "1e-10",
+            "1e-11", "+4.25", "2.5f", "-0.0000"]
+    for _ in range(400):
+        m = int(rng.integers(0, 10 ** int(rng.integers(1, 10))))
+        e = int(rng.integers(-14, 14))
+        toks.append(f"{'-' if rng.random() < 0.3 else ''}{m}e{e}")
+        toks.append(f"{rng.normal() * 10.0 ** int(rng.integers(-6, 8)):.{int(rng.integers(1, 10))}g}")
+    line = "1###0###" + ",".join(f"f{i}:{t}" for i, t in enumerate(toks))
+    r = _parse(line + "\n")
+    assert r["n_errors"] == 0
+    got = np.asarray(r["val"], np.float32)
+    for t, g in zip(toks, got):
+        want = _nearest_f32(t.rstrip("fF").lstrip("+"))
+        assert np.float32(g).tobytes() == np.float32(want).tobytes() or (g == 0 and want == 0), (t, g, want)
+    for bad in ["-", ".", "-.", "1e", "e5", "1.2.3", "nan", "inf", "--1"]:
+        rb = _parse(f"1###0###a:{bad}\n", max_error_tol=1)
+        assert rb["n_errors"] == 1, bad

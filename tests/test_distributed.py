@@ -49,6 +49,20 @@ def test_comm_collectives_gloo(tmp_path):
     assert res["obj"] == {"k0": 1, "k1": 1, "shared": 4}
     assert res["rs"] == [0.0, 2.0]  # rank 0 gets elements [0, 2) summed over 2 ranks
     assert res["range"] == [0, 5]
+    mg = res["merged"]
+    assert mg["f0"] == [2.0, 1.0, 0.0] and mg["f10"] == [1.0, 1.0, 1.0]
+    assert mg["only_0"] == [1.0, 0.0, 0.0] and mg["only_1"] == [1.0, 1.0, 1.0]
+    assert mg["x\u00e9"] == [2.0, 1.0, 0.0] and len(mg) == 14
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_binning_tensor_exchange_matches_per_feature(tmp_path, world):
+    """BinMapper.fit's batched exchange (one distinct-count all-reduce + one ragged tensor
+    all-gather of device-pruned summaries / distinct values) == the per-feature path."""
+    res = _run("binning", tmp_path, world, extra_env={"YTK_COMM_LOG": "1"})
+    for a, b in zip(res["fit"], res["per"]):
+        assert np.array_equal(np.float32(a), np.float32(b))
+    assert all(np.isfinite(res["fill"]))
 
 
 @pytest.mark.parametrize("task", ["gbdt", "gbdt_loss"])

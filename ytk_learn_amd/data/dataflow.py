@@ -176,15 +176,13 @@ def build_dictionary(shard: RawShard, comm, filter_threshold: int, need_bias: bo
                 seen.add(n)
                 names.append(n)
         return {n: i for i, n in enumerate(names)}, names
-    local = dict(zip(shard.names, shard.counts.tolist()))
-
-    def merge(a, b):
-        for k, v in b.items():
-            a[k] = a.get(k, 0) + v
-        return a
-
-    cnt = comm.allreduce_object(local, merge) if comm is not None and comm.is_dist else local
-    keep = sorted(n for n, c in cnt.items() if c >= filter_threshold)
+    if comm is not None and comm.is_dist:
+        # hash-partitioned keyed reduction (CoreData.java:628 allreduceMap of feature counts)
+        nm, cnt = comm.merge_named(list(shard.names), np.asarray(shard.counts, np.float64), ["sum"])
+        keep = [n for n, c in zip(nm, cnt[:, 0].tolist()) if c >= filter_threshold]
+    else:
+        local = dict(zip(shard.names, shard.counts.tolist()))
+        keep = sorted(n for n, c in local.items() if c >= filter_threshold)
     if need_bias:
         keep = [n for n in keep if n != bias_name]
         names = [bias_name] + keep
@@ -237,16 +235,13 @@ def merge_stats(shard: RawShard, comm) -> Dict[str, Tuple[int, float, float, flo
     local = {n: (int(c), float(st["sum"][i]), float(st["sum2"][i]), float(st["max"][i]), float(st["min"][i]))
              for i, (n, c) in enumerate(zip(shard.names, shard.counts.tolist()))}
 
-    def merge(a, b):
-        for k, v in b.items():
-            if k in a:
-                o = a[k]
-                a[k] = (o[0] + v[0], o[1] + v[1], o[2] + v[2], max(o[3], v[3]), min(o[4], v[4]))
-            else:
-                a[k] = v
-        return a
-
-    return comm.allreduce_object(local, merge) if comm is not None and comm.is_dist else local
+    if comm is None or not comm.is_dist:
+        return local
+    # hash-partitioned keyed reduction (CoreData.java:632 allreduceMap of FeatureStat)
+    names = list(local)
+    rows = np.array([local[n] for n in names], np.float64).reshape(len(names), 5)
+    nm, red = comm.merge_named(names, rows, ["sum", "sum", "sum", "max", "min"])
+    return {n: (int(r[0]), float(r[1]), float(r[2]), float(r[3]), float(r[4])) for n, r in zip(nm, red.tolist())}
 
 
 def make_transform_nodes(stats, names: List[str], fp: FeatureParams, need_bias: bool, bias_name: str

@@ -115,6 +115,50 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
     return np.unique(out.astype(np.float32))
 
 
+def _quantile_candidates_batched(X: torch.Tensor, weight: Optional[torch.Tensor], specs: Sequence[SamplerSpec],
+                                 feats: Sequence[int], comm: Comm) -> Dict[int, np.ndarray]:
+    """sample_by_quantile for MANY features across ranks with O(1) collectives (instead of
+    per-feature object collectives of raw distinct values): per feature the sorted distinct
+    values and their weights are built on the device; ONE all-reduce of the per-feature
+    distinct counts (the reference's summed-per-worker count, SampleByQuantile.java:80);
+    features with few distinct values ship their values, the others a device-pruned
+    WQSummary of ``bin_factor * max_cnt`` entries (wquantile.cpp prune rule); all in ONE
+    ragged tensor all-gather, merged in rank order and queried on the host -- the same
+    candidates as the per-feature path."""
+    from ...utils import quantile as wq
+    loc = []
+    for f in feats:
+        sp = specs[f]
+        xs, order = torch.sort(X[:, f].contiguous())
+        vals, inv, counts = torch.unique_consecutive(xs, return_inverse=True, return_counts=True)
+        if sp.use_sample_weight and weight is not None:
+            wsum = torch.zeros(vals.numel(), dtype=torch.float64, device=X.device)
+            wsum.index_add_(0, inv, weight[order].double())
+        else:
+            wsum = counts.double()
+        loc.append((vals.double(), wsum.pow(sp.alpha)))
+    nd = torch.tensor([v.numel() for v, _ in loc], dtype=torch.int64)
+    g_distinct = comm.allreduce(nd).tolist() if comm.is_dist else nd.tolist()
+    send = []
+    for (vals, wv), f, gd in zip(loc, feats, g_distinct):
+        sp = specs[f]
+        if gd <= sp.max_cnt:
+            send.append(torch.nn.functional.pad(vals[:, None], (0, 3)))
+        else:
+            send.append(wq.device_summary(vals, wv, sp.quantile_approximate_bin_factor * sp.max_cnt))
+    parts = wq.allgather_summaries(send, comm)
+    out = {}
+    for i, (f, gd) in enumerate(zip(feats, g_distinct)):
+        sp = specs[f]
+        if gd <= sp.max_cnt:
+            out[f] = np.unique(np.concatenate([p[i][:, 0] for p in parts]).astype(np.float32))
+        else:
+            K = sp.quantile_approximate_bin_factor * sp.max_cnt
+            qs = np.arange(1, sp.max_cnt + 1, dtype=np.float64) / sp.max_cnt
+            out[f] = np.unique(wq.query(wq.merge([p[i] for p in parts], K), qs).astype(np.float32))
+    return out
+
+
 def _precision_candidates(x, spec: SamplerSpec, comm: Comm) -> np.ndarray:
     """SampleByPrecision: optional log, optional global min-max scale, truncate to
     ``dot_precision`` decimals, invert the transform (SampleByPrecision.java)."""
@@ -166,8 +210,13 @@ class BinMapper:
             comm: Comm, split_type: str = "mean", seed: int = 0) -> "BinMapper":
         F = X.shape[1]
         cands = []
+        batched = {}
+        if comm.is_dist:  # all sample_by_quantile features in one exchange
+            qf = [f for f in range(F) if specs[f].type == "sample_by_quantile"]
+            if qf:
+                batched = _quantile_candidates_batched(X, weight, specs, qf, comm)
         for f in range(F):
-            c = feature_candidates(X[:, f].contiguous(), weight, specs[f], comm, seed + f)
+            c = batched[f] if f in batched else feature_candidates(X[:, f].contiguous(), weight, specs[f], comm, seed + f)
             if c.size == 0:
                 c = np.zeros(1, np.float32)
             cands.append(np.sort(c.astype(np.float32)))
@@ -233,8 +282,10 @@ def compute_missing_fill(X: torch.Tensor, weight: Optional[torch.Tensor], spec: 
     for f in range(F):
         col = X[:, f]
         keep = ~torch.isnan(col)
-        local.append(wq.build(col[keep].double().cpu().numpy(), w[keep].double().cpu().numpy(), 4096))
-    parts = comm.allgather_object(local) if comm.is_dist else [local]
+        vals, inv = torch.unique(col[keep].double(), sorted=True, return_inverse=True)
+        ws = torch.zeros(vals.numel(), dtype=torch.float64, device=X.device).index_add_(0, inv, w[keep].double())
+        local.append(wq.device_summary(vals, ws, 4096))
+    parts = wq.allgather_summaries(local, comm)
     for f in range(F):
         s = wq.merge([p[f] for p in parts], 4096)
         if len(s):

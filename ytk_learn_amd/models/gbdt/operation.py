@@ -31,17 +31,15 @@ from .trainer import GBDTData, GBDTTrainer
 
 
 def _dense(raw: RawShard, name2idx, F: int, device) -> torch.Tensor:
+    """CSR shard -> dense [N, F] (NaN = absent) with the native multithreaded scatter
+    (csr_to_dense), then one host->device copy from pinned memory."""
+    from ...ops._ext import native
     lut = np.array([name2idx.get(n, -1) for n in raw.names], np.int64) if raw.names else np.zeros(0, np.int64)
-    gid = lut[raw.feat.astype(np.int64)] if raw.feat.size else np.zeros(0, np.int64)
-    rows = np.repeat(np.arange(raw.n_rows, dtype=np.int64), np.diff(raw.indptr))
-    keep = gid >= 0
-    X = torch.full((raw.n_rows, F), float("nan"), dtype=torch.float32, device=device)
-    if keep.any():
-        r = torch.from_numpy(rows[keep]).to(device)
-        c = torch.from_numpy(gid[keep]).to(device)
-        v = torch.from_numpy(raw.val[keep].astype(np.float32)).to(device)
-        X[r, c] = v
-    return X
+    Xh = torch.from_numpy(native().csr_to_dense(raw.indptr, raw.feat, raw.val, lut, F, 0))
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return Xh
+    return Xh.pin_memory().to(dev, non_blocking=True)
 
 
 class GBDTLoader:

@@ -92,10 +92,10 @@ class TreeRefiner:
         if self.approximate:
             # weighted mergeable summaries (WeightApproximateQuantile), on every world size
             from ...utils import quantile as wq
-            local = {nid: wq.build(v, wt, SUMMARY_POINTS) for nid, (v, wt) in local.items()}
-            parts = self.comm.allgather_object(local) if self.comm.is_dist else [local]
-            for nid in leaves:
-                sm = wq.merge([p[nid] for p in parts], SUMMARY_POINTS)
+            summ = [wq.build(*local[nid], SUMMARY_POINTS) for nid in leaves]
+            parts = wq.allgather_summaries(summ, self.comm)  # two tensor all-gathers
+            for li, nid in enumerate(leaves):
+                sm = wq.merge([p[li] for p in parts], SUMMARY_POINTS)
                 if len(sm) == 0:
                     continue
                 med = float(wq.query(sm, [0.5])[0])

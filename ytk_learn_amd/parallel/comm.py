@@ -147,6 +147,19 @@ class Comm:
         dist.all_gather_into_tensor(out, t.contiguous(), group=g)
         return out
 
+    def allgather_ragged(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """Every rank's ``t`` (dim 0 may differ per rank; trailing dims equal): one size
+        all-gather + one padded all-gather (fixed-shape tensors, RCCL-friendly)."""
+        if not self.is_dist:
+            return [t]
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        ns = self.allgather(n).tolist()
+        m = max(ns)
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        allp = self.allgather(pad)
+        return [allp[r * m: r * m + ns[r]] for r in range(self.world)]
+
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         if not self.is_dist:
             return
@@ -183,6 +196,103 @@ class Comm:
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.cpu_group)
         return lst[0]
+
+    # -- keyed merges (allreduceMap / allreduceMapSetUnion) ---------------------
+    def _a2a_bytes(self, parts: List[bytes]) -> List[bytes]:
+        """All-to-all of per-destination byte strings over the host group (uint8 tensors)."""
+        P = self.world
+        send_sizes = torch.tensor([len(b) for b in parts], dtype=torch.int64)
+        recv_sizes = torch.empty(P, dtype=torch.int64)
+        self.stats["calls"] += 2
+        dist.all_to_all_single(recv_sizes, send_sizes, group=self.cpu_group)
+        payload = b"".join(parts)
+        inp = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if payload else torch.empty(0, dtype=torch.uint8)
+        out = torch.empty(int(recv_sizes.sum()), dtype=torch.uint8)
+        self.stats["bytes"] += len(payload)
+        dist.all_to_all_single(out, inp, recv_sizes.tolist(), send_sizes.tolist(), group=self.cpu_group)
+        res, off, raw = [], 0, out.numpy().tobytes()
+        for n in recv_sizes.tolist():
+            res.append(raw[off:off + n])
+            off += n
+        return res
+
+    def merge_named(self, names: List[str], vals, ops: List[str]):
+        """Global merge of per-name value rows -- the reference's allreduceMap over
+        Map<String, T> (CoreData.java:628-632) -- with fixed-size tensor traffic instead of
+        gathering every rank's whole map: names are hash-partitioned (crc32) to an owner
+        rank (all-to-all), each owner reduces its share (column ops: "sum" | "max" |
+        "min"), and the reduced rows are all-gathered once. Returns (sorted names,
+        float64 [n, m] rows) identical on every rank."""
+        import zlib
+
+        import numpy as np
+
+        vals = np.asarray(vals, dtype=np.float64).reshape(len(names), -1)
+        m = vals.shape[1]
+
+        def reduce(nm, vv):
+            if not len(nm):
+                return [], np.zeros((0, m))
+            arr = np.asarray(nm, dtype=object)
+            order = np.argsort(arr, kind="stable")
+            arr, vv = arr[order], vv[order]
+            start = np.flatnonzero(np.r_[True, arr[1:] != arr[:-1]])
+            out = np.empty((len(start), m))
+            for j, op in enumerate(ops):
+                f = {"sum": np.add, "max": np.maximum, "min": np.minimum}[op]
+                out[:, j] = f.reduceat(vv[:, j], start)
+            return arr[start].tolist(), out
+
+        if not self.is_dist:
+            return reduce(names, vals)
+        P = self.world
+        enc = [n.encode("utf-8") for n in names]
+        owner = np.fromiter((zlib.crc32(b) % P for b in enc), dtype=np.int64, count=len(enc))
+        parts = []
+        for o in range(P):
+            idx = np.flatnonzero(owner == o)
+            blob = b"\n".join(enc[i] for i in idx)
+            head = np.array([len(idx), len(blob)], np.int64).tobytes()
+            parts.append(head + blob + vals[idx].tobytes())
+        got_names, got_vals = [], []
+        for raw in self._a2a_bytes(parts):
+            k, nb = np.frombuffer(raw[:16], np.int64)
+            if k:
+                got_names += raw[16:16 + nb].decode("utf-8").split("\n")
+                got_vals.append(np.frombuffer(raw[16 + nb:], np.float64).reshape(int(k), m))
+        mine_n, mine_v = reduce(got_names, np.concatenate(got_vals) if got_vals else np.zeros((0, m)))
+        blob = "\n".join(mine_n).encode("utf-8")
+        head = np.array([len(mine_n), len(blob)], np.int64).tobytes()
+        allp = self.allgather_bytes(head + blob + np.asarray(mine_v, np.float64).tobytes())
+        out_n, out_v = [], []
+        for raw in allp:
+            k, nb = np.frombuffer(raw[:16], np.int64)
+            if k:
+                out_n += raw[16:16 + nb].decode("utf-8").split("\n")
+                out_v.append(np.frombuffer(raw[16 + nb:], np.float64).reshape(int(k), m))
+        if not out_n:
+            return [], np.zeros((0, m))
+        arr = np.asarray(out_n, dtype=object)
+        order = np.argsort(arr, kind="stable")
+        return arr[order].tolist(), np.concatenate(out_v)[order]
+
+    def allgather_bytes(self, b: bytes) -> List[bytes]:
+        """Variable-size byte strings from every rank (two fixed-shape tensor all-gathers)."""
+        if not self.is_dist:
+            return [b]
+        n = torch.tensor([len(b)], dtype=torch.int64)
+        ns = torch.empty(self.world, dtype=torch.int64)
+        self.stats["calls"] += 2
+        dist.all_gather_into_tensor(ns, n, group=self.cpu_group)
+        mx = int(ns.max())
+        buf = torch.zeros(mx, dtype=torch.uint8)
+        if b:
+            buf[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        out = torch.empty(self.world * mx, dtype=torch.uint8)
+        self.stats["bytes"] += mx
+        dist.all_gather_into_tensor(out, buf, group=self.cpu_group)
+        raw = out.numpy().tobytes()
+        return [raw[r * mx:r * mx + int(ns[r])] for r in range(self.world)]
 
     # -- even partition helper (CommUtils.createThreadArrayFroms/Tos) ---------
     def feature_blocks(self, F: int):

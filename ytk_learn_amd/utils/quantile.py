@@ -43,8 +43,67 @@ def distributed_quantiles(values, weights, fractions, comm, size: int) -> np.nda
     """Quantiles of the union of every rank's (values, weights): local summary of ``size``
     entries, object all-gather, merge in rank order (identical on every rank), query."""
     local = build(values, weights, size)
-    parts: List[np.ndarray] = comm.allgather_object(local) if comm is not None and comm.is_dist else [local]
+    parts = [p[0] for p in allgather_summaries([local], comm)]
     return query(merge(parts, size), fractions)
+
+
+def device_summary(vals, w, size: int):
+    """``WQSummary::from_sorted`` + ``prune(size)`` (csrc/native/wquantile.cpp:22-61) on the
+    device, vectorised: ``vals`` sorted DISTINCT float64, ``w`` their float64 weights.
+    Returns float64 [m, 4] (value, rmin, rmax, wmin) on the same device.
+
+    The prune walk is monotone, so each target rank d_k = W k / (size - 1) maps to
+    i_k = first index >= 1 with mid >= d_k (clamped to n - 1) by one searchsorted; the
+    nearer of i_k - 1 / i_k is kept, duplicates dropped, first and last always kept --
+    the same entries as the sequential loop (bit-identical when the weight prefix sums
+    are exact, e.g. counts)."""
+    import torch
+
+    n = vals.numel()
+    if n == 0:
+        return torch.zeros((0, 4), dtype=torch.float64, device=vals.device)
+    cum = torch.cumsum(w, 0)
+    rmin = torch.cat([cum.new_zeros(1), cum[:-1]])
+    ent = torch.stack([vals, rmin, cum, w], 1)
+    if n <= size or size < 3:
+        return ent
+    mid = (rmin + cum) * 0.5
+    W = cum[-1]
+    k = torch.arange(1, size - 1, dtype=torch.float64, device=vals.device)
+    d = W * k / float(size - 1)
+    i = (1 + torch.searchsorted(mid[1:].contiguous(), d, right=False)).clamp_(max=n - 1)
+    a = (mid[i - 1] - d).abs()
+    b = (mid[i] - d).abs()
+    j = torch.where((i > 1) & (a < b), i - 1, i)
+    j = j[(j >= 1) & (j + 1 < n)]
+    j = torch.unique_consecutive(j)
+    idx = torch.cat([j.new_zeros(1), j, j.new_full((1,), n - 1)])
+    return ent[idx]
+
+
+def allgather_summaries(local, comm) -> List[List[np.ndarray]]:
+    """All ranks' summary lists ([rank][i] -> float64 [m_i, 4]) with two fixed-shape
+    tensor all-gathers (lengths, then the padded concatenation) instead of a pickled
+    object collective. ``local``: list of float64 [m_i, 4] numpy arrays or tensors."""
+    import torch
+
+    ts = [torch.as_tensor(np.asarray(x, np.float64).reshape(-1, 4)) if not torch.is_tensor(x) else x.double()
+          for x in local]
+    dev = ts[0].device if ts else torch.device("cpu")
+    lens = torch.tensor([t.shape[0] for t in ts], dtype=torch.int64, device=dev)
+    flat = torch.cat(ts) if ts else torch.zeros((0, 4), dtype=torch.float64, device=dev)
+    if comm is None or not comm.is_dist:
+        all_lens, all_flat = [lens], [flat]
+    else:
+        all_lens = comm.allgather(lens).view(comm.world, -1)
+        all_flat = comm.allgather_ragged(flat)
+    out = []
+    for r in range(len(all_flat)):
+        L = all_lens[r].cpu().numpy()
+        F = all_flat[r].cpu().numpy()
+        offs = np.concatenate([[0], np.cumsum(L)])
+        out.append([F[offs[i]:offs[i + 1]] for i in range(len(L))])
+    return out
 
 
 def _first_reaching(cum: "np.ndarray", target: "np.ndarray") -> "np.ndarray":
