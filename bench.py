@@ -140,6 +140,9 @@ def main():
     coll = dict(comm.stats)
     if a.profile and rank == 0:
         print(tr.timer.report() if tr.use_device_builder else tr.builder.total_stats, file=sys.stderr)
+    if rank == 0 and hasattr(tr.builder, "prof_report") and os.environ.get("YTK_LW_PROF") == "1":
+        print("leafwise planner profile (warmup + timed trees): " + json.dumps(tr.builder.prof_report()),
+              file=sys.stderr)
     tr_builder = tr.builder
     leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else (10 if world == 1 else 0)
     leaf = None

@@ -167,6 +167,21 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   }
   __syncthreads();
 
+  if (staging && w.w == 1) {
+    // the slot's ONLY item (leaf-wise engine, small nodes): store the block's sums straight
+    // into the slot -- no staging round trip, no zero fill, no reduce
+    long long* out = hist + (size_t)w.x * B * F * 2;
+    const int E = nb_lds * 32;
+    for (int i = tid; i < E; i += kHistThreads) {
+      const int bin = i >> 5, ff = fg * 32 + (i & 31);
+      if (ff < F && bin < B) {
+        const int li = 2 * (i & ~31) + hist_lds_pos(i & 31);
+        *reinterpret_cast<longlong2*>(&out[((size_t)bin * F + ff) * 2]) =
+            make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
+      }
+    }
+    return;
+  }
   if (staging) {
     // two-stage flush: plain 16-B stores of this block's partial (g, h) pairs; the slot
     // sums are formed by hist_reduce_kernel. Global u64 atomics execute at the memory
@@ -214,18 +229,69 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
 // partial with one int64 atomic per value (exact; kReduceSplit-way contention only).
 // The slots must be zero on entry.
 constexpr int kReduceSplit = 8;
+constexpr int kReduceDirect = 16;  // ranged slots with <= this many items: one block, plain stores
 
 __global__ __launch_bounds__(256) void hist_reduce_kernel(
     const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
     const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
-    int groups, int slot_base, const int* __restrict__ slot_ids) {
+    int groups, int slot_base, const int* __restrict__ slot_ids, const int* __restrict__ nslots_dev,
+    const int2* __restrict__ slot_range) {
   __shared__ int s_sel[1024];
   __shared__ int s_wcnt[4];
   __shared__ int s_n;
   const int n = nwork_dev ? min(*nwork_dev, nwork) : nwork;
+  // nslots_dev (optional): device-resident slot count (leaf-wise engine); the grid's y
+  // blocks then stride over the slots. Without it every y block owns one slot.
+  const int ny = nslots_dev ? *nslots_dev * groups : (int)gridDim.y;
+  __shared__ int s_lo, s_hi, s_cnt;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (slot_range) {
+    // ranged slots (leaf-wise engine): items [x, x + y) of each listed slot, no scan, no
+    // barriers. Slots with <= kReduceDirect items are summed by the z == 0 block and
+    // STORED (zeros included: no zero fill needed); larger ones split-K with atomics into
+    // a zeroed slot.
+    const int E = nb_lds * 32;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bin = i >> 5;
+    if (i >= E || bin >= B) return;
+    const longlong2* st = reinterpret_cast<const longlong2*>(staging);
+    for (int by = (int)blockIdx.y; by < ny; by += (int)gridDim.y) {
+      const int2 r = slot_range[by / groups];
+      const int fg = by % groups, ff = fg * 32 + (i & 31);
+      if (ff >= F) continue;
+      const bool direct = r.y <= kReduceDirect;
+      if (direct && blockIdx.z != 0) continue;
+      const int step = direct ? 1 : kReduceSplit;
+      long long g = 0, h = 0;
+      int t = direct ? 0 : (int)blockIdx.z;
+      for (; t + 7 * step < r.y; t += 8 * step) {
+        longlong2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = st[((size_t)(r.x + t + u * step) * groups + fg) * E + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
+      }
+      for (; t < r.y; t += step) {
+        const longlong2 v = st[((size_t)(r.x + t) * groups + fg) * E + i];
+        g += v.x;
+        h += v.y;
+      }
+      const int slot = slot_ids[by / groups];
+      long long* o = hist + (((size_t)slot * B + bin) * F + ff) * 2;
+      if (direct) {
+        *reinterpret_cast<longlong2*>(o) = make_longlong2(g, h);
+      } else if (g | h) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(o), (unsigned long long)g);
+        atomicAdd(reinterpret_cast<unsigned long long*>(o) + 1, (unsigned long long)h);
+      }
+    }
+    return;
+  }
+  for (int by = (int)blockIdx.y; by < ny; by += (int)gridDim.y) {
+  __syncthreads();  // the previous slot's s_sel / s_lo are still being read
   // slot_ids (optional): explicit, possibly non-contiguous target slots (recycled slot pool)
-  const int slot = slot_ids ? slot_ids[(int)blockIdx.y / groups] : slot_base + (int)blockIdx.y / groups;
-  const int fg = (int)blockIdx.y % groups;
+  const int slot = slot_ids ? slot_ids[by / groups] : slot_base + by / groups;
+  const int fg = by % groups;
   // Ordered (stable) compaction of this slot's items: the kReduceSplit blocks of a slot
   // each take a strided subset s_sel[z], s_sel[z + 8], ..., so every block must see the
   // SAME order (an LDS-atomic compaction orders items differently per block whenever a
@@ -233,10 +299,9 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   // Fast path: every caller emits a slot's items contiguously -> one pass finds the
   // range [lo, hi] (min/max of matching indices) and the match count; contiguous iff
   // count == hi - lo + 1. Otherwise fall back to the ordered compaction below.
-  __shared__ int s_lo, s_hi, s_cnt;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) { s_n = 0; s_lo = 0x7fffffff; s_hi = -1; s_cnt = 0; }
   __syncthreads();
+  // slot_range (optional): the slot's items are [x, x + y) -- no scan of the work list
   for (int k0 = 0; k0 < n; k0 += 256) {  // one LDS atomic per wave, not per item
     const int k = k0 + tid;
     const unsigned long long bal = __ballot(k < n && work[k].x == slot);
@@ -273,9 +338,9 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
 #define YTK_SEL(t) (contiguous ? lo + (t) : s_sel[(t)])
   const int E = nb_lds * 32;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E || cnt == 0) return;
+  if (i >= E || cnt == 0) continue;
   const int bin = i >> 5, ff = fg * 32 + (i & 31);
-  if (ff >= F || bin >= B) return;
+  if (ff >= F || bin >= B) continue;
   const longlong2* st = reinterpret_cast<const longlong2*>(staging);
   long long g = 0, h = 0;
   int t = (int)blockIdx.z;
@@ -295,6 +360,7 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     unsigned long long* o = reinterpret_cast<unsigned long long*>(hist + (((size_t)slot * B + bin) * F + ff) * 2);
     atomicAdd(o, (unsigned long long)g);
     atomicAdd(o + 1, (unsigned long long)h);
+  }
   }
 }
 #undef YTK_SEL
@@ -474,7 +540,43 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   const int E = nb_lds * 32;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
-                     (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids);
+                     (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids,
+                     (const int*)nullptr, (const int2*)nullptr);
+  YTK_LAUNCH_CHECK();
+}
+
+// Fully device-driven staged histogram (leaf-wise engine): work count, slot count and
+// slot ids all live on the device; the host passes only upper bounds (max_work items,
+// the y-extent of the slot reduce). Items with w == 1 are their slot's only item and are
+// stored directly; slot_ids / slot_range / *nslots_dev list the multi-item slots.
+void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
+                            uintptr_t work, int max_work, uintptr_t nwork_dev, uintptr_t hist, int B,
+                            uintptr_t scales_dev, uintptr_t staging, uintptr_t slot_ids, uintptr_t nslots_dev,
+                            uintptr_t slot_range, int reduce_y, uintptr_t stream) {
+  if (max_work <= 0) return;
+  const int groups = (F + 31) / 32;
+  const int nb_lds = B;
+  const size_t lds = (size_t)nb_lds * 64 * sizeof(unsigned long long);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    hipLaunchKernelGGL(hist_fx_kernel<true>, dim3(max_work, groups), dim3(kHistThreads), lds, s,
+                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
+                       (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f,
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
+                       (const int*)nullptr);
+  } else {
+    hipLaunchKernelGGL(hist_fx_kernel<false>, dim3(max_work, groups), dim3(kHistThreads), lds, s,
+                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                       (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f,
+                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
+                       (const int*)nullptr);
+  }
+  YTK_LAUNCH_CHECK();
+  const int E = nb_lds * 32;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
+                     dim3(256), 0, s, (const long long*)staging, (const int4*)work, max_work,
+                     (const int*)nwork_dev, (long long*)hist, B, F, nb_lds, groups, 0, (const int*)slot_ids,
+                     (const int*)nslots_dev, (const int2*)slot_range);
   YTK_LAUNCH_CHECK();
 }
 

@@ -18,22 +18,9 @@
 // on the same stream.
 #include "common.h"
 #include "gbdt_split_node.h"  // SplitOut (one definition, layout static_assert'ed there)
+#include "gbdt_tree_node.h"  // DNode, node_leaf_value
 
 namespace ytk {
-
-struct DNode {
-  double G, H;           // node sums
-  double gl, hl;         // best split: left sums
-  long long cnt_global;  // rows in the node (all ranks)
-  int begin, cnt_local;  // this rank's segment of the row permutation
-  int depth, slot;
-  int feat, bin_a, bin_b;
-  int left, right;
-  float loss_chg;
-  float value;           // leaf value (x learning rate)
-  int is_leaf;           // 1 leaf, 0 internal
-};
-static_assert(sizeof(DNode) == 88, "DNode layout");
 
 enum {
   ST_NUM_NODES = 0, ST_NUM_LEAF, ST_N_PENDING, ST_N_SPLIT, ST_N_PART, ST_N_HIST,
@@ -78,22 +65,8 @@ struct LvBufs {
   int* part_cnt;         // per split: rows of this rank's segment (single-pass partition)
 };
 
-__device__ __forceinline__ double thr_l1d(double w, double lam) {
-  if (w > lam) return w - lam;
-  if (w < -lam) return w + lam;
-  return 0.0;
-}
-
-__device__ float leaf_value(double g, double h, const LvParams& p) {
-  double v = 0.0;
-  if (h >= (double)p.mcw) {
-    v = (p.l1 == 0.f) ? -g / (h + p.l2) : -thr_l1d(g, p.l1) / (h + p.l2);
-    if (p.max_abs_leaf > 0.f) {
-      if (v > p.max_abs_leaf) v = p.max_abs_leaf;
-      else if (v < -p.max_abs_leaf) v = -p.max_abs_leaf;
-    }
-  }
-  return (float)v * p.lr;  // (float) nodeValue * learning_rate
+__device__ __forceinline__ float leaf_value(double g, double h, const LvParams& p) {
+  return node_leaf_value(g, h, p.mcw, p.l1, p.l2, p.max_abs_leaf, p.lr);
 }
 
 __device__ void reset_node(DNode& n, int depth) {

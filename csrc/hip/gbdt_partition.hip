@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
-    unsigned long long* __restrict__ cursor) {
+    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift) {
   // one chunk (<= kAtomSub * 256 rows) per block, held in registers: all loads issued
   // up front, ONE cursor reservation per block, then the scatter. The block finds its
   // (split, chunk) by binary search of first_blk (exclusive scan of the splits' chunk
@@ -269,13 +269,17 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const int tv = end - beg;
     const unsigned long long base = s_base;
     const int lofs = (int)(base & 0xffffffffull), rofs = (int)(base >> 32);
-    const int rstart = nend - rofs - (tv - tl);
+    // out_shift (leaf-wise engine): the children land in the OTHER half of a 2N-entry
+    // ping-pong buffer (per split: +N or -N), so no copy-back of the partitioned segments
+    const int sh = out_shift ? out_shift[si] : 0;
+    const int rstart = nend - rofs - (tv - tl) + sh;
+    const int lstart = nbeg + lofs + sh;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int rank = j * kPartThreads + tid;  // rank among the chunk's rows
       if (rank < tv) {
         const int lb = s_l[j * NW + wid] + lrank[j];  // left rows before this one
-        const int dst = left[j] ? nbeg + lofs + lb : rstart + (rank - lb);
+        const int dst = left[j] ? lstart + lb : rstart + (rank - lb);
         rows_out[dst] = r[j];
         gh_out[dst] = g[j];
       }
@@ -409,13 +413,14 @@ extern "C" void ytk_memset_async(uintptr_t dst, int value, long long bytes, uint
 // cursor: per split, zeroed by the caller; on return low 32 bits = left rows, high 32 =
 // right rows (scatter) or the left rows alone (count_only). first_blk: exclusive scan of
 // ceil(node_count / 2048) per split; nsplit_dev / nblocks_dev: device-resident counts;
-// grid = max_blocks (blocks past *nblocks_dev exit).
+// grid = max_blocks (blocks past *nblocks_dev exit). out_shift (optional, per split): offset
+// added to every destination position (ping-pong halves of the leaf-wise engine).
 extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long ncol, uintptr_t rows,
                                      uintptr_t rows_out, uintptr_t ghp, uintptr_t gh_out,
                                      uintptr_t first_blk, uintptr_t nsplit_dev, uintptr_t nblocks_dev,
                                      int max_blocks, uintptr_t feat, uintptr_t thr, uintptr_t node_begin,
                                      uintptr_t node_count, uintptr_t cursor, int count_only,
-                                     uintptr_t stream) {
+                                     uintptr_t out_shift, uintptr_t stream) {
   if (max_blocks <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define YTK_PART_ATOMIC(BT, SC)                                                                   \
@@ -423,7 +428,8 @@ extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long n
                      (const BT*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,  \
                      (float2*)gh_out, (const int*)first_blk, (const int*)nsplit_dev,               \
                      (const int*)nblocks_dev, (const int*)feat, (const int*)thr,                   \
-                     (const int*)node_begin, (const int*)node_count, (unsigned long long*)cursor)
+                     (const int*)node_begin, (const int*)node_count, (unsigned long long*)cursor,   \
+                     (const int*)out_shift)
   if (bin_bytes == 1) {
     if (count_only) YTK_PART_ATOMIC(uint8_t, false); else YTK_PART_ATOMIC(uint8_t, true);
   } else {

@@ -201,6 +201,7 @@ def test_native_leafwise_gpu_paths_match_python(monkeypatch, mode):
         monkeypatch.setenv("YTK_LEAF_NATIVE", native)
         monkeypatch.setenv("YTK_LEAF_FAST", fast)
         p = _params("loss", rounds=3)
+        p.device_builder = False  # the host-planned paths (the device engine is tested below)
         p.tree.max_leaf_cnt = 63
         if mode == "pool":
             p.histogram_pool_capacity = 6 * 256 * 28 * 16 / float(1 << 20)
@@ -212,6 +213,38 @@ def test_native_leafwise_gpu_paths_match_python(monkeypatch, mode):
     assert res[0] == res[1] == res[2]
     if mode == "pool":
         assert res[0][3] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 7}, {"max_depth": 5, "max_leaf_cnt": 40},
+                                {"min_split_samples": 900}, {"min_split_loss": 2.0},
+                                {"l1": 0.5, "max_abs_leaf_val": 0.3},
+                                {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6},
+                                {"max_leaf_cnt": 255}, {"spec": "0"}])
+def test_device_leafwise_matches_host(monkeypatch, kw):
+    """GPU-resident leaf-wise engine (device queue replay + planner kernels,
+    csrc/hip/gbdt_leafwise.hip) == the host-planned leaf-wise builder: model dump (node
+    ids, splits, values, statistics) and losses, bit for bit."""
+    from ytk_learn_amd.models.gbdt.device_leafwise import DeviceLeafBuilder
+    kw = dict(kw)
+    monkeypatch.setenv("YTK_LOSSGUIDE_SPEC", kw.pop("spec", "1"))
+    res = []
+    for dev_builder in (False, True):
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 63
+        for k, v in kw.items():
+            setattr(p.tree, k, v)
+        p.device_builder = dev_builder
+        tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
+        tr.train()
+        assert isinstance(tr.builder, DeviceLeafBuilder) == dev_builder
+        if dev_builder:
+            batches, expanded, overflow = tr.builder.stats()
+            assert overflow == 0 and batches >= 1 and expanded >= batches
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0][0] == res[1][0]
+    assert res[0][1:] == res[1][1:]
+    assert res[0][0].count("leaf=") > 3
 
 
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():

@@ -580,7 +580,7 @@ class TreeBuilder:
         if nblocks > 0:
             h.partition_atomic(self.binsT.data_ptr(), 1, self.binsT.shape[1], rows_in, self.rows_tmp.data_ptr(),
                                gh_in, self.gh_tmp.data_ptr(), a(5), a(6), a(6) + 4, int(nblocks), a(1), a(2),
-                               a(3), a(4), cur, 0, s)
+                               a(3), a(4), cur, 0, 0, s)
         if root:  # the root segment is every row: take the output buffers whole
             self._root_gh = None
             self.rows, self.rows_tmp = self.rows_tmp, self.rows

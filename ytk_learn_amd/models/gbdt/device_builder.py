@@ -428,7 +428,7 @@ class DeviceLevelBuilder:
                 h.partition_atomic(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
                                    gh_in, ptr(self.gh_tmp), ptr(self.part_first), off(3), off(4), npart,
                                    ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
-                                   ptr(self.part_cnt), lloc, 1 if last else 0, s)
+                                   ptr(self.part_cnt), lloc, 1 if last else 0, 0, s)
             elif last:
                 h.partition_count(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.flags),
                                   ptr(self.part_items), npart, ptr(self.part_feat), ptr(self.part_thr),

@@ -1,0 +1,305 @@
+"""GPU-resident leaf-wise (loss-guided) tree builder: no host round trip inside a tree.
+
+Same trees as :class:`.builder.TreeBuilder` with ``grow_policy="loss"`` (reference:
+``J/optimizer/gbdt/DataParallelTreeMaker.java`` make() :104-115,219-295, priority queue by
+lossChg; host equivalent ``csrc/native/leafwise.cpp``). The queue replay, the speculative
+batch choice and the child bookkeeping run in the planner kernels of
+``csrc/hip/gbdt_leafwise.hip``; partition / histogram / split reuse the level engine's
+kernels with device-resident work counts. Per batch the host only ENQUEUES a fixed
+launch sequence; it polls a done flag one batch behind (pinned copy + event), so the GPU
+always has the next batch queued and never waits for the host.
+
+Rows live in a 2N-entry ping-pong buffer: a partition writes a node's children into the
+other half at the same positions (no copy-back of the partitioned segments).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ...ops._ext import hip, ptr, stream
+from ...parallel.comm import Comm
+from ...utils.timestats import PhaseTimer
+from .builder import TimeStats, TreeParams
+from .device_builder import DNODE_DTYPE, DeviceTree
+
+LW_CAP_MAX = 2304      # speculative nodes per tree (kLwCap)
+LW_LEAF_MAX = 512      # kLwLeafMax
+LW_DONE = 8
+LW_BATCHES, LW_EXPANDED, LW_OVERFLOW = 12, 13, 11
+# st words read by the fixed-grid kernels
+W_N_SPLIT, W_N_PBLK, W_N_HIST, W_N_SITEMS, W_N_BUILD, W_N_ZERO = 3, 4, 5, 6, 7, 14
+PART_CHUNK = 2048      # rows per partition block (partition_atomic_kernel)
+REDUCE_DIRECT = 16     # kReduceDirect: slots with <= 16 staged items are stored, not atomically added
+
+
+class DeviceLeafBuilder:
+    HIST_TARGET = int(os.environ.get("YTK_HIST_TARGET", 256))
+    MIN_ROWS = int(os.environ.get("YTK_HIST_MIN_ROWS", 2048))
+    REDUCE_Y = 16       # slot reduce: y blocks striding over the batch's built slots
+    POLL_LAG = 1        # batches enqueued ahead of the done-flag check
+
+    def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
+                 params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
+        if not self.supports(bins, binsT, B, F, params, comm):
+            raise ValueError("device leaf-wise builder: unsupported configuration")
+        p = params
+        self.p = p
+        self.timer = timer if timer is not None else PhaseTimer()
+        self.bins, self.binsT = bins, binsT
+        self.dev = bins.device
+        self.N = N = bins.shape[0]
+        self.F, self.B = F, B
+        self.comm = comm or Comm.local(self.dev)
+        self.nbins_f = torch.from_numpy(np.asarray(nbins_f, np.int32)).to(self.dev)
+        ml = p.max_leaf_cnt
+        self.max_leaf = ml
+        self.max_nodes = 2 * ml - 1
+        self.cap = int(min(8 * ml + 64, LW_CAP_MAX))
+        dev = self.dev
+        i32 = lambda n: torch.zeros(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
+        mn = self.max_nodes
+        # snapshot buffer: st (64 B) | tree node table | scoring arrays (as the level engine)
+        self._snap_sizes = [64, mn * DNODE_DTYPE.itemsize] + [4 * mn] * 5
+        self.snap = torch.zeros(sum(self._snap_sizes), dtype=torch.uint8, device=dev)
+        (self.st, self.tnodes, self.tfeat, self.tthr, self.tleft, self.tright,
+         self.tval) = self._snap_views(self.snap)
+        cap = self.cap
+        self.nd_f64 = torch.zeros((5, cap), dtype=torch.float64, device=dev)  # G, H, gl, hl, cnt (as i64)
+        self.nd_i32 = torch.zeros((11, cap), dtype=torch.int32, device=dev)
+        self.nd_loss = torch.zeros(cap, dtype=torch.float32, device=dev)
+        self.heap, self.batch = i32(ml + 8), i32(ml)
+        self.part = torch.zeros((6, ml), dtype=torch.int32, device=dev)
+        self.cursor = torch.zeros(ml, dtype=torch.int64, device=dev)
+        self.hist_bound = self.HIST_TARGET + ml + 2
+        self.hist_items = i32(4 * self.hist_bound)
+        self.build_ids = i32(ml + 1)
+        self.zero_ids = i32(ml + 1)
+        self.zero_range = i32(2 * (ml + 1))
+        self.n_sitems = 2 * ml + 2
+        self.split_items = i32(4 * self.n_sitems)
+        self.item_sid = i32(self.n_sitems)
+        self.split_out = torch.zeros(self.n_sitems * 48, dtype=torch.uint8, device=dev)
+        self.split_part = torch.zeros(self.n_sitems * F * 48, dtype=torch.uint8, device=dev)
+        self.split_cnt = torch.zeros(self.n_sitems, dtype=torch.int32, device=dev)
+        self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        # histogram slots: one per speculative node (never recycled inside a tree)
+        self.hist = torch.zeros((cap, B, F, 2), dtype=torch.int64, device=dev)
+        self.slot_bytes = B * F * 16
+        groups = (F + 31) // 32
+        self.staging = torch.empty(self.hist_bound * groups * B * 32 * 2, dtype=torch.int64, device=dev)
+        self.rows2 = torch.empty(2 * N, dtype=torch.int32, device=dev)
+        self.gh2 = torch.empty((2 * N, 2), dtype=torch.float32, device=dev)
+        self.scales = torch.ones(2, dtype=torch.float32, device=dev)
+        self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
+        self.gp = p.gain_params()
+        self.max_pblocks = -(-N // PART_CHUNK) + ml + 1
+        self._done_host = torch.zeros(64, dtype=torch.int32).pin_memory()
+        self.tree_count = 0
+        self.last_keep = None
+        self.last_batches = self.last_expanded = 0
+        self.hist_miss = 0  # slots are never evicted on the device (TreeBuilder API parity)
+        self.total_stats = TimeStats()
+        self._fmask_cache = {}
+        self._lr = float(np.float32(p.learning_rate))
+        # YTK_LW_PROF=1: planner phase times + work counters accumulated on the device
+        self.prof = (torch.zeros(32, dtype=torch.int64, device=dev)
+                     if os.environ.get("YTK_LW_PROF") == "1" else None)
+        self._handle = hip().lw_create(self._ptrs(), self._ip(), self._fp())
+        self._ghmax_buf = None
+
+    # ------------------------------------------------------------------ setup
+    @staticmethod
+    def supports(bins: torch.Tensor, binsT: Optional[torch.Tensor], B: int, F: int, params: TreeParams,
+                 comm: Optional[Comm] = None) -> bool:
+        """uint8 row-major bins (B <= 256, 32-aligned stride), a column-major binsT, one
+        rank, 2 <= max_leaf_cnt <= 512 (the planner's LDS-resident queue)."""
+        if os.environ.get("YTK_DEVICE_LEAFWISE", "1") == "0":
+            return False
+        if comm is not None and comm.is_dist:
+            return False
+        if params.grow_policy != "loss" or not (2 <= params.max_leaf_cnt <= LW_LEAF_MAX):
+            return False
+        if bins.dtype != torch.uint8 or binsT is None or binsT.dtype != torch.uint8 or B > 256:
+            return False
+        stride = bins.shape[1]
+        if stride % 32 != 0 or stride < ((F + 31) // 32) * 32 or binsT.shape[0] != F or not binsT.is_contiguous():
+            return False
+        return 2 * bins.shape[0] < (1 << 31)
+
+    def _snap_views(self, buf):
+        out, off = [], 0
+        dts = [torch.int32, torch.uint8, torch.int32, torch.int32, torch.int32, torch.int32, torch.float32]
+        for sz, dt in zip(self._snap_sizes, dts):
+            out.append(buf[off:off + sz].view(dt))
+            off += sz
+        return out
+
+    def _fp(self):
+        p = self.p
+        return [float(np.float32(v)) for v in (p.min_split_loss, p.min_child_hessian_sum, p.l1, p.l2,
+                                              p.max_abs_leaf_val, p.learning_rate)]
+
+    def _ip(self):
+        p = self.p
+        spec = 1 if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
+        return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
+                self.cap, self.N]
+
+    def _ptrs(self):
+        f, i = self.nd_f64, self.nd_i32
+        nodes = [ptr(f[0]), ptr(f[1]), ptr(f[2]), ptr(f[3]), ptr(f[4])]
+        ints = [ptr(i[k]) for k in range(11)]  # begin cnt_local depth feat bin_a bin_b lc tid seq state
+        return ([ptr(self.st), ptr(self.tnodes)] + nodes + ints[:10] + [ptr(self.nd_loss), ptr(self.heap),
+                ptr(self.batch)] + [ptr(self.part[k]) for k in range(6)]
+                + [ptr(self.cursor), ptr(self.hist_items), ptr(self.build_ids), ptr(self.split_items),
+                   ptr(self.item_sid), ptr(self.split_out), ptr(self.root_cnt),
+                   ptr(self.prof) if self.prof is not None else 0, ptr(self.zero_ids), ptr(self.zero_range)])
+
+    def _lv_ptrs(self):
+        """Pointer list of the level engine's finalize / raw-tree kernels (st, nodes, arrays)."""
+        out = [0] * 26
+        out[0], out[1] = ptr(self.st), ptr(self.tnodes)
+        out[19:24] = [ptr(self.tfeat), ptr(self.tthr), ptr(self.tleft), ptr(self.tright), ptr(self.tval)]
+        return out
+
+    def _fmask(self, rng):
+        p = self.p
+        if p.feature_sample_rate < 1.0:
+            n_sam = max(1, int(round(p.feature_sample_rate * self.F)))
+            perm = rng.permutation(self.F)
+            fm = np.zeros(self.F, np.uint8)
+            fm[np.sort(perm[:n_sam])] = 1
+        else:
+            fm = np.ones(self.F, np.uint8)
+        key = fm.tobytes()
+        if key not in self._fmask_cache:
+            if len(self._fmask_cache) > 64:
+                self._fmask_cache.clear()
+            self._fmask_cache[key] = torch.from_numpy(fm).to(self.dev)
+        return self._fmask_cache[key], int(np.nonzero(fm)[0][0])
+
+    # ------------------------------------------------------------------ build
+    def _hist_split(self, h, rows_ptr, gh_ptr, fmask, f0, s):
+        st = ptr(self.st)
+        # multi-item slots are zeroed and reduced; sole-item slots are stored by the hist kernel
+        h.lw_zero_slots(ptr(self.hist), self.slot_bytes, ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
+                        REDUCE_DIRECT, 256, s)
+        h.hist_fx_staged_dev(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
+                             self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
+                             ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
+                             self.REDUCE_Y, s)
+        gp = self.gp
+        h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0, ptr(self.split_items),
+                     self.n_sitems, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"], 1.0, 1.0,
+                     st + 4 * W_N_SITEMS, ptr(self.inv_scales), ptr(self.split_part), ptr(self.split_cnt), s)
+
+    def build(self, gh: torch.Tensor, ghmax: torch.Tensor = None, ghmax_global: bool = False) -> DeviceTree:
+        """Enqueue one tree from ``gh`` [N, 2] (g, h); ``ghmax`` = max |g|, |h| (optional)."""
+        p = self.p
+        h = hip()
+        s = stream(self.bins)
+        lr = float(np.float32(p.learning_rate))
+        if lr != self._lr:
+            h.lw_set_lr(self._handle, lr)
+            self._lr = lr
+        rng = np.random.default_rng((p.seed, self.tree_count))
+        seed_rows = int(rng.integers(1 << 62))
+        sampled = p.instance_sample_rate < 1.0
+        assert gh.is_contiguous() and gh.shape == (self.N, 2)
+        if sampled:  # sampled rows first (stable), in the first half of the ping-pong buffers
+            g = torch.Generator(device=self.dev)
+            g.manual_seed(seed_rows + self.comm.rank)
+            keep = torch.rand(self.N, generator=g, device=self.dev) < p.instance_sample_rate
+            _, order = torch.sort((~keep).to(torch.int32), stable=True)
+            self.rows2[:self.N].copy_(order.to(torch.int32))
+            self.gh2[:self.N].copy_(gh.index_select(0, order))
+            self.root_cnt[0] = keep.sum()
+            self.root_cnt[1] = self.root_cnt[0]
+            self.last_keep = keep
+            rows0, gh0 = ptr(self.rows2), ptr(self.gh2)
+            mx = ghmax if (ghmax is not None and ghmax_global) else (gh.abs() * keep[:, None]).amax(dim=0)
+        else:
+            self.last_keep = None
+            self.root_cnt[0] = self.N
+            self.root_cnt[1] = self.N
+            rows0, gh0 = 0, ptr(gh)
+            mx = ghmax if ghmax is not None else gh.abs().amax(dim=0)
+        fmask, f0 = self._fmask(rng)
+        h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
+        tm = self.timer
+        tm.mark("init_stats")
+        hd = self._handle
+        h.lw_step(hd, 0, s)
+        self._hist_split(h, rows0, gh0, fmask, f0, s)
+        tm.mark("root")
+        st = ptr(self.st)
+        pend = []  # (iteration, event) of the done-flag copies in flight
+        it = 0
+        while True:
+            h.lw_step(hd, 1, s)
+            rows_in, gh_in = (rows0, gh0) if it == 0 else (ptr(self.rows2), ptr(self.gh2))
+            pt = self.part
+            h.partition_atomic(ptr(self.binsT), 1, self.binsT.shape[1], rows_in, ptr(self.rows2), gh_in,
+                               ptr(self.gh2), ptr(pt[4]), st + 4 * W_N_SPLIT, st + 4 * W_N_PBLK, self.max_pblocks,
+                               ptr(pt[0]), ptr(pt[1]), ptr(pt[2]), ptr(pt[3]), ptr(self.cursor), 0, ptr(pt[5]), s)
+            h.lw_step(hd, 2, s)
+            self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
+            slot = it % self._done_host.numel()
+            self._done_host[slot:slot + 1].copy_(self.st[LW_DONE:LW_DONE + 1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            pend.append((slot, ev))
+            it += 1
+            if len(pend) > self.POLL_LAG:
+                slot0, ev0 = pend.pop(0)
+                ev0.synchronize()
+                if int(self._done_host[slot0]) != 0:
+                    break
+            if it > 4 * self.max_leaf + 8:
+                raise RuntimeError("device leaf-wise builder did not terminate")
+        tm.mark("batches")
+        h.lv_step(4, self._lv_ptrs(), [0] * 6, [0.0] * 6, self.max_nodes, 0, s)
+        self.tree_count += 1
+        self.last_batches = it
+        snap = self.snap.clone()
+        st_t, nodes, *arrays = self._snap_views(snap)
+        return DeviceTree(nodes, st_t, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+
+    def prof_report(self) -> dict:
+        """Accumulated planner phase times (us, 100 MHz wall clock) and work counters."""
+        if self.prof is None:
+            return {}
+        v = self.prof.cpu().numpy()
+        names = ["apply", "stage", "replay", "events", "select", "expand", "writeback"]
+        out = {f"plan_{n}_us": round(float(v[i]) / 100.0, 1) for i, n in enumerate(names)}
+        out.update(plan_calls=int(v[8]), part_blocks=int(v[9]), replay_events=int(v[10]), candidates=int(v[11]),
+                   hist_rows=int(v[12]), built_slots=int(v[13]), hist_items=int(v[14]),
+                   replay_local_us=round(float(v[16]) / 100.0, 1), replay_wavemax_us=round(float(v[17]) / 100.0, 1),
+                   replay_locate_us=round(float(v[18]) / 100.0, 1), replay_remove_us=round(float(v[19]) / 100.0, 1),
+                   replay_apply_us=round(float(v[20]) / 100.0, 1), replay_pops=int(v[21]))
+        return out
+
+    def stats(self):
+        """(batches, expanded nodes, overflow flag) of the last tree (synchronises)."""
+        st = self.st.cpu().numpy()
+        return int(st[LW_BATCHES]), int(st[LW_EXPANDED]), int(st[LW_OVERFLOW])
+
+    def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
+        """Raw-threshold arrays of the LAST built tree (test-set scoring)."""
+        mn = self.max_nodes
+        out = {
+            "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nthr": torch.empty(mn, dtype=torch.float32, device=self.dev),
+            "nleft": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nright": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "ndefl": torch.empty(mn, dtype=torch.uint8, device=self.dev),
+            "nval": torch.empty(mn, dtype=torch.float32, device=self.dev),
+        }
+        hip().lv_raw_tree(self._lv_ptrs(), mn, ptr(cand), ptr(coff), ptr(fill) if fill is not None else 0,
+                          1 if split_median else 0, ptr(out["nfeat"]), ptr(out["nthr"]), ptr(out["nleft"]),
+                          ptr(out["nright"]), ptr(out["ndefl"]), ptr(out["nval"]), stream(self.bins))
+        return out

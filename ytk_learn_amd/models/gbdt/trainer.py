@@ -33,6 +33,7 @@ from ...utils.timestats import PhaseTimer, profiling_enabled
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
 from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder, node_table_to_tree
+from .device_leafwise import DeviceLeafBuilder
 from .refine import TreeRefiner
 from .tree import CandTable, GBDTModel, Tree
 
@@ -150,7 +151,15 @@ class GBDTTrainer:
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
                                    and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None
                                    and DeviceLevelBuilder.supports(self.bins, self.binsT, self.B, self.F))
-        if self.use_device_builder:
+        # leaf-wise (the reference's Higgs configuration): GPU-resident queue replay
+        use_leaf = (not self.use_device_builder and self.p.device_builder and self.dev.type == "cuda"
+                    and tp.grow_policy == "loss" and self.refiner is None
+                    and DeviceLeafBuilder.supports(self.bins, self.binsT, self.B, self.F, tp, self.comm))
+        if use_leaf:
+            self.use_device_builder = True
+            self.builder = DeviceLeafBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
+                                             timer=self.timer)
+        elif self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
                                               timer=self.timer)
         else:

@@ -338,7 +338,7 @@ def partition_atomic(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, nblocks
     check_cuda(binsT, rows, rows_out, ghp, gh_out, first_blk, hdr, feat, thr, node_begin, node_count)
     hip().partition_atomic(ptr(binsT), _bin_bytes(binsT), binsT.shape[1], ptr(rows), ptr(rows_out),
                            ptr(ghp), ptr(gh_out), ptr(first_blk), ptr(hdr), ptr(hdr) + 4, nblocks,
-                           ptr(feat), ptr(thr), ptr(node_begin), ptr(node_count), ptr(cursor), 0,
+                           ptr(feat), ptr(thr), ptr(node_begin), ptr(node_count), ptr(cursor), 0, 0,
                            stream(binsT))
     return cursor if raw else cursor & 0xFFFFFFFF
 
