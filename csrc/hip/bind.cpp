@@ -80,7 +80,9 @@ void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
+uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
+void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_zero_slots(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 // gbdt_hist.hip (device-driven staged histogram)
 void ytk_hist_fx_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
@@ -134,11 +136,13 @@ PYBIND11_MODULE(_ytk_hip, m) {
   });
   m.def("lv_scales", &ytk_lv_scales);
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 36 || ip.size() != 8 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 37 || ip.size() != 8 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
+  m.def("host_device_ptr", &ytk_host_device_ptr);
   m.def("lw_step", &ytk_lw_step);
+  m.def("lw_partition", &ytk_lw_partition);
   m.def("lw_zero_slots", &ytk_lw_zero_slots);
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
   m.attr("arch") = "gfx950";

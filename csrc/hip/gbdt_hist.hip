@@ -193,6 +193,12 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
       const int li = 2 * (i & ~31) + hist_lds_pos(i & 31);
       st[i] = make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
     }
+    if (w.w == 2 && fg == 0) {
+      // first item of a slot the split-K reduce adds into (leaf-wise engine): zero it
+      // here instead of in a separate launch (the reduce runs after this kernel)
+      longlong2* hs = reinterpret_cast<longlong2*>(hist + (size_t)w.x * B * F * 2);
+      for (int i = tid; i < B * F; i += kHistThreads) hs[i] = make_longlong2(0, 0);
+    }
     return;
   }
   long long* out = hist + (size_t)w.x * B * F * 2;
@@ -548,7 +554,8 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
 // Fully device-driven staged histogram (leaf-wise engine): work count, slot count and
 // slot ids all live on the device; the host passes only upper bounds (max_work items,
 // the y-extent of the slot reduce). Items with w == 1 are their slot's only item and are
-// stored directly; slot_ids / slot_range / *nslots_dev list the multi-item slots.
+// stored directly; items with w == 2 (first item of a slot with > kReduceDirect items)
+// zero their slot; slot_ids / slot_range / *nslots_dev list the multi-item slots.
 void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
                             uintptr_t work, int max_work, uintptr_t nwork_dev, uintptr_t hist, int B,
                             uintptr_t scales_dev, uintptr_t staging, uintptr_t slot_ids, uintptr_t nslots_dev,

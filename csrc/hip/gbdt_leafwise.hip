@@ -26,8 +26,9 @@
 // Histogram slots are never recycled inside a tree (slot = speculative node id; a
 // 255-leaf tree uses < 600 of them, ~70 MB of the 288 GB of HBM3E).
 #include "common.h"
-#include "gbdt_split_node.h"  // SplitOut
-#include "gbdt_tree_node.h"   // DNode, node_leaf_value
+#include "gbdt_partition_atomic.h"  // partition_atomic_body
+#include "gbdt_split_node.h"        // SplitOut
+#include "gbdt_tree_node.h"         // DNode, node_leaf_value
 
 #include <stdexcept>
 #include <vector>
@@ -37,7 +38,7 @@ namespace ytk {
 enum {
   LW_NUM_TNODES = 0,  // == ST_NUM_NODES of the level engine (finalize / raw-tree kernels)
   LW_NUM_LEAF, LW_N_SIDS, LW_N_SPLIT, LW_N_PBLK, LW_N_HIST, LW_N_SITEMS, LW_N_BUILD, LW_DONE,
-  LW_SEQ, LW_N_HEAP, LW_OVERFLOW, LW_BATCHES, LW_EXPANDED, LW_N_ZERO, LW_WORDS = 16
+  LW_SEQ, LW_N_HEAP, LW_OVERFLOW, LW_BATCHES, LW_EXPANDED, LW_N_ZERO, LW_PART_DONE, LW_WORDS = 16
 };
 
 constexpr int kLwThreads = 256;
@@ -45,6 +46,7 @@ constexpr int kLwCap = 2304;     // speculative nodes per tree (LDS-staged by th
 constexpr int kLwLeafMax = 512;   // max_leaf_cnt supported by the device engine
 constexpr int kLwSort = 4096;     // candidate sort width (power of two >= kLwCap)
 constexpr int kLwChunk = 2048;    // rows per partition block (partition_atomic_kernel CH)
+constexpr int kLwReduceDirect = 16;  // == kReduceDirect (gbdt_hist.hip)
 
 struct LwParams {
   int max_depth, max_leaf, min_split_samples, speculate;
@@ -71,6 +73,7 @@ struct LwBufs {
   SplitOut* split_out;         // [2 max_leaf + 2]
   const long long* root_cnt;   // [0] local rows, [1] global rows
   unsigned long long* prof;    // optional [32]: planner phase times (wall clock ticks), rows
+  int* done_host;              // host-mapped pinned int: set with LW_DONE (optional)
   int* zero_ids;               // [max_leaf + 1] built slots with != 1 histogram item
   int2* zero_range;            // [max_leaf + 1] their items [x, x + y)
 };
@@ -87,39 +90,76 @@ struct LwBufs {
 
 enum { EV_LEAF = 0, EV_SPLIT = 1, EV_LEAFIFY = 2 };
 
-// queue key: larger lossChg first, then the earlier push (seq) -- priority_queue order of
-// LeafGrower::Entry (keys are unique: every push has its own seq)
-__device__ __forceinline__ unsigned long long lw_key(float loss, int seq) {
+constexpr int kLwQueueSort = 1024;  // power of two >= kLwLeafMax + 8
+
+// pop-time leaf rules that do not depend on the running leaf count
+__device__ __forceinline__ bool lw_static_leaf(const LwParams& p, float loss, int depth, int cnt) {
+  return !(loss > p.min_split_loss) || (p.max_depth >= 0 && depth == p.max_depth) ||
+         (p.min_split_samples > 0 && cnt < p.min_split_samples);
+}
+
+constexpr unsigned long long kLwSidMask = 0xfffull;  // node id bits of a queue key
+
+// queue key: larger lossChg first, then the earlier push (smaller seq) -- the
+// priority_queue order of LeafGrower::Entry; the node id rides in the low 12 bits
+// (seq < 4096 and ids < 4096 for max_leaf <= 512; seqs are unique so the id never
+// decides the order)
+__device__ __forceinline__ unsigned long long lw_qkey(float loss, int seq, int sid) {
   unsigned u = __float_as_uint(loss);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving float -> uint
-  return ((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (unsigned)seq);
+  return ((unsigned long long)u << 32) | ((unsigned long long)(4095 - seq) << 12) | (unsigned long long)sid;
 }
 
-constexpr int kQ = (kLwLeafMax + 8 + kWave - 1) / kWave;  // queue entries per lane (registers)
-
-// one DPP step of a 64-bit max (lanes without a source keep their value)
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void lw_dpp_max(unsigned& lo, unsigned& hi) {
-  const unsigned olo = (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, kCtrl, kRowMask, 0xf, false);
-  const unsigned ohi = (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, kCtrl, kRowMask, 0xf, false);
-  const bool gt = ohi > hi || (ohi == hi && olo > lo);
-  lo = gt ? olo : lo;
-  hi = gt ? ohi : hi;
+// binary max-heap of keys in LDS, one thread
+__device__ __forceinline__ void lw_heap_push(unsigned long long* key, int n, unsigned long long k) {
+  int i = n;
+  while (i > 0) {
+    const int par = (i - 1) >> 1;
+    const unsigned long long kp = key[par];
+    if (kp >= k) break;
+    key[i] = kp;
+    i = par;
+  }
+  key[i] = k;
 }
 
-// wave-wide max of a u64 (row_shr 1/2/4/8 -> row maxima in lane 15 of each row,
-// row_bcast 15/31 -> lane 63), broadcast with readlane
-__device__ __forceinline__ unsigned long long lw_wave_max(unsigned long long v) {
-  unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-  lw_dpp_max<0x111, 0xf>(lo, hi);
-  lw_dpp_max<0x112, 0xf>(lo, hi);
-  lw_dpp_max<0x114, 0xf>(lo, hi);
-  lw_dpp_max<0x118, 0xf>(lo, hi);
-  lw_dpp_max<0x142, 0xa>(lo, hi);
-  lw_dpp_max<0x143, 0xc>(lo, hi);
-  lo = __builtin_amdgcn_readlane(lo, 63);
-  hi = __builtin_amdgcn_readlane(hi, 63);
-  return ((unsigned long long)hi << 32) | lo;
+// remove the top of a heap of n + 1 entries whose last entry k is re-inserted
+__device__ __forceinline__ void lw_heap_sift_down(unsigned long long* key, int n, unsigned long long k) {
+  if (n == 0) return;
+  int i = 0;
+  while (true) {
+    const int c = 2 * i + 1;
+    if (c >= n) break;
+    unsigned long long kc = key[c];
+    int cc = c;
+    if (c + 1 < n) {
+      const unsigned long long k2 = key[c + 1];
+      if (k2 > kc) { kc = k2; cc = c + 1; }
+    }
+    if (kc <= k) break;
+    key[i] = kc;
+    i = cc;
+  }
+  key[i] = k;
+}
+
+// block bitonic sort (descending) of a[0..n), n a power of two
+__device__ void lw_bitonic_desc(unsigned long long* a, int n) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (n >> 1); t += kLwThreads) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const unsigned long long x = a[lo], y = a[hi];
+        if ((x < y) == desc) {
+          a[lo] = y;
+          a[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 // Exclusive scan of one int per thread over the block (wave shuffles + LDS totals).
@@ -220,25 +260,29 @@ __global__ __launch_bounds__(kLwThreads) void lw_init_kernel(LwParams p, LwBufs 
     b.item_sid[0] = 0;
   }
   for (int k = threadIdx.x; k < nblk; k += kLwThreads)
-    b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), 0);
+    b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), (k == 0 && nblk > kLwReduceDirect) ? 2 : 0);
 }
 
 __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs b) {
+  // node fields the replay reads, packed: {lc, tid, depth | state << 16 | static_leaf << 24, cnt}
+  __shared__ int4 s_nd[kLwCap];
   __shared__ float s_loss[kLwCap];
-  __shared__ int s_cnt[kLwCap];
-  __shared__ int s_lc[kLwCap];
-  __shared__ int s_tid[kLwCap];
   __shared__ int s_seq[kLwCap];
-  __shared__ short s_depth[kLwCap];
-  __shared__ unsigned char s_state[kLwCap];
   __shared__ int s_hsid[kLwLeafMax + 8];
+  __shared__ unsigned long long s_akey[kLwQueueSort];        // poppable queue entries, sorted
+  __shared__ unsigned long long s_bkey[2 * kLwLeafMax + 8];  // children heap
+  __shared__ int s_uid[3 * kLwLeafMax + 16];                 // blocking entries
+  __shared__ int s_na, s_nu;
   // replay events (then reused as the candidate sort buffer: kLwSort u64 = 32 KiB)
   __shared__ unsigned long long s_buf[kLwSort];
   __shared__ int s_tmp[kLwThreads / kWave + 1];
   __shared__ int s_nev, s_blocked, s_nh, s_num_leaf, s_ntree, s_seqc, s_k, s_ncand;
   int* st = b.st;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  if (st[LW_DONE]) return;
+  const int tid = threadIdx.x;
+  if (st[LW_DONE]) {
+    if (tid == 0) st[LW_PART_DONE] = 0;
+    return;
+  }
   unsigned long long t_prev = b.prof && tid == 0 ? wall_clock64() : 0ull;
   const int nsid = st[LW_N_SIDS];
   const double mcw2 = (double)p.mcw * 2.0;
@@ -267,163 +311,122 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   LW_TICK(0);
   // B. stage what the replay reads
   for (int i = tid; i < nsid; i += kLwThreads) {
-    s_loss[i] = b.loss[i];
-    s_cnt[i] = (int)b.cnt[i];
-    s_lc[i] = b.lc[i];
-    s_tid[i] = b.tid[i];
+    const float loss = b.loss[i];
+    const int cnt = (int)b.cnt[i], depth = b.depth[i];
+    const int sl = lw_static_leaf(p, loss, depth, cnt) ? 1 : 0;
+    s_loss[i] = loss;
     s_seq[i] = b.seq[i];
-    s_depth[i] = (short)b.depth[i];
-    s_state[i] = (unsigned char)b.state[i];
+    s_nd[i] = make_int4(b.lc[i], b.tid[i], depth | (b.state[i] << 16) | (sl << 24), cnt);
   }
   int nh = st[LW_N_HEAP];
   for (int i = tid; i < nh; i += kLwThreads) s_hsid[i] = b.heap[i];
+  if (tid == 0) { s_na = 0; s_nu = 0; }
   __syncthreads();
   LW_TICK(1);
-  // C. replay the queue as far as the known gains allow (wave 0). The queue lives in
-  //    registers (entry i = slot i / 64 of lane i % 64); a pop is a register-local max,
-  //    a DPP wave max and two readlanes -- no LDS round trip on the argmax path.
+  // C. replay the queue as far as the known gains allow. Queue entries are either
+  //    POPPABLE (expanded, or a leaf by the static rules) or BLOCKING (neither): the
+  //    replay stops exactly when the best remaining entry is blocking, so blocking
+  //    entries only need their running max key (u). The poppable entries are sorted
+  //    once (block bitonic); poppable children pushed during the replay go to a small
+  //    binary heap; one lane merges the two. Keys carry the node id, node fields are
+  //    packed: a pop is three dependent LDS round trips.
   int4* s_ev = reinterpret_cast<int4*>(s_buf);  // kLwSort / 2 events
-  if (wid == 0) {
-    unsigned long long qk[kQ];
-    int qs[kQ];
-#pragma unroll
-    for (int j = 0; j < kQ; ++j) {
-      const int i = j * kWave + lane;
-      qs[j] = i < nh ? s_hsid[i] : -1;
-      qk[j] = i < nh ? lw_key(s_loss[qs[j]], s_seq[qs[j]]) : 0ull;
+  {
+    for (int i = tid; i < nh; i += kLwThreads) {
+      const int sid = s_hsid[i];
+      const int4 nd = s_nd[sid];
+      if ((nd.z >> 24) || nd.x >= 0) s_akey[atomicAdd(&s_na, 1)] = lw_qkey(s_loss[sid], s_seq[sid], sid);
+      else s_uid[atomicAdd(&s_nu, 1)] = sid;
+    }
+    __syncthreads();
+    const int na = s_na;
+    int n2 = 1;
+    while (n2 < na) n2 <<= 1;
+    for (int i = na + tid; i < n2; i += kLwThreads) s_akey[i] = 0ull;
+    __syncthreads();
+    lw_bitonic_desc(s_akey, n2);
+  }
+  LW_TICK(7);
+  if (tid == 0) {
+    const int na = s_na;
+    int nu = s_nu;
+    unsigned long long u = 0ull;
+    for (int i = 0; i < nu; ++i) {
+      const int sid = s_uid[i];
+      const unsigned long long k = lw_qkey(s_loss[sid], s_seq[sid], sid);
+      u = k > u ? k : u;
     }
     int num_leaf = st[LW_NUM_LEAF], ntree = st[LW_NUM_TNODES], seqc = st[LW_SEQ];
-    int nev = 0, blocked = -1;
-    unsigned long long r_prev = b.prof ? wall_clock64() : 0ull;
-#define LW_RTICK(slot)                                                  \
-  do {                                                                  \
-    if (b.prof) {                                                       \
-      const unsigned long long t_ = wall_clock64();                     \
-      if (lane == 0) atomicAdd(&b.prof[slot], t_ - r_prev);             \
-      r_prev = t_;                                                      \
-    }                                                                   \
-  } while (0)
-    while (nh > 0) {
-      const int used = (nh + kWave - 1) / kWave;
-      if (p.max_leaf > 0 && num_leaf == p.max_leaf) {
-        // leaf budget used: every queued node pops as a leaf (independent of the order)
-#pragma unroll
-        for (int j = 0; j < kQ; ++j) {
-          const int i = j * kWave + lane;
-          if (j < used && i < nh) {
-            const int sid = qs[j];
-            s_ev[nev + i] = make_int4(EV_LEAF, sid, s_tid[sid], 0);
-            s_state[sid] = 2;
-          }
-        }
-        nev += nh;
-        nh = 0;
-        break;
-      }
-      unsigned long long mine = 0ull;
-#pragma unroll
-      for (int j = 0; j < kQ; ++j)
-        if (j < used && qk[j] > mine) mine = qk[j];
-      LW_RTICK(16);
-      const unsigned long long best = lw_wave_max(mine);
-      LW_RTICK(17);
-      int myj = -1;
-#pragma unroll
-      for (int j = 0; j < kQ; ++j)
-        if (j < used && qk[j] == best) myj = j;
-      const int lb = (int)__ffsll((long long)__ballot(myj >= 0)) - 1;  // keys are unique
-      const int jb = __builtin_amdgcn_readlane(myj, lb);
-      int sv = 0;
-#pragma unroll
-      for (int j = 0; j < kQ; ++j)
-        if (j == jb) sv = qs[j];
-      const int sid = __builtin_amdgcn_readlane(sv, lb);
-      LW_RTICK(18);
-      const float chg = s_loss[sid];
-      const bool leaf = !(chg > p.min_split_loss) || (p.max_depth >= 0 && (int)s_depth[sid] == p.max_depth) ||
-                        (p.min_split_samples > 0 && s_cnt[sid] < p.min_split_samples);
-      const int lcs = s_lc[sid];
-      if (!leaf && lcs < 0) { blocked = sid; break; }
-      {  // remove entry (jb, lb): the last entry moves into its place
-        const int il = nh - 1, jl = il / kWave, ll = il % kWave;
-        unsigned long long kl = 0ull;
-        int sl = 0;
-#pragma unroll
-        for (int j = 0; j < kQ; ++j)
-          if (j == jl) { kl = qk[j]; sl = qs[j]; }
-        const unsigned klo = __builtin_amdgcn_readlane((unsigned)kl, ll);
-        const unsigned khi = __builtin_amdgcn_readlane((unsigned)(kl >> 32), ll);
-        const int sls = __builtin_amdgcn_readlane(sl, ll);
-#pragma unroll
-        for (int j = 0; j < kQ; ++j) {
-          if (lane == lb && j == jb) { qk[j] = ((unsigned long long)khi << 32) | klo; qs[j] = sls; }
-          if (lane == ll && j == jl) { qk[j] = 0ull; qs[j] = -1; }
-        }
-      }
-      --nh;
-      LW_RTICK(19);
-      if (leaf) {
-        if (lane == 0) {
-          s_ev[nev] = make_int4(EV_LEAF, sid, s_tid[sid], 0);
-          s_state[sid] = 2;
-        }
-        ++nev;
+    int nev = 0, blocked = -1, pa = 0, nbh = 0;
+    bool bulk = false;
+    while (true) {
+      if (p.max_leaf > 0 && num_leaf == p.max_leaf) { bulk = true; break; }
+      const unsigned long long ka = pa < na ? s_akey[pa] : 0ull;
+      const unsigned long long kb = nbh > 0 ? s_bkey[0] : 0ull;
+      const unsigned long long top = ka > kb ? ka : kb;
+      if (u > top) { blocked = (int)(u & kLwSidMask); break; }
+      if (top == 0ull) break;  // queue empty
+      const int sid = (int)(top & kLwSidMask);
+      if (ka > kb) {
+        ++pa;
       } else {
-        const int t = s_tid[sid], lt = ntree;
-        ntree += 2;
-        ++num_leaf;
-        const int l = lcs, r = lcs + 1;
-        const float loss_l = s_loss[l], loss_r = s_loss[r];
-        const bool term = (p.max_depth >= 0 && p.max_depth == (int)s_depth[l]) ||
-                          (p.max_leaf > 0 && p.max_leaf == num_leaf) ||
-                          (p.min_split_samples > 0 && s_cnt[l] < p.min_split_samples &&
-                           s_cnt[r] < p.min_split_samples);
-        if (lane == 0) {
-          s_tid[l] = lt;
-          s_tid[r] = lt + 1;
-          s_state[sid] = 2;
-          s_ev[nev] = make_int4(EV_SPLIT, sid, t, lt);
-          if (term) {
-            s_ev[nev + 1] = make_int4(EV_LEAFIFY, sid, lt, 0);
-            s_state[l] = s_state[r] = 2;
-          } else {
-            s_seq[l] = seqc;
-            s_seq[r] = seqc + 1;
-          }
-        }
-        nev += term ? 2 : 1;
-        if (!term) {  // push both children at entries nh, nh + 1
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int ip = nh + c, jp = ip / kWave, lp = ip % kWave;
-            const unsigned long long kc = lw_key(c == 0 ? loss_l : loss_r, seqc + c);
-#pragma unroll
-            for (int j = 0; j < kQ; ++j)
-              if (lane == lp && j == jp) { qk[j] = kc; qs[j] = c == 0 ? l : r; }
-          }
-          nh += 2;
-          seqc += 2;
-        }
+        --nbh;
+        lw_heap_sift_down(s_bkey, nbh, s_bkey[nbh]);
       }
-      __builtin_amdgcn_wave_barrier();
-      LW_RTICK(20);
-      if (b.prof && lane == 0) atomicAdd(&b.prof[21], 1ull);
+      const int4 nd = s_nd[sid];
+      if (nd.z >> 24) {  // leaf by the static rules
+        s_ev[nev++] = make_int4(EV_LEAF, sid, nd.y, 0);
+        s_nd[sid].z = (nd.z & 0xff00ffff) | (2 << 16);
+        continue;
+      }
+      const int t = nd.y, lt = ntree;
+      ntree += 2;
+      ++num_leaf;
+      const int l = nd.x, r = l + 1;
+      const int4 ndl = s_nd[l], ndr = s_nd[r];
+      const float loss_l = s_loss[l], loss_r = s_loss[r];
+      const bool term = (p.max_depth >= 0 && p.max_depth == (ndl.z & 0xffff)) ||
+                        (p.max_leaf > 0 && p.max_leaf == num_leaf) ||
+                        (p.min_split_samples > 0 && ndl.w < p.min_split_samples && ndr.w < p.min_split_samples);
+      s_nd[sid].z = (nd.z & 0xff00ffff) | (2 << 16);
+      s_ev[nev++] = make_int4(EV_SPLIT, sid, t, lt);
+      if (term) {
+        s_ev[nev++] = make_int4(EV_LEAFIFY, sid, lt, 0);
+        s_nd[l] = make_int4(ndl.x, lt, (ndl.z & 0xff00ffff) | (2 << 16), ndl.w);
+        s_nd[r] = make_int4(ndr.x, lt + 1, (ndr.z & 0xff00ffff) | (2 << 16), ndr.w);
+        continue;
+      }
+      s_nd[l].y = lt;
+      s_nd[r].y = lt + 1;
+      s_seq[l] = seqc;
+      s_seq[r] = seqc + 1;
+      const unsigned long long kl = lw_qkey(loss_l, seqc, l), kr = lw_qkey(loss_r, seqc + 1, r);
+      seqc += 2;
+      if ((ndl.z >> 24) || ndl.x >= 0) lw_heap_push(s_bkey, nbh++, kl);
+      else { s_uid[nu++] = l; u = kl > u ? kl : u; }
+      if ((ndr.z >> 24) || ndr.x >= 0) lw_heap_push(s_bkey, nbh++, kr);
+      else { s_uid[nu++] = r; u = kr > u ? kr : u; }
     }
-#undef LW_RTICK
-    // the remaining queue, compact in [0, nh)
-#pragma unroll
-    for (int j = 0; j < kQ; ++j) {
-      const int i = j * kWave + lane;
-      if (i < nh) s_hsid[i] = qs[j];
+    // the remaining queue: A tail, the children heap, the blocking entries
+    int nr = 0;
+    for (int i = pa; i < na; ++i) s_hsid[nr++] = (int)(s_akey[i] & kLwSidMask);
+    for (int i = 0; i < nbh; ++i) s_hsid[nr++] = (int)(s_bkey[i] & kLwSidMask);
+    for (int i = 0; i < nu; ++i) s_hsid[nr++] = s_uid[i];
+    if (bulk) {  // leaf budget used: every queued node pops as a leaf (order-independent)
+      for (int i = 0; i < nr; ++i) {
+        const int sid = s_hsid[i];
+        s_ev[nev++] = make_int4(EV_LEAF, sid, s_nd[sid].y, 0);
+        s_nd[sid].z = (s_nd[sid].z & 0xff00ffff) | (2 << 16);
+      }
+      nr = 0;
     }
-    if (lane == 0) {
-      s_nev = nev;
-      s_blocked = blocked;
-      s_nh = nh;
-      s_num_leaf = num_leaf;
-      s_ntree = ntree;
-      s_seqc = seqc;
-    }
+    s_nev = nev;
+    s_blocked = blocked;
+    s_nh = nr;
+    s_num_leaf = num_leaf;
+    s_ntree = ntree;
+    s_seqc = seqc;
+    if (b.prof) atomicAdd(&b.prof[21], (unsigned long long)(pa));
   }
   __syncthreads();
   LW_TICK(2);
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     } else if (ev.x == EV_SPLIT) {
       lw_write_node(b.tnodes[ev.z], b, sid, false, b.G[sid], b.H[sid], b.loss[sid], b.cnt[sid], ev.w, p);
     } else {  // children made leaves right away: sums from the parent's best split
-      const int l = s_lc[sid];
+      const int l = s_nd[sid].x;
       const double gl = b.gl[sid], hl = b.hl[sid];
       lw_write_node(b.tnodes[ev.z], b, l, true, gl, hl, -INFINITY, b.cnt[l], -1, p);
       lw_write_node(b.tnodes[ev.z + 1], b, l + 1, true, b.G[sid] - gl, b.H[sid] - hl, -INFINITY, b.cnt[l + 1],
@@ -463,16 +466,16 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     const int per = (nsid + kLwThreads - 1) / kLwThreads;
     const int i0 = min(nsid, tid * per), i1 = min(nsid, i0 + per);
     int c = 0;
-    for (int i = i0; i < i1; ++i)
-      c += (s_state[i] == 1 && s_lc[i] < 0 && s_loss[i] > p.min_split_loss &&
-            (p.max_depth < 0 || (int)s_depth[i] < p.max_depth) &&
-            (p.min_split_samples <= 0 || s_cnt[i] >= p.min_split_samples)) ? 1 : 0;
+    // state 1 (known gain, not final), not expanded, not a leaf by the static rules
+    auto cand = [&](int i) {
+      const int4 nd = s_nd[i];
+      return ((nd.z >> 16) & 0xff) == 1 && nd.x < 0 && (nd.z >> 24) == 0;
+    };
+    for (int i = i0; i < i1; ++i) c += cand(i) ? 1 : 0;
     int ncand;
     int pos = lw_scan(c, s_tmp, &ncand);
     for (int i = i0; i < i1; ++i) {
-      if (s_state[i] == 1 && s_lc[i] < 0 && s_loss[i] > p.min_split_loss &&
-          (p.max_depth < 0 || (int)s_depth[i] < p.max_depth) &&
-          (p.min_split_samples <= 0 || s_cnt[i] >= p.min_split_samples)) {
+      if (cand(i)) {
         unsigned u = __float_as_uint(s_loss[i]);
         u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
         s_buf[pos++] = (i == blocked) ? ~0ull
@@ -486,21 +489,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       while (n2 < ncand) n2 <<= 1;
       for (int i = ncand + tid; i < n2; i += kLwThreads) s_buf[i] = 0ull;
       __syncthreads();
-      for (int size = 2; size <= n2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int t = tid; t < (n2 >> 1); t += kLwThreads) {
-            const int lo = 2 * t - (t & (stride - 1));
-            const int hi = lo + stride;
-            const bool desc = (lo & size) == 0;
-            const unsigned long long a = s_buf[lo], c2 = s_buf[hi];
-            if ((a < c2) == desc) {
-              s_buf[lo] = c2;
-              s_buf[hi] = a;
-            }
-          }
-          __syncthreads();
-        }
-      }
+      lw_bitonic_desc(s_buf, n2);
     }
     if (tid == 0) {
       s_k = min(k, ncand);
@@ -515,7 +504,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     const unsigned long long key = s_buf[j];
     const int P = (key == ~0ull) ? blocked : (int)(0xffffffffu - (unsigned)(key & 0xffffffffull));
     const int lc = nsid + 2 * j;
-    s_lc[P] = lc;
+    s_nd[P].x = lc;
     b.batch[j] = P;
     const int dep = b.depth[P] + 1;
     for (int c = lc; c <= lc + 1; ++c) {
@@ -546,13 +535,15 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   LW_TICK(5);
   // G. write back the replay state
   for (int i = tid; i < nsid; i += kLwThreads) {
-    b.lc[i] = s_lc[i];
-    b.tid[i] = s_tid[i];
+    const int4 nd = s_nd[i];
+    b.lc[i] = nd.x;
+    b.tid[i] = nd.y;
     b.seq[i] = s_seq[i];
-    b.state[i] = s_state[i];
+    b.state[i] = (nd.z >> 16) & 0xff;
   }
   for (int i = tid; i < nh; i += kLwThreads) b.heap[i] = s_hsid[i];
   if (tid == 0) {
+    st[LW_PART_DONE] = 0;
     st[LW_NUM_LEAF] = num_leaf;
     st[LW_NUM_TNODES] = s_ntree;
     st[LW_SEQ] = s_seqc;
@@ -562,6 +553,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     st[LW_N_SIDS] = nsid + 2 * k;
     if (k == 0) {
       st[LW_DONE] = 1;
+      if (b.done_host) *(volatile int*)b.done_host = 1;  // polled by the host: no copy launch
       if (blocked >= 0) st[LW_OVERFLOW] = 1;  // cannot happen with cap >= max_leaf + 2
     } else {
       st[LW_BATCHES] += 1;
@@ -579,10 +571,10 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
 
 // Children of the batch: counts from the partition cursors, smaller child, histogram
 // chunks of the built children, split items (built, then derived = parent - built).
-__global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwBufs b) {
-  __shared__ int s_need[kLwLeafMax], s_flag[kLwLeafMax];
-  __shared__ int s_small[kLwLeafMax], s_first[kLwLeafMax], s_beg[kLwLeafMax], s_cntb[kLwLeafMax];
-  __shared__ int s_nch[kLwLeafMax], s_zflag[kLwLeafMax];
+__device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
+  // three LDS arrays only: this body also runs as the fused partition kernel's epilogue,
+  // whose occupancy its LDS footprint sets
+  __shared__ int s_need[kLwLeafMax], s_small[kLwLeafMax], s_first[kLwLeafMax];
   __shared__ int s_tmp[kLwThreads / kWave + 1];
   __shared__ unsigned long long s_total;
   int* st = b.st;
@@ -602,7 +594,8 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
   for (int j = tid; j < k; j += kLwThreads) {
     const int P = b.batch[j];
     const int L = b.lc[P], R = L + 1;
-    const int lloc = (int)(b.cursor[j] & 0xffffffffull);
+    const unsigned long long cur = __hip_atomic_load(&b.cursor[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lloc = (int)(cur & 0xffffffffull);
     const int lb = b.part_begin[j] + b.part_shift[j];
     const int rcnt = b.part_cnt[j] - lloc;
     b.begin[L] = lb;
@@ -617,8 +610,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
                       !(p.min_split_samples > 0 && lloc < p.min_split_samples && rcnt < p.min_split_samples);
     const bool left_small = lloc < rcnt;
     s_need[j] = need ? 1 : 0;
-    s_flag[j] = need ? 1 : 0;
-    s_small[j] = left_small ? L : R;
+    s_small[j] = need ? (left_small ? L : R) : -1;
     if (need) atomicAdd(&s_total, (unsigned long long)(left_small ? lloc : rcnt));
   }
   __syncthreads();
@@ -626,10 +618,10 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
   const long long total = (long long)s_total;
   const int ch = (int)max((long long)p.min_rows, (total + p.hist_target - 1) / max(1, p.hist_target));
   for (int j = tid; j < k; j += kLwThreads) {
-    if (!s_flag[j]) continue;
+    const int S = s_small[j];
+    if (S < 0) continue;
     const int kb = s_need[j];
     const int P = b.batch[j];
-    const int S = s_small[j];
     const int L = b.lc[P];
     const int G = (S == L) ? L + 1 : L;
     b.build_ids[kb] = S;
@@ -637,26 +629,23 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
     b.item_sid[kb] = S;
     b.split_items[nb + kb] = make_int4(G, P, S, 1);
     b.item_sid[nb + kb] = G;
-    s_beg[kb] = b.begin[S];
-    s_cntb[kb] = b.cnt_local[S];
-  }
-  __syncthreads();
-  for (int kb = tid; kb < nb; kb += kLwThreads) {
     // floor(rows / ch) equal chunks (between ch and 2 ch rows each): no short tail
     // chunk paying a whole 128-KiB LDS clear + flush for a few rows
-    const int c = s_cntb[kb] == 0 ? 0 : max(1, s_cntb[kb] / ch);
-    s_first[kb] = c;
-    s_nch[kb] = c;
-    s_zflag[kb] = c != 1 ? 1 : 0;  // sole-item slots are stored directly by the hist kernel
+    const int cnt = b.cnt_local[S];
+    s_first[kb] = cnt == 0 ? 0 : max(1, cnt / ch);
   }
   __syncthreads();
+  for (int kb = tid; kb < nb; kb += kLwThreads) s_need[kb] = s_first[kb] != 1 ? 1 : 0;  // multi-item slots
+  __syncthreads();
   const int nitems = lw_scan_array(s_first, nb, s_tmp);
-  const int nzero = lw_scan_array(s_zflag, nb, s_tmp);  // s_zflag = index among the multi-item slots
+  const int nzero = lw_scan_array(s_need, nb, s_tmp);  // s_need = index among the multi-item slots
+  auto nch = [&](int kb) { return (kb + 1 < nb ? s_first[kb + 1] : nitems) - s_first[kb]; };
   for (int kb = tid; kb < nb; kb += kLwThreads) {
-    if (s_nch[kb] != 1) {
-      const int z = s_zflag[kb];
+    const int c = nch(kb);
+    if (c != 1) {
+      const int z = s_need[kb];
       b.zero_ids[z] = b.build_ids[kb];
-      b.zero_range[z] = make_int2(s_first[kb], s_nch[kb]);
+      b.zero_range[z] = make_int2(s_first[kb], c);
     }
   }
   for (int q = tid; q < nitems; q += kLwThreads) {
@@ -666,11 +655,15 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
       if (s_first[mid] <= q) lo = mid; else hi = mid - 1;
     }
     const int jq = q - s_first[lo];
-    const int nc = s_nch[lo];
-    const long long cnt = s_cntb[lo];
-    const int cb = s_beg[lo] + (int)(cnt * jq / nc);
-    const int ce = s_beg[lo] + (int)(cnt * (jq + 1) / nc);
-    b.hist_items[q] = make_int4(b.build_ids[lo], cb, ce, nc == 1 ? 1 : 0);
+    const int nc = nch(lo);
+    const int S = b.build_ids[lo];
+    const int beg = b.begin[S];
+    const long long cnt = b.cnt_local[S];
+    const int cb = beg + (int)(cnt * jq / nc);
+    const int ce = beg + (int)(cnt * (jq + 1) / nc);
+    // w: 1 = the slot's only item (stored directly), 2 = first item of a split-K slot
+    // (zeroes it), 0 otherwise
+    b.hist_items[q] = make_int4(S, cb, ce, nc == 1 ? 1 : (nc > kLwReduceDirect && jq == 0 ? 2 : 0));
   }
   if (tid == 0) {
     st[LW_N_HIST] = nitems;
@@ -683,6 +676,29 @@ __global__ __launch_bounds__(kLwThreads) void lw_children_kernel(LwParams p, LwB
       atomicAdd(&b.prof[14], (unsigned long long)nitems);  // histogram items
     }
   }
+}
+
+// Partition of the batch's segments (partition_atomic_body; children written into the
+// other half of the ping-pong buffers) + the children planning, run by the LAST block to
+// finish (device-scope counter): one launch and no launch gap between the two.
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void lw_partition_kernel(LwParams p, LwBufs b, const uint8_t* binsT,
+                                                                   long long ncol, const int* rows,
+                                                                   const float2* ghp, int* rows_out,
+                                                                   float2* gh_out) {
+  partition_atomic_body<uint8_t, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
+                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
+                                       b.cursor, b.part_shift);
+  // No fences: the only cross-block data the last block reads are the split cursors,
+  // updated by RETURNING device-scope atomics (complete before this block counts itself)
+  // and read back with atomic loads. (An agent-scope release fence per block writes back
+  // the XCD's L2 on MI355X and doubled this kernel's time.)
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&b.st[LW_PART_DONE], 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  lw_children_body(p, b);
 }
 
 // hist[ids[i]] = 0 for the *n_dev listed slots (grid-stride over all their 16-B words).
@@ -716,7 +732,7 @@ extern "C" {
 // ptrs: st, tnodes, G, H, gl, hl, cnt, begin, cnt_local, depth, feat, bin_a, bin_b, lc, tid, seq,
 //       state, loss, heap, batch, part_feat, part_thr, part_begin, part_cnt, part_first,
 //       part_shift, cursor, hist_items, build_ids, split_items, item_sid, split_out, root_cnt,
-//       prof (0 = off), zero_ids, zero_range
+//       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range
 // ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N
 // fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr. Returns an engine handle.
 int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
@@ -774,6 +790,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   b.split_out = (SplitOut*)a[i++];
   b.root_cnt = (const long long*)a[i++];
   b.prof = (unsigned long long*)a[i++];
+  b.done_host = (int*)a[i++];
   b.zero_ids = (int*)a[i++];
   b.zero_range = (int2*)a[i++];
   g_lw.push_back(e);
@@ -782,16 +799,35 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
 
 void ytk_lw_set_lr(int h, float lr) { g_lw.at(h).p.lr = lr; }
 
-// which: 0 init (root), 1 plan, 2 children
+// device address of pinned host memory (hipHostMalloc'ed by the caller's allocator)
+uintptr_t ytk_host_device_ptr(uintptr_t host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(host), 0) != hipSuccess)
+    throw std::runtime_error("hipHostGetDevicePointer failed (memory not pinned?)");
+  return reinterpret_cast<uintptr_t>(d);
+}
+
+// which: 0 init (root), 1 plan
 void ytk_lw_step(int h, int which, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
     case 0: hipLaunchKernelGGL(lw_init_kernel, dim3(1), dim3(kLwThreads), 0, s, e.p, e.b); break;
     case 1: hipLaunchKernelGGL(lw_plan_kernel, dim3(1), dim3(kLwThreads), 0, s, e.p, e.b); break;
-    case 2: hipLaunchKernelGGL(lw_children_kernel, dim3(1), dim3(kLwThreads), 0, s, e.p, e.b); break;
+
     default: throw std::runtime_error("bad lw step");
   }
+  YTK_LAUNCH_CHECK();
+}
+
+// partition of the current batch (+ children planning in the last block); rows == 0:
+// identity permutation (the root batch of an unsampled tree)
+void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
+                      uintptr_t gh_out, int max_blocks, uintptr_t stream) {
+  const LwEngine& e = g_lw.at(h);
+  hipLaunchKernelGGL(lw_partition_kernel, dim3(std::max(1, std::min(max_blocks, kPartGrid))), dim3(kPartThreads),
+                     0, reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint8_t*)binsT, ncol,
+                     (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
   YTK_LAUNCH_CHECK();
 }
 

@@ -16,15 +16,13 @@
 // items[blk] = {split_idx, begin, end, blk_in_node}; rows == nullptr means the identity
 // permutation (root level without instance sampling: no iota copy).
 #include "common.h"
+#include "gbdt_partition_atomic.h"
 
 #include <algorithm>
 
 namespace ytk {
 
-constexpr int kPartThreads = 256;
 constexpr int kPartSub = 4;
-constexpr int kPartGrid = 256 * 8;  // persistent partition blocks: 8 per CU
-constexpr int kAtomSub = 8;  // single-pass partition: rows per block = 8 x 256 (one chunk)
 
 template <typename BinT>
 __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
@@ -160,15 +158,8 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
 }
 
 
-// Single-pass partition (level engine): each block holds one <= 2048-row chunk in
-// registers, gathers its go-left flags, ranks them with wave ballots, reserves its left
-// run at the front and its right run at the BACK of the node segment with ONE 64-bit
-// atomic on the split's cursor ((right << 32) | left), and scatters row ids and (g, h). No flag
-// array, no count pass, one launch: 25 B/row instead of 31 B/row and two launches.
-// Chunks land in arbitrary order inside the left / right runs (rows inside a chunk keep
-// their order): positions are a free permutation for everything downstream -- the
-// int64 histograms, split counts and leaf values are order independent, so trees are
-// bitwise identical to the stable two-pass partition.
+// Single-pass partition kernel (level engine and host-planned leaf-wise): see
+// partition_atomic_body in gbdt_partition_atomic.h.
 template <typename BinT, bool kScatter>
 __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
@@ -177,116 +168,8 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
     unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift) {
-  // one chunk (<= kAtomSub * 256 rows) per block, held in registers: all loads issued
-  // up front, ONE cursor reservation per block, then the scatter. The block finds its
-  // (split, chunk) by binary search of first_blk (exclusive scan of the splits' chunk
-  // counts) -- no per-block work list. kScatter = false: left counts only (last level).
-  constexpr int NW = kPartThreads / kWave;
-  constexpr int S = kAtomSub;
-  constexpr int CH = kAtomSub * kPartThreads;
-  constexpr int kSplitLds = 1024;  // splits whose chunk table is staged in LDS
-  __shared__ int s_l[S * NW];
-  __shared__ int s_first[kSplitLds];
-  __shared__ unsigned long long s_base;
-  __shared__ int s_tl;
-  const int nblocks = *nblocks_dev, nsplit = *nsplit_dev;
-  if ((int)blockIdx.x >= nblocks) return;
-  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
-  // Persistent blocks: the grid is capped (kPartGrid) and each block walks chunks
-  // bid, bid + gridDim.x, ... Measured: with one short-lived 4-wave block per 2048-row
-  // chunk (~5k blocks per level) the workgroup launch rate, not memory, set the time
-  // (~4 us wave lifetime, < 1/8 of the wave slots ever occupied).
-  // The chunk table is staged in LDS once per block, so locating a chunk's split costs
-  // no dependent global round trips.
-  const bool lds_tab = nsplit <= kSplitLds;
-  if (lds_tab) {
-    for (int i = tid; i < nsplit; i += kPartThreads) s_first[i] = first_blk[i];
-    __syncthreads();
-  }
-  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
-  for (int bid = (int)blockIdx.x; bid < nblocks; bid += (int)gridDim.x) {
-  int lo = 0, hi = nsplit - 1;  // last split with first_blk <= bid
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if ((lds_tab ? s_first[mid] : first_blk[mid]) <= bid) lo = mid; else hi = mid - 1;
-  }
-  const int si = lo;
-  // independent loads of the split's parameters (one round trip)
-  const int fb = first_blk[si], nbeg = node_begin[si], ncnt = node_count[si], fs = feat[si], th = thr[si];
-  const int beg = nbeg + (bid - fb) * CH;
-  const int end = min(beg + CH, nbeg + ncnt);
-  const int nend = nbeg + ncnt;
-  const BinT* col = binsT + (size_t)fs * ncol;
-  // valid rows form a prefix of the chunk in position order: the rank of a valid row
-  // among the chunk's rows is simply j * 256 + tid (no ballot needed)
-  int r[S];
-  float2 g[S];
-  bool left[S];
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const int pos = beg + j * kPartThreads + tid;
-    r[j] = pos < end ? (rows ? rows[pos] : pos) : 0;
-  }
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const int pos = beg + j * kPartThreads + tid;
-    const bool valid = pos < end;
-    g[j] = (kScatter && valid) ? ghp[pos] : make_float2(0.f, 0.f);
-    left[j] = valid && (int)col[(unsigned)r[j]] <= th;
-  }
-  int lrank[S];
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const unsigned long long lm = __ballot(left[j]);
-    lrank[j] = __popcll(lm & lt_mask);
-    if (l == 0) s_l[j * NW + wid] = __popcll(lm);
-  }
-  __syncthreads();
-  // exclusive scan of the S * NW (= 32) per-(sub-chunk, wave) left counts by wave 0
-  if (wid == 0) {
-    const int x = l < S * NW ? s_l[l] : 0;
-    int incl = x;
-#pragma unroll
-    for (int off = 1; off < S * NW; off <<= 1) {
-      const int y = __shfl_up(incl, off, kWave);
-      if (l >= off) incl += y;
-    }
-    if (l < S * NW) s_l[l] = incl - x;
-    const int tl_all = __shfl(incl, S * NW - 1, kWave);
-    if (l == 0) {
-      const int tv = end - beg;
-      if (!kScatter) {
-        atomicAdd(&cursor[si], (unsigned long long)tl_all);  // count-only: the left rows
-      } else {
-        s_base = atomicAdd(&cursor[si], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
-        s_tl = tl_all;
-      }
-    }
-  }
-  __syncthreads();
-  if (kScatter) {
-    const int tl = s_tl;
-    const int tv = end - beg;
-    const unsigned long long base = s_base;
-    const int lofs = (int)(base & 0xffffffffull), rofs = (int)(base >> 32);
-    // out_shift (leaf-wise engine): the children land in the OTHER half of a 2N-entry
-    // ping-pong buffer (per split: +N or -N), so no copy-back of the partitioned segments
-    const int sh = out_shift ? out_shift[si] : 0;
-    const int rstart = nend - rofs - (tv - tl) + sh;
-    const int lstart = nbeg + lofs + sh;
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const int rank = j * kPartThreads + tid;  // rank among the chunk's rows
-      if (rank < tv) {
-        const int lb = s_l[j * NW + wid] + lrank[j];  // left rows before this one
-        const int dst = left[j] ? lstart + lb : rstart + (rank - lb);
-        rows_out[dst] = r[j];
-        gh_out[dst] = g[j];
-      }
-    }
-  }
-  __syncthreads();  // s_l / s_base / s_tl are reused by the next chunk
-  }
+  partition_atomic_body<BinT, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, first_blk, nsplit_dev,
+                                        nblocks_dev, feat, thr, node_begin, node_count, cursor, out_shift);
 }
 
 }  // namespace ytk

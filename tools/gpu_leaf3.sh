@@ -11,9 +11,9 @@ if [ -n "$FULL" ]; then
   step 600 t_gbdt.log python -u -m pytest tests/test_gbdt_train.py tests/test_gbdt_kernels.py tests/test_gbdt_materialize.py -m gpu -x -q --timeout 150 --timeout-method thread
   tail -2 $O/t_gbdt.log
 fi
-step 300 b_leaf.log python bench.py --steps 20 --warmup 3 --policy loss
+step 300 b_leaf.log python bench.py --steps 20 --warmup 3 --policy loss --leafwise-steps 0
 tail -1 $O/b_leaf.log | cut -c1-300
-YTK_LW_PROF=1 step 300 b_leaf_prof.log python bench.py --steps 20 --warmup 3 --policy loss
+YTK_LW_PROF=1 step 300 b_leaf_prof.log python bench.py --steps 20 --warmup 3 --policy loss --leafwise-steps 0
 grep "planner profile" $O/b_leaf_prof.log
 cd /tmp
 step 300 p.log rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 4 --warmup 1 --policy loss

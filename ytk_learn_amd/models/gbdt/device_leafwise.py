@@ -10,7 +10,10 @@ launch sequence; it polls a done flag one batch behind (pinned copy + event), so
 always has the next batch queued and never waits for the host.
 
 Rows live in a 2N-entry ping-pong buffer: a partition writes a node's children into the
-other half at the same positions (no copy-back of the partitioned segments).
+other half at the same positions (no copy-back of the partitioned segments). (g, h) moves
+with the row ids so the histogram reads it in position order (measured: leaving it
+row-indexed -- 9 instead of 25 B per partitioned row -- cut the partition by 22 % but
+the histogram's extra gather cost more).
 """
 from __future__ import annotations
 
@@ -39,8 +42,10 @@ REDUCE_DIRECT = 16     # kReduceDirect: slots with <= 16 staged items are stored
 class DeviceLeafBuilder:
     HIST_TARGET = int(os.environ.get("YTK_HIST_TARGET", 256))
     MIN_ROWS = int(os.environ.get("YTK_HIST_MIN_ROWS", 2048))
-    REDUCE_Y = 16       # slot reduce: y blocks striding over the batch's built slots
-    POLL_LAG = 1        # batches enqueued ahead of the done-flag check
+    REDUCE_Y = 8        # slot reduce: y blocks striding over the batch's multi-item slots
+    # batches enqueued ahead of the done-flag check (capturing batches in HIP graphs was
+    # measured: no gain -- the gaps between dependent kernels are on the device side)
+    POLL_LAG = 2
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
@@ -97,7 +102,9 @@ class DeviceLeafBuilder:
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
         self.max_pblocks = -(-N // PART_CHUNK) + ml + 1
-        self._done_host = torch.zeros(64, dtype=torch.int32).pin_memory()
+        # done flag: the planner writes it straight into pinned host memory (no copy launch)
+        self._done_host = torch.zeros(16, dtype=torch.int32).pin_memory()
+        self._done_dev = hip().host_device_ptr(self._done_host.data_ptr())
         self.tree_count = 0
         self.last_keep = None
         self.last_batches = self.last_expanded = 0
@@ -157,7 +164,8 @@ class DeviceLeafBuilder:
                 ptr(self.batch)] + [ptr(self.part[k]) for k in range(6)]
                 + [ptr(self.cursor), ptr(self.hist_items), ptr(self.build_ids), ptr(self.split_items),
                    ptr(self.item_sid), ptr(self.split_out), ptr(self.root_cnt),
-                   ptr(self.prof) if self.prof is not None else 0, ptr(self.zero_ids), ptr(self.zero_range)])
+                   ptr(self.prof) if self.prof is not None else 0, self._done_dev, ptr(self.zero_ids),
+                   ptr(self.zero_range)])
 
     def _lv_ptrs(self):
         """Pointer list of the level engine's finalize / raw-tree kernels (st, nodes, arrays)."""
@@ -185,9 +193,8 @@ class DeviceLeafBuilder:
     # ------------------------------------------------------------------ build
     def _hist_split(self, h, rows_ptr, gh_ptr, fmask, f0, s):
         st = ptr(self.st)
-        # multi-item slots are zeroed and reduced; sole-item slots are stored by the hist kernel
-        h.lw_zero_slots(ptr(self.hist), self.slot_bytes, ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
-                        REDUCE_DIRECT, 256, s)
+        # sole-item slots are stored by the hist kernel, <= 16-item slots by the reduce, larger
+        # ones zeroed by their first hist item and reduced split-K
         h.hist_fx_staged_dev(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                              self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
@@ -233,31 +240,24 @@ class DeviceLeafBuilder:
         tm = self.timer
         tm.mark("init_stats")
         hd = self._handle
+        # the previous tree's batches all finished (its done flag was observed), so no
+        # kernel writes the flag while it is reset
+        self._done_host[0] = 0
         h.lw_step(hd, 0, s)
         self._hist_split(h, rows0, gh0, fmask, f0, s)
         tm.mark("root")
-        st = ptr(self.st)
-        pend = []  # (iteration, event) of the done-flag copies in flight
+        pend = []  # events of the batches in flight
         it = 0
         while True:
-            h.lw_step(hd, 1, s)
-            rows_in, gh_in = (rows0, gh0) if it == 0 else (ptr(self.rows2), ptr(self.gh2))
-            pt = self.part
-            h.partition_atomic(ptr(self.binsT), 1, self.binsT.shape[1], rows_in, ptr(self.rows2), gh_in,
-                               ptr(self.gh2), ptr(pt[4]), st + 4 * W_N_SPLIT, st + 4 * W_N_PBLK, self.max_pblocks,
-                               ptr(pt[0]), ptr(pt[1]), ptr(pt[2]), ptr(pt[3]), ptr(self.cursor), 0, ptr(pt[5]), s)
-            h.lw_step(hd, 2, s)
-            self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
-            slot = it % self._done_host.numel()
-            self._done_host[slot:slot + 1].copy_(self.st[LW_DONE:LW_DONE + 1], non_blocking=True)
+            self._batch(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2),
+                        fmask, f0, s)
+            it += 1
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
-            pend.append((slot, ev))
-            it += 1
+            pend.append(ev)
             if len(pend) > self.POLL_LAG:
-                slot0, ev0 = pend.pop(0)
-                ev0.synchronize()
-                if int(self._done_host[slot0]) != 0:
+                pend.pop(0).synchronize()
+                if int(self._done_host[0]) != 0:
                     break
             if it > 4 * self.max_leaf + 8:
                 raise RuntimeError("device leaf-wise builder did not terminate")
@@ -276,12 +276,18 @@ class DeviceLeafBuilder:
         v = self.prof.cpu().numpy()
         names = ["apply", "stage", "replay", "events", "select", "expand", "writeback"]
         out = {f"plan_{n}_us": round(float(v[i]) / 100.0, 1) for i, n in enumerate(names)}
+        out["plan_queue_sort_us"] = round(float(v[7]) / 100.0, 1)
         out.update(plan_calls=int(v[8]), part_blocks=int(v[9]), replay_events=int(v[10]), candidates=int(v[11]),
                    hist_rows=int(v[12]), built_slots=int(v[13]), hist_items=int(v[14]),
-                   replay_local_us=round(float(v[16]) / 100.0, 1), replay_wavemax_us=round(float(v[17]) / 100.0, 1),
-                   replay_locate_us=round(float(v[18]) / 100.0, 1), replay_remove_us=round(float(v[19]) / 100.0, 1),
-                   replay_apply_us=round(float(v[20]) / 100.0, 1), replay_pops=int(v[21]))
+                   replay_sorted_pops=int(v[21]))
         return out
+
+    def _batch(self, h, hd, rows_in, gh_in, fmask, f0, s):
+        """One speculative batch: plan, partition (+ children planning), histograms, splits."""
+        h.lw_step(hd, 1, s)
+        h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in, ptr(self.rows2), ptr(self.gh2),
+                       self.max_pblocks, s)
+        self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
 
     def stats(self):
         """(batches, expanded nodes, overflow flag) of the last tree (synchronises)."""
