@@ -77,6 +77,8 @@ void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uint
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                      uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintptr_t, long long, uintptr_t, uintptr_t,
+                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t);
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
@@ -135,6 +137,15 @@ PYBIND11_MODULE(_ytk_hip, m) {
                     nright, ndefl, nval, stream);
   });
   m.def("lv_scales", &ytk_lv_scales);
+  m.def("lv_partition_children", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
+                                     const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
+                                     uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
+                                     int count_only, int a0, int a1, int maxp, uintptr_t stream) {
+    if (ptrs.size() != 26 || ip.size() != 6 || fp.size() != 6)
+      throw std::invalid_argument("lv_partition_children: bad argument sizes");
+    ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
+                              max_blocks, count_only, a0, a1, maxp, stream);
+  });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
     if (ptrs.size() != 37 || ip.size() != 8 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());

@@ -17,14 +17,17 @@
 // synchronisation inside a tree, and multi-GPU all-reduces are fixed-size RCCL calls
 // on the same stream.
 #include "common.h"
+
+#include <algorithm>
 #include "gbdt_split_node.h"  // SplitOut (one definition, layout static_assert'ed there)
 #include "gbdt_tree_node.h"  // DNode, node_leaf_value
+#include "gbdt_partition_atomic.h"  // partition_atomic_body
 
 namespace ytk {
 
 enum {
   ST_NUM_NODES = 0, ST_NUM_LEAF, ST_N_PENDING, ST_N_SPLIT, ST_N_PART, ST_N_HIST,
-  ST_N_SITEMS, ST_N_BUILD, ST_N_HIST_A, ST_WORDS = 16
+  ST_N_SITEMS, ST_N_BUILD, ST_N_HIST_A, ST_PART_DONE, ST_WORDS = 16
 };
 
 constexpr int kPlanThreads = 256;
@@ -243,6 +246,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
                                                                          : 0x7fffffff;
   const int nsplit = min(ncand, limit);
   if (tid == 0) {
+    st[ST_PART_DONE] = 0;
     st[ST_NUM_NODES] = num_nodes0 + 2 * nsplit;
     st[ST_NUM_LEAF] = num_leaf0 + nsplit;
     st[ST_N_SPLIT] = nsplit;
@@ -297,14 +301,16 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
 // they ride in count slots of the level's histogram all-reduce -- so the smaller child
 // is chosen by the (globally identical) hessian sums and cnt_global is patched by the
 // next lv_plan_split. Exact int64 histograms make the choice result-neutral.
-__global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base,
-                                                                    int half, int dgap, int use_loc,
-                                                                    int fused) {
-  __shared__ int s_nb[kMaxPend];     // 1 if the split's children get histograms
-  __shared__ int s_small[kMaxPend];  // small child node id
+// KP: bound on the level's splits (LDS arrays); kAtomicCursor: the cursors were just
+// updated by atomics of other blocks of the same kernel (fused partition epilogue)
+template <int KP, bool kAtomicCursor>
+__device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int build_base, int half, int dgap,
+                                      int use_loc, int fused) {
+  __shared__ int s_nb[KP];     // 1 if the split's children get histograms
+  __shared__ int s_small[KP];  // small child node id
   __shared__ int s_tmp[kPlanThreads + 1];
   __shared__ long long s_total;
-  __shared__ int s_hbeg[kMaxPend], s_hcnt[kMaxPend], s_hslot[kMaxPend];
+  __shared__ int s_hbeg[KP], s_hcnt[KP], s_hslot[KP];
   int* st = b.st;
   const int tid = threadIdx.x;
   const int nsplit = st[ST_N_SPLIT];
@@ -317,7 +323,14 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
     DNode& R = b.nodes[P.right];
     // split cursors pack (right rows << 32) | left rows (single-pass partition); the
     // count-only pass accumulates the left rows alone -- either way the low half
-    const long long lloc = b.left_loc[s] & 0xffffffffll, lglob = lglob_arr[s] & 0xffffffffll;
+    long long lloc, lglob;
+    if (kAtomicCursor) {
+      lloc = __hip_atomic_load(&b.left_loc[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+      lglob = __hip_atomic_load(&lglob_arr[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+    } else {
+      lloc = b.left_loc[s] & 0xffffffffll;
+      lglob = lglob_arr[s] & 0xffffffffll;
+    }
     reset_node(L, P.depth + 1);
     reset_node(R, P.depth + 1);
     L.begin = P.begin;
@@ -389,6 +402,31 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
     st[ST_N_SITEMS] = 2 * nb;
     st[ST_N_HIST] = nitems;
   }
+}
+
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base,
+                                                                    int half, int dgap, int use_loc,
+                                                                    int fused) {
+  lv_plan_children_body<kMaxPend, false>(p, b, build_base, half, dgap, use_loc, fused);
+}
+
+// One-GPU levels: the partition (partition_atomic_body) and the children planning in one
+// launch -- the last block to finish (device-scope counter, no fences: the split cursors
+// are returning atomics, read back with atomic loads) runs lv_plan_children_body.
+template <bool kScatter, int KP>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
+                                  const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
+                                  int dgap, int use_loc, int fused) {
+  partition_atomic_body<uint8_t, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
+                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr);
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&b.st[ST_PART_DONE], 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  lv_plan_children_body<KP, true>(p, b, build_base, half, dgap, use_loc, fused);
 }
 
 // Bin-threshold arrays used by the fused score/gradient kernel.
@@ -536,6 +574,44 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
     case 4: hipLaunchKernelGGL(lv_finalize_kernel, dim3(1), dim3(256), 0, s, b, arg0); break;
     default: throw std::runtime_error("bad lv step");
   }
+  YTK_LAUNCH_CHECK();
+}
+
+// Fused partition + children planning (one GPU, uint8 bins): count_only = last level;
+// arg0 / arg1 as ytk_lv_step(3).
+void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t binsT, long long ncol,
+                               uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
+                               int count_only, int arg0, int arg1, int maxp, uintptr_t stream) {
+  LvParams p;
+  p.max_depth = ip[0];
+  p.max_leaf_cnt = ip[1];
+  p.min_split_samples = ip[2];
+  p.hist_target = ip[3];
+  p.part_target = ip[4];
+  p.min_rows = ip[5];
+  p.min_split_loss = fp[0];
+  p.mcw = fp[1];
+  p.l1 = fp[2];
+  p.l2 = fp[3];
+  p.max_abs_leaf = fp[4];
+  p.lr = fp[5];
+  LvBufs b = make_bufs(ptrs);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
+  const int use_loc = (arg1 >> 30) & 1, fused = (arg1 >> 29) & 1;
+  const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
+#define YTK_LVPC(SC, KP)                                                                                     \
+  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP>), grid, dim3(kPartThreads), 0, s, p, b,            \
+                     (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
+                     (float2*)gh_out, arg0, half, dgap, use_loc, fused)
+  if (maxp <= 64) {
+    if (count_only) YTK_LVPC(false, 64); else YTK_LVPC(true, 64);
+  } else if (maxp <= 512) {
+    if (count_only) YTK_LVPC(false, 512); else YTK_LVPC(true, 512);
+  } else {
+    if (count_only) YTK_LVPC(false, kMaxPend); else YTK_LVPC(true, kMaxPend);
+  }
+#undef YTK_LVPC
   YTK_LAUNCH_CHECK();
 }
 

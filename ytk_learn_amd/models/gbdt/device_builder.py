@@ -107,6 +107,10 @@ class DeviceLevelBuilder:
         # (the kernel holds one chunk of <= 2048 rows per block in registers)
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0" and self.MIN_ROWS == 2048
         self.part_target = (-(-self.N // self.MIN_ROWS) + 1) if self.part_atomic else self.PART_TARGET
+        # one GPU, uint8 bins: the children planner runs in the partition kernel's last block
+        # (YTK_FUSE_PART_CHILDREN=0: separate launches)
+        self.fuse_part_children = (self.part_atomic and not self.comm.is_dist and bins.dtype == torch.uint8
+                                   and os.environ.get("YTK_FUSE_PART_CHILDREN", "1") != "0")
         self.max_items = max(self.hist_target, self.part_target) + self.maxp + 16
         dev = self.dev
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
@@ -421,8 +425,20 @@ class DeviceLevelBuilder:
             lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
+            half = 1 << (c - 1)
+            if last:
+                base, ncs = 0, 0  # no histograms at the last level
+            else:
+                base, cbase, dbase = self.level_slots[c]
+                ncs = dbase - cbase
+            if self.fuse_part_children:
+                # one GPU: partition + children planning in one launch (last block plans)
+                h.lv_partition_children(ptrs, ip, fp, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in,
+                                        ptr(self.rows_tmp), ptr(self.gh_tmp), npart, 1 if last else 0, base,
+                                        half | (ncs << 14) | (1 << 30), self.maxp, s)
+                tm.mark("partition")
             # the flag kernel also accumulates the per-split left totals into left_loc
-            if self.part_atomic:
+            elif self.part_atomic:
                 # the split cursors are the (zeroed) per-split left counters: low half = left
                 # rows, high half = right rows; the last level only counts
                 h.partition_atomic(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
@@ -439,24 +455,19 @@ class DeviceLevelBuilder:
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
                             lloc, s)
-            tm.mark("partition")
-            lvl_fused = fused and not last
-            if dist and not lvl_fused:
-                self.left_glob.copy_(self.left_loc)
-                self.comm.allreduce_(self.left_glob)
-                tm.mark("sync_counts")
-            half = 1 << (c - 1)
-            if last:
-                base, ncs = 0, 0  # no histograms at the last level
-            else:
-                base, cbase, dbase = self.level_slots[c]
-                ncs = dbase - cbase
-            use_loc = (not dist) or lvl_fused
-            if fused and last:  # the last level reads the separately all-reduced counts
-                ptrs = self._ptrs()
-            h.lv_step(3, ptrs, ip, fp, base,
-                      half | (ncs << 14) | ((1 if lvl_fused else 0) << 29) | ((1 if use_loc else 0) << 30), s)
-            tm.mark("plan")
+            if not self.fuse_part_children:
+                tm.mark("partition")
+                lvl_fused = fused and not last
+                if dist and not lvl_fused:
+                    self.left_glob.copy_(self.left_loc)
+                    self.comm.allreduce_(self.left_glob)
+                    tm.mark("sync_counts")
+                use_loc = (not dist) or lvl_fused
+                if fused and last:  # the last level reads the separately all-reduced counts
+                    ptrs = self._ptrs()
+                h.lv_step(3, ptrs, ip, fp, base,
+                          half | (ncs << 14) | ((1 if lvl_fused else 0) << 29) | ((1 if use_loc else 0) << 30), s)
+                tm.mark("plan")
             if last:
                 break
             self.rows, self.rows_tmp = self.rows_tmp, self.rows
