@@ -56,7 +56,7 @@ void ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, u
 // sparse.hip
 void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, long long, int,
                   uintptr_t, long long, float, int, int, int, uintptr_t, uintptr_t);
-void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t);
+void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t, uintptr_t);
 // ffm.hip
 void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, int,
                    uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);

@@ -87,14 +87,16 @@ __global__ __launch_bounds__(256) void seg_spmm_kernel(
 }
 
 // out[col, :] (+)= alpha * sum_{c in chunks of col, in order} part[c, :]
+// ids (optional): the chunk numbers of column col are ids[cbeg[col] .. cbeg[col + 1]) (row-
+// tiled CSC: a column's chunks are spread over the tiles); otherwise they are contiguous.
 __global__ __launch_bounds__(256) void chunk_reduce_kernel(
     const long long* __restrict__ cbeg, int ncol, const float* __restrict__ part, int J,
-    float* __restrict__ out, long long ldo, float alpha, int accumulate) {
+    float* __restrict__ out, long long ldo, float alpha, int accumulate, const long long* __restrict__ ids) {
   const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (t >= (long long)ncol * J) return;
   const int col = (int)(t / J), j = (int)(t % J);
   float acc = 0.f;
-  for (long long c = cbeg[col]; c < cbeg[col + 1]; ++c) acc += part[c * J + j];
+  for (long long c = cbeg[col]; c < cbeg[col + 1]; ++c) acc += part[(ids ? ids[c] : c) * J + j];
   float* o = out + (long long)col * ldo + j;
   *o = accumulate ? *o + alpha * acc : alpha * acc;
 }
@@ -183,12 +185,12 @@ void ytk_seg_spmm(uintptr_t beg, uintptr_t end, int nseg, uintptr_t idx, uintptr
 }
 
 void ytk_chunk_reduce(uintptr_t cbeg, int ncol, uintptr_t part, int J, uintptr_t out,
-                      long long ldo, float alpha, int accumulate, uintptr_t stream) {
+                      long long ldo, float alpha, int accumulate, uintptr_t ids, uintptr_t stream) {
   if (ncol <= 0 || J <= 0) return;
   const long long n = (long long)ncol * J;
   hipLaunchKernelGGL(chunk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), (const long long*)cbeg, ncol,
-                     (const float*)part, J, (float*)out, ldo, alpha, accumulate);
+                     (const float*)part, J, (float*)out, ldo, alpha, accumulate, (const long long*)ids);
   YTK_LAUNCH_CHECK();
 }
 

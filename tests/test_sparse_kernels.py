@@ -177,7 +177,7 @@ def test_ffm_csc_backward_one_hot(cuda):
     Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
     gg = torch.zeros_like(V).to(cuda)
     ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gg)
-    assert Xg._ffm_layout[1][0] is True and Xg._ffm_layout[1][3] is None
+    assert Xg._ffm_layout[1][0] is True and Xg._ffm_layout[1][3] is None  # distinct fields, unit values
     torch.testing.assert_close(gg.cpu(), gc, rtol=1e-3, atol=1e-3)
     g2 = torch.zeros_like(V).to(cuda)
     ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g2)
@@ -210,3 +210,51 @@ def test_fm_fused_gpu_matches_cpu(cuda, k, m, monkeypatch):
     fm_backward(Xg, c.to(cuda), Sg, Vg, glg, gVg)
     torch.testing.assert_close(glg.cpu(), glc, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gVg.cpu(), gVc, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_row_tiled_csc_products(cuda, monkeypatch):
+    """Row-tiled CSC (chunks ordered by (row tile, column); the ordered chunk reduce walks a
+    column's chunks through chunk_ids): transposed SpMV / SpMM, the FM backward and both FFM
+    backward kernels match the CPU path and the untiled GPU path."""
+    from ytk_learn_amd.data.synthetic import criteo_like
+    from ytk_learn_amd.ops.fm import fm_backward, fm_forward
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    monkeypatch.setattr(sparse_mod, "CHUNK", 64)
+    n, F, k = 5000, 600, 4
+    ip, ix, vv, _ = _rand_csr(n, F, 12, seed=5)
+    g = torch.Generator().manual_seed(3)
+    D = torch.randn(n, 5, generator=g)
+    c = torch.randn(n, generator=g)
+    Xc = SparseMatrix(ip, ix, vv, F)
+    ref1 = Xc.t_matmul(c)
+    ref5 = Xc.t_matmul(D, square=True)
+    w = torch.randn(F + F * k, generator=g) * 0.1
+    Vc = w[F:].view(F, k)
+    fc, Sc = fm_forward(Xc, w[:F], Vc)
+    glc, gVc = torch.zeros(F), torch.zeros(F, k)
+    fm_backward(Xc, c, Sc, Vc, glc, gVc)
+    for tile in (700, 0):
+        monkeypatch.setattr(sparse_mod, "ROW_TILE", tile)
+        Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+        assert (Xg.chunk_ids is not None) == (tile > 0)
+        torch.testing.assert_close(Xg.t_matmul(c.to(cuda)).cpu(), ref1, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(Xg.t_matmul(D.to(cuda), square=True).cpu(), ref5, rtol=1e-4, atol=1e-4)
+        fg, Sg = fm_forward(Xg, w[:F].to(cuda), Vc.to(cuda))
+        glg, gVg = torch.zeros(F, device=cuda), torch.zeros(F, k, device=cuda)
+        fm_backward(Xg, c.to(cuda), Sg, Vc.to(cuda), glg, gVg)
+        torch.testing.assert_close(glg.cpu(), glc, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(gVg.cpu(), gVc, rtol=1e-4, atol=1e-3)
+    # FFM (criteo-like rows) through the tiled chunks
+    nf = 6
+    ip2, ix2, vv2, fl2, _ = criteo_like(4000, nf, 600, seed=8)
+    F2 = nf * (600 // nf)
+    V2 = torch.randn(F2 * nf * k, generator=g) * 0.2
+    c2 = torch.randn(4000, generator=g)
+    gref = torch.zeros_like(V2)
+    ffm_backward(ip2, ix2, vv2, fl2, V2, nf, k, c2, gref)
+    monkeypatch.setattr(sparse_mod, "ROW_TILE", 900)
+    Xf = SparseMatrix(ip2.to(cuda), ix2.to(cuda), vv2.to(cuda), F2)
+    gg = torch.zeros_like(V2).to(cuda)
+    ffm_backward_csc(Xf, fl2.to(cuda), V2.to(cuda), nf, k, c2.to(cuda), gg)
+    torch.testing.assert_close(gg.cpu(), gref, rtol=1e-3, atol=1e-3)

@@ -10,6 +10,8 @@ per-model loops listed in SURVEY.md §2.A K16-K21.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -17,6 +19,8 @@ import torch
 from ._ext import check_cuda, hip, ptr, stream
 
 CHUNK = 4096  # nnz per CSC chunk: balances the bias column (all rows) against short columns
+# rows per CSC row tile (GPU, see SparseMatrix._build_csc); 0 disables the tiling
+ROW_TILE = int(os.environ.get("YTK_CSC_ROW_TILE", 524288))
 
 
 def _lanes(avg_nnz: float) -> int:
@@ -52,8 +56,21 @@ class SparseMatrix:
             self._build_csc()
 
     def _build_csc(self):
+        """Column-ordered (CSC) copy in CHUNK-entry chunks for the transposed products.
+
+        On the GPU with more than ROW_TILE rows the entries are ordered (row tile, column,
+        row): the chunks of one row tile run together, so the per-row data the column
+        kernels gather (FM's S rows, FFM's row entries, the row coefficients) is a
+        tile-sized, cache-resident working set (MALL / L2) instead of the whole matrix.
+        A column's chunks then come from several tiles; ``chunk_ids`` lists them column
+        by column for the ordered chunk reduce (deterministic sum order)."""
         cols = self.indices.to(torch.int64)
-        order = torch.sort(cols * (self.n + 1) + self.rows_of_nnz, stable=True).indices
+        rows = self.rows_of_nnz.to(torch.int64)
+        tiled = self.device.type == "cuda" and ROW_TILE > 0 and self.n > ROW_TILE
+        T = -(-self.n // ROW_TILE) if tiled else 1
+        seg = (rows // ROW_TILE) * self.ncols + cols if tiled else cols  # (tile, column) segments
+        order = torch.sort(seg * (self.n + 1) + rows, stable=True).indices
+        del rows
         self.csc_perm = order
         self.csc_rows = self.rows_of_nnz[order].to(torch.int32).contiguous()
         self.csc_vals = self.values[order].contiguous()
@@ -61,16 +78,29 @@ class SparseMatrix:
         colptr = torch.zeros(self.ncols + 1, dtype=torch.int64, device=self.device)
         colptr[1:] = torch.cumsum(counts, 0)
         self.colptr = colptr
-        # chunks: column c is split into ceil(len/CHUNK) segments (at least 1 when non-empty)
-        nch = (counts + CHUNK - 1) // CHUNK
-        cbeg = torch.zeros(self.ncols + 1, dtype=torch.int64, device=self.device)
+        scounts = torch.bincount(seg, minlength=T * self.ncols) if tiled else counts
+        segptr = torch.zeros(scounts.numel() + 1, dtype=torch.int64, device=self.device)
+        segptr[1:] = torch.cumsum(scounts, 0)
+        del seg
+        # chunks: segment s is split into ceil(len/CHUNK) pieces (none when empty)
+        nch = (scounts + CHUNK - 1) // CHUNK
+        cbeg = torch.zeros(scounts.numel() + 1, dtype=torch.int64, device=self.device)
         cbeg[1:] = torch.cumsum(nch, 0)
         total = int(cbeg[-1])
-        chunk_col = torch.repeat_interleave(torch.arange(self.ncols, device=self.device), nch)
-        within = torch.arange(total, device=self.device) - cbeg[:-1][chunk_col]
-        self.chunk_beg = (colptr[:-1][chunk_col] + within * CHUNK).contiguous()
-        self.chunk_end = torch.minimum(self.chunk_beg + CHUNK, colptr[1:][chunk_col]).contiguous()
-        self.chunk_ptr = cbeg.contiguous()
+        chunk_seg = torch.repeat_interleave(torch.arange(scounts.numel(), device=self.device), nch)
+        within = torch.arange(total, device=self.device) - cbeg[:-1][chunk_seg]
+        self.chunk_beg = (segptr[:-1][chunk_seg] + within * CHUNK).contiguous()
+        self.chunk_end = torch.minimum(self.chunk_beg + CHUNK, segptr[1:][chunk_seg]).contiguous()
+        if tiled:
+            chunk_col = chunk_seg % self.ncols
+            self.chunk_ids = torch.sort(chunk_col, stable=True).indices.contiguous()  # column-major, tiles in order
+            per_col = torch.bincount(chunk_col, minlength=self.ncols)
+            cptr = torch.zeros(self.ncols + 1, dtype=torch.int64, device=self.device)
+            cptr[1:] = torch.cumsum(per_col, 0)
+            self.chunk_ptr = cptr.contiguous()
+        else:
+            self.chunk_ids = None
+            self.chunk_ptr = cbeg.contiguous()
         self.n_chunks = total
         self.chunk_lanes = _lanes(self.nnz / max(total, 1))
         # power-law columns (Criteo: a few hot features, a long tail of short columns): one
@@ -142,7 +172,7 @@ class SparseMatrix:
                 h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), self.n_chunks, ptr(self.csc_rows), vp,
                            ptr(D2), D2.stride(0), J, ptr(part), J, 1.0, 0, int(square), min(64, J), 0, s)
             h.chunk_reduce(ptr(self.chunk_ptr), self.ncols, ptr(part), J, ptr(o2), o2.stride(0), float(alpha),
-                           int(accumulate), s)
+                           int(accumulate), ptr(self.chunk_ids), s)
         else:
             vals = self.csc_vals if values is None else values
             v = vals * vals if square else vals
