@@ -17,6 +17,8 @@ void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr
                         uintptr_t);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
+void ytk_hist_set_fw(int);
+int ytk_hist_get_fw();
 int ytk_hist_wide(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, float,
                   float, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 int ytk_hist_wide_group(int, int);
@@ -99,6 +101,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_fx_global", &ytk_hist_fx_global);
   m.def("hist_fx_staged", &ytk_hist_fx_staged);
   m.def("hist_wide", &ytk_hist_wide);
+  m.def("hist_set_fw", &ytk_hist_set_fw);
+  m.def("hist_get_fw", &ytk_hist_get_fw);
   m.def("hist_wide_group", &ytk_hist_wide_group);
   m.def("split_find", &ytk_split_find);
   m.def("split_combine", &ytk_split_combine);

@@ -58,7 +58,10 @@ __device__ __forceinline__ int hist_lds_pos(int fl) {
 constexpr int kHistU = 8;
 constexpr int kHistUGather = 8;  // gathered rows (pipelined: rows two steps ahead)
 
-template <bool kIdentity>
+// kFW: features per block (32: one 128-KiB LDS plane pair per block, 1 block per CU; 16:
+// 64 KiB, 2 blocks per CU with twice the rows in flight -- every row is read by both
+// feature-half blocks, 16 B each)
+template <bool kIdentity, int kFW = 32>
 __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const uint8_t* __restrict__ bins, long long stride, int F,
     const float2* __restrict__ ghp, const int* __restrict__ rows,
@@ -80,22 +83,25 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   const int4 w = work[bx];
   const int fg = blockIdx.y;
   const int tid = threadIdx.x;
-  for (int i = tid; i < nb_lds * 64; i += kHistThreads) sm64[i] = 0ull;
+  constexpr int kRow = 2 * kFW;  // LDS words per bin row: [kFW g | kFW h]
+  for (int i = tid; i < nb_lds * kRow; i += kHistThreads) sm64[i] = 0ull;
   __syncthreads();
 
   const int wave = tid >> 6;
   const int lane = tid & 63;
-  const int wr = lane >> 3;  // row within the wave's 8
-  const int q = lane & 7;    // dword (4 features) within the 32-B group segment
-  constexpr int RW = (kHistThreads / 64) * 8;  // rows per block step
-  const uint8_t* bseg = bins + fg * 32 + 4 * q;
-  const int fbase = fg * 32 + 4 * q;
+  constexpr int kQ = kFW / 4;          // lanes per row (one dword = 4 features each)
+  const int wr = lane / kQ;             // row within the wave's 64 / kQ
+  const int q = lane % kQ;              // dword (4 features) within the group's segment
+  constexpr int RW = (kHistThreads / 64) * (64 / kQ);  // rows per block step
+  const uint8_t* bseg = bins + fg * kFW + 4 * q;
   // LDS word of local feature 4q + c inside a bin row (hist_lds_pos: bank-conflict-free
   // 64-bit atomics)
   int lpos[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) lpos[c] = hist_lds_pos(4 * q + c);
-  constexpr int U = kIdentity ? kHistU : kHistUGather;
+  for (int c = 0; c < 4; ++c) lpos[c] = kFW == 32 ? hist_lds_pos(4 * q + c) : 4 * q + c;
+  // 16-feature blocks hold twice the rows per wave instruction: half the unroll keeps the
+  // rows in flight per wave and fits 2 blocks (32 waves) per CU in the VGPR budget
+  constexpr int U = (kIdentity ? kHistU : kHistUGather) / (kFW == 16 ? 2 : 1);
   constexpr int STEP = RW * U;
   // Software pipeline: the bin dwords and (g, h) of step i+1 are in flight while step i
   // is accumulated into LDS (measured: the un-pipelined loop left the kernel latency
@@ -120,7 +126,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
       v[j] = ok[j] ? t : make_float2(0.f, 0.f);  // rows past the end add 0
     }
   };
-  const int base0 = w.y + wave * 8;
+  const int base0 = w.y + wave * (64 / kQ);
   unsigned d[U];
   float2 v[U];
   bool ok[U];
@@ -151,9 +157,9 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
       for (int k = 0; k < 4; ++k) {
         const int c = (k + wr) & 3;
         const unsigned bin = __builtin_amdgcn_ubfe(d[j], 8 * c, 8);
-        unsigned long long* e = sm64 + (bin * 64 + lpos[c]);
+        unsigned long long* e = sm64 + (bin * kRow + lpos[c]);
         atomicAdd(e, gi);
-        atomicAdd(e + 32, hi);
+        atomicAdd(e + kFW, hi);
       }
     }
     if (more) {
@@ -171,13 +177,13 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     // the slot's ONLY item (leaf-wise engine, small nodes): store the block's sums straight
     // into the slot -- no staging round trip, no zero fill, no reduce
     long long* out = hist + (size_t)w.x * B * F * 2;
-    const int E = nb_lds * 32;
+    const int E = nb_lds * kFW;
     for (int i = tid; i < E; i += kHistThreads) {
-      const int bin = i >> 5, ff = fg * 32 + (i & 31);
+      const int bin = i / kFW, l = i % kFW, ff = fg * kFW + l;
       if (ff < F && bin < B) {
-        const int li = 2 * (i & ~31) + hist_lds_pos(i & 31);
+        const int li = bin * kRow + (kFW == 32 ? hist_lds_pos(l) : l);
         *reinterpret_cast<longlong2*>(&out[((size_t)bin * F + ff) * 2]) =
-            make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
+            make_longlong2((long long)sm64[li], (long long)sm64[li + kFW]);
       }
     }
     return;
@@ -187,11 +193,12 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     // sums are formed by hist_reduce_kernel. Global u64 atomics execute at the memory
     // side at ~1.3 TB/s chip-wide, which made the atomic flush the floor of every
     // launch (~45 us per level at 256 blocks); stores + one ordered read are ~4x cheaper.
-    const int E = nb_lds * 32;
+    const int E = nb_lds * kFW;
     longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.y + fg) * E;
     for (int i = tid; i < E; i += kHistThreads) {
-      const int li = 2 * (i & ~31) + hist_lds_pos(i & 31);
-      st[i] = make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
+      const int l = i % kFW;
+      const int li = (i / kFW) * kRow + (kFW == 32 ? hist_lds_pos(l) : l);
+      st[i] = make_longlong2((long long)sm64[li], (long long)sm64[li + kFW]);
     }
     if (w.w == 2 && fg == 0) {
       // first item of a slot the split-K reduce adds into (leaf-wise engine): zero it
@@ -206,16 +213,16 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
   // thousand addresses at about the same time; starting each block at a different
   // 1024-entry tile spreads the global atomics over the L2 channels instead of
   // serialising hundreds of blocks on one address at a time.
-  const int E = nb_lds * 32;
+  const int E = nb_lds * kFW;
   const int ntile = (E + kHistThreads - 1) / kHistThreads;
   const int rot = (int)((unsigned)bx % (unsigned)ntile);
   for (int t = 0; t < ntile; ++t) {
     const int i = ((t + rot) % ntile) * kHistThreads + tid;
     if (i >= E) continue;
-    const int bin = i >> 5, l = i & 31, ff = fg * 32 + l;
+    const int bin = i / kFW, l = i % kFW, ff = fg * kFW + l;
     if (ff < F) {
-      const int li = 2 * (i & ~31) + hist_lds_pos(l);
-      const unsigned long long g = sm64[li], h = sm64[li + 32];
+      const int li = bin * kRow + (kFW == 32 ? hist_lds_pos(l) : l);
+      const unsigned long long g = sm64[li], h = sm64[li + kFW];
       if (g | h) {
         unsigned long long* o = reinterpret_cast<unsigned long long*>(&out[((size_t)bin * F + ff) * 2]);
         atomicAdd(o, g);
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
     const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
     int groups, int slot_base, const int* __restrict__ slot_ids, const int* __restrict__ nslots_dev,
-    const int2* __restrict__ slot_range) {
+    const int2* __restrict__ slot_range, int gw) {
   __shared__ int s_sel[1024];
   __shared__ int s_wcnt[4];
   __shared__ int s_n;
@@ -256,14 +263,14 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     // barriers. Slots with <= kReduceDirect items are summed by the z == 0 block and
     // STORED (zeros included: no zero fill needed); larger ones split-K with atomics into
     // a zeroed slot.
-    const int E = nb_lds * 32;
+    const int E = nb_lds * gw;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int bin = i >> 5;
+    const int bin = i / gw;
     if (i >= E || bin >= B) return;
     const longlong2* st = reinterpret_cast<const longlong2*>(staging);
     for (int by = (int)blockIdx.y; by < ny; by += (int)gridDim.y) {
       const int2 r = slot_range[by / groups];
-      const int fg = by % groups, ff = fg * 32 + (i & 31);
+      const int fg = by % groups, ff = fg * gw + (i % gw);
       if (ff >= F) continue;
       const bool direct = r.y <= kReduceDirect;
       if (direct && blockIdx.z != 0) continue;
@@ -342,10 +349,10 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   const int lo = s_lo;
   // t-th item of the slot
 #define YTK_SEL(t) (contiguous ? lo + (t) : s_sel[(t)])
-  const int E = nb_lds * 32;
+  const int E = nb_lds * gw;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E || cnt == 0) continue;
-  const int bin = i >> 5, ff = fg * 32 + (i & 31);
+  const int bin = i / gw, ff = fg * gw + (i % gw);
   if (ff >= F || bin >= B) continue;
   const longlong2* st = reinterpret_cast<const longlong2*>(staging);
   long long g = 0, h = 0;
@@ -484,9 +491,34 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
 
 using namespace ytk;
 
+// features per histogram block (32 or 16), process-wide (ytk_hist_set_fw); the staging
+// slabs hold groups * fw columns per bin
+static int g_hist_fw = 32;
+
+template <bool kIdentity>
+static void launch_hist_fx(dim3 grid, size_t lds_unused, hipStream_t s, const uint8_t* bins, long long stride, int F,
+                           const float2* ghp, const int* rows, const int4* work, long long* hist, int B, int nb_lds,
+                           float sg, float sh, const int* nwork_dev, const float* scales_dev, long long* staging,
+                           const int* work_off_dev) {
+  (void)lds_unused;
+  const size_t lds = (size_t)nb_lds * 2 * g_hist_fw * sizeof(unsigned long long);
+  if (g_hist_fw == 16)
+    hipLaunchKernelGGL((hist_fx_kernel<kIdentity, 16>), grid, dim3(kHistThreads), lds, s, bins, stride, F, ghp,
+                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev);
+  else
+    hipLaunchKernelGGL((hist_fx_kernel<kIdentity, 32>), grid, dim3(kHistThreads), lds, s, bins, stride, F, ghp,
+                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev);
+}
+
 extern "C" {
 
 int ytk_hist_wide_group(int B, int F);
+
+void ytk_hist_set_fw(int fw) {
+  if (fw != 16 && fw != 32) throw std::invalid_argument("hist_set_fw: 16 or 32");
+  g_hist_fw = fw;
+}
+int ytk_hist_get_fw() { return g_hist_fw; }
 
 // nwork_dev / scales_dev (optional): device-resident work count (grid = nwork is the
 // maximum) and fixed-point scales, used by the GPU-resident level engine.
@@ -494,28 +526,23 @@ void ytk_hist_fx(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr
                  uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
                  uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t stream) {
   if (nwork <= 0) return;
-  const int groups = (F + 31) / 32;
+  const int fw = g_hist_fw;
+  const int groups = (F + fw - 1) / fw;
   const int nb_lds = B;  // caller guarantees B <= 256
-  const size_t lds = (size_t)nb_lds * 64 * sizeof(unsigned long long);
   dim3 grid(nwork, groups);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (rows == 0) {
-    hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr,
-                       (const int*)nullptr);
-  } else {
-    hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)nullptr,
-                       (const int*)nullptr);
-  }
+  if (rows == 0)
+    launch_hist_fx<true>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, nullptr,
+                         (const int4*)work, (long long*)hist, B, nb_lds, sg, sh, (const int*)nwork_dev,
+                         (const float*)scales_dev, nullptr, nullptr);
+  else
+    launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                          (const int4*)work, (long long*)hist, B, nb_lds, sg, sh, (const int*)nwork_dev,
+                          (const float*)scales_dev, nullptr, nullptr);
   YTK_LAUNCH_CHECK();
 }
 
-// Staged variant: block partials to ``staging`` (>= nwork * groups * B * 32 * 16 bytes),
+// Staged variant: block partials to ``staging`` (>= nwork * groups * B * fw * 16 bytes),
 // then accumulated into the slots [slot_base, slot_base + nslots) -- or slot_ids[0..nslots)
 // when given -- which must be zero.
 void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
@@ -524,30 +551,25 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
                         int slot_base, int nslots, uintptr_t slot_ids, uintptr_t work_off_dev,
                         uintptr_t stream) {
   if (nwork <= 0 || nslots <= 0) return;
-  const int groups = (F + 31) / 32;
+  const int fw = g_hist_fw;
+  const int groups = (F + fw - 1) / fw;
   const int nb_lds = B;
-  const size_t lds = (size_t)nb_lds * 64 * sizeof(unsigned long long);
   dim3 grid(nwork, groups);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (rows == 0) {
-    hipLaunchKernelGGL(hist_fx_kernel<true>, grid, dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
-                       (const int*)work_off_dev);
-  } else {
-    hipLaunchKernelGGL(hist_fx_kernel<false>, grid, dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
-                       (const int4*)work, (long long*)hist, B, nb_lds, sg, sh,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
-                       (const int*)work_off_dev);
-  }
+  if (rows == 0)
+    launch_hist_fx<true>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, nullptr,
+                         (const int4*)work, (long long*)hist, B, nb_lds, sg, sh, (const int*)nwork_dev,
+                         (const float*)scales_dev, (long long*)staging, (const int*)work_off_dev);
+  else
+    launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                          (const int4*)work, (long long*)hist, B, nb_lds, sg, sh, (const int*)nwork_dev,
+                          (const float*)scales_dev, (long long*)staging, (const int*)work_off_dev);
   YTK_LAUNCH_CHECK();
-  const int E = nb_lds * 32;
+  const int E = nb_lds * fw;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
                      (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids,
-                     (const int*)nullptr, (const int2*)nullptr);
+                     (const int*)nullptr, (const int2*)nullptr, fw);
   YTK_LAUNCH_CHECK();
 }
 
@@ -561,29 +583,25 @@ void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t g
                             uintptr_t scales_dev, uintptr_t staging, uintptr_t slot_ids, uintptr_t nslots_dev,
                             uintptr_t slot_range, int reduce_y, uintptr_t stream) {
   if (max_work <= 0) return;
-  const int groups = (F + 31) / 32;
+  const int fw = g_hist_fw;
+  const int groups = (F + fw - 1) / fw;
   const int nb_lds = B;
-  const size_t lds = (size_t)nb_lds * 64 * sizeof(unsigned long long);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (rows == 0) {
-    hipLaunchKernelGGL(hist_fx_kernel<true>, dim3(max_work, groups), dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)nullptr,
-                       (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
-                       (const int*)nullptr);
-  } else {
-    hipLaunchKernelGGL(hist_fx_kernel<false>, dim3(max_work, groups), dim3(kHistThreads), lds, s,
-                       (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
-                       (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f,
-                       (const int*)nwork_dev, (const float*)scales_dev, (long long*)staging,
-                       (const int*)nullptr);
-  }
+  const dim3 grid(max_work, groups);
+  if (rows == 0)
+    launch_hist_fx<true>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, nullptr,
+                         (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f, (const int*)nwork_dev,
+                         (const float*)scales_dev, (long long*)staging, nullptr);
+  else
+    launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                          (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f, (const int*)nwork_dev,
+                          (const float*)scales_dev, (long long*)staging, nullptr);
   YTK_LAUNCH_CHECK();
-  const int E = nb_lds * 32;
+  const int E = nb_lds * fw;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
                      dim3(256), 0, s, (const long long*)staging, (const int4*)work, max_work,
                      (const int*)nwork_dev, (long long*)hist, B, F, nb_lds, groups, 0, (const int*)slot_ids,
-                     (const int*)nslots_dev, (const int2*)slot_range);
+                     (const int*)nslots_dev, (const int2*)slot_range, fw);
   YTK_LAUNCH_CHECK();
 }
 

@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from ytk_learn_amd.ops import gbdt as gops
+from ytk_learn_amd.ops._ext import hist_cols
 
 pytestmark = pytest.mark.gpu
 
@@ -323,7 +324,7 @@ def test_hist_build_staged_matches_cpu(cuda, F, nb, N, items_per_slot):
         hc = torch.zeros((6, B, F, 2), dtype=torch.int64)
         gops.hist_build(bins, F, gh, perm, work_t, hc, B, SG, SH)
         hg = torch.zeros((6, B, F, 2), dtype=torch.int64, device=cuda)
-        staging = torch.empty(len(work) * ((F + 31) // 32) * B * 64, dtype=torch.int64, device=cuda)
+        staging = torch.empty(len(work) * hist_cols(F) * B * 2, dtype=torch.int64, device=cuda)
         gops.hist_build(bins.to(cuda), F, gh.to(cuda), perm.to(cuda), work_t.to(cuda), hg, B, SG, SH,
                         staging=staging, slot_base=2, nslots=nslot,
                         slot_ids=None if slot_ids is None else torch.tensor(slot_ids, dtype=torch.int32, device=cuda))

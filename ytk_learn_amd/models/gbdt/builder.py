@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
-from ...ops._ext import hip, stream
+from ...ops._ext import hip, hist_cols, stream
 from ...parallel.comm import Comm
 from .tree import Tree
 
@@ -610,7 +610,7 @@ class TreeBuilder:
         gp = self.gp_tree
         if nb:
             h.zero_slots(self.hist.data_ptr(), self.slot_bytes, base + 4 * off[2], nb, s)
-            need = nwork * ((self.F + 31) // 32) * self.B * 64
+            need = nwork * hist_cols(self.F) * self.B * 2
             if self._staging is None or self._staging.numel() < need:
                 self._staging = torch.empty(int(need * 1.25), dtype=torch.int64, device=self.dev)
             h.hist_fx_staged(self.bins.data_ptr(), self.bins.shape[1], self.F, self.ghp.data_ptr(),

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
-from ...ops._ext import hip, ptr, stream
+from ...ops._ext import hip, hist_cols, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams, resolve_hist_sync
@@ -171,13 +171,12 @@ class DeviceLevelBuilder:
         self._root_fixed = False
         # staged histogram flush: block partials to a staging slab with plain stores, then a
         # split-K slot reduce (8 int64 atomics per value instead of one per block)
-        groups = (F + 31) // 32
         max_hist_items = self.hist_target + (self.maxp // 2) + 2
         self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0" and not self.wide
         # multi-GPU: overlap the all-reduce of half a level's histograms with the build of
         # the other half (BASELINE: histogram all-reduce overlapped with the next block's build)
         self.overlap = os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
-        self.staging = (torch.empty(max_hist_items * groups * B * 32 * 2, dtype=torch.int64, device=dev)
+        self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
         self.rows = torch.empty(self.N, dtype=torch.int32, device=dev)

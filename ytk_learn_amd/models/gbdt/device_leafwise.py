@@ -23,7 +23,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ...ops._ext import hip, ptr, stream
+from ...ops._ext import hip, hist_cols, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams
@@ -94,8 +94,7 @@ class DeviceLeafBuilder:
         # histogram slots: one per speculative node (never recycled inside a tree)
         self.hist = torch.zeros((cap, B, F, 2), dtype=torch.int64, device=dev)
         self.slot_bytes = B * F * 16
-        groups = (F + 31) // 32
-        self.staging = torch.empty(self.hist_bound * groups * B * 32 * 2, dtype=torch.int64, device=dev)
+        self.staging = torch.empty(self.hist_bound * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
         self.rows2 = torch.empty(2 * N, dtype=torch.int32, device=dev)
         self.gh2 = torch.empty((2 * N, 2), dtype=torch.float32, device=dev)
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)

@@ -37,6 +37,14 @@ def _try_build():
         sys.path.pop(0)
 
 
+HIST_FW = int(os.environ.get("YTK_HIST_FW", "32"))
+
+
+def hist_cols(F: int) -> int:
+    """Histogram staging columns per bin: F rounded up to the per-block feature group."""
+    return -(-F // HIST_FW) * HIST_FW
+
+
 def hip():
     """The HIP kernel module (gfx950). Raises if not built/loadable."""
     global _HIP
@@ -51,6 +59,8 @@ def hip():
                 raise ExtensionMissing(
                     "HIP extension ytk_learn_amd.ops._ytk_hip is not built; run `python csrc/build.py`"
                 ) from e
+        # features per histogram block (YTK_HIST_FW = 32 | 16): see hist_fx_kernel
+        _HIP.hist_set_fw(HIST_FW)
     return _HIP
 
 

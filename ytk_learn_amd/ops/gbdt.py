@@ -15,7 +15,7 @@ import os
 import numpy as np
 import torch
 
-from ._ext import check_cuda, hip, ptr, stream
+from ._ext import check_cuda, hip, hist_cols, ptr, stream
 
 SPLIT_DTYPE = np.dtype(
     [("loss_chg", "<f4"), ("feat", "<i4"), ("bin_a", "<i4"), ("bin_b", "<i4"),
@@ -90,7 +90,7 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
     work: int32 [nwork, 4] = (slot, begin, end, 0); positions index ``rows``
     hist: int64 [slots, B, F, 2], target slots must be zeroed by the caller
     sg, sh: power-of-two fixed-point scales (``fixed_point_scales``)
-    staging: optional int64 scratch (>= nwork * ceil(F/32) * B * 64 elements): block
+    staging: optional int64 scratch (>= nwork * hist_cols(F) * B * 2 elements): block
       partials are stored, then reduced into the work's slots, which must be the
       contiguous range [slot_base, slot_base + nslots) (two-stage flush, no per-block
       global atomics -- see csrc/hip/gbdt_hist.hip); ``slot_ids`` (int32 device tensor of
@@ -112,7 +112,7 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
         h = hip()
         if bins.dtype == torch.uint8 and B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32:
             if staging is not None and nslots > 0:
-                assert staging.numel() >= nwork * ((F + 31) // 32) * B * 64
+                assert staging.numel() >= nwork * hist_cols(F) * B * 2
                 h.hist_fx_staged(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                                  float(sg), float(sh), 0, 0, ptr(staging), slot_base, nslots, ptr(slot_ids),
                                  0, stream(bins))
