@@ -16,8 +16,9 @@
 //   lw_plan      (1 workgroup) apply the last batch's split records, replay the queue
 //                (wave-wide argmax over LDS keys; the sequential part never touches
 //                global memory), write the tree nodes the replay finalised (all lanes,
-//                from an LDS event list), choose the next batch (top-k candidates by gain,
-//                LDS bitonic sort), emit the partition work (device counts).
+//                from an LDS event list), choose the next batch (the unexpanded nodes the
+//                growth would split within the leaf budget, ranked by bottleneck key),
+//                emit the partition work (device counts).
 //   partition    partition_atomic_kernel: children land in the OTHER half of a 2N-entry
 //                ping-pong row buffer (out_shift), so no copy-back of the segments.
 //   lw_children  child counts from the split cursors, smaller child, histogram chunks,
@@ -44,7 +45,7 @@ enum {
 constexpr int kLwThreads = 256;
 constexpr int kLwCap = 2304;     // speculative nodes per tree (LDS-staged by the planner)
 constexpr int kLwLeafMax = 512;   // max_leaf_cnt supported by the device engine
-constexpr int kLwSort = 4096;     // candidate sort width (power of two >= kLwCap)
+constexpr int kLwSort = 4096;     // LDS scratch (u64): replay events, then batch-choice keys
 constexpr int kLwChunk = 2048;    // rows per partition block (partition_atomic_kernel CH)
 constexpr int kLwReduceDirect = 16;  // == kReduceDirect (gbdt_hist.hip)
 
@@ -269,11 +270,12 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   __shared__ float s_loss[kLwCap];
   __shared__ int s_seq[kLwCap];
   __shared__ int s_hsid[kLwLeafMax + 8];
+  __shared__ int s_par[kLwCap];  // batch choice: forest parents (pointer jumping)
   __shared__ unsigned long long s_akey[kLwQueueSort];        // poppable queue entries, sorted
   __shared__ unsigned long long s_bkey[2 * kLwLeafMax + 8];  // children heap
   __shared__ int s_uid[3 * kLwLeafMax + 16];                 // blocking entries
   __shared__ int s_na, s_nu;
-  // replay events (then reused as the candidate sort buffer: kLwSort u64 = 32 KiB)
+  // replay events (then reused by the batch choice: rank keys + bottlenecks, 27 KiB)
   __shared__ unsigned long long s_buf[kLwSort];
   __shared__ int s_tmp[kLwThreads / kWave + 1];
   __shared__ int s_nev, s_blocked, s_nh, s_num_leaf, s_ntree, s_seqc, s_k, s_ncand;
@@ -454,45 +456,137 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   nh = s_nh;
   // E. next batch: the blocked node + the best other candidates
   int k = 0;
+  const int remaining = p.max_leaf > 0 ? p.max_leaf - num_leaf : 1;
   if (blocked >= 0) {
-    const int remaining = p.max_leaf > 0 ? p.max_leaf - num_leaf : 1;
     const int fr = p.cap - nsid;
     // keep one net node pair per future split (LeafGrower slack rule): never runs dry
     k = p.speculate ? max(1, min(remaining, (fr - remaining - 1) >> 1)) : 1;
     if (fr < 2) k = 0;
   }
+  int* s_batch = reinterpret_cast<int*>(s_akey);  // the batch, in pop order (A is consumed)
   if (k > 0) {
-    // candidates: known gain, not expanded, not final, splittable by the static rules
+    // Which unexpanded nodes would the sequential growth split within the leaf budget?
+    // (the host planner's virtual replay, builder.py _grow_loss_guided). A priority queue
+    // over a forest pops nodes in decreasing order of their BOTTLENECK key (the minimum
+    // key on the path from the queue entry that roots them), so with the not-yet-computed
+    // children treated as absent, the nodes popped as splits before the budget runs out
+    // are the top `remaining` splittable known nodes by bottleneck; the batch is the
+    // unexpanded ones among them, best first. Pointer jumping gives the bottlenecks in
+    // log(depth) block steps; each candidate's rank is a count over the splittable set.
+    // (Top-k by the node's own gain expanded ~1.6x as many nodes: docs/performance.md.)
+    unsigned long long* s_rk = s_buf;                                 // [kLwCap] splittable rank keys
+    unsigned* s_m = reinterpret_cast<unsigned*>(s_buf + kLwCap);      // [kLwCap] bottleneck ord(loss)
+    constexpr int kPer = (kLwCap + kLwThreads - 1) / kLwThreads;
+    auto ord = [](float f) {
+      const unsigned u = __float_as_uint(f);
+      return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    };
+    auto live = [&](int i) { return ((s_nd[i].z >> 16) & 0xff) == 1; };  // known gain, not final
+    for (int i = tid; i < nsid; i += kLwThreads) {
+      s_par[i] = -1;
+      s_m[i] = ord(s_loss[i]);
+    }
+    __syncthreads();
+    for (int i = tid; i < nsid; i += kLwThreads) {
+      const int4 nd = s_nd[i];
+      if (((nd.z >> 16) & 0xff) == 1 && nd.x >= 0) s_par[nd.x] = s_par[nd.x + 1] = i;
+    }
+    __syncthreads();
+    while (true) {
+      unsigned nm[kPer];
+      int np[kPer];
+      int any = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int i = tid + j * kLwThreads;
+        np[j] = -1;
+        if (i < nsid) {
+          const int pp = s_par[i];
+          nm[j] = s_m[i];
+          if (pp >= 0) {
+            nm[j] = min(nm[j], s_m[pp]);
+            np[j] = s_par[pp];
+            any = 1;
+          }
+        }
+      }
+      if (!__syncthreads_or(any)) break;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int i = tid + j * kLwThreads;
+        if (i < nsid) {
+          s_m[i] = nm[j];
+          s_par[i] = np[j];
+        }
+      }
+      __syncthreads();
+    }
+    LW_TICK(22);
+    // the splittable live nodes (each pops as a split): rank keys, compacted
+    auto splittable = [&](int i) { return live(i) && (s_nd[i].z >> 24) == 0; };
+    auto rkey = [&](int i) {
+      return i == blocked ? ~0ull
+                          : (((unsigned long long)s_m[i] << 32) |
+                             (unsigned long long)((ord(s_loss[i]) >> 12) << 12) | (unsigned long long)i);
+    };
     const int per = (nsid + kLwThreads - 1) / kLwThreads;
     const int i0 = min(nsid, tid * per), i1 = min(nsid, i0 + per);
-    int c = 0;
-    // state 1 (known gain, not final), not expanded, not a leaf by the static rules
-    auto cand = [&](int i) {
-      const int4 nd = s_nd[i];
-      return ((nd.z >> 16) & 0xff) == 1 && nd.x < 0 && (nd.z >> 24) == 0;
-    };
-    for (int i = i0; i < i1; ++i) c += cand(i) ? 1 : 0;
-    int ncand;
-    int pos = lw_scan(c, s_tmp, &ncand);
+    int c = 0, cc = 0;
     for (int i = i0; i < i1; ++i) {
-      if (cand(i)) {
-        unsigned u = __float_as_uint(s_loss[i]);
-        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-        s_buf[pos++] = (i == blocked) ? ~0ull
-                                      : (((unsigned long long)u << 32) | (unsigned long long)(0xffffffffu - (unsigned)i));
+      const bool sp = splittable(i);
+      c += sp ? 1 : 0;
+      cc += (sp && s_nd[i].x < 0) ? 1 : 0;
+    }
+    int ns, ncand;
+    int pos = lw_scan(c, s_tmp, &ns);
+    int pc = lw_scan(cc, s_tmp, &ncand);
+    int* s_cand = s_par;  // all -1 after the pointer jumping: reused as the candidate list
+    for (int i = i0; i < i1; ++i) {
+      if (!splittable(i)) continue;
+      s_rk[pos++] = rkey(i);
+      if (s_nd[i].x < 0) s_cand[pc++] = i;
+    }
+    const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= kLwCap (a multiple of 128)
+    for (int z = ns + tid; z < ns_pad; z += kLwThreads) s_rk[z] = 0ull;  // never ranks above a key
+    for (int r = tid; r < remaining; r += kLwThreads) s_uid[r] = -1;
+    __syncthreads();
+    LW_TICK(23);
+    // rank of each candidate among the splittable set: a wave takes 4 candidates, every
+    // key it loads is compared with all 4 (ballot + popcount: wave-uniform counts)
+    const int rem = remaining;
+    const int lane = tid & (kWave - 1);
+    for (int g = (tid >> 6) * 4; g < ncand; g += kLwThreads / kWave * 4) {
+      unsigned long long me[4];
+      int rank[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        me[j] = g + j < ncand ? rkey(s_cand[g + j]) : ~0ull;
+        rank[j] = 0;
+      }
+      for (int z0 = 0; z0 < ns_pad; z0 += 2 * kWave) {
+        const unsigned long long a0 = s_rk[z0 + lane], a1 = s_rk[z0 + kWave + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rank[j] += __popcll(__ballot(a0 > me[j])) + __popcll(__ballot(a1 > me[j]));
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (g + j < ncand && rank[j] < rem) s_uid[rank[j]] = s_cand[g + j];
       }
     }
     __syncthreads();
-    if (ncand > k) {
-      // top-k: bitonic sort (descending) of the candidate keys, zero padded
-      int n2 = 1;
-      while (n2 < ncand) n2 <<= 1;
-      for (int i = ncand + tid; i < n2; i += kLwThreads) s_buf[i] = 0ull;
-      __syncthreads();
-      lw_bitonic_desc(s_buf, n2);
-    }
+    LW_TICK(24);
+    // compact the chosen ones in rank order
+    const int pr = (rem + kLwThreads - 1) / kLwThreads;
+    const int r0 = min(rem, tid * pr), r1 = min(rem, r0 + pr);
+    int nc = 0;
+    for (int r = r0; r < r1; ++r) nc += s_uid[r] >= 0 ? 1 : 0;
+    int nsel;
+    int q = lw_scan(nc, s_tmp, &nsel);
+    for (int r = r0; r < r1; ++r)
+      if (s_uid[r] >= 0) s_batch[q++] = s_uid[r];
     if (tid == 0) {
-      s_k = min(k, ncand);
+      s_k = min(k, nsel);
       s_ncand = ncand;
     }
     __syncthreads();
@@ -501,8 +595,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   LW_TICK(4);
   // F. expand the batch: children ids, partition descriptors (chunks of kLwChunk rows)
   for (int j = tid; j < k; j += kLwThreads) {
-    const unsigned long long key = s_buf[j];
-    const int P = (key == ~0ull) ? blocked : (int)(0xffffffffu - (unsigned)(key & 0xffffffffull));
+    const int P = s_batch[j];
     const int lc = nsid + 2 * j;
     s_nd[P].x = lc;
     b.batch[j] = P;

@@ -279,6 +279,8 @@ class DeviceLeafBuilder:
         out.update(plan_calls=int(v[8]), part_blocks=int(v[9]), replay_events=int(v[10]), candidates=int(v[11]),
                    hist_rows=int(v[12]), built_slots=int(v[13]), hist_items=int(v[14]),
                    replay_sorted_pops=int(v[21]))
+        for i, n in ((22, "jump"), (23, "keys"), (24, "rank")):  # parts of "select"
+            out[f"plan_select_{n}_us"] = round(float(v[i]) / 100.0, 1)
         return out
 
     def _batch(self, h, hd, rows_in, gh_in, fmask, f0, s):
