@@ -50,7 +50,7 @@ constexpr int kLwChunk = 2048;    // rows per partition block (partition_atomic_
 constexpr int kLwReduceDirect = 16;  // == kReduceDirect (gbdt_hist.hip)
 
 struct LwParams {
-  int max_depth, max_leaf, min_split_samples, speculate;
+  int max_depth, max_leaf, min_split_samples, speculate;  // speculate: 0 off, else percent
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
   int hist_target, min_rows, cap, N;  // N: half size of the ping-pong row buffers
 };
@@ -548,12 +548,13 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     }
     const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= kLwCap (a multiple of 128)
     for (int z = ns + tid; z < ns_pad; z += kLwThreads) s_rk[z] = 0ull;  // never ranks above a key
-    for (int r = tid; r < remaining; r += kLwThreads) s_uid[r] = -1;
+    // rank window: speculate percent of the leaf budget (s_uid holds 3 kLwLeafMax ranks)
+    const int rem = min(3 * kLwLeafMax, max(1, remaining * p.speculate / 100));
+    for (int r = tid; r < rem; r += kLwThreads) s_uid[r] = -1;
     __syncthreads();
     LW_TICK(23);
     // rank of each candidate among the splittable set: a wave takes 4 candidates, every
     // key it loads is compared with all 4 (ballot + popcount: wave-uniform counts)
-    const int rem = remaining;
     const int lane = tid & (kWave - 1);
     for (int g = (tid >> 6) * 4; g < ncand; g += kLwThreads / kWave * 4) {
       unsigned long long me[4];
@@ -835,6 +836,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.max_leaf = ip[1];
   p.min_split_samples = ip[2];
   p.speculate = ip[3];
+  if (p.speculate < 0 || p.speculate > 300) throw std::invalid_argument("lw_create: speculate percent must be in [0, 300]");
   p.hist_target = ip[4];
   p.min_rows = ip[5];
   p.cap = ip[6];

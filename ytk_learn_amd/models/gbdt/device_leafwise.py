@@ -151,7 +151,9 @@ class DeviceLeafBuilder:
 
     def _ip(self):
         p = self.p
-        spec = 1 if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
+        # speculation: 0 = one node per batch; else the percentage of the remaining leaf
+        # budget the batch choice ranks within (100 = the host planner's virtual replay)
+        spec = int(os.environ.get("YTK_LW_SPEC_PCT", "100")) if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
         return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
                 self.cap, self.N]
 
