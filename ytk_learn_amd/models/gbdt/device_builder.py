@@ -175,7 +175,10 @@ class DeviceLevelBuilder:
         self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0" and not self.wide
         # multi-GPU: overlap the all-reduce of half a level's histograms with the build of
         # the other half (BASELINE: histogram all-reduce overlapped with the next block's build)
-        self.overlap = os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
+        # Only with enough local rows: at a small shard (strong scaling, e.g. Higgs / 8) a
+        # level's build is ~10-20 us, less than the launch latency of the second collective.
+        self.overlap = (os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
+                        and self.N >= int(os.environ.get("YTK_HIST_OVERLAP_MIN_ROWS", "2000000")))
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
