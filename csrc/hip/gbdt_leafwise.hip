@@ -66,7 +66,8 @@ struct LwBufs {
   int* heap;  // [max_leaf + 2] speculative ids of the queue
   int* batch;  // [max_leaf] parents expanded by the current batch
   int *part_feat, *part_thr, *part_begin, *part_cnt, *part_first, *part_shift;  // [max_leaf]
-  unsigned long long* cursor;  // [max_leaf] partition cursors ((right << 32) | left)
+  unsigned long long* cursor;  // [max_leaf * kCurStride + kDoneWords] split cursors ((right << 32) | left)
+                               // a cache line apart, then the done counters
   int4* hist_items;            // [hist bound]
   int* build_ids;              // [max_leaf + 1] slots built this batch
   int4* split_items;           // [2 max_leaf + 2]
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     b.part_cnt[j] = cnt;
     b.part_shift[j] = beg < p.N ? p.N : -p.N;
     b.part_first[j] = (cnt + kLwChunk - 1) / kLwChunk;
-    b.cursor[j] = 0ull;
+    b.cursor[(size_t)j * kCurStride] = 0ull;
   }
   __syncthreads();
   const int nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
@@ -688,7 +689,7 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
   for (int j = tid; j < k; j += kLwThreads) {
     const int P = b.batch[j];
     const int L = b.lc[P], R = L + 1;
-    const unsigned long long cur = __hip_atomic_load(&b.cursor[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long cur = __hip_atomic_load(&b.cursor[(size_t)j * kCurStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int lloc = (int)(cur & 0xffffffffull);
     const int lb = b.part_begin[j] + b.part_shift[j];
     const int rcnt = b.part_cnt[j] - lloc;
@@ -782,16 +783,12 @@ void lw_partition_kernel(LwParams p, LwBufs b, const uint8_t* binsT,
                                                                    float2* gh_out) {
   partition_atomic_body<uint8_t, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
                                        b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                       b.cursor, b.part_shift);
+                                       b.cursor, b.part_shift, kCurStride);
   // No fences: the only cross-block data the last block reads are the split cursors,
   // updated by RETURNING device-scope atomics (complete before this block counts itself)
   // and read back with atomic loads. (An agent-scope release fence per block writes back
   // the XCD's L2 on MI355X and doubled this kernel's time.)
-  __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&b.st[LW_PART_DONE], 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
+  if (!last_block_done(b.cursor + (size_t)p.max_leaf * kCurStride)) return;
   lw_children_body(p, b);
 }
 

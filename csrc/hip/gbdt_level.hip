@@ -271,6 +271,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
       b.part_nblk[s] = n.cnt_local;              // temporarily: count
       b.part_cnt[s] = n.cnt_local;
       b.left_loc[s] = 0;
+      b.left_loc[(size_t)s * kCurStride] = 0;  // the fused partition's line-spaced cursor
       atomicAdd(reinterpret_cast<unsigned long long*>(&s_total), (unsigned long long)n.cnt_local);
     }
   }
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
 // KP: bound on the level's splits (LDS arrays); kAtomicCursor: the cursors were just
 // updated by atomics of other blocks of the same kernel (fused partition epilogue)
 template <int KP, bool kAtomicCursor>
-__device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int build_base, int half, int dgap,
+__device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs, int build_base, int half, int dgap,
                                       int use_loc, int fused) {
   __shared__ int s_nb[KP];     // 1 if the split's children get histograms
   __shared__ int s_small[KP];  // small child node id
@@ -325,11 +326,11 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int bu
     // count-only pass accumulates the left rows alone -- either way the low half
     long long lloc, lglob;
     if (kAtomicCursor) {
-      lloc = __hip_atomic_load(&b.left_loc[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
-      lglob = __hip_atomic_load(&lglob_arr[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+      lloc = __hip_atomic_load(&b.left_loc[(size_t)s * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+      lglob = __hip_atomic_load(&lglob_arr[(size_t)s * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
     } else {
-      lloc = b.left_loc[s] & 0xffffffffll;
-      lglob = lglob_arr[s] & 0xffffffffll;
+      lloc = b.left_loc[(size_t)s * cs] & 0xffffffffll;
+      lglob = lglob_arr[(size_t)s * cs] & 0xffffffffll;
     }
     reset_node(L, P.depth + 1);
     reset_node(R, P.depth + 1);
@@ -407,7 +408,7 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int bu
 __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams p, LvBufs b, int build_base,
                                                                     int half, int dgap, int use_loc,
                                                                     int fused) {
-  lv_plan_children_body<kMaxPend, false>(p, b, build_base, half, dgap, use_loc, fused);
+  lv_plan_children_body<kMaxPend, false>(p, b, 1, build_base, half, dgap, use_loc, fused);
 }
 
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
@@ -417,16 +418,12 @@ template <bool kScatter, int KP>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
-                                  int dgap, int use_loc, int fused) {
+                                  int dgap, int use_loc, int fused, int maxp) {
   partition_atomic_body<uint8_t, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                            b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr);
-  __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&b.st[ST_PART_DONE], 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  lv_plan_children_body<KP, true>(p, b, build_base, half, dgap, use_loc, fused);
+                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
+  if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
+  lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
 }
 
 // Bin-threshold arrays used by the fused score/gradient kernel.
@@ -603,7 +600,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
 #define YTK_LVPC(SC, KP)                                                                                     \
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
-                     (float2*)gh_out, arg0, half, dgap, use_loc, fused)
+                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
   if (maxp <= 64) {
     if (count_only) YTK_LVPC(false, 64); else YTK_LVPC(true, 64);
   } else if (maxp <= 512) {

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
     unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift) {
   partition_atomic_body<BinT, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, first_blk, nsplit_dev,
-                                        nblocks_dev, feat, thr, node_begin, node_count, cursor, out_shift);
+                                        nblocks_dev, feat, thr, node_begin, node_count, cursor, out_shift, 1);
 }
 
 }  // namespace ytk

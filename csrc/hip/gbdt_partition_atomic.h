@@ -9,6 +9,42 @@ namespace ytk {
 constexpr int kPartThreads = 256;
 constexpr int kPartGrid = 256 * 8;  // persistent partition blocks: 8 per CU
 constexpr int kAtomSub = 8;  // single-pass partition: rows per block = 8 x 256 (one chunk)
+// Device-scope atomics on ONE cache line serialise at ~12 ns each on MI355X
+// (tools/microbench/atomic_contention.hip: 5127 returning 64-bit adds, one per 2048-row
+// chunk = one partition level of Higgs, take 63.5 us on one line, 7 us over 32 lines
+// 4 KiB apart). The engines therefore space the split cursors a cache line apart
+// (kCurStride u64) and count finished blocks through kDoneGroups line-spaced counters.
+constexpr int kCurStride = 16;   // u64 per split cursor (128 B)
+constexpr int kDoneGroups = 16;
+constexpr int kDoneWords = (kDoneGroups + 1) * kCurStride;  // u64 of counter space
+
+// true in exactly one block of the grid: the last to arrive. Block b counts itself in
+// group b % G; the block completing its group counts the group at the top counter. All
+// counters reset themselves (atomic exchange by their last arriver), so ctr must be zero
+// only before the first launch. ctr: kDoneWords u64 (zeroed once).
+__device__ __forceinline__ bool last_block_done(unsigned long long* ctr64) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* ctr = reinterpret_cast<unsigned*>(ctr64);
+    const unsigned G = min(gridDim.x, (unsigned)kDoneGroups);
+    const unsigned g = blockIdx.x % G;
+    const unsigned members = (gridDim.x - g + G - 1) / G;
+    unsigned* grp = ctr + (size_t)g * kCurStride * 2;
+    unsigned* top = ctr + (size_t)kDoneGroups * kCurStride * 2;
+    bool last = false;
+    if (atomicAdd(grp, 1u) == members - 1) {
+      atomicExch(grp, 0u);
+      if (atomicAdd(top, 1u) == G - 1) {
+        atomicExch(top, 0u);
+        last = true;
+      }
+    }
+    s_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
 
 // Single-pass partition (level engine): each block holds one <= 2048-row chunk in
 // registers, gathers its go-left flags, ranks them with wave ballots, reserves its left
@@ -26,7 +62,8 @@ __device__ __forceinline__ void partition_atomic_body(
     const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
-    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift) {
+    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs) {
+  // cs: cursor stride (u64; kCurStride in the engines, 1 for the standalone kernel)
   // one chunk (<= kAtomSub * 256 rows) per block, held in registers: all loads issued
   // up front, ONE cursor reservation per block, then the scatter. The block finds its
   // (split, chunk) by binary search of first_blk (exclusive scan of the splits' chunk
@@ -107,9 +144,9 @@ __device__ __forceinline__ void partition_atomic_body(
     if (l == 0) {
       const int tv = end - beg;
       if (!kScatter) {
-        atomicAdd(&cursor[si], (unsigned long long)tl_all);  // count-only: the left rows
+        atomicAdd(&cursor[(size_t)si * cs], (unsigned long long)tl_all);  // count-only: the left rows
       } else {
-        s_base = atomicAdd(&cursor[si], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
+        s_base = atomicAdd(&cursor[(size_t)si * cs], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
         s_tl = tl_all;
       }
     }

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
-from ...ops._ext import hip, hist_cols, ptr, stream
+from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams, resolve_hist_sync
@@ -128,8 +128,12 @@ class DeviceLevelBuilder:
         self.part_first, self.part_nblk = i32(self.maxp), i32(self.maxp)
         self.part_counts = i32(self.max_items)
         self.part_cnt = i32(self.maxp)
-        self.left_loc = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
-        self.left_glob = torch.zeros(self.maxp, dtype=torch.int64, device=dev)
+        # per-split left counters / partition cursors: index s (standalone partition kernels)
+        # or s * CUR_STRIDE (fused partition: one cache line per cursor), then the fused
+        # kernel's self-resetting done counters (csrc/hip/gbdt_partition_atomic.h)
+        ncur = self.maxp * CUR_STRIDE + DONE_WORDS
+        self.left_loc = torch.zeros(ncur, dtype=torch.int64, device=dev)
+        self.left_glob = torch.zeros(ncur, dtype=torch.int64, device=dev)
         self.hist_items = i32(self.max_items * 4)
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)

@@ -23,7 +23,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ...ops._ext import hip, hist_cols, ptr, stream
+from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams
@@ -78,7 +78,8 @@ class DeviceLeafBuilder:
         self.nd_loss = torch.zeros(cap, dtype=torch.float32, device=dev)
         self.heap, self.batch = i32(ml + 8), i32(ml)
         self.part = torch.zeros((6, ml), dtype=torch.int32, device=dev)
-        self.cursor = torch.zeros(ml, dtype=torch.int64, device=dev)
+        # split cursors a cache line apart + the partition kernel's done counters
+        self.cursor = torch.zeros(ml * CUR_STRIDE + DONE_WORDS, dtype=torch.int64, device=dev)
         self.hist_bound = self.HIST_TARGET + ml + 2
         self.hist_items = i32(4 * self.hist_bound)
         self.build_ids = i32(ml + 1)

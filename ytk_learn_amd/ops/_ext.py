@@ -40,6 +40,13 @@ def _try_build():
 HIST_FW = int(os.environ.get("YTK_HIST_FW", "32"))
 
 
+# == kCurStride / kDoneWords (csrc/hip/gbdt_partition_atomic.h): split cursors of the
+# GPU tree engines sit one 128-B line apart, followed by the fused partition kernels'
+# done counters
+CUR_STRIDE = 16
+DONE_WORDS = 17 * CUR_STRIDE
+
+
 def hist_cols(F: int) -> int:
     """Histogram staging columns per bin: F rounded up to the per-block feature group."""
     return -(-F // HIST_FW) * HIST_FW
