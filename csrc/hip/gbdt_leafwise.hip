@@ -75,7 +75,7 @@ struct LwBufs {
   SplitOut* split_out;         // [2 max_leaf + 2]
   const long long* root_cnt;   // [0] local rows, [1] global rows
   unsigned long long* prof;    // optional [32]: planner phase times (wall clock ticks), rows
-  int* done_host;              // host-mapped pinned int: set with LW_DONE (optional)
+  int* done_host;              // host-mapped pinned int[2]: [0] LW_DONE, [1] batches planned (optional)
   int* zero_ids;               // [max_leaf + 1] built slots with != 1 histogram item
   int2* zero_range;            // [max_leaf + 1] their items [x, x + y)
 };
@@ -651,8 +651,11 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       if (b.done_host) *(volatile int*)b.done_host = 1;  // polled by the host: no copy launch
       if (blocked >= 0) st[LW_OVERFLOW] = 1;  // cannot happen with cap >= max_leaf + 2
     } else {
-      st[LW_BATCHES] += 1;
+      const int nb = st[LW_BATCHES] + 1;
+      st[LW_BATCHES] = nb;
       st[LW_EXPANDED] += k;
+      // planner progress for the host's launch throttle (reads pinned memory, no events)
+      if (b.done_host) ((volatile int*)b.done_host)[1] = nb;
     }
   }
   LW_TICK(6);

@@ -18,6 +18,7 @@ the histogram's extra gather cost more).
 from __future__ import annotations
 
 import os
+import time
 from typing import Optional
 
 import numpy as np
@@ -46,6 +47,7 @@ class DeviceLeafBuilder:
     # batches enqueued ahead of the done-flag check (capturing batches in HIP graphs was
     # measured: no gain -- the gaps between dependent kernels are on the device side)
     POLL_LAG = 2
+    POLL_TIMEOUT_S = 60.0
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
@@ -104,6 +106,8 @@ class DeviceLeafBuilder:
         self.max_pblocks = -(-N // PART_CHUNK) + ml + 1
         # done flag: the planner writes it straight into pinned host memory (no copy launch)
         self._done_host = torch.zeros(16, dtype=torch.int32).pin_memory()
+        self._dh_np = self._done_host.numpy()  # [0] done flag, [1] batches planned (written by lw_plan)
+        self.idle_hook = None  # called once per tree while the host waits on the planner
         self._done_dev = hip().host_device_ptr(self._done_host.data_ptr())
         self.tree_count = 0
         self.last_keep = None
@@ -245,24 +249,41 @@ class DeviceLeafBuilder:
         # the previous tree's batches all finished (its done flag was observed), so no
         # kernel writes the flag while it is reset
         self._done_host[0] = 0
+        self._done_host[1] = 0
         h.lw_step(hd, 0, s)
         self._hist_split(h, rows0, gh0, fmask, f0, s)
         tm.mark("root")
-        pend = []  # events of the batches in flight
+        # Launch throttle without events (a recorded event put a ~6 us gap before every
+        # planner launch): the planner writes its batch count to pinned host memory, the
+        # host keeps at most POLL_LAG batches queued beyond the last one planned and stops
+        # at the done flag. While it waits it runs the idle hook once per tree (the trainer
+        # converts the previous round's tree there, off the GPU's critical path).
+        dh = self._dh_np
+        idle = self.idle_hook
         it = 0
+        t_wait = None
         while True:
             self._batch(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2),
                         fmask, f0, s)
             it += 1
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.dev))
-            pend.append(ev)
-            if len(pend) > self.POLL_LAG:
-                pend.pop(0).synchronize()
-                if int(self._done_host[0]) != 0:
-                    break
             if it > 4 * self.max_leaf + 8:
                 raise RuntimeError("device leaf-wise builder did not terminate")
+            if dh[0] != 0:
+                break
+            if dh[1] >= it - self.POLL_LAG:
+                continue
+            if idle is not None:
+                idle()
+                idle = None
+            t_wait = time.perf_counter()
+            while dh[0] == 0 and dh[1] < it - self.POLL_LAG:
+                if time.perf_counter() - t_wait > self.POLL_TIMEOUT_S:
+                    raise RuntimeError(f"device leaf-wise builder: no planner progress for {self.POLL_TIMEOUT_S} s "
+                                       f"(batch {it}, planned {int(dh[1])})")
+            if dh[0] != 0:
+                break
+        if idle is not None:
+            idle()
         tm.mark("batches")
         h.lv_step(4, self._lv_ptrs(), [0] * 6, [0.0] * 6, self.max_nodes, 0, s)
         self.tree_count += 1
