@@ -145,6 +145,36 @@ __device__ __forceinline__ void lw_heap_sift_down(unsigned long long* key, int n
   key[i] = k;
 }
 
+// max of a u64 over the wave (every lane gets it)
+__device__ __forceinline__ unsigned long long lw_wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(v, off, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// (max key, its index) of key[0..n) by one wave, every lane gets both; (0, -1) when
+// n == 0. Keys are unique (node id in the low bits), so the index follows the key.
+__device__ __forceinline__ void lw_wave_argmax(const unsigned long long* key, int n, unsigned long long& kmax,
+                                               int& imax) {
+  const int l = threadIdx.x & (kWave - 1);
+  unsigned long long best = 0ull;
+  for (int i = l; i < n; i += kWave) {
+    const unsigned long long k = key[i];
+    best = k > best ? k : best;
+  }
+  best = lw_wave_max_u64(best);
+  int idx = -1;
+  for (int i = l; i < n; i += kWave)
+    if (key[i] == best) idx = i;
+  // the one lane that found it (if any) -> all lanes
+  const unsigned long long hit = __ballot(idx >= 0);
+  kmax = best;
+  imax = hit ? __shfl(idx, __builtin_ctzll(hit), kWave) : -1;
+}
+
 // block bitonic sort (descending) of a[0..n), n a power of two
 __device__ void lw_bitonic_desc(unsigned long long* a, int n) {
   for (int size = 2; size <= n; size <<= 1) {
@@ -272,6 +302,9 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   __shared__ int s_seq[kLwCap];
   __shared__ int s_hsid[kLwLeafMax + 8];
   __shared__ int s_par[kLwCap];  // batch choice: forest parents (pointer jumping)
+  // children of an expanded node, as the replay needs them (one LDS round trip per pop):
+  // {loss_l bits, loss_r bits, terminal-by-static-rules | poppable_l << 1 | poppable_r << 2, 0}
+  __shared__ int4 s_ch[kLwCap];
   __shared__ unsigned long long s_akey[kLwQueueSort];        // poppable queue entries, sorted
   __shared__ unsigned long long s_bkey[2 * kLwLeafMax + 8];  // children heap
   __shared__ int s_uid[3 * kLwLeafMax + 16];                 // blocking entries
@@ -319,7 +352,17 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     const int sl = lw_static_leaf(p, loss, depth, cnt) ? 1 : 0;
     s_loss[i] = loss;
     s_seq[i] = b.seq[i];
-    s_nd[i] = make_int4(b.lc[i], b.tid[i], depth | (b.state[i] << 16) | (sl << 24), cnt);
+    const int lc = b.lc[i];
+    s_nd[i] = make_int4(lc, b.tid[i], depth | (b.state[i] << 16) | (sl << 24), cnt);
+    if (lc >= 0) {
+      const float ll = b.loss[lc], lr = b.loss[lc + 1];
+      const int dc = b.depth[lc], cl = (int)b.cnt[lc], cr = (int)b.cnt[lc + 1];
+      const bool popl = lw_static_leaf(p, ll, dc, cl) || b.lc[lc] >= 0;
+      const bool popr = lw_static_leaf(p, lr, dc, cr) || b.lc[lc + 1] >= 0;
+      const bool tstat = (p.max_depth >= 0 && p.max_depth == dc) ||
+                         (p.min_split_samples > 0 && cl < p.min_split_samples && cr < p.min_split_samples);
+      s_ch[i] = make_int4(__float_as_int(ll), __float_as_int(lr), (tstat ? 1 : 0) | (popl ? 2 : 0) | (popr ? 4 : 0), 0);
+    }
   }
   int nh = st[LW_N_HEAP];
   for (int i = tid; i < nh; i += kLwThreads) s_hsid[i] = b.heap[i];
@@ -350,33 +393,46 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     lw_bitonic_desc(s_akey, n2);
   }
   LW_TICK(7);
-  if (tid == 0) {
+  if (tid < kWave) {
+    // Wave 0 runs the replay in lockstep: every lane holds the same scalar state and
+    // issues the same (same-address, conflict-free) LDS writes, so no lane ever reads a
+    // value another lane wrote; the lanes split only the scans (blocking max, children
+    // max after a B pop, the queue copy-out). The children of the replayed splits go to
+    // an UNSORTED array B with its running max (push: one store; pop: one wave max scan)
+    // -- a binary heap here cost ~log2(n) dependent LDS round trips per push and pop,
+    // about 1 us per replayed split.
+    const int lane = tid;
     const int na = s_na;
     int nu = s_nu;
     unsigned long long u = 0ull;
-    for (int i = 0; i < nu; ++i) {
+    for (int i = lane; i < nu; i += kWave) {
       const int sid = s_uid[i];
       const unsigned long long k = lw_qkey(s_loss[sid], s_seq[sid], sid);
       u = k > u ? k : u;
     }
+    u = lw_wave_max_u64(u);
     int num_leaf = st[LW_NUM_LEAF], ntree = st[LW_NUM_TNODES], seqc = st[LW_SEQ];
-    int nev = 0, blocked = -1, pa = 0, nbh = 0;
+    int nev = 0, blocked = -1, pa = 0, nbh = 0, bidx = -1;
+    unsigned long long bmax = 0ull;
     bool bulk = false;
+    unsigned long long ka = na > 0 ? s_akey[0] : 0ull;  // the next A key, loaded ahead
     while (true) {
       if (p.max_leaf > 0 && num_leaf == p.max_leaf) { bulk = true; break; }
-      const unsigned long long ka = pa < na ? s_akey[pa] : 0ull;
-      const unsigned long long kb = nbh > 0 ? s_bkey[0] : 0ull;
-      const unsigned long long top = ka > kb ? ka : kb;
+      const unsigned long long top = ka > bmax ? ka : bmax;
       if (u > top) { blocked = (int)(u & kLwSidMask); break; }
       if (top == 0ull) break;  // queue empty
       const int sid = (int)(top & kLwSidMask);
-      if (ka > kb) {
+      const int4 nd = s_nd[sid];
+      const int4 ch = s_ch[sid];
+      if (ka > bmax) {
         ++pa;
+        ka = pa < na ? s_akey[pa] : 0ull;
       } else {
         --nbh;
-        lw_heap_sift_down(s_bkey, nbh, s_bkey[nbh]);
+        const unsigned long long last = s_bkey[nbh];
+        if (bidx != nbh) s_bkey[bidx] = last;
+        lw_wave_argmax(s_bkey, nbh, bmax, bidx);
       }
-      const int4 nd = s_nd[sid];
       if (nd.z >> 24) {  // leaf by the static rules
         s_ev[nev++] = make_int4(EV_LEAF, sid, nd.y, 0);
         s_nd[sid].z = (nd.z & 0xff00ffff) | (2 << 16);
@@ -386,14 +442,11 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       ntree += 2;
       ++num_leaf;
       const int l = nd.x, r = l + 1;
-      const int4 ndl = s_nd[l], ndr = s_nd[r];
-      const float loss_l = s_loss[l], loss_r = s_loss[r];
-      const bool term = (p.max_depth >= 0 && p.max_depth == (ndl.z & 0xffff)) ||
-                        (p.max_leaf > 0 && p.max_leaf == num_leaf) ||
-                        (p.min_split_samples > 0 && ndl.w < p.min_split_samples && ndr.w < p.min_split_samples);
+      const bool term = (ch.z & 1) || (p.max_leaf > 0 && p.max_leaf == num_leaf);
       s_nd[sid].z = (nd.z & 0xff00ffff) | (2 << 16);
       s_ev[nev++] = make_int4(EV_SPLIT, sid, t, lt);
       if (term) {
+        const int4 ndl = s_nd[l], ndr = s_nd[r];
         s_ev[nev++] = make_int4(EV_LEAFIFY, sid, lt, 0);
         s_nd[l] = make_int4(ndl.x, lt, (ndl.z & 0xff00ffff) | (2 << 16), ndl.w);
         s_nd[r] = make_int4(ndr.x, lt + 1, (ndr.z & 0xff00ffff) | (2 << 16), ndr.w);
@@ -403,33 +456,51 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       s_nd[r].y = lt + 1;
       s_seq[l] = seqc;
       s_seq[r] = seqc + 1;
-      const unsigned long long kl = lw_qkey(loss_l, seqc, l), kr = lw_qkey(loss_r, seqc + 1, r);
+      const unsigned long long kl = lw_qkey(__int_as_float(ch.x), seqc, l);
+      const unsigned long long kr = lw_qkey(__int_as_float(ch.y), seqc + 1, r);
       seqc += 2;
-      if ((ndl.z >> 24) || ndl.x >= 0) lw_heap_push(s_bkey, nbh++, kl);
-      else { s_uid[nu++] = l; u = kl > u ? kl : u; }
-      if ((ndr.z >> 24) || ndr.x >= 0) lw_heap_push(s_bkey, nbh++, kr);
-      else { s_uid[nu++] = r; u = kr > u ? kr : u; }
-    }
-    // the remaining queue: A tail, the children heap, the blocking entries
-    int nr = 0;
-    for (int i = pa; i < na; ++i) s_hsid[nr++] = (int)(s_akey[i] & kLwSidMask);
-    for (int i = 0; i < nbh; ++i) s_hsid[nr++] = (int)(s_bkey[i] & kLwSidMask);
-    for (int i = 0; i < nu; ++i) s_hsid[nr++] = s_uid[i];
-    if (bulk) {  // leaf budget used: every queued node pops as a leaf (order-independent)
-      for (int i = 0; i < nr; ++i) {
-        const int sid = s_hsid[i];
-        s_ev[nev++] = make_int4(EV_LEAF, sid, s_nd[sid].y, 0);
-        s_nd[sid].z = (s_nd[sid].z & 0xff00ffff) | (2 << 16);
+      if (ch.z & 2) {
+        s_bkey[nbh] = kl;
+        if (kl > bmax) { bmax = kl; bidx = nbh; }
+        ++nbh;
+      } else {
+        s_uid[nu++] = l;
+        u = kl > u ? kl : u;
       }
+      if (ch.z & 4) {
+        s_bkey[nbh] = kr;
+        if (kr > bmax) { bmax = kr; bidx = nbh; }
+        ++nbh;
+      } else {
+        s_uid[nu++] = r;
+        u = kr > u ? kr : u;
+      }
+    }
+    // the remaining queue: A tail, the children array, the blocking entries (a set)
+    const int ra = na - pa;
+    for (int i = lane; i < ra; i += kWave) s_hsid[i] = (int)(s_akey[pa + i] & kLwSidMask);
+    for (int i = lane; i < nbh; i += kWave) s_hsid[ra + i] = (int)(s_bkey[i] & kLwSidMask);
+    for (int i = lane; i < nu; i += kWave) s_hsid[ra + nbh + i] = s_uid[i];
+    int nr = ra + nbh + nu;
+    if (bulk) {  // leaf budget used: every queued node pops as a leaf (order-independent)
+      for (int i = lane; i < nr; i += kWave) {
+        const int sid = s_hsid[i];
+        const int4 nd = s_nd[sid];
+        s_ev[nev + i] = make_int4(EV_LEAF, sid, nd.y, 0);
+        s_nd[sid].z = (nd.z & 0xff00ffff) | (2 << 16);
+      }
+      nev += nr;
       nr = 0;
     }
-    s_nev = nev;
-    s_blocked = blocked;
-    s_nh = nr;
-    s_num_leaf = num_leaf;
-    s_ntree = ntree;
-    s_seqc = seqc;
-    if (b.prof) atomicAdd(&b.prof[21], (unsigned long long)(pa));
+    if (lane == 0) {
+      s_nev = nev;
+      s_blocked = blocked;
+      s_nh = nr;
+      s_num_leaf = num_leaf;
+      s_ntree = ntree;
+      s_seqc = seqc;
+      if (b.prof) atomicAdd(&b.prof[21], (unsigned long long)(pa));
+    }
   }
   __syncthreads();
   LW_TICK(2);
