@@ -37,6 +37,10 @@ class SamplerSpec:
     dot_precision: int = 5
     use_log: bool = False
     use_min_max: bool = False
+    # no_sample only: neighbouring distinct values closer than this (float32 difference,
+    # > test) are one candidate -- the exact-greedy maker's Constants.MIN_FEA_SPLIT_GAP
+    # (1e-16f, FeatureParallelTreeMakerByLevel.java:384); 0 keeps every distinct value
+    min_split_gap: float = 0.0
 
     @classmethod
     def from_dict(cls, d: dict) -> "SamplerSpec":
@@ -58,6 +62,21 @@ def _weighted_quantile_values(vals: torch.Tensor, w: torch.Tensor, qs: torch.Ten
     return vals[idx]
 
 
+def merge_split_gap(vals: np.ndarray, gap: float) -> np.ndarray:
+    """Sorted distinct float32 values -> the first value of every run whose neighbouring
+    values differ by at most ``gap`` (float32 arithmetic, like the reference's
+    ``Math.abs(feaValue - lastFeaValue) > MIN_FEA_SPLIT_GAP`` on floats): the exact-greedy
+    scan never splits inside such a run, so it is one bin. Bin assignment maps a run's
+    members to its first value (nearest candidate); the threshold between two runs is the
+    midpoint of their first values (the reference takes the node's extreme values: equal
+    unless a run has several members, and then within the run's sub-``gap`` spread)."""
+    if vals.size < 2:
+        return vals
+    d = (vals[1:] - vals[:-1]).astype(np.float32)
+    keep = np.concatenate([[True], np.abs(d) > np.float32(gap)])
+    return vals[keep]
+
+
 def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: SamplerSpec,
                        comm: Comm, seed: int = 0) -> np.ndarray:
     """Sorted candidate split values for one feature column (already NaN-filled)."""
@@ -65,7 +84,8 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
     if t == "no_sample":
         vals = torch.unique(x)
         allv = comm.allgather_object(vals.cpu().numpy())
-        return np.unique(np.concatenate(allv).astype(np.float32))
+        out = np.unique(np.concatenate(allv).astype(np.float32))
+        return merge_split_gap(out, spec.min_split_gap) if spec.min_split_gap > 0 else out
     if t == "sample_by_cnt":
         # reservoir of max_cnt values per worker, union across workers
         g = torch.Generator(device="cpu").manual_seed(seed + comm.rank)

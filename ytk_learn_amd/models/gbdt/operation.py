@@ -10,7 +10,9 @@ a class id / K-vector for softmax; optional init prediction in the 4th field).
 ``tree_maker = "feature"`` (the reference's single-machine exact greedy maker,
 ``FeatureParallelTreeMakerByLevel.java``) is served by the same histogram engine with
 ``no_sample`` bins: every distinct value is a candidate and thresholds are midpoints of
-neighbouring values, which is exactly the exact-greedy split set.
+neighbouring values, which is exactly the exact-greedy split set; neighbouring values
+closer than ``MIN_FEA_SPLIT_GAP`` (1e-16, never a split point there) share one bin
+(``binning.merge_split_gap``). Wide candidate sets (> 256 values) use uint16 bins.
 """
 from __future__ import annotations
 
@@ -108,7 +110,8 @@ def run_gbdt(cfg, comm, log, transform_fn=None, threads=0, profile: bool = False
     if gp.tree_maker == "feature":
         if comm.is_dist:
             raise YtkLearnError("[GBDT] feature parallel only support single machine")
-        gp.approximate = [{"cols": "default", "type": "no_sample"}]
+        # every distinct value a candidate, runs closer than MIN_FEA_SPLIT_GAP merged
+        gp.approximate = [{"cols": "default", "type": "no_sample", "min_split_gap": 1e-16}]
     model = None
     if mp.continue_train or gp.just_evaluate:
         if mp.continue_train and not fs.exists(mp.data_path):
