@@ -9,4 +9,6 @@ step 900 pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 200 --t
 tail -2 $O/pytest_gpu.log
 step 400 bench.log python bench.py
 tail -1 $O/bench.log | cut -c1-900
+step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+tail -2 $O/smoke.log
 echo full ok
