@@ -54,7 +54,9 @@ void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, i
                    uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 void ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
-                   float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
+                   float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t,
+                   uintptr_t);
+int ytk_tree_grad_grid(long long);
 // sparse.hip
 void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, long long, int,
                   uintptr_t, long long, float, int, int, int, uintptr_t, uintptr_t);
@@ -118,6 +120,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("bin_assign", &ytk_bin_assign);
   m.def("grad_hess", &ytk_grad_hess);
   m.def("tree_grad", &ytk_tree_grad);
+  m.def("tree_grad_grid", &ytk_tree_grad_grid);
   m.def("seg_spmm", &ytk_seg_spmm);
   m.def("chunk_reduce", &ytk_chunk_reduce);
   m.def("ffm_pairs", &ytk_ffm_pairs);

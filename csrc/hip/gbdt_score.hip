@@ -267,15 +267,17 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     const float* __restrict__ init, const float* __restrict__ label,
     const float* __restrict__ weight, long long N, int loss_id, float p0, float score_div,
     float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
-    int want_grad, float* __restrict__ ghmax) {
+    int want_grad, float* __restrict__ ghmax, int* __restrict__ leaf_part) {
   extern __shared__ __attribute__((aligned(16))) int tsm[];
   int* sf = tsm;
   int* st = tsm + nnodes;
   int* sl = tsm + 2 * nnodes;
   int* sr = tsm + 3 * nnodes;
   float* sv = reinterpret_cast<float*>(tsm + 4 * nnodes);
+  int* sc = tsm + 5 * nnodes;  // leaf_part: rows per node of this block
   for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
     sf[i] = tfeat[i]; st[i] = tthr[i]; sl[i] = tleft[i]; sr[i] = tright[i]; sv[i] = tval[i];
+    if (leaf_part) sc[i] = 0;
   }
   __syncthreads();
   double lsum = 0.0, wsum = 0.0;
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
       }
       s += sv[n];
       score[r] = s;
+      if (leaf_part) atomicAdd(&sc[n], 1);
     }
     const float w = weight ? weight[r] : 1.f;
     const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)init[r], (double)label[r],
@@ -308,6 +311,27 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     }
   }
   block_acc(lsum, wsum, loss_acc, mg, mh, ghmax);
+  if (leaf_part) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nnodes; i += blockDim.x) leaf_part[(size_t)blockIdx.x * nnodes + i] = sc[i];
+  }
+}
+
+// out[node] = rows of the tree's node over all tree_grad blocks (one block per node, block
+// order sums: deterministic), as doubles next to the round's loss sums
+__global__ __launch_bounds__(256) void leaf_count_reduce_kernel(const int* __restrict__ part, int nblocks, int nnodes,
+                                                                double* __restrict__ out) {
+  __shared__ long long s_red[256];
+  const int node = blockIdx.x;
+  long long a = 0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) a += part[(size_t)b * nnodes + node];
+  s_red[threadIdx.x] = a;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) s_red[threadIdx.x] += s_red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[node] = (double)s_red[0];
 }
 
 // softmax over K classes; ghmax is [K][2] (one (max|g|, max|h|) pair per class tree)
@@ -432,7 +456,7 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
                      (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,            \
                      (float*)score, (const float*)init, (const float*)label,                        \
                      (const float*)weight, N, loss_id, p0, score_div, (float*)pred,                 \
-                     (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax)
+                     (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax, (int*)nullptr)
     switch (loss_id) {
       case 0: YTK_GH(0); break;
       case 1: YTK_GH(1); break;
@@ -453,10 +477,14 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
                    uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
                    long long N, int loss_id, float p0, float score_div, uintptr_t pred,
                    uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
-                   uintptr_t stream) {
+                   uintptr_t leaf_part, uintptr_t leaf_out, uintptr_t stream) {
   if (N <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  // leaf_part (optional, >= grid * nnodes ints) + leaf_out (nnodes doubles): rows per tree
+  // node -- the level engine's last-level leaf counts, taken from this walk instead of a
+  // separate counting partition pass
+  if (leaf_part && nnodes <= 0) leaf_part = 0;
+  const size_t lds = (size_t)nnodes * (leaf_part ? 6 : 5) * sizeof(int);
   const int grid = grid_for(N, 256 * 8);
   const long long row_bytes = stride * bin_bytes;
   const bool aligned = (bins % 16) == 0;
@@ -469,7 +497,7 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
                      (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
                      (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
                      p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,        \
-                     (float*)ghmax)
+                     (float*)ghmax, (int*)leaf_part)
 #define YTK_TG_LAUNCH(BT, DW)                   \
   do {                                          \
     switch (loss_id) {                          \
@@ -495,6 +523,14 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
 #undef YTK_TG_ONE
   hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
   YTK_LAUNCH_CHECK();
+  if (leaf_part) {
+    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes), dim3(256), 0, s, (const int*)leaf_part, grid, nnodes,
+                       (double*)leaf_out);
+    YTK_LAUNCH_CHECK();
+  }
 }
+
+// tree_grad launches min(ceil(N / 256), 2048) blocks: the leaf_part scratch size
+int ytk_tree_grad_grid(long long N) { return grid_for(N, 256 * 8); }
 
 }  // extern "C"

@@ -60,7 +60,14 @@ class DeviceTree:
     def to_tree(self, nodes_np=None, st_np=None) -> Tree:
         nd = (nodes_np if nodes_np is not None else self.nodes.cpu().numpy())
         st = st_np if st_np is not None else self.st.cpu().numpy()
-        return node_table_to_tree(nd, st)
+        tree = node_table_to_tree(nd, st)
+        lc = getattr(self, "leaf_counts", None)
+        if lc is not None:  # deferred last-level counts (this process's rows)
+            leaf = np.asarray(tree.is_leaf, bool)
+            sc = np.asarray(tree.sample_cnt, np.int64)
+            sc[leaf] = np.rint(lc.cpu().numpy()[:leaf.size][leaf]).astype(np.int64)
+            tree.sample_cnt = sc.tolist()
+        return tree
 
 
 def node_table_to_tree(nodes_bytes: np.ndarray, st: np.ndarray) -> Tree:
@@ -197,6 +204,11 @@ class DeviceLevelBuilder:
         self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.hist_target, self.part_target,
                    self.MIN_ROWS]
         self.tree_count = 0
+        # set by the trainer when its fused gradient pass counts the rows per leaf
+        # (tree_grad leaf_counts): the last level then needs no counting partition and no
+        # count all-reduce -- its children are leaves, and only their sample counts were
+        # still missing
+        self.defer_leaf_counts = False
         self.last_keep = None
         self.total_stats = TimeStats()
         self._fmask_cache = {}
@@ -427,6 +439,12 @@ class DeviceLevelBuilder:
             # apply splits + pop depth d (arg0 = 1: the single-pass partition needs no work list)
             h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, 1 if (fused and d >= 1) else 0, s)
             tm.mark("plan")
+            if last and self.defer_leaf_counts and not sampled:
+                # children planning with zero cursors: the leaves' sample counts are placeholders
+                # until the round's gradient pass (tree_grad) has walked every row to its leaf
+                h.lv_step(3, self._ptrs(), ip, fp, 0, (1 << (c - 1)) | (1 << 30), s)
+                tm.mark("plan")
+                break
             npart = self.part_target + (1 << d) + 1
             lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)

@@ -165,6 +165,12 @@ class GBDTTrainer:
         elif self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
                                               timer=self.timer)
+            # the fused K == 1 gradient pass counts the rows per leaf: the level engine's last
+            # level skips its counting partition (and, multi-GPU, the count all-reduce: the
+            # counts ride in the round's loss all-reduce)
+            self.builder.defer_leaf_counts = (self.K == 1 and self.kernel_loss is not None
+                                              and self.kernel_loss != "softmax"
+                                              and os.environ.get("YTK_DEFER_LEAF_COUNTS", "1") != "0")
         else:
             self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
                                        self.comm, profile=self.profile,
@@ -333,13 +339,20 @@ class GBDTTrainer:
         """Copy the round's tree snapshots + loss sums into one pinned buffer (async)."""
         while len(self._inflight) >= 4:  # bounded: at most 4 rounds in flight
             self._drain(len(self._inflight) - 1)
-        accs = torch.stack([acc, acc_te if acc_te is not None else torch.zeros_like(acc)]).to(self.dev)
+        accs = torch.stack([acc, acc_te if acc_te is not None else torch.zeros_like(acc)]).to(self.dev).reshape(-1)
+        # rows per leaf from the gradient pass (level engine, deferred last-level counts):
+        # local counts, summed across ranks by the same all-reduce as the losses
+        lcs = [getattr(dt, "leaf_counts", None) for dt in dev_trees]
+        nlc = [0 if c is None else c.numel() for c in lcs]
+        if any(nlc):
+            accs = torch.cat([accs] + [c for c in lcs if c is not None])
         if self.comm.is_dist:
             self.comm.allreduce_(accs)  # GBDTOptimizer.java:502 (loss, weight) allreduce
         sizes = [dt.snap.numel() for dt in dev_trees]
-        host = self._rb_buffer(32 + sum(sizes))
-        host[:32].view(torch.float64).copy_(accs.reshape(-1), non_blocking=True)
-        off = 32
+        head = 8 * accs.numel()
+        host = self._rb_buffer(head + sum(sizes))
+        host[:head].view(torch.float64).copy_(accs, non_blocking=True)
+        off = head
         for dt, sz in zip(dev_trees, sizes):
             host[off:off + sz].copy_(dt.snap, non_blocking=True)
             off += sz
@@ -347,21 +360,30 @@ class GBDTTrainer:
         if self.dev.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
-        self._inflight.append((i, dev_trees, host, ev, acc_te is not None))
+        self._inflight.append((i, dev_trees, host, ev, acc_te is not None, nlc))
 
     def _drain(self, lag: int = 0):
         """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log."""
         while len(self._inflight) > lag:
-            i, dev_trees, host, ev, has_te = self._inflight.popleft()
+            i, dev_trees, host, ev, has_te, nlc = self._inflight.popleft()
             if ev is not None:
                 ev.synchronize()
             hb = host.numpy()
-            a = hb[:32].view(np.float64)
-            off = 32
-            for dt in dev_trees:
+            head = 32 + 8 * sum(nlc)
+            a = hb[:head].view(np.float64)
+            off = head
+            coff = 4
+            for dt, nc in zip(dev_trees, nlc):
                 sz = dt.snap.numel()
                 nodes_b, st = dt.split_host_snap(hb[off:off + sz])
                 tree = node_table_to_tree(nodes_b, st)
+                if nc:  # leaf sample counts from the gradient pass
+                    cnt = a[coff:coff + nc]
+                    coff += nc
+                    leaf = np.asarray(tree.is_leaf, bool)
+                    sc = np.asarray(tree.sample_cnt, np.int64)
+                    sc[leaf] = np.rint(cnt[:leaf.size][leaf]).astype(np.int64)
+                    tree.sample_cnt = sc.tolist()
                 self._convert(tree)
                 self.model.trees.append(tree)
                 off += sz
@@ -433,9 +455,14 @@ class GBDTTrainer:
             need_max = self.ghmax_fixed is None  # the global bound replaces the per-tree max
             if need_max:
                 self.ghmax.zero_()
+            lc = None
+            if dev_trees and getattr(self.builder, "defer_leaf_counts", False) and self.builder.last_keep is None:
+                lc = torch.empty(arrays[0][0].shape[0], dtype=torch.float64, device=self.dev)
             acc = gops.tree_grad(self.bins, arrays[0], self.score, self.init_score, self.y, self.w,
                                  self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0],
-                                 True, self.ghmax[0] if need_max else None)
+                                 True, self.ghmax[0] if need_max else None, leaf_counts=lc)
+            if lc is not None:
+                dev_trees[0].leaf_counts = lc
         else:
             for k in range(self.K):
                 gops.tree_add_bins(self.binsT, arrays[k], self.score, k)

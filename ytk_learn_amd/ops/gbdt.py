@@ -564,10 +564,12 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
 
 
 def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
-              want_grad=True, ghmax=None):
+              want_grad=True, ghmax=None, leaf_counts=None):
     """Fused K==1 round tail: score += tree(row) (bin space, ROW-MAJOR bins [N, S]), then
     pred (optional) / (g, h) / loss sums / max|g|,|h| (optional ``ghmax`` [1,2]).
-    ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum)."""
+    ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum).
+    ``leaf_counts`` (optional, float64 [nodes], GPU): rows per tree node from the same walk
+    (the level engine's last-level leaf counts without a counting partition pass)."""
     loss_id = LOSS_IDS[loss]
     assert loss_id != 5 and score.shape[1] == 1
     if score.is_cuda:
@@ -580,13 +582,18 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
             tf, tt, tl, tr, tv = tree_arrays
             nn = tf.shape[0]
             assert bins is not None and bins.shape[0] == N and bins.stride(1) == 1
-        check_cuda(bins, score, init, label, weight, pred, gh, ghmax, tf, tt, tl, tr, tv)
+        check_cuda(bins, score, init, label, weight, pred, gh, ghmax, tf, tt, tl, tr, tv, leaf_counts)
+        part = None
+        if leaf_counts is not None:
+            assert nn > 0 and leaf_counts.dtype == torch.float64 and leaf_counts.numel() >= nn
+            part = torch.empty(hip().tree_grad_grid(N) * nn, dtype=torch.int32, device=score.device)
         hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
                         bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
                         ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
                         loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
-                        1 if want_grad else 0, ptr(ghmax), stream(score))
+                        1 if want_grad else 0, ptr(ghmax), ptr(part), ptr(leaf_counts), stream(score))
         return acc[:2]
+    assert leaf_counts is None, "leaf_counts: GPU only"
     if tree_arrays is not None:
         score[:, 0] += _walk_bins(bins.t(), tree_arrays)
     return grad_hess(score, init, label, weight, loss, param, score_div, pred, gh.unsqueeze(0),
