@@ -364,7 +364,12 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
   __syncthreads();
   const int nb = block_exclusive_scan(s_nb, nsplit, s_tmp);  // s_nb = build index
   const long long total = s_total;
-  const int ch = (int)max((long long)p.min_rows, (total + p.hist_target - 1) / max(1, p.hist_target));
+  // sum over the nodes of ceil(rows / ch) <= total / ch + nb: sizing the chunks for
+  // hist_target - nb items keeps the launch within ONE block per CU (the 128-KiB LDS
+  // histogram allows one per CU) -- hist_target + nb items left nb CUs running two
+  // chunks back to back, doubling the kernel's time
+  const int tgt = p.hist_target > 2 * nb ? p.hist_target - nb : p.hist_target;
+  const int ch = (int)max((long long)p.min_rows, (total + tgt - 1) / max(1, tgt));
   for (int s = tid; s < nsplit; s += kPlanThreads) {
     if (!s_hslot[s]) continue;
     const int k = s_nb[s];
