@@ -193,6 +193,10 @@ class DeviceLevelBuilder:
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
+        # True: each tree's snapshot is a copy (K trees per round need their own); the
+        # trainer clears it for K == 1 -- the round reads the snapshot (gradient pass,
+        # host readback) before the next tree overwrites it, in stream order
+        self.snapshot_copy = True
         self.rows = torch.empty(self.N, dtype=torch.int32, device=dev)
         self.rows_tmp = torch.empty(self.N, dtype=torch.int32, device=dev)
         self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
@@ -527,7 +531,7 @@ class DeviceLevelBuilder:
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         tm.mark("plan")
         self.tree_count += 1
-        snap = self.snap.clone()
+        snap = self.snap.clone() if self.snapshot_copy else self.snap
         st, nodes, *arrays = self._snap_views(snap)
         return DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
 

@@ -168,6 +168,7 @@ class GBDTTrainer:
             # the fused K == 1 gradient pass counts the rows per leaf: the level engine's last
             # level skips its counting partition (and, multi-GPU, the count all-reduce: the
             # counts ride in the round's loss all-reduce)
+            self.builder.snapshot_copy = self.K != 1
             self.builder.defer_leaf_counts = (self.K == 1 and self.kernel_loss is not None
                                               and self.kernel_loss != "softmax"
                                               and os.environ.get("YTK_DEFER_LEAF_COUNTS", "1") != "0")
