@@ -354,22 +354,29 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   if (i >= E || cnt == 0) continue;
   const int bin = i / gw, ff = fg * gw + (i % gw);
   if (ff >= F || bin >= B) continue;
+  // few items (deep levels: many slots, ~hist_target / slots items each): the z == 0
+  // block sums them all and STORES -- no 8-way int64 atomics at the memory side
+  const bool direct = cnt <= kReduceDirect;
+  if (direct && blockIdx.z != 0) continue;
+  const int step = direct ? 1 : kReduceSplit;
   const longlong2* st = reinterpret_cast<const longlong2*>(staging);
   long long g = 0, h = 0;
-  int t = (int)blockIdx.z;
-  for (; t + 7 * kReduceSplit < cnt; t += 8 * kReduceSplit) {
+  int t = direct ? 0 : (int)blockIdx.z;
+  for (; t + 7 * step < cnt; t += 8 * step) {
     longlong2 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)YTK_SEL(t + u * kReduceSplit) * groups + fg) * E + i];
+    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)YTK_SEL(t + u * step) * groups + fg) * E + i];
 #pragma unroll
     for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
   }
-  for (; t < cnt; t += kReduceSplit) {
+  for (; t < cnt; t += step) {
     const longlong2 v = st[((size_t)YTK_SEL(t) * groups + fg) * E + i];
     g += v.x;
     h += v.y;
   }
-  if (g | h) {
+  if (direct) {
+    *reinterpret_cast<longlong2*>(hist + (((size_t)slot * B + bin) * F + ff) * 2) = make_longlong2(g, h);
+  } else if (g | h) {
     unsigned long long* o = reinterpret_cast<unsigned long long*>(hist + (((size_t)slot * B + bin) * F + ff) * 2);
     atomicAdd(o, (unsigned long long)g);
     atomicAdd(o + 1, (unsigned long long)h);

@@ -210,7 +210,7 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
 
 // loss_acc[0:2] = sum over the nblocks partials, in block order (fixed per-thread strides,
 // then thread order).
-__global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ loss_acc, int nblocks) {
+__device__ __forceinline__ void acc_finish_body(double* __restrict__ loss_acc, int nblocks) {
   __shared__ double s_red[2][256];
   const double* part = loss_acc + kAccPart;
   double a = 0.0, c = 0.0;
@@ -227,6 +227,10 @@ __global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ lo
     loss_acc[0] = ta;
     loss_acc[1] = tc;
   }
+}
+
+__global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ loss_acc, int nblocks) {
+  acc_finish_body(loss_acc, nblocks);
 }
 
 // Leaf of a bin-threshold tree for one row held in registers (kDw dwords, packed bins):
@@ -320,8 +324,12 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
 // out[node] = rows of the tree's node over all tree_grad blocks (one block per node, block
 // order sums: deterministic), as doubles next to the round's loss sums
 __global__ __launch_bounds__(256) void leaf_count_reduce_kernel(const int* __restrict__ part, int nblocks, int nnodes,
-                                                                double* __restrict__ out) {
+                                                                double* __restrict__ out, double* __restrict__ loss_acc) {
   __shared__ long long s_red[256];
+  if (blockIdx.x == (unsigned)nnodes) {  // the extra block: the loss sums (acc_finish_kernel's work)
+    acc_finish_body(loss_acc, nblocks);
+    return;
+  }
   const int node = blockIdx.x;
   long long a = 0;
   for (int b = threadIdx.x; b < nblocks; b += 256) a += part[(size_t)b * nnodes + node];
@@ -521,13 +529,13 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
   }
 #undef YTK_TG_LAUNCH
 #undef YTK_TG_ONE
-  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
-  YTK_LAUNCH_CHECK();
-  if (leaf_part) {
-    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes), dim3(256), 0, s, (const int*)leaf_part, grid, nnodes,
-                       (double*)leaf_out);
-    YTK_LAUNCH_CHECK();
+  if (leaf_part) {  // leaf counts + the loss sums in one launch (block nnodes = acc_finish)
+    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + 1), dim3(256), 0, s, (const int*)leaf_part, grid,
+                       nnodes, (double*)leaf_out, (double*)loss_acc);
+  } else {
+    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
   }
+  YTK_LAUNCH_CHECK();
 }
 
 // tree_grad launches min(ceil(N / 256), 2048) blocks: the leaf_part scratch size
