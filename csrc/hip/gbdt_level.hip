@@ -37,6 +37,7 @@ struct LvParams {
   int max_depth, max_leaf_cnt, min_split_samples;
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
   int hist_target, part_target, min_rows;
+  int part_chunk;  // rows per single-pass partition chunk (fused kernel: 256 x rows per thread)
 };
 
 struct LvBufs {
@@ -86,9 +87,10 @@ __device__ void reset_node(DNode& n, int depth) {
   n.is_leaf = 1;
 }
 
-// Exclusive scan of one int per thread over the 256-thread block (wave64 shuffles +
-// 4 wave totals through LDS). Returns this thread's exclusive prefix; *total = sum.
-// Must be called by every thread of the block. s_tmp: >= kPlanThreads/64 + 1 ints.
+// Exclusive scan of one int per thread over the block (wave64 shuffles + one total per
+// wave through LDS; 256 threads for the planner launches, 1024 in the fused split + plan
+// kernel). Returns this thread's exclusive prefix; *total = sum.
+// Must be called by every thread of the block. s_tmp: >= blockDim.x/64 + 1 ints.
 __device__ __forceinline__ int block_scan_excl(int v, int* s_tmp, int* total) {
   const int tid = threadIdx.x, l = tid & (kWave - 1), w = tid >> 6;
   int inc = v;
@@ -100,8 +102,8 @@ __device__ __forceinline__ int block_scan_excl(int v, int* s_tmp, int* total) {
   if (l == kWave - 1) s_tmp[w] = inc;
   __syncthreads();
   int before = 0, all = 0;
-#pragma unroll
-  for (int k = 0; k < kPlanThreads / kWave; ++k) {
+  const int nw = (int)blockDim.x / kWave;
+  for (int k = 0; k < nw; ++k) {
     const int t = s_tmp[k];
     if (k < w) before += t;
     all += t;
@@ -111,13 +113,13 @@ __device__ __forceinline__ int block_scan_excl(int v, int* s_tmp, int* total) {
   return before + inc - v;
 }
 
-// In-place exclusive scan of a[0..n) (n <= kMaxPend) by one 256-thread block.
+// In-place exclusive scan of a[0..n) (n <= kMaxPend) by one block.
 // Returns the total. Each thread owns a contiguous run of ceil(n/256) entries; the
 // run totals are scanned with wave shuffles (no serial lane-0 loop: the old
 // 256-step LDS chain cost ~10 us per planner launch).
 __device__ int block_exclusive_scan(int* a, int n, int* s_tmp) {
   const int tid = threadIdx.x;
-  const int per = (n + kPlanThreads - 1) / kPlanThreads;
+  const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
   const int b = min(n, tid * per), e = min(n, b + per);
   int run = 0;
   for (int i = b; i < e; ++i) run += a[i];
@@ -137,7 +139,7 @@ __device__ int block_exclusive_scan(int* a, int n, int* s_tmp) {
 __device__ void emit_all_chunks(int4* items, int total_items, int nseg, const int* first,
                                 const int* begin, const int* count, const int* tag, int ch,
                                 bool blk_index) {
-  for (int k = threadIdx.x; k < total_items; k += kPlanThreads) {
+  for (int k = threadIdx.x; k < total_items; k += (int)blockDim.x) {
     int lo = 0, hi = nseg - 1;  // last s with first[s] <= k
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -184,11 +186,12 @@ __global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBuf
 }
 
 // Apply split results, pop the level's nodes in FIFO order, emit partition chunks.
-__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b, int fused,
-                                                                   int implicit_items) {
-  __shared__ int s_aux[kMaxPend];   // candidate flag, later: split index / -1
-  __shared__ int s_rank[kMaxPend];  // rank among the candidates (FIFO order)
+template <int KP>
+__device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused, int implicit_items) {
+  __shared__ int s_aux[KP];   // candidate flag, later: split index / -1
+  __shared__ int s_rank[KP];  // rank among the candidates (FIFO order)
   __shared__ int s_tmp[kPlanThreads + 1];
+  const int NT = (int)blockDim.x;
   __shared__ long long s_total;
   int* st = b.st;
   const int tid = threadIdx.x;
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
   //    counts from the (now all-reduced) count slots
   if (fused) {
     const int nprev = st[ST_N_SPLIT];
-    for (int s = tid; s < nprev; s += kPlanThreads) {
+    for (int s = tid; s < nprev; s += NT) {
       const DNode& P = b.nodes[b.split_nid[s]];
       const long long lg = b.left_glob[s] & 0xffffffffll;  // low half: left rows (see partition)
       b.nodes[P.left].cnt_global = lg;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
   }
   // 1. apply split-finder results to the node table (canSplit)
   const int nsi = st[ST_N_SITEMS];
-  for (int i = tid; i < nsi; i += kPlanThreads) {
+  for (int i = tid; i < nsi; i += NT) {
     DNode& n = b.nodes[b.item_nid[i]];
     const SplitOut& o = b.split_out[i];
     n.G = o.g;
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
   // 2. pop-time leaf rules that do not depend on the running leaf count
   const int npend = st[ST_N_PENDING];
   const int num_nodes0 = st[ST_NUM_NODES], num_leaf0 = st[ST_NUM_LEAF];
-  for (int i = tid; i < npend; i += kPlanThreads) {
+  for (int i = tid; i < npend; i += NT) {
     const DNode& n = b.nodes[b.pending[i]];
     const bool leaf = !(n.loss_chg > p.min_split_loss) ||
                       (p.max_depth >= 0 && p.max_depth == n.depth) ||
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
     st[ST_N_SPLIT] = nsplit;
   }
   // 4. write decisions back; per-split partition descriptors
-  for (int i = tid; i < npend; i += kPlanThreads) {
+  for (int i = tid; i < npend; i += NT) {
     const int id = b.pending[i];
     DNode& n = b.nodes[id];
     const int s = (s_aux[i] && s_rank[i] < limit) ? s_rank[i] : -1;
@@ -277,22 +280,27 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p,
   }
   __syncthreads();
   const long long total = s_total;
-  const int ch = (int)max((long long)p.min_rows, (total + p.part_target - 1) / max(1, p.part_target));
+  const int ch = (int)max((long long)p.part_chunk, (total + p.part_target - 1) / max(1, p.part_target));
   // counts -> chunk counts (stage counts in LDS for emission)
   int* s_count = s_aux;  // reuse: per split row count
-  for (int s = tid; s < nsplit; s += kPlanThreads) {
+  for (int s = tid; s < nsplit; s += NT) {
     const int c = b.part_nblk[s];
     s_count[s] = c;
     b.part_first[s] = (c + ch - 1) / ch;
   }
   __syncthreads();
   const int nitems = block_exclusive_scan(b.part_first, nsplit, s_tmp);
-  for (int s = tid; s < nsplit; s += kPlanThreads) b.part_nblk[s] = (s + 1 < nsplit ? b.part_first[s + 1] : nitems) - b.part_first[s];
+  for (int s = tid; s < nsplit; s += NT) b.part_nblk[s] = (s + 1 < nsplit ? b.part_first[s + 1] : nitems) - b.part_first[s];
   if (tid == 0) st[ST_N_PART] = nitems;
   __syncthreads();
   // the single-pass partition maps its blocks to (split, chunk) itself from part_first
   if (!implicit_items)
     emit_all_chunks(b.part_items, nitems, nsplit, b.part_first, b.part_begin, s_count, nullptr, ch, true);
+}
+
+__global__ __launch_bounds__(kPlanThreads) void lv_plan_split_kernel(LvParams p, LvBufs b, int fused,
+                                                                   int implicit_items) {
+  lv_plan_split_body<kMaxPend>(p, b, fused, implicit_items);
 }
 
 // Children of this level's splits: segments, terminal check, build / derive lists,
@@ -419,16 +427,45 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
-template <bool kScatter, int KP>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+template <bool kScatter, int KP, int kS>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 ? 8 : 4, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
                                   int dgap, int use_loc, int fused, int maxp) {
-  partition_atomic_body<uint8_t, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+  partition_atomic_body<uint8_t, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                            b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                            reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
   lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
+}
+
+// One GPU: the level's split search (one kNodeThreads block per node item, the node-
+// resident split_node_block) and the next level's split planning in ONE launch -- the
+// last block to finish runs lv_plan_split_body. Saves a launch per level (the planner's
+// ~7 us, mostly launch latency). The SplitOut records are plain stores, so the storing
+// thread fences (release) before its block counts itself done and the last block fences
+// (acquire: its caches may hold a previous level's records) before planning. Blocks past the device item count only
+// count themselves.
+template <int KP>
+__global__ __launch_bounds__(kNodeThreads) void lv_split_plan_kernel(
+    LvParams p, LvBufs b, long long* __restrict__ hist, int B, int F, int Bp, const int* __restrict__ nbins_f,
+    const uint8_t* __restrict__ fmask, int f0, GainParams gp, const double* __restrict__ inv_dev,
+    unsigned long long* __restrict__ done, int implicit_items) {
+  extern __shared__ __attribute__((aligned(16))) longlong2 sh_node[];
+  if (inv_dev) {
+    gp.inv_sg = inv_dev[0];
+    gp.inv_sh = inv_dev[1];
+  }
+  if ((int)blockIdx.x < b.st[ST_N_SITEMS])  // uniform per block
+    split_node_block(hist, B, F, Bp, nbins_f, fmask, f0, b.split_items[blockIdx.x], b.split_out + blockIdx.x, gp,
+                     sh_node);
+  // release by the one thread that stored this block's record (a fence per wave measured
+  // +6 us per launch), acquire by the last block's thread 0 before its barrier
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (!last_block_done(done)) return;
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  lv_plan_split_body<KP>(p, b, 0, implicit_items);
 }
 
 // Bin-threshold arrays used by the fused score/gradient kernel.
@@ -555,6 +592,7 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   p.hist_target = ip[3];
   p.part_target = ip[4];
   p.min_rows = ip[5];
+  p.part_chunk = ip[6];
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -591,6 +629,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   p.hist_target = ip[3];
   p.part_target = ip[4];
   p.min_rows = ip[5];
+  p.part_chunk = ip[6];
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -602,10 +641,14 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
   const int use_loc = (arg1 >> 30) & 1, fused = (arg1 >> 29) & 1;
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
-#define YTK_LVPC(SC, KP)                                                                                     \
-  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP>), grid, dim3(kPartThreads), 0, s, p, b,            \
+  if (p.part_chunk != kPartThreads * kAtomSub && p.part_chunk != kPartThreads * 2 * kAtomSub)
+    throw std::invalid_argument("lv_partition_children: part_chunk must be 2048 or 4096");
+  const bool wide = p.part_chunk == kPartThreads * 2 * kAtomSub;
+#define YTK_LVPC1(SC, KP, S)                                                                                  \
+  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
                      (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
+#define YTK_LVPC(SC, KP) do { if (wide) YTK_LVPC1(SC, KP, 2 * kAtomSub); else YTK_LVPC1(SC, KP, kAtomSub); } while (0)
   if (maxp <= 64) {
     if (count_only) YTK_LVPC(false, 64); else YTK_LVPC(true, 64);
   } else if (maxp <= 512) {
@@ -614,6 +657,60 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
     if (count_only) YTK_LVPC(false, kMaxPend); else YTK_LVPC(true, kMaxPend);
   }
 #undef YTK_LVPC
+#undef YTK_LVPC1
+  YTK_LAUNCH_CHECK();
+}
+
+// Fused split search + next-level split planning (one GPU, all-reduce-free). Falls back to
+// the two launches (split_find + plan_split) when the node-resident kernel's LDS (plus
+// the planner's) does not fit. fp: [6] LvParams floats; gpf: mcw, l1, l2, max_abs_leaf.
+void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask, int f0, uintptr_t items,
+                    int nitems, uintptr_t out, float mcw, float l1, float l2, float max_abs_leaf, double inv_sg,
+                    double inv_sh, uintptr_t nitems_dev, uintptr_t inv_dev, uintptr_t part, uintptr_t counters,
+                    uintptr_t stream);
+
+void ytk_lv_split_plan(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t hist, int B, int F,
+                       uintptr_t nbins_f, uintptr_t fmask, int f0, int nitems, const float* gpf, uintptr_t inv_dev,
+                       uintptr_t part, uintptr_t counters, int implicit_items, int maxp, uintptr_t stream) {
+  LvParams p;
+  p.max_depth = ip[0];
+  p.max_leaf_cnt = ip[1];
+  p.min_split_samples = ip[2];
+  p.hist_target = ip[3];
+  p.part_target = ip[4];
+  p.min_rows = ip[5];
+  p.part_chunk = ip[6];
+  p.min_split_loss = fp[0];
+  p.mcw = fp[1];
+  p.l1 = fp[2];
+  p.l2 = fp[3];
+  p.max_abs_leaf = fp[4];
+  p.lr = fp[5];
+  LvBufs b = make_bufs(ptrs);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int Bp = B + 1;
+  const size_t node_lds = (size_t)F * Bp * sizeof(long long) * 2;
+  const size_t plan_lds = 2 * sizeof(int) * (size_t)(maxp <= 64 ? 64 : maxp <= 512 ? 512 : kMaxPend) + 4096;
+  const bool fits = node_lds <= kNodeLdsMax && node_lds + plan_lds + 4096 <= 160 * 1024 && B <= 4 * kWave &&
+                    B * F <= kNodeLoads * kNodeThreads && F <= kNodeMaxF && F < 0xffff;
+  if (!fits) {
+    ytk_split_find(hist, B, F, nbins_f, fmask, f0, (uintptr_t)b.split_items, nitems, (uintptr_t)b.split_out,
+                   gpf[0], gpf[1], gpf[2], gpf[3], 1.0, 1.0, (uintptr_t)(b.st + ST_N_SITEMS), inv_dev, part,
+                   counters, stream);
+    hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, 0, implicit_items);
+    YTK_LAUNCH_CHECK();
+    return;
+  }
+  GainParams gp{gpf[0], gpf[1], gpf[2], gpf[3], 1.0, 1.0};
+  unsigned long long* done = reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride;
+#define YTK_LVSP(KP)                                                                                        \
+  hipLaunchKernelGGL((lv_split_plan_kernel<KP>), dim3(std::max(1, nitems)), dim3(kNodeThreads), node_lds, s, p, b, \
+                     (long long*)hist, B, F, Bp, (const int*)nbins_f, (const uint8_t*)fmask, f0, gp,               \
+                     (const double*)inv_dev, done, implicit_items)
+  if (maxp <= 64) YTK_LVSP(64);
+  else if (maxp <= 512) YTK_LVSP(512);
+  else YTK_LVSP(kMaxPend);
+#undef YTK_LVSP
   YTK_LAUNCH_CHECK();
 }
 

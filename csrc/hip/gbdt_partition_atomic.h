@@ -55,7 +55,12 @@ __device__ __forceinline__ bool last_block_done(unsigned long long* ctr64) {
 // their order): positions are a free permutation for everything downstream -- the
 // int64 histograms, split counts and leaf values are order independent, so trees are
 // bitwise identical to the stable two-pass partition.
-template <typename BinT, bool kScatter>
+// S: rows per thread (chunk = S x 256 rows). The level engine's fused kernel runs S = 16
+// (4096-row chunks): half the cursor reservations of S = 8, which is what bounds the top
+// levels (one split: every chunk reserves on ONE cursor line, ~12 ns each serialised --
+// tools/microbench/part_bench.py: 68 us for a count-only root split vs 17 us over 512
+// splits). S * (256 / 64) <= 64: the per-(sub-chunk, wave) left counts are scanned by one wave.
+template <typename BinT, bool kScatter, int S = kAtomSub>
 __device__ __forceinline__ void partition_atomic_body(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
@@ -64,13 +69,13 @@ __device__ __forceinline__ void partition_atomic_body(
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
     unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs) {
   // cs: cursor stride (u64; kCurStride in the engines, 1 for the standalone kernel)
-  // one chunk (<= kAtomSub * 256 rows) per block, held in registers: all loads issued
+  // one chunk (<= S * 256 rows) per block, held in registers: all loads issued
   // up front, ONE cursor reservation per block, then the scatter. The block finds its
   // (split, chunk) by binary search of first_blk (exclusive scan of the splits' chunk
   // counts) -- no per-block work list. kScatter = false: left counts only (last level).
   constexpr int NW = kPartThreads / kWave;
-  constexpr int S = kAtomSub;
-  constexpr int CH = kAtomSub * kPartThreads;
+  static_assert(S * NW <= kWave, "one-wave scan of the sub-chunk counts");
+  constexpr int CH = S * kPartThreads;
   constexpr int kSplitLds = 1024;  // splits whose chunk table is staged in LDS
   __shared__ int s_l[S * NW];
   __shared__ int s_first[kSplitLds];

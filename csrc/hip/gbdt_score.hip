@@ -236,18 +236,21 @@ __global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ lo
 // Leaf of a bin-threshold tree for one row held in registers (kDw dwords, packed bins):
 // the whole row is fetched with 16-B loads (a wave reads 64 contiguous rows), then
 // every level extracts its feature with a select chain -- no dependent memory loads.
-template <typename BinT, int kDw>
-__device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, const int* st,
-                                             const int* sl, const int* sr) {
-  constexpr int kPer = 4 / sizeof(BinT);
-  constexpr unsigned kMask = sizeof(BinT) == 1 ? 0xffu : 0xffffu;
-  uint32_t d[kDw];
+template <int kDw>
+__device__ __forceinline__ void load_row_regs(const void* row, uint32_t (&d)[kDw]) {
   const uint4* r4 = reinterpret_cast<const uint4*>(row);
 #pragma unroll
   for (int i = 0; i < kDw / 4; ++i) {
     const uint4 v = r4[i];
     d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
   }
+}
+
+template <typename BinT, int kDw>
+__device__ __forceinline__ int walk_regs(const uint32_t (&d)[kDw], const int* sf, const int* st,
+                                         const int* sl, const int* sr) {
+  constexpr int kPer = 4 / sizeof(BinT);
+  constexpr unsigned kMask = sizeof(BinT) == 1 ? 0xffu : 0xffffu;
   int n = 0;
   while (sf[n] >= 0) {
     const int f = sf[n];
@@ -259,6 +262,14 @@ __device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, con
     n = (b <= st[n]) ? sl[n] : sr[n];
   }
   return n;
+}
+
+template <typename BinT, int kDw>
+__device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, const int* st,
+                                             const int* sl, const int* sr) {
+  uint32_t d[kDw];
+  load_row_regs<kDw>(row, d);
+  return walk_regs<BinT, kDw>(d, sf, st, sl, sr);
 }
 
 // K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
@@ -286,8 +297,47 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
   __syncthreads();
   double lsum = 0.0, wsum = 0.0;
   float mg = 0.f, mh = 0.f;
-  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
-       r += (long long)gridDim.x * blockDim.x) {
+  long long r0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long G = (long long)gridDim.x * blockDim.x;
+  // the leaf / loss / gradient of one row whose inputs are already in registers
+  auto finish_row = [&](long long r, float s, int n, float ini, float lab, float w) {
+    s += sv[n];
+    score[r] = s;
+    if (leaf_part) atomicAdd(&sc[n], 1);
+    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+    lsum += (double)w * o.l;
+    wsum += (double)w;
+    if (pred) pred[r] = o.p;
+    if (want_grad) {
+      const float gg = (float)(o.g * (double)w), hh = (float)(o.h * (double)w);
+      gh[r] = make_float2(gg, hh);
+      mg = fmaxf(mg, fabsf(gg));
+      mh = fmaxf(mh, fabsf(hh));
+    }
+  };
+  if constexpr (kDw > 0) {
+    if (nnodes > 0) {
+      // two rows (r, r + G) per iteration with every load of both issued before either
+      // walk: the row loop was latency bound at one row in flight per thread. The rows of
+      // a thread are still accumulated in the order r, r + G, r + 2G, ... (fp64 sums
+      // unchanged)
+      for (; r0 + G < N; r0 += 2 * G) {
+        const long long r1 = r0 + G;
+        uint32_t d0[kDw], d1[kDw];
+        load_row_regs<kDw>(bins + r0 * stride, d0);
+        load_row_regs<kDw>(bins + r1 * stride, d1);
+        const float s0 = score[r0], s1 = score[r1];
+        const float i0 = init[r0], i1 = init[r1];
+        const float l0 = label[r0], l1 = label[r1];
+        const float w0 = weight ? weight[r0] : 1.f, w1 = weight ? weight[r1] : 1.f;
+        const int n0 = walk_regs<BinT, kDw>(d0, sf, st, sl, sr);
+        const int n1 = walk_regs<BinT, kDw>(d1, sf, st, sl, sr);
+        finish_row(r0, s0, n0, i0, l0, w0);
+        finish_row(r1, s1, n1, i1, l1, w1);
+      }
+    }
+  }
+  for (long long r = r0; r < N; r += G) {
     float s = score[r];
     if (nnodes > 0) {
       const BinT* row = bins + r * stride;

@@ -142,6 +142,29 @@ def test_device_builder_matches_host_builder(cuda, kw):
     assert trees[0][1] == trees[1][1] and trees[0][2] == trees[1][2]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_FUSE_SPLIT_PLAN": "1"},
+                                 {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"}])
+def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
+    """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
+    with the next level's planning) build the default engine's trees byte for byte."""
+    d = _data(40000, 9, cuda)
+    out = []
+    for use_env in (False, True):
+        for k, v in env.items():
+            if use_env:
+                monkeypatch.setenv(k, v)
+            else:
+                monkeypatch.delenv(k, raising=False)
+        p = _params("level", rounds=3, feature_sample_rate=0.7)
+        p.device_builder = True
+        tr = GBDTTrainer(p, d, _data(5000, 10, cuda))
+        tr.train()
+        assert tr.use_device_builder
+        out.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert out[0] == out[1]
+
+
 @pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 7}, {"max_depth": 4, "max_leaf_cnt": 20},
                                 {"min_split_samples": 900}, {"min_split_loss": 2.0},
                                 {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6}])

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-2 (late) GPU pass: GPU tests, headline bench (level-wise + leaf-wise extra keys),
+# one-round kernel timelines of level-wise and leaf-wise. Every GPU step has its own time
+# limit; the chain stops at the first failure. SKIP_TESTS=1 skips pytest.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r2d
+rm -rf $O && mkdir -p $O
+export TMPDIR=/tmp
+cd $R
+step() { local t=$1; shift; local log=$1; shift; timeout -k 10 $t "$@" > $O/$log 2>&1 || { echo "FAILED: $log"; tail -40 $O/$log; exit 1; }; }
+if [ -z "$SKIP_TESTS" ]; then
+  step 500 pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+  tail -1 $O/pytest_gpu.log
+fi
+step 300 bench.log python bench.py --steps 50 --warmup 5
+tail -1 $O/bench.log
+cd /tmp
+step 300 prof_level.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_level -o run -- python $R/bench.py --steps 10 --warmup 2 --leafwise-steps 0
+step 300 prof_leaf.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_leaf -o run -- python $R/bench.py --steps 6 --warmup 2 --policy loss
+cd $R
+python tools/prof_summary.py $(ls $O/prof_level/*kernel_trace.csv | head -1) > $O/level_round.txt
+python tools/prof_summary.py $(ls $O/prof_leaf/*kernel_trace.csv | head -1) > $O/leaf_round.txt
+head -22 $O/level_round.txt
+head -22 $O/leaf_round.txt
+echo r2d ok

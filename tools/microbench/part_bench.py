@@ -18,10 +18,14 @@ gh = torch.randn((N, 2), device=dev, generator=g)
 rows_out = torch.empty(N, dtype=torch.int32, device=dev)
 gh_out = torch.empty((N, 2), device=dev)
 perm = torch.randperm(N, device=dev, generator=g).to(torch.int32)
+# level-4-like order: rows grouped by a random node id of 16 (ascending inside a node)
+node16 = torch.randint(0, 16, (N,), device=dev, generator=g)
+lvl4 = torch.sort(node16 * N + torch.arange(N, device=dev)).indices.to(torch.int32)
 h = hip()
 
 
 def run(nsplit, gathered, count_only=False, reps=10):
+    # gathered: 0 identity rows, 1 random permutation, 2 level-4-like (16 interleaved nodes)
     seg = N // nsplit
     begins = torch.arange(nsplit, dtype=torch.int32) * seg
     counts = torch.full((nsplit,), seg, dtype=torch.int32)
@@ -35,7 +39,7 @@ def run(nsplit, gathered, count_only=False, reps=10):
     thr = torch.full((nsplit,), 127, dtype=torch.int32, device=dev)
     begins, counts, first = begins.to(dev), counts.to(dev), first.to(dev)
     cursor = torch.zeros(nsplit, dtype=torch.int64, device=dev)
-    rows_in = ptr(perm) if gathered else 0
+    rows_in = (0, ptr(perm), ptr(lvl4))[gathered]
     s = stream(binsT)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
@@ -44,7 +48,7 @@ def run(nsplit, gathered, count_only=False, reps=10):
         e0.record()
         h.partition_atomic(ptr(binsT), 1, N, rows_in, ptr(rows_out), ptr(gh), ptr(gh_out), ptr(first),
                            st.data_ptr(), st.data_ptr() + 4, nb, ptr(feat), ptr(thr), ptr(begins), ptr(counts),
-                           ptr(cursor), 1 if count_only else 0, s)
+                           ptr(cursor), 1 if count_only else 0, 0, s)
         e1.record()
         torch.cuda.synchronize()
         if i >= 2:
@@ -52,9 +56,9 @@ def run(nsplit, gathered, count_only=False, reps=10):
     return sum(ts) / len(ts), nb
 
 
-for gathered in (False, True):
+for gathered in (0, 2, 1):
     for nsplit in (1, 32, 512, N // CH):
         for co in (False, True):
             ms, nb = run(nsplit, gathered, co)
-            print(f"gathered={int(gathered)} nsplit={nsplit:5d} blocks={nb} count_only={int(co)}  {ms * 1000:8.1f} us",
+            print(f"gathered={gathered} nsplit={nsplit:5d} blocks={nb} count_only={int(co)}  {ms * 1000:8.1f} us",
                   flush=True)

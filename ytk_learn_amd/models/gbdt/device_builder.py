@@ -113,11 +113,23 @@ class DeviceLevelBuilder:
         # ~N/2048 resident blocks instead of ~10 serial reservations per block
         # (the kernel holds one chunk of <= 2048 rows per block in registers)
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0" and self.MIN_ROWS == 2048
-        self.part_target = (-(-self.N // self.MIN_ROWS) + 1) if self.part_atomic else self.PART_TARGET
         # one GPU, uint8 bins: the children planner runs in the partition kernel's last block
         # (YTK_FUSE_PART_CHILDREN=0: separate launches)
         self.fuse_part_children = (self.part_atomic and not self.comm.is_dist and bins.dtype == torch.uint8
                                    and os.environ.get("YTK_FUSE_PART_CHILDREN", "1") != "0")
+        # rows per partition chunk (= per cursor reservation): 8 rows per thread (2048);
+        # YTK_PART_CHUNK=4096 runs the fused kernel at 16 rows per thread -- half the
+        # reservations on the top levels' few cursors, but 4 instead of 8 waves/SIMD.
+        # Measured (profiles/r2_partition_chunk.md): root level 105 -> 100 us, deep levels
+        # 93 -> 100 us, tree 1.50 ms either way
+        self.part_chunk = (int(os.environ.get("YTK_PART_CHUNK", "2048")) if self.fuse_part_children
+                           else self.MIN_ROWS)
+        self.part_target = (-(-self.N // self.part_chunk) + 1) if self.part_atomic else self.PART_TARGET
+        # one GPU: split search + next level's split planning in one launch (YTK_FUSE_SPLIT_PLAN=1).
+        # Off by default: the release/acquire fences it needs cost what the saved launch
+        # saved (measured 24.2 -> 25.0 us per level, profiles/r2_split_plan_fusion.md)
+        self.fuse_split_plan = (self.fuse_part_children and not self.wide
+                                and os.environ.get("YTK_FUSE_SPLIT_PLAN", "0") == "1")
         self.max_items = max(self.hist_target, self.part_target) + self.maxp + 16
         dev = self.dev
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)
@@ -206,7 +218,7 @@ class DeviceLevelBuilder:
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
         self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.hist_target, self.part_target,
-                   self.MIN_ROWS]
+                   self.MIN_ROWS, self.part_chunk]
         self.tree_count = 0
         # set by the trainer when its fused gradient pass counts the rows per leaf
         # (tree_grad leaf_counts): the last level then needs no counting partition and no
@@ -316,6 +328,14 @@ class DeviceLevelBuilder:
             cap = self.split_local.numel() // 48
             h.split_combine(ptr(allr), self.comm.world, cap, nitems_dev, min(nitems, cap), tot,
                             ptr(self.split_out), s)
+
+    def _split_plan(self, ptrs, fp, fmask, f0: int, nitems: int, s):
+        """One GPU: this level's split search fused with the next level's split planning
+        (lv_split_plan_kernel: the last node block plans) -- one launch instead of two."""
+        gp = self.gp
+        hip().lv_split_plan(ptrs, self.ip, fp, ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask),
+                            f0, nitems, [gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"]], ptr(self.inv_scales),
+                            ptr(self.split_part), ptr(self.split_cnt), 1 if self.part_atomic else 0, self.maxp, s)
 
     def _fmask(self, rng):
         p = self.p
@@ -427,7 +447,10 @@ class DeviceLevelBuilder:
             else:
                 self.comm.allreduce_(self.hist[0:1])
             tm.mark("build_hist_comm")
-        self._split(fmask, f0, self._fmask_np, 1, off(6), s)
+        if self.fuse_split_plan:
+            self._split_plan(ptrs, fp, fmask, f0, 1, s)
+        else:
+            self._split(fmask, f0, self._fmask_np, 1, off(6), s)
         tm.mark("find_best_split")
         bb = 1 if self.bins.dtype == torch.uint8 else 2
         fused = self.fuse_counts
@@ -441,7 +464,8 @@ class DeviceLevelBuilder:
                 ptrs = self._ptrs(loc=ptr(loc) if loc is not None else self._count_ptr(c),
                                   glob=self._count_ptr(d) if d >= 1 else None)
             # apply splits + pop depth d (arg0 = 1: the single-pass partition needs no work list)
-            h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, 1 if (fused and d >= 1) else 0, s)
+            if not self.fuse_split_plan:  # else: planned by the previous split launch
+                h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, 1 if (fused and d >= 1) else 0, s)
             tm.mark("plan")
             if last and self.defer_leaf_counts and not sampled:
                 # children planning with zero cursors: the leaves' sample counts are placeholders
@@ -526,7 +550,10 @@ class DeviceLevelBuilder:
                     else:
                         self.comm.allreduce_(self.hist[base:base + half + ncs])
                     tm.mark("build_hist_comm")
-            self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
+            if self.fuse_split_plan:
+                self._split_plan(ptrs, fp, fmask, f0, 1 << c, s)
+            else:
+                self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
             tm.mark("find_best_split")
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
         tm.mark("plan")
