@@ -68,6 +68,57 @@ __global__ __launch_bounds__(256) void forest_predict_kernel(
   }
 }
 
+// Register walk for narrow dense rows (F = 4 * kF4 <= 32 floats, 16-B aligned): the whole
+// row is fetched with kF4 independent 16-B loads and the nodes are staged in LDS, so a
+// tree level costs a select chain instead of three dependent global round trips (node
+// feature -> x[feature] -> threshold / children). Same comparisons as
+// forest_predict_kernel (missing -> default child, v <= thr -> left).
+template <int kF4>
+__global__ __launch_bounds__(256) void forest_predict_regs_kernel(
+    const float* __restrict__ X, long long N, const int* __restrict__ nfeat, const float* __restrict__ nthr,
+    const int* __restrict__ nleft, const int* __restrict__ nright, const uint8_t* __restrict__ ndefl,
+    const float* __restrict__ nval, const int* __restrict__ troot, const int* __restrict__ tout, int T,
+    int nnodes, float* __restrict__ out, int ostride, float scale, int* __restrict__ leaf_out) {
+  extern __shared__ __attribute__((aligned(16))) int fsm[];
+  int* sf = fsm;  // feature, or -1 (leaf); the default direction rides in bit 30
+  float* sth = reinterpret_cast<float*>(fsm + nnodes);
+  int* sl = fsm + 2 * nnodes;
+  int* sr = fsm + 3 * nnodes;
+  float* sv = reinterpret_cast<float*>(fsm + 4 * nnodes);
+  for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
+    const int f = nfeat[i];
+    sf[i] = f < 0 ? -1 : (f | (ndefl[i] ? (1 << 30) : 0));
+    sth[i] = nthr[i]; sl[i] = nleft[i]; sr[i] = nright[i]; sv[i] = nval[i];
+  }
+  __syncthreads();
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    float x[4 * kF4];
+    const float4* r4 = reinterpret_cast<const float4*>(X + r * (4 * kF4));
+#pragma unroll
+    for (int i = 0; i < kF4; ++i) {
+      const float4 v = r4[i];
+      x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+    }
+    for (int t = 0; t < T; ++t) {
+      const int root = troot[t];
+      int n = root;
+      int fe = sf[n];
+      while (fe >= 0) {
+        const int f = fe & 0xffff;
+        float v = x[0];
+#pragma unroll
+        for (int i = 1; i < 4 * kF4; ++i) v = (f == i) ? x[i] : v;
+        const bool left = (v != v) ? ((fe >> 30) & 1) : (v <= sth[n]);
+        n = left ? sl[n] : sr[n];
+        fe = sf[n];
+      }
+      if (leaf_out) leaf_out[r * T + t] = n - root;
+      else out[r * ostride + tout[t]] += scale * sv[n];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ binning
 template <typename BinT>
 __global__ __launch_bounds__(256) void bin_assign_kernel(
@@ -474,6 +525,40 @@ void ytk_forest_predict(uintptr_t X, long long xstride, long long N, uintptr_t n
                      (const int*)troot, (const int*)tout, T, (float*)out, ostride, scale,
                      (int*)leaf_out);
   YTK_LAUNCH_CHECK();
+}
+
+// forest_predict with the row-register walk; returns 0 (nothing launched) when the layout
+// does not qualify (caller then runs ytk_forest_predict).
+int ytk_forest_predict_regs(uintptr_t X, long long xstride, long long N, uintptr_t nfeat, uintptr_t nthr,
+                            uintptr_t nleft, uintptr_t nright, uintptr_t ndefl, uintptr_t nval, uintptr_t troot,
+                            uintptr_t tout, int T, int nnodes, uintptr_t out, int ostride, float scale,
+                            uintptr_t leaf_out, uintptr_t stream) {
+  if (N <= 0 || T <= 0) return 1;
+  const int kf4 = (int)(xstride / 4);
+  if (xstride % 4 != 0 || kf4 < 1 || kf4 > 8 || (X % 16) != 0 || nnodes <= 0 || nnodes > 2048 ||
+      nnodes >= (1 << 30))
+    return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  const dim3 grid(grid_for(N, 256 * 16));
+#define YTK_FPR(K)                                                                                      \
+  hipLaunchKernelGGL(forest_predict_regs_kernel<K>, grid, dim3(256), lds, s, (const float*)X, N,        \
+                     (const int*)nfeat, (const float*)nthr, (const int*)nleft, (const int*)nright,          \
+                     (const uint8_t*)ndefl, (const float*)nval, (const int*)troot, (const int*)tout, T,     \
+                     nnodes, (float*)out, ostride, scale, (int*)leaf_out)
+  switch (kf4) {
+    case 1: YTK_FPR(1); break;
+    case 2: YTK_FPR(2); break;
+    case 3: YTK_FPR(3); break;
+    case 4: YTK_FPR(4); break;
+    case 5: YTK_FPR(5); break;
+    case 6: YTK_FPR(6); break;
+    case 7: YTK_FPR(7); break;
+    default: YTK_FPR(8); break;
+  }
+#undef YTK_FPR
+  YTK_LAUNCH_CHECK();
+  return 1;
 }
 
 void ytk_bin_assign(uintptr_t X, long long xstride, long long N, int F, uintptr_t cand,

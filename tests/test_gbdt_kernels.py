@@ -202,6 +202,13 @@ def test_tree_add_bins_and_forest(cuda):
     lo_g = torch.zeros((N, 2), dtype=torch.int32, device=cuda)
     gops.forest_predict(X.to(cuda), {k: v.to(cuda) for k, v in fl.items()}, None, 1.0, lo_g)
     assert torch.equal(lo_g.cpu(), lo_c)
+    # F = 8: the row-register kernel ran above; F = 6 (not a multiple of 4) takes the generic one
+    X6 = X[:, :6].contiguous()
+    oc6 = torch.zeros((N, 1))
+    gops.forest_predict(X6, fl, oc6, 0.5)
+    og6 = torch.zeros((N, 1), device=cuda)
+    gops.forest_predict(X6.to(cuda), {k: v.to(cuda) for k, v in fl.items()}, og6, 0.5)
+    torch.testing.assert_close(og6.cpu(), oc6)
 
 
 def test_bin_assign_matches_cpu(cuda):

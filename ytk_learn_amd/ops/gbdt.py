@@ -422,6 +422,13 @@ def forest_predict(X, forest, out, scale=1.0, leaf_out=None):
     N = X.shape[0]
     if X.is_cuda:
         check_cuda(X, out, leaf_out, *forest.values())
+        # narrow contiguous rows: whole row in registers, nodes in LDS (one launch either way)
+        if X.is_contiguous() and hip().forest_predict_regs(
+                ptr(X), X.shape[1], N, ptr(forest["nfeat"]), ptr(forest["nthr"]), ptr(forest["nleft"]),
+                ptr(forest["nright"]), ptr(forest["ndefl"]), ptr(forest["nval"]), ptr(forest["troot"]),
+                ptr(forest["tout"]), T, forest["nfeat"].numel(), ptr(out), out.shape[1] if out is not None else 0,
+                float(scale), ptr(leaf_out), stream(X)):
+            return
         hip().forest_predict(ptr(X), X.shape[1], N, ptr(forest["nfeat"]), ptr(forest["nthr"]),
                              ptr(forest["nleft"]), ptr(forest["nright"]), ptr(forest["ndefl"]),
                              ptr(forest["nval"]), ptr(forest["troot"]), ptr(forest["tout"]), T,
