@@ -42,7 +42,9 @@ enum {
   LW_SEQ, LW_N_HEAP, LW_OVERFLOW, LW_BATCHES, LW_EXPANDED, LW_N_ZERO, LW_PART_DONE, LW_WORDS = 16
 };
 
-constexpr int kLwThreads = 256;
+constexpr int kLwThreads = 256;      // children body (runs in the 256-thread partition blocks)
+constexpr int kLwPlanThreads = 1024;  // planner / init: 16 waves for the block-parallel phases
+                                      // (the replay itself is one wave either way)
 constexpr int kLwCap = 2304;     // speculative nodes per tree (LDS-staged by the planner)
 constexpr int kLwLeafMax = 512;   // max_leaf_cnt supported by the device engine
 constexpr int kLwSort = 4096;     // LDS scratch (u64): replay events, then batch-choice keys
@@ -179,7 +181,7 @@ __device__ __forceinline__ void lw_wave_argmax(const unsigned long long* key, in
 __device__ void lw_bitonic_desc(unsigned long long* a, int n) {
   for (int size = 2; size <= n; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < (n >> 1); t += kLwThreads) {
+      for (int t = threadIdx.x; t < (n >> 1); t += (int)blockDim.x) {
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
@@ -206,8 +208,8 @@ __device__ __forceinline__ int lw_scan(int v, int* s_tmp, int* total) {
   if (l == kWave - 1) s_tmp[w] = inc;
   __syncthreads();
   int before = 0, all = 0;
-#pragma unroll
-  for (int k = 0; k < kLwThreads / kWave; ++k) {
+  const int nw = (int)blockDim.x / kWave;
+  for (int k = 0; k < nw; ++k) {
     const int t = s_tmp[k];
     if (k < w) before += t;
     all += t;
@@ -219,7 +221,7 @@ __device__ __forceinline__ int lw_scan(int v, int* s_tmp, int* total) {
 
 // In-place exclusive scan of a[0..n) by the block (contiguous run per thread).
 __device__ int lw_scan_array(int* a, int n, int* s_tmp) {
-  const int per = (n + kLwThreads - 1) / kLwThreads;
+  const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
   const int b = min(n, (int)threadIdx.x * per), e = min(n, b + per);
   int run = 0;
   for (int i = b; i < e; ++i) run += a[i];
@@ -256,7 +258,7 @@ __device__ void lw_write_node(DNode& n, const LwBufs& b, int sid, bool leaf, dou
 }
 
 // Root: node 0 holds every (local) row; histogram chunks of slot 0; the root is queued.
-__global__ __launch_bounds__(kLwThreads) void lw_init_kernel(LwParams p, LwBufs b) {
+__global__ __launch_bounds__(kLwPlanThreads) void lw_init_kernel(LwParams p, LwBufs b) {
   const int n_local = (int)b.root_cnt[0];
   const int ch = max(p.min_rows, (n_local + p.hist_target - 1) / max(1, p.hist_target));
   const int nblk = (n_local + ch - 1) / ch;
@@ -291,11 +293,11 @@ __global__ __launch_bounds__(kLwThreads) void lw_init_kernel(LwParams p, LwBufs 
     b.split_items[0] = make_int4(0, 0, 0, 0);
     b.item_sid[0] = 0;
   }
-  for (int k = threadIdx.x; k < nblk; k += kLwThreads)
+  for (int k = threadIdx.x; k < nblk; k += kLwPlanThreads)
     b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), (k == 0 && nblk > kLwReduceDirect) ? 2 : 0);
 }
 
-__global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs b) {
+__global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwBufs b) {
   // node fields the replay reads, packed: {lc, tid, depth | state << 16 | static_leaf << 24, cnt}
   __shared__ int4 s_nd[kLwCap];
   __shared__ float s_loss[kLwCap];
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   __shared__ int s_na, s_nu;
   // replay events (then reused by the batch choice: rank keys + bottlenecks, 27 KiB)
   __shared__ unsigned long long s_buf[kLwSort];
-  __shared__ int s_tmp[kLwThreads / kWave + 1];
+  __shared__ int s_tmp[kLwPlanThreads / kWave + 1];
   __shared__ int s_nev, s_blocked, s_nh, s_num_leaf, s_ntree, s_seqc, s_k, s_ncand;
   int* st = b.st;
   const int tid = threadIdx.x;
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   const double mcw2 = (double)p.mcw * 2.0;
   // A. split records of the previous batch (canSplit: UpdateStrategy.java:50-53)
   const int nsi = st[LW_N_SITEMS];
-  for (int i = tid; i < nsi; i += kLwThreads) {
+  for (int i = tid; i < nsi; i += kLwPlanThreads) {
     const int sid = b.item_sid[i];
     const SplitOut o = b.split_out[i];
     b.G[sid] = o.g;
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   __syncthreads();
   LW_TICK(0);
   // B. stage what the replay reads
-  for (int i = tid; i < nsid; i += kLwThreads) {
+  for (int i = tid; i < nsid; i += kLwPlanThreads) {
     const float loss = b.loss[i];
     const int cnt = (int)b.cnt[i], depth = b.depth[i];
     const int sl = lw_static_leaf(p, loss, depth, cnt) ? 1 : 0;
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     }
   }
   int nh = st[LW_N_HEAP];
-  for (int i = tid; i < nh; i += kLwThreads) s_hsid[i] = b.heap[i];
+  for (int i = tid; i < nh; i += kLwPlanThreads) s_hsid[i] = b.heap[i];
   if (tid == 0) { s_na = 0; s_nu = 0; }
   __syncthreads();
   LW_TICK(1);
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   //    packed: a pop is three dependent LDS round trips.
   int4* s_ev = reinterpret_cast<int4*>(s_buf);  // kLwSort / 2 events
   {
-    for (int i = tid; i < nh; i += kLwThreads) {
+    for (int i = tid; i < nh; i += kLwPlanThreads) {
       const int sid = s_hsid[i];
       const int4 nd = s_nd[sid];
       if ((nd.z >> 24) || nd.x >= 0) s_akey[atomicAdd(&s_na, 1)] = lw_qkey(s_loss[sid], s_seq[sid], sid);
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     const int na = s_na;
     int n2 = 1;
     while (n2 < na) n2 <<= 1;
-    for (int i = na + tid; i < n2; i += kLwThreads) s_akey[i] = 0ull;
+    for (int i = na + tid; i < n2; i += kLwPlanThreads) s_akey[i] = 0ull;
     __syncthreads();
     lw_bitonic_desc(s_akey, n2);
   }
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   LW_TICK(2);
   // D. tree nodes finalised by the replay (independent writes, all lanes)
   const int nev = s_nev;
-  for (int e = tid; e < nev; e += kLwThreads) {
+  for (int e = tid; e < nev; e += kLwPlanThreads) {
     const int4 ev = s_ev[e];
     const int sid = ev.y;
     if (ev.x == EV_LEAF) {
@@ -548,18 +550,18 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     // (Top-k by the node's own gain expanded ~1.6x as many nodes: docs/performance.md.)
     unsigned long long* s_rk = s_buf;                                 // [kLwCap] splittable rank keys
     unsigned* s_m = reinterpret_cast<unsigned*>(s_buf + kLwCap);      // [kLwCap] bottleneck ord(loss)
-    constexpr int kPer = (kLwCap + kLwThreads - 1) / kLwThreads;
+    constexpr int kPer = (kLwCap + kLwPlanThreads - 1) / kLwPlanThreads;
     auto ord = [](float f) {
       const unsigned u = __float_as_uint(f);
       return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     };
     auto live = [&](int i) { return ((s_nd[i].z >> 16) & 0xff) == 1; };  // known gain, not final
-    for (int i = tid; i < nsid; i += kLwThreads) {
+    for (int i = tid; i < nsid; i += kLwPlanThreads) {
       s_par[i] = -1;
       s_m[i] = ord(s_loss[i]);
     }
     __syncthreads();
-    for (int i = tid; i < nsid; i += kLwThreads) {
+    for (int i = tid; i < nsid; i += kLwPlanThreads) {
       const int4 nd = s_nd[i];
       if (((nd.z >> 16) & 0xff) == 1 && nd.x >= 0) s_par[nd.x] = s_par[nd.x + 1] = i;
     }
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       int any = 0;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
-        const int i = tid + j * kLwThreads;
+        const int i = tid + j * kLwPlanThreads;
         np[j] = -1;
         if (i < nsid) {
           const int pp = s_par[i];
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       if (!__syncthreads_or(any)) break;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
-        const int i = tid + j * kLwThreads;
+        const int i = tid + j * kLwPlanThreads;
         if (i < nsid) {
           s_m[i] = nm[j];
           s_par[i] = np[j];
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
                           : (((unsigned long long)s_m[i] << 32) |
                              (unsigned long long)((ord(s_loss[i]) >> 12) << 12) | (unsigned long long)i);
     };
-    const int per = (nsid + kLwThreads - 1) / kLwThreads;
+    const int per = (nsid + kLwPlanThreads - 1) / kLwPlanThreads;
     const int i0 = min(nsid, tid * per), i1 = min(nsid, i0 + per);
     int c = 0, cc = 0;
     for (int i = i0; i < i1; ++i) {
@@ -619,16 +621,16 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
       if (s_nd[i].x < 0) s_cand[pc++] = i;
     }
     const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= kLwCap (a multiple of 128)
-    for (int z = ns + tid; z < ns_pad; z += kLwThreads) s_rk[z] = 0ull;  // never ranks above a key
+    for (int z = ns + tid; z < ns_pad; z += kLwPlanThreads) s_rk[z] = 0ull;  // never ranks above a key
     // rank window: speculate percent of the leaf budget (s_uid holds 3 kLwLeafMax ranks)
     const int rem = min(3 * kLwLeafMax, max(1, remaining * p.speculate / 100));
-    for (int r = tid; r < rem; r += kLwThreads) s_uid[r] = -1;
+    for (int r = tid; r < rem; r += kLwPlanThreads) s_uid[r] = -1;
     __syncthreads();
     LW_TICK(23);
     // rank of each candidate among the splittable set: a wave takes 4 candidates, every
     // key it loads is compared with all 4 (ballot + popcount: wave-uniform counts)
     const int lane = tid & (kWave - 1);
-    for (int g = (tid >> 6) * 4; g < ncand; g += kLwThreads / kWave * 4) {
+    for (int g = (tid >> 6) * 4; g < ncand; g += kLwPlanThreads / kWave * 4) {
       unsigned long long me[4];
       int rank[4];
 #pragma unroll
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
     __syncthreads();
     LW_TICK(24);
     // compact the chosen ones in rank order
-    const int pr = (rem + kLwThreads - 1) / kLwThreads;
+    const int pr = (rem + kLwPlanThreads - 1) / kLwPlanThreads;
     const int r0 = min(rem, tid * pr), r1 = min(rem, r0 + pr);
     int nc = 0;
     for (int r = r0; r < r1; ++r) nc += s_uid[r] >= 0 ? 1 : 0;
@@ -667,7 +669,7 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   }
   LW_TICK(4);
   // F. expand the batch: children ids, partition descriptors (chunks of kLwChunk rows)
-  for (int j = tid; j < k; j += kLwThreads) {
+  for (int j = tid; j < k; j += kLwPlanThreads) {
     const int P = s_batch[j];
     const int lc = nsid + 2 * j;
     s_nd[P].x = lc;
@@ -700,14 +702,14 @@ __global__ __launch_bounds__(kLwThreads) void lw_plan_kernel(LwParams p, LwBufs 
   const int nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
   LW_TICK(5);
   // G. write back the replay state
-  for (int i = tid; i < nsid; i += kLwThreads) {
+  for (int i = tid; i < nsid; i += kLwPlanThreads) {
     const int4 nd = s_nd[i];
     b.lc[i] = nd.x;
     b.tid[i] = nd.y;
     b.seq[i] = s_seq[i];
     b.state[i] = (nd.z >> 16) & 0xff;
   }
-  for (int i = tid; i < nh; i += kLwThreads) b.heap[i] = s_hsid[i];
+  for (int i = tid; i < nh; i += kLwPlanThreads) b.heap[i] = s_hsid[i];
   if (tid == 0) {
     st[LW_PART_DONE] = 0;
     st[LW_NUM_LEAF] = num_leaf;
@@ -981,8 +983,8 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
-    case 0: hipLaunchKernelGGL(lw_init_kernel, dim3(1), dim3(kLwThreads), 0, s, e.p, e.b); break;
-    case 1: hipLaunchKernelGGL(lw_plan_kernel, dim3(1), dim3(kLwThreads), 0, s, e.p, e.b); break;
+    case 0: hipLaunchKernelGGL(lw_init_kernel, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b); break;
+    case 1: hipLaunchKernelGGL(lw_plan_kernel, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b); break;
 
     default: throw std::runtime_error("bad lw step");
   }
