@@ -855,14 +855,21 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // Partition of the batch's segments (partition_atomic_body; children written into the
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+// kPrefetch: the software-pipelined body (partition_atomic_body_pf).
+template <bool kPrefetch>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
 void lw_partition_kernel(LwParams p, LwBufs b, const uint8_t* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
                                                                    float2* gh_out) {
-  partition_atomic_body<uint8_t, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
-                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                       b.cursor, b.part_shift, kCurStride);
+  if constexpr (kPrefetch)
+    partition_atomic_body_pf<uint8_t>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
+                                      b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
+                                      b.cursor, b.part_shift, kCurStride);
+  else
+    partition_atomic_body<uint8_t, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
+                                         b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
+                                         b.cursor, b.part_shift, kCurStride);
   // No fences: the only cross-block data the last block reads are the split cursors,
   // updated by RETURNING device-scope atomics (complete before this block counts itself)
   // and read back with atomic loads. (An agent-scope release fence per block writes back
@@ -996,9 +1003,18 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
                       uintptr_t gh_out, int max_blocks, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
-  hipLaunchKernelGGL(lw_partition_kernel, dim3(std::max(1, std::min(max_blocks, kPartGrid))), dim3(kPartThreads),
-                     0, reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint8_t*)binsT, ncol,
-                     (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+  // YTK_LW_PART_PREFETCH=1: the software-pipelined partition body
+  const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
+  const bool prefetch = pf && pf[0] == '1';
+  const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
+  if (prefetch)
+    hipLaunchKernelGGL(lw_partition_kernel<true>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                       (float2*)gh_out);
+  else
+    hipLaunchKernelGGL(lw_partition_kernel<false>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                       (float2*)gh_out);
   YTK_LAUNCH_CHECK();
 }
 

@@ -182,4 +182,138 @@ __device__ __forceinline__ void partition_atomic_body(
   }
 }
 
+// Software-pipelined variant of partition_atomic_body (level engine, scatter levels): the
+// persistent block locates its NEXT chunk and issues that chunk's row-id loads before it
+// ranks, reserves and scatters the current one, so the row-id round trip of chunk i + 1
+// overlaps the ballot / cursor-atomic / scatter phases of chunk i. Same output as the
+// unpipelined body (same reservation per chunk, same placement).
+template <typename BinT, int S = kAtomSub>
+__device__ __forceinline__ void partition_atomic_body_pf(
+    const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
+    const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
+    const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
+    const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
+    const int* __restrict__ node_begin, const int* __restrict__ node_count,
+    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs) {
+  // ghp == nullptr: (g, h) stays row-indexed (leaf-wise engine); out_shift as in
+  // partition_atomic_body (children into the other half of a 2N ping-pong buffer)
+  constexpr int NW = kPartThreads / kWave;
+  static_assert(S * NW <= kWave, "one-wave scan of the sub-chunk counts");
+  constexpr int CH = S * kPartThreads;
+  constexpr int kSplitLds = 1024;
+  __shared__ int s_l[S * NW];
+  __shared__ int s_first[kSplitLds];
+  __shared__ unsigned long long s_base;
+  __shared__ int s_tl;
+  const int nblocks = *nblocks_dev, nsplit = *nsplit_dev;
+  if ((int)blockIdx.x >= nblocks) return;  // uniform per block
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+  const bool lds_tab = nsplit <= kSplitLds;
+  if (lds_tab) {
+    for (int i = tid; i < nsplit; i += kPartThreads) s_first[i] = first_blk[i];
+    __syncthreads();
+  }
+  const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  struct Chunk { int si, beg, end, nbeg, nend, fs, th; };
+  auto locate = [&](int bid) {
+    int lo = 0, hi = nsplit - 1;  // last split with first_blk <= bid
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((lds_tab ? s_first[mid] : first_blk[mid]) <= bid) lo = mid; else hi = mid - 1;
+    }
+    Chunk c;
+    c.si = lo;
+    const int fb = first_blk[lo], nbeg = node_begin[lo], ncnt = node_count[lo];
+    c.fs = feat[lo];
+    c.th = thr[lo];
+    c.beg = nbeg + (bid - fb) * CH;
+    c.end = min(c.beg + CH, nbeg + ncnt);
+    c.nbeg = nbeg;
+    c.nend = nbeg + ncnt;
+    return c;
+  };
+  auto load_rows = [&](const Chunk& c, int (&r)[S]) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int pos = c.beg + j * kPartThreads + tid;
+      r[j] = pos < c.end ? (rows ? rows[pos] : pos) : 0;
+    }
+  };
+  int bid = (int)blockIdx.x;
+  Chunk c = locate(bid);
+  int r[S];
+  load_rows(c, r);
+  while (true) {
+    float2 g[S];
+    bool left[S];
+    const BinT* col = binsT + (size_t)c.fs * ncol;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int pos = c.beg + j * kPartThreads + tid;
+      const bool valid = pos < c.end;
+      g[j] = (valid && ghp) ? ghp[pos] : make_float2(0.f, 0.f);
+      left[j] = valid && (int)col[(unsigned)r[j]] <= c.th;
+    }
+    // next chunk: locate it and put its row-id loads in flight now
+    const int nbid = bid + (int)gridDim.x;
+    const bool more = nbid < nblocks;  // uniform per block
+    Chunk cn = c;
+    int rn[S];
+    if (more) {
+      cn = locate(nbid);
+      load_rows(cn, rn);
+    }
+    int lrank[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const unsigned long long lm = __ballot(left[j]);
+      lrank[j] = __popcll(lm & lt_mask);
+      if (l == 0) s_l[j * NW + wid] = __popcll(lm);
+    }
+    __syncthreads();
+    if (wid == 0) {
+      const int x = l < S * NW ? s_l[l] : 0;
+      int incl = x;
+#pragma unroll
+      for (int off = 1; off < S * NW; off <<= 1) {
+        const int y = __shfl_up(incl, off, kWave);
+        if (l >= off) incl += y;
+      }
+      if (l < S * NW) s_l[l] = incl - x;
+      const int tl_all = __shfl(incl, S * NW - 1, kWave);
+      if (l == 0) {
+        const int tv = c.end - c.beg;
+        s_base = atomicAdd(&cursor[(size_t)c.si * cs], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
+        s_tl = tl_all;
+      }
+    }
+    __syncthreads();
+    {
+      const int tl = s_tl;
+      const int tv = c.end - c.beg;
+      const unsigned long long base = s_base;
+      const int lofs = (int)(base & 0xffffffffull), rofs = (int)(base >> 32);
+      const int sh = out_shift ? out_shift[c.si] : 0;
+      const int rstart = c.nend - rofs - (tv - tl) + sh;
+      const int lstart = c.nbeg + lofs + sh;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const int rank = j * kPartThreads + tid;
+        if (rank < tv) {
+          const int lb = s_l[j * NW + wid] + lrank[j];
+          const int dst = left[j] ? lstart + lb : rstart + (rank - lb);
+          rows_out[dst] = r[j];
+          if (gh_out) gh_out[dst] = g[j];
+        }
+      }
+    }
+    __syncthreads();  // s_l / s_base / s_tl are reused by the next chunk
+    if (!more) break;
+    bid = nbid;
+    c = cn;
+#pragma unroll
+    for (int j = 0; j < S; ++j) r[j] = rn[j];
+  }
+}
+
 }  // namespace ytk

@@ -143,7 +143,7 @@ def test_device_builder_matches_host_builder(cuda, kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_FUSE_SPLIT_PLAN": "1"},
+@pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_FUSE_SPLIT_PLAN": "1"}, {"YTK_PART_PREFETCH": "0"},
                                  {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
@@ -268,6 +268,22 @@ def test_device_leafwise_matches_host(monkeypatch, kw):
     assert res[0][0] == res[1][0]
     assert res[0][1:] == res[1][1:]
     assert res[0][0].count("leaf=") > 3
+
+
+@pytest.mark.gpu
+def test_device_leafwise_partition_prefetch_identical(monkeypatch):
+    """Leaf-wise engine with the software-pipelined partition body (YTK_LW_PART_PREFETCH=1)
+    builds the default engine's trees byte for byte."""
+    res = []
+    for pf in ("0", "1"):
+        monkeypatch.setenv("YTK_LW_PART_PREFETCH", pf)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 63
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
+        tr.train()
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1]
 
 
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():
