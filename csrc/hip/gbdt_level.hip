@@ -427,13 +427,13 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
-template <bool kScatter, int KP, int kS, bool kPrefetch>
+template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
                                   int dgap, int use_loc, int fused, int maxp) {
   if constexpr (kScatter && kPrefetch)
-    partition_atomic_body_pf<uint8_t, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+    partition_atomic_body_pf<uint8_t, kS, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   else
@@ -649,14 +649,18 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   if (p.part_chunk != kPartThreads * kAtomSub && p.part_chunk != kPartThreads * 2 * kAtomSub)
     throw std::invalid_argument("lv_partition_children: part_chunk must be 2048 or 4096");
   const bool wide = p.part_chunk == kPartThreads * 2 * kAtomSub;
-  // software-pipelined partition (next chunk's row ids in flight during this chunk's
-  // rank / reserve / scatter): measured 1.474-1.496 -> 1.441 ms/tree; YTK_PART_PREFETCH=0: off
+  // software-pipelined partition: the next chunk's row ids and (g, h) in flight during this
+  // chunk's rank / reserve / scatter. Measured (profiles/r2_partition_chunk.md): off
+  // 1.474-1.496, row ids only (YTK_PART_PREFETCH=1) 1.430-1.441, row ids + (g, h) (default,
+  // 87 VGPRs) 1.393 ms/tree; YTK_PART_PREFETCH=0: off
   const char* pf = getenv("YTK_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
-#define YTK_LVPC2(SC, KP, S, PF)                                                                              \
-  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF>), grid, dim3(kPartThreads), 0, s, p, b,            \
+  const bool pf_gh = !(pf && (pf[0] == '0' || pf[0] == '1'));
+#define YTK_LVPC3(SC, KP, S, PF, PG)                                                                          \
+  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
                      (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
+#define YTK_LVPC2(SC, KP, S, PF) do { if ((PF) && pf_gh) YTK_LVPC3(SC, KP, S, PF, true); else YTK_LVPC3(SC, KP, S, PF, false); } while (0)
 #define YTK_LVPC1(SC, KP, S) do { if (prefetch && (SC)) YTK_LVPC2(SC, KP, S, true); else YTK_LVPC2(SC, KP, S, false); } while (0)
 #define YTK_LVPC(SC, KP) do { if (wide) YTK_LVPC1(SC, KP, 2 * kAtomSub); else YTK_LVPC1(SC, KP, kAtomSub); } while (0)
   if (maxp <= 64) {
@@ -669,6 +673,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
 #undef YTK_LVPC
 #undef YTK_LVPC1
 #undef YTK_LVPC2
+#undef YTK_LVPC3
   YTK_LAUNCH_CHECK();
 }
 

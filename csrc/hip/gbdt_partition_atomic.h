@@ -187,7 +187,7 @@ __device__ __forceinline__ void partition_atomic_body(
 // ranks, reserves and scatters the current one, so the row-id round trip of chunk i + 1
 // overlaps the ballot / cursor-atomic / scatter phases of chunk i. Same output as the
 // unpipelined body (same reservation per chunk, same placement).
-template <typename BinT, int S = kAtomSub>
+template <typename BinT, int S = kAtomSub, bool kGh = false>
 __device__ __forceinline__ void partition_atomic_body_pf(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
@@ -239,29 +239,38 @@ __device__ __forceinline__ void partition_atomic_body_pf(
       r[j] = pos < c.end ? (rows ? rows[pos] : pos) : 0;
     }
   };
+  auto load_gh = [&](const Chunk& c, float2 (&g)[S]) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int pos = c.beg + j * kPartThreads + tid;
+      g[j] = (pos < c.end && ghp) ? ghp[pos] : make_float2(0.f, 0.f);
+    }
+  };
   int bid = (int)blockIdx.x;
   Chunk c = locate(bid);
   int r[S];
   load_rows(c, r);
+  float2 g[S];
+  if (kGh) load_gh(c, g);
   while (true) {
-    float2 g[S];
     bool left[S];
     const BinT* col = binsT + (size_t)c.fs * ncol;
+    if (!kGh) load_gh(c, g);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int pos = c.beg + j * kPartThreads + tid;
-      const bool valid = pos < c.end;
-      g[j] = (valid && ghp) ? ghp[pos] : make_float2(0.f, 0.f);
-      left[j] = valid && (int)col[(unsigned)r[j]] <= c.th;
+      left[j] = pos < c.end && (int)col[(unsigned)r[j]] <= c.th;
     }
-    // next chunk: locate it and put its row-id loads in flight now
+    // next chunk: locate it and put its row-id (kGh: and (g, h)) loads in flight now
     const int nbid = bid + (int)gridDim.x;
     const bool more = nbid < nblocks;  // uniform per block
     Chunk cn = c;
     int rn[S];
+    float2 gn[kGh ? S : 1];
     if (more) {
       cn = locate(nbid);
       load_rows(cn, rn);
+      if constexpr (kGh) load_gh(cn, gn);
     }
     int lrank[S];
 #pragma unroll
@@ -313,6 +322,10 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     c = cn;
 #pragma unroll
     for (int j = 0; j < S; ++j) r[j] = rn[j];
+    if constexpr (kGh) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) g[j] = gn[j];
+    }
   }
 }
 
