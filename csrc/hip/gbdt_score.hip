@@ -323,6 +323,10 @@ __device__ __forceinline__ int walk_row_regs(const BinT* row, const int* sf, con
   return walk_regs<BinT, kDw>(d, sf, st, sl, sr);
 }
 
+// rows per thread whose loads are in flight together in tree_grad_kernel's register walk
+// (1 -> 2: 148 -> 136 us per Higgs round; 4: 121 VGPRs, 141 us)
+constexpr int kTreeGradRows = 2;
+
 // K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
 // kDw > 0: rows of exactly kDw dwords walked in registers; kDw == 0: generic byte loads.
 template <typename BinT, int kDw, int kLoss>
@@ -368,23 +372,26 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
   };
   if constexpr (kDw > 0) {
     if (nnodes > 0) {
-      // two rows (r, r + G) per iteration with every load of both issued before either
+      // kTreeGradRows rows (r, r + G, ...) per iteration with every load issued before any
       // walk: the row loop was latency bound at one row in flight per thread. The rows of
       // a thread are still accumulated in the order r, r + G, r + 2G, ... (fp64 sums
       // unchanged)
-      for (; r0 + G < N; r0 += 2 * G) {
-        const long long r1 = r0 + G;
-        uint32_t d0[kDw], d1[kDw];
-        load_row_regs<kDw>(bins + r0 * stride, d0);
-        load_row_regs<kDw>(bins + r1 * stride, d1);
-        const float s0 = score[r0], s1 = score[r1];
-        const float i0 = init[r0], i1 = init[r1];
-        const float l0 = label[r0], l1 = label[r1];
-        const float w0 = weight ? weight[r0] : 1.f, w1 = weight ? weight[r1] : 1.f;
-        const int n0 = walk_regs<BinT, kDw>(d0, sf, st, sl, sr);
-        const int n1 = walk_regs<BinT, kDw>(d1, sf, st, sl, sr);
-        finish_row(r0, s0, n0, i0, l0, w0);
-        finish_row(r1, s1, n1, i1, l1, w1);
+      constexpr int U = kTreeGradRows;
+      for (; r0 + (U - 1) * G < N; r0 += U * G) {
+        uint32_t d[U][kDw];
+        float sc0[U], in0[U], lb0[U], wt0[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long r = r0 + u * G;
+          load_row_regs<kDw>(bins + r * stride, d[u]);
+          sc0[u] = score[r];
+          in0[u] = init[r];
+          lb0[u] = label[r];
+          wt0[u] = weight ? weight[r] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          finish_row(r0 + u * G, sc0[u], walk_regs<BinT, kDw>(d[u], sf, st, sl, sr), in0[u], lb0[u], wt0[u]);
       }
     }
   }
