@@ -160,7 +160,10 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
 
 // Single-pass partition kernel (level engine and host-planned leaf-wise): see
 // partition_atomic_body in gbdt_partition_atomic.h.
-template <typename BinT, bool kScatter>
+// kPrefetch (scatter with (g, h) moving: the level engine's multi-GPU levels): the
+// software-pipelined body, next chunk's row ids and (g, h) in flight (see
+// lv_partition_children_kernel; YTK_PART_PREFETCH=0 turns it off).
+template <typename BinT, bool kScatter, bool kPrefetch = false>
 __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
@@ -168,8 +171,13 @@ __global__ __launch_bounds__(kPartThreads) void partition_atomic_kernel(
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
     unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift) {
-  partition_atomic_body<BinT, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, first_blk, nsplit_dev,
-                                        nblocks_dev, feat, thr, node_begin, node_count, cursor, out_shift, 1);
+  if constexpr (kScatter && kPrefetch)
+    partition_atomic_body_pf<BinT, kAtomSub, true>(binsT, ncol, rows, ghp, rows_out, gh_out, first_blk, nsplit_dev,
+                                                   nblocks_dev, feat, thr, node_begin, node_count, cursor,
+                                                   out_shift, 1);
+  else
+    partition_atomic_body<BinT, kScatter>(binsT, ncol, rows, ghp, rows_out, gh_out, first_blk, nsplit_dev,
+                                          nblocks_dev, feat, thr, node_begin, node_count, cursor, out_shift, 1);
 }
 
 }  // namespace ytk
@@ -306,8 +314,11 @@ extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long n
                                      uintptr_t out_shift, uintptr_t stream) {
   if (max_blocks <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define YTK_PART_ATOMIC(BT, SC)                                                                   \
-  hipLaunchKernelGGL((partition_atomic_kernel<BT, SC>), dim3(std::min(max_blocks, kPartGrid)), dim3(kPartThreads), 0, s, \
+  const char* pf = getenv("YTK_PART_PREFETCH");
+  const bool prefetch = ghp && gh_out && !(pf && (pf[0] == '0' || pf[0] == '1'));
+#define YTK_PART_ATOMIC(BT, SC) do { if ((SC) && prefetch) YTK_PART_ATOMIC2(BT, SC, true); else YTK_PART_ATOMIC2(BT, SC, false); } while (0)
+#define YTK_PART_ATOMIC2(BT, SC, PF)                                                              \
+  hipLaunchKernelGGL((partition_atomic_kernel<BT, SC, PF>), dim3(std::min(max_blocks, kPartGrid)), dim3(kPartThreads), 0, s, \
                      (const BT*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,  \
                      (float2*)gh_out, (const int*)first_blk, (const int*)nsplit_dev,               \
                      (const int*)nblocks_dev, (const int*)feat, (const int*)thr,                   \
@@ -319,5 +330,6 @@ extern "C" void ytk_partition_atomic(uintptr_t binsT, int bin_bytes, long long n
     if (count_only) YTK_PART_ATOMIC(uint16_t, false); else YTK_PART_ATOMIC(uint16_t, true);
   }
 #undef YTK_PART_ATOMIC
+#undef YTK_PART_ATOMIC2
   YTK_LAUNCH_CHECK();
 }
