@@ -85,6 +85,8 @@ void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int
 void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, int, int, uintptr_t, uintptr_t, int, int,
                        const float*, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
+                           float, float, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintptr_t, long long, uintptr_t, uintptr_t,
                                uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t);
 // gbdt_leafwise.hip
@@ -136,7 +138,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fm_sgd_update", &ytk_fm_sgd_update);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 7 || fp.size() != 6)
+    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6)
       throw std::invalid_argument("lv_step: bad argument sizes");
     ytk_lv_step(which, ptrs.data(), ip.data(), fp.data(), a0, a1, stream);
   });
@@ -153,16 +155,17 @@ PYBIND11_MODULE(_ytk_hip, m) {
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                      int count_only, int a0, int a1, int maxp, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 7 || fp.size() != 6)
+    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
                               max_blocks, count_only, a0, a1, maxp, stream);
   });
+  m.def("split_node_grouped", &ytk_split_node_grouped);
   m.def("lv_split_plan", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,
                               uintptr_t fmask, int f0, int nitems, const std::vector<float>& gpf, uintptr_t inv_dev,
                               uintptr_t part, uintptr_t counters, int implicit_items, int maxp, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 7 || fp.size() != 6 || gpf.size() != 4)
+    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6 || gpf.size() != 4)
       throw std::invalid_argument("lv_split_plan: bad argument sizes");
     ytk_lv_split_plan(ptrs.data(), ip.data(), fp.data(), hist, B, F, nbins_f, fmask, f0, nitems, gpf.data(), inv_dev,
                       part, counters, implicit_items, maxp, stream);

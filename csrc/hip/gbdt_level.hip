@@ -38,6 +38,7 @@ struct LvParams {
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
   int hist_target, part_target, min_rows;
   int part_chunk;  // rows per single-pass partition chunk (fused kernel: 256 x rows per thread)
+  int split_groups;  // split records per item (feature groups of split_node_kernel; 1 = one)
 };
 
 struct LvBufs {
@@ -212,7 +213,21 @@ __device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused
   const int nsi = st[ST_N_SITEMS];
   for (int i = tid; i < nsi; i += NT) {
     DNode& n = b.nodes[b.item_nid[i]];
-    const SplitOut& o = b.split_out[i];
+    // the item's best over its feature-group records: better() order (larger gain, then
+    // lower feature, then lower bin), "none" (-1) last -- the single block's argmax
+    const int ng = p.split_groups;
+    int bg = 0;
+    auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
+    for (int g = 1; g < ng; ++g) {
+      const SplitOut& c = b.split_out[(size_t)i * ng + g];
+      const SplitOut& bb = b.split_out[(size_t)i * ng + bg];
+      if (better(c.loss_chg, fkey(c.feat), fkey(c.bin_b), bb.loss_chg, fkey(bb.feat), fkey(bb.bin_b))) bg = g;
+    }
+    SplitOut o = b.split_out[(size_t)i * ng + bg];
+    if (bg != 0) {  // node totals: identical exact sums in every group's record
+      o.g = b.split_out[(size_t)i * ng].g;
+      o.h = b.split_out[(size_t)i * ng].h;
+    }
     n.G = o.g;
     n.H = o.h;
     n.gl = o.gl;
@@ -598,6 +613,7 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   p.part_target = ip[4];
   p.min_rows = ip[5];
   p.part_chunk = ip[6];
+  p.split_groups = max(1, ip[7]);
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -635,6 +651,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   p.part_target = ip[4];
   p.min_rows = ip[5];
   p.part_chunk = ip[6];
+  p.split_groups = max(1, ip[7]);
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -696,6 +713,7 @@ void ytk_lv_split_plan(const uintptr_t* ptrs, const int* ip, const float* fp, ui
   p.part_target = ip[4];
   p.min_rows = ip[5];
   p.part_chunk = ip[6];
+  p.split_groups = max(1, ip[7]);
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];

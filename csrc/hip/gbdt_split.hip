@@ -480,7 +480,12 @@ __global__ __launch_bounds__(kNodeThreads) void split_node_kernel(
     gp.inv_sh = inv_dev[1];
   }
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
-  split_node_block(hist, B, F, Bp, nbins_f, fmask, f0, it, out + blockIdx.x, gp, sh_hist);
+  // gridDim.y feature groups per node: block (x, y) searches features [y*FGs, (y+1)*FGs)
+  // and writes record x * gridDim.y + y (the level planner keeps each node's best)
+  const int G = (int)gridDim.y, FGs = (F + G - 1) / G;
+  const int fbeg = (int)blockIdx.y * FGs, fend = min(F, fbeg + FGs);
+  split_node_block(hist, B, F, Bp, nbins_f, fmask, f0, it, out + (size_t)blockIdx.x * G + blockIdx.y, gp, sh_hist,
+                   fbeg, fend);
 }
 
 }  // namespace ytk
@@ -527,6 +532,30 @@ extern "C" void ytk_split_combine(uintptr_t all, int P, int cap, uintptr_t n_dev
                      reinterpret_cast<hipStream_t>(stream), (const SplitOut*)all, P, cap, (const int*)n_dev,
                      n_max, tot_rank, (SplitOut*)out);
   YTK_LAUNCH_CHECK();
+}
+
+// Node-resident split search with `groups` feature groups per node (grid nitems x groups,
+// records [item][group]); returns 0 (nothing launched) if the node-resident kernel does
+// not apply (then use ytk_split_find with one record per item).
+extern "C" int ytk_split_node_grouped(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask, int f0,
+                                      uintptr_t items, int nitems, uintptr_t out, float mcw, float l1, float l2,
+                                      float max_abs_leaf, uintptr_t nitems_dev, uintptr_t inv_dev, int groups,
+                                      uintptr_t stream) {
+  if (nitems <= 0) return 1;
+  const int Bp = B + 1;
+  const int FGs = (F + groups - 1) / std::max(1, groups);
+  if (groups < 1 || groups > F || (groups - 1) * FGs >= F) return 0;  // every group non-empty
+  const size_t node_lds = (size_t)FGs * Bp * sizeof(long long) * 2;
+  if (!(node_lds <= kNodeLdsMax && B <= 4 * kWave && B * FGs <= kNodeLoads * kNodeThreads && F <= kNodeMaxF &&
+        F < 0xffff))
+    return 0;
+  GainParams gp{mcw, l1, l2, max_abs_leaf, 1.0, 1.0};
+  hipLaunchKernelGGL(split_node_kernel, dim3(nitems, groups), dim3(kNodeThreads), node_lds,
+                     reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, Bp, (const int*)nbins_f,
+                     (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp, (const int*)nitems_dev,
+                     (const double*)inv_dev);
+  YTK_LAUNCH_CHECK();
+  return 1;
 }
 
 extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t fmask,

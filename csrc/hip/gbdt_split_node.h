@@ -131,11 +131,18 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // The node-resident split search of one node by one kNodeThreads block: item `it`, result
 // to *out. sh_hist: dynamic LDS of F * Bp longlong2; nb/fm: per-feature bin counts and
 // feature mask (read into LDS here together with the histogram).
+// Features [fbeg, fend) of the node only (feature groups: one node searched by several
+// blocks, each writing its own record; the level planner keeps the best by better()).
+// The node totals come from the group's copy of feature f0 when the group holds it, else
+// from its first feature: every row adds its (g, h) to exactly one bin of EVERY feature, so
+// the exact int64 sums are the same for all features.
 __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, int B, int F, int Bp,
                                                  const int* __restrict__ nbins_f,
                                                  const uint8_t* __restrict__ fmask, int f0, int4 it,
                                                  SplitOut* __restrict__ out, const GainParams& gp,
-                                                 longlong2* sh_hist) {
+                                                 longlong2* sh_hist, int fbeg = 0, int fend = -1) {
+  if (fend < 0) fend = F;
+  const int FG = fend - fbeg;
   constexpr int kW = kNodeThreads / kWave;
   __shared__ float s_chg[kW];
   __shared__ int s_feat[kW], s_a[kW], s_b[kW];
@@ -145,55 +152,58 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
   const int t = threadIdx.x, wid = t >> 6, l = lane_id();
   int nb_t = 0;
   uint8_t fm_t = 0;
-  if (t < F) { nb_t = nbins_f[t]; fm_t = fmask[t]; }
+  if (t < FG) { nb_t = nbins_f[fbeg + t]; fm_t = fmask[fbeg + t]; }
   const size_t slot_sz = (size_t)B * F * 2;
   longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
   const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
   const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
   const bool derived = it.w != 0;
-  // ---- stream the node's histogram into LDS (all loads of a thread in flight at once)
-  const int total = B * F;
+  // ---- stream the node's histogram (this group's features) into LDS (all loads of a
+  // thread in flight at once); local entry i = bin * FG + fl -> global bin * F + fbeg + fl
+  const int total = B * FG;
+  auto gidx = [&](int i) { const int bin = i / FG; return bin * F + fbeg + (i - bin * FG); };
   longlong2 v[kNodeLoads];
   if (derived) {
     longlong2 s[kNodeLoads];
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
       const int i = t + j * kNodeThreads;
-      if (i < total) { v[j] = hp[i]; s[j] = hs[i]; }
+      if (i < total) { const int gi = gidx(i); v[j] = hp[gi]; s[j] = hs[gi]; }
     }
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
       const int i = t + j * kNodeThreads;
       if (i < total) {
         v[j] = make_longlong2(v[j].x - s[j].x, v[j].y - s[j].y);
-        hn[i] = v[j];
+        hn[gidx(i)] = v[j];
       }
     }
   } else {
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
       const int i = t + j * kNodeThreads;
-      if (i < total) v[j] = hn[i];
+      if (i < total) v[j] = hn[gidx(i)];
     }
   }
 #pragma unroll
   for (int j = 0; j < kNodeLoads; ++j) {
     const int i = t + j * kNodeThreads;
     if (i < total) {
-      const int bin = i / F, f = i - bin * F;
+      const int bin = i / FG, f = i - bin * FG;
       sh_hist[f * Bp + bin] = v[j];
     }
   }
-  if (t < F) { s_nb[t] = nb_t; s_fm[t] = fm_t; }
+  if (t < FG) { s_nb[t] = nb_t; s_fm[t] = fm_t; }
   __syncthreads();
   // ---- node totals (exact int64, first sampled feature: DataParallelTreeMaker:543-573);
   // every wave computes them itself (no extra barrier)
   long long Gq, Hq;
   {
-    const int nb0 = s_nb[f0];
+    const int ft = (f0 >= fbeg && f0 < fend) ? f0 - fbeg : 0;  // local feature of the totals
+    const int nb0 = s_nb[ft];
     long long sg = 0, sh = 0;
     for (int bin = l; bin < nb0; bin += kWave) {
-      const longlong2 q = sh_hist[f0 * Bp + bin];
+      const longlong2 q = sh_hist[ft * Bp + bin];
       sg += q.x;
       sh += q.y;
     }
@@ -206,16 +216,17 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
   float best_chg = -INFINITY;
   int best_f = 0xffff, best_a = -1, best_b = 0xffff;
   double best_gl = 0.0, best_hl = 0.0;
-  for (int f = wid; f < F; f += kW) {
-    if (!s_fm[f]) continue;  // wave-uniform
-    const int nb = s_nb[f];
+  for (int fl = wid; fl < FG; fl += kW) {
+    if (!s_fm[fl]) continue;  // wave-uniform
+    const int f = fbeg + fl;  // global feature (record + tie-break order)
+    const int nb = s_nb[fl];
     longlong2 q[4];
     long long sg = 0, sh = 0;
     int lastne = -1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int bin = 4 * l + k;
-      q[k] = (bin < nb) ? sh_hist[f * Bp + bin] : make_longlong2(0, 0);
+      q[k] = (bin < nb) ? sh_hist[fl * Bp + bin] : make_longlong2(0, 0);
       sg += q[k].x;
       sh += q[k].y;
       if (q[k].x != 0 || q[k].y != 0) lastne = bin;

@@ -156,7 +156,17 @@ class DeviceLevelBuilder:
         self.hist_items = i32(self.max_items * 4)
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)
-        self.split_out = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
+        # feature groups per node in the split search (one block per (node, group), each on
+        # its own CU; the planner keeps each node's best record): YTK_SPLIT_GROUPS, default 4.
+        # The owner-computes mode and the fused split + plan kernel write one record per node.
+        self.split_groups = 1
+        owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, B * F * 2 * 8) == "owner"
+        if not owner and not self.wide and not self.fuse_split_plan and gops.split_node_fits(B, F):
+            g = max(1, min(F, int(os.environ.get("YTK_SPLIT_GROUPS", "4"))))
+            while g > 1 and (g - 1) * (-(-F // g)) >= F:  # every group non-empty
+                g -= 1
+            self.split_groups = g
+        self.split_out = torch.zeros(2 * self.maxp * 48 * self.split_groups, dtype=torch.uint8, device=dev)
         # split_find runs one block per (node, feature): per-feature candidates + per-item
         # arrival counters (reset by the combining block)
         self.split_part = torch.zeros(2 * self.maxp * F * 48, dtype=torch.uint8, device=dev)
@@ -218,7 +228,7 @@ class DeviceLevelBuilder:
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
         self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.hist_target, self.part_target,
-                   self.MIN_ROWS, self.part_chunk]
+                   self.MIN_ROWS, self.part_chunk, self.split_groups]
         self.tree_count = 0
         # set by the trainer when its fused gradient pass counts the rows per leaf
         # (tree_grad leaf_counts): the last level then needs no counting partition and no
@@ -319,6 +329,13 @@ class DeviceLevelBuilder:
         if self.owner:
             fmask, f0, tot = self._owner_fmask(fmask_np)
             out = self.split_local
+        if self.split_groups > 1 and not self.owner:
+            if h.split_node_grouped(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
+                                    ptr(self.split_items), nitems, ptr(out), gp["mcw"], gp["l1"], gp["l2"],
+                                    gp["max_abs_leaf"], nitems_dev, ptr(self.inv_scales), self.split_groups, s):
+                return
+            raise RuntimeError("split_node_grouped: node-resident split search does not apply "
+                               f"(B={self.B}, F={self.F}); set YTK_SPLIT_GROUPS=1")
         h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                      ptr(self.split_items), nitems, ptr(out), gp["mcw"], gp["l1"], gp["l2"],
                      gp["max_abs_leaf"], 1.0, 1.0, nitems_dev, ptr(self.inv_scales), ptr(self.split_part),

@@ -285,7 +285,7 @@ class DeviceLeafBuilder:
         if idle is not None:
             idle()
         tm.mark("batches")
-        h.lv_step(4, self._lv_ptrs(), [0] * 7, [0.0] * 6, self.max_nodes, 0, s)
+        h.lv_step(4, self._lv_ptrs(), [0] * 8, [0.0] * 6, self.max_nodes, 0, s)
         self.tree_count += 1
         self.last_batches = it
         snap = self.snap.clone()
