@@ -171,7 +171,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                       part, counters, implicit_items, maxp, stream);
   });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 37 || ip.size() != 8 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 37 || ip.size() != 9 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);

@@ -55,6 +55,7 @@ struct LwParams {
   int max_depth, max_leaf, min_split_samples, speculate;  // speculate: 0 off, else percent
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
   int hist_target, min_rows, cap, N;  // N: half size of the ping-pong row buffers
+  int split_groups;  // split records per item (feature groups of split_node_kernel)
 };
 
 struct LwBufs {
@@ -328,7 +329,21 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
   const int nsi = st[LW_N_SITEMS];
   for (int i = tid; i < nsi; i += kLwPlanThreads) {
     const int sid = b.item_sid[i];
-    const SplitOut o = b.split_out[i];
+    // best of the item's feature-group records (split_node_kernel order: larger gain, then
+    // lower feature, then lower bin; none last); node totals are equal in every record
+    const int ng = p.split_groups;
+    auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
+    int bg = 0;
+    for (int g = 1; g < ng; ++g) {
+      const SplitOut& c = b.split_out[(size_t)i * ng + g];
+      const SplitOut& bb = b.split_out[(size_t)i * ng + bg];
+      if (better(c.loss_chg, fkey(c.feat), fkey(c.bin_b), bb.loss_chg, fkey(bb.feat), fkey(bb.bin_b))) bg = g;
+    }
+    SplitOut o = b.split_out[(size_t)i * ng + bg];
+    if (bg != 0) {
+      o.g = b.split_out[(size_t)i * ng].g;
+      o.h = b.split_out[(size_t)i * ng].h;
+    }
     b.G[sid] = o.g;
     b.H[sid] = o.h;
     b.gl[sid] = o.gl;
@@ -924,6 +939,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.min_rows = ip[5];
   p.cap = ip[6];
   p.N = ip[7];
+  p.split_groups = ip[8] > 0 ? ip[8] : 1;
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];

@@ -24,6 +24,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ...ops import gbdt as gops
 from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
@@ -90,7 +91,15 @@ class DeviceLeafBuilder:
         self.n_sitems = 2 * ml + 2
         self.split_items = i32(4 * self.n_sitems)
         self.item_sid = i32(self.n_sitems)
-        self.split_out = torch.zeros(self.n_sitems * 48, dtype=torch.uint8, device=dev)
+        # split search in feature groups (one block per (node, group); the planner keeps each
+        # node's best record) -- as DeviceLevelBuilder, YTK_SPLIT_GROUPS (default 4)
+        self.split_groups = 1
+        if gops.split_node_fits(B, F):
+            g = max(1, min(F, int(os.environ.get("YTK_SPLIT_GROUPS", "4"))))
+            while g > 1 and (g - 1) * (-(-F // g)) >= F:
+                g -= 1
+            self.split_groups = g
+        self.split_out = torch.zeros(self.n_sitems * 48 * self.split_groups, dtype=torch.uint8, device=dev)
         self.split_part = torch.zeros(self.n_sitems * F * 48, dtype=torch.uint8, device=dev)
         self.split_cnt = torch.zeros(self.n_sitems, dtype=torch.int32, device=dev)
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -160,7 +169,7 @@ class DeviceLeafBuilder:
         # budget the batch choice ranks within (100 = the host planner's virtual replay)
         spec = int(os.environ.get("YTK_LW_SPEC_PCT", "100")) if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
         return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
-                self.cap, self.N]
+                self.cap, self.N, self.split_groups]
 
     def _ptrs(self):
         f, i = self.nd_f64, self.nd_i32
@@ -206,6 +215,13 @@ class DeviceLeafBuilder:
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
                              self.REDUCE_Y, s)
         gp = self.gp
+        if self.split_groups > 1:
+            if not h.split_node_grouped(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
+                                        ptr(self.split_items), self.n_sitems, ptr(self.split_out), gp["mcw"], gp["l1"],
+                                        gp["l2"], gp["max_abs_leaf"], st + 4 * W_N_SITEMS, ptr(self.inv_scales),
+                                        self.split_groups, s):
+                raise RuntimeError("split_node_grouped does not apply; set YTK_SPLIT_GROUPS=1")
+            return
         h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0, ptr(self.split_items),
                      self.n_sitems, ptr(self.split_out), gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"], 1.0, 1.0,
                      st + 4 * W_N_SITEMS, ptr(self.inv_scales), ptr(self.split_part), ptr(self.split_cnt), s)
