@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
       if (ff >= F) continue;
       const bool direct = r.y <= kReduceDirect;
       if (direct && blockIdx.z != 0) continue;
-      const int step = direct ? 1 : kReduceSplit;
+      const int step = direct ? 1 : (int)gridDim.z;  // split-K factor (launch z extent)
       long long g = 0, h = 0;
       int t = direct ? 0 : (int)blockIdx.z;
       for (; t + 7 * step < r.y; t += 8 * step) {
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   // block sums them all and STORES -- no 8-way int64 atomics at the memory side
   const bool direct = cnt <= kReduceDirect;
   if (direct && blockIdx.z != 0) continue;
-  const int step = direct ? 1 : kReduceSplit;
+  const int step = direct ? 1 : (int)gridDim.z;  // split-K factor (launch z extent)
   const longlong2* st = reinterpret_cast<const longlong2*>(staging);
   long long g = 0, h = 0;
   int t = direct ? 0 : (int)blockIdx.z;
@@ -575,7 +575,12 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
                           (const float*)scales_dev, (long long*)staging, (const int*)work_off_dev);
   YTK_LAUNCH_CHECK();
   const int E = nb_lds * fw;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
+  // split-K factor (YTK_REDUCE_SPLIT overrides; exact int64 atomics, so the sums do not
+  // depend on it). 32 / 16-way on the one- / two-slot top levels measured slower (reduce
+  // 66 -> 77 us per tree: more memory-side atomics), so kReduceSplit stays.
+  const char* rs = getenv("YTK_REDUCE_SPLIT");
+  const int zs = rs ? std::max(1, atoi(rs)) : kReduceSplit;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, zs), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
                      (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids,
                      (const int*)nullptr, (const int2*)nullptr, fw);
