@@ -159,13 +159,9 @@ class DeviceLevelBuilder:
         # feature groups per node in the split search (one block per (node, group), each on
         # its own CU; the planner keeps each node's best record): YTK_SPLIT_GROUPS, default 4.
         # The owner-computes mode and the fused split + plan kernel write one record per node.
-        self.split_groups = 1
-        owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, B * F * 2 * 8) == "owner"
-        if not owner and not self.wide and not self.fuse_split_plan and gops.split_node_fits(B, F):
-            g = max(1, min(F, int(os.environ.get("YTK_SPLIT_GROUPS", "4"))))
-            while g > 1 and (g - 1) * (-(-F // g)) >= F:  # every group non-empty
-                g -= 1
-            self.split_groups = g
+        self.owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, B * F * 2 * 8) == "owner"
+        self.split_groups = (gops.split_groups(B, F) if not (self.owner or self.wide or self.fuse_split_plan)
+                             else 1)
         self.split_out = torch.zeros(2 * self.maxp * 48 * self.split_groups, dtype=torch.uint8, device=dev)
         # split_find runs one block per (node, feature): per-feature candidates + per-item
         # arrival counters (reset by the combining block)
@@ -194,7 +190,6 @@ class DeviceLevelBuilder:
         # owner-computes sync (TreeParams.hist_sync): reduce-scatter by feature block (the
         # level's count slots ride along in every rank's block), split search on the owned
         # features, allgather of the 48-B records, device-side argmax (split_combine)
-        self.owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, slot_elems * 8) == "owner"
         if self.owner:
             self.fr, self.fblocks = self.comm.feature_blocks(F)
             self.own = self.fblocks[self.comm.rank]

@@ -93,12 +93,7 @@ class DeviceLeafBuilder:
         self.item_sid = i32(self.n_sitems)
         # split search in feature groups (one block per (node, group); the planner keeps each
         # node's best record) -- as DeviceLevelBuilder, YTK_SPLIT_GROUPS (default 4)
-        self.split_groups = 1
-        if gops.split_node_fits(B, F):
-            g = max(1, min(F, int(os.environ.get("YTK_SPLIT_GROUPS", "4"))))
-            while g > 1 and (g - 1) * (-(-F // g)) >= F:
-                g -= 1
-            self.split_groups = g
+        self.split_groups = gops.split_groups(B, F)
         self.split_out = torch.zeros(self.n_sitems * 48 * self.split_groups, dtype=torch.uint8, device=dev)
         self.split_part = torch.zeros(self.n_sitems * F * 48, dtype=torch.uint8, device=dev)
         self.split_cnt = torch.zeros(self.n_sitems, dtype=torch.int32, device=dev)

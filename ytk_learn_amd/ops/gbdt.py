@@ -152,6 +152,19 @@ def split_node_fits(B: int, F: int) -> bool:
             and os.environ.get("YTK_SPLIT_NODE") != "0")
 
 
+def split_groups(B: int, F: int) -> int:
+    """Feature groups per node for the node-resident split search (split_node_grouped:
+    one block per (node, group), the planner keeps each node's best record). YTK_SPLIT_GROUPS
+    (default 4, profiles/r2_split_groups.md); 1 when the node-resident kernel does not apply.
+    Every group must hold at least one feature."""
+    if not split_node_fits(B, F):
+        return 1
+    g = max(1, min(F, int(os.environ.get("YTK_SPLIT_GROUPS", "4"))))
+    while g > 1 and (g - 1) * (-(-F // g)) >= F:
+        g -= 1
+    return g
+
+
 def split_find(hist, B, F, nbins_f, fmask, f0, items, params):
     """Best split per item. items int32 [n, 4] = (slot, parent, sibling, derived).
 
