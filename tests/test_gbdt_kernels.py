@@ -406,15 +406,3 @@ def test_hist_build_wide_matches_cpu(cuda, F, nb, B, gathered):
                     hg, B, SG, SH, binsT=binsT.to(cuda))
     assert torch.equal(hg.cpu(), hc)
 
-
-def test_split_groups_every_group_nonempty(monkeypatch):
-    """Feature groups of the node-resident split search: every group holds >= 1 feature;
-    no grouping where the node-resident kernel does not apply (B > 256)."""
-    monkeypatch.delenv("YTK_SPLIT_GROUPS", raising=False)
-    for F in range(1, 70):
-        g = gops.split_groups(256, F)
-        fg = -(-F // g)
-        assert 1 <= g <= min(4, F) and (g - 1) * fg < F
-    assert gops.split_groups(300, 28) == 1
-    monkeypatch.setenv("YTK_SPLIT_GROUPS", "1")
-    assert gops.split_groups(256, 28) == 1
