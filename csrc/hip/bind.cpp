@@ -45,6 +45,9 @@ void ytk_partition_count(uintptr_t, int, long long, uintptr_t, uintptr_t, uintpt
 // gbdt_score.hip
 void ytk_tree_add_bins(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, int, uintptr_t, int, int, uintptr_t);
+int ytk_forest_loss_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                         uintptr_t, int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, float, float, uintptr_t,
+                         uintptr_t, uintptr_t);
 int ytk_forest_predict_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                             uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, int, float, uintptr_t, uintptr_t);
 void ytk_forest_predict(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t,
@@ -124,6 +127,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("tree_add_bins", &ytk_tree_add_bins);
   m.def("forest_predict", &ytk_forest_predict);
   m.def("forest_predict_regs", &ytk_forest_predict_regs);
+  m.def("forest_loss_regs", &ytk_forest_loss_regs);
   m.def("bin_assign", &ytk_bin_assign);
   m.def("grad_hess", &ytk_grad_hess);
   m.def("tree_grad", &ytk_tree_grad);

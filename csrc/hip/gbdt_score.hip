@@ -284,6 +284,62 @@ __global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ lo
   acc_finish_body(loss_acc, nblocks);
 }
 
+// Test-set round tail in one pass (K == 1, one new tree): walk the raw row held in
+// registers (as forest_predict_regs_kernel), score += leaf value, then the point loss and
+// prediction (as tree_grad_kernel without gradients). Same grid and row -> thread mapping
+// as the grad_hess launch it replaces, so the fp64 loss sums are bitwise the same.
+template <int kF4, int kLoss>
+__global__ __launch_bounds__(256) void forest_loss_regs_kernel(
+    const float* __restrict__ X, long long N, const int* __restrict__ nfeat, const float* __restrict__ nthr,
+    const int* __restrict__ nleft, const int* __restrict__ nright, const uint8_t* __restrict__ ndefl,
+    const float* __restrict__ nval, int root, int nnodes, float* __restrict__ score,
+    const float* __restrict__ init, const float* __restrict__ label, const float* __restrict__ weight, float p0,
+    float score_div, float* __restrict__ pred, double* __restrict__ loss_acc) {
+  extern __shared__ __attribute__((aligned(16))) int fsm[];
+  int* sf = fsm;
+  float* sth = reinterpret_cast<float*>(fsm + nnodes);
+  int* sl = fsm + 2 * nnodes;
+  int* sr = fsm + 3 * nnodes;
+  float* sv = reinterpret_cast<float*>(fsm + 4 * nnodes);
+  for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
+    const int f = nfeat[i];
+    sf[i] = f < 0 ? -1 : (f | (ndefl[i] ? (1 << 30) : 0));
+    sth[i] = nthr[i]; sl[i] = nleft[i]; sr[i] = nright[i]; sv[i] = nval[i];
+  }
+  __syncthreads();
+  double lsum = 0.0, wsum = 0.0;
+  for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < N;
+       r += (long long)gridDim.x * blockDim.x) {
+    float x[4 * kF4];
+    const float4* r4 = reinterpret_cast<const float4*>(X + r * (4 * kF4));
+#pragma unroll
+    for (int i = 0; i < kF4; ++i) {
+      const float4 v = r4[i];
+      x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+    }
+    const float s0 = score[r], ini = init[r], lab = label[r];
+    const float w = weight ? weight[r] : 1.f;
+    int n = root;
+    int fe = sf[n];
+    while (fe >= 0) {
+      const int f = fe & 0xffff;
+      float v = x[0];
+#pragma unroll
+      for (int i = 1; i < 4 * kF4; ++i) v = (f == i) ? x[i] : v;
+      const bool left = (v != v) ? ((fe >> 30) & 1) : (v <= sth[n]);
+      n = left ? sl[n] : sr[n];
+      fe = sf[n];
+    }
+    const float s = s0 + 1.0f * sv[n];  // forest_predict: out += scale * value, scale 1
+    score[r] = s;
+    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+    lsum += (double)w * o.l;
+    wsum += (double)w;
+    if (pred) pred[r] = o.p;
+  }
+  block_acc(lsum, wsum, loss_acc, 0.f, 0.f, nullptr);
+}
+
 // Leaf of a bin-threshold tree for one row held in registers (kDw dwords, packed bins):
 // the whole row is fetched with 16-B loads (a wave reads 64 contiguous rows), then
 // every level extracts its feature with a select chain -- no dependent memory loads.
@@ -532,6 +588,51 @@ void ytk_forest_predict(uintptr_t X, long long xstride, long long N, uintptr_t n
                      (const int*)troot, (const int*)tout, T, (float*)out, ostride, scale,
                      (int*)leaf_out);
   YTK_LAUNCH_CHECK();
+}
+
+// Fused test-set tail (forest_loss_regs_kernel + the ordered acc finish); returns 0
+// (nothing launched) when the row layout / tree size does not qualify.
+int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t nfeat, uintptr_t nthr,
+                         uintptr_t nleft, uintptr_t nright, uintptr_t ndefl, uintptr_t nval, int root, int nnodes,
+                         uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight, int loss_id, float p0,
+                         float score_div, uintptr_t pred, uintptr_t loss_acc, uintptr_t stream) {
+  if (N <= 0) return 0;
+  const int kf4 = (int)(xstride / 4);
+  if (xstride % 4 != 0 || kf4 < 1 || kf4 > 8 || (X % 16) != 0 || nnodes <= 0 || nnodes > 2048 || loss_id < 0 ||
+      loss_id > 4)
+    return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  const int grid = grid_for(N, 256 * 8);
+#define YTK_FLR(K, L)                                                                                       \
+  hipLaunchKernelGGL((forest_loss_regs_kernel<K, L>), dim3(grid), dim3(256), lds, s, (const float*)X, N,      \
+                     (const int*)nfeat, (const float*)nthr, (const int*)nleft, (const int*)nright,              \
+                     (const uint8_t*)ndefl, (const float*)nval, root, nnodes, (float*)score, (const float*)init, \
+                     (const float*)label, (const float*)weight, p0, score_div, (float*)pred, (double*)loss_acc)
+#define YTK_FLR_L(K)                          \
+  switch (loss_id) {                          \
+    case 0: YTK_FLR(K, 0); break;             \
+    case 1: YTK_FLR(K, 1); break;             \
+    case 2: YTK_FLR(K, 2); break;             \
+    case 3: YTK_FLR(K, 3); break;             \
+    default: YTK_FLR(K, 4); break;            \
+  }
+  switch (kf4) {
+    case 1: YTK_FLR_L(1); break;
+    case 2: YTK_FLR_L(2); break;
+    case 3: YTK_FLR_L(3); break;
+    case 4: YTK_FLR_L(4); break;
+    case 5: YTK_FLR_L(5); break;
+    case 6: YTK_FLR_L(6); break;
+    case 7: YTK_FLR_L(7); break;
+    default: YTK_FLR_L(8); break;
+  }
+#undef YTK_FLR_L
+#undef YTK_FLR
+  YTK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
+  YTK_LAUNCH_CHECK();
+  return 1;
 }
 
 // forest_predict with the row-register walk; returns 0 (nothing launched) when the layout

@@ -479,11 +479,18 @@ class GBDTTrainer:
                 fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
                 fl.trees = host_trees
                 raws = [{k: torch.from_numpy(v).to(self.dev) for k, v in fl.flatten().items()}]
-            for raw in raws:
-                gops.forest_predict(self.Xte, raw, self.te_score, 1.0)
             te = self.test_data
-            acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
-                                     i + 1, False)
+            if (dev_trees and len(raws) == 1 and self.K == 1 and self.kernel_loss not in (None, "softmax")
+                    and os.environ.get("YTK_FUSED_TEST_TAIL", "1") != "0"):
+                # the device builder's raw tree (root 0): scoring + loss in one pass
+                acc_te = gops.forest_predict_loss(self.Xte, raws[0], self.te_score, self.te_init, te.y, te.weight,
+                                                  self.kernel_loss, self._kparam(), self._score_div(i + 1),
+                                                  self.te_pred)
+            if acc_te is None:
+                for raw in raws:
+                    gops.forest_predict(self.Xte, raw, self.te_score, 1.0)
+                acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
+                                         i + 1, False)
             self.timer.mark("test_eval")
         self._acc = (acc, acc_te)
         self.rounds_done = i + 1

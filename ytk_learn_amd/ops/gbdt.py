@@ -511,6 +511,26 @@ def bin_assign(X, cand, coff, out, outT=None):
 ACC_LEN = 4 + 2 * 256 * 8  # == kAccLen (gbdt_score.hip): (loss, weight), counter, block partials
 
 
+def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_div, pred):
+    """Test-set round tail in one GPU pass (K == 1, ONE raw tree ``tree`` rooted at node 0, as
+    forest_predict's dict; its troot / tout are not read): score += tree(row), then the loss sums and prediction -- exactly
+    forest_predict + grad_hess(want_grad=False) (same values, same fp64 summation order).
+    Returns the float64 [2] (loss sum, weight sum) device tensor, or None when the fused
+    kernel does not apply (the caller then runs the two steps)."""
+    loss_id = LOSS_IDS[loss]
+    if not (X.is_cuda and X.is_contiguous() and score.shape[1] == 1 and loss_id != 5
+            and tree["troot"].numel() == 1):
+        return None
+    check_cuda(X, score, init, label, weight, pred, *tree.values())
+    acc = torch.empty(ACC_LEN, dtype=torch.float64, device=X.device)
+    ok = hip().forest_loss_regs(ptr(X), X.shape[1], X.shape[0], ptr(tree["nfeat"]), ptr(tree["nthr"]),
+                                ptr(tree["nleft"]), ptr(tree["nright"]), ptr(tree["ndefl"]), ptr(tree["nval"]),
+                                0, tree["nfeat"].numel(), ptr(score),
+                                ptr(init), ptr(label), ptr(weight), loss_id, float(param), float(score_div),
+                                ptr(pred), ptr(acc), stream(X))
+    return acc[:2] if ok else None
+
+
 def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True,
               ghmax=None):
     """Fill pred [N,K] (optional) and gh [K,N,2]; return (weighted loss sum, weight sum) as a
