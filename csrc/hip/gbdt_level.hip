@@ -663,9 +663,11 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
   const int use_loc = (arg1 >> 30) & 1, fused = (arg1 >> 29) & 1;
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
-  if (p.part_chunk != kPartThreads * kAtomSub && p.part_chunk != kPartThreads * 2 * kAtomSub)
-    throw std::invalid_argument("lv_partition_children: part_chunk must be 2048 or 4096");
+  if (p.part_chunk != kPartThreads * kAtomSub && p.part_chunk != kPartThreads * 2 * kAtomSub &&
+      p.part_chunk != kPartThreads * kAtomSub / 2)
+    throw std::invalid_argument("lv_partition_children: part_chunk must be 1024, 2048 or 4096");
   const bool wide = p.part_chunk == kPartThreads * 2 * kAtomSub;
+  const bool narrow = p.part_chunk == kPartThreads * kAtomSub / 2;  // small shards: 2x the blocks
   // software-pipelined partition: the next chunk's row ids and (g, h) in flight during this
   // chunk's rank / reserve / scatter. Measured (profiles/r2_partition_chunk.md): off
   // 1.474-1.496, row ids only (YTK_PART_PREFETCH=1) 1.430-1.441, row ids + (g, h) (default,
@@ -679,7 +681,12 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
                      (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
 #define YTK_LVPC2(SC, KP, S, PF) do { if ((PF) && pf_gh) YTK_LVPC3(SC, KP, S, PF, true); else YTK_LVPC3(SC, KP, S, PF, false); } while (0)
 #define YTK_LVPC1(SC, KP, S) do { if (prefetch && (SC)) YTK_LVPC2(SC, KP, S, true); else YTK_LVPC2(SC, KP, S, false); } while (0)
-#define YTK_LVPC(SC, KP) do { if (wide) YTK_LVPC1(SC, KP, 2 * kAtomSub); else YTK_LVPC1(SC, KP, kAtomSub); } while (0)
+#define YTK_LVPC(SC, KP)                                                          \
+  do {                                                                            \
+    if (wide) YTK_LVPC1(SC, KP, 2 * kAtomSub);                                    \
+    else if (narrow) YTK_LVPC1(SC, KP, kAtomSub / 2);                             \
+    else YTK_LVPC1(SC, KP, kAtomSub);                                             \
+  } while (0)
   if (maxp <= 64) {
     if (count_only) YTK_LVPC(false, 64); else YTK_LVPC(true, 64);
   } else if (maxp <= 512) {
