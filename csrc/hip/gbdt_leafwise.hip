@@ -871,14 +871,15 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
 // kPrefetch: the software-pipelined body (partition_atomic_body_pf).
-template <bool kPrefetch>
+template <bool kPrefetch, bool kPfGh = false>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
 void lw_partition_kernel(LwParams p, LwBufs b, const uint8_t* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
                                                                    float2* gh_out) {
   if constexpr (kPrefetch)
-    partition_atomic_body_pf<uint8_t>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
+    partition_atomic_body_pf<uint8_t, kAtomSub, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
+                                                       b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                       b.cursor, b.part_shift, kCurStride);
   else
@@ -1019,11 +1020,17 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
                       uintptr_t gh_out, int max_blocks, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
-  // YTK_LW_PART_PREFETCH=1: the software-pipelined partition body
+  // software-pipelined partition body, next chunk's row ids + (g, h) in flight (default:
+  // 3.41 -> 3.28-3.35 ms/tree, profiles/r2_partition_chunk.md); YTK_LW_PART_PREFETCH=1: row
+  // ids only (measured slower), 0: unpipelined
   const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
-  const bool prefetch = pf && pf[0] == '1';
+  const bool prefetch = !(pf && pf[0] == '0');
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
-  if (prefetch)
+  if (prefetch && !(pf && pf[0] == '1'))  // next chunk's (g, h) as well
+    hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint8_t*)binsT, ncol,
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+  else if (prefetch)
     hipLaunchKernelGGL(lw_partition_kernel<true>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
                        (float2*)gh_out);

@@ -277,7 +277,7 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
     """Leaf-wise engine with the software-pipelined partition body (YTK_LW_PART_PREFETCH=1)
     builds the default engine's trees byte for byte."""
     res = []
-    for pf in ("0", "1"):
+    for pf in ("0", "1", "2"):
         monkeypatch.setenv("YTK_LW_PART_PREFETCH", pf)
         p = _params("loss", rounds=3)
         p.tree.max_leaf_cnt = 63
@@ -285,7 +285,7 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
         tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
         tr.train()
         res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
-    assert res[0] == res[1]
+    assert res[0] == res[1] == res[2]
 
 
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():
