@@ -442,13 +442,13 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
-template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false>
+template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, bool kPfCol = false>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
                                   int dgap, int use_loc, int fused, int maxp) {
   if constexpr (kScatter && kPrefetch)
-    partition_atomic_body_pf<uint8_t, kS, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+    partition_atomic_body_pf<uint8_t, kS, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   else
@@ -675,11 +675,17 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const char* pf = getenv("YTK_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const bool pf_gh = !(pf && (pf[0] == '0' || pf[0] == '1'));
-#define YTK_LVPC3(SC, KP, S, PF, PG)                                                                          \
-  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG>), grid, dim3(kPartThreads), 0, s, p, b,            \
+  const bool pf_col = pf && pf[0] == '3';  // YTK_PART_PREFETCH=3: + the next chunk's split-feature bytes
+#define YTK_LVPC4(SC, KP, S, PF, PG, PC)                                                                      \
+  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG, PC>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
                      (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
-#define YTK_LVPC2(SC, KP, S, PF) do { if ((PF) && pf_gh) YTK_LVPC3(SC, KP, S, PF, true); else YTK_LVPC3(SC, KP, S, PF, false); } while (0)
+#define YTK_LVPC2(SC, KP, S, PF)                                                  \
+  do {                                                                            \
+    if ((PF) && pf_col) YTK_LVPC4(SC, KP, S, PF, true, true);                     \
+    else if ((PF) && pf_gh) YTK_LVPC4(SC, KP, S, PF, true, false);                \
+    else YTK_LVPC4(SC, KP, S, PF, false, false);                                  \
+  } while (0)
 #define YTK_LVPC1(SC, KP, S) do { if (prefetch && (SC)) YTK_LVPC2(SC, KP, S, true); else YTK_LVPC2(SC, KP, S, false); } while (0)
 #define YTK_LVPC(SC, KP)                                                          \
   do {                                                                            \
@@ -697,7 +703,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
 #undef YTK_LVPC
 #undef YTK_LVPC1
 #undef YTK_LVPC2
-#undef YTK_LVPC3
+#undef YTK_LVPC4
   YTK_LAUNCH_CHECK();
 }
 

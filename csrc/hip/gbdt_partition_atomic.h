@@ -187,7 +187,7 @@ __device__ __forceinline__ void partition_atomic_body(
 // ranks, reserves and scatters the current one, so the row-id round trip of chunk i + 1
 // overlaps the ballot / cursor-atomic / scatter phases of chunk i. Same output as the
 // unpipelined body (same reservation per chunk, same placement).
-template <typename BinT, int S = kAtomSub, bool kGh = false>
+template <typename BinT, int S = kAtomSub, bool kGh = false, bool kCol = false>
 __device__ __forceinline__ void partition_atomic_body_pf(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
@@ -252,14 +252,31 @@ __device__ __forceinline__ void partition_atomic_body_pf(
   load_rows(c, r);
   float2 g[S];
   if (kGh) load_gh(c, g);
-  while (true) {
-    bool left[S];
+  // kCol: the next chunk's split-feature bytes are gathered before this chunk's scatter
+  // (its row ids have arrived by then), so a chunk starts with all its loads done
+  int cb[kCol ? S : 1];
+  auto load_col = [&](const Chunk& c, const int (&r)[S], int (&cb)[S]) {
     const BinT* col = binsT + (size_t)c.fs * ncol;
-    if (!kGh) load_gh(c, g);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int pos = c.beg + j * kPartThreads + tid;
-      left[j] = pos < c.end && (int)col[(unsigned)r[j]] <= c.th;
+      cb[j] = pos < c.end ? (int)col[(unsigned)r[j]] : 0x7fffffff;
+    }
+  };
+  if constexpr (kCol) load_col(c, r, cb);
+  while (true) {
+    bool left[S];
+    if (!kGh) load_gh(c, g);
+    if constexpr (kCol) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) left[j] = cb[j] <= c.th;
+    } else {
+      const BinT* col = binsT + (size_t)c.fs * ncol;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const int pos = c.beg + j * kPartThreads + tid;
+        left[j] = pos < c.end && (int)col[(unsigned)r[j]] <= c.th;
+      }
     }
     // next chunk: locate it and put its row-id (kGh: and (g, h)) loads in flight now
     const int nbid = bid + (int)gridDim.x;
@@ -297,6 +314,9 @@ __device__ __forceinline__ void partition_atomic_body_pf(
       }
     }
     __syncthreads();
+    if constexpr (kCol) {
+      if (more) load_col(cn, rn, cb);
+    }
     {
       const int tl = s_tl;
       const int tv = c.end - c.beg;
