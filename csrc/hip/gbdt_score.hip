@@ -385,7 +385,7 @@ constexpr int kTreeGradRows = 2;
 
 // K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
 // kDw > 0: rows of exactly kDw dwords walked in registers; kDw == 0: generic byte loads.
-template <typename BinT, int kDw, int kLoss>
+template <typename BinT, int kDw, int kLoss, bool kLdsWalk = false>
 __global__ __launch_bounds__(256) void tree_grad_kernel(
     const BinT* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
     const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
@@ -445,9 +445,30 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
           lb0[u] = label[r];
           wt0[u] = weight ? weight[r] : 1.f;
         }
+        if constexpr (kLdsWalk) {
+          // the rows go to thread-private LDS slots (kDw + 1 dwords: odd stride, the byte
+          // reads of a wave spread over the banks) and each level reads its feature's bin
+          // with one LDS byte load instead of a kDw-way register select chain (the walk's
+          // VALU work; the kernel is VALU-bound with the fp64 loss)
+          uint32_t* s_rows = reinterpret_cast<uint32_t*>(tsm + (leaf_part ? 6 : 5) * nnodes);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          finish_row(r0 + u * G, sc0[u], walk_regs<BinT, kDw>(d[u], sf, st, sl, sr), in0[u], lb0[u], wt0[u]);
+          for (int u = 0; u < U; ++u) {
+            uint32_t* slot = s_rows + ((size_t)u * blockDim.x + threadIdx.x) * (kDw + 1);
+#pragma unroll
+            for (int k = 0; k < kDw; ++k) slot[k] = d[u][k];
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const BinT* rb = reinterpret_cast<const BinT*>(s_rows + ((size_t)u * blockDim.x + threadIdx.x) * (kDw + 1));
+            int n = 0;
+            for (int f = sf[0]; f >= 0; f = sf[n]) n = ((int)rb[f] <= st[n]) ? sl[n] : sr[n];
+            finish_row(r0 + u * G, sc0[u], n, in0[u], lb0[u], wt0[u]);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            finish_row(r0 + u * G, sc0[u], walk_regs<BinT, kDw>(d[u], sf, st, sl, sr), in0[u], lb0[u], wt0[u]);
+        }
       }
     }
   }
@@ -742,8 +763,16 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
   // register walk for 16/32/64-byte rows (F <= 64 uint8 features), byte loads otherwise
   const int dw = (aligned && (row_bytes == 16 || row_bytes == 32 || row_bytes == 64))
                      ? (int)(row_bytes / 4) : 0;
+  // rows staged in LDS for the walk (kDw > 0): 135 -> 124 us per Higgs round (level-wise
+  // 1.364 / 1.353 -> 1.350 / 1.345 ms/tree, leaf-wise 3.339 -> 3.311); YTK_TG_LDS_WALK=0: the
+  // register select-chain walk
+  const char* lw = getenv("YTK_TG_LDS_WALK");
+  const bool lds_walk = !(lw && lw[0] == '0') && dw > 0;
+  const size_t lds_rows = lds_walk ? (size_t)kTreeGradRows * 256 * (dw + 1) * sizeof(uint32_t) : 0;
 #define YTK_TG_ONE(BT, DW, LID)                                                                   \
-  hipLaunchKernelGGL((tree_grad_kernel<BT, DW, LID>), dim3(grid), dim3(256), lds, s, (const BT*)bins, \
+  do { if (lds_walk) YTK_TG_ONE2(BT, DW, LID, true); else YTK_TG_ONE2(BT, DW, LID, false); } while (0)
+#define YTK_TG_ONE2(BT, DW, LID, LW)                                                              \
+  hipLaunchKernelGGL((tree_grad_kernel<BT, DW, LID, LW>), dim3(grid), dim3(256), lds + ((LW) ? lds_rows : 0), s, (const BT*)bins, \
                      stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,                \
                      (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
                      (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
@@ -772,6 +801,7 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
   }
 #undef YTK_TG_LAUNCH
 #undef YTK_TG_ONE
+#undef YTK_TG_ONE2
   if (leaf_part) {  // leaf counts + the loss sums in one launch (block nnodes = acc_finish)
     hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + 1), dim3(256), 0, s, (const int*)leaf_part, grid,
                        nnodes, (double*)leaf_out, (double*)loss_acc);
