@@ -319,13 +319,15 @@ __global__ __launch_bounds__(256) void forest_loss_regs_kernel(
     }
     const float s0 = score[r], ini = init[r], lab = label[r];
     const float w = weight ? weight[r] : 1.f;
+    // the row goes to a thread-private LDS slot (4 kF4 + 1 floats: odd stride) and each level
+    // reads its feature with one LDS load instead of a (4 kF4)-way register select chain
+    float* slot = reinterpret_cast<float*>(fsm + 5 * nnodes) + (size_t)threadIdx.x * (4 * kF4 + 1);
+#pragma unroll
+    for (int i = 0; i < 4 * kF4; ++i) slot[i] = x[i];
     int n = root;
     int fe = sf[n];
     while (fe >= 0) {
-      const int f = fe & 0xffff;
-      float v = x[0];
-#pragma unroll
-      for (int i = 1; i < 4 * kF4; ++i) v = (f == i) ? x[i] : v;
+      const float v = slot[fe & 0xffff];
       const bool left = (v != v) ? ((fe >> 30) & 1) : (v <= sth[n]);
       n = left ? sl[n] : sr[n];
       fe = sf[n];
@@ -623,7 +625,8 @@ int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t 
       loss_id > 4)
     return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const size_t lds = (size_t)nnodes * 5 * sizeof(int);
+  // node arrays + one (4 kf4 + 1)-float row slot per thread (LDS-staged walk)
+  const size_t lds = (size_t)nnodes * 5 * sizeof(int) + (size_t)256 * (4 * kf4 + 1) * sizeof(float);
   const int grid = grid_for(N, 256 * 8);
 #define YTK_FLR(K, L)                                                                                       \
   hipLaunchKernelGGL((forest_loss_regs_kernel<K, L>), dim3(grid), dim3(256), lds, s, (const float*)X, N,      \
