@@ -57,7 +57,7 @@ void ytk_bin_assign(uintptr_t, long long, long long, int, uintptr_t, uintptr_t, 
                     long long, uintptr_t, uintptr_t);
 void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, int, float, float,
                    uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
-void ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+int ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
                    float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t);

@@ -19,6 +19,9 @@
 namespace ytk {
 
 constexpr int kWave = 64;
+// dynamic LDS a kernel may request: 160 KiB per CU on gfx950, minus headroom for the
+// kernels' small static __shared__ reduction scratch
+constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 

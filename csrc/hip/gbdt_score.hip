@@ -387,7 +387,10 @@ constexpr int kTreeGradRows = 2;
 
 // K == 1 losses, optionally fused with the new tree's score update (row-major bins walk).
 // kDw > 0: rows of exactly kDw dwords walked in registers; kDw == 0: generic byte loads.
-template <typename BinT, int kDw, int kLoss, bool kLdsWalk = false>
+// kNodesGlobal: the node arrays do not fit in LDS (trees of > ~8k nodes, e.g. a host-built
+// leaf-wise tree with a large max_leaf_cnt): the walk reads them from global memory (byte
+// walk only, no leaf counts)
+template <typename BinT, int kDw, int kLoss, bool kLdsWalk = false, bool kNodesGlobal = false>
 __global__ __launch_bounds__(256) void tree_grad_kernel(
     const BinT* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
     const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
@@ -397,17 +400,22 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
     int want_grad, float* __restrict__ ghmax, int* __restrict__ leaf_part) {
   extern __shared__ __attribute__((aligned(16))) int tsm[];
-  int* sf = tsm;
-  int* st = tsm + nnodes;
-  int* sl = tsm + 2 * nnodes;
-  int* sr = tsm + 3 * nnodes;
-  float* sv = reinterpret_cast<float*>(tsm + 4 * nnodes);
+  static_assert(!kNodesGlobal || (kDw == 0 && !kLdsWalk), "global-node walk: byte walk only");
+  const int* sf = kNodesGlobal ? tfeat : tsm;
+  const int* st = kNodesGlobal ? tthr : tsm + nnodes;
+  const int* sl = kNodesGlobal ? tleft : tsm + 2 * nnodes;
+  const int* sr = kNodesGlobal ? tright : tsm + 3 * nnodes;
+  const float* sv = kNodesGlobal ? tval : reinterpret_cast<const float*>(tsm + 4 * nnodes);
   int* sc = tsm + 5 * nnodes;  // leaf_part: rows per node of this block
-  for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
-    sf[i] = tfeat[i]; st[i] = tthr[i]; sl[i] = tleft[i]; sr[i] = tright[i]; sv[i] = tval[i];
-    if (leaf_part) sc[i] = 0;
+  if constexpr (!kNodesGlobal) {
+    float* svw = reinterpret_cast<float*>(tsm + 4 * nnodes);
+    for (int i = threadIdx.x; i < nnodes; i += blockDim.x) {
+      tsm[i] = tfeat[i]; tsm[nnodes + i] = tthr[i]; tsm[2 * nnodes + i] = tleft[i];
+      tsm[3 * nnodes + i] = tright[i]; svw[i] = tval[i];
+      if (leaf_part) sc[i] = 0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   double lsum = 0.0, wsum = 0.0;
   float mg = 0.f, mh = 0.f;
   long long r0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -486,7 +494,7 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
       }
       s += sv[n];
       score[r] = s;
-      if (leaf_part) atomicAdd(&sc[n], 1);
+      if (!kNodesGlobal && leaf_part) atomicAdd(&sc[n], 1);
     }
     const float w = weight ? weight[r] : 1.f;
     const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)init[r], (double)label[r],
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     }
   }
   block_acc(lsum, wsum, loss_acc, mg, mh, ghmax);
-  if (leaf_part) {
+  if (!kNodesGlobal && leaf_part) {
     __syncthreads();
     for (int i = threadIdx.x; i < nnodes; i += blockDim.x) leaf_part[(size_t)blockIdx.x * nnodes + i] = sc[i];
   }
@@ -747,19 +755,24 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
 }
 
 // Fused: score += tree(row) (row-major bins walk) then loss / grad (K == 1).
-void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfeat,
+// Returns 1, or 0 (nothing launched) when the per-node leaf counts (leaf_part) do not fit in
+// LDS with the node arrays -- the caller must then count leaves another way.
+int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfeat,
                    uintptr_t tthr, uintptr_t tleft, uintptr_t tright, uintptr_t tval, int nnodes,
                    uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
                    long long N, int loss_id, float p0, float score_div, uintptr_t pred,
                    uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
                    uintptr_t leaf_part, uintptr_t leaf_out, uintptr_t stream) {
-  if (N <= 0) return;
+  if (N <= 0) return 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // leaf_part (optional, >= grid * nnodes ints) + leaf_out (nnodes doubles): rows per tree
   // node -- the level engine's last-level leaf counts, taken from this walk instead of a
   // separate counting partition pass
   if (leaf_part && nnodes <= 0) leaf_part = 0;
   const size_t lds = (size_t)nnodes * (leaf_part ? 6 : 5) * sizeof(int);
+  if (leaf_part && lds > kLdsBudget) return 0;
+  // the node arrays alone exceed the LDS budget: walk them in global memory
+  const bool nodes_global = lds > kLdsBudget;
   const int grid = grid_for(N, 256 * 8);
   const long long row_bytes = stride * bin_bytes;
   const bool aligned = (bins % 16) == 0;
@@ -770,8 +783,10 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
   // 1.364 / 1.353 -> 1.350 / 1.345 ms/tree, leaf-wise 3.339 -> 3.311); YTK_TG_LDS_WALK=0: the
   // register select-chain walk
   const char* lw = getenv("YTK_TG_LDS_WALK");
-  const bool lds_walk = !(lw && lw[0] == '0') && dw > 0;
-  const size_t lds_rows = lds_walk ? (size_t)kTreeGradRows * 256 * (dw + 1) * sizeof(uint32_t) : 0;
+  const size_t lds_rows_need = (size_t)kTreeGradRows * 256 * (dw + 1) * sizeof(uint32_t);
+  // the row slots only where they fit beside the node arrays (else the select-chain walk)
+  const bool lds_walk = !(lw && lw[0] == '0') && dw > 0 && !nodes_global && lds + lds_rows_need <= kLdsBudget;
+  const size_t lds_rows = lds_walk ? lds_rows_need : 0;
 #define YTK_TG_ONE(BT, DW, LID)                                                                   \
   do { if (lds_walk) YTK_TG_ONE2(BT, DW, LID, true); else YTK_TG_ONE2(BT, DW, LID, false); } while (0)
 #define YTK_TG_ONE2(BT, DW, LID, LW)                                                              \
@@ -791,7 +806,26 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
       default: YTK_TG_ONE(BT, DW, 4); break;    \
     }                                           \
   } while (0)
-  if (bin_bytes == 1) {
+  if (nodes_global) {
+#define YTK_TG_G(BT, LID)                                                                          \
+  hipLaunchKernelGGL((tree_grad_kernel<BT, 0, LID, false, true>), dim3(grid), dim3(256), 0, s, (const BT*)bins, \
+                     stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,                \
+                     (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
+                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
+                     p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,        \
+                     (float*)ghmax, (int*)nullptr)
+#define YTK_TG_GL(BT)                         \
+    switch (loss_id) {                        \
+      case 0: YTK_TG_G(BT, 0); break;         \
+      case 1: YTK_TG_G(BT, 1); break;         \
+      case 2: YTK_TG_G(BT, 2); break;         \
+      case 3: YTK_TG_G(BT, 3); break;         \
+      default: YTK_TG_G(BT, 4); break;        \
+    }
+    if (bin_bytes == 1) { YTK_TG_GL(uint8_t); } else { YTK_TG_GL(uint16_t); }
+#undef YTK_TG_GL
+#undef YTK_TG_G
+  } else if (bin_bytes == 1) {
     if (dw == 4) YTK_TG_LAUNCH(uint8_t, 4);
     else if (dw == 8) YTK_TG_LAUNCH(uint8_t, 8);
     else if (dw == 16) YTK_TG_LAUNCH(uint8_t, 16);
@@ -812,6 +846,7 @@ void ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tf
     hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
   }
   YTK_LAUNCH_CHECK();
+  return 1;
 }
 
 // tree_grad launches min(ceil(N / 256), 2048) blocks: the leaf_part scratch size

@@ -62,3 +62,31 @@ def test_distributed_weighted_median_matches_sort(seed, gather_max, buckets):
             continue
         o = np.argsort(v[m], kind="stable")
         assert got[k] == _weighted_median_sorted(v[m][o], w[m][o]), k
+
+
+def test_distributed_weighted_median_heavy_ties_resolve_without_gather():
+    """A leaf of 200k identical integer residuals plus a few outliers: the tied bucket is
+    resolved in place (survivors' range collapses) instead of all-gathering every tied row."""
+    import torch
+
+    from ytk_learn_amd.models.gbdt.refine import _weighted_median_sorted
+    from ytk_learn_amd.parallel.comm import Comm
+    from ytk_learn_amd.utils import quantile as q
+
+    rng = np.random.default_rng(3)
+    n = 200_000
+    v = np.full(n, 1.0)
+    v[:50] = rng.normal(size=50) * 100
+    v[50:90] = 7.0
+    g = np.zeros(n, np.int64)
+    g[n // 2:] = 1
+    v[n // 2:] = rng.integers(-3, 4, n - n // 2).astype(np.float64)  # 7 heavy tie values
+    w = np.ones(n)
+    got = q.distributed_weighted_median(torch.from_numpy(v), torch.from_numpy(w), torch.from_numpy(g), 2,
+                                        Comm.local(), buckets=64, gather_max=16)
+    for k in range(2):
+        m = g == k
+        o = np.argsort(v[m], kind="stable")
+        assert got[k] == _weighted_median_sorted(v[m][o], w[m][o])
+    # the final survivor gather holds no tied bulk
+    assert q.MEDIAN_STATS["gathered_local"] <= 16

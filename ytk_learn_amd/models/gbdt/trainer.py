@@ -105,6 +105,7 @@ class GBDTTrainer:
         self._inflight = deque()
         self._rb_free = []          # recycled pinned readback buffers
         self.round_losses = {}      # round -> (train loss, test loss), filled as rounds land
+        self._round_stats = {}      # round -> phase times of THAT round (for the metric sink)
         self._names_arr = None
 
     # ------------------------------------------------------------ preparation
@@ -171,6 +172,7 @@ class GBDTTrainer:
             self.builder.snapshot_copy = self.K != 1
             self.builder.defer_leaf_counts = (self.K == 1 and self.kernel_loss is not None
                                               and self.kernel_loss != "softmax"
+                                              and gops.leaf_counts_fit(self.builder.max_nodes)
                                               and os.environ.get("YTK_DEFER_LEAF_COUNTS", "1") != "0")
         else:
             self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
@@ -319,6 +321,8 @@ class GBDTTrainer:
         self.timer.begin()
         self.step(i)
         per = self.timer.end()
+        if per:  # this round's phase times, logged when the round lands (one round later)
+            self._round_stats[i] = dict(per)
         logs = self.p.verbose or self.log.enabled_for_round(i)
         if per and logs:
             self.log.info(f"[GBDT] time stats tree {i + 1}: {PhaseTimer.fmt(per)}")
@@ -395,12 +399,13 @@ class GBDTTrainer:
             self._log_round(i, trl, tel, current=(i + 1 == self.rounds_done))
 
     def _log_round(self, i: int, trl: float, tel: Optional[float], current: bool):
+        stats = self._round_stats.pop(i, None)
         if not (self.p.verbose or self.log.enabled_for_round(i)):
             return
         metric = getattr(self.log, "metric", None)
         if metric is not None:
             metric(model="gbdt", loss=self.loss.name, round=i + 1, train_loss=trl, test_loss=tel,
-                   time_stats=dict(self.timer.last) if self.timer.enabled else None)
+                   time_stats=stats if self.timer.enabled else None)
         out = [f"train loss = {jd(trl)}\n"]
         if self.p.watch_train and current:
             out.append(self._eval_str(True))

@@ -603,6 +603,15 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
     return torch.tensor([float((w * lv).sum()), float(w.sum())], dtype=torch.float64)
 
 
+LDS_BUDGET = 160 * 1024 - 1024  # == kLdsBudget (csrc/hip/common.h)
+
+
+def leaf_counts_fit(max_nodes: int) -> bool:
+    """Whether tree_grad can count rows per node for trees of ``max_nodes`` nodes: the
+    per-block counters sit in LDS next to the five node arrays (6 ints per node)."""
+    return max_nodes * 6 * 4 <= LDS_BUDGET
+
+
 def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
               want_grad=True, ghmax=None, leaf_counts=None):
     """Fused K==1 round tail: score += tree(row) (bin space, ROW-MAJOR bins [N, S]), then
@@ -627,11 +636,14 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
         if leaf_counts is not None:
             assert nn > 0 and leaf_counts.dtype == torch.float64 and leaf_counts.numel() >= nn
             part = torch.empty(hip().tree_grad_grid(N) * nn, dtype=torch.int32, device=score.device)
-        hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
+        ok = hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
                         bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
                         ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
                         loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), ptr(part), ptr(leaf_counts), stream(score))
+        if not ok:
+            raise ValueError(f"tree_grad: per-node leaf counts of a {nn}-node tree exceed the LDS budget "
+                             "(see leaf_counts_fit)")
         return acc[:2]
     assert leaf_counts is None, "leaf_counts: GPU only"
     if tree_arrays is not None:

@@ -112,6 +112,9 @@ def _first_reaching(cum: "np.ndarray", target: "np.ndarray") -> "np.ndarray":
     return np.where(ok.any(axis=1), ok.argmax(axis=1), cum.shape[1])
 
 
+MEDIAN_STATS = {"gathered_local": 0}  # rows this rank put into the last survivor gather
+
+
 def distributed_weighted_median(values, weights, groups, n_groups: int, comm, buckets: int = 1024,
                                 gather_max: int = 8192, max_rounds: int = 8):
     """EXACT weighted median per group of the union of every rank's rows, with fixed-size
@@ -144,10 +147,20 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
     below = np.zeros(G, np.float64)
     alive = torch.ones_like(g, dtype=torch.bool)
     lo_np, hi_np = lo.cpu().numpy(), hi.cpu().numpy()
+    # groups whose surviving rows all hold ONE value are resolved on the spot (median = that
+    # value) and leave the gather: heavy ties (e.g. integer residuals) would otherwise keep
+    # landing in one bucket and ship every tied row to every rank
+    resolved = np.full(G, np.nan)
     for _ in range(max_rounds):
         cnt = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, g[alive], torch.ones_like(g[alive]))
         comm.allreduce_(cnt)
         cnt_np = cnt.cpu().numpy()
+        flat = (cnt_np > 0) & (hi_np <= lo_np) & np.isnan(resolved)
+        if flat.any():
+            resolved[flat] = lo_np[flat]
+            fl_t = torch.from_numpy(flat).to(dev)
+            alive &= ~fl_t[g]
+            cnt_np = np.where(flat, 0, cnt_np)
         if cnt_np.max(initial=0) <= gather_max:
             break
         width = (hi_np - lo_np) / K
@@ -169,11 +182,22 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
         below = np.where(small, below, prev)
         new_lo = np.where(small, lo_np, lo_np + kstar * width)
         new_hi = np.where(small, hi_np, np.minimum(hi_np, lo_np + (kstar + 1) * width))
-        lo_np, hi_np = new_lo, new_hi
         alive_idx = torch.nonzero(alive).flatten()
         alive[alive_idx[~keep]] = False
+        # the survivors' actual range (one MIN all-reduce of (min, -max)): a bucket holding a
+        # single distinct value collapses to hi == lo and is resolved next round
+        gi2, vi2 = g[alive], v[alive]
+        mm = torch.full((2 * G,), float("inf"), dtype=torch.float64, device=dev)
+        mm[:G].scatter_reduce_(0, gi2, vi2, "amin")
+        mm[G:].scatter_reduce_(0, gi2, -vi2, "amin")
+        comm.allreduce_(mm, op="min")
+        mm_np = mm.cpu().numpy()
+        act_lo, act_hi = mm_np[:G], -mm_np[G:]
+        lo_np = np.where(small, new_lo, np.where(np.isfinite(act_lo), act_lo, new_lo))
+        hi_np = np.where(small, new_hi, np.where(np.isfinite(act_hi), act_hi, new_hi))
     # gather the survivors (padded all-gather of (group, value, weight))
     idx = torch.nonzero(alive).flatten()
+    MEDIAN_STATS["gathered_local"] = int(idx.numel())
     n_loc = torch.tensor([idx.numel()], dtype=torch.int64, device=dev)
     if comm.is_dist:
         ns = comm.allgather(n_loc).cpu().numpy()
@@ -186,7 +210,7 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
         rows = np.concatenate([allr[r, :ns[r]] for r in range(comm.world)])
     else:
         rows = torch.stack([g[idx].double(), v[idx], w[idx]], 1).cpu().numpy()
-    out = np.full(G, np.nan)
+    out = resolved.copy()
     if rows.size:
         o = np.lexsort((rows[:, 1], rows[:, 0]))
         rows = rows[o]
