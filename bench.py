@@ -19,7 +19,7 @@ Scaling is STRONG: the 10.5M rows are sharded over the N ranks.
 
 ``vs_baseline`` is null: the reference publishes no depth-6 level-wise number. The
 reference-identical shape (leaf-wise, 255 leaves) is timed separately on the same
-data at N=1 and reported as ``leafwise_s_per_tree`` / ``leafwise_vs_reference``
+data (every N) and reported as ``leafwise_s_per_tree`` / ``leafwise_vs_reference``
 (÷ 1.136 s/tree, docs/gbdt_experiments.md:104).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--profile", action="store_true", help="sync per phase and print time stats")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--leafwise-steps", type=int, default=None,
-                    help="extra timed leaf-wise 255-leaf rounds on the same data (default 10 at N=1, 0 at N>1)")
+                    help="extra timed leaf-wise 255-leaf rounds on the same data (default 10)")
     a = ap.parse_args()
 
     comm = Comm.from_env(device=a.device)
@@ -144,7 +144,7 @@ def main():
         print("leafwise planner profile (warmup + timed trees): " + json.dumps(tr.builder.prof_report()),
               file=sys.stderr)
     tr_builder = tr.builder
-    leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else (10 if world == 1 else 0)
+    leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else 10
     leaf = None
     if leaf_steps > 0 and a.policy == "level":
         del tr

@@ -99,6 +99,18 @@ uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
 void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_zero_slots(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+// gbdt_comm.hip
+void ytk_seg_median(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, int, uintptr_t, uintptr_t);
+void ytk_seg_prune(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
+int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
+                       uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
+                       uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int,
+                       uintptr_t);
+int ytk_tree_grad_hist_grid(long long);
+void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, uintptr_t);
+void ytk_lw_msg(int, uintptr_t, long long, uintptr_t, int, int, uintptr_t);
+void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
+void ytk_owner_unpack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 // gbdt_hist.hip (device-driven staged histogram)
 void ytk_hist_fx_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
                             int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
@@ -175,7 +187,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                       part, counters, implicit_items, maxp, stream);
   });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 37 || ip.size() != 9 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 37 || ip.size() != 10 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
@@ -184,5 +196,13 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lw_partition", &ytk_lw_partition);
   m.def("lw_zero_slots", &ytk_lw_zero_slots);
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
+  m.def("owner_pack", &ytk_owner_pack);
+  m.def("lw_msg", &ytk_lw_msg);
+  m.def("tree_grad_hist", &ytk_tree_grad_hist);
+  m.def("tree_grad_hist_grid", &ytk_tree_grad_hist_grid);
+  m.def("hist_reduce", &ytk_hist_reduce);
+  m.def("seg_median", &ytk_seg_median);
+  m.def("seg_prune", &ytk_seg_prune);
+  m.def("owner_unpack", &ytk_owner_unpack);
   m.attr("arch") = "gfx950";
 }

@@ -619,6 +619,22 @@ void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t g
   YTK_LAUNCH_CHECK();
 }
 
+// Second stage alone: staging items [0, nwork) (32-feature groups, work[k].x = slot) summed
+// into the zeroed slots [slot_base, slot_base + nslots) (used by the fused gradient + root
+// histogram pass, tree_grad_hist).
+void ytk_hist_reduce(uintptr_t staging, uintptr_t work, int nwork, uintptr_t hist, int B, int F, int slot_base,
+                     int nslots, uintptr_t stream) {
+  if (nwork <= 0 || nslots <= 0) return;
+  const int fw = 32;
+  const int groups = (F + fw - 1) / fw;
+  const int E = B * fw;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work, nwork,
+                     (const int*)nullptr, (long long*)hist, B, F, B, groups, slot_base, (const int*)nullptr,
+                     (const int*)nullptr, (const int2*)nullptr, fw);
+  YTK_LAUNCH_CHECK();
+}
+
 void ytk_hist_fx_global(uintptr_t bins, int bin_bytes, long long stride, int F, uintptr_t ghp,
                         uintptr_t rows, uintptr_t work, int nwork, uintptr_t hist, int B,
                         float sg, float sh, uintptr_t stream) {

@@ -56,6 +56,7 @@ struct LwParams {
   float min_split_loss, mcw, l1, l2, max_abs_leaf, lr;
   int hist_target, min_rows, cap, N;  // N: half size of the ping-pong row buffers
   int split_groups;  // split records per item (feature groups of split_node_kernel)
+  int dist;  // multi-GPU: per batch the host all-reduces the built slots + split cursors
 };
 
 struct LwBufs {
@@ -323,6 +324,20 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     return;
   }
   unsigned long long t_prev = b.prof && tid == 0 ? wall_clock64() : 0ull;
+  // multi-GPU: the previous batch's split cursors ((right << 32) | left rows) were
+  // all-reduced with its built histograms; the children's GLOBAL row counts replace the
+  // local ones the partition epilogue wrote (DataParallelTreeMaker.java:518,538)
+  if (p.dist) {
+    const int kprev = st[LW_N_SPLIT];
+    for (int j = tid; j < kprev; j += kLwPlanThreads) {
+      const int P = b.batch[j];
+      const int L = b.lc[P];
+      const long long lg = (long long)(b.cursor[(size_t)j * kCurStride] & 0xffffffffull);
+      b.cnt[L] = lg;
+      b.cnt[L + 1] = b.cnt[P] - lg;
+    }
+    __syncthreads();
+  }
   const int nsid = st[LW_N_SIDS];
   const double mcw2 = (double)p.mcw * 2.0;
   // A. split records of the previous batch (canSplit: UpdateStrategy.java:50-53)
@@ -742,8 +757,13 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
       const int nb = st[LW_BATCHES] + 1;
       st[LW_BATCHES] = nb;
       st[LW_EXPANDED] += k;
-      // planner progress for the host's launch throttle (reads pinned memory, no events)
-      if (b.done_host) ((volatile int*)b.done_host)[1] = nb;
+      // planner progress for the host's launch throttle (reads pinned memory, no events);
+      // [2] = the batch's split count (multi-GPU: sizes the batch's all-reduce), written
+      // before the count the host polls
+      if (b.done_host) {
+        ((volatile int*)b.done_host)[2] = k;
+        ((volatile int*)b.done_host)[1] = nb;
+      }
     }
   }
   LW_TICK(6);
@@ -794,7 +814,10 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
     // children that are terminal whatever the replay does get no histograms
     const bool need = !(p.max_depth >= 0 && dep == p.max_depth) &&
                       !(p.min_split_samples > 0 && lloc < p.min_split_samples && rcnt < p.min_split_samples);
-    const bool left_small = lloc < rcnt;
+    // multi-GPU: the counts are still local here, so the built (smaller) child is chosen by
+    // the globally identical hessian sums -- every rank builds the same slot (exact int64
+    // histograms make the choice result-neutral)
+    const bool left_small = p.dist ? (b.hl[P] < b.H[P] - b.hl[P]) : (lloc < rcnt);
     s_need[j] = need ? 1 : 0;
     s_small[j] = need ? (left_small ? L : R) : -1;
     if (need) atomicAdd(&s_total, (unsigned long long)(left_small ? lloc : rcnt));
@@ -908,6 +931,31 @@ __global__ __launch_bounds__(256) void lw_zero_slots_kernel(longlong2* __restric
   }
 }
 
+// Multi-GPU batch message: msg = [kcap slots: the batch's built histograms in build order]
+// [kcap * kCurStride words: the batch's split cursors]; one all-reduce per batch carries both
+// (HistogramBuilder.java:95 + the child-count allreduce). Every rank plans the same batch, so
+// build_ids / nb are identical; slots past nb are never read.
+__global__ __launch_bounds__(256) void lw_msg_kernel(long long* __restrict__ hist, long long slot_elems,
+                                                     const int* __restrict__ build_ids, const int* __restrict__ nb_dev,
+                                                     unsigned long long* __restrict__ cursor, long long* __restrict__ msg,
+                                                     int kcap, int unpack) {
+  const int nb = min(*nb_dev, kcap);
+  const long long nh = (long long)nb * slot_elems;
+  const long long ncur = (long long)kcap * kCurStride;
+  const long long cur0 = (long long)kcap * slot_elems;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nh + ncur; i += (long long)gridDim.x * 256) {
+    if (i < nh) {
+      const long long kb = i / slot_elems, e = i - kb * slot_elems;
+      long long* hs = hist + (size_t)build_ids[kb] * slot_elems + e;
+      if (unpack) *hs = msg[i]; else msg[i] = *hs;
+    } else {
+      const long long j = i - nh;
+      if (unpack) cursor[j] = (unsigned long long)msg[cur0 + j];
+      else msg[cur0 + j] = (long long)cursor[j];
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -926,7 +974,7 @@ extern "C" {
 //       state, loss, heap, batch, part_feat, part_thr, part_begin, part_cnt, part_first,
 //       part_shift, cursor, hist_items, build_ids, split_items, item_sid, split_out, root_cnt,
 //       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range
-// ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N
+// ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N, split_groups, dist
 // fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr. Returns an engine handle.
 int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   LwEngine e;
@@ -941,6 +989,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.cap = ip[6];
   p.N = ip[7];
   p.split_groups = ip[8] > 0 ? ip[8] : 1;
+  p.dist = ip[9];
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -1038,6 +1087,17 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
     hipLaunchKernelGGL(lw_partition_kernel<false>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
                        (float2*)gh_out);
+  YTK_LAUNCH_CHECK();
+}
+
+// pack (unpack = 0) / unpack (1) the batch message of at most kcap splits (see lw_msg_kernel)
+void ytk_lw_msg(int h, uintptr_t hist, long long slot_elems, uintptr_t msg, int kcap, int unpack, uintptr_t stream) {
+  const LwEngine& e = g_lw.at(h);
+  if (kcap <= 0) return;
+  const long long n = (long long)kcap * (slot_elems + kCurStride);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 256 * 8);
+  hipLaunchKernelGGL(lw_msg_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
+                     slot_elems, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor, (long long*)msg, kcap, unpack);
   YTK_LAUNCH_CHECK();
 }
 

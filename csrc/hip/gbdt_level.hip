@@ -199,11 +199,14 @@ __device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused
   const double mcw2 = (double)p.mcw * 2.0;
   // 0. fused counts: the children of the previous level's splits get their global row
   //    counts from the (now all-reduced) count slots
+  // fused == 2: the counts were accumulated by the fused partition kernel into line-spaced
+  // cursors ((right << 32) | left, kCurStride apart); fused == 1: one word per split
   if (fused) {
     const int nprev = st[ST_N_SPLIT];
+    const size_t cs = fused == 2 ? kCurStride : 1;
     for (int s = tid; s < nprev; s += NT) {
       const DNode& P = b.nodes[b.split_nid[s]];
-      const long long lg = b.left_glob[s] & 0xffffffffll;  // low half: left rows (see partition)
+      const long long lg = b.left_glob[(size_t)s * cs] & 0xffffffffll;  // low half: left rows (see partition)
       b.nodes[P.left].cnt_global = lg;
       b.nodes[P.right].cnt_global = P.cnt_global - lg;
     }
@@ -600,7 +603,7 @@ static LvBufs make_bufs(const uintptr_t* a) {
 extern "C" {
 
 // which: 0 init, 1 plan_split (arg1 = fused: patch the previous level's cnt_global from
-//        left_glob), 3 plan_children(arg0=build_base, arg1=half | ncs<<14 | fused<<29 |
+//        left_glob; 2: line-spaced cursors of the fused partition), 3 plan_children(arg0=build_base, arg1=half | ncs<<14 | fused<<29 |
 //        use_loc<<30; derived slots start at build_base + half + ncs),
 //        4 finalize(arg0=max_nodes)
 void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* fp, int arg0,

@@ -516,6 +516,182 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
   }
 }
 
+// ------------------------------------------------------------------ fused root histogram
+// tree_grad + the NEXT tree's root histogram in one pass (K == 1, uint8 rows of 32 bytes,
+// no row sampling, fixed-point scales fixed before the pass -- the sigmoid gradient bound).
+// The gradient pass already holds every row's 32-byte bin row and produces its (g, h), so
+// the root histogram (HistogramBuilder.java:56-90 over all rows) costs LDS atomics here
+// instead of a second read of the bins and (g, h) (~420 MB per Higgs round).
+//
+// Layout: 1024-thread blocks, one per CU (the exact int64 histogram is 256 bins x [32 g | 32 h]
+// words = 128 KiB of LDS). Each block is FOUR virtual 256-thread blocks of tree_grad_kernel:
+// virtual block vb = 4 blockIdx.x + tid / 256 walks exactly the rows tree_grad_kernel's
+// block vb walks and writes its fp64 loss partial to the same slot, so the loss sums, (g, h),
+// scores and leaf counts are bitwise those of the unfused kernel.
+// Histogram adds: a thread owns a whole row; lane l rotates its row by l % 32 bytes so that
+// at step k the 16 lanes of an ds_add_u64 group update 16 distinct features ((k + l) % 32):
+// word bin * 64 + f (g) / + 32 (h) -> bank pair f % 16, conflict free. Bytes past F are the
+// row padding (bin 0): they land in columns the flush never reads.
+constexpr int kTGHThreads = 1024;
+constexpr int kTGHVirtual = kTGHThreads / 256;
+constexpr size_t kTGHHistBytes = (size_t)256 * 64 * sizeof(unsigned long long);
+
+__device__ __forceinline__ unsigned long long tgh_fx_round(float y) {  // == fx_round (gbdt_hist.hip)
+  const float r = __builtin_rintf(y);
+  const float a = fabsf(r);
+  const float hi = floorf(a * 0x1p-32f);
+  const float lo = __builtin_fmaf(hi, -0x1p32f, a);
+  const unsigned long long u = ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+  const unsigned long long m = r < 0.f ? ~0ull : 0ull;
+  return (u ^ m) - m;
+}
+
+__device__ __forceinline__ void tgh_add_row(const uint32_t (&d)[8], int rot, unsigned long long gi,
+                                            unsigned long long hi, unsigned long long* hsm) {
+  // e = the row rotated by rot / 4 dwords, then r = e shifted by rot % 4 bytes: byte k of r is
+  // byte (k + rot) % 32 of the row
+  const int q = rot >> 2, b = rot & 3;
+  uint32_t e[9];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t x = d[i & 7];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) x = (q == j) ? d[(i + j) & 7] : x;
+    e[i] = x;
+  }
+  e[8] = e[0];
+  uint32_t r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], b);
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const unsigned bin = __builtin_amdgcn_ubfe(r[k >> 2], 8 * (k & 3), 8);
+    const int f = (k + rot) & 31;
+    unsigned long long* p = hsm + (bin * 64 + f);
+    atomicAdd(p, gi);
+    atomicAdd(p + 32, hi);
+  }
+}
+
+template <int kLoss>
+__global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
+    const uint8_t* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
+    const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
+    const float* __restrict__ tval, int nnodes, float* __restrict__ score,
+    const float* __restrict__ init, const float* __restrict__ label,
+    const float* __restrict__ weight, long long N, float p0, float score_div,
+    float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
+    float* __restrict__ ghmax, int* __restrict__ leaf_part, int nvb, const float* __restrict__ scales,
+    long long* __restrict__ staging, int B) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];
+  int* tsm = reinterpret_cast<int*>(hsm + 256 * 64);
+  int* sf = tsm;
+  int* st = tsm + nnodes;
+  int* sl = tsm + 2 * nnodes;
+  int* sr = tsm + 3 * nnodes;
+  float* sv = reinterpret_cast<float*>(tsm + 4 * nnodes);
+  int* sc = tsm + 5 * nnodes;  // leaf_part: rows per node of this block's virtual blocks
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256 * 64; i += kTGHThreads) hsm[i] = 0ull;
+  for (int i = tid; i < nnodes; i += kTGHThreads) {
+    sf[i] = tfeat[i]; st[i] = tthr[i]; sl[i] = tleft[i]; sr[i] = tright[i]; sv[i] = tval[i];
+  }
+  if (leaf_part)
+    for (int i = tid; i < kTGHVirtual * nnodes; i += kTGHThreads) sc[i] = 0;
+  __syncthreads();
+  const float sg = scales[0], sh = scales[1];
+  const int vsub = tid >> 8;
+  const int vb = blockIdx.x * kTGHVirtual + vsub;
+  const int rot = tid & 31;
+  int* scv = sc + vsub * nnodes;
+  double lsum = 0.0, wsum = 0.0;
+  float mg = 0.f, mh = 0.f;
+  if (vb < nvb) {
+    const long long G = (long long)nvb * 256;
+    long long r0 = (long long)vb * 256 + (tid & 255);
+    auto finish_row = [&](long long r, const uint32_t (&d)[8], float s, int n, float ini, float lab, float w) {
+      s += sv[n];
+      score[r] = s;
+      if (leaf_part) atomicAdd(&scv[n], 1);
+      const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+      lsum += (double)w * o.l;
+      wsum += (double)w;
+      if (pred) pred[r] = o.p;
+      const float gg = (float)(o.g * (double)w), hh = (float)(o.h * (double)w);
+      gh[r] = make_float2(gg, hh);
+      mg = fmaxf(mg, fabsf(gg));
+      mh = fmaxf(mh, fabsf(hh));
+      tgh_add_row(d, rot, tgh_fx_round(gg * sg), tgh_fx_round(hh * sh), hsm);
+    };
+    constexpr int U = kTreeGradRows;
+    for (; r0 + (U - 1) * G < N; r0 += U * G) {
+      uint32_t d[U][8];
+      float sc0[U], in0[U], lb0[U], wt0[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long r = r0 + u * G;
+        load_row_regs<8>(bins + r * stride, d[u]);
+        sc0[u] = score[r];
+        in0[u] = init[r];
+        lb0[u] = label[r];
+        wt0[u] = weight ? weight[r] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        finish_row(r0 + u * G, d[u], sc0[u], walk_regs<uint8_t, 8>(d[u], sf, st, sl, sr), in0[u], lb0[u], wt0[u]);
+    }
+    for (long long r = r0; r < N; r += G) {
+      uint32_t d[8];
+      load_row_regs<8>(bins + r * stride, d);
+      const float w = weight ? weight[r] : 1.f;
+      finish_row(r, d, score[r], walk_regs<uint8_t, 8>(d, sf, st, sl, sr), init[r], label[r], w);
+    }
+  }
+  // per virtual block: the fp64 partials in tree_grad_kernel's order (wave sums, then the
+  // virtual block's 4 waves left to right), in its partial slot
+  {
+    __shared__ double s_loss[kTGHThreads / 64], s_w[kTGHThreads / 64];
+    __shared__ float s_mg[kTGHThreads / 64], s_mh[kTGHThreads / 64];
+    lsum = wave_sum(lsum);
+    wsum = wave_sum(wsum);
+    mg = wave_maxf(mg);
+    mh = wave_maxf(mh);
+    const int wid = tid >> 6;
+    if (lane_id() == 0) { s_loss[wid] = lsum; s_w[wid] = wsum; s_mg[wid] = mg; s_mh[wid] = mh; }
+    __syncthreads();
+    if (tid < kTGHVirtual) {
+      const int v = blockIdx.x * kTGHVirtual + tid;
+      if (v < nvb) {
+        double* part = loss_acc + kAccPart;
+        const double* a = s_loss + 4 * tid;
+        const double* c = s_w + 4 * tid;
+        part[2 * v] = a[0] + a[1] + a[2] + a[3];
+        part[2 * v + 1] = c[0] + c[1] + c[2] + c[3];
+      }
+    }
+    if (tid == 0 && ghmax) {
+      float x = 0.f, y = 0.f;
+      for (int i = 0; i < kTGHThreads / 64; ++i) { x = fmaxf(x, s_mg[i]); y = fmaxf(y, s_mh[i]); }
+      atomicMax(reinterpret_cast<unsigned*>(&ghmax[0]), __float_as_uint(x));
+      atomicMax(reinterpret_cast<unsigned*>(&ghmax[1]), __float_as_uint(y));
+    }
+  }
+  __syncthreads();
+  if (leaf_part) {
+    for (int i = tid; i < kTGHVirtual * nnodes; i += kTGHThreads) {
+      const int v = blockIdx.x * kTGHVirtual + i / nnodes;
+      if (v < nvb) leaf_part[(size_t)v * nnodes + (i % nnodes)] = sc[i];
+    }
+  }
+  // the block's histogram partial -> staging item blockIdx.x (hist_reduce_kernel layout:
+  // entry bin * 32 + f, one (g, h) pair each; split-K reduced into the root slot)
+  longlong2* stg = reinterpret_cast<longlong2*>(staging) + (size_t)blockIdx.x * B * 32;
+  for (int i = tid; i < B * 32; i += kTGHThreads) {
+    const int bin = i >> 5, f = i & 31;
+    stg[i] = make_longlong2((long long)hsm[bin * 64 + f], (long long)hsm[bin * 64 + 32 + f]);
+  }
+}
+
 // out[node] = rows of the tree's node over all tree_grad blocks (one block per node, block
 // order sums: deterministic), as doubles next to the round's loss sums
 __global__ __launch_bounds__(256) void leaf_count_reduce_kernel(const int* __restrict__ part, int nblocks, int nnodes,
@@ -848,6 +1024,56 @@ int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfe
   YTK_LAUNCH_CHECK();
   return 1;
 }
+
+void ytk_hist_reduce(uintptr_t staging, uintptr_t work, int nwork, uintptr_t hist, int B, int F, int slot_base,
+                     int nslots, uintptr_t stream);
+
+// Fused score/gradient pass + next root histogram (tree_grad_hist_kernel). Returns 0 (nothing
+// launched) when the layout does not qualify; the caller then runs ytk_tree_grad and the
+// root histogram separately. root_slot: the histogram slot to accumulate into (must be
+// zero); staging: >= ceil(grid) * B * 32 * 16 bytes; work: >= grid int4 zeros.
+int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintptr_t tthr, uintptr_t tleft,
+                       uintptr_t tright, uintptr_t tval, int nnodes, uintptr_t score, uintptr_t init, uintptr_t label,
+                       uintptr_t weight, long long N, int loss_id, float p0, float score_div, uintptr_t pred,
+                       uintptr_t gh, uintptr_t loss_acc, uintptr_t ghmax, uintptr_t leaf_part, uintptr_t leaf_out,
+                       uintptr_t scales, uintptr_t staging, uintptr_t work, uintptr_t root_slot, int B, int F,
+                       uintptr_t stream) {
+  if (N <= 0 || nnodes <= 0) return 0;
+  if (stride != 32 || (bins % 16) != 0 || B > 256 || F > 32 || loss_id < 0 || loss_id > 4) return 0;
+  const size_t lds = kTGHHistBytes + (size_t)nnodes * 5 * sizeof(int) +
+                     (leaf_part ? (size_t)kTGHVirtual * nnodes * sizeof(int) : 0);
+  if (lds > kLdsBudget) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nvb = grid_for(N, 256 * 8);  // tree_grad_kernel's grid: the virtual blocks
+  const int grid = (nvb + kTGHVirtual - 1) / kTGHVirtual;
+#define YTK_TGH(LID)                                                                                          \
+  hipLaunchKernelGGL((tree_grad_hist_kernel<LID>), dim3(grid), dim3(kTGHThreads), lds, s, (const uint8_t*)bins,  \
+                     stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft, (const int*)tright,         \
+                     (const float*)tval, nnodes, (float*)score, (const float*)init, (const float*)label,         \
+                     (const float*)weight, N, p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc,       \
+                     (float*)ghmax, (int*)leaf_part, nvb, (const float*)scales, (long long*)staging, B)
+  switch (loss_id) {
+    case 0: YTK_TGH(0); break;
+    case 1: YTK_TGH(1); break;
+    case 2: YTK_TGH(2); break;
+    case 3: YTK_TGH(3); break;
+    default: YTK_TGH(4); break;
+  }
+#undef YTK_TGH
+  YTK_LAUNCH_CHECK();
+  if (leaf_part) {
+    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + 1), dim3(256), 0, s, (const int*)leaf_part, nvb,
+                       nnodes, (double*)leaf_out, (double*)loss_acc);
+  } else {
+    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, nvb);
+  }
+  YTK_LAUNCH_CHECK();
+  ytk_hist_reduce(staging, work, grid, root_slot, B, F, 0, 1, stream);
+  return 1;
+}
+
+// blocks of tree_grad_hist (staging items of its root histogram)
+int ytk_tree_grad_hist_grid(long long N) { return (grid_for(N, 256 * 8) + kTGHVirtual - 1) / kTGHVirtual; }
 
 // tree_grad launches min(ceil(N / 256), 2048) blocks: the leaf_part scratch size
 int ytk_tree_grad_grid(long long N) { return grid_for(N, 256 * 8); }

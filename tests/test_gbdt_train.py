@@ -145,7 +145,8 @@ def test_device_builder_matches_host_builder(cuda, kw):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_PART_CHUNK": "1024"}, {"YTK_FUSE_SPLIT_PLAN": "1"}, {"YTK_PART_PREFETCH": "0"}, {"YTK_PART_PREFETCH": "1"}, {"YTK_PART_PREFETCH": "3"},
                                  {"YTK_SPLIT_GROUPS": "1"}, {"YTK_SPLIT_GROUPS": "3"}, {"YTK_REDUCE_SPLIT": "8"},
-                                 {"YTK_FUSED_TEST_TAIL": "0"}, {"YTK_TG_LDS_WALK": "0"},
+                                 {"YTK_FUSED_TEST_TAIL": "0"}, {"YTK_TG_LDS_WALK": "0"}, {"YTK_FUSE_ROOT_HIST": "0"},
+                                 {"YTK_FUSE_ROOT_HIST": "0", "YTK_DEFER_LEAF_COUNTS": "0"},
                                  {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused

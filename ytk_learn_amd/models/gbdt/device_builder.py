@@ -113,22 +113,35 @@ class DeviceLevelBuilder:
         # ~N/2048 resident blocks instead of ~10 serial reservations per block
         # (the kernel holds one chunk of <= 2048 rows per block in registers)
         self.part_atomic = os.environ.get("YTK_PART_ATOMIC", "1") != "0" and self.MIN_ROWS == 2048
-        # one GPU, uint8 bins: the children planner runs in the partition kernel's last block
-        # (YTK_FUSE_PART_CHILDREN=0: separate launches)
-        self.fuse_part_children = (self.part_atomic and not self.comm.is_dist and bins.dtype == torch.uint8
+        # Multi-GPU with fused counts: the partition kernel accumulates the level's per-split
+        # row counts straight into count slots that ride in the level's histogram message,
+        # so ONE all-reduce of [built slots + count slots] carries the histograms and the
+        # counts of the level (reference: DataParallelTreeMaker.java:518,538 count allreduce +
+        # HistogramBuilder.java:95 reduce-scatter -> one fixed-size RCCL call).
+        self.fuse_counts = (self.comm.is_dist and p.min_split_samples <= 0
+                            and os.environ.get("YTK_FUSE_COUNTS", "1") != "0")
+        # uint8 bins: the children planner runs in the partition kernel's last block
+        # (YTK_FUSE_PART_CHILDREN=0: separate launches). Multi-GPU only with fused counts: the
+        # children are planned from the LOCAL counts (the smaller child by the globally
+        # identical hessian sums) and the next level's planner patches the global counts
+        # from the all-reduced cursors.
+        self.fuse_part_children = (self.part_atomic and bins.dtype == torch.uint8
+                                   and (not self.comm.is_dist or self.fuse_counts)
                                    and os.environ.get("YTK_FUSE_PART_CHILDREN", "1") != "0")
         # rows per partition chunk (= per cursor reservation): 8 rows per thread (2048);
         # YTK_PART_CHUNK=4096 runs the fused kernel at 16 rows per thread -- half the
         # reservations on the top levels' few cursors, but 4 instead of 8 waves/SIMD.
         # Measured (profiles/r2_partition_chunk.md): root level 105 -> 100 us, deep levels
         # 93 -> 100 us, tree 1.50 ms either way
-        self.part_chunk = (int(os.environ.get("YTK_PART_CHUNK", "2048")) if self.fuse_part_children
-                           else self.MIN_ROWS)
+        # (multi-GPU: the last level runs the standalone 2048-row partition, so the chunk stays
+        # at 2048 for every level)
+        self.part_chunk = (int(os.environ.get("YTK_PART_CHUNK", "2048"))
+                           if self.fuse_part_children and not self.comm.is_dist else self.MIN_ROWS)
         self.part_target = (-(-self.N // self.part_chunk) + 1) if self.part_atomic else self.PART_TARGET
         # one GPU: split search + next level's split planning in one launch (YTK_FUSE_SPLIT_PLAN=1).
         # Off by default: the release/acquire fences it needs cost what the saved launch
         # saved (measured 24.2 -> 25.0 us per level, profiles/r2_split_plan_fusion.md)
-        self.fuse_split_plan = (self.fuse_part_children and not self.wide
+        self.fuse_split_plan = (self.fuse_part_children and not self.wide and not self.comm.is_dist
                                 and os.environ.get("YTK_FUSE_SPLIT_PLAN", "0") == "1")
         self.max_items = max(self.hist_target, self.part_target) + self.maxp + 16
         dev = self.dev
@@ -170,15 +183,11 @@ class DeviceLevelBuilder:
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
         # Histogram slots. Level c (children at depth c, 1 <= c < D) owns `half = 2^(c-1)`
         # built slots, then `ncs` count slots, then `half` derived slots; the root is slot 0.
-        # Multi-GPU with fused counts: the partition kernel accumulates the level's per-split
-        # left-row counts straight into the count slots, so ONE all-reduce of
-        # [built slots + count slots] carries the histograms and the counts of the level
-        # (reference: DataParallelTreeMaker.java:518,538 count allreduce + HistogramBuilder
-        # .java:95 reduce-scatter -> one fixed-size RCCL call).
-        self.fuse_counts = (self.comm.is_dist and p.min_split_samples <= 0
-                            and os.environ.get("YTK_FUSE_COUNTS", "1") != "0")
+        # The fused partition kernel's cursors sit a cache line apart (CUR_STRIDE words per
+        # split) followed by its self-resetting done counters, all inside the count slots.
         slot_elems = B * F * 2
-        self.ncs = -(-self.maxp // slot_elems) if self.fuse_counts else 0
+        cnt_words = (self.maxp * CUR_STRIDE + DONE_WORDS) if self.fuse_part_children else self.maxp
+        self.ncs = -(-cnt_words // slot_elems) if self.fuse_counts else 0
         self.level_slots = {}
         nxt = 1
         for c in range(1, D):
@@ -195,6 +204,7 @@ class DeviceLevelBuilder:
             self.own = self.fblocks[self.comm.rank]
             self.split_local = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
             self._own_cache = {}
+            self._pack = None
         self._slot_bytes = slot_elems * 8
         self._root_fixed = False
         # staged histogram flush: block partials to a staging slab with plain stores, then a
@@ -230,6 +240,12 @@ class DeviceLevelBuilder:
         # count all-reduce -- its children are leaves, and only their sample counts were
         # still missing
         self.defer_leaf_counts = False
+        # set by the trainer when its K == 1 gradient pass also builds the NEXT tree's root
+        # histogram (tree_grad_hist): the root slot then arrives pre-built (root_ready) and
+        # is zeroed again at the end of every tree for the next pass to accumulate into
+        self.fuse_root = False
+        self.root_ready = False
+        self._root_bufs = None
         self.last_keep = None
         self.total_stats = TimeStats()
         self._fmask_cache = {}
@@ -280,25 +296,23 @@ class DeviceLevelBuilder:
     def _owner_reduce(self, base: int, nslots: int, ncs: int = 0):
         """Reduce-scatter slots [base, base + nslots) by feature block (+ the ncs count slots
         that follow them, replicated into every block so every rank gets their sums)."""
-        P, fr, B = self.comm.world, self.fr, self.B
-        built = self.hist[base:base + nslots]
+        P, fr, B, F = self.comm.world, self.fr, self.B, self.F
         nb_el = nslots * B * fr * 2
-        cnt = self.hist[base + nslots:base + nslots + ncs].reshape(-1) if ncs else None
-        C = cnt.numel() if cnt is not None else 0
-        x = torch.zeros((P, nb_el + C), dtype=torch.int64, device=self.dev)
-        xb = x[:, :nb_el].view(P, nslots, B, fr, 2)
-        for r, (lo, hi) in enumerate(self.fblocks):
-            if hi > lo:
-                xb[r, :, :, :hi - lo] = built[:, :, lo:hi]
-        if C:
-            x[:, nb_el:] = cnt
-        out = torch.empty(nb_el + C, dtype=torch.int64, device=self.dev)
+        C = ncs * B * F * 2
+        # persistent pack / result buffers sized for the largest level (no per-level alloc)
+        need = P * (nb_el + C)
+        if self._pack is None or self._pack.numel() < need:
+            self._pack = torch.empty(need, dtype=torch.int64, device=self.dev)
+            self._pack_out = torch.empty(need // P, dtype=torch.int64, device=self.dev)
+        x = self._pack[:need].view(P, nb_el + C)
+        out = self._pack_out[:nb_el + C]
+        s = stream(self.bins)
+        h = hip()
+        slot_ptr = ptr(self.hist) + base * self._slot_bytes
+        cnt_ptr = slot_ptr + nslots * self._slot_bytes if C else 0
+        h.owner_pack(slot_ptr, ptr(x), nslots, B, F, fr, P, cnt_ptr, C, s)  # one launch
         self.comm.reduce_scatter_(out, x)
-        lo, hi = self.own
-        if hi > lo:
-            built[:, :, lo:hi] = out[:nb_el].view(nslots, B, fr, 2)[:, :, :hi - lo]
-        if C:
-            cnt.copy_(out[nb_el:])
+        h.owner_unpack(ptr(out), slot_ptr, nslots, B, F, fr, self.comm.rank, cnt_ptr, C, s)
 
     def _owner_fmask(self, fmask_np: np.ndarray):
         """(owned sampled-feature mask on the device, its first feature, totals rank)."""
@@ -451,7 +465,13 @@ class DeviceLevelBuilder:
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
 
-        build_hist(gh0, rows0, self.hist_target + 1, 0, 1)
+        if self.root_ready and not sampled:
+            # the root histogram came with the previous round's gradient pass
+            if self._zero_all:
+                self.hist[1:].zero_()
+        else:
+            build_hist(gh0, rows0, self.hist_target + 1, 0, 1)
+        self.root_ready = False
         tm.mark("build_hist_compute")
         if dist:
             if self.owner:
@@ -477,7 +497,9 @@ class DeviceLevelBuilder:
                                   glob=self._count_ptr(d) if d >= 1 else None)
             # apply splits + pop depth d (arg0 = 1: the single-pass partition needs no work list)
             if not self.fuse_split_plan:  # else: planned by the previous split launch
-                h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, 1 if (fused and d >= 1) else 0, s)
+                # the previous level's counts: line-spaced cursors when its partition was fused
+                patch = (2 if self.fuse_part_children else 1) if (fused and d >= 1) else 0
+                h.lv_step(1, ptrs, ip, fp, 1 if self.part_atomic else 0, patch, s)
             tm.mark("plan")
             if last and self.defer_leaf_counts and not sampled:
                 # children planning with zero cursors: the leaves' sample counts are placeholders
@@ -495,11 +517,14 @@ class DeviceLevelBuilder:
             else:
                 base, cbase, dbase = self.level_slots[c]
                 ncs = dbase - cbase
-            if self.fuse_part_children:
-                # one GPU: partition + children planning in one launch (last block plans)
+            # partition + children planning in one launch (last block plans); multi-GPU: not on
+            # the last level, whose counts need their own all-reduce before the planning
+            fused_part = self.fuse_part_children and not (dist and last)
+            if fused_part:
                 h.lv_partition_children(ptrs, ip, fp, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in,
                                         ptr(self.rows_tmp), ptr(self.gh_tmp), npart, 1 if last else 0, base,
-                                        half | (ncs << 14) | (1 << 30), self.maxp, s)
+                                        half | (ncs << 14) | ((1 if fused else 0) << 29) | (1 << 30),
+                                        self.maxp, s)
                 tm.mark("partition")
             # the flag kernel also accumulates the per-split left totals into left_loc
             elif self.part_atomic:
@@ -519,7 +544,7 @@ class DeviceLevelBuilder:
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
                             lloc, s)
-            if not self.fuse_part_children:
+            if not fused_part:
                 tm.mark("partition")
                 lvl_fused = fused and not last
                 if dist and not lvl_fused:
@@ -568,11 +593,27 @@ class DeviceLevelBuilder:
                 self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
             tm.mark("find_best_split")
         h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
+        if self.fuse_root:
+            self.hist[0].zero_()  # the next gradient pass accumulates the next root here
         tm.mark("plan")
         self.tree_count += 1
         snap = self.snap.clone() if self.snapshot_copy else self.snap
         st, nodes, *arrays = self._snap_views(snap)
         return DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+
+    def root_target(self):
+        """Arguments of the fused gradient + root histogram pass (gops.tree_grad root=)."""
+        if self._root_bufs is None:
+            grid = hip().tree_grad_hist_grid(self.N)
+            self._root_bufs = (torch.empty(grid * 256 * 32 * 2, dtype=torch.int64, device=self.dev),
+                               torch.zeros(4 * grid, dtype=torch.int32, device=self.dev))
+        stg, work = self._root_bufs
+        return {"slot": ptr(self.hist), "scales": ptr(self.scales), "staging": ptr(stg), "work": ptr(work),
+                "B": self.B, "F": self.F}
+
+    def live_tree_views(self):
+        """(node table, leaf-value array) the engine's raw_tree / next snapshot read."""
+        return self.nodes, self.tval
 
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (for test-set scoring), one forest entry."""

@@ -66,7 +66,7 @@ class DeviceLeafBuilder:
         ml = p.max_leaf_cnt
         self.max_leaf = ml
         self.max_nodes = 2 * ml - 1
-        self.cap = int(min(8 * ml + 64, LW_CAP_MAX))
+        self.cap = self.slots_needed(p)
         dev = self.dev
         i32 = lambda n: torch.zeros(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
         mn = self.max_nodes
@@ -110,7 +110,9 @@ class DeviceLeafBuilder:
         self.max_pblocks = -(-N // PART_CHUNK) + ml + 1
         # done flag: the planner writes it straight into pinned host memory (no copy launch)
         self._done_host = torch.zeros(16, dtype=torch.int32).pin_memory()
-        self._dh_np = self._done_host.numpy()  # [0] done flag, [1] batches planned (written by lw_plan)
+        # [0] done flag, [1] batches planned, [2] split count of the last planned batch
+        # (written by lw_plan)
+        self._dh_np = self._done_host.numpy()
         self.idle_hook = None  # called once per tree while the host waits on the planner
         self._done_dev = hip().host_device_ptr(self._done_host.data_ptr())
         self.tree_count = 0
@@ -125,16 +127,29 @@ class DeviceLeafBuilder:
                      if os.environ.get("YTK_LW_PROF") == "1" else None)
         self._handle = hip().lw_create(self._ptrs(), self._ip(), self._fp())
         self._ghmax_buf = None
+        # multi-GPU: one message per batch = its built slots + its split cursors (lw_msg)
+        self.slot_elems = B * F * 2
+        self.msg = (torch.empty(ml * (self.slot_elems + CUR_STRIDE), dtype=torch.int64, device=dev)
+                    if self.comm.is_dist else None)
+        self._root_glob = None
 
     # ------------------------------------------------------------------ setup
     @staticmethod
+    def slots_needed(params: TreeParams) -> int:
+        """Histogram slots the engine allocates (one per speculative node, never evicted)."""
+        return int(min(8 * max(params.max_leaf_cnt, 2) + 64, LW_CAP_MAX))
+
+    @staticmethod
     def supports(bins: torch.Tensor, binsT: Optional[torch.Tensor], B: int, F: int, params: TreeParams,
                  comm: Optional[Comm] = None) -> bool:
-        """uint8 row-major bins (B <= 256, 32-aligned stride), a column-major binsT, one
-        rank, 2 <= max_leaf_cnt <= 512 (the planner's LDS-resident queue)."""
+        """uint8 row-major bins (B <= 256, 32-aligned stride), a column-major binsT,
+        2 <= max_leaf_cnt <= 512 (the planner's LDS-resident queue). Multi-GPU: needs
+        min_split_samples <= 0 (the children's global counts arrive with the batch's
+        all-reduce, after the children planning)."""
         if os.environ.get("YTK_DEVICE_LEAFWISE", "1") == "0":
             return False
-        if comm is not None and comm.is_dist:
+        if comm is not None and comm.is_dist and (params.min_split_samples > 0
+                                                  or os.environ.get("YTK_DEVICE_LEAFWISE_DIST", "1") == "0"):
             return False
         if params.grow_policy != "loss" or not (2 <= params.max_leaf_cnt <= LW_LEAF_MAX):
             return False
@@ -164,7 +179,7 @@ class DeviceLeafBuilder:
         # budget the batch choice ranks within (100 = the host planner's virtual replay)
         spec = int(os.environ.get("YTK_LW_SPEC_PCT", "100")) if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
         return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
-                self.cap, self.N, self.split_groups]
+                self.cap, self.N, self.split_groups, 1 if self.comm.is_dist else 0]
 
     def _ptrs(self):
         f, i = self.nd_f64, self.nd_i32
@@ -202,6 +217,10 @@ class DeviceLeafBuilder:
 
     # ------------------------------------------------------------------ build
     def _hist_split(self, h, rows_ptr, gh_ptr, fmask, f0, s):
+        self._hist(h, rows_ptr, gh_ptr, s)
+        self._split(h, fmask, f0, s)
+
+    def _hist(self, h, rows_ptr, gh_ptr, s):
         st = ptr(self.st)
         # sole-item slots are stored by the hist kernel, <= 16-item slots by the reduce, larger
         # ones zeroed by their first hist item and reduced split-K
@@ -209,6 +228,9 @@ class DeviceLeafBuilder:
                              self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
                              self.REDUCE_Y, s)
+
+    def _split(self, h, fmask, f0, s):
+        st = ptr(self.st)
         gp = self.gp
         if self.split_groups > 1:
             if not h.split_node_grouped(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
@@ -233,6 +255,7 @@ class DeviceLeafBuilder:
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))
         sampled = p.instance_sample_rate < 1.0
+        dist = self.comm.is_dist
         assert gh.is_contiguous() and gh.shape == (self.N, 2)
         if sampled:  # sampled rows first (stable), in the first half of the ping-pong buffers
             g = torch.Generator(device=self.dev)
@@ -243,15 +266,26 @@ class DeviceLeafBuilder:
             self.gh2[:self.N].copy_(gh.index_select(0, order))
             self.root_cnt[0] = keep.sum()
             self.root_cnt[1] = self.root_cnt[0]
+            if dist:
+                self.comm.allreduce_(self.root_cnt[1:2])
             self.last_keep = keep
             rows0, gh0 = ptr(self.rows2), ptr(self.gh2)
             mx = ghmax if (ghmax is not None and ghmax_global) else (gh.abs() * keep[:, None]).amax(dim=0)
         else:
             self.last_keep = None
-            self.root_cnt[0] = self.N
-            self.root_cnt[1] = self.N
+            if self._root_glob is None:  # (local, global) rows: constants of an unsampled run
+                self.root_cnt[0] = self.N
+                self.root_cnt[1] = self.N
+                if dist:
+                    self.comm.allreduce_(self.root_cnt[1:2])
+                self._root_glob = True
             rows0, gh0 = 0, ptr(gh)
             mx = ghmax if ghmax is not None else gh.abs().amax(dim=0)
+        if sampled:
+            self._root_glob = None
+        if dist and not ghmax_global:
+            mx = mx.clone()
+            self.comm.allreduce_(mx, op="max")
         fmask, f0 = self._fmask(rng)
         h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
         tm = self.timer
@@ -261,7 +295,15 @@ class DeviceLeafBuilder:
         # kernel writes the flag while it is reset
         self._done_host[0] = 0
         self._done_host[1] = 0
+        self._done_host[2] = 0
         h.lw_step(hd, 0, s)
+        if dist:
+            self._hist(h, rows0, gh0, s)
+            self.comm.allreduce_(self.hist[0:1])  # the root slot
+            self._split(h, fmask, f0, s)
+            tm.mark("root")
+            it = self._build_dist(h, hd, rows0, gh0, fmask, f0, s)
+            return self._finish(h, s, it)
         self._hist_split(h, rows0, gh0, fmask, f0, s)
         tm.mark("root")
         # Launch throttle without events (a recorded event put a ~6 us gap before every
@@ -295,7 +337,50 @@ class DeviceLeafBuilder:
                 break
         if idle is not None:
             idle()
-        tm.mark("batches")
+        return self._finish(h, s, it)
+
+    def _build_dist(self, h, hd, rows0, gh0, fmask, f0, s) -> int:
+        """Multi-GPU batch loop: plan -> partition (+ children planning) -> histograms are
+        enqueued; the host then waits for THIS batch's planner (pinned progress words, no
+        event) to learn its split count k, packs the built slots + split cursors into one
+        message (device pack), all-reduces it (one fixed-size collective per batch), unpacks
+        and runs the split search. Every rank's planner takes identical decisions from the
+        identical all-reduced histograms; the next planner patches the children's global
+        row counts from the reduced cursors."""
+        dh = self._dh_np
+        idle = self.idle_hook
+        it = 0
+        while True:
+            h.lw_step(hd, 1, s)
+            h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows0 if it == 0 else ptr(self.rows2),
+                           gh0 if it == 0 else ptr(self.gh2), ptr(self.rows2), ptr(self.gh2), self.max_pblocks, s)
+            self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
+            it += 1
+            if it > 4 * self.max_leaf + 8:
+                raise RuntimeError("device leaf-wise builder did not terminate")
+            if dh[1] < it and dh[0] == 0:
+                if idle is not None:
+                    idle()
+                    idle = None
+                t_wait = time.perf_counter()
+                while dh[1] < it and dh[0] == 0:
+                    if time.perf_counter() - t_wait > self.POLL_TIMEOUT_S:
+                        raise RuntimeError(f"device leaf-wise builder: no planner progress for {self.POLL_TIMEOUT_S} s "
+                                           f"(batch {it}, planned {int(dh[1])})")
+            if dh[1] < it:  # this planner found nothing to split: the tree is complete
+                break
+            k = int(dh[2])
+            n = k * (self.slot_elems + CUR_STRIDE)
+            h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 0, s)
+            self.comm.allreduce_(self.msg[:n])
+            h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 1, s)
+            self._split(h, fmask, f0, s)
+        if idle is not None:
+            idle()
+        return it
+
+    def _finish(self, h, s, it) -> DeviceTree:
+        self.timer.mark("batches")
         h.lv_step(4, self._lv_ptrs(), [0] * 8, [0.0] * 6, self.max_nodes, 0, s)
         self.tree_count += 1
         self.last_batches = it
@@ -329,6 +414,10 @@ class DeviceLeafBuilder:
         """(batches, expanded nodes, overflow flag) of the last tree (synchronises)."""
         st = self.st.cpu().numpy()
         return int(st[LW_BATCHES]), int(st[LW_EXPANDED]), int(st[LW_OVERFLOW])
+
+    def live_tree_views(self):
+        """(node table, leaf-value array) the engine's raw_tree reads."""
+        return self.tnodes, self.tval
 
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (test-set scoring)."""

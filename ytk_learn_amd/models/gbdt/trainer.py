@@ -149,12 +149,24 @@ class GBDTTrainer:
             [[0], np.cumsum([len(c) for c in self.mapper.cands])]).astype(np.int32)).to(self.dev)
         self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
         tp = self.p.tree
+        # histogram_pool_capacity (MB, DataParallelTreeMaker.java:192-204): the GPU engines keep
+        # every histogram slot of a tree resident (no eviction); when the configured pool is
+        # smaller than that slab the run goes to the host-driven builder, whose LRU pool honours
+        # the cap (HistogramPool.java:36-273)
+        pool_mb = self.p.histogram_pool_capacity
+        slot_bytes = self.B * self.F * 16
+
+        def fits_pool(n_slots: int) -> bool:
+            return pool_mb is None or pool_mb <= 0 or n_slots * slot_bytes <= pool_mb * (1 << 20)
+
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
-                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and self.refiner is None
+                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE
+                                   and fits_pool(1 << max(tp.max_depth, 1))
                                    and DeviceLevelBuilder.supports(self.bins, self.binsT, self.B, self.F))
         # leaf-wise (the reference's Higgs configuration): GPU-resident queue replay
         use_leaf = (not self.use_device_builder and self.p.device_builder and self.dev.type == "cuda"
-                    and tp.grow_policy == "loss" and self.refiner is None
+                    and tp.grow_policy == "loss"
+                    and fits_pool(DeviceLeafBuilder.slots_needed(tp))
                     and DeviceLeafBuilder.supports(self.bins, self.binsT, self.B, self.F, tp, self.comm))
         if use_leaf:
             self.use_device_builder = True
@@ -170,6 +182,7 @@ class GBDTTrainer:
             # level skips its counting partition (and, multi-GPU, the count all-reduce: the
             # counts ride in the round's loss all-reduce)
             self.builder.snapshot_copy = self.K != 1
+            self._fuse_root_pending = True  # decided once the gradient bound is known (below)
             self.builder.defer_leaf_counts = (self.K == 1 and self.kernel_loss is not None
                                               and self.kernel_loss != "softmax"
                                               and gops.leaf_counts_fit(self.builder.max_nodes)
@@ -199,6 +212,17 @@ class GBDTTrainer:
             zmax = float(self.p.sigmoid_zmax)
             hb = max(0.25, 1.0 / zmax) if zmax > 0 else 0.25
             self.ghmax_fixed = torch.tensor([wmax, wmax * hb], dtype=torch.float32, device=self.dev)
+        if getattr(self, "_fuse_root_pending", False):
+            # the K == 1 gradient pass also builds the next tree's root histogram: needs the
+            # fixed-point scales fixed before the pass (the sigmoid bound), every row in the
+            # root (no row sampling) and the 32-byte uint8 rows of the 32-feature LDS histogram
+            b = self.builder
+            b.fuse_root = (self.ghmax_fixed is not None and self.K == 1 and tp.instance_sample_rate >= 1.0
+                           and self.refiner is None and not b.wide and b.staged
+                           and self.bins.dtype == torch.uint8 and self.bins.stride(0) == 32
+                           and self.F <= 32 and self.B <= 256
+                           and os.environ.get("YTK_FUSE_ROOT_HIST", "1") != "0")
+            self._fuse_root_pending = False
         if self.test_data is not None:
             te = self.test_data
             self.Xte = torch.where(torch.isnan(te.X), self.fill_dev[None, :], te.X).contiguous()
@@ -439,6 +463,10 @@ class GBDTTrainer:
                     dt = self.builder.build(self.gh[k], self.ghmax_fixed, ghmax_global=True)
                 else:
                     dt = self.builder.build(self.gh[k], self.ghmax[k])
+                if self.refiner is not None:  # l1: leaf values -> weighted residual medians, on device
+                    self.refiner.refine_device(dt, self.builder, self.y[:, k],
+                                               self.score[:, k] / self._score_div(i) + self.init_score[:, k], self.w,
+                                               lr)
                 dev_trees.append(dt)
                 arrays.append(dt.bin_arrays)
                 if self.test_data is not None:
@@ -464,9 +492,12 @@ class GBDTTrainer:
             lc = None
             if dev_trees and getattr(self.builder, "defer_leaf_counts", False) and self.builder.last_keep is None:
                 lc = torch.empty(arrays[0][0].shape[0], dtype=torch.float64, device=self.dev)
+            root = self.builder.root_target() if (dev_trees and getattr(self.builder, "fuse_root", False)) else None
             acc = gops.tree_grad(self.bins, arrays[0], self.score, self.init_score, self.y, self.w,
                                  self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0],
-                                 True, self.ghmax[0] if need_max else None, leaf_counts=lc)
+                                 True, self.ghmax[0] if need_max else None, leaf_counts=lc, root=root)
+            if root is not None:
+                self.builder.root_ready = root["done"]
             if lc is not None:
                 dev_trees[0].leaf_counts = lc
         else:

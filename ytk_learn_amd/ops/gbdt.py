@@ -613,12 +613,16 @@ def leaf_counts_fit(max_nodes: int) -> bool:
 
 
 def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
-              want_grad=True, ghmax=None, leaf_counts=None):
+              want_grad=True, ghmax=None, leaf_counts=None, root=None):
     """Fused K==1 round tail: score += tree(row) (bin space, ROW-MAJOR bins [N, S]), then
     pred (optional) / (g, h) / loss sums / max|g|,|h| (optional ``ghmax`` [1,2]).
     ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum).
     ``leaf_counts`` (optional, float64 [nodes], GPU): rows per tree node from the same walk
-    (the level engine's last-level leaf counts without a counting partition pass)."""
+    (the level engine's last-level leaf counts without a counting partition pass).
+    ``root`` (optional dict, GPU): also accumulate the NEXT tree's root histogram in the same
+    pass (tree_grad_hist_kernel) into the zeroed slot ``root["slot"]`` with the fixed-point
+    scales ``root["scales"]``; ``root["done"]`` reports whether the fused pass ran (layouts it
+    does not cover fall back to the plain pass)."""
     loss_id = LOSS_IDS[loss]
     assert loss_id != 5 and score.shape[1] == 1
     if score.is_cuda:
@@ -636,6 +640,17 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
         if leaf_counts is not None:
             assert nn > 0 and leaf_counts.dtype == torch.float64 and leaf_counts.numel() >= nn
             part = torch.empty(hip().tree_grad_grid(N) * nn, dtype=torch.int32, device=score.device)
+        if root is not None:
+            root["done"] = False
+            if (tree_arrays is not None and want_grad and bins.dtype == torch.uint8 and bins.stride(0) == 32
+                    and nn > 0):
+                root["done"] = bool(hip().tree_grad_hist(
+                    ptr(bins), bins.stride(0), ptr(tf), ptr(tt), ptr(tl), ptr(tr), ptr(tv), nn, ptr(score), ptr(init),
+                    ptr(label), ptr(weight), N, loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
+                    ptr(ghmax), ptr(part), ptr(leaf_counts), root["scales"], root["staging"], root["work"],
+                    root["slot"], root["B"], root["F"], stream(score)))
+            if root["done"]:
+                return acc[:2]
         ok = hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
                         bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
                         ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
