@@ -2,11 +2,12 @@
 """Summarise a rocprofv3 kernel-trace CSV: per-kernel totals and the last K-round timeline."""
 import csv, sys, collections
 path = sys.argv[1]
-marker = sys.argv[2] if len(sys.argv) > 2 else "tree_grad_kernel"
+import re
+marker = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"tree_grad_(hist_)?kernel")
 r = list(csv.DictReader(open(path)))
 r.sort(key=lambda x: int(x['Start_Timestamp']))
 ev = [(x['Kernel_Name'], int(x['Start_Timestamp']), int(x['End_Timestamp']), x) for x in r]
-idx = [i for i, e in enumerate(ev) if marker in e[0]]
+idx = [i for i, e in enumerate(ev) if marker.search(e[0])]
 if len(idx) >= 3:
     s, e = idx[-3] + 1, idx[-2]
     t0, t1 = ev[s][1], ev[e][2]
