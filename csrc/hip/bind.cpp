@@ -22,6 +22,8 @@ int ytk_hist_get_fw();
 int ytk_hist_wide(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, float,
                   float, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 int ytk_hist_wide_group(int, int);
+int ytk_hist_wide_rm(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, float, float,
+                     uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
@@ -108,6 +110,8 @@ int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, ui
                        uintptr_t);
 int ytk_tree_grad_hist_grid(long long);
 void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, uintptr_t);
+void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
+                              int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_msg(int, uintptr_t, long long, uintptr_t, int, int, uintptr_t);
 void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 void ytk_owner_unpack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
@@ -127,6 +131,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_set_fw", &ytk_hist_set_fw);
   m.def("hist_get_fw", &ytk_hist_get_fw);
   m.def("hist_wide_group", &ytk_hist_wide_group);
+  m.def("hist_wide_rm", &ytk_hist_wide_rm);
   m.def("split_find", &ytk_split_find);
   m.def("split_combine", &ytk_split_combine);
   m.def("gbst_epilogue", &ytk_gbst_epilogue);
@@ -187,7 +192,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                       part, counters, implicit_items, maxp, stream);
   });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 37 || ip.size() != 10 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 37 || ip.size() != 11 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
@@ -198,6 +203,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
   m.def("owner_pack", &ytk_owner_pack);
   m.def("lw_msg", &ytk_lw_msg);
+  m.def("hist_wide_staged_dev", &ytk_hist_wide_staged_dev);
   m.def("tree_grad_hist", &ytk_tree_grad_hist);
   m.def("tree_grad_hist_grid", &ytk_tree_grad_hist_grid);
   m.def("hist_reduce", &ytk_hist_reduce);

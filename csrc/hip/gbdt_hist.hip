@@ -496,6 +496,127 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
   }
 }
 
+// Row-major wide-bin histogram (uint16 bins [N][stride], B > 256). Same feature groups and
+// LDS planes as hist_wide_kernel, but every row's kFG bins of the group are ONE vector load
+// from the row (2 kFG contiguous bytes) instead of kFG column-major gathers: on the gathered
+// (deep) levels a column-major read fetched a separate 64-B sector per (row, feature), while
+// the groups of one work item now share each row's 64-B line through L2. Columns past F
+// are the row padding (bin 0) and are accumulated branch-free into planes the flush skips.
+// staging (optional): block partials -> staging item (bx, fg) with the entry order
+// bin * kFG + fi of hist_reduce_kernel (gw = kFG), reduced split-K into zeroed slots;
+// otherwise global int64 atomics (zero entries skipped).
+template <int kFG>
+__device__ __forceinline__ void wide_load_row(const uint16_t* p, int (&b)[kFG]) {
+  if constexpr (kFG == 1) {
+    b[0] = p[0];
+  } else if constexpr (kFG == 2) {
+    const unsigned v = *reinterpret_cast<const unsigned*>(p);
+    b[0] = v & 0xffff; b[1] = v >> 16;
+  } else if constexpr (kFG == 4) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    b[0] = v.x & 0xffff; b[1] = v.x >> 16; b[2] = v.y & 0xffff; b[3] = v.y >> 16;
+  } else {
+#pragma unroll
+    for (int q = 0; q < kFG / 8; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(p)[q];
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { b[8 * q + 2 * t] = w[t] & 0xffff; b[8 * q + 2 * t + 1] = w[t] >> 16; }
+    }
+  }
+}
+
+template <bool kIdentity, int kFG>
+__global__ __launch_bounds__(kWideThreads) void hist_wide_rm_kernel(
+    const uint16_t* __restrict__ bins, long long stride, int F,
+    const float2* __restrict__ ghp, const int* __restrict__ rows,
+    const int4* __restrict__ work, long long* __restrict__ hist, int B,
+    float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
+    const int* __restrict__ work_off_dev, long long* __restrict__ staging) {
+  constexpr int kU = kFG >= 8 ? 2 : 16 / kFG;  // rows in flight per thread
+  extern __shared__ __attribute__((aligned(16))) unsigned long long wl[];
+  const int bx = (int)blockIdx.y + (work_off_dev ? *work_off_dev : 0);
+  if (nwork_dev && bx >= *nwork_dev) return;
+  if (scales_dev) {
+    sg = scales_dev[0];
+    sh = scales_dev[1];
+  }
+  const int4 w = work[bx];
+  const int f_lo = (int)blockIdx.x * kFG;
+  const int nf = min(kFG, F - f_lo);
+  const int tid = threadIdx.x;
+  const int E = kFG * B;
+  for (int i = tid; i < 2 * E; i += kWideThreads) wl[i] = 0ull;
+  __syncthreads();
+  const uint16_t* base_row = bins + f_lo;
+  for (int base = w.y + tid; base < w.z; base += kWideThreads * kU) {
+    int r[kU];
+    float2 v[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const int pos = base + j * kWideThreads;
+      const bool ok = pos < w.z;
+      const int p = ok ? pos : w.y;
+      r[j] = kIdentity ? p : rows[p];
+      const float2 t = ghp[p];
+      v[j] = ok ? t : make_float2(0.f, 0.f);  // rows past the end add 0
+    }
+    int bn[kU][kFG];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) wide_load_row<kFG>(base_row + (size_t)(unsigned)r[j] * stride, bn[j]);
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const unsigned long long gi = fx_round(v[j].x * sg);
+      const unsigned long long hi = fx_round(v[j].y * sh);
+#pragma unroll
+      for (int fi = 0; fi < kFG; ++fi) {
+        const int e = fi * B + bn[j][fi];
+        atomicAdd(&wl[e], gi);
+        atomicAdd(&wl[E + e], hi);
+      }
+    }
+  }
+  __syncthreads();
+  if (staging && w.w == 1) {
+    // the slot's ONLY item (leaf-wise engine): this group's columns straight into the slot
+    long long* out = hist + (size_t)w.x * B * F * 2;
+    for (int i = tid; i < nf * B; i += kWideThreads) {
+      const int fi = i / B, bin = i - fi * B;
+      *reinterpret_cast<longlong2*>(&out[((size_t)bin * F + f_lo + fi) * 2]) =
+          make_longlong2((long long)wl[i], (long long)wl[E + i]);
+    }
+    return;
+  }
+  if (staging) {
+    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.x + blockIdx.x) * E;
+    for (int i = tid; i < E; i += kWideThreads) {
+      const int bin = i / kFG, fi = i - bin * kFG;
+      const int e = fi * B + bin;
+      st[i] = make_longlong2((long long)wl[e], (long long)wl[E + e]);
+    }
+    if (w.w == 2) {
+      // first item of a slot the split-K reduce adds into (leaf-wise engine): zero this
+      // group's columns of the slot (the reduce runs after this kernel)
+      long long* out = hist + (size_t)w.x * B * F * 2;
+      for (int i = tid; i < nf * B; i += kWideThreads) {
+        const int fi = i / B, bin = i - fi * B;
+        *reinterpret_cast<longlong2*>(&out[((size_t)bin * F + f_lo + fi) * 2]) = make_longlong2(0, 0);
+      }
+    }
+    return;
+  }
+  long long* out = hist + (size_t)w.x * B * F * 2;
+  for (int i = tid; i < nf * B; i += kWideThreads) {
+    const unsigned long long g = wl[i], h = wl[E + i];
+    if (g | h) {
+      const int fi = i / B, bin = i - fi * B;
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(&out[((size_t)bin * F + f_lo + fi) * 2]);
+      atomicAdd(o, g);
+      atomicAdd(o + 1, h);
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -687,6 +808,74 @@ int ytk_hist_wide(uintptr_t binsT, long long ncol, int F, uintptr_t ghp, uintptr
 #undef YTK_WIDE
   YTK_LAUNCH_CHECK();
   return FG;
+}
+
+// Row-major wide-bin histogram (hist_wide_rm_kernel): bins [N][stride] uint16. staging != 0:
+// block partials to staging (>= nwork * groups * FG * B * 16 bytes), then the split-K reduce
+// into the zeroed slots [slot_base, slot_base + nslots); else global atomics into zeroed
+// slots. Returns the feature-group size.
+int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows, uintptr_t work, int nwork,
+                     uintptr_t hist, int B, float sg, float sh, uintptr_t nwork_dev, uintptr_t scales_dev,
+                     uintptr_t work_off_dev, uintptr_t staging, int slot_base, int nslots, uintptr_t stream) {
+  const int FG = ytk_hist_wide_group(B, F);
+  if (FG <= 0) throw std::invalid_argument("hist_wide_rm: one feature's bins exceed the LDS budget");
+  if (nwork <= 0) return FG;
+  if (stride % FG != 0 || (bins % 16) != 0) throw std::invalid_argument("hist_wide_rm: row stride / alignment");
+  const size_t lds = (size_t)FG * B * 2 * sizeof(unsigned long long);
+  const int groups = (F + FG - 1) / FG;
+  dim3 grid(groups, nwork);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_WRM(ID, G)                                                                                          \
+  hipLaunchKernelGGL((hist_wide_rm_kernel<ID, G>), grid, dim3(kWideThreads), lds, s, (const uint16_t*)bins, stride, \
+                     F, (const float2*)ghp, (const int*)(ID ? 0 : rows), (const int4*)work, (long long*)hist, B, sg, \
+                     sh, (const int*)nwork_dev, (const float*)scales_dev, (const int*)work_off_dev,              \
+                     (long long*)staging)
+#define YTK_WRM_G(ID)                  \
+  switch (FG) {                        \
+    case 1: YTK_WRM(ID, 1); break;     \
+    case 2: YTK_WRM(ID, 2); break;     \
+    case 4: YTK_WRM(ID, 4); break;     \
+    case 8: YTK_WRM(ID, 8); break;     \
+    case 16: YTK_WRM(ID, 16); break;   \
+    default: YTK_WRM(ID, 32); break;   \
+  }
+  if (rows == 0) {
+    YTK_WRM_G(true)
+  } else {
+    YTK_WRM_G(false)
+  }
+#undef YTK_WRM_G
+#undef YTK_WRM
+  YTK_LAUNCH_CHECK();
+  if (staging && nslots > 0) {
+    const int E = B * FG;
+    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
+                       (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev, (long long*)hist, B,
+                       F, B, groups, slot_base, (const int*)nullptr, (const int*)nullptr, (const int2*)nullptr, FG);
+    YTK_LAUNCH_CHECK();
+  }
+  return FG;
+}
+
+// Device-driven wide histogram (leaf-wise engine, uint16 rows): as ytk_hist_fx_staged_dev --
+// work count, slot count and slot ids on the device; items with w == 1 store their slot,
+// w == 2 zero it; slot_ids / slot_range / *nslots_dev list the multi-item slots.
+void ytk_hist_wide_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows, uintptr_t work,
+                              int max_work, uintptr_t nwork_dev, uintptr_t hist, int B, uintptr_t scales_dev,
+                              uintptr_t staging, uintptr_t slot_ids, uintptr_t nslots_dev, uintptr_t slot_range,
+                              int reduce_y, uintptr_t stream) {
+  if (max_work <= 0) return;
+  const int FG = ytk_hist_wide_group(B, F);
+  if (FG <= 0) throw std::invalid_argument("hist_wide_staged_dev: one feature's bins exceed the LDS budget");
+  ytk_hist_wide_rm(bins, stride, F, ghp, rows, work, max_work, hist, B, 1.f, 1.f, nwork_dev, scales_dev, 0, staging,
+                   0, 0, stream);
+  const int groups = (F + FG - 1) / FG;
+  const int E = B * FG;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
+                     dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work,
+                     max_work, (const int*)nwork_dev, (long long*)hist, B, F, B, groups, 0, (const int*)slot_ids,
+                     (const int*)nslots_dev, (const int2*)slot_range, FG);
+  YTK_LAUNCH_CHECK();
 }
 
 // Features per block of hist_wide_kernel: the largest power of two <= 32 whose (g, h)

@@ -57,6 +57,7 @@ struct LwParams {
   int hist_target, min_rows, cap, N;  // N: half size of the ping-pong row buffers
   int split_groups;  // split records per item (feature groups of split_node_kernel)
   int dist;  // multi-GPU: per batch the host all-reduces the built slots + split cursors
+  int bin_bytes;  // 1: uint8 bins, 2: uint16 bins (B > 256)
 };
 
 struct LwBufs {
@@ -894,21 +895,21 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
 // kPrefetch: the software-pipelined body (partition_atomic_body_pf).
-template <bool kPrefetch, bool kPfGh = false>
+template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
-void lw_partition_kernel(LwParams p, LwBufs b, const uint8_t* binsT,
+void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
                                                                    float2* gh_out) {
   if constexpr (kPrefetch)
-    partition_atomic_body_pf<uint8_t, kAtomSub, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
-                                                       b.st + LW_N_SPLIT,
+    partition_atomic_body_pf<BinT, kAtomSub, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
+                                                    b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                       b.cursor, b.part_shift, kCurStride);
   else
-    partition_atomic_body<uint8_t, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
-                                         b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                         b.cursor, b.part_shift, kCurStride);
+    partition_atomic_body<BinT, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
+                                      b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
+                                      b.cursor, b.part_shift, kCurStride);
   // No fences: the only cross-block data the last block reads are the split cursors,
   // updated by RETURNING device-scope atomics (complete before this block counts itself)
   // and read back with atomic loads. (An agent-scope release fence per block writes back
@@ -974,7 +975,8 @@ extern "C" {
 //       state, loss, heap, batch, part_feat, part_thr, part_begin, part_cnt, part_first,
 //       part_shift, cursor, hist_items, build_ids, split_items, item_sid, split_out, root_cnt,
 //       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range
-// ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N, split_groups, dist
+// ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N, split_groups, dist,
+//     bin_bytes
 // fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr. Returns an engine handle.
 int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   LwEngine e;
@@ -990,6 +992,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.N = ip[7];
   p.split_groups = ip[8] > 0 ? ip[8] : 1;
   p.dist = ip[9];
+  p.bin_bytes = ip[10] == 2 ? 2 : 1;
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -1069,6 +1072,14 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
                       uintptr_t gh_out, int max_blocks, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
+  if (e.p.bin_bytes == 2) {  // uint16 bins (B > 256): the pipelined body with (g, h) prefetch
+    const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
+    hipLaunchKernelGGL((lw_partition_kernel<true, true, uint16_t>), grid, dim3(kPartThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint16_t*)binsT, ncol,
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+    YTK_LAUNCH_CHECK();
+    return;
+  }
   // software-pipelined partition body, next chunk's row ids + (g, h) in flight (default:
   // 3.41 -> 3.28-3.35 ms/tree, profiles/r2_partition_chunk.md); YTK_LW_PART_PREFETCH=1: row
   // ids only (measured slower), 0: unpipelined

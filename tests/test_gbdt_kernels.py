@@ -389,9 +389,11 @@ def test_partition_atomic_is_a_segmentwise_partition(cuda, identity):
 
 @pytest.mark.parametrize("F,nb,B", [(7, 300, 300), (28, 5000, 5000), (3, 9000, 9000), (40, 700, 704)])
 @pytest.mark.parametrize("gathered", [False, True])
-def test_hist_build_wide_matches_cpu(cuda, F, nb, B, gathered):
-    """Wide-bin (uint16, B > 256) LDS kernel == the exact CPU integer histogram, with
-    several work items over several slots and (optionally) a row permutation."""
+@pytest.mark.parametrize("staged", [False, True])
+def test_hist_build_wide_matches_cpu(cuda, F, nb, B, gathered, staged):
+    """Wide-bin (uint16, B > 256) row-major LDS kernel == the exact CPU integer histogram,
+    with several work items over several slots, (optionally) a row permutation, and the
+    atomic or the staged (block partials + split-K reduce) flush."""
     N = 60000
     bins = _rand_bins(N, F, nb, seed=3, dtype=torch.int16)
     binsT = bins[:, :F].t().contiguous()
@@ -402,7 +404,9 @@ def test_hist_build_wide_matches_cpu(cuda, F, nb, B, gathered):
     hc = torch.zeros((3, B, F, 2), dtype=torch.int64)
     gops.hist_build(bins, F, gh, rows, work, hc, B, SG, SH)
     hg = torch.zeros((3, B, F, 2), dtype=torch.int64, device=cuda)
+    stg = (torch.empty(len(work) * ((F + 31) // 32) * 32 * B * 2, dtype=torch.int64, device=cuda)
+           if staged else None)
     gops.hist_build(bins.to(cuda), F, gh.to(cuda), rows.to(cuda) if rows is not None else None, work.to(cuda),
-                    hg, B, SG, SH, binsT=binsT.to(cuda))
+                    hg, B, SG, SH, binsT=binsT.to(cuda), staging=stg, slot_base=0, nslots=3 if staged else 0)
     assert torch.equal(hg.cpu(), hc)
 

@@ -313,14 +313,16 @@ def test_histogram_pool_capacity_misses_do_not_change_the_tree():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_cnt", [300, 5000])
-def test_wide_bins_device_builder_matches_cpu(cuda, max_cnt):
-    """> 256 bins (uint16): the GPU level builder (wide LDS histograms) == the host builder
-    on the GPU == the CPU path, tree for tree (silent corruption above 256)."""
+@pytest.mark.parametrize("policy", ["level", "loss"])
+def test_wide_bins_device_builder_matches_cpu(cuda, max_cnt, policy):
+    """> 256 bins (uint16): the GPU level / leaf-wise engines (row-major feature-group LDS
+    histograms) == the host builder on the GPU == the CPU path, tree for tree (ADVICE r1:
+    silent corruption above 256)."""
     d_cpu = _data(40000, 21)
     approx = [{"cols": "default", "type": "sample_by_quantile", "max_cnt": max_cnt, "alpha": 0.5}]
     dumps = []
     for dev, dev_builder in (("cpu", False), (cuda, False), (cuda, True)):
-        p = _params("level", rounds=3)
+        p = _params(policy, rounds=3)
         p.approximate = approx
         p.device_builder = dev_builder
         d = GBDTData(d_cpu.X.to(dev), d_cpu.y.to(dev))

@@ -210,7 +210,7 @@ class DeviceLevelBuilder:
         # staged histogram flush: block partials to a staging slab with plain stores, then a
         # split-K slot reduce (8 int64 atomics per value instead of one per block)
         max_hist_items = self.hist_target + (self.maxp // 2) + 2
-        self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0" and not self.wide
+        self.staged = os.environ.get("YTK_HIST_STAGED", "1") != "0"
         # multi-GPU: overlap the all-reduce of half a level's histograms with the build of
         # the other half (BASELINE: histogram all-reduce overlapped with the next block's build)
         # Only with enough local rows: at a small shard (strong scaling, e.g. Higgs / 8) a
@@ -259,8 +259,9 @@ class DeviceLevelBuilder:
             stride = bins.shape[1]
             return B <= 256 and stride % 32 == 0 and stride >= ((F + 31) // 32) * 32
         if bins.dtype == torch.int16:
+            fg = gops.wide_group(B, F)
             return (binsT is not None and binsT.dtype == torch.int16 and binsT.shape[0] == F
-                    and binsT.is_contiguous() and gops.wide_group(B, F) > 0)
+                    and binsT.is_contiguous() and fg > 0 and bins.shape[1] % fg == 0 and bins.is_contiguous())
         return False
 
     def _snap_views(self, buf):
@@ -452,9 +453,12 @@ class DeviceLevelBuilder:
             else:
                 self.hist[slot_base:slot_base + nslots].zero_()
             if self.wide:
-                h.hist_wide(ptr(self.binsT), self.binsT.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
-                            nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5) if n_dev is None else n_dev,
-                            ptr(self.scales), work_off, s)
+                # row-major uint16 rows (one vector load per row and feature group), staged
+                # flush + split-K reduce into the level's slots
+                h.hist_wide_rm(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
+                               nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5) if n_dev is None else n_dev,
+                               ptr(self.scales), work_off, ptr(self.staging) if self.staged else 0, slot_base,
+                               nslots, s)
                 return
             if self.staged:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,

@@ -58,6 +58,12 @@ class DeviceLeafBuilder:
         self.p = p
         self.timer = timer if timer is not None else PhaseTimer()
         self.bins, self.binsT = bins, binsT
+        # uint16 bins (B > 256, e.g. the reference's 5000-bin run): row-major feature-group LDS
+        # histograms (hist_wide_staged_dev), fewer work items per batch (one per group per CU)
+        self.wide = bins.dtype == torch.int16
+        if self.wide:
+            groups = -(-F // gops.wide_group(B, F))
+            self.HIST_TARGET = min(self.HIST_TARGET, max(32, 1024 // groups))
         self.dev = bins.device
         self.N = N = bins.shape[0]
         self.F, self.B = F, B
@@ -153,6 +159,11 @@ class DeviceLeafBuilder:
             return False
         if params.grow_policy != "loss" or not (2 <= params.max_leaf_cnt <= LW_LEAF_MAX):
             return False
+        if bins.dtype == torch.int16:  # wide bins: uint16 rows, feature-group LDS histograms
+            fg = gops.wide_group(B, F)
+            return (binsT is not None and binsT.dtype == torch.int16 and binsT.shape[0] == F
+                    and binsT.is_contiguous() and bins.is_contiguous() and fg > 0 and bins.shape[1] % fg == 0
+                    and 2 * bins.shape[0] < (1 << 31))
         if bins.dtype != torch.uint8 or binsT is None or binsT.dtype != torch.uint8 or B > 256:
             return False
         stride = bins.shape[1]
@@ -179,7 +190,7 @@ class DeviceLeafBuilder:
         # budget the batch choice ranks within (100 = the host planner's virtual replay)
         spec = int(os.environ.get("YTK_LW_SPEC_PCT", "100")) if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
         return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
-                self.cap, self.N, self.split_groups, 1 if self.comm.is_dist else 0]
+                self.cap, self.N, self.split_groups, 1 if self.comm.is_dist else 0, 2 if self.wide else 1]
 
     def _ptrs(self):
         f, i = self.nd_f64, self.nd_i32
@@ -224,6 +235,12 @@ class DeviceLeafBuilder:
         st = ptr(self.st)
         # sole-item slots are stored by the hist kernel, <= 16-item slots by the reduce, larger
         # ones zeroed by their first hist item and reduced split-K
+        if self.wide:
+            h.hist_wide_staged_dev(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
+                                   self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
+                                   ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
+                                   self.REDUCE_Y, s)
+            return
         h.hist_fx_staged_dev(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                              self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),

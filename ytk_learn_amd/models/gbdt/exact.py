@@ -1,0 +1,299 @@
+"""Exact-greedy, level-wise tree maker on presorted columns (``tree_maker = "feature"``).
+
+Reference: ``J/optimizer/gbdt/FeatureParallelTreeMakerByLevel.java`` (make :150-185,
+initNodeStats :277-312, findSplit :315-343, enumerateSplit :346-398, resetPosition
+:424-444) over ``J/data/gbdt/FeatureColData.java:38-58`` (every column sorted by value
+once, (value, row) pairs). Every distinct value is a split candidate -- no binning, so any
+number of distinct values (a Higgs column has millions) is supported.
+
+Device design (GPU or CPU tensors, no per-row host work):
+  * presort once: ``ord[f]`` = rows of column f in ascending value order (stable).
+  * node-segmented order: every level keeps, for every feature, the rows of each expanding
+    node contiguous and still sorted by value; the node boundaries are the same for every
+    feature (a node holds the same rows in every column). After a level's splits each
+    segment is stably partitioned into its children (one segmented scan of the go-left flags
+    over [F, N] + one scatter), so no re-sort is ever needed.
+  * split search: (g, h) gathered in segment order as exact int64 fixed point (the same
+    power-of-two scales as the histogram path), inclusive prefix sums per feature, the left
+    sums of every candidate = prefix - the node's base; candidates where the value changes
+    by more than MIN_FEA_SPLIT_GAP (1e-16f, Constants.java:34) with both children's hessian
+    >= min_child_hessian_sum; lossChg = (float)(gain(L) + gain(R) - rootGain) exactly as the
+    reference, the best per node = largest lossChg, ties -> lower feature, then lower value
+    (SplitInfo.needReplace :99-104 in the reference's scan order); threshold = (v_prev + v)
+    * 0.5f.
+  * rows go left iff value < threshold (resetPosition :436).
+Features are processed in chunks to bound the [F, N] temporaries.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ...ops import gbdt as gops
+from ...parallel.comm import Comm
+from .builder import TimeStats, TreeParams
+from .tree import Tree
+
+MIN_FEA_SPLIT_GAP = np.float32(1e-16)  # Constants.java:34
+
+
+class ExactGreedyBuilder:
+    def __init__(self, X: torch.Tensor, params: TreeParams, comm: Optional[Comm] = None,
+                 feat_chunk: Optional[int] = None):
+        comm = comm or Comm.local(X.device)
+        if comm.is_dist:
+            # GBDTDataFlow.java:102-107: feature parallel only supports a single machine
+            raise ValueError("[GBDT] feature parallel only support single machine")
+        if params.grow_policy != "level" or params.max_depth < 1:
+            raise ValueError("the exact-greedy maker grows level-wise with max_depth >= 1")
+        self.p = params
+        self.comm = comm
+        self.dev = X.device
+        self.N, self.F = X.shape
+        # [F, N] raw values (NaN already filled) and the presorted row order of every column
+        self.XT = X.t().contiguous().float()
+        self.ord = torch.argsort(self.XT, dim=1, stable=True).to(torch.int64)
+        self.chunk = int(feat_chunk or os.environ.get("YTK_EXACT_CHUNK", 8))
+        gp = params.gain_params()
+        self.gpv = (gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"])
+        self.tree_count = 0
+        self.last_keep = None
+        self.binsT = None  # API parity with the histogram builders
+        self.total_stats = TimeStats()
+        self.last_stats = TimeStats()
+
+    # ------------------------------------------------------------------ gains
+    def _gain(self, G: torch.Tensor, H: torch.Tensor) -> torch.Tensor:
+        """UpdateStrategy.calcGain (:64-80) on float64 tensors."""
+        mcw, l1, l2, mal = self.gpv
+        if mal <= 0:
+            t = G if l1 == 0.0 else torch.sign(G) * torch.clamp(G.abs() - l1, min=0.0)
+            gain = t * t / (H + l2)
+        else:
+            v = self._value(G, H)
+            gain = -2.0 * (G * v + 0.5 * (H + l2) * v * v + l1 * v.abs())
+        return torch.where(H < mcw, torch.zeros_like(gain), gain)
+
+    def _value(self, G: torch.Tensor, H: torch.Tensor) -> torch.Tensor:
+        """UpdateStrategy.calcNodeValue (:83-100)."""
+        mcw, l1, l2, mal = self.gpv
+        t = G if l1 == 0.0 else torch.sign(G) * torch.clamp(G.abs() - l1, min=0.0)
+        v = -t / (H + l2)
+        if mal > 0:
+            v = v.clamp(-mal, mal)
+        return torch.where(H < mcw, torch.zeros_like(v), v)
+
+    # ------------------------------------------------------------------ build
+    def build(self, gh: torch.Tensor, ghmax: Optional[torch.Tensor] = None, ghmax_global: bool = False) -> Tree:
+        p = self.p
+        t_start = time.perf_counter()
+        dev = self.dev
+        rng = np.random.default_rng((p.seed, self.tree_count))
+        seed_rows = int(rng.integers(1 << 62))
+        # --- instance / feature subsampling (initAssistData :188-247)
+        if p.instance_sample_rate < 1.0:
+            g = torch.Generator(device=dev)
+            g.manual_seed(seed_rows)
+            keep = torch.rand(self.N, generator=g, device=dev) < p.instance_sample_rate
+            self.last_keep = keep
+            order = self.ord[keep[self.ord]].view(self.F, -1)  # each column's kept rows, still sorted
+        else:
+            keep = None
+            self.last_keep = None
+            order = self.ord
+        n = order.shape[1]
+        if p.feature_sample_rate < 1.0:
+            n_sam = max(1, int(round(p.feature_sample_rate * self.F)))
+            feats = np.sort(rng.permutation(self.F)[:n_sam])
+        else:
+            feats = np.arange(self.F)
+        # exact int64 fixed point (g, h): order-independent sums, the histogram path's scales
+        ghk = gh if keep is None else gh[keep]
+        mx = ghk.abs().amax(dim=0).double().cpu().numpy() if n > 0 else np.zeros(2)
+        sg, sh = gops.fixed_point_scales(mx[0], mx[1], max(n, 1))
+        q = torch.empty((self.N, 2), dtype=torch.int64, device=dev)
+        q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
+        q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)
+        inv = torch.tensor([1.0 / sg, 1.0 / sh], dtype=torch.float64, device=dev)
+        mcw, l1, l2, mal = self.gpv
+        lr32 = np.float32(p.learning_rate)
+        msl = float(np.float32(p.min_split_loss))
+
+        tree = Tree()
+        # node of every position of the segmented order (same for every feature)
+        seg = [(0, n)]            # (begin, end) per expanding node, in expand order
+        expand = [0]
+        leaf_cnt = 1
+        stats = {}                # nid -> (G, H, cnt, best lossChg)
+        pos_node = torch.zeros(n, dtype=torch.int64, device=dev)
+        for depth in range(p.max_depth):
+            if p.max_leaf_cnt > 0 and leaf_cnt >= p.max_leaf_cnt:
+                break
+            K = len(expand)
+            bnd = torch.tensor([b for b, _ in seg] + [seg[-1][1] if seg else 0], dtype=torch.int64, device=dev)
+            cnt = (bnd[1:] - bnd[:-1])
+            # node sums (initNodeStats): column 0's segments hold each node's rows
+            rows0 = order[0]
+            sums = torch.zeros((K, 2), dtype=torch.int64, device=dev).index_add_(0, pos_node, q[rows0])
+            Gd = sums.double() * inv  # [K, 2] float64 totals
+            root_gain = self._gain(Gd[:, 0], Gd[:, 1]).float()
+            can = (Gd[:, 1] >= 2.0 * mcw) & (cnt >= max(p.min_split_samples, 0))  # canSplit
+            best_chg = torch.full((K,), float("-inf"), dtype=torch.float32, device=dev)
+            best_f = torch.full((K,), -1, dtype=torch.int64, device=dev)
+            best_v = torch.zeros(K, dtype=torch.float32, device=dev)
+            first = torch.zeros(n, dtype=torch.bool, device=dev)
+            first[bnd[:-1][cnt > 0]] = True  # the first row of a node is never a candidate
+            for c0 in range(0, len(feats), self.chunk):
+                fs = torch.from_numpy(feats[c0:c0 + self.chunk]).to(dev)
+                o = order[fs]                                   # [C, n] rows
+                v = torch.gather(self.XT[fs], 1, o)             # [C, n] values, sorted per node
+                gq = q[o]                                       # [C, n, 2] int64
+                cs = torch.cumsum(gq, dim=1)
+                excl = cs - gq                                  # sums of the rows before i
+                base = excl[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K, 2] node start
+                left = excl - base[:, pos_node]                 # left sums at each candidate
+                tot = sums[pos_node]                            # [n, 2]
+                Ld = left.double() * inv
+                Rd = (tot[None] - left).double() * inv
+                dv = torch.zeros_like(v)
+                dv[:, 1:] = (v[:, 1:] - v[:, :-1]).abs()
+                ok = (~first[None]) & (dv > MIN_FEA_SPLIT_GAP) & (left[..., 1] != 0)
+                ok &= (Ld[..., 1] >= mcw) & (Rd[..., 1] >= mcw) & can[pos_node][None]
+                chg = (self._gain(Ld[..., 0], Ld[..., 1]) + self._gain(Rd[..., 0], Rd[..., 1])
+                       - root_gain[pos_node][None].double()).float()
+                chg = torch.where(ok, chg, torch.full_like(chg, float("-inf")))
+                # per (feature, node): max lossChg, its first position (scan order)
+                C = o.shape[0]
+                idx = pos_node[None].expand(C, n)
+                mx_fn = torch.full((C, K), float("-inf"), dtype=torch.float32, device=dev)
+                mx_fn.scatter_reduce_(1, idx, chg, "amax")
+                ar = torch.arange(n, dtype=torch.int64, device=dev)[None].expand(C, n)
+                hit = (chg == mx_fn.gather(1, idx)) & ok
+                pos_fn = torch.full((C, K), n, dtype=torch.int64, device=dev)
+                pos_fn.scatter_reduce_(1, idx, torch.where(hit, ar, torch.full_like(ar, n)), "amin")
+                for ci in range(C):  # features in ascending order: replace only if strictly greater
+                    upd = mx_fn[ci] > best_chg
+                    if bool(upd.any()):
+                        pi = pos_fn[ci].clamp(max=max(n - 1, 0))
+                        thr = (v[ci, pi] + v[ci, (pi - 1).clamp(min=0)]) * np.float32(0.5)
+                        best_chg = torch.where(upd, mx_fn[ci], best_chg)
+                        best_f = torch.where(upd, fs[ci].expand(K), best_f)
+                        best_v = torch.where(upd, thr, best_v)
+                del o, v, gq, cs, excl, base, left, Ld, Rd, chg, hit, ar, idx
+            # --- tree update (findSplit :327-342), host side over the level's nodes
+            bc, bf, bv = best_chg.cpu().numpy(), best_f.cpu().numpy(), best_v.cpu().numpy()
+            Gh = Gd.cpu().numpy()
+            vals = (self._value(Gd[:, 0], Gd[:, 1]).float().cpu().numpy()) * lr32
+            cnt_h = cnt.cpu().numpy()
+            split_nodes, new_expand = [], []
+            go_feat = np.full(K, -1, np.int64)
+            go_thr = np.zeros(K, np.float32)
+            for k, nid in enumerate(expand):
+                stats[nid] = (float(Gh[k, 1]), int(cnt_h[k]), float(bc[k]))
+                if (p.max_leaf_cnt < 0 or leaf_cnt < p.max_leaf_cnt) and bc[k] > msl:
+                    lc, rc = tree.add_children(nid)
+                    leaf_cnt += 1
+                    tree.feat[nid] = int(bf[k])
+                    tree.cond[nid] = float(bv[k])
+                    tree.is_leaf[nid] = False
+                    split_nodes.append(k)
+                    new_expand += [lc, rc]
+                    go_feat[k] = bf[k]
+                    go_thr[k] = bv[k]
+                else:
+                    tree.set_leaf(nid, float(vals[k]))
+            if not split_nodes:
+                expand, seg = [], []
+                break
+            # --- resetPosition + stable re-segmentation of every column's order
+            gf = torch.from_numpy(go_feat).to(dev)
+            gt = torch.from_numpy(go_thr).to(dev)
+            order, pos_node, seg = self._resegment(order, pos_node, bnd, gf, gt, K)
+            expand = new_expand
+        # remaining expand nodes become leaves (make :176-180)
+        if expand:
+            K = len(expand)
+            rows0 = order[0]
+            sums = torch.zeros((K, 2), dtype=torch.int64, device=dev).index_add_(0, pos_node, q[rows0])
+            Gd = sums.double() * inv
+            vals = (self._value(Gd[:, 0], Gd[:, 1]).float().cpu().numpy()) * lr32
+            cnts = torch.bincount(pos_node, minlength=K).cpu().numpy() if n > 0 else np.zeros(K, np.int64)
+            Gh = Gd.cpu().numpy()
+            for k, nid in enumerate(expand):
+                tree.set_leaf(nid, float(vals[k]))
+                stats[nid] = (float(Gh[k, 1]), int(cnts[k]), float("-inf"))
+        for nid, (hs, c, chg) in stats.items():  # updateTreeNodeStat
+            tree.hess_sum[nid] = float(np.float32(hs))
+            tree.sample_cnt[nid] = c
+            tree.loss_chg[nid] = float(np.float32(chg))
+        tree.converted = True  # raw thresholds already
+        self.tree_count += 1
+        self.last_stats = TimeStats()
+        self.last_stats.total = time.perf_counter() - t_start
+        self.last_stats.trees = 1
+        self.total_stats.add(self.last_stats)
+        return tree
+
+    def leaf_ids_of(self, tree: Tree) -> torch.Tensor:
+        """Leaf node id of every training row (raw-threshold walk; l1 leaf refine)."""
+        f, c, l, r, d, v = tree.raw_arrays()
+        fl = {"nfeat": f, "nthr": c, "nleft": l, "nright": r, "ndefl": d, "nval": v,
+              "troot": np.zeros(1, np.int32), "tout": np.zeros(1, np.int32)}
+        fl = {k: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev) for k, a in fl.items()}
+        out = torch.zeros((self.N, 1), dtype=torch.int32, device=self.dev)
+        gops.forest_predict(self.XT.t().contiguous(), fl, None, 1.0, leaf_out=out)
+        return out[:, 0].to(torch.int64)
+
+    def _resegment(self, order, pos_node, bnd, go_feat, go_thr, K):
+        """Children segments of the split nodes, stably partitioned in every column; rows of
+        nodes that became leaves leave the order. Returns (order, pos_node, segments)."""
+        dev = self.dev
+        n = order.shape[1]
+        rows0 = order[0]
+        split = go_feat >= 0                                  # [K]
+        nf = go_feat[pos_node].clamp(min=0)
+        val = self.XT[nf, rows0]                              # row's value of its node's split feature
+        left_row = torch.zeros(self.N, dtype=torch.bool, device=dev)
+        left_row[rows0] = val < go_thr[pos_node]              # resetPosition: value < cond -> left
+        alive_pos = split[pos_node]                           # rows staying in the order
+        # children sizes (identical for every column)
+        nl = torch.zeros(K, dtype=torch.int64, device=dev).index_add_(
+            0, pos_node, (left_row[rows0] & alive_pos).to(torch.int64))
+        cnt = bnd[1:] - bnd[:-1]
+        nr = torch.where(split, cnt - nl, torch.zeros_like(cnt))
+        nl = torch.where(split, nl, torch.zeros_like(nl))
+        sizes = torch.stack([nl, nr], 1).reshape(-1)          # child order: (left, right) per node
+        cbeg = torch.cumsum(sizes, 0) - sizes                 # new segment begins
+        n_new = int(sizes.sum())
+        new_order = torch.empty((self.F, n_new), dtype=torch.int64, device=dev)
+        for c0 in range(0, self.F, self.chunk):
+            o = order[c0:c0 + self.chunk]
+            C = o.shape[0]
+            lf = left_row[o]                                  # [C, n]
+            alive = alive_pos[None].expand(C, n)
+            li = (lf & alive).to(torch.int64)
+            ri = ((~lf) & alive).to(torch.int64)
+            lc = torch.cumsum(li, 1) - li                     # lefts before i (whole column)
+            rcs = torch.cumsum(ri, 1) - ri
+            lbase = lc[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K] at each node start
+            rbase = rcs[:, bnd[:-1].clamp(max=max(n - 1, 0))]
+            k2 = 2 * pos_node[None].expand(C, n)
+            dest = torch.where(lf, cbeg[k2] + lc - lbase[:, pos_node], cbeg[k2 + 1] + rcs - rbase[:, pos_node])
+            dest = torch.where(alive, dest, torch.full_like(dest, n_new))  # dropped rows -> scratch column
+            tmp = torch.empty((C, n_new + 1), dtype=torch.int64, device=dev)
+            tmp.scatter_(1, dest, o)
+            new_order[c0:c0 + C] = tmp[:, :n_new]
+        nz = sizes > 0
+        segs_all = list(zip(cbeg.cpu().tolist(), (cbeg + sizes).cpu().tolist()))
+        # expand-order children of the split nodes (empty children are still tree nodes)
+        seg = [segs_all[2 * k + j] for k in torch.nonzero(split).flatten().cpu().tolist() for j in (0, 1)]
+        node_of = torch.repeat_interleave(torch.arange(2 * K, device=dev)[nz], sizes[nz])
+        # renumber child slots 2k / 2k+1 of split nodes to 0 .. 2 * nsplit - 1
+        remap = torch.full((2 * K,), -1, dtype=torch.int64, device=dev)
+        sk = torch.nonzero(split).flatten()
+        remap[torch.stack([2 * sk, 2 * sk + 1], 1).reshape(-1)] = torch.arange(2 * sk.numel(), device=dev)
+        return new_order, remap[node_of], seg

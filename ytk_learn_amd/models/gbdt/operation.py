@@ -8,14 +8,15 @@ dumpFeatureImportance :400-420) and ``J/dataflow/GBDTCoreData.java`` (labels: on
 a class id / K-vector for softmax; optional init prediction in the 4th field).
 
 ``tree_maker = "feature"`` (the reference's single-machine exact greedy maker,
-``FeatureParallelTreeMakerByLevel.java``) is served by the same histogram engine with
-``no_sample`` bins: every distinct value is a candidate and thresholds are midpoints of
-neighbouring values, which is exactly the exact-greedy split set; neighbouring values
-closer than ``MIN_FEA_SPLIT_GAP`` (1e-16, never a split point there) share one bin
-(``binning.merge_split_gap``). Wide candidate sets (> 256 values) use uint16 bins.
+``FeatureParallelTreeMakerByLevel.java``) runs ``exact.ExactGreedyBuilder``: presorted raw
+columns, node-segmented orders kept by stable re-partitioning, every distinct value a
+candidate (any cardinality). ``YTK_EXACT_BINNED=1`` selects the older emulation on the
+histogram engine with ``no_sample`` bins (neighbouring values closer than
+``MIN_FEA_SPLIT_GAP`` share one bin, ``binning.merge_split_gap``; <= 65,536 values).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -110,8 +111,12 @@ def run_gbdt(cfg, comm, log, transform_fn=None, threads=0, profile: bool = False
     if gp.tree_maker == "feature":
         if comm.is_dist:
             raise YtkLearnError("[GBDT] feature parallel only support single machine")
-        # every distinct value a candidate, runs closer than MIN_FEA_SPLIT_GAP merged
-        gp.approximate = [{"cols": "default", "type": "no_sample", "min_split_gap": 1e-16}]
+        if gp.tree.grow_policy != "level":
+            raise YtkLearnError("[GBDT] feature parallel tree maker grows level-wise (tree_grow_policy = level)")
+        if os.environ.get("YTK_EXACT_BINNED", "0") == "1":
+            # emulation on the histogram path: every distinct value a bin, runs closer than
+            # MIN_FEA_SPLIT_GAP merged (<= 65,536 distinct values per feature)
+            gp.approximate = [{"cols": "default", "type": "no_sample", "min_split_gap": 1e-16}]
     model = None
     if mp.continue_train or gp.just_evaluate:
         if mp.continue_train and not fs.exists(mp.data_path):

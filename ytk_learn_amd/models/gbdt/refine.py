@@ -193,8 +193,11 @@ class TreeRefiner:
     def refine(self, tree, builder, y: torch.Tensor, cur_score: torch.Tensor, w: torch.Tensor, lr: float):
         """Host-built tree: leaf values patched on the host tree (one value per leaf read)."""
         dev = y.device
-        arrs = tuple(torch.from_numpy(a).to(dev) for a in tree.bin_arrays())
-        leaf = self.leaf_ids(arrs, builder.binsT)
+        if hasattr(builder, "leaf_ids_of"):  # raw-threshold (exact-greedy) trees
+            leaf = builder.leaf_ids_of(tree)
+        else:
+            arrs = tuple(torch.from_numpy(a).to(dev) for a in tree.bin_arrays())
+            leaf = self.leaf_ids(arrs, builder.binsT)
         leaves = tree.leaf_nodes()
         med = self.medians(leaf, y, cur_score, w, getattr(builder, "last_keep", None), tree.num_nodes,
                            leaves).cpu().numpy()

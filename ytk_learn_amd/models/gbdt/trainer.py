@@ -34,6 +34,7 @@ from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
 from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder, node_table_to_tree
 from .device_leafwise import DeviceLeafBuilder
+from .exact import ExactGreedyBuilder
 from .refine import TreeRefiner
 from .tree import CandTable, GBDTModel, Tree
 
@@ -139,6 +140,11 @@ class GBDTTrainer:
         self.missing_fill = compute_missing_fill(tr.X, tr.weight, self.p.missing_value, self.comm)
         self.fill_dev = torch.from_numpy(self.missing_fill).to(self.dev)
         Xf = torch.where(torch.isnan(tr.X), self.fill_dev[None, :], tr.X)
+        # tree_maker = "feature": exact greedy on presorted raw columns (no binning at all)
+        self.exact = self.p.tree_maker == "feature" and os.environ.get("YTK_EXACT_BINNED", "0") != "1"
+        if self.exact:
+            self._prepare_exact(Xf)
+            return
         self.mapper = BinMapper.fit(Xf, tr.weight, self._specs(), self.comm, self.p.split_type,
                                     seed=self.p.tree.seed)
         self.bins, self.binsT = self.mapper.transform(Xf)
@@ -191,6 +197,15 @@ class GBDTTrainer:
             self.builder = TreeBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp,
                                        self.comm, profile=self.profile,
                                        pool_mb=self.p.histogram_pool_capacity)
+        self._finish_prepare(t0)
+        nb = self.mapper.nbins
+        self.log.info(f"[GBDT] generate sorted global feature bins complete! feature dim:{self.F}, "
+                      f"total feature bin cnt:{int(nb.sum())}")
+
+    def _finish_prepare(self, t0: float):
+        """Score / gradient buffers, loss bounds, test set, evaluators (every tree maker)."""
+        tr = self.train_data
+        tp = self.p.tree
         N = tr.n
         self.score = torch.zeros((N, self.K), dtype=torch.float32, device=self.dev)
         self.init_score = self._base_score(tr)
@@ -242,9 +257,21 @@ class GBDTTrainer:
         self.rounds_done = len(self.model.trees) // self.K
         self._prepared = True
         self.prep_time = time.perf_counter() - t0
-        nb = self.mapper.nbins
-        self.log.info(f"[GBDT] generate sorted global feature bins complete! feature dim:{self.F}, "
-                      f"total feature bin cnt:{int(nb.sum())}")
+
+    def _prepare_exact(self, Xf: torch.Tensor):
+        """Exact-greedy maker (FeatureParallelTreeMakerByLevel): presorted raw columns; the
+        round's train scores come from raw-threshold walks of the new trees."""
+        t0 = time.perf_counter()
+        tp = self.p.tree
+        self.Xtr = Xf.contiguous()
+        self.mapper = None
+        self.bins = self.binsT = None
+        self.B = 0
+        self.use_device_builder = False
+        self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
+        self.builder = ExactGreedyBuilder(self.Xtr, tp, self.comm)
+        self._finish_prepare(t0)
+        self.log.info(f"[GBDT] exact greedy (presorted columns) ready! feature dim:{self.F}, rows:{self.Xtr.shape[0]}")
 
     def _replay_loaded_trees(self):
         """continue_train: score existing trees with raw features (isOriginTree)."""
@@ -481,7 +508,13 @@ class GBDTTrainer:
                     self.refiner.refine(tree, self.builder, self.y[:, k], self.score[:, k] / self._score_div(i)
                                         + self.init_score[:, k], self.w, lr)
                 host_trees.append(tree)
-                arrays.append(self._tree_to_dev(tree))
+                arrays.append(None if self.exact else self._tree_to_dev(tree))
+        if self.exact:
+            # raw-threshold trees: the round's trees are walked on the filled raw features
+            fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
+            fl.trees = host_trees
+            gops.forest_predict(self.Xtr, {k: torch.from_numpy(v).to(self.dev) for k, v in fl.flatten().items()},
+                                self.score, 1.0)
         if not self.use_device_builder:
             self.timer.mark("build_tree")
         # score update + train loss after this round + gradients for the next round
@@ -502,7 +535,8 @@ class GBDTTrainer:
                 dev_trees[0].leaf_counts = lc
         else:
             for k in range(self.K):
-                gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
+                if arrays[k] is not None:
+                    gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
             acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
         self.timer.mark("grad_and_score")
         # model conversion (slot -> raw threshold, names, default direction) for host trees
@@ -535,10 +569,12 @@ class GBDTTrainer:
     def _convert(self, tree: Tree):
         """convertModel (GBDTOptimizer.java:663-690): slot -> raw threshold, names, default
         direction -- vectorised per tree."""
-        if getattr(self, "_cand_tab", None) is None:  # float32 candidate table, built once
-            self._cand_tab = CandTable(self.mapper.cands)
+        if self._names_arr is None:
             self._names_arr = np.asarray(self.feature_names, dtype=object)
-        tree.convert_split_values(self._cand_tab, self.p.split_type)
+        if self.mapper is not None:  # exact-greedy trees carry raw thresholds already
+            if getattr(self, "_cand_tab", None) is None:  # float32 candidate table, built once
+                self._cand_tab = CandTable(self.mapper.cands)
+            tree.convert_split_values(self._cand_tab, self.p.split_type)
         tree.add_feature_names(self._names_arr)
         tree.add_default_direction(self.missing_fill)
 

@@ -119,11 +119,15 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
             else:
                 h.hist_fx(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                           float(sg), float(sh), 0, 0, stream(bins))
-        elif (binsT is not None and binsT.dtype == torch.int16 and bins.dtype == torch.int16
-              and wide_group(B, F) > 0 and binsT.shape[0] == F and binsT.is_contiguous()):
-            check_cuda(binsT)
-            h.hist_wide(ptr(binsT), binsT.shape[1], F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
-                        float(sg), float(sh), 0, 0, 0, stream(bins))
+        elif (bins.dtype == torch.int16 and wide_group(B, F) > 0 and stride % wide_group(B, F) == 0
+              and bins.is_contiguous()):
+            # row-major wide-bin LDS kernel (feature groups per block, one vector load per row)
+            use_st = staging is not None and nslots > 0 and slot_ids is None
+            if use_st:
+                assert staging.numel() >= nwork * hist_cols(F) * B * 2
+            h.hist_wide_rm(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
+                           float(sg), float(sh), 0, 0, 0, ptr(staging) if use_st else 0, slot_base,
+                           nslots if use_st else 0, stream(bins))
         else:
             h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                              nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
