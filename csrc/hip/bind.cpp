@@ -23,7 +23,7 @@ int ytk_hist_wide(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, in
                   float, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 int ytk_hist_wide_group(int, int);
 int ytk_hist_wide_rm(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, float, float,
-                     uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+                     uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, uintptr_t);
 // gbdt_split.hip
 void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t,
                     float, float, float, float, double, double, uintptr_t, uintptr_t, uintptr_t,
@@ -113,6 +113,12 @@ void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, u
 void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
                               int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_msg(int, uintptr_t, long long, uintptr_t, int, int, uintptr_t);
+int ytk_peer_create(int, int, long long, uintptr_t);
+void ytk_peer_open(int, uintptr_t);
+void ytk_peer_allreduce(int, uintptr_t, long long, long long, uintptr_t);
+uintptr_t ytk_peer_err(int);
+int ytk_peer_check(int);
+void ytk_peer_destroy(int);
 void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 void ytk_owner_unpack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 // gbdt_hist.hip (device-driven staged histogram)
@@ -202,6 +208,12 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lw_zero_slots", &ytk_lw_zero_slots);
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
   m.def("owner_pack", &ytk_owner_pack);
+  m.def("peer_create", &ytk_peer_create);
+  m.def("peer_open", &ytk_peer_open);
+  m.def("peer_allreduce", &ytk_peer_allreduce);
+  m.def("peer_err", &ytk_peer_err);
+  m.def("peer_check", &ytk_peer_check);
+  m.def("peer_destroy", &ytk_peer_destroy);
   m.def("lw_msg", &ytk_lw_msg);
   m.def("hist_wide_staged_dev", &ytk_hist_wide_staged_dev);
   m.def("tree_grad_hist", &ytk_tree_grad_hist);

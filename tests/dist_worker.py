@@ -45,6 +45,9 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
     model = tr.train()
     tl, te = tr._losses()
     owner = bool(getattr(tr.builder, "owner", False))
+    peer = getattr(tr.builder, "peer", None)
+    if peer is not None:
+        peer.check()
     if comm.log is not None:  # every rank's collective sequence (deadlock-freedom check)
         with open(os.path.join(out, f"comm_log_{comm.rank}.json"), "w") as f:
             json.dump(comm.log, f)
@@ -52,7 +55,8 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
         with open(os.path.join(out, "model.txt"), "w") as f:
             f.write(model.dumps())
         with open(os.path.join(out, "res.json"), "w") as f:
-            json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats}, f)
+            json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats,
+                       "peer_calls": peer.calls if peer is not None else 0}, f)
 
 
 def write_lines(path, n, seed):

@@ -127,7 +127,8 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
 @pytest.mark.gpu
 @pytest.mark.parametrize("task,world,mode", [("gbdt", 2, "allreduce"), ("gbdt", 4, "allreduce"),
                                              ("gbdt_loss", 3, "allreduce"), ("gbdt", 3, "owner"),
-                                             ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner")])
+                                             ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner"),
+                                             ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
@@ -137,10 +138,15 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": mode, "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0",
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": "allreduce" if mode == "peer" else mode,
+           "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0",
            "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}  # small shards: keep the overlap covered
+    if mode == "peer":  # one-shot IPC peer-memory histogram all-reduce (the ranks share the GPU)
+        env["YTK_PEER_REDUCE"] = "1"
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
-    _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
+    res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
+    if mode == "peer":
+        assert res["peer_calls"] > 0
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
     _same_collective_sequence(tmp_path / f"w{world}", world)
 

@@ -23,6 +23,7 @@ import torch
 
 from ...ops import gbdt as gops
 from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
+from ...parallel import peer as peer_mod
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams, resolve_hist_sync
@@ -217,6 +218,14 @@ class DeviceLevelBuilder:
         # level's build is ~10-20 us, less than the launch latency of the second collective.
         self.overlap = (os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
                         and self.N >= int(os.environ.get("YTK_HIST_OVERLAP_MIN_ROWS", "2000000")))
+        # YTK_PEER_REDUCE=1: the level messages go through the one-shot peer-memory all-reduce
+        # (parallel/peer.py) instead of RCCL -- all-reduce mode only; stream-ordered, so the
+        # half-level overlap is not needed
+        self.peer = None
+        if peer_mod.enabled(self.comm) and not self.owner:
+            cap = max([1] + [self.level_slots[c][2] - self.level_slots[c][0] for c in self.level_slots]) * slot_elems
+            self.peer = peer_mod.PeerReduce(self.comm, cap)
+            self.overlap = False
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
@@ -293,6 +302,13 @@ class DeviceLevelBuilder:
         if glob is not None:
             out[14] = glob
         return out
+
+    def _hist_allreduce(self, t: torch.Tensor):
+        """A level's histogram (+ count) slots: RCCL, or the peer-memory path."""
+        if self.peer is not None:
+            self.peer.allreduce_(t.view(-1))
+        else:
+            self.comm.allreduce_(t)
 
     def _owner_reduce(self, base: int, nslots: int, ncs: int = 0):
         """Reduce-scatter slots [base, base + nslots) by feature block (+ the ncs count slots
@@ -458,7 +474,7 @@ class DeviceLevelBuilder:
                 h.hist_wide_rm(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                                nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5) if n_dev is None else n_dev,
                                ptr(self.scales), work_off, ptr(self.staging) if self.staged else 0, slot_base,
-                               nslots, s)
+                               nslots, ptr(self.binsT), self.binsT.shape[1], s)
                 return
             if self.staged:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
@@ -481,7 +497,7 @@ class DeviceLevelBuilder:
             if self.owner:
                 self._owner_reduce(0, 1)
             else:
-                self.comm.allreduce_(self.hist[0:1])
+                self._hist_allreduce(self.hist[0:1])
             tm.mark("build_hist_comm")
         if self.fuse_split_plan:
             self._split_plan(ptrs, fp, fmask, f0, 1, s)
@@ -589,7 +605,7 @@ class DeviceLevelBuilder:
                     if self.owner:
                         self._owner_reduce(base, half, ncs)
                     else:
-                        self.comm.allreduce_(self.hist[base:base + half + ncs])
+                        self._hist_allreduce(self.hist[base:base + half + ncs])
                     tm.mark("build_hist_comm")
             if self.fuse_split_plan:
                 self._split_plan(ptrs, fp, fmask, f0, 1 << c, s)

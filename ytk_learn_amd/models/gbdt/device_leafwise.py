@@ -26,6 +26,7 @@ import torch
 
 from ...ops import gbdt as gops
 from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
+from ...parallel import peer as peer_mod
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams
@@ -137,6 +138,9 @@ class DeviceLeafBuilder:
         self.slot_elems = B * F * 2
         self.msg = (torch.empty(ml * (self.slot_elems + CUR_STRIDE), dtype=torch.int64, device=dev)
                     if self.comm.is_dist else None)
+        # YTK_PEER_REDUCE=1: batch messages over the one-shot peer-memory all-reduce
+        self.peer = (peer_mod.PeerReduce(self.comm, max(self.msg.numel(), self.slot_elems))
+                     if peer_mod.enabled(self.comm) else None)
         self._root_glob = None
 
     # ------------------------------------------------------------------ setup
@@ -316,7 +320,7 @@ class DeviceLeafBuilder:
         h.lw_step(hd, 0, s)
         if dist:
             self._hist(h, rows0, gh0, s)
-            self.comm.allreduce_(self.hist[0:1])  # the root slot
+            self._allreduce(self.hist[0:1].view(-1))  # the root slot
             self._split(h, fmask, f0, s)
             tm.mark("root")
             it = self._build_dist(h, hd, rows0, gh0, fmask, f0, s)
@@ -389,12 +393,18 @@ class DeviceLeafBuilder:
             k = int(dh[2])
             n = k * (self.slot_elems + CUR_STRIDE)
             h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 0, s)
-            self.comm.allreduce_(self.msg[:n])
+            self._allreduce(self.msg[:n])
             h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 1, s)
             self._split(h, fmask, f0, s)
         if idle is not None:
             idle()
         return it
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.peer is not None:
+            self.peer.allreduce_(t)
+        else:
+            self.comm.allreduce_(t)
 
     def _finish(self, h, s, it) -> DeviceTree:
         self.timer.mark("batches")

@@ -136,24 +136,26 @@ class ExactGreedyBuilder:
             K = len(expand)
             bnd = torch.tensor([b for b, _ in seg] + [seg[-1][1] if seg else 0], dtype=torch.int64, device=dev)
             cnt = (bnd[1:] - bnd[:-1])
-            # node sums (initNodeStats): column 0's segments hold each node's rows
+            # node sums (initNodeStats): column 0's contiguous node segments, exact int64
+            # prefix differences (no atomics)
             rows0 = order[0]
-            sums = torch.zeros((K, 2), dtype=torch.int64, device=dev).index_add_(0, pos_node, q[rows0])
+            sums = self._seg_sums(q[rows0], bnd)
             Gd = sums.double() * inv  # [K, 2] float64 totals
             root_gain = self._gain(Gd[:, 0], Gd[:, 1]).float()
             can = (Gd[:, 1] >= 2.0 * mcw) & (cnt >= max(p.min_split_samples, 0))  # canSplit
-            best_chg = torch.full((K,), float("-inf"), dtype=torch.float32, device=dev)
-            best_f = torch.full((K,), -1, dtype=torch.int64, device=dev)
-            best_v = torch.zeros(K, dtype=torch.float32, device=dev)
             first = torch.zeros(n, dtype=torch.bool, device=dev)
             first[bnd[:-1][cnt > 0]] = True  # the first row of a node is never a candidate
-            for c0 in range(0, len(feats), self.chunk):
+            nf = len(feats)
+            mx_all = torch.empty((nf, K), dtype=torch.float32, device=dev)
+            thr_all = torch.empty((nf, K), dtype=torch.float32, device=dev)
+            ar = torch.arange(n, dtype=torch.float64, device=dev)
+            for c0 in range(0, nf, self.chunk):
                 fs = torch.from_numpy(feats[c0:c0 + self.chunk]).to(dev)
+                C = fs.numel()
                 o = order[fs]                                   # [C, n] rows
                 v = torch.gather(self.XT[fs], 1, o)             # [C, n] values, sorted per node
                 gq = q[o]                                       # [C, n, 2] int64
-                cs = torch.cumsum(gq, dim=1)
-                excl = cs - gq                                  # sums of the rows before i
+                excl = torch.cumsum(gq, dim=1) - gq             # sums of the rows before i
                 base = excl[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K, 2] node start
                 left = excl - base[:, pos_node]                 # left sums at each candidate
                 tot = sums[pos_node]                            # [n, 2]
@@ -166,24 +168,26 @@ class ExactGreedyBuilder:
                 chg = (self._gain(Ld[..., 0], Ld[..., 1]) + self._gain(Rd[..., 0], Rd[..., 1])
                        - root_gain[pos_node][None].double()).float()
                 chg = torch.where(ok, chg, torch.full_like(chg, float("-inf")))
-                # per (feature, node): max lossChg, its first position (scan order)
-                C = o.shape[0]
-                idx = pos_node[None].expand(C, n)
-                mx_fn = torch.full((C, K), float("-inf"), dtype=torch.float32, device=dev)
-                mx_fn.scatter_reduce_(1, idx, chg, "amax")
-                ar = torch.arange(n, dtype=torch.int64, device=dev)[None].expand(C, n)
-                hit = (chg == mx_fn.gather(1, idx)) & ok
-                pos_fn = torch.full((C, K), n, dtype=torch.int64, device=dev)
-                pos_fn.scatter_reduce_(1, idx, torch.where(hit, ar, torch.full_like(ar, n)), "amin")
-                for ci in range(C):  # features in ascending order: replace only if strictly greater
-                    upd = mx_fn[ci] > best_chg
-                    if bool(upd.any()):
-                        pi = pos_fn[ci].clamp(max=max(n - 1, 0))
-                        thr = (v[ci, pi] + v[ci, (pi - 1).clamp(min=0)]) * np.float32(0.5)
-                        best_chg = torch.where(upd, mx_fn[ci], best_chg)
-                        best_f = torch.where(upd, fs[ci].expand(K), best_f)
-                        best_v = torch.where(upd, thr, best_v)
-                del o, v, gq, cs, excl, base, left, Ld, Rd, chg, hit, ar, idx
+                # per (feature, node): max lossChg and its FIRST position (the scan order),
+                # segmented reductions over the contiguous node segments
+                lens = cnt.expand(C, K).contiguous()
+                mx = torch.segment_reduce(chg, "max", lengths=lens, axis=1, initial=float("-inf"))
+                hit = (chg == mx[:, pos_node]) & ok
+                pf = torch.segment_reduce(torch.where(hit, ar.expand(C, n), torch.full((C, n), float(n), dtype=torch.float64,
+                                                                                        device=dev)),
+                                          "min", lengths=lens, axis=1, initial=float(n)).to(torch.int64)
+                pi = pf.clamp(max=max(n - 1, 0))
+                thr = (torch.gather(v, 1, pi) + torch.gather(v, 1, (pi - 1).clamp(min=0))) * np.float32(0.5)
+                mx_all[c0:c0 + C] = mx
+                thr_all[c0:c0 + C] = thr
+                del o, v, gq, excl, base, left, Ld, Rd, chg, hit, dv, ok
+            # features in ascending order, replaced only when strictly greater: the max
+            # lossChg, ties -> the lowest feature (SplitInfo.needReplace)
+            best_chg = mx_all.max(dim=0).values if nf else torch.full((K,), float("-inf"), device=dev)
+            fi = torch.argmax((mx_all == best_chg[None]).to(torch.int8), dim=0)  # first feature at the max
+            best_f = torch.from_numpy(feats).to(dev)[fi]
+            best_v = thr_all.gather(0, fi[None])[0]
+            best_f = torch.where(torch.isfinite(best_chg), best_f, torch.full_like(best_f, -1))
             # --- tree update (findSplit :327-342), host side over the level's nodes
             bc, bf, bv = best_chg.cpu().numpy(), best_f.cpu().numpy(), best_v.cpu().numpy()
             Gh = Gd.cpu().numpy()
@@ -218,10 +222,11 @@ class ExactGreedyBuilder:
         if expand:
             K = len(expand)
             rows0 = order[0]
-            sums = torch.zeros((K, 2), dtype=torch.int64, device=dev).index_add_(0, pos_node, q[rows0])
+            bnd = torch.tensor([b for b, _ in seg] + [seg[-1][1] if seg else 0], dtype=torch.int64, device=dev)
+            sums = self._seg_sums(q[rows0], bnd)
             Gd = sums.double() * inv
             vals = (self._value(Gd[:, 0], Gd[:, 1]).float().cpu().numpy()) * lr32
-            cnts = torch.bincount(pos_node, minlength=K).cpu().numpy() if n > 0 else np.zeros(K, np.int64)
+            cnts = (bnd[1:] - bnd[:-1]).cpu().numpy()
             Gh = Gd.cpu().numpy()
             for k, nid in enumerate(expand):
                 tree.set_leaf(nid, float(vals[k]))
@@ -237,6 +242,14 @@ class ExactGreedyBuilder:
         self.last_stats.trees = 1
         self.total_stats.add(self.last_stats)
         return tree
+
+    @staticmethod
+    def _seg_sums(x: torch.Tensor, bnd: torch.Tensor) -> torch.Tensor:
+        """Sums of x [n, ...] over the contiguous segments [bnd[k], bnd[k + 1]) (exact for
+        integers): prefix-sum differences, no atomics."""
+        z = torch.zeros((1,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        cs = torch.cat([z, torch.cumsum(x, 0)])
+        return cs[bnd[1:]] - cs[bnd[:-1]]
 
     def leaf_ids_of(self, tree: Tree) -> torch.Tensor:
         """Leaf node id of every training row (raw-threshold walk; l1 leaf refine)."""
@@ -261,8 +274,7 @@ class ExactGreedyBuilder:
         left_row[rows0] = val < go_thr[pos_node]              # resetPosition: value < cond -> left
         alive_pos = split[pos_node]                           # rows staying in the order
         # children sizes (identical for every column)
-        nl = torch.zeros(K, dtype=torch.int64, device=dev).index_add_(
-            0, pos_node, (left_row[rows0] & alive_pos).to(torch.int64))
+        nl = self._seg_sums((left_row[rows0] & alive_pos).to(torch.int64), bnd)
         cnt = bnd[1:] - bnd[:-1]
         nr = torch.where(split, cnt - nl, torch.zeros_like(cnt))
         nl = torch.where(split, nl, torch.zeros_like(nl))

@@ -127,7 +127,10 @@ def hist_build(bins, F, ghp, rows, work, hist, B, sg, sh, staging=None, slot_bas
                 assert staging.numel() >= nwork * hist_cols(F) * B * 2
             h.hist_wide_rm(ptr(bins), stride, F, ptr(ghp), ptr(rows), ptr(work), nwork, ptr(hist), B,
                            float(sg), float(sh), 0, 0, 0, ptr(staging) if use_st else 0, slot_base,
-                           nslots if use_st else 0, stream(bins))
+                           nslots if use_st else 0,
+                           ptr(binsT) if (binsT is not None and binsT.dtype == torch.int16 and binsT.is_contiguous()
+                                          and binsT.shape[0] == F) else 0,
+                           binsT.shape[1] if binsT is not None else 0, stream(bins))
         else:
             h.hist_fx_global(ptr(bins), _bin_bytes(bins), stride, F, ptr(ghp), ptr(rows), ptr(work),
                              nwork, ptr(hist), B, float(sg), float(sh), stream(bins))
