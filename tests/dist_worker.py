@@ -140,6 +140,33 @@ def run_binning(comm, out, device):
                        "fill": fill.tolist()}, f)
 
 
+def run_samplers(comm, out, device):
+    """Non-quantile samplers (no_sample, sample_by_precision, sample_by_cnt, sample_by_rate) on
+    row shards of one global dataset: candidates through ragged tensor all-gathers."""
+    from ytk_learn_amd.models.gbdt import binning as bn
+    g = np.random.default_rng(5)
+    n = 6000
+    X = np.stack([g.integers(0, 300, n).astype(np.float32),
+                  np.round(g.normal(size=n) * 50, 2).astype(np.float32),
+                  np.exp(g.normal(size=n)).astype(np.float32)], 1)
+    Xs = torch.from_numpy(X[comm.rank::comm.world]).to(device)
+    res = {}
+    res["no_sample"] = bn.feature_candidates(Xs[:, 0].contiguous(), None, bn.SamplerSpec(type="no_sample"),
+                                             comm).tolist()
+    res["precision"] = bn.feature_candidates(
+        Xs[:, 2].contiguous(), None, bn.SamplerSpec(type="sample_by_precision", dot_precision=2, use_log=True,
+                                                    use_min_max=True), comm).tolist()
+    # random samplers: the result must be the union of what every rank selected
+    for t, kw in (("sample_by_cnt", {"max_cnt": 100}), ("sample_by_rate", {"sample_rate": 0.3, "min_cnt": 10})):
+        got = bn.feature_candidates(Xs[:, 1].contiguous(), None, bn.SamplerSpec(type=t, **kw), comm, seed=3)
+        res[t + "_size"] = len(got)
+        res[t + "_sorted_unique"] = bool(np.all(np.diff(got) > 0))
+    res["ops"] = sorted({op for op, _, _ in (comm.log or [])})
+    if comm.rank == 0:
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump(res, f)
+
+
 def main():
     task, out, device = sys.argv[1], sys.argv[2], sys.argv[3]
     comm = Comm.from_env(device)
@@ -157,6 +184,8 @@ def main():
             run_linear(comm, out, dev, task.split("_")[0], sgd=True)
         elif task == "binning":
             run_binning(comm, out, dev)
+        elif task == "samplers":
+            run_samplers(comm, out, dev)
         elif task == "comm":
             run_comm(comm, out, dev)
         else:

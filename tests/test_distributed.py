@@ -65,6 +65,20 @@ def test_binning_tensor_exchange_matches_per_feature(tmp_path, world):
     assert all(np.isfinite(res["fill"]))
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_non_quantile_samplers_tensor_union_world_n(tmp_path, world):
+    """no_sample / sample_by_precision candidates over row shards == the single-rank ones
+    (the union travels as ragged tensors, not pickled objects); the random samplers return a
+    sorted union."""
+    r1 = _run("samplers", tmp_path / "w1", 1, extra_env={"YTK_COMM_LOG": "1"})
+    rn = _run("samplers", tmp_path / f"w{world}", world, extra_env={"YTK_COMM_LOG": "1"})
+    assert rn["no_sample"] == r1["no_sample"]
+    np.testing.assert_allclose(rn["precision"], r1["precision"], rtol=1e-6)
+    for t in ("sample_by_cnt", "sample_by_rate"):
+        assert rn[t + "_sorted_unique"] and rn[t + "_size"] > 0
+    assert "allgather_object" not in rn["ops"]  # no pickled collectives
+
+
 @pytest.mark.parametrize("task", ["gbdt", "gbdt_loss"])
 def test_gbdt_world2_identical_to_world1(tmp_path, task):
     r1 = _run(task, tmp_path / "w1", 1)

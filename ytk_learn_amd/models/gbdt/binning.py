@@ -77,14 +77,20 @@ def merge_split_gap(vals: np.ndarray, gap: float) -> np.ndarray:
     return vals[keep]
 
 
+def _union(vals: torch.Tensor, comm: Comm) -> np.ndarray:
+    """Sorted union of every rank's values (allreduceMapSetUnion, SampleManager.java:107-155)
+    through a ragged TENSOR all-gather (sizes, then a padded fixed-shape all-gather) instead
+    of pickled objects."""
+    parts = comm.allgather_ragged(vals.float().contiguous())
+    return torch.unique(torch.cat(parts)).cpu().numpy().astype(np.float32)
+
+
 def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: SamplerSpec,
                        comm: Comm, seed: int = 0) -> np.ndarray:
     """Sorted candidate split values for one feature column (already NaN-filled)."""
     t = spec.type
     if t == "no_sample":
-        vals = torch.unique(x)
-        allv = comm.allgather_object(vals.cpu().numpy())
-        out = np.unique(np.concatenate(allv).astype(np.float32))
+        out = _union(torch.unique(x), comm)
         return merge_split_gap(out, spec.min_split_gap) if spec.min_split_gap > 0 else out
     if t == "sample_by_cnt":
         # reservoir of max_cnt values per worker, union across workers
@@ -93,16 +99,14 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
         if vals.numel() > spec.max_cnt:
             sel = torch.randperm(vals.numel(), generator=g)[: spec.max_cnt].to(vals.device)
             vals = vals[sel]
-        allv = comm.allgather_object(vals.cpu().numpy())
-        return np.unique(np.concatenate(allv).astype(np.float32))
+        return _union(vals, comm)
     if t == "sample_by_rate":
         g = torch.Generator(device="cpu").manual_seed(seed + comm.rank)
         vals = torch.unique(x)
         if vals.numel() > spec.min_cnt:
             keep = torch.rand(vals.numel(), generator=g) < spec.sample_rate
             vals = vals[keep.to(vals.device)]
-        allv = comm.allgather_object(vals.cpu().numpy())
-        return np.unique(np.concatenate(allv).astype(np.float32))
+        return _union(vals, comm)
     if t == "sample_by_precision":
         return _precision_candidates(x, spec, comm)
     if t != "sample_by_quantile":
@@ -122,8 +126,7 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
         g_distinct = int(comm.allreduce_scalars([vals.numel()], dtype=torch.int64)[0])
     qs = torch.arange(1, spec.max_cnt + 1, dtype=torch.float64, device=x.device) / spec.max_cnt
     if g_distinct <= spec.max_cnt:
-        allv = comm.allgather_object(vals.cpu().numpy())
-        return np.unique(np.concatenate(allv).astype(np.float32))
+        return _union(vals, comm)
     if not comm.is_dist:
         out = _weighted_quantile_values(vals, wv, qs)
         return np.unique(out.cpu().numpy().astype(np.float32))
@@ -199,8 +202,7 @@ def _precision_candidates(x, spec: SamplerSpec, comm: Comm) -> np.ndarray:
         xv = (xv - lo) / rng
     scale = 10.0 ** spec.dot_precision
     q = torch.unique(torch.trunc(xv * scale) / scale)
-    allv = comm.allgather_object(q.cpu().numpy())
-    q = np.unique(np.concatenate(allv))
+    q = torch.unique(torch.cat(comm.allgather_ragged(q.double().contiguous()))).cpu().numpy()
     if spec.use_min_max:
         q = q * ((hi - lo) if hi > lo else 1.0) + lo
     if spec.use_log:

@@ -119,6 +119,8 @@ class ExactGreedyBuilder:
         q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
         q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)
         inv = torch.tensor([1.0 / sg, 1.0 / sh], dtype=torch.float64, device=dev)
+        inv_g, inv_h = 1.0 / sg, 1.0 / sh
+        qT = q.t().contiguous()  # [2, N]
         mcw, l1, l2, mal = self.gpv
         lr32 = np.float32(p.learning_rate)
         msl = float(np.float32(p.min_split_loss))
@@ -148,39 +150,38 @@ class ExactGreedyBuilder:
             nf = len(feats)
             mx_all = torch.empty((nf, K), dtype=torch.float32, device=dev)
             thr_all = torch.empty((nf, K), dtype=torch.float32, device=dev)
-            ar = torch.arange(n, dtype=torch.float64, device=dev)
+            pad = self._pad_layout(bnd, cnt, pos_node, K, n)
             for c0 in range(0, nf, self.chunk):
                 fs = torch.from_numpy(feats[c0:c0 + self.chunk]).to(dev)
                 C = fs.numel()
                 o = order[fs]                                   # [C, n] rows
                 v = torch.gather(self.XT[fs], 1, o)             # [C, n] values, sorted per node
-                gq = q[o]                                       # [C, n, 2] int64
-                excl = torch.cumsum(gq, dim=1) - gq             # sums of the rows before i
-                base = excl[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K, 2] node start
-                left = excl - base[:, pos_node]                 # left sums at each candidate
-                tot = sums[pos_node]                            # [n, 2]
-                Ld = left.double() * inv
-                Rd = (tot[None] - left).double() * inv
+                # (g, h) as separate [C, n] planes: the prefix sums run along the innermost
+                # dimension (torch's parallel scan; a middle-dimension scan is sequential)
+                lg, lh = [], []
+                for comp in (0, 1):
+                    x = qT[comp][o]                             # [C, n] int64
+                    excl = torch.cumsum(x, dim=1) - x           # sums of the rows before i
+                    base = excl[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K] node start
+                    (lg if comp == 0 else lh).append(excl - base[:, pos_node])
+                left_g, left_h = lg[0], lh[0]
+                Lg, Lh = left_g.double() * inv_g, left_h.double() * inv_h
+                Rg = (sums[pos_node, 0][None] - left_g).double() * inv_g
+                Rh = (sums[pos_node, 1][None] - left_h).double() * inv_h
                 dv = torch.zeros_like(v)
                 dv[:, 1:] = (v[:, 1:] - v[:, :-1]).abs()
-                ok = (~first[None]) & (dv > MIN_FEA_SPLIT_GAP) & (left[..., 1] != 0)
-                ok &= (Ld[..., 1] >= mcw) & (Rd[..., 1] >= mcw) & can[pos_node][None]
-                chg = (self._gain(Ld[..., 0], Ld[..., 1]) + self._gain(Rd[..., 0], Rd[..., 1])
-                       - root_gain[pos_node][None].double()).float()
+                ok = (~first[None]) & (dv > MIN_FEA_SPLIT_GAP) & (left_h != 0)
+                ok &= (Lh >= mcw) & (Rh >= mcw) & can[pos_node][None]
+                chg = (self._gain(Lg, Lh) + self._gain(Rg, Rh) - root_gain[pos_node][None].double()).float()
                 chg = torch.where(ok, chg, torch.full_like(chg, float("-inf")))
-                # per (feature, node): max lossChg and its FIRST position (the scan order),
-                # segmented reductions over the contiguous node segments
-                lens = cnt.expand(C, K).contiguous()
-                mx = torch.segment_reduce(chg, "max", lengths=lens, axis=1, initial=float("-inf"))
-                hit = (chg == mx[:, pos_node]) & ok
-                pf = torch.segment_reduce(torch.where(hit, ar.expand(C, n), torch.full((C, n), float(n), dtype=torch.float64,
-                                                                                        device=dev)),
-                                          "min", lengths=lens, axis=1, initial=float(n)).to(torch.int64)
-                pi = pf.clamp(max=max(n - 1, 0))
+                # per (feature, node): max lossChg and its FIRST position (the scan order), as
+                # ONE int64 max over keys (orderable lossChg bits << 31 | ~position), reduced
+                # per tile of a segment-aligned padded layout, then over each node's tiles
+                pi, mx = self._seg_argmax(chg, pad)
                 thr = (torch.gather(v, 1, pi) + torch.gather(v, 1, (pi - 1).clamp(min=0))) * np.float32(0.5)
                 mx_all[c0:c0 + C] = mx
                 thr_all[c0:c0 + C] = thr
-                del o, v, gq, excl, base, left, Ld, Rd, chg, hit, dv, ok
+                del o, v, lg, lh, left_g, left_h, Lg, Lh, Rg, Rh, chg, dv, ok
             # features in ascending order, replaced only when strictly greater: the max
             # lossChg, ties -> the lowest feature (SplitInfo.needReplace)
             best_chg = mx_all.max(dim=0).values if nf else torch.full((K,), float("-inf"), device=dev)
@@ -243,13 +244,46 @@ class ExactGreedyBuilder:
         self.total_stats.add(self.last_stats)
         return tree
 
+    TILE = 1024
+
+    def _pad_layout(self, bnd, cnt, pos_node, K, n):
+        """Segment-aligned padded positions: node k's rows start on a tile boundary, so every
+        tile of TILE positions belongs to one node."""
+        T = self.TILE
+        tiles = (cnt + T - 1) // T
+        pstart = (torch.cumsum(tiles, 0) - tiles) * T
+        ppos = torch.arange(n, device=self.dev) - bnd[:-1][pos_node] + pstart[pos_node]
+        ntile = int(tiles.sum())
+        tile_seg = torch.repeat_interleave(torch.arange(K, device=self.dev), tiles)
+        return ppos, ntile, tile_seg, K
+
+    def _seg_argmax(self, chg: torch.Tensor, pad):
+        """(first position of the max, the max) of chg [C, n] over each node segment."""
+        ppos, ntile, tile_seg, K = pad
+        C, n = chg.shape
+        T = self.TILE
+        u = chg.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        u = torch.where(u >= 0x80000000, 0xFFFFFFFF - u, u | 0x80000000)  # order-preserving
+        key = (u << 31) | (0x7FFFFFFF - torch.arange(n, device=self.dev))[None]
+        kp = torch.full((C, max(ntile, 1) * T), -1, dtype=torch.int64, device=self.dev)
+        kp[:, ppos] = key
+        tmax = kp.view(C, -1, T).amax(dim=2)[:, :ntile]
+        best = torch.full((C, K), -1, dtype=torch.int64, device=self.dev)
+        best.scatter_reduce_(1, tile_seg[None].expand(C, ntile), tmax, "amax")
+        pos = (0x7FFFFFFF - (best & 0x7FFFFFFF)).clamp(0, max(n - 1, 0))
+        mx = torch.where(best >= 0, torch.gather(chg, 1, pos), torch.full_like(pos, 0, dtype=chg.dtype)
+                         .fill_(float("-inf")))
+        return pos, mx
+
     @staticmethod
     def _seg_sums(x: torch.Tensor, bnd: torch.Tensor) -> torch.Tensor:
         """Sums of x [n, ...] over the contiguous segments [bnd[k], bnd[k + 1]) (exact for
         integers): prefix-sum differences, no atomics."""
-        z = torch.zeros((1,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        cs = torch.cat([z, torch.cumsum(x, 0)])
-        return cs[bnd[1:]] - cs[bnd[:-1]]
+        xt = x.reshape(x.shape[0], -1).t().contiguous()  # scan along the innermost dimension
+        z = torch.zeros((xt.shape[0], 1), dtype=x.dtype, device=x.device)
+        cs = torch.cat([z, torch.cumsum(xt, 1)], 1)
+        out = (cs[:, bnd[1:]] - cs[:, bnd[:-1]]).t()
+        return out.reshape((bnd.numel() - 1,) + tuple(x.shape[1:]))
 
     def leaf_ids_of(self, tree: Tree) -> torch.Tensor:
         """Leaf node id of every training row (raw-threshold walk; l1 leaf refine)."""
