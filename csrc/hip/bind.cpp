@@ -73,7 +73,7 @@ void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintpt
                    uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
-                      int, int, uintptr_t);
+                      int, int, uintptr_t, uintptr_t);
 // fm.hip
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t);

@@ -122,11 +122,15 @@ __global__ __launch_bounds__(256) void ffm_grad_csc_kernel(
     const long long* __restrict__ csc_pos, const long long* __restrict__ indptr,
     const unsigned* __restrict__ pk, int sh, const float* __restrict__ val,
     const float* __restrict__ Vt, long long nfeat, int nfield, int k, const float* __restrict__ coef,
-    float* __restrict__ part, int skip_feat) {
+    float* __restrict__ part, int skip_feat, const int* __restrict__ chunk_order) {
   extern __shared__ float lds_acc[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long ch = blockIdx.x * (long long)kCscWaves + wave;
-  if (ch >= nch) return;  // no block-level barriers below
+  const long long slot = blockIdx.x * (long long)kCscWaves + wave;
+  if (slot >= nch) return;  // no block-level barriers below
+  // chunk_order (optional): the processing order -- chunks grouped by (row tile, field of the
+  // column), so the gathers of consecutive waves stay in ONE field's 16-B latent slice
+  // Vt[f_i] (MALL / L2 resident) instead of spanning every field's slice
+  const long long ch = chunk_order ? (long long)chunk_order[slot] : slot;
   const int J = nfield * k;
   const unsigned mask = (1u << sh) - 1u;
   const long long fstride = nfeat * k;  // Vt is [nfield][nfeat][k]
@@ -266,7 +270,7 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
 void ytk_ffm_grad_csc(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows,
                       uintptr_t csc_vals, uintptr_t csc_pos, uintptr_t indptr, uintptr_t pk, int sh,
                       uintptr_t val, uintptr_t Vt, long long nfeat, int nfield, int k, uintptr_t coef,
-                      uintptr_t part, int skip_feat, int distinct_fields, uintptr_t stream) {
+                      uintptr_t part, int skip_feat, int distinct_fields, uintptr_t chunk_order, uintptr_t stream) {
   if (nch <= 0 || k <= 0) return;
   const int J = nfield * k;
   if (J > 2048) throw std::invalid_argument("ffm_grad_csc: nfield*k > 2048");  // 4 x 8 KB LDS
@@ -281,7 +285,7 @@ void ytk_ffm_grad_csc(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
                      (const int*)csc_rows, (const float*)csc_vals, (const long long*)csc_pos,  \
                      (const long long*)indptr, (const unsigned*)pk, sh, (const float*)val,     \
                      (const float*)Vt, nfeat, nfield, k, (const float*)coef, (float*)part,     \
-                     skip_feat)
+                     skip_feat, (const int*)chunk_order)
   if (vec4) {
     if (distinct_fields) YTK_FFM_CSC(true, true); else YTK_FFM_CSC(true, false);
   } else {

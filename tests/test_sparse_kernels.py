@@ -182,6 +182,18 @@ def test_ffm_csc_backward_one_hot(cuda):
     g2 = torch.zeros_like(V).to(cuda)
     ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g2)
     assert torch.equal(g2, gg)
+    # the field-grouped chunk processing order only changes WHEN a chunk runs: bitwise equal
+    assert Xg._ffm_layout[1][4] is not None
+    Xo = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    import os
+    os.environ["YTK_FFM_FIELD_ORDER"] = "0"
+    try:
+        g3 = torch.zeros_like(V).to(cuda)
+        ffm_backward_csc(Xo, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g3)
+    finally:
+        del os.environ["YTK_FFM_FIELD_ORDER"]
+    assert Xo._ffm_layout[1][4] is None
+    assert torch.equal(g3, gg)
 
 
 @pytest.mark.gpu

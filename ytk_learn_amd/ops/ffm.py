@@ -6,8 +6,11 @@ Reference: ``J/optimizer/FFMHoagOptimizer.java:90-210``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
+from . import sparse as sparse_mod
 from ._ext import check_cuda, hip, ptr, stream
 
 
@@ -102,7 +105,18 @@ def _csc_layout(X, fld, nfield: int):
     code = X.indices.to(torch.int64) | (f64 << sh)
     code = torch.where(code >= 2 ** 31, code - 2 ** 32, code).to(torch.int32).contiguous()  # uint32 bits
     vals = None if bool((X.values == 1).all()) else X.values
-    lay = (distinct, code, sh, vals)
+    # chunk processing order: (row tile, field of the chunk's column), stable -- the gathers
+    # of concurrently running chunks then stay inside one field's latent slice
+    # (YTK_FFM_FIELD_ORDER=0: CSC order)
+    order = None
+    if X._csc is None:
+        X._build_csc()
+    if os.environ.get("YTK_FFM_FIELD_ORDER", "1") != "0" and X.n_chunks > 0:
+        e0 = X.csc_perm[X.chunk_beg]                                 # first entry of each chunk (CSR pos)
+        tile = X.rows_of_nnz[e0].to(torch.int64) // max(1, sparse_mod.ROW_TILE if X.n > sparse_mod.ROW_TILE else X.n + 1)
+        key = tile * nfield + f64[e0]
+        order = torch.sort(key, stable=True).indices.to(torch.int32).contiguous()
+    lay = (distinct, code, sh, vals, order)
     X._ffm_layout = (key, lay)
     return lay
 
@@ -117,7 +131,7 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
                             skip_feat=skip_feat)
     if X._csc is None:
         X._build_csc()
-    distinct, code, sh, vals = lay
+    distinct, code, sh, vals, order = lay
     J = nfield * k
     check_cuda(fld, V, coef, gV)
     Vt = V.view(X.ncols, nfield, k).transpose(0, 1).contiguous()  # [nfield][F][k]
@@ -129,6 +143,6 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
     # reuses a row's latent blocks across its pairs -- not by the LDS accumulator)
     h.ffm_grad_csc(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
                    ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0, ptr(Vt),
-                   X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), s)
+                   X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), ptr(order), s)
     h.chunk_reduce(ptr(X.chunk_ptr), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, ptr(X.chunk_ids), s)
     return gV
