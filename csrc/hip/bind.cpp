@@ -73,7 +73,9 @@ void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintpt
                    uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
-                      int, int, uintptr_t, uintptr_t);
+                      int, int, uintptr_t);
+void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                         long long, uintptr_t, int, uintptr_t, long long, int, int, uintptr_t, uintptr_t);
 // fm.hip
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t);
@@ -159,6 +161,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("chunk_reduce", &ytk_chunk_reduce);
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
+  m.def("ffm_grad_stream", &ytk_ffm_grad_stream);
   m.def("dot", &ytk_dot);
   m.def("fm_forward", &ytk_fm_forward);
   m.def("fm_backward", &ytk_fm_backward);

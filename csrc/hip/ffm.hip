@@ -122,15 +122,11 @@ __global__ __launch_bounds__(256) void ffm_grad_csc_kernel(
     const long long* __restrict__ csc_pos, const long long* __restrict__ indptr,
     const unsigned* __restrict__ pk, int sh, const float* __restrict__ val,
     const float* __restrict__ Vt, long long nfeat, int nfield, int k, const float* __restrict__ coef,
-    float* __restrict__ part, int skip_feat, const int* __restrict__ chunk_order) {
+    float* __restrict__ part, int skip_feat) {
   extern __shared__ float lds_acc[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long slot = blockIdx.x * (long long)kCscWaves + wave;
-  if (slot >= nch) return;  // no block-level barriers below
-  // chunk_order (optional): the processing order -- chunks grouped by (row tile, field of the
-  // column), so the gathers of consecutive waves stay in ONE field's 16-B latent slice
-  // Vt[f_i] (MALL / L2 resident) instead of spanning every field's slice
-  const long long ch = chunk_order ? (long long)chunk_order[slot] : slot;
+  const long long ch = blockIdx.x * (long long)kCscWaves + wave;
+  if (ch >= nch) return;  // no block-level barriers below
   const int J = nfield * k;
   const unsigned mask = (1u << sh) - 1u;
   const long long fstride = nfeat * k;  // Vt is [nfield][nfeat][k]
@@ -237,6 +233,104 @@ __global__ __launch_bounds__(256) void ffm_grad_csc_kernel(
   for (int j = lane; j < J; j += 64) out[j] = acc[j];
 }
 
+// Fixed-layout, XCD-split, streamed column-ordered backward. When every row holds the same m
+// fields in the same order (one entry per field: Criteo-style data, the bias in position 0),
+// the kernel above is L2-miss bound on two random streams: its 16-B latent gathers
+// V[i_q, f_i] (one field's slice Vt[f_i] is nfeat*16 B = 16 MB at 1M features, four times an
+// XCD's 4-MB L2; 274 GB fetched per Criteo-shape pass) and the row entries it re-reads for
+// every column of the row. Here
+//  * the row POSITIONS are split into 8 groups and group g's work runs on the blocks with
+//    blockIdx % 8 == g -- one XCD (blocks are dealt round-robin over the XCDs) -- so an XCD
+//    only gathers latent rows of its own ~m/8 fields: Vt[f_i] restricted to those fields'
+//    features, an L2-sized working set;
+//  * the row entries each group needs are a setup-time expansion exp_idx[g][e][0..G) of the
+//    CSC entries (entry e's row's feature ids at the group's positions, -1 for the entry
+//    itself and skipped features), read as a coalesced nontemporal stream instead of random
+//    row reads (HBM capacity bought for bandwidth: nnz * 8G * 4 B), and the per-entry scale
+//    s[e] = coef[row] * x_e is one gathered pass per evaluation.
+// Lanes: G = ceil(m / 8) positions x E = 64 / G entries; each lane accumulates its position's
+// k floats in registers over the chunk, then the E lanes of a position are summed in a fixed
+// order through LDS -- deterministic, no atomics. A wave walks a contiguous range of chunks
+// (wave_chunk, ~equal entries per wave) so small columns do not each pay a wave launch.
+constexpr int kFixUnroll = 4;
+
+template <int KV>
+__global__ __launch_bounds__(256) void ffm_grad_stream_kernel(
+    const long long* __restrict__ wave_chunk, long long nwaves, const long long* __restrict__ chunk_beg,
+    const long long* __restrict__ chunk_end, const int* __restrict__ chunk_fa, const int* __restrict__ exp_idx,
+    const float* __restrict__ exp_val, const float* __restrict__ se, long long nnz, int G,
+    const int* __restrict__ lay_field, int m, const float* __restrict__ Vt, long long nfeat, int nfield,
+    float* __restrict__ part) {
+  __shared__ float4 red[kCscWaves][64 * KV];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = blockIdx.x & 7;
+  const long long w = (long long)(blockIdx.x >> 3) * kCscWaves + wave;
+  if (w >= nwaves) return;  // no block-level barriers below
+  constexpr int k = KV * 4;
+  const long long J = (long long)nfield * k;
+  const int E = 64 / G;
+  const int es = lane / G, qi = lane - es * G;
+  const bool lane_ok = es < E && grp * G + qi < m;
+  const long long fstride = nfeat * k;  // Vt is [nfield][nfeat][k]
+  const int* __restrict__ xi = exp_idx + (long long)grp * nnz * G;
+  const float* __restrict__ xv = exp_val ? exp_val + (long long)grp * nnz * G : nullptr;
+  const long long c0 = wave_chunk[w], c1 = wave_chunk[w + 1];
+  for (long long ch = c0; ch < c1; ++ch) {
+    const long long e0 = chunk_beg[ch], e1 = chunk_end[ch];
+    const int fa = chunk_fa[ch];  // field of the chunk's column, -1: skipped column
+    float4 acc[KV];
+#pragma unroll
+    for (int j = 0; j < KV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fa >= 0 && lane_ok) {
+      const float* vbase = Vt + (long long)fa * fstride;
+      for (long long eb = e0; eb < e1; eb += (long long)E * kFixUnroll) {
+        int iq[kFixUnroll];
+        float s[kFixUnroll];
+#pragma unroll
+        for (int u = 0; u < kFixUnroll; ++u) {
+          const long long e = eb + (long long)u * E + es;
+          iq[u] = -1;
+          s[u] = 0.f;
+          if (e < e1) {
+            iq[u] = __builtin_nontemporal_load(xi + e * G + qi);
+            s[u] = __builtin_nontemporal_load(se + e);
+            if (xv) s[u] *= __builtin_nontemporal_load(xv + e * G + qi);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kFixUnroll; ++u) {
+          if (iq[u] < 0) continue;
+          const float* vq = vbase + (long long)iq[u] * k;  // V[i_q, f_i]
+#pragma unroll
+          for (int j = 0; j < KV; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(vq + 4 * j);
+            acc[j].x += s[u] * v.x;
+            acc[j].y += s[u] * v.y;
+            acc[j].z += s[u] * v.z;
+            acc[j].w += s[u] * v.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KV; ++j) red[wave][lane * KV + j] = acc[j];
+    wave_sync();
+    if (lane < G && grp * G + lane < m) {
+      const int f_out = lay_field[grp * G + lane];
+#pragma unroll
+      for (int j = 0; j < KV; ++j) {
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int e = 0; e < E; ++e) {
+          const float4 a = red[wave][(e * G + lane) * KV + j];
+          t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+        }
+        *reinterpret_cast<float4*>(part + ch * J + (long long)f_out * k + 4 * j) = t;
+      }
+    }
+    wave_sync();
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -270,7 +364,7 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
 void ytk_ffm_grad_csc(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows,
                       uintptr_t csc_vals, uintptr_t csc_pos, uintptr_t indptr, uintptr_t pk, int sh,
                       uintptr_t val, uintptr_t Vt, long long nfeat, int nfield, int k, uintptr_t coef,
-                      uintptr_t part, int skip_feat, int distinct_fields, uintptr_t chunk_order, uintptr_t stream) {
+                      uintptr_t part, int skip_feat, int distinct_fields, uintptr_t stream) {
   if (nch <= 0 || k <= 0) return;
   const int J = nfield * k;
   if (J > 2048) throw std::invalid_argument("ffm_grad_csc: nfield*k > 2048");  // 4 x 8 KB LDS
@@ -285,13 +379,42 @@ void ytk_ffm_grad_csc(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
                      (const int*)csc_rows, (const float*)csc_vals, (const long long*)csc_pos,  \
                      (const long long*)indptr, (const unsigned*)pk, sh, (const float*)val,     \
                      (const float*)Vt, nfeat, nfield, k, (const float*)coef, (float*)part,     \
-                     skip_feat, (const int*)chunk_order)
+                     skip_feat)
   if (vec4) {
     if (distinct_fields) YTK_FFM_CSC(true, true); else YTK_FFM_CSC(true, false);
   } else {
     if (distinct_fields) YTK_FFM_CSC(false, true); else YTK_FFM_CSC(false, false);
   }
 #undef YTK_FFM_CSC
+  YTK_LAUNCH_CHECK();
+}
+
+// Fixed-layout XCD-split streamed variant (see ffm_grad_stream_kernel): exp_idx / exp_val
+// [8][nnz][G] (G = ceil(m / 8); exp_val may be 0 for unit values), se[nnz] the per-entry
+// scales, chunk_fa[nch] the chunk's column field (-1: write zeros), lay_field[m] the field of
+// each position (a permutation of 0..nfield-1), wave_chunk[nwaves+1] the chunk range of each
+// wave. Writes every part[chunk] slot.
+void ytk_ffm_grad_stream(uintptr_t wave_chunk, long long nwaves, uintptr_t chunk_beg, uintptr_t chunk_end,
+                         uintptr_t chunk_fa, uintptr_t exp_idx, uintptr_t exp_val, uintptr_t se, long long nnz,
+                         uintptr_t lay_field, int m, uintptr_t Vt, long long nfeat, int nfield, int k,
+                         uintptr_t part, uintptr_t stream) {
+  if (nwaves <= 0) return;
+  if (m < 8 || m > 512 || m != nfield) throw std::invalid_argument("ffm_grad_stream: need 8 <= m == nfield <= 512");
+  if ((Vt & 15) || (part & 15)) throw std::invalid_argument("ffm_grad_stream: Vt / part must be 16-B aligned");
+  const int G = (m + 7) / 8;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)(8 * ((nwaves + kCscWaves - 1) / kCscWaves)));
+#define YTK_FFM_STREAM(KV)                                                                         \
+  hipLaunchKernelGGL((ffm_grad_stream_kernel<KV>), grid, dim3(64 * kCscWaves), 0, s,               \
+                     (const long long*)wave_chunk, nwaves, (const long long*)chunk_beg,            \
+                     (const long long*)chunk_end, (const int*)chunk_fa, (const int*)exp_idx,       \
+                     (const float*)exp_val, (const float*)se, nnz, G, (const int*)lay_field, m,    \
+                     (const float*)Vt, nfeat, nfield, (float*)part)
+  if (k == 4) YTK_FFM_STREAM(1);
+  else if (k == 8) YTK_FFM_STREAM(2);
+  else if (k == 16) YTK_FFM_STREAM(4);
+  else throw std::invalid_argument("ffm_grad_stream: k must be 4, 8 or 16");
+#undef YTK_FFM_STREAM
   YTK_LAUNCH_CHECK();
 }
 

@@ -182,18 +182,57 @@ def test_ffm_csc_backward_one_hot(cuda):
     g2 = torch.zeros_like(V).to(cuda)
     ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g2)
     assert torch.equal(g2, gg)
-    # the field-grouped chunk processing order only changes WHEN a chunk runs: bitwise equal
-    assert Xg._ffm_layout[1][4] is not None
-    Xo = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
+    # fixed field layout (every row: fields 0..8 in order) -> the streamed XCD-split kernel ran
+    assert Xg._ffm_stream[1] is not None
     import os
-    os.environ["YTK_FFM_FIELD_ORDER"] = "0"
+    os.environ["YTK_FFM_STREAM"] = "0"
     try:
+        Xo = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F)
         g3 = torch.zeros_like(V).to(cuda)
         ffm_backward_csc(Xo, fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), g3)
     finally:
-        del os.environ["YTK_FFM_FIELD_ORDER"]
-    assert Xo._ffm_layout[1][4] is None
-    assert torch.equal(g3, gg)
+        del os.environ["YTK_FFM_STREAM"]
+    assert Xo._ffm_stream[1] is None
+    torch.testing.assert_close(g3, gg, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,tile", [(4, 40, 0), (8, 12, 700), (16, 9, 0)])
+def test_ffm_fixed_layout_backward(cuda, monkeypatch, k, m, tile):
+    """Fixed-layout rows (same permuted field order in every row, a bias column in front that
+    is skipped, non-unit values): the streamed XCD-split kernel matches the CPU pair scatter, small
+    per-wave entry targets (many chunks per wave) included, and is bitwise repeatable."""
+    import ytk_learn_amd.ops.ffm as ffm_mod
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    monkeypatch.setattr(sparse_mod, "CHUNK", 50)
+    monkeypatch.setattr(sparse_mod, "ROW_TILE", tile)
+    monkeypatch.setattr(ffm_mod, "WAVE_NNZ", 300)
+    n, per = 3000, 40
+    g = torch.Generator().manual_seed(k + m)
+    perm = torch.randperm(m, generator=g).to(torch.int32)
+    loc = (per * torch.rand((n, m), generator=g).pow(3)).long().clamp_(max=per - 1)
+    ix = (1 + perm.long()[None, :] * per + loc).to(torch.int32)
+    ix[:, 0] = 0  # bias feature in position 0
+    F = 1 + m * per
+    ip = torch.arange(n + 1, dtype=torch.int64) * m
+    vv = torch.rand(n * m, generator=g) + 0.5
+    fl = perm.repeat(n)
+    V = torch.randn(F * m * k, generator=g) * 0.2
+    V.view(F, m * k)[0] = 0.0
+    c = torch.randn(n, generator=g)
+    ixf = ix.reshape(-1).contiguous()
+    gc = torch.zeros_like(V)
+    ffm_backward(ip, ixf, vv, fl, V, m, k, c, gc, skip_feat=0)
+    Xg = SparseMatrix(ip.to(cuda), ixf.to(cuda), vv.to(cuda), F)
+    gg = torch.zeros_like(V).to(cuda)
+    ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), m, k, c.to(cuda), gg, skip_feat=0)
+    st = Xg._ffm_stream[1]
+    assert st is not None and st["wc"].numel() - 1 < st["beg"].numel()  # waves walk several chunks
+    assert st["beg"].numel() > F  # columns split into several chunks
+    torch.testing.assert_close(gg.cpu(), gc, rtol=1e-4, atol=1e-4)
+    g2 = torch.zeros_like(V).to(cuda)
+    ffm_backward_csc(Xg, fl.to(cuda), V.to(cuda), m, k, c.to(cuda), g2, skip_feat=0)
+    assert torch.equal(g2, gg)
 
 
 @pytest.mark.gpu

@@ -141,6 +141,12 @@ class DeviceLeafBuilder:
         # YTK_PEER_REDUCE=1: batch messages over the one-shot peer-memory all-reduce
         self.peer = (peer_mod.PeerReduce(self.comm, max(self.msg.numel(), self.slot_elems))
                      if peer_mod.enabled(self.comm) else None)
+        # the trainer's K == 1 gradient pass can build the next tree's root histogram (slot 0,
+        # tree_grad_hist); it is zeroed again when a tree is done
+        self.staged = True
+        self.fuse_root = False
+        self.root_ready = False
+        self._root_bufs = None
         self._root_glob = None
 
     # ------------------------------------------------------------------ setup
@@ -318,14 +324,19 @@ class DeviceLeafBuilder:
         self._done_host[1] = 0
         self._done_host[2] = 0
         h.lw_step(hd, 0, s)
+        root_done = self.root_ready and not sampled  # built by the previous gradient pass
+        self.root_ready = False
         if dist:
-            self._hist(h, rows0, gh0, s)
+            if not root_done:
+                self._hist(h, rows0, gh0, s)
             self._allreduce(self.hist[0:1].view(-1))  # the root slot
             self._split(h, fmask, f0, s)
             tm.mark("root")
             it = self._build_dist(h, hd, rows0, gh0, fmask, f0, s)
             return self._finish(h, s, it)
-        self._hist_split(h, rows0, gh0, fmask, f0, s)
+        if not root_done:
+            self._hist(h, rows0, gh0, s)
+        self._split(h, fmask, f0, s)
         tm.mark("root")
         # Launch throttle without events (a recorded event put a ~6 us gap before every
         # planner launch): the planner writes its batch count to pinned host memory, the
@@ -406,9 +417,21 @@ class DeviceLeafBuilder:
         else:
             self.comm.allreduce_(t)
 
+    def root_target(self):
+        """Arguments of the fused gradient + root histogram pass (gops.tree_grad root=)."""
+        if self._root_bufs is None:
+            grid = hip().tree_grad_hist_grid(self.N)
+            self._root_bufs = (torch.empty(grid * 256 * 32 * 2, dtype=torch.int64, device=self.dev),
+                               torch.zeros(4 * grid, dtype=torch.int32, device=self.dev))
+        stg, work = self._root_bufs
+        return {"slot": ptr(self.hist), "scales": ptr(self.scales), "staging": ptr(stg), "work": ptr(work),
+                "B": self.B, "F": self.F}
+
     def _finish(self, h, s, it) -> DeviceTree:
         self.timer.mark("batches")
         h.lv_step(4, self._lv_ptrs(), [0] * 8, [0.0] * 6, self.max_nodes, 0, s)
+        if self.fuse_root:
+            self.hist[0].zero_()  # the next gradient pass accumulates the next root here
         self.tree_count += 1
         self.last_batches = it
         snap = self.snap.clone()

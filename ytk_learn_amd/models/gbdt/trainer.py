@@ -181,6 +181,7 @@ class GBDTTrainer:
             # the builder waits on its planner while a tree grows: land the previous rounds
             # (tree conversion, loss log) in that wait instead of between trees
             self.builder.idle_hook = lambda: self._drain(0)
+            self._fuse_root_pending = True
         elif self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
                                               timer=self.timer)

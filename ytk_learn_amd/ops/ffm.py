@@ -10,7 +10,6 @@ import os
 
 import torch
 
-from . import sparse as sparse_mod
 from ._ext import check_cuda, hip, ptr, stream
 
 
@@ -85,6 +84,130 @@ def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=
     return gV
 
 
+WAVE_NNZ = int(os.environ.get("YTK_FFM_WAVE_NNZ", 512))  # entries per wave of the streamed kernel
+STREAM_GB = float(os.environ.get("YTK_FFM_STREAM_GB", 96))  # cap on the streamed expansion's memory
+
+
+def _fixed_layout(X, fld, nfield: int):
+    """(lay_field int32 [m], m) when every row holds the same m == nfield fields in the same
+    order (one entry per field, e.g. Criteo rows with the bias in front), else None."""
+    n = X.n
+    if n == 0 or X.nnz % n:
+        return None
+    m = X.nnz // n
+    if m != nfield or m < 8 or m > 512:
+        return None
+    if not bool(torch.equal(X.indptr, torch.arange(n + 1, device=X.indptr.device, dtype=X.indptr.dtype) * m)):
+        return None
+    lay = fld[:m].to(torch.int32).contiguous()
+    if not bool(torch.equal(torch.sort(lay).values.long(), torch.arange(m, device=lay.device))):
+        return None
+    if not bool((fld.view(n, m) == lay[None, :]).all()):
+        return None
+    return lay, m
+
+
+def _column_chunks(X, chunk: int):
+    """An untiled column order of X's entries for the streamed kernel: (perm, rows, chunk_beg,
+    chunk_end, chunk_ptr). X's own CSC is row-tiled so that the per-row data its kernels gather
+    stays cache resident; the streamed kernel reads no row data, and the tiles would only
+    multiply its chunks (one per (tile, column): 8M instead of 1M on the Criteo shape), each
+    paying an accumulator reduction and a partial-block write."""
+    cols = X.indices.to(torch.int64)
+    perm = torch.sort(cols, stable=True).indices      # CSR order is row-major: rows stay ascending
+    scol = cols[perm]
+    del cols
+    colptr = torch.searchsorted(scol, torch.arange(X.ncols + 1, dtype=torch.int64, device=scol.device))
+    del scol
+    counts = colptr[1:] - colptr[:-1]
+    nch = (counts + chunk - 1) // chunk
+    cptr = torch.zeros(X.ncols + 1, dtype=torch.int64, device=counts.device)
+    cptr[1:] = torch.cumsum(nch, 0)
+    total = int(cptr[-1])
+    chunk_col = torch.repeat_interleave(torch.arange(X.ncols, device=counts.device), nch)
+    within = torch.arange(total, device=counts.device) - cptr[:-1][chunk_col]
+    beg = (colptr[:-1][chunk_col] + within * chunk).contiguous()
+    end = torch.minimum(beg + chunk, colptr[1:][chunk_col]).contiguous()
+    rows = X.rows_of_nnz[perm].to(torch.int32).contiguous()
+    return perm, rows, beg, end, cptr
+
+
+def _wave_chunks(beg, end, target: int):
+    """Chunk ranges of ~``target`` entries per wave (chunks are never split)."""
+    nnz = (end - beg).to(torch.int64)
+    start = torch.cumsum(nnz, 0) - nnz
+    wid = start // max(1, target)
+    _, counts = torch.unique_consecutive(wid, return_counts=True)
+    wc = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=nnz.device)
+    wc[1:] = torch.cumsum(counts, 0)
+    return wc
+
+
+def _stream_layout(X, fld, nfield: int, skip_feat: int, unit_values: bool):
+    """Setup of the streamed XCD-split backward (``ffm_grad_stream_kernel``), cached on X:
+    fixed-layout rows whose columns each sit in one position only. The expansion
+    ``exp_idx[g][e][0..G)`` holds, for CSC entry e, its row's feature ids at position group
+    g's positions (-1 for the entry itself and for ``skip_feat``); ``exp_val`` the matching
+    values (None for unit values). None when the layout does not qualify or the expansion
+    would not fit (``YTK_FFM_STREAM_GB``, free device memory)."""
+    key = (fld.data_ptr(), int(nfield), int(skip_feat))
+    cached = getattr(X, "_ffm_stream", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    X._ffm_stream = (key, None)
+    if os.environ.get("YTK_FFM_STREAM", "1") == "0" or X.n_chunks == 0:
+        return None
+    fl = _fixed_layout(X, fld, nfield)
+    if fl is None:
+        return None
+    lay_field, m = fl
+    G = (m + 7) // 8
+    nnz, n = X.nnz, X.n
+    need = 8 * nnz * G * 4 * (1 if unit_values else 2)
+    free = torch.cuda.mem_get_info(X.indices.device)[0]
+    if need > STREAM_GB * 2 ** 30 or need * 1.25 + 2 * 2 ** 30 > free:
+        return None
+    dev = X.indices.device
+    from . import sparse as sparse_mod
+    perm, rows32, cbeg, cend, cptr = _column_chunks(X, sparse_mod.CHUNK)
+    rows = rows32.to(torch.int64)
+    pa = perm - rows * m                             # position of each column-ordered entry in its row
+    cols = X.indices[perm].to(torch.int64)
+    colpos = torch.full((X.ncols,), -1, dtype=torch.int64, device=dev)
+    colpos[cols] = pa
+    if not bool((colpos[cols] == pa).all()):      # a column in several positions
+        return None
+    del cols
+    chunk_fa = lay_field[pa[cbeg]].to(torch.int32)
+    if skip_feat >= 0:
+        chunk_fa = torch.where(X.indices[perm[cbeg]] == skip_feat, torch.full_like(chunk_fa, -1), chunk_fa)
+    idx2 = X.indices.view(n, m)
+    val2 = None if unit_values else X.values.view(n, m)
+    exp_idx = torch.empty((8, nnz, G), dtype=torch.int32, device=dev)
+    exp_val = None if unit_values else torch.empty((8, nnz, G), dtype=torch.float32, device=dev)
+    step = 1 << 23
+    for b0 in range(0, nnz, step):
+        b1 = min(nnz, b0 + step)
+        r = rows[b0:b1]
+        blk = torch.full((b1 - b0, 8 * G), -1, dtype=torch.int32, device=dev)
+        blk[:, :m] = idx2[r]
+        blk[torch.arange(b1 - b0, device=dev), pa[b0:b1]] = -1
+        if skip_feat >= 0:
+            blk[blk == skip_feat] = -1
+        exp_idx[:, b0:b1, :] = blk.view(b1 - b0, 8, G).permute(1, 0, 2)
+        if val2 is not None:
+            bv = torch.zeros((b1 - b0, 8 * G), dtype=torch.float32, device=dev)
+            bv[:, :m] = val2[r]
+            exp_val[:, b0:b1, :] = bv.view(b1 - b0, 8, G).permute(1, 0, 2)
+        del blk
+    del rows, pa
+    st = dict(lay_field=lay_field, m=m, wc=_wave_chunks(cbeg, cend, WAVE_NNZ), chunk_fa=chunk_fa.contiguous(),
+              exp_idx=exp_idx, exp_val=exp_val, rows=rows32, vals=None if unit_values else X.values[perm].contiguous(),
+              beg=cbeg, end=cend, cptr=cptr)
+    X._ffm_stream = (key, st)
+    return st
+
+
 def _csc_layout(X, fld, nfield: int):
     """Per-dataset inputs of the column-ordered backward, cached on X: whether rows have
     distinct fields (then the LDS accumulator needs no atomics), the packed entry codes
@@ -105,18 +228,7 @@ def _csc_layout(X, fld, nfield: int):
     code = X.indices.to(torch.int64) | (f64 << sh)
     code = torch.where(code >= 2 ** 31, code - 2 ** 32, code).to(torch.int32).contiguous()  # uint32 bits
     vals = None if bool((X.values == 1).all()) else X.values
-    # chunk processing order: (row tile, field of the chunk's column), stable -- the gathers
-    # of concurrently running chunks then stay inside one field's latent slice
-    # (YTK_FFM_FIELD_ORDER=0: CSC order)
-    order = None
-    if X._csc is None:
-        X._build_csc()
-    if os.environ.get("YTK_FFM_FIELD_ORDER", "1") != "0" and X.n_chunks > 0:
-        e0 = X.csc_perm[X.chunk_beg]                                 # first entry of each chunk (CSR pos)
-        tile = X.rows_of_nnz[e0].to(torch.int64) // max(1, sparse_mod.ROW_TILE if X.n > sparse_mod.ROW_TILE else X.n + 1)
-        key = tile * nfield + f64[e0]
-        order = torch.sort(key, stable=True).indices.to(torch.int32).contiguous()
-    lay = (distinct, code, sh, vals, order)
+    lay = (distinct, code, sh, vals)
     X._ffm_layout = (key, lay)
     return lay
 
@@ -131,18 +243,31 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
                             skip_feat=skip_feat)
     if X._csc is None:
         X._build_csc()
-    distinct, code, sh, vals, order = lay
+    distinct, code, sh, vals = lay
     J = nfield * k
     check_cuda(fld, V, coef, gV)
     Vt = V.view(X.ncols, nfield, k).transpose(0, 1).contiguous()  # [nfield][F][k]
-    part = torch.empty((max(X.n_chunks, 1), J), dtype=torch.float32, device=V.device)
     h, s = hip(), stream(V)
-    # (a register-accumulating variant for rows with a fixed field layout measured the same
-    # 75 ms on the Criteo shape: this kernel is bound by the L2 misses of its random 16-B
-    # latent-row gathers -- 274 GB fetched vs 46 GB for the row-oriented forward, which
-    # reuses a row's latent blocks across its pairs -- not by the LDS accumulator)
+    st = _stream_layout(X, fld, nfield, skip_feat, vals is None) if k in (4, 8, 16) else None
+    if st is not None:
+        # fixed-layout rows: the streamed XCD-split kernel (each XCD gathers only its own
+        # fields' latent rows -- an L2-sized working set -- and streams the row entries)
+        se = coef.index_select(0, st["rows"])
+        if st["vals"] is not None:
+            se.mul_(st["vals"])
+        wc, nch = st["wc"], st["beg"].numel()
+        part = torch.empty((max(nch, 1), J), dtype=torch.float32, device=V.device)
+        h.ffm_grad_stream(ptr(wc), wc.numel() - 1, ptr(st["beg"]), ptr(st["end"]), ptr(st["chunk_fa"]),
+                          ptr(st["exp_idx"]), ptr(st["exp_val"]), ptr(se), X.nnz, ptr(st["lay_field"]), st["m"],
+                          ptr(Vt), X.ncols, nfield, k, ptr(part), s)
+        h.chunk_reduce(ptr(st["cptr"]), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, 0, s)
+        return gV
+    part = torch.empty((max(X.n_chunks, 1), J), dtype=torch.float32, device=V.device)
+    # general rows: one wave per chunk, the row entries read per column (L2-miss bound on its
+    # random 16-B latent gathers: 274 GB fetched per Criteo-shape pass vs 46 GB for the
+    # row-oriented forward, which reuses a row's latent blocks across its pairs)
     h.ffm_grad_csc(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
-                   ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0, ptr(Vt),
-                   X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), ptr(order), s)
+                   ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
+                   ptr(Vt), X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), s)
     h.chunk_reduce(ptr(X.chunk_ptr), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, ptr(X.chunk_ids), s)
     return gV
