@@ -419,9 +419,26 @@ __global__ __launch_bounds__(256) void hist_fx_global_kernel(
 // 64-bit word index e uses bank pair e mod 16, interleaving would leave half unused),
 // accumulated with ds_add_u64 (same fixed point as hist_fx_kernel -> bitwise equal to
 // the CPU path). Block partials are flushed with global int64 atomics, zero entries
-// skipped (deep nodes touch few bins). grid = (ceil(F / FG), work items).
+// skipped (deep nodes touch few bins). grid: wide_grid (XCD-local feature groups per item).
 constexpr int kWideThreads = 1024;
 constexpr int kWideLdsBytes = 160 * 1024;    // one block per CU at the widest groups
+
+// XCD-local (group, item) of a wide-histogram block. The grid is 1-D, groups x (work items
+// rounded up to 8): blocks are dealt round-robin over the 8 XCDs, so XCD x = L % 8 runs the
+// blocks L = 8 s + x, and s enumerates (item / 8, group) -- every feature group of work item
+// 8 (s / groups) + x runs on that one XCD, back to back, and the row ids, (g, h) and row
+// lines all groups of an item read are fetched into ONE L2 (with the groups spread over
+// all XCDs each line came from HBM / MALL once per XCD). false: padding block.
+__device__ __forceinline__ bool wide_block(int groups, int nwork_grid, int& g, int& item) {
+  const unsigned L = blockIdx.x, s = L >> 3;
+  g = (int)(s % (unsigned)groups);
+  item = (int)((s / (unsigned)groups) * 8u + (L & 7u));
+  return item < nwork_grid;
+}
+
+static inline dim3 wide_grid(int groups, int nwork) {
+  return dim3((unsigned)((long long)groups * ((nwork + 7) / 8 * 8)));
+}
 
 // kFG features per block (power of two <= 32); every row's kFG bin loads of kU rows are
 // issued together before the LDS atomics (kU * kFG = 16 loads in flight per thread).
@@ -431,19 +448,20 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
-    const int* __restrict__ work_off_dev, long long* __restrict__ staging) {
+    const int* __restrict__ work_off_dev, long long* __restrict__ staging, int nwork_grid) {
   constexpr int kU = kFG >= 16 ? 1 : 16 / kFG;
   extern __shared__ __attribute__((aligned(16))) unsigned long long wl[];
-  // grid = (feature groups, work items): the groups of one item are dispatched together,
-  // so the (g, h) and row-id lines they all read are shared on chip
-  const int bx = (int)blockIdx.y + (work_off_dev ? *work_off_dev : 0);
+  const int groups = (F + kFG - 1) / kFG;
+  int grp, item;
+  if (!wide_block(groups, nwork_grid, grp, item)) return;
+  const int bx = item + (work_off_dev ? *work_off_dev : 0);
   if (nwork_dev && bx >= *nwork_dev) return;
   if (scales_dev) {
     sg = scales_dev[0];
     sh = scales_dev[1];
   }
   const int4 w = work[bx];
-  const int f_lo = (int)blockIdx.x * kFG;
+  const int f_lo = grp * kFG;
   const int nf = min(kFG, F - f_lo);
   const int tid = threadIdx.x;
   const int E = nf * B;
@@ -486,7 +504,7 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_kernel(
   __syncthreads();
   if (staging) {  // block partial -> staging item (bx, group), hist_reduce_kernel entry order
     const int Eg = kFG * B;
-    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.x + blockIdx.x) * Eg;
+    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * groups + grp) * Eg;
     for (int i = tid; i < Eg; i += kWideThreads) {
       const int bin = i / kFG, fi = i - bin * kFG;
       const bool in = fi < nf;
@@ -543,17 +561,20 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_rm_kernel(
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
-    const int* __restrict__ work_off_dev, long long* __restrict__ staging) {
+    const int* __restrict__ work_off_dev, long long* __restrict__ staging, int nwork_grid) {
   constexpr int kU = kFG >= 8 ? 2 : 16 / kFG;  // rows in flight per thread
   extern __shared__ __attribute__((aligned(16))) unsigned long long wl[];
-  const int bx = (int)blockIdx.y + (work_off_dev ? *work_off_dev : 0);
+  const int groups = (F + kFG - 1) / kFG;
+  int grp, item;
+  if (!wide_block(groups, nwork_grid, grp, item)) return;
+  const int bx = item + (work_off_dev ? *work_off_dev : 0);
   if (nwork_dev && bx >= *nwork_dev) return;
   if (scales_dev) {
     sg = scales_dev[0];
     sh = scales_dev[1];
   }
   const int4 w = work[bx];
-  const int f_lo = (int)blockIdx.x * kFG;
+  const int f_lo = grp * kFG;
   const int nf = min(kFG, F - f_lo);
   const int tid = threadIdx.x;
   const int E = kFG * B;
@@ -599,7 +620,7 @@ __global__ __launch_bounds__(kWideThreads) void hist_wide_rm_kernel(
     return;
   }
   if (staging) {
-    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.x + blockIdx.x) * E;
+    longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * groups + grp) * E;
     for (int i = tid; i < E; i += kWideThreads) {
       const int bin = i / kFG, fi = i - bin * kFG;
       const int e = fi * B + bin;
@@ -794,13 +815,13 @@ int ytk_hist_wide(uintptr_t binsT, long long ncol, int F, uintptr_t ghp, uintptr
   if (FG <= 0) throw std::invalid_argument("hist_wide: one feature's bins exceed the LDS budget");
   if (nwork <= 0) return FG;
   const size_t lds = (size_t)FG * B * 2 * sizeof(unsigned long long);
-  dim3 grid((F + FG - 1) / FG, nwork);
+  const dim3 grid = wide_grid((F + FG - 1) / FG, nwork);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define YTK_WIDE(ID, G)                                                                              \
   hipLaunchKernelGGL((hist_wide_kernel<ID, G>), grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT, \
                      ncol, F, (const float2*)ghp, (const int*)(ID ? 0 : rows), (const int4*)work,     \
                      (long long*)hist, B, sg, sh, (const int*)nwork_dev, (const float*)scales_dev,    \
-                     (const int*)work_off_dev, (long long*)nullptr)
+                     (const int*)work_off_dev, (long long*)nullptr, nwork)
 #define YTK_WIDE_G(ID)                  \
   switch (FG) {                         \
     case 1: YTK_WIDE(ID, 1); break;     \
@@ -835,7 +856,7 @@ int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uin
   if (stride % FG != 0 || (bins % 16) != 0) throw std::invalid_argument("hist_wide_rm: row stride / alignment");
   const size_t lds = (size_t)FG * B * 2 * sizeof(unsigned long long);
   const int groups = (F + FG - 1) / FG;
-  dim3 grid(groups, nwork);
+  const dim3 grid = wide_grid(groups, nwork);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (rows == 0 && binsT != 0) {
     // identity rows (a tree's root): the column-major copy is read coalesced -- 2 B per row
@@ -844,7 +865,7 @@ int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uin
 #define YTK_WCM(G)                                                                                            \
   hipLaunchKernelGGL((hist_wide_kernel<true, G>), grid, dim3(kWideThreads), lds, s, (const uint16_t*)binsT, ncol, F, \
                      (const float2*)ghp, (const int*)nullptr, (const int4*)work, (long long*)hist, B, sg, sh,     \
-                     (const int*)nwork_dev, (const float*)scales_dev, (const int*)work_off_dev, (long long*)staging)
+                     (const int*)nwork_dev, (const float*)scales_dev, (const int*)work_off_dev, (long long*)staging, nwork)
     switch (FG) {
       case 1: YTK_WCM(1); break;
       case 2: YTK_WCM(2); break;
@@ -860,7 +881,7 @@ int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uin
   hipLaunchKernelGGL((hist_wide_rm_kernel<ID, G>), grid, dim3(kWideThreads), lds, s, (const uint16_t*)bins, stride, \
                      F, (const float2*)ghp, (const int*)(ID ? 0 : rows), (const int4*)work, (long long*)hist, B, sg, \
                      sh, (const int*)nwork_dev, (const float*)scales_dev, (const int*)work_off_dev,              \
-                     (long long*)staging)
+                     (long long*)staging, nwork)
 #define YTK_WRM_G(ID)                  \
   switch (FG) {                        \
     case 1: YTK_WRM(ID, 1); break;     \

@@ -279,34 +279,45 @@ struct ScanOp {
   }
 };
 constexpr int kFeatThreads = 256;
-using FeatScan = rocprim::block_scan<ScanT, kFeatThreads>;
 
 // kR bins per thread: thread t owns the contiguous bins [t * kR, t * kR + kR) so one
-// block covers B <= 256 * kR (kR > 1: the wide-bin configs). The exclusive block scan
+// block of kT threads covers B <= kT * kR (kR > 1: the wide-bin configs; kT = 1024 above
+// 1024 bins, so a thread's sequential run stays <= 8 bins). The exclusive block scan
 // of the per-thread run totals gives each run its left prefix; the run is then walked
 // bin by bin exactly like the wave kernel (same gain, same tie-break).
-template <int kR>
-__global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
+template <int kR, int kT>
+__global__ __launch_bounds__(kT) void split_feat_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
-    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters) {
-  __shared__ typename FeatScan::storage_type s_scan;
-  __shared__ long long s_tg[kFeatThreads / kWave], s_th[kFeatThreads / kWave];
-  __shared__ float s_chg[kFeatThreads / kWave];
-  __shared__ int s_bin[kFeatThreads / kWave], s_a[kFeatThreads / kWave];
-  __shared__ double s_gl[kFeatThreads / kWave], s_hl[kFeatThreads / kWave];
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max) {
+  using Scan = rocprim::block_scan<ScanT, kT>;
+  __shared__ typename Scan::storage_type s_scan;
+  __shared__ long long s_tg[kT / kWave], s_th[kT / kWave];
+  __shared__ float s_chg[kT / kWave];
+  __shared__ int s_bin[kT / kWave], s_a[kT / kWave];
+  __shared__ double s_gl[kT / kWave], s_hl[kT / kWave];
   __shared__ int s_last;
   __shared__ SplitOut s_part[64];
 
-  if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
+  // XCD-aware block order: the grid is 1-D; a "unit" is 4 neighbouring features of one
+  // node, which share every 64-B line of the [bin][F] histogram (4 x 16 B). Units are dealt
+  // round-robin over the XCDs (blocks L with L % 8 == x run on XCD x) and a unit's 4 blocks
+  // run back to back on its XCD, so each line is fetched into one L2 once instead of once
+  // per feature; consecutive units still spread a level's (possibly few, nitems_dev) nodes
+  // over every XCD.
+  const unsigned Lb = blockIdx.x, sb = Lb >> 3;
+  const int nq = (F + 3) >> 2;
+  const int unit = (int)((sb >> 2) * 8u + (Lb & 7u));
+  const int item = unit / nq;
+  const int f = (unit - item * nq) * 4 + (int)(sb & 3u);
+  if (item >= nitems_max || f >= F || (nitems_dev && item >= *nitems_dev)) return;
   if (inv_dev) {
     gp.inv_sg = inv_dev[0];
     gp.inv_sh = inv_dev[1];
   }
-  const int f = (int)blockIdx.y;
   const int t = threadIdx.x, wid = t >> 6, l = lane_id();
-  const int4 it = items[blockIdx.x];
+  const int4 it = items[item];
   const size_t slot_sz = (size_t)B * F * 2;
   longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
   const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
@@ -323,35 +334,52 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   const int nb = nbins_f[f], nb0 = nbins_f[f0];
   const bool on = fmask[f] != 0;
   const int b0 = t * kR;
-  // ---- one load round trip (this feature's run + the node-total feature's run)
-  longlong2 v[kR], v0[kR];
-#pragma unroll
-  for (int k = 0; k < kR; ++k) {
-    const int bin = b0 + k;
-    v[k] = make_longlong2(0, 0);
-    v0[k] = make_longlong2(0, 0);
-    if (bin < B && (derived || (on && bin < nb))) v[k] = load(f, bin);
-    if (f != f0 && bin < nb0) v0[k] = load(f0, bin);
+  // kR == 1: one load round trip (this feature's bin + the node-total feature's bin).
+  // kR > 1 (wide bins): the bins are loaded bin = t + 256 j -- neighbouring lanes on
+  // neighbouring bins -- into LDS and each thread then walks its contiguous run from LDS
+  // (loading the runs directly put the 64 lanes of a load 32 bins x F x 16 B apart, a
+  // stride that lands on a couple of memory channels, and held 2 x kR 16-B values in
+  // registers: 256 VGPRs, one wave per SIMD)
+  extern __shared__ longlong2 s_bins[];
+  longlong2 v1 = make_longlong2(0, 0);
+  long long tg = 0, th = 0;
+  if constexpr (kR == 1) {
+    longlong2 v0 = make_longlong2(0, 0);
+    if (b0 < B && (derived || (on && b0 < nb))) v1 = load(f, b0);
+    if (f != f0 && b0 < nb0) v0 = load(f0, b0);
+    if (derived && b0 < B) hn[(size_t)b0 * F + f] = v1;  // materialise the derived histogram
+    if (f == f0) v0 = (b0 < nb0) ? v1 : make_longlong2(0, 0);
+    tg = v0.x;
+    th = v0.y;
+  } else {
+#pragma unroll 4
+    for (int bin = t; bin < B; bin += kT) {
+      longlong2 x = make_longlong2(0, 0), x0 = make_longlong2(0, 0);
+      if (derived || (on && bin < nb)) x = load(f, bin);
+      if (f != f0 && bin < nb0) x0 = load(f0, bin);
+      if (derived) hn[(size_t)bin * F + f] = x;
+      if (f == f0) x0 = (bin < nb0) ? x : make_longlong2(0, 0);
+      s_bins[bin] = x;
+      tg += x0.x;
+      th += x0.y;
+    }
   }
-#pragma unroll
-  for (int k = 0; k < kR; ++k) {
+  auto val = [&](int k) -> longlong2 {  // this thread's k-th bin (zero past nb)
     const int bin = b0 + k;
-    if (derived && bin < B) hn[(size_t)bin * F + f] = v[k];  // materialise the derived histogram
-    if (f == f0) v0[k] = (bin < nb0) ? v[k] : make_longlong2(0, 0);
-  }
+    if (bin >= nb || bin >= B) return make_longlong2(0, 0);
+    if constexpr (kR == 1) return v1;
+    else return s_bins[bin];
+  };
   // ---- node totals (exact int64, first sampled feature: DataParallelTreeMaker:543-573)
   {
-    long long sg = 0, sh = 0;
-#pragma unroll
-    for (int k = 0; k < kR; ++k) { sg += v0[k].x; sh += v0[k].y; }
-    sg = wave_sum_ll(sg);
-    sh = wave_sum_ll(sh);
+    const long long sg = wave_sum_ll(tg);
+    const long long sh = wave_sum_ll(th);
     if (l == 0) { s_tg[wid] = sg; s_th[wid] = sh; }
   }
-  __syncthreads();
+  __syncthreads();  // (also publishes s_bins)
   long long Gq = 0, Hq = 0;
 #pragma unroll
-  for (int w = 0; w < kFeatThreads / kWave; ++w) { Gq += s_tg[w]; Hq += s_th[w]; }
+  for (int w = 0; w < kT / kWave; ++w) { Gq += s_tg[w]; Hq += s_th[w]; }
   const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
 
   float best_chg = -INFINITY;
@@ -360,21 +388,20 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   if (on) {  // block-uniform
     long long rg = 0, rh = 0;
     int rlast = -1;
-#pragma unroll
     for (int k = 0; k < kR; ++k) {
-      if (b0 + k >= nb) v[k] = make_longlong2(0, 0);
-      rg += v[k].x;
-      rh += v[k].y;
-      if (v[k].x != 0 || v[k].y != 0) rlast = b0 + k;
+      const longlong2 x = val(k);
+      rg += x.x;
+      rh += x.y;
+      if (x.x != 0 || x.y != 0) rlast = b0 + k;
     }
     ScanT ex;
-    FeatScan().exclusive_scan(ScanT{rg, rh, rlast}, ex, ScanT{0, 0, -1}, s_scan, ScanOp());
+    Scan().exclusive_scan(ScanT{rg, rh, rlast}, ex, ScanT{0, 0, -1}, s_scan, ScanOp());
     const float root_gain = (float)calc_gain(G, H, gp);
     long long pg = ex.g, ph = ex.h;
     int prev = ex.last;
-#pragma unroll
     for (int k = 0; k < kR; ++k) {
-      const bool ne = (v[k].x != 0 || v[k].y != 0);
+      const longlong2 x = val(k);
+      const bool ne = (x.x != 0 || x.y != 0);
       if (!ne) continue;
       if (prev >= 0 && ph != 0) {
         const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
@@ -390,8 +417,8 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
           }
         }
       }
-      pg += v[k].x;
-      ph += v[k].y;
+      pg += x.x;
+      ph += x.y;
       prev = b0 + k;
     }
   }
@@ -413,7 +440,7 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   __syncthreads();
   if (t == 0) {
     int bw = 0;
-    for (int w = 1; w < kFeatThreads / kWave; ++w)
+    for (int w = 1; w < kT / kWave; ++w)
       if (better(s_chg[w], 0, s_bin[w], s_chg[bw], 0, s_bin[bw])) bw = w;
     SplitOut o;
     o.loss_chg = s_chg[bw];
@@ -424,9 +451,9 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
     o.hl = s_hl[bw];
     o.g = G;
     o.h = H;
-    part[(size_t)blockIdx.x * F + f] = o;
+    part[(size_t)item * F + f] = o;
     __threadfence();
-    const int prev = atomicAdd(&counters[blockIdx.x], 1);
+    const int prev = atomicAdd(&counters[item], 1);
     s_last = (prev == F - 1);
   }
   __syncthreads();
@@ -442,7 +469,7 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
   for (int c0 = 0; c0 < F; c0 += 64) {
     const int n = min(64, F - c0);
     if (t < n) {
-      const volatile SplitOut* pp = part + (size_t)blockIdx.x * F + c0 + t;
+      const volatile SplitOut* pp = part + (size_t)item * F + c0 + t;
       SplitOut q;
       q.loss_chg = pp->loss_chg; q.feat = pp->feat; q.bin_a = pp->bin_a; q.bin_b = pp->bin_b;
       q.gl = pp->gl; q.hl = pp->hl; q.g = pp->g; q.h = pp->h;
@@ -456,12 +483,12 @@ __global__ __launch_bounds__(kFeatThreads) void split_feat_kernel(
     __syncthreads();
   }
   if (t == 0) {
-    counters[blockIdx.x] = 0;
+    counters[item] = 0;
     best.g = G;
     best.h = H;
     if (best.feat == 0x7fffffff) best.feat = -1;
     if (best.bin_b == 0x7fffffff) best.bin_b = -1;
-    out[blockIdx.x] = best;
+    out[item] = best;
   }
 }
 
@@ -577,20 +604,23 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
     YTK_LAUNCH_CHECK();
     return;
   }
-  if (B <= 32 * kFeatThreads && part && counters) {
+  if (B <= 8192 && part && counters) {
     // part: >= nitems * F SplitOut; counters: nitems zeroed ints
-#define YTK_SPLIT_FEAT(R)                                                                          \
-  hipLaunchKernelGGL(split_feat_kernel<R>, dim3(nitems, F), dim3(kFeatThreads), 0,                 \
+    const long long units = (long long)nitems * ((F + 3) / 4);
+    if (units * 4 > 0x7fffffffLL - 64) throw std::invalid_argument("split_find: too many (node, feature) blocks");
+    const unsigned nblk = (unsigned)((units + 7) / 8 * 32);  // 4 blocks per unit, whole XCD rounds
+#define YTK_SPLIT_FEAT(R, T)                                                                       \
+  hipLaunchKernelGGL((split_feat_kernel<R, T>), dim3(nblk), dim3(T), R > 1 ? (size_t)B * 16 : 0,     \
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,                \
                      (const int*)nbins_f, (const uint8_t*)fmask, f0, (const int4*)items,           \
                      (SplitOut*)out, gp, (const int*)nitems_dev, (const double*)inv_dev,           \
-                     (SplitOut*)part, (int*)counters)
-    if (B <= kFeatThreads) YTK_SPLIT_FEAT(1);
-    else if (B <= 2 * kFeatThreads) YTK_SPLIT_FEAT(2);
-    else if (B <= 4 * kFeatThreads) YTK_SPLIT_FEAT(4);
-    else if (B <= 8 * kFeatThreads) YTK_SPLIT_FEAT(8);
-    else if (B <= 16 * kFeatThreads) YTK_SPLIT_FEAT(16);
-    else YTK_SPLIT_FEAT(32);
+                     (SplitOut*)part, (int*)counters, nitems)
+    if (B <= kFeatThreads) YTK_SPLIT_FEAT(1, 256);
+    else if (B <= 2 * kFeatThreads) YTK_SPLIT_FEAT(2, 256);
+    else if (B <= 4 * kFeatThreads) YTK_SPLIT_FEAT(4, 256);
+    else if (B <= 2048) YTK_SPLIT_FEAT(2, 1024);
+    else if (B <= 4096) YTK_SPLIT_FEAT(4, 1024);
+    else YTK_SPLIT_FEAT(8, 1024);
 #undef YTK_SPLIT_FEAT
     YTK_LAUNCH_CHECK();
     return;

@@ -96,7 +96,8 @@ class DeviceLevelBuilder:
             raise ValueError(f"device builder: unsupported bin layout (dtype {bins.dtype}, B={B}, F={F})")
         # wide mode: uint16 bins with B > 256 -> feature-grouped LDS histograms over binsT
         self.wide = bins.dtype == torch.int16
-        self.hist_target = (min(self.HIST_TARGET, max(32, 1024 // (-(-F // gops.wide_group(B, F)))))
+        # wide: ~WIDE_HIST_BLOCKS (work item, feature group) blocks per level
+        self.hist_target = (min(self.HIST_TARGET, max(8, gops.WIDE_HIST_BLOCKS // (-(-F // gops.wide_group(B, F)))))
                             if self.wide else self.HIST_TARGET)
         self.p = p
         self.bins, self.binsT = bins, binsT

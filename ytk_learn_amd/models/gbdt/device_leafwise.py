@@ -64,7 +64,7 @@ class DeviceLeafBuilder:
         self.wide = bins.dtype == torch.int16
         if self.wide:
             groups = -(-F // gops.wide_group(B, F))
-            self.HIST_TARGET = min(self.HIST_TARGET, max(32, 1024 // groups))
+            self.HIST_TARGET = min(self.HIST_TARGET, max(8, gops.WIDE_HIST_BLOCKS // groups))
         self.dev = bins.device
         self.N = N = bins.shape[0]
         self.F, self.B = F, B

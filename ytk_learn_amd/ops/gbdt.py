@@ -610,6 +610,9 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
     return torch.tensor([float((w * lv).sum()), float(w.sum())], dtype=torch.float64)
 
 
+# (work item, feature group) blocks per level of the wide-bin (B > 256) histograms: one
+# 160-KiB block per CU, so this many blocks is ~4 rounds over the 256 CUs
+WIDE_HIST_BLOCKS = int(os.environ.get("YTK_WIDE_HIST_BLOCKS", 1024))
 LDS_BUDGET = 160 * 1024 - 1024  # == kLdsBudget (csrc/hip/common.h)
 
 
