@@ -279,6 +279,7 @@ struct ScanOp {
   }
 };
 constexpr int kFeatThreads = 256;
+constexpr int kSplitFeatMaxBlocks = 2048;  // grid cap of split_feat_kernel (a multiple of 32)
 
 // kR bins per thread: thread t owns the contiguous bins [t * kR, t * kR + kR) so one
 // block of kT threads covers B <= kT * kR (kR > 1: the wide-bin configs; kT = 1024 above
@@ -306,17 +307,27 @@ __global__ __launch_bounds__(kT) void split_feat_kernel(
   // run back to back on its XCD, so each line is fetched into one L2 once instead of once
   // per feature; consecutive units still spread a level's (possibly few, nitems_dev) nodes
   // over every XCD.
-  const unsigned Lb = blockIdx.x, sb = Lb >> 3;
+  //
+  // Grid-stride over that block order: a device-counted launch (leaf-wise engine) is sized
+  // for its item BOUND (2 x max leaves), and thousands of empty 1024-thread blocks with a
+  // 80-KB LDS footprint cost more than the real ones (measured 213 us per 5000-bin call).
+  // The grid is capped (a multiple of 32) and each block walks L, L + gridDim.x, ...; the
+  // unit index grows with L, so the first item past the count ends the walk.
   const int nq = (F + 3) >> 2;
-  const int unit = (int)((sb >> 2) * 8u + (Lb & 7u));
-  const int item = unit / nq;
-  const int f = (unit - item * nq) * 4 + (int)(sb & 3u);
-  if (item >= nitems_max || f >= F || (nitems_dev && item >= *nitems_dev)) return;
+  const int nitems_live = nitems_dev ? min(*nitems_dev, nitems_max) : nitems_max;
   if (inv_dev) {
     gp.inv_sg = inv_dev[0];
     gp.inv_sh = inv_dev[1];
   }
   const int t = threadIdx.x, wid = t >> 6, l = lane_id();
+  for (unsigned Lb = blockIdx.x;; Lb += gridDim.x) {
+  const unsigned sb = Lb >> 3;
+  const int unit = (int)((sb >> 2) * 8u + (Lb & 7u));
+  const int item = unit / nq;
+  const int f = (unit - item * nq) * 4 + (int)(sb & 3u);
+  if (item >= nitems_live) break;
+  if (f >= F) continue;
+  __syncthreads();  // the previous unit's LDS (bins, scan, partials) is no longer read
   const int4 it = items[item];
   const size_t slot_sz = (size_t)B * F * 2;
   longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
@@ -457,7 +468,7 @@ __global__ __launch_bounds__(kT) void split_feat_kernel(
     s_last = (prev == F - 1);
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) continue;
   // ---- last block of the node: combine the F feature candidates (64 per pass)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   SplitOut best;
@@ -489,6 +500,244 @@ __global__ __launch_bounds__(kT) void split_feat_kernel(
     if (best.feat == 0x7fffffff) best.feat = -1;
     if (best.bin_b == 0x7fffffff) best.bin_b = -1;
     out[item] = best;
+  }
+  }  // grid-stride unit loop
+}
+
+// ---------------------------------------------------------------------------------
+// Wide-bin split search (256 < B <= 256 * kR): one 256 kFG-thread block per (node, group of
+// kFG neighbouring features), the group's histogram held in registers.
+//
+// Why: the [slot][bin][F] layout puts one feature's consecutive bins F x 16 B apart, so
+// split_feat_kernel's per-feature blocks fetched a separate line per 16-B (g, h) pair --
+// at 5000 bins 3 x 80 KB of scattered lines per (derived node, feature), ~290 us per
+// leaf-wise batch. Here thread t owns feature t % kFG of the contiguous bin run
+// [(t / kFG) kR, (t / kFG) kR + kR): at every load instruction the kFG lanes of a bin read
+// its kFG x 16 contiguous bytes, all kR loads of a thread are in flight together,
+// and the derived (parent - sibling) histogram is written back the same way. The run
+// totals go through ONE block scan per feature (stride-kFG lane scan -- features interleave
+// with the lanes -- then wave 0 scans the wave totals), and each thread walks its run
+// from registers exactly like split_feat_kernel (same gain, same empty-bin rule, same
+// tie-break). Node totals: the group's copy of f0, else its first sampled feature (every
+// row adds to exactly one bin of every feature, so the exact int64 totals agree); the
+// item's last group block combines the groups' records and takes the totals from f0's group.
+constexpr int kWideSplitMaxBlocks = 2048;  // grid cap (a multiple of 8; grid-stride inside)
+
+template <int kR, int kFG>
+__global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
+    long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
+    const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
+    SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max) {
+  constexpr int kT = 256 * kFG;  // 256 bin runs per feature
+  constexpr int kW = kT / kWave;
+  static_assert(kW * kFG <= kWave, "wave 0 scans the (wave, feature) totals");
+  __shared__ long long s_wg[kW][kFG], s_wh[kW][kFG];  // wave totals per feature -> exclusive prefixes
+  __shared__ int s_wl[kW][kFG];
+  __shared__ long long s_tg[kW], s_th[kW];
+  __shared__ float s_chg[kW];
+  __shared__ int s_f[kW], s_b[kW], s_a[kW];
+  __shared__ double s_gl[kW], s_hl[kW];
+  __shared__ int s_last;
+  __shared__ SplitOut s_part[64];
+  const int ng = (F + kFG - 1) / kFG;
+  const int nitems_live = nitems_dev ? min(*nitems_dev, nitems_max) : nitems_max;
+  if (inv_dev) {
+    gp.inv_sg = inv_dev[0];
+    gp.inv_sh = inv_dev[1];
+  }
+  const int t = threadIdx.x, wid = t >> 6, l = lane_id();
+  const int fi = t % kFG, b0 = (t / kFG) * kR;
+  // XCD-local (item, group): blocks L = 8 s + x run on XCD x; s enumerates (item / 8, group),
+  // so all groups of item 8 (s / ng) + x share that XCD's L2 (neighbouring groups share
+  // 128-B lines of each bin row)
+  for (unsigned L = blockIdx.x;; L += gridDim.x) {
+    const unsigned sb = L >> 3;
+    const int grp = (int)(sb % (unsigned)ng);
+    const int item = (int)((sb / (unsigned)ng) * 8u + (L & 7u));
+    if (item >= nitems_live) break;  // item grows with L
+    __syncthreads();  // the previous item's LDS records are no longer read
+    const int4 it = items[item];
+    const size_t slot_sz = (size_t)B * F * 2;
+    longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
+    const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
+    const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
+    const bool derived = it.w != 0;
+    const int f_lo = grp * kFG, f = f_lo + fi;
+    const bool fin = f < F;
+    const int nb = fin ? nbins_f[f] : 0;
+    const bool on = fin && fmask[f] != 0;
+    int tf = -1;  // totals feature of the group (block-uniform)
+    if (f0 >= f_lo && f0 < min(F, f_lo + kFG)) {
+      tf = f0;
+    } else {
+      for (int q = f_lo; q < min(F, f_lo + kFG); ++q)
+        if (fmask[q]) { tf = q; break; }
+    }
+    const bool want = on || f == tf;
+    longlong2 v[kR];
+    if (derived) {  // 4 bins per step: 8 loads in flight, not 2 kR (register budget)
+#pragma unroll
+      for (int k0 = 0; k0 < kR; k0 += 4) {
+        longlong2 a[4], c[4];
+#pragma unroll
+        for (int j = 0; j < 4 && k0 + j < kR; ++j) {
+          const int bin = b0 + k0 + j;
+          a[j] = c[j] = make_longlong2(0, 0);
+          if (fin && bin < B) { a[j] = hp[(size_t)bin * F + f]; c[j] = hs[(size_t)bin * F + f]; }
+        }
+#pragma unroll
+        for (int j = 0; j < 4 && k0 + j < kR; ++j) {
+          const int bin = b0 + k0 + j;
+          const longlong2 x = make_longlong2(a[j].x - c[j].x, a[j].y - c[j].y);
+          if (fin && bin < B) hn[(size_t)bin * F + f] = x;  // materialise the derived histogram
+          v[k0 + j] = bin < nb ? x : make_longlong2(0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        const int bin = b0 + k;
+        v[k] = (want && bin < nb) ? hn[(size_t)bin * F + f] : make_longlong2(0, 0);
+      }
+    }
+    // ---- run totals, node totals (exact int64)
+    long long rg = 0, rh = 0;
+    int rl = -1;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      rg += v[k].x;
+      rh += v[k].y;
+      if ((v[k].x | v[k].y) != 0) rl = b0 + k;
+    }
+    {
+      const long long tg = wave_sum_ll(f == tf ? rg : 0), th = wave_sum_ll(f == tf ? rh : 0);
+      if (l == 0) { s_tg[wid] = tg; s_th[wid] = th; }
+    }
+    // ---- exclusive scan of the run totals per feature: lanes kFG j + fi
+    long long ig = rg, ih = rh;
+    int il = rl;
+#pragma unroll
+    for (int off = kFG; off < kWave; off <<= 1) {
+      const long long og = __shfl_up(ig, off, kWave), oh = __shfl_up(ih, off, kWave);
+      const int ol = __shfl_up(il, off, kWave);
+      if (l >= off) { ig += og; ih += oh; il = max(il, ol); }
+    }
+    int el = __shfl_up(il, kFG, kWave);
+    if (l < kFG) el = -1;
+    if (l >= kWave - kFG) { s_wg[wid][fi] = ig; s_wh[wid][fi] = ih; s_wl[wid][fi] = il; }
+    __syncthreads();
+    if (t < kW * kFG) {  // wave 0: exclusive prefix of the wave totals per feature (lane = kFG w + fi)
+      const long long a0 = (&s_wg[0][0])[t], c0 = (&s_wh[0][0])[t];
+      long long a = a0, c = c0;
+      int m = (&s_wl[0][0])[t];
+#pragma unroll
+      for (int off = kFG; off < kW * kFG; off <<= 1) {
+        const long long oa = __shfl_up(a, off, kWave), oc = __shfl_up(c, off, kWave);
+        const int om = __shfl_up(m, off, kWave);
+        if (t >= off) { a += oa; c += oc; m = max(m, om); }
+      }
+      int em = __shfl_up(m, kFG, kWave);
+      if (t < kFG) em = -1;
+      (&s_wg[0][0])[t] = a - a0;
+      (&s_wh[0][0])[t] = c - c0;
+      (&s_wl[0][0])[t] = em;
+    }
+    __syncthreads();
+    long long Gq = 0, Hq = 0;
+#pragma unroll
+    for (int w = 0; w < kW; ++w) { Gq += s_tg[w]; Hq += s_th[w]; }
+    const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
+    long long pg = s_wg[wid][fi] + ig - rg, ph = s_wh[wid][fi] + ih - rh;  // left of this run
+    int prev = max(s_wl[wid][fi], el);
+    float best_chg = -INFINITY;
+    int best_b = 0x7fffffff, best_a = -1;
+    double best_gl = 0.0, best_hl = 0.0;
+    if (on) {
+      const float root_gain = (float)calc_gain(G, H, gp);
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        const longlong2 x = v[k];
+        if ((x.x | x.y) == 0) continue;
+        if (prev >= 0 && ph != 0) {
+          const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
+          const double dgr = (double)(Gq - pg) * gp.inv_sg, dhr = (double)(Hq - ph) * gp.inv_sh;
+          if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
+            const float chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
+            if (better(chg, 0, b0 + k, best_chg, 0, best_b)) {
+              best_chg = chg; best_b = b0 + k; best_a = prev; best_gl = dgl; best_hl = dhl;
+            }
+          }
+        }
+        pg += x.x;
+        ph += x.y;
+        prev = b0 + k;
+      }
+    }
+    // ---- block argmax over (chg desc, feature asc, bin asc)
+    int best_f = best_b == 0x7fffffff ? 0x7fffffff : f;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+      const float oc = __shfl_xor(best_chg, off, kWave);
+      const int of = __shfl_xor(best_f, off, kWave), ob = __shfl_xor(best_b, off, kWave);
+      const int oa = __shfl_xor(best_a, off, kWave);
+      const double ogl = __shfl_xor(best_gl, off, kWave), ohl = __shfl_xor(best_hl, off, kWave);
+      if (better(oc, of, ob, best_chg, best_f, best_b)) {
+        best_chg = oc; best_f = of; best_b = ob; best_a = oa; best_gl = ogl; best_hl = ohl;
+      }
+    }
+    if (l == 0) {
+      s_chg[wid] = best_chg; s_f[wid] = best_f; s_b[wid] = best_b; s_a[wid] = best_a;
+      s_gl[wid] = best_gl; s_hl[wid] = best_hl;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int bw = 0;
+      for (int w = 1; w < kW; ++w)
+        if (better(s_chg[w], s_f[w], s_b[w], s_chg[bw], s_f[bw], s_b[bw])) bw = w;
+      SplitOut o;
+      o.loss_chg = s_chg[bw]; o.feat = s_f[bw]; o.bin_a = s_a[bw]; o.bin_b = s_b[bw];
+      o.gl = s_gl[bw]; o.hl = s_hl[bw]; o.g = G; o.h = H;
+      part[(size_t)item * ng + grp] = o;
+      __threadfence();
+      const int pv = atomicAdd(&counters[item], 1);
+      s_last = (pv == ng - 1);
+    }
+    __syncthreads();
+    if (!s_last) continue;
+    // ---- last group block of the item: combine the groups' records (64 per pass)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    SplitOut best;
+    best.loss_chg = -INFINITY; best.feat = 0x7fffffff; best.bin_a = -1; best.bin_b = 0x7fffffff;
+    best.gl = best.hl = best.g = best.h = 0.0;
+    double tg = 0.0, th = 0.0;
+    for (int c0 = 0; c0 < ng; c0 += 64) {
+      const int n = min(64, ng - c0);
+      if (t < n) {
+        const volatile SplitOut* pp = part + (size_t)item * ng + c0 + t;
+        SplitOut q;
+        q.loss_chg = pp->loss_chg; q.feat = pp->feat; q.bin_a = pp->bin_a; q.bin_b = pp->bin_b;
+        q.gl = pp->gl; q.hl = pp->hl; q.g = pp->g; q.h = pp->h;
+        s_part[t] = q;
+      }
+      __syncthreads();
+      if (t == 0) {
+        for (int y = 0; y < n; ++y)
+          if (better(s_part[y].loss_chg, s_part[y].feat, s_part[y].bin_b, best.loss_chg, best.feat, best.bin_b))
+            best = s_part[y];
+        const int g0 = f0 / kFG - c0;  // totals from f0's group
+        if (g0 >= 0 && g0 < n) { tg = s_part[g0].g; th = s_part[g0].h; }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      counters[item] = 0;
+      best.g = tg;
+      best.h = th;
+      if (best.feat == 0x7fffffff) best.feat = -1;
+      if (best.bin_b == 0x7fffffff) best.bin_b = -1;
+      out[item] = best;
+    }
   }
 }
 
@@ -604,11 +853,34 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
     YTK_LAUNCH_CHECK();
     return;
   }
+  if (B > kFeatThreads && B <= 20 * 256 && part && counters && F <= 256 && !getenv_flag_off("YTK_SPLIT_WIDE")) {
+    // wide bins: the group's histogram in registers (split_wide_kernel); part: nitems x
+    // ceil(F / kFG) records. 4 features per 1024-thread block up to 1024 bins, above that 2
+    // per 512-thread block (kR 16-B pairs per thread + the walk within 256 VGPRs)
+#define YTK_SPLIT_WIDE(R, FG)                                                                                  \
+  do {                                                                                                         \
+    const long long L = (long long)((F + FG - 1) / FG) * ((nitems + 7) / 8 * 8);                               \
+    const unsigned nblk = (unsigned)std::min<long long>(L, kWideSplitMaxBlocks);                               \
+    hipLaunchKernelGGL((split_wide_kernel<R, FG>), dim3(nblk), dim3(256 * FG), 0,                              \
+                       reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, (const int*)nbins_f,     \
+                       (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp,                     \
+                       (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters, nitems); \
+  } while (0)
+    if (B <= 4 * 256) YTK_SPLIT_WIDE(4, 4);
+    else if (B <= 8 * 256) YTK_SPLIT_WIDE(8, 2);
+    else if (B <= 12 * 256) YTK_SPLIT_WIDE(12, 2);
+    else if (B <= 16 * 256) YTK_SPLIT_WIDE(16, 2);
+    else YTK_SPLIT_WIDE(20, 2);
+#undef YTK_SPLIT_WIDE
+    YTK_LAUNCH_CHECK();
+    return;
+  }
   if (B <= 8192 && part && counters) {
     // part: >= nitems * F SplitOut; counters: nitems zeroed ints
     const long long units = (long long)nitems * ((F + 3) / 4);
     if (units * 4 > 0x7fffffffLL - 64) throw std::invalid_argument("split_find: too many (node, feature) blocks");
-    const unsigned nblk = (unsigned)((units + 7) / 8 * 32);  // 4 blocks per unit, whole XCD rounds
+    // 4 blocks per unit, whole XCD rounds; capped (grid-stride inside): kSplitFeatMaxBlocks
+    const unsigned nblk = (unsigned)std::min<long long>((units + 7) / 8 * 32, kSplitFeatMaxBlocks);
 #define YTK_SPLIT_FEAT(R, T)                                                                       \
   hipLaunchKernelGGL((split_feat_kernel<R, T>), dim3(nblk), dim3(T), R > 1 ? (size_t)B * 16 : 0,     \
                      reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F,                \

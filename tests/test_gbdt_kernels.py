@@ -74,7 +74,7 @@ def test_hist_build_uint16_global(cuda):
 
 
 def _hist_from(N, F, nb, B, seed):
-    bins = _rand_bins(N, F, nb, seed)
+    bins = _rand_bins(N, F, nb, seed, dtype=torch.uint8 if nb <= 256 else torch.int16)
     gh = _gh(N, seed + 1)
     h = torch.zeros((1, B, F, 2), dtype=torch.int64)
     gops.hist_build(bins, F, gh, None, torch.tensor([[0, 0, N, 0]], dtype=torch.int32), h, B, SG, SH)
@@ -87,10 +87,19 @@ def test_split_find_matches_cpu(cuda, l1, l2, mal, nb):
     F, B = 28, nb
     parent = _hist_from(40000, F, nb, B, 5)
     small = _hist_from(15000, F, nb, B, 6)
+    # Structural invariant of real histograms, which the kernels may rely on for the node
+    # totals: every row adds its (g, h) to exactly one bin of EVERY feature, so all features
+    # of a node sum to the same totals, and a feature has no mass past its bin count. The
+    # sparse and short features below move mass between bins instead of dropping it.
+    small[49, 3] += small[50:120, 3].sum(dim=0)
+    small[50:120, 3] = 0  # sparse bins (empty-bin skipping)
+    parent[29, 7] += parent[30:, 7].sum(dim=0)
+    parent[30:, 7] = 0
+    small[29, 7] += small[30:, 7].sum(dim=0)
+    small[30:, 7] = 0
     hist = torch.zeros((4, B, F, 2), dtype=torch.int64)
     hist[0] = parent + small  # parent contains the small child
     hist[1] = small
-    hist[1, 50:120, 3] = 0  # sparse bins (empty-bin skipping)
     nbins = torch.full((F,), nb, dtype=torch.int32)
     nbins[7] = 30
     fmask = torch.ones(F, dtype=torch.uint8)

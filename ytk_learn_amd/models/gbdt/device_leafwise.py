@@ -65,6 +65,9 @@ class DeviceLeafBuilder:
         if self.wide:
             groups = -(-F // gops.wide_group(B, F))
             self.HIST_TARGET = min(self.HIST_TARGET, max(8, gops.WIDE_HIST_BLOCKS // groups))
+            # the slot reduce's y extent is REDUCE_Y x groups: one y block per group already
+            # gives 14 x 40 x 8 blocks at 5000 bins (8 per group launched ~36k mostly idle ones)
+            self.REDUCE_Y = max(1, self.REDUCE_Y // groups)
         self.dev = bins.device
         self.N = N = bins.shape[0]
         self.F, self.B = F, B
