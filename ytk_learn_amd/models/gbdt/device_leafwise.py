@@ -48,7 +48,7 @@ class DeviceLeafBuilder:
     REDUCE_Y = 8        # slot reduce: y blocks striding over the batch's multi-item slots
     # batches enqueued ahead of the done-flag check (capturing batches in HIP graphs was
     # measured: no gain -- the gaps between dependent kernels are on the device side)
-    POLL_LAG = 2
+    POLL_LAG = int(os.environ.get("YTK_LW_POLL_LAG", 2))
     POLL_TIMEOUT_S = 60.0
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
