@@ -49,7 +49,8 @@ void ytk_tree_add_bins(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_
                        uintptr_t, int, uintptr_t, int, int, uintptr_t);
 int ytk_forest_loss_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                          uintptr_t, int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, float, float, uintptr_t,
-                         uintptr_t, uintptr_t);
+                         uintptr_t, int, uintptr_t);
+void ytk_acc_finish(uintptr_t, int, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 int ytk_forest_predict_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                             uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, int, float, uintptr_t, uintptr_t);
 void ytk_forest_predict(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t,
@@ -90,6 +91,9 @@ void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uint
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                      uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_lv_init_scales(const uintptr_t*, const int*, const float*, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_lv_tail(const uintptr_t*, const int*, const float*, int, int, int, int, uintptr_t, uintptr_t, uintptr_t, int,
+                 uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, int, int, uintptr_t, uintptr_t, int, int,
                        const float*, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
@@ -109,7 +113,7 @@ void ytk_seg_prune(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr
 int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int,
-                       uintptr_t);
+                       uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 int ytk_tree_grad_hist_grid(long long);
 void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, uintptr_t);
 void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
@@ -153,6 +157,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("forest_predict", &ytk_forest_predict);
   m.def("forest_predict_regs", &ytk_forest_predict_regs);
   m.def("forest_loss_regs", &ytk_forest_loss_regs);
+  m.def("acc_finish", &ytk_acc_finish);
   m.def("bin_assign", &ytk_bin_assign);
   m.def("grad_hess", &ytk_grad_hess);
   m.def("tree_grad", &ytk_tree_grad);
@@ -181,6 +186,20 @@ PYBIND11_MODULE(_ytk_hip, m) {
                     nright, ndefl, nval, stream);
   });
   m.def("lv_scales", &ytk_lv_scales);
+  m.def("lv_init_scales", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
+                             const std::vector<float>& fp, uintptr_t mx, uintptr_t scales, uintptr_t inv,
+                             uintptr_t stream) {
+    if (ptrs.size() != 26 || ip.size() < 8 || fp.size() < 6) throw std::invalid_argument("lv_init_scales: bad sizes");
+    ytk_lv_init_scales(ptrs.data(), ip.data(), fp.data(), mx, scales, inv, stream);
+  });
+  m.def("lv_tail", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp,
+                      int children, int a0, int a1, int max_nodes, uintptr_t cand, uintptr_t coff, uintptr_t fill,
+                      int median, uintptr_t nfeat, uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
+                      uintptr_t nval, uintptr_t stream) {
+    if (ptrs.size() != 26 || ip.size() < 8 || fp.size() < 6) throw std::invalid_argument("lv_tail: bad sizes");
+    ytk_lv_tail(ptrs.data(), ip.data(), fp.data(), children, a0, a1, max_nodes, cand, coff, fill, median, nfeat, nthr,
+                nleft, nright, ndefl, nval, stream);
+  });
   m.def("lv_partition_children", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,

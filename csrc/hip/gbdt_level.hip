@@ -153,9 +153,29 @@ __device__ void emit_all_chunks(int4* items, int total_items, int nseg, const in
   }
 }
 
-// Root: node 0 holds all (local) rows; one build item; chunked histogram work.
-__global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBufs b) {
+// Fixed-point scales from the (all-reduced) max |g|, |h| and global row count (threads 0, 1).
+__device__ __forceinline__ void lv_scales_body(const float* __restrict__ mx, const long long* __restrict__ cnt,
+                                               float* __restrict__ scales, double* __restrict__ inv_scales) {
+  if (threadIdx.x >= 2) return;
+  const double m = (double)mx[threadIdx.x];
+  double s = 1.0;
+  if (m > 0.0) {
+    const double n = (double)max(1LL, cnt[1]);
+    int k = (int)floor(log2(4611686018427387904.0 / (m * n)));
+    k = min(max(k, -120), 120);
+    s = ldexp(1.0, k);
+  }
+  scales[threadIdx.x] = (float)s;
+  inv_scales[threadIdx.x] = 1.0 / s;
+}
+
+// Root: node 0 holds all (local) rows; one build item; chunked histogram work. mx != nullptr:
+// the tree's fixed-point scales too (lv_scales_kernel's work: one launch less per tree).
+__global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBufs b, const float* __restrict__ mx,
+                                                               float* __restrict__ scales,
+                                                               double* __restrict__ inv_scales) {
   __shared__ int s_first[2], s_begin[1], s_count[1], s_tag[1];
+  if (mx) lv_scales_body(mx, b.root_cnt, scales, inv_scales);
   const int n_local = (int)b.root_cnt[0];
   const int ch = max(p.min_rows, (n_local + p.hist_target - 1) / max(1, p.hist_target));
   const int nblk = (n_local + ch - 1) / ch;
@@ -492,7 +512,7 @@ __global__ __launch_bounds__(kNodeThreads) void lv_split_plan_kernel(
 }
 
 // Bin-threshold arrays used by the fused score/gradient kernel.
-__global__ void lv_finalize_kernel(LvBufs b, int max_nodes) {
+__device__ __forceinline__ void lv_finalize_body(const LvBufs& b, int max_nodes) {
   const int nn = b.st[ST_NUM_NODES];
   for (int i = threadIdx.x; i < max_nodes; i += blockDim.x) {
     if (i < nn) {
@@ -513,15 +533,17 @@ __global__ void lv_finalize_kernel(LvBufs b, int max_nodes) {
   }
 }
 
+__global__ void lv_finalize_kernel(LvBufs b, int max_nodes) { lv_finalize_body(b, max_nodes); }
+
 // Raw-feature version of the finished tree for test-set scoring:
 // cond = mean (0.5*(v_a+v_b)) or median split of the candidate values,
 // default child = left iff fill < cond (Tree.java:293-309, 357-375).
-__global__ void lv_raw_tree_kernel(LvBufs b, int max_nodes, const float* __restrict__ cand,
-                                   const int* __restrict__ coff, const float* __restrict__ fill,
-                                   int split_median, int* __restrict__ nfeat,
-                                   float* __restrict__ nthr, int* __restrict__ nleft,
-                                   int* __restrict__ nright, uint8_t* __restrict__ ndefl,
-                                   float* __restrict__ nval) {
+__device__ __forceinline__ void lv_raw_tree_body(const LvBufs& b, int max_nodes, const float* __restrict__ cand,
+                                                 const int* __restrict__ coff, const float* __restrict__ fill,
+                                                 int split_median, int* __restrict__ nfeat,
+                                                 float* __restrict__ nthr, int* __restrict__ nleft,
+                                                 int* __restrict__ nright, uint8_t* __restrict__ ndefl,
+                                                 float* __restrict__ nval) {
   const int nn = b.st[ST_NUM_NODES];
   for (int i = threadIdx.x; i < max_nodes; i += blockDim.x) {
     if (i >= nn) {
@@ -549,20 +571,49 @@ __global__ void lv_raw_tree_kernel(LvBufs b, int max_nodes, const float* __restr
   }
 }
 
+__global__ void lv_raw_tree_kernel(LvBufs b, int max_nodes, const float* __restrict__ cand,
+                                   const int* __restrict__ coff, const float* __restrict__ fill,
+                                   int split_median, int* __restrict__ nfeat,
+                                   float* __restrict__ nthr, int* __restrict__ nleft,
+                                   int* __restrict__ nright, uint8_t* __restrict__ ndefl,
+                                   float* __restrict__ nval) {
+  lv_raw_tree_body(b, max_nodes, cand, coff, fill, split_median, nfeat, nthr, nleft, nright, ndefl, nval);
+}
+
+struct LvRawArgs {
+  const float* cand;
+  const int* coff;
+  const float* fill;
+  int split_median;
+  int* nfeat;
+  float* nthr;
+  int* nleft;
+  int* nright;
+  uint8_t* ndefl;
+  float* nval;
+};
+
+// Tree tail in ONE single-block launch (each of these was its own ~5-us launch at the end of
+// every tree): the deferred last level's children planning (children = 1), then the
+// bin-threshold arrays (finalize) and the raw-threshold tree for the test-set pass. Same
+// block, so a workgroup barrier orders the node-table writes before the reads.
+__global__ __launch_bounds__(kPlanThreads) void lv_tail_kernel(LvParams p, LvBufs b, int children, int build_base,
+                                                               int half, int dgap, int use_loc, int fused,
+                                                               int max_nodes, LvRawArgs r) {
+  if (children) {
+    lv_plan_children_body<kMaxPend, false>(p, b, 1, build_base, half, dgap, use_loc, fused);
+    __syncthreads();
+  }
+  lv_finalize_body(b, max_nodes);
+  if (r.nfeat)
+    lv_raw_tree_body(b, max_nodes, r.cand, r.coff, r.fill, r.split_median, r.nfeat, r.nthr, r.nleft, r.nright,
+                     r.ndefl, r.nval);
+}
+
 // Fixed-point scales from the (all-reduced) max |g|, |h| and global row count.
 __global__ void lv_scales_kernel(const float* __restrict__ mx, const long long* __restrict__ cnt,
                                  float* __restrict__ scales, double* __restrict__ inv_scales) {
-  if (threadIdx.x >= 2) return;
-  const double m = (double)mx[threadIdx.x];
-  double s = 1.0;
-  if (m > 0.0) {
-    const double n = (double)max(1LL, cnt[1]);
-    int k = (int)floor(log2(4611686018427387904.0 / (m * n)));
-    k = min(max(k, -120), 120);
-    s = ldexp(1.0, k);
-  }
-  scales[threadIdx.x] = (float)s;
-  inv_scales[threadIdx.x] = 1.0 / s;
+  lv_scales_body(mx, cnt, scales, inv_scales);
 }
 
 }  // namespace ytk
@@ -600,14 +651,7 @@ static LvBufs make_bufs(const uintptr_t* a) {
   return b;
 }
 
-extern "C" {
-
-// which: 0 init, 1 plan_split (arg1 = fused: patch the previous level's cnt_global from
-//        left_glob; 2: line-spaced cursors of the fused partition), 3 plan_children(arg0=build_base, arg1=half | ncs<<14 | fused<<29 |
-//        use_loc<<30; derived slots start at build_base + half + ncs),
-//        4 finalize(arg0=max_nodes)
-void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* fp, int arg0,
-                 int arg1, uintptr_t stream) {
+static LvParams make_params(const int* ip, const float* fp) {
   LvParams p;
   p.max_depth = ip[0];
   p.max_leaf_cnt = ip[1];
@@ -623,10 +667,25 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
   p.l2 = fp[3];
   p.max_abs_leaf = fp[4];
   p.lr = fp[5];
+  return p;
+}
+
+extern "C" {
+
+// which: 0 init, 1 plan_split (arg1 = fused: patch the previous level's cnt_global from
+//        left_glob; 2: line-spaced cursors of the fused partition), 3 plan_children(arg0=build_base, arg1=half | ncs<<14 | fused<<29 |
+//        use_loc<<30; derived slots start at build_base + half + ncs),
+//        4 finalize(arg0=max_nodes)
+void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* fp, int arg0,
+                 int arg1, uintptr_t stream) {
+  LvParams p = make_params(ip, fp);
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
-    case 0: hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b); break;
+    case 0:
+      hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, (const float*)nullptr,
+                         (float*)nullptr, (double*)nullptr);
+      break;
     case 1:  // arg0 = 1: no partition work list (single-pass partition maps blocks itself)
       hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1, arg0);
       break;
@@ -646,21 +705,7 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
 void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t binsT, long long ncol,
                                uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                int count_only, int arg0, int arg1, int maxp, uintptr_t stream) {
-  LvParams p;
-  p.max_depth = ip[0];
-  p.max_leaf_cnt = ip[1];
-  p.min_split_samples = ip[2];
-  p.hist_target = ip[3];
-  p.part_target = ip[4];
-  p.min_rows = ip[5];
-  p.part_chunk = ip[6];
-  p.split_groups = max(1, ip[7]);
-  p.min_split_loss = fp[0];
-  p.mcw = fp[1];
-  p.l1 = fp[2];
-  p.l2 = fp[3];
-  p.max_abs_leaf = fp[4];
-  p.lr = fp[5];
+  LvParams p = make_params(ip, fp);
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
@@ -721,21 +766,7 @@ void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, uintptr_t f
 void ytk_lv_split_plan(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t hist, int B, int F,
                        uintptr_t nbins_f, uintptr_t fmask, int f0, int nitems, const float* gpf, uintptr_t inv_dev,
                        uintptr_t part, uintptr_t counters, int implicit_items, int maxp, uintptr_t stream) {
-  LvParams p;
-  p.max_depth = ip[0];
-  p.max_leaf_cnt = ip[1];
-  p.min_split_samples = ip[2];
-  p.hist_target = ip[3];
-  p.part_target = ip[4];
-  p.min_rows = ip[5];
-  p.part_chunk = ip[6];
-  p.split_groups = max(1, ip[7]);
-  p.min_split_loss = fp[0];
-  p.mcw = fp[1];
-  p.l1 = fp[2];
-  p.l2 = fp[3];
-  p.max_abs_leaf = fp[4];
-  p.lr = fp[5];
+  LvParams p = make_params(ip, fp);
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int Bp = B + 1;
@@ -773,6 +804,33 @@ void ytk_lv_raw_tree(const uintptr_t* ptrs, int max_nodes, uintptr_t cand, uintp
                      reinterpret_cast<hipStream_t>(stream), b, max_nodes, (const float*)cand,
                      (const int*)coff, (const float*)fill, split_median, (int*)nfeat, (float*)nthr,
                      (int*)nleft, (int*)nright, (uint8_t*)ndefl, (float*)nval);
+  YTK_LAUNCH_CHECK();
+}
+
+
+// lv_step(0) with the tree's fixed-point scales computed by the same launch
+void ytk_lv_init_scales(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t mx, uintptr_t scales,
+                        uintptr_t inv_scales, uintptr_t stream) {
+  LvParams p = make_params(ip, fp);
+  LvBufs b = make_bufs(ptrs);
+  hipLaunchKernelGGL(lv_init_kernel, dim3(1), dim3(kPlanThreads), 0, reinterpret_cast<hipStream_t>(stream), p, b,
+                     (const float*)mx, (float*)scales, (double*)inv_scales);
+  YTK_LAUNCH_CHECK();
+}
+
+// Tree tail (lv_tail_kernel): children = 1 runs lv_step(3)'s planning first (arg0 / arg1 as
+// there); raw outputs optional (nfeat == 0: finalize only).
+void ytk_lv_tail(const uintptr_t* ptrs, const int* ip, const float* fp, int children, int arg0, int arg1,
+                 int max_nodes, uintptr_t cand, uintptr_t coff, uintptr_t fill, int split_median, uintptr_t nfeat,
+                 uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl, uintptr_t nval,
+                 uintptr_t stream) {
+  LvParams p = make_params(ip, fp);
+  LvBufs b = make_bufs(ptrs);
+  LvRawArgs r{(const float*)cand, (const int*)coff, (const float*)fill, split_median, (int*)nfeat, (float*)nthr,
+              (int*)nleft, (int*)nright, (uint8_t*)ndefl, (float*)nval};
+  hipLaunchKernelGGL(lv_tail_kernel, dim3(1), dim3(kPlanThreads), 0, reinterpret_cast<hipStream_t>(stream), p, b,
+                     children, arg0, arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), (arg1 >> 30) & 1,
+                     (arg1 >> 29) & 1, max_nodes, r);
   YTK_LAUNCH_CHECK();
 }
 

@@ -261,7 +261,10 @@ __device__ __forceinline__ void block_acc(double lsum, double wsum, double* loss
 
 // loss_acc[0:2] = sum over the nblocks partials, in block order (fixed per-thread strides,
 // then thread order).
-__device__ __forceinline__ void acc_finish_body(double* __restrict__ loss_acc, int nblocks) {
+// out (optional): where the two sums go (default loss_acc[0:2]) -- the round tail writes the
+// train and test sums next to each other so one copy reads them back.
+__device__ __forceinline__ void acc_finish_body(double* __restrict__ loss_acc, int nblocks,
+                                                double* __restrict__ out = nullptr) {
   __shared__ double s_red[2][256];
   const double* part = loss_acc + kAccPart;
   double a = 0.0, c = 0.0;
@@ -275,13 +278,19 @@ __device__ __forceinline__ void acc_finish_body(double* __restrict__ loss_acc, i
   if (threadIdx.x == 0) {
     double ta = 0.0, tc = 0.0;
     for (int t = 0; t < 256; ++t) { ta += s_red[0][t]; tc += s_red[1][t]; }
-    loss_acc[0] = ta;
-    loss_acc[1] = tc;
+    double* o = out ? out : loss_acc;
+    o[0] = ta;
+    o[1] = tc;
   }
 }
 
-__global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ loss_acc, int nblocks) {
-  acc_finish_body(loss_acc, nblocks);
+// block 0: loss_acc -> out (or in place); block 1 (acc2 != nullptr): acc2 -> out2 -- a second
+// pass's partials (the test-set tail) finished by the same launch
+__global__ __launch_bounds__(256) void acc_finish_kernel(double* __restrict__ loss_acc, int nblocks,
+                                                         double* __restrict__ out, double* __restrict__ acc2,
+                                                         int nblocks2, double* __restrict__ out2) {
+  if (blockIdx.x == 0) acc_finish_body(loss_acc, nblocks, out);
+  else acc_finish_body(acc2, nblocks2, out2);
 }
 
 // Test-set round tail in one pass (K == 1, one new tree): walk the raw row held in
@@ -695,10 +704,16 @@ __global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
 // out[node] = rows of the tree's node over all tree_grad blocks (one block per node, block
 // order sums: deterministic), as doubles next to the round's loss sums
 __global__ __launch_bounds__(256) void leaf_count_reduce_kernel(const int* __restrict__ part, int nblocks, int nnodes,
-                                                                double* __restrict__ out, double* __restrict__ loss_acc) {
+                                                                double* __restrict__ out, double* __restrict__ loss_acc,
+                                                                double* __restrict__ acc_out, double* __restrict__ acc2,
+                                                                int nblocks2, double* __restrict__ acc2_out) {
   __shared__ long long s_red[256];
   if (blockIdx.x == (unsigned)nnodes) {  // the extra block: the loss sums (acc_finish_kernel's work)
-    acc_finish_body(loss_acc, nblocks);
+    acc_finish_body(loss_acc, nblocks, acc_out);
+    return;
+  }
+  if (blockIdx.x == (unsigned)nnodes + 1) {  // a second pass's loss sums (the test-set tail)
+    acc_finish_body(acc2, nblocks2, acc2_out);
     return;
   }
   const int node = blockIdx.x;
@@ -802,7 +817,7 @@ void ytk_forest_predict(uintptr_t X, long long xstride, long long N, uintptr_t n
 int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t nfeat, uintptr_t nthr,
                          uintptr_t nleft, uintptr_t nright, uintptr_t ndefl, uintptr_t nval, int root, int nnodes,
                          uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight, int loss_id, float p0,
-                         float score_div, uintptr_t pred, uintptr_t loss_acc, uintptr_t stream) {
+                         float score_div, uintptr_t pred, uintptr_t loss_acc, int finish, uintptr_t stream) {
   if (N <= 0) return 0;
   const int kf4 = (int)(xstride / 4);
   if (xstride % 4 != 0 || kf4 < 1 || kf4 > 8 || (X % 16) != 0 || nnodes <= 0 || nnodes > 2048 || loss_id < 0 ||
@@ -838,9 +853,20 @@ int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t 
 #undef YTK_FLR_L
 #undef YTK_FLR
   YTK_LAUNCH_CHECK();
-  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
+  if (finish) {  // else the caller finishes the partials later (ytk_tree_grad_hist's acc2 / ytk_acc_finish)
+    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid, (double*)nullptr,
+                       (double*)nullptr, 0, (double*)nullptr);
+    YTK_LAUNCH_CHECK();
+  }
+  return grid;  // the number of partials
+}
+
+// Ordered finish of one or two partial vectors (see acc_finish_kernel); out == 0: in place.
+void ytk_acc_finish(uintptr_t loss_acc, int nblocks, uintptr_t out, uintptr_t acc2, int nblocks2, uintptr_t out2,
+                    uintptr_t stream) {
+  hipLaunchKernelGGL(acc_finish_kernel, dim3(acc2 ? 2 : 1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (double*)loss_acc, nblocks, (double*)out, (double*)acc2, nblocks2, (double*)out2);
   YTK_LAUNCH_CHECK();
-  return 1;
 }
 
 // forest_predict with the row-register walk; returns 0 (nothing launched) when the layout
@@ -926,7 +952,8 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
 #undef YTK_GH
   }
   YTK_LAUNCH_CHECK();
-  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
+  hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid, (double*)nullptr,
+                     (double*)nullptr, 0, (double*)nullptr);
   YTK_LAUNCH_CHECK();
 }
 
@@ -1017,9 +1044,11 @@ int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfe
 #undef YTK_TG_ONE2
   if (leaf_part) {  // leaf counts + the loss sums in one launch (block nnodes = acc_finish)
     hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + 1), dim3(256), 0, s, (const int*)leaf_part, grid,
-                       nnodes, (double*)leaf_out, (double*)loss_acc);
+                       nnodes, (double*)leaf_out, (double*)loss_acc, (double*)nullptr, (double*)nullptr, 0,
+                       (double*)nullptr);
   } else {
-    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid);
+    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, grid, (double*)nullptr,
+                     (double*)nullptr, 0, (double*)nullptr);
   }
   YTK_LAUNCH_CHECK();
   return 1;
@@ -1037,7 +1066,10 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
                        uintptr_t weight, long long N, int loss_id, float p0, float score_div, uintptr_t pred,
                        uintptr_t gh, uintptr_t loss_acc, uintptr_t ghmax, uintptr_t leaf_part, uintptr_t leaf_out,
                        uintptr_t scales, uintptr_t staging, uintptr_t work, uintptr_t root_slot, int B, int F,
-                       uintptr_t stream) {
+                       uintptr_t acc_out, uintptr_t acc2, int nblocks2, uintptr_t acc2_out, uintptr_t stream) {
+  // acc_out (optional): where the loss sums go (default loss_acc[0:2]); acc2 / nblocks2 /
+  // acc2_out (optional): another pass's partials (the test-set tail) finished by the same
+  // launch -- the round's sums then sit next to each other for one readback copy
   if (N <= 0 || nnodes <= 0) return 0;
   if (stride != 32 || (bins % 16) != 0 || B > 256 || F > 32 || loss_id < 0 || loss_id > 4) return 0;
   const size_t lds = kTGHHistBytes + (size_t)nnodes * 5 * sizeof(int) +
@@ -1062,10 +1094,12 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
 #undef YTK_TGH
   YTK_LAUNCH_CHECK();
   if (leaf_part) {
-    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + 1), dim3(256), 0, s, (const int*)leaf_part, nvb,
-                       nnodes, (double*)leaf_out, (double*)loss_acc);
+    hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + (acc2 ? 2 : 1)), dim3(256), 0, s,
+                       (const int*)leaf_part, nvb, nnodes, (double*)leaf_out, (double*)loss_acc, (double*)acc_out,
+                       (double*)acc2, nblocks2, (double*)acc2_out);
   } else {
-    hipLaunchKernelGGL(acc_finish_kernel, dim3(1), dim3(256), 0, s, (double*)loss_acc, nvb);
+    hipLaunchKernelGGL(acc_finish_kernel, dim3(acc2 ? 2 : 1), dim3(256), 0, s, (double*)loss_acc, nvb,
+                       (double*)acc_out, (double*)acc2, nblocks2, (double*)acc2_out);
   }
   YTK_LAUNCH_CHECK();
   ytk_hist_reduce(staging, work, grid, root_slot, B, F, 0, 1, stream);

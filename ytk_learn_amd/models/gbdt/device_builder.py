@@ -230,6 +230,9 @@ class DeviceLevelBuilder:
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
+        self._slab_zeroed = False  # the whole slab was zeroed at the end of the previous tree
+        self._raw_req = None       # test-set raw tree written by the tree tail (set_raw_request)
+        self._raw_ready = False
         # True: each tree's snapshot is a copy (K trees per round need their own); the
         # trainer clears it for K == 1 -- the round reads the snapshot (gradient pass,
         # host readback) before the next tree overwrites it, in stream order
@@ -454,14 +457,13 @@ class DeviceLevelBuilder:
         if dist and not ghmax_global:
             mx = mx.clone()
             self.comm.allreduce_(mx, op="max")
-        h.lv_scales(ptr(mx), ptr(self.root_cnt), ptr(self.scales), ptr(self.inv_scales), s)
         tm = self.timer
-        tm.mark("init_stats")
-        # root
+        # root (+ the tree's fixed-point scales in the same launch)
         ptrs = self._ptrs()
         st_ptr = self.st.data_ptr()
         off = lambda w: st_ptr + 4 * w
-        h.lv_step(0, ptrs, ip, fp, 0, 0, s)
+        h.lv_init_scales(ptrs, ip, fp, ptr(mx), ptr(self.scales), ptr(self.inv_scales), s)
+        tm.mark("init_stats")
 
         def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0):
             if self._zero_all:
@@ -487,8 +489,9 @@ class DeviceLevelBuilder:
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
 
         if self.root_ready and not sampled:
-            # the root histogram came with the previous round's gradient pass
-            if self._zero_all:
+            # the root histogram came with the previous round's gradient pass (the other
+            # slots were zeroed with the root slot at the end of the previous tree)
+            if self._zero_all and not self._slab_zeroed:
                 self.hist[1:].zero_()
         else:
             build_hist(gh0, rows0, self.hist_target + 1, 0, 1)
@@ -507,6 +510,7 @@ class DeviceLevelBuilder:
         tm.mark("find_best_split")
         bb = 1 if self.bins.dtype == torch.uint8 else 2
         fused = self.fuse_counts
+        tail_children = None
         for d in range(p.max_depth):
             c = d + 1  # depth of the children created at this level
             last = c == p.max_depth
@@ -524,9 +528,9 @@ class DeviceLevelBuilder:
             tm.mark("plan")
             if last and self.defer_leaf_counts and not sampled:
                 # children planning with zero cursors: the leaves' sample counts are placeholders
-                # until the round's gradient pass (tree_grad) has walked every row to its leaf
-                h.lv_step(3, self._ptrs(), ip, fp, 0, (1 << (c - 1)) | (1 << 30), s)
-                tm.mark("plan")
+                # until the round's gradient pass (tree_grad) has walked every row to its leaf;
+                # run by the tree-tail launch below together with finalize + raw tree
+                tail_children = (1 << (c - 1)) | (1 << 30)
                 break
             npart = self.part_target + (1 << d) + 1
             lloc = ptrs[13]
@@ -613,14 +617,39 @@ class DeviceLevelBuilder:
             else:
                 self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
             tm.mark("find_best_split")
-        h.lv_step(4, self._ptrs(), ip, fp, self.max_nodes, 0, s)
+        # tree tail in one launch: [deferred children planning] + finalize + raw tree (when the
+        # trainer registered its test-set request, set_raw_request)
+        rq = self._raw_req
+        ro = rq["out"] if rq is not None else None
+        h.lv_tail(self._ptrs(), ip, fp, 1 if tail_children is not None else 0, 0,
+                  tail_children if tail_children is not None else 0, self.max_nodes,
+                  ptr(rq["cand"]) if rq else 0, ptr(rq["coff"]) if rq else 0, ptr(rq["fill"]) if rq else 0,
+                  rq["median"] if rq else 0, ptr(ro["nfeat"]) if rq else 0, ptr(ro["nthr"]) if rq else 0,
+                  ptr(ro["nleft"]) if rq else 0, ptr(ro["nright"]) if rq else 0, ptr(ro["ndefl"]) if rq else 0,
+                  ptr(ro["nval"]) if rq else 0, s)
+        self._raw_ready = rq is not None
+        self._slab_zeroed = False
         if self.fuse_root:
-            self.hist[0].zero_()  # the next gradient pass accumulates the next root here
+            # the next gradient pass accumulates the next root into slot 0; zero the whole slab
+            # now (one fill instead of slot 0 here + slots 1.. at the next tree's start)
+            if self._zero_all:
+                self.hist.zero_()
+                self._slab_zeroed = True
+            else:
+                self.hist[0].zero_()
         tm.mark("plan")
         self.tree_count += 1
         snap = self.snap.clone() if self.snapshot_copy else self.snap
         st, nodes, *arrays = self._snap_views(snap)
         return DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+
+    def swap_ping_pong(self):
+        """One tree's net effect on the Python-side buffer assignment (the partition swaps
+        rows / (g, h) with their ping-pong buffers once per split level). Used when the
+        trainer leaves graph replay after an odd number of replayed trees."""
+        if max(self.p.max_depth - 1, 0) & 1:
+            self.rows, self.rows_tmp = self.rows_tmp, self.rows
+            self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
 
     def root_target(self):
         """Arguments of the fused gradient + root histogram pass (gops.tree_grad root=)."""
@@ -636,8 +665,28 @@ class DeviceLevelBuilder:
         """(node table, leaf-value array) the engine's raw_tree / next snapshot read."""
         return self.nodes, self.tval
 
+    def set_raw_request(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
+        """Have every build() also write the raw-threshold tree (for test-set scoring) into
+        persistent arrays, by its tree-tail launch; raw_tree() with the same tables then
+        returns them without a launch."""
+        mn = self.max_nodes
+        out = {
+            "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nthr": torch.empty(mn, dtype=torch.float32, device=self.dev),
+            "nleft": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nright": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "ndefl": torch.empty(mn, dtype=torch.uint8, device=self.dev),
+            "nval": torch.empty(mn, dtype=torch.float32, device=self.dev),
+        }
+        self._raw_req = {"cand": cand, "coff": coff, "fill": fill, "median": 1 if split_median else 0, "out": out}
+        self._raw_ready = False
+
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (for test-set scoring), one forest entry."""
+        rq = self._raw_req
+        if (self._raw_ready and rq["cand"] is cand and rq["coff"] is coff and rq["fill"] is fill
+                and rq["median"] == (1 if split_median else 0)):
+            return rq["out"]
         mn = self.max_nodes
         out = {
             "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),

@@ -108,6 +108,9 @@ class GBDTTrainer:
         self.round_losses = {}      # round -> (train loss, test loss), filled as rounds land
         self._round_stats = {}      # round -> phase times of THAT round (for the metric sink)
         self._names_arr = None
+        self._graphs = None         # captured rounds (see _graph_round)
+        self._rb_dev = None         # the round's [train | test | leaf counts] vector (see _step_dev)
+        self._eager_rounds = 0
 
     # ------------------------------------------------------------ preparation
     def _specs(self) -> List[SamplerSpec]:
@@ -242,6 +245,12 @@ class GBDTTrainer:
         if self.test_data is not None:
             te = self.test_data
             self.Xte = torch.where(torch.isnan(te.X), self.fill_dev[None, :], te.X).contiguous()
+            if (isinstance(getattr(self, "builder", None), DeviceLevelBuilder) and self.K == 1
+                    and self.refiner is None):
+                # the tree-tail launch writes the raw-threshold tree for the test-set pass (one
+                # persistent set of arrays: K > 1 rounds keep one raw tree per class; l1 refines
+                # the leaf values after the build)
+                self.builder.set_raw_request(self.cand_dev, self.coff_dev, self.fill_dev, self.p.split_type == "median")
             self.te_score = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
             self.te_init = self._base_score(te)
             self.te_pred = torch.zeros((te.n, self.K), dtype=torch.float32, device=self.dev)
@@ -394,8 +403,23 @@ class GBDTTrainer:
 
     def _enqueue_readback(self, i: int, dev_trees, acc, acc_te):
         """Copy the round's tree snapshots + loss sums into one pinned buffer (async)."""
+        self._bound_inflight()
+        accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
+        self._readback_copy(i, dev_trees, accs, acc_te is not None, nlc)
+
+    def _bound_inflight(self):
         while len(self._inflight) >= 4:  # bounded: at most 4 rounds in flight
             self._drain(len(self._inflight) - 1)
+
+    def _readback_accs(self, dev_trees, acc, acc_te):
+        """Device side of the readback: the round's loss sums (+ leaf counts) in one vector."""
+        rbd = getattr(self, "_rb_dev", None)
+        if rbd is not None:  # already one vector (_step_dev's round tail)
+            self._rb_dev = None
+            accs, nlc = rbd
+            if self.comm.is_dist:
+                self.comm.allreduce_(accs)
+            return accs, nlc
         accs = torch.stack([acc, acc_te if acc_te is not None else torch.zeros_like(acc)]).to(self.dev).reshape(-1)
         # rows per leaf from the gradient pass (level engine, deferred last-level counts):
         # local counts, summed across ranks by the same all-reduce as the losses
@@ -405,6 +429,10 @@ class GBDTTrainer:
             accs = torch.cat([accs] + [c for c in lcs if c is not None])
         if self.comm.is_dist:
             self.comm.allreduce_(accs)  # GBDTOptimizer.java:502 (loss, weight) allreduce
+        return accs, nlc
+
+    def _readback_copy(self, i: int, dev_trees, accs, has_te: bool, nlc):
+        """Host side: async copies into a pinned buffer + an event; landed by _drain."""
         sizes = [dt.snap.numel() for dt in dev_trees]
         head = 8 * accs.numel()
         host = self._rb_buffer(head + sum(sizes))
@@ -417,7 +445,7 @@ class GBDTTrainer:
         if self.dev.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
-        self._inflight.append((i, dev_trees, host, ev, acc_te is not None, nlc))
+        self._inflight.append((i, dev_trees, host, ev, has_te, nlc))
 
     def _drain(self, lag: int = 0):
         """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log."""
@@ -482,6 +510,86 @@ class GBDTTrainer:
     def step(self, i: int):
         """One boosting round: K trees, score update, loss + next gradients, test scoring.
         Enqueues device work only (no host synchronisation on the device-builder path)."""
+        if self._graph_eligible() and self._graph_round(i):
+            return
+        self._graph_release()
+        dev_trees, acc, acc_te, _ = self._step_dev(i)
+        self._acc = (acc, acc_te)
+        self.rounds_done = i + 1
+        self._eager_rounds += 1
+        self._enqueue_readback(i, dev_trees, acc, acc_te)
+
+    # ------------------------------------------------------------ graph rounds
+    def _graph_eligible(self) -> bool:
+        """A level-engine round is a fixed launch sequence with device-resident counts, so on
+        one GPU the whole round (tree, score/gradient + next root histogram, test scoring,
+        loss vector) can be captured once and replayed: the host then spends one graph launch
+        instead of ~45 kernel launches and the Python around them per round (at a 1/8 shard the
+        eager host work, ~0.44 ms per round, was as long as the GPU work). Only rounds whose
+        launch arguments never change qualify: K == 1, no row / feature sampling, no random
+        forest averaging, no L1 refine, no per-phase profiling, one process."""
+        if self._graphs is False:
+            return False
+        tp = self.p.tree
+        ok = (self.dev.type == "cuda" and self.use_device_builder and isinstance(self.builder, DeviceLevelBuilder)
+              and not self.comm.is_dist and self.K == 1 and self.kernel_loss not in (None, "softmax")
+              and not self.rf and self.refiner is None and not self.exact and not self.profile
+              and tp.instance_sample_rate >= 1.0 and tp.feature_sample_rate >= 1.0
+              and getattr(self.builder, "fuse_root", False) and not self.builder.snapshot_copy
+              and os.environ.get("YTK_GRAPH", "1") != "0")
+        if not ok:
+            self._graph_release()
+            self._graphs = False
+        return ok
+
+    def _graph_round(self, i: int) -> bool:
+        """Replay the captured round (capturing it first). The engine swaps its row / (g, h)
+        ping-pong buffers an odd number of times per tree, so consecutive trees alternate
+        between two buffer assignments: two graphs, replayed alternately."""
+        if self._graphs is None:
+            if self._eager_rounds < 1:  # the first round builds its root eagerly
+                return False
+            torch.cuda.synchronize(self.dev)
+            b = self.builder
+            saved = (b.rows, b.rows_tmp, b.ghp, b.gh_tmp, b.tree_count, b.root_ready)
+            graphs, pool = [], None
+            try:
+                for _ in range(2):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        dev_trees, acc, acc_te, host_trees = self._step_dev(i)
+                        accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
+                    assert not host_trees
+                    pool = g.pool()
+                    graphs.append((g, dev_trees, acc, acc_te, accs, nlc))
+            except Exception as e:  # not capturable here: eager rounds, state as before
+                (b.rows, b.rows_tmp, b.ghp, b.gh_tmp, b.tree_count, b.root_ready) = saved
+                torch.cuda.synchronize(self.dev)
+                self.log.info(f"[GBDT] round capture failed ({type(e).__name__}: {e}); eager rounds")
+                self._graphs = False
+                return False
+            self._graphs = {"g": graphs, "n": 0}
+        st = self._graphs
+        self._bound_inflight()
+        g, dev_trees, acc, acc_te, accs, nlc = st["g"][st["n"] & 1]
+        g.replay()
+        st["n"] += 1
+        self._acc = (acc, acc_te)
+        self.rounds_done = i + 1
+        self._readback_copy(i, dev_trees, accs, acc_te is not None, nlc)
+        return True
+
+    def _graph_release(self):
+        """Leave graph mode (an eager round follows): after an odd number of replays the
+        engine's Python-side buffer assignment is one tree behind the device's."""
+        st = self._graphs
+        if isinstance(st, dict):
+            if st["n"] & 1:
+                self.builder.swap_ping_pong()
+            self._graphs = None
+
+    def _step_dev(self, i: int):
+        """The device work of a round; returns (device trees, train acc, test acc, host trees)."""
         lr = 1.0 if self.rf else self.p.tree.learning_rate
         self.builder.p.learning_rate = lr
         arrays, raws, host_trees, dev_trees = [], [], [], []
@@ -519,17 +627,43 @@ class GBDTTrainer:
         if not self.use_device_builder:
             self.timer.mark("build_tree")
         # score update + train loss after this round + gradients for the next round
+        self._rb_dev = None
+        te_early = None
         if self.K == 1 and self.kernel_loss is not None and self.kernel_loss != "softmax":
             need_max = self.ghmax_fixed is None  # the global bound replaces the per-tree max
             if need_max:
                 self.ghmax.zero_()
-            lc = None
-            if dev_trees and getattr(self.builder, "defer_leaf_counts", False) and self.builder.last_keep is None:
-                lc = torch.empty(arrays[0][0].shape[0], dtype=torch.float64, device=self.dev)
+            want_lc = dev_trees and getattr(self.builder, "defer_leaf_counts", False) and self.builder.last_keep is None
+            nlc = arrays[0][0].shape[0] if want_lc else 0
             root = self.builder.root_target() if (dev_trees and getattr(self.builder, "fuse_root", False)) else None
+            # Round tail in two launches fewer: the test-set pass runs FIRST with its loss
+            # partials left unfinished, the train pass's finish launch completes both, and
+            # the (train, test) sums land next to the leaf counts in ONE vector
+            # [train loss, weight | test loss, weight | leaf counts] -- the readback is one
+            # copy with no stack / cat kernels.
+            rb = acc_out = te_acc = None
+            if (root is not None and self.test_data is not None and len(raws) == 1
+                    and os.environ.get("YTK_FUSED_TEST_TAIL", "1") != "0"
+                    and os.environ.get("YTK_ROUND_VECTOR", "1") != "0"):
+                te = self.test_data
+                rb = torch.empty(4 + nlc, dtype=torch.float64, device=self.dev)
+                part = gops.forest_predict_loss(self.Xte, raws[0], self.te_score, self.te_init, te.y, te.weight,
+                                                self.kernel_loss, self._kparam(), self._score_div(i + 1),
+                                                self.te_pred, finish=False)
+                if part is None:
+                    rb = None
+                else:
+                    acc_out, te_acc = rb[0:2], (part[0], part[1], rb[2:4])
+                    te_early = rb[2:4]
+            lc = None
+            if want_lc:
+                lc = rb[4:] if rb is not None else torch.empty(nlc, dtype=torch.float64, device=self.dev)
             acc = gops.tree_grad(self.bins, arrays[0], self.score, self.init_score, self.y, self.w,
                                  self.kernel_loss, self._kparam(), self._score_div(i + 1), self.pred, self.gh[0],
-                                 True, self.ghmax[0] if need_max else None, leaf_counts=lc, root=root)
+                                 True, self.ghmax[0] if need_max else None, leaf_counts=lc, root=root,
+                                 acc_out=acc_out, te_acc=te_acc)
+            if rb is not None:
+                self._rb_dev = (rb, [nlc])
             if root is not None:
                 self.builder.root_ready = root["done"]
             if lc is not None:
@@ -540,12 +674,13 @@ class GBDTTrainer:
                     gops.tree_add_bins(self.binsT, arrays[k], self.score, k)
             acc = self._loss_grad(self.score, self.init_score, self.y, self.w, self.pred, self.gh, i + 1)
         self.timer.mark("grad_and_score")
-        # model conversion (slot -> raw threshold, names, default direction) for host trees
+        # model conversion (slot -> raw threshold, names, default direction) for host trees,
+        # before the test set is scored with their raw thresholds
         for tree in host_trees:
             self._convert(tree)
             self.model.trees.append(tree)
-        acc_te = None
-        if self.test_data is not None:
+        acc_te = te_early
+        if self.test_data is not None and acc_te is None:
             if host_trees:
                 fl = GBDTModel(self.model.base_prediction, self.K, self.model.loss_name)
                 fl.trees = host_trees
@@ -563,9 +698,7 @@ class GBDTTrainer:
                 acc_te = self._loss_grad(self.te_score, self.te_init, te.y, te.weight, self.te_pred, self.te_gh,
                                          i + 1, False)
             self.timer.mark("test_eval")
-        self._acc = (acc, acc_te)
-        self.rounds_done = i + 1
-        self._enqueue_readback(i, dev_trees, acc, acc_te)
+        return dev_trees, acc, acc_te, host_trees
 
     def _convert(self, tree: Tree):
         """convertModel (GBDTOptimizer.java:663-690): slot -> raw threshold, names, default

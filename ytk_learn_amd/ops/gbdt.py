@@ -518,12 +518,14 @@ def bin_assign(X, cand, coff, out, outT=None):
 ACC_LEN = 4 + 2 * 256 * 8  # == kAccLen (gbdt_score.hip): (loss, weight), counter, block partials
 
 
-def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_div, pred):
+def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_div, pred, finish=True):
     """Test-set round tail in one GPU pass (K == 1, ONE raw tree ``tree`` rooted at node 0, as
     forest_predict's dict; its troot / tout are not read): score += tree(row), then the loss sums and prediction -- exactly
     forest_predict + grad_hess(want_grad=False) (same values, same fp64 summation order).
     Returns the float64 [2] (loss sum, weight sum) device tensor, or None when the fused
-    kernel does not apply (the caller then runs the two steps)."""
+    kernel does not apply (the caller then runs the two steps). ``finish=False``: returns
+    (partials [ACC_LEN], number of partials) unfinished -- the caller finishes them with the
+    train-side pass (tree_grad(te_acc=...)), one launch less per round."""
     loss_id = LOSS_IDS[loss]
     if not (X.is_cuda and X.is_contiguous() and score.shape[1] == 1 and loss_id != 5
             and tree["troot"].numel() == 1):
@@ -534,8 +536,10 @@ def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_
                                 ptr(tree["nleft"]), ptr(tree["nright"]), ptr(tree["ndefl"]), ptr(tree["nval"]),
                                 0, tree["nfeat"].numel(), ptr(score),
                                 ptr(init), ptr(label), ptr(weight), loss_id, float(param), float(score_div),
-                                ptr(pred), ptr(acc), stream(X))
-    return acc[:2] if ok else None
+                                ptr(pred), ptr(acc), 1 if finish else 0, stream(X))
+    if not ok:
+        return None
+    return acc[:2] if finish else (acc, int(ok))
 
 
 def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want_grad=True,
@@ -622,8 +626,13 @@ def leaf_counts_fit(max_nodes: int) -> bool:
     return max_nodes * 6 * 4 <= LDS_BUDGET
 
 
+def acc_finish(acc, nblocks, out):
+    """Ordered finish of a pass's loss partials (forest_predict_loss(finish=False)) into out[0:2]."""
+    hip().acc_finish(ptr(acc), int(nblocks), ptr(out), 0, 0, 0, stream(acc))
+
+
 def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_div, pred, gh,
-              want_grad=True, ghmax=None, leaf_counts=None, root=None):
+              want_grad=True, ghmax=None, leaf_counts=None, root=None, acc_out=None, te_acc=None):
     """Fused K==1 round tail: score += tree(row) (bin space, ROW-MAJOR bins [N, S]), then
     pred (optional) / (g, h) / loss sums / max|g|,|h| (optional ``ghmax`` [1,2]).
     ``tree_arrays`` may be None (no tree). Returns float64 [2] (loss sum, weight sum).
@@ -632,7 +641,10 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
     ``root`` (optional dict, GPU): also accumulate the NEXT tree's root histogram in the same
     pass (tree_grad_hist_kernel) into the zeroed slot ``root["slot"]`` with the fixed-point
     scales ``root["scales"]``; ``root["done"]`` reports whether the fused pass ran (layouts it
-    does not cover fall back to the plain pass)."""
+    does not cover fall back to the plain pass).
+    ``acc_out`` (optional, float64 [2], GPU): where the loss sums go (the returned tensor is
+    then ``acc_out``); ``te_acc`` (optional): (partials, count, out [2]) of the test-set pass
+    to finish in the same launch (falls back to its own finish launch)."""
     loss_id = LOSS_IDS[loss]
     assert loss_id != 5 and score.shape[1] == 1
     if score.is_cuda:
@@ -658,9 +670,11 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
                     ptr(bins), bins.stride(0), ptr(tf), ptr(tt), ptr(tl), ptr(tr), ptr(tv), nn, ptr(score), ptr(init),
                     ptr(label), ptr(weight), N, loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                     ptr(ghmax), ptr(part), ptr(leaf_counts), root["scales"], root["staging"], root["work"],
-                    root["slot"], root["B"], root["F"], stream(score)))
+                    root["slot"], root["B"], root["F"], ptr(acc_out),
+                    ptr(te_acc[0]) if te_acc is not None else 0, int(te_acc[1]) if te_acc is not None else 0,
+                    ptr(te_acc[2]) if te_acc is not None else 0, stream(score)))
             if root["done"]:
-                return acc[:2]
+                return acc_out if acc_out is not None else acc[:2]
         ok = hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
                         bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
                         ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
@@ -669,6 +683,11 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
         if not ok:
             raise ValueError(f"tree_grad: per-node leaf counts of a {nn}-node tree exceed the LDS budget "
                              "(see leaf_counts_fit)")
+        if te_acc is not None:
+            acc_finish(te_acc[0], te_acc[1], te_acc[2])
+        if acc_out is not None:
+            acc_out.copy_(acc[:2])
+            return acc_out
         return acc[:2]
     assert leaf_counts is None, "leaf_counts: GPU only"
     if tree_arrays is not None:
