@@ -152,7 +152,12 @@ class DeviceLevelBuilder:
         # buffer so the per-tree snapshot is a single device copy
         mn = self.max_nodes
         self._snap_sizes = [64, mn * DNODE_DTYPE.itemsize] + [4 * mn] * 5
-        self.snap = torch.zeros(sum(self._snap_sizes), dtype=torch.uint8, device=dev)
+        # the snapshot and, 16-B aligned right behind it, the trainer's round vector
+        # [train loss, weight | test loss, weight | leaf counts] (round_vector): one readback copy
+        snap_total = sum(self._snap_sizes)
+        self.rv_off = (snap_total + 15) // 16 * 16
+        self._snap_full = torch.zeros(self.rv_off + 8 * (4 + mn), dtype=torch.uint8, device=dev)
+        self.snap = self._snap_full[:snap_total]
         (self.st, self.nodes, self.tfeat, self.tthr, self.tleft, self.tright,
          self.tval) = self._snap_views(self.snap)
         self.pending, self.next_pending = i32(self.maxp), i32(self.maxp)
@@ -641,7 +646,15 @@ class DeviceLevelBuilder:
         self.tree_count += 1
         snap = self.snap.clone() if self.snapshot_copy else self.snap
         st, nodes, *arrays = self._snap_views(snap)
-        return DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+        dt = DeviceTree(nodes, st, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+        if not self.snapshot_copy:
+            dt.snap_full, dt.rv_off = self._snap_full, self.rv_off
+        return dt
+
+    def round_vector(self, n: int) -> torch.Tensor:
+        """float64 [n] device vector stored right behind the snapshot (n <= 4 + max_nodes)."""
+        assert n <= 4 + self.max_nodes
+        return self._snap_full[self.rv_off:self.rv_off + 8 * n].view(torch.float64)
 
     def swap_ping_pong(self):
         """One tree's net effect on the Python-side buffer assignment (the partition swaps

@@ -433,6 +433,19 @@ class GBDTTrainer:
 
     def _readback_copy(self, i: int, dev_trees, accs, has_te: bool, nlc):
         """Host side: async copies into a pinned buffer + an event; landed by _drain."""
+        dt0 = dev_trees[0] if len(dev_trees) == 1 else None
+        rv_off = getattr(dt0, "rv_off", None)
+        if rv_off is not None and accs.data_ptr() == dt0.snap.data_ptr() + rv_off:
+            # the round vector sits right behind the snapshot: ONE copy of [snap | pad | vector]
+            nb = rv_off + 8 * accs.numel()
+            host = self._rb_buffer(nb)
+            host[:nb].copy_(dt0.snap_full[:nb], non_blocking=True)
+            ev = None
+            if self.dev.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.dev))
+            self._inflight.append((i, dev_trees, host, ev, has_te, nlc, rv_off))
+            return
         sizes = [dt.snap.numel() for dt in dev_trees]
         head = 8 * accs.numel()
         host = self._rb_buffer(head + sum(sizes))
@@ -445,18 +458,22 @@ class GBDTTrainer:
         if self.dev.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
-        self._inflight.append((i, dev_trees, host, ev, has_te, nlc))
+        self._inflight.append((i, dev_trees, host, ev, has_te, nlc, None))
 
     def _drain(self, lag: int = 0):
         """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log."""
         while len(self._inflight) > lag:
-            i, dev_trees, host, ev, has_te, nlc = self._inflight.popleft()
+            i, dev_trees, host, ev, has_te, nlc, rv_off = self._inflight.popleft()
             if ev is not None:
                 ev.synchronize()
             hb = host.numpy()
             head = 32 + 8 * sum(nlc)
-            a = hb[:head].view(np.float64)
-            off = head
+            if rv_off is None:  # [vector | snapshots]
+                a = hb[:head].view(np.float64)
+                off = head
+            else:  # [snapshot | pad | vector]
+                a = hb[rv_off:rv_off + head].view(np.float64)
+                off = 0
             coff = 4
             for dt, nc in zip(dev_trees, nlc):
                 sz = dt.snap.numel()
@@ -646,7 +663,8 @@ class GBDTTrainer:
                     and os.environ.get("YTK_FUSED_TEST_TAIL", "1") != "0"
                     and os.environ.get("YTK_ROUND_VECTOR", "1") != "0"):
                 te = self.test_data
-                rb = torch.empty(4 + nlc, dtype=torch.float64, device=self.dev)
+                rb = (self.builder.round_vector(4 + nlc) if hasattr(self.builder, "round_vector")
+                      else torch.empty(4 + nlc, dtype=torch.float64, device=self.dev))
                 part = gops.forest_predict_loss(self.Xte, raws[0], self.te_score, self.te_init, te.y, te.weight,
                                                 self.kernel_loss, self._kparam(), self._score_div(i + 1),
                                                 self.te_pred, finish=False)
