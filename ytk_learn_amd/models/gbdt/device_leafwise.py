@@ -82,7 +82,14 @@ class DeviceLeafBuilder:
         mn = self.max_nodes
         # snapshot buffer: st (64 B) | tree node table | scoring arrays (as the level engine)
         self._snap_sizes = [64, mn * DNODE_DTYPE.itemsize] + [4 * mn] * 5
-        self.snap = torch.zeros(sum(self._snap_sizes), dtype=torch.uint8, device=dev)
+        # snapshot + the trainer's round vector 16-B aligned behind it (one readback copy)
+        snap_total = sum(self._snap_sizes)
+        self.rv_off = (snap_total + 15) // 16 * 16
+        self._snap_full = torch.zeros(self.rv_off + 8 * (4 + mn), dtype=torch.uint8, device=dev)
+        self.snap = self._snap_full[:snap_total]
+        self._raw_req = None   # test-set raw tree written by the tree-tail launch
+        self._raw_ready = False
+        self.snapshot_copy = True  # the trainer clears it for K == 1 rounds
         (self.st, self.tnodes, self.tfeat, self.tthr, self.tleft, self.tright,
          self.tval) = self._snap_views(self.snap)
         cap = self.cap
@@ -432,14 +439,46 @@ class DeviceLeafBuilder:
 
     def _finish(self, h, s, it) -> DeviceTree:
         self.timer.mark("batches")
-        h.lv_step(4, self._lv_ptrs(), [0] * 8, [0.0] * 6, self.max_nodes, 0, s)
+        # finalize (+ the raw-threshold tree for the test-set pass) in one launch
+        rq = self._raw_req
+        ro = rq["out"] if rq is not None else None
+        h.lv_tail(self._lv_ptrs(), [0] * 8, [0.0] * 6, 0, 0, 0, self.max_nodes,
+                  ptr(rq["cand"]) if rq else 0, ptr(rq["coff"]) if rq else 0, ptr(rq["fill"]) if rq else 0,
+                  rq["median"] if rq else 0, ptr(ro["nfeat"]) if rq else 0, ptr(ro["nthr"]) if rq else 0,
+                  ptr(ro["nleft"]) if rq else 0, ptr(ro["nright"]) if rq else 0, ptr(ro["ndefl"]) if rq else 0,
+                  ptr(ro["nval"]) if rq else 0, s)
+        self._raw_ready = rq is not None
         if self.fuse_root:
             self.hist[0].zero_()  # the next gradient pass accumulates the next root here
         self.tree_count += 1
         self.last_batches = it
-        snap = self.snap.clone()
+        # K > 1 rounds build several trees before their arrays are consumed: copies; a K == 1
+        # round consumes the tree (gradient pass, test pass, readback copy) before the next build
+        snap = self.snap.clone() if self.snapshot_copy else self.snap
         st_t, nodes, *arrays = self._snap_views(snap)
-        return DeviceTree(nodes, st_t, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+        dt = DeviceTree(nodes, st_t, tuple(arrays), self.max_nodes, snap, self._snap_sizes[0])
+        if not self.snapshot_copy:
+            dt.snap_full, dt.rv_off = self._snap_full, self.rv_off
+        return dt
+
+    def round_vector(self, n: int) -> torch.Tensor:
+        """float64 [n] device vector (the trainer's round losses + leaf counts)."""
+        assert n <= 4 + self.max_nodes
+        return self._snap_full[self.rv_off:self.rv_off + 8 * n].view(torch.float64)
+
+    def set_raw_request(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
+        """As DeviceLevelBuilder.set_raw_request: the tree tail writes the raw tree."""
+        mn = self.max_nodes
+        out = {
+            "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nthr": torch.empty(mn, dtype=torch.float32, device=self.dev),
+            "nleft": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "nright": torch.empty(mn, dtype=torch.int32, device=self.dev),
+            "ndefl": torch.empty(mn, dtype=torch.uint8, device=self.dev),
+            "nval": torch.empty(mn, dtype=torch.float32, device=self.dev),
+        }
+        self._raw_req = {"cand": cand, "coff": coff, "fill": fill, "median": 1 if split_median else 0, "out": out}
+        self._raw_ready = False
 
     def prof_report(self) -> dict:
         """Accumulated planner phase times (us, 100 MHz wall clock) and work counters."""
@@ -474,6 +513,10 @@ class DeviceLeafBuilder:
 
     def raw_tree(self, cand: torch.Tensor, coff: torch.Tensor, fill: torch.Tensor, split_median: bool):
         """Raw-threshold arrays of the LAST built tree (test-set scoring)."""
+        rq = self._raw_req
+        if (self._raw_ready and rq["cand"] is cand and rq["coff"] is coff and rq["fill"] is fill
+                and rq["median"] == (1 if split_median else 0)):
+            return rq["out"]
         mn = self.max_nodes
         out = {
             "nfeat": torch.empty(mn, dtype=torch.int32, device=self.dev),

@@ -184,6 +184,7 @@ class GBDTTrainer:
             # the builder waits on its planner while a tree grows: land the previous rounds
             # (tree conversion, loss log) in that wait instead of between trees
             self.builder.idle_hook = lambda: self._drain(0)
+            self.builder.snapshot_copy = self.K != 1
             self._fuse_root_pending = True
         elif self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
@@ -245,7 +246,7 @@ class GBDTTrainer:
         if self.test_data is not None:
             te = self.test_data
             self.Xte = torch.where(torch.isnan(te.X), self.fill_dev[None, :], te.X).contiguous()
-            if (isinstance(getattr(self, "builder", None), DeviceLevelBuilder) and self.K == 1
+            if (isinstance(getattr(self, "builder", None), (DeviceLevelBuilder, DeviceLeafBuilder)) and self.K == 1
                     and self.refiner is None):
                 # the tree-tail launch writes the raw-threshold tree for the test-set pass (one
                 # persistent set of arrays: K > 1 rounds keep one raw tree per class; l1 refines
