@@ -34,6 +34,22 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
+
+
+def _row_cumsum(x: torch.Tensor) -> torch.Tensor:
+    """Inclusive prefix sums along dim 1 of an int64 [C, n] tensor, exact. One device-wide scan
+    of the flattened tensor, then each row's start subtracted: torch's scan along the inner
+    dimension of a 2-D tensor runs one block per row (~5 ms per [4, 2M] call on MI355X, 80 %
+    of an exact-greedy tree), the flat scan is memory bound. Integer wraparound past 2^63
+    cancels in the subtraction (each row's true prefix fits in int64)."""
+    C, n = x.shape
+    if C == 0 or n == 0:
+        return torch.cumsum(x, dim=1)
+    flat = torch.cumsum(x.reshape(-1), 0).view(C, n)
+    if C > 1:
+        starts = flat[:-1, -1:].clone()  # sum of all rows before row r, at row r - 1's end
+        flat[1:] -= starts
+    return flat
 from ...parallel.comm import Comm
 from .builder import TimeStats, TreeParams
 from .tree import Tree
@@ -161,7 +177,7 @@ class ExactGreedyBuilder:
                 lg, lh = [], []
                 for comp in (0, 1):
                     x = qT[comp][o]                             # [C, n] int64
-                    excl = torch.cumsum(x, dim=1) - x           # sums of the rows before i
+                    excl = _row_cumsum(x) - x                    # sums of the rows before i
                     base = excl[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K] node start
                     (lg if comp == 0 else lh).append(excl - base[:, pos_node])
                 left_g, left_h = lg[0], lh[0]
@@ -281,7 +297,7 @@ class ExactGreedyBuilder:
         integers): prefix-sum differences, no atomics."""
         xt = x.reshape(x.shape[0], -1).t().contiguous()  # scan along the innermost dimension
         z = torch.zeros((xt.shape[0], 1), dtype=x.dtype, device=x.device)
-        cs = torch.cat([z, torch.cumsum(xt, 1)], 1)
+        cs = torch.cat([z, _row_cumsum(xt)], 1)
         out = (cs[:, bnd[1:]] - cs[:, bnd[:-1]]).t()
         return out.reshape((bnd.numel() - 1,) + tuple(x.shape[1:]))
 
@@ -323,8 +339,8 @@ class ExactGreedyBuilder:
             alive = alive_pos[None].expand(C, n)
             li = (lf & alive).to(torch.int64)
             ri = ((~lf) & alive).to(torch.int64)
-            lc = torch.cumsum(li, 1) - li                     # lefts before i (whole column)
-            rcs = torch.cumsum(ri, 1) - ri
+            lc = _row_cumsum(li) - li                         # lefts before i (whole column)
+            rcs = _row_cumsum(ri) - ri
             lbase = lc[:, bnd[:-1].clamp(max=max(n - 1, 0))]  # [C, K] at each node start
             rbase = rcs[:, bnd[:-1].clamp(max=max(n - 1, 0))]
             k2 = 2 * pos_node[None].expand(C, n)
