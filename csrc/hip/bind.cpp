@@ -173,7 +173,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fm_sgd_update", &ytk_fm_sgd_update);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6)
+    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_step: bad argument sizes");
     ytk_lv_step(which, ptrs.data(), ip.data(), fp.data(), a0, a1, stream);
   });
@@ -189,14 +189,14 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lv_init_scales", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                              const std::vector<float>& fp, uintptr_t mx, uintptr_t scales, uintptr_t inv,
                              uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() < 8 || fp.size() < 6) throw std::invalid_argument("lv_init_scales: bad sizes");
+    if (ptrs.size() != 26 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_init_scales: bad sizes");
     ytk_lv_init_scales(ptrs.data(), ip.data(), fp.data(), mx, scales, inv, stream);
   });
   m.def("lv_tail", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp,
                       int children, int a0, int a1, int max_nodes, uintptr_t cand, uintptr_t coff, uintptr_t fill,
                       int median, uintptr_t nfeat, uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
                       uintptr_t nval, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() < 8 || fp.size() < 6) throw std::invalid_argument("lv_tail: bad sizes");
+    if (ptrs.size() != 26 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_tail: bad sizes");
     ytk_lv_tail(ptrs.data(), ip.data(), fp.data(), children, a0, a1, max_nodes, cand, coff, fill, median, nfeat, nthr,
                 nleft, nright, ndefl, nval, stream);
   });
@@ -204,7 +204,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                      int count_only, int a0, int a1, int maxp, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6)
+    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
                               max_blocks, count_only, a0, a1, maxp, stream);
@@ -214,7 +214,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,
                               uintptr_t fmask, int f0, int nitems, const std::vector<float>& gpf, uintptr_t inv_dev,
                               uintptr_t part, uintptr_t counters, int implicit_items, int maxp, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 8 || fp.size() != 6 || gpf.size() != 4)
+    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6 || gpf.size() != 4)
       throw std::invalid_argument("lv_split_plan: bad argument sizes");
     ytk_lv_split_plan(ptrs.data(), ip.data(), fp.data(), hist, B, F, nbins_f, fmask, f0, nitems, gpf.data(), inv_dev,
                       part, counters, implicit_items, maxp, stream);

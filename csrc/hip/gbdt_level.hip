@@ -39,7 +39,19 @@ struct LvParams {
   int hist_target, part_target, min_rows;
   int part_chunk;  // rows per single-pass partition chunk (fused kernel: 256 x rows per thread)
   int split_groups;  // split records per item (feature groups of split_node_kernel; 1 = one)
+  // 1: the last level is not partitioned (leaf counts come from the gradient pass), so at
+  // the level before it only the child that gets a histogram is ever read again -- its
+  // partition writes that child's rows alone (scatter mask in part_thr, see keep_row)
+  int small_only;
 };
+
+// The child whose histogram is built (the other is parent - built): by the hessian sums,
+// which every rank knows before the partition (exact int64 histograms make the choice
+// result neutral). Used wherever the choice must precede the row counts.
+__device__ __forceinline__ bool left_small_by_hess(double hl, double H) { return hl < H - hl; }
+__device__ __forceinline__ bool small_only_level(int small_only, int max_depth, int depth) {
+  return small_only && max_depth >= 0 && depth + 2 == max_depth;
+}
 
 struct LvBufs {
   int* st;
@@ -307,7 +319,9 @@ __device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused
       b.split_nid[s] = id;
       b.split_snap[s] = num_leaf0 + s + 1;  // leaf count after this split
       b.part_feat[s] = n.feat;
-      b.part_thr[s] = (n.bin_a + n.bin_b) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
+      const int keep = small_only_level(p.small_only, p.max_depth, n.depth)
+                           ? (left_small_by_hess(n.hl, n.H) ? 1 : 2) : 0;
+      b.part_thr[s] = ((n.bin_a + n.bin_b) >> 1) | (keep << kKeepShift);  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
       b.part_begin[s] = n.begin;
       b.part_nblk[s] = n.cnt_local;              // temporarily: count
       b.part_cnt[s] = n.cnt_local;
@@ -397,7 +411,8 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
       R.value = leaf_value(R.G, R.H, p);
       s_nb[s] = 0;
     } else {
-      const bool left_small = fused ? (P.hl < P.H - P.hl) : (L.cnt_global < R.cnt_global);
+      const bool left_small = (fused || small_only_level(p.small_only, p.max_depth, P.depth))
+                                  ? left_small_by_hess(P.hl, P.H) : (L.cnt_global < R.cnt_global);
       s_small[s] = left_small ? P.left : P.right;
       s_nb[s] = 1;
       atomicAdd(reinterpret_cast<unsigned long long*>(&s_total),
@@ -661,6 +676,7 @@ static LvParams make_params(const int* ip, const float* fp) {
   p.min_rows = ip[5];
   p.part_chunk = ip[6];
   p.split_groups = max(1, ip[7]);
+  p.small_only = ip[8];
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];

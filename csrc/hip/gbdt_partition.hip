@@ -34,7 +34,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_flags_kernel(
   if (nitems_dev && (int)blockIdx.x >= *nitems_dev) return;
   const int4 it = items[blockIdx.x];
   const BinT* col = binsT + (size_t)feat[it.x] * ncol;
-  const int t = thr[it.x];
+  const int t = thr[it.x] & kThrMask;
   int c = 0;
   int pos = it.y + threadIdx.x;
   for (; pos + 3 * kPartThreads < it.z; pos += 4 * kPartThreads) {

@@ -18,6 +18,14 @@ constexpr int kCurStride = 16;   // u64 per split cursor (128 B)
 constexpr int kDoneGroups = 16;
 constexpr int kDoneWords = (kDoneGroups + 1) * kCurStride;  // u64 of counter space
 
+// Split thresholds carry a scatter mask in their top bits (level engine, last scatter level:
+// only the child that gets a histogram is ever read again, so only its rows are written;
+// the counts and the segment geometry are unchanged): 0 both children, 1 left only, 2 right
+// only. Thresholds are bin indices (< 2^16).
+constexpr int kKeepShift = 30;
+constexpr int kThrMask = (1 << kKeepShift) - 1;
+__device__ __forceinline__ bool keep_row(int keep, bool left) { return keep == 0 || (keep == 1) == left; }
+
 // true in exactly one block of the grid: the last to arrive. Block b counts itself in
 // group b % G; the block completing its group counts the group at the top counter. All
 // counters reset themselves (atomic exchange by their last arriver), so ctr must be zero
@@ -104,7 +112,8 @@ __device__ __forceinline__ void partition_atomic_body(
   }
   const int si = lo;
   // independent loads of the split's parameters (one round trip)
-  const int fb = first_blk[si], nbeg = node_begin[si], ncnt = node_count[si], fs = feat[si], th = thr[si];
+  const int fb = first_blk[si], nbeg = node_begin[si], ncnt = node_count[si], fs = feat[si];
+  const int th = thr[si] & kThrMask, keep = (int)((unsigned)thr[si] >> kKeepShift);
   const int beg = nbeg + (bid - fb) * CH;
   const int end = min(beg + CH, nbeg + ncnt);
   const int nend = nbeg + ncnt;
@@ -173,8 +182,10 @@ __device__ __forceinline__ void partition_atomic_body(
       if (rank < tv) {
         const int lb = s_l[j * NW + wid] + lrank[j];  // left rows before this one
         const int dst = left[j] ? lstart + lb : rstart + (rank - lb);
-        rows_out[dst] = r[j];
-        if (gh_out) gh_out[dst] = g[j];
+        if (keep_row(keep, left[j])) {
+          rows_out[dst] = r[j];
+          if (gh_out) gh_out[dst] = g[j];
+        }
       }
     }
   }
@@ -214,7 +225,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     __syncthreads();
   }
   const unsigned long long lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
-  struct Chunk { int si, beg, end, nbeg, nend, fs, th; };
+  struct Chunk { int si, beg, end, nbeg, nend, fs, th, keep; };
   auto locate = [&](int bid) {
     int lo = 0, hi = nsplit - 1;  // last split with first_blk <= bid
     while (lo < hi) {
@@ -225,7 +236,9 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     c.si = lo;
     const int fb = first_blk[lo], nbeg = node_begin[lo], ncnt = node_count[lo];
     c.fs = feat[lo];
-    c.th = thr[lo];
+    const int tr = thr[lo];
+    c.th = tr & kThrMask;
+    c.keep = (int)((unsigned)tr >> kKeepShift);
     c.beg = nbeg + (bid - fb) * CH;
     c.end = min(c.beg + CH, nbeg + ncnt);
     c.nbeg = nbeg;
@@ -331,8 +344,10 @@ __device__ __forceinline__ void partition_atomic_body_pf(
         if (rank < tv) {
           const int lb = s_l[j * NW + wid] + lrank[j];
           const int dst = left[j] ? lstart + lb : rstart + (rank - lb);
-          rows_out[dst] = r[j];
-          if (gh_out) gh_out[dst] = g[j];
+          if (keep_row(c.keep, left[j])) {
+            rows_out[dst] = r[j];
+            if (gh_out) gh_out[dst] = g[j];
+          }
         }
       }
     }

@@ -55,7 +55,9 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
         with open(os.path.join(out, "model.txt"), "w") as f:
             f.write(model.dumps())
         with open(os.path.join(out, "res.json"), "w") as f:
+            backend = torch.distributed.get_backend() if torch.distributed.is_initialized() else "none"
             json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats,
+                       "backend": backend, "is_dist": comm.is_dist,
                        "peer_calls": peer.calls if peer is not None else 0}, f)
 
 

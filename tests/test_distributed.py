@@ -165,6 +165,40 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     _same_collective_sequence(tmp_path / f"w{world}", world)
 
 
+@pytest.mark.parametrize("task,mode", [("gbdt", "allreduce"), ("gbdt_loss", "owner")])
+def test_forced_dist_world1_gloo(tmp_path, task, mode):
+    """YTK_FORCE_DIST=1 at world 1 takes every multi-rank code path (collectives issued to a
+    one-rank group) and must give the plain world-1 model byte for byte."""
+    env = {"YTK_HIST_SYNC": mode}
+    _run(task, tmp_path / "plain", 1, extra_env=env)
+    res = _run(task, tmp_path / "forced", 1, extra_env=dict(env, YTK_FORCE_DIST="1"))
+    assert res["is_dist"] and res["backend"] == "gloo" and res["comm"]["calls"] > 0
+    assert res["owner"] == (mode == "owner")
+    assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "forced" / "model.txt").read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task,mode", [("gbdt", "allreduce"), ("gbdt", "owner"), ("gbdt_loss", "allreduce"),
+                                       ("gbdt_loss", "owner")])
+def test_rccl_world1_forced_dist(tmp_path, task, mode):
+    """The real nccl (= RCCL) backend on the one GPU of the test box: a world-1 process group
+    with YTK_FORCE_DIST=1 runs the multi-GPU engines' RCCL calls (init with device_id, async
+    all-reduce work handles waited on the compute stream, reduce-scatter + all-gather of the
+    owner mode, the gloo side group for host scalars) -- RCCL refuses two ranks on one GPU,
+    so this is the RCCL-semantics check available here; the model must equal the plain
+    world-1 run byte for byte."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_HIST_SYNC": mode, "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}
+    _run(task, tmp_path / "plain", 1, "cuda", extra_env=env)
+    res = _run(task, tmp_path / "rccl", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
+    assert res["is_dist"] and res["backend"] == "nccl" and res["comm"]["calls"] > 0
+    if task == "gbdt":  # the GPU leaf-wise engine has one sync mode (one batch message all-reduced)
+        assert res["owner"] == (mode == "owner")
+    assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "rccl" / "model.txt").read()
+
+
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
 def test_sgd_world2_model_averaging(tmp_path, task):
     """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every

@@ -251,7 +251,8 @@ class DeviceLevelBuilder:
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
         self.ip = [p.max_depth, p.max_leaf_cnt, p.min_split_samples, self.hist_target, self.part_target,
-                   self.MIN_ROWS, self.part_chunk, self.split_groups]
+                   self.MIN_ROWS, self.part_chunk, self.split_groups, 0]  # [8]: small_only (per build)
+        self._ip_cur = self.ip
         self.tree_count = 0
         # set by the trainer when its fused gradient pass counts the rows per leaf
         # (tree_grad leaf_counts): the last level then needs no counting partition and no
@@ -385,7 +386,7 @@ class DeviceLevelBuilder:
         """One GPU: this level's split search fused with the next level's split planning
         (lv_split_plan_kernel: the last node block plans) -- one launch instead of two."""
         gp = self.gp
-        hip().lv_split_plan(ptrs, self.ip, fp, ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask),
+        hip().lv_split_plan(ptrs, self._ip_cur, fp, ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask),
                             f0, nitems, [gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"]], ptr(self.inv_scales),
                             ptr(self.split_part), ptr(self.split_cnt), 1 if self.part_atomic else 0, self.maxp, s)
 
@@ -414,12 +415,17 @@ class DeviceLevelBuilder:
         h = hip()
         s = stream(self.bins)
         fp = self._fp()
-        ip = self.ip
         rng = np.random.default_rng((p.seed, self.tree_count))
         seed_rows = int(rng.integers(1 << 62))
         dist = self.comm.is_dist
         sampled = p.instance_sample_rate < 1.0
         assert gh.is_contiguous() and gh.shape == (self.N, 2)
+        # small_only: the last level is not partitioned (deferred leaf counts), so the level
+        # before it writes only the rows of the children that get histograms
+        # (YTK_SMALL_ONLY=0: both children, as on every other level)
+        small_only = (self.defer_leaf_counts and not sampled and self.fuse_part_children
+                      and os.environ.get("YTK_SMALL_ONLY", "1") != "0")
+        ip = self._ip_cur = self.ip[:8] + [1 if small_only else 0]
         # rows / position-ordered (g, h). Without sampling the root level reads the identity
         # permutation and the caller's gh directly; the first partition writes the buffers.
         if sampled:

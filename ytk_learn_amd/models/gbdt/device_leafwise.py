@@ -442,7 +442,7 @@ class DeviceLeafBuilder:
         # finalize (+ the raw-threshold tree for the test-set pass) in one launch
         rq = self._raw_req
         ro = rq["out"] if rq is not None else None
-        h.lv_tail(self._lv_ptrs(), [0] * 8, [0.0] * 6, 0, 0, 0, self.max_nodes,
+        h.lv_tail(self._lv_ptrs(), [0] * 9, [0.0] * 6, 0, 0, 0, self.max_nodes,
                   ptr(rq["cand"]) if rq else 0, ptr(rq["coff"]) if rq else 0, ptr(rq["fill"]) if rq else 0,
                   rq["median"] if rq else 0, ptr(ro["nfeat"]) if rq else 0, ptr(ro["nthr"]) if rq else 0,
                   ptr(ro["nleft"]) if rq else 0, ptr(ro["nright"]) if rq else 0, ptr(ro["ndefl"]) if rq else 0,

@@ -38,6 +38,10 @@ class Comm:
         self.device = device if device is not None else torch.device("cpu")
         self.group = group
         self.cpu_group = cpu_group
+        # YTK_FORCE_DIST=1 (set before from_env): a world-1 job still takes every
+        # multi-rank code path and issues its collectives -- over RCCL on a GPU this runs the
+        # real nccl-backend calls (work handles, reduce-scatter, all-gather) on one-GPU boxes
+        self.force_dist = group is not None and world == 1
         # per-collective accounting (calls, payload bytes) for the bench / profile reports
         self.stats = {"calls": 0, "bytes": 0}
         # YTK_COMM_LOG=1: record every collective (op, dtype, numel) -- ranks must issue the
@@ -77,13 +81,15 @@ class Comm:
             dev = torch.device("cuda", idx)
         else:
             dev = torch.device("cpu")
-        if world <= 1:
+        force = os.environ.get("YTK_FORCE_DIST") == "1"
+        if world <= 1 and not force:
             return cls(0, 1, dev)
         # YTK_DIST_BACKEND=gloo forces gloo even for GPU tensors: lets several ranks share ONE
         # GPU to rehearse the multi-GPU code paths (RCCL needs one GPU per rank).
         backend = os.environ.get("YTK_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
             kw = {}
             if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
@@ -97,7 +103,7 @@ class Comm:
 
     @property
     def is_dist(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force_dist
 
     @property
     def is_master(self) -> bool:
