@@ -58,6 +58,7 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
             backend = torch.distributed.get_backend() if torch.distributed.is_initialized() else "none"
             json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats,
                        "backend": backend, "is_dist": comm.is_dist,
+                       "graph_replays": tr._graphs["n"] if isinstance(tr._graphs, dict) else 0,
                        "peer_calls": peer.calls if peer is not None else 0}, f)
 
 

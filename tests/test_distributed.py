@@ -186,17 +186,25 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
     all-reduce work handles waited on the compute stream, reduce-scatter + all-gather of the
     owner mode, the gloo side group for host scalars) -- RCCL refuses two ranks on one GPU,
     so this is the RCCL-semantics check available here; the model must equal the plain
-    world-1 run byte for byte."""
+    world-1 run byte for byte. Level-wise rounds replay as graphs that contain the RCCL calls
+    (one capture, then graph replays; YTK_GRAPH_DIST=0 variant: eager rounds)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = {"YTK_HIST_SYNC": mode, "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}
+    if task == "gbdt" and mode == "allreduce":
+        eager = _run(task, tmp_path / "eager", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1", YTK_GRAPH_DIST="0"))
+        assert eager["graph_replays"] == 0
     _run(task, tmp_path / "plain", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / "rccl", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
     assert res["is_dist"] and res["backend"] == "nccl" and res["comm"]["calls"] > 0
     if task == "gbdt":  # the GPU leaf-wise engine has one sync mode (one batch message all-reduced)
         assert res["owner"] == (mode == "owner")
+        # level-wise rounds are captured WITH their RCCL calls and replayed as graphs
+        assert res["graph_replays"] > 0 and res["comm"]["calls"] >= 5 * 6
     assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "rccl" / "model.txt").read()
+    if task == "gbdt" and mode == "allreduce":
+        assert open(tmp_path / "eager" / "model.txt").read() == open(tmp_path / "rccl" / "model.txt").read()
 
 
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])

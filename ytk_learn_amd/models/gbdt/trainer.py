@@ -545,12 +545,17 @@ class GBDTTrainer:
         instead of ~45 kernel launches and the Python around them per round (at a 1/8 shard the
         eager host work, ~0.44 ms per round, was as long as the GPU work). Only rounds whose
         launch arguments never change qualify: K == 1, no row / feature sampling, no random
-        forest averaging, no L1 refine, no per-phase profiling, one process."""
+        forest averaging, no L1 refine, no per-phase profiling. Multi-GPU rounds qualify when
+        every collective of a round is an RCCL call on device tensors (nccl backend: the
+        level messages, the round's loss vector) -- the collectives are captured into the
+        graph with the kernels, so a replayed round costs the host one graph launch instead
+        of ~45 kernel launches + 7 collective calls (YTK_GRAPH_DIST=0: eager multi-GPU rounds)."""
         if self._graphs is False:
             return False
         tp = self.p.tree
         ok = (self.dev.type == "cuda" and self.use_device_builder and isinstance(self.builder, DeviceLevelBuilder)
-              and not self.comm.is_dist and self.K == 1 and self.kernel_loss not in (None, "softmax")
+              and (not self.comm.is_dist or self._dist_capturable())
+              and self.K == 1 and self.kernel_loss not in (None, "softmax")
               and not self.rf and self.refiner is None and not self.exact and not self.profile
               and tp.instance_sample_rate >= 1.0 and tp.feature_sample_rate >= 1.0
               and getattr(self.builder, "fuse_root", False) and not self.builder.snapshot_copy
@@ -559,6 +564,15 @@ class GBDTTrainer:
             self._graph_release()
             self._graphs = False
         return ok
+
+    def _dist_capturable(self) -> bool:
+        """Every collective of a multi-GPU round can be captured: RCCL on device tensors."""
+        if os.environ.get("YTK_GRAPH_DIST", "1") == "0" or self.comm.group is None:
+            return False
+        try:
+            return torch.distributed.get_backend(self.comm.group) == "nccl"
+        except Exception:
+            return False
 
     def _graph_round(self, i: int) -> bool:
         """Replay the captured round (capturing it first). The engine swaps its row / (g, h)
@@ -570,28 +584,47 @@ class GBDTTrainer:
             torch.cuda.synchronize(self.dev)
             b = self.builder
             saved = (b.rows, b.rows_tmp, b.ghp, b.gh_tmp, b.tree_count, b.root_ready)
-            graphs, pool = [], None
+            graphs, pool, err = [], None, None
+            stats0 = dict(self.comm.stats)
+            log0 = len(self.comm.log) if self.comm.log is not None else 0
             try:
                 for _ in range(2):
                     g = torch.cuda.CUDAGraph()
+                    c0 = dict(self.comm.stats)
                     with torch.cuda.graph(g, pool=pool):
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
                         accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
                     assert not host_trees
                     pool = g.pool()
-                    graphs.append((g, dev_trees, acc, acc_te, accs, nlc))
-            except Exception as e:  # not capturable here: eager rounds, state as before
+                    # the collectives a replay issues (captured once, counted per replay)
+                    coll = {k: self.comm.stats[k] - c0.get(k, 0) for k in self.comm.stats}
+                    graphs.append((g, dev_trees, acc, acc_te, accs, nlc, coll))
+            except Exception as e:
+                err = e
+            if self.comm.is_dist:
+                # all ranks replay or none (a rank that fell back alone would still issue the
+                # same collectives, but a failed capture is not worth the risk): one host vote
+                ok = self.comm.allreduce_scalars([0.0 if err is not None else 1.0], op="min")[0] > 0.5
+                if err is None and not ok:
+                    err = RuntimeError("another rank could not capture its round")
+            if err is not None:  # not capturable here: eager rounds, state as before
                 (b.rows, b.rows_tmp, b.ghp, b.gh_tmp, b.tree_count, b.root_ready) = saved
                 torch.cuda.synchronize(self.dev)
-                self.log.info(f"[GBDT] round capture failed ({type(e).__name__}: {e}); eager rounds")
+                self.comm.stats = stats0
+                if self.comm.log is not None:
+                    del self.comm.log[log0:]
+                self.log.info(f"[GBDT] round capture failed ({type(err).__name__}: {err}); eager rounds")
                 self._graphs = False
                 return False
+            self.comm.stats = stats0
             self._graphs = {"g": graphs, "n": 0}
         st = self._graphs
         self._bound_inflight()
-        g, dev_trees, acc, acc_te, accs, nlc = st["g"][st["n"] & 1]
+        g, dev_trees, acc, acc_te, accs, nlc, coll = st["g"][st["n"] & 1]
         g.replay()
         st["n"] += 1
+        for k, v in coll.items():
+            self.comm.stats[k] = self.comm.stats.get(k, 0) + v
         self._acc = (acc, acc_te)
         self.rounds_done = i + 1
         self._readback_copy(i, dev_trees, accs, acc_te is not None, nlc)
