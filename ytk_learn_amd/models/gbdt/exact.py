@@ -34,6 +34,9 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
+from ...parallel.comm import Comm
+from .builder import TimeStats, TreeParams
+from .tree import Tree
 
 
 def _row_cumsum(x: torch.Tensor) -> torch.Tensor:
@@ -50,9 +53,7 @@ def _row_cumsum(x: torch.Tensor) -> torch.Tensor:
         starts = flat[:-1, -1:].clone()  # sum of all rows before row r, at row r - 1's end
         flat[1:] -= starts
     return flat
-from ...parallel.comm import Comm
-from .builder import TimeStats, TreeParams
-from .tree import Tree
+
 
 MIN_FEA_SPLIT_GAP = np.float32(1e-16)  # Constants.java:34
 
