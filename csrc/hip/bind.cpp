@@ -68,7 +68,10 @@ int ytk_tree_grad_grid(long long);
 // sparse.hip
 void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, long long, int,
                   uintptr_t, long long, float, int, int, int, uintptr_t, uintptr_t);
-void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t, uintptr_t);
+void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t, uintptr_t, int,
+                      uintptr_t);
+void ytk_seg_tile_spmv(uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, float, int,
+                       int, uintptr_t);
 // ffm.hip
 void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, int,
                    uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
@@ -163,7 +166,13 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("tree_grad", &ytk_tree_grad);
   m.def("tree_grad_grid", &ytk_tree_grad_grid);
   m.def("seg_spmm", &ytk_seg_spmm);
-  m.def("chunk_reduce", &ytk_chunk_reduce);
+  m.def("chunk_reduce", [](uintptr_t cbeg, int ncol, uintptr_t part, int J, uintptr_t out, long long ldo, float alpha,
+                           int accumulate, uintptr_t ids, uintptr_t stream, uintptr_t heavy, int nheavy) {
+    ytk_chunk_reduce(cbeg, ncol, part, J, out, ldo, alpha, accumulate, ids, heavy, nheavy, stream);
+  }, pybind11::arg("cbeg"), pybind11::arg("ncol"), pybind11::arg("part"), pybind11::arg("J"), pybind11::arg("out"),
+     pybind11::arg("ldo"), pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("ids"),
+     pybind11::arg("stream"), pybind11::arg("heavy") = 0, pybind11::arg("nheavy") = 0);
+  m.def("seg_tile_spmv", &ytk_seg_tile_spmv);
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);

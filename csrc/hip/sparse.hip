@@ -91,14 +91,153 @@ __global__ __launch_bounds__(256) void seg_spmm_kernel(
 // tiled CSC: a column's chunks are spread over the tiles); otherwise they are contiguous.
 __global__ __launch_bounds__(256) void chunk_reduce_kernel(
     const long long* __restrict__ cbeg, int ncol, const float* __restrict__ part, int J,
-    float* __restrict__ out, long long ldo, float alpha, int accumulate, const long long* __restrict__ ids) {
+    float* __restrict__ out, long long ldo, float alpha, int accumulate, const long long* __restrict__ ids,
+    int skip_heavy) {
   const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (t >= (long long)ncol * J) return;
   const int col = (int)(t / J), j = (int)(t % J);
+  if (skip_heavy && cbeg[col + 1] - cbeg[col] > 16) return;  // chunk_reduce_heavy_kernel's (kReduceLight)
   float acc = 0.f;
   for (long long c = cbeg[col]; c < cbeg[col + 1]; ++c) acc += part[(ids ? ids[c] : c) * J + j];
   float* o = out + (long long)col * ldo + j;
   *o = accumulate ? *o + alpha * acc : alpha * acc;
+}
+
+// ---------------------------------------------------------------------------------
+// Entry-tiled segmented SpMV (J == 1) for segments that tile their entry list contiguously
+// (CSR rows: row_end[s] == row_beg[s + 1]; the CSC chunks likewise). seg_spmv_kernel gives
+// each segment its own L lanes: a wave of 4-16 short rows issues one round of loads and
+// exits, so the Criteo-shaped products (40 entries per row, 1M-column tails of 1-4 entry
+// chunks) ran latency bound at ~2.3 TB/s. Here a block takes a run of whole segments
+// (<= 256 segments starting within one kTileCap-entry window; host-built table bseg) and
+// streams the run's entries in passes of kTileCap (one pass unless the last segment reaches
+// past the window: windows are kTileCap - 256 entries): every thread loads kTileCap / 256
+// (index, value) pairs and their x gathers with all loads in flight, the products go to
+// LDS, then G = 256 / segments threads per segment sum its slice of the pass from LDS.
+// Per-segment order is fixed by (the table, G): bitwise deterministic run to run.
+constexpr int kTileThreads = 256;
+constexpr int kTileCap = 4096;
+constexpr int kTileSegs = 256;  // segments per block at most (bseg construction)
+
+template <bool kSquare, bool kOnes>
+__global__ __launch_bounds__(kTileThreads) void seg_tile_spmv_kernel(
+    const long long* __restrict__ beg, const long long* __restrict__ end, const int* __restrict__ bseg,
+    const int* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ x,
+    float* __restrict__ out, float alpha, int accumulate) {
+  __shared__ float sp[kTileCap];
+  __shared__ float sred[kTileThreads];
+  const int s0 = bseg[blockIdx.x], s1 = bseg[blockIdx.x + 1];
+  const int ns = s1 - s0;
+  if (ns <= 0) return;  // uniform per block
+  const int t = threadIdx.x;
+  int G = 1;  // threads per segment: the largest power of two with G * ns <= 256
+  while (2 * G * ns <= kTileThreads) G <<= 1;
+  const int ms = t / G, lane = t % G;
+  const bool mine = ms < ns;
+  const long long e0 = beg[s0], e1 = end[s1 - 1];
+  const long long sb = mine ? beg[s0 + ms] : 0, se = mine ? end[s0 + ms] : 0;
+  constexpr int K = kTileCap / kTileThreads;
+  float acc = 0.f;
+  for (long long p0 = e0; p0 < e1; p0 += kTileCap) {
+    const int n = (int)min((long long)kTileCap, e1 - p0);
+    int ii[K];
+    float vv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int o = k * kTileThreads + t;
+      const bool ok = o < n;
+      ii[k] = ok ? idx[p0 + o] : 0;
+      vv[k] = ok ? (kOnes ? 1.f : val[p0 + o]) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float xv = x[ii[k]];
+      sp[k * kTileThreads + t] = (kSquare ? vv[k] * vv[k] : vv[k]) * xv;
+    }
+    __syncthreads();
+    if (mine) {
+      // this pass's slice of the segment, 4 independent LDS reads in flight (a serial
+      // read-add chain left the kernel LDS-latency bound: 0.94 ms for a 164M-entry product)
+      const int a = (int)(max(sb, p0) - p0), z = (int)(min(se, p0 + n) - p0);
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int e = a + lane;
+      for (; e + 3 * G < z; e += 4 * G) {
+        a0 += sp[e];
+        a1 += sp[e + G];
+        a2 += sp[e + 2 * G];
+        a3 += sp[e + 3 * G];
+      }
+      for (; e < z; e += G) a0 += sp[e];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+  }
+  // the G partials of a segment, combined by a fixed tree
+  if (G <= kWave) {
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1)
+      if (off < G) acc += __shfl_xor(acc, off, kWave);
+  } else {
+    sred[t] = acc;
+    __syncthreads();
+    for (int off = G >> 1; off > 0; off >>= 1) {
+      if (lane < off) sred[t] += sred[t + off];
+      __syncthreads();
+    }
+    acc = sred[t];
+  }
+  if (mine && lane == 0) {
+    const int s = s0 + ms;
+    out[s] = accumulate ? out[s] + alpha * acc : alpha * acc;
+  }
+}
+
+// Heavy columns of the chunk reduce (more than kReduceLight chunks: the bias column holds
+// ~N / 4096 chunks): one block per column, threads = (chunk group g, output j); each thread
+// sums chunks g, g + G, ... of its j (4 loads in flight), then the G group partials are
+// added in group order through LDS. chunk_reduce_kernel skips these columns.
+constexpr int kReduceLight = 16;
+
+__global__ __launch_bounds__(256) void chunk_reduce_heavy_kernel(
+    const long long* __restrict__ cbeg, const int* __restrict__ heavy, const float* __restrict__ part, int J,
+    float* __restrict__ out, long long ldo, float alpha, int accumulate, const long long* __restrict__ ids) {
+  __shared__ float s[256];
+  const int col = heavy[blockIdx.x];
+  const long long c0 = cbeg[col], c1 = cbeg[col + 1];
+  const int JL = min(J, 256);
+  const int G = 256 / JL;
+  const int t = threadIdx.x, g = t / JL, jl = t % JL;
+  for (int jb = 0; jb < J; jb += JL) {
+    const int j = jb + jl;
+    float acc = 0.f;
+    if (g < G && j < J) {
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      long long c = c0 + g;
+      for (; c + 3 * G < c1; c += 4 * G) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long long cc = c + u * G;
+          a4[u] += part[(ids ? ids[cc] : cc) * J + j];
+        }
+      }
+      for (; c < c1; c += G) a4[0] += part[(ids ? ids[c] : c) * J + j];
+      acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    }
+    if (G > 1) {
+      __syncthreads();
+      s[t] = acc;
+      __syncthreads();
+      if (g == 0 && j < J) {
+        float tot = 0.f;
+        for (int q = 0; q < G; ++q) tot += s[q * JL + jl];
+        acc = tot;
+      }
+    }
+    if (g == 0 && j < J) {
+      float* o = out + (long long)col * ldo + j;
+      *o = accumulate ? *o + alpha * acc : alpha * acc;
+    }
+  }
 }
 
 }  // namespace ytk
@@ -184,13 +323,38 @@ void ytk_seg_spmm(uintptr_t beg, uintptr_t end, int nseg, uintptr_t idx, uintptr
   YTK_LAUNCH_CHECK();
 }
 
+// heavy (optional, int32 [nheavy]): the columns with more than kReduceLight chunks, reduced
+// by chunk_reduce_heavy_kernel (one block each) instead of one serial thread per output
 void ytk_chunk_reduce(uintptr_t cbeg, int ncol, uintptr_t part, int J, uintptr_t out,
-                      long long ldo, float alpha, int accumulate, uintptr_t ids, uintptr_t stream) {
+                      long long ldo, float alpha, int accumulate, uintptr_t ids, uintptr_t heavy, int nheavy,
+                      uintptr_t stream) {
   if (ncol <= 0 || J <= 0) return;
   const long long n = (long long)ncol * J;
-  hipLaunchKernelGGL(chunk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), (const long long*)cbeg, ncol,
-                     (const float*)part, J, (float*)out, ldo, alpha, accumulate, (const long long*)ids);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(chunk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     (const long long*)cbeg, ncol, (const float*)part, J, (float*)out, ldo, alpha, accumulate,
+                     (const long long*)ids, heavy ? 1 : 0);
+  if (heavy && nheavy > 0)
+    hipLaunchKernelGGL(chunk_reduce_heavy_kernel, dim3((unsigned)nheavy), dim3(256), 0, s, (const long long*)cbeg,
+                       (const int*)heavy, (const float*)part, J, (float*)out, ldo, alpha, accumulate,
+                       (const long long*)ids);
+  YTK_LAUNCH_CHECK();
+}
+
+// Entry-tiled J == 1 product over contiguous segments (seg_tile_spmv_kernel); bseg: int32
+// [nblk + 1] block -> first segment. val == 0: one-hot values.
+void ytk_seg_tile_spmv(uintptr_t beg, uintptr_t end, uintptr_t bseg, int nblk, uintptr_t idx, uintptr_t val,
+                       uintptr_t x, uintptr_t out, float alpha, int accumulate, int square, uintptr_t stream) {
+  if (nblk <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_TILE(SQ, ON)                                                                                    \
+  hipLaunchKernelGGL((seg_tile_spmv_kernel<SQ, ON>), dim3((unsigned)nblk), dim3(kTileThreads), 0, s,        \
+                     (const long long*)beg, (const long long*)end, (const int*)bseg, (const int*)idx,       \
+                     (const float*)val, (const float*)x, (float*)out, alpha, accumulate)
+  if (val == 0) YTK_TILE(false, true);
+  else if (square) YTK_TILE(true, false);
+  else YTK_TILE(false, false);
+#undef YTK_TILE
   YTK_LAUNCH_CHECK();
 }
 

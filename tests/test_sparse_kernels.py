@@ -121,6 +121,54 @@ def test_spmm_gpu_matches_cpu(cuda, J, one_hot, nnz):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chunk,J", [(64, 1), (4096, 1), (64, 18), (4096, 3)])
+def test_tiled_spmv_and_heavy_chunk_reduce(cuda, monkeypatch, chunk, J):
+    """Entry-tiled SpMV (seg_tile_spmv_kernel: blocks of whole rows / CSC chunks, LDS
+    products, G threads per segment incl. the LDS tree for G > 64, multi-pass rows longer
+    than TILE_CAP) and the heavy-column chunk reduce (one block per column with more than
+    REDUCE_LIGHT chunks) vs the CPU reference and the per-segment kernels; bitwise
+    deterministic."""
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    monkeypatch.setattr(sparse_mod, "CHUNK", chunk)
+    monkeypatch.setattr(sparse_mod, "TILE_ROWS", True)  # rows through the tiled kernel too
+    n, F = 30000, 200
+    ip, ix, vv, _ = _rand_csr(n, F, 8, seed=11)
+    # + rows longer than one tile pass (TILE_CAP entries) and an empty row
+    g = np.random.default_rng(4)
+    extra = [np.sort(g.choice(np.arange(1, 12000), size=9000, replace=False)), np.array([], np.int64),
+             np.sort(g.choice(np.arange(1, 12000), size=5000, replace=False))]
+    F2 = 12000
+    ix2 = torch.cat([ix] + [torch.from_numpy(e.astype(np.int32)) for e in extra])
+    vv2 = torch.cat([vv] + [torch.from_numpy(g.normal(size=e.size).astype(np.float32)) for e in extra])
+    lens = torch.tensor([e.size for e in extra], dtype=torch.int64)
+    ip2 = torch.cat([ip, ip[-1] + torch.cumsum(lens, 0)])
+    n2 = n + len(extra)
+    Xc = SparseMatrix(ip2, ix2, vv2, F2)
+    Xg = SparseMatrix(ip2.to(cuda), ix2.to(cuda), vv2.to(cuda), F2)
+    assert Xg.row_tiles is not None and Xg.chunk_tiles is not None
+    assert (Xg.heavy_cols.numel() > 0) == (chunk == 64)
+    gen = torch.Generator().manual_seed(6)
+    w = torch.randn(F2, generator=gen)
+    D = torch.randn((n2, J), generator=gen) if J > 1 else torch.randn(n2, generator=gen)
+    z = Xg.matmul(w.to(cuda))
+    torch.testing.assert_close(z.cpu(), Xc.matmul(w), rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(Xg.matmul(w.to(cuda), square=True).cpu(), Xc.matmul(w, square=True),
+                               rtol=1e-4, atol=2e-3)
+    tg = Xg.t_matmul(D.to(cuda))
+    torch.testing.assert_close(tg.cpu(), Xc.t_matmul(D), rtol=1e-4, atol=2e-3)
+    assert torch.equal(Xg.matmul(w.to(cuda)), z) and torch.equal(Xg.t_matmul(D.to(cuda)), tg)
+    out = torch.ones_like(z)
+    Xg.matmul(w.to(cuda), out=out, alpha=0.5, accumulate=True)
+    torch.testing.assert_close(out, 1.0 + 0.5 * z, rtol=1e-5, atol=1e-4)
+    # the per-segment kernels (tiling off) agree
+    monkeypatch.setattr(sparse_mod, "TILE_ON", False)
+    Xo = SparseMatrix(ip2.to(cuda), ix2.to(cuda), vv2.to(cuda), F2)
+    assert Xo.row_tiles is None and Xo.chunk_tiles is None
+    torch.testing.assert_close(Xo.matmul(w.to(cuda)), z, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(Xo.t_matmul(D.to(cuda)), tg, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m", [(4, 12), (3, 8), (8, 70)])
 def test_ffm_gpu_matches_cpu(cuda, k, m, monkeypatch):
     n, F, nf = 3000, 400, 7

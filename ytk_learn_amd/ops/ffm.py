@@ -11,6 +11,7 @@ import os
 import torch
 
 from ._ext import check_cuda, hip, ptr, stream
+from .sparse import chunk_reduce, heavy_columns
 
 
 def _pairs_cpu(indptr: torch.Tensor):
@@ -260,7 +261,9 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
         h.ffm_grad_stream(ptr(wc), wc.numel() - 1, ptr(st["beg"]), ptr(st["end"]), ptr(st["chunk_fa"]),
                           ptr(st["exp_idx"]), ptr(st["exp_val"]), ptr(se), X.nnz, ptr(st["lay_field"]), st["m"],
                           ptr(Vt), X.ncols, nfield, k, ptr(part), s)
-        h.chunk_reduce(ptr(st["cptr"]), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, 0, s)
+        if "heavy" not in st:
+            st["heavy"] = heavy_columns(st["cptr"])
+        chunk_reduce(st["cptr"], X.ncols, part, J, gV, J, 1.0, 1, 0, s, st["heavy"])
         return gV
     part = torch.empty((max(X.n_chunks, 1), J), dtype=torch.float32, device=V.device)
     # general rows: one wave per chunk, the row entries read per column (L2-miss bound on its
@@ -269,5 +272,5 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
     h.ffm_grad_csc(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
                    ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
                    ptr(Vt), X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), s)
-    h.chunk_reduce(ptr(X.chunk_ptr), X.ncols, ptr(part), J, ptr(gV), J, 1.0, 1, ptr(X.chunk_ids), s)
+    chunk_reduce(X.chunk_ptr, X.ncols, part, J, gV, J, 1.0, 1, ptr(X.chunk_ids), s, X.heavy_cols)
     return gV

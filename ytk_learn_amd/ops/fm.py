@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import check_cuda, hip, ptr, stream
+from .sparse import chunk_reduce
 
 
 def fm_forward(X, w_lin: torch.Tensor, V: torch.Tensor):
@@ -45,7 +46,7 @@ def fm_backward(X, c: torch.Tensor, S: torch.Tensor, V: torch.Tensor, g_lin: tor
         h, s = hip(), stream(c)
         h.fm_backward(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals), ptr(c),
                       ptr(S.contiguous()), k, ptr(part), s)
-        h.chunk_reduce(ptr(X.chunk_ptr), X.ncols, ptr(part), k + 2, ptr(tot), k + 2, 1.0, 0, ptr(X.chunk_ids), s)
+        chunk_reduce(X.chunk_ptr, X.ncols, part, k + 2, tot, k + 2, 1.0, 0, ptr(X.chunk_ids), s, X.heavy_cols)
         g_lin.copy_(tot[:, k])
         gV.copy_(tot[:, :k])
         gV.addcmul_(V, tot[:, k + 1:k + 2], value=-1.0)

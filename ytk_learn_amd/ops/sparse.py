@@ -21,6 +21,42 @@ from ._ext import check_cuda, hip, ptr, stream
 CHUNK = 4096  # nnz per CSC chunk: balances the bias column (all rows) against short columns
 # rows per CSC row tile (GPU, see SparseMatrix._build_csc); 0 disables the tiling
 ROW_TILE = int(os.environ.get("YTK_CSC_ROW_TILE", 524288))
+TILE_ON = os.environ.get("YTK_SPMV_TILE", "1") != "0"
+TILE_ROWS = os.environ.get("YTK_SPMV_TILE_ROWS", "0") == "1"
+
+
+TILE_CAP = 4096   # == kTileCap (sparse.hip): entries per pass of the tiled SpMV
+TILE_SEGS = 256   # == kTileSegs: segments per tiled-SpMV block at most
+REDUCE_LIGHT = 16  # == kReduceLight: columns with more chunks are reduced one block each
+
+
+def tile_blocks(beg: torch.Tensor, end: torch.Tensor) -> Optional[torch.Tensor]:
+    """Block table of the entry-tiled SpMV (seg_tile_spmv_kernel) for segments that tile their
+    entries contiguously: block b covers segments [bseg[b], bseg[b + 1]) -- at most TILE_SEGS
+    of them, all starting inside one (TILE_CAP - 256)-entry window, so a block is one pass of
+    the kernel unless its last segment is longer than 256 entries. None when the segments
+    are not contiguous (the per-segment kernel is used then)."""
+    n = int(beg.numel())
+    if n == 0 or not bool((end[:-1] == beg[1:]).all()):
+        return None
+    ar = torch.arange(n, device=beg.device, dtype=torch.int64)
+    key = (beg - beg[0]) // (TILE_CAP - 256) + ar // TILE_SEGS  # nondecreasing: equal keys are runs
+    change = torch.nonzero(key[1:] != key[:-1]).flatten() + 1
+    return torch.cat([torch.zeros(1, dtype=torch.int64, device=beg.device), change,
+                      torch.full((1,), n, dtype=torch.int64, device=beg.device)]).to(torch.int32).contiguous()
+
+
+def heavy_columns(cptr: torch.Tensor) -> torch.Tensor:
+    """Columns with more than REDUCE_LIGHT chunks (int32): chunk_reduce gives each a block."""
+    return torch.nonzero((cptr[1:] - cptr[:-1]) > REDUCE_LIGHT).flatten().to(torch.int32).contiguous()
+
+
+def chunk_reduce(cptr, ncol, part, J, out, ldo, alpha, accumulate, ids, s, heavy=None):
+    """out[col, :] (+)= alpha * the column's chunk partials summed in chunk order; ``heavy``
+    (heavy_columns(cptr)) routes the long columns to one block each."""
+    hv = heavy if heavy is not None else heavy_columns(cptr)
+    hip().chunk_reduce(ptr(cptr), ncol, ptr(part), J, ptr(out), ldo, alpha, accumulate, ids, s,
+                       ptr(hv) if hv.numel() else 0, int(hv.numel()))
 
 
 def _lanes(avg_nnz: float) -> int:
@@ -51,6 +87,12 @@ class SparseMatrix:
         self.one_hot = bool(self.nnz > 0 and bool((self.values == 1.0).all()))
         self.rows_of_nnz = torch.repeat_interleave(torch.arange(self.n, device=self.device),
                                                    self.indptr[1:] - self.indptr[:-1])
+        # entry-tiled SpMV over the rows: measured slower than the per-row lane groups for
+        # Criteo-shaped rows (918 vs 846 us per 164M-entry product: both bound by the random
+        # x gathers, tools/microbench/spmv_gather.py), so rows keep seg_spmv_kernel
+        # (YTK_SPMV_TILE_ROWS=1: tiled rows too)
+        self.row_tiles = (tile_blocks(self.row_beg, self.row_end)
+                          if self.device.type == "cuda" and TILE_ON and TILE_ROWS else None)
         self._csc = None
         if build_csc:
             self._build_csc()
@@ -111,6 +153,8 @@ class SparseMatrix:
         # lane count for all chunks idles most lanes on the tail, so J == 1 products launch
         # three length buckets (<= 16, <= 64, longer: 4 / 16 / 64 lanes per chunk)
         clen = (self.chunk_end - self.chunk_beg)
+        self.chunk_tiles = tile_blocks(self.chunk_beg, self.chunk_end) if TILE_ON else None
+        self.heavy_cols = heavy_columns(self.chunk_ptr)
         self.chunk_buckets = []
         for lo, hi, lanes in ((0, 16, 4), (16, 64, 16), (64, 1 << 62, 64)):
             ids = torch.nonzero((clen > lo) & (clen <= hi)).flatten().to(torch.int32).contiguous()
@@ -135,6 +179,11 @@ class SparseMatrix:
         if self.device.type == "cuda":
             check_cuda(W2, o2, vals)
             vp = 0 if (values is None and self.one_hot) else ptr(vals)
+            if J == 1 and self.row_tiles is not None and W2.stride(0) == 1 and o2.stride(0) == 1:
+                hip().seg_tile_spmv(ptr(self.row_beg), ptr(self.row_end), ptr(self.row_tiles),
+                                    self.row_tiles.numel() - 1, ptr(self.indices), vp, ptr(W2), ptr(o2),
+                                    float(alpha), int(accumulate), int(square), stream(W2))
+                return out
             hip().seg_spmm(ptr(self.row_beg), ptr(self.row_end), self.n, ptr(self.indices), vp, ptr(W2),
                            W2.stride(0), J, ptr(o2), o2.stride(0), float(alpha), int(accumulate), int(square),
                            self.row_lanes if J == 1 else min(64, J), 0, stream(W2))
@@ -168,15 +217,19 @@ class SparseMatrix:
             h = hip()
             s = stream(D2)
             vp = 0 if (values is None and self.one_hot) else ptr(csc_vals)
-            if J == 1:  # chunks bucketed by length, each bucket with its own lane count
+            if J == 1 and self.chunk_tiles is not None and D2.stride(0) == 1:
+                h.seg_tile_spmv(ptr(self.chunk_beg), ptr(self.chunk_end), ptr(self.chunk_tiles),
+                                self.chunk_tiles.numel() - 1, ptr(self.csc_rows), vp, ptr(D2), ptr(part), 1.0, 0,
+                                int(square), s)
+            elif J == 1:  # chunks bucketed by length, each bucket with its own lane count
                 for lanes, perm in self.chunk_buckets:
                     h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), perm.numel(), ptr(self.csc_rows), vp,
                                ptr(D2), D2.stride(0), 1, ptr(part), 1, 1.0, 0, int(square), lanes, ptr(perm), s)
             else:
                 h.seg_spmm(ptr(self.chunk_beg), ptr(self.chunk_end), self.n_chunks, ptr(self.csc_rows), vp,
                            ptr(D2), D2.stride(0), J, ptr(part), J, 1.0, 0, int(square), min(64, J), 0, s)
-            h.chunk_reduce(ptr(self.chunk_ptr), self.ncols, ptr(part), J, ptr(o2), o2.stride(0), float(alpha),
-                           int(accumulate), ptr(self.chunk_ids), s)
+            chunk_reduce(self.chunk_ptr, self.ncols, part, J, o2, o2.stride(0), float(alpha), int(accumulate),
+                         ptr(self.chunk_ids), s, self.heavy_cols)
         else:
             vals = self.csc_vals if values is None else values
             v = vals * vals if square else vals
