@@ -70,6 +70,8 @@ void ytk_seg_spmm(uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, lo
                   uintptr_t, long long, float, int, int, int, uintptr_t, uintptr_t);
 void ytk_chunk_reduce(uintptr_t, int, uintptr_t, int, uintptr_t, long long, float, int, uintptr_t, uintptr_t, int,
                       uintptr_t);
+void ytk_fixed_spmv(uintptr_t, uintptr_t, long long, int, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, float, int, int,
+                    uintptr_t);
 void ytk_seg_tile_spmv(uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, float, int,
                        int, uintptr_t);
 // ffm.hip
@@ -173,6 +175,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
      pybind11::arg("ldo"), pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("ids"),
      pybind11::arg("stream"), pybind11::arg("heavy") = 0, pybind11::arg("nheavy") = 0);
   m.def("seg_tile_spmv", &ytk_seg_tile_spmv);
+  m.def("fixed_spmv", &ytk_fixed_spmv);
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);

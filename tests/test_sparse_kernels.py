@@ -169,6 +169,45 @@ def test_tiled_spmv_and_heavy_chunk_reduce(cuda, monkeypatch, chunk, J):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("one_hot", [True, False])
+def test_fixed_layout_spmv(cuda, monkeypatch, one_hot):
+    """Fixed-layout rows (m entries per row, each position's columns in its own range: the
+    Criteo shape) take fixed_spmv_kernel (position slices of w staged in LDS, uint16
+    position-major offsets): X w, X∘X w and accumulate/alpha vs the CPU reference; a layout
+    that does not qualify (ragged rows) keeps the per-row kernel."""
+    import ytk_learn_amd.ops.sparse as sparse_mod
+    monkeypatch.setattr(sparse_mod, "FIX_MIN_ROWS", 1000)
+    n, m, width = 40000, 12, 3000
+    g = np.random.default_rng(8)
+    base = np.concatenate([[0], 1 + width * np.arange(m - 1)])  # bias column + (m - 1) fields
+    cols = np.zeros((n, m), np.int64)
+    cols[:, 1:] = base[None, 1:] + g.integers(0, width, size=(n, m - 1))
+    F = int(base[-1] + width)
+    ip = torch.arange(n + 1, dtype=torch.int64) * m
+    ix = torch.from_numpy(cols.reshape(-1).astype(np.int32))
+    vv = torch.ones(n * m) if one_hot else torch.from_numpy(g.normal(size=n * m).astype(np.float32))
+    Xc = SparseMatrix(ip, ix, vv, F, build_csc=False)
+    Xg = SparseMatrix(ip.to(cuda), ix.to(cuda), vv.to(cuda), F, build_csc=False)
+    w = torch.from_numpy(g.normal(size=F).astype(np.float32))
+    z = Xg.matmul(w.to(cuda))
+    fx = Xg._fixed_layout()
+    assert fx and fx["m"] == m and (fx["valT"] is None) == one_hot and fx["max_span"] <= width
+    torch.testing.assert_close(z.cpu(), Xc.matmul(w), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(Xg.matmul(w.to(cuda), square=True).cpu(), Xc.matmul(w, square=True), rtol=1e-5,
+                               atol=1e-4)
+    out = torch.full_like(z, 2.0)
+    Xg.matmul(w.to(cuda), out=out, alpha=-1.5, accumulate=True)
+    torch.testing.assert_close(out, 2.0 - 1.5 * z, rtol=1e-5, atol=1e-4)
+    assert torch.equal(Xg.matmul(w.to(cuda)), z)  # deterministic
+    # ragged rows: no fixed layout
+    ip2 = ip.clone()
+    ip2[1:n] += 1
+    ip2[n] = ip[n]
+    Xr = SparseMatrix(ip2.to(cuda), ix.to(cuda), vv.to(cuda), F, build_csc=False)
+    assert Xr._fixed_layout() is False
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m", [(4, 12), (3, 8), (8, 70)])
 def test_ffm_gpu_matches_cpu(cuda, k, m, monkeypatch):
     n, F, nf = 3000, 400, 7

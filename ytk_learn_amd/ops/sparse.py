@@ -23,6 +23,9 @@ CHUNK = 4096  # nnz per CSC chunk: balances the bias column (all rows) against s
 ROW_TILE = int(os.environ.get("YTK_CSC_ROW_TILE", 524288))
 TILE_ON = os.environ.get("YTK_SPMV_TILE", "1") != "0"
 TILE_ROWS = os.environ.get("YTK_SPMV_TILE_ROWS", "0") == "1"
+FIXED_ON = os.environ.get("YTK_SPMV_FIXED", "1") != "0"
+FIX_SPAN = 32768      # == kFixSpan (sparse.hip): columns per position slice staged in LDS
+FIX_MIN_ROWS = 1 << 18  # below this the per-row kernel is as fast (one block per 16384 rows)
 
 
 TILE_CAP = 4096   # == kTileCap (sparse.hip): entries per pass of the tiled SpMV
@@ -94,8 +97,37 @@ class SparseMatrix:
         self.row_tiles = (tile_blocks(self.row_beg, self.row_end)
                           if self.device.type == "cuda" and TILE_ON and TILE_ROWS else None)
         self._csc = None
+        self._fixed = None  # fixed-layout row product tables (lazy, see _fixed_layout)
         if build_csc:
             self._build_csc()
+
+    def _fixed_layout(self):
+        """Tables of fixed_spmv_kernel when every row holds the same number m of entries and
+        position j's columns span at most FIX_SPAN (the Criteo shape: bias + one entry per
+        field): uint16 position-major local offsets idxT[j][r] = idx[r][j] - lo[j], the values
+        likewise (None when one-hot), lo / span per position. False when the layout does not
+        qualify (the per-row kernels run then). Built once, on the first product."""
+        if self._fixed is not None:
+            return self._fixed
+        self._fixed = False
+        n, nnz = self.n, self.nnz
+        if not (FIXED_ON and self.device.type == "cuda" and n >= FIX_MIN_ROWS and nnz % n == 0):
+            return False
+        m = nnz // n
+        if not (1 <= m <= 1024):
+            return False
+        if not bool(torch.equal(self.indptr, torch.arange(n + 1, device=self.device, dtype=torch.int64) * m)):
+            return False
+        ix = self.indices.view(n, m)
+        lo = ix.amin(0)
+        span = ix.amax(0) - lo + 1
+        if int(span.max()) > FIX_SPAN:
+            return False
+        idxT = (ix - lo[None, :]).t().contiguous().to(torch.int32).to(torch.uint16)
+        valT = None if self.one_hot else self.values.view(n, m).t().contiguous()
+        self._fixed = {"m": m, "idxT": idxT, "valT": valT, "lo": lo.to(torch.int32).contiguous(),
+                       "span": span.to(torch.int32).contiguous(), "max_span": int(span.max())}
+        return self._fixed
 
     def _build_csc(self):
         """Column-ordered (CSC) copy in CHUNK-entry chunks for the transposed products.
@@ -179,6 +211,12 @@ class SparseMatrix:
         if self.device.type == "cuda":
             check_cuda(W2, o2, vals)
             vp = 0 if (values is None and self.one_hot) else ptr(vals)
+            fx = self._fixed_layout() if (J == 1 and values is None) else False
+            if fx and W2.stride(0) == 1 and o2.stride(0) == 1:
+                hip().fixed_spmv(ptr(fx["idxT"]), ptr(fx["valT"]) if fx["valT"] is not None else 0, self.n, fx["m"],
+                                 ptr(fx["lo"]), ptr(fx["span"]), fx["max_span"], ptr(W2), ptr(o2), float(alpha),
+                                 int(accumulate), int(square), stream(W2))
+                return out
             if J == 1 and self.row_tiles is not None and W2.stride(0) == 1 and o2.stride(0) == 1:
                 hip().seg_tile_spmv(ptr(self.row_beg), ptr(self.row_end), ptr(self.row_tiles),
                                     self.row_tiles.numel() - 1, ptr(self.indices), vp, ptr(W2), ptr(o2),
