@@ -24,6 +24,13 @@ namespace ytk {
 __device__ __forceinline__ float ld_v(const float* p) { return *p; }
 __device__ __forceinline__ float ld_v(const __hip_bfloat16* p) { return __bfloat162float(*p); }
 
+// gathers in flight per lane group in the row / chunk walks (4 measured 3.54 ms forward,
+// 4.46 ms backward per 164M-entry Criteo-shape pass)
+#ifndef YTK_FM_U
+#define YTK_FM_U 8
+#endif
+constexpr int kFmU = YTK_FM_U;
+
 template <int G, typename VT>
 __global__ __launch_bounds__(256) void fm_forward_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
@@ -41,16 +48,16 @@ __global__ __launch_bounds__(256) void fm_forward_kernel(
     if (t + f < e) { my_i = idx[t + f]; my_x = val[t + f]; lin += w[my_i] * my_x; }
     const int n = (int)min<long long>(G, e - t);
     int j = 0;
-    for (; j + 4 <= n; j += 4) {  // four independent gathers in flight
-      float v[4], xs[4];
+    for (; j + kFmU <= n; j += kFmU) {  // kFmU independent gathers in flight
+      float v[kFmU], xs[kFmU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kFmU; ++u) {
         const int i = __shfl(my_i, j + u, G);
         xs[u] = __shfl(my_x, j + u, G);
         v[u] = f < k ? ld_v(V + (long long)i * k + f) : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kFmU; ++u) {
         const float vx = v[u] * xs[u];
         s += vx;
         q += vx * vx;
@@ -96,16 +103,16 @@ __global__ __launch_bounds__(256) void fm_backward_kernel(
     }
     const int n = (int)min<long long>(G, e - t);
     int j = 0;
-    for (; j + 4 <= n; j += 4) {  // four independent gathers in flight
-      float sv[4], cs[4];
+    for (; j + kFmU <= n; j += kFmU) {  // kFmU independent gathers in flight
+      float sv[kFmU], cs[kFmU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kFmU; ++u) {
         const int r = __shfl(my_r, j + u, G);
         cs[u] = __shfl(my_cx, j + u, G);
         sv[u] = f < k ? S[(long long)r * k + f] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) gs += cs[u] * sv[u];
+      for (int u = 0; u < kFmU; ++u) gs += cs[u] * sv[u];
     }
     for (; j < n; ++j) {
       const int r = __shfl(my_r, j, G);
