@@ -587,6 +587,35 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
       return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     };
     auto live = [&](int i) { return ((s_nd[i].z >> 16) & 0xff) == 1; };  // known gain, not final
+    // the splittable live nodes (each pops as a split) and the unexpanded ones among them
+    auto splittable = [&](int i) { return live(i) && (s_nd[i].z >> 24) == 0; };
+    const int per = (nsid + kLwPlanThreads - 1) / kLwPlanThreads;
+    const int i0 = min(nsid, tid * per), i1 = min(nsid, i0 + per);
+    int c = 0, cc = 0;
+    for (int i = i0; i < i1; ++i) {
+      const bool sp = splittable(i);
+      c += sp ? 1 : 0;
+      cc += (sp && s_nd[i].x < 0) ? 1 : 0;
+    }
+    int ns, ncand;
+    int pos = lw_scan(c, s_tmp, &ns);
+    int pc = lw_scan(cc, s_tmp, &ncand);
+    // rank window: speculate percent of the leaf budget (s_uid holds 3 kLwLeafMax ranks)
+    const int rem = min(3 * kLwLeafMax, max(1, remaining * p.speculate / 100));
+    if (ns <= rem && ncand <= k) {
+      // every splittable node ranks inside the window and the batch has room for every
+      // candidate: the batch is all of them, and no bottleneck / rank is needed (the order
+      // only numbers the speculative nodes: the replay orders pops by (gain, push seq), so
+      // the tree is the same). Most batches of a 255-leaf tree take this path.
+      for (int i = i0; i < i1; ++i)
+        if (splittable(i) && s_nd[i].x < 0) s_batch[pc++] = i;
+      if (tid == 0) {
+        s_k = ncand;
+        s_ncand = ncand;
+      }
+      __syncthreads();
+      k = s_k;
+    } else {
     for (int i = tid; i < nsid; i += kLwPlanThreads) {
       s_par[i] = -1;
       s_m[i] = ord(s_loss[i]);
@@ -627,24 +656,12 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
       __syncthreads();
     }
     LW_TICK(22);
-    // the splittable live nodes (each pops as a split): rank keys, compacted
-    auto splittable = [&](int i) { return live(i) && (s_nd[i].z >> 24) == 0; };
+    // rank keys of the splittable nodes, compacted
     auto rkey = [&](int i) {
       return i == blocked ? ~0ull
                           : (((unsigned long long)s_m[i] << 32) |
                              (unsigned long long)((ord(s_loss[i]) >> 12) << 12) | (unsigned long long)i);
     };
-    const int per = (nsid + kLwPlanThreads - 1) / kLwPlanThreads;
-    const int i0 = min(nsid, tid * per), i1 = min(nsid, i0 + per);
-    int c = 0, cc = 0;
-    for (int i = i0; i < i1; ++i) {
-      const bool sp = splittable(i);
-      c += sp ? 1 : 0;
-      cc += (sp && s_nd[i].x < 0) ? 1 : 0;
-    }
-    int ns, ncand;
-    int pos = lw_scan(c, s_tmp, &ns);
-    int pc = lw_scan(cc, s_tmp, &ncand);
     int* s_cand = s_par;  // all -1 after the pointer jumping: reused as the candidate list
     for (int i = i0; i < i1; ++i) {
       if (!splittable(i)) continue;
@@ -653,8 +670,6 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     }
     const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= kLwCap (a multiple of 128)
     for (int z = ns + tid; z < ns_pad; z += kLwPlanThreads) s_rk[z] = 0ull;  // never ranks above a key
-    // rank window: speculate percent of the leaf budget (s_uid holds 3 kLwLeafMax ranks)
-    const int rem = min(3 * kLwLeafMax, max(1, remaining * p.speculate / 100));
     for (int r = tid; r < rem; r += kLwPlanThreads) s_uid[r] = -1;
     __syncthreads();
     LW_TICK(23);
@@ -697,6 +712,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     }
     __syncthreads();
     k = s_k;
+    }  // ranked batch choice
   }
   LW_TICK(4);
   // F. expand the batch: children ids, partition descriptors (chunks of kLwChunk rows)
