@@ -523,12 +523,51 @@ __global__ __launch_bounds__(kT) void split_feat_kernel(
 // item's last group block combines the groups' records and takes the totals from f0's group.
 constexpr int kWideSplitMaxBlocks = 2048;  // grid cap (a multiple of 8; grid-stride inside)
 
+// Derived (parent - sibling) histograms of a wide-bin item list, materialised by one
+// streaming pass before split_wide_kernel: every block subtracts a contiguous 2048-pair
+// slice of one derived item with all its loads in flight (inside split_wide_kernel the
+// subtraction ran 4 bins per step per thread -- its register budget holds the whole run
+// of a feature pair -- and dominated the leaf-wise 5000-bin split search). Blocks past the
+// device item count, or on built items, exit.
+constexpr int kDeriveThreads = 256;
+constexpr int kDerivePer = 8;  // 16-B pairs per thread
+constexpr int kDeriveMaxBlocks = 4096;  // grid cap: the work units are walked grid-stride
+__global__ __launch_bounds__(kDeriveThreads) void derive_wide_kernel(
+    long long* __restrict__ hist, long long pairs, const int4* __restrict__ items,
+    const int* __restrict__ nitems_dev, int nitems_max, int blocks_per_item) {
+  const int live = nitems_dev ? min(*nitems_dev, nitems_max) : nitems_max;
+  const long long units = (long long)live * blocks_per_item;
+  for (long long w = blockIdx.x; w < units; w += gridDim.x) {  // uniform per block
+    const int item = (int)(w / blocks_per_item);
+    const int4 it = items[item];
+    if (it.w == 0) continue;
+    const long long p0 = (w % blocks_per_item) * kDeriveThreads * kDerivePer;
+    longlong2* hn = reinterpret_cast<longlong2*>(hist) + (size_t)it.x * pairs;
+    const longlong2* hp = reinterpret_cast<const longlong2*>(hist) + (size_t)it.y * pairs;
+    const longlong2* hs = reinterpret_cast<const longlong2*>(hist) + (size_t)it.z * pairs;
+    longlong2 a[kDerivePer], c[kDerivePer];
+#pragma unroll
+    for (int u = 0; u < kDerivePer; ++u) {
+      const long long i = p0 + (long long)u * kDeriveThreads + threadIdx.x;
+      if (i < pairs) { a[u] = hp[i]; c[u] = hs[i]; }
+    }
+#pragma unroll
+    for (int u = 0; u < kDerivePer; ++u) {
+      const long long i = p0 + (long long)u * kDeriveThreads + threadIdx.x;
+      if (i < pairs) hn[i] = make_longlong2(a[u].x - c[u].x, a[u].y - c[u].y);
+    }
+  }
+}
+
+// pre_derived: derive_wide_kernel has materialised every derived item's histogram, so all
+// items are read like built ones
 template <int kR, int kFG>
 __global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
-    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max) {
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max,
+    int pre_derived) {
   constexpr int kT = 256 * kFG;  // 256 bin runs per feature
   constexpr int kW = kT / kWave;
   static_assert(kW * kFG <= kWave, "wave 0 scans the (wave, feature) totals");
@@ -562,7 +601,7 @@ __global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
     longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
     const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
     const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
-    const bool derived = it.w != 0;
+    const bool derived = it.w != 0 && !pre_derived;
     const int f_lo = grp * kFG, f = f_lo + fi;
     const bool fin = f < F;
     const int nb = fin ? nbins_f[f] : 0;
@@ -857,6 +896,19 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
     // wide bins: the group's histogram in registers (split_wide_kernel); part: nitems x
     // ceil(F / kFG) records. 4 features per 1024-thread block up to 1024 bins, above that 2
     // per 512-thread block (kR 16-B pairs per thread + the walk within 256 VGPRs)
+    // derived histograms first, in one streaming pass (YTK_WIDE_DERIVE=0: inside the split)
+    static const bool pre = [] {
+      const char* e = getenv("YTK_WIDE_DERIVE");
+      return !(e && e[0] == '0');
+    }();
+    if (pre) {
+      const long long pairs = (long long)B * F;
+      const int bpi = (int)((pairs + kDeriveThreads * kDerivePer - 1) / (kDeriveThreads * kDerivePer));
+      hipLaunchKernelGGL(derive_wide_kernel, dim3((unsigned)std::min<long long>((long long)bpi * nitems, kDeriveMaxBlocks)),
+                         dim3(kDeriveThreads), 0,
+                         reinterpret_cast<hipStream_t>(stream), (long long*)hist, pairs, (const int4*)items,
+                         (const int*)nitems_dev, nitems, bpi);
+    }
 #define YTK_SPLIT_WIDE(R, FG)                                                                                  \
   do {                                                                                                         \
     const long long L = (long long)((F + FG - 1) / FG) * ((nitems + 7) / 8 * 8);                               \
@@ -864,7 +916,8 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
     hipLaunchKernelGGL((split_wide_kernel<R, FG>), dim3(nblk), dim3(256 * FG), 0,                              \
                        reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, (const int*)nbins_f,     \
                        (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp,                     \
-                       (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters, nitems); \
+                       (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters, nitems, \
+                       pre ? 1 : 0);                                                                           \
   } while (0)
     if (B <= 4 * 256) YTK_SPLIT_WIDE(4, 4);
     else if (B <= 8 * 256) YTK_SPLIT_WIDE(8, 2);
