@@ -14,6 +14,8 @@
 // order-dependent reduction in the sparse family (documented).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace ytk {
 
 __device__ __forceinline__ float pair_dot(const float* __restrict__ a, const float* __restrict__ b, int k,
@@ -91,6 +93,63 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
   }
 }
 
+
+// Forward for k == 4 (one float4 per latent block), kPU pairs per lane in flight: the
+// generic loop walks p one pair at a time, two dependent 16-B gathers per step, which left
+// the forward latency bound (one wave per row, 39 serial gather round trips: 25 ms per
+// Criteo-shape pass). Same pairs, same per-lane order of the adds.
+constexpr int kPU = 4;
+__global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
+    const int* __restrict__ fld, long long nrows, const float* __restrict__ V, int nfield,
+    float* __restrict__ fx, int skip_feat) {
+  const long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return;
+  const long long b = indptr[row];
+  const int m = (int)(indptr[row + 1] - b);
+  const long long stride = (long long)nfield * 4;
+  float acc = 0.f;
+  for (int pt = 0; pt < m; pt += 64) {
+    const int pj = pt + lane;
+    int ip = 0, fp = 0;
+    float xp = 0.f;
+    if (pj < m) { ip = idx[b + pj]; xp = val[b + pj]; fp = fld[b + pj]; }
+    for (int qt = pt; qt < m; qt += 64) {
+      const int qj = qt + lane;
+      int iq = 0, fq = 0;
+      float xq = 0.f;
+      if (qj < m) { iq = idx[b + qj]; xq = val[b + qj]; fq = fld[b + qj]; }
+      const int pend = min(64, m - pt);
+      for (int pp0 = 0; pp0 < pend; pp0 += kPU) {
+        float4 va[kPU], vb[kPU];
+        float xx[kPU];
+        bool ok[kPU];
+#pragma unroll
+        for (int u = 0; u < kPU; ++u) {
+          const int pp = min(pp0 + u, pend - 1);  // uniform; the duplicate is masked by ok
+          const int P = pt + pp;
+          const int ipb = __shfl(ip, pp, 64), fpb = __shfl(fp, pp, 64);
+          const float xpb = __shfl(xp, pp, 64);
+          ok[u] = pp0 + u < pend && qj < m && qj > P && ipb != skip_feat && iq != skip_feat;
+          xx[u] = xpb * xq;
+          va[u] = vb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok[u]) {
+            va[u] = *reinterpret_cast<const float4*>(V + (long long)ipb * stride + (long long)fq * 4);
+            vb[u] = *reinterpret_cast<const float4*>(V + (long long)iq * stride + (long long)fpb * 4);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPU; ++u)
+          if (ok[u])
+            acc += (va[u].x * vb[u].x + va[u].y * vb[u].y + va[u].z * vb[u].z + va[u].w * vb[u].w) * xx[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) fx[row] = acc;
+}
 
 // Column-ordered (gather) backward: no global atomics.
 //   gV[i, f_q, :] = sum over entries e of feature i (row r, value x, field f_i) and every
@@ -335,6 +394,11 @@ __global__ __launch_bounds__(256) void ffm_grad_stream_kernel(
 
 using namespace ytk;
 
+static bool getenv_off(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '0';
+}
+
 extern "C" {
 
 // fx[row] = pair interaction sum (forward) or g += pair gradients scaled by coef[row].
@@ -350,6 +414,9 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
     hipLaunchKernelGGL(ffm_pairs_kernel<true>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
                        nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat);
+  else if (vec4 && k == 4 && !getenv_off("YTK_FFM_K4"))
+    hipLaunchKernelGGL(ffm_pairs_k4_kernel, grid, dim3(256), 0, s, (const long long*)indptr, (const int*)idx,
+                       (const float*)val, (const int*)fld, nrows, (const float*)V, nfield, (float*)fx, skip_feat);
   else
     hipLaunchKernelGGL(ffm_pairs_kernel<false>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
