@@ -48,6 +48,35 @@ def test_spmm_cpu_matches_dense():
     assert n > CHUNK // 2 or X.n_chunks >= F
 
 
+def test_tile_blocks_and_heavy_columns_tables():
+    """Host-side tables of the tiled SpMV and the heavy-column reduce: every block holds at
+    most TILE_SEGS whole segments that start inside one (TILE_CAP - 256)-entry window, the
+    blocks cover the segments in order; non-contiguous segments give None; heavy columns are
+    exactly those with more than REDUCE_LIGHT chunks."""
+    import ytk_learn_amd.ops.sparse as sp
+    g = np.random.default_rng(3)
+    lens = torch.from_numpy(np.concatenate([g.integers(0, 40, 5000), [9000, 0, 3], g.integers(0, 3, 2000)]))
+    beg = torch.zeros(lens.numel(), dtype=torch.int64)
+    beg[1:] = torch.cumsum(lens, 0)[:-1]
+    end = beg + lens
+    bseg = sp.tile_blocks(beg, end)
+    assert bseg is not None and int(bseg[0]) == 0 and int(bseg[-1]) == lens.numel()
+    assert bool((bseg[1:] >= bseg[:-1]).all())
+    win = sp.TILE_CAP - 256
+    for b in range(bseg.numel() - 1):
+        s0, s1 = int(bseg[b]), int(bseg[b + 1])
+        if s1 == s0:
+            continue
+        assert s1 - s0 <= sp.TILE_SEGS
+        starts = (beg[s0:s1] - beg[0]) // win
+        assert int(starts.min()) == int(starts.max())  # one window
+    gap = end.clone()
+    gap[10] += 1  # segment 11 no longer starts where 10 ends
+    assert sp.tile_blocks(beg, gap) is None
+    cptr = torch.tensor([0, 1, 18, 20, 57, 57], dtype=torch.int64)  # chunks per column: 1, 17, 2, 37, 0
+    assert sp.heavy_columns(cptr).tolist() == [1, 3]
+
+
 def _pairs_dense(ip, ix, vv, fl, V, nf, k):
     """fp64 reference of the FFM pair sum per row."""
     V3 = V.double().view(-1, nf, k)
