@@ -104,7 +104,7 @@ void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, in
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
                            float, float, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintptr_t, long long, uintptr_t, uintptr_t,
-                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t);
+                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int);
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
@@ -215,12 +215,15 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lv_partition_children", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
-                                     int count_only, int a0, int a1, int maxp, uintptr_t stream) {
+                                     int count_only, int a0, int a1, int maxp, uintptr_t stream, int bin_bytes) {
     if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
-                              max_blocks, count_only, a0, a1, maxp, stream);
-  });
+                              max_blocks, count_only, a0, a1, maxp, stream, bin_bytes);
+  }, pybind11::arg("ptrs"), pybind11::arg("ip"), pybind11::arg("fp"), pybind11::arg("binsT"), pybind11::arg("ncol"),
+     pybind11::arg("rows"), pybind11::arg("ghp"), pybind11::arg("rows_out"), pybind11::arg("gh_out"),
+     pybind11::arg("max_blocks"), pybind11::arg("count_only"), pybind11::arg("a0"), pybind11::arg("a1"),
+     pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1);
   m.def("split_node_grouped", &ytk_split_node_grouped);
   m.def("lv_split_plan", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,

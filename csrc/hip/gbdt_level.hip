@@ -480,17 +480,18 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
-template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, bool kPfCol = false>
+template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, bool kPfCol = false,
+          typename BinT = uint8_t>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
-void lv_partition_children_kernel(LvParams p, LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
+void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
                                   int dgap, int use_loc, int fused, int maxp) {
   if constexpr (kScatter && kPrefetch)
-    partition_atomic_body_pf<uint8_t, kS, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+    partition_atomic_body_pf<BinT, kS, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   else
-    partition_atomic_body<uint8_t, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+    partition_atomic_body<BinT, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                              b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                              reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
@@ -720,13 +721,33 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
 // arg0 / arg1 as ytk_lv_step(3).
 void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t binsT, long long ncol,
                                uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
-                               int count_only, int arg0, int arg1, int maxp, uintptr_t stream) {
+                               int count_only, int arg0, int arg1, int maxp, uintptr_t stream, int bin_bytes) {
   LvParams p = make_params(ip, fp);
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
   const int use_loc = (arg1 >> 30) & 1, fused = (arg1 >> 29) & 1;
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
+  if (bin_bytes == 2) {
+    // uint16 bins (wide): one configuration -- 2048-row chunks, the pipelined body with the
+    // next chunk's row ids and (g, h) in flight
+    if (p.part_chunk != kPartThreads * kAtomSub)
+      throw std::invalid_argument("lv_partition_children: uint16 bins take 2048-row chunks");
+#define YTK_LVPC16(SC, KP)                                                                                   \
+  hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, kAtomSub, SC, SC, false, uint16_t>), grid,        \
+                     dim3(kPartThreads), 0, s, p, b, (const uint16_t*)binsT, ncol, (const int*)rows,        \
+                     (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
+    if (maxp <= 64) {
+      if (count_only) YTK_LVPC16(false, 64); else YTK_LVPC16(true, 64);
+    } else if (maxp <= 512) {
+      if (count_only) YTK_LVPC16(false, 512); else YTK_LVPC16(true, 512);
+    } else {
+      if (count_only) YTK_LVPC16(false, kMaxPend); else YTK_LVPC16(true, kMaxPend);
+    }
+#undef YTK_LVPC16
+    YTK_LAUNCH_CHECK();
+    return;
+  }
   if (p.part_chunk != kPartThreads * kAtomSub && p.part_chunk != kPartThreads * 2 * kAtomSub &&
       p.part_chunk != kPartThreads * kAtomSub / 2)
     throw std::invalid_argument("lv_partition_children: part_chunk must be 1024, 2048 or 4096");

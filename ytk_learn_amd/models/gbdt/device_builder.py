@@ -127,7 +127,8 @@ class DeviceLevelBuilder:
         # children are planned from the LOCAL counts (the smaller child by the globally
         # identical hessian sums) and the next level's planner patches the global counts
         # from the all-reduced cursors.
-        self.fuse_part_children = (self.part_atomic and bins.dtype == torch.uint8
+        # (uint16 bins too: one kernel configuration, 2048-row chunks)
+        self.fuse_part_children = (self.part_atomic and bins.dtype in (torch.uint8, torch.int16)
                                    and (not self.comm.is_dist or self.fuse_counts)
                                    and os.environ.get("YTK_FUSE_PART_CHILDREN", "1") != "0")
         # rows per partition chunk (= per cursor reservation): 8 rows per thread (2048);
@@ -138,7 +139,8 @@ class DeviceLevelBuilder:
         # (multi-GPU: the last level runs the standalone 2048-row partition, so the chunk stays
         # at 2048 for every level)
         self.part_chunk = (int(os.environ.get("YTK_PART_CHUNK", "2048"))
-                           if self.fuse_part_children and not self.comm.is_dist else self.MIN_ROWS)
+                           if self.fuse_part_children and not self.comm.is_dist and bins.dtype == torch.uint8
+                           else self.MIN_ROWS)
         self.part_target = (-(-self.N // self.part_chunk) + 1) if self.part_atomic else self.PART_TARGET
         # one GPU: split search + next level's split planning in one launch (YTK_FUSE_SPLIT_PLAN=1).
         # Off by default: the release/acquire fences it needs cost what the saved launch
@@ -560,7 +562,7 @@ class DeviceLevelBuilder:
                 h.lv_partition_children(ptrs, ip, fp, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in,
                                         ptr(self.rows_tmp), ptr(self.gh_tmp), npart, 1 if last else 0, base,
                                         half | (ncs << 14) | ((1 if fused else 0) << 29) | (1 << 30),
-                                        self.maxp, s)
+                                        self.maxp, s, bb)
                 tm.mark("partition")
             # the flag kernel also accumulates the per-split left totals into left_loc
             elif self.part_atomic:
