@@ -561,13 +561,12 @@ __global__ __launch_bounds__(kDeriveThreads) void derive_wide_kernel(
 
 // pre_derived: derive_wide_kernel has materialised every derived item's histogram, so all
 // items are read like built ones
-template <int kR, int kFG>
+template <int kR, int kFG, bool kPreDerived>
 __global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
     long long* __restrict__ hist, int B, int F, const int* __restrict__ nbins_f,
     const uint8_t* __restrict__ fmask, int f0, const int4* __restrict__ items,
     SplitOut* __restrict__ out, GainParams gp, const int* __restrict__ nitems_dev,
-    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max,
-    int pre_derived) {
+    const double* __restrict__ inv_dev, SplitOut* __restrict__ part, int* __restrict__ counters, int nitems_max) {
   constexpr int kT = 256 * kFG;  // 256 bin runs per feature
   constexpr int kW = kT / kWave;
   static_assert(kW * kFG <= kWave, "wave 0 scans the (wave, feature) totals");
@@ -601,7 +600,7 @@ __global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
     longlong2* hn = reinterpret_cast<longlong2*>(hist + (size_t)it.x * slot_sz);
     const longlong2* hp = reinterpret_cast<const longlong2*>(hist + (size_t)it.y * slot_sz);
     const longlong2* hs = reinterpret_cast<const longlong2*>(hist + (size_t)it.z * slot_sz);
-    const bool derived = it.w != 0 && !pre_derived;
+    const bool derived = !kPreDerived && it.w != 0;
     const int f_lo = grp * kFG, f = f_lo + fi;
     const bool fin = f < F;
     const int nb = fin ? nbins_f[f] : 0;
@@ -615,7 +614,7 @@ __global__ __launch_bounds__(256 * kFG) void split_wide_kernel(
     }
     const bool want = on || f == tf;
     longlong2 v[kR];
-    if (derived) {  // 4 bins per step: 8 loads in flight, not 2 kR (register budget)
+    if (derived) {  // 4 bins per step: 8 loads in flight, not 2 kR (register budget); dead when kPreDerived
 #pragma unroll
       for (int k0 = 0; k0 < kR; k0 += 4) {
         longlong2 a[4], c[4];
@@ -913,11 +912,18 @@ extern "C" void ytk_split_find(uintptr_t hist, int B, int F, uintptr_t nbins_f, 
   do {                                                                                                         \
     const long long L = (long long)((F + FG - 1) / FG) * ((nitems + 7) / 8 * 8);                               \
     const unsigned nblk = (unsigned)std::min<long long>(L, kWideSplitMaxBlocks);                               \
-    hipLaunchKernelGGL((split_wide_kernel<R, FG>), dim3(nblk), dim3(256 * FG), 0,                              \
-                       reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, (const int*)nbins_f,     \
-                       (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp,                     \
-                       (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters, nitems, \
-                       pre ? 1 : 0);                                                                           \
+    if (pre)                                                                                                   \
+      hipLaunchKernelGGL((split_wide_kernel<R, FG, true>), dim3(nblk), dim3(256 * FG), 0,                      \
+                         reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, (const int*)nbins_f,   \
+                         (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp,                   \
+                         (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters,      \
+                         nitems);                                                                              \
+    else                                                                                                       \
+      hipLaunchKernelGGL((split_wide_kernel<R, FG, false>), dim3(nblk), dim3(256 * FG), 0,                     \
+                         reinterpret_cast<hipStream_t>(stream), (long long*)hist, B, F, (const int*)nbins_f,   \
+                         (const uint8_t*)fmask, f0, (const int4*)items, (SplitOut*)out, gp,                   \
+                         (const int*)nitems_dev, (const double*)inv_dev, (SplitOut*)part, (int*)counters,      \
+                         nitems);                                                                              \
   } while (0)
     // (4-feature groups in 1024-thread blocks -- 64 B of every bin row per load instead of
     // 32 B -- measured slower: leaf-wise 5000 bins 8.70 -> 10.45 ms/tree at the 128-VGPR cap)
