@@ -14,7 +14,7 @@ void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int
                  float, float, uintptr_t, uintptr_t, uintptr_t);
 void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                         int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t,
-                        uintptr_t);
+                        uintptr_t, int);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 void ytk_hist_set_fw(int);
@@ -104,7 +104,7 @@ void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, in
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
                            float, float, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintptr_t, long long, uintptr_t, uintptr_t,
-                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int);
+                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, int);
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
@@ -143,7 +143,17 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.doc() = "ytk-learn-amd HIP kernels (gfx950)";
   m.def("hist_fx", &ytk_hist_fx);
   m.def("hist_fx_global", &ytk_hist_fx_global);
-  m.def("hist_fx_staged", &ytk_hist_fx_staged);
+  m.def("hist_fx_staged", [](uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows, uintptr_t work,
+                             int nwork, uintptr_t hist, int B, float sg, float sh, uintptr_t nwork_dev,
+                             uintptr_t scales_dev, uintptr_t staging, int slot_base, int nslots, uintptr_t slot_ids,
+                             uintptr_t work_off_dev, uintptr_t stream, int gh_rows) {
+    ytk_hist_fx_staged(bins, stride, F, ghp, rows, work, nwork, hist, B, sg, sh, nwork_dev, scales_dev, staging,
+                       slot_base, nslots, slot_ids, work_off_dev, stream, gh_rows);
+  }, pybind11::arg("bins"), pybind11::arg("stride"), pybind11::arg("F"), pybind11::arg("ghp"), pybind11::arg("rows"),
+     pybind11::arg("work"), pybind11::arg("nwork"), pybind11::arg("hist"), pybind11::arg("B"), pybind11::arg("sg"),
+     pybind11::arg("sh"), pybind11::arg("nwork_dev"), pybind11::arg("scales_dev"), pybind11::arg("staging"),
+     pybind11::arg("slot_base"), pybind11::arg("nslots"), pybind11::arg("slot_ids"), pybind11::arg("work_off_dev"),
+     pybind11::arg("stream"), pybind11::arg("gh_rows") = 0);
   m.def("hist_wide", &ytk_hist_wide);
   m.def("hist_set_fw", &ytk_hist_set_fw);
   m.def("hist_get_fw", &ytk_hist_get_fw);
@@ -215,15 +225,16 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lv_partition_children", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
-                                     int count_only, int a0, int a1, int maxp, uintptr_t stream, int bin_bytes) {
+                                     int count_only, int a0, int a1, int maxp, uintptr_t stream, int bin_bytes,
+                                     int gh_rows) {
     if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
-                              max_blocks, count_only, a0, a1, maxp, stream, bin_bytes);
+                              max_blocks, count_only, a0, a1, maxp, stream, bin_bytes, gh_rows);
   }, pybind11::arg("ptrs"), pybind11::arg("ip"), pybind11::arg("fp"), pybind11::arg("binsT"), pybind11::arg("ncol"),
      pybind11::arg("rows"), pybind11::arg("ghp"), pybind11::arg("rows_out"), pybind11::arg("gh_out"),
      pybind11::arg("max_blocks"), pybind11::arg("count_only"), pybind11::arg("a0"), pybind11::arg("a1"),
-     pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1);
+     pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1, pybind11::arg("gh_rows") = 0);
   m.def("split_node_grouped", &ytk_split_node_grouped);
   m.def("lv_split_plan", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,

@@ -69,7 +69,9 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     const float2* __restrict__ ghp, const int* __restrict__ rows,
     const int4* __restrict__ work, long long* __restrict__ hist, int B, int nb_lds,
     float sg, float sh, const int* __restrict__ nwork_dev, const float* __restrict__ scales_dev,
-    long long* __restrict__ staging, const int* __restrict__ work_off_dev) {
+    long long* __restrict__ staging, const int* __restrict__ work_off_dev, int gh_rows) {
+  // gh_rows: (g, h) is indexed by ROW id (the level engine's first gathered level: the root
+  // partition moved only the row ids), else by position
   // LDS bin rows of 64 words: [32 g words | 32 h words]; the h atomic of a (bin, feature)
   // is the g address + 256 B (instruction offset), both conflict-free (hist_lds_pos)
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
       ok[j] = pos < w.z;
       const int p = ok[j] ? pos : w.y;
       d[j] = *reinterpret_cast<const unsigned*>(bseg + (size_t)(unsigned)r[j] * stride);
-      const float2 t = ghp[p];
+      const float2 t = ghp[gh_rows ? r[j] : p];
       v[j] = ok[j] ? t : make_float2(0.f, 0.f);  // rows past the end add 0
     }
   };
@@ -661,15 +663,15 @@ template <bool kIdentity>
 static void launch_hist_fx(dim3 grid, size_t lds_unused, hipStream_t s, const uint8_t* bins, long long stride, int F,
                            const float2* ghp, const int* rows, const int4* work, long long* hist, int B, int nb_lds,
                            float sg, float sh, const int* nwork_dev, const float* scales_dev, long long* staging,
-                           const int* work_off_dev) {
+                           const int* work_off_dev, int gh_rows = 0) {
   (void)lds_unused;
   const size_t lds = (size_t)nb_lds * 2 * g_hist_fw * sizeof(unsigned long long);
   if (g_hist_fw == 16)
     hipLaunchKernelGGL((hist_fx_kernel<kIdentity, 16>), grid, dim3(kHistThreads), lds, s, bins, stride, F, ghp,
-                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev);
+                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev, gh_rows);
   else
     hipLaunchKernelGGL((hist_fx_kernel<kIdentity, 32>), grid, dim3(kHistThreads), lds, s, bins, stride, F, ghp,
-                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev);
+                       rows, work, hist, B, nb_lds, sg, sh, nwork_dev, scales_dev, staging, work_off_dev, gh_rows);
 }
 
 extern "C" {
@@ -711,7 +713,7 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
                         uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
                         uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
                         int slot_base, int nslots, uintptr_t slot_ids, uintptr_t work_off_dev,
-                        uintptr_t stream) {
+                        uintptr_t stream, int gh_rows) {
   if (nwork <= 0 || nslots <= 0) return;
   const int fw = g_hist_fw;
   const int groups = (F + fw - 1) / fw;
@@ -725,7 +727,7 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   else
     launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
                           (const int4*)work, (long long*)hist, B, nb_lds, sg, sh, (const int*)nwork_dev,
-                          (const float*)scales_dev, (long long*)staging, (const int*)work_off_dev);
+                          (const float*)scales_dev, (long long*)staging, (const int*)work_off_dev, gh_rows);
   YTK_LAUNCH_CHECK();
   const int E = nb_lds * fw;
   // split-K factor (YTK_REDUCE_SPLIT overrides; exact int64 atomics, so the sums do not

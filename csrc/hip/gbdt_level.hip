@@ -485,11 +485,12 @@ template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, boo
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
-                                  int dgap, int use_loc, int fused, int maxp) {
+                                  int dgap, int use_loc, int fused, int maxp, int gh_rows) {
   if constexpr (kScatter && kPrefetch)
     partition_atomic_body_pf<BinT, kS, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                          reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
+                                          reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride,
+                                          gh_rows);
   else
     partition_atomic_body<BinT, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                              b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
@@ -721,7 +722,10 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
 // arg0 / arg1 as ytk_lv_step(3).
 void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t binsT, long long ncol,
                                uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
-                               int count_only, int arg0, int arg1, int maxp, uintptr_t stream, int bin_bytes) {
+                               int count_only, int arg0, int arg1, int maxp, uintptr_t stream, int bin_bytes,
+                               int gh_rows) {
+  // gh_rows: ghp is row-indexed (pipelined bodies only: the unpipelined ones read (g, h) by
+  // position)
   LvParams p = make_params(ip, fp);
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -736,7 +740,8 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
 #define YTK_LVPC16(SC, KP)                                                                                   \
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, kAtomSub, SC, SC, false, uint16_t>), grid,        \
                      dim3(kPartThreads), 0, s, p, b, (const uint16_t*)binsT, ncol, (const int*)rows,        \
-                     (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
+                     (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
+                     gh_rows)
     if (maxp <= 64) {
       if (count_only) YTK_LVPC16(false, 64); else YTK_LVPC16(true, 64);
     } else if (maxp <= 512) {
@@ -761,10 +766,12 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const bool prefetch = !(pf && pf[0] == '0');
   const bool pf_gh = !(pf && (pf[0] == '0' || pf[0] == '1'));
   const bool pf_col = pf && pf[0] == '3';  // YTK_PART_PREFETCH=3: + the next chunk's split-feature bytes
+  if (gh_rows && (!prefetch || count_only))
+    throw std::invalid_argument("lv_partition_children: row-indexed (g, h) needs the pipelined scatter body");
 #define YTK_LVPC4(SC, KP, S, PF, PG, PC)                                                                      \
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG, PC>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
-                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp)
+                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, gh_rows)
 #define YTK_LVPC2(SC, KP, S, PF)                                                  \
   do {                                                                            \
     if ((PF) && pf_col) YTK_LVPC4(SC, KP, S, PF, true, true);                     \

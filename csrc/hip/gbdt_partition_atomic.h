@@ -205,9 +205,12 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
-    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs) {
+    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs, int gh_rows = 0) {
   // ghp == nullptr: (g, h) stays row-indexed (leaf-wise engine); out_shift as in
-  // partition_atomic_body (children into the other half of a 2N ping-pong buffer)
+  // partition_atomic_body (children into the other half of a 2N ping-pong buffer).
+  // gh_rows: ghp is indexed by ROW id (the level engine's first gathered level), so the next
+  // chunk's (g, h) gather waits for its row ids: it is issued after this chunk's cursor
+  // reservation (like the split-feature bytes of kCol) instead of with the row-id loads.
   constexpr int NW = kPartThreads / kWave;
   static_assert(S * NW <= kWave, "one-wave scan of the sub-chunk counts");
   constexpr int CH = S * kPartThreads;
@@ -252,11 +255,11 @@ __device__ __forceinline__ void partition_atomic_body_pf(
       r[j] = pos < c.end ? (rows ? rows[pos] : pos) : 0;
     }
   };
-  auto load_gh = [&](const Chunk& c, float2 (&g)[S]) {
+  auto load_gh = [&](const Chunk& c, const int (&r)[S], float2 (&g)[S]) {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int pos = c.beg + j * kPartThreads + tid;
-      g[j] = (pos < c.end && ghp) ? ghp[pos] : make_float2(0.f, 0.f);
+      g[j] = (pos < c.end && ghp) ? ghp[gh_rows ? r[j] : pos] : make_float2(0.f, 0.f);
     }
   };
   int bid = (int)blockIdx.x;
@@ -264,7 +267,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
   int r[S];
   load_rows(c, r);
   float2 g[S];
-  if (kGh) load_gh(c, g);
+  if (kGh) load_gh(c, r, g);
   // kCol: the next chunk's split-feature bytes are gathered before this chunk's scatter
   // (its row ids have arrived by then), so a chunk starts with all its loads done
   int cb[kCol ? S : 1];
@@ -279,7 +282,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
   if constexpr (kCol) load_col(c, r, cb);
   while (true) {
     bool left[S];
-    if (!kGh) load_gh(c, g);
+    if (!kGh) load_gh(c, r, g);
     if constexpr (kCol) {
 #pragma unroll
       for (int j = 0; j < S; ++j) left[j] = cb[j] <= c.th;
@@ -300,7 +303,9 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     if (more) {
       cn = locate(nbid);
       load_rows(cn, rn);
-      if constexpr (kGh) load_gh(cn, gn);
+      if constexpr (kGh) {
+        if (!gh_rows) load_gh(cn, rn, gn);
+      }
     }
     int lrank[S];
 #pragma unroll
@@ -329,6 +334,9 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     __syncthreads();
     if constexpr (kCol) {
       if (more) load_col(cn, rn, cb);
+    }
+    if constexpr (kGh) {
+      if (gh_rows && more) load_gh(cn, rn, gn);
     }
     {
       const int tl = s_tl;

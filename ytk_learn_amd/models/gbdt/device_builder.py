@@ -428,6 +428,12 @@ class DeviceLevelBuilder:
         small_only = (self.defer_leaf_counts and not sampled and self.fuse_part_children
                       and os.environ.get("YTK_SMALL_ONLY", "1") != "0")
         ip = self._ip_cur = self.ip[:8] + [1 if small_only else 0]
+        # gh_rows: the root partition moves only the row ids and the first gathered level
+        # (its histograms and its partition) reads (g, h) by row id from the caller's array:
+        # one full (g, h) read + write less per tree (YTK_GH_ROWS=0: moved at the root too)
+        gh_rows = (not sampled and self.fuse_part_children and not self.wide and self.staged and p.max_depth >= 3
+                   and os.environ.get("YTK_GH_ROWS", "1") != "0"
+                   and os.environ.get("YTK_PART_PREFETCH", "2") != "0")
         # rows / position-ordered (g, h). Without sampling the root level reads the identity
         # permutation and the caller's gh directly; the first partition writes the buffers.
         if sampled:
@@ -478,7 +484,7 @@ class DeviceLevelBuilder:
         h.lv_init_scales(ptrs, ip, fp, ptr(mx), ptr(self.scales), ptr(self.inv_scales), s)
         tm.mark("init_stats")
 
-        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0):
+        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0, by_row=0):
             if self._zero_all:
                 if slot_base == 0:
                     self.hist.zero_()  # every slot of the tree in one fill (small slabs)
@@ -496,8 +502,9 @@ class DeviceLevelBuilder:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
                                  ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0,
                                  off(5) if n_dev is None else n_dev, ptr(self.scales), ptr(self.staging),
-                                 slot_base, nslots, 0, work_off, s)
+                                 slot_base, nslots, 0, work_off, s, by_row)
                 return
+            assert not by_row, "row-indexed (g, h) needs the staged histogram kernel"
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                       nitems, ptr(self.hist), self.B, 1.0, 1.0, off(5), ptr(self.scales), s)
 
@@ -549,6 +556,11 @@ class DeviceLevelBuilder:
             lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
+            part_gh_rows = 0
+            if gh_rows and d == 0:
+                gh_in = 0  # the root partition moves the row ids only
+            elif gh_rows and d == 1:
+                gh_in, part_gh_rows = gh0, 1  # (g, h) by row id; this level writes it in position order
             half = 1 << (c - 1)
             if last:
                 base, ncs = 0, 0  # no histograms at the last level
@@ -560,9 +572,10 @@ class DeviceLevelBuilder:
             fused_part = self.fuse_part_children and not (dist and last)
             if fused_part:
                 h.lv_partition_children(ptrs, ip, fp, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in,
-                                        ptr(self.rows_tmp), ptr(self.gh_tmp), npart, 1 if last else 0, base,
+                                        ptr(self.rows_tmp), ptr(self.gh_tmp) if gh_in else 0, npart,
+                                        1 if last else 0, base,
                                         half | (ncs << 14) | ((1 if fused else 0) << 29) | (1 << 30),
-                                        self.maxp, s, bb)
+                                        self.maxp, s, bb, part_gh_rows)
                 tm.mark("partition")
             # the flag kernel also accumulates the per-split left totals into left_loc
             elif self.part_atomic:
@@ -601,22 +614,24 @@ class DeviceLevelBuilder:
             self.ghp, self.gh_tmp = self.gh_tmp, self.ghp
             ptrs = self._ptrs()
             nmax = self.hist_target + half + 1
+            # the first gathered level reads (g, h) by row id from the caller's array (gh_rows)
+            hgh, hrow = (gh0, 1) if (gh_rows and d == 0) else (ptr(self.ghp), 0)
             if dist and self.overlap and half >= 8 and self.staged and not self.owner:  # large levels only:
                 # small ones are latency bound and a second collective would cost more
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
                 # second half's histogram build; the split search waits for both
                 hs = half // 2
-                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A))
+                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow)
                 work = self.comm.allreduce_(self.hist[base:base + hs], async_op=True)
-                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
-                           work_off=off(ST_N_HIST_A))
+                build_hist(hgh, ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
+                           work_off=off(ST_N_HIST_A), by_row=hrow)
                 tm.mark("build_hist_compute")
                 if work is not None:
                     work.wait()
                 self.comm.allreduce_(self.hist[base + hs:base + half + ncs])
                 tm.mark("build_hist_comm")
             else:
-                build_hist(ptr(self.ghp), ptr(self.rows), nmax, base, half)
+                build_hist(hgh, ptr(self.rows), nmax, base, half, by_row=hrow)
                 tm.mark("build_hist_compute")
                 if dist:
                     # built slots (+ this level's count slots when fused): one collective
