@@ -1,0 +1,144 @@
+"""Golden-formula property tests ("golden-value unit tests of every formula ...
+kernel-vs-NumPy property tests (hypothesis is available)"):
+
+* every single-output loss: grad == d loss / dz (torch fp64 autograd) away from its kinks, and
+  hess == d grad / dz where the reference's hessian is the true second derivative
+  (J/loss/*Function.java); softmax: grad == autograd, hess == the reference's 2 p (1 - p);
+* AUC (slot-bucketed, J/eval/AucEvaluator.java) == the brute-force weighted Mann-Whitney
+  statistic with ties counted 1/2, when predictions sit on the bucket grid;
+* the L-BFGS two-loop recursion (HoagOptimizer.hv, HoagOptimizer.java:904-929) == the
+  explicit recursive BFGS inverse-Hessian update applied to the vector.
+"""
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from ytk_learn_amd.losses.functions import create_loss
+from ytk_learn_amd.metrics.evaluators import AucEvaluator
+from ytk_learn_amd.parallel.comm import Comm
+
+# name -> (label sampler, score sampler, kink test: z, y -> bool, hessian is d grad / dz)
+_POS = lambda g, n: g.uniform(0.5, 5.0, n)  # noqa: E731
+_BIN = lambda g, n: g.integers(0, 2, n).astype(np.float64)  # noqa: E731
+_SCORE = lambda g, n: g.uniform(-3.0, 3.0, n)  # noqa: E731
+_LOSSES = {
+    "sigmoid": (_BIN, _SCORE, lambda z, y: np.zeros_like(z, bool), True),
+    "l2": (_POS, _SCORE, lambda z, y: np.zeros_like(z, bool), True),
+    "l1": (_POS, _SCORE, lambda z, y: np.abs(z - y) < 1e-3, False),
+    "huber": (_POS, _SCORE, lambda z, y: np.abs(np.abs(z - y) - 0.5) < 1e-3, False),
+    "poisson": (lambda g, n: g.integers(0, 6, n).astype(np.float64), _SCORE, lambda z, y: np.zeros_like(z, bool),
+                True),
+    "hinge": (_BIN, _SCORE, lambda z, y: np.abs(np.abs(z) - 1.0) < 1e-3, False),
+    "smooth_hinge": (_BIN, _SCORE, lambda z, y: (np.abs(z) < 1e-3) | (np.abs(np.abs(z) - 1.0) < 1e-3), False),
+    "l2_hinge": (_BIN, _SCORE, lambda z, y: np.abs(np.abs(z) - 1.0) < 1e-3, False),
+    "exponential": (_BIN, _SCORE, lambda z, y: np.zeros_like(z, bool), False),
+    "mape": (_POS, _SCORE, lambda z, y: np.abs(z - y) < 1e-3, False),
+    "smape": (_POS, _SCORE, lambda z, y: (np.abs(z - y) < 1e-3) | (np.abs(z) < 1e-3), False),
+    "inv_mape": (_POS, lambda g, n: g.uniform(0.5, 5.0, n), lambda z, y: np.abs(z - y) < 1e-3, False),
+}
+
+
+@pytest.mark.parametrize("name", sorted(_LOSSES))
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(seed=st.integers(0, 2 ** 31 - 1))
+def test_loss_derivatives_match_autograd(name, seed):
+    ys, zs, kink, true_hess = _LOSSES[name]
+    g = np.random.default_rng(seed)
+    n = 64
+    y = torch.from_numpy(ys(g, n))
+    z = torch.from_numpy(zs(g, n))
+    keep = torch.from_numpy(~kink(z.numpy(), y.numpy()))
+    L = create_loss(name)
+    zz = z.clone().requires_grad_(True)
+    L.loss(zz, y).sum().backward()
+    auto = zz.grad
+    got = L.grad(z, y)
+    torch.testing.assert_close(got[keep], auto[keep], rtol=1e-9, atol=1e-12)
+    if true_hess:
+        zz = z.clone().requires_grad_(True)
+        L.grad(zz, y).sum().backward()
+        torch.testing.assert_close(L.hess(z, y)[keep], zz.grad[keep], rtol=1e-9, atol=1e-12)
+
+
+@settings(max_examples=25, deadline=None)
+@given(seed=st.integers(0, 2 ** 31 - 1), K=st.integers(2, 6))
+def test_softmax_derivatives(seed, K):
+    g = np.random.default_rng(seed)
+    n = 32
+    z = torch.from_numpy(g.normal(size=(n, K)) * 2)
+    y = torch.zeros((n, K), dtype=torch.float64)
+    y[torch.arange(n), torch.from_numpy(g.integers(0, K, n))] = 1.0
+    L = create_loss("softmax")
+    zz = z.clone().requires_grad_(True)
+    L.loss(zz, y).sum().backward()
+    torch.testing.assert_close(L.grad(z, y), zz.grad, rtol=1e-9, atol=1e-12)
+    p = torch.softmax(z, 1)
+    torch.testing.assert_close(L.hess(z, y), 2 * p * (1 - p), rtol=0, atol=0)  # the reference's 2 p (1 - p)
+
+
+def _auc_pairs(y, p, w):
+    pos, neg = y == 1.0, y != 1.0
+    wp, wn = w[pos], w[neg]
+    gt = (p[pos][:, None] > p[neg][None, :]).astype(np.float64)
+    eq = (p[pos][:, None] == p[neg][None, :]).astype(np.float64)
+    return float(((gt + 0.5 * eq) * wp[:, None] * wn[None, :]).sum() / (wp.sum() * wn.sum()))
+
+
+@settings(max_examples=40, deadline=None)
+@given(seed=st.integers(0, 2 ** 31 - 1), slots=st.sampled_from([16, 100, 1000]))
+def test_auc_matches_pairwise_statistic(seed, slots):
+    g = np.random.default_rng(seed)
+    n = 300
+    y = g.integers(0, 2, n).astype(np.float32)
+    if y.min() == y.max():
+        y[0] = 1.0 - y[0]
+    k = g.integers(0, slots, n)
+    p = ((k + 0.5) / slots).astype(np.float32)  # on the bucket grid: equal bucket <=> equal score
+    w = g.uniform(0.2, 3.0, n)
+    ev = AucEvaluator(f"auc@{slots}")
+    a_w, a_r = ev.compute(torch.from_numpy(y), torch.from_numpy(p), torch.from_numpy(w), Comm.local())
+    assert a_w == pytest.approx(_auc_pairs(y, p, w), rel=1e-9, abs=1e-12)
+    assert a_r == pytest.approx(_auc_pairs(y, p, np.ones(n)), rel=1e-9, abs=1e-12)
+
+
+@settings(max_examples=20, deadline=None)
+@given(seed=st.integers(0, 2 ** 31 - 1), m=st.integers(1, 6), extra=st.integers(0, 4))
+def test_lbfgs_two_loop_matches_explicit_bfgs(seed, m, extra):
+    from types import SimpleNamespace
+
+    from ytk_learn_amd.optim.lbfgs import HoagOptimizer
+    g = np.random.default_rng(seed)
+    d = 7
+    npairs = m + extra  # the ring buffer wraps when there are more pairs than slots
+    A = g.normal(size=(d, d))
+    Hs = A @ A.T + d * np.eye(d)  # SPD: curvature pairs y = Hs s with s'y > 0
+    opt = HoagOptimizer.__new__(HoagOptimizer)
+    opt.ls = SimpleNamespace(m=m)
+    opt.S = [torch.zeros(d, dtype=torch.float64) for _ in range(m)]
+    opt.Y = [torch.zeros(d, dtype=torch.float64) for _ in range(m)]
+    opt.YS = [0.0] * m
+    pairs = []
+    for i in range(npairs):
+        s = g.normal(size=d)
+        yv = Hs @ s
+        c = i % m
+        opt.S[c] = torch.from_numpy(s.copy())
+        opt.Y[c] = torch.from_numpy(yv.copy())
+        opt.YS[c] = float(s @ yv)
+        pairs.append((s, yv))
+    cursor = npairs % m
+    loops = min(m, npairs)
+    s_l, y_l = pairs[-1]
+    ys, yy = float(s_l @ y_l), float(y_l @ y_l)
+    # explicit: H0 = (ys / yy) I, then the BFGS inverse update for the last `loops` pairs, oldest first
+    H = (ys / yy) * np.eye(d)
+    for s, yv in pairs[-loops:]:
+        rho = 1.0 / float(s @ yv)
+        V = np.eye(d) - rho * np.outer(yv, s)
+        H = V.T @ H @ V + rho * np.outer(s, s)
+    v = g.normal(size=d)
+    p = torch.from_numpy(v.copy())
+    opt.hv(p, cursor, loops, ys, yy)
+    np.testing.assert_allclose(p.numpy(), H @ v, rtol=1e-9, atol=1e-9)
