@@ -207,6 +207,22 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
         assert open(tmp_path / "eager" / "model.txt").read() == open(tmp_path / "rccl" / "model.txt").read()
 
 
+@pytest.mark.gpu
+def test_rccl_world1_capture_failure_falls_back(tmp_path):
+    """A round capture that fails (injected) is voted down and the job continues with eager
+    rounds -- same model, no graph replays, the captured collectives not counted."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_HIST_SYNC": "allreduce", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}
+    _run("gbdt", tmp_path / "plain", 1, "cuda", extra_env=env)
+    good = _run("gbdt", tmp_path / "graph", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
+    bad = _run("gbdt", tmp_path / "fail", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1", YTK_FAULT_CAPTURE="1"))
+    assert good["graph_replays"] > 0 and bad["graph_replays"] == 0
+    assert bad["comm"]["calls"] == good["comm"]["calls"]  # eager rounds issue what replays count
+    assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "fail" / "model.txt").read()
+
+
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
 def test_sgd_world2_model_averaging(tmp_path, task):
     """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every

@@ -595,6 +595,8 @@ class GBDTTrainer:
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
                         accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
                     assert not host_trees
+                    if os.environ.get("YTK_FAULT_CAPTURE") == "1":  # fault injection (tests): the vote + eager fallback
+                        raise RuntimeError("injected capture failure")
                     pool = g.pool()
                     # the collectives a replay issues (captured once, counted per replay)
                     coll = {k: self.comm.stats[k] - c0.get(k, 0) for k in self.comm.stats}
