@@ -118,7 +118,7 @@ void ytk_seg_prune(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr
 int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int,
-                       uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
+                       uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t);
 int ytk_tree_grad_hist_grid(long long);
 void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, uintptr_t);
 void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,

@@ -591,9 +591,19 @@ __global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
     const float* __restrict__ weight, long long N, float p0, float score_div,
     float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
     float* __restrict__ ghmax, int* __restrict__ leaf_part, int nvb, const float* __restrict__ scales,
-    long long* __restrict__ staging, int B) {
+    long long* __restrict__ staging, int B, unsigned long long* __restrict__ zero, long long zero_n) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];
   int* tsm = reinterpret_cast<int*>(hsm + 256 * 64);
+  if (zero) {
+    // the histogram slab of the next tree (16-byte aligned, zero_n uint64): zeroed here instead
+    // of by a fill launch at the end of the previous tree; the root reduce behind this kernel
+    // accumulates into it
+    ulonglong2* z2 = reinterpret_cast<ulonglong2*>(zero);
+    for (long long i = (long long)blockIdx.x * kTGHThreads + threadIdx.x; i < (zero_n >> 1);
+         i += (long long)gridDim.x * kTGHThreads)
+      z2[i] = make_ulonglong2(0ull, 0ull);
+    if ((zero_n & 1) && blockIdx.x == 0 && threadIdx.x == 0) zero[zero_n - 1] = 0ull;
+  }
   int* sf = tsm;
   int* st = tsm + nnodes;
   int* sl = tsm + 2 * nnodes;
@@ -1066,7 +1076,10 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
                        uintptr_t weight, long long N, int loss_id, float p0, float score_div, uintptr_t pred,
                        uintptr_t gh, uintptr_t loss_acc, uintptr_t ghmax, uintptr_t leaf_part, uintptr_t leaf_out,
                        uintptr_t scales, uintptr_t staging, uintptr_t work, uintptr_t root_slot, int B, int F,
-                       uintptr_t acc_out, uintptr_t acc2, int nblocks2, uintptr_t acc2_out, uintptr_t stream) {
+                       uintptr_t acc_out, uintptr_t acc2, int nblocks2, uintptr_t acc2_out, uintptr_t zero,
+                       long long zero_n, uintptr_t stream) {
+  // zero / zero_n (optional): a 16-byte aligned int64 range (the histogram slab) the kernel
+  // zeroes before the root reduce adds into it
   // acc_out (optional): where the loss sums go (default loss_acc[0:2]); acc2 / nblocks2 /
   // acc2_out (optional): another pass's partials (the test-set tail) finished by the same
   // launch -- the round's sums then sit next to each other for one readback copy
@@ -1075,6 +1088,8 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
   const size_t lds = kTGHHistBytes + (size_t)nnodes * 5 * sizeof(int) +
                      (leaf_part ? (size_t)kTGHVirtual * nnodes * sizeof(int) : 0);
   if (lds > kLdsBudget) return 0;
+  if (zero && (zero % 16) != 0) return 0;
+  if (zero_n <= 0) zero = 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nvb = grid_for(N, 256 * 8);  // tree_grad_kernel's grid: the virtual blocks
   const int grid = (nvb + kTGHVirtual - 1) / kTGHVirtual;
@@ -1083,7 +1098,8 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
                      stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft, (const int*)tright,         \
                      (const float*)tval, nnodes, (float*)score, (const float*)init, (const float*)label,         \
                      (const float*)weight, N, p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc,       \
-                     (float*)ghmax, (int*)leaf_part, nvb, (const float*)scales, (long long*)staging, B)
+                     (float*)ghmax, (int*)leaf_part, nvb, (const float*)scales, (long long*)staging, B,    \
+                     (unsigned long long*)zero, zero_n)
   switch (loss_id) {
     case 0: YTK_TGH(0); break;
     case 1: YTK_TGH(1); break;

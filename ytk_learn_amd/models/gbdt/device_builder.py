@@ -238,6 +238,9 @@ class DeviceLevelBuilder:
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
         self._slab_zeroed = False  # the whole slab was zeroed at the end of the previous tree
+        # YTK_ZERO_AT_END=1: zero the slab with a fill launch at the end of each tree (instead of
+        # in the next gradient pass)
+        self._zero_at_end = os.environ.get("YTK_ZERO_AT_END") == "1"
         self._raw_req = None       # test-set raw tree written by the tree tail (set_raw_request)
         self._raw_ready = False
         # True: each tree's snapshot is a copy (K trees per round need their own); the
@@ -656,10 +659,12 @@ class DeviceLevelBuilder:
                   ptr(ro["nleft"]) if rq else 0, ptr(ro["nright"]) if rq else 0, ptr(ro["ndefl"]) if rq else 0,
                   ptr(ro["nval"]) if rq else 0, s)
         self._raw_ready = rq is not None
-        self._slab_zeroed = False
-        if self.fuse_root:
-            # the next gradient pass accumulates the next root into slot 0; zero the whole slab
-            # now (one fill instead of slot 0 here + slots 1.. at the next tree's start)
+        # fuse_root: the next gradient pass (tree_grad_hist, root_target()'s zero range) zeroes
+        # the whole slab (small slabs) or slot 0 before it accumulates the next root into slot
+        # 0 -- no fill launch here. When that pass does not run fused (root_ready stays False),
+        # the next build's root histogram zeroes the slab itself.
+        self._slab_zeroed = self.fuse_root and self._zero_all and not self._zero_at_end
+        if self.fuse_root and self._zero_at_end:
             if self._zero_all:
                 self.hist.zero_()
                 self._slab_zeroed = True
@@ -694,8 +699,9 @@ class DeviceLevelBuilder:
             self._root_bufs = (torch.empty(grid * 256 * 32 * 2, dtype=torch.int64, device=self.dev),
                                torch.zeros(4 * grid, dtype=torch.int32, device=self.dev))
         stg, work = self._root_bufs
+        zero_n = 0 if self._zero_at_end else (self.hist.numel() if self._zero_all else self.hist[0].numel())
         return {"slot": ptr(self.hist), "scales": ptr(self.scales), "staging": ptr(stg), "work": ptr(work),
-                "B": self.B, "F": self.F}
+                "B": self.B, "F": self.F, "zero": ptr(self.hist) if zero_n else 0, "zero_n": zero_n}
 
     def live_tree_views(self):
         """(node table, leaf-value array) the engine's raw_tree / next snapshot read."""

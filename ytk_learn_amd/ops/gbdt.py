@@ -672,7 +672,8 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
                     ptr(ghmax), ptr(part), ptr(leaf_counts), root["scales"], root["staging"], root["work"],
                     root["slot"], root["B"], root["F"], ptr(acc_out),
                     ptr(te_acc[0]) if te_acc is not None else 0, int(te_acc[1]) if te_acc is not None else 0,
-                    ptr(te_acc[2]) if te_acc is not None else 0, stream(score)))
+                    ptr(te_acc[2]) if te_acc is not None else 0, root.get("zero", 0), root.get("zero_n", 0),
+                    stream(score)))
             if root["done"]:
                 return acc_out if acc_out is not None else acc[:2]
         ok = hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
