@@ -156,6 +156,7 @@ class DeviceLeafBuilder:
         self.staged = True
         self.fuse_root = False
         self.root_ready = False
+        self._zero_at_end = os.environ.get("YTK_ZERO_AT_END") == "1"  # as DeviceLevelBuilder
         self._root_bufs = None
         self._root_glob = None
 
@@ -434,8 +435,9 @@ class DeviceLeafBuilder:
             self._root_bufs = (torch.empty(grid * 256 * 32 * 2, dtype=torch.int64, device=self.dev),
                                torch.zeros(4 * grid, dtype=torch.int32, device=self.dev))
         stg, work = self._root_bufs
+        zero_n = 0 if self._zero_at_end else self.hist[0].numel()
         return {"slot": ptr(self.hist), "scales": ptr(self.scales), "staging": ptr(stg), "work": ptr(work),
-                "B": self.B, "F": self.F}
+                "B": self.B, "F": self.F, "zero": ptr(self.hist) if zero_n else 0, "zero_n": zero_n}
 
     def _finish(self, h, s, it) -> DeviceTree:
         self.timer.mark("batches")
@@ -448,8 +450,9 @@ class DeviceLeafBuilder:
                   ptr(ro["nleft"]) if rq else 0, ptr(ro["nright"]) if rq else 0, ptr(ro["ndefl"]) if rq else 0,
                   ptr(ro["nval"]) if rq else 0, s)
         self._raw_ready = rq is not None
-        if self.fuse_root:
+        if self.fuse_root and self._zero_at_end:
             self.hist[0].zero_()  # the next gradient pass accumulates the next root here
+        # (default: that pass zeroes slot 0 itself, root_target()'s zero range)
         self.tree_count += 1
         self.last_batches = it
         # K > 1 rounds build several trees before their arrays are consumed: copies; a K == 1
