@@ -142,3 +142,29 @@ def test_lbfgs_two_loop_matches_explicit_bfgs(seed, m, extra):
     p = torch.from_numpy(v.copy())
     opt.hv(p, cursor, loops, ys, yy)
     np.testing.assert_allclose(p.numpy(), H @ v, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_slot_sums_gpu_matches_bincount_and_cpu_auc():
+    """The evaluators' GPU slot sums (sort + segmented sums) == torch.bincount on the CPU;
+    AUC and the confusion matrix on the GPU == the CPU evaluators."""
+    from ytk_learn_amd.metrics.evaluators import ConfusionMatrixEvaluator, slot_sums
+    g = np.random.default_rng(5)
+    n, S = 200_000, 1000
+    p = 1.0 / (1.0 + np.exp(-g.normal(size=n) * 0.7))
+    y = (g.random(n) < p).astype(np.float32)
+    w = g.uniform(0.5, 2.0, n)
+    slot = torch.from_numpy((np.minimum((p * S).astype(np.int64), S - 1) * 2 + (y != 1.0)).astype(np.int64))
+    ref = torch.stack([torch.bincount(slot, weights=torch.from_numpy(w), minlength=2 * S),
+                       torch.bincount(slot, minlength=2 * S).double()])
+    got = slot_sums(slot.cuda(), torch.from_numpy(w).cuda(), 2 * S).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-12, atol=1e-9)
+    assert slot_sums(slot[:0].cuda(), torch.from_numpy(w[:0]).cuda(), 8).abs().sum() == 0
+    pt, yt, wt = torch.from_numpy(p.astype(np.float32)), torch.from_numpy(y), torch.from_numpy(w)
+    ev = AucEvaluator(f"auc@{S}")
+    cpu = ev.compute(yt, pt, wt, Comm.local())
+    gpu = ev.compute(yt.cuda(), pt.cuda(), wt.cuda(), Comm.local())
+    assert gpu == pytest.approx(cpu, rel=1e-12)
+    cm = ConfusionMatrixEvaluator("confusion_matrix")
+    torch.testing.assert_close(cm.matrix(yt.cuda(), pt.cuda(), wt.cuda(), Comm.local(), 2, False),
+                               cm.matrix(yt, pt, wt, Comm.local(), 2, False), rtol=1e-12, atol=1e-9)

@@ -6,7 +6,8 @@ ties), ``J/eval/ConfusionMatrixEvaluator.java:80-212``,
 ``J/eval/PointWiseEvaluator.java:51-89``, ``J/eval/EvaluatorFactory.java:52-64``
 (accepted names: auc[@...], rmse, mae, confusion_matrix[@thr]).
 
-The histograms are built on the data's device (torch.bincount on HBM) and the
+The histograms are built on the data's device (``slot_sums``: sort + segmented sums on
+the GPU, deterministic and free of hot-slot atomics; torch.bincount on the CPU) and the
 all-reduce is one collective per evaluator (weighted+unweighted stacked).
 Output strings keep the reference's log grammar (users grep them).
 """
@@ -25,6 +26,27 @@ def _jd(x: float) -> str:
     """Java String.valueOf(double)."""
     from ..utils.javafmt import java_double_str
     return java_double_str(x)
+
+
+def slot_sums(slot: torch.Tensor, w: torch.Tensor, n: int) -> torch.Tensor:
+    """float64 [2, n]: per-slot weight sums and row counts of int64 ``slot`` in [0, n).
+
+    On the GPU: one sort of the slot ids, then segmented sums over the runs of equal ids
+    (torch.segment_reduce) scattered to their slots. torch.bincount's fp64 atomics pile onto
+    the few slots clustered predictions fall into (and their order varies run to run); the
+    sorted sums take the same order every run."""
+    if not slot.is_cuda:
+        return torch.stack([torch.bincount(slot, weights=w, minlength=n), torch.bincount(slot, minlength=n).double()])
+    h = torch.zeros((2, n), dtype=torch.float64, device=slot.device)
+    if slot.numel() == 0:
+        return h
+    key = slot.to(torch.int32) if n < 2 ** 31 else slot
+    s, order = torch.sort(key)
+    ids, counts = torch.unique_consecutive(s, return_counts=True)
+    ids = ids.long()
+    h[0, ids] = torch.segment_reduce(w[order], "sum", lengths=counts)
+    h[1, ids] = counts.double()
+    return h
 
 
 class Evaluator:
@@ -53,8 +75,7 @@ class AucEvaluator(Evaluator):
         pos = yy == 1.0
         slot = idx * 2 + (~pos).to(torch.int64)
         ww = w.double() if w is not None else torch.ones_like(p, dtype=torch.float64)
-        h = torch.stack([torch.bincount(slot, weights=ww, minlength=2 * S),
-                         torch.bincount(slot, minlength=2 * S).double()])
+        h = slot_sums(slot, ww, 2 * S)
         if comm.is_dist:
             comm.allreduce_(h)
         res = []
@@ -118,8 +139,7 @@ class ConfusionMatrixEvaluator(Evaluator):
             pr = (p >= self.thr).to(torch.int64)
         cell = (target * K + pr).clamp(0, K * K - 1)
         ww = w.double() if w is not None else torch.ones(cell.shape[0], dtype=torch.float64, device=cell.device)
-        m = torch.stack([torch.bincount(cell, weights=ww, minlength=K * K),
-                         torch.bincount(cell, minlength=K * K).double()])
+        m = slot_sums(cell, ww, K * K)
         if comm.is_dist:
             comm.allreduce_(m)
         return m.cpu().view(2, K, K)
