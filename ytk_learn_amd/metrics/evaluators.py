@@ -18,6 +18,7 @@ from typing import List, Optional
 import torch
 
 from ..parallel.comm import Comm
+from ..utils.segsum import slot_sums  # noqa: F401 (re-exported)
 
 AUC_SLOTS = 100000
 
@@ -26,27 +27,6 @@ def _jd(x: float) -> str:
     """Java String.valueOf(double)."""
     from ..utils.javafmt import java_double_str
     return java_double_str(x)
-
-
-def slot_sums(slot: torch.Tensor, w: torch.Tensor, n: int) -> torch.Tensor:
-    """float64 [2, n]: per-slot weight sums and row counts of int64 ``slot`` in [0, n).
-
-    On the GPU: one sort of the slot ids, then segmented sums over the runs of equal ids
-    (torch.segment_reduce) scattered to their slots. torch.bincount's fp64 atomics pile onto
-    the few slots clustered predictions fall into (and their order varies run to run); the
-    sorted sums take the same order every run."""
-    if not slot.is_cuda:
-        return torch.stack([torch.bincount(slot, weights=w, minlength=n), torch.bincount(slot, minlength=n).double()])
-    h = torch.zeros((2, n), dtype=torch.float64, device=slot.device)
-    if slot.numel() == 0:
-        return h
-    key = slot.to(torch.int32) if n < 2 ** 31 else slot
-    s, order = torch.sort(key)
-    ids, counts = torch.unique_consecutive(s, return_counts=True)
-    ids = ids.long()
-    h[0, ids] = torch.segment_reduce(w[order], "sum", lengths=counts)
-    h[1, ids] = counts.double()
-    return h
 
 
 class Evaluator:

@@ -64,7 +64,13 @@ def leaf_entries(leaf: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, n_nod
     E = first.numel()
     v = rv[first]
     le = lv[first]
-    wx = torch.zeros(E, dtype=torch.float64, device=dev).index_add_(0, eid, wv)
+    if resid.is_cuda:
+        # sorted runs: segmented sums (ties -- e.g. integer labels -- would pile fp64 atomics
+        # onto one entry, ~100x slower at 10M rows; see metrics/evaluators.py:slot_sums)
+        lens = torch.diff(first, append=torch.tensor([lv.numel()], dtype=first.dtype, device=dev))
+        wx = torch.segment_reduce(wv.double(), "sum", lengths=lens)
+    else:
+        wx = torch.zeros(E, dtype=torch.float64, device=dev).index_add_(0, eid, wv)
     seg = torch.searchsorted(le, torch.arange(n_nodes + 1, dtype=le.dtype, device=dev))
     cw = torch.cumsum(wx, 0)
     excl = cw - wx

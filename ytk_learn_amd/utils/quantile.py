@@ -132,12 +132,13 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
     groups). values / weights: float64 tensors, groups: int64 tensor in [0, G)."""
     import torch
 
+    from .segsum import slot_sums
     v = values.double().reshape(-1)
     w = weights.double().reshape(-1)
     g = groups.long().reshape(-1)
     G, K = int(n_groups), int(buckets)
     dev = v.device
-    W = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, g, w)
+    W = slot_sums(g, w, G)[0]
     lo = torch.full((G,), float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, g, v, "amin")
     hi = torch.full((G,), float("-inf"), dtype=torch.float64, device=dev).scatter_reduce(0, g, v, "amax")
     comm.allreduce_(W)
@@ -152,7 +153,8 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
     # landing in one bucket and ship every tied row to every rank
     resolved = np.full(G, np.nan)
     for _ in range(max_rounds):
-        cnt = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, g[alive], torch.ones_like(g[alive]))
+        ga = g[alive]
+        cnt = slot_sums(ga, torch.ones_like(ga, dtype=torch.float64), G)[1].to(torch.int64)
         comm.allreduce_(cnt)
         cnt_np = cnt.cpu().numpy()
         flat = (cnt_np > 0) & (hi_np <= lo_np) & np.isnan(resolved)
@@ -170,7 +172,7 @@ def distributed_weighted_median(values, weights, groups, n_groups: int, comm, bu
         lo_t = torch.from_numpy(lo_np).to(dev)
         wd_t = torch.from_numpy(width).to(dev)
         b = torch.floor((vi - lo_t[gi]) / wd_t[gi]).clamp_(0, K - 1).long()
-        hw = torch.zeros(G * K, dtype=torch.float64, device=dev).index_add_(0, gi * K + b, w[alive])
+        hw = slot_sums(gi * K + b, w[alive], G * K)[0]
         comm.allreduce_(hw)
         cum = below[:, None] + np.cumsum(hw.view(G, K).cpu().numpy(), axis=1)
         kstar = np.minimum(_first_reaching(cum, target), K - 1)
