@@ -1,6 +1,7 @@
 """Weighted mergeable quantile summary (native WQSummary) vs exact weighted quantiles."""
 import numpy as np
 import pytest
+import torch
 
 from ytk_learn_amd.utils import quantile as wq
 
@@ -90,3 +91,30 @@ def test_distributed_weighted_median_heavy_ties_resolve_without_gather():
         assert got[k] == _weighted_median_sorted(v[m][o], w[m][o])
     # the final survivor gather holds no tied bulk
     assert q.MEDIAN_STATS["gathered_local"] <= 16
+
+
+@pytest.mark.gpu
+def test_weighted_binning_gpu_matches_cpu():
+    """Weighted sample_by_quantile candidates (segmented run sums on the GPU) and the
+    quantile missing-value fill equal the CPU path, on tie-heavy columns."""
+    from ytk_learn_amd.models.gbdt import binning as bn
+    from ytk_learn_amd.parallel.comm import Comm
+    g = np.random.default_rng(11)
+    n = 300_000
+    X = np.stack([g.integers(0, 3, n).astype(np.float32),  # 3 distinct values
+                  np.round(g.normal(size=n), 2).astype(np.float32),
+                  g.normal(size=n).astype(np.float32)], 1)
+    X[g.random(n) < 0.05, 2] = np.nan
+    w = g.uniform(0.5, 2.0, n).astype(np.float32)
+    spec = bn.SamplerSpec(max_cnt=31, use_sample_weight=True)
+    Xc, wc = torch.from_numpy(X), torch.from_numpy(w)
+    for f in range(2):
+        cpu = bn.feature_candidates(Xc[:, f], wc, spec, Comm.local())
+        gpu = bn.feature_candidates(Xc[:, f].cuda(), wc.cuda(), spec, Comm.local())
+        np.testing.assert_array_equal(gpu, cpu)
+    bc = bn._quantile_candidates_batched(Xc[:, :2], wc, [spec, spec], [0, 1], Comm.local())
+    bg = bn._quantile_candidates_batched(Xc[:, :2].cuda(), wc.cuda(), [spec, spec], [0, 1], Comm.local())
+    for f in range(2):
+        np.testing.assert_array_equal(bg[f], bc[f])
+    np.testing.assert_array_equal(bn.compute_missing_fill(Xc.cuda(), wc.cuda(), "quantile@0.5", Comm.local()),
+                                  bn.compute_missing_fill(Xc, wc, "quantile@0.5", Comm.local()))

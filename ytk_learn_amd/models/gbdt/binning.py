@@ -23,6 +23,7 @@ import torch
 from ...ops import gbdt as gops
 from ...utils.errors import YtkLearnError
 from ...parallel.comm import Comm
+from ...utils.segsum import run_sums, slot_sums
 
 
 @dataclass
@@ -115,8 +116,7 @@ def feature_candidates(x: torch.Tensor, weight: Optional[torch.Tensor], spec: Sa
     xs, order = torch.sort(x)
     vals, inv, counts = torch.unique_consecutive(xs, return_inverse=True, return_counts=True)
     if spec.use_sample_weight and weight is not None:
-        wsum = torch.zeros(vals.numel(), dtype=torch.float64, device=x.device)
-        wsum.index_add_(0, inv, weight[order].double())
+        wsum = run_sums(weight[order], inv, counts)
     else:
         wsum = counts.double()
     wv = wsum.pow(spec.alpha)
@@ -155,8 +155,7 @@ def _quantile_candidates_batched(X: torch.Tensor, weight: Optional[torch.Tensor]
         xs, order = torch.sort(X[:, f].contiguous())
         vals, inv, counts = torch.unique_consecutive(xs, return_inverse=True, return_counts=True)
         if sp.use_sample_weight and weight is not None:
-            wsum = torch.zeros(vals.numel(), dtype=torch.float64, device=X.device)
-            wsum.index_add_(0, inv, weight[order].double())
+            wsum = run_sums(weight[order], inv, counts)
         else:
             wsum = counts.double()
         loc.append((vals.double(), wsum.pow(sp.alpha)))
@@ -305,7 +304,7 @@ def compute_missing_fill(X: torch.Tensor, weight: Optional[torch.Tensor], spec: 
         col = X[:, f]
         keep = ~torch.isnan(col)
         vals, inv = torch.unique(col[keep].double(), sorted=True, return_inverse=True)
-        ws = torch.zeros(vals.numel(), dtype=torch.float64, device=X.device).index_add_(0, inv, w[keep].double())
+        ws = slot_sums(inv, w[keep].double(), vals.numel())[0]
         local.append(wq.device_summary(vals, ws, 4096))
     parts = wq.allgather_summaries(local, comm)
     for f in range(F):

@@ -29,3 +29,12 @@ def slot_sums(slot: torch.Tensor, w: torch.Tensor, n: int) -> torch.Tensor:
     h[0, ids] = torch.segment_reduce(w[order], "sum", lengths=counts)
     h[1, ids] = counts.double()
     return h
+
+
+def run_sums(w_sorted: torch.Tensor, inv: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    """float64 sums of ``w_sorted`` over its runs (run k = ``counts[k]`` consecutive rows;
+    ``inv`` the run id of every row): segmented sums on the GPU, index_add_ on the CPU."""
+    w = w_sorted.double()
+    if w.is_cuda:
+        return torch.segment_reduce(w, "sum", lengths=counts)
+    return torch.zeros(counts.numel(), dtype=torch.float64).index_add_(0, inv, w)
