@@ -61,6 +61,45 @@ __global__ __launch_bounds__(256) void dot_final_kernel(const double* __restrict
   if (threadIdx.x == 0) *out = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+// p <- (p + alpha * x) * scale, and the partial sums of d . p_new (the two-loop recursion's
+// next dot product) in the same pass: 4 instead of 5 vector streams per step. fp32 update
+// in torch's order (add, then scale); fp64 dot accumulation as dot_partial_kernel.
+__global__ __launch_bounds__(256) void axpy_dot_partial_kernel(float* __restrict__ p, const float* __restrict__ x,
+                                                               float alpha, float scale, const float* __restrict__ d,
+                                                               long long n, int vec, double* __restrict__ part) {
+  double acc = 0.0;
+  const long long tid = blockIdx.x * 256LL + threadIdx.x, nth = (long long)gridDim.x * 256;
+  long long tail = 0;
+  auto upd = [&](float pv, float xv) { return (pv + alpha * xv) * scale; };
+  if (vec) {
+    const long long n4 = n >> 2;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* d4 = reinterpret_cast<const float4*>(d);
+    // (a 2x unrolled variant, both groups loaded before either store: 12.7 -> 13.9 ms for
+    // the 12-pair two-loop at 161M, profiles/r3s4_fused_two_loop_ab/)
+    long long i = tid;
+    for (; i < n4; i += nth) {
+      const float4 a = p4[i], b = x4[i], c = d4[i];
+      float4 r;
+      r.x = upd(a.x, b.x); r.y = upd(a.y, b.y); r.z = upd(a.z, b.z); r.w = upd(a.w, b.w);
+      p4[i] = r;
+      acc += (double)c.x * r.x + (double)c.y * r.y + (double)c.z * r.z + (double)c.w * r.w;
+    }
+    tail = n4 << 2;
+  }
+  for (long long i = tail + tid; i < n; i += nth) {
+    const float r = upd(p[i], x[i]);
+    p[i] = r;
+    acc += (double)d[i] * r;
+  }
+  __shared__ double s[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -84,6 +123,19 @@ void ytk_dot(uintptr_t a, uintptr_t b, long long n, int mode, uintptr_t part, ui
   }
   hipLaunchKernelGGL(dot_final_kernel, dim3(1), dim3(256), 0, s, (const double*)part, nb,
                      (double*)out);
+  YTK_LAUNCH_CHECK();
+}
+
+// p <- (p + alpha * x) * scale; *out (fp64, device) = d . p_new. part: >= 1024 doubles.
+void ytk_axpy_dot(uintptr_t p, uintptr_t x, float alpha, float scale, uintptr_t d, long long n, uintptr_t part,
+                  uintptr_t out, uintptr_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int vec = ((p | x | d) & 15) == 0;
+  long long want = (n / 4 + 255) / 256;
+  const int nb = (int)std::max<long long>(1, std::min<long long>(kDotBlocks, want));
+  hipLaunchKernelGGL(axpy_dot_partial_kernel, dim3(nb), dim3(256), 0, s, (float*)p, (const float*)x, alpha, scale,
+                     (const float*)d, n, vec, (double*)part);
+  hipLaunchKernelGGL(dot_final_kernel, dim3(1), dim3(256), 0, s, (const double*)part, nb, (double*)out);
   YTK_LAUNCH_CHECK();
 }
 

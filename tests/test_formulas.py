@@ -168,3 +168,29 @@ def test_slot_sums_gpu_matches_bincount_and_cpu_auc():
     cm = ConfusionMatrixEvaluator("confusion_matrix")
     torch.testing.assert_close(cm.matrix(yt.cuda(), pt.cuda(), wt.cuda(), Comm.local(), 2, False),
                                cm.matrix(yt, pt, wt, Comm.local(), 2, False), rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,loops,cursor", [(5, 5, 0), (6, 3, 2), (4, 1, 1)])
+def test_fused_two_loop_matches_unfused(monkeypatch, m, loops, cursor):
+    """The GPU two-loop with every update fused with the next dot (blas.axpy_dot) == the
+    unfused dot / axpy sequence (fp32 vectors, fp64 dots; tails off the 16-B path)."""
+    from types import SimpleNamespace
+
+    from ytk_learn_amd.optim.lbfgs import HoagOptimizer
+    g = torch.Generator(device="cuda").manual_seed(m * 10 + loops)
+    d = 100_003
+    opt = HoagOptimizer.__new__(HoagOptimizer)
+    opt.ls = SimpleNamespace(m=m)
+    opt.S = [torch.randn(d, device="cuda", generator=g) for _ in range(m)]
+    opt.Y = [s + 0.3 * torch.randn(d, device="cuda", generator=g) for s in opt.S]
+    opt.YS = [float(torch.dot(s.double(), y.double())) for s, y in zip(opt.S, opt.Y)]
+    p0 = torch.randn(d, device="cuda", generator=g)
+    monkeypatch.setenv("YTK_FUSED_TWO_LOOP", "0")
+    ref = p0.clone()
+    opt.hv(ref, cursor, loops, 2.0, 3.0)
+    monkeypatch.setenv("YTK_FUSED_TWO_LOOP", "1")
+    got = p0.clone()
+    assert opt._fused_two_loop(got)
+    opt.hv(got, cursor, loops, 2.0, 3.0)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)

@@ -56,3 +56,22 @@ def sum_sq(a: torch.Tensor) -> float:
 
 def sum_abs(a: torch.Tensor) -> float:
     return _reduce(a, None, 2)
+
+
+def axpy_dot(p: torch.Tensor, x: torch.Tensor, alpha: float, scale: float, d: torch.Tensor) -> float:
+    """p <- (p + alpha x) * scale in place (fp32, torch's add-then-scale order), returning
+    d . p_new accumulated in fp64 -- one pass over the four vectors (the two-loop
+    recursion's update + next dot product). GPU float32 contiguous operands."""
+    if p.device.type != "cuda":
+        p.add_(x, alpha=alpha)
+        if scale != 1.0:
+            p.mul_(scale)
+        return float(torch.dot(p.reshape(-1).double(), d.reshape(-1).double()))
+    for t in (p, x, d):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != p.numel():
+            raise TypeError("axpy_dot: contiguous float32 operands of one size expected")
+    check_cuda(p, x, d)
+    buf = _buffers(p.device)
+    hip().axpy_dot(ptr(p), ptr(x), float(alpha), float(scale), ptr(d), p.numel(), ptr(buf), ptr(buf[1024:]),
+                   stream(p))
+    return float(buf[1024])

@@ -21,6 +21,7 @@ rank because the all-reduced gradient is.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -244,6 +245,9 @@ class HoagOptimizer:
     def hv(self, p: torch.Tensor, cursor: int, loops: int, ys: float, yy: float):
         """p <- H p with the last ``loops`` pairs ending before ``cursor`` (Hv, :904-929)."""
         m = self.ls.m
+        if loops > 0 and self._fused_two_loop(p):
+            self._hv_fused(p, cursor, loops, ys, yy)
+            return
         alphas = [0.0] * m
         c = cursor
         for _ in range(loops):
@@ -256,6 +260,34 @@ class HoagOptimizer:
             b = _dot(self.Y[c], p) / self.YS[c]
             p.add_(self.S[c], alpha=alphas[c] - b)
             c = (c + 1) % m
+
+    def _fused_two_loop(self, p: torch.Tensor) -> bool:
+        # YTK_FUSED_TWO_LOOP=0: the unfused dot / axpy sequence
+        return (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                and os.environ.get("YTK_FUSED_TWO_LOOP", "1") != "0")
+
+    def _hv_fused(self, p: torch.Tensor, cursor: int, loops: int, ys: float, yy: float):
+        """hv with every update fused with the next dot product (blas.axpy_dot): the same
+        recursion, one pass over (p, update vector, next dot operand) per step."""
+        m = self.ls.m
+        alphas = [0.0] * m
+        c = (cursor + m - 1) % m
+        a = _dot(self.S[c], p) / self.YS[c]
+        for k in range(loops):
+            alphas[c] = a
+            if k + 1 < loops:  # p -= a Y[c]; next: S[c - 1] . p
+                nc = (c + m - 1) % m
+                a = blas.axpy_dot(p, self.Y[c], -a, 1.0, self.S[nc]) / self.YS[nc]
+                c = nc
+            else:  # p = (p - a Y[c]) * ys / yy; the second loop starts at this c: Y[c] . p
+                b = blas.axpy_dot(p, self.Y[c], -a, ys / yy, self.Y[c]) / self.YS[c]
+        for k in range(loops):
+            if k + 1 < loops:  # p += (alpha - b) S[c]; next: Y[c + 1] . p
+                nc = (c + 1) % m
+                b_next = blas.axpy_dot(p, self.S[c], alphas[c] - b, 1.0, self.Y[nc]) / self.YS[nc]
+                c, b = nc, b_next
+            else:
+                p.add_(self.S[c], alpha=alphas[c] - b)
 
     # ------------------------------------------------------------------ grid setup
     def _grid_points(self):
