@@ -40,10 +40,11 @@ import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from ytk_learn_amd.data.synthetic import higgs_like  # noqa: E402
+from ytk_learn_amd.data.synthetic import higgs_like_rows  # noqa: E402
 from ytk_learn_amd.models.gbdt.builder import TreeParams  # noqa: E402
 from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer  # noqa: E402
 from ytk_learn_amd.parallel.comm import Comm  # noqa: E402
+from ytk_learn_amd.utils.fault import fault_point  # noqa: E402
 from ytk_learn_amd.utils.logging import YtkLogger  # noqa: E402
 
 BASELINE_SEC_PER_TREE = 1.136  # ytk-learn 567.83 s / 500 trees (docs/gbdt_experiments.md:104)
@@ -61,6 +62,7 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
     comm.reset_stats()
     t0 = time.perf_counter()
     for i in range(warmup, warmup + steps):
+        fault_point("bench", i, comm.rank)  # YTK_FAULT_INJECT=bench:<rank>:<round>:stall (tests)
         tr.run_round(i)
     tr.materialize()  # the last round's trees and losses land inside the timed region
     if dev.type == "cuda":
@@ -71,6 +73,14 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
     el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
     comm.stats = timed_stats  # the timed rounds' collectives only
     return el
+
+
+def _transport(comm, builder) -> str:
+    if not comm.is_dist:
+        return "none"
+    if getattr(builder, "peer", None) is not None:
+        return "peer"
+    return dist.get_backend(comm.group) if comm.group is not None else "none"
 
 
 def main():
@@ -92,21 +102,30 @@ def main():
                     help="extra timed leaf-wise 255-leaf rounds on the same data (default 10)")
     a = ap.parse_args()
 
-    comm = Comm.from_env(device=a.device)
+    # a stuck rank must fail the job well inside the driver's bench timeout: every collective
+    # (and peer-exchange flag wait) times out after YTK_COMM_TIMEOUT seconds (default 120)
+    os.environ.setdefault("YTK_PEER_TIMEOUT_S", os.environ.get("YTK_COMM_TIMEOUT", "120"))
+    comm = Comm.from_env(device=a.device, timeout_s=120)
+    try:
+        run(a, comm)
+    except BaseException as e:  # noqa: BLE001 -- report, then exit non-zero (never re-exec)
+        print(f"[bench] rank {comm.rank} failed: {type(e).__name__}: {e}; last collective issued: "
+              f"{comm.last_op}", file=sys.stderr, flush=True)
+        os._exit(1)
+    comm.close()
+
+
+def run(a, comm):
     dev = comm.device
     world, rank = comm.world, comm.rank
     if world != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
-    # strong scaling: shard the fixed global row count
-    def shard(n):
-        base, rem = divmod(n, world)
-        return base + (1 if rank < rem else 0)
-
-    n_tr, n_te = shard(a.train_rows), shard(a.test_rows)
+    # strong scaling: ONE global dataset (chunk-seeded), rank r keeps rows
+    # [r * n / N, (r + 1) * n / N) -- every N trains and tests on the same rows
     t0 = time.perf_counter()
-    X, y = higgs_like(n_tr, seed=a.seed * 1000 + rank, device=dev)
-    Xt, yt = higgs_like(n_te, seed=a.seed * 1000 + 500 + rank, device=dev)
+    X, y = higgs_like_rows(a.train_rows, *comm.shard_range(a.train_rows), seed=a.seed * 1000, device=dev)
+    Xt, yt = higgs_like_rows(a.test_rows, *comm.shard_range(a.test_rows), seed=a.seed * 1000 + 500, device=dev)
     gen_s = time.perf_counter() - t0
 
     tp = TreeParams(max_depth=a.depth if a.policy == "level" else -1, max_leaf_cnt=a.leaves,
@@ -133,11 +152,15 @@ def main():
 
     el_max = timed_rounds(tr, comm, dev, a.warmup, a.steps)
     assert len(tr.model.trees) == total_rounds, "every timed tree must be a converted host tree"
-    # quality check after the timed rounds (outside timing)
+    coll = dict(comm.stats)
+    replays = tr._graphs["n"] if isinstance(tr._graphs, dict) else 0
+    # quality check after the timed rounds (outside timing): losses and AUC over the GLOBAL
+    # train / test rows (the evaluators all-reduce their bucket histograms)
     auc = tr.eval_test.evals[0].compute(yt, tr.te_pred, None, comm)[0]
+    train_auc = tr.eval_train.evals[0].compute(y, tr.pred, None, comm)[0]
     train_loss, test_loss = tr.round_losses[total_rounds - 1]
     sec_per_tree = el_max / a.steps
-    coll = dict(comm.stats)
+    transport = _transport(comm, tr.builder)
     if a.profile and rank == 0:
         print(tr.timer.report() if tr.use_device_builder else tr.builder.total_stats, file=sys.stderr)
     if rank == 0 and hasattr(tr.builder, "prof_report") and os.environ.get("YTK_LW_PROF") == "1":
@@ -145,7 +168,8 @@ def main():
               file=sys.stderr)
     tr_builder = tr.builder
     leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else 10
-    leaf = None
+    leaf = leaf_transport = None
+    tr.close()
     if leaf_steps > 0 and a.policy == "level":
         del tr
         tpl = TreeParams(max_depth=-1, max_leaf_cnt=255, min_child_hessian_sum=100.0, min_split_loss=0.0,
@@ -157,6 +181,8 @@ def main():
         trl.init_gradients()
         leaf = timed_rounds(trl, comm, dev, 3, leaf_steps) / leaf_steps
         assert len(trl.model.trees) == 3 + leaf_steps
+        leaf_transport = _transport(comm, trl.builder)
+        trl.close()
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -183,21 +209,26 @@ def main():
             },
             "train_loss": round(float(train_loss), 6),
             "test_loss": round(float(test_loss), 6),
+            "train_auc": round(float(train_auc), 6),
             "test_auc": round(float(auc), 6),
+            "quality_on": "global train / test rows (identical data at every N)",
             "prep_s": round(prep_s, 3),
             "datagen_s": round(gen_s, 3),
             "timed_region": "step + convertModel + per-round loss readback (pipelined), all trees landed",
             "collectives_per_tree": round(coll["calls"] / a.steps, 2),
             "collective_bytes_per_tree": int(coll["bytes"] / a.steps),
-            "hist_sync": ("owner" if getattr(tr_builder, "owner", False) else "allreduce") if world > 1 else "none",
+            "hist_sync": (("owner" if getattr(tr_builder, "owner", False) else "allreduce")
+                          if comm.is_dist else "none"),
+            "hist_transport": transport,
+            "graph_replays": replays,
             "trees_converted": total_rounds,
         }
         if leaf is not None:
             res["leafwise_s_per_tree"] = round(leaf, 6)
             res["leafwise_vs_reference"] = round(leaf / BASELINE_SEC_PER_TREE, 6)
             res["leafwise_rounds_timed"] = leaf_steps
+            res["leafwise_transport"] = leaf_transport
         print(json.dumps(res), flush=True)
-    comm.close()
 
 
 if __name__ == "__main__":

@@ -127,8 +127,9 @@ void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, u
 void ytk_lw_msg(int, uintptr_t, long long, uintptr_t, int, int, uintptr_t);
 int ytk_peer_create(int, int, long long, uintptr_t);
 void ytk_peer_open(int, uintptr_t);
-void ytk_peer_allreduce(int, uintptr_t, long long, long long, uintptr_t);
-uintptr_t ytk_peer_err(int);
+void ytk_peer_allreduce(int, uintptr_t, long long, int, double, uintptr_t);
+void ytk_peer_allreduce_slots(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
+                              double, uintptr_t);
 int ytk_peer_check(int);
 void ytk_peer_destroy(int);
 void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
@@ -261,7 +262,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("peer_create", &ytk_peer_create);
   m.def("peer_open", &ytk_peer_open);
   m.def("peer_allreduce", &ytk_peer_allreduce);
-  m.def("peer_err", &ytk_peer_err);
+  m.def("peer_allreduce_slots", &ytk_peer_allreduce_slots);
   m.def("peer_check", &ytk_peer_check);
   m.def("peer_destroy", &ytk_peer_destroy);
   m.def("lw_msg", &ytk_lw_msg);

@@ -97,91 +97,181 @@ void ytk_owner_unpack(uintptr_t out, uintptr_t hist, int nslots, int B, int F, i
 
 }  // extern "C"
 
-// ------------------------------------------------------------------ one-shot peer reduce
-// Latency-optimised histogram all-reduce over peer memory (xGMI), behind YTK_PEER_REDUCE=1.
-// RCCL stays the default until this path is measured on 8 GPUs.
+// ------------------------------------------------------------------ peer-memory exchange
+// Latency-optimised all-reduce of the tree engines' level / batch messages over peer memory
+// (xGMI), in ONE kernel per exchange and without the host: mp4j's histogram collectives were
+// latency-optimised recursive-halving / Rabenseifner algorithms (docs/gbdt_features.md:36,
+// 142-143; HistogramBuilder.java:95); at a 1/8 shard a level's build is 10-20 us, so the
+// exchange's latency sets the multi-GPU tree time.
 //
-// Each rank owns ONE uncached device allocation (hipDeviceMallocUncached: loads and stores
-// bypass every cache level, so data handed between processes never meets a stale L2 line on
-// any XCD) = [signal words | send slab | recv slab], exported with hipIpcGetMemHandle and
-// opened by every other rank. One all-reduce of n int64 (the level's histogram slots +
-// count words) is five launches on the compute stream, no host involvement:
-//   pack      local: send <- hist
-//   barrier   every rank stamps its epoch into every peer's signal word [rank] (system-scope
-//             release), then waits until all P words of its own signal array reach the epoch
-//   reduce    rank r sums chunk r of all P send slabs (exact int64, rank order) and stores the
-//             sum into chunk r of every rank's recv slab (two-shot: reduce-scatter by reads,
-//             all-gather by writes; each chunk has exactly one writer)
-//   barrier   (next epoch)
-//   unpack    local: hist <- recv
-// Barrier waits are bounded: a wait that outlives its budget raises an error word (checked by
-// the host) and exits, so a missing peer can never hang the GPU.
+// Every rank owns ONE uncached device allocation (hipDeviceMallocUncached: no cache level
+// holds its lines, so data handed between processes never meets a stale line on any XCD)
+//     [flag words: kPeerMax x kXchgGrid u64 | send slab 0 | send slab 1]
+// exported with hipIpcGetMemHandle and opened by every other rank. An exchange of n
+// elements (int64 histogram / count words, or fp64 loss sums) runs G blocks; block b owns
+// chunk b = [n*b/G, n*(b+1)/G) and
+//   1. copies its chunk of the message from the engine's buffer into this rank's send slab
+//      (slab parity = exchange epoch & 1), waits for its stores, releases at system scope
+//      and stamps the epoch into flag word [rank][b] of EVERY rank (remote stores);
+//   2. waits until its own flag words [q][b] of all P ranks reach the epoch;
+//   3. sums chunk b of all P send slabs in rank order (identical bits on every rank; int64
+//      sums are exact) and writes the sums back in place.
+// So the pack, both barriers of a two-shot all-reduce, the reduce and the unpack are one
+// launch, and a message can be described by device words (the leaf-wise batch: its built
+// slots + split cursors, counted by the planner) -- no host round trip per batch.
+//
+// Reuse of a send slab: exchange e writes slab e & 1, exchange e + 2 writes it again. Block
+// 0 takes part in every exchange, so during exchange e + 1 this rank saw a flag e + 1 of
+// every peer, stamped after that peer's exchange-e kernel (which read our slab) had
+// completed (stream order). Exchanges a rank skips (device-side skip word, e.g. the leaf-wise
+// batches queued after the tree finished) advance no epoch; the skip word is identical on
+// every rank because every rank takes the identical planning decisions.
+// The epoch lives in device memory (advanced by each exchange's last block), so a captured
+// HIP graph replays with fresh epochs. Waits are bounded in wall-clock time: a timed-out
+// wait sets the error word (host-mapped; checked where rounds land) and the kernel finishes,
+// and every later exchange of the group returns at once, so a lost peer never hangs the GPU.
 namespace ytk {
 constexpr int kPeerMax = 16;
-constexpr int kSigWords = 64;  // int64 signal words (one per rank, 512 B)
+constexpr int kXchgGrid = 64;      // max blocks of one exchange (flag words per rank)
+constexpr int kXchgThreads = 256;
 
 struct PeerPtrs {
-  long long* send[kPeerMax];
-  long long* recv[kPeerMax];
-  unsigned long long* sig[kPeerMax];
+  long long* send[kPeerMax][2];
+  unsigned long long* sig[kPeerMax];  // [kPeerMax][kXchgGrid] flag words of each rank
 };
 
-__global__ __launch_bounds__(64) void peer_barrier_kernel(PeerPtrs pp, int P, int rank, unsigned long long epoch,
-                                                          int* __restrict__ err, long long max_spins) {
-  const int t = threadIdx.x;
-  __threadfence_system();  // this rank's earlier stores (previous kernels) are visible first
-  if (t < P)
-    __hip_atomic_store(pp.sig[t] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (t < P) {
-    const unsigned long long* mine = pp.sig[rank] + t;
-    long long spins = 0;
-    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++spins > max_spins) {
-        atomicExch(err, 1);
-        break;
+// The message: contiguous (n >= 0: base[0..n)) or a leaf-wise batch (n < 0: the *nb_dev
+// slots listed in ids, slot_elems words each, then *k_dev * cur_stride cursor words).
+struct XchgMsg {
+  long long* base;
+  long long n;
+  long long* hist;
+  const int* ids;
+  const int* nb_dev;
+  const int* k_dev;
+  long long slot_elems;
+  long long* cursor;
+  int cur_stride;
+  const int* skip;  // non-null and non-zero: no exchange
+};
+
+__device__ __forceinline__ long long* xchg_elem(const XchgMsg& m, long long i, long long nh) {
+  if (m.n >= 0) return m.base + i;
+  if (i < nh) {
+    const long long kb = i / m.slot_elems;
+    return m.hist + (size_t)m.ids[kb] * m.slot_elems + (i - kb * m.slot_elems);
+  }
+  return m.cursor + (i - nh);
+}
+
+template <bool kF64>
+__global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, int P, int rank, XchgMsg m,
+                                                                 long long cap, unsigned long long* __restrict__ ctl,
+                                                                 int* __restrict__ err, long long timeout_ticks) {
+  if (m.skip != nullptr && *m.skip != 0) return;
+  // after a timed-out wait (ctl[2] != 0) every later exchange returns at once: the job is
+  // failing (the host check raises), so nothing waits again
+  __shared__ unsigned long long s_e;
+  const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+  long long n = m.n, nh = 0;
+  if (n < 0) {
+    nh = (long long)(*m.nb_dev) * m.slot_elems;
+    n = nh + (long long)(*m.k_dev) * m.cur_stride;
+  }
+  if (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  if (t == 0) s_e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const unsigned long long e = s_e;
+  if (n > cap) {  // identical on every rank: nobody exchanges, the host check raises
+    if (b == 0 && t == 0) atomicExch(err, 2);
+    n = 0;
+  }
+  const long long lo = n * b / G, hi = n * (b + 1) / G;
+  if (hi > lo || b == 0) {
+    const int par = (int)(e & 1ull);
+    long long* mine = pp.send[rank][par];
+    for (long long i = lo + t; i < hi; i += kXchgThreads) __builtin_nontemporal_store(*xchg_elem(m, i, nh), mine + i);
+    __builtin_amdgcn_s_waitcnt(0);  // this thread's slab stores are acknowledged
+    __syncthreads();
+    if (t == 0) __threadfence_system();
+    __syncthreads();
+    if (t < P)
+      __hip_atomic_store(pp.sig[t] + (size_t)rank * kXchgGrid + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < P) {
+      const unsigned long long* w = pp.sig[rank] + (size_t)t * kXchgGrid + b;
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((long long)(wall_clock64() - t0) > timeout_ticks) {
+          atomicExch(err, 1);
+          atomicExch(ctl + 2, 1ull);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) __threadfence_system();
+    __syncthreads();
+    for (long long i = lo + t; i < hi; i += kXchgThreads) {
+      if (kF64) {
+        double s = 0.0;
+        for (int q = 0; q < P; ++q) s += __longlong_as_double(__builtin_nontemporal_load(pp.send[q][par] + i));
+        *xchg_elem(m, i, nh) = __double_as_longlong(s);
+      } else {
+        long long s = 0;
+        for (int q = 0; q < P; ++q) s += __builtin_nontemporal_load(pp.send[q][par] + i);
+        *xchg_elem(m, i, nh) = s;
       }
     }
   }
-  __threadfence_system();
-}
-
-__global__ __launch_bounds__(256) void peer_copy_kernel(const long long* __restrict__ src, long long* __restrict__ dst,
-                                                        long long n) {
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) dst[i] = src[i];
-}
-
-__global__ __launch_bounds__(256) void peer_reduce_kernel(PeerPtrs pp, int P, int rank, long long n) {
-  const long long lo = n * rank / P, hi = n * (rank + 1) / P;
-  for (long long i = lo + blockIdx.x * 256LL + threadIdx.x; i < hi; i += (long long)gridDim.x * 256) {
-    long long s = 0;
-#pragma unroll 4
-    for (int q = 0; q < P; ++q) s += __builtin_nontemporal_load(pp.send[q] + i);
-    for (int q = 0; q < P; ++q) __builtin_nontemporal_store(s, pp.recv[q] + i);
+  // the last block to finish advances the epoch (the next exchange kernel starts after this
+  // one has completed, so every block of it reads the new value)
+  __syncthreads();
+  if (t == 0) {
+    const unsigned long long prev = atomicAdd(ctl + 1, 1ull);
+    if (prev == (unsigned long long)(G - 1)) {
+      __hip_atomic_store(ctl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
 struct PeerGroup {
   int P = 0, rank = 0;
-  long long cap = 0;  // int64 elements per slab
-  char* base = nullptr;  // own allocation
+  long long cap = 0;     // elements per send slab
+  char* base = nullptr;  // own uncached allocation
   std::vector<void*> opened;
   PeerPtrs pp{};
-  int* err = nullptr;  // device error word (fine to be ordinary device memory)
-  unsigned long long epoch = 0;
+  unsigned long long* ctl = nullptr;  // device: [0] last epoch, [1] block arrivals, [2] timed out
+  long long ticks_per_s = 100000000;  // wall_clock64 rate
+  int* err_host = nullptr;            // host-mapped error word
+  int* err = nullptr;                 // its device address
 };
 }  // namespace ytk
 static std::vector<ytk::PeerGroup> g_peer;
 namespace ytk {
 
-static size_t peer_bytes(long long cap) { return (size_t)kSigWords * 8 + 2 * (size_t)cap * 8; }
+static size_t peer_sig_bytes() { return (size_t)kPeerMax * kXchgGrid * 8; }
+static size_t peer_bytes(long long cap) { return peer_sig_bytes() + 2 * (size_t)cap * 8; }
+
+static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int f64, double timeout_s, hipStream_t s) {
+  grid = std::max(1, std::min(grid, kXchgGrid));
+  const long long ticks = (long long)(timeout_s * (double)g.ticks_per_s);
+  if (f64)
+    hipLaunchKernelGGL(peer_xchg_kernel<true>, dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap,
+                       g.ctl, g.err, ticks);
+  else
+    hipLaunchKernelGGL(peer_xchg_kernel<false>, dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap,
+                       g.ctl, g.err, ticks);
+  YTK_LAUNCH_CHECK();
+}
 
 }  // namespace ytk
 
 extern "C" {
 
-// Allocate this rank's uncached [signal | send | recv] block for slabs of cap int64; returns
-// a group handle. The exported IPC handle (64 bytes) goes to out_handle.
+// Allocate this rank's uncached [flags | send 0 | send 1] block for messages of up to cap
+// elements; returns a group handle. The exported IPC handle (64 bytes) goes to out_handle.
 int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   if (P < 1 || P > ytk::kPeerMax || rank < 0 || rank >= P || cap <= 0)
     throw std::invalid_argument("peer_create: bad group");
@@ -193,8 +283,17 @@ int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   YTK_HIP_CHECK(hipExtMallocWithFlags(&p, ytk::peer_bytes(cap), hipDeviceMallocUncached));
   YTK_HIP_CHECK(hipMemset(p, 0, ytk::peer_bytes(cap)));
   g.base = (char*)p;
-  YTK_HIP_CHECK(hipMalloc(&g.err, sizeof(int)));
-  YTK_HIP_CHECK(hipMemset(g.err, 0, sizeof(int)));
+  YTK_HIP_CHECK(hipMalloc(&g.ctl, 4 * sizeof(unsigned long long)));
+  YTK_HIP_CHECK(hipMemset(g.ctl, 0, 4 * sizeof(unsigned long long)));
+  int dev = 0, khz = 0;
+  YTK_HIP_CHECK(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+    g.ticks_per_s = (long long)khz * 1000;
+  YTK_HIP_CHECK(hipHostMalloc(&g.err_host, sizeof(int), hipHostMallocMapped));
+  *g.err_host = 0;
+  void* dp = nullptr;
+  YTK_HIP_CHECK(hipHostGetDevicePointer(&dp, g.err_host, 0));
+  g.err = (int*)dp;
   YTK_HIP_CHECK(hipDeviceSynchronize());
   hipIpcMemHandle_t h;
   YTK_HIP_CHECK(hipIpcGetMemHandle(&h, p));
@@ -220,36 +319,47 @@ void ytk_peer_open(int hnd, uintptr_t handles) {
       b = (char*)p;
     }
     g.pp.sig[q] = reinterpret_cast<unsigned long long*>(b);
-    g.pp.send[q] = reinterpret_cast<long long*>(b + ytk::kSigWords * 8);
-    g.pp.recv[q] = reinterpret_cast<long long*>(b + ytk::kSigWords * 8 + (size_t)g.cap * 8);
+    g.pp.send[q][0] = reinterpret_cast<long long*>(b + ytk::peer_sig_bytes());
+    g.pp.send[q][1] = reinterpret_cast<long long*>(b + ytk::peer_sig_bytes() + (size_t)g.cap * 8);
   }
 }
 
-// hist[0:n] <- the element-wise sum over the group's ranks (n <= cap int64), on `stream`.
-void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, long long max_spins, uintptr_t stream) {
+// data[0:n] <- the element-wise sum over the group's ranks (int64, or fp64 when f64), in
+// place, on `stream`: one kernel launch. n must be identical on every rank.
+void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int f64, double timeout_s, uintptr_t stream) {
   ytk::PeerGroup& g = g_peer.at(hnd);
   if (n <= 0) return;
   if (n > g.cap) throw std::invalid_argument("peer_allreduce: message larger than the slab");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int grid = (int)std::min<long long>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(ytk::peer_copy_kernel, dim3(grid), dim3(256), 0, s, (const long long*)data, g.pp.send[g.rank], n);
-  hipLaunchKernelGGL(ytk::peer_barrier_kernel, dim3(1), dim3(64), 0, s, g.pp, g.P, g.rank, ++g.epoch, g.err, max_spins);
-  const int rgrid = (int)std::min<long long>((n / g.P + 255) / 256 + 1, 1024);
-  hipLaunchKernelGGL(ytk::peer_reduce_kernel, dim3(rgrid), dim3(256), 0, s, g.pp, g.P, g.rank, n);
-  hipLaunchKernelGGL(ytk::peer_barrier_kernel, dim3(1), dim3(64), 0, s, g.pp, g.P, g.rank, ++g.epoch, g.err, max_spins);
-  hipLaunchKernelGGL(ytk::peer_copy_kernel, dim3(grid), dim3(256), 0, s, g.pp.recv[g.rank], (long long*)data, n);
-  YTK_LAUNCH_CHECK();
+  ytk::XchgMsg m{};
+  m.base = reinterpret_cast<long long*>(data);
+  m.n = n;
+  const int grid = (int)std::min<long long>((n + 2047) / 2048, ytk::kXchgGrid);
+  ytk::peer_launch(g, m, grid, f64, timeout_s, reinterpret_cast<hipStream_t>(stream));
 }
 
-// device address of the error word (non-zero: a barrier wait timed out)
-uintptr_t ytk_peer_err(int hnd) { return reinterpret_cast<uintptr_t>(g_peer.at(hnd).err); }
-
-// the error word, read after the device has drained (host check between trees)
-int ytk_peer_check(int hnd) {
-  int v = 0;
-  YTK_HIP_CHECK(hipMemcpy(&v, g_peer.at(hnd).err, sizeof(int), hipMemcpyDeviceToHost));
-  return v;
+// Leaf-wise batch message counted on the device: the *nb_dev built slots listed in ids
+// (slot_elems int64 each, at hist + ids[i] * slot_elems) and the first *k_dev * cur_stride
+// cursor words; skipped (no epoch) while *skip != 0. Fixed grid: one launch, no host wait.
+void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uintptr_t ids, uintptr_t nb_dev,
+                              uintptr_t cursor, uintptr_t k_dev, int cur_stride, uintptr_t skip, double timeout_s,
+                              uintptr_t stream) {
+  ytk::PeerGroup& g = g_peer.at(hnd);
+  ytk::XchgMsg m{};
+  m.n = -1;
+  m.hist = reinterpret_cast<long long*>(hist);
+  m.ids = reinterpret_cast<const int*>(ids);
+  m.nb_dev = reinterpret_cast<const int*>(nb_dev);
+  m.k_dev = reinterpret_cast<const int*>(k_dev);
+  m.slot_elems = slot_elems;
+  m.cursor = reinterpret_cast<long long*>(cursor);
+  m.cur_stride = cur_stride;
+  m.skip = reinterpret_cast<const int*>(skip);
+  ytk::peer_launch(g, m, ytk::kXchgGrid, 0, timeout_s, reinterpret_cast<hipStream_t>(stream));
 }
+
+// the host-mapped error word (1: a flag wait timed out, 2: a device-counted message exceeded
+// the slab); read after the device has drained past the exchanges
+int ytk_peer_check(int hnd) { return *(volatile int*)g_peer.at(hnd).err_host; }
 
 void ytk_peer_destroy(int hnd) {
   ytk::PeerGroup& g = g_peer.at(hnd);
@@ -258,7 +368,8 @@ void ytk_peer_destroy(int hnd) {
   for (void* p : g.opened) (void)hipIpcCloseMemHandle(p);
   g.opened.clear();
   (void)hipFree(g.base);
-  (void)hipFree(g.err);
+  (void)hipFree(g.ctl);
+  (void)hipHostFree(g.err_host);
   g.base = nullptr;
 }
 

@@ -48,6 +48,8 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
     peer = getattr(tr.builder, "peer", None)
     if peer is not None:
         peer.check()
+    peer_calls = peer.calls if peer is not None else 0
+    tr.close()
     if comm.log is not None:  # every rank's collective sequence (deadlock-freedom check)
         with open(os.path.join(out, f"comm_log_{comm.rank}.json"), "w") as f:
             json.dump(comm.log, f)
@@ -59,7 +61,7 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
             json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats,
                        "backend": backend, "is_dist": comm.is_dist,
                        "graph_replays": tr._graphs["n"] if isinstance(tr._graphs, dict) else 0,
-                       "peer_calls": peer.calls if peer is not None else 0}, f)
+                       "peer_calls": peer_calls}, f)
 
 
 def write_lines(path, n, seed):

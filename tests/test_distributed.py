@@ -142,25 +142,29 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
 @pytest.mark.parametrize("task,world,mode", [("gbdt", 2, "allreduce"), ("gbdt", 4, "allreduce"),
                                              ("gbdt_loss", 3, "allreduce"), ("gbdt", 3, "owner"),
                                              ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner"),
-                                             ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer")])
+                                             ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer"),
+                                             ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
     reduce-scatter by feature block + device split-record argmax) and the leaf-wise
     speculative builder (scattered slot all-reduce / reduce-scatter) must give the world-1
-    model byte for byte."""
+    model byte for byte. "peer": every level / batch message and the round vector go through
+    the one-kernel IPC peer-memory exchange (leaf-wise: sized on the device, no host wait per
+    batch); level-wise rounds are then graph-captured even over gloo, so the replays check
+    that the device-resident exchange epochs stay in step across graph replays."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": "allreduce" if mode == "peer" else mode,
-           "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0",
+           "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if mode == "peer" else "0",
            "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}  # small shards: keep the overlap covered
-    if mode == "peer":  # one-shot IPC peer-memory histogram all-reduce (the ranks share the GPU)
-        env["YTK_PEER_REDUCE"] = "1"
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     if mode == "peer":
         assert res["peer_calls"] > 0
+        if task == "gbdt" and world != 3:  # no feature sampling: graph-eligible rounds
+            assert res["graph_replays"] > 0
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
     _same_collective_sequence(tmp_path / f"w{world}", world)
 
@@ -191,7 +195,7 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_HIST_SYNC": mode, "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}
+    env = {"YTK_HIST_SYNC": mode, "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0", "YTK_PEER_REDUCE": "0"}
     if task == "gbdt" and mode == "allreduce":
         eager = _run(task, tmp_path / "eager", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1", YTK_GRAPH_DIST="0"))
         assert eager["graph_replays"] == 0
@@ -208,19 +212,43 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
 
 
 @pytest.mark.gpu
-def test_rccl_world1_capture_failure_falls_back(tmp_path):
-    """A round capture that fails (injected) is voted down and the job continues with eager
-    rounds -- same model, no graph replays, the captured collectives not counted."""
+@pytest.mark.parametrize("where", ["1", "2"])
+def test_rccl_world1_capture_failure_falls_back(tmp_path, where):
+    """A round capture that fails (injected after the capture, "1", or inside it with the
+    round's kernels and RCCL calls half captured, "2") is voted down and the job continues
+    with eager rounds -- same model, no graph replays, the captured collectives not counted."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_HIST_SYNC": "allreduce", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}
+    env = {"YTK_HIST_SYNC": "allreduce", "YTK_HIST_OVERLAP_MIN_ROWS": "0", "YTK_PEER_REDUCE": "0"}
     _run("gbdt", tmp_path / "plain", 1, "cuda", extra_env=env)
     good = _run("gbdt", tmp_path / "graph", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
-    bad = _run("gbdt", tmp_path / "fail", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1", YTK_FAULT_CAPTURE="1"))
+    bad = _run("gbdt", tmp_path / "fail", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1", YTK_FAULT_CAPTURE=where))
     assert good["graph_replays"] > 0 and bad["graph_replays"] == 0
     assert bad["comm"]["calls"] == good["comm"]["calls"]  # eager rounds issue what replays count
     assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "fail" / "model.txt").read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task", ["gbdt", "gbdt_loss"])
+def test_peer_world1_forced_dist(tmp_path, task):
+    """YTK_FORCE_DIST=1 on the nccl backend with the default (single-node) peer path: every
+    level / batch message and the round vector is one peer exchange kernel, level-wise rounds
+    replay as graphs, and the model equals the plain world-1 run byte for byte. Level-wise:
+    one exchange per built level plus the round vector, no RCCL call per round."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_HIST_SYNC": "allreduce", "YTK_COMM_LOG": "1"}
+    _run(task, tmp_path / "plain", 1, "cuda", extra_env=env)
+    res = _run(task, tmp_path / "peer", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
+    assert res["is_dist"] and res["backend"] == "nccl" and res["peer_calls"] > 0
+    if task == "gbdt":
+        assert res["graph_replays"] > 0
+        # the captured round: its level messages + round vector are peer exchanges only
+        log = json.load(open(tmp_path / "peer" / "comm_log_0.json"))
+        assert sum(1 for op, _, _ in log if op == "peer_allreduce") >= 5
+    assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "peer" / "model.txt").read()
 
 
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
@@ -250,3 +278,51 @@ def test_bench_under_torchrun_world2(tmp_path, mode):
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["steps"] == 2
     assert res["collectives_per_tree"] > 0 and res["collective_bytes_per_tree"] > 0
     assert res["hist_sync"] == mode and res["trees_converted"] == 3
+
+
+def _bench(world, extra_args=(), env_extra=None, timeout=600):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **(env_extra or {}))
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "1", "--device", "cpu",
+            "--train-rows", "12000", "--test-rows", "3000", "--depth", "4", "--quiet", "--leafwise-steps", "0",
+            *extra_args]
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _bench_json(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_global_rows_match_world1(world):
+    """Every rank generates the same global data and keeps its contiguous row slice, so the
+    world-N bench trains on the world-1 rows: losses agree to 1e-3 and AUCs to 3e-3 (the
+    quantile sketches merged over ranks may move a bin candidate; 12k rows), and the JSON
+    line names the sync mode."""
+    r1 = _bench_json(_bench(1))
+    rn = _bench_json(_bench(world))
+    assert r1["hist_sync"] == "none" and r1["hist_transport"] == "none"
+    assert rn["hist_sync"] in ("allreduce", "owner") and rn["hist_transport"] == "gloo"
+    assert rn["quality_on"].startswith("global")
+    for k in ("train_loss", "test_loss"):
+        assert abs(rn[k] - r1[k]) < 1e-3, (k, r1[k], rn[k])
+    for k in ("train_auc", "test_auc"):
+        assert abs(rn[k] - r1[k]) < 3e-3, (k, r1[k], rn[k])
+
+
+def test_bench_stalled_rank_fails_fast():
+    """A rank that stops issuing (injected stall at timed round 2) makes the world-2 bench
+    exit non-zero within the collective timeout, naming the last collective."""
+    import time
+    t0 = time.time()
+    r = _bench(2, env_extra={"YTK_FAULT_INJECT": "bench:1:2:stall", "YTK_COMM_TIMEOUT": "15"}, timeout=300)
+    assert r.returncode != 0
+    assert time.time() - t0 < 200
+    assert "failed" in r.stderr and "last collective issued" in r.stderr, r.stderr[-2000:]

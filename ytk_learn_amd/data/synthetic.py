@@ -18,6 +18,33 @@ from typing import Optional, Tuple
 import torch
 
 
+def _higgs_chunk(m: int, g: torch.Generator, dev: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+    Z = torch.randn((m, 28), generator=g, device=dev)
+    U = torch.rand((m, 28), generator=g, device=dev)
+    x = torch.empty((m, 28), device=dev)
+    # 5 objects x (pT, eta, phi, btag)-ish + missing-energy magnitude/phi -> 21 low-level
+    for j in range(21):
+        k = j % 4
+        if k == 0:
+            x[:, j] = -torch.log(U[:, j].clamp_min(1e-7)) * 0.8 + 0.3   # pT ~ exponential
+        elif k == 1:
+            x[:, j] = torch.clamp(Z[:, j] * 1.0, -2.5, 2.5)             # eta
+        elif k == 2:
+            x[:, j] = (U[:, j] * 2.0 - 1.0) * math.pi                      # phi
+        else:
+            x[:, j] = torch.floor(U[:, j] * 3.0) * 1.1                    # b-tag {0,1.1,2.2}
+    for j in range(21, 28):
+        x[:, j] = torch.exp(0.35 * Z[:, j]) * (0.8 + 0.1 * (j - 21))     # masses ~ lognormal
+    logit = (0.9 * (x[:, 25] - 1.0) - 0.7 * (x[:, 26] - 1.2) + 0.5 * torch.tanh(x[:, 0] - 1.0)
+             + 0.4 * x[:, 4] * x[:, 8] / (1.0 + x[:, 4] + x[:, 8])
+             + 0.3 * torch.cos(x[:, 2] - x[:, 6]) + 0.25 * (x[:, 3] > 1.0).float()
+             - 0.35 * (x[:, 27] - 1.4) ** 2 + 0.2 * x[:, 1] * x[:, 5] + 0.3 * torch.sin(x[:, 22]))
+    noise = torch.randn((m,), generator=g, device=dev) * 0.6
+    p = torch.sigmoid(logit + noise)
+    y = (torch.rand((m,), generator=g, device=dev) < p).float()
+    return x, y
+
+
 def higgs_like(n: int, seed: int = 0, device="cpu", chunk: int = 1 << 22) -> Tuple[torch.Tensor, torch.Tensor]:
     dev = torch.device(device)
     X = torch.empty((n, 28), dtype=torch.float32, device=dev)
@@ -26,31 +53,30 @@ def higgs_like(n: int, seed: int = 0, device="cpu", chunk: int = 1 << 22) -> Tup
     g.manual_seed(seed)
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
-        Z = torch.randn((m, 28), generator=g, device=dev)
-        U = torch.rand((m, 28), generator=g, device=dev)
-        x = torch.empty((m, 28), device=dev)
-        # 5 objects x (pT, eta, phi, btag)-ish + missing-energy magnitude/phi -> 21 low-level
-        for j in range(21):
-            k = j % 4
-            if k == 0:
-                x[:, j] = -torch.log(U[:, j].clamp_min(1e-7)) * 0.8 + 0.3   # pT ~ exponential
-            elif k == 1:
-                x[:, j] = torch.clamp(Z[:, j] * 1.0, -2.5, 2.5)             # eta
-            elif k == 2:
-                x[:, j] = (U[:, j] * 2.0 - 1.0) * math.pi                      # phi
-            else:
-                x[:, j] = torch.floor(U[:, j] * 3.0) * 1.1                    # b-tag {0,1.1,2.2}
-        for j in range(21, 28):
-            x[:, j] = torch.exp(0.35 * Z[:, j]) * (0.8 + 0.1 * (j - 21))     # masses ~ lognormal
-        logit = (0.9 * (x[:, 25] - 1.0) - 0.7 * (x[:, 26] - 1.2) + 0.5 * torch.tanh(x[:, 0] - 1.0)
-                 + 0.4 * x[:, 4] * x[:, 8] / (1.0 + x[:, 4] + x[:, 8])
-                 + 0.3 * torch.cos(x[:, 2] - x[:, 6]) + 0.25 * (x[:, 3] > 1.0).float()
-                 - 0.35 * (x[:, 27] - 1.4) ** 2 + 0.2 * x[:, 1] * x[:, 5] + 0.3 * torch.sin(x[:, 22])
-                 + 0.6 * Z[:, 0] * 0.0)
-        noise = torch.randn((m,), generator=g, device=dev) * 0.6
-        p = torch.sigmoid(logit + noise)
-        y[s:s + m, 0] = (torch.rand((m,), generator=g, device=dev) < p).float()
+        x, yy = _higgs_chunk(m, g, dev)
+        y[s:s + m, 0] = yy
         X[s:s + m] = x
+    return X, y
+
+
+def higgs_like_rows(n: int, lo: int, hi: int, seed: int = 0, device="cpu",
+                    chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rows [lo, hi) of ONE global n-row Higgs-shaped dataset: chunk c (rows [c*chunk,
+    (c+1)*chunk)) is drawn from its own generator seeded (seed, c), so every rank of a
+    row-sharded job generates only the chunks that overlap its slice and any world size
+    trains on the same global rows."""
+    dev = torch.device(device)
+    lo, hi = max(0, lo), min(n, hi)
+    X = torch.empty((max(0, hi - lo), 28), dtype=torch.float32, device=dev)
+    y = torch.empty((max(0, hi - lo), 1), dtype=torch.float32, device=dev)
+    g = torch.Generator(device=dev)
+    for c in range(lo // chunk, -(-hi // chunk)):
+        s, e = c * chunk, min(n, (c + 1) * chunk)
+        g.manual_seed(seed * 1_000_003 + c)
+        x, yy = _higgs_chunk(e - s, g, dev)
+        a, b = max(s, lo), min(e, hi)
+        X[a - lo:b - lo] = x[a - s:b - s]
+        y[a - lo:b - lo, 0] = yy[a - s:b - s]
     return X, y
 
 

@@ -226,14 +226,18 @@ class DeviceLevelBuilder:
         # level's build is ~10-20 us, less than the launch latency of the second collective.
         self.overlap = (os.environ.get("YTK_HIST_OVERLAP", "1") != "0"
                         and self.N >= int(os.environ.get("YTK_HIST_OVERLAP_MIN_ROWS", "2000000")))
-        # YTK_PEER_REDUCE=1: the level messages go through the one-shot peer-memory all-reduce
-        # (parallel/peer.py) instead of RCCL -- all-reduce mode only; stream-ordered, so the
-        # half-level overlap is not needed
+        # single-node multi-GPU (default; YTK_PEER_REDUCE=0: RCCL): every level message -- and
+        # the round's loss vector (trainer) -- is ONE peer-memory exchange kernel
+        # (parallel/peer.py) instead of an RCCL call; all-reduce mode only. Stream-ordered and
+        # host-free, so the half-level overlap is not needed, and a round whose collectives are
+        # all peer exchanges can be graph-captured on any process-group backend.
         self.peer = None
-        if peer_mod.enabled(self.comm) and not self.owner:
-            cap = max([1] + [self.level_slots[c][2] - self.level_slots[c][0] for c in self.level_slots]) * slot_elems
-            self.peer = peer_mod.PeerReduce(self.comm, cap)
-            self.overlap = False
+        if not self.owner:
+            lvl = max([1] + [self.level_slots[c][2] - self.level_slots[c][0] for c in self.level_slots]) * slot_elems
+            cap = max(lvl, slot_elems, self.maxp * CUR_STRIDE + DONE_WORDS, 4 + self.max_nodes)
+            self.peer = peer_mod.make(self.comm, cap)
+            if self.peer is not None:
+                self.overlap = False
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
@@ -319,11 +323,18 @@ class DeviceLevelBuilder:
         return out
 
     def _hist_allreduce(self, t: torch.Tensor):
-        """A level's histogram (+ count) slots: RCCL, or the peer-memory path."""
+        """A level's histogram (+ count) slots (or any int64 / fp64 device message): the
+        peer-memory exchange kernel, or RCCL."""
         if self.peer is not None:
             self.peer.allreduce_(t.view(-1))
         else:
             self.comm.allreduce_(t)
+
+    def close(self):
+        """Release the peer-memory group (collective: every rank calls it)."""
+        if self.peer is not None:
+            self.peer.close()
+            self.peer = None
 
     def _owner_reduce(self, base: int, nslots: int, ncs: int = 0):
         """Reduce-scatter slots [base, base + nslots) by feature block (+ the ncs count slots
@@ -603,7 +614,7 @@ class DeviceLevelBuilder:
                 lvl_fused = fused and not last
                 if dist and not lvl_fused:
                     self.left_glob.copy_(self.left_loc)
-                    self.comm.allreduce_(self.left_glob)
+                    self._hist_allreduce(self.left_glob)
                     tm.mark("sync_counts")
                 use_loc = (not dist) or lvl_fused
                 if fused and last:  # the last level reads the separately all-reduced counts

@@ -148,9 +148,11 @@ class DeviceLeafBuilder:
         self.slot_elems = B * F * 2
         self.msg = (torch.empty(ml * (self.slot_elems + CUR_STRIDE), dtype=torch.int64, device=dev)
                     if self.comm.is_dist else None)
-        # YTK_PEER_REDUCE=1: batch messages over the one-shot peer-memory all-reduce
-        self.peer = (peer_mod.PeerReduce(self.comm, max(self.msg.numel(), self.slot_elems))
-                     if peer_mod.enabled(self.comm) else None)
+        # single-node multi-GPU (default; YTK_PEER_REDUCE=0: RCCL): each batch message is ONE
+        # peer-memory exchange kernel that reads its size (built slots, split cursors) from the
+        # planner's device words -- the batch loop is the N = 1 loop, no host wait per batch
+        self.peer = (peer_mod.make(self.comm, max(self.msg.numel(), self.slot_elems, 4 + self.max_nodes))
+                     if self.comm.is_dist else None)
         # the trainer's K == 1 gradient pass can build the next tree's root histogram (slot 0,
         # tree_grad_hist); it is zeroed again when a tree is done
         self.staged = True
@@ -337,7 +339,7 @@ class DeviceLeafBuilder:
         h.lw_step(hd, 0, s)
         root_done = self.root_ready and not sampled  # built by the previous gradient pass
         self.root_ready = False
-        if dist:
+        if dist and self.peer is None:  # RCCL: the host sizes every batch message
             if not root_done:
                 self._hist(h, rows0, gh0, s)
             self._allreduce(self.hist[0:1].view(-1))  # the root slot
@@ -347,6 +349,8 @@ class DeviceLeafBuilder:
             return self._finish(h, s, it)
         if not root_done:
             self._hist(h, rows0, gh0, s)
+        if dist:
+            self._allreduce(self.hist[0:1].view(-1))  # the root slot (peer exchange)
         self._split(h, fmask, f0, s)
         tm.mark("root")
         # Launch throttle without events (a recorded event put a ~6 us gap before every
@@ -499,11 +503,28 @@ class DeviceLeafBuilder:
         return out
 
     def _batch(self, h, hd, rows_in, gh_in, fmask, f0, s):
-        """One speculative batch: plan, partition (+ children planning), histograms, splits."""
+        """One speculative batch: plan, partition (+ children planning), histograms, splits.
+        Multi-GPU (peer path): the batch's built slots + split cursors are all-reduced between
+        the histograms and the split search by one exchange kernel sized on the device (a
+        no-op once the planner has marked the tree done -- every rank takes the same planning
+        decisions, so the exchanges pair up however many batches a host queued past the end)."""
         h.lw_step(hd, 1, s)
         h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in, ptr(self.rows2), ptr(self.gh2),
                        self.max_pblocks, s)
-        self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
+        if self.peer is None:
+            self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
+            return
+        self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
+        st = ptr(self.st)
+        self.peer.allreduce_slots_(self.hist, self.slot_elems, ptr(self.build_ids), st + 4 * W_N_BUILD, self.cursor,
+                                   st + 4 * W_N_SPLIT, CUR_STRIDE, st + 4 * LW_DONE)
+        self._split(h, fmask, f0, s)
+
+    def close(self):
+        """Release the peer-memory group (collective: every rank calls it)."""
+        if self.peer is not None:
+            self.peer.close()
+            self.peer = None
 
     def stats(self):
         """(batches, expanded nodes, overflow flag) of the last tree (synchronises)."""

@@ -190,7 +190,9 @@ class ExactGreedyBuilder:
                 ok = (~first[None]) & (dv > MIN_FEA_SPLIT_GAP) & (left_h != 0)
                 ok &= (Lh >= mcw) & (Rh >= mcw) & can[pos_node][None]
                 chg = (self._gain(Lg, Lh) + self._gain(Rg, Rh) - root_gain[pos_node][None].double()).float()
-                chg = torch.where(ok, chg, torch.full_like(chg, float("-inf")))
+                # a 0/0 gain (zero-hessian child, mcw = l2 = 0) is never taken: the reference's
+                # `newLossChg > lossChg` is false for NaN
+                chg = torch.where(ok & ~torch.isnan(chg), chg, torch.full_like(chg, float("-inf")))
                 # per (feature, node): max lossChg and its FIRST position (the scan order), as
                 # ONE int64 max over keys (orderable lossChg bits << 31 | ~position), reduced
                 # per tile of a segment-aligned padded layout, then over each node's tiles

@@ -149,6 +149,7 @@ def run_gbdt(cfg, comm, log, transform_fn=None, threads=0, profile: bool = False
         dump_gbdt(tr, fs, mp, comm, log)
 
     tr.train(dump_cb=dump_cb)
+    tr.close()  # collective: frees the peer-memory group once every rank has drained
     dump_gbdt(tr, fs, mp, comm, log)
     dump_feature_importance(tr, fs, mp, comm, log)
     return tr

@@ -419,7 +419,7 @@ class GBDTTrainer:
             self._rb_dev = None
             accs, nlc = rbd
             if self.comm.is_dist:
-                self.comm.allreduce_(accs)
+                self._round_allreduce(accs)
             return accs, nlc
         accs = torch.stack([acc, acc_te if acc_te is not None else torch.zeros_like(acc)]).to(self.dev).reshape(-1)
         # rows per leaf from the gradient pass (level engine, deferred last-level counts):
@@ -429,8 +429,25 @@ class GBDTTrainer:
         if any(nlc):
             accs = torch.cat([accs] + [c for c in lcs if c is not None])
         if self.comm.is_dist:
-            self.comm.allreduce_(accs)  # GBDTOptimizer.java:502 (loss, weight) allreduce
+            self._round_allreduce(accs)  # GBDTOptimizer.java:502 (loss, weight) allreduce
         return accs, nlc
+
+    def _round_allreduce(self, accs: torch.Tensor):
+        """The round's (loss, weight | leaf counts) vector: the engine's peer-memory exchange
+        (fp64, rank-order sums) when it has one, else the process group."""
+        peer = getattr(self.builder, "peer", None)
+        if peer is not None and accs.dtype == torch.float64 and accs.is_contiguous() and accs.numel() <= peer.cap:
+            peer.allreduce_(accs)
+        else:
+            self.comm.allreduce_(accs)
+
+    def close(self):
+        """Release the engine's device resources shared with other ranks (the peer-memory
+        group). Collective on multi-GPU runs: every rank calls it after its last round."""
+        self.materialize()
+        close = getattr(self.builder, "close", None)
+        if close is not None:
+            close()
 
     def _readback_copy(self, i: int, dev_trees, accs, has_te: bool, nlc):
         """Host side: async copies into a pinned buffer + an event; landed by _drain."""
@@ -467,6 +484,9 @@ class GBDTTrainer:
             i, dev_trees, host, ev, has_te, nlc, rv_off = self._inflight.popleft()
             if ev is not None:
                 ev.synchronize()
+            peer = getattr(self.builder, "peer", None)
+            if peer is not None:  # a timed-out flag wait (lost / stalled peer) fails the job here
+                peer.check()
             hb = host.numpy()
             head = 32 + 8 * sum(nlc)
             if rv_off is None:  # [vector | snapshots]
@@ -566,9 +586,13 @@ class GBDTTrainer:
         return ok
 
     def _dist_capturable(self) -> bool:
-        """Every collective of a multi-GPU round can be captured: RCCL on device tensors."""
+        """Every collective of a multi-GPU round can be captured: RCCL on device tensors, or
+        peer-memory exchange kernels (level messages + the round vector; their epochs live in
+        device memory, so every replay synchronises afresh) on any backend."""
         if os.environ.get("YTK_GRAPH_DIST", "1") == "0" or self.comm.group is None:
             return False
+        if getattr(self.builder, "peer", None) is not None:
+            return True
         try:
             return torch.distributed.get_backend(self.comm.group) == "nccl"
         except Exception:
@@ -591,11 +615,14 @@ class GBDTTrainer:
                 for _ in range(2):
                     g = torch.cuda.CUDAGraph()
                     c0 = dict(self.comm.stats)
+                    fault = os.environ.get("YTK_FAULT_CAPTURE")  # fault injection (tests): vote + eager fallback
                     with torch.cuda.graph(g, pool=pool):
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
+                        if fault == "2":  # inside the capture: the round's launches half recorded
+                            raise RuntimeError("injected failure inside the capture")
                         accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
                     assert not host_trees
-                    if os.environ.get("YTK_FAULT_CAPTURE") == "1":  # fault injection (tests): the vote + eager fallback
+                    if fault == "1":  # after a complete capture
                         raise RuntimeError("injected capture failure")
                     pool = g.pool()
                     # the collectives a replay issues (captured once, counted per replay)

@@ -47,12 +47,14 @@ class Comm:
         # YTK_COMM_LOG=1: record every collective (op, dtype, numel) -- ranks must issue the
         # identical sequence (a mismatch is a hang under RCCL); checked by the tests
         self.log = [] if os.environ.get("YTK_COMM_LOG") == "1" else None
+        self.last_op = None
 
     def _count(self, t: torch.Tensor, op: str = ""):
         self.stats["calls"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
+        self.last_op = (op, str(t.dtype), int(t.numel()))  # named in timeout / failure reports
         if self.log is not None:
-            self.log.append((op, str(t.dtype), int(t.numel())))
+            self.log.append(self.last_op)
 
     def reset_stats(self):
         self.stats = {"calls": 0, "bytes": 0}
@@ -175,6 +177,7 @@ class Comm:
 
     def barrier(self):
         if self.is_dist:
+            self.last_op = ("barrier", "", 0)
             dist.barrier(group=self.cpu_group)
 
     # -- object collectives ---------------------------------------------------

@@ -1,22 +1,28 @@
-"""One-shot peer-memory all-reduce for the tree engines' histogram messages (xGMI).
+"""Peer-memory exchange for the tree engines' level / batch messages (xGMI), one kernel each.
 
 mp4j's histogram collectives were latency-optimised recursive-halving / Rabenseifner
 algorithms (docs/gbdt_features.md:36,142-143, HistogramBuilder.java:95); at a 1/8 shard a
 level's build takes 10-20 us, so the collective's latency sets the multi-GPU tree time.
-This path replaces the RCCL call of a level with five stream-ordered launches and no host
-involvement (``csrc/hip/gbdt_comm.hip``): every rank exports ONE uncached device block
-[signal | send | recv] with hipIpcGetMemHandle, the handles travel once over the host
-group, and each all-reduce is pack -> device barrier -> two-shot reduce (rank r sums chunk r
-of every send slab and writes it into every recv slab) -> device barrier -> unpack.
-Integer (int64) sums: the result is bitwise the RCCL result.
+Here every rank exports ONE uncached device block [flag words | send slab 0 | send slab 1]
+with hipIpcGetMemHandle, the handles travel once over the host group, and each all-reduce is
+ONE stream-ordered kernel (``csrc/hip/gbdt_comm.hip`` ``peer_xchg_kernel``): every block
+copies its chunk into the send slab, stamps a flag into every peer, waits for the peers'
+flags of that chunk, and sums the chunk of all P slabs in rank order back into place. No
+pack, unpack or barrier launches, no host involvement, and a message may be counted on the
+device (the leaf-wise batch). int64 sums are exact (bitwise the RCCL result); fp64 sums
+(the round's loss vector) are taken in rank order, identical on every rank.
 
-Opt-in (``YTK_PEER_REDUCE=1``) until measured on an 8-GPU node; RCCL stays the default.
-Barrier waits are bounded (``YTK_PEER_MAX_SPINS``); a timed-out wait sets an error word
-that :meth:`check` turns into an exception.
+Default for single-node multi-GPU jobs (every rank on this host: LOCAL_WORLD_SIZE ==
+WORLD_SIZE); every rank must create and open every handle, else an all-rank vote falls back
+to RCCL. ``YTK_PEER_REDUCE=0`` forces RCCL, ``=1`` forces the peer path (e.g. several ranks
+sharing one GPU over gloo). Flag waits are bounded (``YTK_PEER_TIMEOUT_S``, 60 s); a timed-out
+wait sets a host-mapped error word that :meth:`PeerReduce.check` (called where the trainer
+lands its rounds) turns into an exception.
 """
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -26,42 +32,101 @@ from .comm import Comm
 
 
 def enabled(comm: Comm) -> bool:
-    return comm.is_dist and comm.device.type == "cuda" and os.environ.get("YTK_PEER_REDUCE", "0") == "1"
+    mode = os.environ.get("YTK_PEER_REDUCE", "auto")
+    if mode == "0" or not (comm.is_dist and comm.device.type == "cuda") or comm.world > 16:
+        return False
+    if mode == "1":
+        return True
+    # auto: one node, one process per GPU (torchrun sets LOCAL_WORLD_SIZE)
+    return int(os.environ.get("LOCAL_WORLD_SIZE", comm.world)) == comm.world
+
+
+def make(comm: Comm, cap_elems: int) -> Optional["PeerReduce"]:
+    """A peer group for messages of up to ``cap_elems`` words, or None (RCCL) when the peer
+    path is off or any rank failed to create / open its handles (all-rank vote)."""
+    if not enabled(comm):
+        return None
+    return PeerReduce.create(comm, cap_elems)
 
 
 class PeerReduce:
-    MAX_SPINS = int(os.environ.get("YTK_PEER_MAX_SPINS", 20_000_000))
-
-    def __init__(self, comm: Comm, cap_elems: int):
+    def __init__(self, comm: Comm, hnd: int, cap: int):
         self.comm = comm
-        self.cap = int(cap_elems)
-        h = hip()
-        handle = np.zeros(64, np.uint8)
-        self.hnd = h.peer_create(comm.world, comm.rank, self.cap, handle.ctypes.data)
-        parts = comm.allgather_bytes(handle.tobytes())  # rank order, host group
-        allh = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
-        h.peer_open(self.hnd, allh.ctypes.data)
-        comm.barrier()
+        self.TIMEOUT_S = float(os.environ.get("YTK_PEER_TIMEOUT_S", 60.0))  # per flag wait (device wall clock)
+        self.hnd = hnd
+        self.cap = int(cap)
         self.calls = 0
 
-    def allreduce_(self, t: torch.Tensor):
-        """In-place sum over the ranks of a contiguous int64 device tensor (stream-ordered)."""
-        assert t.dtype == torch.int64 and t.is_contiguous() and t.is_cuda
-        n = t.numel()
-        if n > self.cap:
-            raise ValueError(f"peer all-reduce of {n} int64 exceeds the {self.cap}-element slab")
-        hip().peer_allreduce(self.hnd, ptr(t), n, self.MAX_SPINS, stream(t))
+    @classmethod
+    def create(cls, comm: Comm, cap_elems: int) -> Optional["PeerReduce"]:
+        h = hip()
+        cap = int(cap_elems)
+        handle = np.zeros(64, np.uint8)
+        hnd, ok, err = None, 1.0, None
+        try:
+            hnd = h.peer_create(comm.world, comm.rank, cap, handle.ctypes.data)
+        except Exception as e:  # noqa: BLE001 -- any failure votes for RCCL
+            ok = 0.0
+            err = e
+        parts = comm.allgather_bytes(handle.tobytes())  # rank order, host group (every rank)
+        if ok:
+            try:
+                allh = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+                h.peer_open(hnd, allh.ctypes.data)
+            except Exception as e:  # noqa: BLE001
+                ok = 0.0
+                err = e
+        agreed = comm.allreduce_scalars([ok], op="min")[0] > 0.5
+        if not agreed:
+            if hnd is not None:
+                h.peer_destroy(hnd)
+            if comm.is_master:
+                why = f"{type(err).__name__}: {err}" if not ok else "another rank could not open its peers"
+                print(f"[ytk] peer-memory exchange unavailable ({why}); histogram messages use RCCL", flush=True)
+            return None
+        comm.barrier()
+        return cls(comm, hnd, cap)
+
+    def _account(self, t: torch.Tensor, n: int):
         self.calls += 1
         self.comm.stats["calls"] += 1
         self.comm.stats["bytes"] += n * 8
+        self.comm.last_op = ("peer_allreduce", str(t.dtype), int(n))
         if self.comm.log is not None:
-            self.comm.log.append(("peer_allreduce", "torch.int64", int(n)))
+            self.comm.log.append(self.comm.last_op)
+
+    def allreduce_(self, t: torch.Tensor):
+        """In-place sum over the ranks of a contiguous int64 / float64 device tensor (one
+        stream-ordered kernel)."""
+        assert t.dtype in (torch.int64, torch.float64) and t.is_contiguous() and t.is_cuda
+        n = t.numel()
+        if n > self.cap:
+            raise ValueError(f"peer all-reduce of {n} words exceeds the {self.cap}-word slab")
+        hip().peer_allreduce(self.hnd, ptr(t), n, 1 if t.dtype == torch.float64 else 0, self.TIMEOUT_S, stream(t))
+        self._account(t, n)
+
+    def allreduce_slots_(self, hist: torch.Tensor, slot_elems: int, ids: int, nb_dev: int, cursor: torch.Tensor,
+                         k_dev: int, cur_stride: int, skip_dev: int):
+        """Leaf-wise batch message counted on the device: the *nb_dev slots listed at ``ids``
+        plus *k_dev x cur_stride cursor words (skipped while *skip_dev != 0). Its size is
+        known only on the device: counted as a call with 0 bytes in ``comm.stats``."""
+        hip().peer_allreduce_slots(self.hnd, ptr(hist), slot_elems, ids, nb_dev, ptr(cursor), k_dev, cur_stride,
+                                   skip_dev, self.TIMEOUT_S, stream(hist))
+        self._account(hist, 0)
 
     def check(self):
-        if hip().peer_check(self.hnd):
-            raise RuntimeError("peer all-reduce: a device barrier wait timed out (a rank stopped issuing)")
+        v = hip().peer_check(self.hnd) if self.hnd is not None else 0
+        if v == 1:
+            raise RuntimeError("peer exchange: a flag wait timed out (a rank stopped issuing)")
+        if v:
+            raise RuntimeError(f"peer exchange: device error {v} (message larger than the slab)")
 
     def close(self):
-        if self.hnd is not None:
-            hip().peer_destroy(self.hnd)
-            self.hnd = None
+        """Collective: every rank drains its device, then all free their blocks together (a
+        peer may still be reading this rank's slab until it has drained)."""
+        if self.hnd is None:
+            return
+        torch.cuda.synchronize(self.comm.device)
+        self.comm.barrier()
+        hip().peer_destroy(self.hnd)
+        self.hnd = None

@@ -1,10 +1,11 @@
 """Test-only fault injection ("kill rank r at round n to verify resume").
 
 ``YTK_FAULT_INJECT=<loop>:<rank>:<step>[:<mode>]`` makes rank ``<rank>`` fail when loop
-``<loop>`` (``gbdt`` boosting round, ``lbfgs`` iteration, ``gbst`` soft tree) is about to
-run step ``<step>`` (0-based). ``mode`` = ``exit`` (default: the process dies with status
-75 without cleanup, like a killed worker) or ``raise`` (a Python exception, so the normal
-error path runs). Several specs can be given separated by ``;``. With ``YTK_FAULT_ONCE=<file>``
+``<loop>`` (``gbdt`` boosting round, ``lbfgs`` iteration, ``gbst`` soft tree, ``bench``
+timed round) is about to run step ``<step>`` (0-based). ``mode`` = ``exit`` (default: the
+process dies with status 75 without cleanup, like a killed worker), ``raise`` (a Python
+exception, so the normal error path runs) or ``stall`` (the rank hangs without exiting, like
+a wedged worker: the other ranks' collectives must time out and fail the job). Several specs can be given separated by ``;``. With ``YTK_FAULT_ONCE=<file>``
 a spec fires only while ``<file>`` does not exist (it is created when the fault fires), so a
 restarted job runs through. Unset: no cost beyond a dictionary lookup per step.
 """
@@ -47,6 +48,12 @@ def fault_point(loop: str, step: int, rank: int = 0):
             msg = f"[rank {rank}] injected fault at {loop} step {step}"
             if mode == "raise":
                 raise InjectedFault(msg)
+            if mode == "stall":
+                sys.stderr.write(msg + " (stall)\n")
+                sys.stderr.flush()
+                import time
+                while True:
+                    time.sleep(60)
             sys.stderr.write(msg + " (exit)\n")
             sys.stderr.flush()
             os._exit(FAULT_EXIT_CODE)

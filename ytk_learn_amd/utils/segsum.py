@@ -23,7 +23,7 @@ def slot_sums(slot: torch.Tensor, w: torch.Tensor, n: int) -> torch.Tensor:
     if slot.numel() == 0:
         return h
     key = slot.to(torch.int32) if n < 2 ** 31 else slot
-    s, order = torch.sort(key)
+    s, order = torch.sort(key, stable=True)
     ids, counts = torch.unique_consecutive(s, return_counts=True)
     ids = ids.long()
     h[0, ids] = torch.segment_reduce(w[order], "sum", lengths=counts)
