@@ -126,6 +126,9 @@ void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, u
                               int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_msg(int, uintptr_t, long long, uintptr_t, int, int, uintptr_t);
 int ytk_peer_create(int, int, long long, uintptr_t);
+int ytk_ex_create(const uintptr_t*, const long long*, const float*);
+void ytk_ex_tree(int, uintptr_t, uintptr_t, int, int, int, double, double, int, float, uintptr_t);
+int ytk_ex_tile();
 void ytk_peer_open(int, uintptr_t);
 void ytk_peer_allreduce(int, uintptr_t, long long, int, double, uintptr_t);
 void ytk_peer_allreduce_slots(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
@@ -260,6 +263,12 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
   m.def("owner_pack", &ytk_owner_pack);
   m.def("peer_create", &ytk_peer_create);
+  m.def("ex_create", [](std::vector<uintptr_t> p, std::vector<long long> ip, std::vector<float> fp) {
+    if (p.size() != 27 || ip.size() != 7 || fp.size() != 6) throw std::invalid_argument("ex_create: bad arity");
+    return ytk_ex_create(p.data(), ip.data(), fp.data());
+  });
+  m.def("ex_tree", &ytk_ex_tree);
+  m.def("ex_tile", &ytk_ex_tile);
   m.def("peer_open", &ytk_peer_open);
   m.def("peer_allreduce", &ytk_peer_allreduce);
   m.def("peer_allreduce_slots", &ytk_peer_allreduce_slots);

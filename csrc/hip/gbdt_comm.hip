@@ -14,6 +14,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -132,7 +133,7 @@ void ytk_owner_unpack(uintptr_t out, uintptr_t hist, int nslots, int B, int F, i
 // and every later exchange of the group returns at once, so a lost peer never hangs the GPU.
 namespace ytk {
 constexpr int kPeerMax = 16;
-constexpr int kXchgGrid = 64;      // max blocks of one exchange (flag words per rank)
+constexpr int kXchgGrid = 256;     // max blocks of one exchange (flag words per rank)
 constexpr int kXchgThreads = 256;
 
 struct PeerPtrs {
@@ -164,13 +165,28 @@ __device__ __forceinline__ long long* xchg_elem(const XchgMsg& m, long long i, l
   return m.cursor + (i - nh);
 }
 
+// 16-byte units: pairs of consecutive elements (slot sizes, cursor strides and every
+// contiguous message start are even / 16-B aligned); an odd contiguous message's last element
+// goes alone (block G - 1)
+typedef long long xv2 __attribute__((ext_vector_type(2)));  // nontemporal builtins need a native vector
+__device__ __forceinline__ xv2* xchg_pair(const XchgMsg& m, long long u, long long nh) {
+  return reinterpret_cast<xv2*>(xchg_elem(m, 2 * u, nh));
+}
+
 template <bool kF64>
+__device__ __forceinline__ long long xchg_add(long long a, long long b) {
+  if (kF64) return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
+  return a + b;
+}
+
+template <bool kF64, bool kSysFence>
 __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, int P, int rank, XchgMsg m,
                                                                  long long cap, unsigned long long* __restrict__ ctl,
                                                                  int* __restrict__ err, long long timeout_ticks) {
   if (m.skip != nullptr && *m.skip != 0) return;
   // after a timed-out wait (ctl[2] != 0) every later exchange returns at once: the job is
   // failing (the host check raises), so nothing waits again
+  if (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   __shared__ unsigned long long s_e;
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   long long n = m.n, nh = 0;
@@ -178,7 +194,6 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
     nh = (long long)(*m.nb_dev) * m.slot_elems;
     n = nh + (long long)(*m.k_dev) * m.cur_stride;
   }
-  if (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   if (t == 0) s_e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
   const unsigned long long e = s_e;
@@ -186,22 +201,29 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
     if (b == 0 && t == 0) atomicExch(err, 2);
     n = 0;
   }
-  const long long lo = n * b / G, hi = n * (b + 1) / G;
-  if (hi > lo || b == 0) {
+  const long long nu = n >> 1;  // 16-byte units
+  const bool odd = (n & 1) != 0 && b == G - 1;
+  const long long lo = nu * b / G, hi = nu * (b + 1) / G;
+  if (hi > lo || odd || b == 0) {
     const int par = (int)(e & 1ull);
-    long long* mine = pp.send[rank][par];
-    for (long long i = lo + t; i < hi; i += kXchgThreads) __builtin_nontemporal_store(*xchg_elem(m, i, nh), mine + i);
+    xv2* mine = reinterpret_cast<xv2*>(pp.send[rank][par]);
+    // 1. publish this block's chunk: slab stores, acknowledged, then the flags
+    for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_pair(m, u, nh), mine + u);
+    if (odd && t == 0) __builtin_nontemporal_store(*xchg_elem(m, n - 1, nh), pp.send[rank][par] + n - 1);
     __builtin_amdgcn_s_waitcnt(0);  // this thread's slab stores are acknowledged
     __syncthreads();
-    if (t == 0) __threadfence_system();
-    __syncthreads();
-    if (t < P)
+    if (kSysFence) {
+      if (t == 0) __threadfence_system();
+      __syncthreads();
+    }
+    if (t < P && t != rank)
       __hip_atomic_store(pp.sig[t] + (size_t)rank * kXchgGrid + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (t < P) {
+    // 2. wait for every peer's flag of this chunk
+    if (t < P && t != rank) {
       const unsigned long long* w = pp.sig[rank] + (size_t)t * kXchgGrid + b;
       const unsigned long long t0 = wall_clock64();
       while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
         if ((long long)(wall_clock64() - t0) > timeout_ticks) {
           atomicExch(err, 1);
           atomicExch(ctl + 2, 1ull);
@@ -210,18 +232,33 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
       }
     }
     __syncthreads();
-    if (t == 0) __threadfence_system();
-    __syncthreads();
-    for (long long i = lo + t; i < hi; i += kXchgThreads) {
-      if (kF64) {
-        double s = 0.0;
-        for (int q = 0; q < P; ++q) s += __longlong_as_double(__builtin_nontemporal_load(pp.send[q][par] + i));
-        *xchg_elem(m, i, nh) = __double_as_longlong(s);
-      } else {
-        long long s = 0;
-        for (int q = 0; q < P; ++q) s += __builtin_nontemporal_load(pp.send[q][par] + i);
-        *xchg_elem(m, i, nh) = s;
+    if (kSysFence) {
+      if (t == 0) __threadfence_system();
+      __syncthreads();
+    }
+    // 3. sum the chunk over the ranks in rank order (this rank's own term from its buffer)
+    for (long long u = lo + t; u < hi; u += kXchgThreads) {
+      xv2* dst = xchg_pair(m, u, nh);
+      xv2 s = {0, 0};
+      for (int q = 0; q < P; ++q) {
+        const xv2 v = q == rank ? *dst : __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[q][par]) + u);
+        if (q == 0) {
+          s = v;
+        } else {
+          s.x = xchg_add<kF64>(s.x, v.x);
+          s.y = xchg_add<kF64>(s.y, v.y);
+        }
       }
+      *dst = s;
+    }
+    if (odd && t == 0) {
+      long long* dst = xchg_elem(m, n - 1, nh);
+      long long s = 0;
+      for (int q = 0; q < P; ++q) {
+        const long long v = q == rank ? *dst : __builtin_nontemporal_load(pp.send[q][par] + n - 1);
+        s = q == 0 ? v : xchg_add<kF64>(s, v);
+      }
+      *dst = s;
     }
   }
   // the last block to finish advances the epoch (the next exchange kernel starts after this
@@ -244,6 +281,8 @@ struct PeerGroup {
   PeerPtrs pp{};
   unsigned long long* ctl = nullptr;  // device: [0] last epoch, [1] block arrivals, [2] timed out
   long long ticks_per_s = 100000000;  // wall_clock64 rate
+  bool sys_fence = true;              // YTK_PEER_SYS_FENCE=0: waitcnt-ordered publishing only
+  int block_elems = 2048;             // YTK_PEER_BLOCK_ELEMS: elements per block
   int* err_host = nullptr;            // host-mapped error word
   int* err = nullptr;                 // its device address
 };
@@ -257,12 +296,15 @@ static size_t peer_bytes(long long cap) { return peer_sig_bytes() + 2 * (size_t)
 static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int f64, double timeout_s, hipStream_t s) {
   grid = std::max(1, std::min(grid, kXchgGrid));
   const long long ticks = (long long)(timeout_s * (double)g.ticks_per_s);
-  if (f64)
-    hipLaunchKernelGGL(peer_xchg_kernel<true>, dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap,
-                       g.ctl, g.err, ticks);
-  else
-    hipLaunchKernelGGL(peer_xchg_kernel<false>, dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap,
-                       g.ctl, g.err, ticks);
+#define YTK_XCHG(F, S)                                                                                   \
+  hipLaunchKernelGGL((peer_xchg_kernel<F, S>), dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap, \
+                     g.ctl, g.err, ticks)
+  if (g.sys_fence) {
+    if (f64) YTK_XCHG(true, true); else YTK_XCHG(false, true);
+  } else {
+    if (f64) YTK_XCHG(true, false); else YTK_XCHG(false, false);
+  }
+#undef YTK_XCHG
   YTK_LAUNCH_CHECK();
 }
 
@@ -275,6 +317,7 @@ extern "C" {
 int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   if (P < 1 || P > ytk::kPeerMax || rank < 0 || rank >= P || cap <= 0)
     throw std::invalid_argument("peer_create: bad group");
+  cap = (cap + 1) & ~1LL;  // both slabs 16-B aligned
   ytk::PeerGroup g;
   g.P = P;
   g.rank = rank;
@@ -289,6 +332,8 @@ int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   YTK_HIP_CHECK(hipGetDevice(&dev));
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
     g.ticks_per_s = (long long)khz * 1000;
+  if (const char* e = getenv("YTK_PEER_SYS_FENCE")) g.sys_fence = e[0] != '0';
+  if (const char* e = getenv("YTK_PEER_BLOCK_ELEMS")) g.block_elems = std::max(256, atoi(e));
   YTK_HIP_CHECK(hipHostMalloc(&g.err_host, sizeof(int), hipHostMallocMapped));
   *g.err_host = 0;
   void* dp = nullptr;
@@ -328,12 +373,12 @@ void ytk_peer_open(int hnd, uintptr_t handles) {
 // place, on `stream`: one kernel launch. n must be identical on every rank.
 void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int f64, double timeout_s, uintptr_t stream) {
   ytk::PeerGroup& g = g_peer.at(hnd);
-  if (n <= 0) return;
+  if (n <= 0 || g.P == 1) return;  // a one-rank all-reduce is the identity
   if (n > g.cap) throw std::invalid_argument("peer_allreduce: message larger than the slab");
   ytk::XchgMsg m{};
   m.base = reinterpret_cast<long long*>(data);
   m.n = n;
-  const int grid = (int)std::min<long long>((n + 2047) / 2048, ytk::kXchgGrid);
+  const int grid = (int)std::min<long long>((n + g.block_elems - 1) / g.block_elems, ytk::kXchgGrid);
   ytk::peer_launch(g, m, grid, f64, timeout_s, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -344,6 +389,7 @@ void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uin
                               uintptr_t cursor, uintptr_t k_dev, int cur_stride, uintptr_t skip, double timeout_s,
                               uintptr_t stream) {
   ytk::PeerGroup& g = g_peer.at(hnd);
+  if (g.P == 1) return;  // a one-rank all-reduce is the identity
   ytk::XchgMsg m{};
   m.n = -1;
   m.hist = reinterpret_cast<long long*>(hist);

@@ -3,7 +3,7 @@
 //
 // Reference hot loops (one per variant, per row): J/optimizer/GBMLRHoagOptimizer.java:159-222
 // (softmax gate, linear experts), GBSDTHoagOptimizer.java:135-230 (softmax gate, scalar
-// leaves), GBHMLRHoagOptimizer.java:174-223 (heap-indexed sigmoid gate: leaf probability =
+// leaves), GBHMLRHoagOptimizer.java:174-223 (heap-indexed sigmoid gate over any K: leaf probability =
 // product of sigma(+/-) along the path, bottom-up mu sums, gate gradient
 // mu_{2p} - sigma_p mu_p), GBHSDTHoagOptimizer.java:142-250.
 //
@@ -63,6 +63,7 @@ __global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_kernel(GbstArgs a)
   constexpr int kVals = 2 + 2 * kKMax;
   constexpr int NW = kGbstThreads / kWave;
   __shared__ double s_red[NW][kVals];
+  extern __shared__ double s_leaf[];  // tree gate, K < kKMax: [threads][kKMax] leaf probabilities
   const int K = a.K;
   double racc[kVals];
 #pragma unroll
@@ -91,17 +92,42 @@ __global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_kernel(GbstArgs a)
 #pragma unroll
       for (int k = 0; k < kKMax; ++k) g[k] = k < K ? e[k] / se : 0.0;
     } else {  // heap-indexed sigmoid tree: prob[2p] = prob[p] sigma_p, prob[2p+1] = prob[p](1 - sigma_p)
-      // (tree gates are instantiated with K == kKMax: every heap index is static)
+      // Heap nodes 1..2K-1 for ANY K (GBHMLRDataFlow.java:52 accepts every K >= 2): internal
+      // nodes 1..K-1, expert k = node K + k. Every register index below is a compile-time
+      // heap index (the unrolled loops run to kKMax, the next power of two, and test K at run
+      // time); the leaves' probabilities go to expert order through this thread's LDS row
+      // when K is not kKMax (node K + k is then not a static index).
       double prob[2 * kKMax];
       prob[1] = 1.0;
 #pragma unroll
       for (int p = 1; p < kKMax; ++p) {
-        sig[p - 1] = sig_d((double)Ar[p - 1]);
-        prob[2 * p] = prob[p] * sig[p - 1];
-        prob[2 * p + 1] = prob[p] * (1.0 - sig[p - 1]);
+        if (p < K) {
+          sig[p - 1] = sig_d((double)Ar[p - 1]);
+          prob[2 * p] = prob[p] * sig[p - 1];
+          prob[2 * p + 1] = prob[p] * (1.0 - sig[p - 1]);
+        }
+      }
+      if (K == kKMax) {
+#pragma unroll
+        for (int k = 0; k < kKMax; ++k) g[k] = prob[kKMax + k];
+      } else {
+        double* gl = s_leaf + (size_t)threadIdx.x * kKMax;
+#pragma unroll
+        for (int h = 2; h < 2 * kKMax; ++h)
+          if (h >= K && h < 2 * K) gl[h - K] = prob[h];
+#pragma unroll
+        for (int k = 0; k < kKMax; ++k) g[k] = k < K ? gl[k] : 0.0;
       }
 #pragma unroll
-      for (int k = 0; k < kKMax; ++k) g[k] = prob[kKMax + k];
+      for (int h = 1; h < 2 * kKMax; ++h) {  // leaf sums mu[K + k] = g_k H_k, in heap order
+        mu[h] = 0.0;
+        if (h >= K && h < 2 * K)
+          mu[h] = prob[h] * (a.linear ? (double)Ar[K - 1 + (h - K)] : (double)a.leaves[h - K]);
+      }
+#pragma unroll
+      for (int p = kKMax - 1; p >= 1; --p)
+        if (p < K) mu[p] = mu[2 * p] + mu[2 * p + 1];
+      mix = mu[1];
     }
 #pragma unroll
     for (int k = 0; k < kKMax; ++k)
@@ -109,12 +135,6 @@ __global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_kernel(GbstArgs a)
     if (!kTree) {
 #pragma unroll
       for (int k = 0; k < kKMax; ++k) mix += g[k] * H[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < kKMax; ++k) mu[kKMax + k] = g[k] * H[k];
-#pragma unroll
-      for (int p = kKMax - 1; p >= 1; --p) mu[p] = mu[2 * p] + mu[2 * p + 1];
-      mix = mu[1];
     }
     const double zz = (double)a.z[i];
     const double yy = (double)a.y[i];
@@ -144,7 +164,8 @@ __global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_kernel(GbstArgs a)
           if (k < K - 1) Dr[k] = (float)(c * g[k] * (H[k] - purefx));
       } else {
 #pragma unroll
-        for (int p = 1; p < kKMax; ++p) Dr[p - 1] = (float)(c * (mu[2 * p] - sig[p - 1] * mu[p]));
+        for (int p = 1; p < kKMax; ++p)
+          if (p < K) Dr[p - 1] = (float)(c * (mu[2 * p] - sig[p - 1] * mu[p]));
       }
       if (a.linear) {
 #pragma unroll
@@ -186,19 +207,18 @@ extern "C" void ytk_gbst_epilogue(uintptr_t A, int lda, uintptr_t z, uintptr_t y
                                   uintptr_t acc, uintptr_t stream) {
   if (n <= 0) return;
   if (K < 2 || K > 64) throw std::invalid_argument("gbst_epilogue: 2 <= K <= 64");
-  if (tree_gate && (K & (K - 1)) != 0)
-    throw std::invalid_argument("gbst_epilogue: hierarchical gates need a power-of-two K");
   GbstArgs a{(const float*)A, lda, (const float*)z, (const float*)y, (const float*)w, (const uint8_t*)mask,
              inv_rate, (const float*)leaves, n, K, linear, loss_id, rf, T, want_grad, (float*)D, ldd,
              (float*)pred, (double*)acc};
   const int grid = std::min(ceil_div(n, kGbstThreads), 256 * 8);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define YTK_GBST(KM)                                                                               \
-  do {                                                                                             \
-    if (tree_gate)                                                                                 \
-      hipLaunchKernelGGL((gbst_epilogue_kernel<KM, true>), dim3(grid), dim3(kGbstThreads), 0, s, a); \
-    else                                                                                           \
-      hipLaunchKernelGGL((gbst_epilogue_kernel<KM, false>), dim3(grid), dim3(kGbstThreads), 0, s, a); \
+#define YTK_GBST(KM)                                                                                   \
+  do {                                                                                                 \
+    const size_t lds = (tree_gate && K != KM) ? (size_t)kGbstThreads * KM * sizeof(double) : 0;       \
+    if (tree_gate)                                                                                     \
+      hipLaunchKernelGGL((gbst_epilogue_kernel<KM, true>), dim3(grid), dim3(kGbstThreads), lds, s, a); \
+    else                                                                                               \
+      hipLaunchKernelGGL((gbst_epilogue_kernel<KM, false>), dim3(grid), dim3(kGbstThreads), 0, s, a);   \
   } while (0)
   if (K <= 2) YTK_GBST(2);
   else if (K <= 4) YTK_GBST(4);

@@ -187,6 +187,7 @@ def test_exact_greedy_higgs_scale_timed(cuda):
     p = 1.0 / (1.0 + torch.exp(-torch.zeros_like(y[:, 0])))
     gh = torch.stack([p - y[:, 0], p * (1 - p)], 1).contiguous()
     b = ExactGreedyBuilder(torch.nan_to_num(X, 0.0), TreeParams(max_depth=6, min_child_hessian_sum=1.0))
+    tree = b.build(gh)  # warm-up (kernel loads)
     torch.cuda.synchronize()
     t = time.perf_counter()
     tree = b.build(gh)
@@ -194,3 +195,59 @@ def test_exact_greedy_higgs_scale_timed(cuda):
     dt = time.perf_counter() - t
     print(f"exact greedy depth-6 tree, 1M x 28: {dt * 1000:.1f} ms")
     assert tree.leaf_count() > 16
+
+
+def test_exact_greedy_zero_hessian_rows_never_pick_nan():
+    """min_child_hessian_sum = l2 = 0 with zero-weight rows (g = h = 0): a right child made of
+    them gives gain 0/0; such a candidate is never taken (the reference's newLossChg > lossChg
+    is false for NaN), so the tree still splits on the real signal."""
+    rng = np.random.default_rng(3)
+    N = 4000
+    X = rng.normal(size=(N, 3)).astype(np.float32)
+    y = (X[:, 0] > 0.3).astype(np.float32)
+    g = (0.5 - y).astype(np.float32)
+    h = np.full(N, 0.25, np.float32)
+    zero = X[:, 1] > 1.0  # the top of column 1: weight-0 rows
+    g[zero] = 0.0
+    h[zero] = 0.0
+    tp = TreeParams(max_depth=3, min_child_hessian_sum=0.0, l2=0.0, learning_rate=0.1)
+    tree = ExactGreedyBuilder(torch.from_numpy(X), tp).build(torch.from_numpy(np.stack([g, h], 1)))
+    assert not tree.is_leaf[0] and tree.feat[0] == 0
+    assert all(np.isfinite(tree.loss_chg[i]) for i in range(tree.num_nodes) if not tree.is_leaf[i])
+
+
+def _tree_sig(t):
+    return (t.feat, [float(np.float32(c)) for c in t.cond], t.leaf, t.left, t.right, t.is_leaf,
+            [float(np.float32(v)) for v in t.hess_sum], t.sample_cnt, [float(np.float32(v)) for v in t.loss_chg])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["plain", "budget", "sampled", "l1_mal", "zero_h", "min_samples"])
+def test_exact_greedy_hip_matches_tensor_path(cuda, case):
+    """The HIP engine (csrc/hip/gbdt_exact.hip) builds the tensor path's trees exactly: every
+    split feature / threshold, leaf value, hessian sum, sample count and lossChg; with the
+    leaf budget running out mid-level, row + feature sampling over several trees, L1 +
+    max_abs_leaf_val, zero-hessian rows and min_split_samples."""
+    X, gh = _case(9, N=30000, F=7)
+    kw = dict(max_depth=5, min_child_hessian_sum=2.0, l2=1.0, learning_rate=0.1)
+    if case == "budget":
+        kw.update(max_leaf_cnt=7)
+    elif case == "sampled":
+        kw.update(instance_sample_rate=0.7, feature_sample_rate=0.6)
+    elif case == "l1_mal":
+        kw.update(l1=0.3, max_abs_leaf_val=0.05)
+    elif case == "zero_h":
+        kw.update(min_child_hessian_sum=0.0, l2=0.0)
+        gh = gh.copy()
+        gh[X[:, 2] > 1.0] = 0.0  # weight-0 rows
+    elif case == "min_samples":
+        kw.update(min_split_samples=3000)
+    tp = TreeParams(**kw)
+    Xd, ghd = torch.from_numpy(X).to(cuda), torch.from_numpy(gh).to(cuda)
+    bh = ExactGreedyBuilder(Xd, tp, engine="hip")
+    bt = ExactGreedyBuilder(Xd, tp, engine="torch")
+    assert bh.hip and not bt.hip
+    for _ in range(3 if case == "sampled" else 1):
+        a, b = bh.build(ghd), bt.build(ghd)
+        assert _tree_sig(a) == _tree_sig(b)
+        assert a.num_nodes > 7

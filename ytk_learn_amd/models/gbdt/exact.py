@@ -60,7 +60,7 @@ MIN_FEA_SPLIT_GAP = np.float32(1e-16)  # Constants.java:34
 
 class ExactGreedyBuilder:
     def __init__(self, X: torch.Tensor, params: TreeParams, comm: Optional[Comm] = None,
-                 feat_chunk: Optional[int] = None):
+                 feat_chunk: Optional[int] = None, engine: Optional[str] = None):
         comm = comm or Comm.local(X.device)
         if comm.is_dist:
             # GBDTDataFlow.java:102-107: feature parallel only supports a single machine
@@ -77,6 +77,13 @@ class ExactGreedyBuilder:
         self.chunk = int(feat_chunk or os.environ.get("YTK_EXACT_CHUNK", 8))
         gp = params.gain_params()
         self.gpv = (gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"])
+        # on a GPU the level loop runs as the HIP kernels of csrc/hip/gbdt_exact.hip
+        # (YTK_EXACT_TORCH=1: the tensor-op formulation below, kept as the CPU path and the
+        # GPU test oracle)
+        engine = engine or ("torch" if os.environ.get("YTK_EXACT_TORCH", "0") == "1" else "hip")
+        self.hip = self.dev.type == "cuda" and engine == "hip"
+        if self.hip:
+            self._init_hip()
         self.tree_count = 0
         self.last_keep = None
         self.binsT = None  # API parity with the histogram builders
@@ -104,8 +111,143 @@ class ExactGreedyBuilder:
             v = v.clamp(-mal, mal)
         return torch.where(H < mcw, torch.zeros_like(v), v)
 
+    # ------------------------------------------------------------------ HIP engine
+    REC_DTYPE = np.dtype([("G", "<f8"), ("H", "<f8"), ("cnt", "<i8"), ("chg", "<f4"), ("thr", "<f4"),
+                          ("value", "<f4"), ("feat", "<i4"), ("split", "<i4"), ("pad", "<i4")])
+
+    def _init_hip(self):
+        """Device buffers of the HIP exact-greedy engine: the presorted columns as int32 row
+        ids + their values, ping-pong work columns, per-level tiles / node tables / records."""
+        from ...ops._ext import hip, ptr
+        p, dev, F, N = self.p, self.dev, self.F, self.N
+        h = hip()
+        T = h.ex_tile()
+        self.ord0 = self.ord.to(torch.int32).contiguous()
+        self.val0 = torch.gather(self.XT, 1, self.ord).contiguous()
+        del self.ord
+        self.ord = None
+        D = p.max_depth
+        kcap = 2 * p.max_leaf_cnt if p.max_leaf_cnt > 0 else (1 << min(D, 22))
+        self.Kmax = Kmax = int(max(1, min(N, kcap)))
+        self.max_tiles = mt = -(-max(N, 1) // T) + Kmax + 1
+        i32 = lambda n: torch.zeros(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
+        i64 = lambda n: torch.zeros(max(1, n), dtype=torch.int64, device=dev)  # noqa: E731
+        self.ordw = [torch.empty((F, N), dtype=torch.int32, device=dev) for _ in range(2)]
+        self.valw = [torch.empty((F, N), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.ex_tiles = [i32(4 * mt), i32(4 * mt)]
+        self.ex_nbeg = [i32(Kmax + 1), i32(Kmax + 1)]
+        self.ex_ftile = [i32(Kmax + 1), i32(Kmax + 1)]
+        self.ex_ctl = i32(8)
+        self.ex_tsum, self.ex_tpre = i64(F * mt * 2), i64(F * mt * 2)
+        self.ex_nbase, self.ex_nkey = i64(F * Kmax * 2), i64(F * Kmax)
+        self.ex_ntot = i64(Kmax * 2)
+        self.ex_go_feat, self.ex_go_thr = i32(Kmax), torch.zeros(Kmax, dtype=torch.float32, device=dev)
+        self.ex_csplit, self.ex_cbeg = i32(Kmax), i32(2 * Kmax)
+        self.ex_left = torch.zeros(max(1, N), dtype=torch.uint8, device=dev)
+        ks = [min(Kmax, 1 << min(d, 40)) for d in range(D + 1)]
+        self.rec_off = np.concatenate([[0], np.cumsum(ks)[:-1]]).astype(np.int64)
+        self.ex_rec = torch.zeros(int(sum(ks)) * self.REC_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self.ex_rec_off = torch.from_numpy(self.rec_off).to(dev)
+        self.ex_rec_k = i32(D + 1)
+        gp = p.gain_params()
+        ptrs = [ptr(self.ord0), ptr(self.val0), ptr(self.ordw[0]), ptr(self.ordw[1]), ptr(self.valw[0]),
+                ptr(self.valw[1]), ptr(self.XT), ptr(self.ex_tiles[0]), ptr(self.ex_tiles[1]), ptr(self.ex_nbeg[0]),
+                ptr(self.ex_nbeg[1]), ptr(self.ex_ftile[0]), ptr(self.ex_ftile[1]), ptr(self.ex_ctl),
+                ptr(self.ex_tsum), ptr(self.ex_tpre), ptr(self.ex_nbase), ptr(self.ex_nkey), ptr(self.ex_ntot),
+                ptr(self.ex_go_feat), ptr(self.ex_go_thr), ptr(self.ex_csplit), ptr(self.ex_cbeg), ptr(self.ex_left),
+                ptr(self.ex_rec), ptr(self.ex_rec_off), ptr(self.ex_rec_k)]
+        ip = [N, N, N, mt, Kmax, p.min_split_samples, p.max_leaf_cnt]
+        fp = [gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"], float(np.float32(p.min_split_loss)),
+              float(np.float32(p.learning_rate))]
+        self.ex_handle = h.ex_create(ptrs, ip, fp)
+        self._fidx_cache = {}
+
+    def _build_hip(self, gh: torch.Tensor) -> Tree:
+        """One tree on the HIP engine: the whole level loop is enqueued by one call
+        (csrc/hip/gbdt_exact.hip), then the level records come back in one copy and become
+        the host tree (same node order, values and statistics as the tensor path)."""
+        from ...ops._ext import hip, ptr, stream
+        p, dev = self.p, self.dev
+        t_start = time.perf_counter()
+        rng = np.random.default_rng((p.seed, self.tree_count))
+        seed_rows = int(rng.integers(1 << 62))
+        if p.feature_sample_rate < 1.0:
+            n_sam = max(1, int(round(p.feature_sample_rate * self.F)))
+            feats = np.sort(rng.permutation(self.F)[:n_sam])
+        else:
+            feats = np.arange(self.F)
+        key = feats.tobytes()
+        if key not in self._fidx_cache:
+            if len(self._fidx_cache) > 64:
+                self._fidx_cache.clear()
+            self._fidx_cache[key] = torch.from_numpy(feats.astype(np.int32)).to(dev)
+        fidx = self._fidx_cache[key]
+        nf = len(feats)
+        sampled = p.instance_sample_rate < 1.0
+        if sampled:  # each searched column's kept rows, still in value order, into work slab 0
+            g = torch.Generator(device=dev)
+            g.manual_seed(seed_rows)
+            keep = torch.rand(self.N, generator=g, device=dev) < p.instance_sample_rate
+            self.last_keep = keep
+            o = self.ord0[fidx.long()]
+            km = keep[o.long()]
+            n = int(km[0].sum()) if nf else 0
+            self.ordw[0][:nf, :n] = o[km].view(nf, n)
+            self.valw[0][:nf, :n] = self.val0[fidx.long()][km].view(nf, n)
+            ghk = gh[keep]
+        else:
+            keep = None
+            self.last_keep = None
+            n = self.N
+            ghk = gh
+        mx = ghk.abs().amax(dim=0).double().cpu().numpy() if n > 0 else np.zeros(2)
+        sg, sh = gops.fixed_point_scales(mx[0], mx[1], max(n, 1))
+        q = torch.empty((self.N, 2), dtype=torch.int64, device=dev)
+        q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
+        q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)
+        D = p.max_depth
+        hip().ex_tree(self.ex_handle, ptr(q), ptr(fidx), nf, n, 1 if sampled else 0, 1.0 / sg, 1.0 / sh, D,
+                      float(np.float32(p.learning_rate)), stream(q))
+        recs = self.ex_rec.cpu().numpy().view(self.REC_DTYPE)
+        rec_k = self.ex_rec_k.cpu().numpy()
+        err = int(self.ex_ctl[5].item())
+        if err:
+            raise RuntimeError(f"exact-greedy engine: capacity exceeded (code {err}, Kmax={self.Kmax}, "
+                               f"tiles={self.max_tiles})")
+        tree = Tree()
+        expand = [0]
+        for d in range(D + 1):
+            K = int(rec_k[d])
+            if not expand or K == 0:
+                break
+            assert K == len(expand), (d, K, len(expand))
+            r = recs[self.rec_off[d]:self.rec_off[d] + K]
+            new_expand = []
+            for k, nid in enumerate(expand):
+                tree.hess_sum[nid] = float(np.float32(r["H"][k]))
+                tree.sample_cnt[nid] = int(r["cnt"][k])
+                tree.loss_chg[nid] = float(r["chg"][k])
+                if r["split"][k]:
+                    lc, rc = tree.add_children(nid)
+                    tree.feat[nid] = int(r["feat"][k])
+                    tree.cond[nid] = float(r["thr"][k])
+                    tree.is_leaf[nid] = False
+                    new_expand += [lc, rc]
+                else:
+                    tree.set_leaf(nid, float(r["value"][k]))
+            expand = new_expand
+        tree.converted = True
+        self.tree_count += 1
+        self.last_stats = TimeStats()
+        self.last_stats.total = time.perf_counter() - t_start
+        self.last_stats.trees = 1
+        self.total_stats.add(self.last_stats)
+        return tree
+
     # ------------------------------------------------------------------ build
     def build(self, gh: torch.Tensor, ghmax: Optional[torch.Tensor] = None, ghmax_global: bool = False) -> Tree:
+        if self.hip:
+            return self._build_hip(gh)
         p = self.p
         t_start = time.perf_counter()
         dev = self.dev
@@ -207,7 +349,9 @@ class ExactGreedyBuilder:
             fi = torch.argmax((mx_all == best_chg[None]).to(torch.int8), dim=0)  # first feature at the max
             best_f = torch.from_numpy(feats).to(dev)[fi]
             best_v = thr_all.gather(0, fi[None])[0]
-            best_f = torch.where(torch.isfinite(best_chg), best_f, torch.full_like(best_f, -1))
+            # no candidate at all <=> -inf (a +inf lossChg -- a zero-hessian child with
+            # min_child_hessian_sum = l2 = 0 -- is a candidate, as the reference's > takes it)
+            best_f = torch.where(best_chg > float("-inf"), best_f, torch.full_like(best_f, -1))
             # --- tree update (findSplit :327-342), host side over the level's nodes
             bc, bf, bv = best_chg.cpu().numpy(), best_f.cpu().numpy(), best_v.cpu().numpy()
             Gh = Gd.cpu().numpy()

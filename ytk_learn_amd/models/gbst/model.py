@@ -180,11 +180,11 @@ class GBSTModel(ContinuousModelBase):
         return gbst_mixture(A, self.K, self.gate_kind, self.expert_kind, leaves)
 
     def _fused_ok(self, X) -> bool:
-        """The fused HIP epilogue (csrc/hip/gbst.hip) covers sigmoid / l2 losses, K <= 64
-        (hierarchical gates: power-of-two K); otherwise the fp64 torch path runs."""
+        """The fused HIP epilogue (csrc/hip/gbst.hip) covers sigmoid / l2 losses and
+        2 <= K <= 64 (softmax and hierarchical gates, any K); otherwise the fp64 torch path
+        runs."""
         K = self.K
         return (X.values.is_cuda and self.loss.name in ("sigmoid", "l2") and 2 <= K <= 64
-                and (self.gate_kind == "softmax" or (K & (K - 1)) == 0)
                 and os.environ.get("YTK_GBST_FUSED", "1") != "0")
 
     def _forward_fused(self, X, d, z, w, g_out, train: bool):
