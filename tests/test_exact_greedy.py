@@ -216,13 +216,28 @@ def test_exact_greedy_zero_hessian_rows_never_pick_nan():
     assert all(np.isfinite(tree.loss_chg[i]) for i in range(tree.num_nodes) if not tree.is_leaf[i])
 
 
+def test_exact_greedy_rows_of_early_leaves_leave_the_order():
+    """A node that becomes a leaf above max_depth (here: min_split_loss) takes its rows out
+    of the segmented order; the next levels run on the remaining rows only."""
+    X, gh = _case(4, N=6000, F=4)
+    tp = TreeParams(max_depth=4, min_child_hessian_sum=2.0, l2=1.0, min_split_loss=40.0, learning_rate=0.1)
+    tree = ExactGreedyBuilder(torch.from_numpy(X), tp).build(torch.from_numpy(gh))
+    leaves = [i for i in range(tree.num_nodes) if tree.is_leaf[i]]
+    assert sum(tree.sample_cnt[i] for i in leaves) == 6000
+    depth = {0: 0}
+    for i in range(tree.num_nodes):
+        if not tree.is_leaf[i]:
+            depth[tree.left[i]] = depth[tree.right[i]] = depth[i] + 1
+    assert min(depth[i] for i in leaves) < max(depth[i] for i in leaves)  # an early leaf exists
+
+
 def _tree_sig(t):
     return (t.feat, [float(np.float32(c)) for c in t.cond], t.leaf, t.left, t.right, t.is_leaf,
             [float(np.float32(v)) for v in t.hess_sum], t.sample_cnt, [float(np.float32(v)) for v in t.loss_chg])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["plain", "budget", "sampled", "l1_mal", "zero_h", "min_samples"])
+@pytest.mark.parametrize("case", ["plain", "budget", "sampled", "l1_mal", "zero_h", "min_samples", "early_leaves"])
 def test_exact_greedy_hip_matches_tensor_path(cuda, case):
     """The HIP engine (csrc/hip/gbdt_exact.hip) builds the tensor path's trees exactly: every
     split feature / threshold, leaf value, hessian sum, sample count and lossChg; with the
@@ -242,6 +257,8 @@ def test_exact_greedy_hip_matches_tensor_path(cuda, case):
         gh[X[:, 2] > 1.0] = 0.0  # weight-0 rows
     elif case == "min_samples":
         kw.update(min_split_samples=3000)
+    elif case == "early_leaves":
+        kw.update(min_split_loss=40.0)
     tp = TreeParams(**kw)
     Xd, ghd = torch.from_numpy(X).to(cuda), torch.from_numpy(gh).to(cuda)
     bh = ExactGreedyBuilder(Xd, tp, engine="hip")

@@ -118,15 +118,22 @@ def test_train_gpu_matches_cpu(cuda, policy):
 @pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 11}, {"min_split_samples": 3000}, {"l2": 1.0, "l1": 0.5},
                                 {"split_type": "median"}, {"feature_sample_rate": 0.6},
                                 {"instance_sample_rate": 0.7, "feature_sample_rate": 0.5, "split_type": "median"},
-                                {"max_cnt": 300, "feature_sample_rate": 0.6}])
+                                {"max_cnt": 300, "feature_sample_rate": 0.6},
+                                {"max_depth": 14, "max_leaf_cnt": 200}, {"max_depth": 16, "max_leaf_cnt": 1000},
+                                {"max_depth": 14, "max_leaf_cnt": 300, "instance_sample_rate": 0.8}])
 def test_device_builder_matches_host_builder(cuda, kw):
     """GPU-resident level builder == host-driven builder (integer histograms => identical trees),
-    including median split values, feature / instance sampling and > 256 (uint16) bins."""
+    including median split values, feature / instance sampling, > 256 (uint16) bins and
+    max_depth 14 / 16 under a leaf budget (per-level slots and arrays sized by the level width
+    min(2^depth, leaves); these configurations ran on the host builder before)."""
     d = _data(40000, 9, cuda)
     trees = []
-    special = ("max_leaf_cnt", "split_type", "max_cnt")
+    special = ("max_leaf_cnt", "split_type", "max_cnt", "max_depth")
     for dev_builder in (False, True):
         p = _params("level", rounds=3, **{k: v for k, v in kw.items() if k not in special})
+        if "max_depth" in kw:
+            p.tree.max_depth = kw["max_depth"]
+            p.tree.min_child_hessian_sum = 1.0
         if "max_leaf_cnt" in kw:
             p.tree.max_leaf_cnt = kw["max_leaf_cnt"]
         if "split_type" in kw:
@@ -140,6 +147,7 @@ def test_device_builder_matches_host_builder(cuda, kw):
         trees.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
     assert trees[0][0] == trees[1][0]
     assert trees[0][1] == trees[1][1] and trees[0][2] == trees[1][2]
+
 
 
 @pytest.mark.gpu

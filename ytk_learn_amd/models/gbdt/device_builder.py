@@ -38,7 +38,24 @@ assert DNODE_DTYPE.itemsize == 88
 ST_NUM_NODES = 0
 ST_N_HIST_A = 8  # st word: hist items of the first half of a level's build slots
 
-MAX_DEPTH_DEVICE = 12
+MAX_DEPTH_DEVICE = 30
+MAX_LEVEL_NODES = 4096  # kMaxPend (csrc/hip/gbdt_level.hip): nodes of one level in the planner's LDS
+
+
+def level_width(params: TreeParams) -> int:
+    """Most nodes one level can hold: min(2^max_depth, max_leaf_cnt rounded up to a power of
+    two) -- distinct nodes of one depth have disjoint subtrees, each with >= 1 leaf."""
+    D = params.max_depth
+    w = 1 << min(max(D, 0), 40)
+    if params.max_leaf_cnt > 0:
+        w = min(w, 1 << max(0, (params.max_leaf_cnt - 1).bit_length()))
+    return w
+
+
+def level_slots_needed(params: TreeParams) -> int:
+    """Histogram slots of the level engine's slab (without the multi-GPU count slots)."""
+    half_cap = max(1, level_width(params) // 2)
+    return 1 + sum(2 * min(1 << (c - 1), half_cap) for c in range(1, max(params.max_depth, 1)))
 
 
 class DeviceTree:
@@ -90,8 +107,10 @@ class DeviceLevelBuilder:
         assert bins.is_cuda
         self.timer = timer if timer is not None else PhaseTimer()
         p = params
-        if not (1 <= p.max_depth <= MAX_DEPTH_DEVICE) or p.grow_policy != "level":
-            raise ValueError("device builder needs level-wise growth with 1 <= max_depth <= 12")
+        if (not (1 <= p.max_depth <= MAX_DEPTH_DEVICE) or p.grow_policy != "level"
+                or level_width(p) > MAX_LEVEL_NODES):
+            raise ValueError("device builder needs level-wise growth, 1 <= max_depth <= 30 and at most 4096 "
+                             "nodes per level (min(2^max_depth, max_leaf_cnt))")
         if not self.supports(bins, binsT, B, F):
             raise ValueError(f"device builder: unsupported bin layout (dtype {bins.dtype}, B={B}, F={F})")
         # wide mode: uint16 bins with B > 256 -> feature-grouped LDS histograms over binsT
@@ -109,7 +128,10 @@ class DeviceLevelBuilder:
         D = p.max_depth
         ml = p.max_leaf_cnt if p.max_leaf_cnt > 0 else (1 << 30)
         self.max_nodes = int(min((1 << (D + 1)) - 1, 2 * ml - 1))
-        self.maxp = 1 << D
+        # nodes of one level (<= 2^D, and <= the leaf budget): every per-level array and the
+        # histogram slots of a level are sized by it, so deep trees with a leaf budget (e.g.
+        # depth 16, 255 leaves) keep small slabs
+        self.maxp = level_width(p)
         # single-pass partition: one tile reservation (a global atomic round trip) per
         # 1024 rows, so chunks stay at MIN_ROWS (2 tiles) and the latency hides behind
         # ~N/2048 resident blocks instead of ~10 serial reservations per block
@@ -200,7 +222,7 @@ class DeviceLevelBuilder:
         self.level_slots = {}
         nxt = 1
         for c in range(1, D):
-            half = 1 << (c - 1)
+            half = self._half(c)
             self.level_slots[c] = (nxt, nxt + half, nxt + half + self.ncs)  # build, count, derived
             nxt += 2 * half + self.ncs
         self.n_slots = max(1, nxt)
@@ -277,6 +299,10 @@ class DeviceLevelBuilder:
         self.last_keep = None
         self.total_stats = TimeStats()
         self._fmask_cache = {}
+
+    def _half(self, c: int) -> int:
+        """Built-child slots of level c: at most one per split of level c - 1."""
+        return min(1 << (c - 1), max(1, self.maxp // 2))
 
     @staticmethod
     def supports(bins: torch.Tensor, binsT: Optional[torch.Tensor], B: int, F: int) -> bool:
@@ -564,9 +590,9 @@ class DeviceLevelBuilder:
                 # children planning with zero cursors: the leaves' sample counts are placeholders
                 # until the round's gradient pass (tree_grad) has walked every row to its leaf;
                 # run by the tree-tail launch below together with finalize + raw tree
-                tail_children = (1 << (c - 1)) | (1 << 30)
+                tail_children = self._half(c) | (1 << 30)
                 break
-            npart = self.part_target + (1 << d) + 1
+            npart = self.part_target + min(1 << d, self.maxp) + 1
             lloc = ptrs[13]
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
@@ -575,7 +601,7 @@ class DeviceLevelBuilder:
                 gh_in = 0  # the root partition moves the row ids only
             elif gh_rows and d == 1:
                 gh_in, part_gh_rows = gh0, 1  # (g, h) by row id; this level writes it in position order
-            half = 1 << (c - 1)
+            half = self._half(c)
             if last:
                 base, ncs = 0, 0  # no histograms at the last level
             else:
@@ -655,9 +681,9 @@ class DeviceLevelBuilder:
                         self._hist_allreduce(self.hist[base:base + half + ncs])
                     tm.mark("build_hist_comm")
             if self.fuse_split_plan:
-                self._split_plan(ptrs, fp, fmask, f0, 1 << c, s)
+                self._split_plan(ptrs, fp, fmask, f0, min(1 << c, self.maxp), s)
             else:
-                self._split(fmask, f0, self._fmask_np, 1 << c, off(6), s)
+                self._split(fmask, f0, self._fmask_np, min(1 << c, self.maxp), off(6), s)
             tm.mark("find_best_split")
         # tree tail in one launch: [deferred children planning] + finalize + raw tree (when the
         # trainer registered its test-set request, set_raw_request)

@@ -381,6 +381,7 @@ class ExactGreedyBuilder:
             gf = torch.from_numpy(go_feat).to(dev)
             gt = torch.from_numpy(go_thr).to(dev)
             order, pos_node, seg = self._resegment(order, pos_node, bnd, gf, gt, K)
+            n = order.shape[1]  # the rows of nodes that became leaves left the order
             expand = new_expand
         # remaining expand nodes become leaves (make :176-180)
         if expand:

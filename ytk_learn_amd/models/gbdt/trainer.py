@@ -32,7 +32,8 @@ from ...utils.logging import get_logger
 from ...utils.timestats import PhaseTimer, profiling_enabled
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
-from .device_builder import MAX_DEPTH_DEVICE, DeviceLevelBuilder, node_table_to_tree
+from .device_builder import (MAX_DEPTH_DEVICE, MAX_LEVEL_NODES, DeviceLevelBuilder, level_slots_needed, level_width,
+                             node_table_to_tree)
 from .device_leafwise import DeviceLeafBuilder
 from .exact import ExactGreedyBuilder
 from .refine import TreeRefiner
@@ -169,8 +170,8 @@ class GBDTTrainer:
             return pool_mb is None or pool_mb <= 0 or n_slots * slot_bytes <= pool_mb * (1 << 20)
 
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
-                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE
-                                   and fits_pool(1 << max(tp.max_depth, 1))
+                                   and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and level_width(tp) <= MAX_LEVEL_NODES
+                                   and fits_pool(level_slots_needed(tp))
                                    and DeviceLevelBuilder.supports(self.bins, self.binsT, self.B, self.F))
         # leaf-wise (the reference's Higgs configuration): GPU-resident queue replay
         use_leaf = (not self.use_device_builder and self.p.device_builder and self.dev.type == "cuda"
