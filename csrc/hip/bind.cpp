@@ -264,7 +264,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("owner_pack", &ytk_owner_pack);
   m.def("peer_create", &ytk_peer_create);
   m.def("ex_create", [](std::vector<uintptr_t> p, std::vector<long long> ip, std::vector<float> fp) {
-    if (p.size() != 27 || ip.size() != 7 || fp.size() != 6) throw std::invalid_argument("ex_create: bad arity");
+    if (p.size() != 30 || ip.size() != 7 || fp.size() != 6) throw std::invalid_argument("ex_create: bad arity");
     return ytk_ex_create(p.data(), ip.data(), fp.data());
   });
   m.def("ex_tree", &ytk_ex_tree);

@@ -7,27 +7,27 @@
 // resetPosition :424-444 (value < threshold goes left) -- over J/data/gbdt/FeatureColData.java
 // :38-58 (every column sorted once by value).
 //
-// Layout: for each searched feature slot j, ord[j][0..n) are the row ids grouped into the
-// level's node segments (one contiguous range per expanding node, the same ranges for every
-// feature) and sorted by value inside each segment; val[j][i] is the row's value. A level is
-// cut into TILES of at most kExTile positions that never straddle a node, so every per-tile
-// result belongs to one node. A tree is one host call that enqueues, per level, eight
-// fixed-grid launches (work counts in device words, no host round trip until the tree's
-// records are read back):
-//   sums<0>  per (feature, tile): exact int64 (g, h) sums of the tile's rows
-//   scan<0>  per feature: exclusive tile prefixes inside each node (+ node totals, slot 0)
-//   eval     per (feature, tile): in-tile exclusive scan -> left sums at every position, gap
-//            test, both children's hessians, lossChg in double exactly as the reference, per
-//            tile the best key (lossChg bits, lowest position), atomicMax per (feature, node)
+// Layout: for each searched feature slot j, position i of the level's order holds a row id
+// ord[j][i], its value val[j][i] and its fixed-point (g, h) qv[j][i]; the rows of one node
+// are contiguous (the same ranges for every feature) and sorted by value. (g, h) travel with
+// the rows (gathered once per tree), so the split scan reads every array sequentially. A
+// level is cut into TILES of <= kExTile positions that never straddle a node. Per level:
+//   eval     per (feature, tile), in ticket order: tile (g, h) aggregate, decoupled
+//            look-back over the node's earlier tiles for the exact int64 prefix, left sums
+//            at every position, gap test, both children's hessians, lossChg in double as
+//            the reference, tile best key -> atomicMax per (feature, node)
 //   decide   one block: best feature per node (strictly greater: lowest feature on ties),
 //            split iff lossChg > min_split_loss within the leaf budget (a prefix count over
 //            the level's nodes in expand order), node records, split feature / threshold
-//   flag     per tile of slot 0: row -> left (value < threshold) / right / dropped
-//   sums<1>  per (feature, tile): left rows of the tile
-//   scan<1>  per feature: left offsets inside each node; slot 0's block also lays out the
-//            children's segments and the next level's tile table
-//   part     per (feature, tile): stable partition into the children's segments
-// The last level (max_depth) runs sums<0> + scan<0> + decide only (its nodes are leaves).
+//   flag     per tile of slot 0: row -> left / right / dropped, tile partials (left rows,
+//            left (g, h), right (g, h))
+//   layout   one block: node sums of the partials -> the children's exact (g, h) totals,
+//            segments, first tiles and the next level's tile table
+//   part     per (feature, tile), in ticket order: left-count look-back inside the node,
+//            stable partition of (row, value, (g, h)) into the children's segments
+// The last level (max_depth) runs decide only (its nodes are leaves; their totals came from
+// the previous layout). Look-back status words pack (value << 2 | flag): the fixed-point
+// scales leave |sums| < 2^60 (the caller passes 4 N to the scale rule).
 #include "common.h"
 #include "gbdt_split_node.h"
 
@@ -40,7 +40,7 @@ namespace ytk {
 constexpr int kExThreads = 256;
 constexpr int kExPer = 8;
 constexpr int kExTile = kExThreads * kExPer;  // positions per tile
-constexpr int kExScanThreads = 1024;
+constexpr int kExBig = 1024;                  // single-block kernels
 
 struct ExRec {  // one expanding node of a level (48 B)
   double G, H;
@@ -50,7 +50,8 @@ struct ExRec {  // one expanding node of a level (48 B)
 };
 static_assert(sizeof(ExRec) == 48, "ExRec layout");
 
-enum { EX_NT0 = 0, EX_NT1 = 1, EX_K0 = 2, EX_K1 = 3, EX_LEAF = 4, EX_ERR = 5, EX_WORDS = 8 };
+// ctl words; tickets of level d's eval / part at kExTicket + 2 d (+ 1)
+enum { EX_NT0 = 0, EX_NT1 = 1, EX_K0 = 2, EX_K1 = 3, EX_LEAF = 4, EX_ERR = 5, EX_TICKET = 16, EX_CTL_WORDS = 128 };
 
 struct ExArgs {
   const int* ord0;
@@ -58,23 +59,25 @@ struct ExArgs {
   long long ld0;  // presorted columns [F][ld0]
   int* ordw[2];
   float* valw[2];
-  long long ldw;  // work ping-pong [nf][ldw]
-  int sampled;    // level 0 reads ordw[0] / valw[0] (the tree's kept rows) instead of ord0
-  const int* fidx;  // feature of slot j, ascending
+  long long* qvw[2];  // [nf][ldw][2]
+  long long ldw;      // work ping-pong [nf][ldw]
+  int sampled;        // level 0 reads ordw[0] / valw[0] (the tree's kept rows) instead of ord0
+  const int* fidx;    // feature of slot j, ascending
   int nf;
   const float* XT;
-  long long ldx;  // raw values [F][ldx]
-  const long long* q;  // [N][2] fixed-point (g, h)
-  int4* tiles[2];  // (node, p0, p1, 0) per level parity
-  int* nbeg[2];    // [Kmax + 1] node begins
-  int* ftile[2];   // [Kmax + 1] first tile of each node
+  long long ldx;        // raw values [F][ldx]
+  const long long* q;   // [N][2] fixed-point (g, h) by row
+  int4* tiles[2];       // (node, p0, p1, 0) per level parity
+  int* nbeg[2];         // [Kmax + 1] node begins
+  int* ftile[2];        // [Kmax + 1] first tile of each node
   int max_tiles, Kmax;
   int* ctl;
-  long long* tsum;  // [nf][max_tiles][2]
-  long long* tpre;  // [nf][max_tiles][2]
-  long long* nbase;  // [nf][Kmax][2]
+  unsigned long long* st_gh;   // [nf][max_tiles][2] eval look-back words
+  unsigned long long* st_cnt;  // [nf][max_tiles] part look-back words
+  long long* tpart;   // [max_tiles][5] flag partials: left rows, left g, left h, right g, right h
+  long long* nbase;   // [Kmax + 1][5] layout scratch
   unsigned long long* nkey;  // [nf][Kmax] (zero between levels: decide resets)
-  long long* ntot;   // [Kmax][2]
+  long long* ntot;    // [Kmax][2] totals of the current level's nodes
   int* go_feat;
   float* go_thr;
   int* csplit;  // child index (2 * split rank) or -1
@@ -96,9 +99,17 @@ __device__ __forceinline__ const float* ex_src_val(const ExArgs& a, int d, int j
   if (d == 0 && !a.sampled) return a.val0 + (size_t)a.fidx[j] * a.ld0;
   return a.valw[d & 1] + (size_t)j * a.ldw;
 }
+__device__ __forceinline__ const longlong2* ex_src_q(const ExArgs& a, int d, int j) {
+  return reinterpret_cast<const longlong2*>(a.qvw[d & 1] + (size_t)j * a.ldw * 2);
+}
 
-__device__ __forceinline__ long long ld_agent(const long long* p) {
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // order-preserving unsigned image of a float (bits as exact.py's key: -0 below +0)
@@ -110,26 +121,61 @@ __device__ __forceinline__ float ord2f(unsigned o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-// sum of (a, b) over the 256-thread block, returned to every thread
-__device__ __forceinline__ void ex_block_sum2(long long& a, long long& b) {
-  __shared__ long long s[2][kExThreads / kWave];
+// look-back status word: (value << 2) | flag, flag 1 = tile aggregate, 2 = inclusive prefix
+__device__ __forceinline__ unsigned long long lb_word(long long v, int flag) {
+  return ((unsigned long long)v << 2) | (unsigned long long)flag;
+}
+__device__ __forceinline__ long long lb_value(unsigned long long w) { return (long long)w >> 2; }
+
+// Exclusive prefix of tile t inside its node (tiles ft..t-1) for C components, by thread 0:
+// walks back until an inclusive prefix; tiles with lower tickets always publish first.
+template <int C>
+__device__ __forceinline__ void lb_walk(const unsigned long long* st, int t, int ft, long long* excl) {
+  bool done[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    excl[c] = 0;
+    done[c] = false;
+  }
+  for (int p = t - 1; p >= ft; --p) {
+    bool all = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (done[c]) continue;
+      unsigned long long w;
+      while (((w = ld_agent(st + (size_t)p * C + c)) & 3ull) == 0ull) __builtin_amdgcn_s_sleep(1);
+      excl[c] += lb_value(w);
+      if ((w & 3ull) == 2ull) done[c] = true;
+      all = all && done[c];
+    }
+    if (all) break;
+  }
+}
+
+// sum of (a, b, c) over the 256-thread block, to every thread
+__device__ __forceinline__ void ex_block_sum3(long long& a, long long& b, long long& c) {
+  __shared__ long long s[3][kExThreads / kWave];
   const long long wa = readlane64(dpp_scan_add(a), kWave - 1), wb = readlane64(dpp_scan_add(b), kWave - 1);
+  const long long wc = readlane64(dpp_scan_add(c), kWave - 1);
   const int w = threadIdx.x / kWave;
   if (lane_id() == 0) {
     s[0][w] = wa;
     s[1][w] = wb;
+    s[2][w] = wc;
   }
   __syncthreads();
-  a = b = 0;
+  a = b = c = 0;
 #pragma unroll
   for (int k = 0; k < kExThreads / kWave; ++k) {
     a += s[0][k];
     b += s[1][k];
+    c += s[2][k];
   }
+  __syncthreads();
 }
 
-// exclusive prefix of (a, b) over the block's threads in thread order (in place)
-__device__ __forceinline__ void ex_block_excl2(long long& a, long long& b) {
+// exclusive prefix of (a, b) over the block's threads in thread order (in place) + totals
+__device__ __forceinline__ void ex_block_excl2(long long& a, long long& b, long long& ta, long long& tb) {
   __shared__ long long s[2][kExThreads / kWave];
   const long long ia = dpp_scan_add(a), ib = dpp_scan_add(b);
   const int w = threadIdx.x / kWave;
@@ -139,20 +185,27 @@ __device__ __forceinline__ void ex_block_excl2(long long& a, long long& b) {
   }
   __syncthreads();
   long long oa = 0, ob = 0;
+  ta = tb = 0;
 #pragma unroll
-  for (int k = 0; k < kExThreads / kWave; ++k)
+  for (int k = 0; k < kExThreads / kWave; ++k) {
     if (k < w) {
       oa += s[0][k];
       ob += s[1][k];
     }
+    ta += s[0][k];
+    tb += s[1][k];
+  }
   a = oa + ia - a;
   b = ob + ib - b;
+  __syncthreads();
 }
 
-__global__ __launch_bounds__(kExScanThreads) void ex_init_kernel(ExArgs a, int n) {
+__global__ __launch_bounds__(kExBig) void ex_init_kernel(ExArgs a, int n) {
   const int nt = n > 0 ? (n + kExTile - 1) / kExTile : 0;
-  for (int t = threadIdx.x; t < nt; t += kExScanThreads)
+  for (int t = threadIdx.x; t < nt && t < a.max_tiles; t += kExBig)
     a.tiles[0][t] = make_int4(0, t * kExTile, min(n, (t + 1) * kExTile), 0);
+  for (int w = EX_TICKET + threadIdx.x; w < EX_CTL_WORDS; w += kExBig) a.ctl[w] = 0;
+  if (threadIdx.x < 2) a.ntot[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
     if (nt > a.max_tiles) a.ctl[EX_ERR] = 1;
     a.ctl[EX_NT0] = min(nt, a.max_tiles);
@@ -167,179 +220,24 @@ __global__ __launch_bounds__(kExScanThreads) void ex_init_kernel(ExArgs a, int n
   }
 }
 
-// kMode 0: (g, h) sums of the tile's rows; 1: left rows of a split node's tile
-template <int kMode>
-__global__ __launch_bounds__(kExThreads) void ex_sums_kernel(ExArgs a, int d) {
-  const int par = d & 1, t = blockIdx.x, j = blockIdx.y;
-  if (t >= a.ctl[EX_NT0 + par]) return;
-  const int4 tl = a.tiles[par][t];
-  const int* ord = ex_src_ord(a, d, j);
-  long long s0 = 0, s1 = 0;
-  if (kMode == 0) {
-    const longlong2* q2 = reinterpret_cast<const longlong2*>(a.q);
-    for (int i = tl.y + threadIdx.x; i < tl.z; i += kExThreads) {
-      const longlong2 v = q2[ord[i]];
-      s0 += v.x;
-      s1 += v.y;
-    }
-  } else if (a.csplit[tl.x] >= 0) {
-    for (int i = tl.y + threadIdx.x; i < tl.z; i += kExThreads) s0 += a.left_row[ord[i]] == 1;
-  }
-  ex_block_sum2(s0, s1);
-  if (threadIdx.x == 0) {
-    long long* o = a.tsum + ((size_t)j * a.max_tiles + t) * 2;
-    o[0] = s0;
-    o[1] = s1;
-  }
-}
-
-// Exclusive prefixes of the tiles inside their node, per feature (one block each). Slot 0's
-// block then derives per node: mode 0 the totals, mode 1 the children's layout.
-template <int kMode>
-__global__ __launch_bounds__(kExScanThreads) void ex_scan_kernel(ExArgs a, int d) {
-  const int par = d & 1, j = blockIdx.x, tid = threadIdx.x;
-  const int nt = a.ctl[EX_NT0 + par], K = a.ctl[EX_K0 + par];
-  const int4* tiles = a.tiles[par];
-  const int* ftile = a.ftile[par];
-  const long long* ts = a.tsum + (size_t)j * a.max_tiles * 2;
-  long long* tp = a.tpre + (size_t)j * a.max_tiles * 2;
-  long long* nb = a.nbase + (size_t)j * a.Kmax * 2;
-  constexpr int kW = kExScanThreads / kWave;
-  __shared__ long long s0[kW], s1[kW];
-  __shared__ int si[kW];
-  const int w = tid / kWave, l = lane_id();
-  long long c0 = 0, c1 = 0;
-  for (int base = 0; base < nt; base += kExScanThreads) {
-    const int t = base + tid;
-    long long x0 = 0, x1 = 0;
-    int node = 0;
-    if (t < nt) {
-      x0 = ts[2 * t];
-      x1 = ts[2 * t + 1];
-      node = tiles[t].x;
-    }
-    const long long i0 = dpp_scan_add(x0), i1 = dpp_scan_add(x1);
-    if (l == kWave - 1) {
-      s0[w] = i0;
-      s1[w] = i1;
-    }
-    __syncthreads();
-    long long o0 = c0, o1 = c1, T0 = 0, T1 = 0;
-    for (int k = 0; k < kW; ++k) {
-      if (k < w) {
-        o0 += s0[k];
-        o1 += s1[k];
-      }
-      T0 += s0[k];
-      T1 += s1[k];
-    }
-    const long long e0 = o0 + i0 - x0, e1 = o1 + i1 - x1;  // column prefix before tile t
-    if (t < nt && ftile[node] == t) {
-      nb[2 * node] = e0;
-      nb[2 * node + 1] = e1;
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // the node bases are in L2 before any wave reads them
-    __syncthreads();
-    if (t < nt) {
-      tp[2 * t] = e0 - ld_agent(nb + 2 * node);
-      tp[2 * t + 1] = e1 - ld_agent(nb + 2 * node + 1);
-    }
-    c0 += T0;
-    c1 += T1;
-    __syncthreads();
+// level 0: qv[j][i] = q[ord[j][i]] (the only gather of (g, h) in a tree) and the root's totals
+__global__ __launch_bounds__(kExThreads) void ex_gather_kernel(ExArgs a, int n) {
+  const int j = blockIdx.y;
+  const int* ord = ex_src_ord(a, 0, j);
+  longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[0] + (size_t)j * a.ldw * 2);
+  const longlong2* q2 = reinterpret_cast<const longlong2*>(a.q);
+  long long sg = 0, sh = 0, dummy = 0;
+  for (long long i = blockIdx.x * (long long)kExThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kExThreads) {
+    const longlong2 v = q2[ord[i]];
+    qo[i] = v;
+    sg += v.x;
+    sh += v.y;
   }
   if (j != 0) return;
-  // per-node sums (slot 0): node k's rows are its tiles, prefix difference
-  auto node_sum = [&](int k, int c) -> long long {
-    const long long b = ld_agent(nb + 2 * k + c);
-    const long long e = (k + 1 < K) ? ld_agent(nb + 2 * (k + 1) + c) : (c == 0 ? c0 : c1);
-    return e - b;
-  };
-  if (kMode == 0) {
-    for (int k = tid; k < K; k += kExScanThreads) {
-      a.ntot[2 * k] = node_sum(k, 0);
-      a.ntot[2 * k + 1] = node_sum(k, 1);
-    }
-    return;
-  }
-  // children layout: split node k (child index c = csplit[k]) keeps its rows, left child
-  // first: begins S_k and S_k + left_k, S_k = rows of the split nodes before k
-  const int npar = par ^ 1;
-  const int* nbg = a.nbeg[par];
-  const int Kn = a.ctl[EX_K0 + npar];
-  int carry = 0, tcarry = 0;
-  for (int base = 0; base < K; base += kExScanThreads) {
-    const int k = base + tid;
-    int rows = 0, ntl = 0, left = 0, c = -1;
-    if (k < K) {
-      c = a.csplit[k];
-      if (c >= 0) {
-        rows = nbg[k + 1] - nbg[k];
-        left = (int)node_sum(k, 0);
-        ntl = (left + kExTile - 1) / kExTile + (rows - left + kExTile - 1) / kExTile;
-      }
-    }
-    // block exclusive scans of rows and tile counts
-    int ir = rows, it = ntl;
-    for (int off = 1; off < kWave; off <<= 1) {
-      const int vr = __shfl_up(ir, off, kWave), vt = __shfl_up(it, off, kWave);
-      if (l >= off) {
-        ir += vr;
-        it += vt;
-      }
-    }
-    if (l == kWave - 1) {
-      s0[w] = ir;
-      si[w] = it;
-    }
-    __syncthreads();
-    int orr = carry, ot = tcarry, Tr = 0, Tt = 0;
-    for (int q = 0; q < kW; ++q) {
-      if (q < w) {
-        orr += (int)s0[q];
-        ot += si[q];
-      }
-      Tr += (int)s0[q];
-      Tt += si[q];
-    }
-    if (c >= 0) {
-      const int S = orr + ir - rows, ft = ot + it - ntl;
-      a.cbeg[2 * k] = S;
-      a.cbeg[2 * k + 1] = S + left;
-      a.nbeg[npar][c] = S;
-      a.nbeg[npar][c + 1] = S + left;
-      a.ftile[npar][c] = ft;
-      a.ftile[npar][c + 1] = ft + (left + kExTile - 1) / kExTile;
-    }
-    carry += Tr;
-    tcarry += Tt;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    a.nbeg[npar][Kn] = carry;
-    a.ftile[npar][Kn] = tcarry;
-    if (tcarry > a.max_tiles) a.ctl[EX_ERR] = 1;
-    a.ctl[EX_NT0 + npar] = min(tcarry, a.max_tiles);
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // the children's begins / first tiles are in L2
-  __syncthreads();
-  // the next level's tile table: tile t' of child c (binary search over the children's first tiles)
-  const int ntn = min(tcarry, a.max_tiles);
-  const int* ftn = a.ftile[npar];
-  const int* nbn = a.nbeg[npar];
-  for (int t = tid; t < ntn; t += kExScanThreads) {
-    int lo = 0, hi = Kn - 1;  // last child with ftile <= t (children are non-empty: >= 1 tile)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (__hip_atomic_load(ftn + mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= t) lo = mid;
-      else hi = mid - 1;
-    }
-    const int c = lo;
-    const int f0 = __hip_atomic_load(ftn + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int b0 = __hip_atomic_load(nbn + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int b1 = __hip_atomic_load(nbn + c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int p0 = b0 + (t - f0) * kExTile;
-    a.tiles[npar][t] = make_int4(c, p0, min(b1, p0 + kExTile), 0);
+  ex_block_sum3(sg, sh, dummy);
+  if (threadIdx.x == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ntot), (unsigned long long)sg);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ntot + 1), (unsigned long long)sh);
   }
 }
 
@@ -353,21 +251,36 @@ __device__ __forceinline__ ExSpan ex_span(int4 tl) {
   return {i0, max(0, min(kExPer, tl.z - i0))};
 }
 
+// the block's (feature slot, tile) from the level's ticket counter (lower tickets start first)
+__device__ __forceinline__ bool ex_ticket(const ExArgs& a, int word, int nt, int& j, int& t) {
+  __shared__ int s_idx;
+  if (threadIdx.x == 0) s_idx = atomicAdd(a.ctl + word, 1);
+  __syncthreads();
+  const int idx = s_idx;
+  __syncthreads();
+  if (idx >= nt * a.nf) return false;
+  j = idx % a.nf;
+  t = idx / a.nf;
+  return true;
+}
+
 __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
-  const int par = d & 1, t = blockIdx.x, j = blockIdx.y;
-  if (t >= a.ctl[EX_NT0 + par]) return;
+  const int par = d & 1;
+  const int nt = a.ctl[EX_NT0 + par];
+  int j, t;
+  if (!ex_ticket(a, EX_TICKET + 2 * d, nt, j, t)) return;
   const int4 tl = a.tiles[par][t];
   const int k = tl.x;
   const int nb0 = a.nbeg[par][k], nb1 = a.nbeg[par][k + 1];
   const long long NG = a.ntot[2 * k], NH = a.ntot[2 * k + 1];
   const GainParams& gp = a.gp;
   const double G = (double)NG * gp.inv_sg, H = (double)NH * gp.inv_sh;
-  // canSplit (UpdateStrategy.java:50-53): block-uniform
+  // canSplit (UpdateStrategy.java:50-53): the same for every tile of the node, so a node
+  // that cannot split publishes nothing and nobody waits on it
   if (!(H >= 2.0 * (double)gp.mcw && (nb1 - nb0) >= max(a.min_split_samples, 0))) return;
   const float root_gain = (float)calc_gain(G, H, gp);
-  const int* ord = ex_src_ord(a, d, j);
   const float* val = ex_src_val(a, d, j);
-  const longlong2* q2 = reinterpret_cast<const longlong2*>(a.q);
+  const longlong2* qv = ex_src_q(a, d, j);
   const ExSpan sp = ex_span(tl);
   long long g[kExPer], h[kExPer];
   float v[kExPer];
@@ -377,7 +290,7 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
     g[e] = h[e] = 0;
     v[e] = 0.f;
     if (e < sp.n) {
-      const longlong2 x = q2[ord[sp.i0 + e]];
+      const longlong2 x = qv[sp.i0 + e];
       g[e] = x.x;
       h[e] = x.y;
       v[e] = val[sp.i0 + e];
@@ -386,12 +299,30 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
     th += h[e];
   }
   __shared__ float s_last[kExThreads];
+  __shared__ long long s_pre[2];
   s_last[threadIdx.x] = sp.n > 0 ? v[sp.n - 1] : 0.f;
-  long long lg = tg, lh = th;
-  ex_block_excl2(lg, lh);  // includes a __syncthreads (s_last visible)
-  const long long* tp = a.tpre + ((size_t)j * a.max_tiles + t) * 2;
-  lg += tp[0];
-  lh += tp[1];
+  long long lg = tg, lh = th, ag, ah;
+  ex_block_excl2(lg, lh, ag, ah);  // (+ barrier: s_last visible)
+  unsigned long long* st = a.st_gh + (size_t)j * a.max_tiles * 2;
+  const int ft = a.ftile[par][k];
+  if (threadIdx.x == 0) {
+    long long ex[2] = {0, 0};
+    if (t == ft) {
+      st_agent(st + 2 * t, lb_word(ag, 2));
+      st_agent(st + 2 * t + 1, lb_word(ah, 2));
+    } else {
+      st_agent(st + 2 * t, lb_word(ag, 1));
+      st_agent(st + 2 * t + 1, lb_word(ah, 1));
+      lb_walk<2>(st, t, ft, ex);
+      st_agent(st + 2 * t, lb_word(ex[0] + ag, 2));
+      st_agent(st + 2 * t + 1, lb_word(ex[1] + ah, 2));
+    }
+    s_pre[0] = ex[0];
+    s_pre[1] = ex[1];
+  }
+  __syncthreads();
+  lg += s_pre[0];
+  lh += s_pre[1];
   float vp = 0.f;
   if (sp.n > 0 && sp.i0 > nb0) vp = threadIdx.x > 0 ? s_last[threadIdx.x - 1] : val[sp.i0 - 1];
   unsigned long long best = 0;
@@ -427,7 +358,7 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
   }
 }
 
-__global__ __launch_bounds__(kExScanThreads) void ex_decide_kernel(ExArgs a, int d, int final_level) {
+__global__ __launch_bounds__(kExBig) void ex_decide_kernel(ExArgs a, int d, int final_level) {
   const int par = d & 1, tid = threadIdx.x;
   const int K = a.ctl[EX_K0 + par];
   const int leaf0 = a.ctl[EX_LEAF];
@@ -435,11 +366,11 @@ __global__ __launch_bounds__(kExScanThreads) void ex_decide_kernel(ExArgs a, int
   const int room = a.max_leaf > 0 ? a.max_leaf - leaf0 : 0x7fffffff;
   ExRec* rec = a.rec + a.rec_off[d];
   const GainParams& gp = a.gp;
-  constexpr int kW = kExScanThreads / kWave;
+  constexpr int kW = kExBig / kWave;
   __shared__ int s_w[kW];
   const int w = tid / kWave, l = lane_id();
   int carry = 0;
-  for (int base = 0; base < K; base += kExScanThreads) {
+  for (int base = 0; base < K; base += kExBig) {
     const int k = base + tid;
     float bchg = -INFINITY;
     int bj = -1;
@@ -509,6 +440,7 @@ __global__ __launch_bounds__(kExScanThreads) void ex_decide_kernel(ExArgs a, int
   }
 }
 
+// slot 0: go-left flags by row + per-tile partials of the children (exact int64)
 __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
   const int par = d & 1, t = blockIdx.x;
   if (t >= a.ctl[EX_NT0 + par]) return;
@@ -516,25 +448,184 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
   const int f = a.go_feat[tl.x];
   const float thr = a.go_thr[tl.x];
   const int* ord = ex_src_ord(a, d, 0);
+  const longlong2* qv = ex_src_q(a, d, 0);
+  long long nl = 0, lg = 0, lh = 0, rg = 0, rh = 0;
   for (int i = tl.y + threadIdx.x; i < tl.z; i += kExThreads) {
     const int r = ord[i];
-    a.left_row[r] = f < 0 ? 2 : (a.XT[(size_t)f * a.ldx + r] < thr ? 1 : 0);
+    if (f < 0) {
+      a.left_row[r] = 2;
+      continue;
+    }
+    const longlong2 x = qv[i];
+    const bool left = a.XT[(size_t)f * a.ldx + r] < thr;
+    a.left_row[r] = left ? 1 : 0;
+    if (left) {
+      ++nl;
+      lg += x.x;
+      lh += x.y;
+    } else {
+      rg += x.x;
+      rh += x.y;
+    }
+  }
+  long long z = 0;
+  ex_block_sum3(nl, lg, lh);
+  ex_block_sum3(rg, rh, z);
+  if (threadIdx.x == 0) {
+    long long* o = a.tpart + (size_t)t * 5;
+    o[0] = nl;
+    o[1] = lg;
+    o[2] = lh;
+    o[3] = rg;
+    o[4] = rh;
+  }
+}
+
+// One block: node sums of the flag partials (global exclusive tile prefixes recorded at each
+// node's first tile), the children's exact (g, h) totals (the next level's ntot), segments,
+// first tiles and tile table.
+__global__ __launch_bounds__(kExBig) void ex_layout_kernel(ExArgs a, int d) {
+  const int par = d & 1, npar = par ^ 1, tid = threadIdx.x;
+  const int nt = a.ctl[EX_NT0 + par], K = a.ctl[EX_K0 + par], Kn = a.ctl[EX_K0 + npar];
+  const int4* tiles = a.tiles[par];
+  const int* ftile = a.ftile[par];
+  const int* nbg = a.nbeg[par];
+  constexpr int kW = kExBig / kWave;
+  __shared__ long long s5[5][kW];
+  __shared__ int si[2][kW];
+  const int w = tid / kWave, l = lane_id();
+  long long carry[5] = {0, 0, 0, 0, 0};
+  for (int base = 0; base < nt; base += kExBig) {
+    const int t = base + tid;
+    long long x[5] = {0, 0, 0, 0, 0}, inc[5];
+    int node = 0;
+    if (t < nt) {
+      node = tiles[t].x;
+      if (a.go_feat[node] >= 0) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) x[c] = a.tpart[(size_t)t * 5 + c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      inc[c] = dpp_scan_add(x[c]);
+      if (l == kWave - 1) s5[c][w] = inc[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      long long o = carry[c], T = 0;
+      for (int q = 0; q < kW; ++q) {
+        if (q < w) o += s5[c][q];
+        T += s5[c][q];
+      }
+      if (t < nt && ftile[node] == t) a.nbase[(size_t)node * 5 + c] = o + inc[c] - x[c];
+      carry[c] += T;
+    }
+    __syncthreads();
+  }
+  if (tid < 5) a.nbase[(size_t)K * 5 + tid] = carry[tid];
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  auto nsum = [&](int k, int c) -> long long {
+    return ld_agent(a.nbase + (size_t)(k + 1) * 5 + c) - ld_agent(a.nbase + (size_t)k * 5 + c);
+  };
+  // children: split node k (child index c = csplit[k]) keeps its rows, left child first
+  int rcarry = 0, tcarry = 0;
+  for (int base = 0; base < K; base += kExBig) {
+    const int k = base + tid;
+    int rows = 0, ntl = 0, left = 0, c = -1;
+    if (k < K) {
+      c = a.csplit[k];
+      if (c >= 0) {
+        rows = nbg[k + 1] - nbg[k];
+        left = (int)nsum(k, 0);
+        ntl = (left + kExTile - 1) / kExTile + (rows - left + kExTile - 1) / kExTile;
+      }
+    }
+    int ir = rows, it = ntl;
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int vr = __shfl_up(ir, off, kWave), vt = __shfl_up(it, off, kWave);
+      if (l >= off) {
+        ir += vr;
+        it += vt;
+      }
+    }
+    if (l == kWave - 1) {
+      si[0][w] = ir;
+      si[1][w] = it;
+    }
+    __syncthreads();
+    int orr = rcarry, ot = tcarry, Tr = 0, Tt = 0;
+    for (int q = 0; q < kW; ++q) {
+      if (q < w) {
+        orr += si[0][q];
+        ot += si[1][q];
+      }
+      Tr += si[0][q];
+      Tt += si[1][q];
+    }
+    if (c >= 0) {
+      const int S = orr + ir - rows, ft = ot + it - ntl;
+      a.cbeg[2 * k] = S;
+      a.cbeg[2 * k + 1] = S + left;
+      a.nbeg[npar][c] = S;
+      a.nbeg[npar][c + 1] = S + left;
+      a.ftile[npar][c] = ft;
+      a.ftile[npar][c + 1] = ft + (left + kExTile - 1) / kExTile;
+      a.ntot[2 * c] = nsum(k, 1);
+      a.ntot[2 * c + 1] = nsum(k, 2);
+      a.ntot[2 * c + 2] = nsum(k, 3);
+      a.ntot[2 * c + 3] = nsum(k, 4);
+    }
+    rcarry += Tr;
+    tcarry += Tt;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.nbeg[npar][Kn] = rcarry;
+    a.ftile[npar][Kn] = tcarry;
+    if (tcarry > a.max_tiles) a.ctl[EX_ERR] = 1;
+    a.ctl[EX_NT0 + npar] = min(tcarry, a.max_tiles);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the children's begins / first tiles are in L2
+  __syncthreads();
+  // the next level's tile table: tile t' of child c (binary search over the children's first tiles)
+  const int ntn = min(tcarry, a.max_tiles);
+  const int* ftn = a.ftile[npar];
+  const int* nbn = a.nbeg[npar];
+  for (int t = tid; t < ntn; t += kExBig) {
+    int lo = 0, hi = Kn - 1;  // last child with ftile <= t (children are non-empty: >= 1 tile)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (ld_agent(ftn + mid) <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int f0 = ld_agent(ftn + lo), b0 = ld_agent(nbn + lo), b1 = ld_agent(nbn + lo + 1);
+    const int p0 = b0 + (t - f0) * kExTile;
+    a.tiles[npar][t] = make_int4(lo, p0, min(b1, p0 + kExTile), 0);
   }
 }
 
 __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
-  const int par = d & 1, t = blockIdx.x, j = blockIdx.y;
-  if (t >= a.ctl[EX_NT0 + par]) return;
+  const int par = d & 1;
+  const int nt = a.ctl[EX_NT0 + par];
+  int j, t;
+  if (!ex_ticket(a, EX_TICKET + 2 * d + 1, nt, j, t)) return;
   const int4 tl = a.tiles[par][t];
   const int k = tl.x;
-  if (a.csplit[k] < 0) return;  // a leaf: its rows leave the order
+  if (a.csplit[k] < 0) return;  // a leaf: its rows leave the order (block-uniform, nobody waits)
   const int* ord = ex_src_ord(a, d, j);
   const float* val = ex_src_val(a, d, j);
-  int* ordo = a.ordw[(d + 1) & 1] + (size_t)j * a.ldw;
-  float* valo = a.valw[(d + 1) & 1] + (size_t)j * a.ldw;
+  const longlong2* qv = ex_src_q(a, d, j);
+  const int no = (d + 1) & 1;
+  int* ordo = a.ordw[no] + (size_t)j * a.ldw;
+  float* valo = a.valw[no] + (size_t)j * a.ldw;
+  longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[no] + (size_t)j * a.ldw * 2);
   const ExSpan sp = ex_span(tl);
   int r[kExPer];
   float v[kExPer];
+  longlong2 x[kExPer];
   unsigned lmask = 0;
   long long nl = 0, np = sp.n;
 #pragma unroll
@@ -542,25 +633,55 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
     if (e < sp.n) {
       r[e] = ord[sp.i0 + e];
       v[e] = val[sp.i0 + e];
+      x[e] = qv[sp.i0 + e];
       if (a.left_row[r[e]] == 1) {
         lmask |= 1u << e;
         ++nl;
       }
     }
   }
-  ex_block_excl2(nl, np);  // lefts / positions of the tile before this thread
-  const long long* tp = a.tpre + ((size_t)j * a.max_tiles + t) * 2;
-  const int lt = (int)tp[0];                   // lefts of the node before this tile
+  long long tl_left, tl_pos;
+  ex_block_excl2(nl, np, tl_left, tl_pos);  // lefts / positions of the tile before this thread
+  __shared__ long long s_lt;
+  unsigned long long* st = a.st_cnt + (size_t)j * a.max_tiles;
+  const int ft = a.ftile[par][k];
+  if (threadIdx.x == 0) {
+    long long ex = 0;
+    if (t == ft) {
+      st_agent(st + t, lb_word(tl_left, 2));
+    } else {
+      st_agent(st + t, lb_word(tl_left, 1));
+      lb_walk<1>(st, t, ft, &ex);
+      st_agent(st + t, lb_word(ex + tl_left, 2));
+    }
+    s_lt = ex;
+  }
+  __syncthreads();
+  const int lt = (int)s_lt;                    // lefts of the node before this tile
   const int before = tl.y - a.nbeg[par][k];    // node positions before this tile
-  int li = a.cbeg[2 * k] + lt + (int)nl;
-  int ri = a.cbeg[2 * k + 1] + (before - lt) + (int)(np - nl);
+  // stage the tile partitioned in LDS (lefts, then rights, each in order), then store both
+  // runs with consecutive lanes on consecutive positions (coalesced)
+  __shared__ int s_r[kExTile];
+  __shared__ float s_v[kExTile];
+  __shared__ longlong2 s_q[kExTile];
+  int li = (int)nl, ri = (int)tl_left + (int)(np - nl);
 #pragma unroll
   for (int e = 0; e < kExPer; ++e) {
     if (e < sp.n) {
       const int dst = (lmask >> e) & 1 ? li++ : ri++;
-      ordo[dst] = r[e];
-      valo[dst] = v[e];
+      s_r[dst] = r[e];
+      s_v[dst] = v[e];
+      s_q[dst] = x[e];
     }
+  }
+  __syncthreads();
+  const int ntile = tl.z - tl.y;
+  const int l0 = a.cbeg[2 * k] + lt, r0 = a.cbeg[2 * k + 1] + (before - lt) - (int)tl_left;
+  for (int i = threadIdx.x; i < ntile; i += kExThreads) {
+    const int dst = i < (int)tl_left ? l0 + i : r0 + i;
+    ordo[dst] = s_r[i];
+    valo[dst] = s_v[i];
+    qo[dst] = s_q[i];
   }
 }
 
@@ -578,9 +699,9 @@ std::vector<ExEngine> g_ex;
 
 extern "C" {
 
-// ptrs: ord0, val0, ordw0, ordw1, valw0, valw1, XT, tiles0, tiles1, nbeg0, nbeg1, ftile0,
-//       ftile1, ctl, tsum, tpre, nbase, nkey, ntot, go_feat, go_thr, csplit, cbeg, left_row,
-//       rec, rec_off, rec_k
+// ptrs: ord0, val0, ordw0, ordw1, valw0, valw1, qvw0, qvw1, XT, tiles0, tiles1, nbeg0, nbeg1,
+//       ftile0, ftile1, ctl, st_gh, st_cnt, tpart, nbase, nkey, ntot, go_feat, go_thr,
+//       csplit, cbeg, left_row, rec, rec_off, rec_k
 // ip:   ld0, ldw, ldx, max_tiles, Kmax, min_split_samples, max_leaf
 // fp:   mcw, l1, l2, max_abs_leaf, min_split_loss, lr
 int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
@@ -593,6 +714,8 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
   a.ordw[1] = (int*)p[i++];
   a.valw[0] = (float*)p[i++];
   a.valw[1] = (float*)p[i++];
+  a.qvw[0] = (long long*)p[i++];
+  a.qvw[1] = (long long*)p[i++];
   a.XT = (const float*)p[i++];
   a.tiles[0] = (int4*)p[i++];
   a.tiles[1] = (int4*)p[i++];
@@ -601,8 +724,9 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
   a.ftile[0] = (int*)p[i++];
   a.ftile[1] = (int*)p[i++];
   a.ctl = (int*)p[i++];
-  a.tsum = (long long*)p[i++];
-  a.tpre = (long long*)p[i++];
+  a.st_gh = (unsigned long long*)p[i++];
+  a.st_cnt = (unsigned long long*)p[i++];
+  a.tpart = (long long*)p[i++];
   a.nbase = (long long*)p[i++];
   a.nkey = (unsigned long long*)p[i++];
   a.ntot = (long long*)p[i++];
@@ -633,9 +757,9 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
 }
 
 // Enqueue one tree: levels 0 .. depth - 1 search and split, level `depth` only records its
-// nodes (leaves). q: [N][2] int64 fixed-point (g, h) with scales (inv_g, inv_h); fidx: the
-// nf searched feature slots (ascending); n: rows in the tree (sampled: ordw[0] / valw[0]
-// hold each slot's kept rows in value order).
+// nodes (leaves). q: [N][2] int64 fixed-point (g, h) with scales (inv_g, inv_h) leaving
+// |sums| < 2^60; fidx: the nf searched feature slots (ascending); n: rows in the tree (sampled:
+// ordw[0] / valw[0] hold each slot's kept rows in value order).
 void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled, double inv_g, double inv_h,
                  int depth, float lr, uintptr_t stream) {
   ExEngine& e = g_ex.at(h);
@@ -649,19 +773,25 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
   a.lr = lr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (nf < 1 || nf > 65535) throw std::invalid_argument("ex_tree: bad feature count");
-  const dim3 tg(a.max_tiles, nf), t1(a.max_tiles);
-  hipLaunchKernelGGL(ex_init_kernel, dim3(1), dim3(kExScanThreads), 0, s, a, n);
+  if (depth < 0 || EX_TICKET + 2 * depth + 2 > EX_CTL_WORDS) throw std::invalid_argument("ex_tree: depth too large");
+  const long long blocks = (long long)a.max_tiles * nf;
+  if (blocks > 0x7fffffffLL) throw std::invalid_argument("ex_tree: too many (tile, feature) blocks");
+  const size_t st_gh_bytes = (size_t)nf * a.max_tiles * 2 * 8, st_cnt_bytes = (size_t)nf * a.max_tiles * 8;
+  hipLaunchKernelGGL(ex_init_kernel, dim3(1), dim3(kExBig), 0, s, a, n);
+  const int gx = std::max(1, std::min((n + kExThreads - 1) / kExThreads, 1024));
+  hipLaunchKernelGGL(ex_gather_kernel, dim3(gx, nf), dim3(kExThreads), 0, s, a, n);
   for (int d = 0; d <= depth; ++d) {
-    const bool last = d == depth;
-    hipLaunchKernelGGL(ex_sums_kernel<0>, last ? dim3(a.max_tiles, 1) : tg, dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_scan_kernel<0>, dim3(last ? 1 : nf), dim3(kExScanThreads), 0, s, a, d);
-    if (!last) hipLaunchKernelGGL(ex_eval_kernel, tg, dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_decide_kernel, dim3(1), dim3(kExScanThreads), 0, s, a, d, last ? 1 : 0);
-    if (last) break;
-    hipLaunchKernelGGL(ex_flag_kernel, t1, dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_sums_kernel<1>, tg, dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_scan_kernel<1>, dim3(nf), dim3(kExScanThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_part_kernel, tg, dim3(kExThreads), 0, s, a, d);
+    if (d == depth) {
+      hipLaunchKernelGGL(ex_decide_kernel, dim3(1), dim3(kExBig), 0, s, a, d, 1);
+      break;
+    }
+    YTK_HIP_CHECK(hipMemsetAsync(a.st_gh, 0, st_gh_bytes, s));
+    YTK_HIP_CHECK(hipMemsetAsync(a.st_cnt, 0, st_cnt_bytes, s));
+    hipLaunchKernelGGL(ex_eval_kernel, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
+    hipLaunchKernelGGL(ex_decide_kernel, dim3(1), dim3(kExBig), 0, s, a, d, 0);
+    hipLaunchKernelGGL(ex_flag_kernel, dim3(a.max_tiles), dim3(kExThreads), 0, s, a, d);
+    hipLaunchKernelGGL(ex_layout_kernel, dim3(1), dim3(kExBig), 0, s, a, d);
+    hipLaunchKernelGGL(ex_part_kernel, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
   }
   YTK_LAUNCH_CHECK();
 }

@@ -153,6 +153,58 @@ __global__ __launch_bounds__(256) void bin_assign_kernel(
   }
 }
 
+// LDS-tiled bin assignment (<= 256 bins, every feature's candidates in LDS): a block loads
+// kBinRows rows of X coalesced into LDS, then thread (f, r) -- r fastest, so the column-major
+// store of a feature is one contiguous run -- binary-searches its value in the LDS table
+// (the same rule as bin_assign_kernel). Replaces per-element searches through L2 and the
+// stride-N byte stores (prep: 5.8 ms at 7 % of HBM bandwidth for Higgs).
+constexpr int kBinRows = 256;
+constexpr int kBinLdsFloats = 8192;  // candidates + X tile
+template <typename BinT>
+__global__ __launch_bounds__(256) void bin_assign_lds_kernel(
+    const float* __restrict__ X, long long xstride, long long N, int F, const float* __restrict__ cand,
+    const int* __restrict__ coff, BinT* __restrict__ out, long long ostride, BinT* __restrict__ outT) {
+  extern __shared__ float s_mem[];
+  const int C = coff[F];
+  float* s_cand = s_mem;            // [C]
+  float* s_x = s_mem + C;           // [kBinRows][F]
+  int* s_off = reinterpret_cast<int*>(s_x + (size_t)kBinRows * F);  // [F + 1]
+  for (int i = threadIdx.x; i < C; i += 256) s_cand[i] = cand[i];
+  for (int i = threadIdx.x; i <= F; i += 256) s_off[i] = coff[i];
+  for (long long r0 = (long long)blockIdx.x * kBinRows; r0 < N; r0 += (long long)gridDim.x * kBinRows) {
+    const int R = (int)min((long long)kBinRows, N - r0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < R * F; i += 256) {
+      const int rr = i / F, f = i - rr * F;
+      s_x[i] = X[(r0 + rr) * xstride + f];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < R * F; i += 256) {
+      const int f = i / R, rr = i - f * R;
+      const float* c = s_cand + s_off[f];
+      const int n = s_off[f + 1] - s_off[f];
+      int idx = 0;
+      if (n > 1) {
+        const float x = s_x[rr * F + f];
+        if (x > c[n - 1]) {
+          idx = n - 1;
+        } else {
+          int lo = 0, hi = n - 1;
+          while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            if (x >= c[mid]) lo = mid + 1; else hi = mid - 1;
+          }
+          const int u = max(0, hi);
+          idx = (c[u] == x) ? u : min(n - 1, lo);
+          if (idx >= 1 && x < (c[idx] + c[idx - 1]) * 0.5f) idx -= 1;
+        }
+      }
+      out[(r0 + rr) * ostride + f] = (BinT)idx;
+      if (outT) outT[(size_t)f * N + r0 + rr] = (BinT)idx;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ loss / grad
 // loss ids: 0 sigmoid, 1 l2, 2 l1, 3 poisson, 4 huber(delta=p0), 5 softmax (K>1)
 // fp64 like the CPU path and the reference (z = score / div + init in double, the
@@ -919,6 +971,18 @@ void ytk_bin_assign(uintptr_t X, long long xstride, long long N, int F, uintptr_
   if (N <= 0) return;
   const int grid = grid_for(N * F, 256 * 16);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int ncand = 0;
+  YTK_HIP_CHECK(hipMemcpyAsync(&ncand, reinterpret_cast<const int*>(coff) + F, sizeof(int), hipMemcpyDeviceToHost, s));
+  YTK_HIP_CHECK(hipStreamSynchronize(s));
+  const size_t lds = ((size_t)ncand + (size_t)kBinRows * F) * sizeof(float) + (size_t)(F + 1) * sizeof(int);
+  const char* lds_env = getenv("YTK_BIN_ASSIGN_LDS");  // "0": the per-element kernel
+  if (bin_bytes == 1 && lds <= 64 * 1024 && !(lds_env && lds_env[0] == '0')) {
+    const int g2 = (int)std::min<long long>((N + kBinRows - 1) / kBinRows, 256 * 8);
+    hipLaunchKernelGGL(bin_assign_lds_kernel<uint8_t>, dim3(g2), dim3(256), lds, s, (const float*)X, xstride, N, F,
+                       (const float*)cand, (const int*)coff, (uint8_t*)out, ostride, (uint8_t*)outT);
+    YTK_LAUNCH_CHECK();
+    return;
+  }
   if (bin_bytes == 1) {
     hipLaunchKernelGGL(bin_assign_kernel<uint8_t>, dim3(grid), dim3(256), 0, s,
                        (const float*)X, xstride, N, F, (const float*)cand, (const int*)coff,

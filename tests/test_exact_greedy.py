@@ -19,7 +19,7 @@ def _brute(X, gh, tp):
     N, F = X.shape
     mcw = float(np.float32(tp.min_child_hessian_sum))
     l2 = float(np.float32(tp.l2))
-    sg, sh = gops.fixed_point_scales(np.abs(gh[:, 0]).max(), np.abs(gh[:, 1]).max(), N)
+    sg, sh = gops.fixed_point_scales(np.abs(gh[:, 0]).max(), np.abs(gh[:, 1]).max(), 4 * N)  # as the maker
     qg = np.round(gh[:, 0].astype(np.float32) * np.float32(sg)).astype(np.int64)
     qh = np.round(gh[:, 1].astype(np.float32) * np.float32(sh)).astype(np.int64)
 

@@ -220,18 +220,24 @@ def test_tree_add_bins_and_forest(cuda):
     torch.testing.assert_close(og6.cpu(), oc6)
 
 
-def test_bin_assign_matches_cpu(cuda):
-    N, F = 30000, 6
+@pytest.mark.parametrize("lds,N,F", [("1", 30000, 6), ("0", 30000, 6), ("1", 70001, 28)])
+def test_bin_assign_matches_cpu(cuda, monkeypatch, lds, N, F):
+    """GPU bin assignment (LDS-tiled kernel by default, the per-element kernel with
+    YTK_BIN_ASSIGN_LDS=0) == the CPU rule, row-major and column-major outputs."""
+    monkeypatch.setenv("YTK_BIN_ASSIGN_LDS", lds)
     X = torch.randn(N, F)
     X[:, 3] = torch.round(X[:, 3] * 2) / 2  # ties with candidates
     cands = [np.sort(np.unique(np.random.default_rng(f).normal(size=50).astype(np.float32))) for f in range(F)]
     cands[3] = np.array([-1.0, -0.5, 0.0, 0.5, 1.0], np.float32)
     cands[5] = np.array([0.0], np.float32)
+    if F > 6:
+        cands[7] = np.sort(np.unique(np.random.default_rng(99).normal(size=255).astype(np.float32)))
     cand = torch.from_numpy(np.concatenate(cands))
     coff = torch.from_numpy(np.concatenate([[0], np.cumsum([len(c) for c in cands])]).astype(np.int32))
     oc = torch.zeros((N, 32), dtype=torch.uint8)
     ocT = torch.zeros((F, N), dtype=torch.uint8)
     gops.bin_assign(X, cand, coff, oc, ocT)
+    assert int(oc.max()) > 4
     og = torch.zeros((N, 32), dtype=torch.uint8, device=cuda)
     ogT = torch.zeros((F, N), dtype=torch.uint8, device=cuda)
     gops.bin_assign(X.to(cuda), cand.to(cuda), coff.to(cuda), og, ogT)

@@ -134,12 +134,14 @@ class ExactGreedyBuilder:
         i64 = lambda n: torch.zeros(max(1, n), dtype=torch.int64, device=dev)  # noqa: E731
         self.ordw = [torch.empty((F, N), dtype=torch.int32, device=dev) for _ in range(2)]
         self.valw = [torch.empty((F, N), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.qvw = [torch.empty((F, N, 2), dtype=torch.int64, device=dev) for _ in range(2)]
         self.ex_tiles = [i32(4 * mt), i32(4 * mt)]
         self.ex_nbeg = [i32(Kmax + 1), i32(Kmax + 1)]
         self.ex_ftile = [i32(Kmax + 1), i32(Kmax + 1)]
-        self.ex_ctl = i32(8)
-        self.ex_tsum, self.ex_tpre = i64(F * mt * 2), i64(F * mt * 2)
-        self.ex_nbase, self.ex_nkey = i64(F * Kmax * 2), i64(F * Kmax)
+        self.ex_ctl = i32(128)
+        self.ex_st_gh, self.ex_st_cnt = i64(F * mt * 2), i64(F * mt)
+        self.ex_tpart = i64(mt * 5)
+        self.ex_nbase, self.ex_nkey = i64((Kmax + 1) * 5), i64(F * Kmax)
         self.ex_ntot = i64(Kmax * 2)
         self.ex_go_feat, self.ex_go_thr = i32(Kmax), torch.zeros(Kmax, dtype=torch.float32, device=dev)
         self.ex_csplit, self.ex_cbeg = i32(Kmax), i32(2 * Kmax)
@@ -151,9 +153,10 @@ class ExactGreedyBuilder:
         self.ex_rec_k = i32(D + 1)
         gp = p.gain_params()
         ptrs = [ptr(self.ord0), ptr(self.val0), ptr(self.ordw[0]), ptr(self.ordw[1]), ptr(self.valw[0]),
-                ptr(self.valw[1]), ptr(self.XT), ptr(self.ex_tiles[0]), ptr(self.ex_tiles[1]), ptr(self.ex_nbeg[0]),
-                ptr(self.ex_nbeg[1]), ptr(self.ex_ftile[0]), ptr(self.ex_ftile[1]), ptr(self.ex_ctl),
-                ptr(self.ex_tsum), ptr(self.ex_tpre), ptr(self.ex_nbase), ptr(self.ex_nkey), ptr(self.ex_ntot),
+                ptr(self.valw[1]), ptr(self.qvw[0]), ptr(self.qvw[1]), ptr(self.XT), ptr(self.ex_tiles[0]),
+                ptr(self.ex_tiles[1]), ptr(self.ex_nbeg[0]), ptr(self.ex_nbeg[1]), ptr(self.ex_ftile[0]),
+                ptr(self.ex_ftile[1]), ptr(self.ex_ctl), ptr(self.ex_st_gh), ptr(self.ex_st_cnt),
+                ptr(self.ex_tpart), ptr(self.ex_nbase), ptr(self.ex_nkey), ptr(self.ex_ntot),
                 ptr(self.ex_go_feat), ptr(self.ex_go_thr), ptr(self.ex_csplit), ptr(self.ex_cbeg), ptr(self.ex_left),
                 ptr(self.ex_rec), ptr(self.ex_rec_off), ptr(self.ex_rec_k)]
         ip = [N, N, N, mt, Kmax, p.min_split_samples, p.max_leaf_cnt]
@@ -201,7 +204,7 @@ class ExactGreedyBuilder:
             n = self.N
             ghk = gh
         mx = ghk.abs().amax(dim=0).double().cpu().numpy() if n > 0 else np.zeros(2)
-        sg, sh = gops.fixed_point_scales(mx[0], mx[1], max(n, 1))
+        sg, sh = gops.fixed_point_scales(mx[0], mx[1], 4 * max(n, 1))  # |sums| < 2^60 (look-back words)
         q = torch.empty((self.N, 2), dtype=torch.int64, device=dev)
         q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
         q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)
@@ -273,7 +276,8 @@ class ExactGreedyBuilder:
         # exact int64 fixed point (g, h): order-independent sums, the histogram path's scales
         ghk = gh if keep is None else gh[keep]
         mx = ghk.abs().amax(dim=0).double().cpu().numpy() if n > 0 else np.zeros(2)
-        sg, sh = gops.fixed_point_scales(mx[0], mx[1], max(n, 1))
+        # the HIP engine's scales (|sums| < 2^60): both engines build identical trees
+        sg, sh = gops.fixed_point_scales(mx[0], mx[1], 4 * max(n, 1))
         q = torch.empty((self.N, 2), dtype=torch.int64, device=dev)
         q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
         q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)

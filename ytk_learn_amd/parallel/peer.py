@@ -77,15 +77,51 @@ class PeerReduce:
                 ok = 0.0
                 err = e
         agreed = comm.allreduce_scalars([ok], op="min")[0] > 0.5
-        if not agreed:
-            if hnd is not None:
-                h.peer_destroy(hnd)
-            if comm.is_master:
-                why = f"{type(err).__name__}: {err}" if not ok else "another rank could not open its peers"
-                print(f"[ytk] peer-memory exchange unavailable ({why}); histogram messages use RCCL", flush=True)
-            return None
-        comm.barrier()
-        return cls(comm, hnd, cap)
+        if agreed:
+            # self-test before any engine relies on the path: two exchanges of known int64 and
+            # fp64 data under a short flag timeout (a path that cannot deliver -- e.g. peer
+            # memory that is not coherent across these devices -- votes for RCCL instead of
+            # producing wrong histograms or hanging the job)
+            pr = cls(comm, hnd, cap)
+            try:
+                ok = 1.0 if pr._self_test() else 0.0
+                if not ok:
+                    err = RuntimeError("self-test exchange returned wrong sums")
+            except Exception as e:  # noqa: BLE001
+                ok, err = 0.0, e
+            agreed = comm.allreduce_scalars([ok], op="min")[0] > 0.5
+            if agreed:
+                return pr
+        if hnd is not None:
+            torch.cuda.synchronize(comm.device)
+            comm.barrier()
+            h.peer_destroy(hnd)
+        if comm.is_master:
+            why = f"{type(err).__name__}: {err}" if err is not None else "another rank could not use its peers"
+            print(f"[ytk] peer-memory exchange unavailable ({why}); histogram messages use RCCL", flush=True)
+        return None
+
+    def _self_test(self) -> bool:
+        P, r = self.comm.world, self.comm.rank
+        saved = self.TIMEOUT_S
+        self.TIMEOUT_S = min(saved, 10.0)
+        try:
+            n = min(self.cap, 4099)  # odd: the single-element tail too
+            t = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P + r + 1
+            f = torch.full((5,), 0.5 * (r + 1), dtype=torch.float64, device=self.comm.device)
+            self.allreduce_(t)
+            self.allreduce_(f)
+            torch.cuda.synchronize(self.comm.device)
+            self.check()
+            want = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P * P + P * (P + 1) // 2
+            return bool(torch.equal(t, want)) and bool(torch.all(f == 0.25 * P * (P + 1)))
+        finally:
+            self.TIMEOUT_S = saved
+            self.calls = 0
+            self.comm.stats["calls"] -= 2
+            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5)
+            if self.comm.log is not None:
+                del self.comm.log[-2:]
 
     def _account(self, t: torch.Tensor, n: int):
         self.calls += 1
