@@ -99,52 +99,60 @@ void ytk_owner_unpack(uintptr_t out, uintptr_t hist, int nslots, int B, int F, i
 }  // extern "C"
 
 // ------------------------------------------------------------------ peer-memory exchange
-// Latency-optimised all-reduce of the tree engines' level / batch messages over peer memory
-// (xGMI), in ONE kernel per exchange and without the host: mp4j's histogram collectives were
-// latency-optimised recursive-halving / Rabenseifner algorithms (docs/gbdt_features.md:36,
-// 142-143; HistogramBuilder.java:95); at a 1/8 shard a level's build is 10-20 us, so the
-// exchange's latency sets the multi-GPU tree time.
+// All-reduce of the tree engines' level / batch messages and of the L-BFGS gradients over
+// peer memory (xGMI), in ONE kernel per exchange and without the host: mp4j's collectives
+// were latency-optimised recursive-halving / Rabenseifner algorithms for small messages and
+// bandwidth-optimal ones for large (docs/gbdt_features.md:36,142-143; HistogramBuilder.java:95;
+// HoagOptimizer.java:1038); at a 1/8 shard a level's build is 10-20 us, so the exchange's
+// latency sets the multi-GPU tree time, while a 68-628 MB gradient needs every xGMI link.
 //
 // Every rank owns ONE uncached device allocation (hipDeviceMallocUncached: no cache level
 // holds its lines, so data handed between processes never meets a stale line on any XCD)
-//     [flag words: kPeerMax x kXchgGrid u64 | send slab 0 | send slab 1]
-// exported with hipIpcGetMemHandle and opened by every other rank. An exchange of n
-// elements (int64 histogram / count words, or fp64 loss sums) runs G blocks; block b owns
-// chunk b = [n*b/G, n*(b+1)/G) and
-//   1. copies its chunk of the message from the engine's buffer into this rank's send slab
-//      (slab parity = exchange epoch & 1), waits for its stores, releases at system scope
-//      and stamps the epoch into flag word [rank][b] of EVERY rank (remote stores);
-//   2. waits until its own flag words [q][b] of all P ranks reach the epoch;
-//   3. sums chunk b of all P send slabs in rank order (identical bits on every rank; int64
-//      sums are exact) and writes the sums back in place.
-// So the pack, both barriers of a two-shot all-reduce, the reduce and the unpack are one
-// launch, and a message can be described by device words (the leaf-wise batch: its built
-// slots + split cursors, counted by the planner) -- no host round trip per batch.
+//   [send flags: kPeerMax x kXchgGrid u64 | result flags: same | send slab 0, 1 | result slab 0, 1]
+// exported with hipIpcGetMemHandle and opened by every other rank. A message is n elements
+// (int64 histogram / count words, fp64 or fp32 sums) moved in 16-byte units; an exchange runs
+// G blocks and, by its size (the same on every rank, so every rank takes the same path):
+//  one-shot (small messages: latency): block b copies chunk b of the message into this rank's
+//    send slab, releases it and stamps the epoch into send flag [rank][b] of EVERY rank, waits
+//    for the peers' flags of chunk b, then sums chunk b of all P slabs in rank order (this
+//    rank's own term from its buffer) and writes the sums back in place.
+//  two-shot (large messages: bandwidth): rank q owns the q-th 1/P of the units; block b
+//    publishes sub-chunk b of EVERY owner's range, waits for the peers' flags, sums sub-chunk
+//    b of its OWN range over the P slabs (rank order), writes it in place and into its result
+//    slab, stamps result flag [rank][b] everywhere, then copies sub-chunk b of every other
+//    owner's result slab in place once that owner's flag is up. Each rank reads
+//    2 (P - 1) / P of the message instead of P - 1 messages, spread over every peer's link.
+// int64 sums are exact (bitwise the RCCL result); fp64 / fp32 sums are taken in rank order,
+// identical on every rank. A message may be described by device words (the leaf-wise batch:
+// its built slots + split cursors, counted by the planner) -- no host round trip per batch.
 //
-// Reuse of a send slab: exchange e writes slab e & 1, exchange e + 2 writes it again. Block
-// 0 takes part in every exchange, so during exchange e + 1 this rank saw a flag e + 1 of
-// every peer, stamped after that peer's exchange-e kernel (which read our slab) had
+// Slab reuse: exchange e writes slab e & 1, exchange e + 2 writes it again. Block 0 takes
+// part in every exchange (both phases), so during exchange e + 1 this rank saw a flag e + 1
+// of every peer, stamped after that peer's exchange-e kernel (which read our slabs) had
 // completed (stream order). Exchanges a rank skips (device-side skip word, e.g. the leaf-wise
 // batches queued after the tree finished) advance no epoch; the skip word is identical on
-// every rank because every rank takes the identical planning decisions.
-// The epoch lives in device memory (advanced by each exchange's last block), so a captured
-// HIP graph replays with fresh epochs. Waits are bounded in wall-clock time: a timed-out
-// wait sets the error word (host-mapped; checked where rounds land) and the kernel finishes,
-// and every later exchange of the group returns at once, so a lost peer never hangs the GPU.
+// every rank because every rank takes the identical planning decisions. The epoch lives in
+// device memory (advanced by each exchange's last block), so a captured HIP graph replays
+// with fresh epochs. Waits are bounded in wall-clock time: a timed-out wait sets the error
+// word (host-mapped; checked where rounds land) and the kernel finishes, and every later
+// exchange of the group returns at once, so a lost peer never hangs the GPU.
 namespace ytk {
 constexpr int kPeerMax = 16;
 constexpr int kXchgGrid = 256;     // max blocks of one exchange (flag words per rank)
 constexpr int kXchgThreads = 256;
+enum { XT_I64 = 0, XT_F64 = 1, XT_F32 = 2 };
 
 struct PeerPtrs {
-  long long* send[kPeerMax][2];
-  unsigned long long* sig[kPeerMax];  // [kPeerMax][kXchgGrid] flag words of each rank
+  char* send[kPeerMax][2];
+  char* res[kPeerMax][2];
+  unsigned long long* sig[kPeerMax];   // [kPeerMax][kXchgGrid] send flags of each rank
+  unsigned long long* rsig[kPeerMax];  // [kPeerMax][kXchgGrid] result flags
 };
 
-// The message: contiguous (n >= 0: base[0..n)) or a leaf-wise batch (n < 0: the *nb_dev
-// slots listed in ids, slot_elems words each, then *k_dev * cur_stride cursor words).
+// The message: contiguous (n >= 0: base[0..n)) or a leaf-wise batch of int64 words (n < 0:
+// the *nb_dev slots listed in ids, slot_elems words each, then *k_dev * cur_stride cursors).
 struct XchgMsg {
-  long long* base;
+  char* base;
   long long n;
   long long* hist;
   const int* ids;
@@ -156,37 +164,112 @@ struct XchgMsg {
   const int* skip;  // non-null and non-zero: no exchange
 };
 
-__device__ __forceinline__ long long* xchg_elem(const XchgMsg& m, long long i, long long nh) {
-  if (m.n >= 0) return m.base + i;
+typedef long long xv2 __attribute__((ext_vector_type(2)));  // nontemporal builtins need a native vector
+
+// unit u (16 bytes) of the message; gather mode: int64 pairs (slot sizes and cursor strides
+// are even, every slot 16-B aligned)
+__device__ __forceinline__ xv2* xchg_unit(const XchgMsg& m, long long u, long long nh) {
+  if (m.n >= 0) return reinterpret_cast<xv2*>(m.base) + u;
+  const long long i = 2 * u;
   if (i < nh) {
     const long long kb = i / m.slot_elems;
-    return m.hist + (size_t)m.ids[kb] * m.slot_elems + (i - kb * m.slot_elems);
+    return reinterpret_cast<xv2*>(m.hist + (size_t)m.ids[kb] * m.slot_elems + (i - kb * m.slot_elems));
   }
-  return m.cursor + (i - nh);
+  return reinterpret_cast<xv2*>(m.cursor + (i - nh));
 }
 
-// 16-byte units: pairs of consecutive elements (slot sizes, cursor strides and every
-// contiguous message start are even / 16-B aligned); an odd contiguous message's last element
-// goes alone (block G - 1)
-typedef long long xv2 __attribute__((ext_vector_type(2)));  // nontemporal builtins need a native vector
-__device__ __forceinline__ xv2* xchg_pair(const XchgMsg& m, long long u, long long nh) {
-  return reinterpret_cast<xv2*>(xchg_elem(m, 2 * u, nh));
+template <int kType>
+__device__ __forceinline__ xv2 unit_add(xv2 a, xv2 b) {
+  if (kType == XT_I64) return a + b;
+  if (kType == XT_F64) {
+    xv2 r;
+    r.x = __double_as_longlong(__longlong_as_double(a.x) + __longlong_as_double(b.x));
+    r.y = __double_as_longlong(__longlong_as_double(a.y) + __longlong_as_double(b.y));
+    return r;
+  }
+  float fa[4], fb[4];
+  __builtin_memcpy(fa, &a, 16);
+  __builtin_memcpy(fb, &b, 16);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fa[k] += fb[k];
+  xv2 r;
+  __builtin_memcpy(&r, fa, 16);
+  return r;
 }
 
-template <bool kF64>
-__device__ __forceinline__ long long xchg_add(long long a, long long b) {
-  if (kF64) return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
-  return a + b;
+// one element of the (contiguous) tail, summed in rank order
+template <int kType>
+__device__ __forceinline__ void tail_sum(char* dst, char* const* src, int P, int rank) {
+  if (kType == XT_F32) {
+    float s = 0.f;
+    for (int q = 0; q < P; ++q) s += q == rank ? *(float*)dst : __builtin_nontemporal_load((const float*)src[q]);
+    *(float*)dst = s;
+  } else if (kType == XT_F64) {
+    double s = 0.0;
+    for (int q = 0; q < P; ++q) s += q == rank ? *(double*)dst : __builtin_nontemporal_load((const double*)src[q]);
+    *(double*)dst = s;
+  } else {
+    long long s = 0;
+    for (int q = 0; q < P; ++q)
+      s += q == rank ? *(long long*)dst : __builtin_nontemporal_load((const long long*)src[q]);
+    *(long long*)dst = s;
+  }
 }
 
-template <bool kF64, bool kSysFence>
+// stamp flag [rank][b] = e into every peer's array; wait for [q][b] >= e of every peer
+__device__ __forceinline__ void flag_publish(unsigned long long* const* sig, int P, int rank, int b,
+                                             unsigned long long e) {
+  const int t = threadIdx.x;
+  if (t < P && t != rank)
+    __hip_atomic_store(sig[t] + (size_t)rank * kXchgGrid + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void flag_wait(unsigned long long* const* sig, int P, int rank, int b, unsigned long long e,
+                                          int* err, unsigned long long* ctl, long long timeout_ticks, int only = -1) {
+  const int t = threadIdx.x;
+  if (t < P && t != rank && (only < 0 || t == only)) {
+    const unsigned long long* w = sig[rank] + (size_t)t * kXchgGrid + b;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((long long)(wall_clock64() - t0) > timeout_ticks) {
+        atomicExch(err, 1);
+        atomicExch(ctl + 2, 1ull);
+        break;
+      }
+    }
+  }
+}
+
+// the block's stores are acknowledged and released before its flags go out
+template <bool kSysFence>
+__device__ __forceinline__ void publish_fence() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (kSysFence) {
+    if (threadIdx.x == 0) __threadfence_system();
+    __syncthreads();
+  }
+}
+template <bool kSysFence>
+__device__ __forceinline__ void acquire_fence() {
+  __syncthreads();
+  if (kSysFence) {
+    if (threadIdx.x == 0) __threadfence_system();
+    __syncthreads();
+  }
+}
+
+template <int kType, bool kSysFence>
 __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, int P, int rank, XchgMsg m,
-                                                                 long long cap, unsigned long long* __restrict__ ctl,
-                                                                 int* __restrict__ err, long long timeout_ticks) {
+                                                                 long long cap_bytes, unsigned long long* __restrict__ ctl,
+                                                                 int* __restrict__ err, long long timeout_ticks,
+                                                                 long long two_shot_bytes) {
   if (m.skip != nullptr && *m.skip != 0) return;
   // after a timed-out wait (ctl[2] != 0) every later exchange returns at once: the job is
   // failing (the host check raises), so nothing waits again
   if (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  constexpr int ES = kType == XT_F32 ? 4 : 8;  // element bytes
+  constexpr int U = 16 / ES;                   // elements per unit
   __shared__ unsigned long long s_e;
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   long long n = m.n, nh = 0;
@@ -197,70 +280,91 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
   if (t == 0) s_e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
   const unsigned long long e = s_e;
-  if (n > cap) {  // identical on every rank: nobody exchanges, the host check raises
+  if (n * ES > cap_bytes) {  // identical on every rank: nobody exchanges, the host check raises
     if (b == 0 && t == 0) atomicExch(err, 2);
     n = 0;
   }
-  const long long nu = n >> 1;  // 16-byte units
-  const bool odd = (n & 1) != 0 && b == G - 1;
-  const long long lo = nu * b / G, hi = nu * (b + 1) / G;
-  if (hi > lo || odd || b == 0) {
-    const int par = (int)(e & 1ull);
-    xv2* mine = reinterpret_cast<xv2*>(pp.send[rank][par]);
-    // 1. publish this block's chunk: slab stores, acknowledged, then the flags
-    for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_pair(m, u, nh), mine + u);
-    if (odd && t == 0) __builtin_nontemporal_store(*xchg_elem(m, n - 1, nh), pp.send[rank][par] + n - 1);
-    __builtin_amdgcn_s_waitcnt(0);  // this thread's slab stores are acknowledged
-    __syncthreads();
-    if (kSysFence) {
-      if (t == 0) __threadfence_system();
-      __syncthreads();
+  const long long nu = n / U;       // 16-byte units
+  const int tail = (int)(n - nu * U);  // contiguous messages only (gather messages are even)
+  const bool tail_blk = tail > 0 && b == G - 1;
+  const int par = (int)(e & 1ull);
+  xv2* mine = reinterpret_cast<xv2*>(pp.send[rank][par]);
+  const bool two = nu * 16 >= two_shot_bytes && P > 1;
+  if (!two) {
+    const long long lo = nu * b / G, hi = nu * (b + 1) / G;
+    if (!(hi > lo || tail_blk || b == 0)) goto done;
+    for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_unit(m, u, nh), mine + u);
+    if (tail_blk && t < tail) {
+      const long long off = (nu * U + t) * ES;
+      __builtin_memcpy(pp.send[rank][par] + off, m.base + off, ES);
     }
-    if (t < P && t != rank)
-      __hip_atomic_store(pp.sig[t] + (size_t)rank * kXchgGrid + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // 2. wait for every peer's flag of this chunk
-    if (t < P && t != rank) {
-      const unsigned long long* w = pp.sig[rank] + (size_t)t * kXchgGrid + b;
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((long long)(wall_clock64() - t0) > timeout_ticks) {
-          atomicExch(err, 1);
-          atomicExch(ctl + 2, 1ull);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (kSysFence) {
-      if (t == 0) __threadfence_system();
-      __syncthreads();
-    }
-    // 3. sum the chunk over the ranks in rank order (this rank's own term from its buffer)
+    publish_fence<kSysFence>();
+    flag_publish(pp.sig, P, rank, b, e);
+    flag_wait(pp.sig, P, rank, b, e, err, ctl, timeout_ticks);
+    acquire_fence<kSysFence>();
     for (long long u = lo + t; u < hi; u += kXchgThreads) {
-      xv2* dst = xchg_pair(m, u, nh);
-      xv2 s = {0, 0};
-      for (int q = 0; q < P; ++q) {
+      xv2* dst = xchg_unit(m, u, nh);
+      xv2 s = *dst;
+      if (rank > 0) s = __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[0][par]) + u);
+      for (int q = 1; q < P; ++q) {
         const xv2 v = q == rank ? *dst : __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[q][par]) + u);
-        if (q == 0) {
-          s = v;
-        } else {
-          s.x = xchg_add<kF64>(s.x, v.x);
-          s.y = xchg_add<kF64>(s.y, v.y);
-        }
+        s = unit_add<kType>(s, v);
       }
       *dst = s;
     }
-    if (odd && t == 0) {
-      long long* dst = xchg_elem(m, n - 1, nh);
-      long long s = 0;
-      for (int q = 0; q < P; ++q) {
-        const long long v = q == rank ? *dst : __builtin_nontemporal_load(pp.send[q][par] + n - 1);
-        s = q == 0 ? v : xchg_add<kF64>(s, v);
+  } else {
+    // ---- two-shot: owner q's units [nu q / P, nu (q + 1) / P), sub-chunk b of each
+    auto sub = [&](int q, long long& lo, long long& hi) {
+      const long long a = nu * q / P, z = nu * (q + 1) / P;
+      lo = a + (z - a) * b / G;
+      hi = a + (z - a) * (b + 1) / G;
+    };
+    long long lo, hi;
+    for (int q = 0; q < P; ++q) {  // publish sub-chunk b of every owner's range
+      sub(q, lo, hi);
+      for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_unit(m, u, nh), mine + u);
+    }
+    if (tail_blk && t < tail) {
+      const long long off = (nu * U + t) * ES;
+      __builtin_memcpy(pp.send[rank][par] + off, m.base + off, ES);
+    }
+    publish_fence<kSysFence>();
+    flag_publish(pp.sig, P, rank, b, e);
+    flag_wait(pp.sig, P, rank, b, e, err, ctl, timeout_ticks);
+    acquire_fence<kSysFence>();
+    // reduce this rank's sub-chunk b; result in place + into the result slab
+    sub(rank, lo, hi);
+    xv2* rmine = reinterpret_cast<xv2*>(pp.res[rank][par]);
+    for (long long u = lo + t; u < hi; u += kXchgThreads) {
+      xv2* dst = xchg_unit(m, u, nh);
+      xv2 s = *dst;
+      if (rank > 0) s = __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[0][par]) + u);
+      for (int q = 1; q < P; ++q) {
+        const xv2 v = q == rank ? *dst : __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[q][par]) + u);
+        s = unit_add<kType>(s, v);
       }
       *dst = s;
+      __builtin_nontemporal_store(s, rmine + u);
+    }
+    publish_fence<kSysFence>();
+    flag_publish(pp.rsig, P, rank, b, e);
+    // the other owners' reduced sub-chunks b, each as soon as its owner's flag is up
+    for (int q = 0; q < P; ++q) {
+      if (q == rank) continue;
+      flag_wait(pp.rsig, P, rank, b, e, err, ctl, timeout_ticks, q);
+      acquire_fence<kSysFence>();
+      sub(q, lo, hi);
+      const xv2* rq = reinterpret_cast<const xv2*>(pp.res[q][par]);
+      for (long long u = lo + t; u < hi; u += kXchgThreads) *xchg_unit(m, u, nh) = __builtin_nontemporal_load(rq + u);
     }
   }
+  if (tail_blk && t < tail) {  // the last < 16 bytes: every rank sums them itself (block G - 1
+    const long long off = (nu * U + t) * ES;  // waited for every peer's block G - 1 above)
+    char* src[kPeerMax];
+    for (int q = 0; q < P; ++q) src[q] = pp.send[q][par] + off;
+    tail_sum<kType>(m.base + off, src, P, rank);
+  }
+done:
   // the last block to finish advances the epoch (the next exchange kernel starts after this
   // one has completed, so every block of it reads the new value)
   __syncthreads();
@@ -275,14 +379,15 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
 
 struct PeerGroup {
   int P = 0, rank = 0;
-  long long cap = 0;     // elements per send slab
+  long long cap = 0;     // bytes per slab
   char* base = nullptr;  // own uncached allocation
   std::vector<void*> opened;
   PeerPtrs pp{};
   unsigned long long* ctl = nullptr;  // device: [0] last epoch, [1] block arrivals, [2] timed out
   long long ticks_per_s = 100000000;  // wall_clock64 rate
   bool sys_fence = true;              // YTK_PEER_SYS_FENCE=0: waitcnt-ordered publishing only
-  int block_elems = 2048;             // YTK_PEER_BLOCK_ELEMS: elements per block
+  int block_bytes = 16384;            // YTK_PEER_BLOCK_BYTES: message bytes per block
+  long long two_shot_bytes = 1 << 20;  // YTK_PEER_TWO_SHOT_BYTES: two-shot from this size on
   int* err_host = nullptr;            // host-mapped error word
   int* err = nullptr;                 // its device address
 };
@@ -291,18 +396,22 @@ static std::vector<ytk::PeerGroup> g_peer;
 namespace ytk {
 
 static size_t peer_sig_bytes() { return (size_t)kPeerMax * kXchgGrid * 8; }
-static size_t peer_bytes(long long cap) { return peer_sig_bytes() + 2 * (size_t)cap * 8; }
+static size_t peer_bytes(long long cap) { return 2 * peer_sig_bytes() + 4 * (size_t)cap; }
 
-static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int f64, double timeout_s, hipStream_t s) {
+static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int type, double timeout_s, hipStream_t s) {
   grid = std::max(1, std::min(grid, kXchgGrid));
   const long long ticks = (long long)(timeout_s * (double)g.ticks_per_s);
-#define YTK_XCHG(F, S)                                                                                   \
-  hipLaunchKernelGGL((peer_xchg_kernel<F, S>), dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, g.cap, \
-                     g.ctl, g.err, ticks)
+#define YTK_XCHG(T, S)                                                                                     \
+  hipLaunchKernelGGL((peer_xchg_kernel<T, S>), dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, \
+                     g.cap, g.ctl, g.err, ticks, g.two_shot_bytes)
   if (g.sys_fence) {
-    if (f64) YTK_XCHG(true, true); else YTK_XCHG(false, true);
+    if (type == XT_F64) YTK_XCHG(XT_F64, true);
+    else if (type == XT_F32) YTK_XCHG(XT_F32, true);
+    else YTK_XCHG(XT_I64, true);
   } else {
-    if (f64) YTK_XCHG(true, false); else YTK_XCHG(false, false);
+    if (type == XT_F64) YTK_XCHG(XT_F64, false);
+    else if (type == XT_F32) YTK_XCHG(XT_F32, false);
+    else YTK_XCHG(XT_I64, false);
   }
 #undef YTK_XCHG
   YTK_LAUNCH_CHECK();
@@ -312,19 +421,19 @@ static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int f64, doubl
 
 extern "C" {
 
-// Allocate this rank's uncached [flags | send 0 | send 1] block for messages of up to cap
-// elements; returns a group handle. The exported IPC handle (64 bytes) goes to out_handle.
+// Allocate this rank's uncached [flags | send 0, 1 | result 0, 1] block for messages of up to
+// cap bytes; returns a group handle. The exported IPC handle (64 bytes) goes to out_handle.
 int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   if (P < 1 || P > ytk::kPeerMax || rank < 0 || rank >= P || cap <= 0)
     throw std::invalid_argument("peer_create: bad group");
-  cap = (cap + 1) & ~1LL;  // both slabs 16-B aligned
+  cap = (cap + 255) & ~255LL;  // every slab 256-B aligned
   ytk::PeerGroup g;
   g.P = P;
   g.rank = rank;
   g.cap = cap;
   void* p = nullptr;
   YTK_HIP_CHECK(hipExtMallocWithFlags(&p, ytk::peer_bytes(cap), hipDeviceMallocUncached));
-  YTK_HIP_CHECK(hipMemset(p, 0, ytk::peer_bytes(cap)));
+  YTK_HIP_CHECK(hipMemset(p, 0, 2 * ytk::peer_sig_bytes()));
   g.base = (char*)p;
   YTK_HIP_CHECK(hipMalloc(&g.ctl, 4 * sizeof(unsigned long long)));
   YTK_HIP_CHECK(hipMemset(g.ctl, 0, 4 * sizeof(unsigned long long)));
@@ -333,7 +442,8 @@ int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
     g.ticks_per_s = (long long)khz * 1000;
   if (const char* e = getenv("YTK_PEER_SYS_FENCE")) g.sys_fence = e[0] != '0';
-  if (const char* e = getenv("YTK_PEER_BLOCK_ELEMS")) g.block_elems = std::max(256, atoi(e));
+  if (const char* e = getenv("YTK_PEER_BLOCK_BYTES")) g.block_bytes = std::max(1024, atoi(e));
+  if (const char* e = getenv("YTK_PEER_TWO_SHOT_BYTES")) g.two_shot_bytes = std::max(0LL, atoll(e));
   YTK_HIP_CHECK(hipHostMalloc(&g.err_host, sizeof(int), hipHostMallocMapped));
   *g.err_host = 0;
   void* dp = nullptr;
@@ -351,6 +461,7 @@ int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
 void ytk_peer_open(int hnd, uintptr_t handles) {
   ytk::PeerGroup& g = g_peer.at(hnd);
   const char* hs = reinterpret_cast<const char*>(handles);
+  const size_t sb = ytk::peer_sig_bytes();
   for (int q = 0; q < g.P; ++q) {
     char* b = nullptr;
     if (q == g.rank) {
@@ -364,22 +475,27 @@ void ytk_peer_open(int hnd, uintptr_t handles) {
       b = (char*)p;
     }
     g.pp.sig[q] = reinterpret_cast<unsigned long long*>(b);
-    g.pp.send[q][0] = reinterpret_cast<long long*>(b + ytk::peer_sig_bytes());
-    g.pp.send[q][1] = reinterpret_cast<long long*>(b + ytk::peer_sig_bytes() + (size_t)g.cap * 8);
+    g.pp.rsig[q] = reinterpret_cast<unsigned long long*>(b + sb);
+    for (int k = 0; k < 2; ++k) {
+      g.pp.send[q][k] = b + 2 * sb + (size_t)k * g.cap;
+      g.pp.res[q][k] = b + 2 * sb + (size_t)(2 + k) * g.cap;
+    }
   }
 }
 
-// data[0:n] <- the element-wise sum over the group's ranks (int64, or fp64 when f64), in
-// place, on `stream`: one kernel launch. n must be identical on every rank.
-void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int f64, double timeout_s, uintptr_t stream) {
+// data[0:n] <- the element-wise sum over the group's ranks, in place, on `stream`: one kernel
+// launch. type: 0 int64, 1 fp64, 2 fp32. n must be identical on every rank.
+void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream) {
   ytk::PeerGroup& g = g_peer.at(hnd);
   if (n <= 0 || g.P == 1) return;  // a one-rank all-reduce is the identity
-  if (n > g.cap) throw std::invalid_argument("peer_allreduce: message larger than the slab");
+  const long long bytes = n * (type == ytk::XT_F32 ? 4 : 8);
+  if (bytes > g.cap) throw std::invalid_argument("peer_allreduce: message larger than the slab");
+  if (data % 16 != 0) throw std::invalid_argument("peer_allreduce: data must be 16-B aligned");
   ytk::XchgMsg m{};
-  m.base = reinterpret_cast<long long*>(data);
+  m.base = reinterpret_cast<char*>(data);
   m.n = n;
-  const int grid = (int)std::min<long long>((n + g.block_elems - 1) / g.block_elems, ytk::kXchgGrid);
-  ytk::peer_launch(g, m, grid, f64, timeout_s, reinterpret_cast<hipStream_t>(stream));
+  const int grid = (int)std::min<long long>((bytes + g.block_bytes - 1) / g.block_bytes, ytk::kXchgGrid);
+  ytk::peer_launch(g, m, grid, type, timeout_s, reinterpret_cast<hipStream_t>(stream));
 }
 
 // Leaf-wise batch message counted on the device: the *nb_dev built slots listed in ids
@@ -390,6 +506,7 @@ void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uin
                               uintptr_t stream) {
   ytk::PeerGroup& g = g_peer.at(hnd);
   if (g.P == 1) return;  // a one-rank all-reduce is the identity
+  if ((slot_elems & 1) || (cur_stride & 1)) throw std::invalid_argument("peer_allreduce_slots: odd slot / stride");
   ytk::XchgMsg m{};
   m.n = -1;
   m.hist = reinterpret_cast<long long*>(hist);
@@ -400,7 +517,7 @@ void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uin
   m.cursor = reinterpret_cast<long long*>(cursor);
   m.cur_stride = cur_stride;
   m.skip = reinterpret_cast<const int*>(skip);
-  ytk::peer_launch(g, m, ytk::kXchgGrid, 0, timeout_s, reinterpret_cast<hipStream_t>(stream));
+  ytk::peer_launch(g, m, ytk::kXchgGrid, ytk::XT_I64, timeout_s, reinterpret_cast<hipStream_t>(stream));
 }
 
 // the host-mapped error word (1: a flag wait timed out, 2: a device-counted message exceeded

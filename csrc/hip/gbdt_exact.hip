@@ -127,28 +127,29 @@ __device__ __forceinline__ unsigned long long lb_word(long long v, int flag) {
 }
 __device__ __forceinline__ long long lb_value(unsigned long long w) { return (long long)w >> 2; }
 
-// Exclusive prefix of tile t inside its node (tiles ft..t-1) for C components, by thread 0:
-// walks back until an inclusive prefix; tiles with lower tickets always publish first.
+// Exclusive prefix of tile t inside its node (tiles ft..t-1) for C components, by one wave:
+// the 64 lanes read a window of 64 predecessors at once (each lane spins until its tile has
+// published), the window's nearest inclusive prefix ends the walk, else the window's
+// aggregates are added and the next 64 are read. Tiles with lower tickets always publish
+// first, and the node's first tile publishes its inclusive prefix directly. Result in every lane.
 template <int C>
 __device__ __forceinline__ void lb_walk(const unsigned long long* st, int t, int ft, long long* excl) {
-  bool done[C];
+  const int l = lane_id();
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    excl[c] = 0;
-    done[c] = false;
-  }
-  for (int p = t - 1; p >= ft; --p) {
-    bool all = true;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (done[c]) continue;
-      unsigned long long w;
-      while (((w = ld_agent(st + (size_t)p * C + c)) & 3ull) == 0ull) __builtin_amdgcn_s_sleep(1);
-      excl[c] += lb_value(w);
-      if ((w & 3ull) == 2ull) done[c] = true;
-      all = all && done[c];
+    long long acc = 0;
+    for (int hi = t - 1; hi >= ft; hi -= kWave) {
+      const int p = hi - l;
+      unsigned long long w = 0;
+      if (p >= ft)
+        while (((w = ld_agent(st + (size_t)p * C + c)) & 3ull) == 0ull) __builtin_amdgcn_s_sleep(1);
+      const unsigned long long pm = __ballot(p >= ft && (w & 3ull) == 2ull);
+      const int stop = pm ? __builtin_ctzll(pm) : kWave;  // nearest predecessor with a prefix
+      const long long v = (p >= ft && l <= stop) ? lb_value(w) : 0;
+      acc += readlane64(dpp_scan_add(v), kWave - 1);
+      if (pm) break;
     }
-    if (all) break;
+    excl[c] = acc;
   }
 }
 
@@ -305,20 +306,28 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
   ex_block_excl2(lg, lh, ag, ah);  // (+ barrier: s_last visible)
   unsigned long long* st = a.st_gh + (size_t)j * a.max_tiles * 2;
   const int ft = a.ftile[par][k];
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < kWave) {  // wave 0: publish, look back, publish the inclusive prefix
     long long ex[2] = {0, 0};
     if (t == ft) {
-      st_agent(st + 2 * t, lb_word(ag, 2));
-      st_agent(st + 2 * t + 1, lb_word(ah, 2));
+      if (threadIdx.x == 0) {
+        st_agent(st + 2 * t, lb_word(ag, 2));
+        st_agent(st + 2 * t + 1, lb_word(ah, 2));
+      }
     } else {
-      st_agent(st + 2 * t, lb_word(ag, 1));
-      st_agent(st + 2 * t + 1, lb_word(ah, 1));
+      if (threadIdx.x == 0) {
+        st_agent(st + 2 * t, lb_word(ag, 1));
+        st_agent(st + 2 * t + 1, lb_word(ah, 1));
+      }
       lb_walk<2>(st, t, ft, ex);
-      st_agent(st + 2 * t, lb_word(ex[0] + ag, 2));
-      st_agent(st + 2 * t + 1, lb_word(ex[1] + ah, 2));
+      if (threadIdx.x == 0) {
+        st_agent(st + 2 * t, lb_word(ex[0] + ag, 2));
+        st_agent(st + 2 * t + 1, lb_word(ex[1] + ah, 2));
+      }
     }
-    s_pre[0] = ex[0];
-    s_pre[1] = ex[1];
+    if (threadIdx.x == 0) {
+      s_pre[0] = ex[0];
+      s_pre[1] = ex[1];
+    }
   }
   __syncthreads();
   lg += s_pre[0];
@@ -645,16 +654,16 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   __shared__ long long s_lt;
   unsigned long long* st = a.st_cnt + (size_t)j * a.max_tiles;
   const int ft = a.ftile[par][k];
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < kWave) {  // wave 0: publish, look back, publish the inclusive prefix
     long long ex = 0;
     if (t == ft) {
-      st_agent(st + t, lb_word(tl_left, 2));
+      if (threadIdx.x == 0) st_agent(st + t, lb_word(tl_left, 2));
     } else {
-      st_agent(st + t, lb_word(tl_left, 1));
+      if (threadIdx.x == 0) st_agent(st + t, lb_word(tl_left, 1));
       lb_walk<1>(st, t, ft, &ex);
-      st_agent(st + t, lb_word(ex + tl_left, 2));
+      if (threadIdx.x == 0) st_agent(st + t, lb_word(ex + tl_left, 2));
     }
-    s_lt = ex;
+    if (threadIdx.x == 0) s_lt = ex;
   }
   __syncthreads();
   const int lt = (int)s_lt;                    // lefts of the node before this tile

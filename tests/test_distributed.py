@@ -251,6 +251,25 @@ def test_peer_world1_forced_dist(tmp_path, task):
     assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "peer" / "model.txt").read()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("task,two_shot", [("linear", "0"), ("fm", "1"), ("gbmlr", "0")])
+def test_lbfgs_peer_gradient_allreduce_one_gpu(tmp_path, task, two_shot):
+    """Two ranks on the one GPU: the L-BFGS gradient all-reduce over the peer-memory exchange
+    (fp32, rank-order sums; two_shot "0": every message two-shot reduce-scatter + all-gather,
+    "1": the default size split) reaches the gloo run's losses to 1e-6."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_DIST_BACKEND": "gloo"}
+    ref = _run(task, tmp_path / "gloo", 2, "cuda", extra_env=dict(env, YTK_PEER_REDUCE="0"))
+    peer_env = dict(env, YTK_PEER_REDUCE="1")
+    if two_shot == "0":
+        peer_env["YTK_PEER_TWO_SHOT_BYTES"] = "0"
+    got = _run(task, tmp_path / "peer", 2, "cuda", extra_env=peer_env)
+    np.testing.assert_allclose(got["loss"], ref["loss"], rtol=1e-6)
+    np.testing.assert_allclose(got["test_loss"], ref["test_loss"], rtol=1e-6)
+
+
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
 def test_sgd_world2_model_averaging(tmp_path, task):
     """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every

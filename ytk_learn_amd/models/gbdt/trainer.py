@@ -437,7 +437,7 @@ class GBDTTrainer:
         """The round's (loss, weight | leaf counts) vector: the engine's peer-memory exchange
         (fp64, rank-order sums) when it has one, else the process group."""
         peer = getattr(self.builder, "peer", None)
-        if peer is not None and accs.dtype == torch.float64 and accs.is_contiguous() and accs.numel() <= peer.cap:
+        if peer is not None and peer.fits(accs):
             peer.allreduce_(accs)
         else:
             self.comm.allreduce_(accs)

@@ -162,7 +162,7 @@ class HoagOptimizer:
         tot = torch.tensor([pure], dtype=torch.float64)
         if self.comm is not None and self.comm.is_dist:
             self.comm.allreduce_(tot)
-            self.comm.allreduce_(g)
+            self._grad_allreduce(g)
         pure = float(tot[0])
         allloss = pure + reg * self.W
         for r, (s, e) in enumerate(self.groups):
@@ -189,8 +189,18 @@ class HoagOptimizer:
         if self.comm is not None and self.comm.is_dist:
             self.comm.allreduce_(t)
             if g is not None:
-                self.comm.allreduce_(g)
+                self._grad_allreduce(g)
         return float(t[0])
+
+    def _grad_allreduce(self, g: torch.Tensor):
+        """The dim-long gradient all-reduce (HoagOptimizer.java:1038, 68-628 MB for FM / FFM):
+        the peer-memory two-shot exchange on one node (every xGMI link pulls its 1/P share, one
+        kernel, fp32 sums in rank order), else the process group."""
+        peer = getattr(self, "_peer", None)
+        if peer is not None and peer.fits(g):
+            peer.allreduce_(g)
+        else:
+            self.comm.allreduce_(g)
 
     # ------------------------------------------------------------------ line search
     def line_search(self, it: int, step: float, w, wprev, g, gprev, p) -> int:
@@ -309,6 +319,17 @@ class HoagOptimizer:
 
     # ------------------------------------------------------------------ main loop
     def run(self, w: torch.Tensor) -> LbfgsResult:
+        self._peer = None
+        if self.comm is not None and self.comm.is_dist and w.is_cuda:
+            from ..parallel import peer as peer_mod
+            self._peer = peer_mod.make(self.comm, -(-w.numel() * 4 // 8))
+        res = self._run(w)
+        if self._peer is not None:  # collective: every rank leaves run() together
+            self._peer.close()
+            self._peer = None
+        return res
+
+    def _run(self, w: torch.Tensor) -> LbfgsResult:
         ls, m = self.ls, self.ls.m
         dev, dim = w.device, w.numel()
         start = time.perf_counter()

@@ -50,11 +50,14 @@ def make(comm: Comm, cap_elems: int) -> Optional["PeerReduce"]:
 
 
 class PeerReduce:
+    _TYPES = {torch.int64: 0, torch.float64: 1, torch.float32: 2}
+
     def __init__(self, comm: Comm, hnd: int, cap: int):
         self.comm = comm
         self.TIMEOUT_S = float(os.environ.get("YTK_PEER_TIMEOUT_S", 60.0))  # per flag wait (device wall clock)
         self.hnd = hnd
-        self.cap = int(cap)
+        self.cap = int(cap)  # 8-byte words
+        self.cap_bytes = 8 * self.cap
         self.calls = 0
 
     @classmethod
@@ -64,7 +67,7 @@ class PeerReduce:
         handle = np.zeros(64, np.uint8)
         hnd, ok, err = None, 1.0, None
         try:
-            hnd = h.peer_create(comm.world, comm.rank, cap, handle.ctypes.data)
+            hnd = h.peer_create(comm.world, comm.rank, 8 * cap, handle.ctypes.data)
         except Exception as e:  # noqa: BLE001 -- any failure votes for RCCL
             ok = 0.0
             err = e
@@ -109,19 +112,22 @@ class PeerReduce:
             n = min(self.cap, 4099)  # odd: the single-element tail too
             t = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P + r + 1
             f = torch.full((5,), 0.5 * (r + 1), dtype=torch.float64, device=self.comm.device)
+            g = torch.full((1025,), 0.25 * (r + 1), dtype=torch.float32, device=self.comm.device)
             self.allreduce_(t)
             self.allreduce_(f)
+            self.allreduce_(g)
             torch.cuda.synchronize(self.comm.device)
             self.check()
             want = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P * P + P * (P + 1) // 2
-            return bool(torch.equal(t, want)) and bool(torch.all(f == 0.25 * P * (P + 1)))
+            return (bool(torch.equal(t, want)) and bool(torch.all(f == 0.25 * P * (P + 1)))
+                    and bool(torch.all(g == 0.125 * P * (P + 1))))
         finally:
             self.TIMEOUT_S = saved
             self.calls = 0
-            self.comm.stats["calls"] -= 2
-            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5)
+            self.comm.stats["calls"] -= 3
+            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5) + 4 * 1025
             if self.comm.log is not None:
-                del self.comm.log[-2:]
+                del self.comm.log[-3:]
 
     def _account(self, t: torch.Tensor, n: int):
         self.calls += 1
@@ -131,15 +137,18 @@ class PeerReduce:
         if self.comm.log is not None:
             self.comm.log.append(self.comm.last_op)
 
+    def fits(self, t: torch.Tensor) -> bool:
+        return (t.dtype in self._TYPES and t.is_contiguous() and t.is_cuda and t.data_ptr() % 16 == 0
+                and t.numel() * t.element_size() <= self.cap_bytes)
+
     def allreduce_(self, t: torch.Tensor):
-        """In-place sum over the ranks of a contiguous int64 / float64 device tensor (one
-        stream-ordered kernel)."""
-        assert t.dtype in (torch.int64, torch.float64) and t.is_contiguous() and t.is_cuda
+        """In-place sum over the ranks of a contiguous, 16-B aligned int64 / float64 / float32
+        device tensor (one stream-ordered kernel; one-shot below YTK_PEER_TWO_SHOT_BYTES,
+        two-shot reduce-scatter + all-gather above)."""
+        assert self.fits(t), (t.dtype, t.numel(), t.data_ptr() % 16)
         n = t.numel()
-        if n > self.cap:
-            raise ValueError(f"peer all-reduce of {n} words exceeds the {self.cap}-word slab")
-        hip().peer_allreduce(self.hnd, ptr(t), n, 1 if t.dtype == torch.float64 else 0, self.TIMEOUT_S, stream(t))
-        self._account(t, n)
+        hip().peer_allreduce(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
+        self._account(t, n * t.element_size() // 8)
 
     def allreduce_slots_(self, hist: torch.Tensor, slot_elems: int, ids: int, nb_dev: int, cursor: torch.Tensor,
                          k_dev: int, cur_stride: int, skip_dev: int):
