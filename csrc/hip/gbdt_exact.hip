@@ -32,6 +32,7 @@
 #include "gbdt_split_node.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <vector>
 
@@ -91,16 +92,19 @@ struct ExArgs {
   float msl, lr;
 };
 
+template <int kPar>
 __device__ __forceinline__ const int* ex_src_ord(const ExArgs& a, int d, int j) {
   if (d == 0 && !a.sampled) return a.ord0 + (size_t)a.fidx[j] * a.ld0;
-  return a.ordw[d & 1] + (size_t)j * a.ldw;
+  return a.ordw[kPar] + (size_t)j * a.ldw;
 }
+template <int kPar>
 __device__ __forceinline__ const float* ex_src_val(const ExArgs& a, int d, int j) {
   if (d == 0 && !a.sampled) return a.val0 + (size_t)a.fidx[j] * a.ld0;
-  return a.valw[d & 1] + (size_t)j * a.ldw;
+  return a.valw[kPar] + (size_t)j * a.ldw;
 }
+template <int kPar>
 __device__ __forceinline__ const longlong2* ex_src_q(const ExArgs& a, int d, int j) {
-  return reinterpret_cast<const longlong2*>(a.qvw[d & 1] + (size_t)j * a.ldw * 2);
+  return reinterpret_cast<const longlong2*>(a.qvw[kPar] + (size_t)j * a.ldw * 2);
 }
 
 template <typename T>
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kExBig) void ex_init_kernel(ExArgs a, int n) {
 // level 0: qv[j][i] = q[ord[j][i]] (the only gather of (g, h) in a tree) and the root's totals
 __global__ __launch_bounds__(kExThreads) void ex_gather_kernel(ExArgs a, int n) {
   const int j = blockIdx.y;
-  const int* ord = ex_src_ord(a, 0, j);
+  const int* ord = ex_src_ord<0>(a, 0, j);
   longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[0] + (size_t)j * a.ldw * 2);
   const longlong2* q2 = reinterpret_cast<const longlong2*>(a.q);
   long long sg = 0, sh = 0, dummy = 0;
@@ -265,8 +269,9 @@ __device__ __forceinline__ bool ex_ticket(const ExArgs& a, int word, int nt, int
   return true;
 }
 
+template <int kPar>
 __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
-  const int par = d & 1;
+  constexpr int par = kPar;
   const int nt = a.ctl[EX_NT0 + par];
   int j, t;
   if (!ex_ticket(a, EX_TICKET + 2 * d, nt, j, t)) return;
@@ -280,8 +285,8 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
   // that cannot split publishes nothing and nobody waits on it
   if (!(H >= 2.0 * (double)gp.mcw && (nb1 - nb0) >= max(a.min_split_samples, 0))) return;
   const float root_gain = (float)calc_gain(G, H, gp);
-  const float* val = ex_src_val(a, d, j);
-  const longlong2* qv = ex_src_q(a, d, j);
+  const float* val = ex_src_val<par>(a, d, j);
+  const longlong2* qv = ex_src_q<par>(a, d, j);
   const ExSpan sp = ex_span(tl);
   long long g[kExPer], h[kExPer];
   float v[kExPer];
@@ -367,8 +372,10 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
   }
 }
 
+template <int kPar>
 __global__ __launch_bounds__(kExBig) void ex_decide_kernel(ExArgs a, int d, int final_level) {
-  const int par = d & 1, tid = threadIdx.x;
+  constexpr int par = kPar;
+  const int tid = threadIdx.x;
   const int K = a.ctl[EX_K0 + par];
   const int leaf0 = a.ctl[EX_LEAF];
   const bool budget = !final_level && (a.max_leaf <= 0 || leaf0 < a.max_leaf);
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(kExBig) void ex_decide_kernel(ExArgs a, int d, int 
       r.split = split;
       r.pad = 0;
       if (split) {
-        const float* vv = ex_src_val(a, d, bj);
+        const float* vv = ex_src_val<par>(a, d, bj);
         r.thr = (vv[pos] + vv[pos - 1]) * 0.5f;
         r.feat = a.fidx[bj];
       }
@@ -450,14 +457,16 @@ __global__ __launch_bounds__(kExBig) void ex_decide_kernel(ExArgs a, int d, int 
 }
 
 // slot 0: go-left flags by row + per-tile partials of the children (exact int64)
+template <int kPar>
 __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
-  const int par = d & 1, t = blockIdx.x;
+  constexpr int par = kPar;
+  const int t = blockIdx.x;
   if (t >= a.ctl[EX_NT0 + par]) return;
   const int4 tl = a.tiles[par][t];
   const int f = a.go_feat[tl.x];
   const float thr = a.go_thr[tl.x];
-  const int* ord = ex_src_ord(a, d, 0);
-  const longlong2* qv = ex_src_q(a, d, 0);
+  const int* ord = ex_src_ord<par>(a, d, 0);
+  const longlong2* qv = ex_src_q<par>(a, d, 0);
   long long nl = 0, lg = 0, lh = 0, rg = 0, rh = 0;
   for (int i = tl.y + threadIdx.x; i < tl.z; i += kExThreads) {
     const int r = ord[i];
@@ -493,8 +502,10 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
 // One block: node sums of the flag partials (global exclusive tile prefixes recorded at each
 // node's first tile), the children's exact (g, h) totals (the next level's ntot), segments,
 // first tiles and tile table.
+template <int kPar>
 __global__ __launch_bounds__(kExBig) void ex_layout_kernel(ExArgs a, int d) {
-  const int par = d & 1, npar = par ^ 1, tid = threadIdx.x;
+  constexpr int par = kPar, npar = par ^ 1;
+  const int tid = threadIdx.x;
   const int nt = a.ctl[EX_NT0 + par], K = a.ctl[EX_K0 + par], Kn = a.ctl[EX_K0 + npar];
   const int4* tiles = a.tiles[par];
   const int* ftile = a.ftile[par];
@@ -616,37 +627,33 @@ __global__ __launch_bounds__(kExBig) void ex_layout_kernel(ExArgs a, int d) {
   }
 }
 
+template <int kPar>
 __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
-  const int par = d & 1;
+  constexpr int par = kPar;
   const int nt = a.ctl[EX_NT0 + par];
   int j, t;
   if (!ex_ticket(a, EX_TICKET + 2 * d + 1, nt, j, t)) return;
   const int4 tl = a.tiles[par][t];
   const int k = tl.x;
   if (a.csplit[k] < 0) return;  // a leaf: its rows leave the order (block-uniform, nobody waits)
-  const int* ord = ex_src_ord(a, d, j);
-  const float* val = ex_src_val(a, d, j);
-  const longlong2* qv = ex_src_q(a, d, j);
-  const int no = (d + 1) & 1;
+  const int* ord = ex_src_ord<par>(a, d, j);
+  const float* val = ex_src_val<par>(a, d, j);
+  const longlong2* qv = ex_src_q<par>(a, d, j);
+  constexpr int no = par ^ 1;
   int* ordo = a.ordw[no] + (size_t)j * a.ldw;
   float* valo = a.valw[no] + (size_t)j * a.ldw;
   longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[no] + (size_t)j * a.ldw * 2);
   const ExSpan sp = ex_span(tl);
   int r[kExPer];
-  float v[kExPer];
-  longlong2 x[kExPer];
   unsigned lmask = 0;
   long long nl = 0, np = sp.n;
 #pragma unroll
+  for (int e = 0; e < kExPer; ++e) r[e] = e < sp.n ? ord[sp.i0 + e] : 0;
+#pragma unroll
   for (int e = 0; e < kExPer; ++e) {
-    if (e < sp.n) {
-      r[e] = ord[sp.i0 + e];
-      v[e] = val[sp.i0 + e];
-      x[e] = qv[sp.i0 + e];
-      if (a.left_row[r[e]] == 1) {
-        lmask |= 1u << e;
-        ++nl;
-      }
+    if (e < sp.n && a.left_row[r[e]] == 1) {
+      lmask |= 1u << e;
+      ++nl;
     }
   }
   long long tl_left, tl_pos;
@@ -679,8 +686,8 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
     if (e < sp.n) {
       const int dst = (lmask >> e) & 1 ? li++ : ri++;
       s_r[dst] = r[e];
-      s_v[dst] = v[e];
-      s_q[dst] = x[e];
+      s_v[dst] = val[sp.i0 + e];
+      s_q[dst] = qv[sp.i0 + e];
     }
   }
   __syncthreads();
@@ -692,6 +699,16 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
     valo[dst] = s_v[i];
     qo[dst] = s_q[i];
   }
+}
+
+// one level's launches; the level parity picks the ping-pong buffers at compile time
+template <int kPar>
+void ex_level(const ExArgs& a, int d, long long blocks, hipStream_t s) {
+  hipLaunchKernelGGL(ex_eval_kernel<kPar>, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
+  hipLaunchKernelGGL(ex_decide_kernel<kPar>, dim3(1), dim3(kExBig), 0, s, a, d, 0);
+  hipLaunchKernelGGL(ex_flag_kernel<kPar>, dim3(a.max_tiles), dim3(kExThreads), 0, s, a, d);
+  hipLaunchKernelGGL(ex_layout_kernel<kPar>, dim3(1), dim3(kExBig), 0, s, a, d);
+  hipLaunchKernelGGL(ex_part_kernel<kPar>, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
 }
 
 struct ExEngine {
@@ -791,16 +808,18 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
   hipLaunchKernelGGL(ex_gather_kernel, dim3(gx, nf), dim3(kExThreads), 0, s, a, n);
   for (int d = 0; d <= depth; ++d) {
     if (d == depth) {
-      hipLaunchKernelGGL(ex_decide_kernel, dim3(1), dim3(kExBig), 0, s, a, d, 1);
+      if (d & 1)
+        hipLaunchKernelGGL(ex_decide_kernel<1>, dim3(1), dim3(kExBig), 0, s, a, d, 1);
+      else
+        hipLaunchKernelGGL(ex_decide_kernel<0>, dim3(1), dim3(kExBig), 0, s, a, d, 1);
       break;
     }
     YTK_HIP_CHECK(hipMemsetAsync(a.st_gh, 0, st_gh_bytes, s));
     YTK_HIP_CHECK(hipMemsetAsync(a.st_cnt, 0, st_cnt_bytes, s));
-    hipLaunchKernelGGL(ex_eval_kernel, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_decide_kernel, dim3(1), dim3(kExBig), 0, s, a, d, 0);
-    hipLaunchKernelGGL(ex_flag_kernel, dim3(a.max_tiles), dim3(kExThreads), 0, s, a, d);
-    hipLaunchKernelGGL(ex_layout_kernel, dim3(1), dim3(kExBig), 0, s, a, d);
-    hipLaunchKernelGGL(ex_part_kernel, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
+    if (d & 1)
+      ex_level<1>(a, d, blocks, s);
+    else
+      ex_level<0>(a, d, blocks, s);
   }
   YTK_LAUNCH_CHECK();
 }
