@@ -109,6 +109,7 @@ void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintp
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
+long long ytk_lw_ws_bytes(int, int);
 uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
 void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
@@ -252,10 +253,11 @@ PYBIND11_MODULE(_ytk_hip, m) {
                       part, counters, implicit_items, maxp, stream);
   });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 37 || ip.size() != 11 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 38 || ip.size() != 11 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
+  m.def("lw_ws_bytes", &ytk_lw_ws_bytes);
   m.def("host_device_ptr", &ytk_host_device_ptr);
   m.def("lw_step", &ytk_lw_step);
   m.def("lw_partition", &ytk_lw_partition);

@@ -31,6 +31,7 @@
 #include "gbdt_split_node.h"        // SplitOut
 #include "gbdt_tree_node.h"         // DNode, node_leaf_value
 
+#include <algorithm>
 #include <stdexcept>
 #include <vector>
 
@@ -46,7 +47,12 @@ constexpr int kLwThreads = 256;      // children body (runs in the 256-thread pa
 constexpr int kLwPlanThreads = 1024;  // planner / init: 16 waves for the block-parallel phases
                                       // (the replay itself is one wave either way)
 constexpr int kLwCap = 2304;     // speculative nodes per tree (LDS-staged by the planner)
-constexpr int kLwLeafMax = 512;   // max_leaf_cnt supported by the device engine
+constexpr int kLwLeafMax = 512;   // max_leaf_cnt of the LDS-resident planner; also the batch-size cap
+// Larger trees (up to kLwLeafMaxBig leaves, kLwCapBig speculative nodes) run the same planner
+// with its per-node arrays and queues in a global-memory workspace (LwPlanWs): the replay's
+// dependent reads then hit L2 instead of LDS, which is slower per pop but has no size limit.
+constexpr int kLwLeafMaxBig = 4096;
+constexpr int kLwCapBig = 16384;
 constexpr int kLwSort = 4096;     // LDS scratch (u64): replay events, then batch-choice keys
 constexpr int kLwChunk = 2048;    // rows per partition block (partition_atomic_kernel CH)
 constexpr int kLwReduceDirect = 16;  // == kReduceDirect (gbdt_hist.hip)
@@ -58,6 +64,20 @@ struct LwParams {
   int split_groups;  // split records per item (feature groups of split_node_kernel)
   int dist;  // multi-GPU: per batch the host all-reduces the built slots + split cursors
   int bin_bytes;  // 1: uint8 bins, 2: uint16 bins (B > 256)
+};
+
+// global-memory planner workspace (large trees): the arrays the LDS planner keeps in LDS
+struct LwPlanWs {
+  int4* nd;                 // [cap]
+  float* loss;              // [cap]
+  int* seq;                 // [cap]
+  int* par;                 // [cap]
+  int4* ch;                 // [cap]
+  int* hsid;                // [max_leaf + 8]
+  unsigned long long* akey;  // [pow2 >= max_leaf + 8]
+  unsigned long long* bkey;  // [2 max_leaf + 8]
+  int* uid;                 // [3 max_leaf + 16]
+  unsigned long long* buf;  // events (int4) / rank keys + bottlenecks
 };
 
 struct LwBufs {
@@ -83,6 +103,7 @@ struct LwBufs {
   int* done_host;              // host-mapped pinned int[2]: [0] LW_DONE, [1] batches planned (optional)
   int* zero_ids;               // [max_leaf + 1] built slots with != 1 histogram item
   int2* zero_range;            // [max_leaf + 1] their items [x, x + y)
+  LwPlanWs ws;                 // large trees only (max_leaf > kLwLeafMax): else all null
 };
 
 // planner phase timing (YTK_LW_PROF=1): thread 0 accumulates wall-clock ticks per phase
@@ -105,16 +126,24 @@ __device__ __forceinline__ bool lw_static_leaf(const LwParams& p, float loss, in
          (p.min_split_samples > 0 && cnt < p.min_split_samples);
 }
 
-constexpr unsigned long long kLwSidMask = 0xfffull;  // node id bits of a queue key
+// node id bits of a queue key: 12 for the LDS planner (ids and seqs < 4096 for max_leaf <=
+// 512), 16 for the workspace planner (cap <= kLwCapBig)
+template <bool kBig>
+struct LwKey {
+  static constexpr int kBits = kBig ? 16 : 12;
+  static constexpr unsigned long long kMask = (1ull << kBits) - 1;
+};
 
 // queue key: larger lossChg first, then the earlier push (smaller seq) -- the
-// priority_queue order of LeafGrower::Entry; the node id rides in the low 12 bits
-// (seq < 4096 and ids < 4096 for max_leaf <= 512; seqs are unique so the id never
-// decides the order)
+// priority_queue order of LeafGrower::Entry; the node id rides in the low bits (seqs are
+// unique so the id never decides the order)
+template <bool kBig>
 __device__ __forceinline__ unsigned long long lw_qkey(float loss, int seq, int sid) {
   unsigned u = __float_as_uint(loss);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving float -> uint
-  return ((unsigned long long)u << 32) | ((unsigned long long)(4095 - seq) << 12) | (unsigned long long)sid;
+  constexpr int kB = LwKey<kBig>::kBits;
+  return ((unsigned long long)u << 32) | ((LwKey<kBig>::kMask - (unsigned long long)seq) << kB) |
+         (unsigned long long)sid;
 }
 
 // binary max-heap of keys in LDS, one thread
@@ -300,22 +329,37 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_init_kernel(LwParams p, LwB
     b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), (k == 0 && nblk > kLwReduceDirect) ? 2 : 0);
 }
 
+// kBig: the per-node arrays and queues live in the global workspace b.ws (large trees)
+template <bool kBig>
 __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwBufs b) {
+  constexpr int kC = kBig ? 1 : kLwCap, kL = kBig ? 1 : kLwLeafMax;
   // node fields the replay reads, packed: {lc, tid, depth | state << 16 | static_leaf << 24, cnt}
-  __shared__ int4 s_nd[kLwCap];
-  __shared__ float s_loss[kLwCap];
-  __shared__ int s_seq[kLwCap];
-  __shared__ int s_hsid[kLwLeafMax + 8];
-  __shared__ int s_par[kLwCap];  // batch choice: forest parents (pointer jumping)
+  __shared__ int4 l_nd[kC];
+  __shared__ float l_loss[kC];
+  __shared__ int l_seq[kC];
+  __shared__ int l_hsid[kL + 8];
+  __shared__ int l_par[kC];  // batch choice: forest parents (pointer jumping)
   // children of an expanded node, as the replay needs them (one LDS round trip per pop):
   // {loss_l bits, loss_r bits, terminal-by-static-rules | poppable_l << 1 | poppable_r << 2, 0}
-  __shared__ int4 s_ch[kLwCap];
-  __shared__ unsigned long long s_akey[kLwQueueSort];        // poppable queue entries, sorted
-  __shared__ unsigned long long s_bkey[2 * kLwLeafMax + 8];  // children heap
-  __shared__ int s_uid[3 * kLwLeafMax + 16];                 // blocking entries
+  __shared__ int4 l_ch[kC];
+  __shared__ unsigned long long l_akey[kBig ? 1 : kLwQueueSort];  // poppable queue entries, sorted
+  __shared__ unsigned long long l_bkey[2 * kL + 8];               // children heap
+  __shared__ int l_uid[3 * kL + 16];                              // blocking entries
   __shared__ int s_na, s_nu;
   // replay events (then reused by the batch choice: rank keys + bottlenecks, 27 KiB)
-  __shared__ unsigned long long s_buf[kLwSort];
+  __shared__ unsigned long long l_buf[kBig ? 1 : kLwSort];
+  int4* s_nd = kBig ? b.ws.nd : l_nd;
+  float* s_loss = kBig ? b.ws.loss : l_loss;
+  int* s_seq = kBig ? b.ws.seq : l_seq;
+  int* s_hsid = kBig ? b.ws.hsid : l_hsid;
+  int* s_par = kBig ? b.ws.par : l_par;
+  int4* s_ch = kBig ? b.ws.ch : l_ch;
+  unsigned long long* s_akey = kBig ? b.ws.akey : l_akey;
+  unsigned long long* s_bkey = kBig ? b.ws.bkey : l_bkey;
+  int* s_uid = kBig ? b.ws.uid : l_uid;
+  unsigned long long* s_buf = kBig ? b.ws.buf : l_buf;
+  const int capr = kBig ? (p.cap + 127) & ~127 : kLwCap;  // rank-key entries (a multiple of 128)
+  const int leaf_max = kBig ? p.max_leaf : kLwLeafMax;
   __shared__ int s_tmp[kLwPlanThreads / kWave + 1];
   __shared__ int s_nev, s_blocked, s_nh, s_num_leaf, s_ntree, s_seqc, s_k, s_ncand;
   int* st = b.st;
@@ -414,7 +458,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     for (int i = tid; i < nh; i += kLwPlanThreads) {
       const int sid = s_hsid[i];
       const int4 nd = s_nd[sid];
-      if ((nd.z >> 24) || nd.x >= 0) s_akey[atomicAdd(&s_na, 1)] = lw_qkey(s_loss[sid], s_seq[sid], sid);
+      if ((nd.z >> 24) || nd.x >= 0) s_akey[atomicAdd(&s_na, 1)] = lw_qkey<kBig>(s_loss[sid], s_seq[sid], sid);
       else s_uid[atomicAdd(&s_nu, 1)] = sid;
     }
     __syncthreads();
@@ -440,7 +484,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     unsigned long long u = 0ull;
     for (int i = lane; i < nu; i += kWave) {
       const int sid = s_uid[i];
-      const unsigned long long k = lw_qkey(s_loss[sid], s_seq[sid], sid);
+      const unsigned long long k = lw_qkey<kBig>(s_loss[sid], s_seq[sid], sid);
       u = k > u ? k : u;
     }
     u = lw_wave_max_u64(u);
@@ -452,9 +496,9 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     while (true) {
       if (p.max_leaf > 0 && num_leaf == p.max_leaf) { bulk = true; break; }
       const unsigned long long top = ka > bmax ? ka : bmax;
-      if (u > top) { blocked = (int)(u & kLwSidMask); break; }
+      if (u > top) { blocked = (int)(u & LwKey<kBig>::kMask); break; }
       if (top == 0ull) break;  // queue empty
-      const int sid = (int)(top & kLwSidMask);
+      const int sid = (int)(top & LwKey<kBig>::kMask);
       const int4 nd = s_nd[sid];
       const int4 ch = s_ch[sid];
       if (ka > bmax) {
@@ -489,8 +533,8 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
       s_nd[r].y = lt + 1;
       s_seq[l] = seqc;
       s_seq[r] = seqc + 1;
-      const unsigned long long kl = lw_qkey(__int_as_float(ch.x), seqc, l);
-      const unsigned long long kr = lw_qkey(__int_as_float(ch.y), seqc + 1, r);
+      const unsigned long long kl = lw_qkey<kBig>(__int_as_float(ch.x), seqc, l);
+      const unsigned long long kr = lw_qkey<kBig>(__int_as_float(ch.y), seqc + 1, r);
       seqc += 2;
       if (ch.z & 2) {
         s_bkey[nbh] = kl;
@@ -511,8 +555,8 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     }
     // the remaining queue: A tail, the children array, the blocking entries (a set)
     const int ra = na - pa;
-    for (int i = lane; i < ra; i += kWave) s_hsid[i] = (int)(s_akey[pa + i] & kLwSidMask);
-    for (int i = lane; i < nbh; i += kWave) s_hsid[ra + i] = (int)(s_bkey[i] & kLwSidMask);
+    for (int i = lane; i < ra; i += kWave) s_hsid[i] = (int)(s_akey[pa + i] & LwKey<kBig>::kMask);
+    for (int i = lane; i < nbh; i += kWave) s_hsid[ra + i] = (int)(s_bkey[i] & LwKey<kBig>::kMask);
     for (int i = lane; i < nu; i += kWave) s_hsid[ra + nbh + i] = s_uid[i];
     int nr = ra + nbh + nu;
     if (bulk) {  // leaf budget used: every queued node pops as a leaf (order-independent)
@@ -565,7 +609,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
   if (blocked >= 0) {
     const int fr = p.cap - nsid;
     // keep one net node pair per future split (LeafGrower slack rule): never runs dry
-    k = p.speculate ? max(1, min(remaining, (fr - remaining - 1) >> 1)) : 1;
+    k = p.speculate ? max(1, min(min(remaining, kLwLeafMax), (fr - remaining - 1) >> 1)) : 1;
     if (fr < 2) k = 0;
   }
   int* s_batch = reinterpret_cast<int*>(s_akey);  // the batch, in pop order (A is consumed)
@@ -579,9 +623,9 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     // unexpanded ones among them, best first. Pointer jumping gives the bottlenecks in
     // log(depth) block steps; each candidate's rank is a count over the splittable set.
     // (Top-k by the node's own gain expanded ~1.6x as many nodes: docs/performance.md.)
-    unsigned long long* s_rk = s_buf;                                 // [kLwCap] splittable rank keys
-    unsigned* s_m = reinterpret_cast<unsigned*>(s_buf + kLwCap);      // [kLwCap] bottleneck ord(loss)
-    constexpr int kPer = (kLwCap + kLwPlanThreads - 1) / kLwPlanThreads;
+    unsigned long long* s_rk = s_buf;                                 // [capr] splittable rank keys
+    unsigned* s_m = reinterpret_cast<unsigned*>(s_buf + capr);        // [capr] bottleneck ord(loss)
+    constexpr int kPer = ((kBig ? kLwCapBig : kLwCap) + kLwPlanThreads - 1) / kLwPlanThreads;
     auto ord = [](float f) {
       const unsigned u = __float_as_uint(f);
       return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -600,8 +644,8 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     int ns, ncand;
     int pos = lw_scan(c, s_tmp, &ns);
     int pc = lw_scan(cc, s_tmp, &ncand);
-    // rank window: speculate percent of the leaf budget (s_uid holds 3 kLwLeafMax ranks)
-    const int rem = min(3 * kLwLeafMax, max(1, remaining * p.speculate / 100));
+    // rank window: speculate percent of the leaf budget (s_uid holds 3 leaf_max ranks)
+    const int rem = min(3 * leaf_max, max(1, remaining * p.speculate / 100));
     if (ns <= rem && ncand <= k) {
       // every splittable node ranks inside the window and the batch has room for every
       // candidate: the batch is all of them, and no bottleneck / rank is needed (the order
@@ -660,7 +704,8 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     auto rkey = [&](int i) {
       return i == blocked ? ~0ull
                           : (((unsigned long long)s_m[i] << 32) |
-                             (unsigned long long)((ord(s_loss[i]) >> 12) << 12) | (unsigned long long)i);
+                             (unsigned long long)((ord(s_loss[i]) >> LwKey<kBig>::kBits) << LwKey<kBig>::kBits) |
+                             (unsigned long long)i);
     };
     int* s_cand = s_par;  // all -1 after the pointer jumping: reused as the candidate list
     for (int i = i0; i < i1; ++i) {
@@ -668,7 +713,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
       s_rk[pos++] = rkey(i);
       if (s_nd[i].x < 0) s_cand[pc++] = i;
     }
-    const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= kLwCap (a multiple of 128)
+    const int ns_pad = (ns + 2 * kWave - 1) & ~(2 * kWave - 1);  // <= capr (a multiple of 128)
     for (int z = ns + tid; z < ns_pad; z += kLwPlanThreads) s_rk[z] = 0ull;  // never ranks above a key
     for (int r = tid; r < rem; r += kLwPlanThreads) s_uid[r] = -1;
     __syncthreads();
@@ -983,6 +1028,38 @@ struct LwEngine {
   LwBufs b;
 };
 std::vector<LwEngine> g_lw;
+
+// the workspace planner runs above the LDS planner's limits, or everywhere with
+// YTK_LW_PLAN_GLOBAL=1 (tests: both planners must build the same trees)
+bool lw_plan_global(int cap, int max_leaf) {
+  const char* g = getenv("YTK_LW_PLAN_GLOBAL");
+  return max_leaf > kLwLeafMax || cap > kLwCap || (g && g[0] == '1');
+}
+
+// planner workspace layout (16-B aligned arrays); base == nullptr: size only
+size_t lw_carve_ws(char* base, int cap, int max_leaf, LwPlanWs& w) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = base ? base + off : nullptr;
+    off += (bytes + 15) & ~size_t(15);
+    return q;
+  };
+  int q2 = 1;
+  while (q2 < max_leaf + 8) q2 <<= 1;
+  const size_t capr = ((size_t)cap + 127) & ~size_t(127);
+  const size_t buf_u64 = std::max<size_t>(2 * (3 * (size_t)max_leaf + 8), capr + capr / 2 + 1);
+  w.nd = (int4*)take(sizeof(int4) * cap);
+  w.loss = (float*)take(sizeof(float) * cap);
+  w.seq = (int*)take(sizeof(int) * cap);
+  w.par = (int*)take(sizeof(int) * cap);
+  w.ch = (int4*)take(sizeof(int4) * cap);
+  w.hsid = (int*)take(sizeof(int) * (max_leaf + 8));
+  w.akey = (unsigned long long*)take(8 * (size_t)q2);
+  w.bkey = (unsigned long long*)take(8 * (2 * (size_t)max_leaf + 8));
+  w.uid = (int*)take(sizeof(int) * (3 * (size_t)max_leaf + 16));
+  w.buf = (unsigned long long*)take(8 * buf_u64);
+  return off;
+}
 }  // namespace
 
 extern "C" {
@@ -990,7 +1067,8 @@ extern "C" {
 // ptrs: st, tnodes, G, H, gl, hl, cnt, begin, cnt_local, depth, feat, bin_a, bin_b, lc, tid, seq,
 //       state, loss, heap, batch, part_feat, part_thr, part_begin, part_cnt, part_first,
 //       part_shift, cursor, hist_items, build_ids, split_items, item_sid, split_out, root_cnt,
-//       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range
+//       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range,
+//       plan workspace (ytk_lw_ws_bytes bytes; 0 when that is 0)
 // ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N, split_groups, dist,
 //     bin_bytes
 // fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr. Returns an engine handle.
@@ -1015,8 +1093,9 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.l2 = fp[3];
   p.max_abs_leaf = fp[4];
   p.lr = fp[5];
-  if (p.max_leaf < 2 || p.max_leaf > kLwLeafMax || p.cap > kLwCap || p.cap < p.max_leaf + 2)
-    throw std::invalid_argument("lw_create: need 2 <= max_leaf <= 512 and max_leaf + 2 <= cap <= 2304");
+  const bool big = lw_plan_global(p.cap, p.max_leaf);
+  if (p.max_leaf < 2 || p.max_leaf > kLwLeafMaxBig || p.cap > kLwCapBig || p.cap < p.max_leaf + 2)
+    throw std::invalid_argument("lw_create: need 2 <= max_leaf <= 4096 and max_leaf + 2 <= cap <= 16384");
   LwBufs& b = e.b;
   int i = 0;
   b.st = (int*)a[i++];
@@ -1056,11 +1135,22 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   b.done_host = (int*)a[i++];
   b.zero_ids = (int*)a[i++];
   b.zero_range = (int2*)a[i++];
+  char* ws = (char*)a[i++];  // planner workspace (ytk_lw_ws_bytes), large trees only
+  if (big && !ws) throw std::invalid_argument("lw_create: the workspace planner (max_leaf > 512) needs its workspace");
+  b.ws = LwPlanWs{};
+  if (big) lw_carve_ws(ws, p.cap, p.max_leaf, b.ws);
   g_lw.push_back(e);
   return (int)g_lw.size() - 1;
 }
 
 void ytk_lw_set_lr(int h, float lr) { g_lw.at(h).p.lr = lr; }
+
+// bytes of the planner workspace a (cap, max_leaf) engine needs (0: the LDS planner fits)
+long long ytk_lw_ws_bytes(int cap, int max_leaf) {
+  if (!lw_plan_global(cap, max_leaf)) return 0;
+  LwPlanWs w;
+  return (long long)lw_carve_ws(nullptr, cap, max_leaf, w);
+}
 
 // device address of pinned host memory (hipHostMalloc'ed by the caller's allocator)
 uintptr_t ytk_host_device_ptr(uintptr_t host) {
@@ -1076,7 +1166,12 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (which) {
     case 0: hipLaunchKernelGGL(lw_init_kernel, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b); break;
-    case 1: hipLaunchKernelGGL(lw_plan_kernel, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b); break;
+    case 1:
+      if (e.b.ws.nd)
+        hipLaunchKernelGGL(lw_plan_kernel<true>, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b);
+      else
+        hipLaunchKernelGGL(lw_plan_kernel<false>, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b);
+      break;
 
     default: throw std::runtime_error("bad lw step");
   }

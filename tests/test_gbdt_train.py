@@ -1,3 +1,5 @@
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -254,14 +256,18 @@ def test_native_leafwise_gpu_paths_match_python(monkeypatch, mode):
                                 {"min_split_samples": 900}, {"min_split_loss": 2.0},
                                 {"l1": 0.5, "max_abs_leaf_val": 0.3},
                                 {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6},
-                                {"max_leaf_cnt": 255}, {"spec": "0"}])
+                                {"max_leaf_cnt": 255}, {"spec": "0"}, {"max_leaf_cnt": 1024},
+                                {"max_leaf_cnt": 700, "min_split_samples": 60},
+                                {"max_leaf_cnt": 255, "plan_global": "1"}])
 def test_device_leafwise_matches_host(monkeypatch, kw):
     """GPU-resident leaf-wise engine (device queue replay + planner kernels,
     csrc/hip/gbdt_leafwise.hip) == the host-planned leaf-wise builder: model dump (node
-    ids, splits, values, statistics) and losses, bit for bit."""
+    ids, splits, values, statistics) and losses, bit for bit. max_leaf_cnt > 512 runs the
+    planner with its queue in global memory (plan_global: also below 512 leaves)."""
     from ytk_learn_amd.models.gbdt.device_leafwise import DeviceLeafBuilder
     kw = dict(kw)
     monkeypatch.setenv("YTK_LOSSGUIDE_SPEC", kw.pop("spec", "1"))
+    monkeypatch.setenv("YTK_LW_PLAN_GLOBAL", kw.pop("plan_global", "0"))
     res = []
     for dev_builder in (False, True):
         p = _params("loss", rounds=3)
@@ -275,10 +281,14 @@ def test_device_leafwise_matches_host(monkeypatch, kw):
         if dev_builder:
             batches, expanded, overflow = tr.builder.stats()
             assert overflow == 0 and batches >= 1 and expanded >= batches
+            big = p.tree.max_leaf_cnt > 512 or os.environ["YTK_LW_PLAN_GLOBAL"] == "1"
+            assert (tr.builder.plan_ws is not None) == big
         res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
     assert res[0][0] == res[1][0]
     assert res[0][1:] == res[1][1:]
     assert res[0][0].count("leaf=") > 3
+    if p.tree.max_leaf_cnt > 512:  # the budget is reached: the trees really are that large
+        assert max(t.count("leaf=") for t in res[0][0].split("booster[")) > 512
 
 
 @pytest.mark.gpu

@@ -32,8 +32,11 @@ from ...utils.timestats import PhaseTimer
 from .builder import TimeStats, TreeParams
 from .device_builder import DNODE_DTYPE, DeviceTree
 
-LW_CAP_MAX = 2304      # speculative nodes per tree (kLwCap)
-LW_LEAF_MAX = 512      # kLwLeafMax
+LW_CAP_MAX = 2304      # speculative nodes per tree of the LDS-resident planner (kLwCap)
+LW_LEAF_MAX = 512      # kLwLeafMax: max_leaf_cnt of the LDS-resident planner
+# larger trees: the planner keeps its node arrays and queues in a global workspace
+LW_CAP_MAX_BIG = 16384  # kLwCapBig
+LW_LEAF_MAX_BIG = 4096  # kLwLeafMaxBig
 LW_DONE = 8
 LW_BATCHES, LW_EXPANDED, LW_OVERFLOW = 12, 13, 11
 # st words read by the fixed-grid kernels
@@ -142,6 +145,9 @@ class DeviceLeafBuilder:
         # YTK_LW_PROF=1: planner phase times + work counters accumulated on the device
         self.prof = (torch.zeros(32, dtype=torch.int64, device=dev)
                      if os.environ.get("YTK_LW_PROF") == "1" else None)
+        # max_leaf_cnt > 512: the planner's per-node arrays and queues in global memory
+        ws = int(hip().lw_ws_bytes(self.cap, ml))
+        self.plan_ws = torch.zeros(ws, dtype=torch.uint8, device=dev) if ws > 0 else None
         self._handle = hip().lw_create(self._ptrs(), self._ip(), self._fp())
         self._ghmax_buf = None
         # multi-GPU: one message per batch = its built slots + its split cursors (lw_msg)
@@ -166,13 +172,14 @@ class DeviceLeafBuilder:
     @staticmethod
     def slots_needed(params: TreeParams) -> int:
         """Histogram slots the engine allocates (one per speculative node, never evicted)."""
-        return int(min(8 * max(params.max_leaf_cnt, 2) + 64, LW_CAP_MAX))
+        ml = max(params.max_leaf_cnt, 2)
+        return int(min(8 * ml + 64, LW_CAP_MAX if ml <= LW_LEAF_MAX else LW_CAP_MAX_BIG))
 
     @staticmethod
     def supports(bins: torch.Tensor, binsT: Optional[torch.Tensor], B: int, F: int, params: TreeParams,
                  comm: Optional[Comm] = None) -> bool:
         """uint8 row-major bins (B <= 256, 32-aligned stride), a column-major binsT,
-        2 <= max_leaf_cnt <= 512 (the planner's LDS-resident queue). Multi-GPU: needs
+        2 <= max_leaf_cnt <= 4096 (above 512 the planner's queue lives in global memory). Multi-GPU: needs
         min_split_samples <= 0 (the children's global counts arrive with the batch's
         all-reduce, after the children planning)."""
         if os.environ.get("YTK_DEVICE_LEAFWISE", "1") == "0":
@@ -180,7 +187,7 @@ class DeviceLeafBuilder:
         if comm is not None and comm.is_dist and (params.min_split_samples > 0
                                                   or os.environ.get("YTK_DEVICE_LEAFWISE_DIST", "1") == "0"):
             return False
-        if params.grow_policy != "loss" or not (2 <= params.max_leaf_cnt <= LW_LEAF_MAX):
+        if params.grow_policy != "loss" or not (2 <= params.max_leaf_cnt <= LW_LEAF_MAX_BIG):
             return False
         if bins.dtype == torch.int16:  # wide bins: uint16 rows, feature-group LDS histograms
             fg = gops.wide_group(B, F)
@@ -224,7 +231,7 @@ class DeviceLeafBuilder:
                 + [ptr(self.cursor), ptr(self.hist_items), ptr(self.build_ids), ptr(self.split_items),
                    ptr(self.item_sid), ptr(self.split_out), ptr(self.root_cnt),
                    ptr(self.prof) if self.prof is not None else 0, self._done_dev, ptr(self.zero_ids),
-                   ptr(self.zero_range)])
+                   ptr(self.zero_range), ptr(self.plan_ws) if self.plan_ws is not None else 0])
 
     def _lv_ptrs(self):
         """Pointer list of the level engine's finalize / raw-tree kernels (st, nodes, arrays)."""
