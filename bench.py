@@ -31,6 +31,7 @@ import argparse
 import json
 import os
 import sys
+import traceback
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -109,6 +110,7 @@ def main():
     try:
         run(a, comm)
     except BaseException as e:  # noqa: BLE001 -- report, then exit non-zero (never re-exec)
+        traceback.print_exc()
         print(f"[bench] rank {comm.rank} failed: {type(e).__name__}: {e}; last collective issued: "
               f"{comm.last_op}", file=sys.stderr, flush=True)
         os._exit(1)

@@ -329,6 +329,91 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_init_kernel(LwParams p, LwB
     b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), (k == 0 && nblk > kLwReduceDirect) ? 2 : 0);
 }
 
+// Start of every planning step (planner or auto-expansion): multi-GPU, the previous
+// batch's split cursors ((right << 32) | left rows) were all-reduced with its built
+// histograms, so the children's GLOBAL row counts replace the local ones the partition
+// epilogue wrote (DataParallelTreeMaker.java:518,538); then the previous batch's split
+// records are applied (canSplit: UpdateStrategy.java:50-53). Ends without a barrier.
+__device__ void lw_apply_splits(const LwParams& p, const LwBufs& b) {
+  int* st = b.st;
+  const int tid = threadIdx.x;
+  if (p.dist) {
+    const int kprev = st[LW_N_SPLIT];
+    for (int j = tid; j < kprev; j += (int)blockDim.x) {
+      const int P = b.batch[j];
+      const int L = b.lc[P];
+      const long long lg = (long long)(b.cursor[(size_t)j * kCurStride] & 0xffffffffull);
+      b.cnt[L] = lg;
+      b.cnt[L + 1] = b.cnt[P] - lg;
+    }
+    __syncthreads();
+  }
+  const double mcw2 = (double)p.mcw * 2.0;
+  const int nsi = st[LW_N_SITEMS];
+  for (int i = tid; i < nsi; i += (int)blockDim.x) {
+    const int sid = b.item_sid[i];
+    // best of the item's feature-group records (split_node_kernel order: larger gain, then
+    // lower feature, then lower bin; none last); node totals are equal in every record
+    const int ng = p.split_groups;
+    auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
+    int bg = 0;
+    for (int g = 1; g < ng; ++g) {
+      const SplitOut& c = b.split_out[(size_t)i * ng + g];
+      const SplitOut& bb = b.split_out[(size_t)i * ng + bg];
+      if (better(c.loss_chg, fkey(c.feat), fkey(c.bin_b), bb.loss_chg, fkey(bb.feat), fkey(bb.bin_b))) bg = g;
+    }
+    SplitOut o = b.split_out[(size_t)i * ng + bg];
+    if (bg != 0) {
+      o.g = b.split_out[(size_t)i * ng].g;
+      o.h = b.split_out[(size_t)i * ng].h;
+    }
+    b.G[sid] = o.g;
+    b.H[sid] = o.h;
+    b.gl[sid] = o.gl;
+    b.hl[sid] = o.hl;
+    int feat = o.feat;
+    float chg = o.loss_chg;
+    if (!(o.h >= mcw2 && b.cnt[sid] >= (long long)p.min_split_samples)) {
+      chg = -INFINITY;
+      feat = -1;
+    }
+    b.feat[sid] = feat;
+    b.bin_a[sid] = o.bin_a;
+    b.bin_b[sid] = o.bin_b;
+    b.loss[sid] = chg;
+    b.state[sid] = 1;
+  }
+}
+
+// Phase F for batch entry j (parent P): children ids lc, lc + 1, their fresh node state, the
+// partition descriptor (chunks of kLwChunk rows), the split cursor reset.
+__device__ __forceinline__ void lw_expand_one(const LwParams& p, const LwBufs& b, int j, int P, int lc) {
+  b.batch[j] = P;
+  const int dep = b.depth[P] + 1;
+  for (int c = lc; c <= lc + 1; ++c) {
+    b.G[c] = b.H[c] = b.gl[c] = b.hl[c] = 0.0;
+    b.cnt[c] = 0;
+    b.begin[c] = 0;
+    b.cnt_local[c] = 0;
+    b.depth[c] = dep;
+    b.feat[c] = -1;
+    b.bin_a[c] = b.bin_b[c] = -1;
+    b.lc[c] = -1;
+    b.tid[c] = -1;
+    b.seq[c] = 0;
+    b.state[c] = 0;
+    b.loss[c] = -INFINITY;
+  }
+  const int beg = b.begin[P], cnt = b.cnt_local[P];
+  b.part_feat[j] = b.feat[P];
+  b.part_thr[j] = (b.bin_a[P] + b.bin_b[P]) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
+  b.part_begin[j] = beg;
+  b.part_cnt[j] = cnt;
+  b.part_shift[j] = beg < p.N ? p.N : -p.N;
+  b.part_first[j] = (cnt + kLwChunk - 1) / kLwChunk;
+  b.cursor[(size_t)j * kCurStride] = 0ull;
+}
+
 // kBig: the per-node arrays and queues live in the global workspace b.ws (large trees)
 template <bool kBig>
 __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwBufs b) {
@@ -369,57 +454,8 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     return;
   }
   unsigned long long t_prev = b.prof && tid == 0 ? wall_clock64() : 0ull;
-  // multi-GPU: the previous batch's split cursors ((right << 32) | left rows) were
-  // all-reduced with its built histograms; the children's GLOBAL row counts replace the
-  // local ones the partition epilogue wrote (DataParallelTreeMaker.java:518,538)
-  if (p.dist) {
-    const int kprev = st[LW_N_SPLIT];
-    for (int j = tid; j < kprev; j += kLwPlanThreads) {
-      const int P = b.batch[j];
-      const int L = b.lc[P];
-      const long long lg = (long long)(b.cursor[(size_t)j * kCurStride] & 0xffffffffull);
-      b.cnt[L] = lg;
-      b.cnt[L + 1] = b.cnt[P] - lg;
-    }
-    __syncthreads();
-  }
+  lw_apply_splits(p, b);
   const int nsid = st[LW_N_SIDS];
-  const double mcw2 = (double)p.mcw * 2.0;
-  // A. split records of the previous batch (canSplit: UpdateStrategy.java:50-53)
-  const int nsi = st[LW_N_SITEMS];
-  for (int i = tid; i < nsi; i += kLwPlanThreads) {
-    const int sid = b.item_sid[i];
-    // best of the item's feature-group records (split_node_kernel order: larger gain, then
-    // lower feature, then lower bin; none last); node totals are equal in every record
-    const int ng = p.split_groups;
-    auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
-    int bg = 0;
-    for (int g = 1; g < ng; ++g) {
-      const SplitOut& c = b.split_out[(size_t)i * ng + g];
-      const SplitOut& bb = b.split_out[(size_t)i * ng + bg];
-      if (better(c.loss_chg, fkey(c.feat), fkey(c.bin_b), bb.loss_chg, fkey(bb.feat), fkey(bb.bin_b))) bg = g;
-    }
-    SplitOut o = b.split_out[(size_t)i * ng + bg];
-    if (bg != 0) {
-      o.g = b.split_out[(size_t)i * ng].g;
-      o.h = b.split_out[(size_t)i * ng].h;
-    }
-    b.G[sid] = o.g;
-    b.H[sid] = o.h;
-    b.gl[sid] = o.gl;
-    b.hl[sid] = o.hl;
-    int feat = o.feat;
-    float chg = o.loss_chg;
-    if (!(o.h >= mcw2 && b.cnt[sid] >= (long long)p.min_split_samples)) {
-      chg = -INFINITY;
-      feat = -1;
-    }
-    b.feat[sid] = feat;
-    b.bin_a[sid] = o.bin_a;
-    b.bin_b[sid] = o.bin_b;
-    b.loss[sid] = chg;
-    b.state[sid] = 1;
-  }
   __syncthreads();
   LW_TICK(0);
   // B. stage what the replay reads
@@ -608,8 +644,11 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
   const int remaining = p.max_leaf > 0 ? p.max_leaf - num_leaf : 1;
   if (blocked >= 0) {
     const int fr = p.cap - nsid;
-    // keep one net node pair per future split (LeafGrower slack rule): never runs dry
-    k = p.speculate ? max(1, min(min(remaining, kLwLeafMax), (fr - remaining - 1) >> 1)) : 1;
+    // keep a node pair per future split free (2 (remaining + 1) ids): speculative expansions
+    // the replay never splits can then never starve the forced expansion of a blocked node,
+    // which the next replay always splits (so it pays for its pair); cap >= 2 max_leaf + 3
+    // holds the invariant from the root on
+    k = p.speculate ? max(1, min(min(remaining, kLwLeafMax), (fr - 2 * remaining - 2) >> 1)) : 1;
     if (fr < 2) k = 0;
   }
   int* s_batch = reinterpret_cast<int*>(s_akey);  // the batch, in pop order (A is consumed)
@@ -765,30 +804,7 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     const int P = s_batch[j];
     const int lc = nsid + 2 * j;
     s_nd[P].x = lc;
-    b.batch[j] = P;
-    const int dep = b.depth[P] + 1;
-    for (int c = lc; c <= lc + 1; ++c) {
-      b.G[c] = b.H[c] = b.gl[c] = b.hl[c] = 0.0;
-      b.cnt[c] = 0;
-      b.begin[c] = 0;
-      b.cnt_local[c] = 0;
-      b.depth[c] = dep;
-      b.feat[c] = -1;
-      b.bin_a[c] = b.bin_b[c] = -1;
-      b.lc[c] = -1;
-      b.tid[c] = -1;
-      b.seq[c] = 0;
-      b.state[c] = 0;
-      b.loss[c] = -INFINITY;
-    }
-    const int beg = b.begin[P], cnt = b.cnt_local[P];
-    b.part_feat[j] = b.feat[P];
-    b.part_thr[j] = (b.bin_a[P] + b.bin_b[P]) >> 1;  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
-    b.part_begin[j] = beg;
-    b.part_cnt[j] = cnt;
-    b.part_shift[j] = beg < p.N ? p.N : -p.N;
-    b.part_first[j] = (cnt + kLwChunk - 1) / kLwChunk;
-    b.cursor[(size_t)j * kCurStride] = 0ull;
+    lw_expand_one(p, b, j, P, lc);
   }
   __syncthreads();
   const int nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
@@ -1094,8 +1110,8 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.max_abs_leaf = fp[4];
   p.lr = fp[5];
   const bool big = lw_plan_global(p.cap, p.max_leaf);
-  if (p.max_leaf < 2 || p.max_leaf > kLwLeafMaxBig || p.cap > kLwCapBig || p.cap < p.max_leaf + 2)
-    throw std::invalid_argument("lw_create: need 2 <= max_leaf <= 4096 and max_leaf + 2 <= cap <= 16384");
+  if (p.max_leaf < 2 || p.max_leaf > kLwLeafMaxBig || p.cap > kLwCapBig || p.cap < 2 * p.max_leaf + 3)
+    throw std::invalid_argument("lw_create: need 2 <= max_leaf <= 4096 and 2 max_leaf + 3 <= cap <= 16384");
   LwBufs& b = e.b;
   int i = 0;
   b.st = (int*)a[i++];
@@ -1172,7 +1188,6 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
       else
         hipLaunchKernelGGL(lw_plan_kernel<false>, dim3(1), dim3(kLwPlanThreads), 0, s, e.p, e.b);
       break;
-
     default: throw std::runtime_error("bad lw step");
   }
   YTK_LAUNCH_CHECK();

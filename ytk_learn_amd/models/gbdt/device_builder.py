@@ -93,6 +93,10 @@ def node_table_to_tree(nodes_bytes: np.ndarray, st: np.ndarray) -> Tree:
     nn = int(st[ST_NUM_NODES])
     nd = np.asarray(nodes_bytes).view(DNODE_DTYPE).reshape(-1)[:nn]
     leaf = (nd["is_leaf"] != 0) | (nd["left"] < 0)
+    inner = ~leaf
+    if inner.any() and (int(nd["left"][inner].max()) >= nn or int(nd["right"][inner].max()) >= nn):
+        raise RuntimeError(f"device tree engine: inconsistent node table ({nn} nodes, a child id past the end; "
+                           f"leaf-wise: speculative node overflow); state words {np.asarray(st)[:16].tolist()}")
     return Tree.from_arrays(nd["left"], nd["right"], nd["feat"], nd["bin_a"], nd["bin_b"], nd["value"], leaf,
                             nd["loss_chg"], nd["H"], nd["cnt_global"])
 
