@@ -123,7 +123,9 @@ void ytk_owner_unpack(uintptr_t out, uintptr_t hist, int nslots, int B, int F, i
 //    owner's result slab in place once that owner's flag is up. Each rank reads
 //    2 (P - 1) / P of the message instead of P - 1 messages, spread over every peer's link.
 // int64 sums are exact (bitwise the RCCL result); fp64 / fp32 sums are taken in rank order,
-// identical on every rank. A message may be described by device words (the leaf-wise batch:
+// identical on every rank. The two halves of two-shot also run alone (owner-computes sync,
+// the message made of P equal segments): reduce-scatter (segment q summed into place on rank
+// q only) and all-gather (rank q's segment copied into place on every rank). A message may be described by device words (the leaf-wise batch:
 // its built slots + split cursors, counted by the planner) -- no host round trip per batch.
 //
 // Slab reuse: exchange e writes slab e & 1, exchange e + 2 writes it again. Block 0 takes
@@ -141,6 +143,7 @@ constexpr int kPeerMax = 16;
 constexpr int kXchgGrid = 256;     // max blocks of one exchange (flag words per rank)
 constexpr int kXchgThreads = 256;
 enum { XT_I64 = 0, XT_F64 = 1, XT_F32 = 2 };
+enum { XM_ALLREDUCE = 0, XM_REDUCE_SCATTER = 1, XM_ALLGATHER = 2 };
 
 struct PeerPtrs {
   char* send[kPeerMax][2];
@@ -263,7 +266,7 @@ template <int kType, bool kSysFence>
 __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, int P, int rank, XchgMsg m,
                                                                  long long cap_bytes, unsigned long long* __restrict__ ctl,
                                                                  int* __restrict__ err, long long timeout_ticks,
-                                                                 long long two_shot_bytes) {
+                                                                 long long two_shot_bytes, int mode) {
   if (m.skip != nullptr && *m.skip != 0) return;
   // after a timed-out wait (ctl[2] != 0) every later exchange returns at once: the job is
   // failing (the host check raises), so nothing waits again
@@ -289,7 +292,9 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
   const bool tail_blk = tail > 0 && b == G - 1;
   const int par = (int)(e & 1ull);
   xv2* mine = reinterpret_cast<xv2*>(pp.send[rank][par]);
-  const bool two = nu * 16 >= two_shot_bytes && P > 1;
+  // reduce-scatter / all-gather: the owner ranges are the message's P segments (the host
+  // checked that they are whole, equal numbers of units: no tail)
+  const bool two = mode != XM_ALLREDUCE || (nu * 16 >= two_shot_bytes && P > 1);
   if (!two) {
     const long long lo = nu * b / G, hi = nu * (b + 1) / G;
     if (!(hi > lo || tail_blk || b == 0)) goto done;
@@ -320,32 +325,39 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
       hi = a + (z - a) * (b + 1) / G;
     };
     long long lo, hi;
-    for (int q = 0; q < P; ++q) {  // publish sub-chunk b of every owner's range
-      sub(q, lo, hi);
-      for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_unit(m, u, nh), mine + u);
-    }
-    if (tail_blk && t < tail) {
-      const long long off = (nu * U + t) * ES;
-      __builtin_memcpy(pp.send[rank][par] + off, m.base + off, ES);
-    }
-    publish_fence<kSysFence>();
-    flag_publish(pp.sig, P, rank, b, e);
-    flag_wait(pp.sig, P, rank, b, e, err, ctl, timeout_ticks);
-    acquire_fence<kSysFence>();
-    // reduce this rank's sub-chunk b; result in place + into the result slab
-    sub(rank, lo, hi);
     xv2* rmine = reinterpret_cast<xv2*>(pp.res[rank][par]);
-    for (long long u = lo + t; u < hi; u += kXchgThreads) {
-      xv2* dst = xchg_unit(m, u, nh);
-      xv2 s = *dst;
-      if (rank > 0) s = __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[0][par]) + u);
-      for (int q = 1; q < P; ++q) {
-        const xv2 v = q == rank ? *dst : __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[q][par]) + u);
-        s = unit_add<kType>(s, v);
+    if (mode == XM_ALLGATHER) {
+      // this rank's own segment goes straight to its result slab
+      sub(rank, lo, hi);
+      for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_unit(m, u, nh), rmine + u);
+    } else {
+      for (int q = 0; q < P; ++q) {  // publish sub-chunk b of every owner's range
+        sub(q, lo, hi);
+        for (long long u = lo + t; u < hi; u += kXchgThreads) __builtin_nontemporal_store(*xchg_unit(m, u, nh), mine + u);
       }
-      *dst = s;
-      __builtin_nontemporal_store(s, rmine + u);
+      if (tail_blk && t < tail) {
+        const long long off = (nu * U + t) * ES;
+        __builtin_memcpy(pp.send[rank][par] + off, m.base + off, ES);
+      }
+      publish_fence<kSysFence>();
+      flag_publish(pp.sig, P, rank, b, e);
+      flag_wait(pp.sig, P, rank, b, e, err, ctl, timeout_ticks);
+      acquire_fence<kSysFence>();
+      // reduce this rank's sub-chunk b; result in place (+ into the result slab)
+      sub(rank, lo, hi);
+      for (long long u = lo + t; u < hi; u += kXchgThreads) {
+        xv2* dst = xchg_unit(m, u, nh);
+        xv2 s = *dst;
+        if (rank > 0) s = __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[0][par]) + u);
+        for (int q = 1; q < P; ++q) {
+          const xv2 v = q == rank ? *dst : __builtin_nontemporal_load(reinterpret_cast<const xv2*>(pp.send[q][par]) + u);
+          s = unit_add<kType>(s, v);
+        }
+        *dst = s;
+        if (mode == XM_ALLREDUCE) __builtin_nontemporal_store(s, rmine + u);
+      }
     }
+    if (mode == XM_REDUCE_SCATTER) goto done;
     publish_fence<kSysFence>();
     flag_publish(pp.rsig, P, rank, b, e);
     // the other owners' reduced sub-chunks b, each as soon as its owner's flag is up
@@ -398,12 +410,13 @@ namespace ytk {
 static size_t peer_sig_bytes() { return (size_t)kPeerMax * kXchgGrid * 8; }
 static size_t peer_bytes(long long cap) { return 2 * peer_sig_bytes() + 4 * (size_t)cap; }
 
-static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int type, double timeout_s, hipStream_t s) {
+static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int type, double timeout_s, hipStream_t s,
+                        int mode = XM_ALLREDUCE) {
   grid = std::max(1, std::min(grid, kXchgGrid));
   const long long ticks = (long long)(timeout_s * (double)g.ticks_per_s);
 #define YTK_XCHG(T, S)                                                                                     \
   hipLaunchKernelGGL((peer_xchg_kernel<T, S>), dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, \
-                     g.cap, g.ctl, g.err, ticks, g.two_shot_bytes)
+                     g.cap, g.ctl, g.err, ticks, g.two_shot_bytes, mode)
   if (g.sys_fence) {
     if (type == XT_F64) YTK_XCHG(XT_F64, true);
     else if (type == XT_F32) YTK_XCHG(XT_F32, true);
@@ -496,6 +509,34 @@ void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int type, double t
   m.n = n;
   const int grid = (int)std::min<long long>((bytes + g.block_bytes - 1) / g.block_bytes, ytk::kXchgGrid);
   ytk::peer_launch(g, m, grid, type, timeout_s, reinterpret_cast<hipStream_t>(stream));
+}
+
+// Owner-computes halves of the exchange over P equal segments of data[0:n] (n a multiple of
+// P 16-byte units): reduce-scatter leaves the sum over the ranks of segment `rank` in place
+// (the other segments keep this rank's values); all-gather copies every rank's own segment
+// into place on every rank. One kernel each; a one-rank group is the identity.
+static void peer_segments(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream,
+                          int mode) {
+  ytk::PeerGroup& g = g_peer.at(hnd);
+  if (n <= 0 || g.P == 1) return;
+  const int es = type == ytk::XT_F32 ? 4 : 8;
+  const long long bytes = n * es;
+  if (bytes > g.cap) throw std::invalid_argument("peer segments: message larger than the slab");
+  if (data % 16 != 0 || bytes % (16LL * g.P) != 0)
+    throw std::invalid_argument("peer segments: 16-B aligned data of P whole 16-B unit segments needed");
+  ytk::XchgMsg m{};
+  m.base = reinterpret_cast<char*>(data);
+  m.n = n;
+  const int grid = (int)std::min<long long>((bytes + g.block_bytes - 1) / g.block_bytes, ytk::kXchgGrid);
+  ytk::peer_launch(g, m, grid, type, timeout_s, reinterpret_cast<hipStream_t>(stream), mode);
+}
+
+void ytk_peer_reduce_scatter(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream) {
+  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_REDUCE_SCATTER);
+}
+
+void ytk_peer_allgather(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream) {
+  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_ALLGATHER);
 }
 
 // Leaf-wise batch message counted on the device: the *nb_dev built slots listed in ids

@@ -143,7 +143,8 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
                                              ("gbdt_loss", 3, "allreduce"), ("gbdt", 3, "owner"),
                                              ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner"),
                                              ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer"),
-                                             ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer")])
+                                             ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer"), ("gbdt", 2, "peer_owner"),
+                                             ("gbdt", 3, "peer_owner"), ("gbdt", 4, "peer_owner")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
@@ -152,17 +153,22 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     model byte for byte. "peer": every level / batch message and the round vector go through
     the one-kernel IPC peer-memory exchange (leaf-wise: sized on the device, no host wait per
     batch); level-wise rounds are then graph-captured even over gloo, so the replays check
-    that the device-resident exchange epochs stay in step across graph replays."""
+    that the device-resident exchange epochs stay in step across graph replays. "peer_owner":
+    owner-computes with the level's reduce-scatter and the split-record all-gather as one
+    peer kernel each."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": "allreduce" if mode == "peer" else mode,
-           "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if mode == "peer" else "0",
+    peer = mode.startswith("peer")
+    sync = {"peer": "allreduce", "peer_owner": "owner"}.get(mode, mode)
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": sync,
+           "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if peer else "0",
            "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}  # small shards: keep the overlap covered
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
-    if mode == "peer":
+    if peer:
         assert res["peer_calls"] > 0
+        assert res["owner"] == (mode == "peer_owner")
         if task == "gbdt" and world != 3:  # no feature sampling: graph-eligible rounds
             assert res["graph_replays"] > 0
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()

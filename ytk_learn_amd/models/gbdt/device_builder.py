@@ -240,6 +240,7 @@ class DeviceLevelBuilder:
             self.split_local = torch.zeros(2 * self.maxp * 48, dtype=torch.uint8, device=dev)
             self._own_cache = {}
             self._pack = None
+            self._allr = None
         self._slot_bytes = slot_elems * 8
         self._root_fixed = False
         # staged histogram flush: block partials to a staging slab with plain stores, then a
@@ -254,13 +255,19 @@ class DeviceLevelBuilder:
                         and self.N >= int(os.environ.get("YTK_HIST_OVERLAP_MIN_ROWS", "2000000")))
         # single-node multi-GPU (default; YTK_PEER_REDUCE=0: RCCL): every level message -- and
         # the round's loss vector (trainer) -- is ONE peer-memory exchange kernel
-        # (parallel/peer.py) instead of an RCCL call; all-reduce mode only. Stream-ordered and
+        # (parallel/peer.py) instead of an RCCL call; owner mode: the level's reduce-scatter by
+        # feature block and the split-record all-gather are one kernel each. Stream-ordered and
         # host-free, so the half-level overlap is not needed, and a round whose collectives are
         # all peer exchanges can be graph-captured on any process-group backend.
         self.peer = None
-        if not self.owner:
+        if self.comm.is_dist:
             lvl = max([1] + [self.level_slots[c][2] - self.level_slots[c][0] for c in self.level_slots]) * slot_elems
             cap = max(lvl, slot_elems, self.maxp * CUR_STRIDE + DONE_WORDS, 4 + self.max_nodes)
+            if self.owner:  # the largest packed level ([P][build slots x own block + count slots])
+                P = self.comm.world
+                nb = max([1] + [self._half(c) for c in range(1, D)])
+                cap = max(cap, P * (nb * B * self.fr * 2 + self.ncs * B * F * 2) + 2 * P,
+                          P * self.split_local.numel() // 8)
             self.peer = peer_mod.make(self.comm, cap)
             if self.peer is not None:
                 self.overlap = False
@@ -384,7 +391,10 @@ class DeviceLevelBuilder:
         slot_ptr = ptr(self.hist) + base * self._slot_bytes
         cnt_ptr = slot_ptr + nslots * self._slot_bytes if C else 0
         h.owner_pack(slot_ptr, ptr(x), nslots, B, F, fr, P, cnt_ptr, C, s)  # one launch
-        self.comm.reduce_scatter_(out, x)
+        if self.peer is not None and self.peer.fits_segments(x.view(-1)):
+            out = self.peer.reduce_scatter_(x.view(-1))  # one kernel, this rank's block in place
+        else:
+            self.comm.reduce_scatter_(out, x)
         h.owner_unpack(ptr(out), slot_ptr, nslots, B, F, fr, self.comm.rank, cnt_ptr, C, s)
 
     def _owner_fmask(self, fmask_np: np.ndarray):
@@ -423,7 +433,16 @@ class DeviceLevelBuilder:
                      gp["max_abs_leaf"], 1.0, 1.0, nitems_dev, ptr(self.inv_scales), ptr(self.split_part),
                      ptr(self.split_cnt), s)
         if self.owner:
-            allr = self.comm.allgather(self.split_local)
+            if self.peer is not None:  # the records' all-gather as one peer kernel
+                if self._allr is None:
+                    self._allr = torch.zeros(self.comm.world * self.split_local.numel(), dtype=torch.uint8,
+                                             device=self.dev)
+                n = self.split_local.numel()
+                allr = self._allr
+                allr[self.comm.rank * n:(self.comm.rank + 1) * n].copy_(self.split_local)
+                self.peer.allgather_(allr.view(torch.int64))
+            else:
+                allr = self.comm.allgather(self.split_local)
             cap = self.split_local.numel() // 48
             h.split_combine(ptr(allr), self.comm.world, cap, nitems_dev, min(nitems, cap), tot,
                             ptr(self.split_out), s)

@@ -116,18 +116,23 @@ class PeerReduce:
             self.allreduce_(t)
             self.allreduce_(f)
             self.allreduce_(g)
+            # reduce-scatter + all-gather of 2P int64 (one unit per segment) == the all-reduce
+            rs = torch.arange(2 * P, dtype=torch.int64, device=self.comm.device) + 10 * r
+            self.reduce_scatter_(rs)
+            self.allgather_(rs)
             torch.cuda.synchronize(self.comm.device)
             self.check()
             want = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P * P + P * (P + 1) // 2
+            want_rs = P * torch.arange(2 * P, dtype=torch.int64, device=self.comm.device) + 10 * P * (P - 1) // 2
             return (bool(torch.equal(t, want)) and bool(torch.all(f == 0.25 * P * (P + 1)))
-                    and bool(torch.all(g == 0.125 * P * (P + 1))))
+                    and bool(torch.all(g == 0.125 * P * (P + 1))) and bool(torch.equal(rs, want_rs)))
         finally:
             self.TIMEOUT_S = saved
             self.calls = 0
-            self.comm.stats["calls"] -= 3
-            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5) + 4 * 1025
+            self.comm.stats["calls"] -= 5
+            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5) + 4 * 1025 + 2 * 8 * 2 * P
             if self.comm.log is not None:
-                del self.comm.log[-3:]
+                del self.comm.log[-5:]
 
     def _account(self, t: torch.Tensor, n: int):
         self.calls += 1
@@ -148,6 +153,29 @@ class PeerReduce:
         assert self.fits(t), (t.dtype, t.numel(), t.data_ptr() % 16)
         n = t.numel()
         hip().peer_allreduce(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
+        self._account(t, n * t.element_size() // 8)
+
+    def fits_segments(self, t: torch.Tensor) -> bool:
+        """``t`` splits into P equal segments of whole 16-byte units (owner-computes sync)."""
+        return self.fits(t) and (t.numel() * t.element_size()) % (16 * self.comm.world) == 0
+
+    def reduce_scatter_(self, t: torch.Tensor) -> torch.Tensor:
+        """Segment ``rank`` of ``t`` (P equal segments) <- its sum over the ranks, in place; the
+        other segments keep this rank's values. Returns the reduced segment (a view). One
+        kernel: the first half of the two-shot exchange."""
+        assert self.fits_segments(t), (t.dtype, t.numel(), t.data_ptr() % 16)
+        n = t.numel()
+        hip().peer_reduce_scatter(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
+        self._account(t, n * t.element_size() // 8)
+        seg = n // self.comm.world
+        return t.view(-1)[self.comm.rank * seg:(self.comm.rank + 1) * seg]
+
+    def allgather_(self, t: torch.Tensor):
+        """Every segment q of ``t`` (P equal segments) <- rank q's segment q, in place (each rank
+        fills its own segment first). One kernel: the second half of the two-shot exchange."""
+        assert self.fits_segments(t), (t.dtype, t.numel(), t.data_ptr() % 16)
+        n = t.numel()
+        hip().peer_allgather(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
         self._account(t, n * t.element_size() // 8)
 
     def allreduce_slots_(self, hist: torch.Tensor, slot_elems: int, ids: int, nb_dev: int, cursor: torch.Tensor,
