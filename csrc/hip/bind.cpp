@@ -133,7 +133,9 @@ int ytk_ex_tile();
 void ytk_peer_open(int, uintptr_t);
 void ytk_peer_allreduce(int, uintptr_t, long long, int, double, uintptr_t);
 void ytk_peer_reduce_scatter(int, uintptr_t, long long, int, double, uintptr_t);
-void ytk_peer_allgather(int, uintptr_t, long long, int, double, uintptr_t);
+void ytk_peer_allgather(int, uintptr_t, long long, int, double, uintptr_t, uintptr_t);
+void ytk_peer_reduce_scatter_dev(int, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t, double, uintptr_t);
+void ytk_lw_owner(int, uintptr_t, long long, int, int, int, int, int, uintptr_t, int, int, uintptr_t);
 void ytk_peer_allreduce_slots(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                               double, uintptr_t);
 int ytk_peer_check(int);
@@ -277,6 +279,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("peer_allreduce", &ytk_peer_allreduce);
   m.def("peer_reduce_scatter", &ytk_peer_reduce_scatter);
   m.def("peer_allgather", &ytk_peer_allgather);
+  m.def("peer_reduce_scatter_dev", &ytk_peer_reduce_scatter_dev);
+  m.def("lw_owner", &ytk_lw_owner);
   m.def("peer_allreduce_slots", &ytk_peer_allreduce_slots);
   m.def("peer_check", &ytk_peer_check);
   m.def("peer_destroy", &ytk_peer_destroy);

@@ -165,6 +165,8 @@ struct XchgMsg {
   long long* cursor;
   int cur_stride;
   const int* skip;  // non-null and non-zero: no exchange
+  int seg_p;        // > 0 (with n < 0): a CONTIGUOUS message at base of seg_p equal segments of
+                    // *nb_dev * slot_elems + *k_dev * cur_stride words each (leaf-wise owner sync)
 };
 
 typedef long long xv2 __attribute__((ext_vector_type(2)));  // nontemporal builtins need a native vector
@@ -172,7 +174,7 @@ typedef long long xv2 __attribute__((ext_vector_type(2)));  // nontemporal built
 // unit u (16 bytes) of the message; gather mode: int64 pairs (slot sizes and cursor strides
 // are even, every slot 16-B aligned)
 __device__ __forceinline__ xv2* xchg_unit(const XchgMsg& m, long long u, long long nh) {
-  if (m.n >= 0) return reinterpret_cast<xv2*>(m.base) + u;
+  if (m.n >= 0 || m.seg_p > 0) return reinterpret_cast<xv2*>(m.base) + u;
   const long long i = 2 * u;
   if (i < nh) {
     const long long kb = i / m.slot_elems;
@@ -279,6 +281,7 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
   if (n < 0) {
     nh = (long long)(*m.nb_dev) * m.slot_elems;
     n = nh + (long long)(*m.k_dev) * m.cur_stride;
+    if (m.seg_p > 0) n *= m.seg_p;  // contiguous segments
   }
   if (t == 0) s_e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
@@ -516,7 +519,7 @@ void ytk_peer_allreduce(int hnd, uintptr_t data, long long n, int type, double t
 // (the other segments keep this rank's values); all-gather copies every rank's own segment
 // into place on every rank. One kernel each; a one-rank group is the identity.
 static void peer_segments(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream,
-                          int mode) {
+                          int mode, uintptr_t skip) {
   ytk::PeerGroup& g = g_peer.at(hnd);
   if (n <= 0 || g.P == 1) return;
   const int es = type == ytk::XT_F32 ? 4 : 8;
@@ -527,16 +530,41 @@ static void peer_segments(int hnd, uintptr_t data, long long n, int type, double
   ytk::XchgMsg m{};
   m.base = reinterpret_cast<char*>(data);
   m.n = n;
+  m.skip = reinterpret_cast<const int*>(skip);
   const int grid = (int)std::min<long long>((bytes + g.block_bytes - 1) / g.block_bytes, ytk::kXchgGrid);
   ytk::peer_launch(g, m, grid, type, timeout_s, reinterpret_cast<hipStream_t>(stream), mode);
 }
 
 void ytk_peer_reduce_scatter(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream) {
-  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_REDUCE_SCATTER);
+  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_REDUCE_SCATTER, 0);
 }
 
-void ytk_peer_allgather(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream) {
-  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_ALLGATHER);
+// skip (optional): a device word; non-zero = no exchange (leaf-wise batches past the tree's end)
+void ytk_peer_allgather(int hnd, uintptr_t data, long long n, int type, double timeout_s, uintptr_t stream,
+                        uintptr_t skip) {
+  peer_segments(hnd, data, n, type, timeout_s, stream, ytk::XM_ALLGATHER, skip);
+}
+
+// Reduce-scatter of a contiguous int64 message of P equal segments sized on the device: each
+// segment is *nb_dev * seg_slot + *k_dev * cur_stride words (leaf-wise owner-computes batch:
+// the packed feature blocks of the built slots + the split cursors). Skipped while *skip != 0.
+void ytk_peer_reduce_scatter_dev(int hnd, uintptr_t data, long long seg_slot, uintptr_t nb_dev, uintptr_t k_dev,
+                                 int cur_stride, uintptr_t skip, double timeout_s, uintptr_t stream) {
+  ytk::PeerGroup& g = g_peer.at(hnd);
+  if (g.P == 1) return;
+  if ((seg_slot & 1) || (cur_stride & 1) || data % 16 != 0)
+    throw std::invalid_argument("peer_reduce_scatter_dev: even segment parts and 16-B aligned data needed");
+  ytk::XchgMsg m{};
+  m.base = reinterpret_cast<char*>(data);
+  m.n = -1;
+  m.nb_dev = reinterpret_cast<const int*>(nb_dev);
+  m.k_dev = reinterpret_cast<const int*>(k_dev);
+  m.slot_elems = seg_slot;
+  m.cur_stride = cur_stride;
+  m.seg_p = g.P;
+  m.skip = reinterpret_cast<const int*>(skip);
+  ytk::peer_launch(g, m, ytk::kXchgGrid, ytk::XT_I64, timeout_s, reinterpret_cast<hipStream_t>(stream),
+                   ytk::XM_REDUCE_SCATTER);
 }
 
 // Leaf-wise batch message counted on the device: the *nb_dev built slots listed in ids

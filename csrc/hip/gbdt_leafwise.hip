@@ -1034,6 +1034,52 @@ __global__ __launch_bounds__(256) void lw_msg_kernel(long long* __restrict__ his
   }
 }
 
+// Owner-computes batch sync (hist_sync = owner): rank r owns features [r fr, (r + 1) fr).
+// Pack: x = P segments, segment r = the feature-r-block columns of the batch's built slots
+// ([slot][bin][fl][2], zero padded to fr) then the batch's split cursors (replicated into
+// every segment, so every rank gets their sums). Unpack: this rank's reduced segment (x)
+// back into the slots' owned columns and the cursors (unpack 1: x is that segment; 2: x is
+// the whole message, the segment at rank * its device-counted size). kcap >= 0: host-sized
+// segments of kcap slot entries (zero beyond the built count) and kcap cursors (the RCCL
+// loop, which knows the batch's split count); kcap < 0: sized by the device counts (peer).
+__global__ __launch_bounds__(256) void lw_owner_kernel(long long* __restrict__ hist, long long slot_elems, int B,
+                                                       int F, int fr, int P, int rank, const int* __restrict__ build_ids,
+                                                       const int* __restrict__ nb_dev,
+                                                       unsigned long long* __restrict__ cursor,
+                                                       const int* __restrict__ k_dev, long long* __restrict__ x,
+                                                       int kcap, int unpack) {
+  const int nb = kcap >= 0 ? min(*nb_dev, kcap) : *nb_dev;
+  const int ns = kcap >= 0 ? kcap : nb;
+  const int kc = kcap >= 0 ? kcap : *k_dev;
+  const long long sl = (long long)B * fr * 2;
+  const long long nbe = (long long)ns * sl;
+  const long long per = nbe + (long long)kc * kCurStride;
+  const long long total = unpack ? per : per * P;
+  if (unpack == 2) x += (long long)rank * per;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int r = unpack ? rank : (int)(i / per);
+    const long long j = unpack ? i : i - (long long)r * per;
+    long long* xi = x + i;
+    if (j < nbe) {
+      const long long kb = j / sl, e = j - kb * sl;
+      const int c = (int)(e & 1);
+      const long long q = e >> 1;
+      const int fl = (int)(q % fr);
+      const long long bin = q / fr;
+      const int f = r * fr + fl;
+      if (kb < nb && f < F) {
+        long long* hs = hist + (size_t)build_ids[kb] * slot_elems + (bin * F + f) * 2 + c;
+        if (unpack) *hs = *xi; else *xi = *hs;
+      } else if (!unpack) {
+        *xi = 0;
+      }
+    } else {
+      const long long cj = j - nbe;
+      if (unpack) cursor[cj] = (unsigned long long)*xi; else *xi = (long long)cursor[cj];
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -1235,6 +1281,21 @@ void ytk_lw_msg(int h, uintptr_t hist, long long slot_elems, uintptr_t msg, int 
   const int grid = (int)std::min<long long>((n + 255) / 256, 256 * 8);
   hipLaunchKernelGGL(lw_msg_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
                      slot_elems, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor, (long long*)msg, kcap, unpack);
+  YTK_LAUNCH_CHECK();
+}
+
+// owner-computes pack (unpack = 0: x = P segments) / unpack (1: x = this rank's segment) of
+// the batch's built slots + split cursors; kcap < 0: sized by the device counts
+void ytk_lw_owner(int h, uintptr_t hist, long long slot_elems, int B, int F, int fr, int P, int rank, uintptr_t x,
+                  int kcap, int unpack, uintptr_t stream) {
+  const LwEngine& e = g_lw.at(h);
+  const int kmax = kcap >= 0 ? kcap : std::min(e.p.max_leaf, kLwLeafMax);
+  const long long n = (long long)kmax * ((long long)B * fr * 2 + kCurStride) * (unpack ? 1 : P);
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 256 * 8);
+  hipLaunchKernelGGL(lw_owner_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
+                     slot_elems, B, F, fr, P, rank, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor,
+                     e.b.st + LW_N_SPLIT, (long long*)x, kcap, unpack);
   YTK_LAUNCH_CHECK();
 }
 

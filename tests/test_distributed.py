@@ -144,7 +144,8 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
                                              ("gbdt", 4, "owner"), ("gbdt_loss", 2, "owner"),
                                              ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer"),
                                              ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer"), ("gbdt", 2, "peer_owner"),
-                                             ("gbdt", 3, "peer_owner"), ("gbdt", 4, "peer_owner")])
+                                             ("gbdt", 3, "peer_owner"), ("gbdt", 4, "peer_owner"),
+                                             ("gbdt_loss", 2, "peer_owner"), ("gbdt_loss", 3, "peer_owner")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
@@ -155,7 +156,7 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     batch); level-wise rounds are then graph-captured even over gloo, so the replays check
     that the device-resident exchange epochs stay in step across graph replays. "peer_owner":
     owner-computes with the level's reduce-scatter and the split-record all-gather as one
-    peer kernel each."""
+    peer kernel each (leaf-wise: the batch's reduce-scatter sized on the device)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -208,9 +209,8 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
     _run(task, tmp_path / "plain", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / "rccl", 1, "cuda", extra_env=dict(env, YTK_FORCE_DIST="1"))
     assert res["is_dist"] and res["backend"] == "nccl" and res["comm"]["calls"] > 0
-    if task == "gbdt":  # the GPU leaf-wise engine has one sync mode (one batch message all-reduced)
-        assert res["owner"] == (mode == "owner")
-        # level-wise rounds are captured WITH their RCCL calls and replayed as graphs
+    assert res["owner"] == (mode == "owner")
+    if task == "gbdt":  # level-wise rounds are captured WITH their RCCL calls and replayed as graphs
         assert res["graph_replays"] > 0 and res["comm"]["calls"] >= 5 * 6
     assert open(tmp_path / "plain" / "model.txt").read() == open(tmp_path / "rccl" / "model.txt").read()
     if task == "gbdt" and mode == "allreduce":

@@ -29,7 +29,7 @@ from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
 from ...parallel import peer as peer_mod
 from ...parallel.comm import Comm
 from ...utils.timestats import PhaseTimer
-from .builder import TimeStats, TreeParams
+from .builder import TimeStats, TreeParams, resolve_hist_sync
 from .device_builder import DNODE_DTYPE, DeviceTree
 
 LW_CAP_MAX = 2304      # speculative nodes per tree of the LDS-resident planner (kLwCap)
@@ -113,8 +113,24 @@ class DeviceLeafBuilder:
         self.item_sid = i32(self.n_sitems)
         # split search in feature groups (one block per (node, group); the planner keeps each
         # node's best record) -- as DeviceLevelBuilder, YTK_SPLIT_GROUPS (default 4)
-        self.split_groups = gops.split_groups(B, F)
+        # owner-computes sync (TreeParams.hist_sync, multi-GPU): each batch reduce-scatters its
+        # built slots by feature block (the split cursors ride in every block), every rank
+        # searches its own features, and the 48-B split records are all-gathered and combined
+        # on the device (split_combine) -- HistogramBuilder.java:95's reduceScatterArray
+        self.owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, B * F * 16) == "owner"
+        self.split_groups = 1 if self.owner else gops.split_groups(B, F)
         self.split_out = torch.zeros(self.n_sitems * 48 * self.split_groups, dtype=torch.uint8, device=dev)
+        if self.owner:
+            P = self.comm.world
+            self.fr, self.fblocks = self.comm.feature_blocks(F)
+            self.own = self.fblocks[self.comm.rank]
+            self.split_local = torch.zeros(self.n_sitems * 48, dtype=torch.uint8, device=dev)
+            self._allr = torch.zeros(P * self.n_sitems * 48, dtype=torch.uint8, device=dev)
+            kmax = min(ml, LW_LEAF_MAX)  # batches hold <= 512 splits
+            self._own_per = kmax * (B * self.fr * 2 + CUR_STRIDE)  # the largest segment
+            self._own_x = torch.zeros(P * self._own_per, dtype=torch.int64, device=dev)
+            self._own_out = torch.zeros(self._own_per, dtype=torch.int64, device=dev)
+            self._own_cache = {}
         self.split_part = torch.zeros(self.n_sitems * F * 48, dtype=torch.uint8, device=dev)
         self.split_cnt = torch.zeros(self.n_sitems, dtype=torch.int32, device=dev)
         self.root_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -157,8 +173,12 @@ class DeviceLeafBuilder:
         # single-node multi-GPU (default; YTK_PEER_REDUCE=0: RCCL): each batch message is ONE
         # peer-memory exchange kernel that reads its size (built slots, split cursors) from the
         # planner's device words -- the batch loop is the N = 1 loop, no host wait per batch
-        self.peer = (peer_mod.make(self.comm, max(self.msg.numel(), self.slot_elems, 4 + self.max_nodes))
-                     if self.comm.is_dist else None)
+        self.peer = None
+        if self.comm.is_dist:
+            cap = max(self.msg.numel(), self.slot_elems, 4 + self.max_nodes)
+            if self.owner:
+                cap = max(cap, self._own_x.numel(), self._allr.numel() // 8)
+            self.peer = peer_mod.make(self.comm, cap)
         # the trainer's K == 1 gradient pass can build the next tree's root histogram (slot 0,
         # tree_grad_hist); it is zeroed again when a tree is done
         self.staged = True
@@ -249,6 +269,7 @@ class DeviceLeafBuilder:
             fm[np.sort(perm[:n_sam])] = 1
         else:
             fm = np.ones(self.F, np.uint8)
+        self._fmask_np = fm
         key = fm.tobytes()
         if key not in self._fmask_cache:
             if len(self._fmask_cache) > 64:
@@ -276,9 +297,72 @@ class DeviceLeafBuilder:
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
                              self.REDUCE_Y, s)
 
+    def _owner_fmask(self, fmask, f0):
+        """(owned sampled-feature mask on the device, its first feature, the rank whose block
+        holds the first sampled feature -- its records carry the node totals)."""
+        fm_np = self._fmask_np  # the tree's sampled-feature mask (host copy, set by _fmask)
+        key = fm_np.tobytes()
+        if key not in self._own_cache:
+            lo, hi = self.own
+            fm = fm_np.copy()
+            fm[:lo] = 0
+            fm[hi:] = 0
+            nz = np.flatnonzero(fm)
+            f0o = int(nz[0]) if nz.size else (lo if hi > lo else 0)
+            tot = next(r for r, (a, b) in enumerate(self.fblocks) if b > a and fm_np[a:b].any())
+            if len(self._own_cache) > 64:
+                self._own_cache.clear()
+            self._own_cache[key] = (torch.from_numpy(fm).to(self.dev), f0o, tot)
+        return self._own_cache[key]
+
+    def _owner_sync(self, h, hd, s, kcap=-1):
+        """Reduce-scatter the batch's built slots by feature block (+ its cursors): pack, one
+        peer kernel sized on the device (kcap < 0) or an RCCL reduce-scatter of kcap-split
+        segments, unpack this rank's block."""
+        P = self.comm.world
+        fr = self.fr
+        if self.peer is not None and kcap < 0:
+            h.lw_owner(hd, ptr(self.hist), self.slot_elems, self.B, self.F, fr, P, self.comm.rank, ptr(self._own_x),
+                       -1, 0, s)
+            st = ptr(self.st)
+            self.peer.reduce_scatter_dev_(self._own_x, self.B * fr * 2, st + 4 * W_N_BUILD, st + 4 * W_N_SPLIT,
+                                          CUR_STRIDE, st + 4 * LW_DONE)
+            # unpack 2: this rank's segment starts at rank x its device-counted size
+            h.lw_owner(hd, ptr(self.hist), self.slot_elems, self.B, self.F, fr, P, self.comm.rank, ptr(self._own_x),
+                       -1, 2, s)
+            return
+        per = kcap * (self.B * fr * 2 + CUR_STRIDE)
+        if per == 0:
+            return
+        x = self._own_x[:P * per]
+        h.lw_owner(hd, ptr(self.hist), self.slot_elems, self.B, self.F, fr, P, self.comm.rank, ptr(x), kcap, 0, s)
+        out = self._own_out[:per]
+        if self.peer is not None:
+            self.peer.reduce_scatter_(x)
+            out = x[self.comm.rank * per:(self.comm.rank + 1) * per]
+        else:
+            self.comm.reduce_scatter_(out, x.view(P, per))
+        h.lw_owner(hd, ptr(self.hist), self.slot_elems, self.B, self.F, fr, P, self.comm.rank, ptr(out), kcap, 1, s)
+
     def _split(self, h, fmask, f0, s):
         st = ptr(self.st)
         gp = self.gp
+        if self.owner:
+            fm_own, f0o, tot = self._owner_fmask(fmask, f0)
+            h.split_find(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fm_own), f0o, ptr(self.split_items),
+                         self.n_sitems, ptr(self.split_local), gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"], 1.0,
+                         1.0, st + 4 * W_N_SITEMS, ptr(self.inv_scales), ptr(self.split_part), ptr(self.split_cnt), s)
+            n = self.split_local.numel()
+            r = self.comm.rank
+            if self.peer is not None:
+                self._allr[r * n:(r + 1) * n].copy_(self.split_local)
+                self.peer.allgather_(self._allr.view(torch.int64), st + 4 * LW_DONE)
+                allr = self._allr
+            else:
+                allr = self.comm.allgather(self.split_local)
+            h.split_combine(ptr(allr), self.comm.world, self.n_sitems, st + 4 * W_N_SITEMS, self.n_sitems, tot,
+                            ptr(self.split_out), s)
+            return
         if self.split_groups > 1:
             if not h.split_node_grouped(ptr(self.hist), self.B, self.F, ptr(self.nbins_f), ptr(fmask), f0,
                                         ptr(self.split_items), self.n_sitems, ptr(self.split_out), gp["mcw"], gp["l1"],
@@ -424,10 +508,13 @@ class DeviceLeafBuilder:
             if dh[1] < it:  # this planner found nothing to split: the tree is complete
                 break
             k = int(dh[2])
-            n = k * (self.slot_elems + CUR_STRIDE)
-            h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 0, s)
-            self._allreduce(self.msg[:n])
-            h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 1, s)
+            if self.owner:
+                self._owner_sync(h, hd, s, kcap=k)
+            else:
+                n = k * (self.slot_elems + CUR_STRIDE)
+                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 0, s)
+                self._allreduce(self.msg[:n])
+                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 1, s)
             self._split(h, fmask, f0, s)
         if idle is not None:
             idle()
@@ -522,9 +609,12 @@ class DeviceLeafBuilder:
             self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
             return
         self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
-        st = ptr(self.st)
-        self.peer.allreduce_slots_(self.hist, self.slot_elems, ptr(self.build_ids), st + 4 * W_N_BUILD, self.cursor,
-                                   st + 4 * W_N_SPLIT, CUR_STRIDE, st + 4 * LW_DONE)
+        if self.owner:  # reduce-scatter by feature block (one kernel sized on the device)
+            self._owner_sync(h, hd, s)
+        else:
+            st = ptr(self.st)
+            self.peer.allreduce_slots_(self.hist, self.slot_elems, ptr(self.build_ids), st + 4 * W_N_BUILD,
+                                       self.cursor, st + 4 * W_N_SPLIT, CUR_STRIDE, st + 4 * LW_DONE)
         self._split(h, fmask, f0, s)
 
     def close(self):

@@ -134,11 +134,16 @@ class PeerReduce:
             if self.comm.log is not None:
                 del self.comm.log[-5:]
 
-    def _account(self, t: torch.Tensor, n: int):
+    def _account(self, t: torch.Tensor, n: int, skippable: bool = False):
+        """Count an exchange. ``skippable`` ones (device skip word: leaf-wise batches a host
+        queued past the tree's end are no-ops on the device) are not logged in the collective
+        sequence -- hosts queue different numbers of them, and they pair up on the device."""
         self.calls += 1
+        self.comm.last_op = ("peer_allreduce", str(t.dtype), int(n))
+        if skippable:
+            return
         self.comm.stats["calls"] += 1
         self.comm.stats["bytes"] += n * 8
-        self.comm.last_op = ("peer_allreduce", str(t.dtype), int(n))
         if self.comm.log is not None:
             self.comm.log.append(self.comm.last_op)
 
@@ -170,13 +175,24 @@ class PeerReduce:
         seg = n // self.comm.world
         return t.view(-1)[self.comm.rank * seg:(self.comm.rank + 1) * seg]
 
-    def allgather_(self, t: torch.Tensor):
+    def allgather_(self, t: torch.Tensor, skip_dev: int = 0):
         """Every segment q of ``t`` (P equal segments) <- rank q's segment q, in place (each rank
-        fills its own segment first). One kernel: the second half of the two-shot exchange."""
+        fills its own segment first). One kernel: the second half of the two-shot exchange.
+        ``skip_dev`` (optional device word address): no exchange while it is non-zero."""
         assert self.fits_segments(t), (t.dtype, t.numel(), t.data_ptr() % 16)
         n = t.numel()
-        hip().peer_allgather(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
-        self._account(t, n * t.element_size() // 8)
+        hip().peer_allgather(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t), skip_dev)
+        self._account(t, n * t.element_size() // 8, skippable=skip_dev != 0)
+
+    def reduce_scatter_dev_(self, x: torch.Tensor, seg_slot: int, nb_dev: int, k_dev: int, cur_stride: int,
+                            skip_dev: int):
+        """Reduce-scatter of the int64 message at ``x``: P equal segments of *nb_dev * seg_slot +
+        *k_dev * cur_stride words, sized on the device (leaf-wise owner-computes batch); segment
+        ``rank`` ends up reduced in place. Skipped while *skip_dev != 0. Counted with 0 bytes."""
+        assert x.dtype == torch.int64 and x.is_cuda and x.data_ptr() % 16 == 0
+        hip().peer_reduce_scatter_dev(self.hnd, ptr(x), seg_slot, nb_dev, k_dev, cur_stride, skip_dev, self.TIMEOUT_S,
+                                      stream(x))
+        self._account(x, 0, skippable=True)
 
     def allreduce_slots_(self, hist: torch.Tensor, slot_elems: int, ids: int, nb_dev: int, cursor: torch.Tensor,
                          k_dev: int, cur_stride: int, skip_dev: int):
@@ -185,7 +201,7 @@ class PeerReduce:
         known only on the device: counted as a call with 0 bytes in ``comm.stats``."""
         hip().peer_allreduce_slots(self.hnd, ptr(hist), slot_elems, ids, nb_dev, ptr(cursor), k_dev, cur_stride,
                                    skip_dev, self.TIMEOUT_S, stream(hist))
-        self._account(hist, 0)
+        self._account(hist, 0, skippable=True)
 
     def check(self):
         v = hip().peer_check(self.hnd) if self.hnd is not None else 0
