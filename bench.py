@@ -170,7 +170,7 @@ def run(a, comm):
               file=sys.stderr)
     tr_builder = tr.builder
     leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else 10
-    leaf = leaf_transport = None
+    leaf = leaf_transport = leaf_error = None
     tr.close()
     if leaf_steps > 0 and a.policy == "level":
         del tr
@@ -178,13 +178,18 @@ def run(a, comm):
                          min_split_samples=-1, learning_rate=0.1, l1=0.0, l2=0.0, grow_policy="loss")
         pl = GBDTParams(round_num=3 + leaf_steps, loss_function="sigmoid", eval_metric=["auc"],
                         missing_value="value@0", approximate=params.approximate, tree=tpl)
-        trl = GBDTTrainer(pl, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log)
-        trl.prepare()
-        trl.init_gradients()
-        leaf = timed_rounds(trl, comm, dev, 3, leaf_steps) / leaf_steps
-        assert len(trl.model.trees) == 3 + leaf_steps
-        leaf_transport = _transport(comm, trl.builder)
-        trl.close()
+        # an extra key: a failure here is reported in the line instead of losing the headline
+        try:
+            trl = GBDTTrainer(pl, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log)
+            trl.prepare()
+            trl.init_gradients()
+            leaf = timed_rounds(trl, comm, dev, 3, leaf_steps) / leaf_steps
+            assert len(trl.model.trees) == 3 + leaf_steps
+            leaf_transport = _transport(comm, trl.builder)
+            trl.close()
+        except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            leaf, leaf_error = None, f"{type(e).__name__}: {e}"[:300]
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -230,6 +235,8 @@ def run(a, comm):
             res["leafwise_vs_reference"] = round(leaf / BASELINE_SEC_PER_TREE, 6)
             res["leafwise_rounds_timed"] = leaf_steps
             res["leafwise_transport"] = leaf_transport
+        if leaf_error is not None:
+            res["leafwise_error"] = leaf_error
         print(json.dumps(res), flush=True)
 
 

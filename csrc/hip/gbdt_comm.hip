@@ -405,6 +405,7 @@ struct PeerGroup {
   long long two_shot_bytes = 1 << 20;  // YTK_PEER_TWO_SHOT_BYTES: two-shot from this size on
   int* err_host = nullptr;            // host-mapped error word
   int* err = nullptr;                 // its device address
+  int grid_cap = kXchgGrid;           // blocks per exchange (ytk_peer_set_grid_cap)
 };
 }  // namespace ytk
 static std::vector<ytk::PeerGroup> g_peer;
@@ -415,7 +416,7 @@ static size_t peer_bytes(long long cap) { return 2 * peer_sig_bytes() + 4 * (siz
 
 static void peer_launch(PeerGroup& g, const XchgMsg& m, int grid, int type, double timeout_s, hipStream_t s,
                         int mode = XM_ALLREDUCE) {
-  grid = std::max(1, std::min(grid, kXchgGrid));
+  grid = std::max(1, std::min(grid, g.grid_cap));
   const long long ticks = (long long)(timeout_s * (double)g.ticks_per_s);
 #define YTK_XCHG(T, S)                                                                                     \
   hipLaunchKernelGGL((peer_xchg_kernel<T, S>), dim3(grid), dim3(kXchgThreads), 0, s, g.pp, g.P, g.rank, m, \
@@ -592,6 +593,15 @@ void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uin
 // the host-mapped error word (1: a flag wait timed out, 2: a device-counted message exceeded
 // the slab); read after the device has drained past the exchanges
 int ytk_peer_check(int hnd) { return *(volatile int*)g_peer.at(hnd).err_host; }
+
+// At most `cap` blocks per exchange (every rank of the group must use the same cap). An
+// exchange's blocks spin on their peers' flags, so the peers' exchange kernels have to be
+// co-resident; ranks that SHARE one GPU must also leave room for each other's earlier
+// kernels, which a full 256-block exchange per rank can starve (one process per GPU never
+// co-schedules another rank's work).
+void ytk_peer_set_grid_cap(int hnd, int cap) {
+  g_peer.at(hnd).grid_cap = std::max(1, std::min(cap, ytk::kXchgGrid));
+}
 
 void ytk_peer_destroy(int hnd) {
   ytk::PeerGroup& g = g_peer.at(hnd);

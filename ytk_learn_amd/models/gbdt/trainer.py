@@ -184,7 +184,12 @@ class GBDTTrainer:
                                              timer=self.timer)
             # the builder waits on its planner while a tree grows: land the previous rounds
             # (tree conversion, loss log) in that wait instead of between trees
-            self.builder.idle_hook = lambda: self._drain(0)
+            # One GPU only: landing a round can run the eval metrics' collectives (distributed
+            # AUC), and ranks reach this wait at different batches of their trees -- a rank
+            # blocked in a host collective here would wait on a peer whose GPU waits on this
+            # rank's not-yet-enqueued batch exchange
+            if not self.comm.is_dist:
+                self.builder.idle_hook = lambda: self._drain(0)
             self.builder.snapshot_copy = self.K != 1
             self._fuse_root_pending = True
         elif self.use_device_builder:

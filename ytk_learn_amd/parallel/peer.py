@@ -71,11 +71,19 @@ class PeerReduce:
         except Exception as e:  # noqa: BLE001 -- any failure votes for RCCL
             ok = 0.0
             err = e
-        parts = comm.allgather_bytes(handle.tobytes())  # rank order, host group (every rank)
+        # the device's identity travels with the handle: ranks sharing one GPU (a rehearsal of
+        # the multi-GPU paths) cap the exchange grid so their spinning exchanges cannot starve
+        # each other's earlier kernels of compute units
+        props = torch.cuda.get_device_properties(comm.device)
+        ident = str(tuple(getattr(props, a, None) for a in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id")))
+        uuid = np.frombuffer(ident.encode()[:96].ljust(96), dtype=np.uint8)
+        parts = comm.allgather_bytes(handle.tobytes() + uuid.tobytes())  # rank order, host group
         if ok:
             try:
-                allh = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+                allh = np.frombuffer(b"".join(p[:64] for p in parts), dtype=np.uint8).copy()
                 h.peer_open(hnd, allh.ctypes.data)
+                if len({p[64:] for p in parts}) < comm.world:  # several ranks on one GPU
+                    h.peer_set_grid_cap(hnd, max(8, 256 // (2 * comm.world)))
             except Exception as e:  # noqa: BLE001
                 ok = 0.0
                 err = e
