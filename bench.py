@@ -190,6 +190,9 @@ def run(a, comm):
         except Exception as e:  # noqa: BLE001
             traceback.print_exc()
             leaf, leaf_error = None, f"{type(e).__name__}: {e}"[:300]
+            peer = getattr(getattr(locals().get("trl"), "builder", None), "peer", None)
+            if peer is not None:
+                peer.abort()  # queued exchanges return at once: the device drains, the job ends
     if rank == 0:
         res = {
             "metric": METRIC,

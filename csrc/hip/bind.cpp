@@ -139,6 +139,8 @@ void ytk_lw_owner(int, uintptr_t, long long, int, int, int, int, int, uintptr_t,
 void ytk_peer_allreduce_slots(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                               double, uintptr_t);
 int ytk_peer_check(int);
+long long ytk_peer_epoch(int);
+void ytk_peer_abort(int);
 void ytk_peer_set_grid_cap(int, int);
 void ytk_peer_destroy(int);
 void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
@@ -284,6 +286,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lw_owner", &ytk_lw_owner);
   m.def("peer_allreduce_slots", &ytk_peer_allreduce_slots);
   m.def("peer_check", &ytk_peer_check);
+  m.def("peer_epoch", &ytk_peer_epoch);
+  m.def("peer_abort", &ytk_peer_abort);
   m.def("peer_set_grid_cap", &ytk_peer_set_grid_cap);
   m.def("peer_destroy", &ytk_peer_destroy);
   m.def("lw_msg", &ytk_lw_msg);

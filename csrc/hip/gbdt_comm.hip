@@ -236,6 +236,7 @@ __device__ __forceinline__ void flag_wait(unsigned long long* const* sig, int P,
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       __builtin_amdgcn_s_sleep(1);
+      if (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;  // aborted
       if ((long long)(wall_clock64() - t0) > timeout_ticks) {
         atomicExch(err, 1);
         atomicExch(ctl + 2, 1ull);
@@ -593,6 +594,25 @@ void ytk_peer_allreduce_slots(int hnd, uintptr_t hist, long long slot_elems, uin
 // the host-mapped error word (1: a flag wait timed out, 2: a device-counted message exceeded
 // the slab); read after the device has drained past the exchanges
 int ytk_peer_check(int hnd) { return *(volatile int*)g_peer.at(hnd).err_host; }
+
+// Abort the group (the job is failing): every exchange waiting now and every later one
+// returns at once. The word is written from a stream of its own, so it lands while this
+// rank's compute stream is still blocked in an exchange.
+void ytk_peer_abort(int hnd) {
+  ytk::PeerGroup& g = g_peer.at(hnd);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+  (void)hipMemsetAsync(g.ctl + 2, 1, 1, s);
+  (void)hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+}
+
+// the group's last completed exchange epoch (synchronous copy: diagnostics after a failure)
+long long ytk_peer_epoch(int hnd) {
+  unsigned long long e = 0;
+  (void)hipMemcpy(&e, g_peer.at(hnd).ctl, sizeof(e), hipMemcpyDeviceToHost);
+  return (long long)e;
+}
 
 // At most `cap` blocks per exchange (every rank of the group must use the same cap). An
 // exchange's blocks spin on their peers' flags, so the peers' exchange kernels have to be

@@ -72,8 +72,12 @@ class PeerReduce:
             ok = 0.0
             err = e
         # the device's identity travels with the handle: ranks sharing one GPU (a rehearsal of
-        # the multi-GPU paths) cap the exchange grid so their spinning exchanges cannot starve
-        # each other's earlier kernels of compute units
+        # the multi-GPU paths) run every exchange as ONE block. An exchange's blocks spin on
+        # their peers' blocks; with several processes on one GPU the blocks of one rank's
+        # exchange need not all be scheduled while the other ranks' spin (measured: 4 ranks x
+        # 2.6M rows of leaf-wise growth deadlocked until the wait timeout with 32 blocks per
+        # exchange, ran clean with 1 -- profiles/r4/s32_*, s33_*). One process per GPU has no
+        # such coupling: a stream-ordered exchange owns the whole GPU (<= 256 blocks, one per CU).
         props = torch.cuda.get_device_properties(comm.device)
         ident = str(tuple(getattr(props, a, None) for a in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id")))
         uuid = np.frombuffer(ident.encode()[:96].ljust(96), dtype=np.uint8)
@@ -83,7 +87,9 @@ class PeerReduce:
                 allh = np.frombuffer(b"".join(p[:64] for p in parts), dtype=np.uint8).copy()
                 h.peer_open(hnd, allh.ctypes.data)
                 if len({p[64:] for p in parts}) < comm.world:  # several ranks on one GPU
-                    h.peer_set_grid_cap(hnd, max(8, 256 // (2 * comm.world)))
+                    h.peer_set_grid_cap(hnd, 1)
+                if os.environ.get("YTK_PEER_GRID_CAP"):  # (diagnostics) blocks per exchange
+                    h.peer_set_grid_cap(hnd, int(os.environ["YTK_PEER_GRID_CAP"]))
             except Exception as e:  # noqa: BLE001
                 ok = 0.0
                 err = e
@@ -214,9 +220,16 @@ class PeerReduce:
     def check(self):
         v = hip().peer_check(self.hnd) if self.hnd is not None else 0
         if v == 1:
-            raise RuntimeError("peer exchange: a flag wait timed out (a rank stopped issuing)")
+            raise RuntimeError(f"peer exchange: a flag wait timed out (a rank stopped issuing); rank {self.comm.rank}: "
+                               f"{self.calls} exchanges issued, last completed epoch {hip().peer_epoch(self.hnd)}")
         if v:
             raise RuntimeError(f"peer exchange: device error {v} (message larger than the slab)")
+
+    def abort(self):
+        """Local, for a failing job: release every exchange of this rank that waits now or
+        later (their results are void), so the device drains and the process can exit."""
+        if self.hnd is not None:
+            hip().peer_abort(self.hnd)
 
     def close(self):
         """Collective: every rank drains its device, then all free their blocks together (a
