@@ -172,6 +172,43 @@ def run_samplers(comm, out, device):
             json.dump(res, f)
 
 
+def run_peer_ops(comm, out, device):
+    """The peer-memory exchange primitives against their definitions, every dtype and both
+    exchange shapes: all-reduce (one-shot / two-shot by size), reduce-scatter and all-gather
+    of P equal segments (int64 exact, floats summed in rank order)."""
+    from ytk_learn_amd.parallel import peer as peer_mod
+    P, r = comm.world, comm.rank
+    pr = peer_mod.make(comm, 1 << 19)  # 4 MiB slabs: the 2.5 MB message runs two-shot
+    res = {"peer": pr is not None, "ok": []}
+    if pr is not None:
+        for dt in (torch.int64, torch.float64, torch.float32):
+            for n in (4 * P, 4099 * 4 * P, 160000 * 4 * P):  # P segments of whole 16-B units
+                n = min(n, pr.cap_bytes // torch.tensor([], dtype=dt).element_size() // (4 * P) * (4 * P))
+
+                def val(q):  # rank q's contribution, exactly representable in every dtype
+                    return (torch.arange(n, dtype=torch.float64, device=device) % 97 + 3 * q).to(dt)
+
+                want = sum(val(q).double() for q in range(P))
+                t = val(r).clone()
+                pr.allreduce_(t)
+                ok_ar = bool(torch.equal(t.double(), want))
+                t = val(r).clone()
+                seg = pr.reduce_scatter_(t)
+                ok_rs = bool(torch.equal(seg.double(), want.view(P, -1)[r]))
+                g = val(0).view(P, -1).clone()
+                g[r] = val(r).view(P, -1)[r] * 2
+                pr.allgather_(g.view(-1))
+                expect = torch.stack([val(q).view(P, -1)[q] * 2 for q in range(P)])
+                ok_ag = bool(torch.equal(g, expect))
+                res["ok"].append([str(dt), n, ok_ar, ok_rs, ok_ag])
+        torch.cuda.synchronize(device)
+        pr.check()
+        pr.close()
+    if comm.rank == 0:
+        with open(os.path.join(out, "res.json"), "w") as f:
+            json.dump(res, f)
+
+
 def main():
     task, out, device = sys.argv[1], sys.argv[2], sys.argv[3]
     comm = Comm.from_env(device)
@@ -193,6 +230,8 @@ def main():
             run_samplers(comm, out, dev)
         elif task == "comm":
             run_comm(comm, out, dev)
+        elif task == "peer_ops":
+            run_peer_ops(comm, out, dev)
         else:
             raise SystemExit(f"unknown task {task}")
     finally:

@@ -276,6 +276,22 @@ def test_lbfgs_peer_gradient_allreduce_one_gpu(tmp_path, task, two_shot):
     np.testing.assert_allclose(got["test_loss"], ref["test_loss"], rtol=1e-6)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_primitives_one_gpu(tmp_path, world):
+    """Ranks sharing the one GPU: the peer exchange's all-reduce (one-shot and two-shot
+    sizes), reduce-scatter and all-gather equal their definitions exactly for int64, fp64
+    and fp32 (values exactly representable, so rank-order float sums are exact too)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run("peer_ops", tmp_path, world, "cuda", extra_env={"YTK_DIST_BACKEND": "gloo", "YTK_PEER_REDUCE": "1"})
+    res = json.load(open(tmp_path / "res.json"))
+    assert res["peer"] and len(res["ok"]) == 9
+    for dt, n, ok_ar, ok_rs, ok_ag in res["ok"]:
+        assert ok_ar and ok_rs and ok_ag, (dt, n, ok_ar, ok_rs, ok_ag)
+
+
 @pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
 def test_sgd_world2_model_averaging(tmp_path, task):
     """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every
