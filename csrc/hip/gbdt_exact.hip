@@ -84,6 +84,7 @@ struct ExArgs {
   int* csplit;  // child index (2 * split rank) or -1
   int* cbeg;    // [Kmax][2]
   unsigned char* left_row;  // [N]
+  unsigned* left_bits;      // [ceil(N / 32)]: left_row == 1 as bits (behind left_row's bytes)
   ExRec* rec;
   const long long* rec_off;  // [levels] record offset of each level
   int* rec_k;
@@ -499,6 +500,28 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
   }
 }
 
+// left_bits[w] = bit b set iff left_row[32 w + b] == 1 (coalesced: 32 bytes in, one word out)
+__global__ __launch_bounds__(256) void ex_bits_kernel(ExArgs a, int n) {
+  const int nw = (n + 31) >> 5;
+  for (int w = blockIdx.x * 256 + threadIdx.x; w < nw; w += gridDim.x * 256) {
+    unsigned bits = 0;
+    const int base = w << 5;
+    if (base + 32 <= n) {
+      const uint4* p = reinterpret_cast<const uint4*>(a.left_row + base);  // 16-B aligned
+      const uint4 x0 = p[0], x1 = p[1];
+      const unsigned wd[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bits |= (((wd[k] >> (8 * c)) & 0xffu) == 1u ? 1u : 0u) << (4 * k + c);
+      }
+    } else {
+      for (int b = 0; base + b < n; ++b) bits |= (a.left_row[base + b] == 1 ? 1u : 0u) << b;
+    }
+    a.left_bits[w] = bits;
+  }
+}
+
 // One block: node sums of the flag partials (global exclusive tile prefixes recorded at each
 // node's first tile), the children's exact (g, h) totals (the next level's ntot), segments,
 // first tiles and tile table.
@@ -643,21 +666,58 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   int* ordo = a.ordw[no] + (size_t)j * a.ldw;
   float* valo = a.valw[no] + (size_t)j * a.ldw;
   longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[no] + (size_t)j * a.ldw * 2);
-  const ExSpan sp = ex_span(tl);
+  // lane-consecutive elements (element i = e * kExThreads + tid: every load instruction reads
+  // 64 consecutive positions) ranked with wave ballots: lefts before element i = the lefts of
+  // the rows e' < e of the tile, of the waves before this one in row e, and of the lanes
+  // below in this wave (the thread-contiguous layout's loads were 128-B strided per lane)
+  const int i0 = tl.y, n = tl.z - tl.y;
+  const int tid = threadIdx.x, w = tid / kWave, l = lane_id();
+  constexpr int NW = kExThreads / kWave;
   int r[kExPer];
+  float v[kExPer];
+  long long qg[kExPer], qh[kExPer];  // (a longlong2 array was kept in scratch)
   unsigned lmask = 0;
-  long long nl = 0, np = sp.n;
-#pragma unroll
-  for (int e = 0; e < kExPer; ++e) r[e] = e < sp.n ? ord[sp.i0 + e] : 0;
+  // lanes past the tile's end load its first element again (clamped index, n >= 1: a node's
+  // tiles are never empty)
 #pragma unroll
   for (int e = 0; e < kExPer; ++e) {
-    if (e < sp.n && a.left_row[r[e]] == 1) {
-      lmask |= 1u << e;
-      ++nl;
-    }
+    const int i = e * kExThreads + tid;
+    r[e] = ord[i0 + (i < n ? i : 0)];
   }
-  long long tl_left, tl_pos;
-  ex_block_excl2(nl, np, tl_left, tl_pos);  // lefts / positions of the tile before this thread
+#pragma unroll
+  for (int e = 0; e < kExPer; ++e) {
+    const int i = e * kExThreads + tid;
+    const int ic = i < n ? i : 0;
+    v[e] = val[i0 + ic];
+    const longlong2 x = qv[i0 + ic];
+    qg[e] = x.x;
+    qh[e] = x.y;
+    // the row's direction from the bitset (1.3 MB for 10.5M rows: L2 resident, unlike the
+    // 10.5 MB byte array the random gather read before)
+    lmask |= (i < n && ((a.left_bits[(unsigned)r[e] >> 5] >> (r[e] & 31)) & 1u)) ? 1u << e : 0u;
+  }
+  __shared__ int s_wc[kExPer][NW];
+  int lrank[kExPer];
+  const unsigned long long lt_mask = l == 0 ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int e = 0; e < kExPer; ++e) {
+    const unsigned long long bm = __ballot((lmask >> e) & 1u);
+    lrank[e] = __popcll(bm & lt_mask);
+    if (l == 0) s_wc[e][w] = __popcll(bm);
+  }
+  __syncthreads();
+  int off[kExPer];
+  int tl_left = 0;
+#pragma unroll
+  for (int e = 0; e < kExPer; ++e) {
+    int o = tl_left;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+      o += ww < w ? s_wc[e][ww] : 0;
+      tl_left += s_wc[e][ww];
+    }
+    off[e] = o;
+  }
   __shared__ long long s_lt;
   unsigned long long* st = a.st_cnt + (size_t)j * a.max_tiles;
   const int ft = a.ftile[par][k];
@@ -680,21 +740,22 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   __shared__ int s_r[kExTile];
   __shared__ float s_v[kExTile];
   __shared__ longlong2 s_q[kExTile];
-  int li = (int)nl, ri = (int)tl_left + (int)(np - nl);
 #pragma unroll
   for (int e = 0; e < kExPer; ++e) {
-    if (e < sp.n) {
-      const int dst = (lmask >> e) & 1 ? li++ : ri++;
+    const int i = e * kExThreads + tid;
+    if (i < n) {
+      const int lb = off[e] + lrank[e];  // lefts before element i
+      const int dst = (lmask >> e) & 1 ? lb : tl_left + (i - lb);
       s_r[dst] = r[e];
-      s_v[dst] = val[sp.i0 + e];
-      s_q[dst] = qv[sp.i0 + e];
+      s_v[dst] = v[e];
+      s_q[dst] = make_longlong2(qg[e], qh[e]);
     }
   }
   __syncthreads();
   const int ntile = tl.z - tl.y;
-  const int l0 = a.cbeg[2 * k] + lt, r0 = a.cbeg[2 * k + 1] + (before - lt) - (int)tl_left;
+  const int l0 = a.cbeg[2 * k] + lt, r0 = a.cbeg[2 * k + 1] + (before - lt) - tl_left;
   for (int i = threadIdx.x; i < ntile; i += kExThreads) {
-    const int dst = i < (int)tl_left ? l0 + i : r0 + i;
+    const int dst = i < tl_left ? l0 + i : r0 + i;
     ordo[dst] = s_r[i];
     valo[dst] = s_v[i];
     qo[dst] = s_q[i];
@@ -703,11 +764,12 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
 
 // one level's launches; the level parity picks the ping-pong buffers at compile time
 template <int kPar>
-void ex_level(const ExArgs& a, int d, long long blocks, hipStream_t s) {
+void ex_level(const ExArgs& a, int d, long long blocks, int n, int bits_grid, hipStream_t s) {
   hipLaunchKernelGGL(ex_eval_kernel<kPar>, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
   hipLaunchKernelGGL(ex_decide_kernel<kPar>, dim3(1), dim3(kExBig), 0, s, a, d, 0);
   hipLaunchKernelGGL(ex_flag_kernel<kPar>, dim3(a.max_tiles), dim3(kExThreads), 0, s, a, d);
   hipLaunchKernelGGL(ex_layout_kernel<kPar>, dim3(1), dim3(kExBig), 0, s, a, d);
+  hipLaunchKernelGGL(ex_bits_kernel, dim3(bits_grid), dim3(256), 0, s, a, n);
   hipLaunchKernelGGL(ex_part_kernel<kPar>, dim3((unsigned)blocks), dim3(kExThreads), 0, s, a, d);
 }
 
@@ -760,13 +822,14 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
   a.go_thr = (float*)p[i++];
   a.csplit = (int*)p[i++];
   a.cbeg = (int*)p[i++];
-  a.left_row = (unsigned char*)p[i++];
+  a.left_row = (unsigned char*)p[i++];  // [align16(ldw) + 4 * ceil(ldw / 32)] bytes: bytes, then bits
   a.rec = (ExRec*)p[i++];
   a.rec_off = (const long long*)p[i++];
   a.rec_k = (int*)p[i++];
   a.ld0 = ip[0];
   a.ldw = ip[1];
   a.ldx = ip[2];
+  a.left_bits = reinterpret_cast<unsigned*>(a.left_row + ((a.ldw + 15) & ~15LL));
   a.max_tiles = (int)ip[3];
   a.Kmax = (int)ip[4];
   a.min_split_samples = (int)ip[5];
@@ -804,6 +867,7 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
   if (blocks > 0x7fffffffLL) throw std::invalid_argument("ex_tree: too many (tile, feature) blocks");
   const size_t st_gh_bytes = (size_t)nf * a.max_tiles * 2 * 8, st_cnt_bytes = (size_t)nf * a.max_tiles * 8;
   hipLaunchKernelGGL(ex_init_kernel, dim3(1), dim3(kExBig), 0, s, a, n);
+  const int bits_grid = std::max(1, std::min(((n + 31) / 32 + 255) / 256, 2048));
   const int gx = std::max(1, std::min((n + kExThreads - 1) / kExThreads, 1024));
   hipLaunchKernelGGL(ex_gather_kernel, dim3(gx, nf), dim3(kExThreads), 0, s, a, n);
   for (int d = 0; d <= depth; ++d) {
@@ -817,9 +881,9 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
     YTK_HIP_CHECK(hipMemsetAsync(a.st_gh, 0, st_gh_bytes, s));
     YTK_HIP_CHECK(hipMemsetAsync(a.st_cnt, 0, st_cnt_bytes, s));
     if (d & 1)
-      ex_level<1>(a, d, blocks, s);
+      ex_level<1>(a, d, blocks, n, bits_grid, s);
     else
-      ex_level<0>(a, d, blocks, s);
+      ex_level<0>(a, d, blocks, n, bits_grid, s);
   }
   YTK_LAUNCH_CHECK();
 }

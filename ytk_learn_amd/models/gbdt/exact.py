@@ -145,7 +145,8 @@ class ExactGreedyBuilder:
         self.ex_ntot = i64(Kmax * 2)
         self.ex_go_feat, self.ex_go_thr = i32(Kmax), torch.zeros(Kmax, dtype=torch.float32, device=dev)
         self.ex_csplit, self.ex_cbeg = i32(Kmax), i32(2 * Kmax)
-        self.ex_left = torch.zeros(max(1, N), dtype=torch.uint8, device=dev)
+        # left_row bytes [align16(N)] followed by the same flags as bits [ceil(N / 32)] words
+        self.ex_left = torch.zeros(((N + 15) // 16) * 16 + 4 * ((N + 31) // 32) + 16, dtype=torch.uint8, device=dev)
         ks = [min(Kmax, 1 << min(d, 40)) for d in range(D + 1)]
         self.rec_off = np.concatenate([[0], np.cumsum(ks)[:-1]]).astype(np.int64)
         self.ex_rec = torch.zeros(int(sum(ks)) * self.REC_DTYPE.itemsize, dtype=torch.uint8, device=dev)
