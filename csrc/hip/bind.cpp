@@ -91,6 +91,8 @@ void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uint
                      uintptr_t, uintptr_t);
 // blas.hip
 void ytk_dot(uintptr_t, uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t);
+void ytk_row_loss(int, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t, long long, uintptr_t, uintptr_t,
+                  uintptr_t, uintptr_t, uintptr_t);
 void ytk_axpy_dot(uintptr_t, uintptr_t, float, float, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
@@ -203,6 +205,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);
   m.def("dot", &ytk_dot);
+  m.def("row_loss", &ytk_row_loss);
   m.def("axpy_dot", &ytk_axpy_dot);
   m.def("fm_forward", &ytk_fm_forward);
   m.def("fm_backward", &ytk_fm_backward);

@@ -867,7 +867,9 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
   if (blocks > 0x7fffffffLL) throw std::invalid_argument("ex_tree: too many (tile, feature) blocks");
   const size_t st_gh_bytes = (size_t)nf * a.max_tiles * 2 * 8, st_cnt_bytes = (size_t)nf * a.max_tiles * 8;
   hipLaunchKernelGGL(ex_init_kernel, dim3(1), dim3(kExBig), 0, s, a, n);
-  const int bits_grid = std::max(1, std::min(((n + 31) / 32 + 255) / 256, 2048));
+  // the bitset covers every row id (a sampled tree's n counts its kept rows, not the id range)
+  const int nrow = (int)a.ldw;
+  const int bits_grid = std::max(1, std::min(((nrow + 31) / 32 + 255) / 256, 2048));
   const int gx = std::max(1, std::min((n + kExThreads - 1) / kExThreads, 1024));
   hipLaunchKernelGGL(ex_gather_kernel, dim3(gx, nf), dim3(kExThreads), 0, s, a, n);
   for (int d = 0; d <= depth; ++d) {
@@ -881,9 +883,9 @@ void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled,
     YTK_HIP_CHECK(hipMemsetAsync(a.st_gh, 0, st_gh_bytes, s));
     YTK_HIP_CHECK(hipMemsetAsync(a.st_cnt, 0, st_cnt_bytes, s));
     if (d & 1)
-      ex_level<1>(a, d, blocks, n, bits_grid, s);
+      ex_level<1>(a, d, blocks, nrow, bits_grid, s);
     else
-      ex_level<0>(a, d, blocks, n, bits_grid, s);
+      ex_level<0>(a, d, blocks, nrow, bits_grid, s);
   }
   YTK_LAUNCH_CHECK();
 }

@@ -194,3 +194,31 @@ def test_fused_two_loop_matches_unfused(monkeypatch, m, loops, cursor):
     assert opt._fused_two_loop(got)
     opt.hv(got, cursor, loops, 2.0, 3.0)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["sigmoid", "l2"])
+@pytest.mark.parametrize("z64,with_z1", [(False, False), (True, False), (False, True)])
+def test_fused_row_loss_matches_torch_formulas(name, z64, with_z1):
+    """ops.blas.row_loss (one fused HIP pass: loss sum, pred, weight * l') == the loss classes'
+    fp64 torch formulas that the linear / FM / FFM models run otherwise."""
+    from ytk_learn_amd.ops.blas import row_loss
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(5)
+    n = 100_003
+    z0 = (torch.randn(n, generator=g) * 6).to(torch.float64 if z64 else torch.float32)
+    z1 = torch.randn(n, generator=g).float() if with_z1 else None
+    yy = torch.stack([(torch.rand(n, generator=g) < 0.4).float(), torch.rand(n, generator=g)], 1)
+    wt = torch.rand(n, generator=g) + 0.5
+    loss = create_loss(name)
+    out = row_loss(loss, z0.to(dev), yy.to(dev)[:, 0], wt.to(dev), z1=z1.to(dev) if z1 is not None else None)
+    assert out is not None
+    lsum, pred, c = out
+    z = z0.double() + (z1.double() if z1 is not None else 0.0)
+    y, w = yy[:, 0].double(), wt.double()
+    ref_sum = float((w * loss.loss(z, y)).sum())
+    assert abs(lsum - ref_sum) <= 1e-12 * abs(ref_sum) + 1e-9
+    torch.testing.assert_close(pred.cpu(), loss.predict(z).float(), rtol=1e-6, atol=0)
+    torch.testing.assert_close(c.cpu(), (w * loss.grad(z, y)).float(), rtol=1e-6, atol=1e-7)
+    assert row_loss(loss, z0.to(dev), yy.to(dev)[:, 0], wt.to(dev), want_grad=False)[2] is None
+    assert row_loss(create_loss("hinge"), z0.to(dev), yy.to(dev)[:, 0], wt.to(dev)) is None

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from ...data.dataflow import read_dict_files
+from ...ops.blas import row_loss
 from ...ops.ffm import ffm_backward_csc, ffm_forward, ffm_pairs_cpu
 from ...utils.errors import YtkLearnError
 from ...utils.javafmt import java_double_str
@@ -84,18 +85,24 @@ class FFMModel(ContinuousModelBase):
         return self._cache[key]
 
     def _forward(self, X, d, w, g, key):
-        fx = X.matmul(w[:self.F]).double()
+        z_lin = X.matmul(w[:self.F])
         V = w[self.F:]
         cache = self._pairs(key, d)
+        z_pair = None
         if self.stride > 0:
-            fx = fx + ffm_forward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, cache=cache,
-                                 skip_feat=self._skip).double()
-        y = d.y[:, 0].double()
-        wt = d.weight.double()
-        lv = self.loss.loss(fx, y)
-        pred = self.loss.predict(fx).float()
+            z_pair = ffm_forward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, cache=cache,
+                                 skip_feat=self._skip)
+        fused = row_loss(self.loss, z_lin, d.y[:, 0], d.weight, z1=z_pair, want_grad=g is not None)
+        if fused is not None:  # one fused row pass (sigmoid / l2 on the GPU)
+            lsum, pred, c = fused
+        else:
+            fx = z_lin.double() + (z_pair.double() if z_pair is not None else 0.0)
+            y = d.y[:, 0].double()
+            wt = d.weight.double()
+            lsum = float((wt * self.loss.loss(fx, y)).sum())
+            pred = self.loss.predict(fx).float()
+            c = (wt * self.loss.grad(fx, y)).float().contiguous() if g is not None else None
         if g is not None:
-            c = (wt * self.loss.grad(fx, y)).float().contiguous()
             X.t_matmul(c, out=g[:self.F])
             if self.stride > 0:
                 gv = g[self.F:]
@@ -107,7 +114,7 @@ class FFMModel(ContinuousModelBase):
                 g[self.F:] = 0.0
             if not self.bias_latent and self.need_second and self.p.model.need_bias and self.stride > 0:
                 g[self.F:self.F + self.stride] = 0.0
-        return float((wt * lv).sum()), pred
+        return lsum, pred
 
     def pure_loss_grad(self, w, g):
         loss, pred = self._forward(self.X, self.data.train, w, g, "train")

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from ...ops._ext import native
+from ...ops.blas import row_loss
 from ...ops.fm import fm_backward, fm_forward
 from .base import ContinuousModelBase, fmt_f, jfloat
 from ...utils.javafmt import java_double_str
@@ -78,12 +79,16 @@ class FMModel(ContinuousModelBase):
 
     def _forward(self, X, d, w, g):
         fx, S = self._fx(X, w)
-        y = d.y[:, 0].double()
-        wt = d.weight.double()
-        lv = self.loss.loss(fx, y)
-        pred = self.loss.predict(fx).float()
+        fused = row_loss(self.loss, fx, d.y[:, 0], d.weight, want_grad=g is not None)
+        if fused is not None:  # one fused row pass (sigmoid / l2 on the GPU)
+            lsum, pred, c = fused
+        else:
+            y = d.y[:, 0].double()
+            wt = d.weight.double()
+            lsum = float((wt * self.loss.loss(fx, y)).sum())
+            pred = self.loss.predict(fx).float()
+            c = (wt * self.loss.grad(fx, y)).float() if g is not None else None
         if g is not None:
-            c = (wt * self.loss.grad(fx, y)).float()
             if self.kk > 0:
                 fm_backward(X, c, S, w[self.F:].view(self.F, self.kk), g[:self.F], g[self.F:].view(self.F, self.kk))
             else:
@@ -94,7 +99,7 @@ class FMModel(ContinuousModelBase):
                 g[self.F:] = 0.0
             if not self.bias_latent and self.need_second and self.p.model.need_bias and self.kk > 0:
                 g[self.F:self.F + self.kk] = 0.0
-        return float((wt * lv).sum()), pred
+        return lsum, pred
 
     def pure_loss_grad(self, w, g):
         loss, pred = self._forward(self.X, self.data.train, w, g)

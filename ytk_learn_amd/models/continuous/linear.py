@@ -6,7 +6,8 @@ the intercept :179-206) and ``J/dataflow/LinearModelDataFlow.java`` (zero init, 
 train by name :67-121, dump ``name,w,precision`` with ``%f`` and ``_bias_,w,null``).
 
 Device path: z and g are the deterministic segmented SpMV kernels of
-``csrc/hip/sparse.hip``; per-row loss math is fp64 torch on the GPU.
+``csrc/hip/sparse.hip``; the per-row fp64 loss math is one fused pass (``ops.blas.row_loss``)
+for sigmoid / l2 and fp64 torch otherwise.
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ...ops.blas import row_loss
 from .base import ContinuousModelBase, fmt_f, jfloat
 
 
@@ -41,7 +43,14 @@ class LinearModel(ContinuousModelBase):
         return [(self.bias_delta, self.dim)]
 
     def _forward(self, X, d, w, g):
-        z = X.matmul(w).double()
+        z32 = X.matmul(w)
+        fused = row_loss(self.loss, z32, d.y[:, 0], d.weight, want_grad=g is not None)
+        if fused is not None:  # one fused row pass (sigmoid / l2 on the GPU)
+            loss, pred, c = fused
+            if g is not None:
+                X.t_matmul(c, out=g)
+            return loss, pred
+        z = z32.double()
         y = d.y[:, 0].double()
         wt = d.weight.double()
         lv = self.loss.loss(z, y)
@@ -49,12 +58,11 @@ class LinearModel(ContinuousModelBase):
         if g is not None:
             d1 = self.loss.grad(z, y)
             X.t_matmul((wt * d1).float(), out=g)
-        return float((wt * lv).sum()), pred, z, y
+        return float((wt * lv).sum()), pred
 
     def pure_loss_grad(self, w, g):
-        loss, pred, z, y = self._forward(self.X, self.data.train, w, g)
+        loss, pred = self._forward(self.X, self.data.train, w, g)
         self.pred = pred[:, None]
-        self._z = z
         return loss
 
     def test_pure_loss_grad(self, w, g):
@@ -63,7 +71,7 @@ class LinearModel(ContinuousModelBase):
             return 0.0
         if g is not None and self.Xt._csc is None:
             self.Xt._build_csc()
-        loss, pred, _, _ = self._forward(self.Xt, d, w, g)
+        loss, pred = self._forward(self.Xt, d, w, g)
         self.pred_test = pred[:, None]
         return loss
 

@@ -5,6 +5,8 @@ derivatives and regularizer sums over the full model vector. On CPU: torch in fp
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._ext import check_cuda, hip, ptr, stream
@@ -75,3 +77,35 @@ def axpy_dot(p: torch.Tensor, x: torch.Tensor, alpha: float, scale: float, d: to
     hip().axpy_dot(ptr(p), ptr(x), float(alpha), float(scale), ptr(d), p.numel(), ptr(buf), ptr(buf[1024:]),
                    stream(p))
     return float(buf[1024])
+
+
+_ROW_LOSS = {"sigmoid": 0, "l2": 1}
+
+
+def row_loss(loss, z0: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, z1=None, want_grad: bool = True):
+    """One fused pass over the rows of a single-output L-BFGS model (``row_loss_partial_kernel``):
+    z = z0 (+ z1) in fp64 -> (sum weight * loss (fp64 float), pred fp32 [n], c = weight * l'(z)
+    fp32 [n] or None). The formulas are the loss classes' fp64 ones
+    (``losses/functions.py``, reference LinearHoagOptimizer.java:127-147). Returns None when the
+    fused pass does not cover the case (CPU tensors, losses other than sigmoid / l2,
+    YTK_ROW_LOSS=0): the caller runs the torch formulas then."""
+    lid = _ROW_LOSS.get(getattr(loss, "name", None))
+    if lid is None or z0.device.type != "cuda" or os.environ.get("YTK_ROW_LOSS", "1") == "0":
+        return None
+    n = z0.numel()
+    if (z0.dim() != 1 or not z0.is_contiguous() or z0.dtype not in (torch.float32, torch.float64)
+            or y.dim() != 1 or y.dtype != torch.float32 or y.numel() != n or wt.numel() != n):
+        return None
+    if z1 is not None and (z1.dtype != torch.float32 or not z1.is_contiguous() or z1.numel() != n):
+        return None
+    wt = wt.float().contiguous()
+    check_cuda(z0, wt, *([z1] if z1 is not None else []))
+    if not y.is_cuda or y.device != z0.device:
+        raise ValueError("row_loss: labels on another device")
+    pred = torch.empty(n, dtype=torch.float32, device=z0.device)
+    c = torch.empty(n, dtype=torch.float32, device=z0.device) if want_grad else None
+    buf = _buffers(z0.device)
+    hip().row_loss(lid, ptr(z0), 1 if z0.dtype == torch.float64 else 0, ptr(z1) if z1 is not None else 0, ptr(y),
+                   y.stride(0), ptr(wt), n, ptr(pred), ptr(c) if c is not None else 0, ptr(buf), ptr(buf[1024:]),
+                   stream(z0))
+    return float(buf[1024]), pred, c
