@@ -269,7 +269,7 @@ def ffm_backward_csc(X, fld, V, nfield: int, k: int, coef, gV, skip_feat: int = 
     # general rows: one wave per chunk, the row entries read per column (L2-miss bound on its
     # random 16-B latent gathers: 274 GB fetched per Criteo-shape pass vs 46 GB for the
     # row-oriented forward, which reuses a row's latent blocks across its pairs)
-    h.ffm_grad_csc(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
+    h.ffm_grad_csc(ptr(X.chunk_bounds), ptr(X.chunk_end_b), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals),
                    ptr(X.csc_perm), ptr(X.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
                    ptr(Vt), X.ncols, nfield, k, ptr(coef), ptr(part), int(skip_feat), int(distinct), s)
     chunk_reduce(X.chunk_ptr, X.ncols, part, J, gV, J, 1.0, 1, ptr(X.chunk_ids), s, X.heavy_cols)

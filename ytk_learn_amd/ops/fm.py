@@ -44,7 +44,7 @@ def fm_backward(X, c: torch.Tensor, S: torch.Tensor, V: torch.Tensor, g_lin: tor
         part = torch.empty((max(X.n_chunks, 1), k + 2), dtype=torch.float32, device=X.device)
         tot = torch.empty((X.ncols, k + 2), dtype=torch.float32, device=X.device)
         h, s = hip(), stream(c)
-        h.fm_backward(ptr(X.chunk_beg), ptr(X.chunk_end), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals), ptr(c),
+        h.fm_backward(ptr(X.chunk_bounds), ptr(X.chunk_end_b), X.n_chunks, ptr(X.csc_rows), ptr(X.csc_vals), ptr(c),
                       ptr(S.contiguous()), k, ptr(part), s)
         chunk_reduce(X.chunk_ptr, X.ncols, part, k + 2, tot, k + 2, 1.0, 0, ptr(X.chunk_ids), s, X.heavy_cols)
         g_lin.copy_(tot[:, k])
