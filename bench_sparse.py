@@ -117,14 +117,14 @@ def main():
     if a.optimizer == "sgd":
         from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
         ng = model.ngroups if hasattr(model, "ngroups") else 1
-        sgd = SGDOptimizer(model, SGDParams(learning_rate=0.01, batch_size=a.batch, epochs=1, dtype=a.dtype),
+        sgd = SGDOptimizer(model, SGDParams(learning_rate=0.05, batch_size=a.batch, epochs=1, dtype=a.dtype),
                            [0.0] * ng, [1e-6] * ng, comm, log, tot, tot)
         sgd._sync_copy(model.w)
         bounds = [(b, min(b + a.batch, n)) for b in range(0, n, a.batch)]
 
         def epoch():
             for b, e in bounds:
-                sgd._step(model.w, b, e, 0.01)
+                sgd._step(model.w, b, e, 0.05)
             sgd._average(model.w)
 
         for _ in range(a.warmup):

@@ -76,7 +76,7 @@ void ytk_seg_tile_spmv(uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_
                        int, uintptr_t);
 // ffm.hip
 void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, int,
-                   uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+                   uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
 void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
                       int, int, uintptr_t);
@@ -84,7 +84,8 @@ void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, 
                          long long, uintptr_t, int, uintptr_t, long long, int, int, uintptr_t, uintptr_t);
 // fm.hip
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
-                       uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t);
+                       uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t, uintptr_t);
+void ytk_sgd_count(uintptr_t, uintptr_t, long long, long long, uintptr_t, int, uintptr_t);
 void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                     uintptr_t, int, uintptr_t);
 void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
@@ -210,6 +211,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fm_forward", &ytk_fm_forward);
   m.def("fm_backward", &ytk_fm_backward);
   m.def("fm_sgd_update", &ytk_fm_sgd_update);
+  m.def("sgd_count", &ytk_sgd_count);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)

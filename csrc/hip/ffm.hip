@@ -39,7 +39,9 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
     const int* __restrict__ fld, long long nrows, const float* __restrict__ V, int nfield, int k,
     float* __restrict__ fx, const float* __restrict__ coef, float* __restrict__ gV, int vec4,
-    int skip_feat) {
+    int skip_feat, const int* __restrict__ cnt) {
+  // cnt (backward, optional): rows per feature of the SGD batch -- V[i, :] takes the
+  // per-feature mean of the batch's steps (see fm_sgd_update_kernel)
   const long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
@@ -75,11 +77,13 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
             acc += pair_dot(vp, vq, k, vec4 != 0) * xx;
           } else {
             const float s = c * xx;
+            const float sp = cnt ? s / (float)max(1, cnt[ipb]) : s;
+            const float sq = cnt ? s / (float)max(1, cnt[iq]) : s;
             float* gp = gV + (long long)ipb * stride + (long long)fq * k;
             float* gq = gV + (long long)iq * stride + (long long)fpb * k;
             for (int f = 0; f < k; ++f) {
-              unsafeAtomicAdd(gp + f, s * vq[f]);
-              unsafeAtomicAdd(gq + f, s * vp[f]);
+              unsafeAtomicAdd(gp + f, sp * vq[f]);
+              unsafeAtomicAdd(gq + f, sq * vp[f]);
             }
           }
         }
@@ -404,7 +408,7 @@ extern "C" {
 // fx[row] = pair interaction sum (forward) or g += pair gradients scaled by coef[row].
 void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld, long long nrows,
                    uintptr_t V, int nfield, int k, uintptr_t fx, uintptr_t coef, uintptr_t gV,
-                   int backward, int skip_feat, uintptr_t stream) {
+                   int backward, int skip_feat, uintptr_t stream, uintptr_t cnt) {
   if (nrows <= 0 || k <= 0) return;
   const long long threads = nrows * 64;
   const dim3 grid((unsigned)((threads + 255) / 256));
@@ -413,14 +417,14 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
   if (backward)
     hipLaunchKernelGGL(ffm_pairs_kernel<true>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
-                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat);
+                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat, (const int*)cnt);
   else if (vec4 && k == 4 && !getenv_off("YTK_FFM_K4"))
     hipLaunchKernelGGL(ffm_pairs_k4_kernel, grid, dim3(256), 0, s, (const long long*)indptr, (const int*)idx,
                        (const float*)val, (const int*)fld, nrows, (const float*)V, nfield, (float*)fx, skip_feat);
   else
     hipLaunchKernelGGL(ffm_pairs_kernel<false>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
-                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat);
+                       nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat, (const int*)nullptr);
   YTK_LAUNCH_CHECK();
 }
 

@@ -16,6 +16,8 @@
 
 #include <hip/hip_bf16.h>
 
+#include <algorithm>
+
 namespace ytk {
 
 // Latent factors may be stored in bf16 (SGD with optimization.sgd.dtype = bf16): the
@@ -141,19 +143,25 @@ __global__ __launch_bounds__(256) void fm_backward_kernel(
 // race exactly as in Hogwild! (updates are never lost, reads may be stale). reg_skip is
 // the bias index (not regularised; its latent row is frozen unless bias_latent);
 // upd_w = 0 leaves all linear weights but the bias untouched (k[0] < 1).
+// cnt (optional, int32 [F]): the batch's rows per feature (sgd_count_kernel); the step of a
+// weight is then divided by its count -- the per-feature mean of the batch's per-sample
+// gradients (optimization.sgd.average = feature): with thousands of concurrent rows per
+// batch a hot feature (the bias is in every row) otherwise takes the SUM of its rows' steps
+// at once and the model diverges.
 template <int G>
 __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
     long long nrows, float* __restrict__ w, float* __restrict__ V, int k, const float* __restrict__ S,
     const float* __restrict__ c, float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent,
-    __hip_bfloat16* __restrict__ Vb) {
+    __hip_bfloat16* __restrict__ Vb, const int* __restrict__ cnt) {
   const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
   const int f = threadIdx.x & (G - 1);
-  if (gid >= nrows) return;
-  const float cr = c[gid];
-  if (cr == 0.f) return;  // group-uniform
-  const long long b = indptr[gid], e = indptr[gid + 1];
-  const float s = (f < k) ? S[gid * k + f] : 0.f;
+  // the bias weight (reg_skip: in every row) is summed over the block and takes ONE atomic
+  // per block: a device atomic per row on one address serialises the whole batch
+  float bias_acc = 0.f;
+  const float cr = gid < nrows ? c[gid] : 0.f;
+  const long long b = cr != 0.f ? indptr[gid] : 0, e = cr != 0.f ? indptr[gid + 1] : 0;  // group-uniform
+  const float s = (cr != 0.f && f < k) ? S[gid * k + f] : 0.f;
   for (long long t = b; t < e; t += G) {
     int my_i = 0;
     float my_x = 0.f;
@@ -163,9 +171,11 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
       const int i = __shfl(my_i, j, G);
       const float x = __shfl(my_x, j, G);
       const bool is_bias = i == reg_skip;
+      const float lri = cnt ? lr / (float)max(1, cnt[i]) : lr;
       if (f == 0 && (upd_w || is_bias)) {
         const float gw = cr * x + (is_bias ? 0.f : l2w * w[i]);
-        unsafeAtomicAdd(w + i, -lr * gw);
+        if (is_bias) bias_acc += -lri * gw;
+        else unsafeAtomicAdd(w + i, -lri * gw);
       }
       if (f < k && (!is_bias || bias_latent)) {
         const long long o = (long long)i * k + f;
@@ -173,18 +183,75 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
                    // master takes the update (returning atomic), mirror re-rounded from it
           const float v = __bfloat162float(Vb[o]);
           const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
-          const float d = -lr * gv;
+          const float d = -lri * gv;
           const float old = atomicAdd(V + o, d);
           Vb[o] = __float2bfloat16(old + d);  // races with other rows: Hogwild!-tolerant
         } else {
           float* vp = V + o;
           const float v = *vp;
           const float gv = cr * x * (s - v * x) + (is_bias ? 0.f : l2v * v);
-          unsafeAtomicAdd(vp, -lr * gv);
+          unsafeAtomicAdd(vp, -lri * gv);
         }
       }
     }
   }
+  if (reg_skip >= 0) {
+    __shared__ float s_bias[256 / kWave];
+    bias_acc = wave_sumf(bias_acc);
+    if (lane_id() == 0) s_bias[threadIdx.x / kWave] = bias_acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tot = 0.f;
+      for (int q = 0; q < 256 / kWave; ++q) tot += s_bias[q];
+      if (tot != 0.f) unsafeAtomicAdd(w + reg_skip, tot);
+    }
+  }
+}
+
+// Rows per feature of a mini-batch (clear = 0: cnt[i] += 1 per entry) and the reset of the
+// touched counters afterwards (clear = 1: plain stores of 0), over the batch's entries
+// [indptr[0], indptr[nrows]) (device row pointers: no host read). Counting aggregates in
+// an LDS hash table per block first (a block takes one contiguous run of entries): one
+// global atomic per (block, distinct feature) instead of one per entry -- the bias is in
+// every row, and 65536 same-address device atomics per batch serialise (~1 ms per batch).
+// Keys that find no slot within kCntProbe probes go straight to the global counter.
+constexpr int kCntSlots = 4096;
+constexpr int kCntProbe = 8;
+__global__ __launch_bounds__(256) void sgd_count_kernel(const long long* __restrict__ indptr,
+                                                        const int* __restrict__ idx, long long nrows,
+                                                        int* __restrict__ cnt, int clear) {
+  const long long b = indptr[0], e = indptr[nrows];
+  if (clear) {
+    for (long long t = b + blockIdx.x * 256LL + threadIdx.x; t < e; t += (long long)gridDim.x * 256) cnt[idx[t]] = 0;
+    return;
+  }
+  __shared__ int s_key[kCntSlots];
+  __shared__ int s_val[kCntSlots];
+  for (int i = threadIdx.x; i < kCntSlots; i += 256) {
+    s_key[i] = -1;
+    s_val[i] = 0;
+  }
+  __syncthreads();
+  const long long per = (e - b + gridDim.x - 1) / gridDim.x;
+  const long long r0 = b + blockIdx.x * per, r1 = min(e, r0 + per);
+  for (long long t = r0 + threadIdx.x; t < r1; t += 256) {
+    const int k = idx[t];
+    unsigned h = ((unsigned)k * 2654435761u) >> 20;  // 12 bits: kCntSlots
+    bool done = false;
+    for (int p = 0; p < kCntProbe; ++p) {
+      const int old = atomicCAS(&s_key[h], -1, k);
+      if (old == -1 || old == k) {
+        atomicAdd(&s_val[h], 1);
+        done = true;
+        break;
+      }
+      h = (h + 1) & (kCntSlots - 1);
+    }
+    if (!done) atomicAdd(cnt + k, 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kCntSlots; i += 256)
+    if (s_key[i] >= 0) atomicAdd(cnt + s_key[i], s_val[i]);
 }
 
 }  // namespace ytk
@@ -259,7 +326,7 @@ void ytk_fm_backward(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, ui
 // when k == 0 (linear model).
 void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nrows, uintptr_t w,
                        uintptr_t V, int k, uintptr_t S, uintptr_t c, float lr, float l2w, float l2v,
-                       int reg_skip, int upd_w, int bias_latent, uintptr_t Vb, uintptr_t stream) {
+                       int reg_skip, int upd_w, int bias_latent, uintptr_t Vb, uintptr_t cnt, uintptr_t stream) {
   if (nrows <= 0) return;
   if (k < 0 || k > 64) throw std::invalid_argument("fm_sgd_update: 0 <= k <= 64");
   const int G = k == 0 ? 4 : fm_group(k);
@@ -270,7 +337,7 @@ void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long
   hipLaunchKernelGGL(fm_sgd_update_kernel<GG>, grid, dim3(256), 0, s, (const long long*)indptr, \
                      (const int*)idx, (const float*)val, nrows, (float*)w, (float*)V, k,        \
                      (const float*)S, (const float*)c, lr, l2w, l2v, reg_skip, upd_w, bias_latent,     \
-                     (__hip_bfloat16*)Vb)
+                     (__hip_bfloat16*)Vb, (const int*)cnt)
   switch (G) {
     case 4: YTK_FM_S(4); break;
     case 8: YTK_FM_S(8); break;
@@ -279,6 +346,18 @@ void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long
     default: YTK_FM_S(64); break;
   }
 #undef YTK_FM_S
+  YTK_LAUNCH_CHECK();
+}
+
+// cnt[i] += 1 per entry of the batch rows (clear = 0) or cnt[i] = 0 for them (clear = 1).
+void ytk_sgd_count(uintptr_t indptr, uintptr_t idx, long long nrows, long long nnz_hint, uintptr_t cnt, int clear,
+                   uintptr_t stream) {
+  if (nrows <= 0) return;
+  // count: blocks of >= 4096 entries (the hash table pays off per block); clear: 256 per block
+  const long long want = (std::max<long long>(nnz_hint, 1) + (clear ? 255 : 4095)) / (clear ? 256 : 4096);
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, clear ? 4096 : 1024));
+  hipLaunchKernelGGL(sgd_count_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const long long*)indptr, (const int*)idx, nrows, (int*)cnt, clear);
   YTK_LAUNCH_CHECK();
 }
 

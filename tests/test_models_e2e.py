@@ -241,6 +241,34 @@ def test_sgd_optimizer_gpu(cuda, bin_data, tmp_path, model):
     assert abs(rg[1] - rc[1]) < 0.05, (rg, rc)
 
 
+@pytest.mark.parametrize("model", ["linear", "fm", "ffm"])
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_sgd_large_batch_per_feature_average(bin_data, tmp_path, model, dev):
+    """Batches of 1024 rows (every row holds the bias and a few hot features): with
+    optimization.sgd.average = feature each weight takes the mean step of the rows holding
+    its feature and training converges; the summed per-sample steps (average = none) of
+    the same run are ~1024x larger on the bias and diverge -- the NaN / 5e11 training losses
+    of the round-1 Criteo-shape SGD benches."""
+    import math
+
+    import torch
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    tr, te = ("ftrain.txt", "ftest.txt") if model == "ffm" else ("train.txt", "test.txt")
+    res = {}
+    for avg in ("feature", "none"):
+        kw = _sgd_kw(**{"optimization.sgd.batch_size": 1024, "optimization.sgd.learning_rate": 0.5,
+                        "optimization.sgd.epochs": 8, "optimization.sgd.average": avg})
+        if model == "ffm":
+            kw.update({"model.field_dict_path": str(bin_data / "fields.dict"), "k": [1, 2]})
+        if model == "fm":
+            kw["k"] = [1, 4]
+        res[avg] = train(model, _cfg(model, str(tmp_path / avg), str(bin_data / tr), str(bin_data / te), **kw),
+                         comm=_local(dev))
+    assert res["feature"][1] < 0.6 and res["feature"][0] < 0.6, res
+    assert not (math.isfinite(res["none"][1]) and res["none"][1] < 0.6), res
+
+
 @pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 def test_fm_sgd_bf16_matches_fp32(bin_data, tmp_path, dev):
     """optimization.sgd.dtype = bf16 (bf16 working copy of the FM latents, fp32 master):

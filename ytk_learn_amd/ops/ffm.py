@@ -52,7 +52,7 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, out)
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, ptr(out), 0, 0, 0,
-                        int(skip_feat), stream(V))
+                        int(skip_feat), stream(V), 0)
         return out
     r, p, q = cache if cache is not None else ffm_pairs_cpu(indptr, idx, val, skip_feat)
     V3 = V.view(-1, nfield, k)
@@ -64,13 +64,17 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
     return out
 
 
-def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=None, skip_feat: int = -1):
-    """gV += pair gradients (gV, V: [F * nfield * k] flat)."""
+def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=None, skip_feat: int = -1,
+                 cnt=None):
+    """gV += pair gradients (gV, V: [F * nfield * k] flat). ``cnt`` (int32 [F], optional: the
+    SGD batch's rows per feature): the steps into V[i] are divided by cnt[i]."""
     n = indptr.shape[0] - 1
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, coef, gV)
+        if cnt is not None:
+            check_cuda(cnt)
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, 0, ptr(coef), ptr(gV), 1,
-                        int(skip_feat), stream(V))
+                        int(skip_feat), stream(V), ptr(cnt) if cnt is not None else 0)
         return gV
     r, p, q = cache if cache is not None else ffm_pairs_cpu(indptr, idx, val, skip_feat)
     V3 = V.view(-1, nfield, k)
@@ -80,8 +84,12 @@ def ffm_backward(indptr, idx, val, fld, V, nfield: int, k: int, coef, gV, cache=
     s = (coef[r] * val[p] * val[q])[:, None]
     flat = lambda i, f: i * nfield + f
     G2 = G3.view(-1, k)
-    G2.index_add_(0, flat(ip, fq), s * V3[iq, fp])
-    G2.index_add_(0, flat(iq, fp), s * V3[ip, fq])
+    sp = sq = s
+    if cnt is not None:
+        sp = s / cnt[ip].clamp(min=1).to(s.dtype)[:, None]
+        sq = s / cnt[iq].clamp(min=1).to(s.dtype)[:, None]
+    G2.index_add_(0, flat(ip, fq), sp * V3[iq, fp])
+    G2.index_add_(0, flat(iq, fp), sq * V3[ip, fq])
     return gV
 
 

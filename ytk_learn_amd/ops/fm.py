@@ -58,8 +58,25 @@ def fm_backward(X, c: torch.Tensor, S: torch.Tensor, V: torch.Tensor, g_lin: tor
     return g_lin, gV
 
 
+def sgd_count(indptr, indices, cnt: torch.Tensor, clear: bool = False, nnz_hint: int = 0):
+    """Rows per feature of an SGD batch: cnt[i] += 1 for every entry of the rows of ``indptr``
+    (absolute offsets into ``indices``), or cnt[i] = 0 for them (``clear``). GPU: one kernel
+    over the device row pointers (no host read); CPU: index ops."""
+    n = int(indptr.shape[0] - 1)
+    if cnt.is_cuda:
+        check_cuda(indptr, indices, cnt)
+        hip().sgd_count(ptr(indptr), ptr(indices), n, int(nnz_hint), ptr(cnt), 1 if clear else 0, stream(cnt))
+        return cnt
+    idx = indices[int(indptr[0]):int(indptr[-1])].long()
+    if clear:
+        cnt[idx] = 0
+    else:
+        cnt.index_add_(0, idx, torch.ones_like(idx, dtype=cnt.dtype))
+    return cnt
+
+
 def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float, l2v: float,
-                  reg_skip: int = -1, upd_w: bool = True, bias_latent: bool = False, Vb=None):
+                  reg_skip: int = -1, upd_w: bool = True, bias_latent: bool = False, Vb=None, cnt=None):
     """One Hogwild!-style SGD step over the rows of ``indptr`` (absolute offsets into
     ``indices`` / ``values``): w_i -= lr (c_r x_i + l2w w_i), V_if -= lr (c_r x_i (S_rf - V_if x_i)
     + l2v V_if) for every entry of every row. ``V`` [F, k] / ``S`` [n, k] are None for the
@@ -68,16 +85,18 @@ def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float
     GPU: lock-free float atomics, concurrent rows race as in Hogwild!. CPU: the same
     per-sample gradients applied as one synchronous mini-batch step.
     ``Vb`` (bf16 [F, k], optional): working copy the forward read; the gradient uses its
-    values, ``V`` stays the fp32 master and the touched entries of ``Vb`` are re-rounded."""
+    values, ``V`` stays the fp32 master and the touched entries of ``Vb`` are re-rounded.
+    ``cnt`` (int32 [F], optional, :func:`sgd_count`): every weight's step is divided by the
+    batch's rows containing its feature (per-feature mean of the per-sample gradients)."""
     n = int(indptr.shape[0] - 1)
     k = 0 if V is None else int(V.shape[1])
     c = c.float().contiguous()
     if w_lin.is_cuda:
-        check_cuda(indptr, indices, values, w_lin, V, S, c, Vb)
+        check_cuda(indptr, indices, values, w_lin, V, S, c, Vb, cnt)
         assert Vb is None or (Vb.dtype == torch.bfloat16 and Vb.shape == V.shape and Vb.is_contiguous())
         hip().fm_sgd_update(ptr(indptr), ptr(indices), ptr(values), n, ptr(w_lin), ptr(V), k, ptr(S), ptr(c),
                             float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0,
-                            1 if bias_latent else 0, ptr(Vb), stream(w_lin))
+                            1 if bias_latent else 0, ptr(Vb), ptr(cnt) if cnt is not None else 0, stream(w_lin))
         return
     if Vb is not None:  # CPU reference of the bf16 path: gradient from the working copy
         V_use = Vb.float()
@@ -93,12 +112,13 @@ def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float
     gw = cr * x + torch.where(is_bias, zero, l2w * w_lin[idx])
     if not upd_w:
         gw = torch.where(is_bias, gw, zero)
+    lri = lr / cnt[idx].clamp(min=1).float() if cnt is not None else torch.full_like(x, lr)
     if k > 0:
         v = V_use[idx]
         gv = (cr * x)[:, None] * (S[rows] - v * x[:, None]) + torch.where(is_bias[:, None], zero, l2v * v)
         if not bias_latent:
             gv[is_bias] = 0.0
-        V.index_add_(0, idx, -lr * gv)
+        V.index_add_(0, idx, -lri[:, None] * gv)
         if Vb is not None:
             Vb.copy_(V)
-    w_lin.index_add_(0, idx, -lr * gw)
+    w_lin.index_add_(0, idx, -lri * gw)

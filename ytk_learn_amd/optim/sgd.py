@@ -16,6 +16,11 @@ seeded random order every epoch):
 Regularization: l2 of the linear / latent groups is applied to the weights a sample
 touches (sparse weight decay); l1 is not supported by this optimizer. FFM latents get no
 decay (the pair kernel has none).
+Step size (``optimization.sgd.average``): with ``feature`` (default) a weight's step is
+the MEAN of the per-sample steps of the batch rows containing its feature (rows per
+feature counted on the device before the update) -- rare features keep the per-sample
+rate, hot ones (the bias is in every row) take one bounded step per batch. ``none`` applies
+the sum, which for batches of thousands of rows diverges on hot features.
 
 Multi-GPU: every rank runs SGD on its shard; weights are averaged across ranks with one
 RCCL all-reduce every ``sync_every`` batches (0 = once per epoch) -- local SGD / model
@@ -31,7 +36,7 @@ import numpy as np
 import torch
 
 from ..ops.ffm import ffm_backward, ffm_forward
-from ..ops.fm import fm_forward, fm_sgd_update
+from ..ops.fm import fm_forward, fm_sgd_update, sgd_count
 from ..utils.fault import fault_point
 from ..utils.javafmt import java_double_str as jd
 
@@ -47,6 +52,8 @@ class SGDParams:
     sync_every: int = 0               # batches between cross-rank weight averaging; 0 = per epoch
     seed: int = 1
     dtype: str = "fp32"               # "bf16": FM latents read from a bf16 working copy (fp32 master)
+    average: str = "feature"          # "feature": a weight's step is the mean over the batch rows
+    #                                   containing its feature; "none": the sum (per-sample steps)
 
     @classmethod
     def from_config(cls, c, prefix: str = "optimization.sgd.") -> "SGDParams":
@@ -55,8 +62,10 @@ class SGDParams:
                 learning_rate_decay=c.get_double(prefix + "learning_rate_decay", 1.0),
                 batch_size=c.get_int(prefix + "batch_size", 65536), epochs=c.get_int(prefix + "epochs", 10),
                 sync_every=c.get_int(prefix + "sync_every", 0), seed=c.get_int(prefix + "seed", 1),
-                dtype=str(c.get_string(prefix + "dtype", "fp32")).lower())
+                dtype=str(c.get_string(prefix + "dtype", "fp32")).lower(),
+                average=str(c.get_string(prefix + "average", "feature")).lower())
         check(p.dtype in ("fp32", "bf16"), "%sdtype:%s must be fp32 or bf16", prefix, p.dtype)
+        check(p.average in ("feature", "none"), "%saverage:%s must be feature or none", prefix, p.average)
         check(p.learning_rate > 0, "%slearning_rate:%f must > 0", prefix, p.learning_rate)
         check(0 < p.learning_rate_decay <= 1.0, "%slearning_rate_decay:%f must be in (0, 1]", prefix,
               p.learning_rate_decay)
@@ -93,6 +102,10 @@ class SGDOptimizer:
         # gathered from a bf16 working copy by the forward and gradient passes (half the
         # bytes of the dominant V-row gathers); updates land in the fp32 master, whose
         # touched entries re-round the copy; full re-sync after every weight averaging.
+        # per-feature averaging (average = feature): rows per feature of the current batch,
+        # counted before the update and cleared after it (zero between batches)
+        self.cnt = (torch.zeros(model.F, dtype=torch.int32, device=model.w.device)
+                    if sp.average == "feature" else None)
         self.Vb = None
         if sp.dtype == "bf16" and model.name == "fm" and getattr(model, "kk", 0) > 0:
             self.Vb = torch.empty((model.F, model.kk), dtype=torch.bfloat16, device=model.w.device)
@@ -138,10 +151,16 @@ class SGDOptimizer:
         y = d.y[b:e, 0].double()
         c = (d.weight[b:e].double() * m.loss.grad(fx, y)).float().contiguous()
         V = w[F:].view(F, m.kk) if (m.name == "fm" and m.kk > 0) else None
+        cnt = self.cnt
+        if cnt is not None:
+            sgd_count(sl.indptr, X.indices, cnt, nnz_hint=(e - b) * max(1, X.nnz // max(1, X.n)))
         fm_sgd_update(sl.indptr, X.indices, X.values, w_lin, V, S, c, lr, self.l2w, self.l2v, reg_skip, upd_w,
-                      bool(getattr(m, "bias_latent", False)), Vb=self.Vb)
+                      bool(getattr(m, "bias_latent", False)), Vb=self.Vb, cnt=cnt)
         if m.name == "ffm" and m.stride > 0 and getattr(m, "need_second", True):
-            ffm_backward(ip, idx, val, fl, w[F:], m.nf, m.kk, (-lr * c).contiguous(), w[F:], skip_feat=m._skip)
+            ffm_backward(ip, idx, val, fl, w[F:], m.nf, m.kk, (-lr * c).contiguous(), w[F:], skip_feat=m._skip,
+                         cnt=cnt)
+        if cnt is not None:
+            sgd_count(sl.indptr, X.indices, cnt, clear=True, nnz_hint=(e - b) * max(1, X.nnz // max(1, X.n)))
 
     def _average(self, w):
         if self.dist:
