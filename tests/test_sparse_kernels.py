@@ -253,6 +253,14 @@ def test_ffm_gpu_matches_cpu(cuda, k, m, monkeypatch):
     gg = torch.zeros_like(V).to(cuda)
     ffm_backward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), gg)
     torch.testing.assert_close(gg.cpu(), gc, rtol=1e-3, atol=1e-3)
+    # SGD batch counts (optimization.sgd.average = feature): steps into V[i] divided by cnt[i]
+    cnt = torch.randint(1, 5, (F,), generator=g, dtype=torch.int32)
+    gcn = torch.zeros_like(V)
+    ffm_backward(ip, ix, vv, fl, V, nf, k, c, gcn, cnt=cnt)
+    ggn = torch.zeros_like(V).to(cuda)
+    ffm_backward(ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), V.to(cuda), nf, k, c.to(cuda), ggn,
+                 cnt=cnt.to(cuda))
+    torch.testing.assert_close(ggn.cpu(), gcn, rtol=1e-3, atol=1e-3)
     # column-ordered backward (no atomics), with and without a skipped feature
     import ytk_learn_amd.ops.sparse as sparse_mod
     monkeypatch.setattr(sparse_mod, "CHUNK", 100)  # several chunks per column
