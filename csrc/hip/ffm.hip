@@ -155,6 +155,82 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
   if (lane == 0) fx[row] = acc;
 }
 
+// Pair scatter backward for k == 4 (the SGD step's direct update of V: coef = -lr c_r):
+// the generic backward walks p one pair at a time -- two dependent 16-B gathers, then the
+// atomics -- so a Criteo-shape SGD epoch ran latency bound (~1.07 s). Here kPU pairs'
+// gathers per lane are in flight before their atomics, as in ffm_pairs_k4_kernel. Same
+// pairs and updates as ffm_pairs_kernel<true> (Hogwild!: the atomics race either way).
+__global__ __launch_bounds__(256) void ffm_pairs_k4_bwd_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
+    const int* __restrict__ fld, long long nrows, const float* __restrict__ V, int nfield,
+    const float* __restrict__ coef, float* __restrict__ gV, int skip_feat, const int* __restrict__ cnt) {
+  const long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return;
+  const float c = coef[row];
+  if (c == 0.f) return;  // wave-uniform
+  const long long b = indptr[row];
+  const int m = (int)(indptr[row + 1] - b);
+  const long long stride = (long long)nfield * 4;
+  for (int pt = 0; pt < m; pt += 64) {
+    const int pj = pt + lane;
+    int ip = 0, fp = 0;
+    float xp = 0.f, rp = 1.f;
+    if (pj < m) {
+      ip = idx[b + pj]; xp = val[b + pj]; fp = fld[b + pj];
+      if (cnt) rp = 1.f / (float)max(1, cnt[ip]);
+    }
+    for (int qt = pt; qt < m; qt += 64) {
+      const int qj = qt + lane;
+      int iq = 0, fq = 0;
+      float xq = 0.f, rq = 1.f;
+      if (qj < m) {
+        iq = idx[b + qj]; xq = val[b + qj]; fq = fld[b + qj];
+        if (cnt) rq = 1.f / (float)max(1, cnt[iq]);
+      }
+      const int pend = min(64, m - pt);
+      for (int pp0 = 0; pp0 < pend; pp0 += kPU) {
+        float4 va[kPU], vb[kPU];
+        float sp[kPU], sq[kPU];
+        long long op[kPU], oq[kPU];
+        bool ok[kPU];
+#pragma unroll
+        for (int u = 0; u < kPU; ++u) {
+          const int pp = min(pp0 + u, pend - 1);  // uniform; the duplicate is masked by ok
+          const int P = pt + pp;
+          const int ipb = __shfl(ip, pp, 64), fpb = __shfl(fp, pp, 64);
+          const float xpb = __shfl(xp, pp, 64), rpb = __shfl(rp, pp, 64);
+          ok[u] = pp0 + u < pend && qj < m && qj > P && ipb != skip_feat && iq != skip_feat;
+          const float s = c * xpb * xq;
+          sp[u] = s * rpb;  // into V[i_p, f_q]
+          sq[u] = s * rq;   // into V[i_q, f_p]
+          op[u] = (long long)ipb * stride + (long long)fq * 4;
+          oq[u] = (long long)iq * stride + (long long)fpb * 4;
+          va[u] = vb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok[u]) {
+            va[u] = *reinterpret_cast<const float4*>(V + op[u]);
+            vb[u] = *reinterpret_cast<const float4*>(V + oq[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPU; ++u) {
+          if (!ok[u]) continue;
+          float* gp = gV + op[u];
+          float* gq = gV + oq[u];
+          unsafeAtomicAdd(gp, sp[u] * vb[u].x);
+          unsafeAtomicAdd(gp + 1, sp[u] * vb[u].y);
+          unsafeAtomicAdd(gp + 2, sp[u] * vb[u].z);
+          unsafeAtomicAdd(gp + 3, sp[u] * vb[u].w);
+          unsafeAtomicAdd(gq, sq[u] * va[u].x);
+          unsafeAtomicAdd(gq + 1, sq[u] * va[u].y);
+          unsafeAtomicAdd(gq + 2, sq[u] * va[u].z);
+          unsafeAtomicAdd(gq + 3, sq[u] * va[u].w);
+        }
+      }
+    }
+  }
+}
+
 // Column-ordered (gather) backward: no global atomics.
 //   gV[i, f_q, :] = sum over entries e of feature i (row r, value x, field f_i) and every
 //                   other entry q of row r:  c_r x x_q V[i_q, f_i, :]
@@ -414,7 +490,11 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
   const dim3 grid((unsigned)((threads + 255) / 256));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vec4 = ((k & 3) == 0 && (V & 15) == 0) ? 1 : 0;  // 16-B gathers need aligned V
-  if (backward)
+  if (backward && vec4 && k == 4 && (gV & 15) == 0 && !getenv_off("YTK_FFM_K4"))
+    hipLaunchKernelGGL(ffm_pairs_k4_bwd_kernel, grid, dim3(256), 0, s, (const long long*)indptr, (const int*)idx,
+                       (const float*)val, (const int*)fld, nrows, (const float*)V, nfield, (const float*)coef,
+                       (float*)gV, skip_feat, (const int*)cnt);
+  else if (backward)
     hipLaunchKernelGGL(ffm_pairs_kernel<true>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
                        nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat, (const int*)cnt);
