@@ -31,7 +31,7 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
 void ytk_split_combine(uintptr_t, int, int, uintptr_t, int, int, uintptr_t, uintptr_t);
 // gbst.hip
 void ytk_gbst_epilogue(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, double, uintptr_t, int, int, int,
-                       int, int, int, int, int, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t);
+                       int, int, double, int, int, int, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_partition.hip
 void ytk_partition_atomic(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                           uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -86,6 +86,8 @@ void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, 
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t, uintptr_t);
 void ytk_sgd_count(uintptr_t, uintptr_t, long long, long long, uintptr_t, int, uintptr_t);
+void ytk_sgd_apply(uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, int, uintptr_t, uintptr_t, int,
+                   uintptr_t, uintptr_t, long long, float, float, float, int, int, int, int, uintptr_t);
 void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                     uintptr_t, int, uintptr_t);
 void ytk_fm_backward(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
@@ -212,6 +214,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fm_backward", &ytk_fm_backward);
   m.def("fm_sgd_update", &ytk_fm_sgd_update);
   m.def("sgd_count", &ytk_sgd_count);
+  m.def("sgd_apply", &ytk_sgd_apply);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
     if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)

@@ -208,6 +208,64 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
   }
 }
 
+// Column-ordered mini-batch SGD step (optimization.optimizer = "sgd"): the batch's CSC
+// (ops/sgd.py: one SparseMatrix per fixed batch row range, built once) has been reduced
+// per chunk by fm_backward_kernel (part[c] = [sum c x S_f (f < k) | sum c x | sum c x^2]) and,
+// for FFM, by the streamed pair-gradient kernel (lat[c] = the chunk's [nfield * k] pair
+// gradient). One G-lane group per touched feature u (global id ucol[u], cnt[u] batch
+// entries, chunks [ucp[u], ucp[u + 1])) sums its chunks in chunk order -- deterministic, no
+// atomics, no race between the rows of a batch -- and applies the batch step with the
+// weights as the batch read them:
+//   w_i  -= lri * (g_i + cnt_i * l2w * w_i)
+//   V_ij -= lri * (gV_ij + cnt_i * l2v * V_ij),   gV = sum c x S - V sum c x^2 (FM) | lat (FFM)
+// lri = lr / cnt_i (avg: the mean of the per-sample steps of the rows holding feature i) or
+// lr (the sum). FFM latents (lat != null) take the same l2 decay. reg_skip: bias index (no
+// decay; latent row frozen unless bias_latent); upd_w = 0 updates only the bias among the
+// linear weights. Vb (bf16 working copy read by the FM forward) and Vt ([nfield][F][k] copy
+// read by the FFM backward) are rewritten from the new fp32 values of the touched entries.
+template <int G>
+__global__ __launch_bounds__(256) void sgd_apply_kernel(
+    const int* __restrict__ ucol, const long long* __restrict__ ucp, const int* __restrict__ ucnt, int nu,
+    const float* __restrict__ part, int ldp, const float* __restrict__ lat, int J, float* __restrict__ w,
+    float* __restrict__ V, int k, __hip_bfloat16* __restrict__ Vb, float* __restrict__ Vt, long long nfeat,
+    float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
+  const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
+  const int f = threadIdx.x & (G - 1);
+  if (gid >= nu) return;
+  const int i = ucol[gid];
+  const long long c0 = ucp[gid], c1 = ucp[gid + 1];
+  const float cnt = (float)ucnt[gid];
+  const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
+  const bool is_bias = i == reg_skip;
+  const int lin_col = lat ? 0 : k;  // FFM: part = [sum c x | sum c x^2]
+  float glin = 0.f, gsq = 0.f;
+  for (long long c = c0; c < c1; ++c) {
+    glin += part[c * ldp + lin_col];
+    gsq += part[c * ldp + lin_col + 1];
+  }
+  if (f == 0 && (upd_w || is_bias)) {
+    const float wi = w[i];
+    w[i] = wi - lri * (glin + (is_bias ? 0.f : cnt * l2w * wi));
+  }
+  if (J == 0 || (is_bias && !bias_latent)) return;
+  const float dec = is_bias ? 0.f : cnt * l2v;
+  for (int j = f; j < J; j += G) {
+    float g = 0.f;
+    const long long o = (long long)i * J + j;
+    const float v = V[o];
+    if (lat) {
+      for (long long c = c0; c < c1; ++c) g += lat[c * J + j];
+    } else {
+      for (long long c = c0; c < c1; ++c) g += part[c * ldp + j];
+      g -= v * gsq;
+    }
+    const float nv = v - lri * (g + dec * v);
+    V[o] = nv;
+    if (Vb) Vb[o] = __float2bfloat16(nv);
+    if (Vt) Vt[((long long)(j / k) * nfeat + i) * k + (j % k)] = nv;
+  }
+}
+
 // Rows per feature of a mini-batch (clear = 0: cnt[i] += 1 per entry) and the reset of the
 // touched counters afterwards (clear = 1: plain stores of 0), over the batch's entries
 // [indptr[0], indptr[nrows]) (device row pointers: no host read). Counting aggregates in
@@ -297,11 +355,12 @@ void ytk_fm_forward(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long nr
 }
 
 // part[chunk, k + 2] column sums of the FM gradient (see kernel comment).
+// k == 0: part[chunk, 2] = [sum c x | sum c x^2] only (linear gradient; S unused)
 void ytk_fm_backward(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows,
                      uintptr_t csc_vals, uintptr_t coef, uintptr_t S, int k, uintptr_t part,
                      uintptr_t stream) {
   if (nch <= 0) return;
-  if (k < 1 || k > 64) throw std::invalid_argument("fm_backward: 1 <= k <= 64");
+  if (k < 0 || k > 64) throw std::invalid_argument("fm_backward: 0 <= k <= 64");
   const int G = fm_group(k);
   const long long threads = nch * G;
   const dim3 grid((unsigned)((threads + 255) / 256));
@@ -346,6 +405,35 @@ void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long
     default: YTK_FM_S(64); break;
   }
 #undef YTK_FM_S
+  YTK_LAUNCH_CHECK();
+}
+
+// One column-ordered SGD batch step (see sgd_apply_kernel); J latent values per feature
+// (FM: k, gradient folded from part; FFM: nfield * k from lat; 0: linear model).
+void ytk_sgd_apply(uintptr_t ucol, uintptr_t ucp, uintptr_t ucnt, int nu, uintptr_t part, int ldp, uintptr_t lat,
+                   int J, uintptr_t w, uintptr_t V, int k, uintptr_t Vb, uintptr_t Vt, long long nfeat, float lr,
+                   float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg, uintptr_t stream) {
+  if (nu <= 0) return;
+  if (J < 0 || (J > 0 && k < 1) || (!lat && J != k) || (!lat && ldp != k + 2) || (lat && ldp != 2) ||
+      (Vt && !lat))
+    throw std::invalid_argument("sgd_apply: inconsistent part / latent layout");
+  const int G = J <= 4 ? 4 : J <= 8 ? 8 : J <= 16 ? 16 : J <= 32 ? 32 : 64;
+  const long long threads = (long long)nu * G;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define YTK_SGD_A(GG)                                                                                   \
+  hipLaunchKernelGGL(sgd_apply_kernel<GG>, grid, dim3(256), 0, s, (const int*)ucol, (const long long*)ucp, \
+                     (const int*)ucnt, nu, (const float*)part, ldp, (const float*)lat, J, (float*)w,        \
+                     (float*)V, k, (__hip_bfloat16*)Vb, (float*)Vt, nfeat, lr, l2w, l2v, reg_skip, upd_w,  \
+                     bias_latent, avg)
+  switch (G) {
+    case 4: YTK_SGD_A(4); break;
+    case 8: YTK_SGD_A(8); break;
+    case 16: YTK_SGD_A(16); break;
+    case 32: YTK_SGD_A(32); break;
+    default: YTK_SGD_A(64); break;
+  }
+#undef YTK_SGD_A
   YTK_LAUNCH_CHECK();
 }
 

@@ -277,6 +277,26 @@ def test_lbfgs_peer_gradient_allreduce_one_gpu(tmp_path, task, two_shot):
 
 
 @pytest.mark.gpu
+def test_lbfgs_peer_dropped_exchange_raises(tmp_path):
+    """Rank 1 silently drops one L-BFGS gradient exchange (fault mode ``skip``): rank 0's flag
+    wait times out and the error word must surface as an exception -- not as training on
+    stale peer sums -- so the job exits non-zero naming the timed-out wait."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", YTK_DIST_BACKEND="gloo",
+               YTK_PEER_REDUCE="1", YTK_PEER_TIMEOUT_S="5", YTK_COMM_TIMEOUT="30",
+               YTK_FAULT_INJECT="peer:1:4:skip")
+    os.makedirs(tmp_path, exist_ok=True)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), WORKER, "linear", str(tmp_path), "cuda"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "injected fault at peer step 4 (skip)" in r.stderr, r.stderr[-3000:]
+    assert "flag wait timed out" in r.stderr, r.stderr[-3000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 def test_peer_primitives_one_gpu(tmp_path, world):
     """Ranks sharing the one GPU: the peer exchange's all-reduce (one-shot and two-shot

@@ -1,0 +1,189 @@
+"""Column-ordered synchronous mini-batch SGD (ops/sgd.py, sgd_apply_kernel).
+
+CPU: the synchronous step equals its definition (every gradient at the batch's starting
+weights) written out per sample, for linear / FM / FFM with l2 decay, the bias rule and both
+averaging modes. GPU: the four-kernel step (row pass, row loss, column pass + pair gradient,
+sgd_apply) equals the CPU reference step on the same data, batch after batch.
+"""
+import numpy as np
+import pytest
+import torch
+
+from ytk_learn_amd.config.params import CommonParams
+from ytk_learn_amd.data.dataflow import SparseData
+from ytk_learn_amd.data.synthetic import criteo_like
+from ytk_learn_amd.models.continuous.base import LoadedData
+from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
+from ytk_learn_amd.utils.logging import YtkLogger
+
+
+def _model(name, n=3000, nf=6, feats=240, k=4, dev="cpu", seed=5, uneven=False):
+    ip, ix, vv, fl, y = criteo_like(n, nf, feats, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    vv = (0.5 + torch.rand(vv.shape, generator=g)).contiguous()
+    F = nf * (feats // nf) + 1
+    # bias column 0 in front of every row (as the data loader lays it out)
+    m = nf
+    ip2 = torch.arange(n + 1, dtype=torch.int64) * (m + 1)
+    idx2 = torch.zeros(n * (m + 1), dtype=torch.int32)
+    val2 = torch.ones(n * (m + 1), dtype=torch.float32)
+    fld2 = torch.zeros(n * (m + 1), dtype=torch.int32)
+    sel = torch.ones(n * (m + 1), dtype=torch.bool)
+    sel[::m + 1] = False
+    idx2[sel] = ix + 1
+    val2[sel] = vv
+    fld2[sel] = fl + 1
+    if uneven:  # drop some entries: rows of different lengths, not every field present
+        keep = torch.rand(idx2.shape, generator=g) > 0.2
+        keep[::m + 1] = True
+        rows = torch.repeat_interleave(torch.arange(n), m + 1)
+        idx2, val2, fld2 = idx2[keep], val2[keep], fld2[keep]
+        cnt = torch.zeros(n, dtype=torch.int64).index_add_(0, rows[keep], torch.ones(int(keep.sum()), dtype=torch.int64))
+        ip2 = torch.zeros(n + 1, dtype=torch.int64)
+        ip2[1:] = torch.cumsum(cnt, 0)
+    w = torch.ones(n)
+    d = SparseData(ip2.to(dev), idx2.to(dev), val2.to(dev), y.to(dev), w.to(dev),
+                   fld2.to(dev) if name == "ffm" else None, None, float(n), float(n), float(n))
+    p = CommonParams()
+    p.loss.loss_function = "sigmoid"
+    p.loss.evaluate_metric = []
+    p.model.need_bias = True
+    p.model.data_path = "/tmp/ytk_test_sgd_column"
+    p.extra = {"k": [1, k], "bias_need_latent_factor": False}
+    names = ["_bias_"] + [f"f{i}" for i in range(1, F)]
+    loaded = LoadedData(d, None, names, {nm: i for i, nm in enumerate(names)},
+                        ["_bias_"] + [f"c{i}" for i in range(nf)])
+    log = YtkLogger(0)
+    log.quiet = True
+    from ytk_learn_amd.parallel.comm import Comm
+    comm = Comm.local(torch.device(dev))
+    if name == "linear":
+        from ytk_learn_amd.models.continuous.linear import LinearModel
+        return LinearModel(p, loaded, comm, log)
+    if name == "fm":
+        from ytk_learn_amd.models.continuous.fm import FMModel
+        return FMModel(p, loaded, comm, log)
+    from ytk_learn_amd.models.continuous.ffm import FFMModel
+    return FFMModel(p, loaded, comm, log)
+
+
+def _opt(model, avg="feature", dtype="fp32", batch=512, l2=(1e-3, 2e-3)):
+    log = YtkLogger(0)
+    log.quiet = True
+    return SGDOptimizer(model, SGDParams(learning_rate=0.2, batch_size=batch, epochs=1, average=avg, dtype=dtype),
+                        [0.0, 0.0], list(l2), None, log, float(model.data.train.n), 1.0)
+
+
+def _per_sample_step(model, w, b, e, lr, l2w, l2v, avg):
+    """Definition: per-sample gradients at the starting weights, summed per weight, divided by
+    the batch entries holding the feature (avg) -- written with explicit loops over rows."""
+    F = model.F
+    X = model.X
+    w0 = w.clone()
+    upd = torch.zeros_like(w)
+    cnt = torch.zeros(F)
+    ip, ix, xv = X.indptr, X.indices.long(), X.values
+    fl = model.data.train.fields
+    for r in range(b, e):
+        s, t = int(ip[r]), int(ip[r + 1])
+        ii, xx = ix[s:t], xv[s:t]
+        fx = float((w0[ii] * xx).sum())
+        if model.name == "fm":
+            V = w0[F:].view(F, model.kk)
+            S = (V[ii] * xx[:, None]).sum(0)
+            fx += 0.5 * float((S * S - ((V[ii] * xx[:, None]) ** 2).sum(0)).sum())
+        if model.name == "ffm":
+            V = w0[F:].view(F, model.nf, model.kk)
+            ff = fl[s:t].long()
+            for p in range(len(ii)):
+                for q in range(p + 1, len(ii)):
+                    if int(ii[p]) == 0 or int(ii[q]) == 0:
+                        continue
+                    fx += float((V[ii[p], ff[q]] * V[ii[q], ff[p]]).sum()) * float(xx[p] * xx[q])
+        y = float(model.data.train.y[r, 0])
+        c = 1.0 / (1.0 + np.exp(-fx)) - y
+        for p in range(len(ii)):
+            i = int(ii[p])
+            cnt[i] += 1
+            gw = c * float(xx[p]) + (0.0 if i == 0 else l2w * float(w0[i]))
+            upd[i] += gw
+            if model.name == "fm" and i != 0:
+                V = w0[F:].view(F, model.kk)
+                gv = c * float(xx[p]) * (S - V[i] * float(xx[p])) + l2v * V[i]
+                upd[F + i * model.kk:F + (i + 1) * model.kk] += gv
+            if model.name == "ffm" and i != 0:
+                V = w0[F:].view(F, model.nf, model.kk)
+                ff = fl[s:t].long()
+                gv = torch.zeros(model.nf, model.kk)
+                for q in range(len(ii)):
+                    if q != p and int(ii[q]) != 0:
+                        gv[ff[q]] += c * float(xx[p] * xx[q]) * V[ii[q], ff[p]]
+                gv += l2v * V[i]
+                st = model.nf * model.kk
+                upd[F + i * st:F + (i + 1) * st] += gv.reshape(-1)
+    div = cnt.clamp(min=1) if avg == "feature" else torch.ones(F)
+    out = w0.clone()
+    out[:F] -= lr * upd[:F] / div
+    J = (w.numel() - F) // F
+    if J:
+        out[F:] -= (lr * upd[F:].view(F, J) / div[:, None]).reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("name", ["linear", "fm", "ffm"])
+@pytest.mark.parametrize("avg", ["feature", "none"])
+def test_cpu_step_is_synchronous_per_sample_sum(name, avg):
+    m = _model(name, n=40, nf=4, feats=40, k=3, uneven=True)
+    opt = _opt(m, avg=avg, batch=40)
+    w = m.w.clone()
+    want = _per_sample_step(m, w, 0, 40, 0.2, 1e-3, 2e-3, avg)
+    opt._step(w, 0, 40, 0.2)
+    torch.testing.assert_close(w, want, rtol=2e-4, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,dtype,uneven", [("linear", "fp32", False), ("fm", "fp32", False),
+                                               ("fm", "bf16", False), ("ffm", "fp32", False),
+                                               ("ffm", "fp32", True), ("fm", "fp32", True)])
+@pytest.mark.parametrize("avg", ["feature", "none"])
+def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
+    """Three batches through the GPU column-ordered step vs the CPU synchronous step (fp32
+    sums in different orders: rtol 1e-4; bf16: the forward reads the rounded copy on both)."""
+    mc = _model(name, uneven=uneven)
+    mg = _model(name, dev="cuda", uneven=uneven)
+    oc, og = _opt(mc, avg=avg, dtype=dtype), _opt(mg, avg=avg, dtype=dtype)
+    wc, wg = mc.w.clone(), mg.w.clone()
+    oc._sync_copy(wc)
+    og._sync_copy(wg)
+    bounds = [(0, 512), (512, 1024), (2048, 2560)]
+    batches = og._setup(bounds)
+    if name == "ffm" and not uneven:
+        assert all(bt.stream_st is not None for bt in batches)  # the streamed pair kernel ran
+    for j, (b, e) in enumerate(bounds):
+        oc._step(wc, b, e, 0.2)
+        og._step(wg, b, e, 0.2, batches[j])
+        tol = 3e-3 if dtype == "bf16" else 1e-4
+        torch.testing.assert_close(wg.cpu(), wc, rtol=tol, atol=tol * 1e-2)
+    if og.Vt is not None:  # the transposed working copy tracks V
+        F = mg.F
+        torch.testing.assert_close(og.Vt, wg[F:].view(F, mg.nf, mg.kk).transpose(0, 1), rtol=0, atol=0)
+    if og.Vb is not None:
+        F = mg.F
+        torch.testing.assert_close(og.Vb, wg[F:].view(F, mg.kk).to(torch.bfloat16), rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_column_step_deterministic(cuda):
+    """No atomics: two runs of the same batches give bitwise identical weights."""
+    outs = []
+    for _ in range(2):
+        m = _model("ffm", dev="cuda")
+        o = _opt(m)
+        w = m.w.clone()
+        o._sync_copy(w)
+        bounds = [(0, 1000), (1000, 2000)]
+        bts = o._setup(bounds)
+        for j, (b, e) in enumerate(bounds):
+            o._step(w, b, e, 0.2, bts[j])
+        outs.append(w)
+    assert torch.equal(outs[0], outs[1])

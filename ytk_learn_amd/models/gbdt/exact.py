@@ -82,6 +82,8 @@ class ExactGreedyBuilder:
         # GPU test oracle)
         engine = engine or ("torch" if os.environ.get("YTK_EXACT_TORCH", "0") == "1" else "hip")
         self.hip = self.dev.type == "cuda" and engine == "hip"
+        if self.hip and not self._hip_fits():
+            self.hip = False
         if self.hip:
             self._init_hip()
         self.tree_count = 0
@@ -112,6 +114,23 @@ class ExactGreedyBuilder:
         return torch.where(H < mcw, torch.zeros_like(v), v)
 
     # ------------------------------------------------------------------ HIP engine
+    HIP_BYTES_PER_CELL = 4 + 4 + 2 * (4 + 4 + 16)  # ord0, val0, ping-pong ordw / valw / qvw
+
+    def _hip_fits(self) -> bool:
+        """The HIP engine holds ~56 B per (feature, row) cell on top of XT (the tensor path ~12 B,
+        in feature chunks): check it against the free device memory (the int64 presort order,
+        8 B per cell, is released during the set-up) and fall back to the tensor engine, with a
+        log line, when it does not fit."""
+        need = self.F * self.N * self.HIP_BYTES_PER_CELL
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        avail = free + self.F * self.N * 8
+        if need <= 0.9 * avail:
+            return True
+        from ...utils.logging import get_logger
+        get_logger().info(f"[GBDT] exact greedy: the HIP engine needs {need / 2**30:.1f} GiB for {self.F} x {self.N} "
+                          f"cells, {avail / 2**30:.1f} GiB free; using the tensor engine")
+        return False
+
     REC_DTYPE = np.dtype([("G", "<f8"), ("H", "<f8"), ("cnt", "<i8"), ("chg", "<f4"), ("thr", "<f4"),
                           ("value", "<f4"), ("feat", "<i4"), ("split", "<i4"), ("pad", "<i4")])
 

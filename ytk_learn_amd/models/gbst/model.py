@@ -33,6 +33,10 @@ from ...utils.errors import YtkLearnError
 from ...utils.javafmt import java_double_str, java_float_str
 from ..continuous.base import ContinuousModelBase
 
+# loss ids of the fused epilogue (csrc/hip/gbst.hip kLoss*): every scalar loss
+GBST_LOSS_IDS = {"sigmoid": 0, "l2": 1, "l1": 2, "huber": 3, "poisson": 4, "hinge": 5, "smooth_hinge": 6,
+                 "l2_hinge": 7, "exponential": 8, "mape": 9, "smape": 10, "inv_mape": 11}
+
 VARIANTS = {"gbmlr": ("softmax", "linear"), "gbsdt": ("softmax", "scalar"),
             "gbhmlr": ("tree", "linear"), "gbhsdt": ("tree", "scalar")}
 
@@ -180,12 +184,20 @@ class GBSTModel(ContinuousModelBase):
         return gbst_mixture(A, self.K, self.gate_kind, self.expert_kind, leaves)
 
     def _fused_ok(self, X) -> bool:
-        """The fused HIP epilogue (csrc/hip/gbst.hip) covers sigmoid / l2 losses and
-        2 <= K <= 64 (softmax and hierarchical gates, any K); otherwise the fp64 torch path
-        runs."""
+        """The fused HIP epilogue (csrc/hip/gbst.hip) covers every scalar loss
+        (GBST_LOSS_IDS) and 2 <= K <= 64 (softmax and hierarchical gates, any K); otherwise
+        (K > 64, CPU, YTK_GBST_FUSED=0) the fp64 torch path runs."""
         K = self.K
-        return (X.values.is_cuda and self.loss.name in ("sigmoid", "l2") and 2 <= K <= 64
+        return (X.values.is_cuda and self.loss.name in GBST_LOSS_IDS and 2 <= K <= 64
                 and os.environ.get("YTK_GBST_FUSED", "1") != "0")
+
+    def _lgamma_y(self, d):
+        """lgamma(y + 1) per row, fp64 (poisson's label term, computed once per data set)."""
+        cache = self.__dict__.setdefault("_lgy_cache", {})
+        key = d.y.data_ptr()
+        if key not in cache:
+            cache[key] = torch.lgamma(d.y[:, 0].double() + 1.0).contiguous()
+        return cache[key]
 
     def _forward_fused(self, X, d, z, w, g_out, train: bool):
         from ...ops._ext import hip, ptr, stream
@@ -202,9 +214,10 @@ class GBSTModel(ContinuousModelBase):
         leaves = w[:K].contiguous() if self.expert_kind == "scalar" else None
         hip().gbst_epilogue(ptr(A), A.stride(0), ptr(z), ptr(y), ptr(wt), ptr(mask), float(1.0 / self.rate),
                             ptr(leaves), n, K, 1 if self.gate_kind == "tree" else 0,
-                            1 if self.expert_kind == "linear" else 0, 0 if self.loss.name == "sigmoid" else 1,
-                            1 if self.rf else 0, self.finished + 1, 1 if want else 0, ptr(D), self.stride,
-                            ptr(pred), ptr(acc), stream(A))
+                            1 if self.expert_kind == "linear" else 0, GBST_LOSS_IDS[self.loss.name],
+                            float(getattr(self.loss, "delta", 0.0)), 1 if self.rf else 0, self.finished + 1, 1 if want else 0, ptr(D), self.stride,
+                            ptr(pred), ptr(acc), ptr(self._lgamma_y(d)) if self.loss.name == "poisson" else 0,
+                            stream(A))
         if want:
             G = g_out[self.gate_off:].view(self.F, self.stride)
             X.t_matmul(D, out=G)

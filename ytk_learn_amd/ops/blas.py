@@ -82,13 +82,15 @@ def axpy_dot(p: torch.Tensor, x: torch.Tensor, alpha: float, scale: float, d: to
 _ROW_LOSS = {"sigmoid": 0, "l2": 1}
 
 
-def row_loss(loss, z0: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, z1=None, want_grad: bool = True):
+def row_loss(loss, z0: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, z1=None, want_grad: bool = True,
+             want_loss: bool = True):
     """One fused pass over the rows of a single-output L-BFGS model (``row_loss_partial_kernel``):
     z = z0 (+ z1) in fp64 -> (sum weight * loss (fp64 float), pred fp32 [n], c = weight * l'(z)
     fp32 [n] or None). The formulas are the loss classes' fp64 ones
     (``losses/functions.py``, reference LinearHoagOptimizer.java:127-147). Returns None when the
     fused pass does not cover the case (CPU tensors, losses other than sigmoid / l2,
-    YTK_ROW_LOSS=0): the caller runs the torch formulas then."""
+    YTK_ROW_LOSS=0): the caller runs the torch formulas then. ``want_loss=False``: the loss sum
+    is not read back (None; no host synchronisation -- SGD batches)."""
     lid = _ROW_LOSS.get(getattr(loss, "name", None))
     if lid is None or z0.device.type != "cuda" or os.environ.get("YTK_ROW_LOSS", "1") == "0":
         return None
@@ -108,4 +110,4 @@ def row_loss(loss, z0: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, z1=None,
     hip().row_loss(lid, ptr(z0), 1 if z0.dtype == torch.float64 else 0, ptr(z1) if z1 is not None else 0, ptr(y),
                    y.stride(0), ptr(wt), n, ptr(pred), ptr(c) if c is not None else 0, ptr(buf), ptr(buf[1024:]),
                    stream(z0))
-    return float(buf[1024]), pred, c
+    return (float(buf[1024]) if want_loss else None), pred, c

@@ -1,0 +1,156 @@
+"""Column-ordered mini-batch SGD steps for the linear / FM / FFM models (GPU).
+
+The optimizer's batches are fixed row ranges of the rank's CSR shard (only their visiting
+order is shuffled per epoch), so each batch's column order is built ONCE at set-up: a
+:class:`~ytk_learn_amd.ops.sparse.SparseMatrix` of the batch rows (global feature ids, one
+untiled CSC over the batch) plus the list of the features the batch touches with their chunk
+ranges and entry counts. A step is then
+
+  1. the row pass (``fm_forward``; FFM: + the pair forward) on the batch rows, read in place;
+  2. c_r = weight_r * l'(z_r) (fused row-loss pass, no host read);
+  3. the column pass over the batch CSC chunks (``fm_backward_kernel``: sum c x S, sum c x,
+     sum c x^2 per chunk; FFM: + the streamed pair-gradient kernel);
+  4. ``sgd_apply_kernel``: every touched feature sums its chunks in order and updates its
+     weights once -- w, V (FM / FFM, with l2 decay) and the bf16 / transposed working copies.
+
+Against the per-entry Hogwild! float atomics this replaces (42M atomics per 65536-row FM
+batch, 409M for FFM: ``docs/performance.md``), no two threads ever write one weight, the
+step is deterministic, and the per-feature mean step (``optimization.sgd.average =
+feature``) takes its counts from the CSC column lengths instead of a count + clear pass.
+Semantics: a synchronous mini-batch step -- every row's gradient is taken at the weights the
+batch started from (the CPU reference ``fm_sgd_update`` / :func:`ffm_step_cpu` does the same).
+Per-sample math: ``FMHoagOptimizer.java:127-137``, ``FFMHoagOptimizer.java:149-187``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from ._ext import check_cuda, hip, ptr, stream
+from .sparse import SparseMatrix
+
+
+class SGDBatch:
+    """One batch's column structure (device tensors)."""
+
+    __slots__ = ("b", "e", "X", "ucol", "ucp", "ucnt", "nu", "stream_st", "fields")
+
+
+def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None, nfield: int = 0,
+                  skip_feat: int = -1, unit_values: bool = False, want_stream: bool = False) -> List[SGDBatch]:
+    """Set-up of every batch [b, e) of ``bounds`` (rows of ``X``)."""
+    from .ffm import _stream_layout
+    out = []
+    for b, e in bounds:
+        o0, o1 = int(X.indptr[b]), int(X.indptr[e])
+        ip = (X.indptr[b:e + 1] - o0).contiguous()
+        Xb = SparseMatrix(ip, X.indices[o0:o1], X.values[o0:o1], X.ncols, row_tile=False)
+        counts = Xb.colptr[1:] - Xb.colptr[:-1]
+        u = torch.nonzero(counts).flatten()
+        bt = SGDBatch()
+        bt.b, bt.e, bt.X = b, e, Xb
+        bt.ucol = u.to(torch.int32).contiguous()
+        bt.ucnt = counts[u].to(torch.int32).contiguous()
+        # chunks of consecutive touched features are contiguous (empty columns own none)
+        bt.ucp = torch.cat([Xb.chunk_ptr[u], Xb.chunk_ptr[-1:]]).contiguous()
+        bt.nu = int(u.numel())
+        bt.fields = None
+        bt.stream_st = None
+        if fields is not None:
+            bt.fields = fields[o0:o1].contiguous()
+            if want_stream:
+                st = _stream_layout(Xb, bt.fields, nfield, skip_feat, unit_values)
+                if st is not None and torch.equal(st["cptr"], Xb.chunk_ptr):
+                    bt.stream_st = st
+        if fields is not None and bt.stream_st is None:
+            from .ffm import _csc_layout
+            _csc_layout(Xb, bt.fields, nfield)  # packed codes of the general pair-gradient kernel
+        else:
+            Xb.csc_perm = None  # only the general FFM kernel reads the entries' CSR positions
+        Xb.rows_of_nnz = None   # set-up only
+        out.append(bt)
+    return out
+
+
+def apply_step(bt: SGDBatch, part: torch.Tensor, lat: Optional[torch.Tensor], J: int, w_lin: torch.Tensor,
+               V: Optional[torch.Tensor], k: int, lr: float, l2w: float, l2v: float, reg_skip: int, upd_w: bool,
+               bias_latent: bool, avg: bool, Vb: Optional[torch.Tensor] = None, Vt: Optional[torch.Tensor] = None):
+    """``sgd_apply_kernel`` over the batch's touched features (see csrc/hip/fm.hip)."""
+    check_cuda(part, w_lin, *(t for t in (lat, V, Vb, Vt) if t is not None))
+    hip().sgd_apply(ptr(bt.ucol), ptr(bt.ucp), ptr(bt.ucnt), bt.nu, ptr(part), int(part.shape[1]),
+                    ptr(lat) if lat is not None else 0, int(J), ptr(w_lin), ptr(V) if V is not None else 0, int(k),
+                    ptr(Vb) if Vb is not None else 0, ptr(Vt) if Vt is not None else 0, int(w_lin.numel()),
+                    float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0, 1 if bias_latent else 0,
+                    1 if avg else 0, stream(w_lin))
+
+
+def column_sums(bt: SGDBatch, c: torch.Tensor, S: Optional[torch.Tensor], k: int) -> torch.Tensor:
+    """part[chunk, k + 2] = [sum c x S_f | sum c x | sum c x^2] over the batch CSC chunks."""
+    Xb = bt.X
+    part = torch.empty((max(Xb.n_chunks, 1), k + 2), dtype=torch.float32, device=c.device)
+    hip().fm_backward(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
+                      ptr(c), ptr(S) if (S is not None and k > 0) else 0, k, ptr(part), stream(c))
+    return part
+
+
+def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, Vt: torch.Tensor, nfield: int, k: int, skip_feat: int) -> torch.Tensor:
+    """lat[chunk, nfield * k] = the chunk's FFM pair gradient (streamed kernel when the batch
+    has the fixed layout, else the general column-ordered kernel)."""
+    from .ffm import _csc_layout
+    Xb = bt.X
+    J = nfield * k
+    lat = torch.empty((max(Xb.n_chunks, 1), J), dtype=torch.float32, device=c.device)
+    h, s = hip(), stream(c)
+    st = bt.stream_st
+    if st is not None:
+        se = c.index_select(0, st["rows"])
+        if st["vals"] is not None:
+            se.mul_(st["vals"])
+        wc = st["wc"]
+        h.ffm_grad_stream(ptr(wc), wc.numel() - 1, ptr(st["beg"]), ptr(st["end"]), ptr(st["chunk_fa"]),
+                          ptr(st["exp_idx"]), ptr(st["exp_val"]), ptr(se), Xb.nnz, ptr(st["lay_field"]), st["m"],
+                          ptr(Vt), Xb.ncols, nfield, k, ptr(lat), s)
+        return lat
+    lay = _csc_layout(Xb, bt.fields, nfield)
+    if lay is None:
+        raise RuntimeError("ffm sgd: feature / field codes do not fit 32 bits")
+    distinct, code, sh, vals = lay
+    h.ffm_grad_csc(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
+                   ptr(Xb.csc_perm), ptr(Xb.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
+                   ptr(Vt), Xb.ncols, nfield, k, ptr(c), ptr(lat), int(skip_feat), int(distinct), s)
+    return lat
+
+
+def ffm_step_cpu(indptr, idx, val, fld, w_lin, V, nfield: int, k: int, c, lr: float, l2w: float, l2v: float,
+                 reg_skip: int, upd_w: bool, bias_latent: bool, cnt=None, skip_feat: int = -1):
+    """CPU reference of one synchronous FFM batch step (linear part + pairs + l2 decay), all
+    gradients at the batch's starting weights; ``cnt`` (int32 [F]): per-feature mean."""
+    from .ffm import ffm_backward
+    n = int(indptr.shape[0] - 1)
+    b0, e0 = int(indptr[0]), int(indptr[-1])
+    rows = torch.repeat_interleave(torch.arange(n), (indptr[1:] - indptr[:-1]).long())
+    ix = idx[b0:e0].long()
+    x = val[b0:e0]
+    F = w_lin.numel()
+    ones = torch.ones_like(x)
+    ent = torch.zeros(F).index_add_(0, ix, ones)  # entries per feature in the batch
+    div = cnt.clamp(min=1).float() if cnt is not None else torch.ones(F)
+    gw = torch.zeros(F).index_add_(0, ix, c[rows] * x)
+    is_bias = torch.zeros(F, dtype=torch.bool)
+    if reg_skip >= 0:
+        is_bias[reg_skip] = True
+    gw += torch.where(is_bias, torch.zeros(()), ent * l2w * w_lin)
+    if not upd_w:
+        gw = torch.where(is_bias, gw, torch.zeros(()))
+    if V is not None and nfield * k > 0:
+        gV = torch.zeros_like(V)
+        ip_rel = indptr - b0
+        ffm_backward(ip_rel, idx[b0:e0], x, fld[b0:e0], V, nfield, k, c, gV, skip_feat=skip_feat)
+        G2 = gV.view(F, -1)
+        V2 = V.view(F, -1)
+        G2 += torch.where(is_bias[:, None], torch.zeros(()), (ent * l2v)[:, None] * V2)
+        if not bias_latent and reg_skip >= 0:
+            G2[reg_skip] = 0.0
+        V2 -= (lr / div)[:, None] * G2 * (ent > 0)[:, None]
+    w_lin -= (lr / div) * gw

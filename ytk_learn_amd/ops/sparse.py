@@ -75,8 +75,9 @@ class SparseMatrix:
     """Immutable CSR/CSC pair. ``indptr`` int64 [n+1], ``indices`` int32, ``values`` float32."""
 
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, ncols: int,
-                 build_csc: bool = True):
+                 build_csc: bool = True, row_tile: bool = True):
         self.device = indices.device
+        self.row_tile = row_tile  # False: one column order over all rows (SGD batches, ops/sgd.py)
         self.n = int(indptr.shape[0] - 1)
         self.ncols = int(ncols)
         self.indptr = indptr.to(torch.int64).contiguous()
@@ -140,7 +141,7 @@ class SparseMatrix:
         by column for the ordered chunk reduce (deterministic sum order)."""
         cols = self.indices.to(torch.int64)
         rows = self.rows_of_nnz.to(torch.int64)
-        tiled = self.device.type == "cuda" and ROW_TILE > 0 and self.n > ROW_TILE
+        tiled = self.device.type == "cuda" and ROW_TILE > 0 and self.n > ROW_TILE and self.row_tile
         T = -(-self.n // ROW_TILE) if tiled else 1
         seg = (rows // ROW_TILE) * self.ncols + cols if tiled else cols  # (tile, column) segments
         order = torch.sort(seg * (self.n + 1) + rows, stable=True).indices

@@ -182,7 +182,17 @@ class HoagOptimizer:
                 newg = torch.where(part_neg > 0.0, part_neg, torch.where(part_pos < 0.0, part_pos,
                                                                          torch.zeros_like(part_pos)))
                 gs.copy_(newg.float())
+        self._peer_landed()
         return pure, allloss
+
+    def _peer_landed(self):
+        """Raise if the last peer gradient exchange failed (waits only for that exchange; the
+        gradient post-processing above is already queued behind it)."""
+        ev = getattr(self, "_peer_event", None)
+        if ev is not None:
+            self._peer_event = None
+            ev.synchronize()
+            self._peer.check()
 
     def test_loss(self, w: torch.Tensor, g: Optional[torch.Tensor] = None) -> float:
         t = torch.tensor([self.m.test_pure_loss_grad(w, g)], dtype=torch.float64)
@@ -190,6 +200,7 @@ class HoagOptimizer:
             self.comm.allreduce_(t)
             if g is not None:
                 self._grad_allreduce(g)
+                self._peer_landed()
         return float(t[0])
 
     def _grad_allreduce(self, g: torch.Tensor):
@@ -199,6 +210,11 @@ class HoagOptimizer:
         peer = getattr(self, "_peer", None)
         if peer is not None and peer.fits(g):
             peer.allreduce_(g)
+            # a timed-out flag wait would leave g = stale peer sums (and every later exchange a
+            # no-op): loss_and_grad checks the host-mapped error word once this exchange is done
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(g.device))
+            self._peer_event = ev
         else:
             self.comm.allreduce_(g)
 

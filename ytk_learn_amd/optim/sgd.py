@@ -1,26 +1,32 @@
-"""Mini-batch Hogwild!-style SGD for the linear, FM and FFM models.
+"""Mini-batch SGD for the linear, FM and FFM models.
 
 An extension (``optimization.optimizer = "sgd"``): ytk-learn trains these models only
 with full-batch L-BFGS (``J/param/CommonParams.java:55-60``), which stays the default.
 SGD trades the L-BFGS convergence guarantees for cheap passes over data sets too large
 to iterate many times.
 
-Per mini-batch of rows (a contiguous row range of the rank's CSR shard, visited in a
-seeded random order every epoch):
-  1. forward on the batch rows (the training kernels read the CSR slice in place:
-     ``fm_forward`` -- with k = 0 for the linear part -- and the FFM pair kernel);
-  2. c_r = weight_r * dloss/dz (any loss of the framework, on the device);
-  3. lock-free update: ``fm_sgd_update`` (csrc/hip/fm.hip) for the linear weights and
-     FM latents, the FFM pair kernel with coefficient -lr * c_r written straight into V.
-     Concurrent rows sharing a feature race exactly as in Hogwild! (Niu et al., 2011).
-Regularization: l2 of the linear / latent groups is applied to the weights a sample
-touches (sparse weight decay); l1 is not supported by this optimizer. FFM latents get no
-decay (the pair kernel has none).
-Step size (``optimization.sgd.average``): with ``feature`` (default) a weight's step is
-the MEAN of the per-sample steps of the batch rows containing its feature (rows per
-feature counted on the device before the update) -- rare features keep the per-sample
-rate, hot ones (the bias is in every row) take one bounded step per batch. ``none`` applies
-the sum, which for batches of thousands of rows diverges on hot features.
+Batches are fixed contiguous row ranges of the rank's CSR shard, visited in a seeded random
+order every epoch. On the GPU each batch's column order is built once at set-up
+(:mod:`ytk_learn_amd.ops.sgd`) and a step is four kernels: the row pass (``fm_forward``;
+FFM: + the pair forward), the fused row-loss pass (c_r = weight_r * dloss/dz), the
+column pass over the batch CSC (FFM: + the streamed pair gradient) and ``sgd_apply``, where
+every touched feature sums its chunk partials in order and updates its weights ONCE -- a
+deterministic synchronous mini-batch step with no float atomics (round 4 ran per-entry
+Hogwild! atomics: 42M per 65536-row FM batch, 409M for FFM). The CPU path applies the same
+synchronous step with index ops (``fm_sgd_update`` / ``ffm_step_cpu``).
+Regularization: l2 of the linear / latent groups (FFM latents too) is applied to the weights
+a batch touches, once per batch entry holding the feature (sparse weight decay); l1 is not
+supported by this optimizer.
+Step size (``optimization.sgd.average``): with ``feature`` (default since round 4) a
+weight's step is the MEAN of the per-sample steps of the batch entries holding its feature
+(the batch CSC's column length) -- rare features keep the per-sample rate, hot ones (the bias
+is in every row) take one bounded step per batch. ``none`` applies the sum, which for batches
+of thousands of rows diverges on hot features. FFM: the count of V[i, f] is the entries of
+feature i in the batch (not only those whose row also holds a field-f feature), so for rows
+without every field such latents take a smaller step than a per-(feature, field) mean.
+``optimization.sgd.dtype = bf16`` (FM): the row pass gathers the latents from a bf16 working
+copy (half the bytes of its dominant V-row gathers); the fp32 master takes the updates and
+``sgd_apply`` re-rounds the copy of every touched row.
 
 Multi-GPU: every rank runs SGD on its shard; weights are averaged across ranks with one
 RCCL all-reduce every ``sync_every`` batches (0 = once per epoch) -- local SGD / model
@@ -35,7 +41,9 @@ from typing import List
 import numpy as np
 import torch
 
-from ..ops.ffm import ffm_backward, ffm_forward
+from ..ops import sgd as sgd_ops
+from ..ops.blas import row_loss
+from ..ops.ffm import ffm_forward
 from ..ops.fm import fm_forward, fm_sgd_update, sgd_count
 from ..utils.fault import fault_point
 from ..utils.javafmt import java_double_str as jd
@@ -98,69 +106,118 @@ class SGDOptimizer:
         self.l2v = float(l2[1]) if len(l2) > 1 else 0.0
         self.dump_freq = dump_freq
         self.dist = comm is not None and comm.is_dist
-        # bf16 storage (BASELINE config 4, "FM k=16 ... bf16 SGD"): the FM latent matrix is
-        # gathered from a bf16 working copy by the forward and gradient passes (half the
-        # bytes of the dominant V-row gathers); updates land in the fp32 master, whose
-        # touched entries re-round the copy; full re-sync after every weight averaging.
-        # per-feature averaging (average = feature): rows per feature of the current batch,
-        # counted before the update and cleared after it (zero between batches)
-        self.cnt = (torch.zeros(model.F, dtype=torch.int32, device=model.w.device)
-                    if sp.average == "feature" else None)
+        dev = model.w.device
+        F = model.F
+        self.kk = model.kk if model.name == "fm" else 0
+        if dev.type == "cuda" and self.kk > 64:
+            from ..utils.errors import YtkLearnError
+            raise YtkLearnError("optimization.optimizer = sgd on the GPU supports fm k <= 64")
+        # CPU: rows per feature of the current batch (count, step, clear); GPU: the batch CSC
+        self.cnt = (torch.zeros(F, dtype=torch.int32, device=dev)
+                    if sp.average == "feature" and dev.type != "cuda" else None)
         self.Vb = None
-        if sp.dtype == "bf16" and model.name == "fm" and getattr(model, "kk", 0) > 0:
-            self.Vb = torch.empty((model.F, model.kk), dtype=torch.bfloat16, device=model.w.device)
+        if sp.dtype == "bf16" and model.name == "fm" and self.kk > 0:
+            self.Vb = torch.empty((F, self.kk), dtype=torch.bfloat16, device=dev)
+        # FFM on the GPU: the pair-gradient kernels read the latents field-major ([nfield][F][k],
+        # each XCD's fields an L2-sized working set); sgd_apply keeps this copy current
+        self.ffm = model.name == "ffm" and getattr(model, "stride", 0) > 0
+        self.Vt = None
+        if self.ffm and dev.type == "cuda":
+            self.Vt = torch.empty((model.nf, F, model.kk), dtype=torch.float32, device=dev)
+        self._batches = None
 
     # ------------------------------------------------------------------ one batch
-    def _step(self, w: torch.Tensor, b: int, e: int, lr: float):
+    def _setup(self, bounds):
+        m = self.m
+        X = m.X
+        if self._batches is None and X.device.type == "cuda":
+            fld = m.data.train.fields if self.ffm else None
+            unit = bool(X.one_hot)
+            self._batches = sgd_ops.build_batches(X, bounds, fld, m.nf if self.ffm else 0,
+                                                  getattr(m, "_skip", -1), unit, want_stream=self.ffm
+                                                  and m.kk in (4, 8, 16))
+        return self._batches
+
+    def _step(self, w: torch.Tensor, b: int, e: int, lr: float, bt=None):
+        if bt is not None:
+            return self._step_gpu(w, bt, lr)
+        return self._step_cpu(w, b, e, lr)
+
+    def _coef(self, fx, y, wt, z1=None):
+        fused = row_loss(self.m.loss, fx, y, wt, z1=z1, want_grad=True, want_loss=False)
+        if fused is not None:
+            return fused[2]
+        z = fx.double() + (z1.double() if z1 is not None else 0.0)
+        return (wt.double() * self.m.loss.grad(z, y.double())).float().contiguous()
+
+    def _step_gpu(self, w: torch.Tensor, bt, lr: float):
+        """Row pass -> c -> column pass -> one update per touched weight (ops/sgd.py)."""
+        m, sp = self.m, self.sp
+        d = m.data.train
+        X, F = m.X, m.F
+        b, e = bt.b, bt.e
+        sl = _Slice(X, b, e)
+        w_lin = w[:F]
+        kk = self.kk
+        reg_skip = 0 if m.p.model.need_bias else -1
+        upd_w = getattr(m, "need_first", True)
+        Vf = (self.Vb if self.Vb is not None else w[F:].view(F, kk)) if kk > 0 else w_lin.new_zeros((F, 0))
+        fx, S = fm_forward(sl, w_lin, Vf)
+        z1 = None
+        if self.ffm:
+            z1 = ffm_forward(sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m.kk, skip_feat=m._skip)
+        c = self._coef(fx, d.y[b:e, 0], d.weight[b:e], z1)
+        part = sgd_ops.column_sums(bt, c, S if kk > 0 else None, kk)
+        avg = sp.average == "feature"
+        if self.ffm and getattr(m, "need_second", True):
+            lat = sgd_ops.ffm_pair_sums(bt, c, self.Vt, m.nf, m.kk, m._skip)
+            sgd_ops.apply_step(bt, part, lat, m.stride, w_lin, w[F:], m.kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
+                               bool(getattr(m, "bias_latent", False)), avg, Vt=self.Vt)
+        else:
+            V = w[F:].view(F, kk) if kk > 0 else None
+            sgd_ops.apply_step(bt, part, None, kk, w_lin, V, kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
+                               bool(getattr(m, "bias_latent", False)), avg, Vb=self.Vb)
+
+    def _step_cpu(self, w: torch.Tensor, b: int, e: int, lr: float):
+        """The same synchronous step with index ops (reference of the GPU kernels)."""
         m = self.m
         d = m.data.train
         X = m.X
         F = m.F
         reg_skip = 0 if m.p.model.need_bias else -1
         upd_w = getattr(m, "need_first", True)
-        sl = _Slice(X, b, e)
         w_lin = w[:F]
-        # nnz range of the batch: only the CPU paths need it on the host (a device read
-        # would synchronise every batch)
-        o0, o1 = (int(X.indptr[b]), int(X.indptr[e])) if not w.is_cuda else (None, None)
+        o0, o1 = int(X.indptr[b]), int(X.indptr[e])
+        rows = X.rows_of_nnz[o0:o1] - b
+        lin = w_lin[X.indices[o0:o1].long()] * X.values[o0:o1]
+        fx = torch.zeros(e - b, dtype=torch.float64, device=w.device).index_add_(0, rows, lin.double())
         S = None
-        if w.is_cuda and (m.name != "fm" or m.kk <= 64):
-            # fused row pass (k = 0: linear score only): fx and S = X V of the batch
-            kk = m.kk if m.name == "fm" else 0
-            Vf = (self.Vb if self.Vb is not None else w[F:].view(F, kk)) if kk > 0 else w_lin.new_zeros((F, 0))
-            fx, S = fm_forward(sl, w_lin, Vf)
-            if kk == 0:
-                S = None
-        else:
-            rows = X.rows_of_nnz[o0:o1] - b
-            lin = w_lin[X.indices[o0:o1].long()] * X.values[o0:o1]
-            fx = torch.zeros(e - b, dtype=torch.float64, device=w.device).index_add_(0, rows, lin.double())
-            if m.name == "fm" and m.kk > 0:  # CPU: S = X V and the square term from index ops
-                V = self.Vb.float() if self.Vb is not None else w[F:].view(F, m.kk)
-                vx = V[X.indices[o0:o1].long()] * X.values[o0:o1, None]
-                S = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx)
-                Q = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx * vx)
-                fx = fx + 0.5 * (S.double() ** 2 - Q.double()).sum(1)
-        if m.name == "ffm" and m.stride > 0:
-            fld = d.fields
-            ip = sl.indptr if w.is_cuda else sl.indptr - o0
-            idx = X.indices if w.is_cuda else X.indices[o0:o1]
-            val = X.values if w.is_cuda else X.values[o0:o1]
-            fl = fld if w.is_cuda else fld[o0:o1]
-            fx = fx + ffm_forward(ip, idx, val, fl, w[F:], m.nf, m.kk, skip_feat=m._skip).double()
+        if m.name == "fm" and m.kk > 0:  # S = X V and the square term from index ops
+            V = self.Vb.float() if self.Vb is not None else w[F:].view(F, m.kk)
+            vx = V[X.indices[o0:o1].long()] * X.values[o0:o1, None]
+            S = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx)
+            Q = torch.zeros((e - b, m.kk), dtype=torch.float32).index_add_(0, rows, vx * vx)
+            fx = fx + 0.5 * (S.double() ** 2 - Q.double()).sum(1)
+        sl_ip = X.indptr[b:e + 1]
+        if self.ffm:
+            fx = fx + ffm_forward(sl_ip - o0, X.indices[o0:o1], X.values[o0:o1], d.fields[o0:o1], w[F:], m.nf,
+                                  m.kk, skip_feat=m._skip).double()
         y = d.y[b:e, 0].double()
         c = (d.weight[b:e].double() * m.loss.grad(fx, y)).float().contiguous()
-        V = w[F:].view(F, m.kk) if (m.name == "fm" and m.kk > 0) else None
         cnt = self.cnt
         if cnt is not None:
-            sgd_count(sl.indptr, X.indices, cnt, nnz_hint=(e - b) * max(1, X.nnz // max(1, X.n)))
-        fm_sgd_update(sl.indptr, X.indices, X.values, w_lin, V, S, c, lr, self.l2w, self.l2v, reg_skip, upd_w,
-                      bool(getattr(m, "bias_latent", False)), Vb=self.Vb, cnt=cnt)
-        if m.name == "ffm" and m.stride > 0 and getattr(m, "need_second", True):
-            ffm_backward(ip, idx, val, fl, w[F:], m.nf, m.kk, (-lr * c).contiguous(), w[F:], skip_feat=m._skip,
-                         cnt=cnt)
+            sgd_count(sl_ip, X.indices, cnt)
+        if self.ffm:
+            sgd_ops.ffm_step_cpu(sl_ip, X.indices, X.values, d.fields, w_lin,
+                                 w[F:] if getattr(m, "need_second", True) else None, m.nf, m.kk, c, lr, self.l2w,
+                                 self.l2v, reg_skip, upd_w, bool(getattr(m, "bias_latent", False)), cnt=cnt,
+                                 skip_feat=m._skip)
+        else:
+            V = w[F:].view(F, m.kk) if (m.name == "fm" and m.kk > 0) else None
+            fm_sgd_update(sl_ip, X.indices, X.values, w_lin, V, S, c, lr, self.l2w, self.l2v, reg_skip, upd_w,
+                          bool(getattr(m, "bias_latent", False)), Vb=self.Vb, cnt=cnt)
         if cnt is not None:
-            sgd_count(sl.indptr, X.indices, cnt, clear=True, nnz_hint=(e - b) * max(1, X.nnz // max(1, X.n)))
+            sgd_count(sl_ip, X.indices, cnt, clear=True)
 
     def _average(self, w):
         if self.dist:
@@ -169,8 +226,11 @@ class SGDOptimizer:
         self._sync_copy(w)
 
     def _sync_copy(self, w):
+        F = self.m.F
         if self.Vb is not None:
-            self.Vb.copy_(w[self.m.F:].view(self.m.F, self.m.kk))
+            self.Vb.copy_(w[F:].view(F, self.m.kk))
+        if self.Vt is not None:
+            self.Vt.copy_(w[F:].view(F, self.m.nf, self.m.kk).transpose(0, 1))
 
     def _losses(self, w):
         t = torch.tensor([self.m.pure_loss_grad(w, None), self.m.test_pure_loss_grad(w, None)
@@ -191,6 +251,7 @@ class SGDOptimizer:
         nb_all = nb
         if self.dist:  # every rank runs the same number of steps (the sync points must match)
             nb_all = int(self.comm.allreduce_scalars([nb], op="max", dtype=torch.int64)[0])
+        batches = self._setup(bounds)
         rng = np.random.default_rng(sp.seed + (self.comm.rank if self.comm is not None else 0))
         lr = sp.learning_rate
         self._sync_copy(w)
@@ -202,8 +263,9 @@ class SGDOptimizer:
             order = rng.permutation(nb) if nb else np.zeros(0, np.int64)
             for step in range(nb_all):
                 if step < nb:
-                    b, e = bounds[int(order[step])]
-                    self._step(w, b, e, lr)
+                    j = int(order[step])
+                    b, e = bounds[j]
+                    self._step(w, b, e, lr, batches[j] if batches is not None else None)
                 if self.dist and sp.sync_every > 0 and (step + 1) % sp.sync_every == 0:
                     self._average(w)
             if self.dist and (sp.sync_every <= 0 or nb_all % sp.sync_every != 0):

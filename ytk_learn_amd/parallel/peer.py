@@ -15,7 +15,9 @@ device (the leaf-wise batch). int64 sums are exact (bitwise the RCCL result); fp
 Default for single-node multi-GPU jobs (every rank on this host: LOCAL_WORLD_SIZE ==
 WORLD_SIZE); every rank must create and open every handle, else an all-rank vote falls back
 to RCCL. ``YTK_PEER_REDUCE=0`` forces RCCL, ``=1`` forces the peer path (e.g. several ranks
-sharing one GPU over gloo). Flag waits are bounded (``YTK_PEER_TIMEOUT_S``, 60 s); a timed-out
+sharing one GPU over gloo). Flag waits are bounded (``YTK_PEER_TIMEOUT_S``, default the
+process-group timeout ``YTK_COMM_TIMEOUT``, 1800 s -- a rank may legitimately trail its peers by
+rank-0-only host work such as a model dump; the start-up self-test waits at most 10 s); a timed-out
 wait sets a host-mapped error word that :meth:`PeerReduce.check` (called where the trainer
 lands its rounds) turns into an exception.
 """
@@ -28,6 +30,7 @@ import numpy as np
 import torch
 
 from ..ops._ext import hip, ptr, stream
+from ..utils.fault import fault_point
 from .comm import Comm
 
 
@@ -54,7 +57,8 @@ class PeerReduce:
 
     def __init__(self, comm: Comm, hnd: int, cap: int):
         self.comm = comm
-        self.TIMEOUT_S = float(os.environ.get("YTK_PEER_TIMEOUT_S", 60.0))  # per flag wait (device wall clock)
+        # per flag wait (device wall clock): as long as the RCCL path it replaces would wait
+        self.TIMEOUT_S = float(os.environ.get("YTK_PEER_TIMEOUT_S", os.environ.get("YTK_COMM_TIMEOUT", 1800.0)))
         self.hnd = hnd
         self.cap = int(cap)  # 8-byte words
         self.cap_bytes = 8 * self.cap
@@ -122,6 +126,8 @@ class PeerReduce:
         P, r = self.comm.world, self.comm.rank
         saved = self.TIMEOUT_S
         self.TIMEOUT_S = min(saved, 10.0)
+        stats = dict(self.comm.stats)  # the probe exchanges are not the job's traffic
+        nlog = len(self.comm.log) if self.comm.log is not None else 0
         try:
             n = min(self.cap, 4099)  # odd: the single-element tail too
             t = torch.arange(n, dtype=torch.int64, device=self.comm.device) * P + r + 1
@@ -143,10 +149,9 @@ class PeerReduce:
         finally:
             self.TIMEOUT_S = saved
             self.calls = 0
-            self.comm.stats["calls"] -= 5
-            self.comm.stats["bytes"] -= 8 * (min(self.cap, 4099) + 5) + 4 * 1025 + 2 * 8 * 2 * P
+            self.comm.stats = stats
             if self.comm.log is not None:
-                del self.comm.log[-5:]
+                del self.comm.log[nlog:]
 
     def _account(self, t: torch.Tensor, n: int, skippable: bool = False):
         """Count an exchange. ``skippable`` ones (device skip word: leaf-wise batches a host
@@ -171,6 +176,9 @@ class PeerReduce:
         two-shot reduce-scatter + all-gather above)."""
         assert self.fits(t), (t.dtype, t.numel(), t.data_ptr() % 16)
         n = t.numel()
+        if fault_point("peer", self.calls, self.comm.rank):  # tests: an exchange this rank drops
+            self.calls += 1
+            return
         hip().peer_allreduce(self.hnd, ptr(t), n, self._TYPES[t.dtype], self.TIMEOUT_S, stream(t))
         self._account(t, n * t.element_size() // 8)
 

@@ -4,7 +4,9 @@
 ``<loop>`` (``gbdt`` boosting round, ``lbfgs`` iteration, ``gbst`` soft tree, ``bench``
 timed round) is about to run step ``<step>`` (0-based). ``mode`` = ``exit`` (default: the
 process dies with status 75 without cleanup, like a killed worker), ``raise`` (a Python
-exception, so the normal error path runs) or ``stall`` (the rank hangs without exiting, like
+exception, so the normal error path runs), ``skip`` (:func:`fault_point` returns True and the
+caller silently drops that step -- e.g. loop ``peer``: one peer-memory exchange this rank never
+issues, so its peers' flag waits must time out and raise) or ``stall`` (the rank hangs without exiting, like
 a wedged worker: the other ranks' collectives must time out and fail the job). Several specs can be given separated by ``;``. With ``YTK_FAULT_ONCE=<file>``
 a spec fires only while ``<file>`` does not exist (it is created when the fault fires), so a
 restarted job runs through. Unset: no cost beyond a dictionary lookup per step.
@@ -37,7 +39,8 @@ def _specs():
     return specs
 
 
-def fault_point(loop: str, step: int, rank: int = 0):
+def fault_point(loop: str, step: int, rank: int = 0) -> bool:
+    """Fire the matching spec, if any; True only for a ``skip`` spec (the caller drops the step)."""
     for lp, r, st, mode in _specs():
         if lp == loop and r == rank and st == step:
             once = os.environ.get("YTK_FAULT_ONCE")
@@ -46,6 +49,10 @@ def fault_point(loop: str, step: int, rank: int = 0):
                     continue
                 open(once, "w").close()
             msg = f"[rank {rank}] injected fault at {loop} step {step}"
+            if mode == "skip":
+                sys.stderr.write(msg + " (skip)\n")
+                sys.stderr.flush()
+                return True
             if mode == "raise":
                 raise InjectedFault(msg)
             if mode == "stall":
@@ -57,3 +64,4 @@ def fault_point(loop: str, step: int, rank: int = 0):
             sys.stderr.write(msg + " (exit)\n")
             sys.stderr.flush()
             os._exit(FAULT_EXIT_CODE)
+    return False
