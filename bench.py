@@ -44,6 +44,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from ytk_learn_amd.data.synthetic import higgs_like_rows  # noqa: E402
 from ytk_learn_amd.models.gbdt.builder import TreeParams  # noqa: E402
 from ytk_learn_amd.models.gbdt.trainer import GBDTData, GBDTParams, GBDTTrainer  # noqa: E402
+from ytk_learn_amd.parallel import peer as peer_mod  # noqa: E402
 from ytk_learn_amd.parallel.comm import Comm  # noqa: E402
 from ytk_learn_amd.utils.fault import fault_point  # noqa: E402
 from ytk_learn_amd.utils.logging import YtkLogger  # noqa: E402
@@ -61,6 +62,8 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     comm.reset_stats()
+    peer = getattr(tr.builder, "peer", None)
+    x0 = peer.timing() if peer is not None else (0, 0.0)
     t0 = time.perf_counter()
     for i in range(warmup, warmup + steps):
         fault_point("bench", i, comm.rank)  # YTK_FAULT_INJECT=bench:<rank>:<round>:stall (tests)
@@ -71,6 +74,10 @@ def timed_rounds(tr, comm, dev, warmup: int, steps: int) -> float:
     comm.barrier()
     el = time.perf_counter() - t0
     timed_stats = dict(comm.stats)
+    if peer is not None:  # device-timed peer exchanges of the timed rounds (outside the timing)
+        x1 = peer.timing()
+        timed_stats["peer_exchanges"] = x1[0] - x0[0]
+        timed_stats["peer_us"] = x1[1] - x0[1]
     el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
     comm.stats = timed_stats  # the timed rounds' collectives only
     return el
@@ -171,6 +178,7 @@ def run(a, comm):
     tr_builder = tr.builder
     leaf_steps = a.leafwise_steps if a.leafwise_steps is not None else 10
     leaf = leaf_transport = leaf_error = None
+    leaf_coll = {}
     tr.close()
     if leaf_steps > 0 and a.policy == "level":
         del tr
@@ -184,6 +192,7 @@ def run(a, comm):
             trl.prepare()
             trl.init_gradients()
             leaf = timed_rounds(trl, comm, dev, 3, leaf_steps) / leaf_steps
+            leaf_coll = dict(comm.stats)
             assert len(trl.model.trees) == 3 + leaf_steps
             leaf_transport = _transport(comm, trl.builder)
             trl.close()
@@ -232,12 +241,22 @@ def run(a, comm):
             "hist_transport": transport,
             "graph_replays": replays,
             "trees_converted": total_rounds,
+            # multi-GPU diagnostics: the start-up self-test of the peer-memory path (on a vote
+            # for RCCL, the reason) and the device-timed exchanges of the timed trees
+            "peer_selftest": (peer_mod.LAST_STATUS["state"] + (": " + peer_mod.LAST_STATUS["reason"]
+                                                               if peer_mod.LAST_STATUS["reason"] else ""))
+            if comm.is_dist else "n/a",
+            "exchanges_per_tree": round(coll.get("peer_exchanges", coll["calls"]) / a.steps, 2),
+            "exchange_us_per_tree": (round(coll["peer_us"] / a.steps, 2) if "peer_us" in coll else None),
         }
         if leaf is not None:
             res["leafwise_s_per_tree"] = round(leaf, 6)
             res["leafwise_vs_reference"] = round(leaf / BASELINE_SEC_PER_TREE, 6)
             res["leafwise_rounds_timed"] = leaf_steps
             res["leafwise_transport"] = leaf_transport
+            if "peer_us" in leaf_coll:
+                res["leafwise_exchanges_per_tree"] = round(leaf_coll["peer_exchanges"] / leaf_steps, 2)
+                res["leafwise_exchange_us_per_tree"] = round(leaf_coll["peer_us"] / leaf_steps, 2)
         if leaf_error is not None:
             res["leafwise_error"] = leaf_error
         print(json.dumps(res), flush=True)

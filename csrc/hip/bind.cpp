@@ -114,6 +114,7 @@ void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintp
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
+void ytk_lw_set_batch_cap(int, int);
 long long ytk_lw_ws_bytes(int, int);
 uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
@@ -126,6 +127,7 @@ int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, ui
                        uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int,
                        uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t);
+void ytk_copy_to_mapped(uintptr_t, uintptr_t, long long, uintptr_t);
 int ytk_tree_grad_hist_grid(long long);
 void ytk_hist_reduce(uintptr_t, uintptr_t, int, uintptr_t, int, int, int, int, uintptr_t);
 void ytk_hist_wide_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
@@ -147,6 +149,7 @@ int ytk_peer_check(int);
 long long ytk_peer_epoch(int);
 void ytk_peer_abort(int);
 void ytk_peer_set_grid_cap(int, int);
+void ytk_peer_timing(int, uintptr_t);
 void ytk_peer_destroy(int);
 void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 void ytk_owner_unpack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
@@ -272,6 +275,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
+  m.def("lw_set_batch_cap", &ytk_lw_set_batch_cap);
   m.def("lw_ws_bytes", &ytk_lw_ws_bytes);
   m.def("host_device_ptr", &ytk_host_device_ptr);
   m.def("lw_step", &ytk_lw_step);
@@ -296,11 +300,13 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("peer_check", &ytk_peer_check);
   m.def("peer_epoch", &ytk_peer_epoch);
   m.def("peer_abort", &ytk_peer_abort);
+  m.def("peer_timing", &ytk_peer_timing);
   m.def("peer_set_grid_cap", &ytk_peer_set_grid_cap);
   m.def("peer_destroy", &ytk_peer_destroy);
   m.def("lw_msg", &ytk_lw_msg);
   m.def("hist_wide_staged_dev", &ytk_hist_wide_staged_dev);
   m.def("tree_grad_hist", &ytk_tree_grad_hist);
+  m.def("copy_to_mapped", &ytk_copy_to_mapped);
   m.def("tree_grad_hist_grid", &ytk_tree_grad_hist_grid);
   m.def("hist_reduce", &ytk_hist_reduce);
   m.def("seg_median", &ytk_seg_median);

@@ -285,6 +285,9 @@ __global__ __launch_bounds__(kXchgThreads) void peer_xchg_kernel(PeerPtrs pp, in
     if (m.seg_p > 0) n *= m.seg_p;  // contiguous segments
   }
   if (t == 0) s_e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  // device-timed exchanges (diagnostics, ytk_peer_timing): block 0's start, read by the last
+  // block to finish (which arrived after block 0's start, through the ctl[1] counter)
+  if (b == 0 && t == 0) __hip_atomic_store(ctl + 3, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const unsigned long long e = s_e;
   if (n * ES > cap_bytes) {  // identical on every rank: nobody exchanges, the host check raises
@@ -389,6 +392,9 @@ done:
     if (prev == (unsigned long long)(G - 1)) {
       __hip_atomic_store(ctl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ctl[4] += wall_clock64() - t0;  // exchange ticks (only this block writes ctl[4], ctl[5])
+      ctl[5] += 1;
     }
   }
 }
@@ -399,7 +405,8 @@ struct PeerGroup {
   char* base = nullptr;  // own uncached allocation
   std::vector<void*> opened;
   PeerPtrs pp{};
-  unsigned long long* ctl = nullptr;  // device: [0] last epoch, [1] block arrivals, [2] timed out
+  unsigned long long* ctl = nullptr;  // device: [0] last epoch, [1] block arrivals, [2] timed out,
+                                      // [3] exchange start tick, [4] exchange ticks, [5] exchanges
   long long ticks_per_s = 100000000;  // wall_clock64 rate
   bool sys_fence = true;              // YTK_PEER_SYS_FENCE=0: waitcnt-ordered publishing only
   int block_bytes = 16384;            // YTK_PEER_BLOCK_BYTES: message bytes per block
@@ -453,8 +460,8 @@ int ytk_peer_create(int P, int rank, long long cap, uintptr_t out_handle) {
   YTK_HIP_CHECK(hipExtMallocWithFlags(&p, ytk::peer_bytes(cap), hipDeviceMallocUncached));
   YTK_HIP_CHECK(hipMemset(p, 0, 2 * ytk::peer_sig_bytes()));
   g.base = (char*)p;
-  YTK_HIP_CHECK(hipMalloc(&g.ctl, 4 * sizeof(unsigned long long)));
-  YTK_HIP_CHECK(hipMemset(g.ctl, 0, 4 * sizeof(unsigned long long)));
+  YTK_HIP_CHECK(hipMalloc(&g.ctl, 8 * sizeof(unsigned long long)));
+  YTK_HIP_CHECK(hipMemset(g.ctl, 0, 8 * sizeof(unsigned long long)));
   int dev = 0, khz = 0;
   YTK_HIP_CHECK(hipGetDevice(&dev));
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
@@ -612,6 +619,17 @@ long long ytk_peer_epoch(int hnd) {
   unsigned long long e = 0;
   (void)hipMemcpy(&e, g_peer.at(hnd).ctl, sizeof(e), hipMemcpyDeviceToHost);
   return (long long)e;
+}
+
+// Device-timed exchanges so far (synchronous copy; diagnostics): out[0] = exchanges that ran,
+// out[1] = their summed wall time in microseconds (block 0's start to the last block's end).
+void ytk_peer_timing(int hnd, uintptr_t out) {
+  ytk::PeerGroup& g = g_peer.at(hnd);
+  unsigned long long c[8] = {};
+  (void)hipMemcpy(c, g.ctl, sizeof(c), hipMemcpyDeviceToHost);
+  double* o = reinterpret_cast<double*>(out);
+  o[0] = (double)c[5];
+  o[1] = 1e6 * (double)c[4] / (double)g.ticks_per_s;
 }
 
 // At most `cap` blocks per exchange (every rank of the group must use the same cap). An

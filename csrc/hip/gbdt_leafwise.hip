@@ -64,6 +64,8 @@ struct LwParams {
   int split_groups;  // split records per item (feature groups of split_node_kernel)
   int dist;  // multi-GPU: per batch the host all-reduces the built slots + split cursors
   int bin_bytes;  // 1: uint8 bins, 2: uint16 bins (B > 256)
+  int batch_cap;  // > 0: at most this many splits per batch (the RCCL batch loop sizes its fixed
+                  // messages by it, ytk_lw_set_batch_cap); 0: no cap
 };
 
 // global-memory planner workspace (large trees): the arrays the LDS planner keeps in LDS
@@ -649,6 +651,9 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     // which the next replay always splits (so it pays for its pair); cap >= 2 max_leaf + 3
     // holds the invariant from the root on
     k = p.speculate ? max(1, min(min(remaining, kLwLeafMax), (fr - 2 * remaining - 2) >> 1)) : 1;
+    // host-chosen cap (RCCL batch loop): the batch is then the best-ranked prefix of the
+    // candidates -- the replay still splits exactly the sequential growth's nodes
+    if (p.batch_cap > 0) k = min(k, p.batch_cap);
     if (fr < 2) k = 0;
   }
   int* s_batch = reinterpret_cast<int*>(s_akey);  // the batch, in pop order (A is consumed)
@@ -1016,7 +1021,8 @@ __global__ __launch_bounds__(256) void lw_zero_slots_kernel(longlong2* __restric
 __global__ __launch_bounds__(256) void lw_msg_kernel(long long* __restrict__ hist, long long slot_elems,
                                                      const int* __restrict__ build_ids, const int* __restrict__ nb_dev,
                                                      unsigned long long* __restrict__ cursor, long long* __restrict__ msg,
-                                                     int kcap, int unpack) {
+                                                     int kcap, int unpack, const int* __restrict__ skip) {
+  if (*skip) return;  // the tree is done: batches a host queued past its end move nothing
   const int nb = min(*nb_dev, kcap);
   const long long nh = (long long)nb * slot_elems;
   const long long ncur = (long long)kcap * kCurStride;
@@ -1047,7 +1053,8 @@ __global__ __launch_bounds__(256) void lw_owner_kernel(long long* __restrict__ h
                                                        const int* __restrict__ nb_dev,
                                                        unsigned long long* __restrict__ cursor,
                                                        const int* __restrict__ k_dev, long long* __restrict__ x,
-                                                       int kcap, int unpack) {
+                                                       int kcap, int unpack, const int* __restrict__ skip) {
+  if (kcap >= 0 && *skip) return;  // RCCL loop: batches queued past the tree's end move nothing
   const int nb = kcap >= 0 ? min(*nb_dev, kcap) : *nb_dev;
   const int ns = kcap >= 0 ? kcap : nb;
   const int kc = kcap >= 0 ? kcap : *k_dev;
@@ -1149,6 +1156,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.split_groups = ip[8] > 0 ? ip[8] : 1;
   p.dist = ip[9];
   p.bin_bytes = ip[10] == 2 ? 2 : 1;
+  p.batch_cap = 0;
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -1206,6 +1214,8 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
 }
 
 void ytk_lw_set_lr(int h, float lr) { g_lw.at(h).p.lr = lr; }
+// splits per batch of the following planner launches (0: no cap)
+void ytk_lw_set_batch_cap(int h, int cap) { g_lw.at(h).p.batch_cap = std::max(0, cap); }
 
 // bytes of the planner workspace a (cap, max_leaf) engine needs (0: the LDS planner fits)
 long long ytk_lw_ws_bytes(int cap, int max_leaf) {
@@ -1280,7 +1290,8 @@ void ytk_lw_msg(int h, uintptr_t hist, long long slot_elems, uintptr_t msg, int 
   const long long n = (long long)kcap * (slot_elems + kCurStride);
   const int grid = (int)std::min<long long>((n + 255) / 256, 256 * 8);
   hipLaunchKernelGGL(lw_msg_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
-                     slot_elems, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor, (long long*)msg, kcap, unpack);
+                     slot_elems, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor, (long long*)msg, kcap, unpack,
+                     e.b.st + LW_DONE);
   YTK_LAUNCH_CHECK();
 }
 
@@ -1295,7 +1306,7 @@ void ytk_lw_owner(int h, uintptr_t hist, long long slot_elems, int B, int F, int
   const int grid = (int)std::min<long long>((n + 255) / 256, 256 * 8);
   hipLaunchKernelGGL(lw_owner_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
                      slot_elems, B, F, fr, P, rank, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor,
-                     e.b.st + LW_N_SPLIT, (long long*)x, kcap, unpack);
+                     e.b.st + LW_N_SPLIT, (long long*)x, kcap, unpack, e.b.st + LW_DONE);
   YTK_LAUNCH_CHECK();
 }
 

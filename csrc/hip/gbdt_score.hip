@@ -837,6 +837,20 @@ static inline int grid_for(long long n, int cap) {
   return (int)std::min<long long>((n + 255) / 256, (long long)cap);
 }
 
+// Virtual blocks (256 rows each per step) of the fused gradient + root histogram pass: at
+// most YTK_TGH_VBLOCKS (default 2048 = 512 physical 1024-thread blocks, two per CU in
+// turn: each holds the 128-KiB root histogram in LDS). Every physical block flushes a
+// 128-KiB partial that the root reduce reads back, so fewer, longer blocks trade row
+// parallelism for flush + reduce bytes (the 1/8 shard runs ~2.5k rows per block).
+static int tgh_vblocks(long long N) {
+  static const int cap = [] {
+    const char* e = getenv("YTK_TGH_VBLOCKS");
+    const int v = e ? atoi(e) : 2048;
+    return std::max(4, std::min(v, 8192)) & ~3;
+  }();
+  return grid_for(N, cap);
+}
+
 extern "C" {
 
 void ytk_tree_add_bins(uintptr_t binsT, int bin_bytes, long long N, uintptr_t tfeat,
@@ -1155,7 +1169,7 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
   if (zero && (zero % 16) != 0) return 0;
   if (zero_n <= 0) zero = 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int nvb = grid_for(N, 256 * 8);  // tree_grad_kernel's grid: the virtual blocks
+  const int nvb = tgh_vblocks(N);  // virtual blocks (tree_grad_kernel's grid by default)
   const int grid = (nvb + kTGHVirtual - 1) / kTGHVirtual;
 #define YTK_TGH(LID)                                                                                          \
   hipLaunchKernelGGL((tree_grad_hist_kernel<LID>), dim3(grid), dim3(kTGHThreads), lds, s, (const uint8_t*)bins,  \
@@ -1186,8 +1200,25 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
   return 1;
 }
 
+// Device -> pinned host bytes as a kernel (16-B stores through the host mapping): the round's
+// snapshot readback inside a captured round graph -- one graph node instead of a blit copy
+// launched by the host after every replay (profiled: ~4 us copy + ~15 us of gaps per round).
+__global__ __launch_bounds__(256) void copy_to_mapped_kernel(const int4* __restrict__ src, int4* __restrict__ dst,
+                                                             long long n16) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) dst[i] = src[i];
+}
+
+void ytk_copy_to_mapped(uintptr_t dst_dev, uintptr_t src, long long nbytes, uintptr_t stream) {
+  if (nbytes <= 0) return;
+  if ((dst_dev | src | (uintptr_t)nbytes) & 15) throw std::invalid_argument("copy_to_mapped: 16-B aligned sizes");
+  const long long n16 = nbytes / 16;
+  hipLaunchKernelGGL(copy_to_mapped_kernel, dim3((unsigned)std::min<long long>((n16 + 255) / 256, 64)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const int4*)src, (int4*)dst_dev, n16);
+  YTK_LAUNCH_CHECK();
+}
+
 // blocks of tree_grad_hist (staging items of its root histogram)
-int ytk_tree_grad_hist_grid(long long N) { return (grid_for(N, 256 * 8) + kTGHVirtual - 1) / kTGHVirtual; }
+int ytk_tree_grad_hist_grid(long long N) { return (tgh_vblocks(N) + kTGHVirtual - 1) / kTGHVirtual; }
 
 // tree_grad launches min(ceil(N / 256), 2048) blocks: the leaf_part scratch size
 int ytk_tree_grad_grid(long long N) { return grid_for(N, 256 * 8); }

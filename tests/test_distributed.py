@@ -176,6 +176,34 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     _same_collective_sequence(tmp_path / f"w{world}", world)
 
 
+@pytest.mark.gpu
+def test_leafwise_rccl_loop_fixed_messages(tmp_path):
+    """The leaf-wise batch loop over the process group (YTK_PEER_REDUCE=0, two ranks on the one
+    GPU over gloo): every batch message has the size of the host's cap schedule
+    min(2^batch, YTK_LW_RCCL_KCAP) x (slot + cursors) -- the host never reads a batch's split
+    count from the device to size its collective (round 4 waited on each batch's planner for
+    it) -- and the model is the world-1 model byte for byte, the capped batches included."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": "allreduce", "YTK_PEER_REDUCE": "0", "YTK_COMM_LOG": "1",
+           "YTK_LW_RCCL_KCAP": "4"}
+    _run("gbdt_loss", tmp_path / "w1", 1, "cuda", extra_env=env)
+    res = _run("gbdt_loss", tmp_path / "w2", 2, "cuda", extra_env=env)
+    assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / "w2" / "model.txt").read()
+    S, cap = res["slot_elems"], res["rccl_kcap"]
+    assert S > 0 and cap == 4
+    sched = [min(cap, 1 << i) * (S + 16) for i in range(64)]  # CUR_STRIDE 16 words per split
+    log = json.load(open(tmp_path / "w2" / "comm_log_0.json"))
+    sizes = [n for op, dt, n in log if op == "allreduce_sum" and dt == "torch.int64" and n >= S]
+    roots = [i for i, n in enumerate(sizes) if n == S]  # each tree's root slot message
+    assert len(roots) >= 6
+    for a, b in zip(roots, roots[1:] + [len(sizes)]):
+        batch = sizes[a + 1:b]
+        assert batch and batch == sched[:len(batch)], batch[:8]
+    _same_collective_sequence(tmp_path / "w2", 2)
+
+
 @pytest.mark.parametrize("task,mode", [("gbdt", "allreduce"), ("gbdt_loss", "owner")])
 def test_forced_dist_world1_gloo(tmp_path, task, mode):
     """YTK_FORCE_DIST=1 at world 1 takes every multi-rank code path (collectives issued to a

@@ -149,8 +149,9 @@ def test_cpu_step_is_synchronous_per_sample_sum(name, avg):
 def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
     """Three batches through the GPU column-ordered step vs the CPU synchronous step (fp32
     sums in different orders: rtol 1e-4; bf16: the forward reads the rounded copy on both)."""
-    mc = _model(name, uneven=uneven)
-    mg = _model(name, dev="cuda", uneven=uneven)
+    nf = 8  # the streamed FFM pair kernel needs >= 8 positions per row (ops/ffm._fixed_layout)
+    mc = _model(name, nf=nf, feats=320, uneven=uneven)
+    mg = _model(name, nf=nf, feats=320, dev="cuda", uneven=uneven)
     oc, og = _opt(mc, avg=avg, dtype=dtype), _opt(mg, avg=avg, dtype=dtype)
     wc, wg = mc.w.clone(), mg.w.clone()
     oc._sync_copy(wc)

@@ -184,7 +184,8 @@ class DeviceLevelBuilder:
         # [train loss, weight | test loss, weight | leaf counts] (round_vector): one readback copy
         snap_total = sum(self._snap_sizes)
         self.rv_off = (snap_total + 15) // 16 * 16
-        self._snap_full = torch.zeros(self.rv_off + 8 * (4 + mn), dtype=torch.uint8, device=dev)
+        # (+ 16 B: the in-graph readback copies whole 16-B units)
+        self._snap_full = torch.zeros(self.rv_off + 8 * (4 + mn) + 16, dtype=torch.uint8, device=dev)
         self.snap = self._snap_full[:snap_total]
         (self.st, self.nodes, self.tfeat, self.tthr, self.tleft, self.tright,
          self.tval) = self._snap_views(self.snap)

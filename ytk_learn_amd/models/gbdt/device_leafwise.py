@@ -477,45 +477,70 @@ class DeviceLeafBuilder:
             idle()
         return self._finish(h, s, it)
 
+    # RCCL batch loop: splits per batch capped at min(2^batch, YTK_LW_RCCL_KCAP) -- a
+    # schedule every rank knows without reading the device, so each batch's message is a
+    # fixed-size collective the host can issue ahead like the peer loop
+    RCCL_KCAP = int(os.environ.get("YTK_LW_RCCL_KCAP", 32))
+
+    def _rccl_cap(self, it: int) -> int:
+        return max(1, min(self.RCCL_KCAP, min(self.max_leaf, LW_LEAF_MAX), 1 << min(it, 20)))
+
     def _build_dist(self, h, hd, rows0, gh0, fmask, f0, s) -> int:
-        """Multi-GPU batch loop: plan -> partition (+ children planning) -> histograms are
-        enqueued; the host then waits for THIS batch's planner (pinned progress words, no
-        event) to learn its split count k, packs the built slots + split cursors into one
-        message (device pack), all-reduces it (one fixed-size collective per batch), unpacks
-        and runs the split search. Every rank's planner takes identical decisions from the
-        identical all-reduced histograms; the next planner patches the children's global
-        row counts from the reduced cursors."""
+        """Multi-GPU batch loop over RCCL (the peer path off or voted down): plan -> partition
+        (+ children planning) -> histograms -> one fixed-size all-reduce of the batch's built
+        slots + split cursors (device pack / unpack; the planner caps the batch at the
+        message's split capacity, a host schedule identical on every rank) -> split search.
+        The host never waits for a batch's planner (round 4 spun on each one to learn its
+        split count): it queues up to POLL_LAG batches ahead and stops at the done flag, and
+        at the end of the tree the ranks agree on the number of batches issued (one host
+        scalar all-reduce) -- the ones past the tree's end are no-ops on the device, but their
+        collectives must pair up. Every rank's planner takes identical decisions from the
+        identical all-reduced histograms (reference shape: DataParallelTreeMaker.java:229-295)."""
         dh = self._dh_np
         idle = self.idle_hook
         it = 0
-        while True:
+
+        def one(it):
+            kc = self._rccl_cap(it)
+            h.lw_set_batch_cap(hd, kc)
             h.lw_step(hd, 1, s)
             h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows0 if it == 0 else ptr(self.rows2),
                            gh0 if it == 0 else ptr(self.gh2), ptr(self.rows2), ptr(self.gh2), self.max_pblocks, s)
             self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
+            if self.owner:
+                self._owner_sync(h, hd, s, kcap=kc)
+            else:
+                n = kc * (self.slot_elems + CUR_STRIDE)
+                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), kc, 0, s)
+                self.comm.allreduce_(self.msg[:n])
+                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), kc, 1, s)
+            self._split(h, fmask, f0, s)
+
+        while True:
+            one(it)
             it += 1
             if it > 4 * self.max_leaf + 8:
                 raise RuntimeError("device leaf-wise builder did not terminate")
-            if dh[1] < it and dh[0] == 0:
-                if idle is not None:
-                    idle()
-                    idle = None
-                t_wait = time.perf_counter()
-                while dh[1] < it and dh[0] == 0:
-                    if time.perf_counter() - t_wait > self.POLL_TIMEOUT_S:
-                        raise RuntimeError(f"device leaf-wise builder: no planner progress for {self.POLL_TIMEOUT_S} s "
-                                           f"(batch {it}, planned {int(dh[1])})")
-            if dh[1] < it:  # this planner found nothing to split: the tree is complete
+            if dh[0] != 0:
                 break
-            k = int(dh[2])
-            if self.owner:
-                self._owner_sync(h, hd, s, kcap=k)
-            else:
-                n = k * (self.slot_elems + CUR_STRIDE)
-                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 0, s)
-                self._allreduce(self.msg[:n])
-                h.lw_msg(hd, ptr(self.hist), self.slot_elems, ptr(self.msg), k, 1, s)
-            self._split(h, fmask, f0, s)
+            if dh[1] >= it - self.POLL_LAG:
+                continue
+            if idle is not None:
+                idle()
+                idle = None
+            t_wait = time.perf_counter()
+            while dh[0] == 0 and dh[1] < it - self.POLL_LAG:
+                if time.perf_counter() - t_wait > self.POLL_TIMEOUT_S:
+                    raise RuntimeError(f"device leaf-wise builder: no planner progress for {self.POLL_TIMEOUT_S} s "
+                                       f"(batch {it}, planned {int(dh[1])})")
+            if dh[0] != 0:
+                break
+        # every rank issues the same collectives: pad to the largest batch count issued
+        it_all = int(self.comm.allreduce_scalars([it], op="max")[0])
+        while it < it_all:
+            one(it)
+            it += 1
+        h.lw_set_batch_cap(hd, 0)
         if idle is not None:
             idle()
         return it

@@ -25,6 +25,7 @@ import torch
 from ...losses import create_loss
 from ...metrics.evaluators import EvalSet
 from ...ops import gbdt as gops
+from ...ops._ext import hip
 from ...parallel.comm import Comm
 from ...utils.javafmt import java_double_str as jd
 from ...utils.fault import fault_point
@@ -110,6 +111,7 @@ class GBDTTrainer:
         self._round_stats = {}      # round -> phase times of THAT round (for the metric sink)
         self._names_arr = None
         self._graphs = None         # captured rounds (see _graph_round)
+        self._graph_hosts = set()   # pinned readback buffers owned by captured graphs
         self._rb_dev = None         # the round's [train | test | leaf counts] vector (see _step_dev)
         self._eager_rounds = 0
 
@@ -183,13 +185,17 @@ class GBDTTrainer:
             self.builder = DeviceLeafBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
                                              timer=self.timer)
             # the builder waits on its planner while a tree grows: land the previous rounds
-            # (tree conversion, loss log) in that wait instead of between trees
-            # One GPU only: landing a round can run the eval metrics' collectives (distributed
-            # AUC), and ranks reach this wait at different batches of their trees -- a rank
-            # blocked in a host collective here would wait on a peer whose GPU waits on this
-            # rank's not-yet-enqueued batch exchange
+            # (tree conversion, loss log) in that wait instead of between trees (multi-GPU:
+            # the host gap between trees cost +9 % per leaf-wise tree at the 1/8 shard,
+            # profiles/r5). Landing a round that logs eval metrics runs their collectives
+            # (distributed AUC), and ranks reach this wait at different batches of their trees
+            # -- a rank blocked in a host collective here would wait on a peer whose GPU waits
+            # on this rank's not-yet-enqueued batch exchange -- so on several ranks the hook
+            # stops before such a round (run_round lands it after the tree)
             if not self.comm.is_dist:
                 self.builder.idle_hook = lambda: self._drain(0)
+            else:
+                self.builder.idle_hook = lambda: self._drain(0, collective_free=True)
             self.builder.snapshot_copy = self.K != 1
             self._fuse_root_pending = True
         elif self.use_device_builder:
@@ -484,9 +490,19 @@ class GBDTTrainer:
             ev.record(torch.cuda.current_stream(self.dev))
         self._inflight.append((i, dev_trees, host, ev, has_te, nlc, None))
 
-    def _drain(self, lag: int = 0):
-        """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log."""
+    def _lands_with_collectives(self, i: int) -> bool:
+        """Landing round i logs eval metrics of the current predictions (watch_train /
+        watch_test on a logged round): their evaluators all-reduce across ranks."""
+        logs = self.p.verbose or self.log.enabled_for_round(i)
+        return bool(logs and (self.p.watch_train or self.p.watch_test) and i + 1 == self.rounds_done)
+
+    def _drain(self, lag: int = 0, collective_free: bool = False):
+        """Land every in-flight round but the newest ``lag``: trees -> model, losses -> log.
+        ``collective_free``: stop before a round whose landing runs collectives."""
         while len(self._inflight) > lag:
+            if (collective_free and self.comm.is_dist
+                    and self._lands_with_collectives(self._inflight[0][0])):
+                return
             i, dev_trees, host, ev, has_te, nlc, rv_off = self._inflight.popleft()
             if ev is not None:
                 ev.synchronize()
@@ -518,7 +534,8 @@ class GBDTTrainer:
                 off += sz
             trl = float(a[0]) / max(self.train_wsum, 1e-300)
             tel = float(a[2]) / max(self.te_wsum, 1e-300) if has_te else None
-            self._rb_free.append(host)
+            if host.data_ptr() not in self._graph_hosts:  # graph-owned buffers stay with their graph
+                self._rb_free.append(host)
             self.round_losses[i] = (trl, tel)
             self._log_round(i, trl, tel, current=(i + 1 == self.rounds_done))
 
@@ -617,23 +634,36 @@ class GBDTTrainer:
             graphs, pool, err = [], None, None
             stats0 = dict(self.comm.stats)
             log0 = len(self.comm.log) if self.comm.log is not None else 0
+            # in-graph readback (YTK_GRAPH_READBACK=1): each graph ends with a copy kernel of
+            # [snapshot | round vector] into ITS OWN pinned buffer (a blit copy launched by the
+            # host after every replay cost ~4 us + ~15 us of gaps per round): four graphs, two
+            # per ping-pong parity, so a buffer is rewritten only after its round has landed
+            # (_bound_inflight keeps at most 4 rounds in flight)
+            ngraph = 4 if os.environ.get("YTK_GRAPH_READBACK", "1") != "0" else 2
             try:
-                for _ in range(2):
+                for j in range(ngraph):
                     g = torch.cuda.CUDAGraph()
                     c0 = dict(self.comm.stats)
                     fault = os.environ.get("YTK_FAULT_CAPTURE")  # fault injection (tests): vote + eager fallback
+                    # the graph's pinned readback buffer, allocated outside the capture
+                    sf = getattr(self.builder, "_snap_full", None)
+                    host_j = None
+                    if ngraph == 4 and sf is not None:
+                        host_j = torch.empty(sf.numel(), dtype=torch.uint8).pin_memory()
+                        host_j = (host_j, hip().host_device_ptr(host_j.data_ptr()))
                     with torch.cuda.graph(g, pool=pool):
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
                         if fault == "2":  # inside the capture: the round's launches half recorded
                             raise RuntimeError("injected failure inside the capture")
                         accs, nlc = self._readback_accs(dev_trees, acc, acc_te)
+                        host_j = self._graph_readback(dev_trees, accs, host_j) if host_j is not None else None
                     assert not host_trees
                     if fault == "1":  # after a complete capture
                         raise RuntimeError("injected capture failure")
                     pool = g.pool()
                     # the collectives a replay issues (captured once, counted per replay)
                     coll = {k: self.comm.stats[k] - c0.get(k, 0) for k in self.comm.stats}
-                    graphs.append((g, dev_trees, acc, acc_te, accs, nlc, coll))
+                    graphs.append((g, dev_trees, acc, acc_te, accs, nlc, coll, host_j))
             except Exception as e:
                 err = e
             if self.comm.is_dist:
@@ -655,15 +685,37 @@ class GBDTTrainer:
             self._graphs = {"g": graphs, "n": 0}
         st = self._graphs
         self._bound_inflight()
-        g, dev_trees, acc, acc_te, accs, nlc, coll = st["g"][st["n"] & 1]
+        gs = st["g"]
+        g, dev_trees, acc, acc_te, accs, nlc, coll, host_j = gs[st["n"] % len(gs)]
         g.replay()
         st["n"] += 1
         for k, v in coll.items():
             self.comm.stats[k] = self.comm.stats.get(k, 0) + v
         self._acc = (acc, acc_te)
         self.rounds_done = i + 1
-        self._readback_copy(i, dev_trees, accs, acc_te is not None, nlc)
+        if host_j is not None:  # the graph copied the round into host_j: an event only
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self._inflight.append((i, dev_trees, host_j, ev, acc_te is not None, nlc, dev_trees[0].rv_off))
+        else:
+            self._readback_copy(i, dev_trees, accs, acc_te is not None, nlc)
         return True
+
+    def _graph_readback(self, dev_trees, accs, host_buf):
+        """(Inside a round capture) copy kernel of [snapshot | pad | round vector] into the
+        graph's pinned buffer (host_buf = (tensor, device address)); None when the round has no
+        such contiguous view (the host-launched copy then follows every replay)."""
+        host, dptr = host_buf
+        dt0 = dev_trees[0] if len(dev_trees) == 1 else None
+        rv_off = getattr(dt0, "rv_off", None)
+        if rv_off is None or accs.data_ptr() != dt0.snap.data_ptr() + rv_off:
+            return None
+        nb = (rv_off + 8 * accs.numel() + 15) // 16 * 16
+        if nb > min(dt0.snap_full.numel(), host.numel()):
+            return None
+        self._graph_hosts.add(host.data_ptr())
+        hip().copy_to_mapped(dptr, dt0.snap_full.data_ptr(), nb, torch.cuda.current_stream(self.dev).cuda_stream)
+        return host
 
     def _graph_release(self):
         """Leave graph mode (an eager round follows): after an odd number of replays the

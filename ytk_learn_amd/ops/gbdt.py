@@ -661,7 +661,10 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
         part = None
         if leaf_counts is not None:
             assert nn > 0 and leaf_counts.dtype == torch.float64 and leaf_counts.numel() >= nn
-            part = torch.empty(hip().tree_grad_grid(N) * nn, dtype=torch.int32, device=score.device)
+            # rows per (virtual block, node): the fused pass may run more virtual blocks
+            # (YTK_TGH_VBLOCKS) than the plain gradient kernel
+            nvb = max(hip().tree_grad_grid(N), 4 * hip().tree_grad_hist_grid(N))
+            part = torch.empty(nvb * nn, dtype=torch.int32, device=score.device)
         if root is not None:
             root["done"] = False
             if (tree_arrays is not None and want_grad and bins.dtype == torch.uint8 and bins.stride(0) == 32

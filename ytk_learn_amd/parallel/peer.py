@@ -34,6 +34,11 @@ from ..utils.fault import fault_point
 from .comm import Comm
 
 
+# outcome of the last peer-group creation on this process (bench / diagnostics):
+# {"state": "off" | "ok" | "rccl", "reason": why the ranks voted for RCCL}
+LAST_STATUS = {"state": "off", "reason": ""}
+
+
 def enabled(comm: Comm) -> bool:
     mode = os.environ.get("YTK_PEER_REDUCE", "auto")
     if mode == "0" or not (comm.is_dist and comm.device.type == "cuda") or comm.world > 16:
@@ -48,6 +53,7 @@ def make(comm: Comm, cap_elems: int) -> Optional["PeerReduce"]:
     """A peer group for messages of up to ``cap_elems`` words, or None (RCCL) when the peer
     path is off or any rank failed to create / open its handles (all-rank vote)."""
     if not enabled(comm):
+        LAST_STATUS.update(state="off", reason="YTK_PEER_REDUCE=0, not one node, or not a GPU job")
         return None
     return PeerReduce.create(comm, cap_elems)
 
@@ -112,13 +118,15 @@ class PeerReduce:
                 ok, err = 0.0, e
             agreed = comm.allreduce_scalars([ok], op="min")[0] > 0.5
             if agreed:
+                LAST_STATUS.update(state="ok", reason="")
                 return pr
         if hnd is not None:
             torch.cuda.synchronize(comm.device)
             comm.barrier()
             h.peer_destroy(hnd)
+        why = f"{type(err).__name__}: {err}" if err is not None else "another rank could not use its peers"
+        LAST_STATUS.update(state="rccl", reason=why[:300])
         if comm.is_master:
-            why = f"{type(err).__name__}: {err}" if err is not None else "another rank could not use its peers"
             print(f"[ytk] peer-memory exchange unavailable ({why}); histogram messages use RCCL", flush=True)
         return None
 
@@ -224,6 +232,14 @@ class PeerReduce:
         hip().peer_allreduce_slots(self.hnd, ptr(hist), slot_elems, ids, nb_dev, ptr(cursor), k_dev, cur_stride,
                                    skip_dev, self.TIMEOUT_S, stream(hist))
         self._account(hist, 0, skippable=True)
+
+    def timing(self):
+        """(exchanges that ran, their summed device wall time in us) since the group was made
+        (the self-test's five included; synchronous read -- diagnostics)."""
+        out = np.zeros(2, np.float64)
+        if self.hnd is not None:
+            hip().peer_timing(self.hnd, out.ctypes.data)
+        return int(out[0]), float(out[1])
 
     def check(self):
         v = hip().peer_check(self.hnd) if self.hnd is not None else 0
