@@ -239,6 +239,10 @@ def run(a, comm):
             "hist_sync": (("owner" if getattr(tr_builder, "owner", False) else "allreduce")
                           if comm.is_dist else "none"),
             "hist_transport": transport,
+            # half-level exchange / all-reduce overlapped with the other half's build
+            "overlap": bool(getattr(tr_builder, "peer_overlap", False)
+                            or (getattr(tr_builder, "overlap", False) and comm.is_dist
+                                and getattr(tr_builder, "peer", None) is None)),
             "graph_replays": replays,
             "trees_converted": total_rounds,
             # multi-GPU diagnostics: the start-up self-test of the peer-memory path (on a vote

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
       if (valid[j]) {
         left[j] = flags[pos] != 0;
         r[j] = rows ? rows[pos] : pos;
-        g[j] = ghp[pos];
+        if (ghp) g[j] = ghp[pos];
       }
     }
     int lrank[kPartSub], vrank[kPartSub];
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_scatter_kernel(
         if (left[j]) dst = lbase + pl[j] + lrank[j];
         else dst = rbase + (pv[j] - pl[j]) + (vrank[j] - lrank[j]);
         rows_out[dst] = r[j];
-        gh_out[dst] = g[j];
+        if (gh_out) gh_out[dst] = g[j];
       }
     }
     lbase += tl;

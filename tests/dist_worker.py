@@ -50,6 +50,7 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
         peer.check()
     peer_calls = peer.calls if peer is not None else 0
     slot_elems = int(getattr(tr.builder, "slot_elems", 0) or 0)
+    peer_overlap = bool(getattr(tr.builder, "peer_overlap", False))
     rccl_kcap = int(getattr(tr.builder, "RCCL_KCAP", 0) or 0)
     tr.close()
     if comm.log is not None:  # every rank's collective sequence (deadlock-freedom check)
@@ -63,7 +64,8 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
             json.dump({"train_loss": tl, "test_loss": te, "owner": owner, "comm": comm.stats,
                        "backend": backend, "is_dist": comm.is_dist,
                        "graph_replays": tr._graphs["n"] if isinstance(tr._graphs, dict) else 0,
-                       "peer_calls": peer_calls, "slot_elems": slot_elems, "rccl_kcap": rccl_kcap}, f)
+                       "peer_calls": peer_calls, "slot_elems": slot_elems, "rccl_kcap": rccl_kcap,
+                       "peer_overlap": peer_overlap}, f)
 
 
 def write_lines(path, n, seed):

@@ -145,7 +145,8 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
                                              ("gbdt", 2, "peer"), ("gbdt_loss", 2, "peer"), ("gbdt", 3, "peer"),
                                              ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer"), ("gbdt", 2, "peer_owner"),
                                              ("gbdt", 3, "peer_owner"), ("gbdt", 4, "peer_owner"),
-                                             ("gbdt_loss", 2, "peer_owner"), ("gbdt_loss", 3, "peer_owner")])
+                                             ("gbdt_loss", 2, "peer_owner"), ("gbdt_loss", 3, "peer_owner"),
+                                             ("gbdt", 2, "peer_overlap"), ("gbdt", 3, "peer_overlap")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
@@ -161,15 +162,17 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     peer = mode.startswith("peer")
-    sync = {"peer": "allreduce", "peer_owner": "owner"}.get(mode, mode)
+    sync = {"peer": "allreduce", "peer_owner": "owner", "peer_overlap": "allreduce"}.get(mode, mode)
     env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": sync,
            "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if peer else "0",
-           "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}  # small shards: keep the overlap covered
+           "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0",  # small shards: keep the overlap covered
+           "YTK_PEER_OVERLAP": "1" if mode == "peer_overlap" else "0"}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     if peer:
         assert res["peer_calls"] > 0
         assert res["owner"] == (mode == "peer_owner")
+        assert res["peer_overlap"] == (mode == "peer_overlap")
         if task == "gbdt" and world != 3:  # no feature sampling: graph-eligible rounds
             assert res["graph_replays"] > 0
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()

@@ -272,6 +272,23 @@ class DeviceLevelBuilder:
             self.peer = peer_mod.make(self.comm, cap)
             if self.peer is not None:
                 self.overlap = False
+        # peer path + YTK_PEER_OVERLAP=1: levels with >= 8 built slots exchange their first half
+        # on a side stream (a second peer group, a small exchange grid that fits beside the
+        # histogram blocks) while the second half's histograms build; the split waits for both
+        # (BASELINE: histogram exchange overlapped with the next block's build). Off by default:
+        # on one GPU per rank the gain is bounded by the second half's build (~9 us per level at
+        # the 1/8 shard) and it has no multi-GPU measurement yet.
+        self.peer2 = None
+        self.peer_overlap = False
+        if (self.peer is not None and not self.owner and self.staged
+                and os.environ.get("YTK_PEER_OVERLAP", "0") == "1"):
+            half_max = max([1] + [self._half(c) // 2 for c in range(1, D)])
+            if half_max >= 4:
+                self.peer2 = peer_mod.make(self.comm, half_max * slot_elems)
+                if self.peer2 is not None:
+                    hip().peer_set_grid_cap(self.peer2.hnd, int(os.environ.get("YTK_PEER_OVERLAP_GRID", "32")))
+                    self.peer_overlap = True
+                    self._side = torch.cuda.Stream(device=dev)
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
@@ -369,10 +386,13 @@ class DeviceLevelBuilder:
             self.comm.allreduce_(t)
 
     def close(self):
-        """Release the peer-memory group (collective: every rank calls it)."""
+        """Release the peer-memory groups (collective: every rank calls it)."""
         if self.peer is not None:
             self.peer.close()
             self.peer = None
+        if self.peer2 is not None:
+            self.peer2.close()
+            self.peer2 = None
 
     def _owner_reduce(self, base: int, nslots: int, ncs: int = 0):
         """Reduce-scatter slots [base, base + nslots) by feature block (+ the ncs count slots
@@ -495,9 +515,13 @@ class DeviceLevelBuilder:
         # gh_rows: the root partition moves only the row ids and the first gathered level
         # (its histograms and its partition) reads (g, h) by row id from the caller's array:
         # one full (g, h) read + write less per tree (YTK_GH_ROWS=0: moved at the root too)
+        gh_mode = os.environ.get("YTK_GH_ROWS", "2")
         gh_rows = (not sampled and self.fuse_part_children and not self.wide and self.staged and p.max_depth >= 3
-                   and os.environ.get("YTK_GH_ROWS", "1") != "0"
-                   and os.environ.get("YTK_PART_PREFETCH", "2") != "0")
+                   and gh_mode != "0" and os.environ.get("YTK_PART_PREFETCH", "2") != "0")
+        # gh_all (YTK_GH_ROWS=2, default): (g, h) is never moved -- every partition moves the
+        # row ids only (5 B read + 4 B written per row instead of 13 + 12) and every histogram
+        # level gathers (g, h) by row id next to the row's bins (the leaf-wise engine's layout)
+        gh_all = gh_rows and gh_mode == "2"
         # rows / position-ordered (g, h). Without sampling the root level reads the identity
         # permutation and the caller's gh directly; the first partition writes the buffers.
         if sampled:
@@ -621,8 +645,8 @@ class DeviceLevelBuilder:
             rows_in = rows0 if d == 0 else ptr(self.rows)
             gh_in = gh0 if d == 0 else ptr(self.ghp)
             part_gh_rows = 0
-            if gh_rows and d == 0:
-                gh_in = 0  # the root partition moves the row ids only
+            if gh_rows and (d == 0 or gh_all):
+                gh_in = 0  # the partition moves the row ids only
             elif gh_rows and d == 1:
                 gh_in, part_gh_rows = gh0, 1  # (g, h) by row id; this level writes it in position order
             half = self._half(c)
@@ -646,7 +670,7 @@ class DeviceLevelBuilder:
                 # the split cursors are the (zeroed) per-split left counters: low half = left
                 # rows, high half = right rows; the last level only counts
                 h.partition_atomic(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
-                                   gh_in, ptr(self.gh_tmp), ptr(self.part_first), off(3), off(4), npart,
+                                   gh_in, ptr(self.gh_tmp) if gh_in else 0, ptr(self.part_first), off(3), off(4), npart,
                                    ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                                    ptr(self.part_cnt), lloc, 1 if last else 0, 0, s)
             elif last:
@@ -655,7 +679,7 @@ class DeviceLevelBuilder:
                                   ptr(self.part_counts), off(4), lloc, s)
             else:
                 h.partition(ptr(self.binsT), bb, self.binsT.shape[1], rows_in, ptr(self.rows_tmp),
-                            gh_in, ptr(self.gh_tmp), ptr(self.flags), ptr(self.part_items), npart,
+                            gh_in, ptr(self.gh_tmp) if gh_in else 0, ptr(self.flags), ptr(self.part_items), npart,
                             ptr(self.part_feat), ptr(self.part_thr), ptr(self.part_begin),
                             ptr(self.part_first), ptr(self.part_nblk), ptr(self.part_counts), 0, off(4),
                             lloc, s)
@@ -679,8 +703,24 @@ class DeviceLevelBuilder:
             ptrs = self._ptrs()
             nmax = self.hist_target + half + 1
             # the first gathered level reads (g, h) by row id from the caller's array (gh_rows)
-            hgh, hrow = (gh0, 1) if (gh_rows and d == 0) else (ptr(self.ghp), 0)
-            if dist and self.overlap and half >= 8 and self.staged and not self.owner:  # large levels only:
+            hgh, hrow = (gh0, 1) if (gh_rows and (d == 0 or gh_all)) else (ptr(self.ghp), 0)
+            if dist and self.peer_overlap and half >= 8:
+                # first half's exchange on the side stream (second peer group) overlaps the
+                # second half's build; the split search waits for both
+                hs = half // 2
+                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow)
+                main = torch.cuda.current_stream(self.dev)
+                side = self._side
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self.peer2.allreduce_(self.hist[base:base + hs].view(-1))
+                build_hist(hgh, ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
+                           work_off=off(ST_N_HIST_A), by_row=hrow)
+                tm.mark("build_hist_compute")
+                self._hist_allreduce(self.hist[base + hs:base + half + ncs])
+                main.wait_stream(side)
+                tm.mark("build_hist_comm")
+            elif dist and self.overlap and half >= 8 and self.staged and not self.owner:  # large levels only:
                 # small ones are latency bound and a second collective would cost more
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
                 # second half's histogram build; the split search waits for both

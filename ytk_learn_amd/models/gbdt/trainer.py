@@ -506,9 +506,9 @@ class GBDTTrainer:
             i, dev_trees, host, ev, has_te, nlc, rv_off = self._inflight.popleft()
             if ev is not None:
                 ev.synchronize()
-            peer = getattr(self.builder, "peer", None)
-            if peer is not None:  # a timed-out flag wait (lost / stalled peer) fails the job here
-                peer.check()
+            for peer in (getattr(self.builder, "peer", None), getattr(self.builder, "peer2", None)):
+                if peer is not None:  # a timed-out flag wait (lost / stalled peer) fails the job here
+                    peer.check()
             hb = host.numpy()
             head = 32 + 8 * sum(nlc)
             if rv_off is None:  # [vector | snapshots]
@@ -651,7 +651,10 @@ class GBDTTrainer:
                     if ngraph == 4 and sf is not None:
                         host_j = torch.empty(sf.numel(), dtype=torch.uint8).pin_memory()
                         host_j = (host_j, hip().host_device_ptr(host_j.data_ptr()))
-                    with torch.cuda.graph(g, pool=pool):
+                    # thread_local: the process group's watchdog thread may still query the
+                    # events of the eager collectives before the capture (a global-mode
+                    # capture turns those queries into errors and aborts the process)
+                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
                         if fault == "2":  # inside the capture: the round's launches half recorded
                             raise RuntimeError("injected failure inside the capture")

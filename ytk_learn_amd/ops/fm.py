@@ -84,8 +84,8 @@ def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float
     ``bias_latent``); ``upd_w = False`` updates only the bias among the linear weights.
     GPU: lock-free float atomics, concurrent rows race as in Hogwild!. CPU: the same
     per-sample gradients applied as one synchronous mini-batch step.
-    ``Vb`` (bf16 [F, k], optional): working copy the forward read; the gradient uses its
-    values, ``V`` stays the fp32 master and the touched entries of ``Vb`` are re-rounded.
+    ``Vb`` (bf16 [F, k], optional): working copy the forward read (S); the gradient's V terms
+    use the fp32 master ``V``, and ``Vb`` is re-rounded from it after the step.
     ``cnt`` (int32 [F], optional, :func:`sgd_count`): every weight's step is divided by the
     batch's rows containing its feature (per-feature mean of the per-sample gradients)."""
     n = int(indptr.shape[0] - 1)
@@ -98,10 +98,9 @@ def fm_sgd_update(indptr, indices, values, w_lin, V, S, c, lr: float, l2w: float
                             float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0,
                             1 if bias_latent else 0, ptr(Vb), ptr(cnt) if cnt is not None else 0, stream(w_lin))
         return
-    if Vb is not None:  # CPU reference of the bf16 path: gradient from the working copy
-        V_use = Vb.float()
-    else:
-        V_use = V
+    # bf16 path: S came from the forward over the working copy; the V terms of the gradient
+    # use the fp32 master (as sgd_apply_kernel), and the copy is re-rounded after the step
+    V_use = V
     b0, e0 = int(indptr[0]), int(indptr[-1])
     rows = torch.repeat_interleave(torch.arange(n), (indptr[1:] - indptr[:-1]).long())
     idx = indices[b0:e0].long()
