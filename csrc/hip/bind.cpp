@@ -80,6 +80,8 @@ void ytk_ffm_pairs(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintpt
 void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
                       int, int, uintptr_t);
+void ytk_ffm_sgd_grad(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                      uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
 void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                          long long, uintptr_t, int, uintptr_t, long long, int, int, uintptr_t, uintptr_t);
 // fm.hip
@@ -209,6 +211,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("fixed_spmv", &ytk_fixed_spmv);
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
+  m.def("ffm_sgd_grad", &ytk_ffm_sgd_grad);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);
   m.def("dot", &ytk_dot);
   m.def("row_loss", &ytk_row_loss);

@@ -470,6 +470,88 @@ __global__ __launch_bounds__(256) void ffm_grad_stream_kernel(
   }
 }
 
+// SGD batch pair gradient (ops/sgd.py), fixed-layout rows (every row holds the same m ==
+// nfield fields in the same order; each column sits in one position): one group of 8 lanes
+// per CSC chunk of a batch column i (field fa, <= 64 entries: a batch's columns are short,
+// hot ones are split), lane q owning the row positions q, q + 8, ... (< 8 per lane). For
+// every entry (row r, value x_i, coefficient c_r) the lane gathers V[i_q, fa, :] of its
+// positions straight from the model vector ([F][nfield][k]: 16-B aligned k-float slices)
+// and accumulates c_r x_i x_q V[i_q, fa] into its positions' field slots in registers;
+// the group then writes the chunk's [nfield][k] gradient row once. Against the L-BFGS
+// streamed kernel (one wave per column, ~4 entries per column in a 65536-row batch: the
+// per-column latency chain dominated) a wave works 8 columns at once and needs neither the
+// setup-time row expansion nor a transposed copy of V.
+template <int KV, bool kAligned>
+__global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
+    const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
+    const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ chunk_fa,
+    const int* __restrict__ chunk_col, const int* __restrict__ idx, const float* __restrict__ val, int m,
+    const int* __restrict__ lay_field, const float* __restrict__ coef, const float* __restrict__ V, int nfield,
+    float* __restrict__ part) {
+  constexpr int GL = 8, PM = 8, k = 4 * KV, U = 4;
+  const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
+  const int q = threadIdx.x & (GL - 1);
+  if (g >= nch) return;
+  const long long e0 = chunk_beg[g], e1 = chunk_end[g];
+  const int fa = chunk_fa[g], col = chunk_col[g];
+  const long long J = (long long)nfield * k;
+  float4 acc[PM][KV];
+#pragma unroll
+  for (int j = 0; j < PM; ++j)
+#pragma unroll
+    for (int v = 0; v < KV; ++v) acc[j][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (fa >= 0) {
+    const float* vf = V + (long long)fa * k;
+    for (long long eb = e0; eb < e1; eb += U) {
+      int r[U];
+      float sc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // U entries' row ids / scales in flight
+        const long long e = eb + u;
+        r[u] = e < e1 ? csc_rows[e] : -1;
+        sc[u] = e < e1 ? csc_vals[e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) sc[u] = r[u] >= 0 ? sc[u] * coef[r[u]] : 0.f;
+      int iq[U][PM];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < PM; ++j) {
+          const int p = q + GL * j;
+          iq[u][j] = (r[u] >= 0 && p < m) ? idx[(long long)r[u] * m + p] : col;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < PM; ++j) {
+          if (iq[u][j] == col || iq[u][j] < 0) continue;  // the entry itself / a skipped feature
+          const float s = val ? sc[u] * val[(long long)r[u] * m + q + GL * j] : sc[u];
+          const float* vrow = vf + (long long)iq[u][j] * J;
+#pragma unroll
+          for (int v = 0; v < KV; ++v) {
+            // V sits behind the F linear weights in the model vector: 16-B aligned iff F % 4 == 0
+            const float4 x = kAligned ? reinterpret_cast<const float4*>(vrow)[v]
+                                      : make_float4(vrow[4 * v], vrow[4 * v + 1], vrow[4 * v + 2], vrow[4 * v + 3]);
+            acc[j][v].x += s * x.x;
+            acc[j][v].y += s * x.y;
+            acc[j][v].z += s * x.z;
+            acc[j][v].w += s * x.w;
+          }
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PM; ++j) {
+    const int p = q + GL * j;
+    if (p < m) {
+      float4* out = reinterpret_cast<float4*>(part + g * J + (long long)lay_field[p] * k);
+#pragma unroll
+      for (int v = 0; v < KV; ++v) out[v] = acc[j][v];
+    }
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -566,6 +648,33 @@ void ytk_ffm_grad_stream(uintptr_t wave_chunk, long long nwaves, uintptr_t chunk
   else if (k == 16) YTK_FFM_STREAM(4);
   else throw std::invalid_argument("ffm_grad_stream: k must be 4, 8 or 16");
 #undef YTK_FFM_STREAM
+  YTK_LAUNCH_CHECK();
+}
+
+// SGD batch pair gradient over fixed-layout rows (see ffm_sgd_grad_kernel); idx / val: the
+// batch's CSR entries (rows of m entries; val null for unit values); skipped columns have
+// chunk_fa < 0 (their rows of part are zero).
+void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows, uintptr_t csc_vals,
+                      uintptr_t chunk_fa, uintptr_t chunk_col, uintptr_t idx, uintptr_t val, int m, uintptr_t lay_field,
+                      uintptr_t coef, uintptr_t V, int nfield, int k, uintptr_t part, uintptr_t stream) {
+  if (nch <= 0) return;
+  if (m < 1 || m > 64 || m != nfield) throw std::invalid_argument("ffm_sgd_grad: need 1 <= m == nfield <= 64");
+  if ((V & 3) || (part & 15)) throw std::invalid_argument("ffm_sgd_grad: V 4-B / part 16-B aligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((nch * 8 + 255) / 256));
+  const bool al = (V & 15) == 0;
+#define YTK_FFM_SGD(KV)                                                                                     \
+  if (al) YTK_FFM_SGD2(KV, true); else YTK_FFM_SGD2(KV, false)
+#define YTK_FFM_SGD2(KV, AL)                                                                                \
+  hipLaunchKernelGGL((ffm_sgd_grad_kernel<KV, AL>), grid, dim3(256), 0, s, (const long long*)chunk_beg,     \
+                     (const long long*)chunk_end, nch, (const int*)csc_rows, (const float*)csc_vals,        \
+                     (const int*)chunk_fa, (const int*)chunk_col, (const int*)idx, (const float*)val, m,    \
+                     (const int*)lay_field, (const float*)coef, (const float*)V, nfield, (float*)part)
+  if (k == 4) YTK_FFM_SGD(1);
+  else if (k == 8) YTK_FFM_SGD(2);
+  else throw std::invalid_argument("ffm_sgd_grad: k must be 4 or 8");
+#undef YTK_FFM_SGD
+#undef YTK_FFM_SGD2
   YTK_LAUNCH_CHECK();
 }
 

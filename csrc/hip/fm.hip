@@ -238,8 +238,17 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(
   const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
   const bool is_bias = i == reg_skip;
   const int lin_col = lat ? 0 : k;  // FFM: part = [sum c x | sum c x^2]
+  // chunk partials in chunk order, four loads in flight (a hot column has ~N / 64 chunks)
   float glin = 0.f, gsq = 0.f;
-  for (long long c = c0; c < c1; ++c) {
+  long long c = c0;
+  for (; c + 4 <= c1; c += 4) {
+    float a[4], q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { a[u] = part[(c + u) * ldp + lin_col]; q[u] = part[(c + u) * ldp + lin_col + 1]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { glin += a[u]; gsq += q[u]; }
+  }
+  for (; c < c1; ++c) {
     glin += part[c * ldp + lin_col];
     gsq += part[c * ldp + lin_col + 1];
   }
@@ -253,12 +262,18 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(
     float g = 0.f;
     const long long o = (long long)i * J + j;
     const float v = V[o];
-    if (lat) {
-      for (long long c = c0; c < c1; ++c) g += lat[c * J + j];
-    } else {
-      for (long long c = c0; c < c1; ++c) g += part[c * ldp + j];
-      g -= v * gsq;
+    const float* src = lat ? lat + j : part + j;
+    const long long ld = lat ? J : ldp;
+    long long c = c0;
+    for (; c + 4 <= c1; c += 4) {
+      float a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = src[(c + u) * ld];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g += a[u];
     }
+    for (; c < c1; ++c) g += src[c * ld];
+    if (!lat) g -= v * gsq;
     const float nv = v - lri * (g + dec * v);
     V[o] = nv;
     if (Vb) Vb[o] = __float2bfloat16(nv);

@@ -838,14 +838,15 @@ static inline int grid_for(long long n, int cap) {
 }
 
 // Virtual blocks (256 rows each per step) of the fused gradient + root histogram pass: at
-// most YTK_TGH_VBLOCKS (default 2048 = 512 physical 1024-thread blocks, two per CU in
-// turn: each holds the 128-KiB root histogram in LDS). Every physical block flushes a
-// 128-KiB partial that the root reduce reads back, so fewer, longer blocks trade row
-// parallelism for flush + reduce bytes (the 1/8 shard runs ~2.5k rows per block).
+// most YTK_TGH_VBLOCKS (default 1024 = 256 physical 1024-thread blocks, one per CU: each
+// holds the 128-KiB root histogram in LDS). Every physical block flushes a 128-KiB partial
+// that the root reduce reads back, so fewer, longer blocks trade row parallelism for flush +
+// reduce bytes. Measured (profiles/r5/chk4_*_vb*): 2048 -> 1024 virtual blocks 1.333 ->
+// 1.315 ms per full tree, 0.433 -> 0.418 ms at the 1/8 shard; 512: 1.508 / 0.437.
 static int tgh_vblocks(long long N) {
   static const int cap = [] {
     const char* e = getenv("YTK_TGH_VBLOCKS");
-    const int v = e ? atoi(e) : 2048;
+    const int v = e ? atoi(e) : 1024;
     return std::max(4, std::min(v, 8192)) & ~3;
   }();
   return grid_for(N, cap);

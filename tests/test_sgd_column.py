@@ -159,7 +159,7 @@ def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
     bounds = [(0, 512), (512, 1024), (2048, 2560)]
     batches = og._setup(bounds)
     if name == "ffm" and not uneven:
-        assert all(bt.stream_st is not None for bt in batches)  # the streamed pair kernel ran
+        assert all(bt.lay is not None for bt in batches) and og.Vt is None  # ffm_sgd_grad_kernel ran
     for j, (b, e) in enumerate(bounds):
         oc._step(wc, b, e, 0.2)
         og._step(wg, b, e, 0.2, batches[j])

@@ -20,6 +20,10 @@ if has tests; then
     "tests/test_distributed.py::test_rccl_world1_capture_failure_falls_back" > $O/tests.log 2>&1 || { tail -80 $O/tests.log; exit 1; }
   tail -2 $O/tests.log
 fi
+if has sgdtests; then
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_sgd_column.py > $O/sgdtests.log 2>&1 || { tail -80 $O/sgdtests.log; exit 1; }
+  tail -2 $O/sgdtests.log
+fi
 if has tests2; then
   timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
     "tests/test_distributed.py::test_lbfgs_peer_dropped_exchange_raises" "tests/test_distributed.py::test_leafwise_rccl_loop_fixed_messages" \

@@ -31,21 +31,25 @@ from ._ext import check_cuda, hip, ptr, stream
 from .sparse import SparseMatrix
 
 
+SGD_CHUNK = 64  # entries per batch CSC chunk: a batch's hot columns (the bias: every row) are
+#                split so no chunk's serial walk outlasts the rest of the column pass
+
+
 class SGDBatch:
     """One batch's column structure (device tensors)."""
 
-    __slots__ = ("b", "e", "X", "ucol", "ucp", "ucnt", "nu", "stream_st", "fields")
+    __slots__ = ("b", "e", "X", "ucol", "ucp", "ucnt", "nu", "fields", "lay", "chunk_fa", "chunk_col")
 
 
 def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None, nfield: int = 0,
-                  skip_feat: int = -1, unit_values: bool = False, want_stream: bool = False) -> List[SGDBatch]:
+                  skip_feat: int = -1) -> List[SGDBatch]:
     """Set-up of every batch [b, e) of ``bounds`` (rows of ``X``)."""
-    from .ffm import _stream_layout
+    from .ffm import _csc_layout, _fixed_layout
     out = []
     for b, e in bounds:
         o0, o1 = int(X.indptr[b]), int(X.indptr[e])
         ip = (X.indptr[b:e + 1] - o0).contiguous()
-        Xb = SparseMatrix(ip, X.indices[o0:o1], X.values[o0:o1], X.ncols, row_tile=False)
+        Xb = SparseMatrix(ip, X.indices[o0:o1], X.values[o0:o1], X.ncols, row_tile=False, chunk=SGD_CHUNK)
         counts = Xb.colptr[1:] - Xb.colptr[:-1]
         u = torch.nonzero(counts).flatten()
         bt = SGDBatch()
@@ -55,19 +59,25 @@ def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None
         # chunks of consecutive touched features are contiguous (empty columns own none)
         bt.ucp = torch.cat([Xb.chunk_ptr[u], Xb.chunk_ptr[-1:]]).contiguous()
         bt.nu = int(u.numel())
-        bt.fields = None
-        bt.stream_st = None
+        bt.fields = bt.lay = bt.chunk_fa = bt.chunk_col = None
         if fields is not None:
             bt.fields = fields[o0:o1].contiguous()
-            if want_stream:
-                st = _stream_layout(Xb, bt.fields, nfield, skip_feat, unit_values)
-                if st is not None and torch.equal(st["cptr"], Xb.chunk_ptr):
-                    bt.stream_st = st
-        if fields is not None and bt.stream_st is None:
-            from .ffm import _csc_layout
-            _csc_layout(Xb, bt.fields, nfield)  # packed codes of the general pair-gradient kernel
+            fl = _fixed_layout(Xb, bt.fields, nfield) if Xb.n > 0 else None
+            if fl is not None and fl[1] <= 64:
+                # fixed-layout rows: ffm_sgd_grad_kernel (field of each chunk's column; the
+                # skipped feature's chunks marked -1)
+                bt.lay = fl
+                fa = bt.fields[Xb.csc_perm[Xb.chunk_beg]].to(torch.int32)
+                col = Xb.chunk_col.to(torch.int32)
+                if skip_feat >= 0:
+                    fa = torch.where(col == skip_feat, torch.full_like(fa, -1), fa)
+                bt.chunk_fa, bt.chunk_col = fa.contiguous(), col.contiguous()
+                Xb.csc_perm = None
+            else:
+                _csc_layout(Xb, bt.fields, nfield)  # packed codes of the general pair-gradient kernel
         else:
             Xb.csc_perm = None  # only the general FFM kernel reads the entries' CSR positions
+        Xb.chunk_col = None
         Xb.rows_of_nnz = None   # set-up only
         out.append(bt)
     return out
@@ -94,24 +104,24 @@ def column_sums(bt: SGDBatch, c: torch.Tensor, S: Optional[torch.Tensor], k: int
     return part
 
 
-def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, Vt: torch.Tensor, nfield: int, k: int, skip_feat: int) -> torch.Tensor:
-    """lat[chunk, nfield * k] = the chunk's FFM pair gradient (streamed kernel when the batch
-    has the fixed layout, else the general column-ordered kernel)."""
+def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[torch.Tensor], nfield: int, k: int,
+                  skip_feat: int) -> torch.Tensor:
+    """lat[chunk, nfield * k] = the chunk's FFM pair gradient: ffm_sgd_grad_kernel over the
+    model's V ([F][nfield][k]) for fixed-layout batches, else the general column-ordered kernel
+    over the transposed copy Vt ([nfield][F][k])."""
     from .ffm import _csc_layout
     Xb = bt.X
     J = nfield * k
     lat = torch.empty((max(Xb.n_chunks, 1), J), dtype=torch.float32, device=c.device)
     h, s = hip(), stream(c)
-    st = bt.stream_st
-    if st is not None:
-        se = c.index_select(0, st["rows"])
-        if st["vals"] is not None:
-            se.mul_(st["vals"])
-        wc = st["wc"]
-        h.ffm_grad_stream(ptr(wc), wc.numel() - 1, ptr(st["beg"]), ptr(st["end"]), ptr(st["chunk_fa"]),
-                          ptr(st["exp_idx"]), ptr(st["exp_val"]), ptr(se), Xb.nnz, ptr(st["lay_field"]), st["m"],
-                          ptr(Vt), Xb.ncols, nfield, k, ptr(lat), s)
+    if bt.lay is not None and k in (4, 8):
+        lay_field, m = bt.lay
+        h.ffm_sgd_grad(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
+                       ptr(bt.chunk_fa), ptr(bt.chunk_col), ptr(Xb.indices), 0 if Xb.one_hot else ptr(Xb.values), m,
+                       ptr(lay_field), ptr(c), ptr(V), nfield, k, ptr(lat), s)
         return lat
+    if Vt is None:
+        raise RuntimeError("ffm sgd: the general pair-gradient kernel needs the transposed latents")
     lay = _csc_layout(Xb, bt.fields, nfield)
     if lay is None:
         raise RuntimeError("ffm sgd: feature / field codes do not fit 32 bits")
@@ -120,6 +130,11 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, Vt: torch.Tensor, nfield: int, 
                    ptr(Xb.csc_perm), ptr(Xb.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
                    ptr(Vt), Xb.ncols, nfield, k, ptr(c), ptr(lat), int(skip_feat), int(distinct), s)
     return lat
+
+
+def needs_transposed(batches: List[SGDBatch], V: torch.Tensor, k: int) -> bool:
+    """Whether some batch takes the general pair-gradient kernel (which reads Vt)."""
+    return any(bt.lay is None for bt in batches) or k not in (4, 8)
 
 
 def ffm_step_cpu(indptr, idx, val, fld, w_lin, V, nfield: int, k: int, c, lr: float, l2w: float, l2v: float,

@@ -75,9 +75,10 @@ class SparseMatrix:
     """Immutable CSR/CSC pair. ``indptr`` int64 [n+1], ``indices`` int32, ``values`` float32."""
 
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, ncols: int,
-                 build_csc: bool = True, row_tile: bool = True):
+                 build_csc: bool = True, row_tile: bool = True, chunk: int = 0):
         self.device = indices.device
         self.row_tile = row_tile  # False: one column order over all rows (SGD batches, ops/sgd.py)
+        self.chunk = int(chunk) if chunk > 0 else CHUNK  # entries per CSC chunk
         self.n = int(indptr.shape[0] - 1)
         self.ncols = int(ncols)
         self.indptr = indptr.to(torch.int64).contiguous()
@@ -162,14 +163,16 @@ class SparseMatrix:
         colptr[1:] = torch.cumsum(counts, 0)
         self.colptr = colptr
         # chunks: segment s is split into ceil(len/CHUNK) pieces (none when empty)
-        nch = (scounts + CHUNK - 1) // CHUNK
+        C = self.chunk
+        nch = (scounts + C - 1) // C
         cbeg = torch.zeros(scounts.numel() + 1, dtype=torch.int64, device=self.device)
         cbeg[1:] = torch.cumsum(nch, 0)
         total = int(cbeg[-1])
         chunk_seg = torch.repeat_interleave(torch.arange(scounts.numel(), device=self.device), nch)
         within = torch.arange(total, device=self.device) - cbeg[:-1][chunk_seg]
-        self.chunk_beg = (segptr[:-1][chunk_seg] + within * CHUNK).contiguous()
-        self.chunk_end = torch.minimum(self.chunk_beg + CHUNK, segptr[1:][chunk_seg]).contiguous()
+        self.chunk_beg = (segptr[:-1][chunk_seg] + within * C).contiguous()
+        self.chunk_end = torch.minimum(self.chunk_beg + C, segptr[1:][chunk_seg]).contiguous()
+        self.chunk_col = chunk_seg % self.ncols  # column of each chunk
         if tiled:
             chunk_col = chunk_seg % self.ncols
             self.chunk_ids = torch.sort(chunk_col, stable=True).indices.contiguous()  # column-major, tiles in order

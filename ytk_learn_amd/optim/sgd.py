@@ -118,12 +118,11 @@ class SGDOptimizer:
         self.Vb = None
         if sp.dtype == "bf16" and model.name == "fm" and self.kk > 0:
             self.Vb = torch.empty((F, self.kk), dtype=torch.bfloat16, device=dev)
-        # FFM on the GPU: the pair-gradient kernels read the latents field-major ([nfield][F][k],
-        # each XCD's fields an L2-sized working set); sgd_apply keeps this copy current
+        # FFM on the GPU: fixed-layout batches read the model's V directly (ffm_sgd_grad_kernel);
+        # the general pair-gradient kernel reads a field-major copy ([nfield][F][k]) that
+        # sgd_apply keeps current -- allocated only when some batch needs it (_setup)
         self.ffm = model.name == "ffm" and getattr(model, "stride", 0) > 0
         self.Vt = None
-        if self.ffm and dev.type == "cuda":
-            self.Vt = torch.empty((model.nf, F, model.kk), dtype=torch.float32, device=dev)
         self._batches = None
 
     # ------------------------------------------------------------------ one batch
@@ -132,10 +131,10 @@ class SGDOptimizer:
         X = m.X
         if self._batches is None and X.device.type == "cuda":
             fld = m.data.train.fields if self.ffm else None
-            unit = bool(X.one_hot)
-            self._batches = sgd_ops.build_batches(X, bounds, fld, m.nf if self.ffm else 0,
-                                                  getattr(m, "_skip", -1), unit, want_stream=self.ffm
-                                                  and m.kk in (4, 8, 16))
+            self._batches = sgd_ops.build_batches(X, bounds, fld, m.nf if self.ffm else 0, getattr(m, "_skip", -1))
+            if self.ffm and sgd_ops.needs_transposed(self._batches, self.m.w[m.F:], m.kk):
+                self.Vt = torch.empty((m.nf, m.F, m.kk), dtype=torch.float32, device=X.device)
+                self._sync_copy(self.m.w)
         return self._batches
 
     def _step(self, w: torch.Tensor, b: int, e: int, lr: float, bt=None):
@@ -170,7 +169,7 @@ class SGDOptimizer:
         part = sgd_ops.column_sums(bt, c, S if kk > 0 else None, kk)
         avg = sp.average == "feature"
         if self.ffm and getattr(m, "need_second", True):
-            lat = sgd_ops.ffm_pair_sums(bt, c, self.Vt, m.nf, m.kk, m._skip)
+            lat = sgd_ops.ffm_pair_sums(bt, c, w[F:], self.Vt, m.nf, m.kk, m._skip)
             sgd_ops.apply_step(bt, part, lat, m.stride, w_lin, w[F:], m.kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
                                bool(getattr(m, "bias_latent", False)), avg, Vt=self.Vt)
         else:
