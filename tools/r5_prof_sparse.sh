@@ -6,7 +6,9 @@ O=$R/gpurun_out/${1:-psp}
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
-for cfg in ${CFGS:-"fm sgd" "ffm sgd" "gbhsdt lbfgs" "gbmlr lbfgs"}; do
+if [ -n "$CFGS" ]; then LIST="fm:sgd ffm:sgd"; else LIST="fm:sgd ffm:sgd gbhsdt:lbfgs gbmlr:lbfgs"; fi
+for cc in $LIST; do
+  cfg="${cc/:/ }"
   set -- $cfg
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p_$1_$2 -o run -- python3 $R/bench_sparse.py --model $1 --optimizer $2 --rows 4000000 --steps 1 --warmup 1 > $O/p_$1_$2.log 2>&1 || { tail -20 $O/p_$1_$2.log; exit 1; }
   python3 - $O/p_$1_$2/run_kernel_stats.csv <<'PY'
