@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
     const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ chunk_fa,
     const int* __restrict__ chunk_col, const int* __restrict__ idx, const float* __restrict__ val, int m,
     const int* __restrict__ lay_field, const float* __restrict__ coef, const float* __restrict__ V, int nfield,
-    float* __restrict__ part) {
+    float* __restrict__ part, long long vt_nfeat) {
   constexpr int GL = 8, PM = 8, k = 4 * KV, U = 4;
   const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
   const int q = threadIdx.x & (GL - 1);
@@ -501,7 +501,11 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
 #pragma unroll
     for (int v = 0; v < KV; ++v) acc[j][v] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (fa >= 0) {
-    const float* vf = V + (long long)fa * k;
+    // V: the model's [F][nfield][k] (slice fa of row iq at iq * J + fa * k), or with vt_nfeat
+    // > 0 the field-major copy [nfield][F][k] (row iq of slice fa at (fa * F + iq) * k: the
+    // column's gathers then stay inside one 16-MB field slice)
+    const float* vf = vt_nfeat > 0 ? V + (long long)fa * vt_nfeat * k : V + (long long)fa * k;
+    const long long vs = vt_nfeat > 0 ? (long long)k : J;
     for (long long eb = e0; eb < e1; eb += U) {
       int r[U];
       float sc[U];
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
         for (int j = 0; j < PM; ++j) {
           if (iq[u][j] == col || iq[u][j] < 0) continue;  // the entry itself / a skipped feature
           const float s = val ? sc[u] * val[(long long)r[u] * m + q + GL * j] : sc[u];
-          const float* vrow = vf + (long long)iq[u][j] * J;
+          const float* vrow = vf + (long long)iq[u][j] * vs;
 #pragma unroll
           for (int v = 0; v < KV; ++v) {
             // V sits behind the F linear weights in the model vector: 16-B aligned iff F % 4 == 0
@@ -656,7 +660,8 @@ void ytk_ffm_grad_stream(uintptr_t wave_chunk, long long nwaves, uintptr_t chunk
 // chunk_fa < 0 (their rows of part are zero).
 void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows, uintptr_t csc_vals,
                       uintptr_t chunk_fa, uintptr_t chunk_col, uintptr_t idx, uintptr_t val, int m, uintptr_t lay_field,
-                      uintptr_t coef, uintptr_t V, int nfield, int k, uintptr_t part, uintptr_t stream) {
+                      uintptr_t coef, uintptr_t V, int nfield, int k, uintptr_t part, long long vt_nfeat,
+                      uintptr_t stream) {
   if (nch <= 0) return;
   if (m < 1 || m > 64 || m != nfield) throw std::invalid_argument("ffm_sgd_grad: need 1 <= m == nfield <= 64");
   if ((V & 3) || (part & 15)) throw std::invalid_argument("ffm_sgd_grad: V 4-B / part 16-B aligned");
@@ -669,7 +674,7 @@ void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
   hipLaunchKernelGGL((ffm_sgd_grad_kernel<KV, AL>), grid, dim3(256), 0, s, (const long long*)chunk_beg,     \
                      (const long long*)chunk_end, nch, (const int*)csc_rows, (const float*)csc_vals,        \
                      (const int*)chunk_fa, (const int*)chunk_col, (const int*)idx, (const float*)val, m,    \
-                     (const int*)lay_field, (const float*)coef, (const float*)V, nfield, (float*)part)
+                     (const int*)lay_field, (const float*)coef, (const float*)V, nfield, (float*)part, vt_nfeat)
   if (k == 4) YTK_FFM_SGD(1);
   else if (k == 8) YTK_FFM_SGD(2);
   else throw std::invalid_argument("ffm_sgd_grad: k must be 4 or 8");

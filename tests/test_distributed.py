@@ -370,6 +370,9 @@ def test_bench_under_torchrun_world2(tmp_path, mode):
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["steps"] == 2
     assert res["collectives_per_tree"] > 0 and res["collective_bytes_per_tree"] > 0
     assert res["hist_sync"] == mode and res["trees_converted"] == 3
+    # multi-GPU diagnostics carried by every multi-rank line (CPU: no peer-memory path)
+    assert res["peer_selftest"].startswith("off") and res["overlap"] is False
+    assert res["exchanges_per_tree"] == res["collectives_per_tree"] and res["exchange_us_per_tree"] is None
 
 
 def _bench(world, extra_args=(), env_extra=None, timeout=600):

@@ -23,6 +23,7 @@ Per-sample math: ``FMHoagOptimizer.java:127-137``, ``FFMHoagOptimizer.java:149-1
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -31,6 +32,7 @@ from ._ext import check_cuda, hip, ptr, stream
 from .sparse import SparseMatrix
 
 
+FFM_VT = os.environ.get("YTK_SGD_FFM_VT", "0") == "1"
 SGD_CHUNK = 64  # entries per batch CSC chunk: a batch's hot columns (the bias: every row) are
 #                split so no chunk's serial walk outlasts the rest of the column pass
 
@@ -116,9 +118,11 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[t
     h, s = hip(), stream(c)
     if bt.lay is not None and k in (4, 8):
         lay_field, m = bt.lay
+        # YTK_SGD_FFM_VT=1 (with the field-major copy allocated): gather from Vt instead of V
+        src, vt_nfeat = (Vt, Xb.ncols) if (Vt is not None and FFM_VT) else (V, 0)
         h.ffm_sgd_grad(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
                        ptr(bt.chunk_fa), ptr(bt.chunk_col), ptr(Xb.indices), 0 if Xb.one_hot else ptr(Xb.values), m,
-                       ptr(lay_field), ptr(c), ptr(V), nfield, k, ptr(lat), s)
+                       ptr(lay_field), ptr(c), ptr(src), nfield, k, ptr(lat), vt_nfeat, s)
         return lat
     if Vt is None:
         raise RuntimeError("ffm sgd: the general pair-gradient kernel needs the transposed latents")
@@ -134,7 +138,7 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[t
 
 def needs_transposed(batches: List[SGDBatch], V: torch.Tensor, k: int) -> bool:
     """Whether some batch takes the general pair-gradient kernel (which reads Vt)."""
-    return any(bt.lay is None for bt in batches) or k not in (4, 8)
+    return FFM_VT or any(bt.lay is None for bt in batches) or k not in (4, 8)
 
 
 def ffm_step_cpu(indptr, idx, val, fld, w_lin, V, nfield: int, k: int, c, lr: float, l2w: float, l2v: float,
