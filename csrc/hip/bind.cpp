@@ -82,13 +82,18 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
                       int, int, uintptr_t);
 void ytk_ffm_sgd_grad(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, uintptr_t);
+void ytk_ffm_pairs_fwd_e(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int,
+                         uintptr_t, long long, int, uintptr_t);
+void ytk_ffm_sgd_ecol(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                      uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, float,
+                      float, float, int, int, int, int, uintptr_t);
 void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                          long long, uintptr_t, int, uintptr_t, long long, int, int, uintptr_t, uintptr_t);
 // fm.hip
 void ytk_fm_sgd_update(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                        uintptr_t, float, float, float, int, int, int, uintptr_t, uintptr_t, uintptr_t);
 void ytk_sgd_count(uintptr_t, uintptr_t, long long, long long, uintptr_t, int, uintptr_t);
-void ytk_sgd_apply(uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, int, uintptr_t, uintptr_t, int,
+void ytk_sgd_apply(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, int, uintptr_t, uintptr_t, int,
                    uintptr_t, uintptr_t, long long, float, float, float, int, int, int, int, uintptr_t);
 void ytk_fm_forward(uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, int, uintptr_t,
                     uintptr_t, int, uintptr_t);
@@ -157,7 +162,7 @@ void ytk_owner_pack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, in
 void ytk_owner_unpack(uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, uintptr_t);
 // gbdt_hist.hip (device-driven staged histogram)
 void ytk_hist_fx_staged_dev(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t,
-                            int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+                            int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, int);
 }
 
 namespace py = pybind11;
@@ -212,6 +217,8 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("ffm_pairs", &ytk_ffm_pairs);
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("ffm_sgd_grad", &ytk_ffm_sgd_grad);
+  m.def("ffm_pairs_fwd_e", &ytk_ffm_pairs_fwd_e);
+  m.def("ffm_sgd_ecol", &ytk_ffm_sgd_ecol);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);
   m.def("dot", &ytk_dot);
   m.def("row_loss", &ytk_row_loss);

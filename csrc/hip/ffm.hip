@@ -34,6 +34,12 @@ __device__ __forceinline__ float pair_dot(const float* __restrict__ a, const flo
   return s;
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <bool kBackward>
 __global__ __launch_bounds__(256) void ffm_pairs_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
@@ -102,11 +108,24 @@ __global__ __launch_bounds__(256) void ffm_pairs_kernel(
 // generic loop walks p one pair at a time, two dependent 16-B gathers per step, which left
 // the forward latency bound (one wave per row, 39 serial gather round trips: 25 ms per
 // Criteo-shape pass). Same pairs, same per-lane order of the adds.
+//
+// kE (SGD, fixed-layout rows of m <= 64 entries, ops/sgd.py): the kernel also writes the pair
+// terms the batch gradient is made of, E[e_p][q] = x_p x_q V[i_q, f_p, :] for every ordered
+// pair of positions (p, q) of the row (zero for q == p and for pairs with the skipped
+// feature), e_p = the entry's offset from e_base. Both factors of every pair are already in
+// registers for the dot product, so the gradient costs one row write here and one row read
+// per entry in ffm_sgd_ecol_kernel -- instead of a second pass of 16-B gathers scattered over
+// V. Step p's lanes q > p write E[p][q] as one coalesced segment; the transposed terms
+// E[q][p] go to a per-wave LDS triangle first and leave as row segments after the row's last
+// step (written straight from the lanes they were 16-B stores 640 B apart, whose lines were
+// evicted from L2 half written).
 constexpr int kPU = 4;
+template <bool kE>
 __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
     const int* __restrict__ fld, long long nrows, const float* __restrict__ V, int nfield,
-    float* __restrict__ fx, int skip_feat) {
+    float* __restrict__ fx, int skip_feat, float4* __restrict__ E, long long e_base) {
+  extern __shared__ float4 s_tri[];  // kE: [waves][m (m - 1) / 2], entry (q, p < q) at q (q - 1) / 2 + p
   const long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
@@ -119,6 +138,7 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
     int ip = 0, fp = 0;
     float xp = 0.f;
     if (pj < m) { ip = idx[b + pj]; xp = val[b + pj]; fp = fld[b + pj]; }
+    if (kE && pj < m) E[(b - e_base + pj) * m + pj] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int qt = pt; qt < m; qt += 64) {
       const int qj = qt + lane;
       int iq = 0, fq = 0;
@@ -147,7 +167,32 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
         for (int u = 0; u < kPU; ++u)
           if (ok[u])
             acc += (va[u].x * vb[u].x + va[u].y * vb[u].y + va[u].z * vb[u].z + va[u].w * vb[u].w) * xx[u];
+        if (kE) {
+#pragma unroll
+          for (int u = 0; u < kPU; ++u) {
+            const int P = pt + pp0 + u;
+            if (pp0 + u < pend && qj < m && qj > P) {  // every pair slot is written (zero if skipped)
+              const float s = ok[u] ? xx[u] : 0.f;
+              // E[p][q] = x_p x_q V[i_q, f_p]: lanes write consecutive slots of row p
+              E[(b - e_base + P) * m + qj] = make_float4(s * vb[u].x, s * vb[u].y, s * vb[u].z, s * vb[u].w);
+              // E[q][p] = x_p x_q V[i_p, f_q]: into the LDS triangle
+              s_tri[(threadIdx.x >> 6) * (m * (m - 1) / 2) + qj * (qj - 1) / 2 + P] =
+                  make_float4(s * va[u].x, s * va[u].y, s * va[u].z, s * va[u].w);
+            }
+          }
+        }
       }
+    }
+  }
+  if (kE) {  // the transposed terms, row by row: t -> (q, p) with t = q (q - 1) / 2 + p
+    wave_sync();
+    const int ntri = m * (m - 1) / 2;
+    const float4* tri = s_tri + (threadIdx.x >> 6) * ntri;
+    for (int t = lane; t < ntri; t += 64) {
+      int q = (int)(0.5f * (1.f + sqrtf(1.f + 8.f * (float)t)));
+      while (q * (q - 1) / 2 > t) --q;
+      while ((q + 1) * q / 2 <= t) ++q;
+      E[(b - e_base + q) * m + (t - q * (q - 1) / 2)] = tri[t];
     }
   }
 #pragma unroll
@@ -247,12 +292,6 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_bwd_kernel(
 // All LDS traffic is wave-private: wave_sync() orders it.
 constexpr int kCscUnroll = 4;
 constexpr int kCscWaves = 4;
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <bool kVec4, bool kDistinct>
 __global__ __launch_bounds__(256) void ffm_grad_csc_kernel(
@@ -556,6 +595,105 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
   }
 }
 
+// SGD batch step from the forward's pair terms (ffm_pairs_k4_kernel<true>, k == 4,
+// fixed-layout rows): the chunk's pair gradient is sum over its entries e (CSC order:
+// deterministic) of c_{row(e)} * E[perm(e)][q] into field slot f_q, and its linear gradient
+// sum c x. One 32-lane group per chunk, lane q owning positions q and q + 32 (m <= 64); each
+// entry is one contiguous m * 16-B row read, U entries in flight -- the 16-B gathers of V
+// that ffm_sgd_grad_kernel makes are replaced by full-line reads of E.
+// A chunk that is its column's only one (solo[g]: most columns of a batch) applies the step
+// here, exactly as sgd_apply_kernel would from a single chunk (w -= lri (g + cnt l2w w),
+// V -= lri (gV + cnt l2v V), bias rules); the others write lat[g] / lin[g] = (sum c x, 0)
+// for sgd_apply over the multi-chunk columns. chunk_fa < 0 (the skipped column): no latent
+// gradient (zeros).
+__global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
+    const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
+    const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ csc_perm,
+    const int* __restrict__ chunk_fa, const int* __restrict__ chunk_col, const unsigned char* __restrict__ solo,
+    const float4* __restrict__ E, int m, const int* __restrict__ lay_field, const float* __restrict__ coef,
+    float* __restrict__ lat, float* __restrict__ lin, float* __restrict__ w, float* __restrict__ V, float lr,
+    float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
+  constexpr int GL = 32, U = 8;
+  const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
+  const int q = threadIdx.x & (GL - 1);
+  if (g >= nch) return;
+  const long long e0 = chunk_beg[g], e1 = chunk_end[g];
+  const int fa = chunk_fa[g];
+  const bool has0 = q < m, has1 = q + GL < m;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+  float glin = 0.f;
+  // windows of 2 GL entries: their CSR positions, coefficients and values are loaded by the
+  // lanes at once (one round trip) and broadcast; then U entries' E rows are in flight
+  for (long long wb = e0; wb < e1; wb += 2 * GL) {
+    const int n = (int)min<long long>(2 * GL, e1 - wb);
+    int prA = -1, prB = -1;
+    float scA = 0.f, scB = 0.f, xA = 0.f, xB = 0.f;
+    if (q < n) { prA = csc_perm[wb + q]; scA = coef[csc_rows[wb + q]]; xA = csc_vals[wb + q]; }
+    if (q + GL < n) { prB = csc_perm[wb + q + GL]; scB = coef[csc_rows[wb + q + GL]]; xB = csc_vals[wb + q + GL]; }
+    for (int i = 0; i < n; i += U) {
+      int pr[U];
+      float sc[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(i + u, n - 1);  // uniform; the duplicate is masked below
+        const int src = e & (GL - 1);
+        const bool lo = e < GL;
+        pr[u] = __shfl(lo ? prA : prB, src, GL);
+        sc[u] = __shfl(lo ? scA : scB, src, GL);
+        xv[u] = __shfl(lo ? xA : xB, src, GL);
+        if (i + u >= n) { pr[u] = -1; sc[u] = 0.f; xv[u] = 0.f; }
+      }
+      float4 x0[U], x1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (fa >= 0 && pr[u] >= 0) {
+          const float4* row = E + (long long)pr[u] * m;
+          if (has0) x0[u] = row[q];
+          if (has1) x1[u] = row[q + GL];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        glin += sc[u] * xv[u];
+        a0.x += sc[u] * x0[u].x; a0.y += sc[u] * x0[u].y; a0.z += sc[u] * x0[u].z; a0.w += sc[u] * x0[u].w;
+        a1.x += sc[u] * x1[u].x; a1.y += sc[u] * x1[u].y; a1.z += sc[u] * x1[u].z; a1.w += sc[u] * x1[u].w;
+      }
+    }
+  }
+  const long long J4 = m;  // float4 slots per feature (nfield == m, k == 4)
+  if (!solo[g]) {
+    float4* out = reinterpret_cast<float4*>(lat) + g * J4;
+    if (has0) out[lay_field[q]] = a0;
+    if (has1) out[lay_field[q + GL]] = a1;
+    if (q == 0) { lin[2 * g] = glin; lin[2 * g + 1] = 0.f; }
+    return;
+  }
+  const int col = chunk_col[g];
+  const float cnt = (float)(e1 - e0);
+  const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
+  const bool is_bias = col == reg_skip;
+  if (q == 0 && (upd_w || is_bias)) {
+    const float wi = w[col];
+    w[col] = wi - lri * (glin + (is_bias ? 0.f : cnt * l2w * wi));
+  }
+  if (fa < 0 || (is_bias && !bias_latent)) return;
+  const float dec = is_bias ? 0.f : cnt * l2v;
+  float4* vr = reinterpret_cast<float4*>(V) + (long long)col * J4;
+  if (has0) {
+    float4* p = vr + lay_field[q];
+    const float4 v = *p;
+    *p = make_float4(v.x - lri * (a0.x + dec * v.x), v.y - lri * (a0.y + dec * v.y), v.z - lri * (a0.z + dec * v.z),
+                     v.w - lri * (a0.w + dec * v.w));
+  }
+  if (has1) {
+    float4* p = vr + lay_field[q + GL];
+    const float4 v = *p;
+    *p = make_float4(v.x - lri * (a1.x + dec * v.x), v.y - lri * (a1.y + dec * v.y), v.z - lri * (a1.z + dec * v.z),
+                     v.w - lri * (a1.w + dec * v.w));
+  }
+}
+
 }  // namespace ytk
 
 using namespace ytk;
@@ -585,8 +723,9 @@ void ytk_ffm_pairs(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
                        nfield, k, (float*)fx, (const float*)coef, (float*)gV, vec4, skip_feat, (const int*)cnt);
   else if (vec4 && k == 4 && !getenv_off("YTK_FFM_K4"))
-    hipLaunchKernelGGL(ffm_pairs_k4_kernel, grid, dim3(256), 0, s, (const long long*)indptr, (const int*)idx,
-                       (const float*)val, (const int*)fld, nrows, (const float*)V, nfield, (float*)fx, skip_feat);
+    hipLaunchKernelGGL(ffm_pairs_k4_kernel<false>, grid, dim3(256), 0, s, (const long long*)indptr,
+                       (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V, nfield,
+                       (float*)fx, skip_feat, (float4*)nullptr, 0LL);
   else
     hipLaunchKernelGGL(ffm_pairs_kernel<false>, grid, dim3(256), 0, s, (const long long*)indptr,
                        (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float*)V,
@@ -680,6 +819,43 @@ void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
   else throw std::invalid_argument("ffm_sgd_grad: k must be 4 or 8");
 #undef YTK_FFM_SGD
 #undef YTK_FFM_SGD2
+  YTK_LAUNCH_CHECK();
+}
+
+// Forward pair sums of fixed-layout rows (k == 4, V 16-B aligned) that also write the pair
+// terms E[entry - e_base][m] (float4) for ffm_sgd_ecol (see ffm_pairs_k4_kernel).
+void ytk_ffm_pairs_fwd_e(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld, long long nrows,
+                         uintptr_t V, int nfield, uintptr_t fx, int skip_feat, uintptr_t E, long long e_base, int m,
+                         uintptr_t stream) {
+  if (nrows <= 0) return;
+  if ((V & 15) || (E & 15)) throw std::invalid_argument("ffm_pairs_fwd_e: V / E must be 16-B aligned");
+  if (m < 1 || m > 64) throw std::invalid_argument("ffm_pairs_fwd_e: rows of 1..64 entries");
+  const long long threads = nrows * 64;
+  const size_t lds = (size_t)4 * (m * (m - 1) / 2) * sizeof(float4);  // 4 waves per block
+  hipLaunchKernelGGL(ffm_pairs_k4_kernel<true>, dim3((unsigned)((threads + 255) / 256)), dim3(256), lds,
+                     reinterpret_cast<hipStream_t>(stream), (const long long*)indptr, (const int*)idx,
+                     (const float*)val, (const int*)fld, nrows, (const float*)V, nfield, (float*)fx, skip_feat,
+                     (float4*)E, e_base);
+  YTK_LAUNCH_CHECK();
+}
+
+// One SGD batch step's pair gradient + the update of every single-chunk column (see
+// ffm_sgd_ecol_kernel); csc_perm: the batch-relative CSR position of each CSC entry (int32);
+// nfield == m <= 64, k == 4; lat [nch][m * 4] / lin [nch][2]: the multi-chunk columns' partials.
+void ytk_ffm_sgd_ecol(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows, uintptr_t csc_vals,
+                      uintptr_t csc_perm, uintptr_t chunk_fa, uintptr_t chunk_col, uintptr_t solo, uintptr_t E, int m,
+                      uintptr_t lay_field, uintptr_t coef, uintptr_t lat, uintptr_t lin, uintptr_t w, uintptr_t V,
+                      float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg,
+                      uintptr_t stream) {
+  if (nch <= 0) return;
+  if (m < 1 || m > 64) throw std::invalid_argument("ffm_sgd_ecol: need 1 <= m <= 64");
+  if ((E & 15) || (lat & 15) || (V & 15)) throw std::invalid_argument("ffm_sgd_ecol: E / lat / V must be 16-B aligned");
+  hipLaunchKernelGGL(ffm_sgd_ecol_kernel, dim3((unsigned)((nch * 32 + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const long long*)chunk_beg, (const long long*)chunk_end,
+                     nch, (const int*)csc_rows, (const float*)csc_vals, (const int*)csc_perm, (const int*)chunk_fa,
+                     (const int*)chunk_col, (const unsigned char*)solo, (const float4*)E, m, (const int*)lay_field,
+                     (const float*)coef, (float*)lat, (float*)lin, (float*)w, (float*)V, lr, l2w, l2v, reg_skip,
+                     upd_w, bias_latent, avg);
   YTK_LAUNCH_CHECK();
 }
 

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
 // per chunk by fm_backward_kernel (part[c] = [sum c x S_f (f < k) | sum c x | sum c x^2]) and,
 // for FFM, by the streamed pair-gradient kernel (lat[c] = the chunk's [nfield * k] pair
 // gradient). One G-lane group per touched feature u (global id ucol[u], cnt[u] batch
-// entries, chunks [ucp[u], ucp[u + 1])) sums its chunks in chunk order -- deterministic, no
+// entries, chunks [ucb[u], uce[u])) sums its chunks in chunk order -- deterministic, no
 // atomics, no race between the rows of a batch -- and applies the batch step with the
 // weights as the batch read them:
 //   w_i  -= lri * (g_i + cnt_i * l2w * w_i)
@@ -225,15 +225,15 @@ __global__ __launch_bounds__(256) void fm_sgd_update_kernel(
 // read by the FFM backward) are rewritten from the new fp32 values of the touched entries.
 template <int G>
 __global__ __launch_bounds__(256) void sgd_apply_kernel(
-    const int* __restrict__ ucol, const long long* __restrict__ ucp, const int* __restrict__ ucnt, int nu,
-    const float* __restrict__ part, int ldp, const float* __restrict__ lat, int J, float* __restrict__ w,
+    const int* __restrict__ ucol, const long long* __restrict__ ucb, const long long* __restrict__ uce,
+    const int* __restrict__ ucnt, int nu, const float* __restrict__ part, int ldp, const float* __restrict__ lat, int J, float* __restrict__ w,
     float* __restrict__ V, int k, __hip_bfloat16* __restrict__ Vb, float* __restrict__ Vt, long long nfeat,
     float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
   const long long gid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
   const int f = threadIdx.x & (G - 1);
   if (gid >= nu) return;
   const int i = ucol[gid];
-  const long long c0 = ucp[gid], c1 = ucp[gid + 1];
+  const long long c0 = ucb[gid], c1 = uce[gid];
   const float cnt = (float)ucnt[gid];
   const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
   const bool is_bias = i == reg_skip;
@@ -424,8 +424,9 @@ void ytk_fm_sgd_update(uintptr_t indptr, uintptr_t idx, uintptr_t val, long long
 }
 
 // One column-ordered SGD batch step (see sgd_apply_kernel); J latent values per feature
-// (FM: k, gradient folded from part; FFM: nfield * k from lat; 0: linear model).
-void ytk_sgd_apply(uintptr_t ucol, uintptr_t ucp, uintptr_t ucnt, int nu, uintptr_t part, int ldp, uintptr_t lat,
+// (FM: k, gradient folded from part; FFM: nfield * k from lat; 0: linear model). Feature u's
+// chunks are [ucb[u], uce[u]) (the full touched list: ucb = ucp, uce = ucp + 1).
+void ytk_sgd_apply(uintptr_t ucol, uintptr_t ucb, uintptr_t uce, uintptr_t ucnt, int nu, uintptr_t part, int ldp, uintptr_t lat,
                    int J, uintptr_t w, uintptr_t V, int k, uintptr_t Vb, uintptr_t Vt, long long nfeat, float lr,
                    float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg, uintptr_t stream) {
   if (nu <= 0) return;
@@ -437,8 +438,8 @@ void ytk_sgd_apply(uintptr_t ucol, uintptr_t ucp, uintptr_t ucnt, int nu, uintpt
   const dim3 grid((unsigned)((threads + 255) / 256));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define YTK_SGD_A(GG)                                                                                   \
-  hipLaunchKernelGGL(sgd_apply_kernel<GG>, grid, dim3(256), 0, s, (const int*)ucol, (const long long*)ucp, \
-                     (const int*)ucnt, nu, (const float*)part, ldp, (const float*)lat, J, (float*)w,        \
+  hipLaunchKernelGGL(sgd_apply_kernel<GG>, grid, dim3(256), 0, s, (const int*)ucol, (const long long*)ucb, \
+                     (const long long*)uce, (const int*)ucnt, nu, (const float*)part, ldp, (const float*)lat, J, (float*)w,        \
                      (float*)V, k, (__hip_bfloat16*)Vb, (float*)Vt, nfeat, lr, l2w, l2v, reg_skip, upd_w,  \
                      bias_latent, avg)
   switch (G) {

@@ -747,10 +747,12 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
 // the y-extent of the slot reduce). Items with w == 1 are their slot's only item and are
 // stored directly; items with w == 2 (first item of a slot with > kReduceDirect items)
 // zero their slot; slot_ids / slot_range / *nslots_dev list the multi-item slots.
+// gh_rows: ghp is indexed by row id (the leaf-wise engine's row-indexed (g, h)), else by
+// position in rows.
 void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows,
                             uintptr_t work, int max_work, uintptr_t nwork_dev, uintptr_t hist, int B,
                             uintptr_t scales_dev, uintptr_t staging, uintptr_t slot_ids, uintptr_t nslots_dev,
-                            uintptr_t slot_range, int reduce_y, uintptr_t stream) {
+                            uintptr_t slot_range, int reduce_y, uintptr_t stream, int gh_rows) {
   if (max_work <= 0) return;
   const int fw = g_hist_fw;
   const int groups = (F + fw - 1) / fw;
@@ -764,7 +766,7 @@ void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t g
   else
     launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
                           (const int4*)work, (long long*)hist, B, nb_lds, 1.f, 1.f, (const int*)nwork_dev,
-                          (const float*)scales_dev, (long long*)staging, nullptr);
+                          (const float*)scales_dev, (long long*)staging, nullptr, gh_rows);
   YTK_LAUNCH_CHECK();
   const int E = nb_lds * fw;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),

@@ -1264,11 +1264,11 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   }
   // software-pipelined partition body, next chunk's row ids + (g, h) in flight (default:
   // 3.41 -> 3.28-3.35 ms/tree, profiles/r2_partition_chunk.md); YTK_LW_PART_PREFETCH=1: row
-  // ids only (measured slower), 0: unpipelined
+  // ids only (measured slower), 0: unpipelined -- ghp == 0 ((g, h) row-indexed, only row ids move): row ids only
   const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
-  if (prefetch && !(pf && pf[0] == '1'))  // next chunk's (g, h) as well
+  if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
     hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint8_t*)binsT, ncol,
                        (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);

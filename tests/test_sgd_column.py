@@ -17,11 +17,11 @@ from ytk_learn_amd.optim.sgd import SGDOptimizer, SGDParams
 from ytk_learn_amd.utils.logging import YtkLogger
 
 
-def _model(name, n=3000, nf=6, feats=240, k=4, dev="cpu", seed=5, uneven=False):
+def _model(name, n=3000, nf=6, feats=240, k=4, dev="cpu", seed=5, uneven=False, pad=0):
     ip, ix, vv, fl, y = criteo_like(n, nf, feats, seed=seed)
     g = torch.Generator().manual_seed(seed)
     vv = (0.5 + torch.rand(vv.shape, generator=g)).contiguous()
-    F = nf * (feats // nf) + 1
+    F = nf * (feats // nf) + 1 + pad  # pad: unused features (F % 4 == 0 puts V 16-B aligned)
     # bias column 0 in front of every row (as the data loader lays it out)
     m = nf
     ip2 = torch.arange(n + 1, dtype=torch.int64) * (m + 1)
@@ -142,16 +142,19 @@ def test_cpu_step_is_synchronous_per_sample_sum(name, avg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,dtype,uneven", [("linear", "fp32", False), ("fm", "fp32", False),
-                                               ("fm", "bf16", False), ("ffm", "fp32", False),
-                                               ("ffm", "fp32", True), ("fm", "fp32", True)])
+@pytest.mark.parametrize("name,dtype,uneven,pad", [("linear", "fp32", False, 0), ("fm", "fp32", False, 0),
+                                                   ("fm", "bf16", False, 0), ("ffm", "fp32", False, 0),
+                                                   ("ffm", "fp32", False, 3), ("ffm", "fp32", True, 0),
+                                                   ("fm", "fp32", True, 0)])
 @pytest.mark.parametrize("avg", ["feature", "none"])
-def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
+def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, pad, avg):
     """Three batches through the GPU column-ordered step vs the CPU synchronous step (fp32
-    sums in different orders: rtol 1e-4; bf16: the forward reads the rounded copy on both)."""
+    sums in different orders: rtol 1e-4; bf16: the forward reads the rounded copy on both).
+    FFM fixed layout: pad 0 (V unaligned) takes ffm_sgd_grad_kernel, pad 3 (F % 4 == 0) the
+    forward-written pair terms + ffm_sgd_ecol_kernel."""
     nf = 8  # the streamed FFM pair kernel needs >= 8 positions per row (ops/ffm._fixed_layout)
-    mc = _model(name, nf=nf, feats=320, uneven=uneven)
-    mg = _model(name, nf=nf, feats=320, dev="cuda", uneven=uneven)
+    mc = _model(name, nf=nf, feats=320, uneven=uneven, pad=pad)
+    mg = _model(name, nf=nf, feats=320, dev="cuda", uneven=uneven, pad=pad)
     oc, og = _opt(mc, avg=avg, dtype=dtype), _opt(mg, avg=avg, dtype=dtype)
     wc, wg = mc.w.clone(), mg.w.clone()
     oc._sync_copy(wc)
@@ -159,7 +162,8 @@ def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
     bounds = [(0, 512), (512, 1024), (2048, 2560)]
     batches = og._setup(bounds)
     if name == "ffm" and not uneven:
-        assert all(bt.lay is not None for bt in batches) and og.Vt is None  # ffm_sgd_grad_kernel ran
+        assert all(bt.lay is not None for bt in batches) and og.Vt is None  # fixed-layout kernels ran
+        assert (og.E is not None) == (pad == 3)
     for j, (b, e) in enumerate(bounds):
         oc._step(wc, b, e, 0.2)
         og._step(wg, b, e, 0.2, batches[j])
@@ -174,11 +178,13 @@ def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, avg):
 
 
 @pytest.mark.gpu
-def test_gpu_column_step_deterministic(cuda):
-    """No atomics: two runs of the same batches give bitwise identical weights."""
+@pytest.mark.parametrize("nf,pad", [(6, 0), (8, 3)])
+def test_gpu_column_step_deterministic(cuda, nf, pad):
+    """No atomics: two runs of the same batches give bitwise identical weights (general pair
+    kernel; fixed layout with the forward-written pair terms)."""
     outs = []
     for _ in range(2):
-        m = _model("ffm", dev="cuda")
+        m = _model("ffm", dev="cuda", nf=nf, feats=320, pad=pad)
         o = _opt(m)
         w = m.w.clone()
         o._sync_copy(w)

@@ -14,5 +14,5 @@ for eg in 16 0; do
   cat $O/ffm_e$eg.json
 done
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python $R/bench_sparse.py --model ffm --optimizer sgd --rows 4000000 --steps 2 --warmup 1 > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench_sparse.py --model ffm --optimizer sgd --rows 4000000 --steps 2 --warmup 1 > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
 echo "ffme ok"

@@ -139,7 +139,13 @@ class DeviceLeafBuilder:
         self.slot_bytes = B * F * 16
         self.staging = torch.empty(self.hist_bound * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
         self.rows2 = torch.empty(2 * N, dtype=torch.int32, device=dev)
-        self.gh2 = torch.empty((2 * N, 2), dtype=torch.float32, device=dev)
+        # (g, h) stays ROW-indexed through the tree (YTK_LW_GH_ROWS, default on; byte-B bins):
+        # the partition moves row ids only (4 instead of 12 B per row, both ways) and the
+        # histogram gathers (g, h) by row id -- as the level engine's gh_all mode
+        self.gh_rows = os.environ.get("YTK_LW_GH_ROWS", "1") != "0" and not self.wide
+        self._ghr = 0  # the tree's row-indexed (g, h) (build)
+        self.gh2 = (torch.empty((2 * N, 2), dtype=torch.float32, device=dev) if not self.gh_rows
+                    else torch.empty((1, 2), dtype=torch.float32, device=dev))
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
@@ -282,8 +288,20 @@ class DeviceLeafBuilder:
         self._hist(h, rows_ptr, gh_ptr, s)
         self._split(h, fmask, f0, s)
 
+    def _part(self, h, hd, rows_in, gh_in, s):
+        """lw_partition of the current batch into rows2 (+ gh2 unless (g, h) is row-indexed)."""
+        if self._ghr:
+            h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, 0, ptr(self.rows2), 0,
+                           self.max_pblocks, s)
+        else:
+            h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in, ptr(self.rows2), ptr(self.gh2),
+                           self.max_pblocks, s)
+
     def _hist(self, h, rows_ptr, gh_ptr, s):
         st = ptr(self.st)
+        gh_rows = 0
+        if self._ghr and rows_ptr:  # gathered rows: (g, h) by row id
+            gh_ptr, gh_rows = self._ghr, 1
         # sole-item slots are stored by the hist kernel, <= 16-item slots by the reduce, larger
         # ones zeroed by their first hist item and reduced split-K
         if self.wide:
@@ -295,7 +313,7 @@ class DeviceLeafBuilder:
         h.hist_fx_staged_dev(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
                              self.hist_bound, st + 4 * W_N_HIST, ptr(self.hist), self.B, ptr(self.scales),
                              ptr(self.staging), ptr(self.zero_ids), st + 4 * W_N_ZERO, ptr(self.zero_range),
-                             self.REDUCE_Y, s)
+                             self.REDUCE_Y, s, gh_rows)
 
     def _owner_fmask(self, fmask, f0):
         """(owned sampled-feature mask on the device, its first feature, the rank whose block
@@ -388,13 +406,15 @@ class DeviceLeafBuilder:
         sampled = p.instance_sample_rate < 1.0
         dist = self.comm.is_dist
         assert gh.is_contiguous() and gh.shape == (self.N, 2)
+        self._ghr = ptr(gh) if self.gh_rows else 0
         if sampled:  # sampled rows first (stable), in the first half of the ping-pong buffers
             g = torch.Generator(device=self.dev)
             g.manual_seed(seed_rows + self.comm.rank)
             keep = torch.rand(self.N, generator=g, device=self.dev) < p.instance_sample_rate
             _, order = torch.sort((~keep).to(torch.int32), stable=True)
             self.rows2[:self.N].copy_(order.to(torch.int32))
-            self.gh2[:self.N].copy_(gh.index_select(0, order))
+            if not self.gh_rows:
+                self.gh2[:self.N].copy_(gh.index_select(0, order))
             self.root_cnt[0] = keep.sum()
             self.root_cnt[1] = self.root_cnt[0]
             if dist:
@@ -504,8 +524,7 @@ class DeviceLeafBuilder:
             kc = self._rccl_cap(it)
             h.lw_set_batch_cap(hd, kc)
             h.lw_step(hd, 1, s)
-            h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows0 if it == 0 else ptr(self.rows2),
-                           gh0 if it == 0 else ptr(self.gh2), ptr(self.rows2), ptr(self.gh2), self.max_pblocks, s)
+            self._part(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2), s)
             self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
             if self.owner:
                 self._owner_sync(h, hd, s, kcap=kc)
@@ -628,8 +647,7 @@ class DeviceLeafBuilder:
         no-op once the planner has marked the tree done -- every rank takes the same planning
         decisions, so the exchanges pair up however many batches a host queued past the end)."""
         h.lw_step(hd, 1, s)
-        h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in, ptr(self.rows2), ptr(self.gh2),
-                       self.max_pblocks, s)
+        self._part(h, hd, rows_in, gh_in, s)
         if self.peer is None:
             self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
             return

@@ -180,6 +180,14 @@ class GBDTTrainer:
                     and tp.grow_policy == "loss"
                     and fits_pool(DeviceLeafBuilder.slots_needed(tp))
                     and DeviceLeafBuilder.supports(self.bins, self.binsT, self.B, self.F, tp, self.comm))
+        if (self.p.device_builder and self.dev.type == "cuda" and pool_mb is not None and pool_mb > 0
+                and not (self.use_device_builder or use_leaf)):
+            need = level_slots_needed(tp) if tp.grow_policy == "level" else DeviceLeafBuilder.slots_needed(tp)
+            if not fits_pool(need):  # not silent: the capped pool costs the GPU engines
+                self.log.info(f"[GBDT] histogram_pool_capacity {pool_mb:g} MB < the GPU engine's resident "
+                              f"histogram slab ({need} slots x {slot_bytes / (1 << 20):.2f} MB): the tree is "
+                              f"grown by the host-driven builder, whose LRU pool honours the cap (the model is "
+                              f"the same; set histogram_pool_capacity = -1 to keep the GPU engine)")
         if use_leaf:
             self.use_device_builder = True
             self.builder = DeviceLeafBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,

@@ -13,6 +13,14 @@ ranges and entry counts. A step is then
   4. ``sgd_apply_kernel``: every touched feature sums its chunks in order and updates its
      weights once -- w, V (FM / FFM, with l2 decay) and the bf16 / transposed working copies.
 
+FFM with fixed-layout rows and k == 4 (Criteo shape) takes the pair-term path instead of
+steps 3-4: the pair forward also writes E[entry][q] = x_p x_q V[i_q, f_p] for every ordered
+pair of the row (both factors are in registers for the dot product), and one column kernel
+(``ffm_sgd_ecol_kernel``) sums c_row * E rows per chunk -- full-line reads instead of the 16-B
+V gathers of ``ffm_sgd_grad_kernel`` -- and applies the step of every column with a single
+chunk in place; ``sgd_apply`` then runs over the multi-chunk columns only. E costs
+entries x m x 16 B (1.7 GB for a 65536-row, 40-field batch; ``YTK_SGD_FFM_E_GB`` caps it).
+
 Against the per-entry Hogwild! float atomics this replaces (42M atomics per 65536-row FM
 batch, 409M for FFM: ``docs/performance.md``), no two threads ever write one weight, the
 step is deterministic, and the per-feature mean step (``optimization.sgd.average =
@@ -33,6 +41,9 @@ from .sparse import SparseMatrix
 
 
 FFM_VT = os.environ.get("YTK_SGD_FFM_VT", "0") == "1"
+# fixed-layout FFM with k == 4: the forward writes the pair terms E (entries x m x 16 B) and
+# the chunk sums read them back (ffm_sgd_ecol) -- unless E would exceed this many GB
+FFM_E_GB = float(os.environ.get("YTK_SGD_FFM_E_GB", 16))
 SGD_CHUNK = 64  # entries per batch CSC chunk: a batch's hot columns (the bias: every row) are
 #                split so no chunk's serial walk outlasts the rest of the column pass
 
@@ -40,7 +51,8 @@ SGD_CHUNK = 64  # entries per batch CSC chunk: a batch's hot columns (the bias: 
 class SGDBatch:
     """One batch's column structure (device tensors)."""
 
-    __slots__ = ("b", "e", "X", "ucol", "ucp", "ucnt", "nu", "fields", "lay", "chunk_fa", "chunk_col")
+    __slots__ = ("b", "e", "o0", "X", "ucol", "ucp", "ucnt", "nu", "fields", "lay", "chunk_fa", "chunk_col",
+                 "perm", "solo", "multi")
 
 
 def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None, nfield: int = 0,
@@ -55,7 +67,8 @@ def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None
         counts = Xb.colptr[1:] - Xb.colptr[:-1]
         u = torch.nonzero(counts).flatten()
         bt = SGDBatch()
-        bt.b, bt.e, bt.X = b, e, Xb
+        bt.b, bt.e, bt.o0, bt.X = b, e, o0, Xb
+        bt.perm = bt.solo = bt.multi = None
         bt.ucol = u.to(torch.int32).contiguous()
         bt.ucnt = counts[u].to(torch.int32).contiguous()
         # chunks of consecutive touched features are contiguous (empty columns own none)
@@ -74,6 +87,7 @@ def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None
                 if skip_feat >= 0:
                     fa = torch.where(col == skip_feat, torch.full_like(fa, -1), fa)
                 bt.chunk_fa, bt.chunk_col = fa.contiguous(), col.contiguous()
+                bt.perm = Xb.csc_perm.to(torch.int32).contiguous()  # CSC entry -> batch CSR position
                 Xb.csc_perm = None
             else:
                 _csc_layout(Xb, bt.fields, nfield)  # packed codes of the general pair-gradient kernel
@@ -87,10 +101,18 @@ def build_batches(X: SparseMatrix, bounds, fields: Optional[torch.Tensor] = None
 
 def apply_step(bt: SGDBatch, part: torch.Tensor, lat: Optional[torch.Tensor], J: int, w_lin: torch.Tensor,
                V: Optional[torch.Tensor], k: int, lr: float, l2w: float, l2v: float, reg_skip: int, upd_w: bool,
-               bias_latent: bool, avg: bool, Vb: Optional[torch.Tensor] = None, Vt: Optional[torch.Tensor] = None):
-    """``sgd_apply_kernel`` over the batch's touched features (see csrc/hip/fm.hip)."""
+               bias_latent: bool, avg: bool, Vb: Optional[torch.Tensor] = None, Vt: Optional[torch.Tensor] = None,
+               multi: bool = False):
+    """``sgd_apply_kernel`` over the batch's touched features (see csrc/hip/fm.hip); ``multi``:
+    only the columns of more than one chunk (the pair-term path updated the others)."""
     check_cuda(part, w_lin, *(t for t in (lat, V, Vb, Vt) if t is not None))
-    hip().sgd_apply(ptr(bt.ucol), ptr(bt.ucp), ptr(bt.ucnt), bt.nu, ptr(part), int(part.shape[1]),
+    if multi:
+        ucol, ucb, uce, ucnt, nu = bt.multi
+        if nu == 0:
+            return
+    else:
+        ucol, ucb, uce, ucnt, nu = bt.ucol, bt.ucp, bt.ucp[1:], bt.ucnt, bt.nu
+    hip().sgd_apply(ptr(ucol), ptr(ucb), ptr(uce), ptr(ucnt), nu, ptr(part), int(part.shape[1]),
                     ptr(lat) if lat is not None else 0, int(J), ptr(w_lin), ptr(V) if V is not None else 0, int(k),
                     ptr(Vb) if Vb is not None else 0, ptr(Vt) if Vt is not None else 0, int(w_lin.numel()),
                     float(lr), float(l2w), float(l2v), int(reg_skip), 1 if upd_w else 0, 1 if bias_latent else 0,
@@ -134,6 +156,57 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[t
                    ptr(Xb.csc_perm), ptr(Xb.indptr), ptr(code), sh, ptr(vals) if vals is not None else 0,
                    ptr(Vt), Xb.ncols, nfield, k, ptr(c), ptr(lat), int(skip_feat), int(distinct), s)
     return lat
+
+
+def pair_terms_elems(batches: List[SGDBatch], V: torch.Tensor, k: int) -> int:
+    """Floats of the pair-term buffer E when every batch takes the E path (fixed layout, k ==
+    4, V 16-B aligned, E within YTK_SGD_FFM_E_GB), else 0."""
+    if FFM_E_GB <= 0 or FFM_VT or k != 4 or V.data_ptr() % 16 or not batches:
+        return 0
+    if any(bt.lay is None for bt in batches):
+        return 0
+    m = batches[0].lay[1]
+    n = max(bt.X.nnz for bt in batches) * m * 4
+    return n if n * 4 <= FFM_E_GB * (1 << 30) else 0
+
+
+def ffm_forward_e(bt: SGDBatch, indptr, idx, val, fld, V: torch.Tensor, nfield: int, skip_feat: int,
+                  E: torch.Tensor) -> torch.Tensor:
+    """Pair sums of the batch rows (float32 [n]) + their pair terms into E (ffm_pairs_k4_kernel<true>)."""
+    n = bt.e - bt.b
+    out = torch.empty(n, dtype=torch.float32, device=V.device)
+    check_cuda(indptr, idx, val, fld, V, E)
+    hip().ffm_pairs_fwd_e(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat),
+                          ptr(E), int(bt.o0), int(bt.lay[1]), stream(V))
+    return out
+
+
+def prepare_pair_terms(bt: SGDBatch):
+    """Set-up of the pair-term path: solo[chunk] = its column has no other chunk (updated by
+    ffm_sgd_ecol_kernel itself), and the multi-chunk columns (ucol, chunk begin, chunk end,
+    count, n) left to sgd_apply."""
+    nch_u = bt.ucp[1:] - bt.ucp[:-1]  # chunks per touched column (contiguous, in column order)
+    bt.solo = (torch.repeat_interleave(nch_u, nch_u) == 1).to(torch.uint8).contiguous()
+    mu = nch_u > 1
+    bt.multi = (bt.ucol[mu].contiguous(), bt.ucp[:-1][mu].contiguous(), bt.ucp[1:][mu].contiguous(),
+                bt.ucnt[mu].contiguous(), int(mu.sum()))
+
+
+def ffm_step_e(bt: SGDBatch, c: torch.Tensor, E: torch.Tensor, w_lin: torch.Tensor, V: torch.Tensor, nfield: int,
+               k: int, lr: float, l2w: float, l2v: float, reg_skip: int, upd_w: bool, bias_latent: bool, avg: bool):
+    """ffm_sgd_ecol_kernel: the step of every single-chunk column; returns (lin, lat), the
+    multi-chunk columns' chunk partials for :func:`apply_step` (``multi=True``)."""
+    Xb = bt.X
+    lay_field, m = bt.lay
+    nch = max(Xb.n_chunks, 1)
+    lat = torch.empty((nch, nfield * k), dtype=torch.float32, device=c.device)
+    lin = torch.empty((nch, 2), dtype=torch.float32, device=c.device)
+    check_cuda(c, E, w_lin, V)
+    hip().ffm_sgd_ecol(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
+                       ptr(bt.perm), ptr(bt.chunk_fa), ptr(bt.chunk_col), ptr(bt.solo), ptr(E), m, ptr(lay_field),
+                       ptr(c), ptr(lat), ptr(lin), ptr(w_lin), ptr(V), float(lr), float(l2w), float(l2v),
+                       int(reg_skip), 1 if upd_w else 0, 1 if bias_latent else 0, 1 if avg else 0, stream(c))
+    return lin, lat
 
 
 def needs_transposed(batches: List[SGDBatch], V: torch.Tensor, k: int) -> bool:

@@ -123,6 +123,7 @@ class SGDOptimizer:
         # sgd_apply keeps current -- allocated only when some batch needs it (_setup)
         self.ffm = model.name == "ffm" and getattr(model, "stride", 0) > 0
         self.Vt = None
+        self.E = None  # FFM pair terms written by the forward (ops/sgd.pair_terms_elems)
         self._batches = None
 
     # ------------------------------------------------------------------ one batch
@@ -132,6 +133,14 @@ class SGDOptimizer:
         if self._batches is None and X.device.type == "cuda":
             fld = m.data.train.fields if self.ffm else None
             self._batches = sgd_ops.build_batches(X, bounds, fld, m.nf if self.ffm else 0, getattr(m, "_skip", -1))
+            ne = sgd_ops.pair_terms_elems(self._batches, m.w[m.F:], m.kk) if self.ffm else 0
+            if ne:
+                self.E = torch.empty(ne, dtype=torch.float32, device=X.device)
+                for bt in self._batches:
+                    sgd_ops.prepare_pair_terms(bt)
+            else:
+                for bt in self._batches:
+                    bt.perm = None
             if self.ffm and sgd_ops.needs_transposed(self._batches, self.m.w[m.F:], m.kk):
                 self.Vt = torch.empty((m.nf, m.F, m.kk), dtype=torch.float32, device=X.device)
                 self._sync_copy(self.m.w)
@@ -163,11 +172,21 @@ class SGDOptimizer:
         Vf = (self.Vb if self.Vb is not None else w[F:].view(F, kk)) if kk > 0 else w_lin.new_zeros((F, 0))
         fx, S = fm_forward(sl, w_lin, Vf)
         z1 = None
-        if self.ffm:
+        use_e = self.E is not None and getattr(m, "need_second", True)
+        if use_e:
+            z1 = sgd_ops.ffm_forward_e(bt, sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m._skip, self.E)
+        elif self.ffm:
             z1 = ffm_forward(sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m.kk, skip_feat=m._skip)
         c = self._coef(fx, d.y[b:e, 0], d.weight[b:e], z1)
-        part = sgd_ops.column_sums(bt, c, S if kk > 0 else None, kk)
         avg = sp.average == "feature"
+        bias_latent = bool(getattr(m, "bias_latent", False))
+        if use_e:  # single-chunk columns step inside ffm_sgd_ecol_kernel, the rest in sgd_apply
+            lin, lat = sgd_ops.ffm_step_e(bt, c, self.E, w_lin, w[F:], m.nf, m.kk, lr, self.l2w, self.l2v, reg_skip,
+                                          upd_w, bias_latent, avg)
+            sgd_ops.apply_step(bt, lin, lat, m.stride, w_lin, w[F:], m.kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
+                               bias_latent, avg, multi=True)
+            return
+        part = sgd_ops.column_sums(bt, c, S if kk > 0 else None, kk)
         if self.ffm and getattr(m, "need_second", True):
             lat = sgd_ops.ffm_pair_sums(bt, c, w[F:], self.Vt, m.nf, m.kk, m._skip)
             sgd_ops.apply_step(bt, part, lat, m.stride, w_lin, w[F:], m.kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
