@@ -613,7 +613,7 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
     const float4* __restrict__ E, int m, const int* __restrict__ lay_field, const float* __restrict__ coef,
     float* __restrict__ lat, float* __restrict__ lin, float* __restrict__ w, float* __restrict__ V, float lr,
     float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
-  constexpr int GL = 32, U = 8;
+  constexpr int GL = 32, U = 4;
   const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
   const int q = threadIdx.x & (GL - 1);
   if (g >= nch) return;
@@ -622,43 +622,33 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
   const bool has0 = q < m, has1 = q + GL < m;
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
   float glin = 0.f;
-  // windows of 2 GL entries: their CSR positions, coefficients and values are loaded by the
-  // lanes at once (one round trip) and broadcast; then U entries' E rows are in flight
-  for (long long wb = e0; wb < e1; wb += 2 * GL) {
-    const int n = (int)min<long long>(2 * GL, e1 - wb);
-    int prA = -1, prB = -1;
-    float scA = 0.f, scB = 0.f, xA = 0.f, xB = 0.f;
-    if (q < n) { prA = csc_perm[wb + q]; scA = coef[csc_rows[wb + q]]; xA = csc_vals[wb + q]; }
-    if (q + GL < n) { prB = csc_perm[wb + q + GL]; scB = coef[csc_rows[wb + q + GL]]; xB = csc_vals[wb + q + GL]; }
-    for (int i = 0; i < n; i += U) {
-      int pr[U];
-      float sc[U], xv[U];
+  // (a variant loading a 64-entry window's positions / coefficients / values by the lanes at
+  // once, then 8 E rows in flight, measured level: 34.3M vs 34.7M rows/s)
+  for (long long eb = e0; eb < e1; eb += U) {
+    int pr[U];
+    float sc[U], xv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = min(i + u, n - 1);  // uniform; the duplicate is masked below
-        const int src = e & (GL - 1);
-        const bool lo = e < GL;
-        pr[u] = __shfl(lo ? prA : prB, src, GL);
-        sc[u] = __shfl(lo ? scA : scB, src, GL);
-        xv[u] = __shfl(lo ? xA : xB, src, GL);
-        if (i + u >= n) { pr[u] = -1; sc[u] = 0.f; xv[u] = 0.f; }
-      }
-      float4 x0[U], x1[U];
+    for (int u = 0; u < U; ++u) {
+      const long long e = eb + u;
+      pr[u] = e < e1 ? csc_perm[e] : -1;
+      sc[u] = e < e1 ? coef[csc_rows[e]] : 0.f;
+      xv[u] = e < e1 ? csc_vals[e] : 0.f;
+    }
+    float4 x0[U], x1[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (fa >= 0 && pr[u] >= 0) {
-          const float4* row = E + (long long)pr[u] * m;
-          if (has0) x0[u] = row[q];
-          if (has1) x1[u] = row[q + GL];
-        }
+    for (int u = 0; u < U; ++u) {
+      x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (fa >= 0 && pr[u] >= 0) {
+        const float4* row = E + (long long)pr[u] * m;
+        if (has0) x0[u] = row[q];
+        if (has1) x1[u] = row[q + GL];
       }
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        glin += sc[u] * xv[u];
-        a0.x += sc[u] * x0[u].x; a0.y += sc[u] * x0[u].y; a0.z += sc[u] * x0[u].z; a0.w += sc[u] * x0[u].w;
-        a1.x += sc[u] * x1[u].x; a1.y += sc[u] * x1[u].y; a1.z += sc[u] * x1[u].z; a1.w += sc[u] * x1[u].w;
-      }
+    for (int u = 0; u < U; ++u) {
+      glin += sc[u] * xv[u];
+      a0.x += sc[u] * x0[u].x; a0.y += sc[u] * x0[u].y; a0.z += sc[u] * x0[u].z; a0.w += sc[u] * x0[u].w;
+      a1.x += sc[u] * x1[u].x; a1.y += sc[u] * x1[u].y; a1.z += sc[u] * x1[u].z; a1.w += sc[u] * x1[u].w;
     }
   }
   const long long J4 = m;  // float4 slots per feature (nfield == m, k == 4)

@@ -307,6 +307,27 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
     assert res[0] == res[1] == res[2]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("sample", [1.0, 0.7])
+def test_device_leafwise_row_indexed_gh_identical(monkeypatch, sample):
+    """YTK_LW_GH_ROWS=1: (g, h) stays row-indexed (the partition moves row ids only, the
+    histograms gather (g, h) by row) -- the same trees byte for byte, with and without row
+    sampling."""
+    from ytk_learn_amd.models.gbdt.device_leafwise import DeviceLeafBuilder
+    res = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("YTK_LW_GH_ROWS", on)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 63
+        p.tree.instance_sample_rate = sample
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
+        tr.train()
+        assert isinstance(tr.builder, DeviceLeafBuilder) and tr.builder.gh_rows == (on == "1")
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1]
+
+
 def test_histogram_pool_capacity_misses_do_not_change_the_tree():
     """histogram_pool_capacity (MB) bounds the live histograms of leaf-wise growth; evicted
     parents are rebuilt (pool miss) instead of derived -- exact int64 sums => same model."""

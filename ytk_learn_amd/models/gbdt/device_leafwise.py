@@ -139,10 +139,13 @@ class DeviceLeafBuilder:
         self.slot_bytes = B * F * 16
         self.staging = torch.empty(self.hist_bound * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
         self.rows2 = torch.empty(2 * N, dtype=torch.int32, device=dev)
-        # (g, h) stays ROW-indexed through the tree (YTK_LW_GH_ROWS, default on; byte-B bins):
-        # the partition moves row ids only (4 instead of 12 B per row, both ways) and the
-        # histogram gathers (g, h) by row id -- as the level engine's gh_all mode
-        self.gh_rows = os.environ.get("YTK_LW_GH_ROWS", "1") != "0" and not self.wide
+        # YTK_LW_GH_ROWS=1 (byte-B bins): (g, h) stays ROW-indexed through the tree -- the
+        # partition moves row ids only (4 instead of 12 B per row, both ways) and the histogram
+        # gathers (g, h) by row id, as the level engine's gh_all mode. Off by default: on the
+        # 255-leaf Higgs tree the partition saves what the histogram gathers cost (late tree
+        # partition 1164 -> 1057 us, histograms 678 -> 764 us; 500 trees 3.99 -> 4.05 ms,
+        # profiles/r5/leaf_gh_rows_*)
+        self.gh_rows = os.environ.get("YTK_LW_GH_ROWS", "0") == "1" and not self.wide
         self._ghr = 0  # the tree's row-indexed (g, h) (build)
         self.gh2 = (torch.empty((2 * N, 2), dtype=torch.float32, device=dev) if not self.gh_rows
                     else torch.empty((1, 2), dtype=torch.float32, device=dev))
