@@ -8,9 +8,10 @@
 // :38-58 (every column sorted once by value).
 //
 // Layout: for each searched feature slot j, position i of the level's order holds a row id
-// ord[j][i], its value val[j][i] and its fixed-point (g, h) qv[j][i]; the rows of one node
-// are contiguous (the same ranges for every feature) and sorted by value. (g, h) travel with
-// the rows (gathered once per tree), so the split scan reads every array sequentially. A
+// ord[j][i], its value val[j][i] and its (g, h) qv[j][i] (float32, converted to the exact
+// int64 fixed point where it is summed: 8 instead of 16 B per position moved); the rows of one
+// node are contiguous (the same ranges for every feature) and sorted by value. (g, h) travel
+// with the rows (gathered once per tree), so the split scan reads every array sequentially. A
 // level is cut into TILES of <= kExTile positions that never straddle a node. Per level:
 //   eval     per (feature, tile), in ticket order: tile (g, h) aggregate, decoupled
 //            look-back over the node's earlier tiles for the exact int64 prefix, left sums
@@ -60,14 +61,15 @@ struct ExArgs {
   long long ld0;  // presorted columns [F][ld0]
   int* ordw[2];
   float* valw[2];
-  long long* qvw[2];  // [nf][ldw][2]
+  float2* qvw[2];     // [nf][ldw] (g, h)
   long long ldw;      // work ping-pong [nf][ldw]
   int sampled;        // level 0 reads ordw[0] / valw[0] (the tree's kept rows) instead of ord0
   const int* fidx;    // feature of slot j, ascending
   int nf;
   const float* XT;
   long long ldx;        // raw values [F][ldx]
-  const long long* q;   // [N][2] fixed-point (g, h) by row
+  const float2* gh;     // [N] (g, h) by row
+  float sg, sh;         // fixed-point scales (powers of two): q = rint(g * sg)
   int4* tiles[2];       // (node, p0, p1, 0) per level parity
   int* nbeg[2];         // [Kmax + 1] node begins
   int* ftile[2];        // [Kmax + 1] first tile of each node
@@ -104,8 +106,23 @@ __device__ __forceinline__ const float* ex_src_val(const ExArgs& a, int d, int j
   return a.valw[kPar] + (size_t)j * a.ldw;
 }
 template <int kPar>
-__device__ __forceinline__ const longlong2* ex_src_q(const ExArgs& a, int d, int j) {
-  return reinterpret_cast<const longlong2*>(a.qvw[kPar] + (size_t)j * a.ldw * 2);
+__device__ __forceinline__ const float2* ex_src_q(const ExArgs& a, int d, int j) {
+  return a.qvw[kPar] + (size_t)j * a.ldw;
+}
+
+// the exact int64 fixed point of a float: (long long) rint(y), as torch.round(y).to(int64)
+// in exact.py (the tensor engine's q; |y| < 2^63)
+__device__ __forceinline__ long long ex_fx(float y) {
+  const float r = __builtin_rintf(y);
+  const float m = fabsf(r);
+  const float hi = floorf(m * 0x1p-32f);
+  const float lo = __builtin_fmaf(hi, -0x1p32f, m);
+  const unsigned long long u = ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+  const unsigned long long neg = r < 0.f ? ~0ull : 0ull;
+  return (long long)((u ^ neg) - neg);
+}
+__device__ __forceinline__ longlong2 ex_q(const ExArgs& a, float2 x) {
+  return make_longlong2(ex_fx(x.x * a.sg), ex_fx(x.y * a.sh));
 }
 
 template <typename T>
@@ -226,18 +243,20 @@ __global__ __launch_bounds__(kExBig) void ex_init_kernel(ExArgs a, int n) {
   }
 }
 
-// level 0: qv[j][i] = q[ord[j][i]] (the only gather of (g, h) in a tree) and the root's totals
+// level 0: qv[j][i] = gh[ord[j][i]] (the only gather of (g, h) in a tree) and the root's totals
 __global__ __launch_bounds__(kExThreads) void ex_gather_kernel(ExArgs a, int n) {
   const int j = blockIdx.y;
   const int* ord = ex_src_ord<0>(a, 0, j);
-  longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[0] + (size_t)j * a.ldw * 2);
-  const longlong2* q2 = reinterpret_cast<const longlong2*>(a.q);
+  float2* qo = a.qvw[0] + (size_t)j * a.ldw;
   long long sg = 0, sh = 0, dummy = 0;
   for (long long i = blockIdx.x * (long long)kExThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kExThreads) {
-    const longlong2 v = q2[ord[i]];
-    qo[i] = v;
-    sg += v.x;
-    sh += v.y;
+    const float2 x = a.gh[ord[i]];
+    qo[i] = x;
+    if (j == 0) {
+      const longlong2 v = ex_q(a, x);
+      sg += v.x;
+      sh += v.y;
+    }
   }
   if (j != 0) return;
   ex_block_sum3(sg, sh, dummy);
@@ -287,7 +306,7 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
   if (!(H >= 2.0 * (double)gp.mcw && (nb1 - nb0) >= max(a.min_split_samples, 0))) return;
   const float root_gain = (float)calc_gain(G, H, gp);
   const float* val = ex_src_val<par>(a, d, j);
-  const longlong2* qv = ex_src_q<par>(a, d, j);
+  const float2* qv = ex_src_q<par>(a, d, j);
   const ExSpan sp = ex_span(tl);
   long long g[kExPer], h[kExPer];
   float v[kExPer];
@@ -297,7 +316,7 @@ __global__ __launch_bounds__(kExThreads) void ex_eval_kernel(ExArgs a, int d) {
     g[e] = h[e] = 0;
     v[e] = 0.f;
     if (e < sp.n) {
-      const longlong2 x = qv[sp.i0 + e];
+      const longlong2 x = ex_q(a, qv[sp.i0 + e]);
       g[e] = x.x;
       h[e] = x.y;
       v[e] = val[sp.i0 + e];
@@ -467,7 +486,7 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
   const int f = a.go_feat[tl.x];
   const float thr = a.go_thr[tl.x];
   const int* ord = ex_src_ord<par>(a, d, 0);
-  const longlong2* qv = ex_src_q<par>(a, d, 0);
+  const float2* qv = ex_src_q<par>(a, d, 0);
   long long nl = 0, lg = 0, lh = 0, rg = 0, rh = 0;
   for (int i = tl.y + threadIdx.x; i < tl.z; i += kExThreads) {
     const int r = ord[i];
@@ -475,7 +494,7 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(ExArgs a, int d) {
       a.left_row[r] = 2;
       continue;
     }
-    const longlong2 x = qv[i];
+    const longlong2 x = ex_q(a, qv[i]);
     const bool left = a.XT[(size_t)f * a.ldx + r] < thr;
     a.left_row[r] = left ? 1 : 0;
     if (left) {
@@ -534,40 +553,36 @@ __global__ __launch_bounds__(kExBig) void ex_layout_kernel(ExArgs a, int d) {
   const int* ftile = a.ftile[par];
   const int* nbg = a.nbeg[par];
   constexpr int kW = kExBig / kWave;
-  __shared__ long long s5[5][kW];
+  __shared__ long long s1[kW];
   __shared__ int si[2][kW];
   const int w = tid / kWave, l = lane_id();
-  long long carry[5] = {0, 0, 0, 0, 0};
-  for (int base = 0; base < nt; base += kExBig) {
-    const int t = base + tid;
-    long long x[5] = {0, 0, 0, 0, 0}, inc[5];
-    int node = 0;
-    if (t < nt) {
-      node = tiles[t].x;
-      if (a.go_feat[node] >= 0) {
-#pragma unroll
-        for (int c = 0; c < 5; ++c) x[c] = a.tpart[(size_t)t * 5 + c];
+  // one component per pass over the tiles (not all five at once: five int64 scans in flight
+  // spilled 79 VGPRs to scratch at 1024 threads)
+#pragma unroll 1
+  for (int c = 0; c < 5; ++c) {
+    long long carry = 0;
+    for (int base = 0; base < nt; base += kExBig) {
+      const int t = base + tid;
+      long long x = 0;
+      int node = 0;
+      if (t < nt) {
+        node = tiles[t].x;
+        if (a.go_feat[node] >= 0) x = a.tpart[(size_t)t * 5 + c];
       }
-    }
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      inc[c] = dpp_scan_add(x[c]);
-      if (l == kWave - 1) s5[c][w] = inc[c];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      long long o = carry[c], T = 0;
+      const long long inc = dpp_scan_add(x);
+      if (l == kWave - 1) s1[w] = inc;
+      __syncthreads();
+      long long o = carry, T = 0;
       for (int q = 0; q < kW; ++q) {
-        if (q < w) o += s5[c][q];
-        T += s5[c][q];
+        if (q < w) o += s1[q];
+        T += s1[q];
       }
-      if (t < nt && ftile[node] == t) a.nbase[(size_t)node * 5 + c] = o + inc[c] - x[c];
-      carry[c] += T;
+      if (t < nt && ftile[node] == t) a.nbase[(size_t)node * 5 + c] = o + inc - x;
+      carry += T;
+      __syncthreads();
     }
-    __syncthreads();
+    if (tid == 0) a.nbase[(size_t)K * 5 + c] = carry;
   }
-  if (tid < 5) a.nbase[(size_t)K * 5 + tid] = carry[tid];
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   auto nsum = [&](int k, int c) -> long long {
@@ -661,11 +676,11 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   if (a.csplit[k] < 0) return;  // a leaf: its rows leave the order (block-uniform, nobody waits)
   const int* ord = ex_src_ord<par>(a, d, j);
   const float* val = ex_src_val<par>(a, d, j);
-  const longlong2* qv = ex_src_q<par>(a, d, j);
+  const float2* qv = ex_src_q<par>(a, d, j);
   constexpr int no = par ^ 1;
   int* ordo = a.ordw[no] + (size_t)j * a.ldw;
   float* valo = a.valw[no] + (size_t)j * a.ldw;
-  longlong2* qo = reinterpret_cast<longlong2*>(a.qvw[no] + (size_t)j * a.ldw * 2);
+  float2* qo = a.qvw[no] + (size_t)j * a.ldw;
   // lane-consecutive elements (element i = e * kExThreads + tid: every load instruction reads
   // 64 consecutive positions) ranked with wave ballots: lefts before element i = the lefts of
   // the rows e' < e of the tile, of the waves before this one in row e, and of the lanes
@@ -675,7 +690,7 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   constexpr int NW = kExThreads / kWave;
   int r[kExPer];
   float v[kExPer];
-  long long qg[kExPer], qh[kExPer];  // (a longlong2 array was kept in scratch)
+  float2 q[kExPer];
   unsigned lmask = 0;
   // lanes past the tile's end load its first element again (clamped index, n >= 1: a node's
   // tiles are never empty)
@@ -689,9 +704,7 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
     const int i = e * kExThreads + tid;
     const int ic = i < n ? i : 0;
     v[e] = val[i0 + ic];
-    const longlong2 x = qv[i0 + ic];
-    qg[e] = x.x;
-    qh[e] = x.y;
+    q[e] = qv[i0 + ic];
     // the row's direction from the bitset (1.3 MB for 10.5M rows: L2 resident, unlike the
     // 10.5 MB byte array the random gather read before)
     lmask |= (i < n && ((a.left_bits[(unsigned)r[e] >> 5] >> (r[e] & 31)) & 1u)) ? 1u << e : 0u;
@@ -739,7 +752,7 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
   // runs with consecutive lanes on consecutive positions (coalesced)
   __shared__ int s_r[kExTile];
   __shared__ float s_v[kExTile];
-  __shared__ longlong2 s_q[kExTile];
+  __shared__ float2 s_q[kExTile];
 #pragma unroll
   for (int e = 0; e < kExPer; ++e) {
     const int i = e * kExThreads + tid;
@@ -748,7 +761,7 @@ __global__ __launch_bounds__(kExThreads) void ex_part_kernel(ExArgs a, int d) {
       const int dst = (lmask >> e) & 1 ? lb : tl_left + (i - lb);
       s_r[dst] = r[e];
       s_v[dst] = v[e];
-      s_q[dst] = make_longlong2(qg[e], qh[e]);
+      s_q[dst] = q[e];
     }
   }
   __syncthreads();
@@ -802,8 +815,8 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
   a.ordw[1] = (int*)p[i++];
   a.valw[0] = (float*)p[i++];
   a.valw[1] = (float*)p[i++];
-  a.qvw[0] = (long long*)p[i++];
-  a.qvw[1] = (long long*)p[i++];
+  a.qvw[0] = (float2*)p[i++];
+  a.qvw[1] = (float2*)p[i++];
   a.XT = (const float*)p[i++];
   a.tiles[0] = (int4*)p[i++];
   a.tiles[1] = (int4*)p[i++];
@@ -846,14 +859,17 @@ int ytk_ex_create(const uintptr_t* p, const long long* ip, const float* fp) {
 }
 
 // Enqueue one tree: levels 0 .. depth - 1 search and split, level `depth` only records its
-// nodes (leaves). q: [N][2] int64 fixed-point (g, h) with scales (inv_g, inv_h) leaving
-// |sums| < 2^60; fidx: the nf searched feature slots (ascending); n: rows in the tree (sampled:
-// ordw[0] / valw[0] hold each slot's kept rows in value order).
-void ytk_ex_tree(int h, uintptr_t q, uintptr_t fidx, int nf, int n, int sampled, double inv_g, double inv_h,
+// nodes (leaves). gh: [N] float (g, h) by row; the int64 fixed point is rint(g * sg),
+// rint(h * sh) with power-of-two scales leaving |sums| < 2^60 (inv_g = 1 / sg, inv_h = 1 / sh);
+// fidx: the nf searched feature slots (ascending); n: rows in the tree (sampled: ordw[0] /
+// valw[0] hold each slot's kept rows in value order).
+void ytk_ex_tree(int h, uintptr_t gh, uintptr_t fidx, int nf, int n, int sampled, double inv_g, double inv_h,
                  int depth, float lr, uintptr_t stream) {
   ExEngine& e = g_ex.at(h);
   ExArgs a = e.a;
-  a.q = (const long long*)q;
+  a.gh = (const float2*)gh;
+  a.sg = (float)(1.0 / inv_g);
+  a.sh = (float)(1.0 / inv_h);
   a.fidx = (const int*)fidx;
   a.nf = nf;
   a.sampled = sampled;

@@ -19,7 +19,6 @@ from kernel_resources import HIP_DIR, demangle, kernel_table  # noqa: E402
 
 # (pattern on the demangled name, why scratch is tolerated there)
 ALLOWED = [
-    (r"ex_layout_kernel", "one block per level (tile-table rebuild), not a streaming pass"),
     (r"lv_partition_children_kernel<true, \d+, 16, true, true", "YTK_PART_CHUNK=4096 prefetch variant (off by default)"),
     (r"tree_grad_hist_kernel<3>", "Poisson loss: inlined lgamma of the label"),
     (r"tree_grad_hist_kernel<0>", "sigmoid fused pass at the 128-VGPR cap of 1024-thread blocks: one dword per 2 rows"),

@@ -114,10 +114,10 @@ class ExactGreedyBuilder:
         return torch.where(H < mcw, torch.zeros_like(v), v)
 
     # ------------------------------------------------------------------ HIP engine
-    HIP_BYTES_PER_CELL = 4 + 4 + 2 * (4 + 4 + 16)  # ord0, val0, ping-pong ordw / valw / qvw
+    HIP_BYTES_PER_CELL = 4 + 4 + 2 * (4 + 4 + 8)  # ord0, val0, ping-pong ordw / valw / qvw (float (g, h))
 
     def _hip_fits(self) -> bool:
-        """The HIP engine holds ~56 B per (feature, row) cell on top of XT (the tensor path ~12 B,
+        """The HIP engine holds ~40 B per (feature, row) cell on top of XT (the tensor path ~12 B,
         in feature chunks): check it against the free device memory (the int64 presort order,
         8 B per cell, is released during the set-up) and fall back to the tensor engine, with a
         log line, when it does not fit."""
@@ -153,7 +153,9 @@ class ExactGreedyBuilder:
         i64 = lambda n: torch.zeros(max(1, n), dtype=torch.int64, device=dev)  # noqa: E731
         self.ordw = [torch.empty((F, N), dtype=torch.int32, device=dev) for _ in range(2)]
         self.valw = [torch.empty((F, N), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.qvw = [torch.empty((F, N, 2), dtype=torch.int64, device=dev) for _ in range(2)]
+        # (g, h) travel with the rows as float32 (the kernels convert to the exact int64 fixed
+        # point where they sum: rint(g * sg), the q of the tensor engine)
+        self.qvw = [torch.empty((F, N, 2), dtype=torch.float32, device=dev) for _ in range(2)]
         self.ex_tiles = [i32(4 * mt), i32(4 * mt)]
         self.ex_nbeg = [i32(Kmax + 1), i32(Kmax + 1)]
         self.ex_ftile = [i32(Kmax + 1), i32(Kmax + 1)]
@@ -225,12 +227,10 @@ class ExactGreedyBuilder:
             ghk = gh
         mx = ghk.abs().amax(dim=0).double().cpu().numpy() if n > 0 else np.zeros(2)
         sg, sh = gops.fixed_point_scales(mx[0], mx[1], 4 * max(n, 1))  # |sums| < 2^60 (look-back words)
-        q = torch.empty((self.N, 2), dtype=torch.int64, device=dev)
-        q[:, 0] = torch.round(gh[:, 0].float() * np.float32(sg)).to(torch.int64)
-        q[:, 1] = torch.round(gh[:, 1].float() * np.float32(sh)).to(torch.int64)
+        ghf = gh.float().contiguous()  # the kernels quantize rint(g * sg) themselves (== quantize_gh)
         D = p.max_depth
-        hip().ex_tree(self.ex_handle, ptr(q), ptr(fidx), nf, n, 1 if sampled else 0, 1.0 / sg, 1.0 / sh, D,
-                      float(np.float32(p.learning_rate)), stream(q))
+        hip().ex_tree(self.ex_handle, ptr(ghf), ptr(fidx), nf, n, 1 if sampled else 0, 1.0 / sg, 1.0 / sh, D,
+                      float(np.float32(p.learning_rate)), stream(ghf))
         recs = self.ex_rec.cpu().numpy().view(self.REC_DTYPE)
         rec_k = self.ex_rec_k.cpu().numpy()
         err = int(self.ex_ctl[5].item())
