@@ -82,6 +82,8 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
                       int, int, uintptr_t);
 void ytk_ffm_sgd_grad(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, uintptr_t);
+void ytk_ffm_pairs_lds(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int, int,
+                       uintptr_t, long long, uintptr_t);
 void ytk_ffm_pairs_fwd_e(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int,
                          uintptr_t, long long, int, uintptr_t);
 void ytk_ffm_sgd_ecol(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
@@ -218,6 +220,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("ffm_grad_csc", &ytk_ffm_grad_csc);
   m.def("ffm_sgd_grad", &ytk_ffm_sgd_grad);
   m.def("ffm_pairs_fwd_e", &ytk_ffm_pairs_fwd_e);
+  m.def("ffm_pairs_lds", &ytk_ffm_pairs_lds);
   m.def("ffm_sgd_ecol", &ytk_ffm_sgd_ecol);
   m.def("ffm_grad_stream", &ytk_ffm_grad_stream);
   m.def("dot", &ytk_dot);

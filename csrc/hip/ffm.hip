@@ -14,6 +14,7 @@
 // order-dependent reduction in the sparse family (documented).
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace ytk {
@@ -198,6 +199,87 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if (lane == 0) fx[row] = acc;
+}
+
+// Forward for k == 4 with the row's latent rows staged in LDS: one wave per row (64-thread
+// blocks walking rows grid-stride), the m latent rows V[i_j, 0..nfield) of the row copied whole
+// into LDS with coalesced 16-B loads, then the m (m - 1) / 2 pairs read from LDS, pair index
+// pi = q (q - 1) / 2 + p (p < q) decoded per lane. ffm_pairs_k4_kernel gathers the same bytes
+// as 16-B pieces, one per lane and pair: 64 distinct lines per load instruction for V[i_q, f_p]
+// (every latent row is touched 2 (m - 1) times, in slices), so it is bound by the cache
+// request rate, not by bytes. Rows of at most max_m entries (LDS: max_m * (nfield + 1) * 16 B;
+// the padded row stride keeps a column read -- lanes q at slot f -- off one bank group).
+// kE (SGD pair terms, as ffm_pairs_k4_kernel<true>): then E[e_p][q] = x_p x_q V[i_q, f_p] row by
+// row, lanes q reading LDS column f_p -- every store a coalesced row, no transpose.
+constexpr int kLdsU = 4;  // staging loads in flight per lane
+template <bool kE>
+__global__ __launch_bounds__(64) void ffm_pairs_lds_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
+    const int* __restrict__ fld, long long nrows, const float4* __restrict__ V, int nfield,
+    float* __restrict__ fx, int skip_feat, float4* __restrict__ E, long long e_base) {
+  extern __shared__ float4 s_v[];  // [m][nfield + 1]
+  const int lane = threadIdx.x;
+  const int S = nfield + 1;
+  const int step_j = 64 / nfield, step_t = 64 - step_j * nfield;
+  const int lane_j = lane / nfield, lane_t = lane - lane_j * nfield;
+  for (long long row = blockIdx.x; row < nrows; row += gridDim.x) {
+    const long long b = indptr[row];
+    const int m = (int)(indptr[row + 1] - b);
+    int ij = 0, fj = 0;
+    float xj = 0.f;
+    if (lane < m) { ij = idx[b + lane]; fj = fld[b + lane]; xj = val[b + lane]; }
+    const int tot = m * nfield;
+    int j = lane_j, t = lane_t;  // (entry, slot) of position s0 + u * 64 + lane
+    for (int s0 = 0; s0 < tot; s0 += 64 * kLdsU) {
+      float4 v[kLdsU];
+      int dst[kLdsU];
+#pragma unroll
+      for (int u = 0; u < kLdsU; ++u) {
+        const int sp = s0 + u * 64 + lane;
+        const int i = __shfl(ij, min(j, 63), 64);
+        dst[u] = sp < tot ? j * S + t : -1;
+        v[u] = sp < tot ? V[(long long)i * nfield + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        t += step_t;
+        j += step_j;
+        if (t >= nfield) { t -= nfield; ++j; }
+      }
+#pragma unroll
+      for (int u = 0; u < kLdsU; ++u)
+        if (dst[u] >= 0) s_v[dst[u]] = v[u];
+    }
+    wave_sync();
+    float acc = 0.f;
+    const int np = m * (m - 1) / 2;
+    for (int pi = lane; pi < np; pi += 64) {
+      int q = (int)(0.5f * (1.f + sqrtf(1.f + 8.f * (float)pi)));
+      while (q * (q - 1) / 2 > pi) --q;
+      while ((q + 1) * q / 2 <= pi) ++q;
+      const int p = pi - q * (q - 1) / 2;
+      const int ip = __shfl(ij, p, 64), iq = __shfl(ij, q, 64);
+      const int fp = __shfl(fj, p, 64), fq = __shfl(fj, q, 64);
+      const float xx = __shfl(xj, p, 64) * __shfl(xj, q, 64);
+      if (ip != skip_feat && iq != skip_feat) {
+        const float4 a = s_v[p * S + fq], c = s_v[q * S + fp];  // V[i_p, f_q], V[i_q, f_p]
+        acc += (a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w) * xx;
+      }
+    }
+    if (kE) {  // E rows: entry p, lanes q
+      const bool qs = lane < m && ij != skip_feat;
+      for (int p = 0; p < m; ++p) {
+        const int fp = __shfl(fj, p, 64), ip = __shfl(ij, p, 64);
+        const float xp = __shfl(xj, p, 64);
+        if (lane < m) {
+          const float s = (qs && lane != p && ip != skip_feat) ? xp * xj : 0.f;
+          const float4 c = s_v[lane * S + fp];
+          E[(b - e_base + p) * m + lane] = make_float4(s * c.x, s * c.y, s * c.z, s * c.w);
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) fx[row] = acc;
+    wave_sync();  // the next row's staging overwrites s_v
+  }
 }
 
 // Pair scatter backward for k == 4 (the SGD step's direct update of V: coef = -lr c_r):
@@ -846,6 +928,31 @@ void ytk_ffm_sgd_ecol(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
                      (const int*)chunk_col, (const unsigned char*)solo, (const float4*)E, m, (const int*)lay_field,
                      (const float*)coef, (float*)lat, (float*)lin, (float*)w, (float*)V, lr, l2w, l2v, reg_skip,
                      upd_w, bias_latent, avg);
+  YTK_LAUNCH_CHECK();
+}
+
+// Forward pair sums with the row's latent rows staged in LDS (see ffm_pairs_lds_kernel):
+// k == 4, V 16-B aligned, every row of <= max_m <= 64 entries, max_m * (nfield + 1) * 16 B of
+// LDS. E != 0: fixed-layout rows of exactly max_m entries, also writing the SGD pair terms
+// E[entry - e_base][max_m] (float4).
+void ytk_ffm_pairs_lds(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld, long long nrows, uintptr_t V,
+                       int nfield, uintptr_t fx, int skip_feat, int max_m, uintptr_t E, long long e_base,
+                       uintptr_t stream) {
+  if (nrows <= 0) return;
+  if ((V & 15) || (E & 15)) throw std::invalid_argument("ffm_pairs_lds: V / E must be 16-B aligned");
+  if (max_m < 1 || max_m > 64 || nfield < 1) throw std::invalid_argument("ffm_pairs_lds: 1 <= max_m <= 64");
+  const size_t lds = (size_t)max_m * (nfield + 1) * sizeof(float4);
+  if (lds > 64 * 1024) throw std::invalid_argument("ffm_pairs_lds: max_m * (nfield + 1) * 16 B > 64 KiB");
+  const long long grid = std::min<long long>(nrows, 256LL * 32);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (E)
+    hipLaunchKernelGGL(ffm_pairs_lds_kernel<true>, dim3((unsigned)grid), dim3(64), lds, s, (const long long*)indptr,
+                       (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float4*)V, nfield,
+                       (float*)fx, skip_feat, (float4*)E, e_base);
+  else
+    hipLaunchKernelGGL(ffm_pairs_lds_kernel<false>, dim3((unsigned)grid), dim3(64), lds, s, (const long long*)indptr,
+                       (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float4*)V, nfield,
+                       (float*)fx, skip_feat, (float4*)nullptr, 0LL);
   YTK_LAUNCH_CHECK();
 }
 

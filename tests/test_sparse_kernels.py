@@ -286,6 +286,31 @@ def test_ffm_gpu_matches_cpu(cuda, k, m, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("avg,nf", [(12, 7), (20, 40), (31, 16)])
+def test_ffm_lds_forward_matches_cpu(cuda, avg, nf):
+    """LDS-staged pair forward (ffm_pairs_lds_kernel, max_m given): ragged rows of up to 64
+    entries, fields repeating inside a row, with and without a skipped feature -- against the
+    CPU sums and the gather kernel (fp32 sums in another order)."""
+    from ytk_learn_amd.ops.ffm import lds_forward_ok
+    n, F, k = 3000, 400, 4
+    ip, ix, vv, _ = _rand_csr(n, F, avg, seed=avg)
+    g = torch.Generator().manual_seed(avg)
+    fl = torch.randint(0, nf, (ix.shape[0],), generator=g, dtype=torch.int32)
+    V = torch.randn(F * nf * k, generator=g) * 0.2
+    max_m = int((ip[1:] - ip[:-1]).max())
+    Vg = V.to(cuda)
+    assert max_m <= 64 and lds_forward_ok(max_m, nf, k, Vg)
+    args = (ip.to(cuda), ix.to(cuda), vv.to(cuda), fl.to(cuda), Vg, nf, k)
+    for skip in (-1, int(ix[0])):
+        fx_c = ffm_forward(ip, ix, vv, fl, V, nf, k, skip_feat=skip)
+        fx_l = ffm_forward(*args, skip_feat=skip, max_m=max_m)
+        fx_g = ffm_forward(*args, skip_feat=skip)
+        torch.testing.assert_close(fx_l.cpu(), fx_c, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(fx_l, fx_g, rtol=1e-5, atol=1e-5)
+        assert torch.equal(fx_l, ffm_forward(*args, skip_feat=skip, max_m=max_m))  # deterministic
+
+
+@pytest.mark.gpu
 def test_ffm_csc_backward_one_hot(cuda):
     """Distinct fields per row and unit values: the atomic-free LDS path and the value-free
     codes; checked against the CPU pair scatter, and bitwise repeatable."""

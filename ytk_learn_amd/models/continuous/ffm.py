@@ -77,6 +77,16 @@ class FFMModel(ContinuousModelBase):
     def regular_groups(self) -> List[Tuple[int, int]]:
         return [(self.bias_delta, self.F), (self.F, self.dim)]
 
+    def _max_m(self, key, d) -> int:
+        """Entries of the longest row (GPU; the LDS-staged pair forward needs it), cached."""
+        if not d.indptr.is_cuda:
+            return 0
+        ck = ("max_m", key)
+        if ck not in self._cache:
+            n = d.indptr.shape[0] - 1
+            self._cache[ck] = int((d.indptr[1:] - d.indptr[:-1]).max()) if n > 0 else 0
+        return self._cache[ck]
+
     def _pairs(self, key, d):
         if d.indptr.is_cuda:
             return None
@@ -91,7 +101,7 @@ class FFMModel(ContinuousModelBase):
         z_pair = None
         if self.stride > 0:
             z_pair = ffm_forward(d.indptr, d.indices, d.values, d.fields, V, self.nf, self.kk, cache=cache,
-                                 skip_feat=self._skip)
+                                 skip_feat=self._skip, max_m=self._max_m(key, d))
         fused = row_loss(self.loss, z_lin, d.y[:, 0], d.weight, z1=z_pair, want_grad=g is not None)
         if fused is not None:  # one fused row pass (sigmoid / l2 on the GPU)
             lsum, pred, c = fused

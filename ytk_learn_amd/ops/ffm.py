@@ -44,11 +44,28 @@ def ffm_pairs_cpu(indptr, idx, val, skip_feat: int = -1):
     return r[keep], p[keep], q[keep]
 
 
-def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=None, skip_feat: int = -1):
-    """Pair-interaction sum per row (float32 [n]). CPU: ``cache`` = :func:`ffm_pairs_cpu` output."""
+LDS_FWD = os.environ.get("YTK_FFM_LDS", "1") != "0"  # ffm_pairs_lds_kernel where it applies
+
+
+def lds_forward_ok(max_m: int, nfield: int, k: int, V) -> bool:
+    """The LDS-staged forward applies: k == 4, V 16-B aligned, rows of <= 64 entries whose
+    latent rows (max_m x (nfield + 1) x 16 B, padded) fit 64 KiB of LDS."""
+    return (LDS_FWD and k == 4 and V.is_cuda and V.data_ptr() % 16 == 0 and 1 <= max_m <= 64
+            and max_m * (nfield + 1) * 16 <= 64 * 1024)
+
+
+def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=None, skip_feat: int = -1,
+                max_m: int = 0):
+    """Pair-interaction sum per row (float32 [n]). CPU: ``cache`` = :func:`ffm_pairs_cpu` output.
+    ``max_m`` (GPU, optional): the longest row's entries -- enables the LDS-staged kernel."""
     n = indptr.shape[0] - 1
     if out is None:
         out = torch.zeros(n, dtype=torch.float32, device=V.device)
+    if V.is_cuda and max_m and lds_forward_ok(max_m, nfield, k, V):
+        check_cuda(indptr, idx, val, fld, V, out)
+        hip().ffm_pairs_lds(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat),
+                            int(max_m), 0, 0, stream(V))
+        return out
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, out)
         hip().ffm_pairs(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, k, ptr(out), 0, 0, 0,

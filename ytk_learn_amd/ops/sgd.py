@@ -173,9 +173,15 @@ def pair_terms_elems(batches: List[SGDBatch], V: torch.Tensor, k: int) -> int:
 def ffm_forward_e(bt: SGDBatch, indptr, idx, val, fld, V: torch.Tensor, nfield: int, skip_feat: int,
                   E: torch.Tensor) -> torch.Tensor:
     """Pair sums of the batch rows (float32 [n]) + their pair terms into E (ffm_pairs_k4_kernel<true>)."""
+    from .ffm import lds_forward_ok
     n = bt.e - bt.b
     out = torch.empty(n, dtype=torch.float32, device=V.device)
     check_cuda(indptr, idx, val, fld, V, E)
+    m = int(bt.lay[1])
+    if lds_forward_ok(m, nfield, 4, V):  # the row's latent rows staged in LDS (ffm_pairs_lds_kernel<true>)
+        hip().ffm_pairs_lds(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat), m,
+                            ptr(E), int(bt.o0), stream(V))
+        return out
     hip().ffm_pairs_fwd_e(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat),
                           ptr(E), int(bt.o0), int(bt.lay[1]), stream(V))
     return out
