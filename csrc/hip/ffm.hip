@@ -250,7 +250,10 @@ __global__ __launch_bounds__(64) void ffm_pairs_lds_kernel(
     wave_sync();
     float acc = 0.f;
     const int np = m * (m - 1) / 2;
-    for (int pi = lane; pi < np; pi += 64) {
+    // uniform trip count: the shuffles read lanes p, q, which must be active (a lane that left
+    // a divergent loop returns no data to ds_bpermute)
+    for (int base = 0; base < np; base += 64) {
+      const int pi = min(base + lane, np - 1);
       int q = (int)(0.5f * (1.f + sqrtf(1.f + 8.f * (float)pi)));
       while (q * (q - 1) / 2 > pi) --q;
       while ((q + 1) * q / 2 <= pi) ++q;
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(64) void ffm_pairs_lds_kernel(
       const int ip = __shfl(ij, p, 64), iq = __shfl(ij, q, 64);
       const int fp = __shfl(fj, p, 64), fq = __shfl(fj, q, 64);
       const float xx = __shfl(xj, p, 64) * __shfl(xj, q, 64);
-      if (ip != skip_feat && iq != skip_feat) {
+      if (base + lane < np && ip != skip_feat && iq != skip_feat) {
         const float4 a = s_v[p * S + fq], c = s_v[q * S + fp];  // V[i_p, f_q], V[i_q, f_p]
         acc += (a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w) * xx;
       }
