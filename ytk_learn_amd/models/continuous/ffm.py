@@ -79,7 +79,8 @@ class FFMModel(ContinuousModelBase):
 
     def _max_m(self, key, d) -> int:
         """Entries of the longest row (GPU; the LDS-staged pair forward needs it), cached."""
-        if not d.indptr.is_cuda:
+        from ...ops.ffm import LDS_FWD_FULL
+        if not d.indptr.is_cuda or not LDS_FWD_FULL:
             return 0
         ck = ("max_m", key)
         if ck not in self._cache:

@@ -45,6 +45,11 @@ def ffm_pairs_cpu(indptr, idx, val, skip_feat: int = -1):
 
 
 LDS_FWD = os.environ.get("YTK_FFM_LDS", "1") != "0"  # ffm_pairs_lds_kernel where it applies
+# ... and over a whole data set (the L-BFGS forward, 4M Criteo-shape rows): off by default,
+# the gather kernel measured faster there (22.9 vs 25.5 ms: every latent row misses to HBM and
+# LDS capacity caps the rows in flight at ~6 per CU), while SGD batches gain (0.70 vs 1.05 ms
+# per 65536-row pair-term forward; profiles/r5/ffm_lds/)
+LDS_FWD_FULL = os.environ.get("YTK_FFM_LDS_FULL", "0") == "1"
 
 
 def lds_forward_ok(max_m: int, nfield: int, k: int, V) -> bool:
