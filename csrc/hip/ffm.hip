@@ -680,17 +680,21 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
   }
 }
 
-// SGD batch step from the forward's pair terms (ffm_pairs_k4_kernel<true>, k == 4,
-// fixed-layout rows): the chunk's pair gradient is sum over its entries e (CSC order:
-// deterministic) of c_{row(e)} * E[perm(e)][q] into field slot f_q, and its linear gradient
-// sum c x. One 32-lane group per chunk, lane q owning positions q and q + 32 (m <= 64); each
-// entry is one contiguous m * 16-B row read, U entries in flight -- the 16-B gathers of V
-// that ffm_sgd_grad_kernel makes are replaced by full-line reads of E.
-// A chunk that is its column's only one (solo[g]: most columns of a batch) applies the step
-// here, exactly as sgd_apply_kernel would from a single chunk (w -= lri (g + cnt l2w w),
-// V -= lri (gV + cnt l2v V), bias rules); the others write lat[g] / lin[g] = (sum c x, 0)
-// for sgd_apply over the multi-chunk columns. chunk_fa < 0 (the skipped column): no latent
-// gradient (zeros).
+// SGD batch step from the forward's pair terms (ffm_pairs_lds_kernel<true> /
+// ffm_pairs_k4_kernel<true>, k == 4, fixed-layout rows): a chunk's pair gradient is the sum
+// over its entries e (CSC order: deterministic) of c_{row(e)} * E[perm(e)][q] into field slot
+// f_q, its linear gradient sum c x. One 32-lane group per kEcolCpg consecutive chunks, lane q
+// owning positions q and q + 32 (m <= 64): the group's chunk bounds / fields / columns are
+// loaded by its lanes at once, the entries walked in order in windows of 32 whose positions,
+// coefficients and values the lanes also load at once (one round trip per window, not a
+// dependent chain per chunk: a 65536-row batch has ~2 entries per chunk), U entry rows of E
+// in flight (contiguous m x 16 B each -- the 16-B gathers of V that ffm_sgd_grad_kernel makes
+// are replaced by whole-line reads). Crossing a chunk end flushes the chunk: a chunk that is
+// its column's only one (solo: most columns of a batch) applies the step here, exactly as
+// sgd_apply_kernel would from a single chunk (w -= lri (g + cnt l2w w), V -= lri (gV + cnt
+// l2v V), bias rules); the others write lat / lin = (sum c x, 0) for sgd_apply over the
+// multi-chunk columns. The skipped column (chunk_fa < 0) has all-zero E rows: no latent step.
+constexpr int kEcolCpg = 8;
 __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
     const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
     const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ csc_perm,
@@ -699,74 +703,109 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
     float* __restrict__ lat, float* __restrict__ lin, float* __restrict__ w, float* __restrict__ V, float lr,
     float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
   constexpr int GL = 32, U = 4;
-  const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
+  const long long grp = (blockIdx.x * 256LL + threadIdx.x) / GL;
   const int q = threadIdx.x & (GL - 1);
-  if (g >= nch) return;
-  const long long e0 = chunk_beg[g], e1 = chunk_end[g];
-  const int fa = chunk_fa[g];
+  const long long c0 = grp * kEcolCpg;
+  if (c0 >= nch) return;  // group-uniform
+  const int nc = (int)min<long long>(kEcolCpg, nch - c0);
+  long long my_e1 = 0;
+  int my_fa = -1, my_col = 0, my_solo = 0;
+  if (q < nc) {
+    my_e1 = chunk_end[c0 + q];
+    my_fa = chunk_fa[c0 + q];
+    my_col = chunk_col[c0 + q];
+    my_solo = solo[c0 + q];
+  }
+  const long long E0 = chunk_beg[c0];
+  const long long E1 = __shfl(my_e1, nc - 1, GL);
   const bool has0 = q < m, has1 = q + GL < m;
+  const int lf0 = has0 ? lay_field[q] : 0, lf1 = has1 ? lay_field[q + GL] : 0;
+  const long long J4 = m;  // float4 slots per feature (nfield == m, k == 4)
+  int ci = 0;
+  long long cbeg = E0, cend = __shfl(my_e1, 0, GL);
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
   float glin = 0.f;
-  // (a variant loading a 64-entry window's positions / coefficients / values by the lanes at
-  // once, then 8 E rows in flight, measured level: 34.3M vs 34.7M rows/s)
-  for (long long eb = e0; eb < e1; eb += U) {
-    int pr[U];
-    float sc[U], xv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long e = eb + u;
-      pr[u] = e < e1 ? csc_perm[e] : -1;
-      sc[u] = e < e1 ? coef[csc_rows[e]] : 0.f;
-      xv[u] = e < e1 ? csc_vals[e] : 0.f;
+  auto flush = [&]() {  // chunk c0 + ci, entries [cbeg, cend); group-uniform
+    const long long gc = c0 + ci;
+    const int fa = __shfl(my_fa, ci, GL), col = __shfl(my_col, ci, GL), sl = __shfl(my_solo, ci, GL);
+    if (!sl) {
+      float4* out = reinterpret_cast<float4*>(lat) + gc * J4;
+      if (has0) out[lf0] = a0;
+      if (has1) out[lf1] = a1;
+      if (q == 0) { lin[2 * gc] = glin; lin[2 * gc + 1] = 0.f; }
+      return;
     }
-    float4 x0[U], x1[U];
+    const float cnt = (float)(cend - cbeg);
+    const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
+    const bool is_bias = col == reg_skip;
+    if (q == 0 && (upd_w || is_bias)) {
+      const float wi = w[col];
+      w[col] = wi - lri * (glin + (is_bias ? 0.f : cnt * l2w * wi));
+    }
+    if (fa < 0 || (is_bias && !bias_latent)) return;
+    const float dec = is_bias ? 0.f : cnt * l2v;
+    float4* vr = reinterpret_cast<float4*>(V) + (long long)col * J4;
+    if (has0) {
+      float4* p = vr + lf0;
+      const float4 v = *p;
+      *p = make_float4(v.x - lri * (a0.x + dec * v.x), v.y - lri * (a0.y + dec * v.y),
+                       v.z - lri * (a0.z + dec * v.z), v.w - lri * (a0.w + dec * v.w));
+    }
+    if (has1) {
+      float4* p = vr + lf1;
+      const float4 v = *p;
+      *p = make_float4(v.x - lri * (a1.x + dec * v.x), v.y - lri * (a1.y + dec * v.y),
+                       v.z - lri * (a1.z + dec * v.z), v.w - lri * (a1.w + dec * v.w));
+    }
+  };
+  for (long long wb = E0; wb < E1; wb += GL) {
+    const int n = (int)min<long long>(GL, E1 - wb);
+    int prL = -1;
+    float scL = 0.f, xL = 0.f;
+    if (q < n) {
+      prL = csc_perm[wb + q];
+      xL = csc_vals[wb + q];
+      scL = coef[csc_rows[wb + q]];
+    }
+    for (int i = 0; i < n; i += U) {
+      int pr[U];
+      float sc[U], xv[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (fa >= 0 && pr[u] >= 0) {
-        const float4* row = E + (long long)pr[u] * m;
-        if (has0) x0[u] = row[q];
-        if (has1) x1[u] = row[q + GL];
+      for (int u = 0; u < U; ++u) {
+        const int src = min(i + u, n - 1);
+        pr[u] = __shfl(prL, src, GL);
+        sc[u] = __shfl(scL, src, GL);
+        xv[u] = __shfl(xL, src, GL);
+      }
+      float4 x0[U], x1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i + u < n) {
+          const float4* row = E + (long long)pr[u] * m;
+          if (has0) x0[u] = row[q];
+          if (has1) x1[u] = row[q + GL];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i + u >= n) break;  // group-uniform
+        const long long e = wb + i + u;
+        while (e >= cend) {  // the entry opens the next chunk(s)
+          flush();
+          ++ci;
+          cbeg = cend;
+          cend = __shfl(my_e1, ci, GL);
+          a0 = a1 = make_float4(0.f, 0.f, 0.f, 0.f);
+          glin = 0.f;
+        }
+        glin += sc[u] * xv[u];
+        a0.x += sc[u] * x0[u].x; a0.y += sc[u] * x0[u].y; a0.z += sc[u] * x0[u].z; a0.w += sc[u] * x0[u].w;
+        a1.x += sc[u] * x1[u].x; a1.y += sc[u] * x1[u].y; a1.z += sc[u] * x1[u].z; a1.w += sc[u] * x1[u].w;
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      glin += sc[u] * xv[u];
-      a0.x += sc[u] * x0[u].x; a0.y += sc[u] * x0[u].y; a0.z += sc[u] * x0[u].z; a0.w += sc[u] * x0[u].w;
-      a1.x += sc[u] * x1[u].x; a1.y += sc[u] * x1[u].y; a1.z += sc[u] * x1[u].z; a1.w += sc[u] * x1[u].w;
-    }
   }
-  const long long J4 = m;  // float4 slots per feature (nfield == m, k == 4)
-  if (!solo[g]) {
-    float4* out = reinterpret_cast<float4*>(lat) + g * J4;
-    if (has0) out[lay_field[q]] = a0;
-    if (has1) out[lay_field[q + GL]] = a1;
-    if (q == 0) { lin[2 * g] = glin; lin[2 * g + 1] = 0.f; }
-    return;
-  }
-  const int col = chunk_col[g];
-  const float cnt = (float)(e1 - e0);
-  const float lri = avg ? lr / fmaxf(cnt, 1.f) : lr;
-  const bool is_bias = col == reg_skip;
-  if (q == 0 && (upd_w || is_bias)) {
-    const float wi = w[col];
-    w[col] = wi - lri * (glin + (is_bias ? 0.f : cnt * l2w * wi));
-  }
-  if (fa < 0 || (is_bias && !bias_latent)) return;
-  const float dec = is_bias ? 0.f : cnt * l2v;
-  float4* vr = reinterpret_cast<float4*>(V) + (long long)col * J4;
-  if (has0) {
-    float4* p = vr + lay_field[q];
-    const float4 v = *p;
-    *p = make_float4(v.x - lri * (a0.x + dec * v.x), v.y - lri * (a0.y + dec * v.y), v.z - lri * (a0.z + dec * v.z),
-                     v.w - lri * (a0.w + dec * v.w));
-  }
-  if (has1) {
-    float4* p = vr + lay_field[q + GL];
-    const float4 v = *p;
-    *p = make_float4(v.x - lri * (a1.x + dec * v.x), v.y - lri * (a1.y + dec * v.y), v.z - lri * (a1.z + dec * v.z),
-                     v.w - lri * (a1.w + dec * v.w));
-  }
+  flush();
 }
 
 }  // namespace ytk
@@ -925,7 +964,7 @@ void ytk_ffm_sgd_ecol(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
   if (nch <= 0) return;
   if (m < 1 || m > 64) throw std::invalid_argument("ffm_sgd_ecol: need 1 <= m <= 64");
   if ((E & 15) || (lat & 15) || (V & 15)) throw std::invalid_argument("ffm_sgd_ecol: E / lat / V must be 16-B aligned");
-  hipLaunchKernelGGL(ffm_sgd_ecol_kernel, dim3((unsigned)((nch * 32 + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(ffm_sgd_ecol_kernel, dim3((unsigned)(((nch + kEcolCpg - 1) / kEcolCpg * 32 + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), (const long long*)chunk_beg, (const long long*)chunk_end,
                      nch, (const int*)csc_rows, (const float*)csc_vals, (const int*)csc_perm, (const int*)chunk_fa,
                      (const int*)chunk_col, (const unsigned char*)solo, (const float4*)E, m, (const int*)lay_field,
