@@ -199,15 +199,38 @@ class GBSTModel(ContinuousModelBase):
             cache[key] = torch.lgamma(d.y[:, 0].double() + 1.0).contiguous()
         return cache[key]
 
+    def _row_ld(self) -> int:
+        """Row pitch (floats) of W, A and D in the fused path: the gate / expert row of
+        2K - 1 floats padded to a line multiple (31 -> 32: a 124-B row straddles two 128-B
+        lines at 31 of every 32 offsets, so every SpMM gather fetched two lines); the model
+        vector keeps its [F][stride] layout (YTK_GBST_PAD=0: unpadded)."""
+        J = self.stride
+        if os.environ.get("YTK_GBST_PAD", "1") == "0" or J < 6:
+            return J
+        p = 8
+        while p < J and p < 32:
+            p <<= 1
+        return p if J <= 32 else -(-J // 32) * 32
+
     def _forward_fused(self, X, d, z, w, g_out, train: bool):
         from ...ops._ext import hip, ptr, stream
         fmask = self.fmask
-        A = X.matmul(self._masked_W(w, fmask).contiguous())  # float32 [n, stride] (segmented SpMM)
+        J, ld = self.stride, self._row_ld()
+        Wm = self._masked_W(w, fmask)
+        if ld != J:  # line-aligned rows: W copied into a padded buffer, A and D pitched alike
+            Wp = self.__dict__.get("_wpad")
+            if Wp is None or Wp.shape != (self.F, ld) or Wp.device != Wm.device:
+                Wp = self._wpad = torch.zeros((self.F, ld), dtype=torch.float32, device=Wm.device)
+            Wp[:, :J].copy_(Wm)
+            A = torch.empty((X.n, ld), dtype=torch.float32, device=Wm.device)[:, :J]
+            X.matmul(Wp[:, :J], out=A)  # float32 [n, stride], row pitch ld (segmented SpMM)
+        else:
+            A = X.matmul(Wm.contiguous())  # float32 [n, stride] (segmented SpMM)
         n, K = A.shape[0], self.K
         acc = torch.zeros(2 + 2 * K, dtype=torch.float64, device=A.device)
         pred = torch.empty(n, dtype=torch.float32, device=A.device)
         want = g_out is not None
-        D = torch.empty((n, self.stride), dtype=torch.float32, device=A.device) if want else None
+        D = torch.empty((n, ld), dtype=torch.float32, device=A.device)[:, :J] if want else None
         y = d.y[:, 0].contiguous()
         wt = d.weight.contiguous()
         mask = self.rmask.view(torch.uint8) if train else None
@@ -215,7 +238,7 @@ class GBSTModel(ContinuousModelBase):
         hip().gbst_epilogue(ptr(A), A.stride(0), ptr(z), ptr(y), ptr(wt), ptr(mask), float(1.0 / self.rate),
                             ptr(leaves), n, K, 1 if self.gate_kind == "tree" else 0,
                             1 if self.expert_kind == "linear" else 0, GBST_LOSS_IDS[self.loss.name],
-                            float(getattr(self.loss, "delta", 0.0)), 1 if self.rf else 0, self.finished + 1, 1 if want else 0, ptr(D), self.stride,
+                            float(getattr(self.loss, "delta", 0.0)), 1 if self.rf else 0, self.finished + 1, 1 if want else 0, ptr(D), ld,
                             ptr(pred), ptr(acc), ptr(self._lgamma_y(d)) if self.loss.name == "poisson" else 0,
                             stream(A))
         if want:

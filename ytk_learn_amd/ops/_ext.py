@@ -106,14 +106,17 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
-def check_cuda(*ts):
+def check_cuda(*ts, rows_ok=()):
+    """Every tensor on the same GPU and contiguous; those in ``rows_ok`` may be row-pitched
+    2-D views (contiguous rows, any row stride >= the row length: padded row layouts)."""
     dev = None
     for t in ts:
         if t is None:
             continue
         if not t.is_cuda:
             raise ValueError("expected a GPU tensor")
-        if not t.is_contiguous():
+        pitched = any(t is r for r in rows_ok) and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]
+        if not (t.is_contiguous() or pitched):
             raise ValueError("expected a contiguous tensor")
         if dev is None:
             dev = t.device

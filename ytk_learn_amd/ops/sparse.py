@@ -220,7 +220,7 @@ class SparseMatrix:
             accumulate = False
         o2 = out.reshape(self.n, -1)
         if self.device.type == "cuda":
-            check_cuda(W2, o2, vals)
+            check_cuda(W2, o2, vals, rows_ok=(W2, o2))  # the kernels take row strides
             vp = 0 if (values is None and self.one_hot) else ptr(vals)
             fx = self._fixed_layout() if (J == 1 and values is None) else False
             if fx and W2.stride(0) == 1 and o2.stride(0) == 1:
@@ -262,7 +262,7 @@ class SparseMatrix:
         o2 = out.reshape(self.ncols, -1)
         if self.device.type == "cuda":
             csc_vals = self.csc_vals if values is None else values
-            check_cuda(D2, o2, csc_vals)
+            check_cuda(D2, o2, csc_vals, rows_ok=(D2, o2))  # the kernels take row strides
             part = torch.empty((max(self.n_chunks, 1), J), dtype=torch.float32, device=self.device)
             h = hip()
             s = stream(D2)
