@@ -114,6 +114,10 @@ void ytk_lv_scales(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_init_scales(const uintptr_t*, const int*, const float*, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void ytk_lv_tail(const uintptr_t*, const int*, const float*, int, int, int, int, uintptr_t, uintptr_t, uintptr_t, int,
                  uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void ytk_hist_fx_stage(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t,
+                       uintptr_t, uintptr_t, int);
+void ytk_lv_reduce_split(const uintptr_t*, uintptr_t, uintptr_t, int, int, int, int, uintptr_t, uintptr_t, int,
+                         const float*, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, int, int, uintptr_t, uintptr_t, int, int,
                        const float*, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
@@ -233,7 +237,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("sgd_apply", &ytk_sgd_apply);
   m.def("lv_step", [](int which, const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                       const std::vector<float>& fp, int a0, int a1, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
+    if (ptrs.size() != 27 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_step: bad argument sizes");
     ytk_lv_step(which, ptrs.data(), ip.data(), fp.data(), a0, a1, stream);
   });
@@ -241,7 +245,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                           uintptr_t coff, uintptr_t fill, int split_median, uintptr_t nfeat,
                           uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
                           uintptr_t nval, uintptr_t stream) {
-    if (ptrs.size() != 26) throw std::invalid_argument("lv_raw_tree: bad ptrs");
+    if (ptrs.size() != 27) throw std::invalid_argument("lv_raw_tree: bad ptrs");
     ytk_lv_raw_tree(ptrs.data(), max_nodes, cand, coff, fill, split_median, nfeat, nthr, nleft,
                     nright, ndefl, nval, stream);
   });
@@ -249,14 +253,14 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lv_init_scales", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                              const std::vector<float>& fp, uintptr_t mx, uintptr_t scales, uintptr_t inv,
                              uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_init_scales: bad sizes");
+    if (ptrs.size() != 27 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_init_scales: bad sizes");
     ytk_lv_init_scales(ptrs.data(), ip.data(), fp.data(), mx, scales, inv, stream);
   });
   m.def("lv_tail", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp,
                       int children, int a0, int a1, int max_nodes, uintptr_t cand, uintptr_t coff, uintptr_t fill,
                       int median, uintptr_t nfeat, uintptr_t nthr, uintptr_t nleft, uintptr_t nright, uintptr_t ndefl,
                       uintptr_t nval, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_tail: bad sizes");
+    if (ptrs.size() != 27 || ip.size() < 9 || fp.size() < 6) throw std::invalid_argument("lv_tail: bad sizes");
     ytk_lv_tail(ptrs.data(), ip.data(), fp.data(), children, a0, a1, max_nodes, cand, coff, fill, median, nfeat, nthr,
                 nleft, nright, ndefl, nval, stream);
   });
@@ -265,7 +269,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                      int count_only, int a0, int a1, int maxp, uintptr_t stream, int bin_bytes,
                                      int gh_rows) {
-    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6)
+    if (ptrs.size() != 27 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
                               max_blocks, count_only, a0, a1, maxp, stream, bin_bytes, gh_rows);
@@ -274,11 +278,20 @@ PYBIND11_MODULE(_ytk_hip, m) {
      pybind11::arg("max_blocks"), pybind11::arg("count_only"), pybind11::arg("a0"), pybind11::arg("a1"),
      pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1, pybind11::arg("gh_rows") = 0);
   m.def("split_node_grouped", &ytk_split_node_grouped);
+  m.def("hist_fx_stage", &ytk_hist_fx_stage);
+  m.def("lv_reduce_split", [](const std::vector<uintptr_t>& ptrs, uintptr_t staging, uintptr_t hist, int B, int F,
+                                int slot_base, int nslots, uintptr_t nbins_f, uintptr_t fmask, int f0,
+                                const std::vector<float>& gpf, uintptr_t inv_dev, uintptr_t counters, int zs,
+                                uintptr_t stream, uintptr_t prof) {
+    if (ptrs.size() != 27 || gpf.size() != 4) throw std::invalid_argument("lv_reduce_split: bad argument sizes");
+    ytk_lv_reduce_split(ptrs.data(), staging, hist, B, F, slot_base, nslots, nbins_f, fmask, f0, gpf.data(), inv_dev,
+                        counters, zs, stream, prof);
+  });
   m.def("lv_split_plan", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,
                               uintptr_t fmask, int f0, int nitems, const std::vector<float>& gpf, uintptr_t inv_dev,
                               uintptr_t part, uintptr_t counters, int implicit_items, int maxp, uintptr_t stream) {
-    if (ptrs.size() != 26 || ip.size() != 9 || fp.size() != 6 || gpf.size() != 4)
+    if (ptrs.size() != 27 || ip.size() != 9 || fp.size() != 6 || gpf.size() != 4)
       throw std::invalid_argument("lv_split_plan: bad argument sizes");
     ytk_lv_split_plan(ptrs.data(), ip.data(), fp.data(), hist, B, F, nbins_f, fmask, f0, nitems, gpf.data(), inv_dev,
                       part, counters, implicit_items, maxp, stream);

@@ -742,6 +742,27 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   YTK_LAUNCH_CHECK();
 }
 
+// First stage alone (block partials to ``staging``): the level engine's one-GPU gathered
+// levels reduce and split-search the partials in one launch (ytk_lv_reduce_split).
+void ytk_hist_fx_stage(uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows, uintptr_t work,
+                       int nwork, int B, uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
+                       uintptr_t stream, int gh_rows) {
+  if (nwork <= 0) return;
+  if (g_hist_fw != 32) throw std::invalid_argument("hist_fx_stage: 32-feature groups only");
+  const int groups = (F + 31) / 32;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(nwork, groups);
+  if (rows == 0)
+    launch_hist_fx<true>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, nullptr, (const int4*)work,
+                         nullptr, B, B, 1.f, 1.f, (const int*)nwork_dev, (const float*)scales_dev,
+                         (long long*)staging, nullptr);
+  else
+    launch_hist_fx<false>(grid, 0, s, (const uint8_t*)bins, stride, F, (const float2*)ghp, (const int*)rows,
+                          (const int4*)work, nullptr, B, B, 1.f, 1.f, (const int*)nwork_dev, (const float*)scales_dev,
+                          (long long*)staging, nullptr, gh_rows);
+  YTK_LAUNCH_CHECK();
+}
+
 // Fully device-driven staged histogram (leaf-wise engine): work count, slot count and
 // slot ids all live on the device; the host passes only upper bounds (max_work items,
 // the y-extent of the slot reduce). Items with w == 1 are their slot's only item and are

@@ -80,6 +80,7 @@ struct LvBufs {
   float* tval;
   long long* root_cnt;   // [0] local, [1] global
   int* part_cnt;         // per split: rows of this rank's segment (single-pass partition)
+  int* hist_first;       // per build k: first histogram item of the build's slot ([nb] = item count)
 };
 
 __device__ __forceinline__ float leaf_value(double g, double h, const LvParams& p) {
@@ -459,6 +460,12 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
   __syncthreads();
   const int nitems = block_exclusive_scan(s_small, nb, s_tmp);
   emit_all_chunks(b.hist_items, nitems, nb, s_small, s_hbeg, s_hcnt, s_hslot, ch, false);
+  // the items of build k are [s_small[k], s_small[k + 1]) (the fused reduce + split kernel
+  // reads its slot's range from here instead of scanning the work list)
+  if (b.hist_first) {
+    for (int k = tid; k < nb; k += kPlanThreads) b.hist_first[k] = s_small[k];
+    if (tid == 0) b.hist_first[nb] = nitems;
+  }
   if (tid == 0) {
     // items of the first half of the build slots (k < half/2): the multi-GPU engine
     // all-reduces that half while the second half is still being built
@@ -526,6 +533,230 @@ __global__ __launch_bounds__(kNodeThreads) void lv_split_plan_kernel(
   if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __syncthreads();
   lv_plan_split_body<KP>(p, b, 0, implicit_items);
+}
+
+// One GPU, gathered levels: the staged histogram's split-K slot reduce and the split search
+// in ONE launch (replaces hist_reduce_kernel + split_node_kernel: ~10 us per level, mostly two
+// dependent global round trips and a launch). Block (chunk, g8) x build k x z: 256 threads =
+// 32 bins x 8 features (one 128-B segment of a staged bin row per thread octet), summing the
+// build's items [hist_first[k], hist_first[k + 1]) with split-K over z into the zeroed slot
+// (exact int64 memory-side atomics, as hist_reduce_kernel). The LAST block to arrive for
+// (k, g8) -- a self-resetting counter -- searches the 8-feature group of the built child and
+// of its derived sibling (parent - built, materialised as in split_node_kernel) and writes
+// the two group records the level planner combines (split_groups = ceil(F / 8)).
+// Ordering: every wave waits for its own atomics (vmcnt) before the block barrier; thread 0
+// then releases (agent) before counting the block in, and the last block acquires before it
+// reads the slot -- the per-thread fences of a plain-store design cost +6 us per launch
+// (profiles/r2_split_plan_fusion.md).
+constexpr int kRsThreads = 1024;
+constexpr int kRsBins = kRsThreads / 8;  // bins per block (thread octet = one bin's 8 features)
+constexpr int kRsDirect = 16;            // slots with <= this many items: one z block sums them
+
+// Split search of a built node AND its derived sibling over one group of <= 8 features by one
+// 1024-thread block: the built slot (coherent loads: accumulated by memory-side atomics in
+// this launch) and the parent slot are streamed once, the derived slot (parent - built) is
+// materialised, both transposed into LDS as [node][feature][B + 1]; wave w scans feature
+// w & 7 of node w >> 3 (one DPP scan per wave -- the serial per-node, per-feature scans of
+// split_node_block with 4 waves took ~10 us per node). Same arithmetic, totals feature and
+// tie order as split_node_block, so the records are the split kernel's.
+__device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, int B, int F, int Bp,
+                                                 const int* __restrict__ nbins_f, const uint8_t* __restrict__ fmask,
+                                                 int f0, int sS, int sP, int sL, SplitOut* __restrict__ outS,
+                                                 SplitOut* __restrict__ outL, const GainParams& gp, longlong2* sh,
+                                                 int fbeg, int fend, unsigned long long* pr) {
+  const int FG = fend - fbeg;  // 1..8
+  constexpr int kW = kRsThreads / kWave;  // 16
+  __shared__ float s_chg[kW];
+  __shared__ int s_feat[kW], s_a[kW], s_b[kW];
+  __shared__ double s_gl[kW], s_hl[kW];
+  __shared__ long long s_G[2], s_H[2];
+  __shared__ int s_nb[8];
+  __shared__ uint8_t s_fm[8];
+  const int t = threadIdx.x, wid = t >> 6, l = lane_id();
+  if (t < FG) { s_nb[t] = nbins_f[fbeg + t]; s_fm[t] = fmask[fbeg + t]; }
+  const size_t slot_sz = (size_t)B * F * 2;
+  const longlong2* hS = reinterpret_cast<const longlong2*>(hist + (size_t)sS * slot_sz);
+  const longlong2* hP = reinterpret_cast<const longlong2*>(hist + (size_t)sP * slot_sz);
+  longlong2* hL = reinterpret_cast<longlong2*>(hist + (size_t)sL * slot_sz);
+  const int total = B * FG;
+  constexpr int kL = 2;  // entries per thread (B * 8 <= 2048)
+  longlong2 vs[kL], vp[kL];
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {
+    const int i = t + j * kRsThreads;
+    if (i < total) {
+      const int bin = i / FG, gi = bin * F + fbeg + (i - bin * FG);
+      vs[j] = hist_ld2<true>(hS + gi);
+      vp[j] = hP[gi];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {
+    const int i = t + j * kRsThreads;
+    if (i < total) {
+      const int bin = i / FG, fl = i - bin * FG, gi = bin * F + fbeg + fl;
+      const longlong2 d = make_longlong2(vp[j].x - vs[j].x, vp[j].y - vs[j].y);
+      hL[gi] = d;  // the derived histogram (the next level subtracts from it)
+      sh[fl * Bp + bin] = vs[j];
+      sh[(8 + fl) * Bp + bin] = d;
+    }
+  }
+  __syncthreads();
+  if (pr && t == 0) pr[3] = wall_clock64();
+  const int node = wid >> 3, fl = wid & 7;
+  const longlong2* hn = sh + node * 8 * Bp;
+  // node totals (exact int64) from the group's copy of f0, else its first feature -- waves 0
+  // and 8 compute them for their node
+  if (fl == 0) {
+    const int ft = (f0 >= fbeg && f0 < fend) ? f0 - fbeg : 0;
+    const int nb0 = s_nb[ft];
+    long long sg = 0, shh = 0;
+    for (int bin = l; bin < nb0; bin += kWave) {
+      const longlong2 q = hn[ft * Bp + bin];
+      sg += q.x;
+      shh += q.y;
+    }
+    const long long Gq = readlane64(dpp_scan_add(sg), kWave - 1), Hq = readlane64(dpp_scan_add(shh), kWave - 1);
+    if (l == 0) { s_G[node] = Gq; s_H[node] = Hq; }
+  }
+  __syncthreads();
+  if (pr && t == 0) pr[4] = wall_clock64();
+  const long long Gq = s_G[node], Hq = s_H[node];
+  const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
+  const float root_gain = (float)calc_gain(G, H, gp);
+  float best_chg = -INFINITY;
+  int best_f = 0xffff, best_a = -1, best_b = 0xffff;
+  double best_gl = 0.0, best_hl = 0.0;
+  if (fl < FG && s_fm[fl])  // wave-uniform
+    wave_feature_scan(hn + fl * Bp, s_nb[fl], fbeg + fl, Gq, Hq, root_gain, gp, best_chg, best_f, best_a, best_b,
+                      best_gl, best_hl, (pr && wid == 0) ? pr + 8 : nullptr);
+  {
+    const unsigned u = __float_as_uint(best_chg + 0.0f);
+    const unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    const unsigned long long key = ((unsigned long long)ord << 32) |
+                                   ((unsigned)(0xffff - best_f) << 16) | (unsigned)(0xffff - best_b);
+    const unsigned long long kmax = (unsigned long long)readlane64((long long)dpp_max_u64(key), kWave - 1);
+    const unsigned long long hit = __ballot(key == kmax);
+    const int src = __builtin_ctzll(hit);
+    if (l == 0) {
+      s_chg[wid] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best_chg), src));
+      s_feat[wid] = __builtin_amdgcn_readlane(best_f, src);
+      s_a[wid] = __builtin_amdgcn_readlane(best_a, src);
+      s_b[wid] = __builtin_amdgcn_readlane(best_b, src);
+    }
+    const double gl = readlane_f64(best_gl, src), hl = readlane_f64(best_hl, src);
+    if (l == 0) { s_gl[wid] = gl; s_hl[wid] = hl; }
+  }
+  if (pr && t == 0) pr[5] = wall_clock64();
+  __syncthreads();
+  if (pr && t == 0) pr[6] = wall_clock64();
+  if (l == 0 && fl == 0) {  // waves 0 and 8: the node's record
+    const int w0 = node * 8;
+    int bw = w0;
+    for (int w = w0 + 1; w < w0 + 8; ++w)
+      if (better(s_chg[w], s_feat[w], s_b[w], s_chg[bw], s_feat[bw], s_b[bw])) bw = w;
+    SplitOut o;
+    o.loss_chg = s_chg[bw];
+    o.feat = (s_feat[bw] == 0xffff) ? -1 : s_feat[bw];
+    o.bin_a = s_a[bw];
+    o.bin_b = (s_b[bw] == 0xffff) ? -1 : s_b[bw];
+    o.gl = s_gl[bw];
+    o.hl = s_hl[bw];
+    o.g = G;
+    o.h = H;
+    *(node == 0 ? outS : outL) = o;
+  }
+}
+
+// One GPU, gathered levels: the staged histogram's split-K slot reduce and the split search
+// in ONE launch (replaces hist_reduce_kernel + split_node_kernel). Block (chunk, g8) x build k
+// x z: 1024 threads = 128 bins x 8 features (one 128-B segment of a staged bin row per thread
+// octet), summing the build's items [hist_first[k], hist_first[k + 1]) with split-K over z
+// into the zeroed slot (exact int64 memory-side atomics, as hist_reduce_kernel). The LAST
+// block to arrive for (k, g8) -- a self-resetting counter -- searches the 8-feature group of
+// the built child and of its derived sibling (split_pair_block) and writes the two group
+// records the level planner combines (split_groups = ceil(F / 8)).
+// Ordering without fences: every wave waits for its own atomics (vmcnt: performed at the
+// memory side) before the block barrier and the counter atomic; the last block reads the
+// slot with coherent atomic loads. (An agent-scope release per block -- buffer_wbl2 of the
+// XCD's L2 -- cost more than the launch it saves.)
+__global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
+    LvBufs b, const long long* __restrict__ staging, long long* __restrict__ hist, int B, int F, int groups32,
+    int slot_base, const int* __restrict__ nbins_f, const uint8_t* __restrict__ fmask, int f0, GainParams gp,
+    const double* __restrict__ inv_dev, unsigned* __restrict__ counters, int nchunks, int ng8,
+    unsigned long long* __restrict__ prof, int getenv_dummy_twice) {
+  extern __shared__ __attribute__((aligned(16))) longlong2 sh_rs[];  // tail: [2][8][B + 1]
+  __shared__ int s_last;
+  // prof (optional, YTK_RS_PROF): per block [entry, counted in, tail start, tail end] wall
+  // clocks (100 MHz)
+  unsigned long long* pr = prof ? prof + 16 * ((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x)
+                                : nullptr;
+  if (pr && threadIdx.x == 0) pr[0] = wall_clock64();
+  const int k = (int)blockIdx.y;
+  const int nb = b.st[ST_N_BUILD];
+  if (k >= nb) return;  // uniform: no build in this slot
+  const int lo = b.hist_first[k], cnt = b.hist_first[k + 1] - lo;
+  const bool direct = cnt <= kRsDirect;
+  if (direct && blockIdx.z != 0) return;  // uniform; such blocks are not counted
+  const int Z = direct ? 1 : (int)gridDim.z;
+  const int g8 = (int)blockIdx.x / nchunks, ch = (int)blockIdx.x - g8 * nchunks;
+  const int t = threadIdx.x, j = t & 7;
+  const int bin = ch * kRsBins + (t >> 3), f = g8 * 8 + j;
+  const int slot = slot_base + k;
+  if (bin < B && f < F) {
+    const int E = B * 32;
+    const int fg = f >> 5, l = f & 31;
+    const longlong2* st = reinterpret_cast<const longlong2*>(staging) + (size_t)fg * E + bin * 32 + l;
+    const size_t istride = (size_t)groups32 * E;
+    long long g = 0, h = 0;
+    int it = lo + (direct ? 0 : (int)blockIdx.z);
+    const int end = lo + cnt;
+    for (; it + 7 * Z < end; it += 8 * Z) {
+      longlong2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = st[(size_t)(it + u * Z) * istride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
+    }
+    for (; it < end; it += Z) {
+      const longlong2 v = st[(size_t)it * istride];
+      g += v.x;
+      h += v.y;
+    }
+    if (g | h) {
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(hist + (((size_t)slot * B + bin) * F + f) * 2);
+      atomicAdd(o, (unsigned long long)g);
+      atomicAdd(o + 1, (unsigned long long)h);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's atomics have been performed (memory side)
+  __syncthreads();
+  if (t == 0) {
+    unsigned* c = counters + (size_t)k * ng8 + g8;
+    const unsigned target = (unsigned)(nchunks * Z);
+    const bool last = atomicAdd(c, 1u) == target - 1;
+    if (last) atomicExch(c, 0u);  // self-resetting for the next level / tree
+    s_last = last ? 1 : 0;
+    if (pr) pr[1] = wall_clock64();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (pr && threadIdx.x == 0) pr[2] = wall_clock64();
+  if (inv_dev) {
+    gp.inv_sg = inv_dev[0];
+    gp.inv_sh = inv_dev[1];
+  }
+  const int4 d = b.split_items[nb + k];  // (derived slot, parent slot, built slot, 1)
+  const int fbeg = g8 * 8, fend = min(F, fbeg + 8);
+  if (pr && getenv_dummy_twice) {  // diagnosis: a warm second pass (same results, idempotent)
+    split_pair_block(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng8 + g8,
+                     b.split_out + (size_t)(nb + k) * ng8 + g8, gp, sh_rs, fbeg, fend, nullptr);
+    __syncthreads();
+    if (threadIdx.x == 0) pr[2] = wall_clock64();
+  }
+  split_pair_block(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng8 + g8,
+                   b.split_out + (size_t)(nb + k) * ng8 + g8, gp, sh_rs, fbeg, fend, pr);
+  if (pr && threadIdx.x == 0) pr[7] = wall_clock64();
 }
 
 // Bin-threshold arrays used by the fused score/gradient kernel.
@@ -665,6 +896,7 @@ static LvBufs make_bufs(const uintptr_t* a) {
   b.tval = (float*)a[23];
   b.root_cnt = (long long*)a[24];
   b.part_cnt = (int*)a[25];
+  b.hist_first = (int*)a[26];
   return b;
 }
 
@@ -836,6 +1068,27 @@ void ytk_lv_split_plan(const uintptr_t* ptrs, const int* ip, const float* fp, ui
   else if (maxp <= 512) YTK_LVSP(512);
   else YTK_LVSP(kMaxPend);
 #undef YTK_LVSP
+  YTK_LAUNCH_CHECK();
+}
+
+// Staged histogram reduce + split search of a gathered level (lv_reduce_split_kernel): nslots
+// builds from slot_base; records [item][ceil(F / 8)]; counters: nslots * ceil(F / 8) zeroed
+// (self-resetting) words; zs: split-K factor.
+void ytk_lv_reduce_split(const uintptr_t* ptrs, uintptr_t staging, uintptr_t hist, int B, int F, int slot_base,
+                         int nslots, uintptr_t nbins_f, uintptr_t fmask, int f0, const float* gpf, uintptr_t inv_dev,
+                         uintptr_t counters, int zs, uintptr_t stream, uintptr_t prof) {
+  if (nslots <= 0) return;
+  if (B > 256 || F > kNodeMaxF) throw std::invalid_argument("lv_reduce_split: B <= 256 and F <= 256 only");
+  LvBufs b = make_bufs(ptrs);
+  if (!b.hist_first) throw std::invalid_argument("lv_reduce_split: hist_first is required");
+  const int nchunks = (B + kRsBins - 1) / kRsBins, ng8 = (F + 7) / 8, groups32 = (F + 31) / 32;
+  GainParams gp{gpf[0], gpf[1], gpf[2], gpf[3], 1.0, 1.0};
+  const size_t lds = (size_t)2 * 8 * (B + 1) * sizeof(longlong2);
+  hipLaunchKernelGGL(lv_reduce_split_kernel, dim3(nchunks * ng8, nslots, std::max(1, zs)), dim3(kRsThreads), lds,
+                     reinterpret_cast<hipStream_t>(stream), b, (const long long*)staging, (long long*)hist, B, F,
+                     groups32, slot_base, (const int*)nbins_f, (const uint8_t*)fmask, f0, gp, (const double*)inv_dev,
+                     (unsigned*)counters, nchunks, ng8, (unsigned long long*)prof,
+                     prof && getenv("YTK_RS_PROF_TWICE") ? 1 : 0);
   YTK_LAUNCH_CHECK();
 }
 

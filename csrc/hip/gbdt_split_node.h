@@ -128,6 +128,141 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(readlane64(__double_as_longlong(v), lane));
 }
 
+__device__ __forceinline__ unsigned dpp_max_u32(unsigned x) {  // lane 63 = max
+  x = max(x, (unsigned)dpp32<kShr1, 0xf>((int)x, 0));
+  x = max(x, (unsigned)dpp32<kShr2, 0xf>((int)x, 0));
+  x = max(x, (unsigned)dpp32<kShr4, 0xf>((int)x, 0));
+  x = max(x, (unsigned)dpp32<kShr8, 0xf>((int)x, 0));
+  x = max(x, (unsigned)dpp32<kBcast15, 0xa>((int)x, 0));
+  x = max(x, (unsigned)dpp32<kBcast31, 0xc>((int)x, 0));
+  return x;
+}
+// wave max of a float (NaN-free input): order-preserving unsigned map, DPP max, readlane 63
+__device__ __forceinline__ float wave_max_f32(float v) {
+  const unsigned u = __float_as_uint(v);
+  const unsigned o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const unsigned m = (unsigned)__builtin_amdgcn_readlane((int)dpp_max_u32(o), kWave - 1);
+  return __uint_as_float((m & 0x80000000u) ? (m & 0x7fffffffu) : ~m);
+}
+
+// One wave scans one feature's histogram row (LDS, bins [0, nb)): lane l owns bins 4l..4l+3,
+// DPP prefix sums of the exact int64 (g, h), and the wave's best split (better() order) over
+// the bins whose both sides hold >= mcw hessian. The gains are evaluated in double, as the
+// reference (UpdateStrategy.java:50-100) -- but two fp64 divisions per bin on every lane made
+// the scan the slowest part of a split search (~2.4-4.7 us per wave with 4 scanning waves per
+// SIMD). Without l1 / max_abs_leaf (gain = g^2 / (h + l2)) a float pass filters first:
+// |approx - exact| <= (|gain_l| + |gain_r| + |root|) 2^-20 (fp32 rounding of the inputs, the
+// fast division, the sums), so every bin within twice the wave's largest error bound (a 4x
+// margin: 2^-17 per bin) of the wave's approximate maximum -- which the exact best always is
+// -- is re-evaluated exactly, and only those. Non-finite approximations are always exact.
+__device__ __forceinline__ void wave_feature_scan(const longlong2* __restrict__ hrow, int nb, int f, long long Gq,
+                                                  long long Hq, float root_gain, const GainParams& gp,
+                                                  float& best_chg, int& best_f, int& best_a, int& best_b,
+                                                  double& best_gl, double& best_hl,
+                                                  unsigned long long* tp = nullptr) {
+  const int l = lane_id();
+  if (tp && l == 0) tp[0] = wall_clock64();
+  longlong2 q[4];
+  long long sg = 0, sh = 0;
+  int lastne = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int bin = 4 * l + k;
+    q[k] = (bin < nb) ? hrow[bin] : make_longlong2(0, 0);
+    sg += q[k].x;
+    sh += q[k].y;
+    if (q[k].x != 0 || q[k].y != 0) lastne = bin;
+  }
+  if (tp && l == 0) tp[1] = wall_clock64() + (unsigned long long)(q[0].x + q[1].x + q[2].x + q[3].x == 12345);
+  const long long ig = dpp_scan_add(sg), ih = dpp_scan_add(sh);
+  const int im = dpp_scan_max(lastne);
+  int prev = __shfl_up(im, 1, kWave);
+  if (l == 0) prev = -1;
+  long long pg = ig - sg, ph = ih - sh;
+  if (tp && l == 0) tp[2] = wall_clock64() + (unsigned long long)(prev == 12345);
+  auto exact = [&](int bin, int pv, long long pgv, long long phv) {
+    const double dgl = (double)pgv * gp.inv_sg, dhl = (double)phv * gp.inv_sh;
+    const double dgr = (double)(Gq - pgv) * gp.inv_sg, dhr = (double)(Hq - phv) * gp.inv_sh;
+    if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
+      const float chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
+      if (better(chg, f, bin, best_chg, best_f, best_b)) {
+        best_chg = chg; best_f = f; best_a = pv; best_b = bin;
+        best_gl = dgl; best_hl = dhl;
+      }
+    }
+  };
+  if (!(gp.l1 == 0.f && gp.max_abs_leaf <= 0.f)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int bin = 4 * l + k;
+      if (q[k].x != 0 || q[k].y != 0) {
+        if (prev >= 0 && ph != 0) exact(bin, prev, pg, ph);
+        pg += q[k].x;
+        ph += q[k].y;
+        prev = bin;
+      }
+    }
+    return;
+  }
+  float a[4], e[4];
+  long long pgk[4], phk[4];
+  int pvk[4];
+  bool ok[4];
+  float amax = -INFINITY, emax = 0.f;
+  const float l2f = gp.l2;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int bin = 4 * l + k;
+    ok[k] = false;
+    a[k] = -INFINITY;
+    e[k] = 0.f;
+    pgk[k] = pg;
+    phk[k] = ph;
+    pvk[k] = prev;
+    if (q[k].x != 0 || q[k].y != 0) {
+      if (prev >= 0 && ph != 0) {
+        const double dhl = (double)ph * gp.inv_sh, dhr = (double)(Hq - ph) * gp.inv_sh;
+        if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
+          const float gl = (float)((double)pg * gp.inv_sg), gr = (float)((double)(Gq - pg) * gp.inv_sg);
+          const float ga = __fdividef(gl * gl, (float)dhl + l2f), gb = __fdividef(gr * gr, (float)dhr + l2f);
+          a[k] = ga + gb - root_gain;
+          e[k] = (fabsf(ga) + fabsf(gb) + fabsf(root_gain)) * 0x1p-17f;
+          ok[k] = true;
+        }
+      }
+      pg += q[k].x;
+      ph += q[k].y;
+      prev = bin;
+    }
+    // non-finite approximations are always re-evaluated (kept out of the maxima)
+    const bool fin = __builtin_isfinite(a[k]) && __builtin_isfinite(e[k]);
+    if (fin) {
+      amax = fmaxf(amax, a[k]);
+      emax = fmaxf(emax, e[k]);
+    }
+  }
+  if (tp && l == 0) tp[3] = wall_clock64() + (unsigned long long)(amax == 12345.f);
+  const float thr = wave_max_f32(amax) - 2.f * wave_max_f32(emax);
+  if (tp && l == 0) tp[4] = wall_clock64() + (unsigned long long)(thr == 12345.f);
+  unsigned cm = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (ok[k] && !(a[k] < thr)) cm |= 1u << k;
+  // candidates one per lane per pass (a pass costs two fp64 divisions of latency for the whole
+  // wave -- typically one pass: few bins of the wave are near its maximum)
+  while (__ballot(cm != 0)) {
+    if (cm) {
+      const int k = __builtin_ctz(cm);
+      cm &= cm - 1;
+      const long long pgv = k == 0 ? pgk[0] : k == 1 ? pgk[1] : k == 2 ? pgk[2] : pgk[3];
+      const long long phv = k == 0 ? phk[0] : k == 1 ? phk[1] : k == 2 ? phk[2] : phk[3];
+      const int pv = k == 0 ? pvk[0] : k == 1 ? pvk[1] : k == 2 ? pvk[2] : pvk[3];
+      exact(4 * l + k, pv, pgv, phv);
+    }
+  }
+  if (tp && l == 0) tp[5] = wall_clock64() + (unsigned long long)(best_chg == 12345.f);
+}
+
 // The node-resident split search of one node by one kNodeThreads block: item `it`, result
 // to *out. sh_hist: dynamic LDS of F * Bp longlong2; nb/fm: per-feature bin counts and
 // feature mask (read into LDS here together with the histogram).
@@ -136,6 +271,23 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // The node totals come from the group's copy of feature f0 when the group holds it, else
 // from its first feature: every row adds its (g, h) to exactly one bin of EVERY feature, so
 // the exact int64 sums are the same for all features.
+// 16-B histogram pair; kCoh: read with device-coherent atomic loads (data just accumulated
+// by other blocks' memory-side atomics in the same launch, no acquire fence)
+template <bool kCoh>
+__device__ __forceinline__ longlong2 hist_ld2(const longlong2* p) {
+  if constexpr (kCoh) {
+    long long* q = const_cast<long long*>(reinterpret_cast<const long long*>(p));
+    return make_longlong2(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                          __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  } else {
+    return *p;
+  }
+}
+
+// kThreads: block size (1024 for the split kernels; 256 in the reduce + split tail of
+// lv_reduce_split_kernel, which searches one 8-feature group). kCoh: the built slot (hn of a
+// built item, hs of a derived one) is read with coherent loads (hist_ld2).
+template <int kThreads = kNodeThreads, bool kCoh = false>
 __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, int B, int F, int Bp,
                                                  const int* __restrict__ nbins_f,
                                                  const uint8_t* __restrict__ fmask, int f0, int4 it,
@@ -143,7 +295,7 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
                                                  longlong2* sh_hist, int fbeg = 0, int fend = -1) {
   if (fend < 0) fend = F;
   const int FG = fend - fbeg;
-  constexpr int kW = kNodeThreads / kWave;
+  constexpr int kW = kThreads / kWave;
   __shared__ float s_chg[kW];
   __shared__ int s_feat[kW], s_a[kW], s_b[kW];
   __shared__ double s_gl[kW], s_hl[kW];
@@ -167,12 +319,12 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
     longlong2 s[kNodeLoads];
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
-      const int i = t + j * kNodeThreads;
-      if (i < total) { const int gi = gidx(i); v[j] = hp[gi]; s[j] = hs[gi]; }
+      const int i = t + j * kThreads;
+      if (i < total) { const int gi = gidx(i); v[j] = hp[gi]; s[j] = hist_ld2<kCoh>(hs + gi); }
     }
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
-      const int i = t + j * kNodeThreads;
+      const int i = t + j * kThreads;
       if (i < total) {
         v[j] = make_longlong2(v[j].x - s[j].x, v[j].y - s[j].y);
         hn[gidx(i)] = v[j];
@@ -181,13 +333,13 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
   } else {
 #pragma unroll
     for (int j = 0; j < kNodeLoads; ++j) {
-      const int i = t + j * kNodeThreads;
-      if (i < total) v[j] = hn[gidx(i)];
+      const int i = t + j * kThreads;
+      if (i < total) v[j] = hist_ld2<kCoh>(hn + gidx(i));
     }
   }
 #pragma unroll
   for (int j = 0; j < kNodeLoads; ++j) {
-    const int i = t + j * kNodeThreads;
+    const int i = t + j * kThreads;
     if (i < total) {
       const int bin = i / FG, f = i - bin * FG;
       sh_hist[f * Bp + bin] = v[j];
@@ -218,45 +370,8 @@ __device__ __forceinline__ void split_node_block(long long* __restrict__ hist, i
   double best_gl = 0.0, best_hl = 0.0;
   for (int fl = wid; fl < FG; fl += kW) {
     if (!s_fm[fl]) continue;  // wave-uniform
-    const int f = fbeg + fl;  // global feature (record + tie-break order)
-    const int nb = s_nb[fl];
-    longlong2 q[4];
-    long long sg = 0, sh = 0;
-    int lastne = -1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int bin = 4 * l + k;
-      q[k] = (bin < nb) ? sh_hist[fl * Bp + bin] : make_longlong2(0, 0);
-      sg += q[k].x;
-      sh += q[k].y;
-      if (q[k].x != 0 || q[k].y != 0) lastne = bin;
-    }
-    const long long ig = dpp_scan_add(sg), ih = dpp_scan_add(sh);
-    const int im = dpp_scan_max(lastne);
-    int prev = __shfl_up(im, 1, kWave);  // exclusive: last non-empty bin of the lanes below
-    if (l == 0) prev = -1;
-    long long pg = ig - sg, ph = ih - sh;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int bin = 4 * l + k;
-      if (q[k].x != 0 || q[k].y != 0) {
-        if (prev >= 0 && ph != 0) {
-          const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
-          const double dgr = (double)(Gq - pg) * gp.inv_sg, dhr = (double)(Hq - ph) * gp.inv_sh;
-          if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
-            const float chg =
-                (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
-            if (better(chg, f, bin, best_chg, best_f, best_b)) {
-              best_chg = chg; best_f = f; best_a = prev; best_b = bin;
-              best_gl = dgl; best_hl = dhl;
-            }
-          }
-        }
-        pg += q[k].x;
-        ph += q[k].y;
-        prev = bin;
-      }
-    }
+    wave_feature_scan(sh_hist + fl * Bp, s_nb[fl], fbeg + fl, Gq, Hq, root_gain, gp, best_chg, best_f, best_a, best_b,
+                      best_gl, best_hl);
   }
   // ---- wave argmax: max of (ordered gain bits, ~feature, ~bin) == better()
   {

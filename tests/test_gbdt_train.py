@@ -157,7 +157,9 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_SPLIT_GROUPS": "1"}, {"YTK_SPLIT_GROUPS": "3"}, {"YTK_REDUCE_SPLIT": "8"},
                                  {"YTK_FUSED_TEST_TAIL": "0"}, {"YTK_TG_LDS_WALK": "0"}, {"YTK_FUSE_ROOT_HIST": "0"},
                                  {"YTK_FUSE_ROOT_HIST": "0", "YTK_DEFER_LEAF_COUNTS": "0"},
-                                 {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"}])
+                                 {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"},
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1"}, {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "1"},
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""
@@ -402,3 +404,25 @@ def test_split_groups_every_group_nonempty(monkeypatch):
     assert gops.split_groups(300, 28) == 1
     monkeypatch.setenv("YTK_SPLIT_GROUPS", "1")
     assert gops.split_groups(256, 28) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{}, {"feature_sample_rate": 0.6}, {"max_leaf_cnt": 40}])
+def test_fused_reduce_split_identical_depth6(cuda, monkeypatch, kw):
+    """The one-launch staged reduce + split search (lv_reduce_split_kernel, YTK_FUSE_REDUCE_SPLIT=1)
+    builds the trees of the separate hist_reduce + split_node launches byte for byte on a
+    depth-6 tree (split-K slots at the top levels, direct slots below)."""
+    d = _data(300000, 21, cuda)
+    out = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("YTK_FUSE_REDUCE_SPLIT", fuse)
+        p = _params("level", rounds=4, **{k: v for k, v in kw.items() if k != "max_leaf_cnt"})
+        p.tree.max_depth = 6
+        p.tree.max_leaf_cnt = kw.get("max_leaf_cnt", 64)
+        p.device_builder = True
+        tr = GBDTTrainer(p, d, _data(5000, 22, cuda))
+        tr.train()
+        assert tr.use_device_builder
+        out.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert out[0] == out[1]
+    assert out[0][0].count("leaf=") > 40

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from ...ops import gbdt as gops
+from ...ops import _ext
 from ...ops._ext import CUR_STRIDE, DONE_WORDS, hip, hist_cols, ptr, stream
 from ...parallel import peer as peer_mod
 from ...parallel.comm import Comm
@@ -205,12 +206,34 @@ class DeviceLevelBuilder:
         self.hist_items = i32(self.max_items * 4)
         self.split_items = i32(2 * self.maxp * 4)
         self.item_nid = i32(2 * self.maxp)
+        self.hist_first = i32(self.maxp + 2)  # per build: first histogram item (+ the item count)
         # feature groups per node in the split search (one block per (node, group), each on
         # its own CU; the planner keeps each node's best record): YTK_SPLIT_GROUPS, default 4.
         # The owner-computes mode and the fused split + plan kernel write one record per node.
         self.owner = self.comm.is_dist and resolve_hist_sync(p.hist_sync, B * F * 2 * 8) == "owner"
         self.split_groups = (gops.split_groups(B, F) if not (self.owner or self.wide or self.fuse_split_plan)
                              else 1)
+        # one GPU, uint8 bins: every gathered level's staged slot reduce and its split search run
+        # as ONE launch (lv_reduce_split_kernel: the last reduce block of each (build, 8-feature
+        # group) searches the built child and its derived sibling) -- one record per 8-feature
+        # group, so the planner combines ceil(F / 8) records per node (opt-in: YTK_FUSE_REDUCE_SPLIT=1; default
+        # hist_reduce + split_node launches)
+        ng8 = -(-F // 8)
+        self.fuse_rs = (not self.comm.is_dist and not self.wide and not self.fuse_split_plan
+                        and bins.dtype == torch.uint8 and B <= 256 and F <= 256
+                        and os.environ.get("YTK_HIST_STAGED", "1") != "0" and _ext.HIST_FW == 32
+                        and (ng8 == 1 or (ng8 - 1) * -(-F // ng8) < F)
+                        and os.environ.get("YTK_FUSE_REDUCE_SPLIT", "0") == "1")
+        if self.fuse_rs:
+            self.rs_split = int(os.environ.get("YTK_REDUCE_SPLIT", "8"))  # split-K factor (exact sums)
+            self.split_groups = ng8
+            # YTK_RS_PROF=1: per-level block timestamps of the fused kernel (tools/dbg_rs_prof.py)
+            self.rs_prof = None
+            if os.environ.get("YTK_RS_PROF") == "1":
+                nbx = -(-B // 128) * ng8 * self.rs_split
+                self.rs_prof = [torch.zeros((self._half(max(1, c)) * nbx, 16), dtype=torch.int64, device=dev)
+                                for c in range(D)]
+            self.rs_cnt = torch.zeros(self.maxp * ng8 + 16, dtype=torch.int32, device=dev)
         self.split_out = torch.zeros(2 * self.maxp * 48 * self.split_groups, dtype=torch.uint8, device=dev)
         # split_find runs one block per (node, feature): per-feature candidates + per-item
         # arrival counters (reset by the combining block)
@@ -370,7 +393,7 @@ class DeviceLevelBuilder:
                                 self.part_begin, self.part_first, self.part_nblk, self.part_counts,
                                 self.left_loc, self.left_glob, self.hist_items, self.split_items,
                                 self.item_nid, self.split_out, self.tfeat, self.tthr, self.tleft,
-                                self.tright, self.tval, self.root_cnt, self.part_cnt)]
+                                self.tright, self.tval, self.root_cnt, self.part_cnt, self.hist_first)]
         if loc is not None:
             out[13] = loc
         if glob is not None:
@@ -734,6 +757,22 @@ class DeviceLevelBuilder:
                     work.wait()
                 self.comm.allreduce_(self.hist[base + hs:base + half + ncs])
                 tm.mark("build_hist_comm")
+            elif self.fuse_rs:
+                # block partials, then reduce + split search in one launch (no _split below)
+                if not self._zero_all:
+                    self.hist[base:base + half].zero_()
+                h.hist_fx_stage(ptr(self.bins), self.bins.shape[1], self.F, hgh, ptr(self.rows),
+                                ptr(self.hist_items), nmax, self.B, off(5), ptr(self.scales), ptr(self.staging), s,
+                                hrow)
+                tm.mark("build_hist_compute")
+                gp = self.gp
+                h.lv_reduce_split(self._ptrs(), ptr(self.staging), ptr(self.hist), self.B, self.F, base, half,
+                                  ptr(self.nbins_f), ptr(fmask), f0,
+                                  [gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"]], ptr(self.inv_scales),
+                                  ptr(self.rs_cnt), self.rs_split, s,
+                                  ptr(self.rs_prof[c]) if self.rs_prof is not None else 0)
+                tm.mark("find_best_split")
+                continue
             else:
                 build_hist(hgh, ptr(self.rows), nmax, base, half, by_row=hrow)
                 tm.mark("build_hist_compute")

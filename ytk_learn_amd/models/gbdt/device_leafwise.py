@@ -264,7 +264,7 @@ class DeviceLeafBuilder:
 
     def _lv_ptrs(self):
         """Pointer list of the level engine's finalize / raw-tree kernels (st, nodes, arrays)."""
-        out = [0] * 26
+        out = [0] * 27
         out[0], out[1] = ptr(self.st), ptr(self.tnodes)
         out[19:24] = [ptr(self.tfeat), ptr(self.tthr), ptr(self.tleft), ptr(self.tright), ptr(self.tval)]
         return out
