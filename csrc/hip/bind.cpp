@@ -117,7 +117,7 @@ void ytk_lv_tail(const uintptr_t*, const int*, const float*, int, int, int, int,
 void ytk_hist_fx_stage(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t,
                        uintptr_t, uintptr_t, int);
 void ytk_lv_reduce_split(const uintptr_t*, uintptr_t, uintptr_t, int, int, int, int, uintptr_t, uintptr_t, int,
-                         const float*, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
+                         const float*, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, int);
 void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, int, int, uintptr_t, uintptr_t, int, int,
                        const float*, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
@@ -282,10 +282,10 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lv_reduce_split", [](const std::vector<uintptr_t>& ptrs, uintptr_t staging, uintptr_t hist, int B, int F,
                                 int slot_base, int nslots, uintptr_t nbins_f, uintptr_t fmask, int f0,
                                 const std::vector<float>& gpf, uintptr_t inv_dev, uintptr_t counters, int zs,
-                                uintptr_t stream, uintptr_t prof) {
+                                uintptr_t stream, uintptr_t prof, int group) {
     if (ptrs.size() != 27 || gpf.size() != 4) throw std::invalid_argument("lv_reduce_split: bad argument sizes");
     ytk_lv_reduce_split(ptrs.data(), staging, hist, B, F, slot_base, nslots, nbins_f, fmask, f0, gpf.data(), inv_dev,
-                        counters, zs, stream, prof);
+                        counters, zs, stream, prof, group);
   });
   m.def("lv_split_plan", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip,
                               const std::vector<float>& fp, uintptr_t hist, int B, int F, uintptr_t nbins_f,

@@ -549,7 +549,6 @@ __global__ __launch_bounds__(kNodeThreads) void lv_split_plan_kernel(
 // reads the slot -- the per-thread fences of a plain-store design cost +6 us per launch
 // (profiles/r2_split_plan_fusion.md).
 constexpr int kRsThreads = 1024;
-constexpr int kRsBins = kRsThreads / 8;  // bins per block (thread octet = one bin's 8 features)
 constexpr int kRsDirect = 16;            // slots with <= this many items: one z block sums them
 
 // Split search of a built node AND its derived sibling over one group of <= 8 features by one
@@ -559,19 +558,20 @@ constexpr int kRsDirect = 16;            // slots with <= this many items: one z
 // w & 7 of node w >> 3 (one DPP scan per wave -- the serial per-node, per-feature scans of
 // split_node_block with 4 waves took ~10 us per node). Same arithmetic, totals feature and
 // tie order as split_node_block, so the records are the split kernel's.
+template <int GF>
 __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, int B, int F, int Bp,
                                                  const int* __restrict__ nbins_f, const uint8_t* __restrict__ fmask,
                                                  int f0, int sS, int sP, int sL, SplitOut* __restrict__ outS,
                                                  SplitOut* __restrict__ outL, const GainParams& gp, longlong2* sh,
                                                  int fbeg, int fend, unsigned long long* pr) {
-  const int FG = fend - fbeg;  // 1..8
+  const int FG = fend - fbeg;  // 1..GF
   constexpr int kW = kRsThreads / kWave;  // 16
   __shared__ float s_chg[kW];
   __shared__ int s_feat[kW], s_a[kW], s_b[kW];
   __shared__ double s_gl[kW], s_hl[kW];
   __shared__ long long s_G[2], s_H[2];
-  __shared__ int s_nb[8];
-  __shared__ uint8_t s_fm[8];
+  __shared__ int s_nb[GF];
+  __shared__ uint8_t s_fm[GF];
   const int t = threadIdx.x, wid = t >> 6, l = lane_id();
   if (t < FG) { s_nb[t] = nbins_f[fbeg + t]; s_fm[t] = fmask[fbeg + t]; }
   const size_t slot_sz = (size_t)B * F * 2;
@@ -579,7 +579,7 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
   const longlong2* hP = reinterpret_cast<const longlong2*>(hist + (size_t)sP * slot_sz);
   longlong2* hL = reinterpret_cast<longlong2*>(hist + (size_t)sL * slot_sz);
   const int total = B * FG;
-  constexpr int kL = 2;  // entries per thread (B * 8 <= 2048)
+  constexpr int kL = (256 * GF + kRsThreads - 1) / kRsThreads;  // entries per thread (B <= 256)
   longlong2 vs[kL], vp[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) {
@@ -598,16 +598,17 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
       const longlong2 d = make_longlong2(vp[j].x - vs[j].x, vp[j].y - vs[j].y);
       hL[gi] = d;  // the derived histogram (the next level subtracts from it)
       sh[fl * Bp + bin] = vs[j];
-      sh[(8 + fl) * Bp + bin] = d;
+      sh[(GF + fl) * Bp + bin] = d;
     }
   }
   __syncthreads();
   if (pr && t == 0) pr[3] = wall_clock64();
-  const int node = wid >> 3, fl = wid & 7;
-  const longlong2* hn = sh + node * 8 * Bp;
+  // wave w: node w / GF, feature w % GF (waves >= 2G idle in the scan)
+  const int node = min(wid / GF, 1), fl = wid < 2 * GF ? wid % GF : GF;
+  const longlong2* hn = sh + node * GF * Bp;
   // node totals (exact int64) from the group's copy of f0, else its first feature -- waves 0
   // and 8 compute them for their node
-  if (fl == 0) {
+  if (fl == 0 && wid < 2 * GF) {
     const int ft = (f0 >= fbeg && f0 < fend) ? f0 - fbeg : 0;
     const int nb0 = s_nb[ft];
     long long sg = 0, shh = 0;
@@ -622,8 +623,8 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
   __syncthreads();
   if (pr && t == 0) pr[4] = wall_clock64();
   const long long Gq = s_G[node], Hq = s_H[node];
-  const double G = (double)Gq * gp.inv_sg, H = (double)Hq * gp.inv_sh;
-  const float root_gain = (float)calc_gain(G, H, gp);
+  const double Gd = (double)Gq * gp.inv_sg, Hd = (double)Hq * gp.inv_sh;
+  const float root_gain = (float)calc_gain(Gd, Hd, gp);
   float best_chg = -INFINITY;
   int best_f = 0xffff, best_a = -1, best_b = 0xffff;
   double best_gl = 0.0, best_hl = 0.0;
@@ -650,10 +651,10 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
   if (pr && t == 0) pr[5] = wall_clock64();
   __syncthreads();
   if (pr && t == 0) pr[6] = wall_clock64();
-  if (l == 0 && fl == 0) {  // waves 0 and 8: the node's record
-    const int w0 = node * 8;
+  if (l == 0 && fl == 0 && wid < 2 * GF) {  // waves 0 and GF: the node's record
+    const int w0 = node * GF;
     int bw = w0;
-    for (int w = w0 + 1; w < w0 + 8; ++w)
+    for (int w = w0 + 1; w < w0 + GF; ++w)
       if (better(s_chg[w], s_feat[w], s_b[w], s_chg[bw], s_feat[bw], s_b[bw])) bw = w;
     SplitOut o;
     o.loss_chg = s_chg[bw];
@@ -662,8 +663,8 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
     o.bin_b = (s_b[bw] == 0xffff) ? -1 : s_b[bw];
     o.gl = s_gl[bw];
     o.hl = s_hl[bw];
-    o.g = G;
-    o.h = H;
+    o.g = Gd;
+    o.h = Hd;
     *(node == 0 ? outS : outL) = o;
   }
 }
@@ -680,10 +681,11 @@ __device__ __forceinline__ void split_pair_block(long long* __restrict__ hist, i
 // memory side) before the block barrier and the counter atomic; the last block reads the
 // slot with coherent atomic loads. (An agent-scope release per block -- buffer_wbl2 of the
 // XCD's L2 -- cost more than the launch it saves.)
+template <int G>
 __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
     LvBufs b, const long long* __restrict__ staging, long long* __restrict__ hist, int B, int F, int groups32,
     int slot_base, const int* __restrict__ nbins_f, const uint8_t* __restrict__ fmask, int f0, GainParams gp,
-    const double* __restrict__ inv_dev, unsigned* __restrict__ counters, int nchunks, int ng8,
+    const double* __restrict__ inv_dev, unsigned* __restrict__ counters, int nchunks, int ng,
     unsigned long long* __restrict__ prof, int getenv_dummy_twice) {
   extern __shared__ __attribute__((aligned(16))) longlong2 sh_rs[];  // tail: [2][8][B + 1]
   __shared__ int s_last;
@@ -699,9 +701,10 @@ __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
   const bool direct = cnt <= kRsDirect;
   if (direct && blockIdx.z != 0) return;  // uniform; such blocks are not counted
   const int Z = direct ? 1 : (int)gridDim.z;
+  constexpr int kBins = kRsThreads / G;  // bins per block (G consecutive threads: one bin row segment)
   const int g8 = (int)blockIdx.x / nchunks, ch = (int)blockIdx.x - g8 * nchunks;
-  const int t = threadIdx.x, j = t & 7;
-  const int bin = ch * kRsBins + (t >> 3), f = g8 * 8 + j;
+  const int t = threadIdx.x, j = t % G;
+  const int bin = ch * kBins + t / G, f = g8 * G + j;
   const int slot = slot_base + k;
   if (bin < B && f < F) {
     const int E = B * 32;
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
   __builtin_amdgcn_s_waitcnt(0);  // this wave's atomics have been performed (memory side)
   __syncthreads();
   if (t == 0) {
-    unsigned* c = counters + (size_t)k * ng8 + g8;
+    unsigned* c = counters + (size_t)k * ng + g8;
     const unsigned target = (unsigned)(nchunks * Z);
     const bool last = atomicAdd(c, 1u) == target - 1;
     if (last) atomicExch(c, 0u);  // self-resetting for the next level / tree
@@ -747,15 +750,15 @@ __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
     gp.inv_sh = inv_dev[1];
   }
   const int4 d = b.split_items[nb + k];  // (derived slot, parent slot, built slot, 1)
-  const int fbeg = g8 * 8, fend = min(F, fbeg + 8);
+  const int fbeg = g8 * G, fend = min(F, fbeg + G);
   if (pr && getenv_dummy_twice) {  // diagnosis: a warm second pass (same results, idempotent)
-    split_pair_block(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng8 + g8,
-                     b.split_out + (size_t)(nb + k) * ng8 + g8, gp, sh_rs, fbeg, fend, nullptr);
+    split_pair_block<G>(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng + g8,
+                        b.split_out + (size_t)(nb + k) * ng + g8, gp, sh_rs, fbeg, fend, nullptr);
     __syncthreads();
     if (threadIdx.x == 0) pr[2] = wall_clock64();
   }
-  split_pair_block(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng8 + g8,
-                   b.split_out + (size_t)(nb + k) * ng8 + g8, gp, sh_rs, fbeg, fend, pr);
+  split_pair_block<G>(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng + g8,
+                      b.split_out + (size_t)(nb + k) * ng + g8, gp, sh_rs, fbeg, fend, pr);
   if (pr && threadIdx.x == 0) pr[7] = wall_clock64();
 }
 
@@ -1076,19 +1079,28 @@ void ytk_lv_split_plan(const uintptr_t* ptrs, const int* ip, const float* fp, ui
 // (self-resetting) words; zs: split-K factor.
 void ytk_lv_reduce_split(const uintptr_t* ptrs, uintptr_t staging, uintptr_t hist, int B, int F, int slot_base,
                          int nslots, uintptr_t nbins_f, uintptr_t fmask, int f0, const float* gpf, uintptr_t inv_dev,
-                         uintptr_t counters, int zs, uintptr_t stream, uintptr_t prof) {
+                         uintptr_t counters, int zs, uintptr_t stream, uintptr_t prof, int group) {
   if (nslots <= 0) return;
   if (B > 256 || F > kNodeMaxF) throw std::invalid_argument("lv_reduce_split: B <= 256 and F <= 256 only");
   LvBufs b = make_bufs(ptrs);
   if (!b.hist_first) throw std::invalid_argument("lv_reduce_split: hist_first is required");
-  const int nchunks = (B + kRsBins - 1) / kRsBins, ng8 = (F + 7) / 8, groups32 = (F + 31) / 32;
+  const int groups32 = (F + 31) / 32;
   GainParams gp{gpf[0], gpf[1], gpf[2], gpf[3], 1.0, 1.0};
-  const size_t lds = (size_t)2 * 8 * (B + 1) * sizeof(longlong2);
-  hipLaunchKernelGGL(lv_reduce_split_kernel, dim3(nchunks * ng8, nslots, std::max(1, zs)), dim3(kRsThreads), lds,
-                     reinterpret_cast<hipStream_t>(stream), b, (const long long*)staging, (long long*)hist, B, F,
-                     groups32, slot_base, (const int*)nbins_f, (const uint8_t*)fmask, f0, gp, (const double*)inv_dev,
-                     (unsigned*)counters, nchunks, ng8, (unsigned long long*)prof,
-                     prof && getenv("YTK_RS_PROF_TWICE") ? 1 : 0);
+  const int twice = prof && getenv("YTK_RS_PROF_TWICE") ? 1 : 0;
+#define YTK_RS(GS)                                                                                                \
+  do {                                                                                                            \
+    const int nchunks = (B + kRsThreads / GS - 1) / (kRsThreads / GS), ng = (F + GS - 1) / GS;                    \
+    const size_t lds = (size_t)2 * GS * (B + 1) * sizeof(longlong2);                                             \
+    hipLaunchKernelGGL((lv_reduce_split_kernel<GS>), dim3(nchunks * ng, nslots, std::max(1, zs)), dim3(kRsThreads), \
+                       lds, reinterpret_cast<hipStream_t>(stream), b, (const long long*)staging, (long long*)hist, B, F, \
+                       groups32, slot_base, (const int*)nbins_f, (const uint8_t*)fmask, f0, gp, (const double*)inv_dev, \
+                       (unsigned*)counters, nchunks, ng, (unsigned long long*)prof, twice);                          \
+  } while (0)
+  if (group == 8) YTK_RS(8);
+  else if (group == 4) YTK_RS(4);
+  else if (group == 2) YTK_RS(2);
+  else throw std::invalid_argument("lv_reduce_split: group must be 2, 4 or 8");
+#undef YTK_RS
   YTK_LAUNCH_CHECK();
 }
 

@@ -128,33 +128,12 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(readlane64(__double_as_longlong(v), lane));
 }
 
-__device__ __forceinline__ unsigned dpp_max_u32(unsigned x) {  // lane 63 = max
-  x = max(x, (unsigned)dpp32<kShr1, 0xf>((int)x, 0));
-  x = max(x, (unsigned)dpp32<kShr2, 0xf>((int)x, 0));
-  x = max(x, (unsigned)dpp32<kShr4, 0xf>((int)x, 0));
-  x = max(x, (unsigned)dpp32<kShr8, 0xf>((int)x, 0));
-  x = max(x, (unsigned)dpp32<kBcast15, 0xa>((int)x, 0));
-  x = max(x, (unsigned)dpp32<kBcast31, 0xc>((int)x, 0));
-  return x;
-}
-// wave max of a float (NaN-free input): order-preserving unsigned map, DPP max, readlane 63
-__device__ __forceinline__ float wave_max_f32(float v) {
-  const unsigned u = __float_as_uint(v);
-  const unsigned o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  const unsigned m = (unsigned)__builtin_amdgcn_readlane((int)dpp_max_u32(o), kWave - 1);
-  return __uint_as_float((m & 0x80000000u) ? (m & 0x7fffffffu) : ~m);
-}
-
 // One wave scans one feature's histogram row (LDS, bins [0, nb)): lane l owns bins 4l..4l+3,
 // DPP prefix sums of the exact int64 (g, h), and the wave's best split (better() order) over
-// the bins whose both sides hold >= mcw hessian. The gains are evaluated in double, as the
-// reference (UpdateStrategy.java:50-100) -- but two fp64 divisions per bin on every lane made
-// the scan the slowest part of a split search (~2.4-4.7 us per wave with 4 scanning waves per
-// SIMD). Without l1 / max_abs_leaf (gain = g^2 / (h + l2)) a float pass filters first:
-// |approx - exact| <= (|gain_l| + |gain_r| + |root|) 2^-20 (fp32 rounding of the inputs, the
-// fast division, the sums), so every bin within twice the wave's largest error bound (a 4x
-// margin: 2^-17 per bin) of the wave's approximate maximum -- which the exact best always is
-// -- is re-evaluated exactly, and only those. Non-finite approximations are always exact.
+// the bins whose both sides hold >= mcw hessian, gains in double as the reference
+// (UpdateStrategy.java:50-100). (A float pre-filter that evaluated only near-maximal bins in
+// double was tried and measured no faster: the scan is latency bound, not fp64 bound --
+// docs/performance.md, round 5.) tp (optional): wave-0 timestamps for tools/dbg_rs_prof.py.
 __device__ __forceinline__ void wave_feature_scan(const longlong2* __restrict__ hrow, int nb, int f, long long Gq,
                                                   long long Hq, float root_gain, const GainParams& gp,
                                                   float& best_chg, int& best_f, int& best_a, int& best_b,
@@ -173,94 +152,33 @@ __device__ __forceinline__ void wave_feature_scan(const longlong2* __restrict__ 
     sh += q[k].y;
     if (q[k].x != 0 || q[k].y != 0) lastne = bin;
   }
-  if (tp && l == 0) tp[1] = wall_clock64() + (unsigned long long)(q[0].x + q[1].x + q[2].x + q[3].x == 12345);
   const long long ig = dpp_scan_add(sg), ih = dpp_scan_add(sh);
   const int im = dpp_scan_max(lastne);
   int prev = __shfl_up(im, 1, kWave);
   if (l == 0) prev = -1;
   long long pg = ig - sg, ph = ih - sh;
-  if (tp && l == 0) tp[2] = wall_clock64() + (unsigned long long)(prev == 12345);
-  auto exact = [&](int bin, int pv, long long pgv, long long phv) {
-    const double dgl = (double)pgv * gp.inv_sg, dhl = (double)phv * gp.inv_sh;
-    const double dgr = (double)(Gq - pgv) * gp.inv_sg, dhr = (double)(Hq - phv) * gp.inv_sh;
-    if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
-      const float chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
-      if (better(chg, f, bin, best_chg, best_f, best_b)) {
-        best_chg = chg; best_f = f; best_a = pv; best_b = bin;
-        best_gl = dgl; best_hl = dhl;
-      }
-    }
-  };
-  if (!(gp.l1 == 0.f && gp.max_abs_leaf <= 0.f)) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int bin = 4 * l + k;
-      if (q[k].x != 0 || q[k].y != 0) {
-        if (prev >= 0 && ph != 0) exact(bin, prev, pg, ph);
-        pg += q[k].x;
-        ph += q[k].y;
-        prev = bin;
-      }
-    }
-    return;
-  }
-  float a[4], e[4];
-  long long pgk[4], phk[4];
-  int pvk[4];
-  bool ok[4];
-  float amax = -INFINITY, emax = 0.f;
-  const float l2f = gp.l2;
+  if (tp && l == 0) tp[1] = wall_clock64() + (unsigned long long)(prev == 12345);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int bin = 4 * l + k;
-    ok[k] = false;
-    a[k] = -INFINITY;
-    e[k] = 0.f;
-    pgk[k] = pg;
-    phk[k] = ph;
-    pvk[k] = prev;
     if (q[k].x != 0 || q[k].y != 0) {
       if (prev >= 0 && ph != 0) {
-        const double dhl = (double)ph * gp.inv_sh, dhr = (double)(Hq - ph) * gp.inv_sh;
+        const double dgl = (double)pg * gp.inv_sg, dhl = (double)ph * gp.inv_sh;
+        const double dgr = (double)(Gq - pg) * gp.inv_sg, dhr = (double)(Hq - ph) * gp.inv_sh;
         if (dhl >= (double)gp.mcw && dhr >= (double)gp.mcw) {
-          const float gl = (float)((double)pg * gp.inv_sg), gr = (float)((double)(Gq - pg) * gp.inv_sg);
-          const float ga = __fdividef(gl * gl, (float)dhl + l2f), gb = __fdividef(gr * gr, (float)dhr + l2f);
-          a[k] = ga + gb - root_gain;
-          e[k] = (fabsf(ga) + fabsf(gb) + fabsf(root_gain)) * 0x1p-17f;
-          ok[k] = true;
+          const float chg = (float)(calc_gain(dgl, dhl, gp) + calc_gain(dgr, dhr, gp) - (double)root_gain);
+          if (better(chg, f, bin, best_chg, best_f, best_b)) {
+            best_chg = chg; best_f = f; best_a = prev; best_b = bin;
+            best_gl = dgl; best_hl = dhl;
+          }
         }
       }
       pg += q[k].x;
       ph += q[k].y;
       prev = bin;
     }
-    // non-finite approximations are always re-evaluated (kept out of the maxima)
-    const bool fin = __builtin_isfinite(a[k]) && __builtin_isfinite(e[k]);
-    if (fin) {
-      amax = fmaxf(amax, a[k]);
-      emax = fmaxf(emax, e[k]);
-    }
   }
-  if (tp && l == 0) tp[3] = wall_clock64() + (unsigned long long)(amax == 12345.f);
-  const float thr = wave_max_f32(amax) - 2.f * wave_max_f32(emax);
-  if (tp && l == 0) tp[4] = wall_clock64() + (unsigned long long)(thr == 12345.f);
-  unsigned cm = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (ok[k] && !(a[k] < thr)) cm |= 1u << k;
-  // candidates one per lane per pass (a pass costs two fp64 divisions of latency for the whole
-  // wave -- typically one pass: few bins of the wave are near its maximum)
-  while (__ballot(cm != 0)) {
-    if (cm) {
-      const int k = __builtin_ctz(cm);
-      cm &= cm - 1;
-      const long long pgv = k == 0 ? pgk[0] : k == 1 ? pgk[1] : k == 2 ? pgk[2] : pgk[3];
-      const long long phv = k == 0 ? phk[0] : k == 1 ? phk[1] : k == 2 ? phk[2] : phk[3];
-      const int pv = k == 0 ? pvk[0] : k == 1 ? pvk[1] : k == 2 ? pvk[2] : pvk[3];
-      exact(4 * l + k, pv, pgv, phv);
-    }
-  }
-  if (tp && l == 0) tp[5] = wall_clock64() + (unsigned long long)(best_chg == 12345.f);
+  if (tp && l == 0) tp[2] = wall_clock64() + (unsigned long long)(best_chg == 12345.f);
 }
 
 // The node-resident split search of one node by one kNodeThreads block: item `it`, result

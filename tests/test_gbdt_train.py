@@ -159,7 +159,9 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_FUSE_ROOT_HIST": "0", "YTK_DEFER_LEAF_COUNTS": "0"},
                                  {"YTK_PART_CHUNK": "4096", "YTK_FUSE_SPLIT_PLAN": "1"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1"}, {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "1"},
-                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"}])
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"},
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "8"},
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""

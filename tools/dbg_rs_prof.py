@@ -57,6 +57,6 @@ for c, t in enumerate(b.rs_prof):
         msg += (f" | tails {len(tails)}: start p50 {np.median(tb):.2f} max {tb.max():.2f}, search {np.median(t2):.2f}"
                 f" (max {t2.max():.2f}) = load {ph[0]:.2f} + totals {ph[1]:.2f} + scan {ph[2]:.2f} + barrier {ph[3]:.2f}"
                 f" + record {ph[4]:.2f}, last end {end.max():.2f} us")
-        sc = [np.median((tails[:, 9 + i] - tails[:, 8 + i]) / 100.0) for i in range(5)]
-        msg += ("\n   wave-0 scan: lds %.2f dpp %.2f float %.2f wmax %.2f exact %.2f" % tuple(sc))
+        sc = [np.median((tails[:, 9 + i] - tails[:, 8 + i]) / 100.0) for i in range(2)]
+        msg += ("\n   wave-0 scan: loads + prefix scans %.2f, gains %.2f" % tuple(sc))
     print(msg)

@@ -29,6 +29,12 @@ if has ab; then
     YTK_FUSE_REDUCE_SPLIT=$f run eighth_f$f 300 python bench.py --steps 50 --warmup 5 --leafwise-steps 0 $E8
   done
 fi
+if has groups; then
+  for g in 2 8; do
+    YTK_FUSE_REDUCE_SPLIT=1 YTK_RS_GROUP=$g run full_g$g 300 python bench.py --steps 50 --warmup 5 --leafwise-steps 0
+    YTK_FUSE_REDUCE_SPLIT=1 YTK_RS_GROUP=$g run eighth_g$g 300 python bench.py --steps 50 --warmup 5 --leafwise-steps 0 $E8
+  done
+fi
 if has prof; then
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_full -o run -- python $R/bench.py --steps 10 --warmup 2 --leafwise-steps 0 > $O/prof_full.log 2>&1 || { tail -20 $O/prof_full.log; exit 1; }

@@ -218,7 +218,8 @@ class DeviceLevelBuilder:
         # group) searches the built child and its derived sibling) -- one record per 8-feature
         # group, so the planner combines ceil(F / 8) records per node (opt-in: YTK_FUSE_REDUCE_SPLIT=1; default
         # hist_reduce + split_node launches)
-        ng8 = -(-F // 8)
+        self.rs_group = int(os.environ.get("YTK_RS_GROUP", "4"))  # features per tail block (2 | 4 | 8)
+        ng8 = -(-F // self.rs_group)
         self.fuse_rs = (not self.comm.is_dist and not self.wide and not self.fuse_split_plan
                         and bins.dtype == torch.uint8 and B <= 256 and F <= 256
                         and os.environ.get("YTK_HIST_STAGED", "1") != "0" and _ext.HIST_FW == 32
@@ -230,7 +231,7 @@ class DeviceLevelBuilder:
             # YTK_RS_PROF=1: per-level block timestamps of the fused kernel (tools/dbg_rs_prof.py)
             self.rs_prof = None
             if os.environ.get("YTK_RS_PROF") == "1":
-                nbx = -(-B // 128) * ng8 * self.rs_split
+                nbx = -(-B // (1024 // self.rs_group)) * ng8 * self.rs_split
                 self.rs_prof = [torch.zeros((self._half(max(1, c)) * nbx, 16), dtype=torch.int64, device=dev)
                                 for c in range(D)]
             self.rs_cnt = torch.zeros(self.maxp * ng8 + 16, dtype=torch.int32, device=dev)
@@ -770,7 +771,7 @@ class DeviceLevelBuilder:
                                   ptr(self.nbins_f), ptr(fmask), f0,
                                   [gp["mcw"], gp["l1"], gp["l2"], gp["max_abs_leaf"]], ptr(self.inv_scales),
                                   ptr(self.rs_cnt), self.rs_split, s,
-                                  ptr(self.rs_prof[c]) if self.rs_prof is not None else 0)
+                                  ptr(self.rs_prof[c]) if self.rs_prof is not None else 0, self.rs_group)
                 tm.mark("find_best_split")
                 continue
             else:
