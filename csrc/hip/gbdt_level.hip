@@ -219,9 +219,151 @@ __global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBuf
   emit_all_chunks(b.hist_items, nblk, 1, s_first, s_begin, s_count, s_tag, ch, false);
 }
 
+// Fast path of lv_plan_split_body for levels of <= kPlanThreads pending nodes whose split
+// items follow lv_plan_children_body's layout (pending [2k, 2k+1] = the children of build k;
+// item k = its built child, item nb + k = the derived one; the root: one item, one node):
+// ONE thread per pending node keeps that node in registers from its records to its
+// partition descriptor, so the dependent global round trips are st -> (pending, item_nid)
+// -> (records, node fields) instead of ~12 (node-table writes read back by other threads,
+// the chunk counts and their scan in global memory). Same decisions, same outputs.
+__device__ void lv_plan_split_fast(const LvParams& p, const LvBufs& b, int fused, int implicit_items, int nsi,
+                                   int npend, int num_nodes0, int num_leaf0, int nprev) {
+  __shared__ int s_tmp[kPlanThreads / kWave + 1];
+  __shared__ int s_cnt[kPlanThreads], s_first[kPlanThreads], s_beg[kPlanThreads];
+  __shared__ long long s_total;
+  int* st = b.st;
+  const int tid = threadIdx.x;
+  const double mcw2 = (double)p.mcw * 2.0;
+  if (fused) {  // previous level's children: global counts from the all-reduced cursors
+    const size_t cs = fused == 2 ? kCurStride : 1;
+    for (int s = tid; s < nprev; s += kPlanThreads) {
+      const DNode& P = b.nodes[b.split_nid[s]];
+      const long long lg = b.left_glob[(size_t)s * cs] & 0xffffffffll;
+      b.nodes[P.left].cnt_global = lg;
+      b.nodes[P.right].cnt_global = P.cnt_global - lg;
+    }
+    // (nothing below reads cnt_global when counts are fused: min_split_samples <= 0 there)
+  }
+  if (tid == 0) s_total = 0;
+  const bool mine = tid < npend;
+  int nid = 0, item = 0;
+  if (mine) {
+    nid = b.pending[tid];
+    const int k = tid >> 1;
+    item = b.item_nid[k] == nid ? k : (nsi >> 1) + k;
+  }
+  double G = 0.0, H = 0.0, gl = 0.0, hl = 0.0;
+  int feat = -1, bin_a = -1, bin_b = -1, depth = 0, beg = 0, cnt_local = 0;
+  long long cnt_global = 0;
+  float loss_chg = -INFINITY;
+  bool cand = false;
+  if (mine) {
+    const int ng = p.split_groups;
+    const SplitOut* rec = b.split_out + (size_t)item * ng;
+    auto fkey = [](int f) { return f < 0 ? 0x7fffffff : f; };
+    int bg = 0;
+    for (int g = 1; g < ng; ++g)
+      if (better(rec[g].loss_chg, fkey(rec[g].feat), fkey(rec[g].bin_b), rec[bg].loss_chg, fkey(rec[bg].feat),
+                 fkey(rec[bg].bin_b)))
+        bg = g;
+    const SplitOut o = rec[bg];
+    G = rec[0].g;  // node totals: identical exact sums in every group's record
+    H = rec[0].h;
+    gl = o.gl;
+    hl = o.hl;
+    feat = o.feat;
+    bin_a = o.bin_a;
+    bin_b = o.bin_b;
+    loss_chg = o.loss_chg;
+    DNode& n = b.nodes[nid];
+    cnt_global = n.cnt_global;
+    depth = n.depth;
+    beg = n.begin;
+    cnt_local = n.cnt_local;
+    if (!(H >= mcw2 && cnt_global >= (long long)p.min_split_samples)) {  // canSplit
+      loss_chg = -INFINITY;
+      feat = -1;
+    }
+    n.G = G;
+    n.H = H;
+    n.gl = gl;
+    n.hl = hl;
+    n.feat = feat;
+    n.bin_a = bin_a;
+    n.bin_b = bin_b;
+    n.loss_chg = loss_chg;
+    // pop-time leaf rules that do not depend on the running leaf count
+    cand = !(!(loss_chg > p.min_split_loss) || (p.max_depth >= 0 && p.max_depth == depth) ||
+             (p.min_split_samples > 0 && cnt_global < p.min_split_samples));
+  }
+  // FIFO leaf budget: the first (max_leaf_cnt - num_leaf0) candidates split
+  int ncand;
+  const int rank = block_scan_excl(cand ? 1 : 0, s_tmp, &ncand);
+  const int limit = (p.max_leaf_cnt > 0 && num_leaf0 <= p.max_leaf_cnt) ? p.max_leaf_cnt - num_leaf0 : 0x7fffffff;
+  const int nsplit = min(ncand, limit);
+  if (tid == 0) {
+    st[ST_PART_DONE] = 0;
+    st[ST_NUM_NODES] = num_nodes0 + 2 * nsplit;
+    st[ST_NUM_LEAF] = num_leaf0 + nsplit;
+    st[ST_N_SPLIT] = nsplit;
+  }
+  if (mine) {
+    DNode& n = b.nodes[nid];
+    const int s = (cand && rank < limit) ? rank : -1;
+    if (s < 0) {
+      n.is_leaf = 1;
+      n.value = leaf_value(G, H, p);
+    } else {
+      n.is_leaf = 0;
+      n.left = num_nodes0 + 2 * s;
+      n.right = num_nodes0 + 2 * s + 1;
+      b.split_nid[s] = nid;
+      b.split_snap[s] = num_leaf0 + s + 1;  // leaf count after this split
+      b.part_feat[s] = feat;
+      const int keep = small_only_level(p.small_only, p.max_depth, depth) ? (left_small_by_hess(hl, H) ? 1 : 2) : 0;
+      b.part_thr[s] = ((bin_a + bin_b) >> 1) | (keep << kKeepShift);  // bin <= floor((a+b)/2) <=> bin < (a+b)/2
+      b.part_begin[s] = beg;
+      b.part_cnt[s] = cnt_local;
+      b.left_loc[s] = 0;
+      b.left_loc[(size_t)s * kCurStride] = 0;  // the fused partition's line-spaced cursor
+      s_cnt[s] = cnt_local;
+      s_beg[s] = beg;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_total), (unsigned long long)cnt_local);
+    }
+  }
+  __syncthreads();
+  const long long total = s_total;
+  const int ch = (int)max((long long)p.part_chunk, (total + p.part_target - 1) / max(1, p.part_target));
+  const int nblk = tid < nsplit ? (s_cnt[tid] + ch - 1) / ch : 0;
+  int nitems;
+  const int first = block_scan_excl(nblk, s_tmp, &nitems);
+  if (tid < nsplit) {
+    b.part_first[tid] = first;
+    b.part_nblk[tid] = nblk;
+    s_first[tid] = first;
+  }
+  if (tid == 0) st[ST_N_PART] = nitems;
+  if (!implicit_items) {
+    __syncthreads();
+    emit_all_chunks(b.part_items, nitems, nsplit, s_first, s_beg, s_cnt, nullptr, ch, true);
+  }
+}
+
 // Apply split results, pop the level's nodes in FIFO order, emit partition chunks.
 template <int KP>
 __device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused, int implicit_items) {
+  {
+    // one round trip for every state word; the fast path when the level fits one thread per
+    // node (implicit_items bit 1: YTK_PLAN_FAST=0, the general path below)
+    const bool fast_ok = !(implicit_items & 2);
+    implicit_items &= 1;
+    const int nsi = b.st[ST_N_SITEMS], npend = b.st[ST_N_PENDING];
+    const int num_nodes0 = b.st[ST_NUM_NODES], num_leaf0 = b.st[ST_NUM_LEAF], nprev = b.st[ST_N_SPLIT];
+    if (fast_ok && npend <= kPlanThreads && npend == nsi && (int)blockDim.x == kPlanThreads) {
+      lv_plan_split_fast(p, b, fused, implicit_items, nsi, npend, num_nodes0, num_leaf0, nprev);
+      return;
+    }
+  }
   __shared__ int s_aux[KP];   // candidate flag, later: split index / -1
   __shared__ int s_rank[KP];  // rank among the candidates (FIFO order)
   __shared__ int s_tmp[kPlanThreads + 1];
@@ -376,9 +518,112 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
   int* st = b.st;
   const int tid = threadIdx.x;
   const int nsplit = st[ST_N_SPLIT];
+  const bool fast_ok = !(use_loc & 2);  // bit 1: YTK_PLAN_FAST=0 (the general path below)
+  use_loc &= 1;
   const long long* lglob_arr = use_loc ? b.left_loc : b.left_glob;
   if (tid == 0) s_total = 0;
   __syncthreads();
+  if (fast_ok && nsplit <= kPlanThreads && (int)blockDim.x == kPlanThreads) {
+    // Fast path: one thread per split keeps the parent and its children in registers from
+    // the cursors to the histogram work list -- dependent global round trips st ->
+    // (split_nid, cursors, snap) -> parent fields, instead of re-reading the node table
+    // (written by other threads) and a pending copy through memory. Same outputs.
+    const int s = tid;
+    const bool mine = s < nsplit;
+    int pid = 0, snap = 0;
+    long long lloc = 0, lglob = 0;
+    if (mine) {
+      pid = b.split_nid[s];
+      snap = b.split_snap[s];
+      if (kAtomicCursor) {
+        lloc = __hip_atomic_load(&b.left_loc[(size_t)s * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+        lglob = __hip_atomic_load(&lglob_arr[(size_t)s * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffll;
+      } else {
+        lloc = b.left_loc[(size_t)s * cs] & 0xffffffffll;
+        lglob = lglob_arr[(size_t)s * cs] & 0xffffffffll;
+      }
+    }
+    bool need = false, left_small = false;
+    int lid = 0, rid = 0, pslot = 0, pbeg = 0, lcnt = 0, rcnt = 0;
+    if (mine) {
+      const DNode& P = b.nodes[pid];
+      lid = P.left;
+      rid = P.right;
+      pslot = P.slot;
+      pbeg = P.begin;
+      const int pdepth = P.depth, pcnt = P.cnt_local;
+      const long long pcg = P.cnt_global;
+      const double pG = P.G, pH = P.H, pgl = P.gl, phl = P.hl;
+      DNode& L = b.nodes[lid];
+      DNode& R = b.nodes[rid];
+      reset_node(L, pdepth + 1);
+      reset_node(R, pdepth + 1);
+      lcnt = (int)lloc;
+      rcnt = pcnt - (int)lloc;
+      const long long lcg = lglob, rcg = pcg - lglob;
+      L.begin = pbeg;
+      L.cnt_local = lcnt;
+      L.cnt_global = lcg;
+      R.begin = pbeg + lcnt;
+      R.cnt_local = rcnt;
+      R.cnt_global = rcg;
+      const bool terminal = (p.max_depth >= 0 && p.max_depth == pdepth + 1) ||
+                            (p.max_leaf_cnt > 0 && p.max_leaf_cnt == snap) ||
+                            (p.min_split_samples > 0 && lcg < p.min_split_samples && rcg < p.min_split_samples);
+      if (terminal) {
+        L.G = pgl; L.H = phl;
+        R.G = pG - pgl; R.H = pH - phl;
+        L.value = leaf_value(pgl, phl, p);
+        R.value = leaf_value(pG - pgl, pH - phl, p);
+      } else {
+        left_small = (fused || small_only_level(p.small_only, p.max_depth, pdepth)) ? left_small_by_hess(phl, pH)
+                                                                                     : (lcg < rcg);
+        need = true;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&s_total), (unsigned long long)(left_small ? lcnt : rcnt));
+      }
+    }
+    int nb;
+    const int k = block_scan_excl(need ? 1 : 0, s_tmp, &nb);  // build index (scan barriers order s_total)
+    const long long total = s_total;
+    const int tgt = p.hist_target > 2 * nb ? p.hist_target - nb : p.hist_target;
+    const int ch = (int)max((long long)p.min_rows, (total + tgt - 1) / max(1, tgt));
+    int hbeg = 0, hcnt = 0;
+    if (need) {
+      const int small_id = left_small ? lid : rid, large_id = left_small ? rid : lid;
+      const int sslot = build_base + k, lslot = build_base + dgap + k;
+      b.nodes[small_id].slot = sslot;
+      b.nodes[large_id].slot = lslot;
+      b.split_items[k] = make_int4(sslot, 0, 0, 0);
+      b.item_nid[k] = small_id;
+      b.split_items[nb + k] = make_int4(lslot, pslot, sslot, 1);
+      b.item_nid[nb + k] = large_id;
+      b.pending[2 * k] = lid;
+      b.pending[2 * k + 1] = rid;
+      hbeg = left_small ? pbeg : pbeg + lcnt;
+      hcnt = left_small ? lcnt : rcnt;
+    }
+    int nitems;
+    const int first = block_scan_excl(need ? (hcnt + ch - 1) / ch : 0, s_tmp, &nitems);
+    if (need) {  // per build k (emit_all_chunks reads them by build index)
+      s_small[k] = first;
+      s_hbeg[k] = hbeg;
+      s_hcnt[k] = hcnt;
+      s_hslot[k] = build_base + k;
+      if (b.hist_first) b.hist_first[k] = first;
+    }
+    __syncthreads();
+    emit_all_chunks(b.hist_items, nitems, nb, s_small, s_hbeg, s_hcnt, s_hslot, ch, false);
+    if (tid == 0) {
+      if (b.hist_first) b.hist_first[nb] = nitems;
+      const int hs = half >> 1;
+      st[ST_N_HIST_A] = (hs > 0 && nb > hs) ? s_small[hs] : nitems;
+      st[ST_N_PENDING] = 2 * nb;
+      st[ST_N_BUILD] = nb;
+      st[ST_N_SITEMS] = 2 * nb;
+      st[ST_N_HIST] = nitems;
+    }
+    return;
+  }
   for (int s = tid; s < nsplit; s += kPlanThreads) {
     DNode& P = b.nodes[b.split_nid[s]];
     DNode& L = b.nodes[P.left];
@@ -923,6 +1168,11 @@ static LvParams make_params(const int* ip, const float* fp) {
   return p;
 }
 
+static int plan_fast_off() {  // YTK_PLAN_FAST=1: the planners' one-thread-per-node fast paths
+  const char* e = getenv("YTK_PLAN_FAST");  // read per launch (~0.1 us): tests toggle it
+  return (e && e[0] == '1') ? 0 : 2;
+}
+
 extern "C" {
 
 // which: 0 init, 1 plan_split (arg1 = fused: patch the previous level's cnt_global from
@@ -940,11 +1190,11 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
                          (float*)nullptr, (double*)nullptr);
       break;
     case 1:  // arg0 = 1: no partition work list (single-pass partition maps blocks itself)
-      hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1, arg0);
+      hipLaunchKernelGGL(lv_plan_split_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg1, arg0 | plan_fast_off());
       break;
     case 3:
       hipLaunchKernelGGL(lv_plan_children_kernel, dim3(1), dim3(kPlanThreads), 0, s, p, b, arg0,
-                         arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), (arg1 >> 30) & 1,
+                         arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), ((arg1 >> 30) & 1) | plan_fast_off(),
                          (arg1 >> 29) & 1);
       break;
     case 4: hipLaunchKernelGGL(lv_finalize_kernel, dim3(1), dim3(256), 0, s, b, arg0); break;
@@ -965,7 +1215,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   LvBufs b = make_bufs(ptrs);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int half = arg1 & 0x3fff, dgap = (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff);
-  const int use_loc = (arg1 >> 30) & 1, fused = (arg1 >> 29) & 1;
+  const int use_loc = ((arg1 >> 30) & 1) | plan_fast_off(), fused = (arg1 >> 29) & 1;
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
   if (bin_bytes == 2) {
     // uint16 bins (wide): one configuration -- 2048-row chunks, the pipelined body with the
@@ -1138,8 +1388,8 @@ void ytk_lv_tail(const uintptr_t* ptrs, const int* ip, const float* fp, int chil
   LvRawArgs r{(const float*)cand, (const int*)coff, (const float*)fill, split_median, (int*)nfeat, (float*)nthr,
               (int*)nleft, (int*)nright, (uint8_t*)ndefl, (float*)nval};
   hipLaunchKernelGGL(lv_tail_kernel, dim3(1), dim3(kPlanThreads), 0, reinterpret_cast<hipStream_t>(stream), p, b,
-                     children, arg0, arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff), (arg1 >> 30) & 1,
-                     (arg1 >> 29) & 1, max_nodes, r);
+                     children, arg0, arg1 & 0x3fff, (arg1 & 0x3fff) + ((arg1 >> 14) & 0x3fff),
+                     ((arg1 >> 30) & 1) | plan_fast_off(), (arg1 >> 29) & 1, max_nodes, r);
   YTK_LAUNCH_CHECK();
 }
 
