@@ -1168,9 +1168,9 @@ static LvParams make_params(const int* ip, const float* fp) {
   return p;
 }
 
-static int plan_fast_off() {  // YTK_PLAN_FAST=1: the planners' one-thread-per-node fast paths
+static int plan_fast_off() {  // YTK_PLAN_FAST=0: the planners' general paths (default: fast paths)
   const char* e = getenv("YTK_PLAN_FAST");  // read per launch (~0.1 us): tests toggle it
-  return (e && e[0] == '1') ? 0 : 2;
+  return (e && e[0] == '0') ? 2 : 0;
 }
 
 extern "C" {

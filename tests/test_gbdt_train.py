@@ -161,7 +161,7 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_FUSE_REDUCE_SPLIT": "1"}, {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "1"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "8"},
-                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "1"}])
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "0"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""
