@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
 constexpr int kReduceSplit = 8;
 constexpr int kReduceDirect = 16;  // ranged slots with <= this many items: one block, plain stores
 
+template <int U = 8>  // staged partials in flight per thread (YTK_REDUCE_U = 8 | 16)
 __global__ __launch_bounds__(256) void hist_reduce_kernel(
     const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
     const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
@@ -281,12 +282,12 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
       const int step = direct ? 1 : (int)gridDim.z;  // split-K factor (launch z extent)
       long long g = 0, h = 0;
       int t = direct ? 0 : (int)blockIdx.z;
-      for (; t + 7 * step < r.y; t += 8 * step) {
-        longlong2 v[8];
+      for (; t + (U - 1) * step < r.y; t += U * step) {
+        longlong2 v[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = st[((size_t)(r.x + t + u * step) * groups + fg) * E + i];
+        for (int u = 0; u < U; ++u) v[u] = st[((size_t)(r.x + t + u * step) * groups + fg) * E + i];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
+        for (int u = 0; u < U; ++u) { g += v[u].x; h += v[u].y; }
       }
       for (; t < r.y; t += step) {
         const longlong2 v = st[((size_t)(r.x + t) * groups + fg) * E + i];
@@ -366,12 +367,12 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   const longlong2* st = reinterpret_cast<const longlong2*>(staging);
   long long g = 0, h = 0;
   int t = direct ? 0 : (int)blockIdx.z;
-  for (; t + 7 * step < cnt; t += 8 * step) {
-    longlong2 v[8];
+  for (; t + (U - 1) * step < cnt; t += U * step) {
+    longlong2 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = st[((size_t)YTK_SEL(t + u * step) * groups + fg) * E + i];
+    for (int u = 0; u < U; ++u) v[u] = st[((size_t)YTK_SEL(t + u * step) * groups + fg) * E + i];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) { g += v[u].x; h += v[u].y; }
+    for (int u = 0; u < U; ++u) { g += v[u].x; h += v[u].y; }
   }
   for (; t < cnt; t += step) {
     const longlong2 v = st[((size_t)YTK_SEL(t) * groups + fg) * E + i];
@@ -658,6 +659,11 @@ using namespace ytk;
 // features per histogram block (32 or 16), process-wide (ytk_hist_set_fw); the staging
 // slabs hold groups * fw columns per bin
 static int g_hist_fw = 32;
+// staged partials in flight per reduce thread (YTK_REDUCE_U, read per launch: tests toggle it)
+static int reduce_u() {
+  const char* e = getenv("YTK_REDUCE_U");
+  return (e && atoi(e) == 16) ? 16 : 8;
+}
 
 template <bool kIdentity>
 static void launch_hist_fx(dim3 grid, size_t lds_unused, hipStream_t s, const uint8_t* bins, long long stride, int F,
@@ -735,7 +741,7 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   // 66 -> 77 us per tree: more memory-side atomics), so kReduceSplit stays.
   const char* rs = getenv("YTK_REDUCE_SPLIT");
   const int zs = rs ? std::max(1, atoi(rs)) : kReduceSplit;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, zs), dim3(256), 0, s,
+  hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, zs), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
                      (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids,
                      (const int*)nullptr, (const int2*)nullptr, fw);
@@ -790,7 +796,7 @@ void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t g
                           (const float*)scales_dev, (long long*)staging, nullptr, gh_rows);
   YTK_LAUNCH_CHECK();
   const int E = nb_lds * fw;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
+  hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
                      dim3(256), 0, s, (const long long*)staging, (const int4*)work, max_work,
                      (const int*)nwork_dev, (long long*)hist, B, F, nb_lds, groups, 0, (const int*)slot_ids,
                      (const int*)nslots_dev, (const int2*)slot_range, fw);
@@ -806,7 +812,7 @@ void ytk_hist_reduce(uintptr_t staging, uintptr_t work, int nwork, uintptr_t his
   const int fw = 32;
   const int groups = (F + fw - 1) / fw;
   const int E = B * fw;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0,
+  hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work, nwork,
                      (const int*)nullptr, (long long*)hist, B, F, B, groups, slot_base, (const int*)nullptr,
                      (const int*)nullptr, (const int2*)nullptr, fw);
@@ -927,7 +933,7 @@ int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uin
   }
   if (staging && nslots > 0) {
     const int E = B * FG;
-    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
+    hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
                        (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev, (long long*)hist, B,
                        F, B, groups, slot_base, (const int*)nullptr, (const int*)nullptr, (const int2*)nullptr, FG);
     YTK_LAUNCH_CHECK();
@@ -950,7 +956,7 @@ void ytk_hist_wide_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t
                    0, 0, 0, 0, stream);
   const int groups = (F + FG - 1) / FG;
   const int E = B * FG;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
+  hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
                      dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work,
                      max_work, (const int*)nwork_dev, (long long*)hist, B, F, B, groups, 0, (const int*)slot_ids,
                      (const int*)nslots_dev, (const int2*)slot_range, FG);
