@@ -66,6 +66,7 @@ struct LwParams {
   int bin_bytes;  // 1: uint8 bins, 2: uint16 bins (B > 256)
   int batch_cap;  // > 0: at most this many splits per batch (the RCCL batch loop sizes its fixed
                   // messages by it, ytk_lw_set_batch_cap); 0: no cap
+  int slow_children;  // set per partition launch: 1 = YTK_PLAN_FAST=0 (general children path)
 };
 
 // global-memory planner workspace (large trees): the arrays the LDS planner keeps in LDS
@@ -880,6 +881,101 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
   }
   if (tid == 0) s_total = 0ull;
   __syncthreads();
+  if (!p.slow_children && k <= kLwThreads && (int)blockDim.x == kLwThreads) {
+    // Fast path (<= 256 splits): one thread per split keeps the parent, its children and the
+    // built child's segment in registers from the cursor to the histogram work list --
+    // dependent global round trips st -> (batch, cursor, part_*) -> lc -> depth instead of
+    // re-reading the node arrays other threads wrote (build ids, begins, counts). Same
+    // outputs as the general path below.
+    __shared__ int s_cntb[kLwThreads];
+    const int j = tid;
+    const bool mine = j < k;
+    int P = 0, lloc = 0, lb = 0, rcnt = 0;
+    if (mine) {
+      P = b.batch[j];
+      const unsigned long long cur =
+          __hip_atomic_load(&b.cursor[(size_t)j * kCurStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lloc = (int)(cur & 0xffffffffull);
+      lb = b.part_begin[j] + b.part_shift[j];
+      rcnt = b.part_cnt[j] - lloc;
+    }
+    bool need = false, left_small = false;
+    int L = 0;
+    if (mine) {
+      L = b.lc[P];
+      const int R = L + 1;
+      const bool ls = p.dist ? (b.hl[P] < b.H[P] - b.hl[P]) : (lloc < rcnt);
+      b.begin[L] = lb;
+      b.cnt_local[L] = lloc;
+      b.cnt[L] = lloc;
+      b.begin[R] = lb + lloc;
+      b.cnt_local[R] = rcnt;
+      b.cnt[R] = rcnt;
+      const int dep = b.depth[L];
+      need = !(p.max_depth >= 0 && dep == p.max_depth) &&
+             !(p.min_split_samples > 0 && lloc < p.min_split_samples && rcnt < p.min_split_samples);
+      left_small = ls;
+      if (need) atomicAdd(&s_total, (unsigned long long)(left_small ? lloc : rcnt));
+    }
+    int nb;
+    const int kb = lw_scan(need ? 1 : 0, s_tmp, &nb);  // build index (the scan's barriers order s_total)
+    const long long total = (long long)s_total;
+    const int ch = (int)max((long long)p.min_rows, (total + p.hist_target - 1) / max(1, p.hist_target));
+    int S = 0, cntS = 0, begS = 0, nfirst = 0;
+    if (need) {
+      S = left_small ? L : L + 1;
+      const int G = left_small ? L + 1 : L;
+      b.build_ids[kb] = S;
+      b.split_items[kb] = make_int4(S, 0, 0, 0);
+      b.item_sid[kb] = S;
+      b.split_items[nb + kb] = make_int4(G, P, S, 1);
+      b.item_sid[nb + kb] = G;
+      cntS = left_small ? lloc : rcnt;
+      begS = left_small ? lb : lb + lloc;
+      nfirst = cntS == 0 ? 0 : max(1, cntS / ch);
+    }
+    int nitems, nzero;
+    const int first = lw_scan(nfirst, s_tmp, &nitems);
+    const bool multi = need && nfirst != 1;  // slots the split-K reduce adds into (zeroed)
+    const int z = lw_scan(multi ? 1 : 0, s_tmp, &nzero);
+    if (multi) {
+      b.zero_ids[z] = S;
+      b.zero_range[z] = make_int2(first, nfirst);
+    }
+    if (need) {
+      s_first[kb] = first;
+      s_small[kb] = S;
+      s_need[kb] = begS;
+      s_cntb[kb] = cntS;
+    }
+    __syncthreads();
+    for (int q = tid; q < nitems; q += kLwThreads) {
+      int lo = 0, hi = nb - 1;  // last build with s_first <= q
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_first[mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      const int jq = q - s_first[lo];
+      const int nc = (lo + 1 < nb ? s_first[lo + 1] : nitems) - s_first[lo];
+      const int beg = s_need[lo];
+      const long long cnt = s_cntb[lo];
+      const int cb = beg + (int)(cnt * jq / nc);
+      const int ce = beg + (int)(cnt * (jq + 1) / nc);
+      b.hist_items[q] = make_int4(s_small[lo], cb, ce, nc == 1 ? 1 : (nc > kLwReduceDirect && jq == 0 ? 2 : 0));
+    }
+    if (tid == 0) {
+      st[LW_N_HIST] = nitems;
+      st[LW_N_BUILD] = nb;
+      st[LW_N_ZERO] = nzero;
+      st[LW_N_SITEMS] = 2 * nb;
+      if (b.prof) {
+        atomicAdd(&b.prof[12], (unsigned long long)total);
+        atomicAdd(&b.prof[13], (unsigned long long)nb);
+        atomicAdd(&b.prof[14], (unsigned long long)nitems);
+      }
+    }
+    return;
+  }
   for (int j = tid; j < k; j += kLwThreads) {
     const int P = b.batch[j];
     const int L = b.lc[P], R = L + 1;
@@ -1157,6 +1253,7 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.dist = ip[9];
   p.bin_bytes = ip[10] == 2 ? 2 : 1;
   p.batch_cap = 0;
+  p.slow_children = 0;
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -1254,10 +1351,15 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
                       uintptr_t gh_out, int max_blocks, uintptr_t stream) {
   const LwEngine& e = g_lw.at(h);
+  LwParams pp = e.p;  // YTK_PLAN_FAST=0: the children planning's general path (read per launch)
+  {
+    const char* pf = getenv("YTK_PLAN_FAST");
+    pp.slow_children = (pf && pf[0] == '0') ? 1 : 0;
+  }
   if (e.p.bin_bytes == 2) {  // uint16 bins (B > 256): the pipelined body with (g, h) prefetch
     const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint16_t>), grid, dim3(kPartThreads), 0,
-                       reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint16_t*)binsT, ncol,
+                       reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint16_t*)binsT, ncol,
                        (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
     YTK_LAUNCH_CHECK();
     return;
@@ -1270,15 +1372,15 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
   if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
     hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
-                       reinterpret_cast<hipStream_t>(stream), e.p, e.b, (const uint8_t*)binsT, ncol,
+                       reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
                        (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
   else if (prefetch)
     hipLaunchKernelGGL(lw_partition_kernel<true>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                       e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                       pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
                        (float2*)gh_out);
   else
     hipLaunchKernelGGL(lw_partition_kernel<false>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                       e.p, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                       pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
                        (float2*)gh_out);
   YTK_LAUNCH_CHECK();
 }

@@ -312,6 +312,28 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{"max_leaf_cnt": 63}, {"max_leaf_cnt": 255, "min_split_samples": 200},
+                                {"max_leaf_cnt": 300, "instance_sample_rate": 0.7}])
+def test_device_leafwise_children_fast_path_identical(monkeypatch, kw):
+    """The partition kernel's one-thread-per-split children planning (default) and the
+    general path (YTK_PLAN_FAST=0) build the same trees byte for byte (batches above 256
+    splits take the general path either way)."""
+    res = []
+    for fast in ("0", "1"):
+        monkeypatch.setenv("YTK_PLAN_FAST", fast)
+        p = _params("loss", rounds=3)
+        for k, v in kw.items():
+            setattr(p.tree, k, v)
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(120000, 31, "cuda"), _data(6000, 32, "cuda"))
+        tr.train()
+        assert tr.use_device_builder
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1]
+    assert res[0][0].count("leaf=") > 100
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sample", [1.0, 0.7])
 def test_device_leafwise_row_indexed_gh_identical(monkeypatch, sample):
     """YTK_LW_GH_ROWS=1: (g, h) stays row-indexed (the partition moves row ids only, the
