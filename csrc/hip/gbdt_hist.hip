@@ -199,8 +199,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_fx_kernel(
     // launch (~45 us per level at 256 blocks); stores + one ordered read are ~4x cheaper.
     const int E = nb_lds * kFW;
     longlong2* st = reinterpret_cast<longlong2*>(staging) + ((size_t)bx * gridDim.y + fg) * E;
+    const int fw = min(kFW, F - fg * kFW);  // features of this group (the reduce reads no padding)
     for (int i = tid; i < E; i += kHistThreads) {
       const int l = i % kFW;
+      if (l >= fw) continue;
       const int li = (i / kFW) * kRow + (kFW == 32 ? hist_lds_pos(l) : l);
       st[i] = make_longlong2((long long)sm64[li], (long long)sm64[li + kFW]);
     }
