@@ -228,7 +228,8 @@ __global__ __launch_bounds__(kPlanThreads) void lv_init_kernel(LvParams p, LvBuf
 // the chunk counts and their scan in global memory). Same decisions, same outputs.
 __device__ void lv_plan_split_fast(const LvParams& p, const LvBufs& b, int fused, int implicit_items, int nsi,
                                    int npend, int num_nodes0, int num_leaf0, int nprev) {
-  __shared__ int s_tmp[kPlanThreads / kWave + 1];
+  // (256-thread planner launches and the 1024-thread fused split + plan kernel's last block)
+  __shared__ int s_tmp[1024 / kWave + 1];
   __shared__ int s_cnt[kPlanThreads], s_first[kPlanThreads], s_beg[kPlanThreads];
   __shared__ long long s_total;
   int* st = b.st;
@@ -236,7 +237,7 @@ __device__ void lv_plan_split_fast(const LvParams& p, const LvBufs& b, int fused
   const double mcw2 = (double)p.mcw * 2.0;
   if (fused) {  // previous level's children: global counts from the all-reduced cursors
     const size_t cs = fused == 2 ? kCurStride : 1;
-    for (int s = tid; s < nprev; s += kPlanThreads) {
+    for (int s = tid; s < nprev; s += (int)blockDim.x) {
       const DNode& P = b.nodes[b.split_nid[s]];
       const long long lg = b.left_glob[(size_t)s * cs] & 0xffffffffll;
       b.nodes[P.left].cnt_global = lg;
@@ -359,7 +360,7 @@ __device__ void lv_plan_split_body(const LvParams& p, const LvBufs& b, int fused
     implicit_items &= 1;
     const int nsi = b.st[ST_N_SITEMS], npend = b.st[ST_N_PENDING];
     const int num_nodes0 = b.st[ST_NUM_NODES], num_leaf0 = b.st[ST_NUM_LEAF], nprev = b.st[ST_N_SPLIT];
-    if (fast_ok && npend <= kPlanThreads && npend == nsi && (int)blockDim.x == kPlanThreads) {
+    if (fast_ok && npend <= kPlanThreads && npend == nsi && (int)blockDim.x >= kPlanThreads) {
       lv_plan_split_fast(p, b, fused, implicit_items, nsi, npend, num_nodes0, num_leaf0, nprev);
       return;
     }
