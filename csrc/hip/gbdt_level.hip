@@ -932,7 +932,7 @@ __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
     LvBufs b, const long long* __restrict__ staging, long long* __restrict__ hist, int B, int F, int groups32,
     int slot_base, const int* __restrict__ nbins_f, const uint8_t* __restrict__ fmask, int f0, GainParams gp,
     const double* __restrict__ inv_dev, unsigned* __restrict__ counters, int nchunks, int ng,
-    unsigned long long* __restrict__ prof, int getenv_dummy_twice) {
+    unsigned long long* __restrict__ prof, int warm_twice) {
   extern __shared__ __attribute__((aligned(16))) longlong2 sh_rs[];  // tail: [2][8][B + 1]
   __shared__ int s_last;
   // prof (optional, YTK_RS_PROF): per block [entry, counted in, tail start, tail end] wall
@@ -997,7 +997,7 @@ __global__ __launch_bounds__(kRsThreads) void lv_reduce_split_kernel(
   }
   const int4 d = b.split_items[nb + k];  // (derived slot, parent slot, built slot, 1)
   const int fbeg = g8 * G, fend = min(F, fbeg + G);
-  if (pr && getenv_dummy_twice) {  // diagnosis: a warm second pass (same results, idempotent)
+  if (pr && warm_twice) {  // YTK_RS_PROF_TWICE: search twice, time the warm second pass (idempotent)
     split_pair_block<G>(hist, B, F, B + 1, nbins_f, fmask, f0, slot, d.y, d.x, b.split_out + (size_t)k * ng + g8,
                         b.split_out + (size_t)(nb + k) * ng + g8, gp, sh_rs, fbeg, fend, nullptr);
     __syncthreads();
