@@ -14,7 +14,7 @@ void ytk_hist_fx(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int
                  float, float, uintptr_t, uintptr_t, uintptr_t);
 void ytk_hist_fx_staged(uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
                         int, float, float, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t,
-                        uintptr_t, int);
+                        uintptr_t, int, uintptr_t, int);
 void ytk_hist_fx_global(uintptr_t, int, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                         uintptr_t, int, float, float, uintptr_t);
 void ytk_hist_set_fw(int);
@@ -180,14 +180,16 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("hist_fx_staged", [](uintptr_t bins, long long stride, int F, uintptr_t ghp, uintptr_t rows, uintptr_t work,
                              int nwork, uintptr_t hist, int B, float sg, float sh, uintptr_t nwork_dev,
                              uintptr_t scales_dev, uintptr_t staging, int slot_base, int nslots, uintptr_t slot_ids,
-                             uintptr_t work_off_dev, uintptr_t stream, int gh_rows) {
+                             uintptr_t work_off_dev, uintptr_t stream, int gh_rows, uintptr_t slot_first,
+                             int one_slot) {
     ytk_hist_fx_staged(bins, stride, F, ghp, rows, work, nwork, hist, B, sg, sh, nwork_dev, scales_dev, staging,
-                       slot_base, nslots, slot_ids, work_off_dev, stream, gh_rows);
+                       slot_base, nslots, slot_ids, work_off_dev, stream, gh_rows, slot_first, one_slot);
   }, pybind11::arg("bins"), pybind11::arg("stride"), pybind11::arg("F"), pybind11::arg("ghp"), pybind11::arg("rows"),
      pybind11::arg("work"), pybind11::arg("nwork"), pybind11::arg("hist"), pybind11::arg("B"), pybind11::arg("sg"),
      pybind11::arg("sh"), pybind11::arg("nwork_dev"), pybind11::arg("scales_dev"), pybind11::arg("staging"),
      pybind11::arg("slot_base"), pybind11::arg("nslots"), pybind11::arg("slot_ids"), pybind11::arg("work_off_dev"),
-     pybind11::arg("stream"), pybind11::arg("gh_rows") = 0);
+     pybind11::arg("stream"), pybind11::arg("gh_rows") = 0, pybind11::arg("slot_first") = 0,
+     pybind11::arg("one_slot") = 0);
   m.def("hist_wide", &ytk_hist_wide);
   m.def("hist_set_fw", &ytk_hist_set_fw);
   m.def("hist_get_fw", &ytk_hist_get_fw);

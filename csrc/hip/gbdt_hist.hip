@@ -255,7 +255,10 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     const long long* __restrict__ staging, const int4* __restrict__ work, int nwork,
     const int* __restrict__ nwork_dev, long long* __restrict__ hist, int B, int F, int nb_lds,
     int groups, int slot_base, const int* __restrict__ slot_ids, const int* __restrict__ nslots_dev,
-    const int2* __restrict__ slot_range, int gw) {
+    const int2* __restrict__ slot_range, int gw, const int* __restrict__ slot_first = nullptr, int one_slot = 0) {
+  // slot_first (optional): slot slot_base + k owns the items [slot_first[k], slot_first[k + 1])
+  // (the level engine's hist_first); one_slot: every item belongs to the one slot -- either
+  // way no scan of the work list
   __shared__ int s_sel[1024];
   __shared__ int s_wcnt[4];
   __shared__ int s_n;
@@ -319,10 +322,16 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
   // Fast path: every caller emits a slot's items contiguously -> one pass finds the
   // range [lo, hi] (min/max of matching indices) and the match count; contiguous iff
   // count == hi - lo + 1. Otherwise fall back to the ordered compaction below.
+  const bool known = slot_first != nullptr || one_slot;  // uniform
+  int known_lo = 0, known_cnt = n;
+  if (slot_first) {
+    known_lo = slot_first[by / groups];
+    known_cnt = slot_first[by / groups + 1] - known_lo;
+  }
   if (tid == 0) { s_n = 0; s_lo = 0x7fffffff; s_hi = -1; s_cnt = 0; }
   __syncthreads();
   // slot_range (optional): the slot's items are [x, x + y) -- no scan of the work list
-  for (int k0 = 0; k0 < n; k0 += 256) {  // one LDS atomic per wave, not per item
+  for (int k0 = 0; !known && k0 < n; k0 += 256) {  // one LDS atomic per wave, not per item
     const int k = k0 + tid;
     const unsigned long long bal = __ballot(k < n && work[k].x == slot);
     if (lane == 0 && bal) {
@@ -333,8 +342,8 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     }
   }
   __syncthreads();
-  const bool contiguous = s_cnt == 0 || s_cnt == s_hi - s_lo + 1;
-  if (contiguous) {
+  const bool contiguous = known || s_cnt == 0 || s_cnt == s_hi - s_lo + 1;
+  if (contiguous && !known) {
     if (tid == 0) s_n = s_cnt;
   }
   for (int k0 = 0; !contiguous && k0 < n; k0 += 256) {
@@ -352,8 +361,8 @@ __global__ __launch_bounds__(256) void hist_reduce_kernel(
     __syncthreads();
   }
   __syncthreads();
-  const int cnt = contiguous ? s_n : min(s_n, 1024);
-  const int lo = s_lo;
+  const int cnt = known ? known_cnt : contiguous ? s_n : min(s_n, 1024);
+  const int lo = known ? known_lo : s_lo;
   // t-th item of the slot
 #define YTK_SEL(t) (contiguous ? lo + (t) : s_sel[(t)])
   const int E = nb_lds * gw;
@@ -721,7 +730,8 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
                         uintptr_t work, int nwork, uintptr_t hist, int B, float sg, float sh,
                         uintptr_t nwork_dev, uintptr_t scales_dev, uintptr_t staging,
                         int slot_base, int nslots, uintptr_t slot_ids, uintptr_t work_off_dev,
-                        uintptr_t stream, int gh_rows) {
+                        uintptr_t stream, int gh_rows, uintptr_t slot_first, int one_slot) {
+  // slot_first / one_slot (optional): the slots' item ranges are known (hist_reduce_kernel)
   if (nwork <= 0 || nslots <= 0) return;
   const int fw = g_hist_fw;
   const int groups = (F + fw - 1) / fw;
@@ -746,7 +756,7 @@ void ytk_hist_fx_staged(uintptr_t bins, long long stride, int F, uintptr_t ghp, 
   hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, zs), dim3(256), 0, s,
                      (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev,
                      (long long*)hist, B, F, nb_lds, groups, slot_base, (const int*)slot_ids,
-                     (const int*)nullptr, (const int2*)nullptr, fw);
+                     (const int*)nullptr, (const int2*)nullptr, fw, (const int*)slot_first, one_slot);
   YTK_LAUNCH_CHECK();
 }
 
@@ -801,7 +811,7 @@ void ytk_hist_fx_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t g
   hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
                      dim3(256), 0, s, (const long long*)staging, (const int4*)work, max_work,
                      (const int*)nwork_dev, (long long*)hist, B, F, nb_lds, groups, 0, (const int*)slot_ids,
-                     (const int*)nslots_dev, (const int2*)slot_range, fw);
+                     (const int*)nslots_dev, (const int2*)slot_range, fw, (const int*)nullptr, 0);
   YTK_LAUNCH_CHECK();
 }
 
@@ -817,7 +827,7 @@ void ytk_hist_reduce(uintptr_t staging, uintptr_t work, int nwork, uintptr_t his
   hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work, nwork,
                      (const int*)nullptr, (long long*)hist, B, F, B, groups, slot_base, (const int*)nullptr,
-                     (const int*)nullptr, (const int2*)nullptr, fw);
+                     (const int*)nullptr, (const int2*)nullptr, fw, (const int*)nullptr, nslots == 1 ? 1 : 0);
   YTK_LAUNCH_CHECK();
 }
 
@@ -937,7 +947,8 @@ int ytk_hist_wide_rm(uintptr_t bins, long long stride, int F, uintptr_t ghp, uin
     const int E = B * FG;
     hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, nslots * groups, kReduceSplit), dim3(256), 0, s,
                        (const long long*)staging, (const int4*)work, nwork, (const int*)nwork_dev, (long long*)hist, B,
-                       F, B, groups, slot_base, (const int*)nullptr, (const int*)nullptr, (const int2*)nullptr, FG);
+                       F, B, groups, slot_base, (const int*)nullptr, (const int*)nullptr, (const int2*)nullptr, FG,
+                       (const int*)nullptr, 0);
     YTK_LAUNCH_CHECK();
   }
   return FG;
@@ -961,7 +972,7 @@ void ytk_hist_wide_staged_dev(uintptr_t bins, long long stride, int F, uintptr_t
   hipLaunchKernelGGL(reduce_u() == 16 ? hist_reduce_kernel<16> : hist_reduce_kernel<8>, dim3((E + 255) / 256, std::max(1, reduce_y) * groups, kReduceSplit),
                      dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (const long long*)staging, (const int4*)work,
                      max_work, (const int*)nwork_dev, (long long*)hist, B, F, B, groups, 0, (const int*)slot_ids,
-                     (const int*)nslots_dev, (const int2*)slot_range, FG);
+                     (const int*)nslots_dev, (const int2*)slot_range, FG, (const int*)nullptr, 0);
   YTK_LAUNCH_CHECK();
 }
 

@@ -596,7 +596,11 @@ class DeviceLevelBuilder:
         h.lv_init_scales(ptrs, ip, fp, ptr(mx), ptr(self.scales), ptr(self.inv_scales), s)
         tm.mark("init_stats")
 
-        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0, by_row=0):
+        # YTK_REDUCE_KNOWN=0: the slot reduce scans the work list for each slot's items instead
+        # of reading the ranges the children planner wrote (hist_first) / the root's one slot
+        known = os.environ.get("YTK_REDUCE_KNOWN", "1") != "0"
+
+        def build_hist(gh_ptr, rows_ptr, nitems, slot_base, nslots, n_dev=None, work_off=0, by_row=0, first=0):
             if self._zero_all:
                 if slot_base == 0:
                     self.hist.zero_()  # every slot of the tree in one fill (small slabs)
@@ -614,7 +618,8 @@ class DeviceLevelBuilder:
                 h.hist_fx_staged(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr,
                                  ptr(self.hist_items), nitems, ptr(self.hist), self.B, 1.0, 1.0,
                                  off(5) if n_dev is None else n_dev, ptr(self.scales), ptr(self.staging),
-                                 slot_base, nslots, 0, work_off, s, by_row)
+                                 slot_base, nslots, 0, work_off, s, by_row, first if known else 0,
+                                 1 if (known and slot_base == 0 and nslots == 1) else 0)
                 return
             assert not by_row, "row-indexed (g, h) needs the staged histogram kernel"
             h.hist_fx(ptr(self.bins), self.bins.shape[1], self.F, gh_ptr, rows_ptr, ptr(self.hist_items),
@@ -732,14 +737,15 @@ class DeviceLevelBuilder:
                 # first half's exchange on the side stream (second peer group) overlaps the
                 # second half's build; the split search waits for both
                 hs = half // 2
-                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow)
+                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow,
+                           first=ptr(self.hist_first))
                 main = torch.cuda.current_stream(self.dev)
                 side = self._side
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     self.peer2.allreduce_(self.hist[base:base + hs].view(-1))
                 build_hist(hgh, ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
-                           work_off=off(ST_N_HIST_A), by_row=hrow)
+                           work_off=off(ST_N_HIST_A), by_row=hrow, first=ptr(self.hist_first) + 4 * hs)
                 tm.mark("build_hist_compute")
                 self._hist_allreduce(self.hist[base + hs:base + half + ncs])
                 main.wait_stream(side)
@@ -749,10 +755,11 @@ class DeviceLevelBuilder:
                 # two node halves: the first half's all-reduce (RCCL, async) overlaps the
                 # second half's histogram build; the split search waits for both
                 hs = half // 2
-                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow)
+                build_hist(hgh, ptr(self.rows), nmax, base, hs, n_dev=off(ST_N_HIST_A), by_row=hrow,
+                           first=ptr(self.hist_first))
                 work = self.comm.allreduce_(self.hist[base:base + hs], async_op=True)
                 build_hist(hgh, ptr(self.rows), nmax, base + hs, half - hs, n_dev=off(5),
-                           work_off=off(ST_N_HIST_A), by_row=hrow)
+                           work_off=off(ST_N_HIST_A), by_row=hrow, first=ptr(self.hist_first) + 4 * hs)
                 tm.mark("build_hist_compute")
                 if work is not None:
                     work.wait()
@@ -775,7 +782,7 @@ class DeviceLevelBuilder:
                 tm.mark("find_best_split")
                 continue
             else:
-                build_hist(hgh, ptr(self.rows), nmax, base, half, by_row=hrow)
+                build_hist(hgh, ptr(self.rows), nmax, base, half, by_row=hrow, first=ptr(self.hist_first))
                 tm.mark("build_hist_compute")
                 if dist:
                     # built slots (+ this level's count slots when fused): one collective
