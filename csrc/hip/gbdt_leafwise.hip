@@ -390,7 +390,8 @@ __device__ void lw_apply_splits(const LwParams& p, const LwBufs& b) {
 
 // Phase F for batch entry j (parent P): children ids lc, lc + 1, their fresh node state, the
 // partition descriptor (chunks of kLwChunk rows), the split cursor reset.
-__device__ __forceinline__ void lw_expand_one(const LwParams& p, const LwBufs& b, int j, int P, int lc) {
+// Returns the entry's partition chunk count (also stored in part_first[j] for the general scan).
+__device__ __forceinline__ int lw_expand_one(const LwParams& p, const LwBufs& b, int j, int P, int lc) {
   b.batch[j] = P;
   const int dep = b.depth[P] + 1;
   for (int c = lc; c <= lc + 1; ++c) {
@@ -413,8 +414,10 @@ __device__ __forceinline__ void lw_expand_one(const LwParams& p, const LwBufs& b
   b.part_begin[j] = beg;
   b.part_cnt[j] = cnt;
   b.part_shift[j] = beg < p.N ? p.N : -p.N;
-  b.part_first[j] = (cnt + kLwChunk - 1) / kLwChunk;
+  const int nch = (cnt + kLwChunk - 1) / kLwChunk;
+  b.part_first[j] = nch;
   b.cursor[(size_t)j * kCurStride] = 0ull;
+  return nch;
 }
 
 // kBig: the per-node arrays and queues live in the global workspace b.ws (large trees)
@@ -806,14 +809,23 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
   }
   LW_TICK(4);
   // F. expand the batch: children ids, partition descriptors (chunks of kLwChunk rows)
+  int s_nch = 0;  // this thread's entry's chunk count (k <= kLwPlanThreads: entry tid)
   for (int j = tid; j < k; j += kLwPlanThreads) {
     const int P = s_batch[j];
     const int lc = nsid + 2 * j;
     s_nd[P].x = lc;
-    lw_expand_one(p, b, j, P, lc);
+    const int nch = lw_expand_one(p, b, j, P, lc);
+    if (k <= kLwPlanThreads) s_nch = nch;  // one entry per thread: scanned in registers below
   }
-  __syncthreads();
-  const int nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
+  int nblocks = 0;
+  if (k > 0 && k <= kLwPlanThreads) {
+    // exclusive scan of the chunk counts in registers (no read-back of part_first)
+    const int first = lw_scan(tid < k ? s_nch : 0, s_tmp, &nblocks);
+    if (tid < k) b.part_first[tid] = first;
+  } else {
+    __syncthreads();
+    nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
+  }
   LW_TICK(5);
   // G. write back the replay state
   for (int i = tid; i < nsid; i += kLwPlanThreads) {
