@@ -35,7 +35,8 @@ import traceback
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see ytk_learn_amd/__init__.py
+if os.environ.get("WORLD_SIZE", "1") == "1":
+    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see ytk_learn_amd/__init__.py
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
