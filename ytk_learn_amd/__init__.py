@@ -1,12 +1,8 @@
-"""ytk-learn on MI355X (gfx950): GBDT, linear / FM / FFM and soft-tree models over HIP kernels."""
-import os as _os
+"""ytk-learn on MI355X (gfx950): GBDT, linear / FM / FFM and soft-tree models over HIP kernels.
 
-# Kernel arguments in device memory: the host-launched engines (leaf-wise batches: ~5 launches
-# per speculative batch, ~25 batches per tree) measured 3.43 -> 3.29 ms per 255-leaf tree with
-# it (profiles/r5/leafab/); graph-replayed level-wise rounds are unchanged. Read by the HIP
-# runtime at its first device call, so it only applies when the package is imported before
-# anything touches the GPU; an explicit user setting wins. Single-process jobs only: the
-# multi-GPU path (RCCL / peer exchanges) was not measured with it, and its graph-replayed
-# level-wise rounds do not gain from it.
-if _os.environ.get("WORLD_SIZE", "1") == "1":
-    _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+Runtime note: single-process jobs that grow leaf-wise trees gain ~4 % with kernel arguments in
+device memory (``HIP_FORCE_DEV_KERNARG=1`` in the environment before the first GPU call:
+3.43 -> 3.29 ms per 255-leaf tree, profiles/r5/leafab/); ``bench.py`` sets it for its
+one-GPU runs. The package does not set it: child processes inherit the environment, and the
+multi-GPU RCCL paths were not measured with it.
+"""
