@@ -22,6 +22,15 @@ reference-identical shape (leaf-wise, 255 leaves) is timed separately on the sam
 data (every N) and reported as ``leafwise_s_per_tree`` / ``leafwise_vs_reference``
 (÷ 1.136 s/tree, docs/gbdt_experiments.md:104).
 
+Multi-GPU design A/B (N > 1, ``--variants auto``): after the headline, short extra timed runs
+(2 untimed + ``--variant-steps`` timed level-wise trees each, a fresh trainer per variant) of
+the choices a one-GPU box cannot measure -- the half-level exchange overlapped with the build
+(``peer_overlap``), the other histogram sync mode (``owner`` / ``allreduce``), RCCL instead of
+the peer-memory exchange (``rccl``) and RCCL with its half-level overlap (``rccl_overlap``) --
+reported under ``variants`` in the same JSON line. Each runs in its own try block followed by
+an all-rank vote: a variant that fails on any rank is reported as ``{"error": ...}``, ends the
+variant list and leaves the headline intact.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 For N>1 the driver launches it under torch.distributed.run (RANK/WORLD_SIZE env).
 """
@@ -35,7 +44,7 @@ import traceback
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-if os.environ.get("WORLD_SIZE", "1") == "1":
+if os.environ.get("WORLD_SIZE", "1") == "1" and os.environ.get("YTK_FORCE_DIST") != "1":
     os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see ytk_learn_amd/__init__.py
 
 import torch  # noqa: E402
@@ -93,6 +102,104 @@ def _transport(comm, builder) -> str:
     return dist.get_backend(comm.group) if comm.group is not None else "none"
 
 
+# (name, environment of the variant's trainer); "sync_alt" is the histogram sync mode the
+# headline did not use (owner <-> allreduce)
+VARIANTS = [
+    ("peer_overlap", {"YTK_PEER_OVERLAP": "1"}),
+    ("sync_alt", {}),
+    ("rccl", {"YTK_PEER_REDUCE": "0"}),
+    ("rccl_overlap", {"YTK_PEER_REDUCE": "0", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}),
+]
+VARIANT_NAMES = [v[0] for v in VARIANTS]
+
+
+def _exchange_keys(coll, steps):
+    """Per-tree collective / device-timed exchange accounting of a timed run."""
+    n_x = coll.get("peer_exchanges", coll["calls"])
+    out = {"collectives_per_tree": round(coll["calls"] / steps, 2),
+           "exchanges_per_tree": round(n_x / steps, 2),
+           "exchange_us_per_tree": (round(coll["peer_us"] / steps, 2) if "peer_us" in coll else None),
+           # device wall time of one exchange (a built level's histogram message, or the round
+           # vector) -- the per-level exchange cost at this N
+           "exchange_us_per_level": (round(coll["peer_us"] / n_x, 2) if "peer_us" in coll and n_x else None)}
+    return out
+
+
+class _Env:
+    """Temporarily set environment variables (identical on every rank)."""
+
+    def __init__(self, kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def run_variants(a, comm, dev, data, params, headline_sync, log):
+    """The multi-GPU design A/B (module docstring): each variant is a fresh trainer, 2 untimed
+    + a.variant_steps timed trees; an all-rank vote after each one stops the list on a failure
+    anywhere (the ranks then agree on the collectives they issue next)."""
+    if a.variants == "none" or (a.variants == "auto" and comm.world <= 1):
+        return None
+    names = VARIANT_NAMES if a.variants in ("auto", "all") else [v for v in a.variants.split(",") if v]
+    X, y, Xt, yt = data
+    out = {}
+    for name in names:
+        env = dict(dict(VARIANTS).get(name, {}))
+        if name == "sync_alt":
+            env["YTK_HIST_SYNC"] = "owner" if headline_sync != "owner" else "allreduce"
+        t0 = time.perf_counter()
+        res, err = None, None
+        try:
+            with _Env(env):
+                if os.environ.get("YTK_BENCH_FAIL_VARIANT") == name:  # tests: a variant that fails
+                    raise RuntimeError(f"injected failure in variant {name}")
+                pv = GBDTParams(round_num=2 + a.variant_steps, loss_function="sigmoid", eval_metric=[],
+                                missing_value="value@0", approximate=params.approximate, tree=params.tree)
+                trv = GBDTTrainer(pv, GBDTData(X, y), GBDTData(Xt, yt), comm=comm, log=log)
+                trv.prepare()
+                trv.init_gradients()
+                el = timed_rounds(trv, comm, dev, 2, a.variant_steps)
+                coll = dict(comm.stats)
+                res = {"s_per_tree": round(el / a.variant_steps, 6), "env": env,
+                       "transport": _transport(comm, trv.builder),
+                       "hist_sync": "owner" if getattr(trv.builder, "owner", False) else "allreduce",
+                       "overlap": _overlap(comm, trv.builder),
+                       "graph_replays": trv._graphs["n"] if isinstance(trv._graphs, dict) else 0}
+                res.update(_exchange_keys(coll, a.variant_steps))
+                trv.close()
+                del trv
+        except Exception as e:  # noqa: BLE001 -- reported in the line; the headline stands
+            traceback.print_exc()
+            err = f"{type(e).__name__}: {e}"[:300]
+            peer = getattr(getattr(locals().get("trv"), "builder", None), "peer", None)
+            if peer is not None:
+                peer.abort()
+        ok = comm.allreduce_scalars([0.0 if err is not None else 1.0], op="min")[0] > 0.5 if comm.is_dist \
+            else err is None
+        if not ok:
+            out[name] = {"error": err or "failed on another rank", "env": env}
+            break
+        res["wall_s"] = round(time.perf_counter() - t0, 2)
+        out[name] = res
+    return out
+
+
+def _overlap(comm, builder) -> bool:
+    """Half-level exchange / all-reduce overlapped with the other half's build."""
+    return bool(getattr(builder, "peer_overlap", False)
+                or (getattr(builder, "overlap", False) and comm.is_dist and getattr(builder, "peer", None) is None))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +217,10 @@ def main():
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--leafwise-steps", type=int, default=None,
                     help="extra timed leaf-wise 255-leaf rounds on the same data (default 10)")
+    ap.add_argument("--variants", default="auto",
+                    help="multi-GPU design A/B after the headline: auto (N > 1 only) | none | all | "
+                         "comma list of " + ",".join(VARIANT_NAMES))
+    ap.add_argument("--variant-steps", type=int, default=8, help="timed level-wise trees per variant")
     a = ap.parse_args()
 
     # a stuck rank must fail the job well inside the driver's bench timeout: every collective
@@ -204,6 +315,8 @@ def run(a, comm):
             peer = getattr(getattr(locals().get("trl"), "builder", None), "peer", None)
             if peer is not None:
                 peer.abort()  # queued exchanges return at once: the device drains, the job ends
+    headline_sync = ("owner" if getattr(tr_builder, "owner", False) else "allreduce") if comm.is_dist else "none"
+    variants = run_variants(a, comm, dev, (X, y, Xt, yt), params, headline_sync, log) if a.policy == "level" else None
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -238,13 +351,10 @@ def run(a, comm):
             "timed_region": "step + convertModel + per-round loss readback (pipelined), all trees landed",
             "collectives_per_tree": round(coll["calls"] / a.steps, 2),
             "collective_bytes_per_tree": int(coll["bytes"] / a.steps),
-            "hist_sync": (("owner" if getattr(tr_builder, "owner", False) else "allreduce")
-                          if comm.is_dist else "none"),
+            "hist_sync": headline_sync,
             "hist_transport": transport,
             # half-level exchange / all-reduce overlapped with the other half's build
-            "overlap": bool(getattr(tr_builder, "peer_overlap", False)
-                            or (getattr(tr_builder, "overlap", False) and comm.is_dist
-                                and getattr(tr_builder, "peer", None) is None)),
+            "overlap": _overlap(comm, tr_builder),
             "graph_replays": replays,
             "trees_converted": total_rounds,
             # multi-GPU diagnostics: the start-up self-test of the peer-memory path (on a vote
@@ -252,9 +362,8 @@ def run(a, comm):
             "peer_selftest": (peer_mod.LAST_STATUS["state"] + (": " + peer_mod.LAST_STATUS["reason"]
                                                                if peer_mod.LAST_STATUS["reason"] else ""))
             if comm.is_dist else "n/a",
-            "exchanges_per_tree": round(coll.get("peer_exchanges", coll["calls"]) / a.steps, 2),
-            "exchange_us_per_tree": (round(coll["peer_us"] / a.steps, 2) if "peer_us" in coll else None),
         }
+        res.update({k: v for k, v in _exchange_keys(coll, a.steps).items() if k != "collectives_per_tree"})
         if leaf is not None:
             res["leafwise_s_per_tree"] = round(leaf, 6)
             res["leafwise_vs_reference"] = round(leaf / BASELINE_SEC_PER_TREE, 6)
@@ -265,6 +374,8 @@ def run(a, comm):
                 res["leafwise_exchange_us_per_tree"] = round(leaf_coll["peer_us"] / leaf_steps, 2)
         if leaf_error is not None:
             res["leafwise_error"] = leaf_error
+        if variants is not None:
+            res["variants"] = variants
         print(json.dumps(res), flush=True)
 
 

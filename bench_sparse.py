@@ -49,7 +49,9 @@ class _Names(list):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="fm", choices=["linear", "fm", "ffm", "gbmlr", "gbsdt", "gbhmlr", "gbhsdt"])
+    ap.add_argument("--model", default="fm", choices=["linear", "fm", "ffm", "gbmlr", "gbsdt", "gbhmlr", "gbhsdt", "multiclass"])
+    ap.add_argument("--classes", type=int, default=10, help="multiclass: K classes (K-1 weight columns)")
+    ap.add_argument("--loss", default=None, help="multiclass: softmax (default) | multiclass_hinge | ... | hsoftmax")
     ap.add_argument("--experts", type=int, default=16, help="soft-tree experts K (gbmlr/gbsdt/gbhmlr/gbhsdt)")
     ap.add_argument("--rows", type=int, default=4_000_000, help="rows per GPU")
     ap.add_argument("--features", type=int, default=1_000_000)
@@ -84,14 +86,22 @@ def main():
     fld2[pos] = fields + 1
     del idx, vals, fields, rows, pos
     w = torch.ones(n, dtype=torch.float32, device=dev)
+    if a.model == "multiclass":  # one-hot labels of a class drawn per row (the binary label picks the half)
+        gen = torch.Generator(device=dev).manual_seed(5 + comm.rank)
+        half = max(1, a.classes // 2)
+        cls = torch.randint(0, half, (n,), device=dev, generator=gen) + (y[:, 0] > 0.5).long() * (a.classes - half)
+        y = torch.nn.functional.one_hot(cls.clamp_max(a.classes - 1), a.classes).float()
+        del cls
     tot = comm.allreduce_scalars([float(n)])[0]
     data = SparseData(ip2, idx2, val2, y, w, fld2 if a.model == "ffm" else None, None, tot, tot, float(n))
     params = CommonParams()
-    params.loss.loss_function = "sigmoid"
+    params.loss.loss_function = (a.loss or "softmax") if a.model == "multiclass" else "sigmoid"
     params.loss.evaluate_metric = []
     params.model.need_bias = True
     params.model.data_path = "/tmp/ytk_bench_sparse_model"
     params.extra = {"k": [1, k], "bias_need_latent_factor": False}
+    if a.model == "multiclass":
+        params.extra = {"k": a.classes}
     if a.model.startswith("gb"):
         params.extra = {"k": a.experts, "tree_num": 1, "learning_rate": 1.0}
     log = YtkLogger(comm.rank, stream=sys.stderr)
@@ -104,6 +114,10 @@ def main():
     elif a.model == "fm":
         from ytk_learn_amd.models.continuous.fm import FMModel
         model = FMModel(params, loaded, comm, log)
+    elif a.model == "multiclass":
+        from ytk_learn_amd.models.continuous.multiclass import MulticlassLinearModel
+        model = MulticlassLinearModel(params, loaded, comm, log)
+        k = a.classes
     elif a.model == "ffm":
         from ytk_learn_amd.models.continuous.ffm import FFMModel
         model = FFMModel(params, loaded, comm, log)
@@ -192,6 +206,8 @@ def main():
             "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "setup_s": round(setup_s, 2),
             "scaling": "weak", "dtype": "fp32", "data": "synthetic Criteo-shape", "loss": loss / tot,
             "gbst_fused": (os.environ.get("YTK_GBST_FUSED", "1") != "0") if a.model.startswith("gb") else None,
+            "row_loss_fused": os.environ.get("YTK_ROW_LOSS", "1") != "0",
+            "loss_function": params.loss.loss_function,
         }), flush=True)
     comm.close()
 

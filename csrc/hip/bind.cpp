@@ -106,6 +106,8 @@ void ytk_dot(uintptr_t, uintptr_t, long long, int, uintptr_t, uintptr_t, uintptr
 void ytk_row_loss(int, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t, long long, uintptr_t, uintptr_t,
                   uintptr_t, uintptr_t, uintptr_t);
 void ytk_axpy_dot(uintptr_t, uintptr_t, float, float, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t);
+void ytk_mc_row_loss(int, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, int,
+                     uintptr_t, uintptr_t);
 // gbdt_level.hip
 void ytk_lv_step(int, const uintptr_t*, const int*, const float*, int, int, uintptr_t);
 void ytk_lv_raw_tree(const uintptr_t*, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
@@ -232,6 +234,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("dot", &ytk_dot);
   m.def("row_loss", &ytk_row_loss);
   m.def("axpy_dot", &ytk_axpy_dot);
+  m.def("mc_row_loss", &ytk_mc_row_loss);
   m.def("fm_forward", &ytk_fm_forward);
   m.def("fm_backward", &ytk_fm_backward);
   m.def("fm_sgd_update", &ytk_fm_sgd_update);

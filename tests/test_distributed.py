@@ -27,6 +27,12 @@ def _free_port():
     return p
 
 
+def _head_tail(text, n=4000):
+    if len(text) <= 2 * n:
+        return text
+    return text[:n] + f"\n[... {len(text) - 2 * n} characters ...]\n" + text[-n:]
+
+
 def _run(task, out, world, device="cpu", timeout=600, extra_env=None):
     os.makedirs(out, exist_ok=True)
     env = dict(os.environ)
@@ -36,7 +42,10 @@ def _run(task, out, world, device="cpu", timeout=600, extra_env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, task, str(out), device]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    with open(os.path.join(out, "stderr.log"), "w") as f:  # the whole worker stderr, kept with the run
+        f.write(r.stderr)
+    # the head of stderr holds an abort's what() message, the tail the launcher's report
+    assert r.returncode == 0, r.stdout[-3000:] + _head_tail(r.stderr)
     with open(os.path.join(out, "res.json")) as f:
         return json.load(f)
 
@@ -421,3 +430,52 @@ def test_bench_stalled_rank_fails_fast():
     assert r.returncode != 0
     assert time.time() - t0 < 200
     assert "failed" in r.stderr and "last collective issued" in r.stderr, r.stderr[-2000:]
+
+
+VARIANT_KEYS = {"s_per_tree", "env", "transport", "hist_sync", "overlap", "graph_replays", "collectives_per_tree",
+                "exchanges_per_tree", "exchange_us_per_tree", "exchange_us_per_level", "wall_s"}
+
+
+def test_bench_variants_world2_failing_variant_keeps_headline():
+    """bench.py at N > 1 runs the multi-GPU design A/B after the headline (overlap, the other
+    sync mode, RCCL, RCCL + overlap): every variant reports its keys, and a variant that fails
+    (injected into the last one) is reported as an error without losing the headline line."""
+    r = _bench(2, extra_args=("--variant-steps", "2"), env_extra={"YTK_BENCH_FAIL_VARIANT": "rccl_overlap"})
+    res = _bench_json(r)
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["hist_sync"] in ("allreduce", "owner")
+    v = res["variants"]
+    assert list(v) == ["peer_overlap", "sync_alt", "rccl", "rccl_overlap"]
+    for name in ("peer_overlap", "sync_alt", "rccl"):
+        assert VARIANT_KEYS <= set(v[name]), (name, v[name])
+        assert v[name]["s_per_tree"] > 0 and v[name]["collectives_per_tree"] > 0
+    assert v["sync_alt"]["hist_sync"] != res["hist_sync"]
+    assert v["rccl_overlap"]["error"].startswith("RuntimeError: injected failure")
+    assert "exchange_us_per_level" in res
+
+
+def test_bench_world1_has_no_variants():
+    res = _bench_json(_bench(1))
+    assert "variants" not in res
+
+
+@pytest.mark.gpu
+def test_bench_variants_two_ranks_one_gpu():
+    """Two ranks share the one GPU (gloo process group, forced peer-memory path): the bench
+    line carries every variant's keys with the peer transport device-timed."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {"YTK_DIST_BACKEND": "gloo", "YTK_PEER_REDUCE": "1", "YTK_PEER_TIMEOUT_S": "60"}
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--train-rows", "200000",
+            "--test-rows", "20000", "--quiet", "--leafwise-steps", "0", "--variant-steps", "2",
+            "--variants", "peer_overlap,sync_alt"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port())] + args
+    r = subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **env),
+                       capture_output=True, text=True, timeout=300)
+    res = _bench_json(r)
+    assert res["hist_transport"] == "peer" and res["exchange_us_per_level"] is not None
+    for name in ("peer_overlap", "sync_alt"):
+        assert VARIANT_KEYS <= set(res["variants"][name]), res["variants"][name]
+        assert res["variants"][name]["transport"] == "peer"
+    assert res["variants"]["peer_overlap"]["overlap"] is True

@@ -222,3 +222,40 @@ def test_fused_row_loss_matches_torch_formulas(name, z64, with_z1):
     torch.testing.assert_close(c.cpu(), (w * loss.grad(z, y)).float(), rtol=1e-6, atol=1e-7)
     assert row_loss(loss, z0.to(dev), yy.to(dev)[:, 0], wt.to(dev), want_grad=False)[2] is None
     assert row_loss(create_loss("hinge"), z0.to(dev), yy.to(dev)[:, 0], wt.to(dev)) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["softmax", "multiclass_hinge", "multiclass_l2_hinge", "multiclass_smooth_hinge",
+                                  "hsoftmax"])
+@pytest.mark.parametrize("K", [2, 3, 10, 33, 64])
+def test_fused_multiclass_row_loss_matches_torch(name, K):
+    """ops.blas.multiclass_row_loss (one fused HIP pass over the n x (K-1) scores with the
+    implicit zero K-th logit: loss sum, pred [n, K], D = weight * d1[:, :K-1]) == the loss
+    classes' fp64 torch formulas that MulticlassLinearModel runs otherwise (reference
+    MulticlassLinearHoagOptimizer.java:82-149). n is not a multiple of the 64-row tile."""
+    from ytk_learn_amd.ops.blas import multiclass_row_loss
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(K)
+    n = 20_011
+    S = (torch.randn(n, K - 1, generator=g) * 3).float()
+    cls = torch.randint(0, K, (n,), generator=g)
+    if name in ("softmax", "hsoftmax"):  # soft labels summing to 1 on half the rows, one-hot on the rest
+        soft = torch.softmax(torch.randn(n, K, generator=g), 1)
+        y = torch.where((torch.arange(n) % 2 == 0)[:, None], soft, torch.nn.functional.one_hot(cls, K).double())
+    else:
+        y = torch.nn.functional.one_hot(cls, K).double()
+    y = y.float()
+    wt = torch.rand(n, generator=g) + 0.5
+    loss = create_loss(name)
+    out = multiclass_row_loss(loss, S.to(dev), y.to(dev), wt.to(dev))
+    assert out is not None
+    lsum, pred, D = out
+    z = torch.zeros((n, K), dtype=torch.float64)
+    z[:, :K - 1] = S.double()
+    lv, p_ref, d1 = loss.all(z, y.double())
+    w = wt.double()
+    ref_sum = float((w * lv).sum())
+    assert abs(lsum - ref_sum) <= 1e-11 * abs(ref_sum) + 1e-9, (lsum, ref_sum)
+    torch.testing.assert_close(pred.cpu(), p_ref.float(), rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(D.cpu(), (d1[:, :K - 1] * w[:, None]).float(), rtol=2e-6, atol=1e-6)
+    assert multiclass_row_loss(loss, S.to(dev), y.to(dev), wt.to(dev), want_grad=False)[2] is None

@@ -5,7 +5,9 @@ row-major per feature; scores wx[0..K-2] = X W, wx[K-1] = 0; ``loss.all`` gives 
 prediction and d1; g[f, p] += weight * d1[p] * x; regularization group starts at the bias
 row, i.e. index K-1) and ``J/dataflow/MulticlassLinearModelDataFlow.java`` (labels are a
 class id or a K-vector summing to 1; dump ``name,w_0,...,w_{K-2}`` with Float.toString).
-Device path: S = X W and G = X^T D as the segmented SpMM kernel (J = K-1 columns).
+Device path: S = X W and G = X^T D as the segmented SpMM kernel (J = K-1 columns); the
+per-row loss / prediction / D epilogue is one fused HIP pass (``ops.blas.multiclass_row_loss``,
+every multiclass loss, K <= 64) and fp64 torch otherwise.
 Note: y_sampling keys on the first label value (a class id line); K-vector label lines are
 not sampled by class.
 """
@@ -16,6 +18,7 @@ from typing import List, Tuple
 import numpy as np
 import torch
 
+from ...ops.blas import multiclass_row_loss
 from .base import ContinuousModelBase, jfloat
 
 
@@ -49,8 +52,15 @@ class MulticlassLinearModel(ContinuousModelBase):
 
     def _forward(self, X, d, w, g):
         W = w.view(self.F, self.S)
+        s32 = X.matmul(W)
+        fused = multiclass_row_loss(self.loss, s32, d.y, d.weight, want_grad=g is not None)
+        if fused is not None:  # one fused row pass on the GPU
+            loss, pred, D = fused
+            if g is not None:
+                X.t_matmul(D, out=g.view(self.F, self.S))
+            return loss, pred
         z = torch.zeros((X.n, self.K), dtype=torch.float64, device=self.device)
-        z[:, :self.S] = X.matmul(W).double()
+        z[:, :self.S] = s32.double()
         y = d.y.double()
         lv, pred, d1 = self.loss.all(z, y)
         wt = d.weight.double()

@@ -637,6 +637,9 @@ class GBDTTrainer:
             if self._eager_rounds < 1:  # the first round builds its root eagerly
                 return False
             torch.cuda.synchronize(self.dev)
+            # the nccl watchdog must hold no eager work while the rounds are captured: its
+            # event queries inside a capture abort the process (Comm.drain_pending)
+            self.comm.drain_pending()
             b = self.builder
             saved = (b.rows, b.rows_tmp, b.ghp, b.gh_tmp, b.tree_count, b.root_ready)
             graphs, pool, err = [], None, None
@@ -659,9 +662,8 @@ class GBDTTrainer:
                     if ngraph == 4 and sf is not None:
                         host_j = torch.empty(sf.numel(), dtype=torch.uint8).pin_memory()
                         host_j = (host_j, hip().host_device_ptr(host_j.data_ptr()))
-                    # thread_local: the process group's watchdog thread may still query the
-                    # events of the eager collectives before the capture (a global-mode
-                    # capture turns those queries into errors and aborts the process)
+                    # thread_local: only this thread's capture-unsafe calls are checked (the
+                    # drain above keeps the watchdog from querying events meanwhile)
                     with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                         dev_trees, acc, acc_te, host_trees = self._step_dev(i)
                         if fault == "2":  # inside the capture: the round's launches half recorded

@@ -111,3 +111,39 @@ def row_loss(loss, z0: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, z1=None,
                    y.stride(0), ptr(wt), n, ptr(pred), ptr(c) if c is not None else 0, ptr(buf), ptr(buf[1024:]),
                    stream(z0))
     return (float(buf[1024]) if want_loss else None), pred, c
+
+
+_MC_LOSS = {"softmax": 0, "multiclass_hinge": 1, "multiclass_l2_hinge": 2, "multiclass_smooth_hinge": 3,
+            "hsoftmax": 4}
+MC_MAX_BLOCKS = 4096  # grid cap of the multiclass epilogue (64-row tiles, grid-stride beyond)
+_mc_scratch = {}
+
+
+def multiclass_row_loss(loss, S: torch.Tensor, y: torch.Tensor, wt: torch.Tensor, want_grad: bool = True):
+    """One fused pass over the rows of the multiclass linear model (``mc_row_loss_kernel``):
+    scores S fp32 [n, K-1] (the K-th logit is the implicit 0), labels y [n, K], weights [n] ->
+    (sum weight * loss (fp64 float), pred fp32 [n, K], D = weight * d1[:, :K-1] fp32 or None).
+    The formulas are the loss classes' fp64 ones (``losses/functions.py``; reference
+    MulticlassLinearHoagOptimizer.java:82-149). Returns None when the fused pass does not cover
+    the case (CPU tensors, K > 64, another loss, YTK_ROW_LOSS=0): the caller runs torch then."""
+    lid = _MC_LOSS.get(getattr(loss, "name", None))
+    if lid is None or S.device.type != "cuda" or os.environ.get("YTK_ROW_LOSS", "1") == "0":
+        return None
+    n, J = S.shape
+    K = J + 1
+    if K < 2 or K > 64 or S.dtype != torch.float32 or tuple(y.shape) != (n, K) or wt.numel() != n:
+        return None
+    S = S.contiguous()
+    y = y.float().contiguous()
+    wt = wt.float().contiguous()
+    check_cuda(S, y, wt)
+    dev = S.device
+    key = (dev.type, dev.index)
+    if key not in _mc_scratch:
+        _mc_scratch[key] = torch.empty(MC_MAX_BLOCKS + 8, dtype=torch.float64, device=dev)
+    buf = _mc_scratch[key]
+    pred = torch.empty((n, K), dtype=torch.float32, device=dev)
+    D = torch.empty((n, J), dtype=torch.float32, device=dev) if want_grad else None
+    hip().mc_row_loss(lid, ptr(S), K, ptr(y), ptr(wt), n, ptr(pred), ptr(D) if D is not None else 0, ptr(buf),
+                      MC_MAX_BLOCKS, ptr(buf[MC_MAX_BLOCKS:]), stream(S))
+    return float(buf[MC_MAX_BLOCKS]), pred, D

@@ -175,6 +175,26 @@ class Comm:
         g = self.group if t.device.type == "cuda" else self.cpu_group
         dist.broadcast(t, src=src, group=g)
 
+    def drain_pending(self):
+        """Before a HIP graph capture: wait until the nccl process group's watchdog thread has
+        retired every eager work handle. The watchdog polls its list of eager collectives
+        (~every 100 ms) and queries each one's end event; a query that lands while this thread
+        is capturing is refused by the HIP runtime, the watchdog throws, and the process
+        aborts (SIGABRT from ProcessGroupNCCL::Watchdog::run -- round 5's intermittent abort,
+        reproduced deterministically by tools/probe_capture_watchdog.py). Collectives issued
+        inside a capture are never handed to the watchdog, so after this drain the watchdog
+        has nothing to query until the capture ends."""
+        if not self.is_dist or self.group is None:
+            return
+        try:
+            if dist.get_backend(self.group) != "nccl":
+                return
+        except Exception:  # noqa: BLE001 -- no backend: nothing to drain
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.group._wait_for_pending_works()
+
     def barrier(self):
         if self.is_dist:
             self.last_op = ("barrier", "", 0)
