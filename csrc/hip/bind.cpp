@@ -81,7 +81,7 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
                       uintptr_t, int, uintptr_t, uintptr_t, long long, int, int, uintptr_t, uintptr_t,
                       int, int, uintptr_t);
 void ytk_ffm_sgd_grad(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                      uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, uintptr_t);
+                      uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, int, uintptr_t);
 void ytk_ffm_pairs_lds(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int, int,
                        uintptr_t, long long, uintptr_t);
 void ytk_ffm_pairs_fwd_e(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int,

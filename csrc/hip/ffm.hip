@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
     const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ chunk_fa,
     const int* __restrict__ chunk_col, const int* __restrict__ idx, const float* __restrict__ val, int m,
     const int* __restrict__ lay_field, const float* __restrict__ coef, const float* __restrict__ V, int nfield,
-    float* __restrict__ part, long long vt_nfeat) {
+    float* __restrict__ part, long long vt_nfeat, int skip_feat) {
   constexpr int GL = 8, PM = 8, k = 4 * KV, U = 4;
   const long long g = (blockIdx.x * 256LL + threadIdx.x) / GL;
   const int q = threadIdx.x & (GL - 1);
@@ -653,7 +653,9 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < PM; ++j) {
-          if (iq[u][j] == col || iq[u][j] < 0) continue;  // the entry itself / a skipped feature
+          // the entry itself / a padded position / the skipped feature (the bias without a
+          // latent factor: its V row need not be zero, e.g. continued from a model saved with one)
+          if (iq[u][j] == col || iq[u][j] < 0 || iq[u][j] == skip_feat) continue;
           const float s = val ? sc[u] * val[(long long)r[u] * m + q + GL * j] : sc[u];
           const float* vrow = vf + (long long)iq[u][j] * vs;
 #pragma unroll
@@ -915,7 +917,7 @@ void ytk_ffm_grad_stream(uintptr_t wave_chunk, long long nwaves, uintptr_t chunk
 void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, uintptr_t csc_rows, uintptr_t csc_vals,
                       uintptr_t chunk_fa, uintptr_t chunk_col, uintptr_t idx, uintptr_t val, int m, uintptr_t lay_field,
                       uintptr_t coef, uintptr_t V, int nfield, int k, uintptr_t part, long long vt_nfeat,
-                      uintptr_t stream) {
+                      int skip_feat, uintptr_t stream) {
   if (nch <= 0) return;
   if (m < 1 || m > 64 || m != nfield) throw std::invalid_argument("ffm_sgd_grad: need 1 <= m == nfield <= 64");
   if ((V & 3) || (part & 15)) throw std::invalid_argument("ffm_sgd_grad: V 4-B / part 16-B aligned");
@@ -928,7 +930,8 @@ void ytk_ffm_sgd_grad(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
   hipLaunchKernelGGL((ffm_sgd_grad_kernel<KV, AL>), grid, dim3(256), 0, s, (const long long*)chunk_beg,     \
                      (const long long*)chunk_end, nch, (const int*)csc_rows, (const float*)csc_vals,        \
                      (const int*)chunk_fa, (const int*)chunk_col, (const int*)idx, (const float*)val, m,    \
-                     (const int*)lay_field, (const float*)coef, (const float*)V, nfield, (float*)part, vt_nfeat)
+                     (const int*)lay_field, (const float*)coef, (const float*)V, nfield, (float*)part, vt_nfeat, \
+                     skip_feat)
   if (k == 4) YTK_FFM_SGD(1);
   else if (k == 8) YTK_FFM_SGD(2);
   else throw std::invalid_argument("ffm_sgd_grad: k must be 4 or 8");

@@ -614,6 +614,10 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
     }
     __syncthreads();
     emit_all_chunks(b.hist_items, nitems, nb, s_small, s_hbeg, s_hcnt, s_hslot, ch, false);
+    // build slots nb < k < half have no node this level: empty ranges, so the known-range
+    // reduce (one y block per build slot) reads no stale items left by an earlier level
+    if (b.hist_first)
+      for (int k = nb + 1 + tid; k <= half; k += kPlanThreads) b.hist_first[k] = nitems;
     if (tid == 0) {
       if (b.hist_first) b.hist_first[nb] = nitems;
       const int hs = half >> 1;
@@ -710,7 +714,7 @@ __device__ void lv_plan_children_body(const LvParams& p, const LvBufs& b, int cs
   // reads its slot's range from here instead of scanning the work list)
   if (b.hist_first) {
     for (int k = tid; k < nb; k += kPlanThreads) b.hist_first[k] = s_small[k];
-    if (tid == 0) b.hist_first[nb] = nitems;
+    for (int k = nb + tid; k <= half; k += kPlanThreads) b.hist_first[k] = nitems;  // nb < k: empty
   }
   if (tid == 0) {
     // items of the first half of the build slots (k < half/2): the multi-GPU engine

@@ -258,6 +258,25 @@ def test_rccl_world1_forced_dist(tmp_path, task, mode):
 
 
 @pytest.mark.gpu
+def test_capture_after_eager_rccl_drains_watchdog(tmp_path):
+    """Forced interleaving of the round-5 abort: eager RCCL all-reduces, then a GLOBAL-mode
+    capture held open ~0.8 s (8 watchdog polls) that also records captured all-reduces. Without
+    a drain this aborts the process from the watchdog's event query (tools/
+    probe_capture_watchdog.py global_nodrain, profiles/r6/watchdog_probe/); with
+    Comm.drain_pending -- what GBDTTrainer._graph_round calls before capturing -- the watchdog
+    holds no eager work during the capture and the process runs clean."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "probe_capture_watchdog.py"), str(tmp_path),
+                        "global_comm"], capture_output=True, text=True, timeout=200,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    log = open(tmp_path / "global_comm.log").read() if (tmp_path / "global_comm.log").exists() else ""
+    assert r.returncode == 0, r.stdout + _head_tail(log)
+    assert "PROBE_OK" in log and "Comm.drain_pending" in log
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("where", ["1", "2"])
 def test_rccl_world1_capture_failure_falls_back(tmp_path, where):
     """A round capture that fails (injected after the capture, "1", or inside it with the

@@ -194,3 +194,48 @@ def test_gpu_column_step_deterministic(cuda, nf, pad):
             o._step(w, b, e, 0.2, bts[j])
         outs.append(w)
     assert torch.equal(outs[0], outs[1])
+
+
+def _run_gpu_vs_cpu(name, nf, feats, pad, bounds, tol=1e-4, prep=None):
+    mc = _model(name, nf=nf, feats=feats, pad=pad)
+    mg = _model(name, nf=nf, feats=feats, dev="cuda", pad=pad)
+    if prep is not None:
+        prep(mc)
+        prep(mg)
+    oc, og = _opt(mc), _opt(mg)
+    wc, wg = mc.w.clone(), mg.w.clone()
+    oc._sync_copy(wc)
+    og._sync_copy(wg)
+    batches = og._setup(bounds)
+    for j, (b, e) in enumerate(bounds):
+        oc._step(wc, b, e, 0.2)
+        og._step(wg, b, e, 0.2, batches[j])
+        torch.testing.assert_close(wg.cpu(), wc, rtol=tol, atol=tol * 1e-2)
+    return og, batches
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nf,feats", [(8, 320), (62, 620)])
+def test_gpu_ffm_pair_terms_path_matches_cpu(cuda, monkeypatch, nf, feats):
+    """The forward-written pair terms path (ffm_pairs_k4_kernel<true>: E through a per-wave LDS
+    triangle, then ffm_sgd_ecol_kernel) against the CPU synchronous step -- taken in production
+    when the LDS-staged forward does not fit (m * (nfield + 1) * 16 > 64 KiB, e.g. m near 64) or
+    with YTK_FFM_LDS=0; forced here with the LDS-staged forward off, at m = 9 and m = 63."""
+    import ytk_learn_amd.ops.ffm as offm
+    monkeypatch.setattr(offm, "LDS_FWD", False)
+    og, batches = _run_gpu_vs_cpu("ffm", nf, feats, (-(nf * (feats // nf) + 1)) % 4,
+                                  [(0, 256), (256, 512)])
+    assert og.E is not None and all(bt.lay is not None for bt in batches)
+
+
+@pytest.mark.gpu
+def test_gpu_ffm_sgd_skips_bias_pairs_with_nonzero_bias_latent(cuda):
+    """bias_need_latent_factor = false excludes the bias from every pair even when its latent
+    row is not zero (a model continued from one saved with a bias latent): the GPU fixed-layout
+    pair gradient (ffm_sgd_grad_kernel, skip_feat) equals the CPU step, which skips it."""
+    def prep(m):
+        F, J = m.F, m.nf * m.kk
+        m.w[F:F + J] = torch.linspace(0.5, 1.5, J, device=m.w.device)  # feature 0 = the bias
+
+    og, batches = _run_gpu_vs_cpu("ffm", 8, 320, 0, [(0, 512), (512, 1024)], prep=prep)
+    assert og.E is None and all(bt.lay is not None for bt in batches)  # ffm_sgd_grad_kernel ran

@@ -15,7 +15,14 @@ in its own child process (a watchdog abort kills the process) and its FULL stder
   variants: <capture mode>_<drain>
     capture mode: global | thread_local | relaxed
     drain: nodrain (capture right after torch.cuda.synchronize), drain (also wait until the
-           process group's watchdog has retired every eager work: ProcessGroup._wait_for_pending_works)
+           process group's watchdog has retired every eager work: ProcessGroup._wait_for_pending_works),
+           comm (the package's Comm.drain_pending, which the GBDT trainer calls before its captures)
+
+Measured on MI355X (profiles/r6/watchdog_probe/): global_nodrain aborts with the round-5
+signature -- "Process group watchdog thread terminated with exception: HIP error: operation not
+permitted when stream is capturing", raised from the event query (HIPEvent.h:109) and rethrown
+at ProcessGroupNCCL.cpp:2099 -- while global_drain, thread_local_nodrain and thread_local_drain
+run clean.
 
 Usage: python tools/probe_capture_watchdog.py [outdir] [variant ...]
 """
@@ -43,6 +50,14 @@ def child(variant: str) -> None:
     for _ in range(4):  # eager collectives: work handles the watchdog tracks
         dist.all_reduce(x, async_op=True).wait()
     torch.cuda.synchronize(dev)
+    if drain == "comm":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from ytk_learn_amd.parallel.comm import Comm
+        c = Comm(0, 1, dev, pg, pg)
+        assert c.is_dist
+        t0 = time.perf_counter()
+        c.drain_pending()
+        print(f"[probe] Comm.drain_pending in {1e3 * (time.perf_counter() - t0):.1f} ms", file=sys.stderr, flush=True)
     if drain == "drain":
         t0 = time.perf_counter()
         pg._wait_for_pending_works()

@@ -144,7 +144,7 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[t
         src, vt_nfeat = (Vt, Xb.ncols) if (Vt is not None and FFM_VT) else (V, 0)
         h.ffm_sgd_grad(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
                        ptr(bt.chunk_fa), ptr(bt.chunk_col), ptr(Xb.indices), 0 if Xb.one_hot else ptr(Xb.values), m,
-                       ptr(lay_field), ptr(c), ptr(src), nfield, k, ptr(lat), vt_nfeat, s)
+                       ptr(lay_field), ptr(c), ptr(src), nfield, k, ptr(lat), vt_nfeat, int(skip_feat), s)
         return lat
     if Vt is None:
         raise RuntimeError("ffm sgd: the general pair-gradient kernel needs the transposed latents")

@@ -177,13 +177,14 @@ class Comm:
 
     def drain_pending(self):
         """Before a HIP graph capture: wait until the nccl process group's watchdog thread has
-        retired every eager work handle. The watchdog polls its list of eager collectives
-        (~every 100 ms) and queries each one's end event; a query that lands while this thread
-        is capturing is refused by the HIP runtime, the watchdog throws, and the process
-        aborts (SIGABRT from ProcessGroupNCCL::Watchdog::run -- round 5's intermittent abort,
-        reproduced deterministically by tools/probe_capture_watchdog.py). Collectives issued
-        inside a capture are never handed to the watchdog, so after this drain the watchdog
-        has nothing to query until the capture ends."""
+        retired every eager work handle. The watchdog keeps each eager collective until its
+        next poll (~100 ms) and then queries the work's end event; a query the HIP runtime
+        refuses because a capture is open ("operation not permitted when stream is
+        capturing") throws in the watchdog thread and aborts the process with SIGABRT from
+        ProcessGroupNCCL::Watchdog::run (reproduced in global capture mode by
+        tools/probe_capture_watchdog.py; docs/performance.md, round 6). Collectives issued
+        inside a capture are never handed to the watchdog, so after this drain it has nothing
+        to query until the capture ends, whatever the capture mode."""
         if not self.is_dist or self.group is None:
             return
         try:
