@@ -186,16 +186,25 @@ def main():
     el = time.perf_counter() - t0
     el = comm.allreduce_scalars([el], op="max")[0] if comm.is_dist else el
     # one L-BFGS two-loop + direction update (history full: m pairs)
+    # (history sharded over the ranks unless YTK_LBFGS_SHARD=0: this rank's slice of every pair,
+    # the per-step dot partials all-reduced, p all-gathered once -- timed with that traffic)
     m = 12
-    S = torch.randn((m, model.w.numel()), device=dev) * 1e-3
-    Y = torch.randn((m, model.w.numel()), device=dev) * 1e-3
-    opt.S, opt.Y, opt.YS = S, Y, [1.0] * m
+    opt.setup_history(model.w.numel(), dev)
+    if opt.shard and dev.type == "cuda":
+        from ytk_learn_amd.parallel import peer as peer_mod
+        P = comm.world
+        opt._peer = peer_mod.make(comm, -(-max(model.w.numel(), P * opt.seg) * 4 // 8))
+    opt.S.normal_(0.0, 1e-3)
+    opt.Y.normal_(0.0, 1e-3)
     p = -g
     sync()
     t1 = time.perf_counter()
     opt.hv(p, 0, m, 1.0, 1.0)
     sync()
     hv_ms = (time.perf_counter() - t1) * 1000
+    hist_mb = round(2 * opt.S.numel() * 4 / 2 ** 20, 1)
+    if getattr(opt, "_peer", None) is not None:
+        opt._peer.close()
     ms = 1000.0 * el / a.steps
     if comm.rank == 0:
         print(json.dumps({
@@ -203,7 +212,8 @@ def main():
                       f"{a.features} features, k={k})",
             "value": round(a.rows * comm.world / (el / a.steps), 1), "unit": "rows/s",
             "ms_per_step": round(ms, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows, "dim": int(model.w.numel()),
-            "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "setup_s": round(setup_s, 2),
+            "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "lbfgs_history_shard": bool(opt.shard),
+            "lbfgs_history_mib_per_rank": hist_mb, "setup_s": round(setup_s, 2),
             "scaling": "weak", "dtype": "fp32", "data": "synthetic Criteo-shape", "loss": loss / tot,
             "gbst_fused": (os.environ.get("YTK_GBST_FUSED", "1") != "0") if a.model.startswith("gb") else None,
             "row_loss_fused": os.environ.get("YTK_ROW_LOSS", "1") != "0",

@@ -68,30 +68,38 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
                        "peer_overlap": peer_overlap}, f)
 
 
-def write_lines(path, n, seed):
+def write_lines(path, n, seed, fields=False):
+    """Sparse binary lines; fields=True names feature i "f<i % 3>@x<i>" (FFM field@name)."""
     w = np.random.default_rng(99).normal(size=30)
     g = np.random.default_rng(seed)
+    name = (lambda i: f"f{i % 3}@x{i}") if fields else (lambda i: f"x{i}")
     with open(path, "w") as f:
         for _ in range(n):
             idx = np.unique(g.integers(0, 30, size=6))
             v = g.random(len(idx))
             y = int((w[idx] * v).sum() > 0)
-            f.write("1###%d###%s\n" % (y, ",".join(f"x{i}:{x:.4f}" for i, x in zip(idx, v))))
+            f.write("1###%d###%s\n" % (y, ",".join(f"{name(i)}:{x:.4f}" for i, x in zip(idx, v))))
 
 
 def run_linear(comm, out, device, model_name, sgd=False):
     from ytk_learn_amd.config.hocon import parse_file
     from ytk_learn_amd.train import train
     tr_path, te_path = os.path.join(out, "train.txt"), os.path.join(out, "test.txt")
+    ffm = model_name == "ffm"
+    fd_path = os.path.join(out, "fields.txt")
     if comm.rank == 0 and not os.path.exists(tr_path):
-        write_lines(tr_path, 4000, 1)
-        write_lines(te_path, 1000, 2)
+        write_lines(tr_path, 4000, 1, fields=ffm)
+        write_lines(te_path, 1000, 2, fields=ffm)
+        with open(fd_path, "w") as f:
+            f.write("f0\nf1\nf2\n")
     comm.barrier()
     cfg = parse_file(os.path.join(ROOT, "config", "model", f"{model_name}.conf")).with_overrides({
         "data.train.data_path": tr_path, "data.test.data_path": te_path,
         "model.data_path": os.path.join(out, f"{model_name}_w{comm.world}.model"),
         "optimization.line_search.lbfgs.convergence.max_iter": 10, "k": 4 if model_name != "fm" else [1, 4],
         "tree_num": 2})
+    if ffm:
+        cfg = cfg.with_overrides({"model.field_dict_path": fd_path, "k": [1, 4]})
     if sgd:
         cfg = cfg.with_overrides({"optimization.optimizer": "sgd", "optimization.sgd.learning_rate": 0.05,
                                   "optimization.sgd.batch_size": 128, "optimization.sgd.epochs": 4,
@@ -224,7 +232,7 @@ def main():
             run_gbdt(comm, out, dev, "loss")
         elif task == "gbdt_l1":  # l1 loss: leaf refine by the exact distributed weighted median
             run_gbdt(comm, out, dev, "level", loss="l1")
-        elif task in ("linear", "fm", "gbmlr", "gbhsdt"):
+        elif task in ("linear", "fm", "ffm", "gbmlr", "gbhsdt", "multiclass_linear"):
             run_linear(comm, out, dev, task)
         elif task in ("fm_sgd", "linear_sgd"):
             run_linear(comm, out, dev, task.split("_")[0], sgd=True)

@@ -136,10 +136,16 @@ def test_gbdt_l1_exact_refine_world_n(tmp_path, world):
     _same_collective_sequence(tmp_path / f"w{world}", world)
 
 
-@pytest.mark.parametrize("task,world", [("linear", 2), ("gbmlr", 2), ("linear", 8), ("gbmlr", 4)])
-def test_lbfgs_world_n_matches_world1(tmp_path, task, world):
+@pytest.mark.parametrize("task,world,shard", [("linear", 2, "1"), ("gbmlr", 2, "1"), ("linear", 8, "1"),
+                                              ("gbmlr", 4, "1"), ("fm", 2, "1"), ("fm", 4, "1"), ("ffm", 2, "1"),
+                                              ("ffm", 4, "1"), ("linear", 4, "1"), ("linear", 2, "0"),
+                                              ("ffm", 2, "0")])
+def test_lbfgs_world_n_matches_world1(tmp_path, task, world, shard):
+    """L-BFGS at world N (gloo) reaches the world-1 losses: with the (s, y) history sharded
+    over the ranks (shard "1", the default: per-step dot partials all-reduced, p all-gathered;
+    HoagOptimizer.java:441-449,904-929) and replicated (YTK_LBFGS_SHARD=0)."""
     r1 = _run(task, tmp_path / "w1", 1)
-    r2 = _run(task, tmp_path / f"w{world}", world)
+    r2 = _run(task, tmp_path / f"w{world}", world, extra_env={"YTK_LBFGS_SHARD": shard})
     np.testing.assert_allclose(r2["loss"], r1["loss"], rtol=1e-4)
     np.testing.assert_allclose(r2["test_loss"], r1["test_loss"], rtol=1e-3)
     if task == "linear":
@@ -317,11 +323,12 @@ def test_peer_world1_forced_dist(tmp_path, task):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("task,two_shot", [("linear", "0"), ("fm", "1"), ("gbmlr", "0")])
+@pytest.mark.parametrize("task,two_shot", [("linear", "0"), ("fm", "1"), ("gbmlr", "0"), ("ffm", "1")])
 def test_lbfgs_peer_gradient_allreduce_one_gpu(tmp_path, task, two_shot):
     """Two ranks on the one GPU: the L-BFGS gradient all-reduce over the peer-memory exchange
     (fp32, rank-order sums; two_shot "0": every message two-shot reduce-scatter + all-gather,
-    "1": the default size split) reaches the gloo run's losses to 1e-6."""
+    "1": the default size split) reaches the gloo run's losses to 1e-6. The sharded (s, y)
+    history's dot partials and the p all-gather ride the peer exchange too."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

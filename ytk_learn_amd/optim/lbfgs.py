@@ -10,13 +10,18 @@ Reference: ``J/optimizer/HoagOptimizer.java``
   Hv two-loop               :904-929
   hyper search              :314-434 (grid), :813-902 (HOAG)
 
-MI355X design: w, g, p and the (s, y) history are fp32 device tensors; every rank holds
-the full history (m x dim x 2 x 4 B: 15 GB even for a 157M-dim FFM -- HBM is 288 GB) and
-runs the two-loop redundantly. That replaces the reference's sharded history (2m scalar
-allreduces + 2 allgathers per iteration) with zero communication; the only per-evaluation
-collective is the fp32 gradient all-reduce (RCCL over xGMI) plus one small fp64 loss
-vector. Dots/norms are computed in fp64 on the device; results are identical on every
-rank because the all-reduced gradient is.
+MI355X design: w, g, p and the (s, y) history are fp32 device tensors. With P > 1 ranks the
+history is SHARDED like the reference's TwoLoop slices (HoagOptimizer.java:441-449): rank r
+keeps [r * seg, (r + 1) * seg) of every s and y (seg = ceil(dim / P) rounded to 16 B), so
+per-rank history memory and two-loop traffic drop by P. Each two-loop step's dot product is
+a local fp64 partial summed over the ranks (one 8-byte all-reduce; the peer-memory exchange
+on one node), the ys / yy pair rides one all-reduce, and the finished direction is
+all-gathered ONCE (the reference gathers p twice, :904-929; the middle gather is redundant
+because the scaling is element-wise). YTK_LBFGS_SHARD=0 keeps the full history on every
+rank (redundant two-loop, no two-loop communication). The per-evaluation collectives are
+the fp32 gradient all-reduce (RCCL over xGMI or the peer exchange) plus one small fp64 loss
+vector. Dots/norms are computed in fp64 on the device; results are identical on every rank
+because the all-reduced gradient and the all-reduced dot products are.
 """
 from __future__ import annotations
 
@@ -267,10 +272,69 @@ class HoagOptimizer:
                 return -3
             step *= factor
 
+    # ------------------------------------------------------------------ history shards
+    def setup_history(self, dim: int, dev) -> None:
+        """Allocate the (s, y) history: this rank's slice [lo, hi) of every pair (the whole
+        vector on one rank or with YTK_LBFGS_SHARD=0)."""
+        m = self.ls.m
+        P = self.comm.world if (self.comm is not None and self.comm.is_dist) else 1
+        self.shard = P > 1 and os.environ.get("YTK_LBFGS_SHARD", "1") != "0"
+        self.dim = dim
+        if self.shard:
+            seg = -(-dim // P)
+            seg = -(-seg // 4) * 4  # whole 16-B units: equal all-gather segments
+            r = self.comm.rank
+            self.seg, self.lo, self.hi = seg, min(dim, r * seg), min(dim, (r + 1) * seg)
+            self._gbuf = torch.zeros(P * seg, dtype=torch.float32, device=dev)  # all-gather buffer
+            self.log.info(f"[lbfgs] (s, y) history sharded over {P} ranks: this rank keeps "
+                          f"[{self.lo}, {self.hi}) of {dim}")
+        else:
+            self.seg, self.lo, self.hi = dim, 0, dim
+            self._gbuf = None
+        n = self.hi - self.lo
+        self.S = torch.zeros((m, n), dtype=torch.float32, device=dev)
+        self.Y = torch.zeros((m, n), dtype=torch.float32, device=dev)
+        self.YS = [1.0] * m
+
+    def _gsum(self, vals: List[float]) -> List[float]:
+        """Sum per-rank fp64 partials of the sharded history over the ranks (one collective;
+        the peer-memory exchange when the job has one); identity when not sharded."""
+        if not getattr(self, "shard", False):
+            return vals
+        peer = getattr(self, "_peer", None)
+        if peer is not None:
+            t = torch.tensor(vals, dtype=torch.float64, device=self.S.device)
+            peer.allreduce_(t)
+            out = t.tolist()  # synchronises: the exchange has landed
+            peer.check()
+            return out
+        return self.comm.allreduce_scalars(vals)
+
+    def _gather_p(self, p: torch.Tensor):
+        """p's slices [lo, hi) from every rank -> the whole p on every rank (one all-gather)."""
+        P, r, seg = self.comm.world, self.comm.rank, self.seg
+        buf = self._gbuf
+        mine = buf[r * seg:(r + 1) * seg]
+        n = self.hi - self.lo
+        if n:
+            mine[:n].copy_(p[self.lo:self.hi])
+        peer = getattr(self, "_peer", None)
+        if peer is not None and peer.fits_segments(buf):
+            peer.allgather_(buf)
+            p.copy_(buf[:self.dim])
+            torch.cuda.current_stream(p.device).synchronize()
+            peer.check()
+        else:
+            allp = self.comm.allgather(mine)
+            p.copy_(allp[:self.dim])
+
     # ------------------------------------------------------------------ two loop
     def hv(self, p: torch.Tensor, cursor: int, loops: int, ys: float, yy: float):
         """p <- H p with the last ``loops`` pairs ending before ``cursor`` (Hv, :904-929)."""
         m = self.ls.m
+        if getattr(self, "shard", False):
+            self._hv_sharded(p, cursor, loops, ys, yy)
+            return
         if loops > 0 and self._fused_two_loop(p):
             self._hv_fused(p, cursor, loops, ys, yy)
             return
@@ -315,6 +379,46 @@ class HoagOptimizer:
             else:
                 p.add_(self.S[c], alpha=alphas[c] - b)
 
+    def _hv_sharded(self, p: torch.Tensor, cursor: int, loops: int, ys: float, yy: float):
+        """hv over this rank's history slice: every dot product is a local partial summed over
+        the ranks (_gsum), every update touches only p[lo:hi]; one all-gather of p at the end.
+        The update + next dot of a step are one pass (blas.axpy_dot) on the GPU."""
+        m = self.ls.m
+        pl = p[self.lo:self.hi]
+        fused = self._fused_two_loop(p) and pl.numel() > 0
+
+        def step(x, alpha, scale, d):  # pl <- (pl + alpha x) * scale; local d . pl
+            if fused:
+                return blas.axpy_dot(pl, x, alpha, scale, d)
+            pl.add_(x, alpha=alpha)
+            if scale != 1.0:
+                pl.mul_(scale)
+            return _dot(d, pl)
+
+        if loops <= 0:
+            p.mul_(ys / yy)
+            return
+        alphas = [0.0] * m
+        c = (cursor + m - 1) % m
+        a = self._gsum([_dot(self.S[c], pl)])[0] / self.YS[c]
+        b = 0.0
+        for k in range(loops):
+            alphas[c] = a
+            if k + 1 < loops:  # pl -= a Y[c]; next: S[c - 1] . p
+                nc = (c + m - 1) % m
+                a = self._gsum([step(self.Y[c], -a, 1.0, self.S[nc])])[0] / self.YS[nc]
+                c = nc
+            else:  # pl = (pl - a Y[c]) * ys / yy; the second loop starts at this c: Y[c] . p
+                b = self._gsum([step(self.Y[c], -a, ys / yy, self.Y[c])])[0] / self.YS[c]
+        for k in range(loops):
+            if k + 1 < loops:  # pl += (alpha - b) S[c]; next: Y[c + 1] . p
+                nc = (c + 1) % m
+                b_next = self._gsum([step(self.S[c], alphas[c] - b, 1.0, self.Y[nc])])[0] / self.YS[nc]
+                c, b = nc, b_next
+            else:
+                pl.add_(self.S[c], alpha=alphas[c] - b)
+        self._gather_p(p)
+
     # ------------------------------------------------------------------ grid setup
     def _grid_points(self):
         hp = self.hp
@@ -338,7 +442,9 @@ class HoagOptimizer:
         self._peer = None
         if self.comm is not None and self.comm.is_dist and w.is_cuda:
             from ..parallel import peer as peer_mod
-            self._peer = peer_mod.make(self.comm, -(-w.numel() * 4 // 8))
+            P = self.comm.world
+            gather = P * (-(-(-(-w.numel() // P)) // 4) * 4)  # the sharded p all-gather buffer
+            self._peer = peer_mod.make(self.comm, -(-max(w.numel(), gather) * 4 // 8))
         res = self._run(w)
         if self._peer is not None:  # collective: every rank leaves run() together
             self._peer.close()
@@ -362,9 +468,8 @@ class HoagOptimizer:
         g = torch.zeros(dim, dtype=torch.float32, device=dev)
         wprev, gprev = torch.empty_like(w), torch.empty_like(w)
         p = torch.empty_like(w)
-        self.S = torch.zeros((m, dim), dtype=torch.float32, device=dev)
-        self.Y = torch.zeros((m, dim), dtype=torch.float32, device=dev)
-        self.YS = [1.0] * m
+        self.setup_history(dim, dev)
+        lo, hi = self.lo, self.hi
         test_loss = None
         status, it, cursor = 0, 1, 0
         ys = yy = 1.0
@@ -441,10 +546,9 @@ class HoagOptimizer:
                     break
                 if self.dump_freq > 0 and it % self.dump_freq == 0:
                     self._dump(w)
-                torch.sub(w, wprev, out=self.S[cursor])
-                torch.sub(g, gprev, out=self.Y[cursor])
-                ys = _dot(self.Y[cursor], self.S[cursor])
-                yy = _dot(self.Y[cursor], self.Y[cursor])
+                torch.sub(w[lo:hi], wprev[lo:hi], out=self.S[cursor])
+                torch.sub(g[lo:hi], gprev[lo:hi], out=self.Y[cursor])
+                ys, yy = self._gsum([_dot(self.Y[cursor], self.S[cursor]), _dot(self.Y[cursor], self.Y[cursor])])
                 if ys < 1.0e-60:
                     self._info(it, f"ys:{jd(ys)} is too small or is negtive(you may change to wolfe condition!), "
                                    "set to 0.01*yy!")
