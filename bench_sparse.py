@@ -203,6 +203,21 @@ def main():
     sync()
     hv_ms = (time.perf_counter() - t1) * 1000
     hist_mb = round(2 * opt.S.numel() * 4 / 2 ** 20, 1)
+    # the local compute of one rank's sharded two-loop at P = 8: the same 12-pair recursion over
+    # a 1/8 slice of the model vector (its 24 scalar all-reduces and the p all-gather excluded)
+    seg8 = -(-(-(-model.w.numel() // 8)) // 4) * 4
+    opt8 = HoagOptimizer(model, LineSearchParams(m=12), [0.0] * ng, [1e-6] * ng, None, log, tot)
+    opt8.setup_history(seg8, dev)
+    opt8.S.normal_(0.0, 1e-3)
+    opt8.Y.normal_(0.0, 1e-3)
+    p8 = torch.randn(seg8, device=dev)
+    opt8.hv(p8, 0, m, 1.0, 1.0)  # warm
+    sync()
+    t1 = time.perf_counter()
+    opt8.hv(p8, 0, m, 1.0, 1.0)
+    sync()
+    hv8_ms = (time.perf_counter() - t1) * 1000
+    del opt8, p8
     if getattr(opt, "_peer", None) is not None:
         opt._peer.close()
     ms = 1000.0 * el / a.steps
@@ -213,6 +228,7 @@ def main():
             "value": round(a.rows * comm.world / (el / a.steps), 1), "unit": "rows/s",
             "ms_per_step": round(ms, 3), "n_gpus": comm.world, "rows_per_gpu": a.rows, "dim": int(model.w.numel()),
             "nnz_per_row": a.fields + 1, "lbfgs_two_loop_ms": round(hv_ms, 3), "lbfgs_history_shard": bool(opt.shard),
+            "lbfgs_two_loop_ms_local_at_1_8_slice": round(hv8_ms, 3),
             "lbfgs_history_mib_per_rank": hist_mb, "setup_s": round(setup_s, 2),
             "scaling": "weak", "dtype": "fp32", "data": "synthetic Criteo-shape", "loss": loss / tot,
             "gbst_fused": (os.environ.get("YTK_GBST_FUSED", "1") != "0") if a.model.startswith("gb") else None,
