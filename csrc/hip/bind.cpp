@@ -48,8 +48,8 @@ void ytk_partition_count(uintptr_t, int, long long, uintptr_t, uintptr_t, uintpt
 void ytk_tree_add_bins(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, int, uintptr_t, int, int, uintptr_t);
 int ytk_forest_loss_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                         uintptr_t, int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, float, float, uintptr_t,
-                         uintptr_t, int, uintptr_t);
+                         uintptr_t, int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, float, float,
+                         uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_acc_finish(uintptr_t, int, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 int ytk_forest_predict_regs(uintptr_t, long long, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                             uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, int, float, uintptr_t, uintptr_t);
@@ -58,10 +58,10 @@ void ytk_forest_predict(uintptr_t, long long, long long, uintptr_t, uintptr_t, u
                         float, uintptr_t, uintptr_t);
 void ytk_bin_assign(uintptr_t, long long, long long, int, uintptr_t, uintptr_t, uintptr_t, int,
                     long long, uintptr_t, uintptr_t);
-void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, int, float, float,
+void ytk_grad_hess(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, int, float, float,
                    uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t);
 int ytk_tree_grad(uintptr_t, int, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                   uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
+                   uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int,
                    float, float, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t,
                    uintptr_t);
 int ytk_tree_grad_grid(long long);
@@ -139,7 +139,7 @@ void ytk_lw_zero_slots(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, in
 void ytk_seg_median(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, int, uintptr_t, uintptr_t);
 void ytk_seg_prune(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
 int ytk_tree_grad_hist(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
-                       uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
+                       uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, int, float, float, uintptr_t, uintptr_t, uintptr_t,
                        uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int,
                        uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, long long, uintptr_t);
 void ytk_copy_to_mapped(uintptr_t, uintptr_t, long long, uintptr_t);

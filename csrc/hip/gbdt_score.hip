@@ -16,6 +16,8 @@
 // fixed-point histogram scales need (block max -> one uint atomicMax per block).
 #include "common.h"
 
+#include <stdexcept>
+
 namespace ytk {
 
 // ------------------------------------------------------------------ scoring
@@ -219,8 +221,11 @@ struct LossOut {
 
 // kLoss is a compile-time parameter of the kernels: only the selected loss's fp64 code is
 // compiled into a kernel (a runtime switch over all five kept ~200 VGPRs live: 2 waves/SIMD)
+// lgy1: the Poisson loss's label term lgamma(y + 1), computed once per data set on the host side
+// (ops/gbdt.py): the device lgamma inlined into the fused gradient + histogram kernel cost 238
+// VGPR spills and 512 B of scratch per thread (as gbst.hip's GbstArgs::lgy)
 template <int kLoss>
-__device__ __forceinline__ LossOut point_loss(double z, double y, double p0) {
+__device__ __forceinline__ LossOut point_loss(double z, double y, double p0, double lgy1 = 0.0) {
   LossOut o;
   switch (kLoss) {
     case 0: {  // sigmoid (SigmoidFunction: stable log-loss, zmax hessian clamp)
@@ -252,7 +257,7 @@ __device__ __forceinline__ LossOut point_loss(double z, double y, double p0) {
     case 3: {
       const double zc = fmin(z, 30.0);
       const double ez = exp(zc);
-      o.l = -y * z + ez + lgamma(y + 1.0);
+      o.l = -y * z + ez + lgy1;
       o.p = (float)ez;
       o.g = (double)o.p - y; o.h = (double)o.p;
       break;
@@ -354,8 +359,9 @@ __global__ __launch_bounds__(256) void forest_loss_regs_kernel(
     const float* __restrict__ X, long long N, const int* __restrict__ nfeat, const float* __restrict__ nthr,
     const int* __restrict__ nleft, const int* __restrict__ nright, const uint8_t* __restrict__ ndefl,
     const float* __restrict__ nval, int root, int nnodes, float* __restrict__ score,
-    const float* __restrict__ init, const float* __restrict__ label, const float* __restrict__ weight, float p0,
-    float score_div, float* __restrict__ pred, double* __restrict__ loss_acc) {
+    const float* __restrict__ init, const float* __restrict__ label, const double* __restrict__ lgy,
+    const float* __restrict__ weight, float p0, float score_div, float* __restrict__ pred,
+    double* __restrict__ loss_acc) {
   extern __shared__ __attribute__((aligned(16))) int fsm[];
   int* sf = fsm;
   float* sth = reinterpret_cast<float*>(fsm + nnodes);
@@ -395,7 +401,8 @@ __global__ __launch_bounds__(256) void forest_loss_regs_kernel(
     }
     const float s = s0 + 1.0f * sv[n];  // forest_predict: out += scale * value, scale 1
     score[r] = s;
-    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0,
+                                        kLoss == 3 ? lgy[r] : 0.0);
     lsum += (double)w * o.l;
     wsum += (double)w;
     if (pred) pred[r] = o.p;
@@ -456,7 +463,7 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     const BinT* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
     const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
     const float* __restrict__ tval, int nnodes, float* __restrict__ score,
-    const float* __restrict__ init, const float* __restrict__ label,
+    const float* __restrict__ init, const float* __restrict__ label, const double* __restrict__ lgy,
     const float* __restrict__ weight, long long N, int loss_id, float p0, float score_div,
     float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
     int want_grad, float* __restrict__ ghmax, int* __restrict__ leaf_part) {
@@ -486,7 +493,8 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     s += sv[n];
     score[r] = s;
     if (leaf_part) atomicAdd(&sc[n], 1);
-    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+    const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0,
+                                        kLoss == 3 ? lgy[r] : 0.0);
     lsum += (double)w * o.l;
     wsum += (double)w;
     if (pred) pred[r] = o.p;
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(256) void tree_grad_kernel(
     }
     const float w = weight ? weight[r] : 1.f;
     const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)init[r], (double)label[r],
-                                        (double)p0);
+                                        (double)p0, kLoss == 3 ? lgy[r] : 0.0);
     lsum += (double)w * o.l;
     wsum += (double)w;
     if (pred) pred[r] = o.p;
@@ -634,12 +642,12 @@ __device__ __forceinline__ void tgh_add_row(const uint32_t (&d)[8], int rot, uns
   }
 }
 
-template <int kLoss>
+template <int kLoss, int kRows>
 __global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
     const uint8_t* __restrict__ bins, long long stride, const int* __restrict__ tfeat,
     const int* __restrict__ tthr, const int* __restrict__ tleft, const int* __restrict__ tright,
     const float* __restrict__ tval, int nnodes, float* __restrict__ score,
-    const float* __restrict__ init, const float* __restrict__ label,
+    const float* __restrict__ init, const float* __restrict__ label, const double* __restrict__ lgy,
     const float* __restrict__ weight, long long N, float p0, float score_div,
     float* __restrict__ pred, float2* __restrict__ gh, double* __restrict__ loss_acc,
     float* __restrict__ ghmax, int* __restrict__ leaf_part, int nvb, const float* __restrict__ scales,
@@ -684,7 +692,8 @@ __global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
       s += sv[n];
       score[r] = s;
       if (leaf_part) atomicAdd(&scv[n], 1);
-      const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0);
+      const LossOut o = point_loss<kLoss>((double)s / (double)score_div + (double)ini, (double)lab, (double)p0,
+                                          kLoss == 3 ? lgy[r] : 0.0);
       lsum += (double)w * o.l;
       wsum += (double)w;
       if (pred) pred[r] = o.p;
@@ -694,7 +703,7 @@ __global__ __launch_bounds__(kTGHThreads) void tree_grad_hist_kernel(
       mh = fmaxf(mh, fabsf(hh));
       tgh_add_row(d, rot, tgh_fx_round(gg * sg), tgh_fx_round(hh * sh), hsm);
     };
-    constexpr int U = kTreeGradRows;
+    constexpr int U = kRows;  // rows in flight per thread (YTK_TGH_ROWS)
     for (; r0 + (U - 1) * G < N; r0 += U * G) {
       uint32_t d[U][8];
       float sc0[U], in0[U], lb0[U], wt0[U];
@@ -843,6 +852,15 @@ static inline int grid_for(long long n, int cap) {
 // that the root reduce reads back, so fewer, longer blocks trade row parallelism for flush +
 // reduce bytes. Measured (profiles/r5/chk4_*_vb*): 2048 -> 1024 virtual blocks 1.333 ->
 // 1.315 ms per full tree, 0.433 -> 0.418 ms at the 1/8 shard; 512: 1.508 / 0.437.
+// rows each thread of the fused pass keeps in flight (YTK_TGH_ROWS = 1 | 2)
+static int tgh_rows() {
+  static const int v = [] {
+    const char* e = getenv("YTK_TGH_ROWS");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
+
 static int tgh_vblocks(long long N) {
   static const int cap = [] {
     const char* e = getenv("YTK_TGH_VBLOCKS");
@@ -893,9 +911,11 @@ void ytk_forest_predict(uintptr_t X, long long xstride, long long N, uintptr_t n
 // (nothing launched) when the row layout / tree size does not qualify.
 int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t nfeat, uintptr_t nthr,
                          uintptr_t nleft, uintptr_t nright, uintptr_t ndefl, uintptr_t nval, int root, int nnodes,
-                         uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight, int loss_id, float p0,
-                         float score_div, uintptr_t pred, uintptr_t loss_acc, int finish, uintptr_t stream) {
+                         uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t lgy, uintptr_t weight,
+                         int loss_id, float p0, float score_div, uintptr_t pred, uintptr_t loss_acc, int finish,
+                         uintptr_t stream) {
   if (N <= 0) return 0;
+  if (loss_id == 3 && !lgy) throw std::invalid_argument("forest_loss_regs: poisson needs lgamma(y + 1)");
   const int kf4 = (int)(xstride / 4);
   if (xstride % 4 != 0 || kf4 < 1 || kf4 > 8 || (X % 16) != 0 || nnodes <= 0 || nnodes > 2048 || loss_id < 0 ||
       loss_id > 4)
@@ -908,7 +928,8 @@ int ytk_forest_loss_regs(uintptr_t X, long long xstride, long long N, uintptr_t 
   hipLaunchKernelGGL((forest_loss_regs_kernel<K, L>), dim3(grid), dim3(256), lds, s, (const float*)X, N,      \
                      (const int*)nfeat, (const float*)nthr, (const int*)nleft, (const int*)nright,              \
                      (const uint8_t*)ndefl, (const float*)nval, root, nnodes, (float*)score, (const float*)init, \
-                     (const float*)label, (const float*)weight, p0, score_div, (float*)pred, (double*)loss_acc)
+                     (const float*)label, (const double*)lgy, (const float*)weight, p0, score_div, (float*)pred, \
+                     (double*)loss_acc)
 #define YTK_FLR_L(K)                          \
   switch (loss_id) {                          \
     case 0: YTK_FLR(K, 0); break;             \
@@ -1011,11 +1032,12 @@ void ytk_bin_assign(uintptr_t X, long long xstride, long long N, int F, uintptr_
 }
 
 // score [N][K], init [N][K], label [N][K], gh [K][N]; pred / ghmax optional (0)
-void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
+void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t lgy, uintptr_t weight,
                    long long N, int K, int loss_id, float p0, float score_div, uintptr_t pred,
                    uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
                    uintptr_t stream) {
   if (N <= 0) return;
+  if (loss_id == 3 && !lgy) throw std::invalid_argument("grad_hess: poisson needs lgamma(y + 1)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_for(N, 256 * 8);
   if (loss_id == 5) {
@@ -1028,7 +1050,7 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
   hipLaunchKernelGGL((tree_grad_kernel<uint8_t, 0, LID>), dim3(grid), dim3(256), 0, s,             \
                      (const uint8_t*)nullptr, 0LL, (const int*)nullptr, (const int*)nullptr,        \
                      (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, 0,            \
-                     (float*)score, (const float*)init, (const float*)label,                        \
+                     (float*)score, (const float*)init, (const float*)label, (const double*)lgy,    \
                      (const float*)weight, N, loss_id, p0, score_div, (float*)pred,                 \
                      (float2*)gh, (double*)loss_acc, want_grad, (float*)ghmax, (int*)nullptr)
     switch (loss_id) {
@@ -1051,11 +1073,12 @@ void ytk_grad_hess(uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t w
 // LDS with the node arrays -- the caller must then count leaves another way.
 int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfeat,
                    uintptr_t tthr, uintptr_t tleft, uintptr_t tright, uintptr_t tval, int nnodes,
-                   uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t weight,
+                   uintptr_t score, uintptr_t init, uintptr_t label, uintptr_t lgy, uintptr_t weight,
                    long long N, int loss_id, float p0, float score_div, uintptr_t pred,
                    uintptr_t gh, uintptr_t loss_acc, int want_grad, uintptr_t ghmax,
                    uintptr_t leaf_part, uintptr_t leaf_out, uintptr_t stream) {
   if (N <= 0) return 1;
+  if (loss_id == 3 && !lgy) throw std::invalid_argument("tree_grad: poisson needs lgamma(y + 1)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // leaf_part (optional, >= grid * nnodes ints) + leaf_out (nnodes doubles): rows per tree
   // node -- the level engine's last-level leaf counts, taken from this walk instead of a
@@ -1085,7 +1108,7 @@ int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfe
   hipLaunchKernelGGL((tree_grad_kernel<BT, DW, LID, LW>), dim3(grid), dim3(256), lds + ((LW) ? lds_rows : 0), s, (const BT*)bins, \
                      stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,                \
                      (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
-                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
+                     (const float*)init, (const float*)label, (const double*)lgy, (const float*)weight, N, loss_id, \
                      p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,        \
                      (float*)ghmax, (int*)leaf_part)
 #define YTK_TG_LAUNCH(BT, DW)                   \
@@ -1103,7 +1126,7 @@ int ytk_tree_grad(uintptr_t bins, int bin_bytes, long long stride, uintptr_t tfe
   hipLaunchKernelGGL((tree_grad_kernel<BT, 0, LID, false, true>), dim3(grid), dim3(256), 0, s, (const BT*)bins, \
                      stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft,                \
                      (const int*)tright, (const float*)tval, nnodes, (float*)score,                 \
-                     (const float*)init, (const float*)label, (const float*)weight, N, loss_id,     \
+                     (const float*)init, (const float*)label, (const double*)lgy, (const float*)weight, N, loss_id, \
                      p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc, want_grad,        \
                      (float*)ghmax, (int*)nullptr)
 #define YTK_TG_GL(BT)                         \
@@ -1152,7 +1175,8 @@ void ytk_hist_reduce(uintptr_t staging, uintptr_t work, int nwork, uintptr_t his
 // zero); staging: >= ceil(grid) * B * 32 * 16 bytes; work: >= grid int4 zeros.
 int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintptr_t tthr, uintptr_t tleft,
                        uintptr_t tright, uintptr_t tval, int nnodes, uintptr_t score, uintptr_t init, uintptr_t label,
-                       uintptr_t weight, long long N, int loss_id, float p0, float score_div, uintptr_t pred,
+                       uintptr_t lgy, uintptr_t weight, long long N, int loss_id, float p0, float score_div,
+                       uintptr_t pred,
                        uintptr_t gh, uintptr_t loss_acc, uintptr_t ghmax, uintptr_t leaf_part, uintptr_t leaf_out,
                        uintptr_t scales, uintptr_t staging, uintptr_t work, uintptr_t root_slot, int B, int F,
                        uintptr_t acc_out, uintptr_t acc2, int nblocks2, uintptr_t acc2_out, uintptr_t zero,
@@ -1163,6 +1187,7 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
   // acc2_out (optional): another pass's partials (the test-set tail) finished by the same
   // launch -- the round's sums then sit next to each other for one readback copy
   if (N <= 0 || nnodes <= 0) return 0;
+  if (loss_id == 3 && !lgy) throw std::invalid_argument("tree_grad_hist: poisson needs lgamma(y + 1)");
   if (stride != 32 || (bins % 16) != 0 || B > 256 || F > 32 || loss_id < 0 || loss_id > 4) return 0;
   const size_t lds = kTGHHistBytes + (size_t)nnodes * 5 * sizeof(int) +
                      (leaf_part ? (size_t)kTGHVirtual * nnodes * sizeof(int) : 0);
@@ -1172,11 +1197,13 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int nvb = tgh_vblocks(N);  // virtual blocks (tree_grad_kernel's grid by default)
   const int grid = (nvb + kTGHVirtual - 1) / kTGHVirtual;
-#define YTK_TGH(LID)                                                                                          \
-  hipLaunchKernelGGL((tree_grad_hist_kernel<LID>), dim3(grid), dim3(kTGHThreads), lds, s, (const uint8_t*)bins,  \
+#define YTK_TGH(LID) \
+  do { if (tgh_rows() == 1) YTK_TGH2(LID, 1); else YTK_TGH2(LID, 2); } while (0)
+#define YTK_TGH2(LID, U)                                                                                      \
+  hipLaunchKernelGGL((tree_grad_hist_kernel<LID, U>), dim3(grid), dim3(kTGHThreads), lds, s, (const uint8_t*)bins, \
                      stride, (const int*)tfeat, (const int*)tthr, (const int*)tleft, (const int*)tright,         \
                      (const float*)tval, nnodes, (float*)score, (const float*)init, (const float*)label,         \
-                     (const float*)weight, N, p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc,       \
+                     (const double*)lgy, (const float*)weight, N, p0, score_div, (float*)pred, (float2*)gh, (double*)loss_acc,       \
                      (float*)ghmax, (int*)leaf_part, nvb, (const float*)scales, (long long*)staging, B,    \
                      (unsigned long long*)zero, zero_n)
   switch (loss_id) {
@@ -1187,6 +1214,7 @@ int ytk_tree_grad_hist(uintptr_t bins, long long stride, uintptr_t tfeat, uintpt
     default: YTK_TGH(4); break;
   }
 #undef YTK_TGH
+#undef YTK_TGH2
   YTK_LAUNCH_CHECK();
   if (leaf_part) {
     hipLaunchKernelGGL(leaf_count_reduce_kernel, dim3(nnodes + (acc2 ? 2 : 1)), dim3(256), 0, s,

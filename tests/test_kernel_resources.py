@@ -20,8 +20,7 @@ from kernel_resources import HIP_DIR, demangle, kernel_table  # noqa: E402
 # (pattern on the demangled name, why scratch is tolerated there)
 ALLOWED = [
     (r"lv_partition_children_kernel<true, \d+, 16, true, true", "YTK_PART_CHUNK=4096 prefetch variant (off by default)"),
-    (r"tree_grad_hist_kernel<3>", "Poisson loss: inlined lgamma of the label"),
-    (r"tree_grad_hist_kernel<0>", "sigmoid fused pass at the 128-VGPR cap of 1024-thread blocks: one dword per 2 rows"),
+    (r"tree_grad_hist_kernel<0, 2>", "sigmoid fused pass at the 128-VGPR cap of 1024-thread blocks: one dword per 2 rows"),
     (r"split_feat_kernel<\d+, 1024>", "wide-bin (> 1024 bins) split search, 1024-thread blocks"),
     (r"lw_plan_kernel<true>", "one-block leaf-wise planner, workspace mode (> 512 leaves) at 1024 threads"),
 ]

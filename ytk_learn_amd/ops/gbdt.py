@@ -518,6 +518,27 @@ def bin_assign(X, cand, coff, out, outT=None):
 ACC_LEN = 4 + 2 * 256 * 8  # == kAccLen (gbdt_score.hip): (loss, weight), counter, block partials
 
 
+_LGY = {}  # id(label) -> (weakref to label, lgamma(label + 1) float64 on its device)
+
+
+def label_term(label, loss) -> int:
+    """Device address of lgamma(label + 1) (float64, one per label entry) for the Poisson loss,
+    else 0: the kernels add this label term to the point loss instead of evaluating lgamma
+    themselves (that inlined lgamma cost the fused gradient + histogram kernel 238 VGPR
+    spills). Computed once per label tensor (cached while the tensor lives)."""
+    if LOSS_IDS[loss] != 3:
+        return 0
+    import weakref
+    hit = _LGY.get(id(label))
+    if hit is None or hit[0]() is not label:
+        if len(_LGY) > 16:
+            for k in [k for k, (r, _) in _LGY.items() if r() is None]:
+                del _LGY[k]
+        hit = (weakref.ref(label), torch.lgamma(label.double() + 1.0).contiguous())
+        _LGY[id(label)] = hit
+    return ptr(hit[1])
+
+
 def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_div, pred, finish=True):
     """Test-set round tail in one GPU pass (K == 1, ONE raw tree ``tree`` rooted at node 0, as
     forest_predict's dict; its troot / tout are not read): score += tree(row), then the loss sums and prediction -- exactly
@@ -535,7 +556,8 @@ def forest_predict_loss(X, tree, score, init, label, weight, loss, param, score_
     ok = hip().forest_loss_regs(ptr(X), X.shape[1], X.shape[0], ptr(tree["nfeat"]), ptr(tree["nthr"]),
                                 ptr(tree["nleft"]), ptr(tree["nright"]), ptr(tree["ndefl"]), ptr(tree["nval"]),
                                 0, tree["nfeat"].numel(), ptr(score),
-                                ptr(init), ptr(label), ptr(weight), loss_id, float(param), float(score_div),
+                                ptr(init), ptr(label), label_term(label, loss), ptr(weight), loss_id, float(param),
+                                float(score_div),
                                 ptr(pred), ptr(acc), 1 if finish else 0, stream(X))
     if not ok:
         return None
@@ -554,7 +576,7 @@ def grad_hess(score, init, label, weight, loss, param, score_div, pred, gh, want
     if score.is_cuda:
         check_cuda(score, init, label, weight, pred, gh, ghmax)
         acc = torch.empty(ACC_LEN, dtype=torch.float64, device=score.device)  # fully written by the kernels
-        hip().grad_hess(ptr(score), ptr(init), ptr(label), ptr(weight), N, K, loss_id,
+        hip().grad_hess(ptr(score), ptr(init), ptr(label), label_term(label, loss), ptr(weight), N, K, loss_id,
                         float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), stream(score))
         return acc[:2]
@@ -671,7 +693,8 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
                     and nn > 0):
                 root["done"] = bool(hip().tree_grad_hist(
                     ptr(bins), bins.stride(0), ptr(tf), ptr(tt), ptr(tl), ptr(tr), ptr(tv), nn, ptr(score), ptr(init),
-                    ptr(label), ptr(weight), N, loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
+                    ptr(label), label_term(label, loss), ptr(weight), N, loss_id, float(param), float(score_div),
+                    ptr(pred), ptr(gh), ptr(acc),
                     ptr(ghmax), ptr(part), ptr(leaf_counts), root["scales"], root["staging"], root["work"],
                     root["slot"], root["B"], root["F"], ptr(acc_out),
                     ptr(te_acc[0]) if te_acc is not None else 0, int(te_acc[1]) if te_acc is not None else 0,
@@ -681,7 +704,8 @@ def tree_grad(bins, tree_arrays, score, init, label, weight, loss, param, score_
                 return acc_out if acc_out is not None else acc[:2]
         ok = hip().tree_grad(ptr(bins), _bin_bytes(bins) if bins is not None else 1,
                         bins.stride(0) if bins is not None else 0, ptr(tf), ptr(tt), ptr(tl),
-                        ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), ptr(weight), N,
+                        ptr(tr), ptr(tv), nn, ptr(score), ptr(init), ptr(label), label_term(label, loss),
+                        ptr(weight), N,
                         loss_id, float(param), float(score_div), ptr(pred), ptr(gh), ptr(acc),
                         1 if want_grad else 0, ptr(ghmax), ptr(part), ptr(leaf_counts), stream(score))
         if not ok:
