@@ -153,8 +153,19 @@ def run_variants(a, comm, dev, data, params, headline_sync, log):
     names = VARIANT_NAMES if a.variants in ("auto", "all") else [v for v in a.variants.split(",") if v]
     X, y, Xt, yt = data
     out = {}
+    t_start = time.perf_counter()
     for name in names:
+        # bounded: the variants never cost the headline more than --variant-budget seconds
+        # (agreed over the ranks, so every rank stops at the same variant)
+        spent = time.perf_counter() - t_start
+        if comm.is_dist:
+            spent = comm.allreduce_scalars([spent], op="max")[0]
+        if spent > a.variant_budget:
+            out[name] = {"skipped": f"variant time budget ({a.variant_budget:.0f} s) spent"}
+            continue
         env = dict(dict(VARIANTS).get(name, {}))
+        # a stuck peer exchange fails the variant in seconds, not the job's 120 s
+        env.setdefault("YTK_PEER_TIMEOUT_S", "30")
         if name == "sync_alt":
             env["YTK_HIST_SYNC"] = "owner" if headline_sync != "owner" else "allreduce"
         t0 = time.perf_counter()
@@ -221,6 +232,8 @@ def main():
                     help="multi-GPU design A/B after the headline: auto (N > 1 only) | none | all | "
                          "comma list of " + ",".join(VARIANT_NAMES))
     ap.add_argument("--variant-steps", type=int, default=8, help="timed level-wise trees per variant")
+    ap.add_argument("--variant-budget", type=float, default=90.0,
+                    help="seconds after which the remaining variants are skipped")
     a = ap.parse_args()
 
     # a stuck rank must fail the job well inside the driver's bench timeout: every collective

@@ -479,6 +479,12 @@ def test_bench_variants_world2_failing_variant_keeps_headline():
     assert "exchange_us_per_level" in res
 
 
+def test_bench_variant_budget_skips():
+    """Past --variant-budget seconds the remaining variants are skipped (every rank agrees)."""
+    res = _bench_json(_bench(2, extra_args=("--variant-budget", "0", "--variants", "peer_overlap,rccl")))
+    assert all("skipped" in v for v in res["variants"].values()) and len(res["variants"]) == 2
+
+
 def test_bench_world1_has_no_variants():
     res = _bench_json(_bench(1))
     assert "variants" not in res
