@@ -234,7 +234,7 @@ def main():
             run_gbdt(comm, out, dev, "level", loss="l1")
         elif task in ("linear", "fm", "ffm", "gbmlr", "gbhsdt", "multiclass_linear"):
             run_linear(comm, out, dev, task)
-        elif task in ("fm_sgd", "linear_sgd"):
+        elif task in ("fm_sgd", "linear_sgd", "ffm_sgd"):
             run_linear(comm, out, dev, task.split("_")[0], sgd=True)
         elif task == "binning":
             run_binning(comm, out, dev)

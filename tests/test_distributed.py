@@ -378,7 +378,7 @@ def test_peer_primitives_one_gpu(tmp_path, world):
         assert ok_ar and ok_rs and ok_ag, (dt, n, ok_ar, ok_rs, ok_ag)
 
 
-@pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd"])
+@pytest.mark.parametrize("task", ["linear_sgd", "fm_sgd", "ffm_sgd"])
 def test_sgd_world2_model_averaging(tmp_path, task):
     """SGD on 2 ranks (shards differ in size: uneven step counts must still meet at every
     averaging point) learns like the single-rank run."""
