@@ -25,7 +25,8 @@ data (every N) and reported as ``leafwise_s_per_tree`` / ``leafwise_vs_reference
 Multi-GPU design A/B (N > 1, ``--variants auto``): after the headline, short extra timed runs
 (2 untimed + ``--variant-steps`` timed level-wise trees each, a fresh trainer per variant) of
 the choices a one-GPU box cannot measure -- the half-level exchange overlapped with the build
-(``peer_overlap``), the other histogram sync mode (``owner`` / ``allreduce``), RCCL instead of
+forced on / off (``overlap_on`` / ``overlap_off``; the headline's default ``auto`` times both on
+trees 1-4 and keeps the faster, reported as ``overlap_auto_us``), the other histogram sync mode (``owner`` / ``allreduce``), RCCL instead of
 the peer-memory exchange (``rccl``) and RCCL with its half-level overlap (``rccl_overlap``) --
 reported under ``variants`` in the same JSON line. Each runs in its own try block followed by
 an all-rank vote: a variant that fails on any rank is reported as ``{"error": ...}``, ends the
@@ -105,7 +106,8 @@ def _transport(comm, builder) -> str:
 # (name, environment of the variant's trainer); "sync_alt" is the histogram sync mode the
 # headline did not use (owner <-> allreduce)
 VARIANTS = [
-    ("peer_overlap", {"YTK_PEER_OVERLAP": "1"}),
+    ("overlap_on", {"YTK_PEER_OVERLAP": "1"}),
+    ("overlap_off", {"YTK_PEER_OVERLAP": "0"}),
     ("sync_alt", {}),
     ("rccl", {"YTK_PEER_REDUCE": "0"}),
     ("rccl_overlap", {"YTK_PEER_REDUCE": "0", "YTK_HIST_OVERLAP_MIN_ROWS": "0"}),
@@ -368,6 +370,8 @@ def run(a, comm):
             "hist_transport": transport,
             # half-level exchange / all-reduce overlapped with the other half's build
             "overlap": _overlap(comm, tr_builder),
+            # auto-tuned overlap: (off, on) device us per trial tree, max over ranks
+            "overlap_auto_us": getattr(tr_builder, "overlap_times", None),
             "graph_replays": replays,
             "trees_converted": total_rounds,
             # multi-GPU diagnostics: the start-up self-test of the peer-memory path (on a vote

@@ -51,6 +51,7 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
     peer_calls = peer.calls if peer is not None else 0
     slot_elems = int(getattr(tr.builder, "slot_elems", 0) or 0)
     peer_overlap = bool(getattr(tr.builder, "peer_overlap", False))
+    overlap_times = getattr(tr.builder, "overlap_times", None)
     rccl_kcap = int(getattr(tr.builder, "RCCL_KCAP", 0) or 0)
     tr.close()
     if comm.log is not None:  # every rank's collective sequence (deadlock-freedom check)
@@ -65,7 +66,7 @@ def run_gbdt(comm, out, device, policy, loss="sigmoid"):
                        "backend": backend, "is_dist": comm.is_dist,
                        "graph_replays": tr._graphs["n"] if isinstance(tr._graphs, dict) else 0,
                        "peer_calls": peer_calls, "slot_elems": slot_elems, "rccl_kcap": rccl_kcap,
-                       "peer_overlap": peer_overlap}, f)
+                       "peer_overlap": peer_overlap, "overlap_times": overlap_times}, f)
 
 
 def write_lines(path, n, seed, fields=False):

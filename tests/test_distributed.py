@@ -161,7 +161,8 @@ def test_lbfgs_world_n_matches_world1(tmp_path, task, world, shard):
                                              ("gbdt_loss", 3, "peer"), ("gbdt", 4, "peer"), ("gbdt", 2, "peer_owner"),
                                              ("gbdt", 3, "peer_owner"), ("gbdt", 4, "peer_owner"),
                                              ("gbdt_loss", 2, "peer_owner"), ("gbdt_loss", 3, "peer_owner"),
-                                             ("gbdt", 2, "peer_overlap"), ("gbdt", 3, "peer_overlap")])
+                                             ("gbdt", 2, "peer_overlap"), ("gbdt", 3, "peer_overlap"),
+                                             ("gbdt", 2, "peer_auto")])
 def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     """Several ranks share the one GPU over gloo: the GPU level engine (fused count slots,
     overlapped half-level all-reduce, global gradient bound; or owner-computes:
@@ -177,17 +178,22 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     peer = mode.startswith("peer")
-    sync = {"peer": "allreduce", "peer_owner": "owner", "peer_overlap": "allreduce"}.get(mode, mode)
+    sync = {"peer": "allreduce", "peer_owner": "owner", "peer_overlap": "allreduce",
+            "peer_auto": "allreduce"}.get(mode, mode)
     env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": sync,
            "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if peer else "0",
            "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0",  # small shards: keep the overlap covered
-           "YTK_PEER_OVERLAP": "1" if mode == "peer_overlap" else "0"}
+           "YTK_PEER_OVERLAP": {"peer_overlap": "1", "peer_auto": "auto_force"}.get(mode, "0")}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     if peer:
         assert res["peer_calls"] > 0
         assert res["owner"] == (mode == "peer_owner")
-        assert res["peer_overlap"] == (mode == "peer_overlap")
+        if mode == "peer_auto":  # trees 1-4 timed off / on, the faster mode kept (either is fine)
+            off_us, on_us = res["overlap_times"]
+            assert off_us > 0 and on_us > 0 and res["peer_overlap"] == (on_us < off_us)
+        else:
+            assert res["peer_overlap"] == (mode == "peer_overlap")
         if task == "gbdt" and world != 3:  # no feature sampling: graph-eligible rounds
             assert res["graph_replays"] > 0
     assert open(tmp_path / "w1" / "model.txt").read() == open(tmp_path / f"w{world}" / "model.txt").read()
@@ -470,8 +476,8 @@ def test_bench_variants_world2_failing_variant_keeps_headline():
     res = _bench_json(r)
     assert res["n_gpus"] == 2 and res["value"] > 0 and res["hist_sync"] in ("allreduce", "owner")
     v = res["variants"]
-    assert list(v) == ["peer_overlap", "sync_alt", "rccl", "rccl_overlap"]
-    for name in ("peer_overlap", "sync_alt", "rccl"):
+    assert list(v) == ["overlap_on", "overlap_off", "sync_alt", "rccl", "rccl_overlap"]
+    for name in ("overlap_on", "overlap_off", "sync_alt", "rccl"):
         assert VARIANT_KEYS <= set(v[name]), (name, v[name])
         assert v[name]["s_per_tree"] > 0 and v[name]["collectives_per_tree"] > 0
     assert v["sync_alt"]["hist_sync"] != res["hist_sync"]
@@ -481,7 +487,7 @@ def test_bench_variants_world2_failing_variant_keeps_headline():
 
 def test_bench_variant_budget_skips():
     """Past --variant-budget seconds the remaining variants are skipped (every rank agrees)."""
-    res = _bench_json(_bench(2, extra_args=("--variant-budget", "0", "--variants", "peer_overlap,rccl")))
+    res = _bench_json(_bench(2, extra_args=("--variant-budget", "0", "--variants", "overlap_on,rccl")))
     assert all("skipped" in v for v in res["variants"].values()) and len(res["variants"]) == 2
 
 
@@ -500,14 +506,14 @@ def test_bench_variants_two_ranks_one_gpu():
     env = {"YTK_DIST_BACKEND": "gloo", "YTK_PEER_REDUCE": "1", "YTK_PEER_TIMEOUT_S": "60"}
     args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--train-rows", "200000",
             "--test-rows", "20000", "--quiet", "--leafwise-steps", "0", "--variant-steps", "2",
-            "--variants", "peer_overlap,sync_alt"]
+            "--variants", "overlap_on,overlap_off,sync_alt"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port())] + args
     r = subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **env),
                        capture_output=True, text=True, timeout=300)
     res = _bench_json(r)
     assert res["hist_transport"] == "peer" and res["exchange_us_per_level"] is not None
-    for name in ("peer_overlap", "sync_alt"):
+    for name in ("overlap_on", "overlap_off", "sync_alt"):
         assert VARIANT_KEYS <= set(res["variants"][name]), res["variants"][name]
         assert res["variants"][name]["transport"] == "peer"
-    assert res["variants"]["peer_overlap"]["overlap"] is True
+    assert res["variants"]["overlap_on"]["overlap"] is True and res["variants"]["overlap_off"]["overlap"] is False

@@ -296,23 +296,34 @@ class DeviceLevelBuilder:
             self.peer = peer_mod.make(self.comm, cap)
             if self.peer is not None:
                 self.overlap = False
-        # peer path + YTK_PEER_OVERLAP=1: levels with >= 8 built slots exchange their first half
-        # on a side stream (a second peer group, a small exchange grid that fits beside the
-        # histogram blocks) while the second half's histograms build; the split waits for both
-        # (BASELINE: histogram exchange overlapped with the next block's build). Off by default:
-        # on one GPU per rank the gain is bounded by the second half's build (~9 us per level at
-        # the 1/8 shard) and it has no multi-GPU measurement yet.
+        # peer path: levels with >= 8 built slots may exchange their first half on a side stream
+        # (a second peer group, a small exchange grid that fits beside the histogram blocks)
+        # while the second half's histograms build; the split waits for both (BASELINE:
+        # histogram exchange overlapped with the next block's build).
+        # YTK_PEER_OVERLAP=auto (default): measured per job -- trees 1..4 (eager rounds, before
+        # any graph capture) alternate overlap off / on with device events around each build,
+        # the ranks agree on the max-over-ranks times and the faster mode builds the rest
+        # (overlap_tune()). Whether it pays depends on the shard (the second half's build must
+        # outlast the exchange) and on the links, so it is not decided blind. Ranks sharing one
+        # GPU (a rehearsal) never overlap under auto: their exchanges contend with each other's
+        # builds (auto_force: tune there too -- tests). 1: always on, 0: never.
         self.peer2 = None
         self.peer_overlap = False
-        if (self.peer is not None and not self.owner and self.staged
-                and os.environ.get("YTK_PEER_OVERLAP", "0") == "1"):
+        self.overlap_mode = os.environ.get("YTK_PEER_OVERLAP", "auto")
+        auto = self.overlap_mode in ("auto", "auto_force")
+        self.overlap_trial = None  # auto: [(tree, on, start event, end event)], then None
+        self.overlap_times = None  # auto: (off us, on us) per tree, max over ranks
+        if (self.peer is not None and not self.owner and self.staged and (auto or self.overlap_mode == "1")
+                and not (self.overlap_mode == "auto" and getattr(self.peer, "shared_gpu", False))):
             half_max = max([1] + [self._half(c) // 2 for c in range(1, D)])
             if half_max >= 4:
                 self.peer2 = peer_mod.make(self.comm, half_max * slot_elems)
                 if self.peer2 is not None:
                     hip().peer_set_grid_cap(self.peer2.hnd, int(os.environ.get("YTK_PEER_OVERLAP_GRID", "32")))
-                    self.peer_overlap = True
                     self._side = torch.cuda.Stream(device=dev)
+                    self.peer_overlap = self.overlap_mode == "1"
+                    if auto:
+                        self.overlap_trial = []
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
         self._zero_all = self.hist.numel() * 8 <= (64 << 20)
@@ -400,6 +411,47 @@ class DeviceLevelBuilder:
         if glob is not None:
             out[14] = glob
         return out
+
+    # ------------------------------------------------------------------ overlap auto-tune
+    OVERLAP_TRIAL = (1, 2, 3, 4)  # trees timed (tree 0 warms up): off, on, off, on
+
+    @property
+    def tuning(self) -> bool:
+        """True while the overlap auto-tune still needs eager (uncaptured) trees."""
+        return self.overlap_trial is not None
+
+    def _trial_begin(self):
+        """Auto-tune: the mode of this tree and its start event (None outside the trial)."""
+        if self.overlap_trial is None or self.tree_count not in self.OVERLAP_TRIAL:
+            return None
+        self.peer_overlap = (self.tree_count - self.OVERLAP_TRIAL[0]) % 2 == 1
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.dev))
+        return ev
+
+    def _trial_end(self, ev0):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record(torch.cuda.current_stream(self.dev))
+        self.overlap_trial.append((self.tree_count, self.peer_overlap, ev0, ev1))
+        if len(self.overlap_trial) == len(self.OVERLAP_TRIAL):
+            self._trial_decide()
+
+    def _trial_decide(self):
+        """The faster mode over the trial trees (device time, max over ranks: the slowest
+        rank sets the pace), identical on every rank."""
+        off = on = 0.0
+        for _, o, e0, e1 in self.overlap_trial:
+            e1.synchronize()
+            t = 1000.0 * e0.elapsed_time(e1)
+            if o:
+                on += t
+            else:
+                off += t
+        off, on = self.comm.allreduce_scalars([off, on], op="max")
+        n = len(self.OVERLAP_TRIAL) // 2
+        self.overlap_times = (round(off / n, 1), round(on / n, 1))
+        self.peer_overlap = on < off
+        self.overlap_trial = None
 
     def _hist_allreduce(self, t: torch.Tensor):
         """A level's histogram (+ count) slots (or any int64 / fp64 device message): the
@@ -521,6 +573,13 @@ class DeviceLevelBuilder:
     def build(self, gh: torch.Tensor, ghmax: torch.Tensor = None, ghmax_global: bool = False) -> DeviceTree:
         """Enqueue one tree. ``gh`` [N, 2] contiguous (g, h); ``ghmax`` (float32 [2], optional)
         = max |g|, max |h| over all local rows, already produced by the gradient kernel."""
+        trial = self._trial_begin()
+        dt = self._build(gh, ghmax, ghmax_global)
+        if trial is not None:
+            self._trial_end(trial)
+        return dt
+
+    def _build(self, gh: torch.Tensor, ghmax: torch.Tensor = None, ghmax_global: bool = False) -> DeviceTree:
         p = self.p
         h = hip()
         s = stream(self.bins)

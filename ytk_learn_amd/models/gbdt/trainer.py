@@ -636,6 +636,8 @@ class GBDTTrainer:
         if self._graphs is None:
             if self._eager_rounds < 1:  # the first round builds its root eagerly
                 return False
+            if getattr(self.builder, "tuning", False):  # the overlap auto-tune times eager trees
+                return False
             torch.cuda.synchronize(self.dev)
             # the nccl watchdog must hold no eager work while the rounds are captured: its
             # event queries inside a capture abort the process (Comm.drain_pending)

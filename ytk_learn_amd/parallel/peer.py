@@ -69,13 +69,14 @@ class PeerReduce:
         self.cap = int(cap)  # 8-byte words
         self.cap_bytes = 8 * self.cap
         self.calls = 0
+        self.shared_gpu = False  # several ranks of the group on one GPU (a rehearsal)
 
     @classmethod
     def create(cls, comm: Comm, cap_elems: int) -> Optional["PeerReduce"]:
         h = hip()
         cap = int(cap_elems)
         handle = np.zeros(64, np.uint8)
-        hnd, ok, err = None, 1.0, None
+        hnd, ok, err, shared = None, 1.0, None, False
         try:
             hnd = h.peer_create(comm.world, comm.rank, 8 * cap, handle.ctypes.data)
         except Exception as e:  # noqa: BLE001 -- any failure votes for RCCL
@@ -96,7 +97,8 @@ class PeerReduce:
             try:
                 allh = np.frombuffer(b"".join(p[:64] for p in parts), dtype=np.uint8).copy()
                 h.peer_open(hnd, allh.ctypes.data)
-                if len({p[64:] for p in parts}) < comm.world:  # several ranks on one GPU
+                shared = len({p[64:] for p in parts}) < comm.world
+                if shared:  # several ranks on one GPU
                     h.peer_set_grid_cap(hnd, 1)
                 if os.environ.get("YTK_PEER_GRID_CAP"):  # (diagnostics) blocks per exchange
                     h.peer_set_grid_cap(hnd, int(os.environ["YTK_PEER_GRID_CAP"]))
@@ -110,6 +112,7 @@ class PeerReduce:
             # memory that is not coherent across these devices -- votes for RCCL instead of
             # producing wrong histograms or hanging the job)
             pr = cls(comm, hnd, cap)
+            pr.shared_gpu = shared
             try:
                 ok = 1.0 if pr._self_test() else 0.0
                 if not ok:
