@@ -30,6 +30,7 @@ void ytk_split_find(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, i
                     uintptr_t, uintptr_t);
 void ytk_split_combine(uintptr_t, int, int, uintptr_t, int, int, uintptr_t, uintptr_t);
 // gbst.hip
+int ytk_gbst_wide_max();
 void ytk_gbst_epilogue(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, double, uintptr_t, int, int, int,
                        int, int, double, int, int, int, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_partition.hip
@@ -200,6 +201,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("split_find", &ytk_split_find);
   m.def("split_combine", &ytk_split_combine);
   m.def("gbst_epilogue", &ytk_gbst_epilogue);
+  m.def("gbst_wide_max", &ytk_gbst_wide_max);
   m.def("partition", &ytk_partition);
   m.def("partition_count", &ytk_partition_count);
   m.def("segment_copy", &ytk_segment_copy);

@@ -251,16 +251,170 @@ __global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_kernel(GbstArgs a)
   }
 }
 
+// K > 64 (up to kGbstWideMax): ONE wave per row, lane l owning experts l + 64 j (j < KPL) in
+// registers; softmax max / sums and the mixture are wave butterflies over the lanes' partials.
+// The tree gate keeps the row's internal-node sigmas [K - 1] and heap sums mu [2K] in a per-wave
+// LDS row (a leaf walks its <= log2(2K) ancestors' sigmas from LDS; the heap sums are formed one
+// depth at a time, deepest first, the lanes striding over a depth's nodes). Same formulas and
+// the same leaf-to-root product order as gbst_epilogue_kernel (sums differ from it only in
+// association). Block accumulators: LDS fp64 atomics, then one global atomic per value.
+constexpr int kGbstWideMax = 512;
+
+__device__ __forceinline__ double wave_maxd(double v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+template <int KPL, bool kTree>
+__global__ __launch_bounds__(kGbstThreads) void gbst_epilogue_wide_kernel(GbstArgs a) {
+  constexpr int NW = kGbstThreads / kWave;  // rows per block step: one per wave
+  extern __shared__ __attribute__((aligned(16))) double gw_sm[];
+  const int K = a.K;
+  const int wid = threadIdx.x >> 6, l = lane_id();
+  double* s_acc = gw_sm;                                    // [2 + 2K]: losses, samples, leaf grads
+  double* s_sg = gw_sm + (2 + 2 * K) + (size_t)wid * 3 * K;  // tree gate: sigma of node p at [p - 1]
+  double* s_mu = s_sg + K;                                  // tree gate: heap sums mu [2K]
+  for (int v = threadIdx.x; v < 2 + 2 * K; v += kGbstThreads) s_acc[v] = 0.0;
+  __syncthreads();
+  double acc_loss = 0.0, acc_rf = 0.0, acc_smp[KPL], acc_leaf[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; ++j) acc_smp[j] = acc_leaf[j] = 0.0;
+  const int top = 31 - __clz(K - 1);  // deepest internal-node depth (K - 1 >= 1)
+  const long long nsteps = ((long long)a.n + NW - 1) / NW;
+  for (long long st = blockIdx.x; st < nsteps; st += gridDim.x) {
+    const long long i = st * NW + wid;
+    if (i >= a.n) continue;  // wave-uniform
+    const float* Ar = a.A + i * a.lda;
+    double H[KPL], g[KPL], sg[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      const int k = l + kWave * j;
+      H[j] = k < K ? (a.linear ? (double)Ar[K - 1 + k] : (double)a.leaves[k]) : 0.0;
+    }
+    double mix;
+    if (!kTree) {  // softmax over K-1 logits + an implicit 0 logit (expert K-1)
+      double mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int k = l + kWave * j;
+        g[j] = k < K - 1 ? (double)Ar[k] : 0.0;  // the logit, then the gate probability
+        if (k < K) mx = fmax(mx, g[j]);
+      }
+      mx = wave_maxd(mx);
+      double es = 0.0;
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int k = l + kWave * j;
+        g[j] = k < K ? exp(g[j] - mx) : 0.0;
+        es += g[j];
+      }
+      es = wave_sum(es);
+      double m = 0.0;
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        g[j] = g[j] / es;
+        m += g[j] * H[j];
+      }
+      mix = wave_sum(m);
+    } else {  // heap-indexed sigmoid tree: leaf k is heap node K + k
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int k = l + kWave * j;
+        sg[j] = k < K - 1 ? sig_d((double)Ar[k]) : 0.0;  // sigma of internal node k + 1
+        if (k < K - 1) s_sg[k] = sg[j];
+      }
+      gbst_wave_sync();
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int k = l + kWave * j;
+        double prob = 0.0;
+        if (k < K) {
+          prob = 1.0;
+          for (int h = K + k; h > 1; h >>= 1) {
+            const double sp = s_sg[(h >> 1) - 1];
+            prob *= (h & 1) ? (1.0 - sp) : sp;
+          }
+          s_mu[K + k] = prob * H[j];
+        }
+        g[j] = prob;
+      }
+      gbst_wave_sync();
+      for (int dd = top; dd >= 0; --dd) {  // internal nodes [2^dd, min(2^(dd+1), K)), deepest first
+        const int n1 = min(2 << dd, K);
+        for (int q = (1 << dd) + l; q < n1; q += kWave) s_mu[q] = s_mu[2 * q] + s_mu[2 * q + 1];
+        gbst_wave_sync();
+      }
+      mix = s_mu[1];
+    }
+    const double zz = (double)a.z[i];
+    const double yy = (double)a.y[i];
+    const double fx = a.rf ? mix : zz + mix;
+    double wt = a.w ? (double)a.w[i] : 1.0;
+    const double m = a.mask ? (double)a.mask[i] : 1.0;
+    if (a.mask) wt = wt * m * a.inv_rate;
+    if (l == 0) {
+      const double ly = a.lgy ? a.lgy[i] : 0.0;
+      acc_loss += wt * (loss_val(a.loss_id, fx, yy, a.lparam) + ly);
+      if (a.rf) {
+        const double avg = (zz + mix) / (double)a.T;
+        acc_rf += wt * (loss_val(a.loss_id, avg, yy, a.lparam) + ly);
+        if (a.pred) a.pred[i] = (float)loss_pred(a.loss_id, avg);
+      } else if (a.pred) {
+        a.pred[i] = (float)loss_pred(a.loss_id, fx);
+      }
+    }
+    if (a.mask) {
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) acc_smp[j] += g[j] * m;
+    }
+    if (a.want_grad) {
+      const double c = wt * loss_grad(a.loss_id, fx, yy, a.lparam);
+      const double purefx = fx - zz;  // reference quirk kept: in RF mode fx excludes z
+      float* Dr = a.D + i * a.ldd;
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int k = l + kWave * j;
+        if (k < K - 1)
+          Dr[k] = kTree ? (float)(c * (s_mu[2 * (k + 1)] - sg[j] * s_mu[k + 1])) : (float)(c * g[j] * (H[j] - purefx));
+        if (a.linear) {
+          if (k < K) Dr[K - 1 + k] = (float)(c * g[j]);
+        } else {
+          acc_leaf[j] += c * g[j];
+        }
+      }
+    }
+    if (kTree) gbst_wave_sync();  // the wave's sigma / mu rows are rewritten by its next row
+  }
+  if (l == 0) {
+    atomicAdd(&s_acc[0], acc_loss);
+    atomicAdd(&s_acc[1], acc_rf);
+  }
+#pragma unroll
+  for (int j = 0; j < KPL; ++j) {
+    const int k = l + kWave * j;
+    if (k < K) {
+      if (acc_smp[j] != 0.0) atomicAdd(&s_acc[2 + k], acc_smp[j]);
+      if (acc_leaf[j] != 0.0) atomicAdd(&s_acc[2 + K + k], acc_leaf[j]);
+    }
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < 2 + 2 * K; v += kGbstThreads)
+    if (s_acc[v] != 0.0) atomicAdd(&a.acc[v], s_acc[v]);
+}
+
 }  // namespace ytk
 
 using namespace ytk;
+
+extern "C" int ytk_gbst_wide_max() { return kGbstWideMax; }
 
 extern "C" void ytk_gbst_epilogue(uintptr_t A, int lda, uintptr_t z, uintptr_t y, uintptr_t w, uintptr_t mask,
                                   double inv_rate, uintptr_t leaves, int n, int K, int tree_gate, int linear,
                                   int loss_id, double lparam, int rf, int T, int want_grad, uintptr_t D, int ldd,
                                   uintptr_t pred, uintptr_t acc, uintptr_t lgy, uintptr_t stream) {
   if (n <= 0) return;
-  if (K < 2 || K > 64) throw std::invalid_argument("gbst_epilogue: 2 <= K <= 64");
+  if (K < 2 || K > kGbstWideMax) throw std::invalid_argument("gbst_epilogue: 2 <= K <= 512");
   if (loss_id < kLossSigmoid || loss_id > kLossInvMape) throw std::invalid_argument("gbst_epilogue: loss id");
   if (loss_id == kLossPoisson && !lgy) throw std::invalid_argument("gbst_epilogue: poisson needs lgamma(y + 1)");
   GbstArgs a{(const float*)A, lda, (const float*)z, (const float*)y, (const float*)w, (const uint8_t*)mask,
@@ -275,12 +429,25 @@ extern "C" void ytk_gbst_epilogue(uintptr_t A, int lda, uintptr_t z, uintptr_t y
     else                                                                                                   \
       hipLaunchKernelGGL((gbst_epilogue_kernel<GG, false>), dim3(grid), dim3(kGbstThreads), 0, s, a);      \
   } while (0)
+#define YTK_GBSTW(KPL)                                                                                     \
+  do {                                                                                                     \
+    const int grid = std::min(ceil_div(n, kGbstThreads / kWave), 256 * 8);                                 \
+    const size_t lds = (size_t)(2 + 2 * K) * 8 + (tree_gate ? (size_t)(kGbstThreads / kWave) * 3 * K * 8 : 0); \
+    if (tree_gate)                                                                                         \
+      hipLaunchKernelGGL((gbst_epilogue_wide_kernel<KPL, true>), dim3(grid), dim3(kGbstThreads), lds, s, a); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((gbst_epilogue_wide_kernel<KPL, false>), dim3(grid), dim3(kGbstThreads), lds, s, a); \
+  } while (0)
   if (K <= 2) YTK_GBST(2);
   else if (K <= 4) YTK_GBST(4);
   else if (K <= 8) YTK_GBST(8);
   else if (K <= 16) YTK_GBST(16);
   else if (K <= 32) YTK_GBST(32);
-  else YTK_GBST(64);
+  else if (K <= 64) YTK_GBST(64);
+  else if (K <= 128) YTK_GBSTW(2);
+  else if (K <= 256) YTK_GBSTW(4);
+  else YTK_GBSTW(8);
 #undef YTK_GBST
+#undef YTK_GBSTW
   YTK_LAUNCH_CHECK();
 }

@@ -106,3 +106,15 @@ def test_gbst_epilogue_every_loss(cuda, loss, gate, expert, K):
     in the fused kernel and matches the loss classes' fp64 formulas."""
     a, D, pred, ref = _run(cuda, gate, expert, K, loss, False, True)
     _check(a, D, pred, ref, K, rtol=1e-9)
+
+
+@pytest.mark.parametrize("gate,expert", [("softmax", "linear"), ("softmax", "scalar"), ("tree", "linear"),
+                                         ("tree", "scalar")])
+@pytest.mark.parametrize("K", [65, 96, 128, 200, 512])
+@pytest.mark.parametrize("loss,rf,train", [("sigmoid", False, True), ("poisson", True, False)])
+def test_gbst_epilogue_wide_k_matches_torch(cuda, gate, expert, K, loss, rf, train):
+    """K > 64 (gbst_epilogue_wide_kernel: one wave per row, several experts per lane, the tree
+    gate's sigmas and heap sums in a per-wave LDS row) against the same fp64 reference -- the
+    reference optimizers are K-generic (GBMLRHoagOptimizer.java:159-222)."""
+    a, D, pred, ref = _run(cuda, gate, expert, K, loss, rf, train, n=3000)
+    _check(a, D, pred, ref, K, rtol=1e-9)

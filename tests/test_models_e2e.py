@@ -178,13 +178,29 @@ def test_gbdt_multiclass_and_feature_maker(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model,kw", [("linear", {}), ("fm", {"k": [1, 4]}), ("gbmlr", {"k": 4}),
-                                      ("gbhsdt", {"k": 4})])
+                                      ("gbhsdt", {"k": 4}), ("gbmlr", {"k": 80}), ("gbhsdt", {"k": 70})])
 def test_continuous_models_gpu_match_cpu(cuda, bin_data, tmp_path, model, kw):
     kw = dict(kw, **{"optimization.line_search.lbfgs.convergence.max_iter": 8})
     rc = train(model, _cfg(model, str(tmp_path / "c"), str(bin_data / "train.txt"), str(bin_data / "test.txt"),
                            **kw), comm=_local("cpu"))
     rg = train(model, _cfg(model, str(tmp_path / "g"), str(bin_data / "train.txt"), str(bin_data / "test.txt"),
                            **kw), comm=_local(cuda))
+    np.testing.assert_allclose(rg.loss, rc.loss, rtol=2e-3)
+    np.testing.assert_allclose(rg.test_loss, rc.test_loss, rtol=5e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loss", ["softmax", "multiclass_hinge", "hsoftmax"])
+def test_multiclass_linear_gpu_matches_cpu(cuda, tmp_path, loss):
+    """The fused multiclass epilogue (mc_row_loss_kernel) inside L-BFGS training reaches the CPU
+    (fp64 torch) run's losses."""
+    write_multiclass(str(tmp_path / "tr.txt"), 2000, seed=1)
+    write_multiclass(str(tmp_path / "te.txt"), 500, seed=2)
+    kw = {"k": 4, "loss.loss_function": loss, "optimization.line_search.lbfgs.convergence.max_iter": 8}
+    rc = train("multiclass_linear", _cfg("multiclass_linear", str(tmp_path / "c"), str(tmp_path / "tr.txt"),
+                                         str(tmp_path / "te.txt"), **kw), comm=_local("cpu"))
+    rg = train("multiclass_linear", _cfg("multiclass_linear", str(tmp_path / "g"), str(tmp_path / "tr.txt"),
+                                         str(tmp_path / "te.txt"), **kw), comm=_local(cuda))
     np.testing.assert_allclose(rg.loss, rc.loss, rtol=2e-3)
     np.testing.assert_allclose(rg.test_loss, rc.test_loss, rtol=5e-3)
 

@@ -34,6 +34,7 @@ from ...utils.javafmt import java_double_str, java_float_str
 from ..continuous.base import ContinuousModelBase
 
 # loss ids of the fused epilogue (csrc/hip/gbst.hip kLoss*): every scalar loss
+GBST_FUSED_MAX_K = 512  # == kGbstWideMax (csrc/hip/gbst.hip)
 GBST_LOSS_IDS = {"sigmoid": 0, "l2": 1, "l1": 2, "huber": 3, "poisson": 4, "hinge": 5, "smooth_hinge": 6,
                  "l2_hinge": 7, "exponential": 8, "mape": 9, "smape": 10, "inv_mape": 11}
 
@@ -185,10 +186,11 @@ class GBSTModel(ContinuousModelBase):
 
     def _fused_ok(self, X) -> bool:
         """The fused HIP epilogue (csrc/hip/gbst.hip) covers every scalar loss
-        (GBST_LOSS_IDS) and 2 <= K <= 64 (softmax and hierarchical gates, any K); otherwise
-        (K > 64, CPU, YTK_GBST_FUSED=0) the fp64 torch path runs."""
+        (GBST_LOSS_IDS) and 2 <= K <= 512 (softmax and hierarchical gates: lane groups per row
+        up to K = 64, one wave per row with several experts per lane above); otherwise
+        (K > 512, CPU, YTK_GBST_FUSED=0) the fp64 torch path runs."""
         K = self.K
-        return (X.values.is_cuda and self.loss.name in GBST_LOSS_IDS and 2 <= K <= 64
+        return (X.values.is_cuda and self.loss.name in GBST_LOSS_IDS and 2 <= K <= GBST_FUSED_MAX_K
                 and os.environ.get("YTK_GBST_FUSED", "1") != "0")
 
     def _lgamma_y(self, d):
