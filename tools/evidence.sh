@@ -10,6 +10,8 @@
 #   sparse  L-BFGS evaluations (linear, fm, ffm, multiclass, gbmlr, gbhsdt)
 #   sgd     SGD epochs (linear, fm fp32 / bf16, ffm)
 #   prof    rocprofv3 kernel statistics + one-round breakdowns (full data, 1/8 shard, leaf-wise)
+#   roof    PMC roofline of the level-wise bench (full data and 1/8 shard): three counter passes,
+#           each its own run with no tracing domains, then tools/roofline.py
 # Every GPU step runs under its own timeout; the first failure ends the script (nothing more
 # runs on the GPU in that call). Output: gpurun_out/<tag>/.
 set -o pipefail
@@ -73,5 +75,24 @@ if has prof; then
   prof prof_full 300 --steps 10 --warmup 2 --leafwise-steps 0
   prof prof_e8 300 --steps 10 --warmup 2 --leafwise-steps 0 $E8
   prof prof_leaf 300 --policy loss --steps 10 --warmup 40 --leafwise-steps 0
+fi
+roof() {  # name bench-args...
+  local n=$1; shift
+  local i=0
+  for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
+      "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES"; do
+    i=$((i + 1))
+    (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $ctrs --output-format csv -d "$O/${n}_pmc$i" -o run -- \
+        python3 "$R/bench.py" "$@") > "$O/${n}_pmc$i.log" 2>&1 || { tail -20 "$O/${n}_pmc$i.log"; exit 1; }
+  done
+  python3 tools/roofline.py "$O/${n}_pmc1/run_counter_collection.csv" "$O/${n}_pmc2/run_counter_collection.csv" \
+      "$O/${n}_pmc3/run_counter_collection.csv" > "$O/${n}.md"
+  python3 tools/pmc_summary.py "$O/${n}_pmc3/run_counter_collection.csv" > "$O/${n}_wave_states.txt"
+  rm -rf "$O/${n}_pmc1" "$O/${n}_pmc2" "$O/${n}_pmc3"
+  head -12 "$O/${n}.md"
+}
+if has roof; then
+  roof roofline_full --steps 4 --warmup 2 --leafwise-steps 0
+  roof roofline_eighth --steps 4 --warmup 2 --leafwise-steps 0 $E8
 fi
 echo "evidence $TAG ok"
