@@ -1085,14 +1085,14 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
 // kPrefetch: the software-pipelined body (partition_atomic_body_pf).
-template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t>
+template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t, bool kPfCol = false>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
 void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
                                                                    float2* gh_out) {
   if constexpr (kPrefetch)
-    partition_atomic_body_pf<BinT, kAtomSub, kPfGh>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
+    partition_atomic_body_pf<BinT, kAtomSub, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
                                                     b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                       b.cursor, b.part_shift, kCurStride);
@@ -1382,7 +1382,11 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
-  if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
+  if (prefetch && pf && pf[0] == '3' && ghp)  // + the next chunk's split-feature bytes
+    hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, true>), grid, dim3(kPartThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+  else if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
     hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
                        (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);

@@ -1250,12 +1250,15 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const bool narrow = p.part_chunk == kPartThreads * kAtomSub / 2;  // small shards: 2x the blocks
   // software-pipelined partition: the next chunk's row ids and (g, h) in flight during this
   // chunk's rank / reserve / scatter. Measured (profiles/r2_partition_chunk.md): off
-  // 1.474-1.496, row ids only (YTK_PART_PREFETCH=1) 1.430-1.441, row ids + (g, h) (default,
-  // 87 VGPRs) 1.393 ms/tree; YTK_PART_PREFETCH=0: off
+  // 1.474-1.496, row ids only (YTK_PART_PREFETCH=1) 1.430-1.441, row ids + (g, h) (=2,
+  // 87 VGPRs) 1.393 ms/tree; YTK_PART_PREFETCH=0: off. Default (unset or 3): also the next
+  // chunk's split-feature bytes, gathered once its row ids have arrived (after this chunk's
+  // cursor reservation): 1.287-1.304 -> 1.245-1.250 ms/tree, 500 trees 1.146 -> 1.130
+  // (profiles/r6/level_knobs/); the 1/8 shard is unchanged (0.390)
   const char* pf = getenv("YTK_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const bool pf_gh = !(pf && (pf[0] == '0' || pf[0] == '1'));
-  const bool pf_col = pf && pf[0] == '3';  // YTK_PART_PREFETCH=3: + the next chunk's split-feature bytes
+  const bool pf_col = !pf || pf[0] == '3';
   if (gh_rows && (!prefetch || count_only))
     throw std::invalid_argument("lv_partition_children: row-indexed (g, h) needs the pipelined scatter body");
 #define YTK_LVPC4(SC, KP, S, PF, PG, PC)                                                                      \

@@ -153,7 +153,7 @@ def test_device_builder_matches_host_builder(cuda, kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_PART_CHUNK": "1024"}, {"YTK_FUSE_SPLIT_PLAN": "1"}, {"YTK_PART_PREFETCH": "0"}, {"YTK_PART_PREFETCH": "1"}, {"YTK_PART_PREFETCH": "3"},
+@pytest.mark.parametrize("env", [{"YTK_PART_CHUNK": "4096"}, {"YTK_PART_CHUNK": "1024"}, {"YTK_FUSE_SPLIT_PLAN": "1"}, {"YTK_PART_PREFETCH": "0"}, {"YTK_PART_PREFETCH": "1"}, {"YTK_PART_PREFETCH": "2"},
                                  {"YTK_SPLIT_GROUPS": "1"}, {"YTK_SPLIT_GROUPS": "3"}, {"YTK_REDUCE_SPLIT": "8"},
                                  {"YTK_FUSED_TEST_TAIL": "0"}, {"YTK_TG_LDS_WALK": "0"}, {"YTK_FUSE_ROOT_HIST": "0"},
                                  {"YTK_FUSE_ROOT_HIST": "0", "YTK_DEFER_LEAF_COUNTS": "0"},
@@ -297,10 +297,10 @@ def test_device_leafwise_matches_host(monkeypatch, kw):
 
 @pytest.mark.gpu
 def test_device_leafwise_partition_prefetch_identical(monkeypatch):
-    """Leaf-wise engine with the software-pipelined partition body (YTK_LW_PART_PREFETCH=1)
-    builds the default engine's trees byte for byte."""
+    """Leaf-wise engine with the software-pipelined partition body (YTK_LW_PART_PREFETCH=1;
+    3: + the next chunk's split-feature bytes) builds the default engine's trees byte for byte."""
     res = []
-    for pf in ("0", "1", "2"):
+    for pf in ("0", "1", "2", "3"):
         monkeypatch.setenv("YTK_LW_PART_PREFETCH", pf)
         p = _params("loss", rounds=3)
         p.tree.max_leaf_cnt = 63
@@ -308,7 +308,7 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
         tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
         tr.train()
         res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
-    assert res[0] == res[1] == res[2]
+    assert res[0] == res[1] == res[2] == res[3]
 
 
 @pytest.mark.gpu
