@@ -136,6 +136,8 @@ uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
 void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lw_zero_slots(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
+void ytk_lw_subtree(int, uintptr_t, long long, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                    uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t);
 // gbdt_comm.hip
 void ytk_seg_median(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, int, uintptr_t, uintptr_t);
 void ytk_seg_prune(uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t);
@@ -304,7 +306,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
                       part, counters, implicit_items, maxp, stream);
   });
   m.def("lw_create", [](const std::vector<uintptr_t>& ptrs, const std::vector<int>& ip, const std::vector<float>& fp) {
-    if (ptrs.size() != 38 || ip.size() != 11 || fp.size() != 6) throw std::invalid_argument("lw_create: bad argument sizes");
+    if (ptrs.size() != 40 || ip.size() != 13 || fp.size() != 7) throw std::invalid_argument("lw_create: bad argument sizes");
     return ytk_lw_create(ptrs.data(), ip.data(), fp.data());
   });
   m.def("lw_set_lr", &ytk_lw_set_lr);
@@ -314,6 +316,7 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lw_step", &ytk_lw_step);
   m.def("lw_partition", &ytk_lw_partition);
   m.def("lw_zero_slots", &ytk_lw_zero_slots);
+  m.def("lw_subtree", &ytk_lw_subtree);
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);
   m.def("owner_pack", &ytk_owner_pack);
   m.def("peer_create", &ytk_peer_create);

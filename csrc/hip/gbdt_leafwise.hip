@@ -27,6 +27,7 @@
 // Histogram slots are never recycled inside a tree (slot = speculative node id; a
 // 255-leaf tree uses < 600 of them, ~70 MB of the 288 GB of HBM3E).
 #include "common.h"
+#include "gbdt_fx.h"                 // fx_round, hist_lds_pos (subtree histograms)
 #include "gbdt_partition_atomic.h"  // partition_atomic_body
 #include "gbdt_split_node.h"        // SplitOut
 #include "gbdt_tree_node.h"         // DNode, node_leaf_value
@@ -67,6 +68,11 @@ struct LwParams {
   int batch_cap;  // > 0: at most this many splits per batch (the RCCL batch loop sizes its fixed
                   // messages by it, ytk_lw_set_batch_cap); 0: no cap
   int slow_children;  // set per partition launch: 1 = YTK_PLAN_FAST=0 (general children path)
+  // small-node subtrees (single GPU): batch entries with <= sub_rows rows are grown by
+  // lw_subtree_kernel, up to sub_max more splits each, expanding nodes whose path-minimum
+  // gain is >= sub_alpha x the previous tree's smallest split gain; sub_rows = 0: off
+  int sub_rows, sub_max;
+  float sub_alpha;
 };
 
 // global-memory planner workspace (large trees): the arrays the LDS planner keeps in LDS
@@ -107,7 +113,14 @@ struct LwBufs {
   int* zero_ids;               // [max_leaf + 1] built slots with != 1 histogram item
   int2* zero_range;            // [max_leaf + 1] their items [x, x + y)
   LwPlanWs ws;                 // large trees only (max_leaf > kLwLeafMax): else all null
+  int* sub;                    // [SUB_WORDS] subtree state (below)
+  int2* sub_list;              // [max_leaf] (parent, first child id) of the batch's subtree roots
 };
+
+// sub words: the batch's subtree roots, the node-id limit their expansions may reach (keeps
+// 2 (remaining + 1) ids free, the planner's invariant), the leaf budget left, the previous
+// tree's smallest split gain (float bits), the running minimum of this tree's split gains
+enum { SUB_N = 0, SUB_LIMIT, SUB_REM, SUB_LAMBDA, SUB_MIN, SUB_WORDS = 8 };
 
 // planner phase timing (YTK_LW_PROF=1): thread 0 accumulates wall-clock ticks per phase
 #define LW_TICK(slot)                                                         \
@@ -327,6 +340,12 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_init_kernel(LwParams p, LwB
     b.zero_range[0] = make_int2(0, nblk);
     b.split_items[0] = make_int4(0, 0, 0, 0);
     b.item_sid[0] = 0;
+    if (b.sub) {  // the last tree's smallest split gain becomes this tree's expansion floor
+      const unsigned m = (unsigned)b.sub[SUB_MIN];
+      if (m != 0x7f800000u) b.sub[SUB_LAMBDA] = (int)m;
+      b.sub[SUB_MIN] = 0x7f800000;  // +inf
+      b.sub[SUB_N] = 0;
+    }
   }
   for (int k = threadIdx.x; k < nblk; k += kLwPlanThreads)
     b.hist_items[k] = make_int4(0, k * ch, min((k + 1) * ch, n_local), (k == 0 && nblk > kLwReduceDirect) ? 2 : 0);
@@ -631,7 +650,9 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     if (ev.x == EV_LEAF) {
       lw_write_node(b.tnodes[ev.z], b, sid, true, b.G[sid], b.H[sid], b.loss[sid], b.cnt[sid], -1, p);
     } else if (ev.x == EV_SPLIT) {
-      lw_write_node(b.tnodes[ev.z], b, sid, false, b.G[sid], b.H[sid], b.loss[sid], b.cnt[sid], ev.w, p);
+      const float ls = b.loss[sid];
+      lw_write_node(b.tnodes[ev.z], b, sid, false, b.G[sid], b.H[sid], ls, b.cnt[sid], ev.w, p);
+      if (b.sub && ls >= 0.f) atomicMin(reinterpret_cast<unsigned*>(&b.sub[SUB_MIN]), __float_as_uint(ls));
     } else {  // children made leaves right away: sums from the parent's best split
       const int l = s_nd[sid].x;
       const double gl = b.gl[sid], hl = b.hl[sid];
@@ -809,22 +830,28 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
   }
   LW_TICK(4);
   // F. expand the batch: children ids, partition descriptors (chunks of kLwChunk rows)
-  int s_nch = 0;  // this thread's entry's chunk count (k <= kLwPlanThreads: entry tid)
-  for (int j = tid; j < k; j += kLwPlanThreads) {
-    const int P = s_batch[j];
-    const int lc = nsid + 2 * j;
-    s_nd[P].x = lc;
-    const int nch = lw_expand_one(p, b, j, P, lc);
-    if (k <= kLwPlanThreads) s_nch = nch;  // one entry per thread: scanned in registers below
-  }
-  int nblocks = 0;
-  if (k > 0 && k <= kLwPlanThreads) {
+  // (k <= kLwLeafMax < kLwPlanThreads: one entry per thread.) Entries with <= sub_rows rows
+  // go to the subtree kernel (sub_list); the others, compacted, to the partition pipeline.
+  // Child ids follow the batch order either way.
+  static_assert(kLwLeafMax <= kLwPlanThreads, "one batch entry per planner thread");
+  int nblocks = 0, kn = k, ks = 0;
+  if (k > 0) {
+    const int j = tid;
+    const bool mine = j < k;
+    const int P = mine ? s_batch[j] : 0;
+    const bool sub = mine && p.sub_rows > 0 && s_nd[P].w <= p.sub_rows;
+    const int jn = lw_scan(mine && !sub ? 1 : 0, s_tmp, &kn);
+    const int js = lw_scan(sub ? 1 : 0, s_tmp, &ks);
+    int nch = 0;
+    if (mine) {
+      const int lc = nsid + 2 * j;
+      s_nd[P].x = lc;
+      if (sub) b.sub_list[js] = make_int2(P, lc);
+      else nch = lw_expand_one(p, b, jn, P, lc);
+    }
     // exclusive scan of the chunk counts in registers (no read-back of part_first)
-    const int first = lw_scan(tid < k ? s_nch : 0, s_tmp, &nblocks);
-    if (tid < k) b.part_first[tid] = first;
-  } else {
-    __syncthreads();
-    nblocks = k > 0 ? lw_scan_array(b.part_first, k, s_tmp) : 0;
+    const int first = lw_scan(nch, s_tmp, &nblocks);
+    if (mine && !sub) b.part_first[jn] = first;
   }
   LW_TICK(5);
   // G. write back the replay state
@@ -842,9 +869,14 @@ __global__ __launch_bounds__(kLwPlanThreads) void lw_plan_kernel(LwParams p, LwB
     st[LW_NUM_TNODES] = s_ntree;
     st[LW_SEQ] = s_seqc;
     st[LW_N_HEAP] = nh;
-    st[LW_N_SPLIT] = k;
+    st[LW_N_SPLIT] = kn;
     st[LW_N_PBLK] = nblocks;
     st[LW_N_SIDS] = nsid + 2 * k;
+    if (b.sub) {
+      b.sub[SUB_N] = ks;
+      b.sub[SUB_LIMIT] = p.cap - 2 * remaining - 2;
+      b.sub[SUB_REM] = remaining;
+    }
     if (k == 0) {
       st[LW_DONE] = 1;
       if (b.done_host) *(volatile int*)b.done_host = 1;  // polled by the host: no copy launch
@@ -1108,6 +1140,326 @@ void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
   lw_children_body(p, b);
 }
 
+// ---------------------------------------------------------------------------------
+// Small-node subtrees (single GPU). A late 255-leaf Higgs tree is ~20 levels deep, but most
+// of its splits sit in nodes of <= 32K rows (tools/lw_tree_shape.py): on the batch pipeline
+// each of those levels costs a planner call + four launches (~90 us) for a few thousand
+// rows. Here one 1024-thread workgroup per small batch entry P partitions P, builds the
+// smaller child's exact int64 histogram in LDS (hist_fx_kernel's layout and rounding),
+// derives the sibling and searches both children with the split kernels' own block search
+// (split_node_block: bit-identical records), then keeps growing P's subtree best-first --
+// up to sub_max more splits, only nodes whose path-minimum gain reaches sub_alpha x the
+// previous tree's smallest split gain, child ids taken under the planner's id limit. Every
+// expansion is speculative: the next planner's replay pops exactly the sequential growth's
+// nodes (an expansion it never pops only permuted rows inside its own segment), so trees
+// are identical to the batch path's (reference: DataParallelTreeMaker.java:219-295).
+constexpr int kSubThreads = 1024;
+constexpr int kSubU = 4;        // partition: rows per thread per step (kSubU x 16 wave counts)
+constexpr int kSubFront = 160;  // local frontier entries (<= sub_max + 2 live)
+constexpr int kSubHistU = 8;    // histogram: gathered rows in flight per lane
+constexpr int kSubMaxSplits = 128;
+
+struct SubArgs {
+  const uint8_t* bins;   // row-major bins [N][stride]
+  long long stride;
+  const uint8_t* binsT;  // column-major bins [F][ncol]
+  long long ncol;
+  const int* rows_in;    // the batch input's row ids by position (nullptr: identity)
+  const float2* gh_in;   // the batch input's (g, h) by position
+  int* rows2;            // 2N ping-pong row ids
+  float2* gh2;           // 2N ping-pong (g, h) (unused when ghr is set)
+  const float2* ghr;     // (g, h) by ROW id (YTK_LW_GH_ROWS=1), else nullptr
+  long long* hist;
+  int B, F, Bp;
+  const int* nbins_f;
+  const uint8_t* fmask;
+  int f0;
+  const float* scales;       // fixed-point scales (g, h) of the tree
+  const double* inv_scales;  // their inverses
+};
+
+// Rows [xb, xb + n) of rin (nullptr: identity) / ghin into the other half of the ping-pong
+// buffers: left rows from the front, right rows from the back (the order inside a child is
+// free: every downstream sum is exact). Returns the left count. s_c: 2 * 64 + 2 ints.
+__device__ int sub_partition(const SubArgs& a, const int* rin, const float2* ghin, int xb, int n, int feat, int thr,
+                             int N, int* s_c) {
+  constexpr int NW = kSubThreads / kWave;
+  constexpr int NE = kSubU * NW;
+  static_assert(NE == kWave, "one lane of wave 0 per (step row, wave) count");
+  const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+  const int sh = xb < N ? N : -N;
+  const int lstart = xb + sh, rend = xb + sh + n, end = xb + n;
+  const uint8_t* col = a.binsT + (size_t)feat * a.ncol;
+  const unsigned long long lt = l == 0 ? 0ull : (~0ull >> (64 - l));
+  int nl = 0, nr = 0;
+  for (int base = xb; base < end; base += kSubU * kSubThreads) {
+    int r[kSubU];
+    float2 g[kSubU];
+    bool ok[kSubU], lf[kSubU];
+#pragma unroll
+    for (int j = 0; j < kSubU; ++j) {
+      const int pos = base + j * kSubThreads + tid;
+      ok[j] = pos < end;
+      r[j] = ok[j] ? (rin ? rin[pos] : pos) : 0;
+      g[j] = (ok[j] && !a.ghr) ? ghin[pos] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < kSubU; ++j) lf[j] = ok[j] && (int)col[(unsigned)r[j]] <= thr;
+    int lr[kSubU], rr[kSubU];
+#pragma unroll
+    for (int j = 0; j < kSubU; ++j) {
+      const unsigned long long lm = __ballot(lf[j]), rm = __ballot(ok[j] && !lf[j]);
+      lr[j] = __popcll(lm & lt);
+      rr[j] = __popcll(rm & lt);
+      if (l == 0) {
+        s_c[j * NW + w] = __popcll(lm);
+        s_c[NE + j * NW + w] = __popcll(rm);
+      }
+    }
+    __syncthreads();
+    if (w == 0) {  // exclusive scans of the 64 left and 64 right counts
+      const int x = s_c[l], y = s_c[NE + l];
+      int ix = x, iy = y;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const int ux = __shfl_up(ix, off, kWave), uy = __shfl_up(iy, off, kWave);
+        if (l >= off) {
+          ix += ux;
+          iy += uy;
+        }
+      }
+      s_c[l] = ix - x;
+      s_c[NE + l] = iy - y;
+      if (l == kWave - 1) {
+        s_c[2 * NE] = ix;
+        s_c[2 * NE + 1] = iy;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSubU; ++j) {
+      if (!ok[j]) continue;
+      const int dst = lf[j] ? lstart + nl + s_c[j * NW + w] + lr[j]
+                            : rend - 1 - (nr + s_c[NE + j * NW + w] + rr[j]);
+      a.rows2[dst] = r[j];
+      if (!a.ghr) a.gh2[dst] = g[j];
+    }
+    nl += s_c[2 * NE];
+    nr += s_c[2 * NE + 1];
+    __syncthreads();  // s_c is rewritten by the next step
+  }
+  return nl;
+}
+
+// Exact histogram of the rows at positions [cb, cb + cn) of rows2 in LDS (hist_fx_kernel's
+// bin rows of [32 g | 32 h] words at hist_lds_pos, the same fx_round), stored to `slot`.
+__device__ void sub_hist(const SubArgs& a, unsigned long long* sm64, int cb, int cn, int slot, float sg, float sh) {
+  constexpr int kRow = 64;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < a.B * kRow; i += kSubThreads) sm64[i] = 0ull;
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, wr = lane >> 3, q = lane & 7;
+  constexpr int RW = (kSubThreads / kWave) * 8;  // rows per block step (8 per wave instruction)
+  const uint8_t* bseg = a.bins + 4 * q;
+  int lpos[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) lpos[c] = hist_lds_pos(4 * q + c);
+  const int end = cb + cn;
+  for (int base = cb + wave * 8; base < end; base += RW * kSubHistU) {
+    int r[kSubHistU];
+    bool ok[kSubHistU];
+#pragma unroll
+    for (int j = 0; j < kSubHistU; ++j) {
+      const int pos = base + j * RW + wr;
+      ok[j] = pos < end;
+      r[j] = a.rows2[ok[j] ? pos : cb];
+    }
+    unsigned d[kSubHistU];
+    float2 v[kSubHistU];
+#pragma unroll
+    for (int j = 0; j < kSubHistU; ++j) {
+      const int pos = base + j * RW + wr;
+      d[j] = *reinterpret_cast<const unsigned*>(bseg + (size_t)(unsigned)r[j] * a.stride);
+      const float2 t = a.ghr ? a.ghr[r[j]] : a.gh2[ok[j] ? pos : cb];
+      v[j] = ok[j] ? t : make_float2(0.f, 0.f);  // rows past the end add 0
+    }
+#pragma unroll
+    for (int j = 0; j < kSubHistU; ++j) {
+      const unsigned long long gi = fx_round(v[j].x * sg), hi = fx_round(v[j].y * sh);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = (k + wr) & 3;
+        const unsigned bin = __builtin_amdgcn_ubfe(d[j], 8 * c, 8);
+        unsigned long long* e = sm64 + (bin * kRow + lpos[c]);
+        atomicAdd(e, gi);
+        atomicAdd(e + 32, hi);
+      }
+    }
+  }
+  __syncthreads();
+  longlong2* out = reinterpret_cast<longlong2*>(a.hist + (size_t)slot * a.B * a.F * 2);
+  for (int i = tid; i < a.B * 32; i += kSubThreads) {
+    const int bin = i >> 5, fl = i & 31;
+    if (fl < a.F) {
+      const int li = bin * kRow + hist_lds_pos(fl);
+      out[(size_t)bin * a.F + fl] = make_longlong2((long long)sm64[li], (long long)sm64[li + 32]);
+    }
+  }
+  __syncthreads();  // the slot is read back (split search) and the LDS reused
+}
+
+// a child's split record -> its node fields (lw_apply_splits; canSplit: UpdateStrategy.java:50-53)
+__device__ void sub_apply(const LwParams& p, const LwBufs& b, int sid, long long cnt, const SplitOut& o) {
+  b.G[sid] = o.g;
+  b.H[sid] = o.h;
+  b.gl[sid] = o.gl;
+  b.hl[sid] = o.hl;
+  int feat = o.feat;
+  float chg = o.loss_chg;
+  if (!(o.h >= (double)p.mcw * 2.0 && cnt >= (long long)p.min_split_samples)) {
+    chg = -INFINITY;
+    feat = -1;
+  }
+  b.feat[sid] = feat;
+  b.bin_a[sid] = o.bin_a;
+  b.bin_b[sid] = o.bin_b;
+  b.loss[sid] = chg;
+  b.state[sid] = 1;
+}
+
+__global__ __launch_bounds__(kSubThreads) void lw_subtree_kernel(LwParams p, LwBufs b, SubArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long sm64[];  // histogram / split LDS
+  __shared__ int s_c[2 * kSubU * (kSubThreads / kWave) + 2];
+  __shared__ SplitOut s_rec[2];
+  __shared__ int f_sid[kSubFront];
+  __shared__ float f_loss[kSubFront], f_bl[kSubFront];
+  __shared__ int s_nf, s_x, s_lc, s_splits;
+  __shared__ float s_bl;
+  if (b.st[LW_DONE]) return;
+  const int nsub = b.sub[SUB_N];
+  if ((int)blockIdx.x >= nsub) return;  // block-uniform
+  const int tid = threadIdx.x;
+  const int limit = b.sub[SUB_LIMIT];
+  const int smax = min(p.sub_max, b.sub[SUB_REM] - 1);
+  const float floor_gain = p.sub_alpha * __int_as_float(b.sub[SUB_LAMBDA]);
+  const float sg = a.scales[0], sh = a.scales[1];
+  const GainParams gp{p.mcw, p.l1, p.l2, p.max_abs_leaf, a.inv_scales[0], a.inv_scales[1]};
+  longlong2* sh_hist = reinterpret_cast<longlong2*>(sm64);
+  unsigned long long n_splits = 0, n_roots = 0;
+  for (int e = blockIdx.x; e < nsub; e += gridDim.x) {
+    ++n_roots;
+    const int2 ent = b.sub_list[e];
+    int X = ent.x, L = ent.y;
+    bool root = true;
+    float bl = b.loss[X];  // minimum gain on the path from P (P's own)
+    if (tid == 0) {
+      s_nf = 0;
+      s_splits = 0;
+    }
+    __syncthreads();
+    while (true) {
+      // ---- split X into L, L + 1 (X's fields: written by earlier launches or by thread 0)
+      const int xb = b.begin[X], n = b.cnt_local[X];
+      const int feat = b.feat[X], thr = (b.bin_a[X] + b.bin_b[X]) >> 1;
+      const int dep = b.depth[X] + 1;
+      const int nl = sub_partition(a, root ? a.rows_in : a.rows2, root ? a.gh_in : a.gh2, xb, n, feat, thr, p.N, s_c);
+      const int nr = n - nl;
+      const int lb = xb + (xb < p.N ? p.N : -p.N);
+      ++n_splits;
+      // children that are terminal whatever the replay does get no histograms (lw_children_body)
+      const bool need = !(p.max_depth >= 0 && dep == p.max_depth) &&
+                        !(p.min_split_samples > 0 && nl < p.min_split_samples && nr < p.min_split_samples);
+      if (tid == 0) {  // fresh children (lw_expand_one) with their segments (lw_children_body)
+        for (int c = 0; c < 2; ++c) {
+          const int sid = L + c;
+          b.G[sid] = b.H[sid] = b.gl[sid] = b.hl[sid] = 0.0;
+          b.cnt[sid] = c ? nr : nl;
+          b.begin[sid] = c ? lb + nl : lb;
+          b.cnt_local[sid] = c ? nr : nl;
+          b.depth[sid] = dep;
+          b.feat[sid] = -1;
+          b.bin_a[sid] = b.bin_b[sid] = -1;
+          b.lc[sid] = -1;
+          b.tid[sid] = -1;
+          b.seq[sid] = 0;
+          b.state[sid] = 0;
+          b.loss[sid] = -INFINITY;
+        }
+        b.lc[X] = L;
+      }
+      if (need) {
+        const bool ls = nl < nr;  // build the smaller child, derive the other
+        const int S = ls ? L : L + 1, G = ls ? L + 1 : L;
+        sub_hist(a, sm64, ls ? lb : lb + nl, ls ? nl : nr, S, sg, sh);
+        split_node_block<kSubThreads>(a.hist, a.B, a.F, a.Bp, a.nbins_f, a.fmask, a.f0, make_int4(S, 0, 0, 0),
+                                      &s_rec[0], gp, sh_hist);
+        __syncthreads();
+        split_node_block<kSubThreads>(a.hist, a.B, a.F, a.Bp, a.nbins_f, a.fmask, a.f0, make_int4(G, X, S, 1),
+                                      &s_rec[1], gp, sh_hist);
+        __syncthreads();
+        if (tid == 0) {
+          sub_apply(p, b, S, ls ? nl : nr, s_rec[0]);
+          sub_apply(p, b, G, ls ? nr : nl, s_rec[1]);
+          for (int c = 0; c < 2; ++c) {  // frontier: splittable children above the gain floor
+            const int sid = L + c;
+            const float lc_loss = b.loss[sid];
+            const float blc = fminf(bl, lc_loss);
+            if (!lw_static_leaf(p, lc_loss, dep, c ? nr : nl) && blc >= floor_gain && s_nf < kSubFront) {
+              f_sid[s_nf] = sid;
+              f_loss[s_nf] = lc_loss;
+              f_bl[s_nf] = blc;
+              ++s_nf;
+            }
+          }
+        }
+      }
+      // ---- next: the frontier's best gain (the subtree's own best-first order), if the
+      // split budget and a child id pair under the planner's limit allow
+      if (tid == 0) {
+        int nx = -1;
+        if (s_splits < smax && s_nf > 0) {
+          int bi = 0;
+          for (int i = 1; i < s_nf; ++i)
+            if (f_loss[i] > f_loss[bi]) bi = i;
+          int cur = __hip_atomic_load(&b.st[LW_N_SIDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          int got = -1;
+          while (cur + 2 <= limit) {
+            const int old = atomicCAS(&b.st[LW_N_SIDS], cur, cur + 2);
+            if (old == cur) {
+              got = cur;
+              break;
+            }
+            cur = old;
+          }
+          if (got >= 0) {
+            nx = f_sid[bi];
+            s_lc = got;
+            s_bl = f_bl[bi];
+            --s_nf;
+            f_sid[bi] = f_sid[s_nf];
+            f_loss[bi] = f_loss[s_nf];
+            f_bl[bi] = f_bl[s_nf];
+            ++s_splits;
+          }
+        }
+        s_x = nx;
+      }
+      __syncthreads();
+      const int nx = s_x;
+      if (nx < 0) break;
+      X = nx;
+      L = s_lc;
+      bl = s_bl;
+      root = false;
+      __syncthreads();  // s_x / s_lc / s_bl are rewritten by the next step
+    }
+  }
+  if (b.prof && tid == 0) {
+    atomicAdd(&b.prof[16], n_roots);   // subtree roots
+    atomicAdd(&b.prof[17], n_splits);  // splits computed by subtrees (roots included)
+  }
+}
+
 // hist[ids[i]] = 0 for the *n_dev listed slots (grid-stride over all their 16-B words).
 // Slots listed with more than min_items items (the split-K reduce adds into them with
 // atomics) are zeroed; the others are stored whole by the reduce / histogram kernels.
@@ -1245,10 +1597,11 @@ extern "C" {
 //       state, loss, heap, batch, part_feat, part_thr, part_begin, part_cnt, part_first,
 //       part_shift, cursor, hist_items, build_ids, split_items, item_sid, split_out, root_cnt,
 //       prof (0 = off), done_host (device pointer of a pinned int, 0 = off), zero_ids, zero_range,
-//       plan workspace (ytk_lw_ws_bytes bytes; 0 when that is 0)
+//       plan workspace (ytk_lw_ws_bytes bytes; 0 when that is 0), sub words (int[8], zeroed),
+//       sub_list (int2[max_leaf])
 // ip: max_depth, max_leaf, min_split_samples, speculate, hist_target, min_rows, cap, N, split_groups, dist,
-//     bin_bytes
-// fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr. Returns an engine handle.
+//     bin_bytes, sub_rows (0: no subtrees), sub_max
+// fp: min_split_loss, mcw, l1, l2, max_abs_leaf, lr, sub_alpha. Returns an engine handle.
 int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   LwEngine e;
   LwParams& p = e.p;
@@ -1266,6 +1619,10 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   p.bin_bytes = ip[10] == 2 ? 2 : 1;
   p.batch_cap = 0;
   p.slow_children = 0;
+  // subtrees: single GPU, byte bins (multi-GPU batches all-reduce every built histogram)
+  p.sub_rows = (p.dist || p.bin_bytes != 1) ? 0 : std::max(0, ip[11]);
+  p.sub_max = std::min(std::max(0, ip[12]), kSubMaxSplits);
+  p.sub_alpha = fp[6];
   p.min_split_loss = fp[0];
   p.mcw = fp[1];
   p.l1 = fp[2];
@@ -1318,6 +1675,9 @@ int ytk_lw_create(const uintptr_t* a, const int* ip, const float* fp) {
   if (big && !ws) throw std::invalid_argument("lw_create: the workspace planner (max_leaf > 512) needs its workspace");
   b.ws = LwPlanWs{};
   if (big) lw_carve_ws(ws, p.cap, p.max_leaf, b.ws);
+  b.sub = (int*)a[i++];
+  b.sub_list = (int2*)a[i++];
+  if (p.sub_rows > 0 && (!b.sub || !b.sub_list)) throw std::invalid_argument("lw_create: subtrees need their buffers");
   g_lw.push_back(e);
   return (int)g_lw.size() - 1;
 }
@@ -1425,6 +1785,29 @@ void ytk_lw_owner(int h, uintptr_t hist, long long slot_elems, int B, int F, int
   hipLaunchKernelGGL(lw_owner_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), (long long*)hist,
                      slot_elems, B, F, fr, P, rank, e.b.build_ids, e.b.st + LW_N_BUILD, e.b.cursor,
                      e.b.st + LW_N_SPLIT, (long long*)x, kcap, unpack, e.b.st + LW_DONE);
+  YTK_LAUNCH_CHECK();
+}
+
+// small-node subtrees of the current batch (after its split search; no-op when the
+// engine has none). bins / binsT: uint8 row- / column-major; rows_in / gh_in: the batch's input
+// (as ytk_lw_partition); ghr: row-indexed (g, h) (YTK_LW_GH_ROWS=1) or 0.
+void ytk_lw_subtree(int h, uintptr_t bins, long long stride, uintptr_t binsT, long long ncol, uintptr_t rows_in,
+                    uintptr_t gh_in, uintptr_t rows2, uintptr_t gh2, uintptr_t ghr, uintptr_t hist, int B, int F,
+                    uintptr_t nbins_f, uintptr_t fmask, int f0, uintptr_t scales, uintptr_t inv_scales,
+                    uintptr_t stream) {
+  const LwEngine& e = g_lw.at(h);
+  if (e.p.sub_rows <= 0) return;
+  const int Bp = B + 1;
+  if (F > 32 || B > 4 * kWave || stride % 32 != 0 || (size_t)F * Bp * 16 > kNodeLdsMax ||
+      B * F > kNodeLoads * kNodeThreads)
+    throw std::invalid_argument("lw_subtree: needs F <= 32, B <= 256, a 32-aligned bin stride");
+  SubArgs a{(const uint8_t*)bins, stride, (const uint8_t*)binsT, ncol, (const int*)rows_in, (const float2*)gh_in,
+            (int*)rows2, (float2*)gh2, (const float2*)ghr, (long long*)hist, B, F, Bp, (const int*)nbins_f,
+            (const uint8_t*)fmask, f0, (const float*)scales, (const double*)inv_scales};
+  const size_t lds = std::max((size_t)B * 64 * 8, (size_t)F * Bp * 16);
+  const int grid = std::min(e.p.max_leaf, 256);
+  hipLaunchKernelGGL(lw_subtree_kernel, dim3(grid), dim3(kSubThreads), lds, reinterpret_cast<hipStream_t>(stream),
+                     e.p, e.b, a);
   YTK_LAUNCH_CHECK();
 }
 

@@ -334,6 +334,44 @@ def test_device_leafwise_children_fast_path_identical(monkeypatch, kw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{}, {"max_leaf_cnt": 255, "rows": "1000000000"}, {"sub_max": "2", "alpha": "0"},
+                                {"max_depth": 7, "max_leaf_cnt": 40}, {"min_split_samples": 700},
+                                {"instance_sample_rate": 0.7, "feature_sample_rate": 0.6, "gh_rows": "1"},
+                                {"max_leaf_cnt": 255, "min_split_loss": 1.0, "rows": "4000", "sub_max": "128"},
+                                {"l1": 0.5, "max_abs_leaf_val": 0.3, "alpha": "3"}])
+def test_device_leafwise_subtrees_identical(monkeypatch, kw):
+    """Small-node subtrees (lw_subtree_kernel: one workgroup grows a small batch entry's
+    subtree speculatively) build the batch pipeline's trees byte for byte, whatever the row
+    threshold (1e9: the root batch itself is one subtree), split budget and gain floor."""
+    kw = dict(kw)
+    monkeypatch.setenv("YTK_LW_PROF", "1")
+    monkeypatch.setenv("YTK_LW_SUB_MAX", kw.pop("sub_max", "32"))
+    monkeypatch.setenv("YTK_LW_SUB_ALPHA", kw.pop("alpha", "1.0"))
+    monkeypatch.setenv("YTK_LW_GH_ROWS", kw.pop("gh_rows", "0"))
+    rows = kw.pop("rows", "16384")
+    res = []
+    for sub in ("0", rows):
+        monkeypatch.setenv("YTK_LW_SUB_ROWS", sub)
+        p = _params("loss", rounds=4)
+        p.tree.max_leaf_cnt = 63
+        for k, v in kw.items():
+            setattr(p.tree, k, v)
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(120000, 41, "cuda"), _data(6000, 42, "cuda"))
+        tr.train()
+        assert tr.use_device_builder and tr.builder.sub_on == (sub != "0")
+        prof = tr.builder.prof_report()
+        if sub != "0":
+            assert prof["sub_roots"] > 0 and prof["sub_splits"] >= prof["sub_roots"]
+        else:
+            assert prof["sub_roots"] == 0
+        assert tr.builder.stats()[2] == 0  # no overflow
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1]
+    assert res[0][0].count("leaf=") > 40
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sample", [1.0, 0.7])
 def test_device_leafwise_row_indexed_gh_identical(monkeypatch, sample):
     """YTK_LW_GH_ROWS=1: (g, h) stays row-indexed (the partition moves row ids only, the

@@ -23,6 +23,8 @@ ALLOWED = [
     (r"tree_grad_hist_kernel<0, 2>", "sigmoid fused pass at the 128-VGPR cap of 1024-thread blocks: one dword per 2 rows"),
     (r"split_feat_kernel<\d+, 1024>", "wide-bin (> 1024 bins) split search, 1024-thread blocks"),
     (r"lw_plan_kernel<true>", "one-block leaf-wise planner, workspace mode (> 512 leaves) at 1024 threads"),
+    (r"lw_subtree_kernel", "opt-in small-node subtree kernel (YTK_LW_SUB_ROWS, off by default): "
+                           "split_node_block's register tiles at the 1024-thread VGPR cap"),
 ]
 
 pytestmark = pytest.mark.skipif(not shutil.which(os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")),

@@ -53,6 +53,13 @@ class DeviceLeafBuilder:
     # measured: no gain -- the gaps between dependent kernels are on the device side)
     POLL_LAG = int(os.environ.get("YTK_LW_POLL_LAG", 2))
     POLL_TIMEOUT_S = 60.0
+    # small-node subtrees (opt-in YTK_LW_SUB_ROWS > 0; single GPU, byte bins, F <= 32): batch
+    # entries with <= SUB_ROWS rows are grown by one workgroup each (lw_subtree_kernel), up to
+    # SUB_MAX more splits, through nodes whose path-minimum gain is >= SUB_ALPHA x the previous
+    # tree's smallest split gain (speculative: the trees are identical whatever these are).
+    # Off by default: one CU per subtree needs ~25-45 us per split, slower than the batch
+    # pipeline at every setting measured (500 trees: 4.06 -> 5.1-24 ms, docs/performance.md)
+    SUB_ROWS_DEFAULT, SUB_MAX_DEFAULT, SUB_ALPHA_DEFAULT = 0, 32, 1.0
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
                  params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
@@ -170,6 +177,12 @@ class DeviceLeafBuilder:
         # YTK_LW_PROF=1: planner phase times + work counters accumulated on the device
         self.prof = (torch.zeros(32, dtype=torch.int64, device=dev)
                      if os.environ.get("YTK_LW_PROF") == "1" else None)
+        self.SUB_ROWS = int(os.environ.get("YTK_LW_SUB_ROWS", self.SUB_ROWS_DEFAULT))
+        self.SUB_MAX = int(os.environ.get("YTK_LW_SUB_MAX", self.SUB_MAX_DEFAULT))
+        self.SUB_ALPHA = float(os.environ.get("YTK_LW_SUB_ALPHA", self.SUB_ALPHA_DEFAULT))
+        self.sub_on = (self.SUB_ROWS > 0 and not self.comm.is_dist and not self.wide and F <= 32 and B <= 256)
+        self.sub_words = i32(8)
+        self.sub_list = i32(2 * ml)
         # max_leaf_cnt > 512: the planner's per-node arrays and queues in global memory
         ws = int(hip().lw_ws_bytes(self.cap, ml))
         self.plan_ws = torch.zeros(ws, dtype=torch.uint8, device=dev) if ws > 0 else None
@@ -241,7 +254,7 @@ class DeviceLeafBuilder:
     def _fp(self):
         p = self.p
         return [float(np.float32(v)) for v in (p.min_split_loss, p.min_child_hessian_sum, p.l1, p.l2,
-                                              p.max_abs_leaf_val, p.learning_rate)]
+                                              p.max_abs_leaf_val, p.learning_rate, self.SUB_ALPHA)]
 
     def _ip(self):
         p = self.p
@@ -249,7 +262,8 @@ class DeviceLeafBuilder:
         # budget the batch choice ranks within (100 = the host planner's virtual replay)
         spec = int(os.environ.get("YTK_LW_SPEC_PCT", "100")) if os.environ.get("YTK_LOSSGUIDE_SPEC", "1") != "0" else 0
         return [p.max_depth, p.max_leaf_cnt, p.min_split_samples, spec, self.HIST_TARGET, self.MIN_ROWS,
-                self.cap, self.N, self.split_groups, 1 if self.comm.is_dist else 0, 2 if self.wide else 1]
+                self.cap, self.N, self.split_groups, 1 if self.comm.is_dist else 0, 2 if self.wide else 1,
+                self.SUB_ROWS if self.sub_on else 0, self.SUB_MAX]
 
     def _ptrs(self):
         f, i = self.nd_f64, self.nd_i32
@@ -260,7 +274,8 @@ class DeviceLeafBuilder:
                 + [ptr(self.cursor), ptr(self.hist_items), ptr(self.build_ids), ptr(self.split_items),
                    ptr(self.item_sid), ptr(self.split_out), ptr(self.root_cnt),
                    ptr(self.prof) if self.prof is not None else 0, self._done_dev, ptr(self.zero_ids),
-                   ptr(self.zero_range), ptr(self.plan_ws) if self.plan_ws is not None else 0])
+                   ptr(self.zero_range), ptr(self.plan_ws) if self.plan_ws is not None else 0,
+                   ptr(self.sub_words), ptr(self.sub_list)])
 
     def _lv_ptrs(self):
         """Pointer list of the level engine's finalize / raw-tree kernels (st, nodes, arrays)."""
@@ -638,7 +653,7 @@ class DeviceLeafBuilder:
         out["plan_queue_sort_us"] = round(float(v[7]) / 100.0, 1)
         out.update(plan_calls=int(v[8]), part_blocks=int(v[9]), replay_events=int(v[10]), candidates=int(v[11]),
                    hist_rows=int(v[12]), built_slots=int(v[13]), hist_items=int(v[14]),
-                   replay_sorted_pops=int(v[21]))
+                   replay_sorted_pops=int(v[21]), sub_roots=int(v[16]), sub_splits=int(v[17]))
         for i, n in ((22, "jump"), (23, "keys"), (24, "rank")):  # parts of "select"
             out[f"plan_select_{n}_us"] = round(float(v[i]) / 100.0, 1)
         return out
@@ -653,6 +668,10 @@ class DeviceLeafBuilder:
         self._part(h, hd, rows_in, gh_in, s)
         if self.peer is None:
             self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
+            if self.sub_on:  # the batch's small entries: whole subtrees, one workgroup each
+                h.lw_subtree(hd, ptr(self.bins), self.bins.shape[1], ptr(self.binsT), self.binsT.shape[1], rows_in,
+                             gh_in, ptr(self.rows2), ptr(self.gh2), self._ghr, ptr(self.hist), self.B, self.F,
+                             ptr(self.nbins_f), ptr(fmask), f0, ptr(self.scales), ptr(self.inv_scales), s)
             return
         self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
         if self.owner:  # reduce-scatter by feature block (one kernel sized on the device)
