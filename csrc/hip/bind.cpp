@@ -84,12 +84,12 @@ void ytk_ffm_grad_csc(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uin
 void ytk_ffm_sgd_grad(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t, long long, int, uintptr_t);
 void ytk_ffm_pairs_lds(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int, int,
-                       uintptr_t, long long, uintptr_t);
+                       uintptr_t, long long, int, uintptr_t);
 void ytk_ffm_pairs_fwd_e(uintptr_t, uintptr_t, uintptr_t, uintptr_t, long long, uintptr_t, int, uintptr_t, int,
                          uintptr_t, long long, int, uintptr_t);
 void ytk_ffm_sgd_ecol(uintptr_t, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                       uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, float,
-                      float, float, int, int, int, int, uintptr_t);
+                      float, float, int, int, int, int, uintptr_t, uintptr_t);
 void ytk_ffm_grad_stream(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                          long long, uintptr_t, int, uintptr_t, long long, int, int, uintptr_t, uintptr_t);
 // fm.hip

@@ -212,40 +212,70 @@ __global__ __launch_bounds__(256) void ffm_pairs_k4_kernel(
 // kE (SGD pair terms, as ffm_pairs_k4_kernel<true>): then E[e_p][q] = x_p x_q V[i_q, f_p] row by
 // row, lanes q reading LDS column f_p -- every store a coalesced row, no transpose.
 constexpr int kLdsU = 16;  // staging loads in flight per lane (4: 30.7 ms per 4M-row forward, bytes-in-flight bound)
-template <bool kE>
+
+// bf16 latent slots (k == 4: one 8-B uint2 of packed bf16 pairs per (feature, field)):
+// widened exactly to fp32, narrowed round-to-nearest-even (finite values)
+__device__ __forceinline__ float4 bf4_to_f4(uint2 h) {
+  return make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u), __uint_as_float(h.y << 16),
+                     __uint_as_float(h.y & 0xffff0000u));
+}
+__device__ __forceinline__ unsigned f_to_bf(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ uint2 f4_to_bf4(float4 v) {
+  return make_uint2(f_to_bf(v.x) | (f_to_bf(v.y) << 16), f_to_bf(v.z) | (f_to_bf(v.w) << 16));
+}
+
+// kBf (SGD dtype = bf16): V is the bf16 working copy (8-B slots, half the staging bytes)
+// and the pair terms E are written as bf16 (half the bytes the chunk sums read back); the LDS
+// rows, the pair dot products and the row sums stay fp32.
+template <bool kE, bool kBf = false>
 __global__ __launch_bounds__(64) void ffm_pairs_lds_kernel(
     const long long* __restrict__ indptr, const int* __restrict__ idx, const float* __restrict__ val,
-    const int* __restrict__ fld, long long nrows, const float4* __restrict__ V, int nfield,
-    float* __restrict__ fx, int skip_feat, float4* __restrict__ E, long long e_base) {
+    const int* __restrict__ fld, long long nrows, const void* __restrict__ Vv, int nfield,
+    float* __restrict__ fx, int skip_feat, void* __restrict__ Ev, long long e_base) {
+  // bf16: 8-B slot loads (16-B slot-pair loads widened into two LDS rows measured slower, 0.91
+  // vs 0.70 ms per batch: this kernel is bound by its LDS and shuffle work, not by bytes)
+  const float4* __restrict__ V = reinterpret_cast<const float4*>(Vv);
+  const uint2* __restrict__ Vh = reinterpret_cast<const uint2*>(Vv);
+  float4* __restrict__ E = reinterpret_cast<float4*>(Ev);
   extern __shared__ float4 s_v[];  // [m][nfield + 1]
   const int lane = threadIdx.x;
   const int S = nfield + 1;
-  const int step_j = 64 / nfield, step_t = 64 - step_j * nfield;
-  const int lane_j = lane / nfield, lane_t = lane - lane_j * nfield;
+  const int tn = nfield;  // staging units per entry
+  const int step_j = 64 / tn, step_t = 64 - step_j * tn;
+  const int lane_j = lane / tn, lane_t = lane - lane_j * tn;
   for (long long row = blockIdx.x; row < nrows; row += gridDim.x) {
     const long long b = indptr[row];
     const int m = (int)(indptr[row + 1] - b);
     int ij = 0, fj = 0;
     float xj = 0.f;
     if (lane < m) { ij = idx[b + lane]; fj = fld[b + lane]; xj = val[b + lane]; }
-    const int tot = m * nfield;
-    int j = lane_j, t = lane_t;  // (entry, slot) of position s0 + u * 64 + lane
+    const int tot = m * tn;
+    int j = lane_j, t = lane_t;  // (entry, unit) of position s0 + u * 64 + lane
     for (int s0 = 0; s0 < tot; s0 += 64 * kLdsU) {
       float4 v[kLdsU];
+      uint2 vh[kLdsU];  // bf16: raw slots, every load issued before any is widened (widening in
+                        // this loop made the compiler wait on each load in turn)
       int dst[kLdsU];
 #pragma unroll
       for (int u = 0; u < kLdsU; ++u) {
         const int sp = s0 + u * 64 + lane;
         const int i = __shfl(ij, min(j, 63), 64);
         dst[u] = sp < tot ? j * S + t : -1;
-        v[u] = sp < tot ? V[(long long)i * nfield + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (kBf)
+          vh[u] = sp < tot ? Vh[(long long)i * nfield + t] : make_uint2(0u, 0u);
+        else
+          v[u] = sp < tot ? V[(long long)i * nfield + t] : make_float4(0.f, 0.f, 0.f, 0.f);
         t += step_t;
         j += step_j;
-        if (t >= nfield) { t -= nfield; ++j; }
+        if (t >= tn) { t -= tn; ++j; }
       }
 #pragma unroll
-      for (int u = 0; u < kLdsU; ++u)
-        if (dst[u] >= 0) s_v[dst[u]] = v[u];
+      for (int u = 0; u < kLdsU; ++u) {
+        if (dst[u] >= 0) s_v[dst[u]] = kBf ? bf4_to_f4(vh[u]) : v[u];
+      }
     }
     wave_sync();
     float acc = 0.f;
@@ -266,11 +296,25 @@ __global__ __launch_bounds__(64) void ffm_pairs_lds_kernel(
         acc += (a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w) * xx;
       }
     }
-    if (kE) {  // E rows: entry p, lanes q
+    if constexpr (kE && kBf) {  // E rows: entry p, lanes q, one 8-B bf16 slot each (16-B slot
+      // pairs per lane measured slower: 1.02 vs 0.70 ms per batch -- twice the LDS reads per lane
+      // at a doubled lane stride)
+      uint2* Eq = reinterpret_cast<uint2*>(Ev);
+      const bool qs = lane < m && ij != skip_feat;
+      for (int p = 0; p < m; ++p) {  // p is wave-uniform: readlane, no LDS-routed shuffles
+        const int fp = __builtin_amdgcn_readlane(fj, p), ip = __builtin_amdgcn_readlane(ij, p);
+        const float xp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xj), p));
+        if (lane < m) {
+          const float s = (qs && lane != p && ip != skip_feat) ? xp * xj : 0.f;
+          const float4 c = s_v[lane * S + fp];
+          Eq[(b - e_base + p) * m + lane] = f4_to_bf4(make_float4(s * c.x, s * c.y, s * c.z, s * c.w));
+        }
+      }
+    } else if constexpr (kE) {  // E rows: entry p, lanes q
       const bool qs = lane < m && ij != skip_feat;
       for (int p = 0; p < m; ++p) {
-        const int fp = __shfl(fj, p, 64), ip = __shfl(ij, p, 64);
-        const float xp = __shfl(xj, p, 64);
+        const int fp = __builtin_amdgcn_readlane(fj, p), ip = __builtin_amdgcn_readlane(ij, p);
+        const float xp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xj), p));
         if (lane < m) {
           const float s = (qs && lane != p && ip != skip_feat) ? xp * xj : 0.f;
           const float4 c = s_v[lane * S + fp];
@@ -697,15 +741,20 @@ __global__ __launch_bounds__(256) void ffm_sgd_grad_kernel(
 // sgd_apply_kernel would from a single chunk (w -= lri (g + cnt l2w w), V -= lri (gV + cnt
 // l2v V), bias rules); the others write lat / lin = (sum c x, 0) for sgd_apply over the
 // multi-chunk columns. The skipped column (chunk_fa < 0) has all-zero E rows: no latent step.
+// kBf: E holds bf16 pair terms (packed 8-B slots; the sums stay fp32) and the bf16 working copy Vb of
+// every updated latent slot is re-rounded from its new fp32 value.
 constexpr int kEcolCpg = 8;
+template <bool kBf = false>
 __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
     const long long* __restrict__ chunk_beg, const long long* __restrict__ chunk_end, long long nch,
     const int* __restrict__ csc_rows, const float* __restrict__ csc_vals, const int* __restrict__ csc_perm,
     const int* __restrict__ chunk_fa, const int* __restrict__ chunk_col, const unsigned char* __restrict__ solo,
-    const float4* __restrict__ E, int m, const int* __restrict__ lay_field, const float* __restrict__ coef,
+    const void* __restrict__ Ev, int m, const int* __restrict__ lay_field, const float* __restrict__ coef,
     float* __restrict__ lat, float* __restrict__ lin, float* __restrict__ w, float* __restrict__ V, float lr,
-    float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg) {
-  constexpr int GL = 32, U = 4;
+    float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg, uint2* __restrict__ Vb) {
+  const float4* __restrict__ E = reinterpret_cast<const float4*>(Ev);
+  const uint2* __restrict__ Eh = reinterpret_cast<const uint2*>(Ev);
+  constexpr int GL = 32, U = kBf ? 8 : 4;  // bf16: half the registers per row in flight
   const long long grp = (blockIdx.x * 256LL + threadIdx.x) / GL;
   const int q = threadIdx.x & (GL - 1);
   const long long c0 = grp * kEcolCpg;
@@ -721,8 +770,11 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
   }
   const long long E0 = chunk_beg[c0];
   const long long E1 = __shfl(my_e1, nc - 1, GL);
-  const bool has0 = q < m, has1 = q + GL < m;
-  const int lf0 = has0 ? lay_field[q] : 0, lf1 = has1 ? lay_field[q + GL] : 0;
+  // lane q owns positions (q, q + 32); bf16 (m even): the adjacent pair (2q, 2q + 1), read as
+  // one 16-B load -- the chunk sums are bound by load requests, not bytes
+  const int pos0 = kBf ? 2 * q : q, pos1 = kBf ? 2 * q + 1 : q + GL;
+  const bool has0 = pos0 < m, has1 = pos1 < m;
+  const int lf0 = has0 ? lay_field[pos0] : 0, lf1 = has1 ? lay_field[pos1] : 0;
   const long long J4 = m;  // float4 slots per feature (nfield == m, k == 4)
   int ci = 0;
   long long cbeg = E0, cend = __shfl(my_e1, 0, GL);
@@ -751,14 +803,18 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
     if (has0) {
       float4* p = vr + lf0;
       const float4 v = *p;
-      *p = make_float4(v.x - lri * (a0.x + dec * v.x), v.y - lri * (a0.y + dec * v.y),
-                       v.z - lri * (a0.z + dec * v.z), v.w - lri * (a0.w + dec * v.w));
+      const float4 nv = make_float4(v.x - lri * (a0.x + dec * v.x), v.y - lri * (a0.y + dec * v.y),
+                                    v.z - lri * (a0.z + dec * v.z), v.w - lri * (a0.w + dec * v.w));
+      *p = nv;
+      if constexpr (kBf) Vb[(long long)col * J4 + lf0] = f4_to_bf4(nv);
     }
     if (has1) {
       float4* p = vr + lf1;
       const float4 v = *p;
-      *p = make_float4(v.x - lri * (a1.x + dec * v.x), v.y - lri * (a1.y + dec * v.y),
-                       v.z - lri * (a1.z + dec * v.z), v.w - lri * (a1.w + dec * v.w));
+      const float4 nv = make_float4(v.x - lri * (a1.x + dec * v.x), v.y - lri * (a1.y + dec * v.y),
+                                    v.z - lri * (a1.z + dec * v.z), v.w - lri * (a1.w + dec * v.w));
+      *p = nv;
+      if constexpr (kBf) Vb[(long long)col * J4 + lf1] = f4_to_bf4(nv);
     }
   };
   for (long long wb = E0; wb < E1; wb += GL) {
@@ -781,13 +837,30 @@ __global__ __launch_bounds__(256) void ffm_sgd_ecol_kernel(
         xv[u] = __shfl(xL, src, GL);
       }
       float4 x0[U], x1[U];
+      uint2 h0[U], h1[U];  // bf16: raw slots, every load issued before any is widened
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         x0[u] = x1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        h0[u] = h1[u] = make_uint2(0u, 0u);
         if (i + u < n) {
-          const float4* row = E + (long long)pr[u] * m;
-          if (has0) x0[u] = row[q];
-          if (has1) x1[u] = row[q + GL];
+          if constexpr (kBf) {
+            if (has0) {  // m even: has0 implies has1
+              const uint4 pair = reinterpret_cast<const uint4*>(Eh + (long long)pr[u] * m)[q];
+              h0[u] = make_uint2(pair.x, pair.y);
+              h1[u] = make_uint2(pair.z, pair.w);
+            }
+          } else {
+            const float4* row = E + (long long)pr[u] * m;
+            if (has0) x0[u] = row[q];
+            if (has1) x1[u] = row[q + GL];
+          }
+        }
+      }
+      if constexpr (kBf) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          x0[u] = bf4_to_f4(h0[u]);
+          x1[u] = bf4_to_f4(h1[u]);
         }
       }
 #pragma unroll
@@ -964,16 +1037,23 @@ void ytk_ffm_sgd_ecol(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
                       uintptr_t csc_perm, uintptr_t chunk_fa, uintptr_t chunk_col, uintptr_t solo, uintptr_t E, int m,
                       uintptr_t lay_field, uintptr_t coef, uintptr_t lat, uintptr_t lin, uintptr_t w, uintptr_t V,
                       float lr, float l2w, float l2v, int reg_skip, int upd_w, int bias_latent, int avg,
-                      uintptr_t stream) {
+                      uintptr_t Vb, uintptr_t stream) {
+  // Vb != 0: E holds bf16 pair terms and the bf16 working copy Vb ([F][m] 8-B slots) is kept
   if (nch <= 0) return;
   if (m < 1 || m > 64) throw std::invalid_argument("ffm_sgd_ecol: need 1 <= m <= 64");
-  if ((E & 15) || (lat & 15) || (V & 15)) throw std::invalid_argument("ffm_sgd_ecol: E / lat / V must be 16-B aligned");
-  hipLaunchKernelGGL(ffm_sgd_ecol_kernel, dim3((unsigned)(((nch + kEcolCpg - 1) / kEcolCpg * 32 + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), (const long long*)chunk_beg, (const long long*)chunk_end,
-                     nch, (const int*)csc_rows, (const float*)csc_vals, (const int*)csc_perm, (const int*)chunk_fa,
-                     (const int*)chunk_col, (const unsigned char*)solo, (const float4*)E, m, (const int*)lay_field,
-                     (const float*)coef, (float*)lat, (float*)lin, (float*)w, (float*)V, lr, l2w, l2v, reg_skip,
-                     upd_w, bias_latent, avg);
+  if ((E & 15) || (lat & 15) || (V & 15) || (Vb & 7) || (Vb && (m & 1)))
+    throw std::invalid_argument("ffm_sgd_ecol: E / lat / V 16-B aligned, Vb 8-B; bf16 needs an even m");
+  const dim3 grid((unsigned)(((nch + kEcolCpg - 1) / kEcolCpg * 32 + 255) / 256));
+#define YTK_ECOL(BF)                                                                                          \
+  hipLaunchKernelGGL(ffm_sgd_ecol_kernel<BF>, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),     \
+                     (const long long*)chunk_beg, (const long long*)chunk_end, nch, (const int*)csc_rows,     \
+                     (const float*)csc_vals, (const int*)csc_perm, (const int*)chunk_fa, (const int*)chunk_col, \
+                     (const unsigned char*)solo, (const void*)E, m, (const int*)lay_field, (const float*)coef, \
+                     (float*)lat, (float*)lin, (float*)w, (float*)V, lr, l2w, l2v, reg_skip, upd_w, bias_latent, \
+                     avg, (uint2*)Vb)
+  if (Vb) YTK_ECOL(true);
+  else YTK_ECOL(false);
+#undef YTK_ECOL
   YTK_LAUNCH_CHECK();
 }
 
@@ -981,24 +1061,27 @@ void ytk_ffm_sgd_ecol(uintptr_t chunk_beg, uintptr_t chunk_end, long long nch, u
 // k == 4, V 16-B aligned, every row of <= max_m <= 64 entries, max_m * (nfield + 1) * 16 B of
 // LDS. E != 0: fixed-layout rows of exactly max_m entries, also writing the SGD pair terms
 // E[entry - e_base][max_m] (float4).
+// bf16 = 1: V is the bf16 working copy ([F][nfield] 8-B slots) and E (SGD) is written as bf16.
 void ytk_ffm_pairs_lds(uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t fld, long long nrows, uintptr_t V,
                        int nfield, uintptr_t fx, int skip_feat, int max_m, uintptr_t E, long long e_base,
-                       uintptr_t stream) {
+                       int bf16, uintptr_t stream) {
   if (nrows <= 0) return;
   if ((V & 15) || (E & 15)) throw std::invalid_argument("ffm_pairs_lds: V / E must be 16-B aligned");
+  if (bf16 && E && (max_m & 1)) throw std::invalid_argument("ffm_pairs_lds: bf16 pair terms need even rows");
   if (max_m < 1 || max_m > 64 || nfield < 1) throw std::invalid_argument("ffm_pairs_lds: 1 <= max_m <= 64");
   const size_t lds = (size_t)max_m * (nfield + 1) * sizeof(float4);
   if (lds > 64 * 1024) throw std::invalid_argument("ffm_pairs_lds: max_m * (nfield + 1) * 16 B > 64 KiB");
   const long long grid = std::min<long long>(nrows, 256LL * 32);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (E)
-    hipLaunchKernelGGL(ffm_pairs_lds_kernel<true>, dim3((unsigned)grid), dim3(64), lds, s, (const long long*)indptr,
-                       (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float4*)V, nfield,
-                       (float*)fx, skip_feat, (float4*)E, e_base);
-  else
-    hipLaunchKernelGGL(ffm_pairs_lds_kernel<false>, dim3((unsigned)grid), dim3(64), lds, s, (const long long*)indptr,
-                       (const int*)idx, (const float*)val, (const int*)fld, nrows, (const float4*)V, nfield,
-                       (float*)fx, skip_feat, (float4*)nullptr, 0LL);
+#define YTK_LDS(KE, BF)                                                                                   \
+  hipLaunchKernelGGL((ffm_pairs_lds_kernel<KE, BF>), dim3((unsigned)grid), dim3(64), lds, s,              \
+                     (const long long*)indptr, (const int*)idx, (const float*)val, (const int*)fld, nrows, \
+                     (const void*)V, nfield, (float*)fx, skip_feat, (void*)E, KE ? e_base : 0LL)
+  if (E && bf16) YTK_LDS(true, true);
+  else if (E) YTK_LDS(true, false);
+  else if (bf16) YTK_LDS(false, true);
+  else YTK_LDS(false, false);
+#undef YTK_LDS
   YTK_LAUNCH_CHECK();
 }
 

@@ -141,18 +141,40 @@ def test_cpu_step_is_synchronous_per_sample_sum(name, avg):
     torch.testing.assert_close(w, want, rtol=2e-4, atol=2e-6)
 
 
+def test_cpu_ffm_bf16_step_close_to_fp32():
+    """The CPU emulation of the FFM bf16 path (forward from the bf16 copy, bf16 pair terms) moves
+    the weights like the fp32 step up to bf16 rounding, and really rounds (not bitwise equal)."""
+    outs = []
+    for dt in ("fp32", "bf16"):
+        m = _model("ffm", nf=9, feats=320, pad=3)
+        o = _opt(m, dtype=dt)
+        w = m.w.clone()
+        o._sync_copy(w)
+        o._step(w, 0, 512, 0.2)
+        outs.append((w, m.w.clone()))
+    (w32, w0), (w16, _) = outs
+    d32, d16 = w32 - w0, w16 - w0
+    assert not torch.equal(d32, d16)
+    assert float((d16 - d32).norm() / d32.norm()) < 2e-2
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,dtype,uneven,pad", [("linear", "fp32", False, 0), ("fm", "fp32", False, 0),
                                                    ("fm", "bf16", False, 0), ("ffm", "fp32", False, 0),
-                                                   ("ffm", "fp32", False, 3), ("ffm", "fp32", True, 0),
+                                                   ("ffm", "fp32", False, 3), ("ffm", "bf16", False, 3),
+                                                   ("ffm", "fp32", True, 0),
                                                    ("fm", "fp32", True, 0)])
 @pytest.mark.parametrize("avg", ["feature", "none"])
 def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, pad, avg):
     """Three batches through the GPU column-ordered step vs the CPU synchronous step (fp32
     sums in different orders: rtol 1e-4; bf16: the forward reads the rounded copy on both).
     FFM fixed layout: pad 0 (V unaligned) takes ffm_sgd_grad_kernel, pad 3 (F % 4 == 0) the
-    forward-written pair terms + ffm_sgd_ecol_kernel."""
+    forward-written pair terms + ffm_sgd_ecol_kernel; FFM bf16 (pad 3) stages the bf16 copy and
+    writes bf16 pair terms -- the CPU step reads the same copy and rounds the same terms."""
     nf = 8  # the streamed FFM pair kernel needs >= 8 positions per row (ops/ffm._fixed_layout)
+    if name == "ffm" and dtype == "bf16":
+        nf = 9  # bf16 pair terms move slot pairs: rows of nf + 1 (bias) = 10 positions
+        pad = (-(nf * (320 // nf) + 1)) % 4  # V 16-B aligned: the pair-term path (pad 3 at nf = 8)
     mc = _model(name, nf=nf, feats=320, uneven=uneven, pad=pad)
     mg = _model(name, nf=nf, feats=320, dev="cuda", uneven=uneven, pad=pad)
     oc, og = _opt(mc, avg=avg, dtype=dtype), _opt(mg, avg=avg, dtype=dtype)
@@ -163,7 +185,9 @@ def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, pad, a
     batches = og._setup(bounds)
     if name == "ffm" and not uneven:
         assert all(bt.lay is not None for bt in batches) and og.Vt is None  # fixed-layout kernels ran
-        assert (og.E is not None) == (pad == 3)
+        assert (og.E is not None) == (pad == 3 or dtype == "bf16")
+        if dtype == "bf16":
+            assert og.Vb is not None and og.E is not None and og.E.dtype == torch.bfloat16
     for j, (b, e) in enumerate(bounds):
         oc._step(wc, b, e, 0.2)
         og._step(wg, b, e, 0.2, batches[j])
@@ -174,7 +198,7 @@ def test_gpu_column_step_matches_cpu_reference(cuda, name, dtype, uneven, pad, a
         torch.testing.assert_close(og.Vt, wg[F:].view(F, mg.nf, mg.kk).transpose(0, 1), rtol=0, atol=0)
     if og.Vb is not None:
         F = mg.F
-        torch.testing.assert_close(og.Vb, wg[F:].view(F, mg.kk).to(torch.bfloat16), rtol=0, atol=0)
+        torch.testing.assert_close(og.Vb, wg[F:].view(F, -1).to(torch.bfloat16), rtol=0, atol=0)
 
 
 @pytest.mark.gpu

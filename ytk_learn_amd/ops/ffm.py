@@ -69,7 +69,7 @@ def ffm_forward(indptr, idx, val, fld, V, nfield: int, k: int, out=None, cache=N
     if V.is_cuda and max_m and lds_forward_ok(max_m, nfield, k, V):
         check_cuda(indptr, idx, val, fld, V, out)
         hip().ffm_pairs_lds(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat),
-                            int(max_m), 0, 0, stream(V))
+                            int(max_m), 0, 0, 0, stream(V))
         return out
     if V.is_cuda:
         check_cuda(indptr, idx, val, fld, V, out)

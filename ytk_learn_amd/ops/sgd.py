@@ -158,29 +158,36 @@ def ffm_pair_sums(bt: SGDBatch, c: torch.Tensor, V: torch.Tensor, Vt: Optional[t
     return lat
 
 
-def pair_terms_elems(batches: List[SGDBatch], V: torch.Tensor, k: int) -> int:
-    """Floats of the pair-term buffer E when every batch takes the E path (fixed layout, k ==
-    4, V 16-B aligned, E within YTK_SGD_FFM_E_GB), else 0."""
+def pair_terms_elems(batches: List[SGDBatch], V: torch.Tensor, k: int, elem_bytes: int = 4) -> int:
+    """Elements of the pair-term buffer E when every batch takes the E path (fixed layout, k ==
+    4, V 16-B aligned, E within YTK_SGD_FFM_E_GB at ``elem_bytes`` per element), else 0."""
     if FFM_E_GB <= 0 or FFM_VT or k != 4 or V.data_ptr() % 16 or not batches:
         return 0
     if any(bt.lay is None for bt in batches):
         return 0
     m = batches[0].lay[1]
     n = max(bt.X.nnz for bt in batches) * m * 4
-    return n if n * 4 <= FFM_E_GB * (1 << 30) else 0
+    return n if n * elem_bytes <= FFM_E_GB * (1 << 30) else 0
 
 
 def ffm_forward_e(bt: SGDBatch, indptr, idx, val, fld, V: torch.Tensor, nfield: int, skip_feat: int,
-                  E: torch.Tensor) -> torch.Tensor:
-    """Pair sums of the batch rows (float32 [n]) + their pair terms into E (ffm_pairs_k4_kernel<true>)."""
+                  E: torch.Tensor, Vb: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Pair sums of the batch rows (float32 [n]) + their pair terms into E (ffm_pairs_k4_kernel<true>).
+    ``Vb`` (bf16 working copy of V; E is then bf16): the LDS-staged kernel reads it instead of V."""
     from .ffm import lds_forward_ok
     n = bt.e - bt.b
     out = torch.empty(n, dtype=torch.float32, device=V.device)
     check_cuda(indptr, idx, val, fld, V, E)
     m = int(bt.lay[1])
+    if Vb is not None:
+        if not (lds_forward_ok(m, nfield, 4, V) and E.dtype == torch.bfloat16):
+            raise RuntimeError("ffm sgd bf16: needs the LDS-staged pair forward (k = 4, rows of <= 64 entries)")
+        hip().ffm_pairs_lds(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(Vb), nfield, ptr(out), int(skip_feat),
+                            m, ptr(E), int(bt.o0), 1, stream(V))
+        return out
     if lds_forward_ok(m, nfield, 4, V):  # the row's latent rows staged in LDS (ffm_pairs_lds_kernel<true>)
         hip().ffm_pairs_lds(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat), m,
-                            ptr(E), int(bt.o0), stream(V))
+                            ptr(E), int(bt.o0), 0, stream(V))
         return out
     hip().ffm_pairs_fwd_e(ptr(indptr), ptr(idx), ptr(val), ptr(fld), n, ptr(V), nfield, ptr(out), int(skip_feat),
                           ptr(E), int(bt.o0), int(bt.lay[1]), stream(V))
@@ -199,9 +206,11 @@ def prepare_pair_terms(bt: SGDBatch):
 
 
 def ffm_step_e(bt: SGDBatch, c: torch.Tensor, E: torch.Tensor, w_lin: torch.Tensor, V: torch.Tensor, nfield: int,
-               k: int, lr: float, l2w: float, l2v: float, reg_skip: int, upd_w: bool, bias_latent: bool, avg: bool):
+               k: int, lr: float, l2w: float, l2v: float, reg_skip: int, upd_w: bool, bias_latent: bool, avg: bool,
+               Vb: Optional[torch.Tensor] = None):
     """ffm_sgd_ecol_kernel: the step of every single-chunk column; returns (lin, lat), the
-    multi-chunk columns' chunk partials for :func:`apply_step` (``multi=True``)."""
+    multi-chunk columns' chunk partials for :func:`apply_step` (``multi=True``). ``Vb``: E is
+    bf16 and the bf16 working copy of every updated latent slot is re-rounded."""
     Xb = bt.X
     lay_field, m = bt.lay
     nch = max(Xb.n_chunks, 1)
@@ -211,7 +220,8 @@ def ffm_step_e(bt: SGDBatch, c: torch.Tensor, E: torch.Tensor, w_lin: torch.Tens
     hip().ffm_sgd_ecol(ptr(Xb.chunk_bounds), ptr(Xb.chunk_end_b), Xb.n_chunks, ptr(Xb.csc_rows), ptr(Xb.csc_vals),
                        ptr(bt.perm), ptr(bt.chunk_fa), ptr(bt.chunk_col), ptr(bt.solo), ptr(E), m, ptr(lay_field),
                        ptr(c), ptr(lat), ptr(lin), ptr(w_lin), ptr(V), float(lr), float(l2w), float(l2v),
-                       int(reg_skip), 1 if upd_w else 0, 1 if bias_latent else 0, 1 if avg else 0, stream(c))
+                       int(reg_skip), 1 if upd_w else 0, 1 if bias_latent else 0, 1 if avg else 0,
+                       ptr(Vb) if Vb is not None else 0, stream(c))
     return lin, lat
 
 
@@ -220,10 +230,32 @@ def needs_transposed(batches: List[SGDBatch], V: torch.Tensor, k: int) -> bool:
     return FFM_VT or any(bt.lay is None for bt in batches) or k not in (4, 8)
 
 
+def _ffm_pair_grad_bf16(indptr, idx, x, fld, Vb: torch.Tensor, nfield: int, k: int, c, gV, skip_feat: int):
+    """gV[i_p, f_q] += c_r bf16(x_p x_q Vb[i_q, f_p]) over the ordered pairs p != q of every row --
+    the GPU bf16 path's pair terms (ffm_pairs_lds_kernel<true, true>) rounded where it rounds."""
+    n = int(indptr.shape[0] - 1)
+    lens = (indptr[1:] - indptr[:-1]).long()
+    rows = torch.repeat_interleave(torch.arange(n), lens)
+    nnz = rows.numel()
+    ent = torch.arange(nnz)
+    cnts = lens[rows]
+    e1 = torch.repeat_interleave(ent, cnts)
+    first = torch.cumsum(cnts, 0) - cnts
+    e2 = (indptr[rows].long() - indptr[0].long())[e1] + (torch.arange(e1.numel()) - torch.repeat_interleave(first, cnts))
+    ii, ff = idx.long(), fld.long()
+    keep = (e1 != e2) & (ii[e1] != skip_feat) & (ii[e2] != skip_feat)
+    e1, e2 = e1[keep], e2[keep]
+    V3 = Vb.float().view(-1, nfield, k)
+    t = ((x[e1] * x[e2])[:, None] * V3[ii[e2], ff[e1]]).to(torch.bfloat16).float()
+    G3 = gV.view(-1, nfield, k)
+    G3.index_put_((ii[e1], ff[e2]), c[rows[e1]][:, None] * t, accumulate=True)
+
+
 def ffm_step_cpu(indptr, idx, val, fld, w_lin, V, nfield: int, k: int, c, lr: float, l2w: float, l2v: float,
-                 reg_skip: int, upd_w: bool, bias_latent: bool, cnt=None, skip_feat: int = -1):
+                 reg_skip: int, upd_w: bool, bias_latent: bool, cnt=None, skip_feat: int = -1, Vb=None):
     """CPU reference of one synchronous FFM batch step (linear part + pairs + l2 decay), all
-    gradients at the batch's starting weights; ``cnt`` (int32 [F]): per-feature mean."""
+    gradients at the batch's starting weights; ``cnt`` (int32 [F]): per-feature mean; ``Vb``
+    (bf16 copy of V): the pair terms come from it, rounded to bf16 (the GPU bf16 path)."""
     from .ffm import ffm_backward
     n = int(indptr.shape[0] - 1)
     b0, e0 = int(indptr[0]), int(indptr[-1])
@@ -244,7 +276,10 @@ def ffm_step_cpu(indptr, idx, val, fld, w_lin, V, nfield: int, k: int, c, lr: fl
     if V is not None and nfield * k > 0:
         gV = torch.zeros_like(V)
         ip_rel = indptr - b0
-        ffm_backward(ip_rel, idx[b0:e0], x, fld[b0:e0], V, nfield, k, c, gV, skip_feat=skip_feat)
+        if Vb is not None:
+            _ffm_pair_grad_bf16(ip_rel, idx[b0:e0], x, fld[b0:e0], Vb, nfield, k, c, gV, skip_feat)
+        else:
+            ffm_backward(ip_rel, idx[b0:e0], x, fld[b0:e0], V, nfield, k, c, gV, skip_feat=skip_feat)
         G2 = gV.view(F, -1)
         V2 = V.view(F, -1)
         G2 += torch.where(is_bias[:, None], torch.zeros(()), (ent * l2v)[:, None] * V2)

@@ -24,9 +24,13 @@ is in every row) take one bounded step per batch. ``none`` applies the sum, whic
 of thousands of rows diverges on hot features. FFM: the count of V[i, f] is the entries of
 feature i in the batch (not only those whose row also holds a field-f feature), so for rows
 without every field such latents take a smaller step than a per-(feature, field) mean.
-``optimization.sgd.dtype = bf16`` (FM): the row pass gathers the latents from a bf16 working
+``optimization.sgd.dtype = bf16``: FM -- the row pass gathers the latents from a bf16 working
 copy (half the bytes of its dominant V-row gathers); the fp32 master takes the updates and
-``sgd_apply`` re-rounds the copy of every touched row.
+``sgd_apply`` re-rounds the copy of every touched row. FFM (pair-term path: k = 4, fixed-layout
+rows of <= 64 entries) -- the LDS-staged pair forward stages each row's latent rows from the
+bf16 copy (half the bytes of its whole-row reads) and writes the pair terms E as bf16 (half the
+bytes the chunk sums read back); dot products, sums and the fp32 master stay fp32, and both
+update kernels re-round the copy of every slot they change.
 
 Multi-GPU: every rank runs SGD on its shard; weights are averaged across ranks with one
 RCCL all-reduce every ``sync_every`` batches (0 = once per epoch) -- local SGD / model
@@ -59,7 +63,8 @@ class SGDParams:
     epochs: int = 10
     sync_every: int = 0               # batches between cross-rank weight averaging; 0 = per epoch
     seed: int = 1
-    dtype: str = "fp32"               # "bf16": FM latents read from a bf16 working copy (fp32 master)
+    dtype: str = "fp32"               # "bf16": latents read from a bf16 working copy (fp32 master);
+    #                                   FFM: the pair terms are bf16 too
     average: str = "feature"          # "feature": a weight's step is the mean over the batch rows
     #                                   containing its feature; "none": the sum (per-sample steps)
 
@@ -118,6 +123,9 @@ class SGDOptimizer:
         self.Vb = None
         if sp.dtype == "bf16" and model.name == "fm" and self.kk > 0:
             self.Vb = torch.empty((F, self.kk), dtype=torch.bfloat16, device=dev)
+        if sp.dtype == "bf16" and model.name == "ffm" and dev.type != "cuda":
+            # the CPU step's bf16 emulation of the GPU pair-term path (GPU: allocated by _setup)
+            self.Vb = torch.empty((F, model.nf * model.kk), dtype=torch.bfloat16, device=dev)
         # FFM on the GPU: fixed-layout batches read the model's V directly (ffm_sgd_grad_kernel);
         # the general pair-gradient kernel reads a field-major copy ([nfield][F][k]) that
         # sgd_apply keeps current -- allocated only when some batch needs it (_setup)
@@ -133,9 +141,19 @@ class SGDOptimizer:
         if self._batches is None and X.device.type == "cuda":
             fld = m.data.train.fields if self.ffm else None
             self._batches = sgd_ops.build_batches(X, bounds, fld, m.nf if self.ffm else 0, getattr(m, "_skip", -1))
-            ne = sgd_ops.pair_terms_elems(self._batches, m.w[m.F:], m.kk) if self.ffm else 0
+            bf = self.ffm and self.sp.dtype == "bf16"
+            ne = sgd_ops.pair_terms_elems(self._batches, m.w[m.F:], m.kk, 2 if bf else 4) if self.ffm else 0
+            if bf:
+                from ..ops.ffm import lds_forward_ok
+                mm = self._batches[0].lay[1] if (ne and self._batches[0].lay is not None) else 0
+                if ne and lds_forward_ok(mm, m.nf, m.kk, m.w[m.F:]) and mm % 2 == 0 and m.nf % 2 == 0:
+                    self.Vb = m.w[m.F:].view(m.F, -1).to(torch.bfloat16)  # run() re-syncs it from w
+                else:
+                    self.log.info("[sgd] dtype = bf16 needs the ffm pair-term path (k = 4, fixed-layout rows of "
+                                  "<= 64 entries, even row length and field count): running fp32")
             if ne:
-                self.E = torch.empty(ne, dtype=torch.float32, device=X.device)
+                self.E = torch.empty(ne, dtype=torch.bfloat16 if self.Vb is not None else torch.float32,
+                                     device=X.device)
                 for bt in self._batches:
                     sgd_ops.prepare_pair_terms(bt)
             else:
@@ -174,7 +192,8 @@ class SGDOptimizer:
         z1 = None
         use_e = self.E is not None and getattr(m, "need_second", True)
         if use_e:
-            z1 = sgd_ops.ffm_forward_e(bt, sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m._skip, self.E)
+            z1 = sgd_ops.ffm_forward_e(bt, sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m._skip, self.E,
+                                       Vb=self.Vb)
         elif self.ffm:
             z1 = ffm_forward(sl.indptr, X.indices, X.values, d.fields, w[F:], m.nf, m.kk, skip_feat=m._skip)
         c = self._coef(fx, d.y[b:e, 0], d.weight[b:e], z1)
@@ -182,9 +201,9 @@ class SGDOptimizer:
         bias_latent = bool(getattr(m, "bias_latent", False))
         if use_e:  # single-chunk columns step inside ffm_sgd_ecol_kernel, the rest in sgd_apply
             lin, lat = sgd_ops.ffm_step_e(bt, c, self.E, w_lin, w[F:], m.nf, m.kk, lr, self.l2w, self.l2v, reg_skip,
-                                          upd_w, bias_latent, avg)
+                                          upd_w, bias_latent, avg, Vb=self.Vb)
             sgd_ops.apply_step(bt, lin, lat, m.stride, w_lin, w[F:], m.kk, lr, self.l2w, self.l2v, reg_skip, upd_w,
-                               bias_latent, avg, multi=True)
+                               bias_latent, avg, Vb=self.Vb, multi=True)
             return
         part = sgd_ops.column_sums(bt, c, S if kk > 0 else None, kk)
         if self.ffm and getattr(m, "need_second", True):
@@ -218,7 +237,8 @@ class SGDOptimizer:
             fx = fx + 0.5 * (S.double() ** 2 - Q.double()).sum(1)
         sl_ip = X.indptr[b:e + 1]
         if self.ffm:
-            fx = fx + ffm_forward(sl_ip - o0, X.indices[o0:o1], X.values[o0:o1], d.fields[o0:o1], w[F:], m.nf,
+            Vf = self.Vb.float().view(-1) if self.Vb is not None else w[F:]
+            fx = fx + ffm_forward(sl_ip - o0, X.indices[o0:o1], X.values[o0:o1], d.fields[o0:o1], Vf, m.nf,
                                   m.kk, skip_feat=m._skip).double()
         y = d.y[b:e, 0].double()
         c = (d.weight[b:e].double() * m.loss.grad(fx, y)).float().contiguous()
@@ -229,7 +249,9 @@ class SGDOptimizer:
             sgd_ops.ffm_step_cpu(sl_ip, X.indices, X.values, d.fields, w_lin,
                                  w[F:] if getattr(m, "need_second", True) else None, m.nf, m.kk, c, lr, self.l2w,
                                  self.l2v, reg_skip, upd_w, bool(getattr(m, "bias_latent", False)), cnt=cnt,
-                                 skip_feat=m._skip)
+                                 skip_feat=m._skip, Vb=self.Vb)
+            if self.Vb is not None:  # the GPU kernels re-round every slot they change
+                self.Vb.copy_(w[F:].view(F, -1))
         else:
             V = w[F:].view(F, m.kk) if (m.name == "fm" and m.kk > 0) else None
             fm_sgd_update(sl_ip, X.indices, X.values, w_lin, V, S, c, lr, self.l2w, self.l2v, reg_skip, upd_w,
@@ -246,7 +268,7 @@ class SGDOptimizer:
     def _sync_copy(self, w):
         F = self.m.F
         if self.Vb is not None:
-            self.Vb.copy_(w[F:].view(F, self.m.kk))
+            self.Vb.copy_(w[F:].view(F, -1))
         if self.Vt is not None:
             self.Vt.copy_(w[F:].view(F, self.m.nf, self.m.kk).transpose(0, 1))
 
