@@ -126,7 +126,7 @@ void ytk_lv_split_plan(const uintptr_t*, const int*, const float*, uintptr_t, in
 int ytk_split_node_grouped(uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, int, uintptr_t, float, float,
                            float, float, uintptr_t, uintptr_t, int, uintptr_t);
 void ytk_lv_partition_children(const uintptr_t*, const int*, const float*, uintptr_t, long long, uintptr_t, uintptr_t,
-                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, int);
+                               uintptr_t, uintptr_t, int, int, int, int, int, uintptr_t, int, int, uintptr_t);
 // gbdt_leafwise.hip
 int ytk_lw_create(const uintptr_t*, const int*, const float*);
 void ytk_lw_set_lr(int, float);
@@ -134,7 +134,8 @@ void ytk_lw_set_batch_cap(int, int);
 long long ytk_lw_ws_bytes(int, int);
 uintptr_t ytk_host_device_ptr(uintptr_t);
 void ytk_lw_step(int, int, uintptr_t);
-void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+void ytk_lw_partition(int, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t,
+                      uintptr_t);
 void ytk_lw_zero_slots(uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, int, int, uintptr_t);
 void ytk_lw_subtree(int, uintptr_t, long long, uintptr_t, long long, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                     uintptr_t, uintptr_t, int, int, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t);
@@ -277,15 +278,16 @@ PYBIND11_MODULE(_ytk_hip, m) {
                                      const std::vector<float>& fp, uintptr_t binsT, long long ncol, uintptr_t rows,
                                      uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                      int count_only, int a0, int a1, int maxp, uintptr_t stream, int bin_bytes,
-                                     int gh_rows) {
+                                     int gh_rows, uintptr_t chunk_io) {
     if (ptrs.size() != 27 || ip.size() != 9 || fp.size() != 6)
       throw std::invalid_argument("lv_partition_children: bad argument sizes");
     ytk_lv_partition_children(ptrs.data(), ip.data(), fp.data(), binsT, ncol, rows, ghp, rows_out, gh_out,
-                              max_blocks, count_only, a0, a1, maxp, stream, bin_bytes, gh_rows);
+                              max_blocks, count_only, a0, a1, maxp, stream, bin_bytes, gh_rows, chunk_io);
   }, pybind11::arg("ptrs"), pybind11::arg("ip"), pybind11::arg("fp"), pybind11::arg("binsT"), pybind11::arg("ncol"),
      pybind11::arg("rows"), pybind11::arg("ghp"), pybind11::arg("rows_out"), pybind11::arg("gh_out"),
      pybind11::arg("max_blocks"), pybind11::arg("count_only"), pybind11::arg("a0"), pybind11::arg("a1"),
-     pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1, pybind11::arg("gh_rows") = 0);
+     pybind11::arg("maxp"), pybind11::arg("stream"), pybind11::arg("bin_bytes") = 1, pybind11::arg("gh_rows") = 0,
+     pybind11::arg("chunk_io") = 0);
   m.def("split_node_grouped", &ytk_split_node_grouped);
   m.def("hist_fx_stage", &ytk_hist_fx_stage);
   m.def("lv_reduce_split", [](const std::vector<uintptr_t>& ptrs, uintptr_t staging, uintptr_t hist, int B, int F,
@@ -314,7 +316,9 @@ PYBIND11_MODULE(_ytk_hip, m) {
   m.def("lw_ws_bytes", &ytk_lw_ws_bytes);
   m.def("host_device_ptr", &ytk_host_device_ptr);
   m.def("lw_step", &ytk_lw_step);
-  m.def("lw_partition", &ytk_lw_partition);
+  m.def("lw_partition", &ytk_lw_partition, pybind11::arg("h"), pybind11::arg("binsT"), pybind11::arg("ncol"),
+        pybind11::arg("rows"), pybind11::arg("ghp"), pybind11::arg("rows_out"), pybind11::arg("gh_out"),
+        pybind11::arg("max_blocks"), pybind11::arg("stream"), pybind11::arg("chunk_io") = 0);
   m.def("lw_zero_slots", &ytk_lw_zero_slots);
   m.def("lw_subtree", &ytk_lw_subtree);
   m.def("hist_fx_staged_dev", &ytk_hist_fx_staged_dev);

@@ -1117,17 +1117,19 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
 // kPrefetch: the software-pipelined body (partition_atomic_body_pf).
-template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t, bool kPfCol = false>
+// kMode 2 (the first batches: one or two splits of thousands of chunks): the chunks scatter at
+// the reservations lw_part_count_kernel + lw_part_scan_kernel computed (partition_atomic_body_pf)
+template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t, bool kPfCol = false, int kMode = 0>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
 void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
-                                                                   float2* gh_out) {
+                                                                   float2* gh_out, unsigned long long* chunk_io) {
   if constexpr (kPrefetch)
-    partition_atomic_body_pf<BinT, kAtomSub, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
+    partition_atomic_body_pf<BinT, kAtomSub, kPfGh, kPfCol, kMode>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
                                                     b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                      b.cursor, b.part_shift, kCurStride);
+                                      b.cursor, b.part_shift, kCurStride, 0, chunk_io);
   else
     partition_atomic_body<BinT, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
@@ -1138,6 +1140,23 @@ void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
   // the XCD's L2 on MI355X and doubled this kernel's time.)
   if (!last_block_done(b.cursor + (size_t)p.max_leaf * kCurStride)) return;
   lw_children_body(p, b);
+}
+
+// kMode 1 of the partition body over the batch's chunks: (right << 32) | left rows per chunk
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void lw_part_count_kernel(LwBufs b, const uint8_t* binsT, long long ncol, const int* rows,
+                          unsigned long long* chunk_io) {
+  if (b.st[LW_DONE]) return;
+  partition_atomic_body_pf<uint8_t, kAtomSub, false, true, 1>(binsT, ncol, rows, nullptr, nullptr, nullptr, b.part_first,
+                                                              b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.part_feat,
+                                                              b.part_thr, b.part_begin, b.part_cnt, b.cursor,
+                                                              b.part_shift, kCurStride, 0, chunk_io);
+}
+
+// the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
+__global__ __launch_bounds__(kChunkScanThreads) void lw_part_scan_kernel(LwBufs b, unsigned long long* chunk_io) {
+  if (b.st[LW_DONE]) return;
+  part_chunk_scan_body(chunk_io, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.cursor, kCurStride);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1721,7 +1740,10 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 // partition of the current batch (+ children planning in the last block); rows == 0:
 // identity permutation (the root batch of an unsampled tree)
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
-                      uintptr_t gh_out, int max_blocks, uintptr_t stream) {
+                      uintptr_t gh_out, int max_blocks, uintptr_t stream, uintptr_t chunk_io) {
+  // chunk_io (optional, >= max_blocks u64; batches of <= kChunkScanMaxSplits splits): count
+  // pass + one-block scan instead of the split cursor atomics (the root batch's chunks all
+  // reserve on one cursor line)
   const LwEngine& e = g_lw.at(h);
   LwParams pp = e.p;  // YTK_PLAN_FAST=0: the children planning's general path (read per launch)
   {
@@ -1732,7 +1754,7 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
     const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint16_t>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint16_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
     YTK_LAUNCH_CHECK();
     return;
   }
@@ -1742,22 +1764,34 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
+  if (chunk_io && prefetch && ghp) {
+    unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(lw_part_count_kernel, grid, dim3(kPartThreads), 0, s, e.b, (const uint8_t*)binsT, ncol,
+                       (const int*)rows, cio);
+    hipLaunchKernelGGL(lw_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, e.b, cio);
+    hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 2>), grid, dim3(kPartThreads), 0, s, pp, e.b,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                       (float2*)gh_out, cio);
+    YTK_LAUNCH_CHECK();
+    return;
+  }
   if (prefetch && pf && pf[0] == '3' && ghp)  // + the next chunk's split-feature bytes
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
   else if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
     hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
   else if (prefetch)
     hipLaunchKernelGGL(lw_partition_kernel<true>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                       (float2*)gh_out);
+                       (float2*)gh_out, nullptr);
   else
     hipLaunchKernelGGL(lw_partition_kernel<false>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                       (float2*)gh_out);
+                       (float2*)gh_out, nullptr);
   YTK_LAUNCH_CHECK();
 }
 

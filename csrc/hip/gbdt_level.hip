@@ -737,23 +737,44 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
+// kMode 2 (levels of a few splits, the root's above all): the chunks scatter at the
+// reservations lv_part_count_kernel + lv_part_scan_kernel computed (partition_atomic_body_pf).
 template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, bool kPfCol = false,
-          typename BinT = uint8_t>
+          typename BinT = uint8_t, int kMode = 0>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
 void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
-                                  int dgap, int use_loc, int fused, int maxp, int gh_rows) {
+                                  int dgap, int use_loc, int fused, int maxp, int gh_rows,
+                                  unsigned long long* chunk_io) {
   if constexpr (kScatter && kPrefetch)
-    partition_atomic_body_pf<BinT, kS, kPfGh, kPfCol>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
+    partition_atomic_body_pf<BinT, kS, kPfGh, kPfCol, kMode>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride,
-                                          gh_rows);
+                                          gh_rows, chunk_io);
   else
     partition_atomic_body<BinT, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                              b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                              reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
   lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
+}
+
+// kMode 1 of the partition body: per-chunk (right << 32) | left counts into chunk_io
+template <int kS, bool kPfCol>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void lv_part_count_kernel(LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
+                          unsigned long long* chunk_io) {
+  partition_atomic_body_pf<uint8_t, kS, false, kPfCol, 1>(binsT, ncol, rows, nullptr, nullptr, nullptr, b.part_first,
+                                                          b.st + ST_N_SPLIT, b.st + ST_N_PART, b.part_feat, b.part_thr,
+                                                          b.part_begin, b.part_cnt,
+                                                          reinterpret_cast<unsigned long long*>(b.left_loc), nullptr,
+                                                          kCurStride, 0, chunk_io);
+}
+
+// the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
+__global__ __launch_bounds__(kChunkScanThreads) void lv_part_scan_kernel(LvBufs b, unsigned long long* chunk_io) {
+  part_chunk_scan_body(chunk_io, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART,
+                       reinterpret_cast<unsigned long long*>(b.left_loc), kCurStride);
 }
 
 // One GPU: the level's split search (one kNodeThreads block per node item, the node-
@@ -1213,7 +1234,9 @@ void ytk_lv_step(int which, const uintptr_t* ptrs, const int* ip, const float* f
 void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float* fp, uintptr_t binsT, long long ncol,
                                uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                int count_only, int arg0, int arg1, int maxp, uintptr_t stream, int bin_bytes,
-                               int gh_rows) {
+                               int gh_rows, uintptr_t chunk_io) {
+  // chunk_io (optional, >= max_blocks u64; for levels of <= kChunkScanMaxSplits splits): the
+  // chunks reserve through a count pass + one-block scan instead of the split cursor atomics
   // gh_rows: ghp is row-indexed (pipelined bodies only: the unpipelined ones read (g, h) by
   // position)
   LvParams p = make_params(ip, fp);
@@ -1231,7 +1254,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, kAtomSub, SC, SC, false, uint16_t>), grid,        \
                      dim3(kPartThreads), 0, s, p, b, (const uint16_t*)binsT, ncol, (const int*)rows,        \
                      (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
-                     gh_rows)
+                     gh_rows, nullptr)
     if (maxp <= 64) {
       if (count_only) YTK_LVPC16(false, 64); else YTK_LVPC16(true, 64);
     } else if (maxp <= 512) {
@@ -1261,10 +1284,28 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   const bool pf_col = !pf || pf[0] == '3';
   if (gh_rows && (!prefetch || count_only))
     throw std::invalid_argument("lv_partition_children: row-indexed (g, h) needs the pipelined scatter body");
+  if (chunk_io && !count_only && prefetch && pf_col && !wide && !narrow) {
+    // count pass (same chunks, same split-feature gathers, no scatter) -> scan -> scatter
+    unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
+    hipLaunchKernelGGL((lv_part_count_kernel<kAtomSub, true>), grid, dim3(kPartThreads), 0, s, b, (const uint8_t*)binsT,
+                       ncol, (const int*)rows, cio);
+    hipLaunchKernelGGL(lv_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, b, cio);
+#define YTK_LVPC_SCAN(KP)                                                                                       \
+  hipLaunchKernelGGL((lv_partition_children_kernel<true, KP, kAtomSub, true, true, true, uint8_t, 2>), grid,    \
+                     dim3(kPartThreads), 0, s, p, b, (const uint8_t*)binsT, ncol, (const int*)rows,             \
+                     (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
+                     gh_rows, cio)
+    if (maxp <= 64) YTK_LVPC_SCAN(64);
+    else if (maxp <= 512) YTK_LVPC_SCAN(512);
+    else YTK_LVPC_SCAN(kMaxPend);
+#undef YTK_LVPC_SCAN
+    YTK_LAUNCH_CHECK();
+    return;
+  }
 #define YTK_LVPC4(SC, KP, S, PF, PG, PC)                                                                      \
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG, PC>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
-                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, gh_rows)
+                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, gh_rows, nullptr)
 #define YTK_LVPC2(SC, KP, S, PF)                                                  \
   do {                                                                            \
     if ((PF) && pf_col) YTK_LVPC4(SC, KP, S, PF, true, true);                     \

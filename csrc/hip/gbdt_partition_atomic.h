@@ -198,14 +198,22 @@ __device__ __forceinline__ void partition_atomic_body(
 // ranks, reserves and scatters the current one, so the row-id round trip of chunk i + 1
 // overlaps the ballot / cursor-atomic / scatter phases of chunk i. Same output as the
 // unpipelined body (same reservation per chunk, same placement).
-template <typename BinT, int S = kAtomSub, bool kGh = false, bool kCol = false>
+// kMode (splits with thousands of chunks each -- the root level: every one of Higgs' 5127
+// chunks reserved on ONE cursor line, ~12 ns apiece serialised, 62 of the level's 77 us):
+//   0: reserve with the cursor atomic;
+//   1: count only -- chunk_io[chunk] = (right rows << 32) | left rows, nothing scattered;
+//   2: scatter at chunk_io[chunk], the reservation a scan of the mode-1 counts computed
+//      (part_chunk_scan_kernel: the same (right, left) prefix an atomic would have returned
+//      in chunk order; the split cursors hold the totals).
+template <typename BinT, int S = kAtomSub, bool kGh = false, bool kCol = false, int kMode = 0>
 __device__ __forceinline__ void partition_atomic_body_pf(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
     const float2* __restrict__ ghp, int* __restrict__ rows_out, float2* __restrict__ gh_out,
     const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
-    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs, int gh_rows = 0) {
+    unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs, int gh_rows = 0,
+    unsigned long long* __restrict__ chunk_io = nullptr) {
   // ghp == nullptr: (g, h) stays row-indexed (leaf-wise engine); out_shift as in
   // partition_atomic_body (children into the other half of a 2N ping-pong buffer).
   // gh_rows: ghp is indexed by ROW id (the level engine's first gathered level), so the next
@@ -259,7 +267,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int pos = c.beg + j * kPartThreads + tid;
-      g[j] = (pos < c.end && ghp) ? ghp[gh_rows ? r[j] : pos] : make_float2(0.f, 0.f);
+      g[j] = (kMode != 1 && pos < c.end && ghp) ? ghp[gh_rows ? r[j] : pos] : make_float2(0.f, 0.f);
     }
   };
   int bid = (int)blockIdx.x;
@@ -327,7 +335,10 @@ __device__ __forceinline__ void partition_atomic_body_pf(
       const int tl_all = __shfl(incl, S * NW - 1, kWave);
       if (l == 0) {
         const int tv = c.end - c.beg;
-        s_base = atomicAdd(&cursor[(size_t)c.si * cs], ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all);
+        const unsigned long long cnt = ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all;
+        if constexpr (kMode == 1) chunk_io[bid] = cnt;
+        else if constexpr (kMode == 2) s_base = chunk_io[bid];
+        else s_base = atomicAdd(&cursor[(size_t)c.si * cs], cnt);
         s_tl = tl_all;
       }
     }
@@ -338,7 +349,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     if constexpr (kGh) {
       if (gh_rows && more) load_gh(cn, rn, gn);
     }
-    {
+    if constexpr (kMode != 1) {
       const int tl = s_tl;
       const int tv = c.end - c.beg;
       const unsigned long long base = s_base;
@@ -369,6 +380,78 @@ __device__ __forceinline__ void partition_atomic_body_pf(
 #pragma unroll
       for (int j = 0; j < S; ++j) g[j] = gn[j];
     }
+  }
+}
+
+// One block: exclusive scan of the mode-1 chunk counts within each split (chunks of split si:
+// [first_blk[si], first_blk[si + 1])), in chunk order -> chunk_io[chunk] = (right rows before
+// it << 32) | left rows before it; cursor[si * cs] = the split's (right << 32) | left totals
+// (what the atomic mode leaves there). One pass: each thread scans a contiguous run of chunks
+// (left and right rows as two packed 32-bit sums in one u64: neither half overflows), the run
+// totals are scanned across the block, and every chunk's global prefix is rebased to its
+// split's first chunk.
+constexpr int kChunkScanThreads = 1024;
+constexpr int kChunkScanMaxSplits = 256;  // the caller's levels (a few splits each) stay below
+__device__ __forceinline__ void part_chunk_scan_body(unsigned long long* __restrict__ chunk_io,
+                                                     const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
+                                                     const int* __restrict__ nblocks_dev,
+                                                     unsigned long long* __restrict__ cursor, int cs) {
+  constexpr int NW = kChunkScanThreads / kWave;
+  constexpr int kRun = 16;  // chunks per thread held in registers (16K chunks per pass)
+  __shared__ unsigned long long s_w[NW + 1];
+  __shared__ unsigned long long s_sb[kChunkScanMaxSplits + 1];
+  __shared__ int s_sf[kChunkScanMaxSplits + 1];
+  const int nblocks = *nblocks_dev, nsplit = *nsplit_dev;
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+  for (int si = tid; si < nsplit; si += kChunkScanThreads) s_sf[si] = first_blk[si];
+  if (tid == 0) s_sf[nsplit] = nblocks;
+  unsigned long long carry = 0ull;  // packed (right, left) rows of the chunks before this pass
+  for (int base = 0; base < nblocks; base += kChunkScanThreads * kRun) {
+    const int i0 = base + tid * kRun;
+    unsigned long long v[kRun], run = 0ull;
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      v[k] = i0 + k < nblocks ? chunk_io[i0 + k] : 0ull;
+      run += v[k];
+    }
+    unsigned long long inc = run;  // inclusive wave scan of the runs
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const unsigned long long u = __shfl_up(inc, off, kWave);
+      if (l >= off) inc += u;
+    }
+    if (l == kWave - 1) s_w[wid] = inc;
+    __syncthreads();
+    unsigned long long pre = carry;
+    for (int w = 0; w < wid; ++w) pre += s_w[w];
+    pre += inc - run;  // exclusive prefix of this thread's run
+    unsigned long long tot = carry;
+    for (int w = 0; w < NW; ++w) tot += s_w[w];
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      if (i0 + k < nblocks) chunk_io[i0 + k] = pre;
+      pre += v[k];
+    }
+    carry = tot;
+    __syncthreads();  // s_w is rewritten by the next pass
+  }
+  __syncthreads();  // every global prefix is stored
+  // per split: the prefix at its first chunk (the rebase value) and its totals (the prefix at
+  // the next split's first chunk, the grand totals for the last)
+  for (int si = tid; si <= nsplit; si += kChunkScanThreads) {
+    const int f0 = s_sf[si];
+    s_sb[si] = f0 < nblocks ? chunk_io[f0] : carry;
+  }
+  __syncthreads();  // every rebase value is read before any chunk is rewritten
+  for (int si = tid; si < nsplit; si += kChunkScanThreads)
+    cursor[(size_t)si * cs] = s_sb[si + 1] - s_sb[si];  // both halves: no borrow (prefixes grow)
+  for (int i = tid; i < nblocks; i += kChunkScanThreads) {
+    int lo = 0, hi = nsplit - 1;  // the chunk's split: the last with first_blk <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_sf[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    chunk_io[i] -= s_sb[lo];
   }
 }
 

@@ -161,7 +161,9 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_FUSE_REDUCE_SPLIT": "1"}, {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "1"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "8"},
-                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "0"}])
+                                 {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "0"},
+                                 {"YTK_PART_SCAN_LEVELS": "0"}, {"YTK_PART_SCAN_LEVELS": "3"},
+                                 {"YTK_PART_SCAN_LEVELS": "8"}, {"YTK_PART_SCAN_LEVELS": "2", "YTK_PART_PREFETCH": "2"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""
@@ -309,6 +311,25 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
         tr.train()
         res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
     assert res[0] == res[1] == res[2] == res[3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sample", [1.0, 0.7])
+def test_device_leafwise_part_scan_identical(monkeypatch, sample):
+    """The first leaf-wise batches reserve their partition chunks by a count pass + scan
+    (YTK_LW_PART_SCAN batches; 0: the cursor atomics everywhere) -- the same trees."""
+    res = []
+    for n in ("0", "2", "8"):
+        monkeypatch.setenv("YTK_LW_PART_SCAN", n)
+        p = _params("loss", rounds=3)
+        p.tree.max_leaf_cnt = 63
+        p.tree.instance_sample_rate = sample
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(60000, 21, "cuda"), _data(6000, 22, "cuda"))
+        tr.train()
+        assert tr.builder.PART_SCAN == int(n)
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1] == res[2]
 
 
 @pytest.mark.gpu

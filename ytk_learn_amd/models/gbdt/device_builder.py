@@ -342,6 +342,14 @@ class DeviceLevelBuilder:
         self.ghp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
         self.gh_tmp = torch.empty((self.N, 2), dtype=torch.float32, device=dev)
         self.flags = torch.empty(self.N, dtype=torch.uint8, device=dev)
+        # levels [0, PART_SCAN_LEVELS) of the fused partition reserve their chunks through a
+        # count pass + one-block scan instead of the split cursor atomics (the root level's
+        # 5127 Higgs chunks on ONE cursor line serialise ~62 us): root partition 77 -> 30 us,
+        # 1.248 -> 1.219 / 1.215 / 1.219 ms per tree with 1 / 2 / 3 levels
+        # (profiles/r6/part_scan/); YTK_PART_SCAN_LEVELS=0: off
+        self.part_scan_levels = min(int(os.environ.get("YTK_PART_SCAN_LEVELS", "2")), 8)
+        self.chunk_io = (torch.zeros(self.N // 2048 + self.maxp + 2, dtype=torch.int64, device=dev)
+                         if self.part_scan_levels > 0 else None)
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)
         self.gp = p.gain_params()
@@ -747,11 +755,12 @@ class DeviceLevelBuilder:
             # the last level, whose counts need their own all-reduce before the planning
             fused_part = self.fuse_part_children and not (dist and last)
             if fused_part:
+                scan = self.chunk_io is not None and d < self.part_scan_levels and bb == 1 and not last
                 h.lv_partition_children(ptrs, ip, fp, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in,
                                         ptr(self.rows_tmp), ptr(self.gh_tmp) if gh_in else 0, npart,
                                         1 if last else 0, base,
                                         half | (ncs << 14) | ((1 if fused else 0) << 29) | (1 << 30),
-                                        self.maxp, s, bb, part_gh_rows)
+                                        self.maxp, s, bb, part_gh_rows, ptr(self.chunk_io) if scan else 0)
                 tm.mark("partition")
             # the flag kernel also accumulates the per-split left totals into left_loc
             elif self.part_atomic:

@@ -153,6 +153,9 @@ class DeviceLeafBuilder:
         # partition 1164 -> 1057 us, histograms 678 -> 764 us; 500 trees 3.99 -> 4.05 ms,
         # profiles/r5/leaf_gh_rows_*)
         self.gh_rows = os.environ.get("YTK_LW_GH_ROWS", "0") == "1" and not self.wide
+        # first batches (root: one split, then <= 2) reserve partition chunks by count + scan
+        self.PART_SCAN = min(int(os.environ.get("YTK_LW_PART_SCAN", "2")), 8)
+        self.chunk_io = torch.zeros(N // PART_CHUNK + ml + 2, dtype=torch.int64, device=dev)
         self._ghr = 0  # the tree's row-indexed (g, h) (build)
         self.gh2 = (torch.empty((2 * N, 2), dtype=torch.float32, device=dev) if not self.gh_rows
                     else torch.empty((1, 2), dtype=torch.float32, device=dev))
@@ -306,14 +309,17 @@ class DeviceLeafBuilder:
         self._hist(h, rows_ptr, gh_ptr, s)
         self._split(h, fmask, f0, s)
 
-    def _part(self, h, hd, rows_in, gh_in, s):
-        """lw_partition of the current batch into rows2 (+ gh2 unless (g, h) is row-indexed)."""
+    def _part(self, h, hd, rows_in, gh_in, s, it=-1):
+        """lw_partition of the current batch into rows2 (+ gh2 unless (g, h) is row-indexed).
+        Batches it < PART_SCAN (one or two splits, thousands of chunks each) reserve their
+        chunks through a count pass + scan instead of the split cursor atomics."""
         if self._ghr:
             h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, 0, ptr(self.rows2), 0,
                            self.max_pblocks, s)
         else:
+            scan = 0 <= it < self.PART_SCAN and not self.wide
             h.lw_partition(hd, ptr(self.binsT), self.binsT.shape[1], rows_in, gh_in, ptr(self.rows2), ptr(self.gh2),
-                           self.max_pblocks, s)
+                           self.max_pblocks, s, ptr(self.chunk_io) if scan else 0)
 
     def _hist(self, h, rows_ptr, gh_ptr, s):
         st = ptr(self.st)
@@ -493,7 +499,7 @@ class DeviceLeafBuilder:
         t_wait = None
         while True:
             self._batch(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2),
-                        fmask, f0, s)
+                        fmask, f0, s, it)
             it += 1
             if it > 4 * self.max_leaf + 8:
                 raise RuntimeError("device leaf-wise builder did not terminate")
@@ -542,7 +548,7 @@ class DeviceLeafBuilder:
             kc = self._rccl_cap(it)
             h.lw_set_batch_cap(hd, kc)
             h.lw_step(hd, 1, s)
-            self._part(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2), s)
+            self._part(h, hd, rows0 if it == 0 else ptr(self.rows2), gh0 if it == 0 else ptr(self.gh2), s, it)
             self._hist(h, ptr(self.rows2), ptr(self.gh2), s)
             if self.owner:
                 self._owner_sync(h, hd, s, kcap=kc)
@@ -658,14 +664,14 @@ class DeviceLeafBuilder:
             out[f"plan_select_{n}_us"] = round(float(v[i]) / 100.0, 1)
         return out
 
-    def _batch(self, h, hd, rows_in, gh_in, fmask, f0, s):
+    def _batch(self, h, hd, rows_in, gh_in, fmask, f0, s, it=-1):
         """One speculative batch: plan, partition (+ children planning), histograms, splits.
         Multi-GPU (peer path): the batch's built slots + split cursors are all-reduced between
         the histograms and the split search by one exchange kernel sized on the device (a
         no-op once the planner has marked the tree done -- every rank takes the same planning
         decisions, so the exchanges pair up however many batches a host queued past the end)."""
         h.lw_step(hd, 1, s)
-        self._part(h, hd, rows_in, gh_in, s)
+        self._part(h, hd, rows_in, gh_in, s, it)
         if self.peer is None:
             self._hist_split(h, ptr(self.rows2), ptr(self.gh2), fmask, f0, s)
             if self.sub_on:  # the batch's small entries: whole subtrees, one workgroup each
