@@ -405,6 +405,61 @@ __device__ __forceinline__ void part_chunk_scan_body(unsigned long long* __restr
   const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
   for (int si = tid; si < nsplit; si += kChunkScanThreads) s_sf[si] = first_blk[si];
   if (tid == 0) s_sf[nsplit] = nblocks;
+  if (nblocks <= kChunkScanThreads * kRun) {
+    // one pass (<= 16K chunks): the run prefixes stay in registers; the owners of each split's
+    // first chunk publish its prefix, every chunk is rebased and stored once
+    const int i0 = tid * kRun;
+    unsigned long long v[kRun], run = 0ull;
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      v[k] = i0 + k < nblocks ? chunk_io[i0 + k] : 0ull;
+      run += v[k];
+    }
+    unsigned long long inc = run;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const unsigned long long u = __shfl_up(inc, off, kWave);
+      if (l >= off) inc += u;
+    }
+    if (l == kWave - 1) s_w[wid] = inc;
+    __syncthreads();  // also orders s_sf
+    unsigned long long pre = 0ull, tot = 0ull;
+    for (int w = 0; w < NW; ++w) {
+      if (w < wid) pre += s_w[w];
+      tot += s_w[w];
+    }
+    pre += inc - run;
+    // v[k] <- the exclusive prefix of chunk i0 + k; publish split first-chunk prefixes
+    int lo = 0;  // split of chunk i0 (then advanced along the run)
+    {
+      int hi = nsplit - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_sf[mid] <= i0) lo = mid; else hi = mid - 1;
+      }
+    }
+    int sk[kRun];
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      const unsigned long long c = v[k];
+      v[k] = pre;
+      pre += c;
+      while (lo + 1 < nsplit && s_sf[lo + 1] <= i0 + k) ++lo;
+      sk[k] = lo;
+      // the chunk opens split lo -- and every empty split before it that starts here too
+      for (int t = lo; t >= 0 && i0 + k < nblocks && s_sf[t] == i0 + k; --t) s_sb[t] = v[k];
+    }
+    if (tid == 0) s_sb[nsplit] = tot;
+    for (int si = tid; si < nsplit; si += kChunkScanThreads)
+      if (s_sf[si] >= nblocks) s_sb[si] = tot;  // splits without chunks
+    __syncthreads();
+    for (int si = tid; si < nsplit; si += kChunkScanThreads)
+      cursor[(size_t)si * cs] = s_sb[si + 1] - s_sb[si];
+#pragma unroll
+    for (int k = 0; k < kRun; ++k)
+      if (i0 + k < nblocks) chunk_io[i0 + k] = v[k] - s_sb[sk[k]];
+    return;
+  }
   unsigned long long carry = 0ull;  // packed (right, left) rows of the chunks before this pass
   for (int base = 0; base < nblocks; base += kChunkScanThreads * kRun) {
     const int i0 = base + tid * kRun;

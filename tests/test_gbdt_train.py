@@ -162,8 +162,9 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_REDUCE_SPLIT": "3"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "8"},
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "0"},
-                                 {"YTK_PART_SCAN_LEVELS": "0"}, {"YTK_PART_SCAN_LEVELS": "3"},
-                                 {"YTK_PART_SCAN_LEVELS": "8"}, {"YTK_PART_SCAN_LEVELS": "2", "YTK_PART_PREFETCH": "2"}])
+                                 {"YTK_PART_SCAN_MIN_ROWS": "0"}, {"YTK_PART_SCAN_LEVELS": "3", "YTK_PART_SCAN_MIN_ROWS": "0"},
+                                 {"YTK_PART_SCAN_LEVELS": "8", "YTK_PART_SCAN_MIN_ROWS": "0"},
+                                 {"YTK_PART_SCAN_LEVELS": "2", "YTK_PART_PREFETCH": "2", "YTK_PART_SCAN_MIN_ROWS": "0"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""
@@ -319,6 +320,7 @@ def test_device_leafwise_part_scan_identical(monkeypatch, sample):
     """The first leaf-wise batches reserve their partition chunks by a count pass + scan
     (YTK_LW_PART_SCAN batches; 0: the cursor atomics everywhere) -- the same trees."""
     res = []
+    monkeypatch.setenv("YTK_PART_SCAN_MIN_ROWS", "0")  # the scan path at this small shard too
     for n in ("0", "2", "8"):
         monkeypatch.setenv("YTK_LW_PART_SCAN", n)
         p = _params("loss", rounds=3)

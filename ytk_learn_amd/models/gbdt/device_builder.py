@@ -348,6 +348,10 @@ class DeviceLevelBuilder:
         # 1.248 -> 1.219 / 1.215 / 1.219 ms per tree with 1 / 2 / 3 levels
         # (profiles/r6/part_scan/); YTK_PART_SCAN_LEVELS=0: off
         self.part_scan_levels = min(int(os.environ.get("YTK_PART_SCAN_LEVELS", "2")), 8)
+        # a small shard's few chunks contend little (1/8 of Higgs: 641 root chunks, ~8 us of
+        # serialised atomics) and the count + scan launches cost ~19 us: 0.393 -> 0.397 ms
+        if self.N < int(os.environ.get("YTK_PART_SCAN_MIN_ROWS", 4_000_000)):
+            self.part_scan_levels = 0
         self.chunk_io = (torch.zeros(self.N // 2048 + self.maxp + 2, dtype=torch.int64, device=dev)
                          if self.part_scan_levels > 0 else None)
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
