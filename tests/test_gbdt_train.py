@@ -315,6 +315,38 @@ def test_device_leafwise_partition_prefetch_identical(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("depth,sample", [(6, 1.0), (9, 0.8)])
+def test_device_level_histogram_pool_pingpong_identical(depth, sample):
+    """histogram_pool_capacity below the level engine's full slab but above its two live levels:
+    the GPU engine stays (odd / even levels alternate between two slot regions, each level's
+    built slots zeroed before it accumulates) and builds the uncapped engine's trees byte for
+    byte; below the two regions the run falls back to the host builder (same trees)."""
+    from ytk_learn_amd.models.gbdt.device_builder import DeviceLevelBuilder, level_slots_needed, level_slots_pingpong
+    res = []
+    for cap in (None, "pingpong", "host"):
+        p = _params("level", rounds=3, instance_sample_rate=sample)
+        p.tree.max_depth = depth
+        p.tree.max_leaf_cnt = 1 << depth
+        p.tree.min_child_hessian_sum = 1.0
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(60000, 23, "cuda"), _data(6000, 24, "cuda"))
+        tr.prepare()
+        slot_mb = tr.B * tr.F * 16 / float(1 << 20)
+        if cap is not None:
+            full, pp = level_slots_needed(p.tree), level_slots_pingpong(p.tree)
+            assert pp < full
+            p.histogram_pool_capacity = (pp if cap == "pingpong" else pp - 1) * slot_mb
+            tr = GBDTTrainer(p, _data(60000, 23, "cuda"), _data(6000, 24, "cuda"))
+        tr.train()
+        on_dev = isinstance(tr.builder, DeviceLevelBuilder)
+        assert on_dev == (cap != "host")
+        if cap == "pingpong":
+            assert tr.builder.pingpong and tr.builder.n_slots == level_slots_pingpong(p.tree)
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1] == res[2]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sample", [1.0, 0.7])
 def test_device_leafwise_part_scan_identical(monkeypatch, sample):
     """The first leaf-wise batches reserve their partition chunks by a count pass + scan

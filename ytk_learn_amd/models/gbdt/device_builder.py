@@ -59,6 +59,18 @@ def level_slots_needed(params: TreeParams) -> int:
     return 1 + sum(2 * min(1 << (c - 1), half_cap) for c in range(1, max(params.max_depth, 1)))
 
 
+def level_slots_pingpong(params: TreeParams, ncs: int = 0) -> int:
+    """Slots of the level engine's capped slab (histogram_pool_capacity below the full one):
+    only two levels are ever live -- level c's histograms are the parents its children's
+    derived histograms subtract from, level c - 1's are dead once level c is searched -- so
+    odd and even levels alternate between two regions (the root keeps slot 0)."""
+    half_cap = max(1, level_width(params) // 2)
+    reg = [0, 0]
+    for c in range(1, max(params.max_depth, 1)):
+        reg[c % 2] = max(reg[c % 2], 2 * min(1 << (c - 1), half_cap) + ncs)
+    return 1 + reg[0] + reg[1]
+
+
 class DeviceTree:
     """Handle of a tree built on the device: node-table snapshot + scoring arrays."""
 
@@ -108,7 +120,8 @@ class DeviceLevelBuilder:
     MIN_ROWS = int(os.environ.get("YTK_HIST_MIN_ROWS", 2048))
 
     def __init__(self, bins: torch.Tensor, binsT: torch.Tensor, F: int, B: int, nbins_f: np.ndarray,
-                 params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None):
+                 params: TreeParams, comm: Comm = None, timer: Optional[PhaseTimer] = None,
+                 pool_slots: Optional[int] = None):
         assert bins.is_cuda
         self.timer = timer if timer is not None else PhaseTimer()
         p = params
@@ -255,6 +268,23 @@ class DeviceLevelBuilder:
             self.level_slots[c] = (nxt, nxt + half, nxt + half + self.ncs)  # build, count, derived
             nxt += 2 * half + self.ncs
         self.n_slots = max(1, nxt)
+        # histogram_pool_capacity (HistogramPool.java:36-273 bounds the live histograms): a pool
+        # below the full slab alternates odd and even levels between two regions -- a level
+        # only ever subtracts from its parents' level -- and zeroes each level's built slots
+        # before it accumulates into them (level_slots_pingpong)
+        self.pingpong = pool_slots is not None and self.n_slots > pool_slots
+        if self.pingpong:
+            reg = [0, 0]
+            for c in range(1, D):
+                reg[c % 2] = max(reg[c % 2], 2 * self._half(c) + self.ncs)
+            for c in range(1, D):
+                b0 = 1 if c % 2 == 1 else 1 + reg[1]
+                half = self._half(c)
+                self.level_slots[c] = (b0, b0 + half, b0 + half + self.ncs)
+            self.n_slots = 1 + reg[0] + reg[1]
+            if self.n_slots > pool_slots:
+                raise ValueError(f"histogram pool of {pool_slots} slots below the level engine's two live "
+                                 f"levels ({self.n_slots} slots)")
         self.hist = torch.zeros((self.n_slots, B, F, 2), dtype=torch.int64, device=dev)
         # owner-computes sync (TreeParams.hist_sync): reduce-scatter by feature block (the
         # level's count slots ride along in every rank's block), split search on the owned
@@ -326,7 +356,9 @@ class DeviceLevelBuilder:
                         self.overlap_trial = []
         self.staging = (torch.empty(max_hist_items * hist_cols(F) * B * 2, dtype=torch.int64, device=dev)
                         if self.staged else None)
-        self._zero_all = self.hist.numel() * 8 <= (64 << 20)
+        # small slabs are zeroed whole once per tree; a ping-pong slab reuses its regions within
+        # the tree, so every level zeroes its own built slots
+        self._zero_all = self.hist.numel() * 8 <= (64 << 20) and not self.pingpong
         self._slab_zeroed = False  # the whole slab was zeroed at the end of the previous tree
         # YTK_ZERO_AT_END=1: zero the slab with a fill launch at the end of each tree (instead of
         # in the next gradient pass)

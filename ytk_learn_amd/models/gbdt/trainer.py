@@ -33,8 +33,8 @@ from ...utils.logging import get_logger
 from ...utils.timestats import PhaseTimer, profiling_enabled
 from .binning import BinMapper, SamplerSpec, compute_missing_fill
 from .builder import TimeStats, TreeBuilder, TreeParams
-from .device_builder import (MAX_DEPTH_DEVICE, MAX_LEVEL_NODES, DeviceLevelBuilder, level_slots_needed, level_width,
-                             node_table_to_tree)
+from .device_builder import (MAX_DEPTH_DEVICE, MAX_LEVEL_NODES, DeviceLevelBuilder,
+                             level_slots_pingpong, level_width, node_table_to_tree)
 from .device_leafwise import DeviceLeafBuilder
 from .exact import ExactGreedyBuilder
 from .refine import TreeRefiner
@@ -161,19 +161,24 @@ class GBDTTrainer:
             [[0], np.cumsum([len(c) for c in self.mapper.cands])]).astype(np.int32)).to(self.dev)
         self.refiner = TreeRefiner(self.comm, self.p.lad_refine_appr) if self.loss.name == "l1" else None
         tp = self.p.tree
-        # histogram_pool_capacity (MB, DataParallelTreeMaker.java:192-204): the GPU engines keep
-        # every histogram slot of a tree resident (no eviction); when the configured pool is
-        # smaller than that slab the run goes to the host-driven builder, whose LRU pool honours
+        # histogram_pool_capacity (MB, DataParallelTreeMaker.java:192-204): the level engine
+        # honours a pool below its full slab with two alternating level regions (the only live
+        # histograms: a level's and its parents', level_slots_pingpong); the leaf-wise engine keeps
+        # every speculative node's slot resident, so a pool below that slab (or below the level
+        # engine's two regions) sends the run to the host-driven builder, whose LRU pool honours
         # the cap (HistogramPool.java:36-273)
         pool_mb = self.p.histogram_pool_capacity
         slot_bytes = self.B * self.F * 16
+        pool_slots = (int(pool_mb * (1 << 20) // slot_bytes)
+                      if (pool_mb is not None and pool_mb > 0) else None)
 
         def fits_pool(n_slots: int) -> bool:
-            return pool_mb is None or pool_mb <= 0 or n_slots * slot_bytes <= pool_mb * (1 << 20)
+            return pool_slots is None or n_slots <= pool_slots
 
+        lvl_ncs = 1 if self.comm.is_dist else 0  # the multi-GPU count slots (one per level)
         self.use_device_builder = (self.p.device_builder and self.dev.type == "cuda" and tp.grow_policy == "level"
                                    and 1 <= tp.max_depth <= MAX_DEPTH_DEVICE and level_width(tp) <= MAX_LEVEL_NODES
-                                   and fits_pool(level_slots_needed(tp))
+                                   and fits_pool(level_slots_pingpong(tp, lvl_ncs))
                                    and DeviceLevelBuilder.supports(self.bins, self.binsT, self.B, self.F))
         # leaf-wise (the reference's Higgs configuration): GPU-resident queue replay
         use_leaf = (not self.use_device_builder and self.p.device_builder and self.dev.type == "cuda"
@@ -182,7 +187,8 @@ class GBDTTrainer:
                     and DeviceLeafBuilder.supports(self.bins, self.binsT, self.B, self.F, tp, self.comm))
         if (self.p.device_builder and self.dev.type == "cuda" and pool_mb is not None and pool_mb > 0
                 and not (self.use_device_builder or use_leaf)):
-            need = level_slots_needed(tp) if tp.grow_policy == "level" else DeviceLeafBuilder.slots_needed(tp)
+            need = (level_slots_pingpong(tp, lvl_ncs) if tp.grow_policy == "level"
+                    else DeviceLeafBuilder.slots_needed(tp))
             if not fits_pool(need):  # not silent: the capped pool costs the GPU engines
                 self.log.info(f"[GBDT] histogram_pool_capacity {pool_mb:g} MB < the GPU engine's resident "
                               f"histogram slab ({need} slots x {slot_bytes / (1 << 20):.2f} MB): the tree is "
@@ -208,7 +214,7 @@ class GBDTTrainer:
             self._fuse_root_pending = True
         elif self.use_device_builder:
             self.builder = DeviceLevelBuilder(self.bins, self.binsT, self.F, self.B, self.mapper.nbins, tp, self.comm,
-                                              timer=self.timer)
+                                              timer=self.timer, pool_slots=pool_slots)
             # the fused K == 1 gradient pass counts the rows per leaf: the level engine's last
             # level skips its counting partition (and, multi-GPU, the count all-reduce: the
             # counts ride in the round's loss all-reduce)
