@@ -183,7 +183,10 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
     env = {"YTK_DIST_BACKEND": "gloo", "YTK_HIST_SYNC": sync,
            "YTK_TEST_FSAMPLE": "0.7" if world == 3 else "1.0", "YTK_PEER_REDUCE": "1" if peer else "0",
            "YTK_COMM_LOG": "1", "YTK_HIST_OVERLAP_MIN_ROWS": "0",  # small shards: keep the overlap covered
-           "YTK_PEER_OVERLAP": {"peer_overlap": "1", "peer_auto": "auto_force"}.get(mode, "0")}
+           "YTK_PEER_OVERLAP": {"peer_overlap": "1", "peer_auto": "auto_force"}.get(mode, "0"),
+           # the first levels / batches reserve partition chunks by count + scan at these small
+           # shards too (splits with no local rows give empty chunk ranges)
+           "YTK_PART_SCAN_MIN_ROWS": "0"}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     if peer:
