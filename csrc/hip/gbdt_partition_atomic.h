@@ -390,14 +390,17 @@ __device__ __forceinline__ void partition_atomic_body_pf(
 // (left and right rows as two packed 32-bit sums in one u64: neither half overflows), the run
 // totals are scanned across the block, and every chunk's global prefix is rebased to its
 // split's first chunk.
-constexpr int kChunkScanThreads = 1024;
+// 256 threads (one small block, not a whole CU: a 1024-thread block at ~120 VGPRs needs a CU
+// with no other wave on it, which ranks sharing one GPU -- a peer exchange spinning on every
+// CU it was given -- may never leave free: the 2-rank leaf-wise test deadlocked with it)
+constexpr int kChunkScanThreads = 256;
 constexpr int kChunkScanMaxSplits = 256;  // the caller's levels (a few splits each) stay below
 __device__ __forceinline__ void part_chunk_scan_body(unsigned long long* __restrict__ chunk_io,
                                                      const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
                                                      const int* __restrict__ nblocks_dev,
                                                      unsigned long long* __restrict__ cursor, int cs) {
   constexpr int NW = kChunkScanThreads / kWave;
-  constexpr int kRun = 16;  // chunks per thread held in registers (16K chunks per pass)
+  constexpr int kRun = 32;  // chunks per thread held in registers (8K chunks per pass)
   __shared__ unsigned long long s_w[NW + 1];
   __shared__ unsigned long long s_sb[kChunkScanMaxSplits + 1];
   __shared__ int s_sf[kChunkScanMaxSplits + 1];
@@ -406,7 +409,7 @@ __device__ __forceinline__ void part_chunk_scan_body(unsigned long long* __restr
   for (int si = tid; si < nsplit; si += kChunkScanThreads) s_sf[si] = first_blk[si];
   if (tid == 0) s_sf[nsplit] = nblocks;
   if (nblocks <= kChunkScanThreads * kRun) {
-    // one pass (<= 16K chunks): the run prefixes stay in registers; the owners of each split's
+    // one pass (<= 8K chunks): the run prefixes stay in registers; the owners of each split's
     // first chunk publish its prefix, every chunk is rebased and stored once
     const int i0 = tid * kRun;
     unsigned long long v[kRun], run = 0ull;

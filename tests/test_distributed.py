@@ -186,7 +186,7 @@ def test_gpu_builders_multi_rank_one_gpu(tmp_path, task, world, mode):
            "YTK_PEER_OVERLAP": {"peer_overlap": "1", "peer_auto": "auto_force"}.get(mode, "0"),
            # the first levels / batches reserve partition chunks by count + scan at these small
            # shards too (splits with no local rows give empty chunk ranges)
-           "YTK_PART_SCAN_MIN_ROWS": "0"}
+           "YTK_PART_SCAN_MIN_ROWS": os.environ.get("YTK_TEST_PART_SCAN_MIN_ROWS", "0")}
     _run(task, tmp_path / "w1", 1, "cuda", extra_env=env)
     res = _run(task, tmp_path / f"w{world}", world, "cuda", extra_env=env)
     if peer:
