@@ -1139,6 +1139,9 @@ void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
   // and read back with atomic loads. (An agent-scope release fence per block writes back
   // the XCD's L2 on MI355X and doubled this kernel's time.)
   if (!last_block_done(b.cursor + (size_t)p.max_leaf * kCurStride)) return;
+  if constexpr (kMode == 3)  // the split totals the children planning reads from the cursors
+    part_split_totals<kPartThreads>(chunk_io, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.cursor,
+                                    kCurStride);
   lw_children_body(p, b);
 }
 
@@ -1151,6 +1154,13 @@ void lw_part_count_kernel(LwBufs b, const uint8_t* binsT, long long ncol, const 
                                                               b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.part_feat,
                                                               b.part_thr, b.part_begin, b.part_cnt, b.cursor,
                                                               b.part_shift, kCurStride, 0, chunk_io);
+}
+
+// one block per chunk (part_count_lean_body); no chunks once the tree is done (N_PBLK = 0)
+__global__ __launch_bounds__(kPartThreads) void lw_part_count_lean_kernel(LwBufs b, const uint8_t* binsT, long long ncol,
+                                                                          const int* rows, unsigned long long* chunk_io) {
+  part_count_lean_body(binsT, ncol, rows, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.part_feat, b.part_thr,
+                       b.part_begin, b.part_cnt, chunk_io);
 }
 
 // the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
@@ -1767,12 +1777,19 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   if (chunk_io && prefetch && ghp) {
     unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(lw_part_count_kernel, grid, dim3(kPartThreads), 0, s, e.b, (const uint8_t*)binsT, ncol,
-                       (const int*)rows, cio);
-    hipLaunchKernelGGL(lw_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, e.b, cio);
-    hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 2>), grid, dim3(kPartThreads), 0, s, pp, e.b,
-                       (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                       (float2*)gh_out, cio);
+    hipLaunchKernelGGL(lw_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, e.b,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, cio);
+    const char* sk = getenv("YTK_PART_SCAN_KERNEL");  // 1: the separate scan launch (mode 2)
+    if (sk && sk[0] == '1') {
+      hipLaunchKernelGGL(lw_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, e.b, cio);
+      hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 2>), grid, dim3(kPartThreads), 0, s, pp,
+                         e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                         (float2*)gh_out, cio);
+    } else {
+      hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 3>), grid, dim3(kPartThreads), 0, s, pp,
+                         e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
+                         (float2*)gh_out, cio);
+    }
     YTK_LAUNCH_CHECK();
     return;
   }

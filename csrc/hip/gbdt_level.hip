@@ -756,6 +756,9 @@ void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long 
                                              b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                              reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
+  if constexpr (kMode == 3)  // the split totals the children planning reads from the cursors
+    part_split_totals<kPartThreads>(chunk_io, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART,
+                                    reinterpret_cast<unsigned long long*>(b.left_loc), kCurStride);
   lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
 }
 
@@ -769,6 +772,13 @@ void lv_part_count_kernel(LvBufs b, const uint8_t* binsT, long long ncol, const 
                                                           b.part_begin, b.part_cnt,
                                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr,
                                                           kCurStride, 0, chunk_io);
+}
+
+// one block per chunk (part_count_lean_body)
+__global__ __launch_bounds__(kPartThreads) void lv_part_count_lean_kernel(LvBufs b, const uint8_t* binsT, long long ncol,
+                                                                          const int* rows, unsigned long long* chunk_io) {
+  part_count_lean_body(binsT, ncol, rows, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART, b.part_feat, b.part_thr,
+                       b.part_begin, b.part_cnt, chunk_io);
 }
 
 // the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
@@ -1287,18 +1297,29 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   if (chunk_io && !count_only && prefetch && pf_col && !wide && !narrow) {
     // count pass (same chunks, same split-feature gathers, no scatter) -> scan -> scatter
     unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
-    hipLaunchKernelGGL((lv_part_count_kernel<kAtomSub, true>), grid, dim3(kPartThreads), 0, s, b, (const uint8_t*)binsT,
-                       ncol, (const int*)rows, cio);
-    hipLaunchKernelGGL(lv_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, b, cio);
-#define YTK_LVPC_SCAN(KP)                                                                                       \
-  hipLaunchKernelGGL((lv_partition_children_kernel<true, KP, kAtomSub, true, true, true, uint8_t, 2>), grid,    \
+    // one block per chunk: max_blocks bounds the level's chunks (extra blocks return at once)
+    hipLaunchKernelGGL(lv_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, b,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, cio);
+    // YTK_PART_SCAN_KERNEL=1: a one-block scan launch between the two (mode 2) instead of each
+    // partition block summing its chunk's prefix (mode 3)
+    const char* sk = getenv("YTK_PART_SCAN_KERNEL");
+    const bool scan_launch = sk && sk[0] == '1';
+    if (scan_launch) hipLaunchKernelGGL(lv_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, b, cio);
+#define YTK_LVPC_SCAN1(KP, MODE)                                                                                \
+  hipLaunchKernelGGL((lv_partition_children_kernel<true, KP, kAtomSub, true, true, true, uint8_t, MODE>), grid, \
                      dim3(kPartThreads), 0, s, p, b, (const uint8_t*)binsT, ncol, (const int*)rows,             \
                      (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
                      gh_rows, cio)
+#define YTK_LVPC_SCAN(KP)                                                                                       \
+  do {                                                                                                          \
+    if (scan_launch) YTK_LVPC_SCAN1(KP, 2);                                                                     \
+    else YTK_LVPC_SCAN1(KP, 3);                                                                                 \
+  } while (0)
     if (maxp <= 64) YTK_LVPC_SCAN(64);
     else if (maxp <= 512) YTK_LVPC_SCAN(512);
     else YTK_LVPC_SCAN(kMaxPend);
 #undef YTK_LVPC_SCAN
+#undef YTK_LVPC_SCAN1
     YTK_LAUNCH_CHECK();
     return;
   }

@@ -204,7 +204,12 @@ __device__ __forceinline__ void partition_atomic_body(
 //   1: count only -- chunk_io[chunk] = (right rows << 32) | left rows, nothing scattered;
 //   2: scatter at chunk_io[chunk], the reservation a scan of the mode-1 counts computed
 //      (part_chunk_scan_kernel: the same (right, left) prefix an atomic would have returned
-//      in chunk order; the split cursors hold the totals).
+//      in chunk order; the split cursors hold the totals);
+//   3: chunk_io holds the raw per-chunk counts (part_count_lean_body) and the block sums its
+//      chunk's prefix itself -- a strided block reduction over the split's earlier chunks,
+//      continued from its previous chunk of the same split -- so no scan launch sits between
+//      the count pass and the scatter (the caller's last block writes the split totals,
+//      part_split_totals).
 template <typename BinT, int S = kAtomSub, bool kGh = false, bool kCol = false, int kMode = 0>
 __device__ __forceinline__ void partition_atomic_body_pf(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
@@ -288,8 +293,30 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     }
   };
   if constexpr (kCol) load_col(c, r, cb);
+  // kMode 3: running (right, left) rows of this block's split before chunk pre_idx
+  __shared__ unsigned long long s_red[NW];
+  int pre_si = -1, pre_idx = 0;
+  unsigned long long pre_sum = 0ull;
   while (true) {
     bool left[S];
+    if constexpr (kMode == 3) {
+      if (c.si != pre_si) {  // first chunk of a split for this block: from its first chunk
+        pre_si = c.si;
+        pre_idx = lds_tab ? s_first[c.si] : first_blk[c.si];
+        pre_sum = 0ull;
+      }
+      unsigned long long part = 0ull;
+      for (int i = pre_idx + tid; i < bid; i += kPartThreads)
+        part += chunk_io[i];  // written by the previous launch (the count pass)
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
+      if (l == 0) s_red[wid] = part;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < NW; ++w) pre_sum += s_red[w];
+      pre_idx = bid;
+      __syncthreads();  // s_red is rewritten by the next chunk
+    }
     if (!kGh) load_gh(c, r, g);
     if constexpr (kCol) {
 #pragma unroll
@@ -338,6 +365,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
         const unsigned long long cnt = ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all;
         if constexpr (kMode == 1) chunk_io[bid] = cnt;
         else if constexpr (kMode == 2) s_base = chunk_io[bid];
+        else if constexpr (kMode == 3) s_base = pre_sum;
         else s_base = atomicAdd(&cursor[(size_t)c.si * cs], cnt);
         s_tl = tl_all;
       }
@@ -380,6 +408,85 @@ __device__ __forceinline__ void partition_atomic_body_pf(
 #pragma unroll
       for (int j = 0; j < S; ++j) g[j] = gn[j];
     }
+  }
+}
+
+// Lean count pass (the scan path's first kernel): ONE block per 2048-row chunk, the chunk
+// geometry of partition_atomic_body_pf (S = kAtomSub rows per thread), no persistence, no
+// prefetch pipeline -- each thread's row ids (or positions) and split-feature bytes in flight
+// at once, the left rows popcounted per wave -> chunk_io[chunk] = (right << 32) | left. (The
+// partition body in count mode walked ~2.5 chunks per persistent block: 14 us at the root.)
+__device__ __forceinline__ void part_count_lean_body(const uint8_t* __restrict__ binsT, long long ncol,
+                                                     const int* __restrict__ rows, const int* __restrict__ first_blk,
+                                                     const int* __restrict__ nsplit_dev,
+                                                     const int* __restrict__ nblocks_dev, const int* __restrict__ feat,
+                                                     const int* __restrict__ thr, const int* __restrict__ node_begin,
+                                                     const int* __restrict__ node_count,
+                                                     unsigned long long* __restrict__ chunk_io) {
+  constexpr int S = kAtomSub, NW = kPartThreads / kWave, CH = S * kPartThreads;
+  __shared__ int s_c[NW];
+  const int bid = (int)blockIdx.x;
+  if (bid >= *nblocks_dev) return;  // uniform per block
+  const int nsplit = *nsplit_dev;
+  int lo = 0, hi = nsplit - 1;  // last split with first_blk <= bid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first_blk[mid] <= bid) lo = mid; else hi = mid - 1;
+  }
+  const int nbeg = node_begin[lo], fb = first_blk[lo];
+  const int beg = nbeg + (bid - fb) * CH, end = min(beg + CH, nbeg + node_count[lo]);
+  const uint8_t* col = binsT + (size_t)feat[lo] * ncol;
+  const int th = thr[lo] & kThrMask;
+  const int tid = threadIdx.x;
+  int r[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int pos = beg + j * kPartThreads + tid;
+    r[j] = pos < end ? (rows ? rows[pos] : pos) : -1;
+  }
+  int cb[S];  // every split-feature byte in flight before the first ballot waits on one
+#pragma unroll
+  for (int j = 0; j < S; ++j) cb[j] = r[j] >= 0 ? (int)col[(unsigned)r[j]] : 0x7fffffff;
+  int nl = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) nl += __popcll(__ballot(cb[j] <= th));
+  if (lane_id() == 0) s_c[tid >> 6] = nl;
+  __syncthreads();
+  if (tid == 0) {
+    int tl = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tl += s_c[w];
+    chunk_io[bid] = ((unsigned long long)(unsigned)(end - beg - tl) << 32) | (unsigned)tl;
+  }
+}
+
+// The split cursors' (right << 32) | left totals from the raw per-chunk counts (kMode 3: the
+// partition kernel's last block, before its children planning reads them). Per split, one
+// strided block reduction over its chunks.
+template <int kThreads>
+__device__ __forceinline__ void part_split_totals(const unsigned long long* __restrict__ chunk_io,
+                                                  const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
+                                                  const int* __restrict__ nblocks_dev,
+                                                  unsigned long long* __restrict__ cursor, int cs) {
+  constexpr int NW = kThreads / kWave;
+  __shared__ unsigned long long s_t[NW];
+  const int nsplit = *nsplit_dev, nblocks = *nblocks_dev;
+  const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
+  for (int si = 0; si < nsplit; ++si) {
+    const int f0 = first_blk[si], f1 = si + 1 < nsplit ? first_blk[si + 1] : nblocks;
+    unsigned long long part = 0ull;
+    for (int i = f0 + tid; i < f1; i += kThreads) part += chunk_io[i];
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
+    if (l == 0) s_t[wid] = part;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long t = 0ull;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += s_t[w];
+      cursor[(size_t)si * cs] = t;
+    }
+    __syncthreads();
   }
 }
 

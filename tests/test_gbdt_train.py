@@ -164,7 +164,8 @@ def test_device_builder_matches_host_builder(cuda, kw):
                                  {"YTK_FUSE_REDUCE_SPLIT": "1", "YTK_RS_GROUP": "2"}, {"YTK_PLAN_FAST": "0"},
                                  {"YTK_PART_SCAN_MIN_ROWS": "0"}, {"YTK_PART_SCAN_LEVELS": "3", "YTK_PART_SCAN_MIN_ROWS": "0"},
                                  {"YTK_PART_SCAN_LEVELS": "8", "YTK_PART_SCAN_MIN_ROWS": "0"},
-                                 {"YTK_PART_SCAN_LEVELS": "2", "YTK_PART_PREFETCH": "2", "YTK_PART_SCAN_MIN_ROWS": "0"}])
+                                 {"YTK_PART_SCAN_LEVELS": "2", "YTK_PART_PREFETCH": "2", "YTK_PART_SCAN_MIN_ROWS": "0"},
+                                 {"YTK_PART_SCAN_MIN_ROWS": "0", "YTK_PART_SCAN_KERNEL": "1"}])
 def test_device_builder_kernel_variants_identical(cuda, monkeypatch, env):
     """Level-engine kernel variants (16-row-per-thread partition chunks; split search fused
     with the next level's planning) build the default engine's trees byte for byte."""
@@ -353,8 +354,9 @@ def test_device_leafwise_part_scan_identical(monkeypatch, sample):
     (YTK_LW_PART_SCAN batches; 0: the cursor atomics everywhere) -- the same trees."""
     res = []
     monkeypatch.setenv("YTK_PART_SCAN_MIN_ROWS", "0")  # the scan path at this small shard too
-    for n in ("0", "2", "8"):
+    for n, kern in (("0", "0"), ("2", "0"), ("8", "0"), ("2", "1")):  # kern 1: the scan launch
         monkeypatch.setenv("YTK_LW_PART_SCAN", n)
+        monkeypatch.setenv("YTK_PART_SCAN_KERNEL", kern)
         p = _params("loss", rounds=3)
         p.tree.max_leaf_cnt = 63
         p.tree.instance_sample_rate = sample
@@ -363,7 +365,7 @@ def test_device_leafwise_part_scan_identical(monkeypatch, sample):
         tr.train()
         assert tr.builder.PART_SCAN == int(n)
         res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
-    assert res[0] == res[1] == res[2]
+    assert res[0] == res[1] == res[2] == res[3]
 
 
 @pytest.mark.gpu
