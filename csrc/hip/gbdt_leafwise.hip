@@ -1124,12 +1124,13 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kP
 void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
                                                                    long long ncol, const int* rows,
                                                                    const float2* ghp, int* rows_out,
-                                                                   float2* gh_out, unsigned long long* chunk_io) {
+                                                                   float2* gh_out, unsigned long long* chunk_io,
+                                                                   unsigned long long* gsum) {
   if constexpr (kPrefetch)
     partition_atomic_body_pf<BinT, kAtomSub, kPfGh, kPfCol, kMode>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first,
                                                     b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
-                                      b.cursor, b.part_shift, kCurStride, 0, chunk_io);
+                                      b.cursor, b.part_shift, kCurStride, 0, chunk_io, gsum);
   else
     partition_atomic_body<BinT, true>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + LW_N_SPLIT,
                                       b.st + LW_N_PBLK, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
@@ -1140,7 +1141,7 @@ void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
   // the XCD's L2 on MI355X and doubled this kernel's time.)
   if (!last_block_done(b.cursor + (size_t)p.max_leaf * kCurStride)) return;
   if constexpr (kMode == 3)  // the split totals the children planning reads from the cursors
-    part_split_totals<kPartThreads>(chunk_io, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.cursor,
+    part_split_totals<kPartThreads>(chunk_io, gsum, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.cursor,
                                     kCurStride);
   lw_children_body(p, b);
 }
@@ -1158,9 +1159,10 @@ void lw_part_count_kernel(LwBufs b, const uint8_t* binsT, long long ncol, const 
 
 // one block per chunk (part_count_lean_body); no chunks once the tree is done (N_PBLK = 0)
 __global__ __launch_bounds__(kPartThreads) void lw_part_count_lean_kernel(LwBufs b, const uint8_t* binsT, long long ncol,
-                                                                          const int* rows, unsigned long long* chunk_io) {
+                                                                          const int* rows, unsigned long long* chunk_io,
+                                                                          unsigned long long* gsum) {
   part_count_lean_body(binsT, ncol, rows, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.part_feat, b.part_thr,
-                       b.part_begin, b.part_cnt, chunk_io);
+                       b.part_begin, b.part_cnt, chunk_io, gsum);
 }
 
 // the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
@@ -1751,7 +1753,8 @@ void ytk_lw_step(int h, int which, uintptr_t stream) {
 // identity permutation (the root batch of an unsampled tree)
 void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, uintptr_t ghp, uintptr_t rows_out,
                       uintptr_t gh_out, int max_blocks, uintptr_t stream, uintptr_t chunk_io) {
-  // chunk_io (optional, >= max_blocks u64; batches of <= kChunkScanMaxSplits splits): count
+  // chunk_io (optional, >= max_blocks + max_blocks / 32 + 1 u64, the group sums zeroed once;
+  // batches of <= kChunkScanMaxSplits splits): count
   // pass + one-block scan instead of the split cursor atomics (the root batch's chunks all
   // reserve on one cursor line)
   const LwEngine& e = g_lw.at(h);
@@ -1764,7 +1767,7 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
     const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint16_t>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint16_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr, nullptr);
     YTK_LAUNCH_CHECK();
     return;
   }
@@ -1776,19 +1779,21 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
   if (chunk_io && prefetch && ghp) {
     unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
+    unsigned long long* gsum = cio + std::max(1, max_blocks);  // group sums past the counts
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(lw_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, e.b,
-                       (const uint8_t*)binsT, ncol, (const int*)rows, cio);
     const char* sk = getenv("YTK_PART_SCAN_KERNEL");  // 1: the separate scan launch (mode 2)
-    if (sk && sk[0] == '1') {
+    const bool scan_launch = sk && sk[0] == '1';
+    hipLaunchKernelGGL(lw_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, e.b,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, cio, scan_launch ? nullptr : gsum);
+    if (scan_launch) {
       hipLaunchKernelGGL(lw_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, e.b, cio);
       hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 2>), grid, dim3(kPartThreads), 0, s, pp,
                          e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                         (float2*)gh_out, cio);
+                         (float2*)gh_out, cio, gsum);
     } else {
       hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, false, 3>), grid, dim3(kPartThreads), 0, s, pp,
                          e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                         (float2*)gh_out, cio);
+                         (float2*)gh_out, cio, gsum);
     }
     YTK_LAUNCH_CHECK();
     return;
@@ -1796,19 +1801,19 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
   if (prefetch && pf && pf[0] == '3' && ghp)  // + the next chunk's split-feature bytes
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr, nullptr);
   else if (prefetch && !(pf && pf[0] == '1') && ghp)  // next chunk's (g, h) as well
     hipLaunchKernelGGL((lw_partition_kernel<true, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
-                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr);
+                       (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr, nullptr);
   else if (prefetch)
     hipLaunchKernelGGL(lw_partition_kernel<true>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                       (float2*)gh_out, nullptr);
+                       (float2*)gh_out, nullptr, nullptr);
   else
     hipLaunchKernelGGL(lw_partition_kernel<false>, grid, dim3(kPartThreads), 0, reinterpret_cast<hipStream_t>(stream),
                        pp, e.b, (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,
-                       (float2*)gh_out, nullptr);
+                       (float2*)gh_out, nullptr, nullptr);
   YTK_LAUNCH_CHECK();
 }
 

@@ -745,19 +745,19 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS
 void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long long ncol, const int* rows,
                                   const float2* ghp, int* rows_out, float2* gh_out, int build_base, int half,
                                   int dgap, int use_loc, int fused, int maxp, int gh_rows,
-                                  unsigned long long* chunk_io) {
+                                  unsigned long long* chunk_io, unsigned long long* gsum) {
   if constexpr (kScatter && kPrefetch)
     partition_atomic_body_pf<BinT, kS, kPfGh, kPfCol, kMode>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                           b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                           reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride,
-                                          gh_rows, chunk_io);
+                                          gh_rows, chunk_io, gsum);
   else
     partition_atomic_body<BinT, kScatter, kS>(binsT, ncol, rows, ghp, rows_out, gh_out, b.part_first, b.st + ST_N_SPLIT,
                                              b.st + ST_N_PART, b.part_feat, b.part_thr, b.part_begin, b.part_cnt,
                                              reinterpret_cast<unsigned long long*>(b.left_loc), nullptr, kCurStride);
   if (!last_block_done(reinterpret_cast<unsigned long long*>(b.left_loc) + (size_t)maxp * kCurStride)) return;
   if constexpr (kMode == 3)  // the split totals the children planning reads from the cursors
-    part_split_totals<kPartThreads>(chunk_io, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART,
+    part_split_totals<kPartThreads>(chunk_io, gsum, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART,
                                     reinterpret_cast<unsigned long long*>(b.left_loc), kCurStride);
   lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
 }
@@ -776,9 +776,10 @@ void lv_part_count_kernel(LvBufs b, const uint8_t* binsT, long long ncol, const 
 
 // one block per chunk (part_count_lean_body)
 __global__ __launch_bounds__(kPartThreads) void lv_part_count_lean_kernel(LvBufs b, const uint8_t* binsT, long long ncol,
-                                                                          const int* rows, unsigned long long* chunk_io) {
+                                                                          const int* rows, unsigned long long* chunk_io,
+                                                                          unsigned long long* gsum) {
   part_count_lean_body(binsT, ncol, rows, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART, b.part_feat, b.part_thr,
-                       b.part_begin, b.part_cnt, chunk_io);
+                       b.part_begin, b.part_cnt, chunk_io, gsum);
 }
 
 // the chunk counts -> reservations + split cursor totals (part_chunk_scan_body)
@@ -1245,7 +1246,8 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
                                uintptr_t rows, uintptr_t ghp, uintptr_t rows_out, uintptr_t gh_out, int max_blocks,
                                int count_only, int arg0, int arg1, int maxp, uintptr_t stream, int bin_bytes,
                                int gh_rows, uintptr_t chunk_io) {
-  // chunk_io (optional, >= max_blocks u64; for levels of <= kChunkScanMaxSplits splits): the
+  // chunk_io (optional, >= max_blocks + max_blocks / 32 + 1 u64, the group sums zeroed once;
+  // for levels of <= kChunkScanMaxSplits splits): the
   // chunks reserve through a count pass + one-block scan instead of the split cursor atomics
   // gh_rows: ghp is row-indexed (pipelined bodies only: the unpipelined ones read (g, h) by
   // position)
@@ -1264,7 +1266,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, kAtomSub, SC, SC, false, uint16_t>), grid,        \
                      dim3(kPartThreads), 0, s, p, b, (const uint16_t*)binsT, ncol, (const int*)rows,        \
                      (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
-                     gh_rows, nullptr)
+                     gh_rows, nullptr, nullptr)
     if (maxp <= 64) {
       if (count_only) YTK_LVPC16(false, 64); else YTK_LVPC16(true, 64);
     } else if (maxp <= 512) {
@@ -1297,19 +1299,21 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
   if (chunk_io && !count_only && prefetch && pf_col && !wide && !narrow) {
     // count pass (same chunks, same split-feature gathers, no scatter) -> scan -> scatter
     unsigned long long* cio = reinterpret_cast<unsigned long long*>(chunk_io);
+    // group sums past the counts (zero between levels: the partition's last block re-zeroes)
+    unsigned long long* gsum = cio + std::max(1, max_blocks);
     // one block per chunk: max_blocks bounds the level's chunks (extra blocks return at once)
-    hipLaunchKernelGGL(lv_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, b,
-                       (const uint8_t*)binsT, ncol, (const int*)rows, cio);
     // YTK_PART_SCAN_KERNEL=1: a one-block scan launch between the two (mode 2) instead of each
-    // partition block summing its chunk's prefix (mode 3)
+    // partition block summing its chunk's prefix (mode 3; the count pass adds the group sums)
     const char* sk = getenv("YTK_PART_SCAN_KERNEL");
     const bool scan_launch = sk && sk[0] == '1';
+    hipLaunchKernelGGL(lv_part_count_lean_kernel, dim3(std::max(1, max_blocks)), dim3(kPartThreads), 0, s, b,
+                       (const uint8_t*)binsT, ncol, (const int*)rows, cio, scan_launch ? nullptr : gsum);
     if (scan_launch) hipLaunchKernelGGL(lv_part_scan_kernel, dim3(1), dim3(kChunkScanThreads), 0, s, b, cio);
 #define YTK_LVPC_SCAN1(KP, MODE)                                                                                \
   hipLaunchKernelGGL((lv_partition_children_kernel<true, KP, kAtomSub, true, true, true, uint8_t, MODE>), grid, \
                      dim3(kPartThreads), 0, s, p, b, (const uint8_t*)binsT, ncol, (const int*)rows,             \
                      (const float2*)ghp, (int*)rows_out, (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, \
-                     gh_rows, cio)
+                     gh_rows, cio, gsum)
 #define YTK_LVPC_SCAN(KP)                                                                                       \
   do {                                                                                                          \
     if (scan_launch) YTK_LVPC_SCAN1(KP, 2);                                                                     \
@@ -1326,7 +1330,7 @@ void ytk_lv_partition_children(const uintptr_t* ptrs, const int* ip, const float
 #define YTK_LVPC4(SC, KP, S, PF, PG, PC)                                                                      \
   hipLaunchKernelGGL((lv_partition_children_kernel<SC, KP, S, PF, PG, PC>), grid, dim3(kPartThreads), 0, s, p, b,            \
                      (const uint8_t*)binsT, ncol, (const int*)rows, (const float2*)ghp, (int*)rows_out,          \
-                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, gh_rows, nullptr)
+                     (float2*)gh_out, arg0, half, dgap, use_loc, fused, maxp, gh_rows, nullptr, nullptr)
 #define YTK_LVPC2(SC, KP, S, PF)                                                  \
   do {                                                                            \
     if ((PF) && pf_col) YTK_LVPC4(SC, KP, S, PF, true, true);                     \

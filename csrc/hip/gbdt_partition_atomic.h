@@ -193,6 +193,34 @@ __device__ __forceinline__ void partition_atomic_body(
   }
 }
 
+// kMode 3 prefix geometry: the chunk counts of [f0, f1) (one split's chunks) summed as the
+// partial group at each end read count by count plus the whole 32-chunk groups between them
+// read from their group sums (gsum[g] = sum of chunks [32 g, 32 g + 32), all splits'):
+// item t of ntot -> its address.
+constexpr int kGrpShift = 5;
+constexpr int kPreLoads = 2;  // unrolled prefix loads per thread (covers 25M-row splits)
+struct ChunkRange {
+  int f0, g0, c1, na, nab, ntot;
+  __device__ __forceinline__ ChunkRange(int f0_, int f1) : f0(f0_) {
+    g0 = f0 >> kGrpShift;
+    const int g1 = f1 >> kGrpShift;
+    if (g0 == g1) {
+      na = f1 - f0;
+      nab = na;
+      c1 = f1;
+    } else {
+      na = ((g0 + 1) << kGrpShift) - f0;
+      nab = na + (g1 - g0 - 1);
+      c1 = g1 << kGrpShift;
+    }
+    ntot = nab + (f1 - c1);
+  }
+  __device__ __forceinline__ const unsigned long long* item(const unsigned long long* cnt,
+                                                            const unsigned long long* gsum, int t) const {
+    return t < na ? cnt + f0 + t : t < nab ? gsum + (g0 + 1 + t - na) : cnt + c1 + (t - nab);
+  }
+};
+
 // Software-pipelined variant of partition_atomic_body (level engine, scatter levels): the
 // persistent block locates its NEXT chunk and issues that chunk's row-id loads before it
 // ranks, reserves and scatters the current one, so the row-id round trip of chunk i + 1
@@ -205,11 +233,13 @@ __device__ __forceinline__ void partition_atomic_body(
 //   2: scatter at chunk_io[chunk], the reservation a scan of the mode-1 counts computed
 //      (part_chunk_scan_kernel: the same (right, left) prefix an atomic would have returned
 //      in chunk order; the split cursors hold the totals);
-//   3: chunk_io holds the raw per-chunk counts (part_count_lean_body) and the block sums its
-//      chunk's prefix itself -- a strided block reduction over the split's earlier chunks,
-//      continued from its previous chunk of the same split -- so no scan launch sits between
-//      the count pass and the scatter (the caller's last block writes the split totals,
-//      part_split_totals).
+//   3: chunk_io holds the raw per-chunk counts and gsum their sums per group of 32 chunks
+//      (part_count_lean_body) and the block sums its chunk's prefix itself -- the split's
+//      earlier chunks as whole groups plus at most 2 x 31 single counts (ChunkRange: 230
+//      values at Higgs' root, one load per thread, issued before the next chunk's row ids and
+//      reduced under the rank phase's barrier) -- so no scan launch sits between the count
+//      pass and the scatter (the caller's last block writes the split totals and re-zeroes
+//      gsum, part_split_totals).
 template <typename BinT, int S = kAtomSub, bool kGh = false, bool kCol = false, int kMode = 0>
 __device__ __forceinline__ void partition_atomic_body_pf(
     const BinT* __restrict__ binsT, long long ncol, const int* __restrict__ rows,
@@ -218,7 +248,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     const int* __restrict__ nblocks_dev, const int* __restrict__ feat, const int* __restrict__ thr,
     const int* __restrict__ node_begin, const int* __restrict__ node_count,
     unsigned long long* __restrict__ cursor, const int* __restrict__ out_shift, int cs, int gh_rows = 0,
-    unsigned long long* __restrict__ chunk_io = nullptr) {
+    unsigned long long* __restrict__ chunk_io = nullptr, const unsigned long long* __restrict__ gsum = nullptr) {
   // ghp == nullptr: (g, h) stays row-indexed (leaf-wise engine); out_shift as in
   // partition_atomic_body (children into the other half of a 2N ping-pong buffer).
   // gh_rows: ghp is indexed by ROW id (the level engine's first gathered level), so the next
@@ -293,29 +323,22 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     }
   };
   if constexpr (kCol) load_col(c, r, cb);
-  // kMode 3: running (right, left) rows of this block's split before chunk pre_idx
+  // kMode 3: per-wave partial prefixes of the current chunk
   __shared__ unsigned long long s_red[NW];
-  int pre_si = -1, pre_idx = 0;
-  unsigned long long pre_sum = 0ull;
   while (true) {
     bool left[S];
+    // kMode 3: this thread's share of the chunk's prefix in flight first (the counts and group
+    // sums the previous launch wrote); reduced after the next chunk's loads are issued
+    unsigned long long pv[kPreLoads];
     if constexpr (kMode == 3) {
-      if (c.si != pre_si) {  // first chunk of a split for this block: from its first chunk
-        pre_si = c.si;
-        pre_idx = lds_tab ? s_first[c.si] : first_blk[c.si];
-        pre_sum = 0ull;
+      const ChunkRange cr(lds_tab ? s_first[c.si] : first_blk[c.si], bid);
+#pragma unroll
+      for (int k = 0; k < kPreLoads; ++k) {
+        const int t = tid + k * kPartThreads;
+        pv[k] = t < cr.ntot ? *cr.item(chunk_io, gsum, t) : 0ull;
       }
-      unsigned long long part = 0ull;
-      for (int i = pre_idx + tid; i < bid; i += kPartThreads)
-        part += chunk_io[i];  // written by the previous launch (the count pass)
-#pragma unroll
-      for (int off = kWave / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
-      if (l == 0) s_red[wid] = part;
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < NW; ++w) pre_sum += s_red[w];
-      pre_idx = bid;
-      __syncthreads();  // s_red is rewritten by the next chunk
+      for (int t = tid + kPreLoads * kPartThreads; t < cr.ntot; t += kPartThreads)
+        pv[0] += *cr.item(chunk_io, gsum, t);  // splits beyond ~25M rows
     }
     if (!kGh) load_gh(c, r, g);
     if constexpr (kCol) {
@@ -342,6 +365,14 @@ __device__ __forceinline__ void partition_atomic_body_pf(
         if (!gh_rows) load_gh(cn, rn, gn);
       }
     }
+    if constexpr (kMode == 3) {
+      unsigned long long part = pv[0];
+#pragma unroll
+      for (int k = 1; k < kPreLoads; ++k) part += pv[k];
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
+      if (l == 0) s_red[wid] = part;
+    }
     int lrank[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -365,7 +396,12 @@ __device__ __forceinline__ void partition_atomic_body_pf(
         const unsigned long long cnt = ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all;
         if constexpr (kMode == 1) chunk_io[bid] = cnt;
         else if constexpr (kMode == 2) s_base = chunk_io[bid];
-        else if constexpr (kMode == 3) s_base = pre_sum;
+        else if constexpr (kMode == 3) {
+          unsigned long long pre = 0ull;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) pre += s_red[w];
+          s_base = pre;
+        }
         else s_base = atomicAdd(&cursor[(size_t)c.si * cs], cnt);
         s_tl = tl_all;
       }
@@ -422,7 +458,8 @@ __device__ __forceinline__ void part_count_lean_body(const uint8_t* __restrict__
                                                      const int* __restrict__ nblocks_dev, const int* __restrict__ feat,
                                                      const int* __restrict__ thr, const int* __restrict__ node_begin,
                                                      const int* __restrict__ node_count,
-                                                     unsigned long long* __restrict__ chunk_io) {
+                                                     unsigned long long* __restrict__ chunk_io,
+                                                     unsigned long long* __restrict__ gsum) {
   constexpr int S = kAtomSub, NW = kPartThreads / kWave, CH = S * kPartThreads;
   __shared__ int s_c[NW];
   const int bid = (int)blockIdx.x;
@@ -456,7 +493,9 @@ __device__ __forceinline__ void part_count_lean_body(const uint8_t* __restrict__
     int tl = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) tl += s_c[w];
-    chunk_io[bid] = ((unsigned long long)(unsigned)(end - beg - tl) << 32) | (unsigned)tl;
+    const unsigned long long v = ((unsigned long long)(unsigned)(end - beg - tl) << 32) | (unsigned)tl;
+    chunk_io[bid] = v;
+    if (gsum) atomicAdd(&gsum[bid >> kGrpShift], v);  // non-returning; 32 blocks per line
   }
 }
 
@@ -465,6 +504,7 @@ __device__ __forceinline__ void part_count_lean_body(const uint8_t* __restrict__
 // strided block reduction over its chunks.
 template <int kThreads>
 __device__ __forceinline__ void part_split_totals(const unsigned long long* __restrict__ chunk_io,
+                                                  unsigned long long* __restrict__ gsum,
                                                   const int* __restrict__ first_blk, const int* __restrict__ nsplit_dev,
                                                   const int* __restrict__ nblocks_dev,
                                                   unsigned long long* __restrict__ cursor, int cs) {
@@ -474,8 +514,9 @@ __device__ __forceinline__ void part_split_totals(const unsigned long long* __re
   const int tid = threadIdx.x, wid = tid >> 6, l = lane_id();
   for (int si = 0; si < nsplit; ++si) {
     const int f0 = first_blk[si], f1 = si + 1 < nsplit ? first_blk[si + 1] : nblocks;
+    const ChunkRange cr(f0, f1);
     unsigned long long part = 0ull;
-    for (int i = f0 + tid; i < f1; i += kThreads) part += chunk_io[i];
+    for (int t = tid; t < cr.ntot; t += kThreads) part += *cr.item(chunk_io, gsum, t);
 #pragma unroll
     for (int off = kWave / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
     if (l == 0) s_t[wid] = part;
@@ -488,6 +529,8 @@ __device__ __forceinline__ void part_split_totals(const unsigned long long* __re
     }
     __syncthreads();
   }
+  // every block has read the group sums: zero them for the next count pass
+  for (int g = tid; g <= (nblocks - 1) >> kGrpShift; g += kThreads) gsum[g] = 0ull;
 }
 
 // One block: exclusive scan of the mode-1 chunk counts within each split (chunks of split si:

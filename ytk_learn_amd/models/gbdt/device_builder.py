@@ -384,7 +384,10 @@ class DeviceLevelBuilder:
         # serialised atomics) and the count + scan launches cost ~19 us: 0.393 -> 0.397 ms
         if self.N < int(os.environ.get("YTK_PART_SCAN_MIN_ROWS", 4_000_000)):
             self.part_scan_levels = 0
-        self.chunk_io = (torch.zeros(self.N // 2048 + self.maxp + 2, dtype=torch.int64, device=dev)
+        # per-chunk counts (<= max_blocks of a level) then their sums per 32 chunks (zero between
+        # levels: the partition's last block re-zeroes them)
+        cap = self.N // 2048 + self.maxp + 4
+        self.chunk_io = (torch.zeros(cap + cap // 32 + 8, dtype=torch.int64, device=dev)
                          if self.part_scan_levels > 0 else None)
         self.scales = torch.ones(2, dtype=torch.float32, device=dev)
         self.inv_scales = torch.ones(2, dtype=torch.float64, device=dev)

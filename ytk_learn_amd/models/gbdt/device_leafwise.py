@@ -157,7 +157,10 @@ class DeviceLeafBuilder:
         self.PART_SCAN = min(int(os.environ.get("YTK_LW_PART_SCAN", "2")), 8)
         if N < int(os.environ.get("YTK_PART_SCAN_MIN_ROWS", 4_000_000)):
             self.PART_SCAN = 0  # few chunks per split: the atomics contend little (level engine)
-        self.chunk_io = torch.zeros(N // PART_CHUNK + ml + 2, dtype=torch.int64, device=dev)
+        # per-chunk counts (<= max_pblocks) then their sums per 32 chunks (kept zero between
+        # batches by the partition's last block)
+        cap = N // PART_CHUNK + ml + 4
+        self.chunk_io = torch.zeros(cap + cap // 32 + 8, dtype=torch.int64, device=dev)
         self._ghr = 0  # the tree's row-indexed (g, h) (build)
         self.gh2 = (torch.empty((2 * N, 2), dtype=torch.float32, device=dev) if not self.gh_rows
                     else torch.empty((1, 2), dtype=torch.float32, device=dev))
