@@ -287,9 +287,12 @@ def run(a, comm):
         torch.cuda.synchronize(dev)
     prep_s = time.perf_counter() - t0
     # multi-GPU: the histogram-exchange overlap is auto-tuned on trees 1-4 (eager, event-timed;
-    # DeviceLevelBuilder.OVERLAP_TRIAL), so those trees are always untimed: a warmup below 5
-    # gets the missing rounds added when the engine tunes (reported as warmup_autotune_extra)
-    extra = max(0, 5 - a.warmup) if getattr(tr.builder, "tuning", False) else 0
+    # DeviceLevelBuilder.OVERLAP_TRIAL) and the round graphs are captured on the tree after
+    # them (with the RCCL watchdog drain before it, ~100 ms: Comm.drain_pending), so those
+    # trees are always untimed: a warmup below 6 gets the missing rounds added when the
+    # engine tunes (reported as warmup_autotune_extra)
+    need = max(getattr(tr.builder, "OVERLAP_TRIAL", (4,))) + 2
+    extra = max(0, need - a.warmup) if getattr(tr.builder, "tuning", False) else 0
     warmup = a.warmup + extra
     total_rounds += extra
 
