@@ -69,6 +69,7 @@ fi
 if has sgd; then
   for m in linear fm ffm; do run sgd_$m 300 python bench_sparse.py --model $m --optimizer sgd --steps 3 --warmup 1; done
   run sgd_fm_bf16 300 python bench_sparse.py --model fm --optimizer sgd --dtype bf16 --steps 3 --warmup 1
+  run sgd_ffm_bf16 300 python bench_sparse.py --model ffm --optimizer sgd --dtype bf16 --steps 3 --warmup 1
 fi
 if has prof; then
   prof prof_full 300 --steps 10 --warmup 2 --leafwise-steps 0
