@@ -11,6 +11,7 @@
 #   leafscan [values...]     YTK_LW_PART_SCAN sweep of the 500-tree leaf-wise bench
 #   leafsub ROWS:MAX:ALPHA.. leaf-wise small-node subtree knobs (500-tree leaf-wise bench;
 #                            STEPS / WARM / PROF=1 from the environment)
+#   env VAR "v1 v2 .." [bench-args]  the bench once per value of the environment variable VAR
 #   sgd                      SGD GPU tests + fp32 / bf16 FM and FFM epochs
 #   sgdprof                  rocprofv3 kernel statistics of the FFM SGD epoch, fp32 and bf16
 #   distdbg                  two ranks on one GPU (gloo + peer exchange), gbdt_loss, verbose log
@@ -74,6 +75,16 @@ case "$STAGE" in
         bench "$n" 300 --policy loss --steps "${STEPS:-500}" --warmup "${WARM:-5}"
       echo "$cfg $(ms "$O/$n.json")"
       grep -h "planner profile" "$O/$n.err" | cut -c1-600 || true
+    done ;;
+  env)
+    var=$1 vals=$2
+    shift 2
+    i=0
+    for v in $vals; do
+      i=$((i + 1))
+      (export "$var=$v"; timeout -k 10 300 python bench.py "$@" > "$O/e$i.json" 2> "$O/e$i.err") \
+          || { tail -20 "$O/e$i.err"; exit 1; }
+      echo "$var=$v $(ms "$O/e$i.json")"
     done ;;
   sgd)
     timeout -k 10 300 python -u -m pytest tests/test_sgd_column.py tests/test_models_e2e.py -x -q --timeout 200 \
