@@ -369,6 +369,31 @@ def test_device_leafwise_part_scan_identical(monkeypatch, sample):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("policy,sample", [("level", 1.0), ("level", 0.7), ("loss", 1.0)])
+def test_part_scan_group_sums_identical(monkeypatch, policy, sample):
+    """Partition reservations from the count pass's 32-chunk group sums (splits spanning
+    several groups, first chunks mid-group: 300K rows = 147 root chunks) equal the cursor
+    atomics' -- the same trees, level-wise (every level scanned) and leaf-wise."""
+    monkeypatch.setenv("YTK_PART_SCAN_MIN_ROWS", "0")
+    res = []
+    for n in ("0", "8"):
+        monkeypatch.setenv("YTK_PART_SCAN_LEVELS", n)
+        monkeypatch.setenv("YTK_LW_PART_SCAN", n)
+        p = _params(policy, rounds=3)
+        p.tree.instance_sample_rate = sample
+        if policy == "loss":
+            p.tree.max_leaf_cnt = 63
+        p.device_builder = True
+        tr = GBDTTrainer(p, _data(300000, 31, "cuda"), _data(6000, 32, "cuda"))
+        tr.train()
+        assert tr.use_device_builder
+        b = tr.builder
+        assert (b.part_scan_levels if policy == "level" else b.PART_SCAN) == int(n)
+        res.append((tr.model.dumps(), tr.last_train_loss, tr.last_test_loss))
+    assert res[0] == res[1]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kw", [{"max_leaf_cnt": 63}, {"max_leaf_cnt": 255, "min_split_samples": 200},
                                 {"max_leaf_cnt": 300, "instance_sample_rate": 0.7}])
 def test_device_leafwise_children_fast_path_identical(monkeypatch, kw):
