@@ -1771,9 +1771,12 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
     YTK_LAUNCH_CHECK();
     return;
   }
-  // software-pipelined partition body, next chunk's row ids + (g, h) in flight (default:
-  // 3.41 -> 3.28-3.35 ms/tree, profiles/r2_partition_chunk.md); YTK_LW_PART_PREFETCH=1: row
-  // ids only (measured slower), 0: unpipelined -- ghp == 0 ((g, h) row-indexed, only row ids move): row ids only
+  // software-pipelined partition body, next chunk's row ids + (g, h) in flight (=2:
+  // 3.41 -> 3.28-3.35 ms/tree, profiles/r2_partition_chunk.md); default (unset or 3): also the
+  // next chunk's split-feature bytes, gathered once its row ids have arrived (500 trees
+  // 4.013-4.023 -> 3.962-3.970 ms/tree, same trees; profiles/r6/fin/lwpf_*.json);
+  // YTK_LW_PART_PREFETCH=1: row ids only (measured slower), 0: unpipelined -- ghp == 0 ((g, h)
+  // row-indexed, only row ids move): row ids only
   const char* pf = getenv("YTK_LW_PART_PREFETCH");  // read per launch (~0.1 us): tests toggle it
   const bool prefetch = !(pf && pf[0] == '0');
   const dim3 grid(std::max(1, std::min(max_blocks, kPartGrid)));
@@ -1798,7 +1801,7 @@ void ytk_lw_partition(int h, uintptr_t binsT, long long ncol, uintptr_t rows, ui
     YTK_LAUNCH_CHECK();
     return;
   }
-  if (prefetch && pf && pf[0] == '3' && ghp)  // + the next chunk's split-feature bytes
+  if (prefetch && (!pf || pf[0] == '3') && ghp)  // + the next chunk's split-feature bytes
     hipLaunchKernelGGL((lw_partition_kernel<true, true, uint8_t, true>), grid, dim3(kPartThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), pp, e.b, (const uint8_t*)binsT, ncol,
                        (const int*)rows, (const float2*)ghp, (int*)rows_out, (float2*)gh_out, nullptr, nullptr);
