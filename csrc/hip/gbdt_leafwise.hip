@@ -1117,8 +1117,9 @@ __device__ void lw_children_body(const LwParams& p, const LwBufs& b) {
 // other half of the ping-pong buffers) + the children planning, run by the LAST block to
 // finish (device-scope counter): one launch and no launch gap between the two.
 // kPrefetch: the software-pipelined body (partition_atomic_body_pf).
-// kMode 2 (the first batches: one or two splits of thousands of chunks): the chunks scatter at
-// the reservations lw_part_count_kernel + lw_part_scan_kernel computed (partition_atomic_body_pf)
+// kMode 3 (the first batches: one or two splits of thousands of chunks): the chunks scatter at
+// prefix sums of the lw_part_count_lean_kernel counts (kMode 2: reservations lw_part_scan_kernel
+// computed)
 template <bool kPrefetch, bool kPfGh = false, typename BinT = uint8_t, bool kPfCol = false, int kMode = 0>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kPrefetch ? 4 : 8, 8)))
 void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
@@ -1144,17 +1145,6 @@ void lw_partition_kernel(LwParams p, LwBufs b, const BinT* binsT,
     part_split_totals<kPartThreads>(chunk_io, gsum, b.part_first, b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.cursor,
                                     kCurStride);
   lw_children_body(p, b);
-}
-
-// kMode 1 of the partition body over the batch's chunks: (right << 32) | left rows per chunk
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
-void lw_part_count_kernel(LwBufs b, const uint8_t* binsT, long long ncol, const int* rows,
-                          unsigned long long* chunk_io) {
-  if (b.st[LW_DONE]) return;
-  partition_atomic_body_pf<uint8_t, kAtomSub, false, true, 1>(binsT, ncol, rows, nullptr, nullptr, nullptr, b.part_first,
-                                                              b.st + LW_N_SPLIT, b.st + LW_N_PBLK, b.part_feat,
-                                                              b.part_thr, b.part_begin, b.part_cnt, b.cursor,
-                                                              b.part_shift, kCurStride, 0, chunk_io);
 }
 
 // one block per chunk (part_count_lean_body); no chunks once the tree is done (N_PBLK = 0)

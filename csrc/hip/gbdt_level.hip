@@ -737,8 +737,8 @@ __global__ __launch_bounds__(kPlanThreads) void lv_plan_children_kernel(LvParams
 // One-GPU levels: the partition (partition_atomic_body) and the children planning in one
 // launch -- the last block to finish (device-scope counter, no fences: the split cursors
 // are returning atomics, read back with atomic loads) runs lv_plan_children_body.
-// kMode 2 (levels of a few splits, the root's above all): the chunks scatter at the
-// reservations lv_part_count_kernel + lv_part_scan_kernel computed (partition_atomic_body_pf).
+// kMode 3 (the first levels, the root's above all): the chunks scatter at prefix sums of the
+// lv_part_count_lean_kernel counts (kMode 2: reservations lv_part_scan_kernel computed).
 template <bool kScatter, int KP, int kS, bool kPrefetch, bool kPfGh = false, bool kPfCol = false,
           typename BinT = uint8_t, int kMode = 0>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(kS <= 8 && !kPrefetch ? 8 : 4, 8)))
@@ -760,18 +760,6 @@ void lv_partition_children_kernel(LvParams p, LvBufs b, const BinT* binsT, long 
     part_split_totals<kPartThreads>(chunk_io, gsum, b.part_first, b.st + ST_N_SPLIT, b.st + ST_N_PART,
                                     reinterpret_cast<unsigned long long*>(b.left_loc), kCurStride);
   lv_plan_children_body<KP, true>(p, b, kCurStride, build_base, half, dgap, use_loc, fused);
-}
-
-// kMode 1 of the partition body: per-chunk (right << 32) | left counts into chunk_io
-template <int kS, bool kPfCol>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
-void lv_part_count_kernel(LvBufs b, const uint8_t* binsT, long long ncol, const int* rows,
-                          unsigned long long* chunk_io) {
-  partition_atomic_body_pf<uint8_t, kS, false, kPfCol, 1>(binsT, ncol, rows, nullptr, nullptr, nullptr, b.part_first,
-                                                          b.st + ST_N_SPLIT, b.st + ST_N_PART, b.part_feat, b.part_thr,
-                                                          b.part_begin, b.part_cnt,
-                                                          reinterpret_cast<unsigned long long*>(b.left_loc), nullptr,
-                                                          kCurStride, 0, chunk_io);
 }
 
 // one block per chunk (part_count_lean_body)

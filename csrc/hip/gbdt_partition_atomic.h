@@ -229,8 +229,7 @@ struct ChunkRange {
 // kMode (splits with thousands of chunks each -- the root level: every one of Higgs' 5127
 // chunks reserved on ONE cursor line, ~12 ns apiece serialised, 62 of the level's 77 us):
 //   0: reserve with the cursor atomic;
-//   1: count only -- chunk_io[chunk] = (right rows << 32) | left rows, nothing scattered;
-//   2: scatter at chunk_io[chunk], the reservation a scan of the mode-1 counts computed
+//   2: scatter at chunk_io[chunk], the reservation a scan of the chunk counts computed
 //      (part_chunk_scan_kernel: the same (right, left) prefix an atomic would have returned
 //      in chunk order; the split cursors hold the totals);
 //   3: chunk_io holds the raw per-chunk counts and gsum their sums per group of 32 chunks
@@ -302,7 +301,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int pos = c.beg + j * kPartThreads + tid;
-      g[j] = (kMode != 1 && pos < c.end && ghp) ? ghp[gh_rows ? r[j] : pos] : make_float2(0.f, 0.f);
+      g[j] = (pos < c.end && ghp) ? ghp[gh_rows ? r[j] : pos] : make_float2(0.f, 0.f);
     }
   };
   int bid = (int)blockIdx.x;
@@ -394,8 +393,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
       if (l == 0) {
         const int tv = c.end - c.beg;
         const unsigned long long cnt = ((unsigned long long)(tv - tl_all) << 32) | (unsigned long long)tl_all;
-        if constexpr (kMode == 1) chunk_io[bid] = cnt;
-        else if constexpr (kMode == 2) s_base = chunk_io[bid];
+        if constexpr (kMode == 2) s_base = chunk_io[bid];
         else if constexpr (kMode == 3) {
           unsigned long long pre = 0ull;
 #pragma unroll
@@ -413,7 +411,7 @@ __device__ __forceinline__ void partition_atomic_body_pf(
     if constexpr (kGh) {
       if (gh_rows && more) load_gh(cn, rn, gn);
     }
-    if constexpr (kMode != 1) {
+    {
       const int tl = s_tl;
       const int tv = c.end - c.beg;
       const unsigned long long base = s_base;
@@ -533,7 +531,7 @@ __device__ __forceinline__ void part_split_totals(const unsigned long long* __re
   for (int g = tid; g <= (nblocks - 1) >> kGrpShift; g += kThreads) gsum[g] = 0ull;
 }
 
-// One block: exclusive scan of the mode-1 chunk counts within each split (chunks of split si:
+// One block: exclusive scan of the lean count pass's chunk counts within each split (chunks of split si:
 // [first_blk[si], first_blk[si + 1])), in chunk order -> chunk_io[chunk] = (right rows before
 // it << 32) | left rows before it; cursor[si * cs] = the split's (right << 32) | left totals
 // (what the atomic mode leaves there). One pass: each thread scans a contiguous run of chunks
