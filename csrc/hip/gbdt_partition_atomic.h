@@ -3,6 +3,7 @@
 // (gbdt_leafwise.hip).
 #pragma once
 #include "common.h"
+#include "gbdt_chunk_range.h"
 
 namespace ytk {
 
@@ -193,33 +194,7 @@ __device__ __forceinline__ void partition_atomic_body(
   }
 }
 
-// kMode 3 prefix geometry: the chunk counts of [f0, f1) (one split's chunks) summed as the
-// partial group at each end read count by count plus the whole 32-chunk groups between them
-// read from their group sums (gsum[g] = sum of chunks [32 g, 32 g + 32), all splits'):
-// item t of ntot -> its address.
-constexpr int kGrpShift = 5;
-constexpr int kPreLoads = 2;  // unrolled prefix loads per thread (covers 25M-row splits)
-struct ChunkRange {
-  int f0, g0, c1, na, nab, ntot;
-  __device__ __forceinline__ ChunkRange(int f0_, int f1) : f0(f0_) {
-    g0 = f0 >> kGrpShift;
-    const int g1 = f1 >> kGrpShift;
-    if (g0 == g1) {
-      na = f1 - f0;
-      nab = na;
-      c1 = f1;
-    } else {
-      na = ((g0 + 1) << kGrpShift) - f0;
-      nab = na + (g1 - g0 - 1);
-      c1 = g1 << kGrpShift;
-    }
-    ntot = nab + (f1 - c1);
-  }
-  __device__ __forceinline__ const unsigned long long* item(const unsigned long long* cnt,
-                                                            const unsigned long long* gsum, int t) const {
-    return t < na ? cnt + f0 + t : t < nab ? gsum + (g0 + 1 + t - na) : cnt + c1 + (t - nab);
-  }
-};
+constexpr int kPreLoads = 2;  // kMode 3: unrolled prefix loads per thread (covers 25M-row splits)
 
 // Software-pipelined variant of partition_atomic_body (level engine, scatter levels): the
 // persistent block locates its NEXT chunk and issues that chunk's row-id loads before it
